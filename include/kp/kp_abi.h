@@ -1,0 +1,345 @@
+/*
+ * kp_abi.h — C ABI of the MI355X-native Karpenter bin-packing hot path.
+ *
+ * This is the drop-in boundary a Go cgo shim binds. Every entry point
+ * replaces one reference surface:
+ *
+ *   kp_catalog_upload      <- cloudprovider.CloudProvider.GetInstanceTypes result
+ *                             (R:pkg/cloudprovider/cloudprovider.go:177-193 -> instancetype.DefaultProvider.List
+ *                              R:pkg/providers/instancetype/instancetype.go:129-171 + offering.InjectOfferings
+ *                              R:pkg/providers/instancetype/offering/offering.go:68-98), resident on device
+ *                             until its seqnum changes (R:instancetype.go:225-237 cacheKey).
+ *   kp_instance_type_resolve <- instancetype.NewInstanceType (R:pkg/providers/instancetype/types.go:123-155)
+ *   kp_filter_compatible_available <- filter.CompatibleAvailableFilter
+ *                             (R:pkg/providers/instance/filter/filter.go:39-64), batched: many
+ *                             (requirements, requests) rows × one catalogue on the GPU.
+ *   kp_solve               <- upstream scheduling.Scheduler.Solve (sigs.k8s.io/karpenter
+ *                             pkg/controllers/provisioning/scheduling/scheduler.go), reached from
+ *                             R:pkg/providers/instancetype/suite_test.go:93,279 (NewProvisioner/ExpectProvisioned),
+ *                             followed by Results.TruncateInstanceTypes(MaxInstanceTypes).
+ *
+ * Conventions
+ *   - Every function returns int32: KP_OK (0) or a negative KP_E_* code. kp_last_error() gives text.
+ *     KP_E_UNSUPPORTED means the input uses a feature the device path does not implement; the Go
+ *     shim then runs the original CPU path.
+ *   - Caller owns every input buffer; nothing is retained after a call returns (catalogues copy).
+ *   - Quantities are int64 milli-units (resource.Quantity.MilliValue()): cpu "1" = 1000,
+ *     memory "1Mi" = 1048576000. kp_resource_list.present marks which resources are set; it
+ *     matters only for NodePool limits (R: upstream filterByRemainingResources iterates limit keys).
+ *   - No C++ exceptions and no torch types cross this boundary.
+ */
+#ifndef KP_ABI_H
+#define KP_ABI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KP_ABI_VERSION 1
+
+enum kp_status {
+  KP_OK = 0,
+  KP_E_INVAL = -1,
+  KP_E_NOMEM = -2,
+  KP_E_DEVICE = -3,
+  KP_E_UNSUPPORTED = -4,
+  KP_E_NOTFOUND = -5,
+};
+
+/* Resource axis, fixed (R:pkg/providers/instancetype/types.go:317-329,151-153; R:pkg/apis/v1/labels.go:69-81). */
+enum kp_resource {
+  KP_RES_CPU = 0,
+  KP_RES_MEMORY = 1,
+  KP_RES_EPHEMERAL_STORAGE = 2,
+  KP_RES_PODS = 3,
+  KP_RES_POD_ENI = 4,        /* vpc.amazonaws.com/pod-eni */
+  KP_RES_EFA = 5,            /* vpc.amazonaws.com/efa */
+  KP_RES_NVIDIA_GPU = 6,     /* nvidia.com/gpu */
+  KP_RES_AMD_GPU = 7,        /* amd.com/gpu */
+  KP_RES_NEURON = 8,         /* aws.amazon.com/neuron */
+  KP_RES_NEURONCORE = 9,     /* aws.amazon.com/neuroncore */
+  KP_RES_GAUDI = 10,         /* habana.ai/gaudi */
+  KP_RES_PRIVATE_IPV4 = 11,  /* vpc.amazonaws.com/PrivateIPv4Address */
+  KP_NUM_RESOURCES = 12
+};
+
+typedef struct kp_resource_list {
+  int64_t milli[KP_NUM_RESOURCES];
+  uint32_t present; /* bit r set <=> resource r present in the ResourceList */
+  uint32_t reserved_;
+} kp_resource_list;
+
+/* corev1.NodeSelectorOperator */
+enum kp_operator {
+  KP_OP_IN = 0,
+  KP_OP_NOT_IN = 1,
+  KP_OP_EXISTS = 2,
+  KP_OP_DOES_NOT_EXIST = 3,
+  KP_OP_GT = 4,
+  KP_OP_LT = 5
+};
+
+/* scheduling.NewRequirementWithFlexibility(key, op, minValues, values...) */
+typedef struct kp_requirement {
+  const char* key;
+  int32_t op;          /* enum kp_operator */
+  int32_t min_values;  /* < 0: nil */
+  const char* const* values;
+  uint32_t n_values;
+  uint32_t reserved_;
+} kp_requirement;
+
+typedef struct kp_requirements {
+  const kp_requirement* items;
+  uint32_t n;
+  uint32_t reserved_;
+} kp_requirements;
+
+typedef struct kp_label {
+  const char* key;
+  const char* value;
+} kp_label;
+
+enum kp_taint_effect {
+  KP_EFFECT_ANY = 0, /* tolerations only: empty effect matches all */
+  KP_EFFECT_NO_SCHEDULE = 1,
+  KP_EFFECT_PREFER_NO_SCHEDULE = 2,
+  KP_EFFECT_NO_EXECUTE = 3
+};
+
+typedef struct kp_taint {
+  const char* key;
+  const char* value;
+  int32_t effect;
+  int32_t reserved_;
+} kp_taint;
+
+enum kp_toleration_operator { KP_TOL_EQUAL = 0, KP_TOL_EXISTS = 1 };
+
+typedef struct kp_toleration {
+  const char* key;   /* "" or NULL: any key (requires KP_TOL_EXISTS) */
+  const char* value;
+  int32_t op;        /* enum kp_toleration_operator */
+  int32_t effect;    /* enum kp_taint_effect; KP_EFFECT_ANY = all effects */
+} kp_toleration;
+
+/* cloudprovider.Offering as built by createOfferings (R:offering.go:115-147). */
+typedef struct kp_offering {
+  const char* capacity_type; /* karpenter.sh/capacity-type In {capacity_type} */
+  const char* zone;          /* topology.kubernetes.io/zone In {zone}; NULL: no zone requirement */
+  const char* zone_id;       /* topology.k8s.aws/zone-id In {zone_id}; NULL: no zone-id requirement */
+  const char* reservation_id;   /* capacity-reservation-id In {id}; NULL: DoesNotExist (R:offering.go:136) */
+  const char* reservation_type; /* capacity-reservation-type In {type}; NULL: DoesNotExist (R:offering.go:137) */
+  double price;
+  int32_t available;
+  int32_t reservation_capacity; /* reserved offerings: device path returns KP_E_UNSUPPORTED in ABI v1 */
+} kp_offering;
+
+/* cloudprovider.InstanceType after InjectOfferings. */
+typedef struct kp_instance_type {
+  const char* name;
+  kp_requirements requirements;
+  kp_resource_list capacity;
+  kp_resource_list overhead; /* Overhead.Total() = kube-reserved + system-reserved + eviction */
+  const kp_offering* offerings;
+  uint32_t n_offerings;
+  uint32_t reserved_;
+} kp_instance_type;
+
+typedef struct kp_catalog_desc {
+  const kp_instance_type* types;
+  uint32_t n_types;
+  uint32_t reserved_;
+} kp_catalog_desc;
+
+/* NodePool -> NodeClaimTemplate (upstream NewNodeClaimTemplate). Order does not matter: the solver
+ * orders pools by weight desc then name asc (upstream nodepoolutils.OrderByWeight). */
+typedef struct kp_nodepool {
+  const char* name;
+  int32_t weight;
+  uint32_t catalog; /* index into kp_solve_in.catalogs / catalog_descs: GetInstanceTypes(nodePool) */
+  kp_requirements requirements;  /* spec.template.spec.requirements (minValues allowed) */
+  const kp_label* labels;        /* spec.template.metadata.labels (karpenter.sh/nodepool is added) */
+  uint32_t n_labels;
+  uint32_t n_taints;
+  const kp_taint* taints;        /* spec.template.spec.taints */
+  kp_resource_list limits;       /* remaining limits (spec.limits minus existing capacity); present = limited */
+  kp_resource_list daemon_requests; /* daemonset overhead for this template */
+} kp_nodepool;
+
+typedef struct kp_preferred_term {
+  int32_t weight;
+  int32_t reserved_;
+  kp_requirements preference;
+} kp_preferred_term;
+
+/* A pod "shape": everything the scheduler reads from a pod except its identity. */
+typedef struct kp_pod_shape {
+  kp_resource_list requests;                 /* resources.RequestsForPods(pod) */
+  const kp_label* node_selector;
+  uint32_t n_node_selector;
+  uint32_t n_required_terms;
+  const kp_requirements* required_terms;     /* nodeAffinity required NodeSelectorTerms (ORed) */
+  const kp_preferred_term* preferred_terms;  /* nodeAffinity preferred terms */
+  uint32_t n_preferred_terms;
+  uint32_t n_tolerations;
+  const kp_toleration* tolerations;
+  uint32_t n_topology_spread;                /* ABI v1: must be 0 (else KP_E_UNSUPPORTED) */
+  uint32_t reserved_;
+} kp_pod_shape;
+
+typedef struct kp_pod {
+  uint32_t shape;
+  uint32_t reserved_;
+  int64_t creation_unix;  /* metadata.creationTimestamp (1 s resolution, as in the API) */
+  uint64_t uid_key;       /* order-preserving key of metadata.uid (string order of UIDs) */
+} kp_pod;
+
+/* In-flight or real node already in the cluster (upstream ExistingNode). */
+typedef struct kp_existing_node {
+  const char* name;
+  const kp_label* labels;   /* node labels -> NewLabelRequirements */
+  uint32_t n_labels;
+  uint32_t n_taints;
+  const kp_taint* taints;
+  kp_resource_list available;  /* cachedAvailable: allocatable minus bound pods' requests */
+  kp_resource_list requests;   /* initial requests: daemonset pods expected but not yet bound */
+  int32_t initialized;
+  int32_t reserved_;
+} kp_existing_node;
+
+typedef struct kp_ctx kp_ctx;
+typedef struct kp_catalog kp_catalog;
+typedef struct kp_solve_result kp_solve_result;
+
+typedef struct kp_solve_in {
+  const kp_catalog* const* catalogs;      /* device path: resident catalogue handles */
+  const kp_catalog_desc* catalog_descs;   /* CPU oracle path: the same catalogues as plain arrays */
+  uint32_t n_catalogs;
+  uint32_t n_nodepools;
+  const kp_nodepool* nodepools;
+  const kp_existing_node* existing;
+  uint32_t n_existing;
+  uint32_t n_shapes;
+  const kp_pod_shape* shapes;
+  const kp_pod* pods;
+  uint32_t n_pods;
+  uint32_t max_instance_types;  /* scheduling.MaxInstanceTypes = 100; 0 = no truncation */
+} kp_solve_in;
+
+typedef struct kp_nodeclaim_info {
+  uint32_t nodepool;        /* index into kp_solve_in.nodepools */
+  uint32_t n_pods;
+  uint32_t n_remaining;     /* InstanceTypeOptions before truncation */
+  uint32_t n_options;       /* after OrderByPrice + Truncate */
+  const uint32_t* pods;     /* pod indices in the order they were added */
+  const uint32_t* options;  /* catalogue indices, cheapest-compatible-offering price asc then name asc */
+  kp_resource_list requests;
+} kp_nodeclaim_info;
+
+typedef struct kp_solve_stats {
+  double device_ms;         /* kernel time, HIP events on the solve stream */
+  double host_ms;           /* whole kp_solve wall time */
+  uint64_t attempts;        /* NodeClaim.Add / ExistingNode.CanAdd evaluations */
+  uint64_t bytes_algorithmic; /* bytes the device algorithm reads+writes */
+  uint64_t pops;            /* queue pops */
+} kp_solve_stats;
+
+/* ---- context ---------------------------------------------------------------------------- */
+typedef struct kp_options {
+  double vm_memory_overhead_percent; /* R:pkg/operator/options/options.go:53 default 0.075 */
+  int32_t reserved_enis;             /* R:pkg/operator/options/options.go:55 default 0 */
+  int32_t device;                    /* HIP device ordinal */
+} kp_options;
+
+int32_t kp_ctx_create(const kp_options* opts, kp_ctx** out);
+void kp_ctx_destroy(kp_ctx* ctx);
+const char* kp_last_error(void);
+int32_t kp_abi_version(void);
+
+/* ---- catalogue ---------------------------------------------------------------------------- */
+int32_t kp_catalog_upload(kp_ctx* ctx, const kp_catalog_desc* desc, uint64_t seqnum, kp_catalog** out);
+uint64_t kp_catalog_seqnum(const kp_catalog* cat);
+uint32_t kp_catalog_size(const kp_catalog* cat);
+void kp_catalog_destroy(kp_catalog* cat);
+
+/* EC2 facts the reference reads from ec2types.InstanceTypeInfo (+ the static tables it joins). */
+typedef struct kp_ec2_info {
+  const char* name;
+  int32_t vcpu;
+  int32_t reserved0_;
+  int64_t memory_mib;
+  const char* arch;               /* "amd64" | "arm64" (already mapped via AWSToKubeArchitectures) */
+  const char* hypervisor;
+  int32_t encryption_in_transit;
+  int32_t clock_mhz;              /* 0: no ProcessorInfo clock */
+  const char* cpu_manufacturer;   /* "" : none */
+  int64_t ebs_bandwidth_mbps;     /* 0: not EBS-optimized by default */
+  int64_t network_bandwidth_mbps; /* 0: not in the bandwidth table */
+  int64_t local_nvme_gb;          /* 0: none */
+  const char* gpu_name;           /* "" : no GPU */
+  const char* gpu_manufacturer;
+  int32_t gpu_count;
+  int32_t reserved1_;
+  int64_t gpu_memory_mib;
+  const char* accel_name;         /* "" : none */
+  const char* accel_manufacturer;
+  int32_t accel_count;
+  int32_t neuron_devices;         /* NeuronInfo */
+  int32_t neuron_cores_per_device;
+  int32_t efa;
+  int32_t max_enis;               /* NetworkCards[DefaultNetworkCardIndex].MaximumNetworkInterfaces */
+  int32_t ipv4_per_eni;
+  int32_t trunking;               /* Limits[name].IsTrunkingCompatible */
+  int32_t branch_enis;            /* Limits[name].BranchInterface */
+  int32_t in_limits_table;        /* name present in zz_generated.vpclimits.go */
+  int32_t reserved2_;
+} kp_ec2_info;
+
+/* EC2NodeClass subset that changes results (AL2023 family; kubelet overrides). */
+typedef struct kp_nodeclass {
+  const char* region;
+  const char* const* zones;      /* subnet zones (ZoneInfo) */
+  const char* const* zone_ids;   /* parallel to zones; NULL entries allowed */
+  uint32_t n_zones;
+  int32_t max_pods;              /* < 0: nil */
+  int32_t pods_per_core;         /* <= 0: nil */
+  int32_t reserved_;
+} kp_nodeclass;
+
+/* instancetype.NewInstanceType capacity + Overhead.Total() for the AL2023 family (R:types.go:123-155,
+ * 313-598). The label half (computeRequirements, R:types.go:158-292) is plain string marshalling and
+ * stays with the caller (kpamd/catalog.py mirrors it). */
+int32_t kp_instance_type_resolve(const kp_options* opts, const kp_ec2_info* info, const kp_nodeclass* nc,
+                                 kp_resource_list* capacity, kp_resource_list* overhead);
+
+/* ---- feasibility (CompatibleAvailableFilter, batched) ------------------------------------- */
+typedef struct kp_feasibility_query {
+  kp_requirements requirements;
+  kp_resource_list requests;
+} kp_feasibility_query;
+
+/* For each query q: bit t of out_mask[q*words + t/64] <=> instance type t is compatible, fits and has
+ * a compatible available offering (R:filter.go:51-64; AllowUndefinedWellKnownLabels). out_cheapest
+ * (optional, n_queries × n_types) = cheapest compatible available offering price, +inf if none.
+ * words = (n_types + 63) / 64. */
+int32_t kp_filter_compatible_available(kp_ctx* ctx, const kp_catalog* cat, const kp_feasibility_query* queries,
+                                       uint32_t n_queries, uint64_t* out_mask, double* out_cheapest,
+                                       kp_solve_stats* stats);
+
+/* ---- Solve -------------------------------------------------------------------------------- */
+int32_t kp_solve(kp_ctx* ctx, const kp_solve_in* in, kp_solve_result** out);
+uint32_t kp_result_nodeclaim_count(const kp_solve_result* res);
+/* out[p] for every input pod: >= 0 new NodeClaim index; -1 pod error; <= -2 existing node -(2+i) */
+int32_t kp_result_pod_placements(const kp_solve_result* res, int32_t* out, uint32_t n_pods);
+int32_t kp_result_nodeclaim(const kp_solve_result* res, uint32_t i, kp_nodeclaim_info* out);
+int32_t kp_result_stats(const kp_solve_result* res, kp_solve_stats* out);
+void kp_result_destroy(kp_solve_result* res);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KP_ABI_H */

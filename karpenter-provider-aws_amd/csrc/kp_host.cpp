@@ -1,0 +1,1508 @@
+// kp_host.cpp — host side of the C ABI (include/kp/kp_abi.h).
+//
+// Compiles the string-keyed reference objects (InstanceType, NodePool, Pod, Node) into the device data
+// model of kp_model.h, owns device memory and the HIP stream, launches the kernels of kp_kernels.hip and
+// copies results back. There is no CPU fallback: without a HIP device every compute entry point returns
+// KP_E_DEVICE (the Go shim's own CPU path is the fallback).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <set>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "kp/kp_abi.h"
+#include "kp_device.h"
+#include "kp_model.h"
+
+using std::map;
+using std::string;
+using std::vector;
+
+namespace {
+
+thread_local string g_err;
+int32_t fail(int32_t code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+#define HIPCHK(x)                                                                          \
+  do {                                                                                     \
+    hipError_t e_ = (x);                                                                   \
+    if (e_ != hipSuccess) return fail(KP_E_DEVICE, "%s: %s", #x, hipGetErrorString(e_));   \
+  } while (0)
+
+const char* kHostname = "kubernetes.io/hostname";
+const char* kZone = "topology.kubernetes.io/zone";
+const char* kCapType = "karpenter.sh/capacity-type";
+const char* kZoneID = "topology.k8s.aws/zone-id";
+const char* kResID = "karpenter.k8s.aws/capacity-reservation-id";
+const char* kResType = "karpenter.k8s.aws/capacity-reservation-type";
+const char* kNodePool = "karpenter.sh/nodepool";
+
+// karpv1.WellKnownLabels + R:pkg/apis/v1/labels.go:31-56
+const std::set<string>& WellKnown() {
+  static const std::set<string> s = {
+      "karpenter.sh/nodepool", "topology.kubernetes.io/zone", "topology.kubernetes.io/region",
+      "node.kubernetes.io/instance-type", "kubernetes.io/arch", "kubernetes.io/os", "karpenter.sh/capacity-type",
+      "node.kubernetes.io/windows-build", "karpenter.k8s.aws/capacity-reservation-id",
+      "karpenter.k8s.aws/capacity-reservation-type", "karpenter.k8s.aws/instance-hypervisor",
+      "karpenter.k8s.aws/instance-encryption-in-transit-supported", "karpenter.k8s.aws/instance-category",
+      "karpenter.k8s.aws/instance-family", "karpenter.k8s.aws/instance-generation", "karpenter.k8s.aws/instance-size",
+      "karpenter.k8s.aws/instance-local-nvme", "karpenter.k8s.aws/instance-cpu",
+      "karpenter.k8s.aws/instance-cpu-manufacturer", "karpenter.k8s.aws/instance-cpu-sustained-clock-speed-mhz",
+      "karpenter.k8s.aws/instance-memory", "karpenter.k8s.aws/instance-ebs-bandwidth",
+      "karpenter.k8s.aws/instance-network-bandwidth", "karpenter.k8s.aws/instance-gpu-name",
+      "karpenter.k8s.aws/instance-gpu-manufacturer", "karpenter.k8s.aws/instance-gpu-count",
+      "karpenter.k8s.aws/instance-gpu-memory", "karpenter.k8s.aws/instance-accelerator-name",
+      "karpenter.k8s.aws/instance-accelerator-manufacturer", "karpenter.k8s.aws/instance-accelerator-count",
+      "topology.k8s.aws/zone-id"};
+  return s;
+}
+string Normalize(const string& k) {  // karpv1.NormalizedLabels (+ R:kwok/operator/operator.go:73)
+  static const map<string, string> m = {
+      {"failure-domain.beta.kubernetes.io/zone", "topology.kubernetes.io/zone"},
+      {"beta.kubernetes.io/arch", "kubernetes.io/arch"},
+      {"beta.kubernetes.io/os", "kubernetes.io/os"},
+      {"beta.kubernetes.io/instance-type", "node.kubernetes.io/instance-type"},
+      {"failure-domain.beta.kubernetes.io/region", "topology.kubernetes.io/region"},
+      {"topology.ebs.csi.aws.com/zone", "topology.kubernetes.io/zone"},
+  };
+  auto it = m.find(k);
+  return it == m.end() ? k : it->second;
+}
+bool Atoi(const string& s, int64_t* out) {  // Go strconv.Atoi
+  if (s.empty()) return false;
+  size_t i = 0;
+  bool neg = false;
+  if (s[0] == '+' || s[0] == '-') {
+    neg = s[0] == '-';
+    if (s.size() == 1) return false;
+    i = 1;
+  }
+  unsigned __int128 v = 0;
+  const unsigned __int128 lim = (unsigned __int128)std::numeric_limits<int64_t>::max() + (neg ? 1 : 0);
+  for (; i < s.size(); i++) {
+    if (s[i] < '0' || s[i] > '9') return false;
+    v = v * 10 + (unsigned)(s[i] - '0');
+    if (v > lim) return false;
+  }
+  *out = neg ? (int64_t)(-(__int128)v) : (int64_t)v;
+  return true;
+}
+
+// ------------------------------------------------------------------------------------------------
+// raw (string) model
+// ------------------------------------------------------------------------------------------------
+struct RawReq {
+  string key;
+  int op;
+  vector<string> values;
+  int minv;  // < 0 nil
+};
+using RawReqs = vector<RawReq>;
+
+RawReqs ParseReqs(const kp_requirements& in) {
+  RawReqs out;
+  for (uint32_t i = 0; i < in.n; i++) {
+    const kp_requirement& q = in.items[i];
+    RawReq r;
+    r.key = Normalize(q.key ? q.key : "");
+    r.op = q.op;
+    r.minv = q.min_values;
+    for (uint32_t j = 0; j < q.n_values; j++) r.values.push_back(q.values[j] ? q.values[j] : "");
+    out.push_back(std::move(r));
+  }
+  return out;
+}
+RawReqs LabelReqs(const kp_label* l, uint32_t n, bool drop_hostname) {
+  RawReqs out;
+  for (uint32_t i = 0; i < n; i++) {
+    string k = Normalize(l[i].key ? l[i].key : "");
+    if (drop_hostname && k == kHostname) continue;
+    out.push_back({k, KP_OP_IN, {l[i].value ? l[i].value : ""}, -1});
+  }
+  return out;
+}
+
+struct HostOffering {
+  string ct, zone, zid;
+  bool has_zone, has_zid;
+  double price;
+  bool available;
+};
+struct HostType {
+  string name;
+  RawReqs reqs;
+  int64_t cap[KP_NRES];
+  int64_t ovh[KP_NRES];
+  uint32_t cap_present;
+  vector<HostOffering> offs;
+};
+
+}  // namespace
+
+struct kp_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  kp_options opts;
+  std::mutex mu;
+};
+
+struct kp_catalog {
+  kp_ctx* ctx;
+  uint64_t seqnum;
+  vector<HostType> types;
+};
+
+namespace {
+
+// ------------------------------------------------------------------------------------------------
+// dictionary
+// ------------------------------------------------------------------------------------------------
+struct Dict {
+  vector<string> keys;
+  std::unordered_map<string, int> key_id;
+  vector<vector<string>> vals;
+  vector<std::unordered_map<string, int>> val_id;  // value -> bit (global)
+  DevDict dd;
+  vector<int64_t> vint;  // [W*64]
+  int key(const string& k) const {
+    auto it = key_id.find(k);
+    return it == key_id.end() ? -1 : it->second;
+  }
+  int bit(int k, const string& v) const {
+    auto it = val_id[k].find(v);
+    return it == val_id[k].end() ? -1 : it->second;
+  }
+};
+
+struct DictBuilder {
+  map<string, bool> bounded;  // key -> needs bound slot
+  map<string, std::set<string>> values;
+  void addReqs(const RawReqs& rs) {
+    for (auto& r : rs) {
+      auto& b = bounded[r.key];
+      if (r.op == KP_OP_GT || r.op == KP_OP_LT || r.minv >= 0) b = true;
+      auto& s = values[r.key];
+      if (r.op == KP_OP_IN || r.op == KP_OP_NOT_IN) s.insert(r.values.begin(), r.values.end());
+    }
+  }
+  void addLabel(const string& k, const string& v) {
+    bounded[k];
+    values[k].insert(v);
+  }
+  int32_t build(Dict& d) {
+    vector<string> order;
+    for (auto& kv : bounded)
+      if (kv.second) order.push_back(kv.first);
+    const int KB = (int)order.size();
+    if (KB > KP_MAX_BOUND_KEYS) return fail(KP_E_UNSUPPORTED, "%d keys with Gt/Lt/minValues (max %d)", KB, KP_MAX_BOUND_KEYS);
+    for (auto& kv : bounded)
+      if (!kv.second) order.push_back(kv.first);
+    if ((int)order.size() > KP_MAX_KEYS) return fail(KP_E_UNSUPPORTED, "%zu label keys (max %d)", order.size(), KP_MAX_KEYS);
+    memset(&d.dd, 0, sizeof(d.dd));
+    d.keys = order;
+    d.vals.assign(order.size(), {});
+    d.val_id.assign(order.size(), {});
+    int w = 0;
+    for (size_t k = 0; k < order.size(); k++) {
+      d.key_id[order[k]] = (int)k;
+      auto& s = values[order[k]];
+      d.vals[k].assign(s.begin(), s.end());
+      const int nw = std::max<int>(1, (int)((s.size() + 63) / 64));
+      d.dd.wofs[k] = w;
+      d.dd.nval[k] = (int)s.size();
+      if (w + nw > KP_MAX_WORDS) return fail(KP_E_UNSUPPORTED, "label values need > %d words", KP_MAX_WORDS);
+      for (int i = 0; i < nw; i++) d.dd.wkey[w + i] = (int8_t)k;
+      int b = 0;
+      for (auto& v : d.vals[k]) {
+        d.val_id[k][v] = w * 64 + b;
+        d.dd.validbits[w + b / 64] |= 1ull << (b % 64);
+        b++;
+      }
+      w += nw;
+    }
+    for (int i = w; i < KP_MAX_WORDS; i++) d.dd.wkey[i] = -1;
+    d.dd.K = (int)order.size();
+    d.dd.W = w;
+    d.dd.KB = KB;
+    d.vint.assign((size_t)std::max(w, 1) * 64, 0);
+    for (size_t k = 0; k < order.size(); k++)
+      for (auto& kv : d.val_id[k]) {
+        int64_t x;
+        if (Atoi(kv.first, &x)) {
+          d.vint[kv.second] = x;
+          d.dd.vint_ok[kv.second / 64] |= 1ull << (kv.second % 64);
+        }
+      }
+    for (size_t k = 0; k < order.size(); k++)
+      if (WellKnown().count(order[k])) d.dd.wellknown |= 1ull << k;
+    int rk = d.key(kResID), tk = d.key(kResType);
+    d.dd.resid_key_bit = rk >= 0 ? 1ull << rk : 0;
+    d.dd.restype_key_bit = tk >= 0 ? 1ull << tk : 0;
+    return KP_OK;
+  }
+};
+
+// ------------------------------------------------------------------------------------------------
+// host requirement algebra on KReqs (same encoding the device uses)
+// ------------------------------------------------------------------------------------------------
+bool Within(const Dict& d, int bit, bool hg, int64_t gt, bool hl, int64_t lt) {
+  if (!hg && !hl) return true;
+  if (!((d.dd.vint_ok[bit / 64] >> (bit % 64)) & 1)) return false;
+  int64_t x = d.vint[bit];
+  if (hg && gt >= x) return false;
+  if (hl && lt <= x) return false;
+  return true;
+}
+int nwords(const Dict& d, int k) { return std::max(1, (d.dd.nval[k] + 63) / 64); }
+
+KReqs Single(const Dict& d, const RawReq& r) {
+  KReqs q;
+  memset(&q, 0, sizeof q);
+  const int k = d.key(r.key);
+  q.present = 1ull << k;
+  if (r.minv >= 0) {
+    q.hmin = 1ull << k;
+    q.minv[k] = r.minv;
+  }
+  auto setvals = [&]() {
+    for (auto& v : r.values) {
+      int b = d.bit(k, v);
+      q.vals[b / 64] |= 1ull << (b % 64);
+    }
+  };
+  switch (r.op) {
+    case KP_OP_IN:
+      setvals();
+      break;
+    case KP_OP_NOT_IN:
+      q.compl_ = 1ull << k;
+      setvals();
+      break;
+    case KP_OP_EXISTS:
+      q.compl_ = 1ull << k;
+      break;
+    case KP_OP_DOES_NOT_EXIST:
+      break;
+    case KP_OP_GT:
+    case KP_OP_LT: {
+      q.compl_ = 1ull << k;
+      int64_t x = 0;
+      Atoi(r.values.empty() ? string() : r.values[0], &x);
+      if (r.op == KP_OP_GT) {
+        q.hgt = 1ull << k;
+        q.gt[k] = x;
+      } else {
+        q.hlt = 1ull << k;
+        q.lt[k] = x;
+      }
+      break;
+    }
+  }
+  return q;
+}
+
+// A = A.Add(B) per key (Requirement.Intersection for shared keys).
+void HostAdd(const Dict& d, KReqs& A, const KReqs& B) {
+  for (int k = 0; k < d.dd.K; k++) {
+    const uint64_t kb = 1ull << k;
+    if (!(B.present & kb)) continue;
+    const int w0 = d.dd.wofs[k], nw = nwords(d, k);
+    const bool bnd = k < KP_MAX_BOUND_KEYS;
+    if (!(A.present & kb)) {
+      A.present |= kb;
+      A.compl_ = (A.compl_ & ~kb) | (B.compl_ & kb);
+      A.hgt = (A.hgt & ~kb) | (B.hgt & kb);
+      A.hlt = (A.hlt & ~kb) | (B.hlt & kb);
+      A.hmin = (A.hmin & ~kb) | (B.hmin & kb);
+      if (bnd) {
+        A.gt[k] = B.gt[k];
+        A.lt[k] = B.lt[k];
+        A.minv[k] = B.minv[k];
+      }
+      for (int w = w0; w < w0 + nw; w++) A.vals[w] = B.vals[w];
+      continue;
+    }
+    const bool c1 = A.compl_ & kb, c2 = B.compl_ & kb;
+    const bool ag = A.hgt & kb, bg = B.hgt & kb, al = A.hlt & kb, bl = B.hlt & kb;
+    const bool hg = ag || bg, hl = al || bl;
+    int64_t gt = 0, lt = 0;
+    if (bnd) {
+      gt = ag && bg ? std::max(A.gt[k], B.gt[k]) : (ag ? A.gt[k] : B.gt[k]);
+      lt = al && bl ? std::min(A.lt[k], B.lt[k]) : (al ? A.lt[k] : B.lt[k]);
+      const bool am = A.hmin & kb, bm = B.hmin & kb;
+      A.minv[k] = am && bm ? std::max(A.minv[k], B.minv[k]) : (am ? A.minv[k] : B.minv[k]);
+    }
+    A.hmin |= B.hmin & kb;
+    if (hg && hl && gt >= lt) {  // DoesNotExist
+      A.compl_ &= ~kb;
+      A.hgt &= ~kb;
+      A.hlt &= ~kb;
+      for (int w = w0; w < w0 + nw; w++) A.vals[w] = 0;
+      continue;
+    }
+    for (int w = w0; w < w0 + nw; w++) {
+      const uint64_t a = A.vals[w], b = B.vals[w];
+      uint64_t v = (c1 && c2) ? (a | b) : c1 ? (b & ~a) : c2 ? (a & ~b) : (a & b);
+      if (hg || hl) {
+        uint64_t m = v, o = 0;
+        while (m) {
+          int bb = __builtin_ctzll(m);
+          m &= m - 1;
+          if (Within(d, w * 64 + bb, hg, gt, hl, lt)) o |= 1ull << bb;
+        }
+        v = o;
+      }
+      A.vals[w] = v;
+    }
+    const bool c = c1 && c2;
+    if (c) {
+      A.compl_ |= kb;
+      if (hg) A.hgt |= kb, A.gt[k] = gt;
+      if (hl) A.hlt |= kb, A.lt[k] = lt;
+    } else {
+      A.compl_ &= ~kb;
+      A.hgt &= ~kb;
+      A.hlt &= ~kb;
+    }
+  }
+}
+
+KReqs Compile(const Dict& d, const RawReqs& rs) {
+  KReqs q;
+  memset(&q, 0, sizeof q);
+  for (auto& r : rs) HostAdd(d, q, Single(d, r));
+  return q;
+}
+bool KeyNonEmptyVals(const Dict& d, const KReqs& q, int k) {
+  for (int w = d.dd.wofs[k]; w < d.dd.wofs[k] + nwords(d, k); w++)
+    if (q.vals[w]) return true;
+  return false;
+}
+uint64_t NegOp(const Dict& d, const KReqs& q) {
+  uint64_t m = 0;
+  for (int k = 0; k < d.dd.K; k++) {
+    if (!((q.present >> k) & 1)) continue;
+    bool c = (q.compl_ >> k) & 1, nz = KeyNonEmptyVals(d, q, k);
+    if ((c && nz) || (!c && !nz)) m |= 1ull << k;
+  }
+  return m;
+}
+bool Has(const Dict& d, const KReqs& q, int k, int bit) {
+  if (!((q.present >> k) & 1)) return true;
+  bool in = (q.vals[bit / 64] >> (bit % 64)) & 1;
+  if ((q.compl_ >> k) & 1) {
+    const bool bnd = k < KP_MAX_BOUND_KEYS;
+    return !in && Within(d, bit, bnd && ((q.hgt >> k) & 1), bnd ? q.gt[k] : 0, bnd && ((q.hlt >> k) & 1),
+                         bnd ? q.lt[k] : 0);
+  }
+  return in;
+}
+
+// ------------------------------------------------------------------------------------------------
+// catalogue compile (per solve dictionary)
+// ------------------------------------------------------------------------------------------------
+struct HostCat {
+  int T = 0;
+  vector<KReqs> treqs;
+  vector<uint64_t> TM, DNE, NOKEY;    // [nbits][TW], [K][TW], [K][TW]
+  vector<int64_t> alloc, cap;         // [R][T]
+  vector<uint64_t> nonneg;            // [TW]
+  vector<int64_t> fit_vals;           // [R][T]
+  vector<int32_t> fit_n;              // [R]
+  vector<uint64_t> fit_mask;          // [R][T][TW]
+  vector<uint64_t> offer_avail;       // [C][TW]
+  vector<double> price;               // [T][C]
+  vector<uint32_t> name_rank;         // [T]
+  vector<uint16_t> code;              // [K][T]
+  vector<uint64_t> multi;             // [K][T]
+  vector<uint64_t> custom_nonneg;     // [T]
+  uint64_t multi_valued = 0;
+};
+
+struct ClassKey {
+  int ct, zone, zid;
+  bool operator<(const ClassKey& o) const { return std::tie(ct, zone, zid) < std::tie(o.ct, o.zone, o.zid); }
+};
+
+int32_t CompileCatalog(const Dict& d, const vector<HostType>& types, int TW, map<ClassKey, int>& classes, HostCat& hc) {
+  const int T = (int)types.size(), K = d.dd.K, NB = d.dd.W * 64;
+  hc.T = T;
+  hc.treqs.resize(T);
+  hc.TM.assign((size_t)NB * TW, 0);
+  hc.DNE.assign((size_t)K * TW, 0);
+  hc.NOKEY.assign((size_t)K * TW, 0);
+  hc.code.assign((size_t)K * T, 0xFFFF);
+  hc.multi.assign((size_t)K * T, 0);
+  hc.custom_nonneg.assign(T, 0);
+  for (int t = 0; t < T; t++) {
+    KReqs q = Compile(d, types[t].reqs);
+    hc.treqs[t] = q;
+    const uint64_t tb = 1ull << (t % 64);
+    const int tw = t / 64;
+    const uint64_t neg = NegOp(d, q);
+    for (int k = 0; k < K; k++) {
+      const uint64_t kb = 1ull << k;
+      if (!(q.present & kb)) {
+        hc.NOKEY[(size_t)k * TW + tw] |= tb;
+        continue;
+      }
+      if ((q.compl_ & kb) || (q.hgt & kb) || (q.hlt & kb))
+        return fail(KP_E_UNSUPPORTED, "instance type %s: requirement %s is not In/DoesNotExist", types[t].name.c_str(),
+                    d.keys[k].c_str());
+      if (!(d.dd.wellknown & kb) && !(neg & kb)) hc.custom_nonneg[t] |= kb;
+      int cnt = 0, last = -1;
+      for (int w = d.dd.wofs[k]; w < d.dd.wofs[k] + nwords(d, k); w++) {
+        uint64_t m = q.vals[w];
+        while (m) {
+          int b = __builtin_ctzll(m);
+          m &= m - 1;
+          int bit = w * 64 + b;
+          hc.TM[(size_t)bit * TW + tw] |= tb;
+          cnt++;
+          last = bit;
+        }
+      }
+      if (cnt == 0) {
+        hc.DNE[(size_t)k * TW + tw] |= tb;
+        hc.code[(size_t)k * T + t] = 0xFFFE;
+      } else if (cnt == 1) {
+        hc.code[(size_t)k * T + t] = (uint16_t)last;
+      } else {
+        if (d.dd.nval[k] > 64) return fail(KP_E_UNSUPPORTED, "multi-valued key %s has > 64 values", d.keys[k].c_str());
+        hc.multi_valued |= kb;
+        hc.code[(size_t)k * T + t] = 0xFFFD;
+        hc.multi[(size_t)k * T + t] = q.vals[d.dd.wofs[k]];
+      }
+    }
+  }
+  for (int k = 0; k < K; k++)  // keys whose types are multi-valued keep multi masks for every type
+    if ((hc.multi_valued >> k) & 1)
+      for (int t = 0; t < T; t++) {
+        uint16_t& c = hc.code[(size_t)k * T + t];
+        if (c < 0xFFFD) {
+          hc.multi[(size_t)k * T + t] = 1ull << (c % 64);
+          c = 0xFFFD;
+        }
+      }
+  // resources
+  hc.alloc.assign((size_t)KP_NRES * T, 0);
+  hc.cap.assign((size_t)KP_NRES * T, 0);
+  hc.nonneg.assign(TW, 0);
+  for (int t = 0; t < T; t++) {
+    bool nn = true;
+    for (int r = 0; r < KP_NRES; r++) {
+      const bool pr = (types[t].cap_present >> r) & 1;
+      const int64_t c = pr ? types[t].cap[r] : 0;
+      const int64_t a = pr ? c - types[t].ovh[r] : 0;  // resources.Subtract(capacity, overhead): capacity keys
+      hc.cap[(size_t)r * T + t] = c;
+      hc.alloc[(size_t)r * T + t] = a;
+      if (pr && a < 0) nn = false;
+    }
+    if (nn) hc.nonneg[t / 64] |= 1ull << (t % 64);
+  }
+  hc.fit_vals.assign((size_t)KP_NRES * T, 0);
+  hc.fit_n.assign(KP_NRES, 0);
+  hc.fit_mask.assign((size_t)KP_NRES * T * TW, 0);
+  for (int r = 0; r < KP_NRES; r++) {
+    vector<int64_t> v(hc.alloc.begin() + (size_t)r * T, hc.alloc.begin() + (size_t)(r + 1) * T);
+    std::sort(v.begin(), v.end());
+    v.erase(std::unique(v.begin(), v.end()), v.end());
+    hc.fit_n[r] = (int)v.size();
+    std::copy(v.begin(), v.end(), hc.fit_vals.begin() + (size_t)r * T);
+    // fit_mask[r][j] = types with alloc >= v[j]: build from the top down
+    vector<uint64_t> acc(TW, 0);
+    vector<std::pair<int64_t, int>> byv;
+    for (int t = 0; t < T; t++) byv.push_back({hc.alloc[(size_t)r * T + t], t});
+    std::sort(byv.begin(), byv.end());
+    int p = T - 1;
+    for (int j = (int)v.size() - 1; j >= 0; j--) {
+      while (p >= 0 && byv[p].first >= v[j]) {
+        acc[byv[p].second / 64] |= 1ull << (byv[p].second % 64);
+        p--;
+      }
+      std::copy(acc.begin(), acc.end(), hc.fit_mask.begin() + ((size_t)r * T + j) * TW);
+    }
+  }
+  // offerings
+  const int C = (int)classes.size();
+  hc.offer_avail.assign((size_t)C * TW, 0);
+  hc.price.assign((size_t)T * C, std::numeric_limits<double>::infinity());
+  const int kct = d.key(kCapType), kz = d.key(kZone), kzid = d.key(kZoneID);
+  for (int t = 0; t < T; t++)
+    for (auto& o : types[t].offs) {
+      ClassKey ck{d.bit(kct, o.ct), o.has_zone ? d.bit(kz, o.zone) : -1, o.has_zid ? d.bit(kzid, o.zid) : -1};
+      const int c = classes.at(ck);
+      if (!o.available) continue;
+      hc.offer_avail[(size_t)c * TW + t / 64] |= 1ull << (t % 64);
+      double& p = hc.price[(size_t)t * C + c];
+      if (o.price < p) p = o.price;
+    }
+  vector<int> idx(T);
+  for (int t = 0; t < T; t++) idx[t] = t;
+  std::sort(idx.begin(), idx.end(), [&](int a, int b) { return types[a].name < types[b].name; });
+  hc.name_rank.assign(T, 0);
+  for (int i = 0; i < T; i++) hc.name_rank[idx[i]] = (uint32_t)i;
+  return KP_OK;
+}
+
+// Pass_k(q_k) over the catalogue (host version, every key of q): NOKEY ∪ ∪_{Has(v)} TM[v] ∪ (negop ? DNE)
+void HostFilterTypes(const Dict& d, const HostCat& hc, const KReqs& q, int TW, const int64_t* total,
+                     vector<uint64_t>& X) {
+  const uint64_t neg = NegOp(d, q);
+  for (int k = 0; k < d.dd.K; k++) {
+    if (!((q.present >> k) & 1)) continue;
+    vector<uint64_t> acc(TW, 0);
+    for (int w = 0; w < TW; w++) acc[w] = hc.NOKEY[(size_t)k * TW + w] | (((neg >> k) & 1) ? hc.DNE[(size_t)k * TW + w] : 0);
+    for (int w = d.dd.wofs[k]; w < d.dd.wofs[k] + nwords(d, k); w++) {
+      uint64_t m = d.dd.validbits[w];
+      while (m) {
+        int b = __builtin_ctzll(m);
+        m &= m - 1;
+        if (Has(d, q, k, w * 64 + b))
+          for (int x = 0; x < TW; x++) acc[x] |= hc.TM[(size_t)(w * 64 + b) * TW + x];
+      }
+    }
+    for (int w = 0; w < TW; w++) X[w] &= acc[w];
+  }
+  // Fits(total, allocatable)
+  for (int t = 0; t < hc.T; t++) {
+    bool ok = (hc.nonneg[t / 64] >> (t % 64)) & 1;
+    for (int r = 0; r < KP_NRES && ok; r++)
+      if (total[r] > 0 && total[r] > hc.alloc[(size_t)r * hc.T + t]) ok = false;
+    if (!ok) X[t / 64] &= ~(1ull << (t % 64));
+  }
+}
+
+uint64_t HostAllowedClasses(const Dict& d, const KReqs& q, const vector<OfferClass>& cls) {
+  const uint64_t neg = NegOp(d, q);
+  const bool res_ok = !(q.present & d.dd.resid_key_bit) || (neg & d.dd.resid_key_bit);
+  const bool rt_ok = !(q.present & d.dd.restype_key_bit) || (neg & d.dd.restype_key_bit);
+  if (!res_ok || !rt_ok) return 0;
+  uint64_t m = 0;
+  auto keyof = [&](int bit) { return (int)d.dd.wkey[bit / 64]; };
+  for (size_t c = 0; c < cls.size(); c++) {
+    bool ok = Has(d, q, keyof(cls[c].ct_bit), cls[c].ct_bit);
+    if (cls[c].zone_bit >= 0) ok = ok && Has(d, q, keyof(cls[c].zone_bit), cls[c].zone_bit);
+    if (cls[c].zid_bit >= 0) ok = ok && Has(d, q, keyof(cls[c].zid_bit), cls[c].zid_bit);
+    if (ok) m |= 1ull << c;
+  }
+  return m;
+}
+
+int CountDistinct(const Dict& d, const HostCat& hc, int k, const vector<int>& types) {
+  std::set<int> vals;
+  for (int t : types) {
+    const KReqs& q = hc.treqs[t];
+    for (int w = d.dd.wofs[k]; w < d.dd.wofs[k] + nwords(d, k); w++) {
+      uint64_t m = q.vals[w];
+      while (m) {
+        int b = __builtin_ctzll(m);
+        m &= m - 1;
+        vals.insert(w * 64 + b);
+      }
+    }
+  }
+  return (int)vals.size();
+}
+bool HostMinValuesOK(const Dict& d, const HostCat& hc, const KReqs& q, const vector<int>& types) {
+  for (int k = 0; k < d.dd.K; k++) {
+    if (!((q.hmin >> k) & 1) || !((q.present >> k) & 1)) continue;
+    if (CountDistinct(d, hc, k, types) < q.minv[k]) return false;
+  }
+  return true;
+}
+
+// ------------------------------------------------------------------------------------------------
+// device buffer arena: everything of one solve in one allocation
+// ------------------------------------------------------------------------------------------------
+struct Blob {
+  vector<uint8_t> host;
+  template <class T>
+  size_t put(const T* p, size_t n) {
+    size_t off = (host.size() + 255) & ~(size_t)255;
+    host.resize(off + n * sizeof(T));
+    if (n) memcpy(host.data() + off, p, n * sizeof(T));
+    return off;
+  }
+  template <class T>
+  size_t put(const vector<T>& v) {
+    return put(v.data(), v.size());
+  }
+  size_t reserve(size_t bytes) {
+    size_t off = (host.size() + 255) & ~(size_t)255;
+    host.resize(off + bytes);
+    return off;
+  }
+};
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t n = 0;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
+
+}  // namespace
+
+struct kp_solve_result {
+  vector<int32_t> placement;
+  struct NC {
+    uint32_t nodepool, n_remaining;
+    vector<uint32_t> pods, options;
+    kp_resource_list requests;
+  };
+  vector<NC> ncs;
+  kp_solve_stats stats;
+};
+
+extern "C" {
+
+const char* kp_last_error(void) { return g_err.c_str(); }
+int32_t kp_abi_version(void) { return KP_ABI_VERSION; }
+
+int32_t kp_ctx_create(const kp_options* opts, kp_ctx** out) {
+  if (!out) return fail(KP_E_INVAL, "out is null");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n == 0) return fail(KP_E_DEVICE, "no HIP device: %s", hipGetErrorString(e));
+  auto* c = new kp_ctx();
+  c->opts = opts ? *opts : kp_options{0.075, 0, 0};
+  c->device = c->opts.device;
+  if (c->device < 0 || c->device >= n) {
+    delete c;
+    return fail(KP_E_INVAL, "device %d out of range", opts ? opts->device : 0);
+  }
+  if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+    delete c;
+    return fail(KP_E_DEVICE, "stream/event creation failed");
+  }
+  *out = c;
+  return KP_OK;
+}
+void kp_ctx_destroy(kp_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int32_t kp_catalog_upload(kp_ctx* ctx, const kp_catalog_desc* desc, uint64_t seqnum, kp_catalog** out) {
+  if (!ctx || !desc || !out) return fail(KP_E_INVAL, "null argument");
+  if (desc->n_types > 4096) return fail(KP_E_UNSUPPORTED, "%u instance types (max 4096)", desc->n_types);
+  auto* c = new kp_catalog();
+  c->ctx = ctx;
+  c->seqnum = seqnum;
+  for (uint32_t i = 0; i < desc->n_types; i++) {
+    const kp_instance_type& t = desc->types[i];
+    HostType h;
+    h.name = t.name ? t.name : "";
+    h.reqs = ParseReqs(t.requirements);
+    for (int r = 0; r < KP_NRES; r++) {
+      h.cap[r] = t.capacity.milli[r];
+      h.ovh[r] = (t.overhead.present >> r) & 1 ? t.overhead.milli[r] : 0;
+    }
+    h.cap_present = t.capacity.present;
+    for (uint32_t j = 0; j < t.n_offerings; j++) {
+      const kp_offering& o = t.offerings[j];
+      if (o.reservation_id || o.reservation_type) {
+        delete c;
+        return fail(KP_E_UNSUPPORTED, "reserved offerings (ABI v1)");
+      }
+      h.offs.push_back({o.capacity_type ? o.capacity_type : "", o.zone ? o.zone : "", o.zone_id ? o.zone_id : "",
+                        o.zone != nullptr, o.zone_id != nullptr, o.price, o.available != 0});
+    }
+    c->types.push_back(std::move(h));
+  }
+  *out = c;
+  return KP_OK;
+}
+uint64_t kp_catalog_seqnum(const kp_catalog* c) { return c ? c->seqnum : 0; }
+uint32_t kp_catalog_size(const kp_catalog* c) { return c ? (uint32_t)c->types.size() : 0; }
+void kp_catalog_destroy(kp_catalog* c) { delete c; }
+
+// instancetype.NewInstanceType capacity + Overhead.Total() for the AL2023 family (R:types.go:313-598).
+int32_t kp_instance_type_resolve(const kp_options* opts, const kp_ec2_info* info, const kp_nodeclass* nc,
+                                 kp_resource_list* capacity, kp_resource_list* overhead) {
+  if (!opts || !info || !capacity || !overhead) return fail(KP_E_INVAL, "null argument");
+  auto mi = [](int64_t x) { return x * 1048576ll * 1000ll; };
+  auto eniPods = [&](int reserved) -> int64_t {  // ENILimitedPods (R:types.go:461-475)
+    int64_t usable = std::max<int64_t>((int64_t)info->max_enis - reserved, 0);
+    return usable == 0 ? 0 : usable * ((int64_t)info->ipv4_per_eni - 1) + 2;
+  };
+  memset(capacity, 0, sizeof *capacity);
+  memset(overhead, 0, sizeof *overhead);
+  auto set = [](kp_resource_list* l, int r, int64_t v) {
+    l->milli[r] = v;
+    l->present |= 1u << r;
+  };
+  set(capacity, KP_RES_CPU, (int64_t)info->vcpu * 1000);
+  int64_t mib = info->memory_mib;
+  if (info->arch && strcmp(info->arch, "arm64") == 0) mib -= 64;  // Graviton CMA (R:types.go:339-342)
+  const int64_t ovMiB = (int64_t)std::ceil((double)(mib * 1048576ll) * opts->vm_memory_overhead_percent / 1024 / 1024);
+  set(capacity, KP_RES_MEMORY, mi(mib - ovMiB));
+  const int64_t storage = 20ll << 30;  // AL2023 default /dev/xvda, no BDMs (R:amifamily/al2023.go:98-108)
+  set(capacity, KP_RES_EPHEMERAL_STORAGE, storage * 1000);
+  int64_t pods = (nc && nc->max_pods >= 0) ? nc->max_pods : eniPods(opts->reserved_enis);
+  if (nc && nc->pods_per_core > 0) pods = std::min<int64_t>((int64_t)nc->pods_per_core * info->vcpu, pods);
+  set(capacity, KP_RES_PODS, pods * 1000);
+  set(capacity, KP_RES_POD_ENI, (info->in_limits_table && info->trunking) ? (int64_t)info->branch_enis * 1000 : 0);
+  const string gm = info->gpu_manufacturer ? info->gpu_manufacturer : "";
+  set(capacity, KP_RES_NVIDIA_GPU, gm == "nvidia" ? info->gpu_count * 1000ll : 0);
+  set(capacity, KP_RES_AMD_GPU, gm == "amd" ? info->gpu_count * 1000ll : 0);
+  set(capacity, KP_RES_NEURON, (int64_t)info->neuron_devices * 1000);
+  set(capacity, KP_RES_NEURONCORE, (int64_t)info->neuron_devices * info->neuron_cores_per_device * 1000);
+  set(capacity, KP_RES_GAUDI, gm == "habana" ? info->gpu_count * 1000ll : 0);
+  set(capacity, KP_RES_EFA, (int64_t)info->efa * 1000);
+  // kube-reserved (AL2023 UsesENILimitedMemoryOverhead) + eviction threshold (R:types.go:492-551)
+  int64_t cpuOverhead = 0;
+  const struct {
+    int64_t s, e;
+    double p;
+  } rg[4] = {{0, 1000, 0.06}, {1000, 2000, 0.01}, {2000, 4000, 0.005}, {4000, 1ll << 31, 0.0025}};
+  const int64_t cpuM = capacity->milli[KP_RES_CPU];
+  for (auto& x : rg)
+    if (cpuM >= x.s) cpuOverhead += (int64_t)((double)(cpuM < x.e ? cpuM - x.s : x.e - x.s) * x.p);
+  set(overhead, KP_RES_CPU, cpuOverhead);
+  set(overhead, KP_RES_MEMORY, mi(11 * eniPods(0) + 255) + mi(100));
+  set(overhead, KP_RES_EPHEMERAL_STORAGE, (1ll << 30) * 1000 + (int64_t)std::ceil((double)storage / 100 * 10) * 1000);
+  return KP_OK;
+}
+
+}  // extern "C"
+
+// ==================================================================================================
+// Solve
+// ==================================================================================================
+namespace {
+
+struct Compiled {
+  Dict d;
+  int TW = 1, C = 0;
+  vector<HostCat> cats;
+  vector<OfferClass> classes;
+  // templates (ordered)
+  vector<int> tmpl_nodepool;
+  vector<KReqs> tmpl_reqs;
+  vector<int32_t> tmpl_taintset, tmpl_catalog;
+  vector<uint64_t> tmpl_X;
+  vector<int64_t> tmpl_daemon, tmpl_remaining;
+  vector<uint32_t> tmpl_limit_present;
+  // shapes
+  vector<int32_t> shape_level_base, shape_nlevels;
+  vector<KReqs> shape_reqs;
+  vector<uint64_t> shape_negop, shape_tolerates;
+  vector<int64_t> shape_requests;
+  vector<uint64_t> pvp;
+  vector<int32_t> pvp_base, pvp_slot;
+  // existing (sorted)
+  vector<int> ex_input;
+  vector<KReqs> ex_reqs;
+  vector<int32_t> ex_taintset;
+  vector<int64_t> ex_available, ex_requests;
+  // pods
+  vector<int32_t> pod_shape, queue;
+};
+
+struct TaintT {
+  string key, value;
+  int effect;
+  bool operator<(const TaintT& o) const { return std::tie(key, value, effect) < std::tie(o.key, o.value, o.effect); }
+};
+
+int32_t CompileSolve(const kp_solve_in* in, Compiled& cp) {
+  if (in->n_catalogs == 0 || !in->catalogs) return fail(KP_E_INVAL, "no catalogues");
+  vector<const kp_catalog*> cats(in->catalogs, in->catalogs + in->n_catalogs);
+  DictBuilder db;
+  int maxT = 1;
+  for (auto* c : cats) {
+    if (!c) return fail(KP_E_INVAL, "null catalogue");
+    maxT = std::max(maxT, (int)c->types.size());
+    for (auto& t : c->types) {
+      db.addReqs(t.reqs);
+      for (auto& o : t.offs) {
+        db.addLabel(kCapType, o.ct);
+        if (o.has_zone) db.addLabel(kZone, o.zone);
+        if (o.has_zid) db.addLabel(kZoneID, o.zid);
+      }
+    }
+  }
+  db.bounded[kResID];
+  db.bounded[kResType];
+  // NodePools
+  vector<RawReqs> np_reqs(in->n_nodepools);
+  vector<vector<TaintT>> np_taints(in->n_nodepools);
+  for (uint32_t i = 0; i < in->n_nodepools; i++) {
+    const kp_nodepool& np = in->nodepools[i];
+    if (np.catalog >= in->n_catalogs) return fail(KP_E_INVAL, "nodepool %u: catalogue %u", i, np.catalog);
+    RawReqs r = ParseReqs(np.requirements);
+    RawReqs l = LabelReqs(np.labels, np.n_labels, false);
+    r.insert(r.end(), l.begin(), l.end());
+    r.push_back({kNodePool, KP_OP_IN, {np.name ? np.name : ""}, -1});
+    for (auto& x : r)
+      if (x.key == kHostname) return fail(KP_E_UNSUPPORTED, "hostname requirement on nodepool");
+    db.addReqs(r);
+    np_reqs[i] = std::move(r);
+    for (uint32_t j = 0; j < np.n_taints; j++)
+      np_taints[i].push_back({np.taints[j].key ? np.taints[j].key : "", np.taints[j].value ? np.taints[j].value : "",
+                              np.taints[j].effect});
+  }
+  // shapes -> relaxation levels (NewPodRequirements after successive Preferences.Relax)
+  vector<vector<RawReqs>> levels(in->n_shapes);
+  for (uint32_t s = 0; s < in->n_shapes; s++) {
+    const kp_pod_shape& sh = in->shapes[s];
+    if (sh.n_topology_spread) return fail(KP_E_UNSUPPORTED, "topology spread constraints (ABI v1)");
+    if (sh.n_preferred_terms > 12) return fail(KP_E_UNSUPPORTED, "> 12 preferred terms");
+    RawReqs ns = LabelReqs(sh.node_selector, sh.n_node_selector, false);
+    vector<RawReqs> req;
+    for (uint32_t j = 0; j < sh.n_required_terms; j++) req.push_back(ParseReqs(sh.required_terms[j]));
+    vector<std::pair<int, RawReqs>> pref;
+    for (uint32_t j = 0; j < sh.n_preferred_terms; j++)
+      pref.push_back({sh.preferred_terms[j].weight, ParseReqs(sh.preferred_terms[j].preference)});
+    auto byw = [](const std::pair<int, RawReqs>& a, const std::pair<int, RawReqs>& b) { return a.first > b.first; };
+    std::stable_sort(pref.begin(), pref.end(), byw);  // sort.Slice on <= 12 = insertion sort (stable)
+    for (;;) {
+      RawReqs r = ns;
+      if (!pref.empty()) r.insert(r.end(), pref[0].second.begin(), pref[0].second.end());
+      if (!req.empty()) r.insert(r.end(), req[0].begin(), req[0].end());
+      for (auto& x : r)
+        if (x.key == kHostname) return fail(KP_E_UNSUPPORTED, "hostname requirement on pod");
+      db.addReqs(r);
+      levels[s].push_back(std::move(r));
+      if (req.size() > 1) req.erase(req.begin());
+      else if (!pref.empty()) pref.erase(pref.begin());
+      else break;
+    }
+  }
+  // existing nodes
+  for (uint32_t i = 0; i < in->n_existing; i++) {
+    const kp_existing_node& e = in->existing[i];
+    for (auto& r : LabelReqs(e.labels, e.n_labels, true)) db.addLabel(r.key, r.values[0]);
+  }
+  int32_t rc = db.build(cp.d);
+  if (rc) return rc;
+  const Dict& d = cp.d;
+  const int TW = (maxT + 63) / 64;
+  cp.TW = TW;
+  cp.d.dd.TW = TW;
+  cp.d.dd.T = maxT;
+  // offering classes
+  map<ClassKey, int> classes;
+  for (auto* c : cats)
+    for (auto& t : c->types)
+      for (auto& o : t.offs) {
+        ClassKey ck{d.bit(d.key(kCapType), o.ct), o.has_zone ? d.bit(d.key(kZone), o.zone) : -1, o.has_zid ? d.bit(d.key(kZoneID), o.zid) : -1};
+        if (!classes.count(ck)) {
+          int id = (int)classes.size();
+          classes[ck] = id;
+        }
+      }
+  if (classes.size() > KP_MAX_CLASSES) return fail(KP_E_UNSUPPORTED, "%zu offering classes", classes.size());
+  cp.C = (int)classes.size();
+  cp.classes.resize(cp.C);
+  for (auto& kv : classes) cp.classes[kv.second] = {kv.first.ct, kv.first.zone, kv.first.zid, 0};
+  cp.d.dd.C = cp.C;
+  cp.cats.resize(cats.size());
+  uint64_t catalog_keys = 0, multi = 0;
+  for (size_t i = 0; i < cats.size(); i++) {
+    rc = CompileCatalog(d, cats[i]->types, TW, classes, cp.cats[i]);
+    if (rc) return rc;
+    multi |= cp.cats[i].multi_valued;
+    for (int k = 0; k < d.dd.K; k++) {
+      bool any = false;
+      for (int w = 0; w < TW && !any; w++) any = ~cp.cats[i].NOKEY[(size_t)k * TW + w] != 0;
+      // NOKEY covers every type only if no type has the key; mask padding bits
+      bool all = true;
+      for (int t = 0; t < cp.cats[i].T && all; t++)
+        if (!((cp.cats[i].NOKEY[(size_t)k * TW + t / 64] >> (t % 64)) & 1)) all = false;
+      if (!all) catalog_keys |= 1ull << k;
+      (void)any;
+    }
+  }
+  cp.d.dd.catalog_keys = catalog_keys;
+  cp.d.dd.single_valued = catalog_keys & ~multi;
+  for (auto& hc : cp.cats) hc.multi_valued = multi;
+  // taint sets
+  map<vector<TaintT>, int> tsets;
+  auto tset = [&](vector<TaintT> v) {
+    std::sort(v.begin(), v.end());
+    auto it = tsets.find(v);
+    if (it != tsets.end()) return it->second;
+    int id = (int)tsets.size();
+    tsets[v] = id;
+    return id;
+  };
+  // templates: weight desc, name asc; pre-filter options with empty requests (upstream NewScheduler)
+  vector<int> order(in->n_nodepools);
+  for (uint32_t i = 0; i < in->n_nodepools; i++) order[i] = (int)i;
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+    const kp_nodepool &x = in->nodepools[a], &y = in->nodepools[b];
+    if (x.weight != y.weight) return x.weight > y.weight;
+    return strcmp(x.name ? x.name : "", y.name ? y.name : "") < 0;
+  });
+  for (int i : order) {
+    const kp_nodepool& np = in->nodepools[i];
+    KReqs q = Compile(d, np_reqs[i]);
+    const HostCat& hc = cp.cats[np.catalog];
+    vector<uint64_t> X(TW, 0);
+    for (int t = 0; t < hc.T; t++) X[t / 64] |= 1ull << (t % 64);
+    int64_t zero[KP_NRES] = {0};
+    HostFilterTypes(d, hc, q, TW, zero, X);
+    const uint64_t cls = HostAllowedClasses(d, q, cp.classes);
+    vector<uint64_t> offer(TW, 0);
+    for (int c = 0; c < cp.C; c++)
+      if ((cls >> c) & 1)
+        for (int w = 0; w < TW; w++) offer[w] |= hc.offer_avail[(size_t)c * TW + w];
+    bool any = false;
+    for (int w = 0; w < TW; w++) any |= (X[w] &= offer[w]) != 0;
+    if (any && q.hmin) {
+      vector<int> ts;
+      for (int t = 0; t < hc.T; t++)
+        if ((X[t / 64] >> (t % 64)) & 1) ts.push_back(t);
+      if (!HostMinValuesOK(d, hc, q, ts)) any = false;
+    }
+    if (!any) continue;  // "skipping, nodepool requirements filtered out all instance types"
+    cp.tmpl_nodepool.push_back(i);
+    cp.tmpl_reqs.push_back(q);
+    cp.tmpl_taintset.push_back(tset(np_taints[i]));
+    cp.tmpl_catalog.push_back((int32_t)np.catalog);
+    cp.tmpl_X.insert(cp.tmpl_X.end(), X.begin(), X.end());
+    for (int r = 0; r < KP_NRES; r++) {
+      cp.tmpl_daemon.push_back((np.daemon_requests.present >> r) & 1 ? np.daemon_requests.milli[r] : 0);
+      cp.tmpl_remaining.push_back((np.limits.present >> r) & 1 ? np.limits.milli[r] : 0);
+    }
+    cp.tmpl_limit_present.push_back(np.limits.present);
+  }
+  // existing nodes: initialized first, then by name
+  vector<int> ex(in->n_existing);
+  for (uint32_t i = 0; i < in->n_existing; i++) ex[i] = (int)i;
+  std::stable_sort(ex.begin(), ex.end(), [&](int a, int b) {
+    const kp_existing_node &x = in->existing[a], &y = in->existing[b];
+    if ((x.initialized != 0) != (y.initialized != 0)) return x.initialized != 0;
+    return strcmp(x.name ? x.name : "", y.name ? y.name : "") < 0;
+  });
+  for (int i : ex) {
+    const kp_existing_node& e = in->existing[i];
+    cp.ex_input.push_back(i);
+    cp.ex_reqs.push_back(Compile(d, LabelReqs(e.labels, e.n_labels, true)));
+    vector<TaintT> ts;
+    for (uint32_t j = 0; j < e.n_taints; j++)
+      ts.push_back({e.taints[j].key ? e.taints[j].key : "", e.taints[j].value ? e.taints[j].value : "", e.taints[j].effect});
+    cp.ex_taintset.push_back(tset(ts));
+    for (int r = 0; r < KP_NRES; r++) {
+      cp.ex_available.push_back((e.available.present >> r) & 1 ? e.available.milli[r] : 0);
+      cp.ex_requests.push_back((e.requests.present >> r) & 1 ? e.requests.milli[r] : 0);
+    }
+  }
+  if (tsets.size() > 64) return fail(KP_E_UNSUPPORTED, "%zu distinct taint sets (max 64)", tsets.size());
+  // shapes: levels, negop, tolerations, requests, per-catalogue PVP rows
+  int sl = 0;
+  for (uint32_t s = 0; s < in->n_shapes; s++) {
+    const kp_pod_shape& sh = in->shapes[s];
+    cp.shape_level_base.push_back(sl);
+    cp.shape_nlevels.push_back((int32_t)levels[s].size());
+    for (int r = 0; r < KP_NRES; r++) cp.shape_requests.push_back((sh.requests.present >> r) & 1 ? sh.requests.milli[r] : 0);
+    uint64_t tol = 0;
+    for (auto& kv : tsets) {
+      bool all = true;
+      for (auto& taint : kv.first) {  // Taints.ToleratesPod
+        bool ok = false;
+        for (uint32_t j = 0; j < sh.n_tolerations && !ok; j++) {
+          const kp_toleration& t = sh.tolerations[j];
+          const string tk = t.key ? t.key : "", tv = t.value ? t.value : "";
+          if (t.effect != KP_EFFECT_ANY && t.effect != taint.effect) continue;
+          if (!tk.empty() && tk != taint.key) continue;
+          if (t.op == KP_TOL_EQUAL) ok = tv == taint.value;
+          else if (t.op == KP_TOL_EXISTS) ok = true;
+        }
+        if (!ok) all = false;
+      }
+      if (all) tol |= 1ull << kv.second;
+    }
+    cp.shape_tolerates.push_back(tol);
+    for (auto& lv : levels[s]) {
+      KReqs q = Compile(d, lv);
+      cp.shape_reqs.push_back(q);
+      cp.shape_negop.push_back(NegOp(d, q));
+      vector<int32_t> slots(KP_MAX_KEYS, 0);
+      for (size_t ci = 0; ci < cp.cats.size(); ci++) {
+        const HostCat& hc = cp.cats[ci];
+        cp.pvp_base.push_back((int32_t)(cp.pvp.size() / TW));
+        int row = 0;
+        for (int k = 0; k < d.dd.K; k++) {
+          if (!((q.present >> k) & 1) || !((cp.d.dd.single_valued >> k) & 1)) continue;
+          vector<uint64_t> acc(hc.NOKEY.begin() + (size_t)k * TW, hc.NOKEY.begin() + (size_t)(k + 1) * TW);
+          for (int w = d.dd.wofs[k]; w < d.dd.wofs[k] + nwords(d, k); w++) {
+            uint64_t m = d.dd.validbits[w];
+            while (m) {
+              int b = __builtin_ctzll(m);
+              m &= m - 1;
+              if (Has(d, q, k, w * 64 + b))
+                for (int x = 0; x < TW; x++) acc[x] |= hc.TM[(size_t)(w * 64 + b) * TW + x];
+            }
+          }
+          cp.pvp.insert(cp.pvp.end(), acc.begin(), acc.end());
+          slots[k] = row++;  // same key order for every catalogue -> same relative slot
+        }
+      }
+      cp.pvp_slot.insert(cp.pvp_slot.end(), slots.begin(), slots.end());
+      sl++;
+    }
+  }
+  if (cp.pvp.empty()) cp.pvp.assign(TW, 0);
+  // pods: Queue order byCPUAndMemoryDescending (cpu desc, memory desc, creation asc, uid asc)
+  cp.pod_shape.resize(in->n_pods);
+  cp.queue.resize(in->n_pods);
+  for (uint32_t p = 0; p < in->n_pods; p++) {
+    if (in->pods[p].shape >= in->n_shapes) return fail(KP_E_INVAL, "pod %u: shape %u", p, in->pods[p].shape);
+    cp.pod_shape[p] = (int32_t)in->pods[p].shape;
+    cp.queue[p] = (int32_t)p;
+  }
+  std::sort(cp.queue.begin(), cp.queue.end(), [&](int a, int b) {
+    const int64_t* ra = &cp.shape_requests[(size_t)cp.pod_shape[a] * KP_NRES];
+    const int64_t* rb = &cp.shape_requests[(size_t)cp.pod_shape[b] * KP_NRES];
+    if (ra[KP_RES_CPU] != rb[KP_RES_CPU]) return ra[KP_RES_CPU] > rb[KP_RES_CPU];
+    if (ra[KP_RES_MEMORY] != rb[KP_RES_MEMORY]) return ra[KP_RES_MEMORY] > rb[KP_RES_MEMORY];
+    if (in->pods[a].creation_unix != in->pods[b].creation_unix) return in->pods[a].creation_unix < in->pods[b].creation_unix;
+    return in->pods[a].uid_key < in->pods[b].uid_key;
+  });
+  return KP_OK;
+}
+
+// Lays out dict + catalogues in `blob`; fills `catoffs` with the device DevCatalog array offset.
+struct CatOffsets {
+  size_t TM, DNE, NOKEY, alloc, cap, nonneg, fit_vals, fit_n, fit_mask, cls, offer, price, rank, code, multi, custom;
+};
+
+void PutCatalogs(Blob& blob, const Compiled& cp, vector<CatOffsets>& offs) {
+  for (auto& hc : cp.cats) {
+    CatOffsets o;
+    o.TM = blob.put(hc.TM);
+    o.DNE = blob.put(hc.DNE);
+    o.NOKEY = blob.put(hc.NOKEY);
+    o.alloc = blob.put(hc.alloc);
+    o.cap = blob.put(hc.cap);
+    o.nonneg = blob.put(hc.nonneg);
+    o.fit_vals = blob.put(hc.fit_vals);
+    o.fit_n = blob.put(hc.fit_n);
+    o.fit_mask = blob.put(hc.fit_mask);
+    o.cls = blob.put(cp.classes);
+    o.offer = blob.put(hc.offer_avail);
+    o.price = blob.put(hc.price);
+    o.rank = blob.put(hc.name_rank);
+    o.code = blob.put(hc.code);
+    o.multi = blob.put(hc.multi);
+    o.custom = blob.put(hc.custom_nonneg);
+    offs.push_back(o);
+  }
+}
+vector<DevCatalog> DevCats(uint8_t* base, const Compiled& cp, const vector<CatOffsets>& offs) {
+  vector<DevCatalog> out;
+  for (size_t i = 0; i < offs.size(); i++) {
+    const CatOffsets& o = offs[i];
+    DevCatalog c;
+    c.TM = (const uint64_t*)(base + o.TM);
+    c.DNE = (const uint64_t*)(base + o.DNE);
+    c.NOKEY = (const uint64_t*)(base + o.NOKEY);
+    c.vint = nullptr;
+    c.alloc = (const int64_t*)(base + o.alloc);
+    c.cap = (const int64_t*)(base + o.cap);
+    c.nonneg = (const uint64_t*)(base + o.nonneg);
+    c.fit_vals = (const int64_t*)(base + o.fit_vals);
+    c.fit_n = (const int32_t*)(base + o.fit_n);
+    c.fit_mask = (const uint64_t*)(base + o.fit_mask);
+    c.cls = (const OfferClass*)(base + o.cls);
+    c.offer_avail = (const uint64_t*)(base + o.offer);
+    c.price = (const double*)(base + o.price);
+    c.name_rank = (const uint32_t*)(base + o.rank);
+    c.code = (const uint16_t*)(base + o.code);
+    c.multi = (const uint64_t*)(base + o.multi);
+    c.custom_nonneg = (const uint64_t*)(base + o.custom);
+    c.multi_valued = cp.cats[i].multi_valued;
+    out.push_back(c);
+  }
+  return out;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t kp_solve(kp_ctx* ctx, const kp_solve_in* in, kp_solve_result** out) {
+  auto t0 = std::chrono::steady_clock::now();
+  if (!ctx || !in || !out) return fail(KP_E_INVAL, "null argument");
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device));
+  auto cp = std::make_unique<Compiled>();
+  int32_t rc = CompileSolve(in, *cp);
+  if (rc) return rc;
+  const Dict& d = cp->d;
+  const int TW = cp->TW, P = (int)in->n_pods, NT = (int)cp->tmpl_reqs.size(), E = (int)cp->ex_reqs.size();
+  const int SLn = (int)cp->shape_reqs.size();
+  const int Pc = std::max(P, 1);
+
+  Blob blob;
+  const size_t o_dict = blob.put(&cp->d.dd, 1);
+  const size_t o_vint = blob.put(cp->d.vint);
+  vector<CatOffsets> coffs;
+  PutCatalogs(blob, *cp, coffs);
+  const size_t o_cats = blob.reserve(sizeof(DevCatalog) * coffs.size());
+  const size_t o_pod_shape = blob.put(cp->pod_shape);
+  vector<int32_t> zeros_p(Pc, 0);
+  const size_t o_pod_level = blob.put(zeros_p);
+  const size_t o_queue = blob.put(cp->queue);
+  const size_t o_lastlen = blob.put(zeros_p);
+  const size_t o_lastlen_ep = blob.put(zeros_p);
+  const size_t o_slb = blob.put(cp->shape_level_base);
+  const size_t o_snl = blob.put(cp->shape_nlevels);
+  const size_t o_sreqs = blob.put(cp->shape_reqs);
+  const size_t o_sneg = blob.put(cp->shape_negop);
+  const size_t o_sreq = blob.put(cp->shape_requests);
+  const size_t o_stol = blob.put(cp->shape_tolerates);
+  const size_t o_pvp = blob.put(cp->pvp);
+  const size_t o_pvpb = blob.put(cp->pvp_base);
+  const size_t o_pvps = blob.put(cp->pvp_slot);
+  const size_t o_treqs = blob.put(cp->tmpl_reqs);
+  const size_t o_tts = blob.put(cp->tmpl_taintset);
+  const size_t o_tcat = blob.put(cp->tmpl_catalog);
+  const size_t o_tX = blob.put(cp->tmpl_X);
+  const size_t o_tdm = blob.put(cp->tmpl_daemon);
+  const size_t o_tlp = blob.put(cp->tmpl_limit_present);
+  const size_t o_trem = blob.put(cp->tmpl_remaining);
+  const size_t o_exr = blob.put(cp->ex_reqs);
+  const size_t o_exts = blob.put(cp->ex_taintset);
+  const size_t o_exav = blob.put(cp->ex_available);
+  const size_t o_exrq = blob.put(cp->ex_requests);
+  const size_t host_bytes = blob.host.size();
+  // device-only regions (not copied)
+  const size_t o_ncr = blob.reserve(sizeof(KReqs) * Pc);
+  const size_t o_ncX = blob.reserve(sizeof(uint64_t) * (size_t)Pc * TW);
+  const size_t o_ncrq = blob.reserve(sizeof(int64_t) * (size_t)Pc * KP_NRES);
+  const size_t o_nct = blob.reserve(sizeof(int32_t) * Pc);
+  const size_t o_npods = blob.reserve(sizeof(int32_t) * Pc);
+  const size_t o_order = blob.reserve(sizeof(int32_t) * Pc);
+  const size_t o_place = blob.reserve(sizeof(int32_t) * Pc);
+  const size_t o_events = blob.reserve(sizeof(int32_t) * Pc);
+  const size_t o_stats = blob.reserve(sizeof(uint64_t) * 8);
+  const int opt_stride = in->max_instance_types ? (int)in->max_instance_types : std::max(1, d.dd.T);
+  const size_t o_opts = blob.reserve(sizeof(uint32_t) * (size_t)Pc * opt_stride);
+  const size_t o_nrem = blob.reserve(sizeof(uint32_t) * Pc);
+  const size_t o_nopt = blob.reserve(sizeof(uint32_t) * Pc);
+  const size_t total_bytes = blob.host.size();
+
+  DevBuf buf;
+  HIPCHK(hipMalloc(&buf.p, total_bytes));
+  uint8_t* base = (uint8_t*)buf.p;
+  {
+    vector<DevCatalog> dc = DevCats(base, *cp, coffs);
+    memcpy(blob.host.data() + o_cats, dc.data(), sizeof(DevCatalog) * dc.size());
+  }
+  HIPCHK(hipMemcpyAsync(base, blob.host.data(), host_bytes, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipMemsetAsync(base + o_stats, 0, sizeof(uint64_t) * 8, ctx->stream));
+  HIPCHK(hipMemsetAsync(base + o_npods, 0, sizeof(int32_t) * Pc, ctx->stream));
+
+  SolveArgs a;
+  memset(&a, 0, sizeof a);
+  a.dict = (const DevDict*)(base + o_dict);
+  a.cats = (const DevCatalog*)(base + o_cats);
+  a.n_catalogs = (int32_t)coffs.size();
+  a.vint = (const int64_t*)(base + o_vint);
+  a.n_pods = P;
+  a.pod_shape = (const int32_t*)(base + o_pod_shape);
+  a.pod_level = (int32_t*)(base + o_pod_level);
+  a.queue = (int32_t*)(base + o_queue);
+  a.lastlen = (int32_t*)(base + o_lastlen);
+  a.lastlen_epoch = (int32_t*)(base + o_lastlen_ep);
+  a.shape_level_base = (const int32_t*)(base + o_slb);
+  a.shape_nlevels = (const int32_t*)(base + o_snl);
+  a.shape_reqs = base + o_sreqs;
+  a.shape_negop = (const uint64_t*)(base + o_sneg);
+  a.shape_requests = (const int64_t*)(base + o_sreq);
+  a.shape_tolerates = (const uint64_t*)(base + o_stol);
+  a.shape_pvp = (const uint64_t*)(base + o_pvp);
+  a.pvp_base = (const int32_t*)(base + o_pvpb);
+  a.pvp_slot = (const int32_t*)(base + o_pvps);
+  a.n_tmpl = NT;
+  a.tmpl_reqs = base + o_treqs;
+  a.tmpl_taintset = (const int32_t*)(base + o_tts);
+  a.tmpl_catalog = (const int32_t*)(base + o_tcat);
+  a.tmpl_X = (const uint64_t*)(base + o_tX);
+  a.tmpl_daemon = (const int64_t*)(base + o_tdm);
+  a.tmpl_limit_present = (const uint32_t*)(base + o_tlp);
+  a.tmpl_remaining = (int64_t*)(base + o_trem);
+  a.n_existing = E;
+  a.ex_reqs = base + o_exr;
+  a.ex_taintset = (const int32_t*)(base + o_exts);
+  a.ex_available = (const int64_t*)(base + o_exav);
+  a.ex_requests = (int64_t*)(base + o_exrq);
+  a.nc_reqs = base + o_ncr;
+  a.nc_X = (uint64_t*)(base + o_ncX);
+  a.nc_requests = (int64_t*)(base + o_ncrq);
+  a.nc_tmpl = (int32_t*)(base + o_nct);
+  a.g_npods = (int32_t*)(base + o_npods);
+  a.g_order = (int32_t*)(base + o_order);
+  const int sort_cap = 8192;
+  a.sort_in_lds = P <= sort_cap ? 1 : 0;
+  a.sort_cap = sort_cap;
+  a.placement = (int32_t*)(base + o_place);
+  a.events = (int32_t*)(base + o_events);
+  a.stats = (uint64_t*)(base + o_stats);
+  (void)SLn;
+  const size_t dyn = a.sort_in_lds ? (size_t)2 * sort_cap * sizeof(int32_t) : 0;
+  HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
+  HIPCHK(launch_solve(a, 8, dyn, ctx->stream));
+  uint64_t stats[8];
+  HIPCHK(hipMemcpyAsync(stats, base + o_stats, sizeof stats, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  const int n_nc = (int)stats[3];
+  FinalizeArgs f;
+  f.dict = a.dict;
+  f.cats = a.cats;
+  f.vint = a.vint;
+  f.n_nc = n_nc;
+  f.nc_tmpl = a.nc_tmpl;
+  f.tmpl_catalog = a.tmpl_catalog;
+  f.nc_reqs = a.nc_reqs;
+  f.nc_X = a.nc_X;
+  f.max_types = (int32_t)in->max_instance_types;
+  f.opt_stride = opt_stride;
+  f.out_options = (uint32_t*)(base + o_opts);
+  f.out_n_remaining = (uint32_t*)(base + o_nrem);
+  f.out_n_options = (uint32_t*)(base + o_nopt);
+  HIPCHK(launch_finalize(f, ctx->stream));
+  HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));
+
+  auto* res = new kp_solve_result();
+  std::unique_ptr<kp_solve_result> guard(res);
+  res->placement.assign(P, -1);
+  vector<int32_t> place(Pc), events(Pc), nct(std::max(n_nc, 1));
+  vector<int64_t> ncrq((size_t)std::max(n_nc, 1) * KP_NRES);
+  vector<uint32_t> opts((size_t)std::max(n_nc, 1) * opt_stride), nrem(std::max(n_nc, 1)), nopt(std::max(n_nc, 1));
+  HIPCHK(hipMemcpyAsync(place.data(), base + o_place, sizeof(int32_t) * Pc, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipMemcpyAsync(events.data(), base + o_events, sizeof(int32_t) * Pc, hipMemcpyDeviceToHost, ctx->stream));
+  if (n_nc) {
+    HIPCHK(hipMemcpyAsync(nct.data(), base + o_nct, sizeof(int32_t) * n_nc, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(ncrq.data(), base + o_ncrq, sizeof(int64_t) * n_nc * KP_NRES, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(opts.data(), base + o_opts, sizeof(uint32_t) * (size_t)n_nc * opt_stride, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(nrem.data(), base + o_nrem, sizeof(uint32_t) * n_nc, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(nopt.data(), base + o_nopt, sizeof(uint32_t) * n_nc, hipMemcpyDeviceToHost, ctx->stream));
+  }
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+
+  res->ncs.resize(n_nc);
+  const int n_ev = (int)stats[4];
+  for (int i = 0; i < n_ev; i++) {
+    const int p = events[i];
+    const int t = place[p];
+    if (t >= 0) {
+      res->ncs[t].pods.push_back((uint32_t)p);
+      res->placement[p] = t;
+    } else if (t <= -2) {
+      res->placement[p] = -2 - cp->ex_input[-2 - t];
+    }
+  }
+  for (int i = 0; i < n_nc; i++) {
+    auto& nc = res->ncs[i];
+    const int tm = nct[i];
+    nc.nodepool = (uint32_t)cp->tmpl_nodepool[tm];
+    nc.n_remaining = nrem[i];
+    memset(&nc.requests, 0, sizeof nc.requests);
+    for (int r = 0; r < KP_NRES; r++) {
+      nc.requests.milli[r] = ncrq[(size_t)i * KP_NRES + r];
+      if (nc.requests.milli[r]) nc.requests.present |= 1u << r;
+    }
+    nc.options.assign(opts.begin() + (size_t)i * opt_stride, opts.begin() + (size_t)i * opt_stride + nopt[i]);
+    // Truncate: minValues must still hold on the truncated options, else the NodeClaim's pods fail
+    const KReqs* R = nullptr;
+    (void)R;
+  }
+  // minValues re-check needs the final requirements: copy them for NodeClaims whose template had minValues
+  {
+    bool any = false;
+    for (auto& q : cp->tmpl_reqs) any |= q.hmin != 0;
+    for (auto& lv : cp->shape_reqs) any |= lv.hmin != 0;
+    if (any && n_nc) {
+      vector<KReqs> fin(n_nc);
+      HIPCHK(hipMemcpy(fin.data(), base + o_ncr, sizeof(KReqs) * n_nc, hipMemcpyDeviceToHost));
+      for (int i = 0; i < n_nc; i++) {
+        if (!(fin[i].hmin & fin[i].present)) continue;
+        const HostCat& hc = cp->cats[cp->tmpl_catalog[nct[i]]];
+        vector<int> ts(res->ncs[i].options.begin(), res->ncs[i].options.end());
+        if (!HostMinValuesOK(d, hc, fin[i], ts)) {
+          for (uint32_t p : res->ncs[i].pods) res->placement[p] = -1;
+          res->ncs[i].options.clear();
+        }
+      }
+    }
+  }
+  memset(&res->stats, 0, sizeof res->stats);
+  res->stats.device_ms = ms;
+  res->stats.attempts = stats[0];
+  res->stats.bytes_algorithmic = stats[1];
+  res->stats.pops = stats[2];
+  res->stats.host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  *out = guard.release();
+  return KP_OK;
+}
+
+uint32_t kp_result_nodeclaim_count(const kp_solve_result* r) { return r ? (uint32_t)r->ncs.size() : 0; }
+int32_t kp_result_pod_placements(const kp_solve_result* r, int32_t* out, uint32_t n) {
+  if (!r || !out || n != r->placement.size()) return fail(KP_E_INVAL, "bad placement buffer");
+  memcpy(out, r->placement.data(), sizeof(int32_t) * n);
+  return KP_OK;
+}
+int32_t kp_result_nodeclaim(const kp_solve_result* r, uint32_t i, kp_nodeclaim_info* out) {
+  if (!r || !out || i >= r->ncs.size()) return fail(KP_E_INVAL, "bad nodeclaim index");
+  const auto& n = r->ncs[i];
+  out->nodepool = n.nodepool;
+  out->n_pods = (uint32_t)n.pods.size();
+  out->n_remaining = n.n_remaining;
+  out->n_options = (uint32_t)n.options.size();
+  out->pods = n.pods.data();
+  out->options = n.options.data();
+  out->requests = n.requests;
+  return KP_OK;
+}
+int32_t kp_result_stats(const kp_solve_result* r, kp_solve_stats* out) {
+  if (!r || !out) return fail(KP_E_INVAL, "null");
+  *out = r->stats;
+  return KP_OK;
+}
+void kp_result_destroy(kp_solve_result* r) { delete r; }
+
+// CompatibleAvailableFilter batched on the GPU.
+int32_t kp_filter_compatible_available(kp_ctx* ctx, const kp_catalog* cat, const kp_feasibility_query* queries,
+                                       uint32_t n_queries, uint64_t* out_mask, double* out_cheapest,
+                                       kp_solve_stats* stats) {
+  auto t0 = std::chrono::steady_clock::now();
+  if (!ctx || !cat || (!queries && n_queries) || !out_mask) return fail(KP_E_INVAL, "null argument");
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device));
+  Compiled cp;
+  DictBuilder db;
+  vector<RawReqs> qs(n_queries);
+  for (auto& t : cat->types) {
+    db.addReqs(t.reqs);
+    for (auto& o : t.offs) {
+      db.addLabel(kCapType, o.ct);
+      db.addLabel(kZone, o.zone);
+      if (o.has_zid) db.addLabel(kZoneID, o.zid);
+    }
+  }
+  db.bounded[kResID];
+  db.bounded[kResType];
+  for (uint32_t i = 0; i < n_queries; i++) {
+    qs[i] = ParseReqs(queries[i].requirements);
+    db.addReqs(qs[i]);
+  }
+  int32_t rc = db.build(cp.d);
+  if (rc) return rc;
+  const int T = (int)cat->types.size(), TW = std::max(1, (T + 63) / 64);
+  cp.d.dd.T = T;
+  cp.d.dd.TW = TW;
+  map<ClassKey, int> classes;
+  const Dict& d = cp.d;
+  for (auto& t : cat->types)
+    for (auto& o : t.offs) {
+      ClassKey ck{d.bit(d.key(kCapType), o.ct), o.has_zone ? d.bit(d.key(kZone), o.zone) : -1, o.has_zid ? d.bit(d.key(kZoneID), o.zid) : -1};
+      if (!classes.count(ck)) {
+        int id = (int)classes.size();
+        classes[ck] = id;
+      }
+    }
+  if (classes.size() > KP_MAX_CLASSES) return fail(KP_E_UNSUPPORTED, "%zu offering classes", classes.size());
+  cp.C = (int)classes.size();
+  cp.d.dd.C = cp.C;
+  cp.classes.resize(cp.C);
+  for (auto& kv : classes) cp.classes[kv.second] = {kv.first.ct, kv.first.zone, kv.first.zid, 0};
+  cp.cats.resize(1);
+  rc = CompileCatalog(d, cat->types, TW, classes, cp.cats[0]);
+  if (rc) return rc;
+  uint64_t catalog_keys = 0;
+  for (int k = 0; k < d.dd.K; k++)
+    for (int t = 0; t < T; t++)
+      if (!((cp.cats[0].NOKEY[(size_t)k * TW + t / 64] >> (t % 64)) & 1)) catalog_keys |= 1ull << k;
+  cp.d.dd.catalog_keys = catalog_keys;
+  cp.d.dd.single_valued = catalog_keys & ~cp.cats[0].multi_valued;
+  vector<KReqs> qreqs(std::max<uint32_t>(n_queries, 1));
+  vector<int64_t> qrq((size_t)std::max<uint32_t>(n_queries, 1) * KP_NRES, 0);
+  for (uint32_t i = 0; i < n_queries; i++) {
+    qreqs[i] = Compile(d, qs[i]);
+    for (int r = 0; r < KP_NRES; r++)
+      qrq[(size_t)i * KP_NRES + r] = (queries[i].requests.present >> r) & 1 ? queries[i].requests.milli[r] : 0;
+  }
+  Blob blob;
+  const size_t o_dict = blob.put(&cp.d.dd, 1);
+  const size_t o_vint = blob.put(cp.d.vint);
+  vector<CatOffsets> coffs;
+  PutCatalogs(blob, cp, coffs);
+  const size_t o_cats = blob.reserve(sizeof(DevCatalog));
+  const size_t o_q = blob.put(qreqs);
+  const size_t o_qr = blob.put(qrq);
+  const size_t host_bytes = blob.host.size();
+  const size_t tiles = (size_t)(T + 63) / 64;
+  const size_t o_mask = blob.reserve(sizeof(uint64_t) * std::max<size_t>(1, n_queries * tiles));
+  const size_t o_ch = out_cheapest ? blob.reserve(sizeof(double) * std::max<size_t>(1, (size_t)n_queries * T)) : 0;
+  DevBuf buf;
+  HIPCHK(hipMalloc(&buf.p, blob.host.size()));
+  uint8_t* base = (uint8_t*)buf.p;
+  vector<DevCatalog> dc = DevCats(base, cp, coffs);
+  memcpy(blob.host.data() + o_cats, dc.data(), sizeof(DevCatalog));
+  HIPCHK(hipMemcpyAsync(base, blob.host.data(), host_bytes, hipMemcpyHostToDevice, ctx->stream));
+  FeasArgs fa;
+  fa.dict = (const DevDict*)(base + o_dict);
+  fa.cat = (const DevCatalog*)(base + o_cats);
+  fa.vint = (const int64_t*)(base + o_vint);
+  fa.T = T;
+  fa.n_queries = (int32_t)n_queries;
+  fa.mode_compatible = 1;
+  fa.pad_ = 0;
+  fa.q_reqs = base + o_q;
+  fa.q_requests = (const int64_t*)(base + o_qr);
+  fa.out_mask = (uint64_t*)(base + o_mask);
+  fa.out_cheapest = out_cheapest ? (double*)(base + o_ch) : nullptr;
+  HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
+  if (n_queries) HIPCHK(launch_feasibility(fa, ctx->stream));
+  HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));
+  if (n_queries) {
+    HIPCHK(hipMemcpyAsync(out_mask, base + o_mask, sizeof(uint64_t) * n_queries * tiles, hipMemcpyDeviceToHost, ctx->stream));
+    if (out_cheapest)
+      HIPCHK(hipMemcpyAsync(out_cheapest, base + o_ch, sizeof(double) * (size_t)n_queries * T, hipMemcpyDeviceToHost, ctx->stream));
+  }
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+  if (stats) {
+    memset(stats, 0, sizeof *stats);
+    stats->device_ms = ms;
+    stats->attempts = (uint64_t)n_queries * T;
+    stats->host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
+  return KP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,827 @@
+// kp_kernels.hip — CDNA4 (gfx950) kernels of the Karpenter bin-packing hot path.
+//
+//  solve_kernel       upstream Scheduler.Solve (FFD). The whole pod loop runs device-resident in ONE
+//                     workgroup per Solve; each wave evaluates one placement candidate (existing node,
+//                     in-flight NodeClaim or NodeClaimTemplate) with the exact requirement algebra held one
+//                     64-bit word per lane (kp_model.h), and NodeClaim.Add's instance-type filter
+//                     (upstream filterInstanceTypesByRequirements) as bitmask algebra over the catalogue.
+//  finalize_kernel    Results.TruncateInstanceTypes: cheapest compatible available offering per option
+//                     (min over offering classes), OrderByPrice (price asc, name asc) + cut to max.
+//  feasibility_kernel CompatibleAvailableFilter (R:pkg/providers/instance/filter/filter.go:39-64) for many
+//                     (requirements, requests) rows × one catalogue: lane = instance type, ballot -> mask
+//                     words, cheapest offering by a per-lane min over offering classes.
+//
+// No MFMA: the path is bitwise/integer. Wave = 64 lanes everywhere.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kp_device.h"
+#include "kp_model.h"
+
+#define LANE ((int)(threadIdx.x & 63))
+
+// ------------------------------------------------------------------------------------------------
+// wave helpers
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+__device__ __forceinline__ uint64_t wave_or(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v |= __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ int64_t wave_max_i64(int64_t v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    int64_t w = __shfl_xor(v, o, 64);
+    v = w > v ? w : v;
+  }
+  return v;
+}
+// every lane must call (uniform control flow)
+__device__ __forceinline__ uint64_t lane_bcast(uint64_t v, int src) { return __shfl(v, src, 64); }
+
+// Requirement bounds filter (withinIntPtrs) applied to the value bits of one word.
+__device__ __forceinline__ uint64_t within_word(uint64_t v, int word, const int64_t* vint, uint64_t intok, bool hg,
+                                                int64_t gt, bool hl, int64_t lt) {
+  if (!hg && !hl) return v;
+  uint64_t out = 0, m = v & intok;
+  while (m) {
+    const int b = __builtin_ctzll(m);
+    m &= m - 1;
+    const int64_t x = vint[word * 64 + b];
+    if ((!hg || x > gt) && (!hl || x < lt)) out |= 1ull << b;
+  }
+  return out;
+}
+
+// Key masks + bound slots of one requirement set; values stay in registers (one word per lane).
+struct ReqView {
+  uint64_t present, compl_, hgt, hlt, hmin, nz, dne;
+  const int64_t* gt;
+  const int64_t* lt;
+  const int32_t* minv;
+};
+
+// operator in {NotIn, DoesNotExist}: complement with values, or no complement and no values.
+__device__ __forceinline__ uint64_t negop_mask(uint64_t present, uint64_t compl_, uint64_t nz) {
+  return present & ((compl_ & nz) | (~compl_ & ~nz));
+}
+
+__device__ __forceinline__ uint64_t nz_keys(const DevDict& D, uint64_t v) {
+  const int lane = LANE;
+  const int k = lane < D.W ? (int)D.wkey[lane] : -1;
+  return wave_or((v != 0 && k >= 0) ? (1ull << k) : 0ull);
+}
+
+// Per-wave LDS scratch holding a merged requirement set's bound slots.
+struct WaveSlots {
+  int64_t gt[KP_MAX_BOUND_KEYS];
+  int64_t lt[KP_MAX_BOUND_KEYS];
+  int32_t minv[KP_MAX_BOUND_KEYS];
+};
+
+// Requirements.Compatible(A, B, allowUndefined) followed by A.Add(B) (= per key Requirement.Intersection).
+// On success: m_v = merged value word of this lane, rv = merged key masks, slots = merged bounds.
+__device__ bool merge_compatible(const DevDict& D, const KReqs* A, const KReqs* B, uint64_t b_negop, bool allow_wk,
+                                 uint64_t& m_v, ReqView& rv, WaveSlots* slots, const int64_t* vint) {
+  const int lane = LANE;
+  const int k = lane < D.W ? (int)D.wkey[lane] : -1;
+  const uint64_t aP = A->present, bP = B->present;
+  const uint64_t shared = aP & bP;
+  // (a) keys the pod defines but the candidate does not: only NotIn/DoesNotExist (or well-known) pass
+  uint64_t undef = bP & ~aP & ~b_negop;
+  if (allow_wk) undef &= ~D.wellknown;
+  if (undef) return false;
+  const uint64_t a_v = lane < D.W ? A->vals[lane] : 0;
+  const uint64_t b_v = lane < D.W ? B->vals[lane] : 0;
+  const uint64_t aC = A->compl_ & aP, bC = B->compl_ & bP;
+  // bound slots: lane l < KB owns key l
+  bool hg = false, hl = false, dneb = false;
+  if (lane < D.KB) {
+    const bool inA = (aP >> lane) & 1, inB = (bP >> lane) & 1;
+    const bool agt = inA && ((A->hgt >> lane) & 1), bgt = inB && ((B->hgt >> lane) & 1);
+    const bool alt = inA && ((A->hlt >> lane) & 1), blt = inB && ((B->hlt >> lane) & 1);
+    hg = agt || bgt;
+    hl = alt || blt;
+    const int64_t g = agt && bgt ? max(A->gt[lane], B->gt[lane]) : (agt ? A->gt[lane] : (bgt ? B->gt[lane] : 0));
+    const int64_t l = alt && blt ? min(A->lt[lane], B->lt[lane]) : (alt ? A->lt[lane] : (blt ? B->lt[lane] : 0));
+    const bool amin = inA && ((A->hmin >> lane) & 1), bmin = inB && ((B->hmin >> lane) & 1);
+    const int32_t mv =
+        amin && bmin ? max(A->minv[lane], B->minv[lane]) : (amin ? A->minv[lane] : (bmin ? B->minv[lane] : 0));
+    dneb = inA && inB && hg && hl && g >= l;
+    slots->gt[lane] = g;
+    slots->lt[lane] = l;
+    slots->minv[lane] = mv;
+  }
+  const uint64_t hgt_any = __ballot(hg), hlt_any = __ballot(hl), dne = __ballot(dneb);
+  wave_sync();
+  uint64_t v = 0;
+  if (k >= 0) {
+    if ((shared >> k) & 1) {
+      const bool c1 = (aC >> k) & 1, c2 = (bC >> k) & 1;
+      v = (c1 && c2) ? (a_v | b_v) : c1 ? (b_v & ~a_v) : c2 ? (a_v & ~b_v) : (a_v & b_v);
+      if ((dne >> k) & 1) {
+        v = 0;  // gt >= lt: NewRequirementWithFlexibility(key, DoesNotExist, minValues)
+      } else if (k < D.KB && (((hgt_any | hlt_any) >> k) & 1)) {
+        v = within_word(v, lane, vint, D.vint_ok[lane], (hgt_any >> k) & 1, slots->gt[k], (hlt_any >> k) & 1,
+                        slots->lt[k]);
+      }
+    } else {
+      v = ((aP >> k) & 1) ? a_v : b_v;
+    }
+  }
+  m_v = v;
+  const uint64_t compl_new = ((aC & bC) | (aC & ~bP) | (bC & ~aP)) & ~dne;
+  const uint64_t nz = nz_keys(D, v);
+  rv.present = aP | bP;
+  rv.compl_ = compl_new;
+  rv.hgt = hgt_any & compl_new;
+  rv.hlt = hlt_any & compl_new;
+  rv.hmin = (A->hmin & aP) | (B->hmin & bP);
+  rv.nz = nz;
+  rv.dne = dne;
+  rv.gt = slots->gt;
+  rv.lt = slots->lt;
+  rv.minv = slots->minv;
+  // (b) Intersects over shared keys: empty intersection is an error unless both ops are NotIn/DNE
+  const uint64_t empty = shared & (dne | (~compl_new & ~nz));
+  const uint64_t nzA = nz_keys(D, a_v);
+  const uint64_t negA = negop_mask(aP, aC, nzA);
+  return (empty & ~(negA & b_negop)) == 0;
+}
+
+// Allowed-value bits (Requirement.Has) of this lane's word under requirement set rv; absent key -> all.
+__device__ __forceinline__ uint64_t allowed_word(const DevDict& D, const ReqView& rv, uint64_t v, const int64_t* vint) {
+  const int lane = LANE;
+  if (lane >= D.W) return 0;
+  const int k = D.wkey[lane];
+  if (!((rv.present >> k) & 1)) return D.validbits[lane];
+  if ((rv.compl_ >> k) & 1) {
+    uint64_t a = ~v & D.validbits[lane];
+    if (k < D.KB && (((rv.hgt | rv.hlt) >> k) & 1))
+      a = within_word(a, lane, vint, D.vint_ok[lane], (rv.hgt >> k) & 1, rv.gt[k], (rv.hlt >> k) & 1, rv.lt[k]);
+    return a;
+  }
+  return v;
+}
+
+__device__ __forceinline__ bool bit_of(uint64_t allowed_lane_word, int bit) {
+  const uint64_t w = lane_bcast(allowed_lane_word, bit >> 6);
+  return (w >> (bit & 63)) & 1;
+}
+
+// Offering classes compatible with requirement set rv (Offerings.Compatible + reservation-key DNE test).
+__device__ uint64_t allowed_classes(const DevDict& D, const DevCatalog& Cg, const ReqView& rv, uint64_t allowed,
+                                   uint64_t negR) {
+  const bool res_ok = !(rv.present & D.resid_key_bit) || (negR & D.resid_key_bit);
+  const bool rt_ok = !(rv.present & D.restype_key_bit) || (negR & D.restype_key_bit);
+  uint64_t cls = 0;
+  for (int c = 0; c < D.C; c++) {
+    const OfferClass oc = Cg.cls[c];
+    bool ok = bit_of(allowed, oc.ct_bit);
+    if (oc.zone_bit >= 0) ok = (int)ok & (int)bit_of(allowed, oc.zone_bit);
+    if (oc.zid_bit >= 0) ok = (int)ok & (int)bit_of(allowed, oc.zid_bit);
+    if (ok) cls |= 1ull << c;
+  }
+  return (res_ok && rt_ok) ? cls : 0;
+}
+
+// first j in [0, n) with vals[j] >= q (ascending vals), n if none; 64-ary search across the wave.
+__device__ int wave_lower_bound(const int64_t* vals, int n, int64_t q, uint64_t* bytes) {
+  const int lane = LANE;
+  int lo = 0, hi = n;  // vals[j] < q for j < lo; answer <= hi
+  while (lo < hi) {
+    const int span = hi - lo;
+    if (span <= 64) {
+      const bool ge = lane < span && vals[lo + lane] >= q;
+      const uint64_t bal = __ballot(ge);
+      *bytes += 8ull * span;
+      return bal ? lo + __builtin_ctzll(bal) : hi;
+    }
+    const int step = (span + 63) / 64;
+    const int idx = lo + lane * step;
+    const bool ge = idx < hi && vals[idx] >= q;
+    const uint64_t bal = __ballot(ge);
+    *bytes += 512;
+    if (!bal) {
+      const int last = min(hi - 1, lo + 63 * step);
+      lo = last + 1;
+    } else {
+      const int f = __builtin_ctzll(bal);
+      if (f == 0) return lo;
+      const int nlo = lo + (f - 1) * step + 1;
+      hi = lo + f * step;
+      lo = nlo;
+    }
+  }
+  return lo;
+}
+
+// NodeClaim.Add's instance-type filter after a successful merge. X: this lane's word of the candidate's
+// remaining types (invariant: X already passes every key the pod did not touch). Returns the new word.
+__device__ uint64_t filter_types(const DevDict& D, const DevCatalog& Cg, const ReqView& rv, uint64_t m_v, uint64_t X,
+                                 uint64_t pod_keys, const uint64_t* pvp, const int32_t* pvp_slot, const int64_t* total,
+                                 const int64_t* vint, uint32_t* scratch, uint64_t* bytes) {
+  const int lane = LANE;
+  const int TW = D.TW;
+  const uint64_t negM = negop_mask(rv.present, rv.compl_, rv.nz);
+  const uint64_t allowed = allowed_word(D, rv, m_v, vint);
+  uint64_t nb = 0;
+  // 1) Intersects(type, merged) for the keys the pod changed
+  uint64_t keys = pod_keys & D.catalog_keys;
+  while (keys) {
+    const int k = __builtin_ctzll(keys);
+    keys &= keys - 1;
+    const bool ng = (negM >> k) & 1;
+    if ((D.single_valued >> k) & 1) {
+      // X ⊆ Pass(candidate_k) and Has_merged = Has_candidate ∧ Has_pod, so for single-valued keys
+      // X ∩ ∪_{Has_merged(v)} TM[v] = X ∩ ∪_{Has_pod(v)} TM[v] (precomputed PVP row, incl. NOKEY)
+      uint64_t p = lane < TW ? pvp[(size_t)pvp_slot[k] * TW + lane] : 0;
+      if (ng && lane < TW) p |= Cg.DNE[(size_t)k * TW + lane];
+      X &= p;
+      nb += (uint64_t)TW * 8 * (ng ? 2 : 1);
+    } else {
+      uint64_t acc = lane < TW ? Cg.NOKEY[(size_t)k * TW + lane] : 0;
+      if (ng && lane < TW) acc |= Cg.DNE[(size_t)k * TW + lane];
+      const int w0 = D.wofs[k], nw = (D.nval[k] + 63) >> 6;
+      for (int w = w0; w < w0 + nw; w++) {
+        uint64_t a = lane_bcast(allowed, w);
+        while (a) {
+          const int b = __builtin_ctzll(a);
+          a &= a - 1;
+          if (lane < TW) acc |= Cg.TM[(size_t)(w * 64 + b) * TW + lane];
+          nb += (uint64_t)TW * 8;
+        }
+      }
+      X &= acc;
+    }
+  }
+  // 2) resources.Fits(total, allocatable): per requested resource, a threshold mask
+  for (int r = 0; r < KP_NRES; r++) {
+    const int64_t q = total[r];
+    if (q <= 0) continue;
+    const int n = Cg.fit_n[r];
+    const int j = wave_lower_bound(Cg.fit_vals + (size_t)r * D.T, n, q, &nb);
+    if (j >= n) X = 0;
+    else if (lane < TW) X &= Cg.fit_mask[((size_t)r * D.T + j) * TW + lane];
+    nb += (uint64_t)TW * 8;
+  }
+  // 3) some available offering compatible with the merged requirements
+  {
+    const uint64_t cls = allowed_classes(D, Cg, rv, allowed, negM);
+    uint64_t offer = 0;
+    uint64_t m = cls;
+    while (m) {
+      const int c = __builtin_ctzll(m);
+      m &= m - 1;
+      if (lane < TW) offer |= Cg.offer_avail[(size_t)c * TW + lane];
+    }
+    nb += (uint64_t)__builtin_popcountll(cls) * TW * 8;
+    X &= offer;
+  }
+  // 4) minValues (relaxMinValues = false): distinct values of each minValues key over remaining types
+  uint64_t mk = rv.hmin & rv.present;
+  while (mk) {
+    const int k = __builtin_ctzll(mk);
+    mk &= mk - 1;
+    const int w0 = D.wofs[k], nw = (D.nval[k] + 63) >> 6;
+    int count = 0;
+    if ((D.single_valued >> k) & 1) {
+      for (int w = lane; w < 2 * nw; w += 64) scratch[w] = 0;
+      wave_sync();
+      uint64_t m = lane < TW ? X : 0;
+      while (m) {
+        const int b = __builtin_ctzll(m);
+        m &= m - 1;
+        const uint16_t code = Cg.code[(size_t)k * D.T + lane * 64 + b];
+        if (code < 0xFFFD) {
+          const int rel = (int)code - w0 * 64;
+          atomicOr(&scratch[rel >> 5], 1u << (rel & 31));
+        }
+      }
+      wave_sync();
+      int c = 0;
+      for (int w = lane; w < 2 * nw; w += 64) c += __builtin_popcount(scratch[w]);
+      count = wave_sum(c);
+      wave_sync();
+    } else {
+      for (int w = w0; w < w0 + nw; w++) {
+        uint64_t vb = D.validbits[w];
+        while (vb) {
+          const int b = __builtin_ctzll(vb);
+          vb &= vb - 1;
+          const uint64_t hit = lane < TW ? (X & Cg.TM[(size_t)(w * 64 + b) * TW + lane]) : 0;
+          count += __ballot(hit != 0) ? 1 : 0;
+        }
+      }
+    }
+    if (count < rv.minv[k]) X = 0;
+  }
+  *bytes += nb;
+  return X;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Go sort.Slice (pdqsort_func) over the in-flight NodeClaims by len(Pods), executed by one lane.
+// ------------------------------------------------------------------------------------------------
+struct NCSort {
+  int32_t* ord;        // newNodeClaims (NodeClaim ids)
+  const int32_t* key;  // len(Pods) per NodeClaim id
+  __device__ bool Less(int i, int j) const { return key[ord[i]] < key[ord[j]]; }
+  __device__ void Swap(int i, int j) const {
+    const int32_t t = ord[i];
+    ord[i] = ord[j];
+    ord[j] = t;
+  }
+};
+#include "kp_pdqsort.h"
+
+// ------------------------------------------------------------------------------------------------
+// solve_kernel: one workgroup runs one Solve.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ const KReqs* kreq_at(const uint8_t* base, size_t i) {
+  return reinterpret_cast<const KReqs*>(base + i * sizeof(KReqs));
+}
+
+__device__ void store_merged(KReqs* dst, const ReqView& rv, uint64_t m_v, int W, int KB) {
+  const int lane = LANE;
+  if (lane < W) dst->vals[lane] = m_v;
+  if (lane < KB) {
+    dst->gt[lane] = rv.gt[lane];
+    dst->lt[lane] = rv.lt[lane];
+    dst->minv[lane] = rv.minv[lane];
+  }
+  if (lane == 0) {
+    dst->present = rv.present;
+    dst->compl_ = rv.compl_;
+    dst->hgt = rv.hgt;
+    dst->hlt = rv.hlt;
+    dst->hmin = rv.hmin;
+  }
+}
+
+// pick the lowest wave that succeeded (first-fit inside one round of NW candidates)
+template <int NW>
+__device__ __forceinline__ int first_ok(const int32_t* s_ok) {
+  for (int w = 0; w < NW; w++)
+    if (s_ok[w]) return w;
+  return -1;
+}
+
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
+  __shared__ DevDict D;
+  __shared__ WaveSlots slots[NW];
+  __shared__ int32_t s_ok[NW];
+  __shared__ int32_t s_ctl[8];
+  __shared__ uint32_t s_scratch[NW][2 * KP_MAX_WORDS];
+  extern __shared__ int32_t s_dyn[];  // sort arrays when they fit: ord[cap], npods[cap]
+
+  const int wave = threadIdx.x >> 6;
+  const int lane = LANE;
+  if (threadIdx.x == 0) D = *a.dict;
+  int32_t* ord = a.sort_in_lds ? s_dyn : a.g_order;
+  int32_t* npods = a.sort_in_lds ? s_dyn + a.sort_cap : a.g_npods;
+  uint64_t bytes = 0, attempts = 0, pops = 0;
+  // control block (thread 0 owns): 0 head, 1 len, 2 n_nc, 3 lastLen epoch, 4 n_events, 6 popped pod
+  if (threadIdx.x == 0) {
+    s_ctl[0] = 0;
+    s_ctl[1] = a.n_pods;
+    s_ctl[2] = 0;
+    s_ctl[3] = 1;
+    s_ctl[4] = 0;
+  }
+  __syncthreads();
+
+  for (;;) {
+    // ---- Queue.Pop: stop when the head pod was last pushed at the current queue length ----------
+    if (threadIdx.x == 0) {
+      const int len = s_ctl[1];
+      int pod = -1;
+      if (len > 0) {
+        const int head = s_ctl[0];
+        const int p = a.queue[head];
+        if (!(a.lastlen_epoch[p] == s_ctl[3] && a.lastlen[p] == len)) {
+          pod = p;
+          s_ctl[0] = head + 1 == a.n_pods ? 0 : head + 1;
+          s_ctl[1] = len - 1;
+        }
+      }
+      s_ctl[6] = pod;
+    }
+    __syncthreads();
+    const int pod = s_ctl[6];
+    if (pod < 0) break;
+    pops++;
+    const int shape = a.pod_shape[pod];
+    const int lvl = a.pod_level[pod];
+    const int sl = a.shape_level_base[shape] + lvl;
+    const KReqs* B = kreq_at(a.shape_reqs, sl);
+    const uint64_t b_negop = a.shape_negop[sl];
+    const uint64_t b_keys = B->present;
+    const int64_t* preq = a.shape_requests + (size_t)shape * KP_NRES;
+    const uint64_t tolmask = a.shape_tolerates[shape];
+    const int32_t* pslot = a.pvp_slot + (size_t)sl * KP_MAX_KEYS;
+    int placed = -1;  // >= 0 NodeClaim id; <= -2 existing node; -1 not placed
+
+    // ---- addToExistingNode: lowest index whose CanAdd succeeds -------------------------------
+    for (int base = 0; base < a.n_existing; base += NW) {
+      const int e = base + wave;
+      bool ok = false;
+      uint64_t m_v = 0;
+      ReqView rv;
+      if (e < a.n_existing && ((tolmask >> a.ex_taintset[e]) & 1)) {
+        attempts++;
+        const int64_t* av = a.ex_available + (size_t)e * KP_NRES;
+        const int64_t* rq = a.ex_requests + (size_t)e * KP_NRES;
+        bool fits = true;  // Fits(Merge(requests, pod), available)
+        for (int r = 0; r < KP_NRES; r++) fits = fits && av[r] >= 0 && rq[r] + preq[r] <= av[r];
+        bytes += 2 * KP_NRES * 8;
+        if (fits) {
+          ok = merge_compatible(D, kreq_at(a.ex_reqs, e), B, b_negop, false, m_v, rv, &slots[wave], a.vint);
+          bytes += sizeof(KReqs);
+        }
+      }
+      if (lane == 0) s_ok[wave] = ok ? 1 : 0;
+      __syncthreads();
+      const int win = first_ok<NW>(s_ok);
+      if (win >= 0) {
+        if (wave == win) {
+          store_merged(reinterpret_cast<KReqs*>(a.ex_reqs + (size_t)e * sizeof(KReqs)), rv, m_v, D.W, D.KB);
+          if (lane < KP_NRES) a.ex_requests[(size_t)e * KP_NRES + lane] += preq[lane];
+        }
+        placed = -2 - (base + win);
+      }
+      __syncthreads();
+      if (win >= 0) break;
+    }
+
+    if (placed == -1) {
+      // ---- sort.Slice(newNodeClaims, len(Pods) asc) -----------------------------------------------
+      if (threadIdx.x == 0) go_sort_slice(NCSort{ord, npods}, s_ctl[2]);
+      __syncthreads();
+      const int n_nc = s_ctl[2];
+      // ---- addToInflightNode: first NodeClaim in that order whose Add succeeds ------------------
+      for (int base = 0; base < n_nc; base += NW) {
+        const int i = base + wave;
+        bool ok = false;
+        uint64_t m_v = 0, X = 0;
+        ReqView rv;
+        int nc = -1;
+        if (i < n_nc) {
+          nc = ord[i];
+          const int tm = a.nc_tmpl[nc];
+          if ((tolmask >> a.tmpl_taintset[tm]) & 1) {
+            attempts++;
+            const int cat = a.tmpl_catalog[tm];
+            ok = merge_compatible(D, kreq_at(a.nc_reqs, nc), B, b_negop, true, m_v, rv, &slots[wave], a.vint);
+            bytes += sizeof(KReqs);
+            if (ok) {
+              int64_t total[KP_NRES];
+              for (int r = 0; r < KP_NRES; r++) total[r] = a.nc_requests[(size_t)nc * KP_NRES + r] + preq[r];
+              X = lane < D.TW ? a.nc_X[(size_t)nc * D.TW + lane] : 0;
+              const uint64_t* pvp = a.shape_pvp + (size_t)a.pvp_base[sl * a.n_catalogs + cat] * D.TW;
+              X = filter_types(D, a.cats[cat], rv, m_v, X, b_keys, pvp, pslot, total, a.vint, s_scratch[wave], &bytes);
+              ok = __ballot(X != 0) != 0;
+              bytes += (uint64_t)D.TW * 8 + KP_NRES * 8;
+            }
+          }
+        }
+        if (lane == 0) s_ok[wave] = ok ? 1 : 0;
+        __syncthreads();
+        const int win = first_ok<NW>(s_ok);
+        if (win >= 0) {
+          if (wave == win) {
+            store_merged(reinterpret_cast<KReqs*>(a.nc_reqs + (size_t)nc * sizeof(KReqs)), rv, m_v, D.W, D.KB);
+            if (lane < D.TW) a.nc_X[(size_t)nc * D.TW + lane] = X;
+            if (lane < KP_NRES) a.nc_requests[(size_t)nc * KP_NRES + lane] += preq[lane];
+            if (lane == 0) npods[nc] += 1;
+          }
+          placed = ord[base + win];
+        }
+        __syncthreads();
+        if (win >= 0) break;
+      }
+    }
+
+    if (placed == -1) {
+      // ---- addToNewNodeClaim: templates in weight order --------------------------------------------
+      for (int base = 0; base < a.n_tmpl; base += NW) {
+        const int tm = base + wave;
+        bool ok = false;
+        uint64_t m_v = 0, X = 0;
+        ReqView rv;
+        if (tm < a.n_tmpl && ((tolmask >> a.tmpl_taintset[tm]) & 1)) {
+          const int cat = a.tmpl_catalog[tm];
+          const DevCatalog& Cg = a.cats[cat];
+          X = lane < D.TW ? a.tmpl_X[(size_t)tm * D.TW + lane] : 0;
+          const uint32_t lim = a.tmpl_limit_present[tm];
+          if (lim) {  // filterByRemainingResources: capacity <= remaining for every limited resource
+            const int64_t* rem = a.tmpl_remaining + (size_t)tm * KP_NRES;
+            uint64_t m = lane < D.TW ? X : 0, keep = 0;
+            while (m) {
+              const int b = __builtin_ctzll(m);
+              m &= m - 1;
+              const int t = lane * 64 + b;
+              bool viable = true;
+              for (int r = 0; r < KP_NRES; r++)
+                if (((lim >> r) & 1) && Cg.cap[(size_t)r * D.T + t] > rem[r]) viable = false;
+              if (viable) keep |= 1ull << b;
+            }
+            X = keep;
+            bytes += (uint64_t)D.T * 8;
+          }
+          if (__ballot(X != 0)) {
+            attempts++;
+            ok = merge_compatible(D, kreq_at(a.tmpl_reqs, tm), B, b_negop, true, m_v, rv, &slots[wave], a.vint);
+            if (ok) {
+              int64_t total[KP_NRES];
+              for (int r = 0; r < KP_NRES; r++) total[r] = a.tmpl_daemon[(size_t)tm * KP_NRES + r] + preq[r];
+              const uint64_t* pvp = a.shape_pvp + (size_t)a.pvp_base[sl * a.n_catalogs + cat] * D.TW;
+              X = filter_types(D, Cg, rv, m_v, X, b_keys, pvp, pslot, total, a.vint, s_scratch[wave], &bytes);
+              ok = __ballot(X != 0) != 0;
+            }
+          }
+        }
+        if (lane == 0) s_ok[wave] = ok ? 1 : 0;
+        __syncthreads();
+        const int win = first_ok<NW>(s_ok);
+        const int nc = s_ctl[2];
+        if (win >= 0) {
+          if (wave == win) {
+            store_merged(reinterpret_cast<KReqs*>(a.nc_reqs + (size_t)nc * sizeof(KReqs)), rv, m_v, D.W, D.KB);
+            if (lane < D.TW) a.nc_X[(size_t)nc * D.TW + lane] = X;
+            if (lane < KP_NRES)
+              a.nc_requests[(size_t)nc * KP_NRES + lane] = a.tmpl_daemon[(size_t)tm * KP_NRES + lane] + preq[lane];
+            if (lane == 0) {
+              a.nc_tmpl[nc] = tm;
+              npods[nc] = 1;
+              ord[nc] = nc;  // append to newNodeClaims
+            }
+            // subtractMax: remaining -= max capacity over the new NodeClaim's InstanceTypeOptions
+            const uint32_t lim = a.tmpl_limit_present[tm];
+            if (lim) {
+              const DevCatalog& Cg = a.cats[a.tmpl_catalog[tm]];
+              for (int r = 0; r < KP_NRES; r++) {
+                if (!((lim >> r) & 1)) continue;
+                int64_t mx = INT64_MIN;
+                uint64_t m = lane < D.TW ? X : 0;
+                while (m) {
+                  const int b = __builtin_ctzll(m);
+                  m &= m - 1;
+                  const int64_t c = Cg.cap[(size_t)r * D.T + lane * 64 + b];
+                  mx = c > mx ? c : mx;
+                }
+                mx = wave_max_i64(mx);
+                if (lane == 0) a.tmpl_remaining[(size_t)tm * KP_NRES + r] -= mx;
+              }
+            }
+          }
+          placed = nc;
+        }
+        __syncthreads();
+        if (win >= 0) {
+          if (threadIdx.x == 0) s_ctl[2] = nc + 1;
+          break;
+        }
+      }
+    }
+
+    // ---- bookkeeping (thread 0): placement, or Preferences.Relax + Queue.Push -------------------
+    if (threadIdx.x == 0) {
+      if (placed != -1) {
+        a.placement[pod] = placed;
+        a.events[s_ctl[4]++] = pod;
+      } else {
+        a.placement[pod] = -1;
+        const bool relaxed = lvl + 1 < a.shape_nlevels[shape];
+        if (relaxed) a.pod_level[pod] = lvl + 1;
+        int len = s_ctl[1];
+        int tail = s_ctl[0] + len;
+        if (tail >= a.n_pods) tail -= a.n_pods;
+        a.queue[tail] = pod;
+        len += 1;
+        s_ctl[1] = len;
+        if (relaxed) {
+          s_ctl[3] += 1;  // lastLen = map{}
+        } else {
+          a.lastlen[pod] = len;
+          a.lastlen_epoch[pod] = s_ctl[3];
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  if (lane == 0) {
+    atomicAdd((unsigned long long*)&a.stats[0], (unsigned long long)attempts);
+    atomicAdd((unsigned long long*)&a.stats[1], (unsigned long long)bytes);
+  }
+  if (threadIdx.x == 0) {
+    a.stats[2] = pops;
+    a.stats[3] = (uint64_t)s_ctl[2];
+    a.stats[4] = (uint64_t)s_ctl[4];
+  }
+  if (a.sort_in_lds)
+    for (int i = threadIdx.x; i < s_ctl[2]; i += NW * 64) {
+      a.g_npods[i] = npods[i];
+      a.g_order[i] = ord[i];
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// finalize_kernel: one workgroup per NodeClaim. OrderByPrice(reqs) + Truncate(max).
+// ------------------------------------------------------------------------------------------------
+#define FIN_THREADS 256
+#define FIN_MAX_T 4096
+__global__ __launch_bounds__(FIN_THREADS) void finalize_kernel(FinalizeArgs a) {
+  __shared__ DevDict D;
+  __shared__ uint64_t s_cls;
+  __shared__ uint64_t s_key[FIN_MAX_T];
+  __shared__ uint32_t s_idx[FIN_MAX_T];
+  __shared__ uint32_t s_cnt;
+  const int nc = blockIdx.x;
+  if (threadIdx.x == 0) {
+    D = *a.dict;
+    s_cnt = 0;
+  }
+  __syncthreads();
+  const int tm = a.nc_tmpl[nc];
+  const DevCatalog& Cg = a.cats[a.tmpl_catalog[tm]];
+  const KReqs* R = reinterpret_cast<const KReqs*>(a.nc_reqs + (size_t)nc * sizeof(KReqs));
+  if (threadIdx.x < 64) {  // wave 0: offering classes compatible with the final requirements
+    const int lane = LANE;
+    const uint64_t v = lane < D.W ? R->vals[lane] : 0;
+    ReqView rv;
+    rv.present = R->present;
+    rv.compl_ = R->compl_ & R->present;
+    rv.hgt = R->hgt;
+    rv.hlt = R->hlt;
+    rv.hmin = R->hmin;
+    rv.nz = nz_keys(D, v);
+    rv.dne = 0;
+    rv.gt = R->gt;
+    rv.lt = R->lt;
+    rv.minv = R->minv;
+    const uint64_t negR = negop_mask(rv.present, rv.compl_, rv.nz);
+    const uint64_t allowed = allowed_word(D, rv, v, a.vint);
+    const uint64_t cls = allowed_classes(D, Cg, rv, allowed, negR);
+    if (lane == 0) s_cls = cls;
+  }
+  __syncthreads();
+  const uint64_t cls = s_cls;
+  for (int t = threadIdx.x; t < D.T; t += FIN_THREADS) {
+    const uint64_t xw = a.nc_X[(size_t)nc * D.TW + (t >> 6)];
+    if (!((xw >> (t & 63)) & 1)) continue;
+    double p = __builtin_huge_val();
+    uint64_t m = cls;
+    while (m) {
+      const int c = __builtin_ctzll(m);
+      m &= m - 1;
+      const double q = Cg.price[(size_t)t * D.C + c];
+      p = q < p ? q : p;
+    }
+    const uint32_t slot = atomicAdd(&s_cnt, 1u);
+    s_key[slot] = (uint64_t)__double_as_longlong(p);  // non-negative doubles order like their bits
+    s_idx[slot] = (Cg.name_rank[t] << 12) | (uint32_t)t;
+  }
+  __syncthreads();
+  const uint32_t n = s_cnt;
+  uint32_t n2 = 1;
+  while (n2 < n) n2 <<= 1;
+  for (uint32_t i = n + threadIdx.x; i < n2; i += FIN_THREADS) {
+    s_key[i] = ~0ull;
+    s_idx[i] = ~0u;
+  }
+  __syncthreads();
+  for (uint32_t k = 2; k <= n2; k <<= 1) {  // bitonic sort by (price bits, name rank)
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t i = threadIdx.x; i < n2; i += FIN_THREADS) {
+        const uint32_t ixj = i ^ j;
+        if (ixj > i) {
+          const uint64_t ki = s_key[i], kj = s_key[ixj];
+          const uint32_t ii = s_idx[i], ij = s_idx[ixj];
+          const bool gt = ki > kj || (ki == kj && ii > ij);
+          if (gt == ((i & k) == 0)) {
+            s_key[i] = kj;
+            s_key[ixj] = ki;
+            s_idx[i] = ij;
+            s_idx[ixj] = ii;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  const uint32_t lim = a.max_types ? min(n, (uint32_t)a.max_types) : n;
+  for (uint32_t i = threadIdx.x; i < lim; i += FIN_THREADS)
+    a.out_options[(size_t)nc * a.opt_stride + i] = s_idx[i] & 4095u;
+  if (threadIdx.x == 0) {
+    a.out_n_remaining[nc] = n;
+    a.out_n_options[nc] = lim;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// feasibility_kernel: CompatibleAvailableFilter, (query, 64-type tile) per wave, lane = type.
+// ------------------------------------------------------------------------------------------------
+#define FEAS_WAVES 4
+__global__ __launch_bounds__(FEAS_WAVES * 64) void feasibility_kernel(FeasArgs a) {
+  __shared__ DevDict D;
+  __shared__ uint64_t s_allowed[FEAS_WAVES][KP_MAX_WORDS];
+  if (threadIdx.x == 0) D = *a.dict;
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = LANE;
+  const DevCatalog& Cg = *a.cat;
+  const int tiles = (D.T + 63) >> 6;
+  const long total = (long)a.n_queries * tiles;
+  // items are query-major so consecutive waves share a query row (L1/L2 reuse) and stream type tiles
+  for (long item = (long)blockIdx.x * FEAS_WAVES + wave; item < total; item += (long)gridDim.x * FEAS_WAVES) {
+    const int q = (int)(item / tiles), tile = (int)(item % tiles);
+    const KReqs* Q = reinterpret_cast<const KReqs*>(a.q_reqs + (size_t)q * sizeof(KReqs));
+    const uint64_t v = lane < D.W ? Q->vals[lane] : 0;
+    ReqView rv;
+    rv.present = Q->present;
+    rv.compl_ = Q->compl_ & Q->present;
+    rv.hgt = Q->hgt;
+    rv.hlt = Q->hlt;
+    rv.hmin = Q->hmin;
+    rv.nz = nz_keys(D, v);
+    rv.dne = 0;
+    rv.gt = Q->gt;
+    rv.lt = Q->lt;
+    rv.minv = Q->minv;
+    const uint64_t negQ = negop_mask(rv.present, rv.compl_, rv.nz);
+    const uint64_t allowed = allowed_word(D, rv, v, a.vint);
+    const uint64_t cls = allowed_classes(D, Cg, rv, allowed, negQ);
+    s_allowed[wave][lane] = allowed;
+    wave_sync();
+    const int t = tile * 64 + lane;
+    bool keep = t < D.T;
+    double cheapest = __builtin_huge_val();
+    if (keep) {
+      // Compatible(q, type, WK) part (a): non-well-known type keys q does not define
+      if (a.mode_compatible && (Cg.custom_nonneg[t] & ~rv.present)) keep = false;
+      // Intersects over the shared keys
+      uint64_t keys = rv.present & D.catalog_keys;
+      while (keep && keys) {
+        const int k = __builtin_ctzll(keys);
+        keys &= keys - 1;
+        const uint16_t code = Cg.code[(size_t)k * D.T + t];
+        if (code == 0xFFFF) continue;                   // type lacks the key
+        if (code == 0xFFFE) keep = (negQ >> k) & 1;     // type DoesNotExist: only NotIn/DNE intersect
+        else if (code == 0xFFFD) keep = (s_allowed[wave][D.wofs[k]] & Cg.multi[(size_t)k * D.T + t]) != 0;
+        else keep = (s_allowed[wave][code >> 6] >> (code & 63)) & 1;
+      }
+      if (keep && !((Cg.nonneg[t >> 6] >> (t & 63)) & 1)) keep = false;  // Fits: negative totals never fit
+      for (int r = 0; r < KP_NRES && keep; r++) {
+        const int64_t qv = a.q_requests[(size_t)q * KP_NRES + r];
+        if (qv > 0 && qv > Cg.alloc[(size_t)r * D.T + t]) keep = false;
+      }
+      uint64_t m = cls;
+      while (m) {
+        const int c = __builtin_ctzll(m);
+        m &= m - 1;
+        const double p = Cg.price[(size_t)t * D.C + c];
+        cheapest = p < cheapest ? p : cheapest;
+      }
+      if (!(cheapest < __builtin_huge_val())) keep = false;
+    }
+    const uint64_t bal = __ballot(keep);
+    if (lane == 0) a.out_mask[(size_t)q * tiles + tile] = bal;
+    if (a.out_cheapest && t < D.T) a.out_cheapest[(size_t)q * D.T + t] = cheapest;
+    wave_sync();
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// launchers
+// ------------------------------------------------------------------------------------------------
+hipError_t launch_solve(const SolveArgs& a, int nw, size_t dyn_lds, hipStream_t s) {
+  if (nw == 4) hipLaunchKernelGGL(solve_kernel<4>, dim3(1), dim3(4 * 64), dyn_lds, s, a);
+  else if (nw == 16) hipLaunchKernelGGL(solve_kernel<16>, dim3(1), dim3(16 * 64), dyn_lds, s, a);
+  else hipLaunchKernelGGL(solve_kernel<8>, dim3(1), dim3(8 * 64), dyn_lds, s, a);
+  return hipGetLastError();
+}
+hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s) {
+  if (a.n_nc == 0) return hipSuccess;
+  hipLaunchKernelGGL(finalize_kernel, dim3(a.n_nc), dim3(FIN_THREADS), 0, s, a);
+  return hipGetLastError();
+}
+hipError_t launch_feasibility(const FeasArgs& a, hipStream_t s) {
+  const long tiles = (a.T + 63) / 64;
+  const long items = (long)a.n_queries * tiles;
+  long blocks = (items + FEAS_WAVES - 1) / FEAS_WAVES;
+  if (blocks > 16384) blocks = 16384;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(feasibility_kernel, dim3((unsigned)blocks), dim3(FEAS_WAVES * 64), 0, s, a);
+  return hipGetLastError();
+}

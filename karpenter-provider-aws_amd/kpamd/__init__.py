@@ -1,0 +1,179 @@
+"""kpamd — Python host binding of the MI355X bin-packing hot path (libkp.so, include/kp/kp_abi.h).
+
+The surfaces mirror the reference's plugin/operator interface for the path:
+  CloudProvider.get_instance_types(nodepool)  <- R:pkg/cloudprovider/cloudprovider.go:177-193
+  Scheduler(...).solve(pods)                  <- upstream scheduling.Scheduler.Solve
+  compatible_available_filter(...)            <- R:pkg/providers/instance/filter/filter.go:39-64
+Everything computes behind the C ABI on the GPU; a missing libkp.so or HIP device raises.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import abi
+from .abi import Arena
+
+_LIB = None
+LIB_PATH = os.path.join(abi.PKG_ROOT, "libkp.so")
+
+
+class KPError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"kp error {code}: {msg}")
+        self.code = code
+
+
+def load_lib(path=LIB_PATH):
+    """Load libkp.so (built in-tree by __graft_entry__.build()). Raises if absent — no fallback."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(path):
+        raise KPError(abi.KP_E_DEVICE, f"{path} missing: run __graft_entry__.build()")
+    lib = C.CDLL(path)
+    P = C.POINTER
+    sig = {
+        "kp_last_error": (C.c_char_p, []),
+        "kp_abi_version": (C.c_int32, []),
+        "kp_ctx_create": (C.c_int32, [P(abi.Options), P(C.c_void_p)]),
+        "kp_ctx_destroy": (None, [C.c_void_p]),
+        "kp_catalog_upload": (C.c_int32, [C.c_void_p, P(abi.CatalogDesc), C.c_uint64, P(C.c_void_p)]),
+        "kp_catalog_seqnum": (C.c_uint64, [C.c_void_p]),
+        "kp_catalog_size": (C.c_uint32, [C.c_void_p]),
+        "kp_catalog_destroy": (None, [C.c_void_p]),
+        "kp_instance_type_resolve": (C.c_int32, [P(abi.Options), P(abi.EC2Info), P(abi.NodeClass),
+                                                 P(abi.ResourceList), P(abi.ResourceList)]),
+        "kp_filter_compatible_available": (C.c_int32, [C.c_void_p, C.c_void_p, P(abi.FeasibilityQuery), C.c_uint32,
+                                                       P(C.c_uint64), P(C.c_double), P(abi.SolveStats)]),
+        "kp_solve": (C.c_int32, [C.c_void_p, P(abi.SolveIn), P(C.c_void_p)]),
+        "kp_result_nodeclaim_count": (C.c_uint32, [C.c_void_p]),
+        "kp_result_pod_placements": (C.c_int32, [C.c_void_p, P(C.c_int32), C.c_uint32]),
+        "kp_result_nodeclaim": (C.c_int32, [C.c_void_p, C.c_uint32, P(abi.NodeClaimInfo)]),
+        "kp_result_stats": (C.c_int32, [C.c_void_p, P(abi.SolveStats)]),
+        "kp_result_destroy": (None, [C.c_void_p]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    _LIB = lib
+    return lib
+
+
+def _check(lib, rc):
+    if rc != 0:
+        raise KPError(rc, lib.kp_last_error().decode())
+
+
+class Context:
+    """kp_ctx: one HIP device + stream."""
+
+    def __init__(self, device=0, vm_memory_overhead_percent=0.075, reserved_enis=0):
+        self.lib = load_lib()
+        self.opts = abi.Options(vm_memory_overhead_percent, reserved_enis, device)
+        h = C.c_void_p()
+        _check(self.lib, self.lib.kp_ctx_create(C.byref(self.opts), C.byref(h)))
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self.lib.kp_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Catalog:
+    """A GetInstanceTypes result uploaded behind the ABI (kp_catalog_upload)."""
+
+    def __init__(self, ctx, instance_types, seqnum=0):
+        self.ctx = ctx
+        self.instance_types = instance_types
+        arena = Arena()
+        desc = arena.catalog_desc(instance_types)
+        h = C.c_void_p()
+        _check(ctx.lib, ctx.lib.kp_catalog_upload(ctx.h, C.byref(desc), seqnum, C.byref(h)))
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self.ctx.lib.kp_catalog_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def read_result(lib, res, n_pods, prefix="kp_result_"):
+    """Copy a (kp|kpo)_solve_result into plain Python: placement + NodeClaims in creation order."""
+    get = lambda n: getattr(lib, prefix + n)
+    placement = np.zeros(n_pods, dtype=np.int32)
+    if n_pods:
+        _check_generic(lib, get("pod_placements")(res, placement.ctypes.data_as(C.POINTER(C.c_int32)), n_pods))
+    ncs = []
+    n = get("nodeclaim_count")(res)
+    for i in range(n):
+        info = abi.NodeClaimInfo()
+        _check_generic(lib, get("nodeclaim")(res, i, C.byref(info)))
+        ncs.append({
+            "nodepool": int(info.nodepool),
+            "pods": [int(info.pods[j]) for j in range(info.n_pods)],
+            "options": [int(info.options[j]) for j in range(info.n_options)],
+            "n_remaining": int(info.n_remaining),
+        })
+    st = abi.SolveStats()
+    get("stats")(res, C.byref(st))
+    stats = {f: getattr(st, f) for f, _ in abi.SolveStats._fields_}
+    return {"placement": placement, "nodeclaims": ncs, "stats": stats}
+
+
+def _check_generic(lib, rc):
+    if rc != 0:
+        msg = lib.kp_last_error().decode() if hasattr(lib, "kp_last_error") else ""
+        raise KPError(rc, msg)
+
+
+class Scheduler:
+    """upstream scheduling.Scheduler for one batch: NodePools (templates), existing nodes, catalogues."""
+
+    def __init__(self, ctx, problem, catalogs=None):
+        self.ctx = ctx
+        self.problem = problem
+        self.catalogs = catalogs or [Catalog(ctx, c) for c in problem.catalogs]
+
+    def solve(self):
+        lib = self.ctx.lib
+        arena = Arena()
+        si = abi.build_solve_in(arena, self.problem, catalog_handles=[c.h.value for c in self.catalogs])
+        res = C.c_void_p()
+        _check(lib, lib.kp_solve(self.ctx.h, C.byref(si), C.byref(res)))
+        try:
+            return read_result(lib, res, self.problem.n_pods)
+        finally:
+            lib.kp_result_destroy(res)
+
+
+def compatible_available_filter(ctx, catalog, queries):
+    """queries: list of (requirements, requests). Returns (kept bool[Q,T], cheapest f64[Q,T], stats)."""
+    lib = ctx.lib
+    arena = Arena()
+    qs = arena.arr(abi.FeasibilityQuery, [abi.FeasibilityQuery(arena.requirements(r), arena.resources(q))
+                                          for r, q in queries])
+    T = len(catalog.instance_types)
+    tiles = (T + 63) // 64
+    mask = np.zeros(max(1, len(queries) * tiles), dtype=np.uint64)
+    cheapest = np.zeros(max(1, len(queries) * T), dtype=np.float64)
+    st = abi.SolveStats()
+    _check(lib, lib.kp_filter_compatible_available(ctx.h, catalog.h, qs, len(queries),
+                                                   mask.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                                   cheapest.ctypes.data_as(C.POINTER(C.c_double)), C.byref(st)))
+    bits = np.unpackbits(mask[:len(queries) * tiles].view(np.uint8), bitorder="little").reshape(len(queries), tiles * 64)
+    return bits[:, :T].astype(bool), cheapest[:len(queries) * T].reshape(len(queries), T), st

@@ -1,0 +1,251 @@
+"""ctypes mirror of include/kp/kp_abi.h and the marshalling from Python model objects.
+
+This is the Python analogue of the cgo shim a Go maintainer would add: it only
+lays out C structs; every computation happens behind the C ABI.
+"""
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(HERE)
+
+KP_OK, KP_E_INVAL, KP_E_NOMEM, KP_E_DEVICE, KP_E_UNSUPPORTED, KP_E_NOTFOUND = 0, -1, -2, -3, -4, -5
+NUM_RES = 12
+RES_NAMES = ["cpu", "memory", "ephemeral-storage", "pods", "vpc.amazonaws.com/pod-eni", "vpc.amazonaws.com/efa",
+             "nvidia.com/gpu", "amd.com/gpu", "aws.amazon.com/neuron", "aws.amazon.com/neuroncore",
+             "habana.ai/gaudi", "vpc.amazonaws.com/PrivateIPv4Address"]
+RES_INDEX = {n: i for i, n in enumerate(RES_NAMES)}
+OPS = {"In": 0, "NotIn": 1, "Exists": 2, "DoesNotExist": 3, "Gt": 4, "Lt": 5}
+EFFECTS = {"": 0, "NoSchedule": 1, "PreferNoSchedule": 2, "NoExecute": 3}
+TOL_OPS = {"Equal": 0, "": 0, "Exists": 1}
+
+
+class ResourceList(C.Structure):
+    _fields_ = [("milli", C.c_int64 * NUM_RES), ("present", C.c_uint32), ("reserved_", C.c_uint32)]
+
+
+class Requirement(C.Structure):
+    _fields_ = [("key", C.c_char_p), ("op", C.c_int32), ("min_values", C.c_int32),
+                ("values", C.POINTER(C.c_char_p)), ("n_values", C.c_uint32), ("reserved_", C.c_uint32)]
+
+
+class Requirements(C.Structure):
+    _fields_ = [("items", C.POINTER(Requirement)), ("n", C.c_uint32), ("reserved_", C.c_uint32)]
+
+
+class Label(C.Structure):
+    _fields_ = [("key", C.c_char_p), ("value", C.c_char_p)]
+
+
+class Taint(C.Structure):
+    _fields_ = [("key", C.c_char_p), ("value", C.c_char_p), ("effect", C.c_int32), ("reserved_", C.c_int32)]
+
+
+class Toleration(C.Structure):
+    _fields_ = [("key", C.c_char_p), ("value", C.c_char_p), ("op", C.c_int32), ("effect", C.c_int32)]
+
+
+class Offering(C.Structure):
+    _fields_ = [("capacity_type", C.c_char_p), ("zone", C.c_char_p), ("zone_id", C.c_char_p),
+                ("reservation_id", C.c_char_p), ("reservation_type", C.c_char_p),
+                ("price", C.c_double), ("available", C.c_int32), ("reservation_capacity", C.c_int32)]
+
+
+class InstanceType(C.Structure):
+    _fields_ = [("name", C.c_char_p), ("requirements", Requirements), ("capacity", ResourceList),
+                ("overhead", ResourceList), ("offerings", C.POINTER(Offering)), ("n_offerings", C.c_uint32),
+                ("reserved_", C.c_uint32)]
+
+
+class CatalogDesc(C.Structure):
+    _fields_ = [("types", C.POINTER(InstanceType)), ("n_types", C.c_uint32), ("reserved_", C.c_uint32)]
+
+
+class NodePool(C.Structure):
+    _fields_ = [("name", C.c_char_p), ("weight", C.c_int32), ("catalog", C.c_uint32),
+                ("requirements", Requirements), ("labels", C.POINTER(Label)), ("n_labels", C.c_uint32),
+                ("n_taints", C.c_uint32), ("taints", C.POINTER(Taint)), ("limits", ResourceList),
+                ("daemon_requests", ResourceList)]
+
+
+class PreferredTerm(C.Structure):
+    _fields_ = [("weight", C.c_int32), ("reserved_", C.c_int32), ("preference", Requirements)]
+
+
+class PodShape(C.Structure):
+    _fields_ = [("requests", ResourceList), ("node_selector", C.POINTER(Label)), ("n_node_selector", C.c_uint32),
+                ("n_required_terms", C.c_uint32), ("required_terms", C.POINTER(Requirements)),
+                ("preferred_terms", C.POINTER(PreferredTerm)), ("n_preferred_terms", C.c_uint32),
+                ("n_tolerations", C.c_uint32), ("tolerations", C.POINTER(Toleration)),
+                ("n_topology_spread", C.c_uint32), ("reserved_", C.c_uint32)]
+
+
+class Pod(C.Structure):
+    _fields_ = [("shape", C.c_uint32), ("reserved_", C.c_uint32), ("creation_unix", C.c_int64), ("uid_key", C.c_uint64)]
+
+
+class ExistingNode(C.Structure):
+    _fields_ = [("name", C.c_char_p), ("labels", C.POINTER(Label)), ("n_labels", C.c_uint32),
+                ("n_taints", C.c_uint32), ("taints", C.POINTER(Taint)), ("available", ResourceList),
+                ("requests", ResourceList), ("initialized", C.c_int32), ("reserved_", C.c_int32)]
+
+
+class SolveIn(C.Structure):
+    _fields_ = [("catalogs", C.POINTER(C.c_void_p)), ("catalog_descs", C.POINTER(CatalogDesc)),
+                ("n_catalogs", C.c_uint32), ("n_nodepools", C.c_uint32), ("nodepools", C.POINTER(NodePool)),
+                ("existing", C.POINTER(ExistingNode)), ("n_existing", C.c_uint32), ("n_shapes", C.c_uint32),
+                ("shapes", C.POINTER(PodShape)), ("pods", C.POINTER(Pod)), ("n_pods", C.c_uint32),
+                ("max_instance_types", C.c_uint32)]
+
+
+class NodeClaimInfo(C.Structure):
+    _fields_ = [("nodepool", C.c_uint32), ("n_pods", C.c_uint32), ("n_remaining", C.c_uint32),
+                ("n_options", C.c_uint32), ("pods", C.POINTER(C.c_uint32)), ("options", C.POINTER(C.c_uint32)),
+                ("requests", ResourceList)]
+
+
+class SolveStats(C.Structure):
+    _fields_ = [("device_ms", C.c_double), ("host_ms", C.c_double), ("attempts", C.c_uint64),
+                ("bytes_algorithmic", C.c_uint64), ("pops", C.c_uint64)]
+
+
+class Options(C.Structure):
+    _fields_ = [("vm_memory_overhead_percent", C.c_double), ("reserved_enis", C.c_int32), ("device", C.c_int32)]
+
+
+class EC2Info(C.Structure):
+    _fields_ = [("name", C.c_char_p), ("vcpu", C.c_int32), ("reserved0_", C.c_int32), ("memory_mib", C.c_int64),
+                ("arch", C.c_char_p), ("hypervisor", C.c_char_p), ("encryption_in_transit", C.c_int32),
+                ("clock_mhz", C.c_int32), ("cpu_manufacturer", C.c_char_p), ("ebs_bandwidth_mbps", C.c_int64),
+                ("network_bandwidth_mbps", C.c_int64), ("local_nvme_gb", C.c_int64), ("gpu_name", C.c_char_p),
+                ("gpu_manufacturer", C.c_char_p), ("gpu_count", C.c_int32), ("reserved1_", C.c_int32),
+                ("gpu_memory_mib", C.c_int64), ("accel_name", C.c_char_p), ("accel_manufacturer", C.c_char_p),
+                ("accel_count", C.c_int32), ("neuron_devices", C.c_int32), ("neuron_cores_per_device", C.c_int32),
+                ("efa", C.c_int32), ("max_enis", C.c_int32), ("ipv4_per_eni", C.c_int32), ("trunking", C.c_int32),
+                ("branch_enis", C.c_int32), ("in_limits_table", C.c_int32), ("reserved2_", C.c_int32)]
+
+
+class NodeClass(C.Structure):
+    _fields_ = [("region", C.c_char_p), ("zones", C.POINTER(C.c_char_p)), ("zone_ids", C.POINTER(C.c_char_p)),
+                ("n_zones", C.c_uint32), ("max_pods", C.c_int32), ("pods_per_core", C.c_int32),
+                ("reserved_", C.c_int32)]
+
+
+class FeasibilityQuery(C.Structure):
+    _fields_ = [("requirements", Requirements), ("requests", ResourceList)]
+
+
+# ------------------------------------------------------------------------------------------------
+# Marshalling: Python model objects (kpamd.model) -> ctypes, keeping every buffer alive on `self.keep`.
+# ------------------------------------------------------------------------------------------------
+class Arena:
+    def __init__(self):
+        self.keep = []
+        self._str = {}
+
+    def s(self, x):
+        if x is None:
+            return None
+        b = self._str.get(x)
+        if b is None:
+            b = x.encode() if isinstance(x, str) else bytes(x)
+            self._str[x] = b
+        return b
+
+    def arr(self, ctype, items):
+        a = (ctype * max(1, len(items)))()
+        for i, it in enumerate(items):
+            a[i] = it
+        self.keep.append(a)
+        return a
+
+    def resources(self, d):
+        r = ResourceList()
+        for k, v in (d or {}).items():
+            i = RES_INDEX[k] if isinstance(k, str) else int(k)
+            r.milli[i] = int(v)
+            r.present |= 1 << i
+        return r
+
+    def requirement(self, req):
+        key, op, values = req[0], req[1], list(req[2]) if len(req) > 2 and req[2] is not None else []
+        min_values = req[3] if len(req) > 3 and req[3] is not None else -1
+        vals = self.arr(C.c_char_p, [self.s(v) for v in values])
+        return Requirement(self.s(key), OPS[op] if isinstance(op, str) else int(op), min_values, vals, len(values), 0)
+
+    def requirements(self, reqs):
+        items = self.arr(Requirement, [self.requirement(r) for r in (reqs or [])])
+        return Requirements(items, len(reqs or []), 0)
+
+    def labels(self, d):
+        items = list((d or {}).items())
+        return self.arr(Label, [Label(self.s(k), self.s(v)) for k, v in items]), len(items)
+
+    def taints(self, ts):
+        ts = ts or []
+        return self.arr(Taint, [Taint(self.s(t[0]), self.s(t[1]), EFFECTS[t[2]], 0) for t in ts]), len(ts)
+
+    def tolerations(self, ts):
+        ts = ts or []
+        out = []
+        for t in ts:  # (key, operator, value, effect)
+            out.append(Toleration(self.s(t[0] or ""), self.s(t[2] or ""), TOL_OPS[t[1]], EFFECTS[t[3] or ""]))
+        return self.arr(Toleration, out), len(ts)
+
+    def instance_types(self, its):
+        out = []
+        for it in its:
+            ofs = self.arr(Offering, [Offering(self.s(o.capacity_type), self.s(o.zone), self.s(o.zone_id),
+                                               self.s(getattr(o, "reservation_id", None)),
+                                               self.s(getattr(o, "reservation_type", None)),
+                                               float(o.price), 1 if o.available else 0,
+                                               int(getattr(o, "reservation_capacity", 0))) for o in it.offerings])
+            out.append(InstanceType(self.s(it.name), self.requirements(it.requirements), self.resources(it.capacity),
+                                    self.resources(it.overhead), ofs, len(it.offerings), 0))
+        return self.arr(InstanceType, out), len(its)
+
+    def catalog_desc(self, its):
+        a, n = self.instance_types(its)
+        d = CatalogDesc(a, n, 0)
+        self.keep.append(d)
+        return d
+
+    def nodepool(self, np, catalog_index):
+        labels, nl = self.labels(np.labels)
+        taints, nt = self.taints(np.taints)
+        return NodePool(self.s(np.name), int(np.weight), catalog_index, self.requirements(np.requirements), labels, nl,
+                        nt, taints, self.resources(np.limits), self.resources(np.daemon_requests))
+
+    def shape(self, sh):
+        ns, nns = self.labels(sh.node_selector)
+        terms = self.arr(Requirements, [self.requirements(t) for t in sh.required_terms])
+        prefs = self.arr(PreferredTerm, [PreferredTerm(int(w), 0, self.requirements(t)) for w, t in sh.preferred_terms])
+        tols, ntol = self.tolerations(sh.tolerations)
+        return PodShape(self.resources(sh.requests), ns, nns, len(sh.required_terms), terms, prefs,
+                        len(sh.preferred_terms), ntol, tols, 0, 0)
+
+    def existing_node(self, n):
+        labels, nl = self.labels(n.labels)
+        taints, nt = self.taints(n.taints)
+        return ExistingNode(self.s(n.name), labels, nl, nt, taints, self.resources(n.available),
+                            self.resources(n.requests), 1 if n.initialized else 0, 0)
+
+
+def build_solve_in(arena, problem, catalog_handles=None):
+    """problem: kpamd.model.Problem. catalog_handles: list of kp_catalog* (device path) or None."""
+    descs = arena.arr(CatalogDesc, [arena.catalog_desc(c) for c in problem.catalogs]) if catalog_handles is None else None
+    handles = arena.arr(C.c_void_p, catalog_handles) if catalog_handles is not None else None
+    nps = arena.arr(NodePool, [arena.nodepool(np, np.catalog) for np in problem.nodepools])
+    ex = arena.arr(ExistingNode, [arena.existing_node(n) for n in problem.existing])
+    shapes = arena.arr(PodShape, [arena.shape(s) for s in problem.shapes])
+    import numpy as np
+    pods_np = np.zeros(len(problem.pod_shape), dtype=[("shape", "<u4"), ("r", "<u4"), ("c", "<i8"), ("u", "<u8")])
+    pods_np["shape"] = problem.pod_shape
+    pods_np["c"] = problem.pod_creation
+    pods_np["u"] = problem.pod_uid
+    arena.keep.append(pods_np)
+    pods_ptr = pods_np.ctypes.data_as(C.POINTER(Pod))
+    si = SolveIn(handles, descs, len(problem.catalogs), len(problem.nodepools), nps, ex, len(problem.existing),
+                 len(problem.shapes), shapes, pods_ptr, len(problem.pod_shape), problem.max_instance_types)
+    arena.keep.append(si)
+    return si

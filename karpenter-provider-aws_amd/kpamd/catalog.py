@@ -1,0 +1,226 @@
+"""Instance-type catalogue: host-side mirror of the reference's instancetype + offering providers.
+
+  load_ec2_table()         the committed EC2 facts (tools/extract_fixtures.py; data, not source)
+  compute_requirements()   R:pkg/providers/instancetype/types.go:158-292 computeRequirements (AL2023)
+  resolve()                R:types.go:123-155 NewInstanceType — capacity and Overhead.Total() are
+                           computed behind the C ABI by kp_instance_type_resolve (libkp)
+  create_offerings()       R:pkg/providers/instancetype/offering/offering.go:101-150 createOfferings
+                           with pricing lookups R:pkg/providers/pricing/pricing.go:145-170
+
+Synthetic pricing: on-demand from the static us-east-1 table; spot = OD × U(0.3, 0.7)
+per (type, zone) from splitmix64(seed=20250704), in table order then zone order.
+"""
+import ctypes as C
+import os
+import re
+
+from . import abi
+from .model import InstanceType, Offering
+
+DATA = os.path.join(abi.PKG_ROOT, "data", "ec2_instance_types.tsv")
+ZONES = ["test-zone-1a", "test-zone-1b", "test-zone-1c"]          # R:pkg/fake/ec2api.go:480-505
+ZONE_IDS = ["tstz1-1a", "tstz1-1b", "tstz1-1c"]
+REGION = "us-east-1"
+SPOT_SEED = 20250704
+
+INSTANCE_TYPE_SCHEME = re.compile(r"(^[a-z]+)(\-[0-9]+tb)?([0-9]+).*\.")  # R:types.go:49
+K = "karpenter.k8s.aws/"
+
+_INT_COLS = {"vcpu", "memory_mib", "gpu_count", "accel_count", "neuron_devices", "neuron_cores_per_device", "efa",
+             "max_enis", "ipv4_per_eni", "trunking", "branch_enis"}
+
+
+def load_ec2_table(path=DATA):
+    rows = []
+    with open(path) as f:
+        header = None
+        for line in f:
+            if line.startswith("#"):
+                continue
+            parts = line.rstrip("\n").split("\t")
+            if header is None:
+                header = parts
+                continue
+            r = dict(zip(header, parts))
+            for c in _INT_COLS:
+                r[c] = int(r[c])
+            r["od_price"] = float(r["od_price"])
+            rows.append(r)
+    return rows
+
+
+class SplitMix64:
+    def __init__(self, seed):
+        self.s = seed & 0xFFFFFFFFFFFFFFFF
+
+    def next(self):
+        self.s = (self.s + 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+        z = self.s
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+        return z ^ (z >> 31)
+
+    def uniform(self):
+        return (self.next() >> 11) * (1.0 / (1 << 53))
+
+
+def compute_requirements(row, region=REGION, zones=ZONES, zone_ids=ZONE_IDS, offering_zones=None):
+    """computeRequirements (R:types.go:158-292) for the AL2023 family, no capacity reservations."""
+    name = row["name"]
+    offering_zones = zones if offering_zones is None else offering_zones
+    available = [z for z in zones if z in set(offering_zones)]
+    DNE = lambda k: (k, "DoesNotExist", [])
+    reqs = {
+        "node.kubernetes.io/instance-type": ("node.kubernetes.io/instance-type", "In", [name]),
+        "kubernetes.io/arch": ("kubernetes.io/arch", "In", [row["arch"]]),
+        "kubernetes.io/os": ("kubernetes.io/os", "In", ["linux"]),
+        "topology.kubernetes.io/zone": ("topology.kubernetes.io/zone", "In", available),
+        "topology.kubernetes.io/region": ("topology.kubernetes.io/region", "In", [region]),
+        "node.kubernetes.io/windows-build": DNE("node.kubernetes.io/windows-build"),
+        "karpenter.sh/capacity-type": ("karpenter.sh/capacity-type", "In", ["on-demand", "spot"]),
+        K + "instance-cpu": (K + "instance-cpu", "In", [str(row["vcpu"])]),
+        K + "instance-memory": (K + "instance-memory", "In", [str(row["memory_mib"])]),
+        K + "instance-hypervisor": (K + "instance-hypervisor", "In", [row["hypervisor"]]),
+        K + "instance-encryption-in-transit-supported": (K + "instance-encryption-in-transit-supported", "In",
+                                                         [row["encryption_in_transit"]]),
+    }
+    for k in ["instance-cpu-manufacturer", "instance-cpu-sustained-clock-speed-mhz", "instance-ebs-bandwidth",
+              "instance-network-bandwidth", "instance-category", "instance-family", "instance-generation",
+              "instance-local-nvme", "instance-size", "instance-gpu-name", "instance-gpu-manufacturer",
+              "instance-gpu-count", "instance-gpu-memory", "instance-accelerator-name",
+              "instance-accelerator-manufacturer", "instance-accelerator-count"]:
+        reqs[K + k] = DNE(K + k)
+    ids = [zid for z, zid in zip(zones, zone_ids) if z in set(available) and zid]
+    if ids:
+        reqs["topology.k8s.aws/zone-id"] = ("topology.k8s.aws/zone-id", "In", ids)
+    reqs[K + "capacity-reservation-id"] = DNE(K + "capacity-reservation-id")
+    reqs[K + "capacity-reservation-type"] = DNE(K + "capacity-reservation-type")
+
+    def ins(k, v):
+        reqs[K + k] = (K + k, "In", [v])
+
+    m = INSTANCE_TYPE_SCHEME.search(name)
+    if m:
+        ins("instance-category", m.group(1))
+        ins("instance-generation", m.group(3))
+    parts = name.split(".")
+    if len(parts) == 2:
+        ins("instance-family", parts[0])
+        ins("instance-size", parts[1])
+    if row["local_nvme_gb"]:
+        ins("instance-local-nvme", row["local_nvme_gb"])
+    if row["network_bandwidth"]:
+        ins("instance-network-bandwidth", row["network_bandwidth"])
+    if row["gpu_name"]:
+        ins("instance-gpu-name", row["gpu_name"])
+        ins("instance-gpu-manufacturer", row["gpu_manufacturer"])
+        ins("instance-gpu-count", str(row["gpu_count"]))
+        ins("instance-gpu-memory", row["gpu_memory_mib"])
+    if row["accel_name"]:
+        ins("instance-accelerator-name", row["accel_name"])
+        ins("instance-accelerator-manufacturer", row["accel_manufacturer"])
+        ins("instance-accelerator-count", str(row["accel_count"]))
+    ins("instance-cpu-manufacturer", row["cpu_manufacturer"])
+    ins("instance-cpu-sustained-clock-speed-mhz", row["clock_mhz"])
+    if row["ebs_bandwidth"]:
+        ins("instance-ebs-bandwidth", row["ebs_bandwidth"])
+    return list(reqs.values())
+
+
+def ec2_info(arena, row):
+    i = abi.EC2Info()
+    s = arena.s
+    i.name = s(row["name"])
+    i.vcpu = row["vcpu"]
+    i.memory_mib = row["memory_mib"]
+    i.arch = s(row["arch"])
+    i.hypervisor = s(row["hypervisor"])
+    i.encryption_in_transit = 1 if row["encryption_in_transit"] == "true" else 0
+    i.clock_mhz = int(row["clock_mhz"] or 0)
+    i.cpu_manufacturer = s(row["cpu_manufacturer"])
+    i.ebs_bandwidth_mbps = int(row["ebs_bandwidth"] or 0)
+    i.network_bandwidth_mbps = int(row["network_bandwidth"] or 0)
+    i.local_nvme_gb = int(row["local_nvme_gb"] or 0)
+    i.gpu_name = s(row["gpu_name"])
+    i.gpu_manufacturer = s(row["gpu_manufacturer"])
+    i.gpu_count = row["gpu_count"]
+    i.gpu_memory_mib = int(row["gpu_memory_mib"] or 0)
+    i.accel_name = s(row["accel_name"])
+    i.accel_manufacturer = s(row["accel_manufacturer"])
+    i.accel_count = row["accel_count"]
+    i.neuron_devices = row["neuron_devices"]
+    i.neuron_cores_per_device = row["neuron_cores_per_device"]
+    i.efa = row["efa"]
+    i.max_enis = row["max_enis"]
+    i.ipv4_per_eni = row["ipv4_per_eni"]
+    i.trunking = row["trunking"]
+    i.branch_enis = row["branch_enis"]
+    i.in_limits_table = 1 if row["eni_source"] == "vpclimits" else 0
+    return i
+
+
+def nodeclass(arena, zones=ZONES, zone_ids=ZONE_IDS, max_pods=None, pods_per_core=None):
+    nc = abi.NodeClass()
+    nc.region = arena.s(REGION)
+    nc.zones = arena.arr(C.c_char_p, [arena.s(z) for z in zones])
+    nc.zone_ids = arena.arr(C.c_char_p, [arena.s(z) for z in zone_ids])
+    nc.n_zones = len(zones)
+    nc.max_pods = -1 if max_pods is None else max_pods
+    nc.pods_per_core = 0 if pods_per_core is None else pods_per_core
+    return nc
+
+
+def resource_dict(rl):
+    return {abi.RES_NAMES[i]: int(rl.milli[i]) for i in range(abi.NUM_RES) if rl.present & (1 << i)}
+
+
+def create_offerings(row, reqs, spot_prices, zones=ZONES, zone_ids=ZONE_IDS, unavailable=frozenset()):
+    """createOfferings (R:offering.go:101-150): zones × {on-demand, spot}; Available = !ICE ∧ hasPrice ∧ zone∈itZones."""
+    it_zones = set(next(r for r in reqs if r[0] == "topology.kubernetes.io/zone")[2])
+    zid = dict(zip(zones, zone_ids))
+    out = []
+    od = row["od_price"]
+    for z in zones:
+        for ct in ("on-demand", "spot"):
+            if ct == "on-demand":
+                price, has = (od, True) if od >= 0 else (0.0, False)
+            else:
+                price, has = (spot_prices[(row["name"], z)], True) if od >= 0 else (0.0, False)
+            ice = (ct, row["name"], z) in unavailable or ct in unavailable or z in unavailable
+            out.append(Offering(ct, z, zid.get(z), price, (not ice) and has and z in it_zones))
+    return out
+
+
+def spot_price_table(rows, zones=ZONES, seed=SPOT_SEED):
+    g = SplitMix64(seed)
+    out = {}
+    for r in rows:
+        for z in zones:
+            u = g.uniform()
+            out[(r["name"], z)] = (r["od_price"] if r["od_price"] >= 0 else 0.0) * (0.3 + 0.4 * u)
+    return out
+
+
+def build_catalog(lib, rows=None, opts=None, max_pods=None, pods_per_core=None, zones=ZONES, zone_ids=ZONE_IDS,
+                  unavailable=frozenset()):
+    """GetInstanceTypes for one EC2NodeClass: NewInstanceType for every row, then InjectOfferings."""
+    rows = load_ec2_table() if rows is None else rows
+    arena = abi.Arena()
+    opts = opts or default_options()
+    nc = nodeclass(arena, zones, zone_ids, max_pods, pods_per_core)
+    spot = spot_price_table(rows, zones)
+    out = []
+    for r in rows:
+        info = ec2_info(arena, r)
+        cap, ovh = abi.ResourceList(), abi.ResourceList()
+        rc = lib.kp_instance_type_resolve(C.byref(opts), C.byref(info), C.byref(nc), C.byref(cap), C.byref(ovh))
+        if rc != 0:
+            raise RuntimeError(f"kp_instance_type_resolve({r['name']}) = {rc}")
+        reqs = compute_requirements(r, zones=zones, zone_ids=zone_ids)
+        out.append(InstanceType(r["name"], reqs, resource_dict(cap), resource_dict(ovh),
+                                create_offerings(r, reqs, spot, zones, zone_ids, unavailable)))
+    return out
+
+
+def default_options(device=0):
+    return abi.Options(0.075, 0, device)

@@ -1,0 +1,106 @@
+"""Python mirror of the reference objects on the hot path (names follow the reference).
+
+  InstanceType / Offering   <- sigs.k8s.io/karpenter pkg/cloudprovider types, built by
+                               R:pkg/providers/instancetype/types.go:123-155 and offering.go:101-150
+  NodePool                  <- karpv1.NodePool (the fields NewNodeClaimTemplate reads)
+  PodShape / pods           <- corev1.Pod fields the scheduler reads (requests, nodeSelector, node
+                               affinity, tolerations); pods are (shape, creationTimestamp, uid)
+  ExistingNode              <- state.StateNode as seen by upstream scheduling.ExistingNode
+
+Requirements are lists of tuples (key, operator, values[, minValues]) exactly like
+scheduling.NewRequirementWithFlexibility's arguments. Quantities are int milli-units.
+"""
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+
+Req = Tuple  # (key, op, [values], minValues|None)
+
+
+@dataclass
+class Offering:
+    capacity_type: str
+    zone: str
+    zone_id: Optional[str]
+    price: float
+    available: bool
+    reservation_id: Optional[str] = None
+    reservation_type: Optional[str] = None
+    reservation_capacity: int = 0
+
+
+@dataclass
+class InstanceType:
+    name: str
+    requirements: List[Req]
+    capacity: Dict[str, int]
+    overhead: Dict[str, int]
+    offerings: List[Offering] = field(default_factory=list)
+
+    def allocatable(self):
+        out = dict(self.capacity)
+        for k, v in self.overhead.items():
+            if k in out:
+                out[k] -= v
+        return out
+
+
+@dataclass
+class NodePool:
+    name: str
+    weight: int = 0
+    catalog: int = 0
+    requirements: List[Req] = field(default_factory=list)
+    labels: Dict[str, str] = field(default_factory=dict)
+    taints: List[Tuple[str, str, str]] = field(default_factory=list)  # (key, value, effect)
+    limits: Dict[str, int] = field(default_factory=dict)
+    daemon_requests: Dict[str, int] = field(default_factory=dict)
+
+
+@dataclass
+class PodShape:
+    requests: Dict[str, int]
+    node_selector: Dict[str, str] = field(default_factory=dict)
+    required_terms: List[List[Req]] = field(default_factory=list)
+    preferred_terms: List[Tuple[int, List[Req]]] = field(default_factory=list)
+    tolerations: List[Tuple[str, str, str, str]] = field(default_factory=list)  # (key, op, value, effect)
+
+
+@dataclass
+class ExistingNode:
+    name: str
+    labels: Dict[str, str]
+    available: Dict[str, int]
+    requests: Dict[str, int] = field(default_factory=dict)
+    taints: List[Tuple[str, str, str]] = field(default_factory=list)
+    initialized: bool = True
+
+
+@dataclass
+class Problem:
+    catalogs: List[List[InstanceType]]
+    nodepools: List[NodePool]
+    shapes: List[PodShape]
+    pod_shape: np.ndarray           # uint32 [P]
+    pod_creation: np.ndarray        # int64 [P]
+    pod_uid: np.ndarray             # uint64 [P] (order-preserving UID key)
+    existing: List[ExistingNode] = field(default_factory=list)
+    max_instance_types: int = 100
+    name: str = ""
+
+    @property
+    def n_pods(self):
+        return int(len(self.pod_shape))
+
+
+MI = 1 << 20
+GI = 1 << 30
+
+
+def cpu(m):
+    return int(m)
+
+
+def mem_mi(x):
+    return int(x) * MI * 1000

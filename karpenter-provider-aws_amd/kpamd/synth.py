@@ -1,0 +1,215 @@
+"""Synthetic workloads of BASELINE.json's configs and randomized parity scenarios.
+
+All generators are deterministic in their seed. Pods are (shape, creationTimestamp, uid); every shape's
+requests include pods=1 the way resources.RequestsForPods adds it.
+"""
+import numpy as np
+
+from .catalog import ZONES
+from .model import ExistingNode, NodePool, PodShape, Problem
+
+K = "karpenter.k8s.aws/"
+MI = 1 << 20
+CPU_GRID = [100, 250, 500, 1000, 2000, 4000]
+MEM_GRID = [128, 256, 512, 1024, 2048, 4096, 8192]
+
+
+def req_res(cpu_m, mem_mi, extra=None):
+    r = {"cpu": int(cpu_m), "memory": int(mem_mi) * MI * 1000, "pods": 1000}
+    if extra:
+        r.update(extra)
+    return r
+
+
+def _pods(rng, n, n_shapes, weights=None):
+    if weights is None:
+        shape = rng.integers(0, n_shapes, size=n).astype(np.uint32)
+    else:
+        p = np.asarray(weights, dtype=np.float64)
+        shape = rng.choice(n_shapes, size=n, p=p / p.sum()).astype(np.uint32)
+    creation = (1_750_000_000 + rng.integers(0, 600, size=n)).astype(np.int64)
+    uid = rng.integers(0, np.iinfo(np.int64).max, size=n, dtype=np.int64).astype(np.uint64)
+    return shape, creation, uid
+
+
+KWOK_POOL_REQS = [  # R:kwok/README.md:32-61
+    ("kubernetes.io/arch", "In", ["amd64"]),
+    ("kubernetes.io/os", "In", ["linux"]),
+    ("karpenter.sh/capacity-type", "In", ["on-demand"]),
+    (K + "instance-category", "In", ["c", "m", "r"]),
+    (K + "instance-generation", "Gt", ["2"]),
+]
+
+
+def config1(catalog, n_pods=1000, seed=1):
+    """1,000 pending pods (cpu/mem only) × full catalogue, the kwok README NodePool (limits cpu 1000)."""
+    rng = np.random.default_rng(seed)
+    shapes = [PodShape(req_res(c, m)) for c in CPU_GRID for m in MEM_GRID]
+    s, c, u = _pods(rng, n_pods, len(shapes))
+    np_ = NodePool("default", 0, 0, list(KWOK_POOL_REQS), limits={"cpu": 1000 * 1000})
+    return Problem([catalog], [np_], shapes, s, c, u, name=f"config1-{n_pods}")
+
+
+def config2(catalog, n_pods=50_000, seed=2, n_shapes=256):
+    """50k pods from 256 deployment shapes with mixed nodeSelector / node affinity / tolerations."""
+    rng = np.random.default_rng(seed)
+    shapes = []
+    for i in range(n_shapes):
+        cpu_m = int(rng.choice(CPU_GRID))
+        mem = int(rng.choice(MEM_GRID))
+        f = i / n_shapes
+        sh = PodShape(req_res(cpu_m, mem))
+        if f < 0.40:
+            pass
+        elif f < 0.60:
+            sh.node_selector = {"topology.kubernetes.io/zone": ZONES[i % 3]}
+        elif f < 0.75:
+            if i % 2 == 0:
+                sh.required_terms = [[(K + "instance-category", "In", ["c", "m", "r"])]]
+            else:
+                sh.required_terms = [[(K + "instance-cpu", "Gt", ["3"])]]
+        elif f < 0.85:
+            sh.required_terms = [[("kubernetes.io/arch", "NotIn", ["arm64"])]]
+        else:
+            sh.tolerations = [("dedicated", "Equal", "gpu", "NoSchedule")]
+            sh.node_selector = {"karpenter.sh/nodepool": "dedicated"}
+        shapes.append(sh)
+    s, c, u = _pods(rng, n_pods, len(shapes))
+    pools = [
+        NodePool("general", 10, 0, [("kubernetes.io/os", "In", ["linux"]),
+                                    ("karpenter.sh/capacity-type", "In", ["on-demand", "spot"]),
+                                    (K + "instance-generation", "Gt", ["2"])]),
+        NodePool("spot-compute", 5, 0, [("karpenter.sh/capacity-type", "In", ["spot"]),
+                                        (K + "instance-category", "In", ["c", "m"])]),
+        NodePool("dedicated", 1, 0, [("karpenter.sh/capacity-type", "In", ["on-demand"]),
+                                     (K + "instance-generation", "Gt", ["4"])],
+                 taints=[("dedicated", "gpu", "NoSchedule")]),
+    ]
+    return Problem([catalog], pools, shapes, s, c, u, name=f"config2-{n_pods}")
+
+
+def config5(catalog, n_pods=1_000_000, seed=5, n_shapes=512):
+    """1M-pod burst over 20 weighted NodePools with cpu limits; 4 NVIDIA-GPU pools, 2 Neuron pools (tainted)."""
+    rng = np.random.default_rng(seed)
+    pools = []
+    for w in range(1, 21):
+        name = f"pool-{w:02d}"
+        limits = {"cpu": int(rng.integers(2_000, 20_000)) * 1000}
+        if w <= 4:
+            pools.append(NodePool(name, w, 0, [(K + "instance-gpu-manufacturer", "In", ["nvidia"])],
+                                  taints=[("nvidia.com/gpu", "true", "NoSchedule")], limits=limits))
+        elif w <= 6:
+            pools.append(NodePool(name, w, 0, [(K + "instance-accelerator-manufacturer", "In", ["aws"])],
+                                  taints=[("aws.amazon.com/neuron", "true", "NoSchedule")], limits=limits))
+        else:
+            cats = [["c"], ["m"], ["r"], ["c", "m"], ["m", "r"], ["c", "m", "r"], ["t"]][w % 7]
+            pools.append(NodePool(name, w, 0, [(K + "instance-category", "In", cats),
+                                               ("karpenter.sh/capacity-type", "In", ["on-demand", "spot"])],
+                                  limits=limits))
+    shapes = []
+    weights = []
+    for i in range(n_shapes):
+        cpu_m = int(rng.choice(CPU_GRID))
+        mem = int(rng.choice(MEM_GRID))
+        r = i % 16
+        if r == 0:
+            sh = PodShape(req_res(cpu_m, mem, {"nvidia.com/gpu": 1000 * int(rng.choice([1, 2, 4]))}),
+                          tolerations=[("nvidia.com/gpu", "Exists", "", "NoSchedule")])
+        elif r == 1:
+            sh = PodShape(req_res(cpu_m, mem, {"aws.amazon.com/neuron": 1000}),
+                          tolerations=[("aws.amazon.com/neuron", "Exists", "", "NoSchedule")])
+        elif r < 6:
+            sh = PodShape(req_res(cpu_m, mem), node_selector={"topology.kubernetes.io/zone": ZONES[i % 3]})
+        else:
+            sh = PodShape(req_res(cpu_m, mem))
+        shapes.append(sh)
+        weights.append(0.25 if r <= 1 else 1.0)
+    s, c, u = _pods(rng, n_pods, len(shapes), weights)
+    return Problem([catalog], pools, shapes, s, c, u, name=f"config5-{n_pods}")
+
+
+# ------------------------------------------------------------------------------------------------
+# randomized parity scenarios (oracle vs device), small enough for the set-based oracle
+# ------------------------------------------------------------------------------------------------
+def random_problem(catalog, seed, n_types=120, n_pods=300, n_pools=3, n_existing=0, n_shapes=24):
+    rng = np.random.default_rng(seed)
+    idx = np.sort(rng.choice(len(catalog), size=min(n_types, len(catalog)), replace=False))
+    cat = [catalog[i] for i in idx]
+    fams = sorted({r[2][0] for it in cat for r in it.requirements if r[0] == K + "instance-family" and r[2]})
+
+    def rand_req(for_pool):
+        kind = rng.integers(0, 14)
+        if kind == 0:
+            return (K + "instance-category", "In", list(rng.choice(["c", "m", "r", "t", "g", "x"], size=2, replace=False)))
+        if kind == 1:
+            return (K + "instance-category", "NotIn", [str(rng.choice(["c", "m", "r", "t"]))])
+        if kind == 2:
+            return (K + "instance-cpu", "Gt", [str(int(rng.choice([1, 2, 3, 4, 8, 16])))])
+        if kind == 3:
+            return (K + "instance-cpu", "Lt", [str(int(rng.choice([4, 8, 16, 33, 64])))])
+        if kind == 4:
+            return ("kubernetes.io/arch", "In", [str(rng.choice(["amd64", "arm64"]))])
+        if kind == 5:
+            return ("kubernetes.io/arch", "NotIn", ["arm64"])
+        if kind == 6:
+            return ("topology.kubernetes.io/zone", "In", list(rng.choice(ZONES, size=int(rng.integers(1, 3)), replace=False)))
+        if kind == 7:
+            return ("topology.kubernetes.io/zone", "NotIn", [str(rng.choice(ZONES))])
+        if kind == 8:
+            return ("karpenter.sh/capacity-type", "In", list(rng.choice(["spot", "on-demand"], size=int(rng.integers(1, 3)), replace=False)))
+        if kind == 9:
+            return (K + "instance-gpu-manufacturer", "DoesNotExist", [])
+        if kind == 10:
+            return (K + "instance-local-nvme", "Exists", [])
+        if kind == 11:
+            return (K + "instance-generation", "Gt", [str(int(rng.integers(1, 6)))])
+        if kind == 12 and fams:
+            return (K + "instance-family", "In" if rng.random() < 0.5 else "NotIn",
+                    list(rng.choice(fams, size=min(len(fams), int(rng.integers(1, 6))), replace=False)))
+        return (K + "instance-hypervisor", "In", ["nitro"])
+
+    pools = []
+    for i in range(n_pools):
+        reqs = [rand_req(True) for _ in range(int(rng.integers(0, 3)))]
+        if rng.random() < 0.15:
+            reqs.append((K + "instance-family", "Exists", [], int(rng.integers(2, 5))))  # minValues
+        taints = [("dedicated", f"team{i}", "NoSchedule")] if rng.random() < 0.3 else []
+        limits = {"cpu": int(rng.integers(8, 200)) * 1000} if rng.random() < 0.5 else {}
+        daemon = {"cpu": int(rng.choice([0, 100, 250])), "memory": 64 * MI * 1000, "pods": 1000} if rng.random() < 0.5 else {}
+        pools.append(NodePool(f"pool-{i}", int(rng.integers(0, 4)), 0, reqs, labels={"team": f"t{i % 2}"},
+                              taints=taints, limits=limits, daemon_requests=daemon))
+    shapes = []
+    for s in range(n_shapes):
+        sh = PodShape(req_res(int(rng.choice(CPU_GRID)), int(rng.choice(MEM_GRID))))
+        r = rng.random()
+        if r < 0.2:
+            sh.node_selector = {"topology.kubernetes.io/zone": str(rng.choice(ZONES))}
+        elif r < 0.3:
+            sh.node_selector = {"team": f"t{int(rng.integers(0, 3))}"}
+        if rng.random() < 0.4:
+            sh.required_terms = [[rand_req(False) for _ in range(int(rng.integers(1, 3)))]
+                                 for _ in range(int(rng.integers(1, 3)))]
+        if rng.random() < 0.25:
+            sh.preferred_terms = [(int(rng.integers(1, 100)), [rand_req(False)]) for _ in range(int(rng.integers(1, 3)))]
+        if rng.random() < 0.3:
+            sh.tolerations = [("dedicated", "Exists", "", "NoSchedule")] if rng.random() < 0.5 else \
+                [("dedicated", "Equal", f"team{int(rng.integers(0, n_pools))}", "")]
+        if rng.random() < 0.05:
+            sh.requests["nvidia.com/gpu"] = 1000
+        shapes.append(sh)
+    existing = []
+    for e in range(n_existing):
+        it = cat[int(rng.integers(0, len(cat)))]
+        labels = {r[0]: r[2][0] for r in it.requirements if r[1] == "In" and len(r[2]) == 1}
+        labels["topology.kubernetes.io/zone"] = str(rng.choice(ZONES))
+        labels["karpenter.sh/capacity-type"] = str(rng.choice(["spot", "on-demand"]))
+        labels["karpenter.sh/nodepool"] = pools[int(rng.integers(0, n_pools))].name
+        labels["kubernetes.io/hostname"] = f"node-{e:05d}"
+        alloc = it.allocatable()
+        frac = float(rng.uniform(0.1, 0.9))
+        avail = {k: int(v * frac) for k, v in alloc.items() if k in ("cpu", "memory", "pods")}
+        existing.append(ExistingNode(f"node-{e:05d}", labels, avail, {},
+                                     [("dedicated", "team0", "NoSchedule")] if rng.random() < 0.1 else [],
+                                     bool(rng.random() < 0.9)))
+    s, c, u = _pods(rng, n_pods, len(shapes))
+    return Problem([cat], pools, shapes, s, c, u, existing=existing, name=f"random-{seed}")

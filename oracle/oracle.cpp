@@ -1,0 +1,1247 @@
+/*
+ * oracle.cpp — CPU restatement of the reference's bin-packing hot path.  TEST INFRASTRUCTURE ONLY.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library, and
+ * only as the checker / the timed CPU baseline ("kind": "port"). The product (libkp.so) never links
+ * or calls it.
+ *
+ * It is written the way the reference computes: string-keyed maps of string sets (Go
+ * map[string]*Requirement with sets.Set[string]), resource maps, per-type scans, Go's pdqsort.
+ * Nothing here shares code with the device path's bitset encoding — that is the point.
+ *
+ * What it restates (file:line in /root/reference, "UP" = sigs.k8s.io/karpenter
+ * v1.5.1-0.20250617212656-d0f1c47a99dd pinned at R:go.mod:49, absent from this container; its
+ * behaviour is restated from SURVEY.md §8(a) a10-a19 and Appendix B):
+ *   - instancetype.NewInstanceType / computeRequirements / computeCapacity / overhead
+ *     R:pkg/providers/instancetype/types.go:123-598 (AL2023 family flags R:amifamily/resolver.go:110-117)
+ *   - offering.createOfferings R:pkg/providers/instancetype/offering/offering.go:101-150
+ *   - filter.CompatibleAvailableFilter / SpotInstanceFilter / ExoticInstanceTypeFilter
+ *     R:pkg/providers/instance/filter/filter.go:39-64,279-386
+ *   - UP scheduling.Requirement(s): NewRequirementWithFlexibility, Intersection, Len, Operator,
+ *     Has, Add, Compatible, Intersects, IsCompatible (call sites R:filter.go:53,59, R:types.go:151)
+ *   - UP resources.Fits / Merge / Subtract (call site R:filter.go:56)
+ *   - UP Scheduler.Solve / Queue / add / addToExistingNode / addToInflightNode / addToNewNodeClaim /
+ *     NodeClaim.Add / ExistingNode.CanAdd / filterInstanceTypesByRequirements / filterByRemainingResources /
+ *     subtractMax / Preferences.Relax / Results.TruncateInstanceTypes / InstanceTypes.OrderByPrice /
+ *     SatisfiesMinValues  (driver: R:pkg/providers/instancetype/suite_test.go:93,279)
+ *   - Go 1.24 sort.Slice (pdqsort_func, zsortfunc.go) — upstream sorts newNodeClaims by len(Pods)
+ *     with it before every addToInflightNode.
+ *
+ * Parity: the catalogue half is pinned by R:website/content/en/preview/reference/instance-types.md
+ * (tests/golden/docs_*.tsv) and the KATs of R:pkg/providers/instancetype/suite_test.go; the filter half
+ * by R:pkg/providers/instance/filter/filter_test.go (tests/golden/filter_cases.json). Solve tie-breaks
+ * (queue order, in-flight order, relaxation order) are "parity unpinned": no Go toolchain and no
+ * upstream module here, so this file IS the written spec for them.
+ */
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <map>
+#include <memory>
+#include <regex>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "kp/kp_abi.h"
+
+namespace oracle {
+
+using std::map;
+using std::set;
+using std::string;
+using std::vector;
+
+static const int64_t kMaxInt64 = std::numeric_limits<int64_t>::max();
+
+// ---------------------------------------------------------------------------------------------
+// Label keys (R:pkg/apis/v1/labels.go, corev1, karpv1)
+// ---------------------------------------------------------------------------------------------
+static const char* kLabelZone = "topology.kubernetes.io/zone";
+static const char* kLabelRegion = "topology.kubernetes.io/region";
+static const char* kLabelInstanceType = "node.kubernetes.io/instance-type";
+static const char* kLabelArch = "kubernetes.io/arch";
+static const char* kLabelOS = "kubernetes.io/os";
+static const char* kLabelWindowsBuild = "node.kubernetes.io/windows-build";
+static const char* kLabelCapacityType = "karpenter.sh/capacity-type";
+static const char* kLabelNodePool = "karpenter.sh/nodepool";
+static const char* kLabelHostname = "kubernetes.io/hostname";
+static const char* kLabelZoneID = "topology.k8s.aws/zone-id";
+static const char* kLabelResID = "karpenter.k8s.aws/capacity-reservation-id";   // cloudprovider.ReservationIDLabel (R:pkg/apis/v1/doc.go:38)
+static const char* kLabelResType = "karpenter.k8s.aws/capacity-reservation-type";
+#define AWSL(x) "karpenter.k8s.aws/" x
+
+// karpv1.WellKnownLabels + the AWS insertions of R:pkg/apis/v1/labels.go:31-56.
+static const set<string>& WellKnown() {
+  static const set<string> s = {
+      kLabelNodePool, kLabelZone, kLabelRegion, kLabelInstanceType, kLabelArch, kLabelOS, kLabelCapacityType,
+      kLabelWindowsBuild, kLabelResID, kLabelResType, AWSL("instance-hypervisor"),
+      AWSL("instance-encryption-in-transit-supported"), AWSL("instance-category"), AWSL("instance-family"),
+      AWSL("instance-generation"), AWSL("instance-size"), AWSL("instance-local-nvme"), AWSL("instance-cpu"),
+      AWSL("instance-cpu-manufacturer"), AWSL("instance-cpu-sustained-clock-speed-mhz"), AWSL("instance-memory"),
+      AWSL("instance-ebs-bandwidth"), AWSL("instance-network-bandwidth"), AWSL("instance-gpu-name"),
+      AWSL("instance-gpu-manufacturer"), AWSL("instance-gpu-count"), AWSL("instance-gpu-memory"),
+      AWSL("instance-accelerator-name"), AWSL("instance-accelerator-manufacturer"),
+      AWSL("instance-accelerator-count"), kLabelZoneID};
+  return s;
+}
+
+// karpv1.NormalizedLabels (+ the kwok/test-env addition, R:kwok/operator/operator.go:73).
+static string Normalize(const string& k) {
+  static const map<string, string> m = {
+      {"failure-domain.beta.kubernetes.io/zone", kLabelZone},
+      {"beta.kubernetes.io/arch", kLabelArch},
+      {"beta.kubernetes.io/os", kLabelOS},
+      {"beta.kubernetes.io/instance-type", kLabelInstanceType},
+      {"failure-domain.beta.kubernetes.io/region", kLabelRegion},
+      {"topology.ebs.csi.aws.com/zone", kLabelZone},
+  };
+  auto it = m.find(k);
+  return it == m.end() ? k : it->second;
+}
+
+// Go strconv.Atoi (64-bit int): optional sign, decimal digits, no overflow.
+static bool GoAtoi(const string& s, int64_t* out) {
+  if (s.empty()) return false;
+  size_t i = 0;
+  bool neg = false;
+  if (s[0] == '+' || s[0] == '-') {
+    neg = s[0] == '-';
+    i = 1;
+    if (s.size() == 1) return false;
+  }
+  unsigned __int128 v = 0;
+  for (; i < s.size(); i++) {
+    if (s[i] < '0' || s[i] > '9') return false;
+    v = v * 10 + (unsigned)(s[i] - '0');
+    if (v > (unsigned __int128)kMaxInt64 + 1) return false;
+  }
+  if (!neg && v > (unsigned __int128)kMaxInt64) return false;
+  *out = neg ? (int64_t)(-(__int128)v) : (int64_t)v;
+  return true;
+}
+
+// ---------------------------------------------------------------------------------------------
+// UP scheduling.Requirement
+// ---------------------------------------------------------------------------------------------
+struct Requirement {
+  string key;
+  set<string> values;
+  bool complement = false;
+  bool has_gt = false, has_lt = false;
+  int64_t gt = 0, lt = 0;
+  bool has_min = false;
+  int min_values = 0;
+
+  int64_t Len() const { return complement ? kMaxInt64 - (int64_t)values.size() : (int64_t)values.size(); }
+  // Operator(): Gt/Lt are "Exists with bounds".
+  int Op() const {
+    if (complement) return Len() < kMaxInt64 ? KP_OP_NOT_IN : KP_OP_EXISTS;
+    return Len() > 0 ? KP_OP_IN : KP_OP_DOES_NOT_EXIST;
+  }
+  bool NegOp() const {
+    int o = Op();
+    return o == KP_OP_NOT_IN || o == KP_OP_DOES_NOT_EXIST;
+  }
+};
+
+static bool Within(const string& v, bool hg, int64_t gt, bool hl, int64_t lt) {
+  if (!hg && !hl) return true;
+  int64_t x;
+  if (!GoAtoi(v, &x)) return false;
+  if (hg && gt >= x) return false;
+  if (hl && lt <= x) return false;
+  return true;
+}
+
+static bool Has(const Requirement& r, const string& v) {
+  bool in = r.values.count(v) > 0;
+  if (r.complement) return !in && Within(v, r.has_gt, r.gt, r.has_lt, r.lt);
+  return in && Within(v, r.has_gt, r.gt, r.has_lt, r.lt);
+}
+
+static Requirement NewRequirement(const string& key_in, int op, const vector<string>& values, int min_values) {
+  Requirement r;
+  r.key = Normalize(key_in);
+  if (min_values >= 0) {
+    r.has_min = true;
+    r.min_values = min_values;
+  }
+  if (op == KP_OP_IN) {
+    r.values.insert(values.begin(), values.end());
+    r.complement = false;
+    return r;
+  }
+  r.complement = !(op == KP_OP_DOES_NOT_EXIST);
+  if (op == KP_OP_NOT_IN) r.values.insert(values.begin(), values.end());
+  if (op == KP_OP_GT) {
+    int64_t x = 0;
+    GoAtoi(values.empty() ? "" : values[0], &x);  // prevalidated upstream; Atoi error -> 0
+    r.has_gt = true;
+    r.gt = x;
+  }
+  if (op == KP_OP_LT) {
+    int64_t x = 0;
+    GoAtoi(values.empty() ? "" : values[0], &x);
+    r.has_lt = true;
+    r.lt = x;
+  }
+  return r;
+}
+
+// Requirement.Intersection.
+static Requirement Intersection(const Requirement& a, const Requirement& b) {
+  Requirement out;
+  out.key = a.key;
+  bool comp = a.complement && b.complement;
+  bool hg = a.has_gt || b.has_gt, hl = a.has_lt || b.has_lt;
+  int64_t gt = 0, lt = 0;
+  if (a.has_gt && b.has_gt) gt = std::max(a.gt, b.gt);
+  else if (a.has_gt) gt = a.gt;
+  else if (b.has_gt) gt = b.gt;
+  if (a.has_lt && b.has_lt) lt = std::min(a.lt, b.lt);
+  else if (a.has_lt) lt = a.lt;
+  else if (b.has_lt) lt = b.lt;
+  out.has_min = a.has_min || b.has_min;
+  if (a.has_min && b.has_min) out.min_values = std::max(a.min_values, b.min_values);
+  else if (a.has_min) out.min_values = a.min_values;
+  else if (b.has_min) out.min_values = b.min_values;
+  if (hg && hl && gt >= lt) {
+    // NewRequirementWithFlexibility(key, DoesNotExist, minValues)
+    out.complement = false;
+    return out;
+  }
+  set<string> vals;
+  if (a.complement && b.complement) {
+    vals = a.values;
+    vals.insert(b.values.begin(), b.values.end());
+  } else if (a.complement && !b.complement) {
+    for (auto& v : b.values)
+      if (!a.values.count(v)) vals.insert(v);
+  } else if (!a.complement && b.complement) {
+    for (auto& v : a.values)
+      if (!b.values.count(v)) vals.insert(v);
+  } else {
+    for (auto& v : a.values)
+      if (b.values.count(v)) vals.insert(v);
+  }
+  for (auto it = vals.begin(); it != vals.end();) {
+    if (!Within(*it, hg, gt, hl, lt)) it = vals.erase(it);
+    else ++it;
+  }
+  out.values = std::move(vals);
+  out.complement = comp;
+  if (comp) {
+    out.has_gt = hg;
+    out.gt = gt;
+    out.has_lt = hl;
+    out.lt = lt;
+  }
+  return out;
+}
+
+using Requirements = map<string, Requirement>;
+
+static void Add(Requirements& r, const Requirement& req) {
+  auto it = r.find(req.key);
+  if (it != r.end()) it->second = Intersection(req, it->second);
+  else r[req.key] = req;
+}
+static void AddAll(Requirements& r, const Requirements& o) {
+  for (auto& kv : o) Add(r, kv.second);
+}
+static bool HasMinValues(const Requirements& r) {
+  for (auto& kv : r)
+    if (kv.second.has_min) return true;
+  return false;
+}
+
+// Requirements.Intersects: for every shared key the intersection must be non-empty, unless both
+// operators are in {NotIn, DoesNotExist}.
+static bool Intersects(const Requirements& r, const Requirements& q) {
+  for (auto& kv : r) {
+    auto it = q.find(kv.first);
+    if (it == q.end()) continue;
+    const Requirement& existing = kv.second;
+    const Requirement& incoming = it->second;
+    if (Intersection(existing, incoming).Len() == 0) {
+      if (incoming.NegOp() && existing.NegOp()) continue;
+      return false;
+    }
+  }
+  return true;
+}
+
+// Requirements.Compatible(q, AllowUndefined?)
+static bool Compatible(const Requirements& r, const Requirements& q, bool allow_undefined_wellknown) {
+  for (auto& kv : q) {
+    if (r.count(kv.first)) continue;
+    if (kv.second.NegOp()) continue;
+    if (allow_undefined_wellknown && WellKnown().count(kv.first)) continue;
+    return false;
+  }
+  return Intersects(r, q);
+}
+
+static Requirements FromABI(const kp_requirements& in) {
+  Requirements r;
+  for (uint32_t i = 0; i < in.n; i++) {
+    const kp_requirement& q = in.items[i];
+    vector<string> vals;
+    for (uint32_t j = 0; j < q.n_values; j++) vals.push_back(q.values[j] ? q.values[j] : "");
+    Add(r, NewRequirement(q.key, q.op, vals, q.min_values));
+  }
+  return r;
+}
+static Requirements LabelRequirements(const kp_label* labels, uint32_t n) {
+  Requirements r;
+  for (uint32_t i = 0; i < n; i++) Add(r, NewRequirement(labels[i].key, KP_OP_IN, {labels[i].value}, -1));
+  return r;
+}
+
+// ---------------------------------------------------------------------------------------------
+// UP resources (map semantics: a missing key is zero)
+// ---------------------------------------------------------------------------------------------
+using ResourceList = map<int, int64_t>;
+
+static ResourceList FromABI(const kp_resource_list& in) {
+  ResourceList r;
+  for (int i = 0; i < KP_NUM_RESOURCES; i++)
+    if (in.present & (1u << i)) r[i] = in.milli[i];
+  return r;
+}
+static kp_resource_list ToABI(const ResourceList& r) {
+  kp_resource_list o;
+  memset(&o, 0, sizeof(o));
+  for (auto& kv : r) {
+    o.milli[kv.first] = kv.second;
+    o.present |= 1u << kv.first;
+  }
+  return o;
+}
+static int64_t Get(const ResourceList& r, int k) {
+  auto it = r.find(k);
+  return it == r.end() ? 0 : it->second;
+}
+static ResourceList Merge(const ResourceList& a, const ResourceList& b) {
+  ResourceList o = a;
+  for (auto& kv : b) o[kv.first] += kv.second;
+  return o;
+}
+// resources.Subtract(a, b): keys of a, minus b's value when present.
+static ResourceList Subtract(const ResourceList& a, const ResourceList& b) {
+  ResourceList o = a;
+  for (auto& kv : o) kv.second -= Get(b, kv.first);
+  return o;
+}
+// resources.Fits(candidate, total)
+static bool Fits(const ResourceList& candidate, const ResourceList& total) {
+  for (auto& kv : total)
+    if (kv.second < 0) return false;
+  for (auto& kv : candidate)
+    if (kv.second > Get(total, kv.first)) return false;
+  return true;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Taints (UP scheduling.Taints.ToleratesPod + corev1 Toleration.ToleratesTaint)
+// ---------------------------------------------------------------------------------------------
+struct Taint {
+  string key, value;
+  int effect;
+};
+struct Toleration {
+  string key, value;
+  int op, effect;
+};
+static bool ToleratesTaint(const Toleration& t, const Taint& taint) {
+  if (t.effect != KP_EFFECT_ANY && t.effect != taint.effect) return false;
+  if (!t.key.empty() && t.key != taint.key) return false;
+  if (t.op == KP_TOL_EQUAL) return t.value == taint.value;
+  if (t.op == KP_TOL_EXISTS) return true;
+  return false;
+}
+static bool ToleratesAll(const vector<Taint>& taints, const vector<Toleration>& tols) {
+  for (auto& taint : taints) {
+    bool ok = false;
+    for (auto& t : tols) ok = ok || ToleratesTaint(t, taint);
+    if (!ok) return false;
+  }
+  return true;
+}
+
+// ---------------------------------------------------------------------------------------------
+// cloudprovider.InstanceType / Offering (UP pkg/cloudprovider/types.go)
+// ---------------------------------------------------------------------------------------------
+struct Offering {
+  Requirements reqs;
+  double price;
+  bool available;
+};
+struct InstanceType {
+  string name;
+  Requirements reqs;
+  ResourceList capacity, overhead, allocatable;
+  vector<Offering> offerings;
+};
+
+static std::shared_ptr<vector<InstanceType>> CatalogFromABI(const kp_catalog_desc& d) {
+  auto out = std::make_shared<vector<InstanceType>>();
+  out->reserve(d.n_types);
+  for (uint32_t i = 0; i < d.n_types; i++) {
+    const kp_instance_type& t = d.types[i];
+    InstanceType it;
+    it.name = t.name;
+    it.reqs = FromABI(t.requirements);
+    it.capacity = FromABI(t.capacity);
+    it.overhead = FromABI(t.overhead);
+    it.allocatable = Subtract(it.capacity, it.overhead);  // InstanceType.Allocatable()
+    for (uint32_t j = 0; j < t.n_offerings; j++) {
+      const kp_offering& o = t.offerings[j];
+      Offering of;
+      Add(of.reqs, NewRequirement(kLabelCapacityType, KP_OP_IN, {o.capacity_type}, -1));
+      if (o.zone) Add(of.reqs, NewRequirement(kLabelZone, KP_OP_IN, {o.zone}, -1));
+      if (o.reservation_id) Add(of.reqs, NewRequirement(kLabelResID, KP_OP_IN, {o.reservation_id}, -1));
+      else Add(of.reqs, NewRequirement(kLabelResID, KP_OP_DOES_NOT_EXIST, {}, -1));
+      if (o.reservation_type) Add(of.reqs, NewRequirement(kLabelResType, KP_OP_IN, {o.reservation_type}, -1));
+      else Add(of.reqs, NewRequirement(kLabelResType, KP_OP_DOES_NOT_EXIST, {}, -1));
+      if (o.zone_id) Add(of.reqs, NewRequirement(kLabelZoneID, KP_OP_IN, {o.zone_id}, -1));
+      of.price = o.price;
+      of.available = o.available != 0;
+      it.offerings.push_back(std::move(of));
+    }
+    out->push_back(std::move(it));
+  }
+  return out;
+}
+
+// Offerings.Available().Compatible(reqs) non-empty (R:filter.go:59; UP filterInstanceTypesByRequirements)
+static bool HasCompatibleAvailable(const InstanceType& it, const Requirements& reqs) {
+  for (auto& o : it.offerings)
+    if (o.available && Compatible(reqs, o.reqs, true)) return true;
+  return false;
+}
+// Cheapest compatible available offering price, MaxFloat64 when none (UP OrderByPrice).
+static double CheapestPrice(const InstanceType& it, const Requirements& reqs) {
+  double p = std::numeric_limits<double>::max();
+  bool any = false;
+  for (auto& o : it.offerings)
+    if (o.available && Compatible(reqs, o.reqs, true)) {
+      if (!any || o.price < p) p = o.price;
+      any = true;
+    }
+  return p;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Go sort.Slice — pdqsort_func (Go 1.24 src/sort/zsortfunc.go), restated over less/swap.
+// ---------------------------------------------------------------------------------------------
+template <class LS>
+struct PDQ {
+  LS& d;
+  enum { increasingHint, decreasingHint, unknownHint };
+  void insertionSort(int a, int b) {
+    for (int i = a + 1; i < b; i++)
+      for (int j = i; j > a && d.Less(j, j - 1); j--) d.Swap(j, j - 1);
+  }
+  void siftDown(int lo, int hi, int first) {
+    int root = lo;
+    for (;;) {
+      int child = 2 * root + 1;
+      if (child >= hi) return;
+      if (child + 1 < hi && d.Less(first + child, first + child + 1)) child++;
+      if (!d.Less(first + root, first + child)) return;
+      d.Swap(first + root, first + child);
+      root = child;
+    }
+  }
+  void heapSort(int a, int b) {
+    int first = a, lo = 0, hi = b - a;
+    for (int i = (hi - 1) / 2; i >= 0; i--) siftDown(i, hi, first);
+    for (int i = hi - 1; i >= 0; i--) {
+      d.Swap(first, first + i);
+      siftDown(lo, i, first);
+    }
+  }
+  static int bitsLen(uint64_t x) { return x == 0 ? 0 : 64 - __builtin_clzll(x); }
+  void breakPatterns(int a, int b) {
+    int length = b - a;
+    if (length >= 8) {
+      uint64_t random = (uint64_t)length;
+      uint64_t modulus = 1ull << bitsLen((uint64_t)length);
+      int idx = a + (length / 4) * 2 - 1;
+      for (int i = 0; i < 3; i++) {
+        random ^= random << 13;
+        random ^= random >> 7;
+        random ^= random << 17;
+        int other = (int)((unsigned)random & (unsigned)(modulus - 1));
+        if (other >= length) other -= length;
+        d.Swap(idx - 1 + i, a + other);
+      }
+    }
+  }
+  void order2(int& a, int& b, int* swaps) {
+    if (d.Less(b, a)) {
+      (*swaps)++;
+      std::swap(a, b);
+    }
+  }
+  int median(int a, int b, int c, int* swaps) {
+    order2(a, b, swaps);
+    order2(b, c, swaps);
+    order2(a, b, swaps);
+    return b;
+  }
+  int medianAdjacent(int a, int* swaps) { return median(a - 1, a, a + 1, swaps); }
+  int choosePivot(int a, int b, int* hint) {
+    const int shortestNinther = 50, maxSwaps = 4 * 3;
+    int l = b - a, swaps = 0;
+    int i = a + l / 4 * 1, j = a + l / 4 * 2, k = a + l / 4 * 3;
+    if (l >= 8) {
+      if (l >= shortestNinther) {
+        i = medianAdjacent(i, &swaps);
+        j = medianAdjacent(j, &swaps);
+        k = medianAdjacent(k, &swaps);
+      }
+      j = median(i, j, k, &swaps);
+    }
+    *hint = swaps == 0 ? increasingHint : (swaps == maxSwaps ? decreasingHint : unknownHint);
+    return j;
+  }
+  void reverseRange(int a, int b) {
+    int i = a, j = b - 1;
+    while (i < j) d.Swap(i++, j--);
+  }
+  bool partialInsertionSort(int a, int b) {
+    const int maxSteps = 5, shortestShifting = 50;
+    int i = a + 1;
+    for (int j = 0; j < maxSteps; j++) {
+      while (i < b && !d.Less(i, i - 1)) i++;
+      if (i == b) return true;
+      if (b - a < shortestShifting) return false;
+      d.Swap(i, i - 1);
+      if (i - a >= 2) {
+        for (int k = i - 1; k >= 1; k--) {
+          if (!d.Less(k, k - 1)) break;
+          d.Swap(k, k - 1);
+        }
+      }
+      if (b - i >= 2) {
+        for (int k = i + 1; k < b; k++) {
+          if (!d.Less(k, k - 1)) break;
+          d.Swap(k, k - 1);
+        }
+      }
+    }
+    return false;
+  }
+  int partitionEqual(int a, int b, int pivot) {
+    d.Swap(a, pivot);
+    int i = a + 1, j = b - 1;
+    for (;;) {
+      while (i <= j && !d.Less(a, i)) i++;
+      while (i <= j && d.Less(a, j)) j--;
+      if (i > j) break;
+      d.Swap(i, j);
+      i++;
+      j--;
+    }
+    return i;
+  }
+  int partition(int a, int b, int pivot, bool* already) {
+    d.Swap(a, pivot);
+    int i = a + 1, j = b - 1;
+    while (i <= j && d.Less(i, a)) i++;
+    while (i <= j && !d.Less(j, a)) j--;
+    if (i > j) {
+      d.Swap(j, a);
+      *already = true;
+      return j;
+    }
+    d.Swap(i, j);
+    i++;
+    j--;
+    for (;;) {
+      while (i <= j && d.Less(i, a)) i++;
+      while (i <= j && !d.Less(j, a)) j--;
+      if (i > j) break;
+      d.Swap(i, j);
+      i++;
+      j--;
+    }
+    d.Swap(j, a);
+    *already = false;
+    return j;
+  }
+  void pdqsort(int a, int b, int limit) {
+    const int maxInsertion = 12;
+    bool wasBalanced = true, wasPartitioned = true;
+    for (;;) {
+      int length = b - a;
+      if (length <= maxInsertion) {
+        insertionSort(a, b);
+        return;
+      }
+      if (limit == 0) {
+        heapSort(a, b);
+        return;
+      }
+      if (!wasBalanced) {
+        breakPatterns(a, b);
+        limit--;
+      }
+      int hint;
+      int pivot = choosePivot(a, b, &hint);
+      if (hint == decreasingHint) {
+        reverseRange(a, b);
+        pivot = (b - 1) - (pivot - a);
+        hint = increasingHint;
+      }
+      if (wasBalanced && wasPartitioned && hint == increasingHint) {
+        if (partialInsertionSort(a, b)) return;
+      }
+      if (a > 0 && !d.Less(a - 1, pivot)) {
+        int mid = partitionEqual(a, b, pivot);
+        a = mid;
+        continue;
+      }
+      bool already = false;
+      int mid = partition(a, b, pivot, &already);
+      wasPartitioned = already;
+      int leftLen = mid - a, rightLen = b - mid;
+      int balanceThreshold = length / 8;
+      if (leftLen < rightLen) {
+        wasBalanced = leftLen >= balanceThreshold;
+        pdqsort(a, mid, limit);
+        a = mid + 1;
+      } else {
+        wasBalanced = rightLen >= balanceThreshold;
+        pdqsort(mid + 1, b, limit);
+        b = mid;
+      }
+    }
+  }
+};
+template <class LS>
+static void GoSortSlice(LS& ls, int n) {
+  PDQ<LS> p{ls};
+  p.pdqsort(0, n, PDQ<LS>::bitsLen((uint64_t)n));
+}
+
+// ---------------------------------------------------------------------------------------------
+// UP scheduler
+// ---------------------------------------------------------------------------------------------
+struct Template {
+  int nodepool;       // index into input nodepools
+  string name;
+  int weight;
+  Requirements reqs;  // NewNodeClaimTemplate
+  vector<Taint> taints;
+  const vector<InstanceType>* catalog;
+  vector<int> options;  // InstanceTypeOptions (indices into catalog)
+  ResourceList daemon;
+  bool has_limits;
+  ResourceList remaining;
+};
+
+struct PodState {
+  int index;
+  int shape;
+  int64_t cpu, mem;  // sort keys
+  int64_t creation;
+  uint64_t uid;
+  // relaxable spec (Preferences.Relax mutates the pod)
+  vector<Requirements> required_terms;
+  vector<std::pair<int, Requirements>> preferred;  // (weight, preference)
+  Requirements node_selector;
+  ResourceList requests;
+  vector<Toleration> tolerations;
+  Requirements reqs;  // cached NewPodRequirements
+};
+
+// NewPodRequirements (UP scheduling/requirements.go): nodeSelector + heaviest preferred term (treated
+// as required) + the first required term.
+static Requirements PodRequirements(PodState& p) {
+  Requirements r = p.node_selector;
+  if (!p.preferred.empty()) {
+    // sort.Slice(preferred, weight desc) mutates the pod; len <= 12 is insertion sort (stable)
+    struct LS {
+      vector<std::pair<int, Requirements>>& v;
+      bool Less(int i, int j) { return v[i].first > v[j].first; }
+      void Swap(int i, int j) { std::swap(v[i], v[j]); }
+    } ls{p.preferred};
+    GoSortSlice(ls, (int)p.preferred.size());
+    AddAll(r, p.preferred[0].second);
+  }
+  if (!p.required_terms.empty()) AddAll(r, p.required_terms[0]);
+  return r;
+}
+
+// Preferences.Relax (UP preferences.go): first applicable of removeRequiredNodeAffinityTerm (only when
+// >1 terms), [pod affinity/anti-affinity: not modelled], removePreferredNodeAffinityTermByWeight,
+// [ScheduleAnyway spreads: ABI v1 has none].
+static bool Relax(PodState& p) {
+  if (p.required_terms.size() > 1) {
+    p.required_terms.erase(p.required_terms.begin());
+    return true;
+  }
+  if (!p.preferred.empty()) {
+    std::stable_sort(p.preferred.begin(), p.preferred.end(),
+                     [](const std::pair<int, Requirements>& a, const std::pair<int, Requirements>& b) {
+                       return a.first > b.first;
+                     });
+    p.preferred.erase(p.preferred.begin());
+    return true;
+  }
+  return false;
+}
+
+struct NodeClaim {
+  int id;  // creation order
+  const Template* tmpl;
+  Requirements reqs;
+  vector<int> options;
+  ResourceList requests;
+  vector<int> pods;
+};
+
+struct ExistingNode {
+  int index;  // input index
+  string name;
+  bool initialized;
+  Requirements reqs;
+  vector<Taint> taints;
+  ResourceList available, requests;
+  vector<int> pods;
+};
+
+static bool SatisfiesMinValues(const vector<InstanceType>& cat, const vector<int>& its, const Requirements& reqs) {
+  if (!HasMinValues(reqs)) return true;
+  map<string, set<string>> valuesForKey;
+  for (int t : its) {
+    for (auto& kv : reqs) {
+      if (!kv.second.has_min) continue;
+      auto& s = valuesForKey[kv.first];
+      auto f = cat[t].reqs.find(kv.first);
+      if (f != cat[t].reqs.end()) s.insert(f->second.values.begin(), f->second.values.end());  // Get(key).Values()
+    }
+    bool ok = true;
+    for (auto& kv : valuesForKey)
+      if ((int)kv.second.size() < reqs.at(kv.first).min_values) ok = false;
+    if (ok) return true;
+  }
+  return false;
+}
+
+struct Counters {
+  uint64_t attempts = 0, type_checks = 0, pops = 0;
+};
+
+// filterInstanceTypesByRequirements (UP nodeclaim.go) with relaxMinValues = false.
+static bool FilterInstanceTypes(const vector<InstanceType>& cat, const vector<int>& its, const Requirements& reqs,
+                                const ResourceList& total, vector<int>* out, Counters* c) {
+  out->clear();
+  for (int t : its) {
+    c->type_checks++;
+    const InstanceType& it = cat[t];
+    bool compat = Intersects(it.reqs, reqs);
+    bool fits = Fits(total, it.allocatable);
+    bool hasOffering = false;
+    for (auto& o : it.offerings)
+      if (o.available && Compatible(reqs, o.reqs, true)) {
+        hasOffering = true;
+        break;
+      }
+    if (compat && fits && hasOffering) out->push_back(t);
+  }
+  if (HasMinValues(reqs) && !SatisfiesMinValues(cat, *out, reqs)) out->clear();
+  return !out->empty();
+}
+
+struct Scheduler {
+  vector<Template> templates;  // ordered by weight desc, name asc
+  vector<ExistingNode> existing;
+  vector<std::unique_ptr<NodeClaim>> created;  // creation order
+  vector<NodeClaim*> newNodeClaims;            // the slice the scheduler sorts
+  map<int, vector<int>> unused;
+  Counters counters;
+
+  // NodeClaim.Add
+  bool NodeClaimAdd(NodeClaim& n, PodState& p) {
+    counters.attempts++;
+    if (!ToleratesAll(n.tmpl->taints, p.tolerations)) return false;
+    Requirements ncr = n.reqs;
+    if (!Compatible(ncr, p.reqs, true)) return false;
+    AddAll(ncr, p.reqs);
+    ResourceList requests = Merge(n.requests, p.requests);
+    vector<int> remaining;
+    if (!FilterInstanceTypes(*n.tmpl->catalog, n.options, ncr, requests, &remaining, &counters)) return false;
+    n.pods.push_back(p.index);
+    n.options = std::move(remaining);
+    n.requests = requests;
+    n.reqs = std::move(ncr);
+    return true;
+  }
+
+  bool ExistingCanAddAndAdd(ExistingNode& n, PodState& p) {
+    counters.attempts++;
+    if (!ToleratesAll(n.taints, p.tolerations)) return false;
+    ResourceList requests = Merge(n.requests, p.requests);
+    if (!Fits(requests, n.available)) return false;
+    Requirements nr = n.reqs;
+    if (!Compatible(nr, p.reqs, false)) return false;
+    AddAll(nr, p.reqs);
+    n.pods.push_back(p.index);
+    n.requests = requests;
+    n.reqs = std::move(nr);
+    return true;
+  }
+
+  bool add(PodState& p) {
+    for (auto& n : existing)
+      if (ExistingCanAddAndAdd(n, p)) return true;
+    struct LS {
+      vector<NodeClaim*>& v;
+      bool Less(int i, int j) { return v[i]->pods.size() < v[j]->pods.size(); }
+      void Swap(int i, int j) { std::swap(v[i], v[j]); }
+    } ls{newNodeClaims};
+    GoSortSlice(ls, (int)newNodeClaims.size());
+    for (NodeClaim* n : newNodeClaims)
+      if (NodeClaimAdd(*n, p)) return true;
+    if (templates.empty()) return false;
+    for (auto& t : templates) {
+      vector<int> its = t.options;
+      if (t.has_limits) {
+        vector<int> f;
+        for (int i : its) {
+          bool viable = true;
+          for (auto& kv : t.remaining)
+            if (Get((*t.catalog)[i].capacity, kv.first) > kv.second) viable = false;
+          if (viable) f.push_back(i);
+        }
+        its.swap(f);
+        if (its.empty()) continue;
+      }
+      auto nc = std::make_unique<NodeClaim>();
+      nc->id = (int)created.size();
+      nc->tmpl = &t;
+      nc->reqs = t.reqs;  // + hostname In {placeholder}: inert here (ABI v1 rejects hostname selectors)
+      nc->options = its;
+      nc->requests = t.daemon;
+      if (!NodeClaimAdd(*nc, p)) continue;
+      if (t.has_limits) {  // subtractMax over the new NodeClaim's InstanceTypeOptions
+        ResourceList mx;
+        for (int i : nc->options)
+          for (auto& kv : (*t.catalog)[i].capacity) {
+            auto f = mx.find(kv.first);
+            if (f == mx.end() || kv.second > f->second) mx[kv.first] = kv.second;
+          }
+        for (auto& kv : t.remaining) kv.second -= Get(mx, kv.first);
+      }
+      newNodeClaims.push_back(nc.get());
+      created.push_back(std::move(nc));
+      return true;
+    }
+    return false;
+  }
+};
+
+}  // namespace oracle
+
+// =============================================================================================
+// C API (tests / bench cpu_baseline only)
+// =============================================================================================
+using namespace oracle;
+
+struct kpo_result {
+  std::vector<int32_t> placement;
+  struct NC {
+    uint32_t nodepool;
+    std::vector<uint32_t> pods, options;
+    uint32_t n_remaining;
+    kp_resource_list requests;
+  };
+  std::vector<NC> ncs;
+  kp_solve_stats stats;
+};
+
+extern "C" {
+
+typedef struct kpo_nodeclaim {
+  uint32_t nodepool, n_pods, n_remaining, n_options;
+  const uint32_t* pods;
+  const uint32_t* options;
+  kp_resource_list requests;
+} kpo_nodeclaim;
+
+static std::vector<Taint> TaintsFromABI(const kp_taint* t, uint32_t n) {
+  std::vector<Taint> v;
+  for (uint32_t i = 0; i < n; i++) v.push_back({t[i].key ? t[i].key : "", t[i].value ? t[i].value : "", t[i].effect});
+  return v;
+}
+
+int32_t kpo_solve(const kp_solve_in* in, kpo_result** out) {
+  auto t0 = std::chrono::steady_clock::now();
+  if (!in || !out || (!in->catalog_descs && in->n_catalogs)) return KP_E_INVAL;
+  std::vector<std::shared_ptr<std::vector<InstanceType>>> cats;
+  for (uint32_t i = 0; i < in->n_catalogs; i++) cats.push_back(CatalogFromABI(in->catalog_descs[i]));
+
+  Scheduler s;
+  // NewScheduler: templates per NodePool ordered by weight desc, name asc; options pre-filtered by the
+  // template requirements with empty requests.
+  std::vector<int> order(in->n_nodepools);
+  for (uint32_t i = 0; i < in->n_nodepools; i++) order[i] = (int)i;
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+    if (in->nodepools[a].weight != in->nodepools[b].weight) return in->nodepools[a].weight > in->nodepools[b].weight;
+    return strcmp(in->nodepools[a].name, in->nodepools[b].name) < 0;
+  });
+  for (int idx : order) {
+    const kp_nodepool& np = in->nodepools[idx];
+    if (np.catalog >= in->n_catalogs) return KP_E_INVAL;
+    Template t;
+    t.nodepool = idx;
+    t.name = np.name;
+    t.weight = np.weight;
+    t.reqs = FromABI(np.requirements);
+    AddAll(t.reqs, LabelRequirements(np.labels, np.n_labels));
+    Add(t.reqs, NewRequirement(kLabelNodePool, KP_OP_IN, {np.name}, -1));
+    t.taints = TaintsFromABI(np.taints, np.n_taints);
+    t.catalog = cats[np.catalog].get();
+    std::vector<int> all(t.catalog->size());
+    for (size_t i = 0; i < all.size(); i++) all[i] = (int)i;
+    if (!FilterInstanceTypes(*t.catalog, all, t.reqs, ResourceList{}, &t.options, &s.counters)) continue;
+    t.daemon = FromABI(np.daemon_requests);
+    t.has_limits = np.limits.present != 0;
+    t.remaining = FromABI(np.limits);
+    s.templates.push_back(std::move(t));
+  }
+  for (uint32_t i = 0; i < in->n_existing; i++) {
+    const kp_existing_node& e = in->existing[i];
+    ExistingNode n;
+    n.index = (int)i;
+    n.name = e.name;
+    n.initialized = e.initialized != 0;
+    n.reqs = LabelRequirements(e.labels, e.n_labels);
+    n.taints = TaintsFromABI(e.taints, e.n_taints);
+    n.available = FromABI(e.available);
+    n.requests = FromABI(e.requests);
+    s.existing.push_back(std::move(n));
+  }
+  std::stable_sort(s.existing.begin(), s.existing.end(), [](const ExistingNode& a, const ExistingNode& b) {
+    if (a.initialized != b.initialized) return a.initialized;
+    return a.name < b.name;
+  });
+
+  std::vector<PodState> pods(in->n_pods);
+  for (uint32_t i = 0; i < in->n_pods; i++) {
+    const kp_pod& p = in->pods[i];
+    if (p.shape >= in->n_shapes) return KP_E_INVAL;
+    const kp_pod_shape& sh = in->shapes[p.shape];
+    if (sh.n_topology_spread) return KP_E_UNSUPPORTED;
+    PodState& ps = pods[i];
+    ps.index = (int)i;
+    ps.shape = (int)p.shape;
+    ps.creation = p.creation_unix;
+    ps.uid = p.uid_key;
+    ps.requests = FromABI(sh.requests);
+    ps.cpu = Get(ps.requests, KP_RES_CPU);
+    ps.mem = Get(ps.requests, KP_RES_MEMORY);
+    ps.node_selector = LabelRequirements(sh.node_selector, sh.n_node_selector);
+    for (uint32_t j = 0; j < sh.n_required_terms; j++) ps.required_terms.push_back(FromABI(sh.required_terms[j]));
+    for (uint32_t j = 0; j < sh.n_preferred_terms; j++)
+      ps.preferred.push_back({sh.preferred_terms[j].weight, FromABI(sh.preferred_terms[j].preference)});
+    for (uint32_t j = 0; j < sh.n_tolerations; j++) {
+      const kp_toleration& t = sh.tolerations[j];
+      ps.tolerations.push_back({t.key ? t.key : "", t.value ? t.value : "", t.op, t.effect});
+    }
+    ps.reqs = PodRequirements(ps);
+  }
+
+  // Queue (UP queue.go): byCPUAndMemoryDescending, a total order (UID tie-break).
+  std::vector<int> q(in->n_pods);
+  for (uint32_t i = 0; i < in->n_pods; i++) q[i] = (int)i;
+  std::sort(q.begin(), q.end(), [&](int a, int b) {
+    const PodState &l = pods[a], &r = pods[b];
+    if (l.cpu != r.cpu) return l.cpu > r.cpu;
+    if (l.mem != r.mem) return l.mem > r.mem;
+    if (l.creation != r.creation) return l.creation < r.creation;
+    return l.uid < r.uid;
+  });
+  std::vector<int> queue(q.begin(), q.end());
+  size_t head = 0;
+  std::map<int, size_t> lastLen;
+  std::vector<char> errored(in->n_pods, 0);
+  for (;;) {
+    size_t len = queue.size() - head;
+    if (len == 0) break;
+    int pi = queue[head];
+    auto ll = lastLen.find(pi);
+    if (ll != lastLen.end() && ll->second == len) break;
+    head++;
+    s.counters.pops++;
+    PodState& p = pods[pi];
+    if (s.add(p)) {
+      errored[pi] = 0;
+      continue;
+    }
+    errored[pi] = 1;
+    bool relaxed = Relax(p);
+    queue.push_back(pi);
+    if (relaxed) {
+      lastLen.clear();
+      p.reqs = PodRequirements(p);
+    } else {
+      lastLen[pi] = queue.size() - head;
+    }
+    // compact occasionally
+    if (head > 1024 && head * 2 > queue.size()) {
+      queue.erase(queue.begin(), queue.begin() + (long)head);
+      head = 0;
+    }
+  }
+
+  auto* res = new kpo_result();
+  res->placement.assign(in->n_pods, -1);
+  for (auto& e : s.existing)
+    for (int p : e.pods) res->placement[p] = -(2 + e.index);
+  // FinalizeScheduling + Results.TruncateInstanceTypes(max): OrderByPrice(reqs) then cut; minValues
+  // re-checked on the truncated list, failures turn the NodeClaim's pods into errors.
+  for (auto& ncp : s.created) {
+    NodeClaim& n = *ncp;
+    kpo_result::NC o;
+    o.nodepool = (uint32_t)n.tmpl->nodepool;
+    o.n_remaining = (uint32_t)n.options.size();
+    o.requests = ToABI(n.requests);
+    const auto& cat = *n.tmpl->catalog;
+    std::vector<std::pair<double, int>> keyed;
+    for (int t : n.options) keyed.push_back({CheapestPrice(cat[t], n.reqs), t});
+    std::stable_sort(keyed.begin(), keyed.end(), [&](const std::pair<double, int>& a, const std::pair<double, int>& b) {
+      if (a.first == b.first) return cat[a.second].name < cat[b.second].name;
+      return a.first < b.first;
+    });
+    std::vector<int> trunc;
+    size_t lim = in->max_instance_types ? std::min<size_t>(keyed.size(), in->max_instance_types) : keyed.size();
+    for (size_t i = 0; i < lim; i++) trunc.push_back(keyed[i].second);
+    bool ok = !HasMinValues(n.reqs) || SatisfiesMinValues(cat, trunc, n.reqs);
+    if (ok) {
+      for (int t : trunc) o.options.push_back((uint32_t)t);
+      for (int p : n.pods) {
+        o.pods.push_back((uint32_t)p);
+        res->placement[p] = n.id;
+      }
+    } else {
+      for (int p : n.pods) o.pods.push_back((uint32_t)p);  // pods listed, placement stays -1
+    }
+    res->ncs.push_back(std::move(o));
+  }
+  (void)errored;
+  memset(&res->stats, 0, sizeof(res->stats));
+  res->stats.attempts = s.counters.attempts;
+  res->stats.pops = s.counters.pops;
+  res->stats.bytes_algorithmic = s.counters.type_checks;  // type rows visited (SURVEY §8d counter)
+  res->stats.host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  *out = res;
+  return KP_OK;
+}
+
+uint32_t kpo_result_nodeclaim_count(const kpo_result* r) { return (uint32_t)r->ncs.size(); }
+int32_t kpo_result_pod_placements(const kpo_result* r, int32_t* out, uint32_t n) {
+  if (n != r->placement.size()) return KP_E_INVAL;
+  memcpy(out, r->placement.data(), n * sizeof(int32_t));
+  return KP_OK;
+}
+int32_t kpo_result_nodeclaim(const kpo_result* r, uint32_t i, kpo_nodeclaim* out) {
+  if (i >= r->ncs.size()) return KP_E_INVAL;
+  const auto& n = r->ncs[i];
+  out->nodepool = n.nodepool;
+  out->n_pods = (uint32_t)n.pods.size();
+  out->n_remaining = n.n_remaining;
+  out->n_options = (uint32_t)n.options.size();
+  out->pods = n.pods.data();
+  out->options = n.options.data();
+  out->requests = n.requests;
+  return KP_OK;
+}
+int32_t kpo_result_stats(const kpo_result* r, kp_solve_stats* out) {
+  *out = r->stats;
+  return KP_OK;
+}
+void kpo_result_destroy(kpo_result* r) { delete r; }
+
+// CompatibleAvailableFilter (R:filter.go:39-64) for one query; out_kept[t] = 1 when kept.
+// out_cheapest[t] = cheapest compatible available price (+inf when none).
+int32_t kpo_filter_compatible_available(const kp_catalog_desc* cat, const kp_feasibility_query* q, uint8_t* out_kept,
+                                        double* out_cheapest) {
+  auto types = CatalogFromABI(*cat);
+  Requirements reqs = FromABI(q->requirements);
+  ResourceList requests = FromABI(q->requests);
+  for (size_t t = 0; t < types->size(); t++) {
+    const InstanceType& it = (*types)[t];
+    bool kept = Compatible(reqs, it.reqs, true) && Fits(requests, it.allocatable) && HasCompatibleAvailable(it, reqs);
+    out_kept[t] = kept ? 1 : 0;
+    if (out_cheapest) {
+      bool any = false;
+      double p = INFINITY;
+      for (auto& o : it.offerings)
+        if (o.available && Compatible(reqs, o.reqs, true)) {
+          if (!any || o.price < p) p = o.price;
+          any = true;
+        }
+      out_cheapest[t] = p;
+    }
+  }
+  return KP_OK;
+}
+
+// SpotInstanceFilter (R:filter.go:328-386); reserved offerings are not representable in ABI v1.
+int32_t kpo_filter_spot(const kp_catalog_desc* cat, const kp_requirements* req, uint8_t* out_kept) {
+  auto types = CatalogFromABI(*cat);
+  Requirements reqs = FromABI(*req);
+  for (size_t t = 0; t < types->size(); t++) out_kept[t] = 1;
+  if (HasMinValues(reqs)) return KP_OK;
+  auto ct = reqs.find(kLabelCapacityType);
+  if (ct == reqs.end() || !Has(ct->second, "on-demand") || !Has(ct->second, "spot")) return KP_OK;
+  double cheapestOD = std::numeric_limits<double>::max();
+  bool hasSpot = false, hasOD = false;
+  auto capType = [](const Offering& o) { return *o.reqs.at(kLabelCapacityType).values.begin(); };
+  for (auto& it : *types)
+    for (auto& o : it.offerings) {
+      if (!Compatible(reqs, o.reqs, true) || !o.available) continue;
+      std::string c = capType(o);
+      if (c == "on-demand") {
+        hasOD = true;
+        if (o.price < cheapestOD) cheapestOD = o.price;
+      } else if (c == "spot") {
+        hasSpot = true;
+      }
+    }
+  if (!hasOD || !hasSpot) return KP_OK;
+  for (size_t t = 0; t < types->size(); t++) {
+    bool hasSpotOffering = false, keep = false;
+    for (auto& o : (*types)[t].offerings) {
+      if (!Compatible(reqs, o.reqs, true) || !o.available) continue;
+      std::string c = capType(o);
+      if (c == "reserved") {
+        keep = true;
+        break;
+      }
+      if (c == "spot") {
+        hasSpotOffering = true;
+        if (o.price <= cheapestOD) {
+          keep = true;
+          break;
+        }
+      }
+    }
+    out_kept[t] = (keep || !hasSpotOffering) ? 1 : 0;
+  }
+  return KP_OK;
+}
+
+// ExoticInstanceTypeFilter (R:filter.go:279-318)
+int32_t kpo_filter_exotic(const kp_catalog_desc* cat, const kp_requirements* req, uint8_t* out_kept) {
+  auto types = CatalogFromABI(*cat);
+  Requirements reqs = FromABI(*req);
+  size_t n = types->size();
+  for (size_t t = 0; t < n; t++) out_kept[t] = 1;
+  if (HasMinValues(reqs)) return KP_OK;
+  std::vector<uint8_t> generic(n, 0);
+  size_t ng = 0;
+  for (size_t t = 0; t < n; t++) {
+    const InstanceType& it = (*types)[t];
+    bool exotic = false;
+    auto sz = it.reqs.find(AWSL("instance-size"));
+    if (sz != it.reqs.end() && !sz->second.complement)
+      for (auto& v : sz->second.values)
+        if (v.find("metal") != std::string::npos) exotic = true;
+    for (int r : {KP_RES_NEURON, KP_RES_NEURONCORE, KP_RES_AMD_GPU, KP_RES_NVIDIA_GPU, KP_RES_GAUDI})
+      if (Get(it.capacity, r) != 0) exotic = true;
+    generic[t] = !exotic;
+    ng += !exotic;
+  }
+  if (ng == 0) return KP_OK;
+  for (size_t t = 0; t < n; t++) out_kept[t] = generic[t];
+  return KP_OK;
+}
+
+// Requirements algebra probe for tests: Compatible(a, b, allowUndefinedWellKnown) and Intersects(a, b).
+int32_t kpo_requirements_compatible(const kp_requirements* a, const kp_requirements* b, int32_t allow_wk) {
+  return Compatible(FromABI(*a), FromABI(*b), allow_wk != 0) ? 1 : 0;
+}
+int32_t kpo_requirements_intersects(const kp_requirements* a, const kp_requirements* b) {
+  return Intersects(FromABI(*a), FromABI(*b)) ? 1 : 0;
+}
+
+// ---- catalogue: NewInstanceType (R:types.go:123-598), AL2023 family ----------------------------
+typedef struct kpo_overhead {
+  kp_resource_list kube_reserved, system_reserved, eviction_threshold;
+} kpo_overhead;
+
+static int64_t Mi(int64_t x) { return x * 1048576ll * 1000ll; }
+
+static int64_t ENILimitedPods(const kp_ec2_info* info, int reservedENIs) {
+  int64_t usable = std::max<int64_t>((int64_t)info->max_enis - reservedENIs, 0);
+  if (usable == 0) return 0;
+  return usable * ((int64_t)info->ipv4_per_eni - 1) + 2;
+}
+
+int32_t kpo_instance_type_resolve(const kp_options* opts, const kp_ec2_info* info, const kp_nodeclass* nc,
+                                  kp_resource_list* capacity, kpo_overhead* overhead) {
+  ResourceList cap;
+  cap[KP_RES_CPU] = (int64_t)info->vcpu * 1000;
+  // memory(): arm64 loses 64 MiB of CMA; then subtract ceil(bytes*VMMemoryOverheadPercent/1024/1024) MiB
+  int64_t mib = info->memory_mib;
+  if (info->arch && std::string(info->arch) == "arm64") mib -= 64;
+  double bytes = (double)(mib * 1048576ll);
+  int64_t ovMiB = (int64_t)std::ceil(bytes * opts->vm_memory_overhead_percent / 1024 / 1024);
+  cap[KP_RES_MEMORY] = Mi(mib - ovMiB);
+  // ephemeralStorage(): no BDMs -> AL2023 default /dev/xvda 20Gi (R:amifamily/al2023.go:98-108, resolver.go:39-43)
+  int64_t storageBytes = 20ll * 1073741824ll;
+  cap[KP_RES_EPHEMERAL_STORAGE] = storageBytes * 1000;
+  // pods(): maxPods, else ENI-limited (AL2023 SupportsENILimitedPodDensity), then podsPerCore cap
+  int64_t pods;
+  if (nc && nc->max_pods >= 0) pods = nc->max_pods;
+  else pods = ENILimitedPods(info, opts->reserved_enis);
+  if (nc && nc->pods_per_core > 0) pods = std::min<int64_t>((int64_t)nc->pods_per_core * info->vcpu, pods);
+  cap[KP_RES_PODS] = pods * 1000;
+  cap[KP_RES_POD_ENI] = (info->in_limits_table && info->trunking) ? (int64_t)info->branch_enis * 1000 : 0;
+  std::string gm = info->gpu_manufacturer ? info->gpu_manufacturer : "";
+  cap[KP_RES_NVIDIA_GPU] = (gm == "nvidia" ? info->gpu_count : 0) * 1000ll;
+  cap[KP_RES_AMD_GPU] = (gm == "amd" ? info->gpu_count : 0) * 1000ll;
+  cap[KP_RES_NEURON] = (int64_t)info->neuron_devices * 1000;
+  cap[KP_RES_NEURONCORE] = (int64_t)info->neuron_devices * info->neuron_cores_per_device * 1000;
+  cap[KP_RES_GAUDI] = (gm == "habana" ? info->gpu_count : 0) * 1000ll;
+  cap[KP_RES_EFA] = (int64_t)info->efa * 1000;
+  *capacity = ToABI(cap);
+
+  // kubeReservedResources (memory uses ENILimitedPods(ctx, info, 0) for AL2023)
+  ResourceList kube;
+  kube[KP_RES_MEMORY] = Mi(11 * ENILimitedPods(info, 0) + 255);
+  kube[KP_RES_EPHEMERAL_STORAGE] = 1073741824ll * 1000;
+  struct R {
+    int64_t start, end;
+    double pct;
+  } ranges[4] = {{0, 1000, 0.06}, {1000, 2000, 0.01}, {2000, 4000, 0.005}, {4000, 1ll << 31, 0.0025}};
+  int64_t cpuM = cap[KP_RES_CPU];
+  for (auto& rg : ranges) {
+    if (cpuM >= rg.start) {
+      double r = (double)(rg.end - rg.start);
+      if (cpuM < rg.end) r = (double)(cpuM - rg.start);
+      kube[KP_RES_CPU] = Get(kube, KP_RES_CPU) + (int64_t)(r * rg.pct);
+    }
+  }
+  // evictionThreshold: memory 100Mi, ephemeral ceil(storage/100*10)
+  ResourceList ev;
+  ev[KP_RES_MEMORY] = Mi(100);
+  ev[KP_RES_EPHEMERAL_STORAGE] = (int64_t)std::ceil((double)storageBytes / 100 * 10) * 1000;
+  overhead->kube_reserved = ToABI(kube);
+  overhead->system_reserved = ToABI(ResourceList{});
+  overhead->eviction_threshold = ToABI(ev);
+  return KP_OK;
+}
+
+}  // extern "C"

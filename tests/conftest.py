@@ -1,0 +1,32 @@
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "karpenter-provider-aws_amd"))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
+
+
+@pytest.fixture(scope="session")
+def lib():
+    import kpamd
+    return kpamd.load_lib()
+
+
+@pytest.fixture(scope="session")
+def catalog(lib):
+    from kpamd import catalog as c
+    return c.build_catalog(lib)
+
+
+@pytest.fixture(scope="session")
+def ctx():
+    import kpamd
+    c = kpamd.Context(0)
+    yield c
+    c.close()

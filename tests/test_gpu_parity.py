@@ -1,0 +1,86 @@
+"""Device path (libkp.so on the MI355X) vs the CPU oracle on identical inputs — bit-exact.
+
+Compared: every pod's placement (NodeClaim creation index / existing node / error) and every NodeClaim's
+NodePool, pod list in add order, and instance-type options after OrderByPrice + Truncate(100).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def canon(r):
+    return [(n["nodepool"], n["pods"], n["options"], n["n_remaining"]) for n in r["nodeclaims"]]
+
+
+def check_same(got, want):
+    diff = np.nonzero(got["placement"] != want["placement"])[0]
+    assert len(diff) == 0, f"{len(diff)} placements differ, first pod {diff[:5]}: " \
+                           f"{got['placement'][diff[:5]]} vs {want['placement'][diff[:5]]}"
+    g, w = canon(got), canon(want)
+    assert len(g) == len(w)
+    for i, (a, b) in enumerate(zip(g, w)):
+        assert a == b, f"NodeClaim {i} differs: {a[:2]} {a[3]} vs {b[:2]} {b[3]}"
+
+
+def run_both(ctx, prob):
+    import kpamd
+    from oracle import pyoracle
+    got = kpamd.Scheduler(ctx, prob).solve()
+    want = pyoracle.solve(prob)
+    return got, want
+
+
+def test_config2_small(ctx, catalog):
+    from kpamd import synth
+    got, want = run_both(ctx, synth.config2(catalog, n_pods=400, seed=7))
+    check_same(got, want)
+
+
+def test_config1(ctx, catalog):
+    from kpamd import synth
+    got, want = run_both(ctx, synth.config1(catalog, n_pods=1000, seed=1))
+    check_same(got, want)
+    assert len(got["nodeclaims"]) > 0
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_scenarios(ctx, catalog, seed):
+    from kpamd import synth
+    prob = synth.random_problem(catalog, seed, n_types=150, n_pods=250, n_pools=3,
+                                n_existing=[0, 5, 40][seed % 3], n_shapes=20)
+    got, want = run_both(ctx, prob)
+    check_same(got, want)
+
+
+def test_config5_scaled(ctx, catalog):
+    from kpamd import synth
+    got, want = run_both(ctx, synth.config5(catalog, n_pods=3000, seed=5))
+    check_same(got, want)
+
+
+def test_config2_medium(ctx, catalog):
+    from kpamd import synth
+    got, want = run_both(ctx, synth.config2(catalog, n_pods=3000, seed=2))
+    check_same(got, want)
+
+
+def test_feasibility_kernel_vs_oracle(ctx, catalog):
+    """CompatibleAvailableFilter over the full catalogue for randomized (requirements, requests) rows."""
+    import kpamd
+    from kpamd import synth
+    from oracle import pyoracle
+    prob = synth.random_problem(catalog, 99, n_types=919, n_pods=10, n_shapes=40)
+    rng = np.random.default_rng(3)
+    queries = []
+    for sh in prob.shapes:
+        reqs = [r for t in sh.required_terms[:1] for r in t] + [(k, "In", [v]) for k, v in sh.node_selector.items()]
+        queries.append((reqs, sh.requests))
+    queries.append(([("karpenter.k8s.aws/instance-cpu", "Gt", ["15"]), ("kubernetes.io/arch", "NotIn", ["arm64"])],
+                    {"cpu": 8000, "memory": 1 << 40}))
+    cat = kpamd.Catalog(ctx, prob.catalogs[0])
+    kept, cheapest, _ = kpamd.compatible_available_filter(ctx, cat, queries)
+    for qi, (reqs, rq) in enumerate(queries):
+        want_k, want_c = pyoracle.compatible_available_filter(prob.catalogs[0], reqs, rq)
+        assert (kept[qi] == want_k).all(), f"query {qi}"
+        np.testing.assert_array_equal(cheapest[qi][want_k], want_c[want_k])
