@@ -421,7 +421,7 @@ bool Has(const Dict& d, const KReqs& q, int k, int bit) {
 // catalogue compile (per solve dictionary)
 // ------------------------------------------------------------------------------------------------
 struct HostCat {
-  int T = 0;
+  int T = 0, S = 0;
   vector<KReqs> treqs;
   vector<uint64_t> TM, DNE, NOKEY;    // [nbits][TW], [K][TW], [K][TW]
   vector<int64_t> alloc, cap;         // [R][T]
@@ -445,14 +445,16 @@ struct ClassKey {
 
 int32_t CompileCatalog(const Dict& d, const vector<HostType>& types, int TW, map<ClassKey, int>& classes, HostCat& hc) {
   const int T = (int)types.size(), K = d.dd.K, NB = d.dd.W * 64;
+  const int S = std::max(d.dd.T, T);  // row stride shared by every catalogue of the solve (device uses D.T)
   hc.T = T;
+  hc.S = S;
   hc.treqs.resize(T);
   hc.TM.assign((size_t)NB * TW, 0);
   hc.DNE.assign((size_t)K * TW, 0);
   hc.NOKEY.assign((size_t)K * TW, 0);
-  hc.code.assign((size_t)K * T, 0xFFFF);
-  hc.multi.assign((size_t)K * T, 0);
-  hc.custom_nonneg.assign(T, 0);
+  hc.code.assign((size_t)K * S, 0xFFFF);
+  hc.multi.assign((size_t)K * S, 0);
+  hc.custom_nonneg.assign(S, 0);
   for (int t = 0; t < T; t++) {
     KReqs q = Compile(d, types[t].reqs);
     hc.treqs[t] = q;
@@ -462,7 +464,7 @@ int32_t CompileCatalog(const Dict& d, const vector<HostType>& types, int TW, map
     for (int k = 0; k < K; k++) {
       const uint64_t kb = 1ull << k;
       if (!(q.present & kb)) {
-        hc.NOKEY[(size_t)k * TW + tw] |= tb;
+        hc.NOKEY[(size_t)k * SW + tw] |= tb;
         continue;
       }
       if ((q.compl_ & kb) || (q.hgt & kb) || (q.hlt & kb))
@@ -482,30 +484,30 @@ int32_t CompileCatalog(const Dict& d, const vector<HostType>& types, int TW, map
         }
       }
       if (cnt == 0) {
-        hc.DNE[(size_t)k * TW + tw] |= tb;
-        hc.code[(size_t)k * T + t] = 0xFFFE;
+        hc.DNE[(size_t)k * SW + tw] |= tb;
+        hc.code[(size_t)k * S + t] = 0xFFFE;
       } else if (cnt == 1) {
-        hc.code[(size_t)k * T + t] = (uint16_t)last;
+        hc.code[(size_t)k * S + t] = (uint16_t)last;
       } else {
         if (d.dd.nval[k] > 64) return fail(KP_E_UNSUPPORTED, "multi-valued key %s has > 64 values", d.keys[k].c_str());
         hc.multi_valued |= kb;
-        hc.code[(size_t)k * T + t] = 0xFFFD;
-        hc.multi[(size_t)k * T + t] = q.vals[d.dd.wofs[k]];
+        hc.code[(size_t)k * S + t] = 0xFFFD;
+        hc.multi[(size_t)k * S + t] = q.vals[d.dd.wofs[k]];
       }
     }
   }
   for (int k = 0; k < K; k++)  // keys whose types are multi-valued keep multi masks for every type
     if ((hc.multi_valued >> k) & 1)
       for (int t = 0; t < T; t++) {
-        uint16_t& c = hc.code[(size_t)k * T + t];
+        uint16_t& c = hc.code[(size_t)k * S + t];
         if (c < 0xFFFD) {
-          hc.multi[(size_t)k * T + t] = 1ull << (c % 64);
+          hc.multi[(size_t)k * S + t] = 1ull << (c % 64);
           c = 0xFFFD;
         }
       }
   // resources
-  hc.alloc.assign((size_t)KP_NRES * T, 0);
-  hc.cap.assign((size_t)KP_NRES * T, 0);
+  hc.alloc.assign((size_t)KP_NRES * S, 0);
+  hc.cap.assign((size_t)KP_NRES * S, 0);
   hc.nonneg.assign(TW, 0);
   for (int t = 0; t < T; t++) {
     bool nn = true;
@@ -513,25 +515,25 @@ int32_t CompileCatalog(const Dict& d, const vector<HostType>& types, int TW, map
       const bool pr = (types[t].cap_present >> r) & 1;
       const int64_t c = pr ? types[t].cap[r] : 0;
       const int64_t a = pr ? c - types[t].ovh[r] : 0;  // resources.Subtract(capacity, overhead): capacity keys
-      hc.cap[(size_t)r * T + t] = c;
-      hc.alloc[(size_t)r * T + t] = a;
+      hc.cap[(size_t)r * S + t] = c;
+      hc.alloc[(size_t)r * S + t] = a;
       if (pr && a < 0) nn = false;
     }
     if (nn) hc.nonneg[t / 64] |= 1ull << (t % 64);
   }
-  hc.fit_vals.assign((size_t)KP_NRES * T, 0);
+  hc.fit_vals.assign((size_t)KP_NRES * S, 0);
   hc.fit_n.assign(KP_NRES, 0);
-  hc.fit_mask.assign((size_t)KP_NRES * T * TW, 0);
+  hc.fit_mask.assign((size_t)KP_NRES * S * TW, 0);
   for (int r = 0; r < KP_NRES; r++) {
-    vector<int64_t> v(hc.alloc.begin() + (size_t)r * T, hc.alloc.begin() + (size_t)(r + 1) * T);
+    vector<int64_t> v(hc.alloc.begin() + (size_t)r * S, hc.alloc.begin() + (size_t)r * S + T);
     std::sort(v.begin(), v.end());
     v.erase(std::unique(v.begin(), v.end()), v.end());
     hc.fit_n[r] = (int)v.size();
-    std::copy(v.begin(), v.end(), hc.fit_vals.begin() + (size_t)r * T);
+    std::copy(v.begin(), v.end(), hc.fit_vals.begin() + (size_t)r * S);
     // fit_mask[r][j] = types with alloc >= v[j]: build from the top down
     vector<uint64_t> acc(TW, 0);
     vector<std::pair<int64_t, int>> byv;
-    for (int t = 0; t < T; t++) byv.push_back({hc.alloc[(size_t)r * T + t], t});
+    for (int t = 0; t < T; t++) byv.push_back({hc.alloc[(size_t)r * S + t], t});
     std::sort(byv.begin(), byv.end());
     int p = T - 1;
     for (int j = (int)v.size() - 1; j >= 0; j--) {
@@ -539,7 +541,7 @@ int32_t CompileCatalog(const Dict& d, const vector<HostType>& types, int TW, map
         acc[byv[p].second / 64] |= 1ull << (byv[p].second % 64);
         p--;
       }
-      std::copy(acc.begin(), acc.end(), hc.fit_mask.begin() + ((size_t)r * T + j) * TW);
+      std::copy(acc.begin(), acc.end(), hc.fit_mask.begin() + ((size_t)r * S + j) * TW);
     }
   }
   // offerings
@@ -559,7 +561,7 @@ int32_t CompileCatalog(const Dict& d, const vector<HostType>& types, int TW, map
   vector<int> idx(T);
   for (int t = 0; t < T; t++) idx[t] = t;
   std::sort(idx.begin(), idx.end(), [&](int a, int b) { return types[a].name < types[b].name; });
-  hc.name_rank.assign(T, 0);
+  hc.name_rank.assign(S, 0);
   for (int i = 0; i < T; i++) hc.name_rank[idx[i]] = (uint32_t)i;
   return KP_OK;
 }
@@ -587,7 +589,7 @@ void HostFilterTypes(const Dict& d, const HostCat& hc, const KReqs& q, int TW, c
   for (int t = 0; t < hc.T; t++) {
     bool ok = (hc.nonneg[t / 64] >> (t % 64)) & 1;
     for (int r = 0; r < KP_NRES && ok; r++)
-      if (total[r] > 0 && total[r] > hc.alloc[(size_t)r * hc.T + t]) ok = false;
+      if (total[r] > 0 && total[r] > hc.alloc[(size_t)r * hc.S + t]) ok = false;
     if (!ok) X[t / 64] &= ~(1ull << (t % 64));
   }
 }
