@@ -464,7 +464,7 @@ int32_t CompileCatalog(const Dict& d, const vector<HostType>& types, int TW, map
     for (int k = 0; k < K; k++) {
       const uint64_t kb = 1ull << k;
       if (!(q.present & kb)) {
-        hc.NOKEY[(size_t)k * SW + tw] |= tb;
+        hc.NOKEY[(size_t)k * TW + tw] |= tb;
         continue;
       }
       if ((q.compl_ & kb) || (q.hgt & kb) || (q.hlt & kb))
@@ -484,7 +484,7 @@ int32_t CompileCatalog(const Dict& d, const vector<HostType>& types, int TW, map
         }
       }
       if (cnt == 0) {
-        hc.DNE[(size_t)k * SW + tw] |= tb;
+        hc.DNE[(size_t)k * TW + tw] |= tb;
         hc.code[(size_t)k * S + t] = 0xFFFE;
       } else if (cnt == 1) {
         hc.code[(size_t)k * S + t] = (uint16_t)last;
