@@ -214,6 +214,7 @@ typedef struct kp_existing_node {
 typedef struct kp_ctx kp_ctx;
 typedef struct kp_catalog kp_catalog;
 typedef struct kp_solve_result kp_solve_result;
+typedef struct kp_solve_plan kp_solve_plan;
 
 typedef struct kp_solve_in {
   const kp_catalog* const* catalogs;      /* device path: resident catalogue handles */
@@ -241,8 +242,11 @@ typedef struct kp_nodeclaim_info {
 } kp_nodeclaim_info;
 
 typedef struct kp_solve_stats {
-  double device_ms;         /* kernel time, HIP events on the solve stream */
-  double host_ms;           /* whole kp_solve wall time */
+  double device_ms;         /* solve + finalize kernel time, HIP events on the solve stream */
+  double host_ms;           /* kp_solve_run wall time (restore state, kernels, result copy-back) */
+  double prepare_ms;        /* kp_solve_prepare wall time (compile + upload) */
+  double solve_kernel_ms;   /* solve_kernel alone */
+  double finalize_kernel_ms;
   uint64_t attempts;        /* NodeClaim.Add / ExistingNode.CanAdd evaluations */
   uint64_t bytes_algorithmic; /* bytes the device algorithm reads+writes */
   uint64_t pops;            /* queue pops */
@@ -331,7 +335,13 @@ int32_t kp_filter_compatible_available(kp_ctx* ctx, const kp_catalog* cat, const
                                        kp_solve_stats* stats);
 
 /* ---- Solve -------------------------------------------------------------------------------- */
+/* kp_solve = kp_solve_prepare + kp_solve_run + kp_solve_plan_destroy. prepare compiles the batch (string
+ * dictionaries -> bitsets, catalogue SoA, NodeClaimTemplates, pod queue order) and uploads it; run
+ * executes Solve on the resident inputs and may be repeated (state is restored on device each run). */
 int32_t kp_solve(kp_ctx* ctx, const kp_solve_in* in, kp_solve_result** out);
+int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out);
+int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out);
+void kp_solve_plan_destroy(kp_solve_plan* plan);
 uint32_t kp_result_nodeclaim_count(const kp_solve_result* res);
 /* out[p] for every input pod: >= 0 new NodeClaim index; -1 pod error; <= -2 existing node -(2+i) */
 int32_t kp_result_pod_placements(const kp_solve_result* res, int32_t* out, uint32_t n_pods);

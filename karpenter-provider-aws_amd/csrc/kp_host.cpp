@@ -160,7 +160,7 @@ struct HostType {
 struct kp_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
   kp_options opts;
   std::mutex mu;
 };
@@ -695,7 +695,8 @@ int32_t kp_ctx_create(const kp_options* opts, kp_ctx** out) {
     return fail(KP_E_INVAL, "device %d out of range", opts ? opts->device : 0);
   }
   if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+      hipEventCreate(&c->ev2) != hipSuccess || hipEventCreate(&c->ev3) != hipSuccess) {
     delete c;
     return fail(KP_E_DEVICE, "stream/event creation failed");
   }
@@ -707,6 +708,8 @@ void kp_ctx_destroy(kp_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->ev2) (void)hipEventDestroy(c->ev2);
+  if (c->ev3) (void)hipEventDestroy(c->ev3);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -1152,53 +1155,84 @@ vector<DevCatalog> DevCats(uint8_t* base, const Compiled& cp, const vector<CatOf
 
 extern "C" {
 
-int32_t kp_solve(kp_ctx* ctx, const kp_solve_in* in, kp_solve_result** out) {
+}  // extern "C"
+
+struct kp_solve_plan {
+  kp_ctx* ctx = nullptr;
+  std::unique_ptr<Compiled> cp;
+  DevBuf buf;
+  SolveArgs a;
+  size_t o_mut = 0, n_mut = 0, o_pristine = 0;
+  size_t o_stats = 0, o_npods = 0, o_place = 0, o_events = 0, o_nct = 0, o_ncrq = 0, o_opts = 0, o_nrem = 0,
+         o_nopt = 0, o_ncr = 0;
+  int opt_stride = 0, P = 0, Pc = 1;
+  uint32_t max_types = 0;
+  bool any_min = false;
+  double prepare_ms = 0;
+};
+
+extern "C" {
+
+// Compile the batch (dictionary, bitsets, catalogue SoA, templates, shapes, queue order) and upload it:
+// after this the whole Solve input is resident in HBM.
+int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out) {
   auto t0 = std::chrono::steady_clock::now();
   if (!ctx || !in || !out) return fail(KP_E_INVAL, "null argument");
   std::lock_guard<std::mutex> lock(ctx->mu);
   HIPCHK(hipSetDevice(ctx->device));
-  auto cp = std::make_unique<Compiled>();
-  int32_t rc = CompileSolve(in, *cp);
+  auto plan = std::make_unique<kp_solve_plan>();
+  plan->ctx = ctx;
+  plan->cp = std::make_unique<Compiled>();
+  Compiled& C = *plan->cp;
+  int32_t rc = CompileSolve(in, C);
   if (rc) return rc;
-  const Dict& d = cp->d;
-  const int TW = cp->TW, P = (int)in->n_pods, NT = (int)cp->tmpl_reqs.size(), E = (int)cp->ex_reqs.size();
-  const int SLn = (int)cp->shape_reqs.size();
+  const Dict& d = C.d;
+  const int TW = C.TW, P = (int)in->n_pods, NT = (int)C.tmpl_reqs.size(), E = (int)C.ex_reqs.size();
   const int Pc = std::max(P, 1);
+  plan->P = P;
+  plan->Pc = Pc;
+  plan->max_types = in->max_instance_types;
+  for (auto& q : C.tmpl_reqs) plan->any_min |= q.hmin != 0;
+  for (auto& q : C.shape_reqs) plan->any_min |= q.hmin != 0;
 
   Blob blob;
-  const size_t o_dict = blob.put(&cp->d.dd, 1);
-  const size_t o_vint = blob.put(cp->d.vint);
+  const size_t o_dict = blob.put(&C.d.dd, 1);
+  const size_t o_vint = blob.put(C.d.vint);
   vector<CatOffsets> coffs;
-  PutCatalogs(blob, *cp, coffs);
+  PutCatalogs(blob, C, coffs);
   const size_t o_cats = blob.reserve(sizeof(DevCatalog) * coffs.size());
-  const size_t o_pod_shape = blob.put(cp->pod_shape);
+  const size_t o_pod_shape = blob.put(C.pod_shape);
+  const size_t o_slb = blob.put(C.shape_level_base);
+  const size_t o_snl = blob.put(C.shape_nlevels);
+  const size_t o_sreqs = blob.put(C.shape_reqs);
+  const size_t o_sneg = blob.put(C.shape_negop);
+  const size_t o_sreq = blob.put(C.shape_requests);
+  const size_t o_stol = blob.put(C.shape_tolerates);
+  const size_t o_pvp = blob.put(C.pvp);
+  const size_t o_pvpb = blob.put(C.pvp_base);
+  const size_t o_pvps = blob.put(C.pvp_slot);
+  const size_t o_treqs = blob.put(C.tmpl_reqs);
+  const size_t o_tts = blob.put(C.tmpl_taintset);
+  const size_t o_tcat = blob.put(C.tmpl_catalog);
+  const size_t o_tX = blob.put(C.tmpl_X);
+  const size_t o_tdm = blob.put(C.tmpl_daemon);
+  const size_t o_tlp = blob.put(C.tmpl_limit_present);
+  const size_t o_exts = blob.put(C.ex_taintset);
+  const size_t o_exav = blob.put(C.ex_available);
+  // ---- mutable state: restored from a pristine device copy before every run ----
   vector<int32_t> zeros_p(Pc, 0);
+  const size_t o_mut = blob.reserve(0);
   const size_t o_pod_level = blob.put(zeros_p);
-  const size_t o_queue = blob.put(cp->queue);
+  const size_t o_queue = blob.put(C.queue);
   const size_t o_lastlen = blob.put(zeros_p);
   const size_t o_lastlen_ep = blob.put(zeros_p);
-  const size_t o_slb = blob.put(cp->shape_level_base);
-  const size_t o_snl = blob.put(cp->shape_nlevels);
-  const size_t o_sreqs = blob.put(cp->shape_reqs);
-  const size_t o_sneg = blob.put(cp->shape_negop);
-  const size_t o_sreq = blob.put(cp->shape_requests);
-  const size_t o_stol = blob.put(cp->shape_tolerates);
-  const size_t o_pvp = blob.put(cp->pvp);
-  const size_t o_pvpb = blob.put(cp->pvp_base);
-  const size_t o_pvps = blob.put(cp->pvp_slot);
-  const size_t o_treqs = blob.put(cp->tmpl_reqs);
-  const size_t o_tts = blob.put(cp->tmpl_taintset);
-  const size_t o_tcat = blob.put(cp->tmpl_catalog);
-  const size_t o_tX = blob.put(cp->tmpl_X);
-  const size_t o_tdm = blob.put(cp->tmpl_daemon);
-  const size_t o_tlp = blob.put(cp->tmpl_limit_present);
-  const size_t o_trem = blob.put(cp->tmpl_remaining);
-  const size_t o_exr = blob.put(cp->ex_reqs);
-  const size_t o_exts = blob.put(cp->ex_taintset);
-  const size_t o_exav = blob.put(cp->ex_available);
-  const size_t o_exrq = blob.put(cp->ex_requests);
+  const size_t o_trem = blob.put(C.tmpl_remaining);
+  const size_t o_exr = blob.put(C.ex_reqs);
+  const size_t o_exrq = blob.put(C.ex_requests);
+  const size_t n_mut = blob.host.size() - o_mut;
   const size_t host_bytes = blob.host.size();
-  // device-only regions (not copied)
+  const size_t o_pristine = blob.reserve(n_mut);
+  // ---- device-only regions ----
   const size_t o_ncr = blob.reserve(sizeof(KReqs) * Pc);
   const size_t o_ncX = blob.reserve(sizeof(uint64_t) * (size_t)Pc * TW);
   const size_t o_ncrq = blob.reserve(sizeof(int64_t) * (size_t)Pc * KP_NRES);
@@ -1214,18 +1248,17 @@ int32_t kp_solve(kp_ctx* ctx, const kp_solve_in* in, kp_solve_result** out) {
   const size_t o_nopt = blob.reserve(sizeof(uint32_t) * Pc);
   const size_t total_bytes = blob.host.size();
 
-  DevBuf buf;
-  HIPCHK(hipMalloc(&buf.p, total_bytes));
-  uint8_t* base = (uint8_t*)buf.p;
+  HIPCHK(hipMalloc(&plan->buf.p, total_bytes));
+  uint8_t* base = (uint8_t*)plan->buf.p;
   {
-    vector<DevCatalog> dc = DevCats(base, *cp, coffs);
+    vector<DevCatalog> dc = DevCats(base, C, coffs);
     memcpy(blob.host.data() + o_cats, dc.data(), sizeof(DevCatalog) * dc.size());
   }
   HIPCHK(hipMemcpyAsync(base, blob.host.data(), host_bytes, hipMemcpyHostToDevice, ctx->stream));
-  HIPCHK(hipMemsetAsync(base + o_stats, 0, sizeof(uint64_t) * 8, ctx->stream));
-  HIPCHK(hipMemsetAsync(base + o_npods, 0, sizeof(int32_t) * Pc, ctx->stream));
+  HIPCHK(hipMemcpyAsync(base + o_pristine, base + o_mut, n_mut, hipMemcpyDeviceToDevice, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
 
-  SolveArgs a;
+  SolveArgs& a = plan->a;
   memset(&a, 0, sizeof a);
   a.dict = (const DevDict*)(base + o_dict);
   a.cats = (const DevCatalog*)(base + o_cats);
@@ -1271,13 +1304,56 @@ int32_t kp_solve(kp_ctx* ctx, const kp_solve_in* in, kp_solve_result** out) {
   a.placement = (int32_t*)(base + o_place);
   a.events = (int32_t*)(base + o_events);
   a.stats = (uint64_t*)(base + o_stats);
-  (void)SLn;
-  const size_t dyn = a.sort_in_lds ? (size_t)2 * sort_cap * sizeof(int32_t) : 0;
-  HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
-  HIPCHK(launch_solve(a, 8, dyn, ctx->stream));
+
+  plan->o_mut = o_mut;
+  plan->n_mut = n_mut;
+  plan->o_pristine = o_pristine;
+  plan->o_stats = o_stats;
+  plan->o_npods = o_npods;
+  plan->o_place = o_place;
+  plan->o_events = o_events;
+  plan->o_nct = o_nct;
+  plan->o_ncrq = o_ncrq;
+  plan->o_opts = o_opts;
+  plan->o_nrem = o_nrem;
+  plan->o_nopt = o_nopt;
+  plan->o_ncr = o_ncr;
+  plan->opt_stride = opt_stride;
+  plan->prepare_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  *out = plan.release();
+  return KP_OK;
+}
+
+void kp_solve_plan_destroy(kp_solve_plan* p) {
+  if (!p) return;
+  (void)hipSetDevice(p->ctx->device);
+  delete p;
+}
+
+// One Solve over resident inputs: restore mutable state, solve_kernel, finalize_kernel, copy results.
+int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out) {
+  auto t0 = std::chrono::steady_clock::now();
+  if (!plan || !out) return fail(KP_E_INVAL, "null argument");
+  kp_ctx* ctx = plan->ctx;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device));
+  const Compiled& C = *plan->cp;
+  const Dict& d = C.d;
+  uint8_t* base = (uint8_t*)plan->buf.p;
+  const int P = plan->P, Pc = plan->Pc, opt_stride = plan->opt_stride;
+  hipStream_t st = ctx->stream;
+  HIPCHK(hipMemcpyAsync(base + plan->o_mut, base + plan->o_pristine, plan->n_mut, hipMemcpyDeviceToDevice, st));
+  HIPCHK(hipMemsetAsync(base + plan->o_stats, 0, sizeof(uint64_t) * 8, st));
+  HIPCHK(hipMemsetAsync(base + plan->o_npods, 0, sizeof(int32_t) * Pc, st));
+  HIPCHK(hipMemsetAsync(base + plan->o_place, 0xFF, sizeof(int32_t) * Pc, st));
+  const SolveArgs& a = plan->a;
+  const size_t dyn = a.sort_in_lds ? (size_t)2 * a.sort_cap * sizeof(int32_t) : 0;
+  HIPCHK(hipEventRecord(ctx->ev0, st));
+  HIPCHK(launch_solve(a, 8, dyn, st));
+  HIPCHK(hipEventRecord(ctx->ev1, st));
   uint64_t stats[8];
-  HIPCHK(hipMemcpyAsync(stats, base + o_stats, sizeof stats, hipMemcpyDeviceToHost, ctx->stream));
-  HIPCHK(hipStreamSynchronize(ctx->stream));
+  HIPCHK(hipMemcpyAsync(stats, base + plan->o_stats, sizeof stats, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
   const int n_nc = (int)stats[3];
   FinalizeArgs f;
   f.dict = a.dict;
@@ -1288,32 +1364,40 @@ int32_t kp_solve(kp_ctx* ctx, const kp_solve_in* in, kp_solve_result** out) {
   f.tmpl_catalog = a.tmpl_catalog;
   f.nc_reqs = a.nc_reqs;
   f.nc_X = a.nc_X;
-  f.max_types = (int32_t)in->max_instance_types;
+  f.max_types = (int32_t)plan->max_types;
   f.opt_stride = opt_stride;
-  f.out_options = (uint32_t*)(base + o_opts);
-  f.out_n_remaining = (uint32_t*)(base + o_nrem);
-  f.out_n_options = (uint32_t*)(base + o_nopt);
-  HIPCHK(launch_finalize(f, ctx->stream));
-  HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));
+  f.out_options = (uint32_t*)(base + plan->o_opts);
+  f.out_n_remaining = (uint32_t*)(base + plan->o_nrem);
+  f.out_n_options = (uint32_t*)(base + plan->o_nopt);
+  HIPCHK(hipEventRecord(ctx->ev2, st));
+  HIPCHK(launch_finalize(f, st));
+  HIPCHK(hipEventRecord(ctx->ev3, st));
 
-  auto* res = new kp_solve_result();
-  std::unique_ptr<kp_solve_result> guard(res);
+  auto res = std::make_unique<kp_solve_result>();
   res->placement.assign(P, -1);
-  vector<int32_t> place(Pc), events(Pc), nct(std::max(n_nc, 1));
-  vector<int64_t> ncrq((size_t)std::max(n_nc, 1) * KP_NRES);
-  vector<uint32_t> opts((size_t)std::max(n_nc, 1) * opt_stride), nrem(std::max(n_nc, 1)), nopt(std::max(n_nc, 1));
-  HIPCHK(hipMemcpyAsync(place.data(), base + o_place, sizeof(int32_t) * Pc, hipMemcpyDeviceToHost, ctx->stream));
-  HIPCHK(hipMemcpyAsync(events.data(), base + o_events, sizeof(int32_t) * Pc, hipMemcpyDeviceToHost, ctx->stream));
+  const int nn = std::max(n_nc, 1);
+  vector<int32_t> place(Pc), events(Pc), nct(nn);
+  vector<int64_t> ncrq((size_t)nn * KP_NRES);
+  vector<uint32_t> opts((size_t)nn * opt_stride), nrem(nn), nopt(nn);
+  HIPCHK(hipMemcpyAsync(place.data(), base + plan->o_place, sizeof(int32_t) * Pc, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(events.data(), base + plan->o_events, sizeof(int32_t) * Pc, hipMemcpyDeviceToHost, st));
   if (n_nc) {
-    HIPCHK(hipMemcpyAsync(nct.data(), base + o_nct, sizeof(int32_t) * n_nc, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipMemcpyAsync(ncrq.data(), base + o_ncrq, sizeof(int64_t) * n_nc * KP_NRES, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipMemcpyAsync(opts.data(), base + o_opts, sizeof(uint32_t) * (size_t)n_nc * opt_stride, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipMemcpyAsync(nrem.data(), base + o_nrem, sizeof(uint32_t) * n_nc, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipMemcpyAsync(nopt.data(), base + o_nopt, sizeof(uint32_t) * n_nc, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(nct.data(), base + plan->o_nct, sizeof(int32_t) * n_nc, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(ncrq.data(), base + plan->o_ncrq, sizeof(int64_t) * n_nc * KP_NRES, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(opts.data(), base + plan->o_opts, sizeof(uint32_t) * (size_t)n_nc * opt_stride,
+                          hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(nrem.data(), base + plan->o_nrem, sizeof(uint32_t) * n_nc, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(nopt.data(), base + plan->o_nopt, sizeof(uint32_t) * n_nc, hipMemcpyDeviceToHost, st));
   }
-  HIPCHK(hipStreamSynchronize(ctx->stream));
-  float ms = 0;
-  HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+  vector<KReqs> fin;
+  if (plan->any_min && n_nc) {
+    fin.resize(n_nc);
+    HIPCHK(hipMemcpyAsync(fin.data(), base + plan->o_ncr, sizeof(KReqs) * n_nc, hipMemcpyDeviceToHost, st));
+  }
+  HIPCHK(hipStreamSynchronize(st));
+  float ms_solve = 0, ms_fin = 0;
+  HIPCHK(hipEventElapsedTime(&ms_solve, ctx->ev0, ctx->ev1));
+  HIPCHK(hipEventElapsedTime(&ms_fin, ctx->ev2, ctx->ev3));
 
   res->ncs.resize(n_nc);
   const int n_ev = (int)stats[4];
@@ -1324,13 +1408,12 @@ int32_t kp_solve(kp_ctx* ctx, const kp_solve_in* in, kp_solve_result** out) {
       res->ncs[t].pods.push_back((uint32_t)p);
       res->placement[p] = t;
     } else if (t <= -2) {
-      res->placement[p] = -2 - cp->ex_input[-2 - t];
+      res->placement[p] = -2 - C.ex_input[-2 - t];
     }
   }
   for (int i = 0; i < n_nc; i++) {
     auto& nc = res->ncs[i];
-    const int tm = nct[i];
-    nc.nodepool = (uint32_t)cp->tmpl_nodepool[tm];
+    nc.nodepool = (uint32_t)C.tmpl_nodepool[nct[i]];
     nc.n_remaining = nrem[i];
     memset(&nc.requests, 0, sizeof nc.requests);
     for (int r = 0; r < KP_NRES; r++) {
@@ -1338,37 +1421,36 @@ int32_t kp_solve(kp_ctx* ctx, const kp_solve_in* in, kp_solve_result** out) {
       if (nc.requests.milli[r]) nc.requests.present |= 1u << r;
     }
     nc.options.assign(opts.begin() + (size_t)i * opt_stride, opts.begin() + (size_t)i * opt_stride + nopt[i]);
-    // Truncate: minValues must still hold on the truncated options, else the NodeClaim's pods fail
-    const KReqs* R = nullptr;
-    (void)R;
-  }
-  // minValues re-check needs the final requirements: copy them for NodeClaims whose template had minValues
-  {
-    bool any = false;
-    for (auto& q : cp->tmpl_reqs) any |= q.hmin != 0;
-    for (auto& lv : cp->shape_reqs) any |= lv.hmin != 0;
-    if (any && n_nc) {
-      vector<KReqs> fin(n_nc);
-      HIPCHK(hipMemcpy(fin.data(), base + o_ncr, sizeof(KReqs) * n_nc, hipMemcpyDeviceToHost));
-      for (int i = 0; i < n_nc; i++) {
-        if (!(fin[i].hmin & fin[i].present)) continue;
-        const HostCat& hc = cp->cats[cp->tmpl_catalog[nct[i]]];
-        vector<int> ts(res->ncs[i].options.begin(), res->ncs[i].options.end());
-        if (!HostMinValuesOK(d, hc, fin[i], ts)) {
-          for (uint32_t p : res->ncs[i].pods) res->placement[p] = -1;
-          res->ncs[i].options.clear();
-        }
+    // Truncate(reqs, max): minValues must still hold on the truncated options, else the pods fail
+    if (!fin.empty() && (fin[i].hmin & fin[i].present)) {
+      const HostCat& hc = C.cats[C.tmpl_catalog[nct[i]]];
+      vector<int> ts(nc.options.begin(), nc.options.end());
+      if (!HostMinValuesOK(d, hc, fin[i], ts)) {
+        for (uint32_t p : nc.pods) res->placement[p] = -1;
+        nc.options.clear();
       }
     }
   }
   memset(&res->stats, 0, sizeof res->stats);
-  res->stats.device_ms = ms;
+  res->stats.device_ms = ms_solve + ms_fin;
+  res->stats.solve_kernel_ms = ms_solve;
+  res->stats.finalize_kernel_ms = ms_fin;
   res->stats.attempts = stats[0];
   res->stats.bytes_algorithmic = stats[1];
   res->stats.pops = stats[2];
+  res->stats.prepare_ms = plan->prepare_ms;
   res->stats.host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  *out = guard.release();
+  *out = res.release();
   return KP_OK;
+}
+
+int32_t kp_solve(kp_ctx* ctx, const kp_solve_in* in, kp_solve_result** out) {
+  kp_solve_plan* plan = nullptr;
+  int32_t rc = kp_solve_prepare(ctx, in, &plan);
+  if (rc) return rc;
+  rc = kp_solve_run(plan, out);
+  kp_solve_plan_destroy(plan);
+  return rc;
 }
 
 uint32_t kp_result_nodeclaim_count(const kp_solve_result* r) { return r ? (uint32_t)r->ncs.size() : 0; }

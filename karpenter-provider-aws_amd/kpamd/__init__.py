@@ -47,6 +47,9 @@ def load_lib(path=LIB_PATH):
         "kp_filter_compatible_available": (C.c_int32, [C.c_void_p, C.c_void_p, P(abi.FeasibilityQuery), C.c_uint32,
                                                        P(C.c_uint64), P(C.c_double), P(abi.SolveStats)]),
         "kp_solve": (C.c_int32, [C.c_void_p, P(abi.SolveIn), P(C.c_void_p)]),
+        "kp_solve_prepare": (C.c_int32, [C.c_void_p, P(abi.SolveIn), P(C.c_void_p)]),
+        "kp_solve_run": (C.c_int32, [C.c_void_p, P(C.c_void_p)]),
+        "kp_solve_plan_destroy": (None, [C.c_void_p]),
         "kp_result_nodeclaim_count": (C.c_uint32, [C.c_void_p]),
         "kp_result_pod_placements": (C.c_int32, [C.c_void_p, P(C.c_int32), C.c_uint32]),
         "kp_result_nodeclaim": (C.c_int32, [C.c_void_p, C.c_uint32, P(abi.NodeClaimInfo)]),
@@ -159,6 +162,45 @@ class Scheduler:
             return read_result(lib, res, self.problem.n_pods)
         finally:
             lib.kp_result_destroy(res)
+
+    def prepare(self):
+        """kp_solve_prepare: compile + upload once; returns a SolvePlan whose run() repeats Solve."""
+        return SolvePlan(self)
+
+
+class SolvePlan:
+    def __init__(self, sched):
+        self.sched = sched
+        lib = sched.ctx.lib
+        arena = Arena()
+        si = abi.build_solve_in(arena, sched.problem, catalog_handles=[c.h.value for c in sched.catalogs])
+        h = C.c_void_p()
+        _check(lib, lib.kp_solve_prepare(sched.ctx.h, C.byref(si), C.byref(h)))
+        self.h = h
+
+    def run(self, read=True):
+        lib = self.sched.ctx.lib
+        res = C.c_void_p()
+        _check(lib, lib.kp_solve_run(self.h, C.byref(res)))
+        try:
+            if read:
+                return read_result(lib, res, self.sched.problem.n_pods)
+            st = abi.SolveStats()
+            lib.kp_result_stats(res, C.byref(st))
+            return {"stats": {f: getattr(st, f) for f, _ in abi.SolveStats._fields_}}
+        finally:
+            lib.kp_result_destroy(res)
+
+    def close(self):
+        if self.h:
+            self.sched.ctx.lib.kp_solve_plan_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def compatible_available_filter(ctx, catalog, queries):
