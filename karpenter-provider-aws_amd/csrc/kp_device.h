@@ -49,8 +49,17 @@ struct SolveArgs {
   int32_t* nc_tmpl;                  // [P]
   int32_t* g_npods;                  // [P] len(Pods)
   int32_t* g_order;                  // [P] newNodeClaims order
-  int32_t sort_in_lds;
+  int32_t sort_in_lds;               // unused (LDS until SORT_CAP NodeClaims, then global)
   int32_t sort_cap;
+  // exact failure memo: outcome of Add/CanAdd depends only on (candidate state, pod shape-level), so a
+  // recorded failure stays valid while the candidate's version is unchanged
+  int32_t ncc;                       // NodeClaim ids < ncc are memoised
+  int32_t* nc_ver;                   // [P]
+  int32_t* nc_fail;                  // [SL][ncc]
+  int32_t* ex_ver;                   // [E]
+  int32_t* ex_fail;                  // [SL][E]
+  int32_t* tmpl_ver;                 // [NT]
+  int32_t* tmpl_fail;                // [SL][NT]
   // outputs
   int32_t* placement;                // [P]
   int32_t* events;                   // [P] pods in placement order

@@ -1162,7 +1162,7 @@ struct kp_solve_plan {
   std::unique_ptr<Compiled> cp;
   DevBuf buf;
   SolveArgs a;
-  size_t o_mut = 0, n_mut = 0, o_pristine = 0;
+  size_t o_mut = 0, n_mut = 0, o_pristine = 0, o_ver = 0, n_ver = 0, o_fail = 0, n_fail = 0;
   size_t o_stats = 0, o_npods = 0, o_place = 0, o_events = 0, o_nct = 0, o_ncrq = 0, o_opts = 0, o_nrem = 0,
          o_nopt = 0, o_ncr = 0;
   int opt_stride = 0, P = 0, Pc = 1;
@@ -1242,6 +1242,19 @@ int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out
   const size_t o_place = blob.reserve(sizeof(int32_t) * Pc);
   const size_t o_events = blob.reserve(sizeof(int32_t) * Pc);
   const size_t o_stats = blob.reserve(sizeof(uint64_t) * 8);
+  // failure memo (see SolveArgs): versions start at 0, memo entries at -1
+  const size_t SLn = std::max<size_t>(1, C.shape_reqs.size());
+  const int ncc = (int)std::min<size_t>((size_t)Pc, std::max<size_t>(1, ((size_t)256 << 20) / (4 * SLn)));
+  const size_t o_ver0 = blob.reserve(0);
+  const size_t o_ncver = blob.reserve(sizeof(int32_t) * Pc);
+  const size_t o_exver = blob.reserve(sizeof(int32_t) * std::max(E, 1));
+  const size_t o_tver = blob.reserve(sizeof(int32_t) * std::max(NT, 1));
+  const size_t n_ver = blob.host.size() - o_ver0;
+  const size_t o_fail0 = blob.reserve(0);
+  const size_t o_ncfail = blob.reserve(sizeof(int32_t) * SLn * ncc);
+  const size_t o_exfail = blob.reserve(sizeof(int32_t) * SLn * std::max(E, 1));
+  const size_t o_tfail = blob.reserve(sizeof(int32_t) * SLn * std::max(NT, 1));
+  const size_t n_fail = blob.host.size() - o_fail0;
   const int opt_stride = in->max_instance_types ? (int)in->max_instance_types : std::max(1, d.dd.T);
   const size_t o_opts = blob.reserve(sizeof(uint32_t) * (size_t)Pc * opt_stride);
   const size_t o_nrem = blob.reserve(sizeof(uint32_t) * Pc);
@@ -1298,13 +1311,24 @@ int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out
   a.nc_tmpl = (int32_t*)(base + o_nct);
   a.g_npods = (int32_t*)(base + o_npods);
   a.g_order = (int32_t*)(base + o_order);
-  const int sort_cap = 8192;
-  a.sort_in_lds = P <= sort_cap ? 1 : 0;
-  a.sort_cap = sort_cap;
+  a.sort_in_lds = 1;
+  a.sort_cap = 8192;  // newNodeClaims order lives in LDS (64 KiB) up to this many NodeClaims, then spills
+  if (const char* e = getenv("KP_SORT_CAP")) a.sort_cap = std::max(1, std::min(8192, atoi(e)));  // test hook
+  a.ncc = ncc;
+  a.nc_ver = (int32_t*)(base + o_ncver);
+  a.nc_fail = (int32_t*)(base + o_ncfail);
+  a.ex_ver = (int32_t*)(base + o_exver);
+  a.ex_fail = (int32_t*)(base + o_exfail);
+  a.tmpl_ver = (int32_t*)(base + o_tver);
+  a.tmpl_fail = (int32_t*)(base + o_tfail);
   a.placement = (int32_t*)(base + o_place);
   a.events = (int32_t*)(base + o_events);
   a.stats = (uint64_t*)(base + o_stats);
 
+  plan->o_ver = o_ver0;
+  plan->n_ver = n_ver;
+  plan->o_fail = o_fail0;
+  plan->n_fail = n_fail;
   plan->o_mut = o_mut;
   plan->n_mut = n_mut;
   plan->o_pristine = o_pristine;
@@ -1346,8 +1370,10 @@ int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out) {
   HIPCHK(hipMemsetAsync(base + plan->o_stats, 0, sizeof(uint64_t) * 8, st));
   HIPCHK(hipMemsetAsync(base + plan->o_npods, 0, sizeof(int32_t) * Pc, st));
   HIPCHK(hipMemsetAsync(base + plan->o_place, 0xFF, sizeof(int32_t) * Pc, st));
+  HIPCHK(hipMemsetAsync(base + plan->o_ver, 0, plan->n_ver, st));
+  HIPCHK(hipMemsetAsync(base + plan->o_fail, 0xFF, plan->n_fail, st));
   const SolveArgs& a = plan->a;
-  const size_t dyn = a.sort_in_lds ? (size_t)2 * a.sort_cap * sizeof(int32_t) : 0;
+  const size_t dyn = (size_t)2 * a.sort_cap * sizeof(int32_t);
   HIPCHK(hipEventRecord(ctx->ev0, st));
   HIPCHK(launch_solve(a, 8, dyn, st));
   HIPCHK(hipEventRecord(ctx->ev1, st));

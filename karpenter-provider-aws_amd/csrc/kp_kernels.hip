@@ -368,7 +368,24 @@ __device__ void store_merged(KReqs* dst, const ReqView& rv, uint64_t m_v, int W,
   }
 }
 
-// pick the lowest wave that succeeded (first-fit inside one round of NW candidates)
+// Ordered compaction of per-thread candidate flags into s_list (positions in scan order). Returns count.
+template <int NW>
+__device__ __forceinline__ int compact_candidates(bool cand, int pos, int32_t* s_list, int32_t* s_wcnt) {
+  const int wave = threadIdx.x >> 6, lane = LANE;
+  const uint64_t bal = __ballot(cand);
+  if (lane == 0) s_wcnt[wave] = __builtin_popcountll(bal);
+  __syncthreads();
+  int before = 0, total = 0;
+  for (int w = 0; w < NW; w++) {
+    const int c = s_wcnt[w];
+    before += w < wave ? c : 0;
+    total += c;
+  }
+  if (cand) s_list[before + __builtin_popcountll(bal & ((1ull << lane) - 1))] = pos;
+  __syncthreads();
+  return total;
+}
+
 template <int NW>
 __device__ __forceinline__ int first_ok(const int32_t* s_ok) {
   for (int w = 0; w < NW; w++)
@@ -376,34 +393,39 @@ __device__ __forceinline__ int first_ok(const int32_t* s_ok) {
   return -1;
 }
 
+
 template <int NW>
 __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
+  constexpr int NT = NW * 64;
   __shared__ DevDict D;
   __shared__ WaveSlots slots[NW];
   __shared__ int32_t s_ok[NW];
+  __shared__ int32_t s_wcnt[NW];
   __shared__ int32_t s_ctl[8];
+  __shared__ int32_t s_list[NT];
   __shared__ uint32_t s_scratch[NW][2 * KP_MAX_WORDS];
-  extern __shared__ int32_t s_dyn[];  // sort arrays when they fit: ord[cap], npods[cap]
+  __shared__ KReqs s_B;  // the popped pod's requirements, staged once per pod
+  extern __shared__ int32_t s_dyn[];  // ord[a.sort_cap], npods[a.sort_cap] while n_nc <= a.sort_cap
 
-  const int wave = threadIdx.x >> 6;
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
   const int lane = LANE;
-  if (threadIdx.x == 0) D = *a.dict;
-  int32_t* ord = a.sort_in_lds ? s_dyn : a.g_order;
-  int32_t* npods = a.sort_in_lds ? s_dyn + a.sort_cap : a.g_npods;
+  if (tid == 0) D = *a.dict;
   uint64_t bytes = 0, attempts = 0, pops = 0;
-  // control block (thread 0 owns): 0 head, 1 len, 2 n_nc, 3 lastLen epoch, 4 n_events, 6 popped pod
-  if (threadIdx.x == 0) {
+  // control block (thread 0 owns): 0 head, 1 len, 2 n_nc, 3 lastLen epoch, 4 n_events, 5 sort arrays in LDS, 6 pod
+  if (tid == 0) {
     s_ctl[0] = 0;
     s_ctl[1] = a.n_pods;
     s_ctl[2] = 0;
     s_ctl[3] = 1;
     s_ctl[4] = 0;
+    s_ctl[5] = 1;
   }
   __syncthreads();
 
   for (;;) {
     // ---- Queue.Pop: stop when the head pod was last pushed at the current queue length ----------
-    if (threadIdx.x == 0) {
+    if (tid == 0) {
       const int len = s_ctl[1];
       int pod = -1;
       if (len > 0) {
@@ -424,64 +446,92 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
     const int shape = a.pod_shape[pod];
     const int lvl = a.pod_level[pod];
     const int sl = a.shape_level_base[shape] + lvl;
-    const KReqs* B = kreq_at(a.shape_reqs, sl);
+    {
+      const uint64_t* src = reinterpret_cast<const uint64_t*>(kreq_at(a.shape_reqs, sl));
+      uint64_t* dst = reinterpret_cast<uint64_t*>(&s_B);
+      for (int i = tid; i < (int)(sizeof(KReqs) / 8); i += NT) dst[i] = src[i];
+    }
+    __syncthreads();
+    const KReqs* B = &s_B;
     const uint64_t b_negop = a.shape_negop[sl];
-    const uint64_t b_keys = B->present;
+    const uint64_t b_keys = s_B.present;
     const int64_t* preq = a.shape_requests + (size_t)shape * KP_NRES;
     const uint64_t tolmask = a.shape_tolerates[shape];
     const int32_t* pslot = a.pvp_slot + (size_t)sl * KP_MAX_KEYS;
     int placed = -1;  // >= 0 NodeClaim id; <= -2 existing node; -1 not placed
 
     // ---- addToExistingNode: lowest index whose CanAdd succeeds -------------------------------
-    for (int base = 0; base < a.n_existing; base += NW) {
-      const int e = base + wave;
-      bool ok = false;
-      uint64_t m_v = 0;
-      ReqView rv;
-      if (e < a.n_existing && ((tolmask >> a.ex_taintset[e]) & 1)) {
-        attempts++;
+    for (int base = 0; base < a.n_existing && placed == -1; base += NT) {
+      const int e = base + tid;
+      bool cand = false;
+      if (e < a.n_existing && ((tolmask >> a.ex_taintset[e]) & 1) && a.ex_fail[(size_t)sl * a.n_existing + e] != a.ex_ver[e]) {
         const int64_t* av = a.ex_available + (size_t)e * KP_NRES;
         const int64_t* rq = a.ex_requests + (size_t)e * KP_NRES;
-        bool fits = true;  // Fits(Merge(requests, pod), available)
+        bool fits = true;  // Fits(Merge(requests, pod), available): CanAdd's resource check, exact
         for (int r = 0; r < KP_NRES; r++) fits = fits && av[r] >= 0 && rq[r] + preq[r] <= av[r];
-        bytes += 2 * KP_NRES * 8;
-        if (fits) {
-          ok = merge_compatible(D, kreq_at(a.ex_reqs, e), B, b_negop, false, m_v, rv, &slots[wave], a.vint);
+        cand = fits;
+      }
+      const int n = compact_candidates<NW>(cand, e, s_list, s_wcnt);
+      bytes += (uint64_t)min(NT, a.n_existing - base) * (2 * KP_NRES * 8 + 8);
+      for (int r0 = 0; r0 < n; r0 += NW) {
+        const int li = r0 + wave;
+        bool ok = false;
+        uint64_t m_v = 0;
+        ReqView rv;
+        int ei = -1;
+        if (li < n) {
+          ei = s_list[li];
+          attempts++;
+          ok = merge_compatible(D, kreq_at(a.ex_reqs, ei), B, b_negop, false, m_v, rv, &slots[wave], a.vint);
           bytes += sizeof(KReqs);
+          if (!ok && lane == 0) a.ex_fail[(size_t)sl * a.n_existing + ei] = a.ex_ver[ei];
         }
-      }
-      if (lane == 0) s_ok[wave] = ok ? 1 : 0;
-      __syncthreads();
-      const int win = first_ok<NW>(s_ok);
-      if (win >= 0) {
-        if (wave == win) {
-          store_merged(reinterpret_cast<KReqs*>(a.ex_reqs + (size_t)e * sizeof(KReqs)), rv, m_v, D.W, D.KB);
-          if (lane < KP_NRES) a.ex_requests[(size_t)e * KP_NRES + lane] += preq[lane];
+        if (lane == 0) s_ok[wave] = ok ? 1 : 0;
+        __syncthreads();
+        const int win = first_ok<NW>(s_ok);
+        if (win >= 0) {
+          if (wave == win) {
+            store_merged(reinterpret_cast<KReqs*>(a.ex_reqs + (size_t)ei * sizeof(KReqs)), rv, m_v, D.W, D.KB);
+            if (lane < KP_NRES) a.ex_requests[(size_t)ei * KP_NRES + lane] += preq[lane];
+            if (lane == 0) a.ex_ver[ei] += 1;
+          }
+          placed = -2 - s_list[r0 + win];
         }
-        placed = -2 - (base + win);
+        __syncthreads();
+        if (win >= 0) break;
       }
-      __syncthreads();
-      if (win >= 0) break;
     }
 
     if (placed == -1) {
+      const bool in_lds = s_ctl[5] != 0;
+      int32_t* ord = in_lds ? s_dyn : a.g_order;
+      int32_t* npods = in_lds ? s_dyn + a.sort_cap : a.g_npods;
       // ---- sort.Slice(newNodeClaims, len(Pods) asc) -----------------------------------------------
-      if (threadIdx.x == 0) go_sort_slice(NCSort{ord, npods}, s_ctl[2]);
+      if (tid == 0) go_sort_slice(NCSort{ord, npods}, s_ctl[2]);
       __syncthreads();
       const int n_nc = s_ctl[2];
       // ---- addToInflightNode: first NodeClaim in that order whose Add succeeds ------------------
-      for (int base = 0; base < n_nc; base += NW) {
-        const int i = base + wave;
-        bool ok = false;
-        uint64_t m_v = 0, X = 0;
-        ReqView rv;
-        int nc = -1;
+      for (int base = 0; base < n_nc && placed == -1; base += NT) {
+        const int i = base + tid;
+        bool cand = false;
         if (i < n_nc) {
-          nc = ord[i];
-          const int tm = a.nc_tmpl[nc];
-          if ((tolmask >> a.tmpl_taintset[tm]) & 1) {
-            attempts++;
+          const int nc = ord[i];
+          cand = ((tolmask >> a.tmpl_taintset[a.nc_tmpl[nc]]) & 1) &&
+                 !(nc < a.ncc && a.nc_fail[(size_t)sl * a.ncc + nc] == a.nc_ver[nc]);
+        }
+        const int n = compact_candidates<NW>(cand, i, s_list, s_wcnt);
+        bytes += (uint64_t)min(NT, n_nc - base) * 12;
+        for (int r0 = 0; r0 < n; r0 += NW) {
+          const int li = r0 + wave;
+          bool ok = false;
+          uint64_t m_v = 0, X = 0;
+          ReqView rv;
+          int nc = -1;
+          if (li < n) {
+            nc = ord[s_list[li]];
+            const int tm = a.nc_tmpl[nc];
             const int cat = a.tmpl_catalog[tm];
+            attempts++;
             ok = merge_compatible(D, kreq_at(a.nc_reqs, nc), B, b_negop, true, m_v, rv, &slots[wave], a.vint);
             bytes += sizeof(KReqs);
             if (ok) {
@@ -493,110 +543,137 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
               ok = __ballot(X != 0) != 0;
               bytes += (uint64_t)D.TW * 8 + KP_NRES * 8;
             }
+            if (!ok && lane == 0 && nc < a.ncc) a.nc_fail[(size_t)sl * a.ncc + nc] = a.nc_ver[nc];
           }
-        }
-        if (lane == 0) s_ok[wave] = ok ? 1 : 0;
-        __syncthreads();
-        const int win = first_ok<NW>(s_ok);
-        if (win >= 0) {
-          if (wave == win) {
-            store_merged(reinterpret_cast<KReqs*>(a.nc_reqs + (size_t)nc * sizeof(KReqs)), rv, m_v, D.W, D.KB);
-            if (lane < D.TW) a.nc_X[(size_t)nc * D.TW + lane] = X;
-            if (lane < KP_NRES) a.nc_requests[(size_t)nc * KP_NRES + lane] += preq[lane];
-            if (lane == 0) npods[nc] += 1;
+          if (lane == 0) s_ok[wave] = ok ? 1 : 0;
+          __syncthreads();
+          const int win = first_ok<NW>(s_ok);
+          if (win >= 0) {
+            if (wave == win) {
+              store_merged(reinterpret_cast<KReqs*>(a.nc_reqs + (size_t)nc * sizeof(KReqs)), rv, m_v, D.W, D.KB);
+              if (lane < D.TW) a.nc_X[(size_t)nc * D.TW + lane] = X;
+              if (lane < KP_NRES) a.nc_requests[(size_t)nc * KP_NRES + lane] += preq[lane];
+              if (lane == 0) {
+                npods[nc] += 1;
+                a.nc_ver[nc] += 1;
+              }
+            }
+            placed = ord[s_list[r0 + win]];
           }
-          placed = ord[base + win];
+          __syncthreads();
+          if (win >= 0) break;
         }
-        __syncthreads();
-        if (win >= 0) break;
       }
     }
 
     if (placed == -1) {
       // ---- addToNewNodeClaim: templates in weight order --------------------------------------------
-      for (int base = 0; base < a.n_tmpl; base += NW) {
-        const int tm = base + wave;
-        bool ok = false;
-        uint64_t m_v = 0, X = 0;
-        ReqView rv;
-        if (tm < a.n_tmpl && ((tolmask >> a.tmpl_taintset[tm]) & 1)) {
-          const int cat = a.tmpl_catalog[tm];
-          const DevCatalog& Cg = a.cats[cat];
-          X = lane < D.TW ? a.tmpl_X[(size_t)tm * D.TW + lane] : 0;
-          const uint32_t lim = a.tmpl_limit_present[tm];
-          if (lim) {  // filterByRemainingResources: capacity <= remaining for every limited resource
-            const int64_t* rem = a.tmpl_remaining + (size_t)tm * KP_NRES;
-            uint64_t m = lane < D.TW ? X : 0, keep = 0;
-            while (m) {
-              const int b = __builtin_ctzll(m);
-              m &= m - 1;
-              const int t = lane * 64 + b;
-              bool viable = true;
-              for (int r = 0; r < KP_NRES; r++)
-                if (((lim >> r) & 1) && Cg.cap[(size_t)r * D.T + t] > rem[r]) viable = false;
-              if (viable) keep |= 1ull << b;
-            }
-            X = keep;
-            bytes += (uint64_t)D.T * 8;
-          }
-          if (__ballot(X != 0)) {
-            attempts++;
-            ok = merge_compatible(D, kreq_at(a.tmpl_reqs, tm), B, b_negop, true, m_v, rv, &slots[wave], a.vint);
-            if (ok) {
-              int64_t total[KP_NRES];
-              for (int r = 0; r < KP_NRES; r++) total[r] = a.tmpl_daemon[(size_t)tm * KP_NRES + r] + preq[r];
-              const uint64_t* pvp = a.shape_pvp + (size_t)a.pvp_base[sl * a.n_catalogs + cat] * D.TW;
-              X = filter_types(D, Cg, rv, m_v, X, b_keys, pvp, pslot, total, a.vint, s_scratch[wave], &bytes);
-              ok = __ballot(X != 0) != 0;
-            }
-          }
-        }
-        if (lane == 0) s_ok[wave] = ok ? 1 : 0;
-        __syncthreads();
-        const int win = first_ok<NW>(s_ok);
-        const int nc = s_ctl[2];
-        if (win >= 0) {
-          if (wave == win) {
-            store_merged(reinterpret_cast<KReqs*>(a.nc_reqs + (size_t)nc * sizeof(KReqs)), rv, m_v, D.W, D.KB);
-            if (lane < D.TW) a.nc_X[(size_t)nc * D.TW + lane] = X;
-            if (lane < KP_NRES)
-              a.nc_requests[(size_t)nc * KP_NRES + lane] = a.tmpl_daemon[(size_t)tm * KP_NRES + lane] + preq[lane];
-            if (lane == 0) {
-              a.nc_tmpl[nc] = tm;
-              npods[nc] = 1;
-              ord[nc] = nc;  // append to newNodeClaims
-            }
-            // subtractMax: remaining -= max capacity over the new NodeClaim's InstanceTypeOptions
+      for (int base = 0; base < a.n_tmpl && placed == -1; base += NT) {
+        const int t = base + tid;
+        const bool cand = t < a.n_tmpl && ((tolmask >> a.tmpl_taintset[t]) & 1) &&
+                          a.tmpl_fail[(size_t)sl * a.n_tmpl + t] != a.tmpl_ver[t];
+        const int n = compact_candidates<NW>(cand, t, s_list, s_wcnt);
+        for (int r0 = 0; r0 < n; r0 += NW) {
+          const int li = r0 + wave;
+          bool ok = false;
+          uint64_t m_v = 0, X = 0;
+          ReqView rv;
+          int tm = -1;
+          if (li < n) {
+            tm = s_list[li];
+            const int cat = a.tmpl_catalog[tm];
+            const DevCatalog& Cg = a.cats[cat];
+            X = lane < D.TW ? a.tmpl_X[(size_t)tm * D.TW + lane] : 0;
             const uint32_t lim = a.tmpl_limit_present[tm];
-            if (lim) {
-              const DevCatalog& Cg = a.cats[a.tmpl_catalog[tm]];
-              for (int r = 0; r < KP_NRES; r++) {
-                if (!((lim >> r) & 1)) continue;
-                int64_t mx = INT64_MIN;
-                uint64_t m = lane < D.TW ? X : 0;
-                while (m) {
-                  const int b = __builtin_ctzll(m);
-                  m &= m - 1;
-                  const int64_t c = Cg.cap[(size_t)r * D.T + lane * 64 + b];
-                  mx = c > mx ? c : mx;
-                }
-                mx = wave_max_i64(mx);
-                if (lane == 0) a.tmpl_remaining[(size_t)tm * KP_NRES + r] -= mx;
+            if (lim) {  // filterByRemainingResources: capacity <= remaining for every limited resource
+              const int64_t* rem = a.tmpl_remaining + (size_t)tm * KP_NRES;
+              uint64_t m = lane < D.TW ? X : 0, keep = 0;
+              while (m) {
+                const int b = __builtin_ctzll(m);
+                m &= m - 1;
+                const int ty = lane * 64 + b;
+                bool viable = true;
+                for (int r = 0; r < KP_NRES; r++)
+                  if (((lim >> r) & 1) && Cg.cap[(size_t)r * D.T + ty] > rem[r]) viable = false;
+                if (viable) keep |= 1ull << b;
+              }
+              X = keep;
+              bytes += (uint64_t)D.T * 8;
+            }
+            if (__ballot(X != 0)) {
+              attempts++;
+              ok = merge_compatible(D, kreq_at(a.tmpl_reqs, tm), B, b_negop, true, m_v, rv, &slots[wave], a.vint);
+              if (ok) {
+                int64_t total[KP_NRES];
+                for (int r = 0; r < KP_NRES; r++) total[r] = a.tmpl_daemon[(size_t)tm * KP_NRES + r] + preq[r];
+                const uint64_t* pvp = a.shape_pvp + (size_t)a.pvp_base[sl * a.n_catalogs + cat] * D.TW;
+                X = filter_types(D, Cg, rv, m_v, X, b_keys, pvp, pslot, total, a.vint, s_scratch[wave], &bytes);
+                ok = __ballot(X != 0) != 0;
               }
             }
+            if (!ok && lane == 0) a.tmpl_fail[(size_t)sl * a.n_tmpl + tm] = a.tmpl_ver[tm];
           }
-          placed = nc;
-        }
-        __syncthreads();
-        if (win >= 0) {
-          if (threadIdx.x == 0) s_ctl[2] = nc + 1;
-          break;
+          if (lane == 0) s_ok[wave] = ok ? 1 : 0;
+          __syncthreads();
+          const int win = first_ok<NW>(s_ok);
+          const int nc = s_ctl[2];
+          const bool in_lds = s_ctl[5] != 0;
+          if (win >= 0) {
+            if (wave == win) {
+              store_merged(reinterpret_cast<KReqs*>(a.nc_reqs + (size_t)nc * sizeof(KReqs)), rv, m_v, D.W, D.KB);
+              if (lane < D.TW) a.nc_X[(size_t)nc * D.TW + lane] = X;
+              if (lane < KP_NRES)
+                a.nc_requests[(size_t)nc * KP_NRES + lane] = a.tmpl_daemon[(size_t)tm * KP_NRES + lane] + preq[lane];
+              if (lane == 0) a.nc_tmpl[nc] = tm;
+              // subtractMax: remaining -= max capacity over the new NodeClaim's InstanceTypeOptions
+              const uint32_t lim = a.tmpl_limit_present[tm];
+              if (lim) {
+                const DevCatalog& Cg = a.cats[a.tmpl_catalog[tm]];
+                for (int r = 0; r < KP_NRES; r++) {
+                  if (!((lim >> r) & 1)) continue;
+                  int64_t mx = INT64_MIN;
+                  uint64_t m = lane < D.TW ? X : 0;
+                  while (m) {
+                    const int b = __builtin_ctzll(m);
+                    m &= m - 1;
+                    const int64_t c = Cg.cap[(size_t)r * D.T + lane * 64 + b];
+                    mx = c > mx ? c : mx;
+                  }
+                  mx = wave_max_i64(mx);
+                  if (lane == 0) a.tmpl_remaining[(size_t)tm * KP_NRES + r] -= mx;
+                }
+                if (lane == 0) a.tmpl_ver[tm] += 1;
+              }
+            }
+            placed = nc;
+          }
+          __syncthreads();
+          if (win >= 0) {
+            // append to newNodeClaims (spill the sort arrays to global memory past a.sort_cap)
+            if (in_lds && nc == a.sort_cap) {
+              for (int i = tid; i < nc; i += NT) {
+                a.g_order[i] = s_dyn[i];
+                a.g_npods[i] = s_dyn[a.sort_cap + i];
+              }
+            }
+            __syncthreads();
+            if (tid == 0) {
+              const bool lds_now = in_lds && nc < a.sort_cap;
+              int32_t* ord = lds_now ? s_dyn : a.g_order;
+              int32_t* npods = lds_now ? s_dyn + a.sort_cap : a.g_npods;
+              ord[nc] = nc;
+              npods[nc] = 1;
+              s_ctl[5] = lds_now ? 1 : 0;
+              s_ctl[2] = nc + 1;
+            }
+            break;
+          }
         }
       }
     }
 
     // ---- bookkeeping (thread 0): placement, or Preferences.Relax + Queue.Push -------------------
-    if (threadIdx.x == 0) {
+    if (tid == 0) {
       if (placed != -1) {
         a.placement[pod] = placed;
         a.events[s_ctl[4]++] = pod;
@@ -625,15 +702,15 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
     atomicAdd((unsigned long long*)&a.stats[0], (unsigned long long)attempts);
     atomicAdd((unsigned long long*)&a.stats[1], (unsigned long long)bytes);
   }
-  if (threadIdx.x == 0) {
+  if (tid == 0) {
     a.stats[2] = pops;
     a.stats[3] = (uint64_t)s_ctl[2];
     a.stats[4] = (uint64_t)s_ctl[4];
   }
-  if (a.sort_in_lds)
-    for (int i = threadIdx.x; i < s_ctl[2]; i += NW * 64) {
-      a.g_npods[i] = npods[i];
-      a.g_order[i] = ord[i];
+  if (s_ctl[5])
+    for (int i = tid; i < s_ctl[2]; i += NT) {
+      a.g_npods[i] = s_dyn[a.sort_cap + i];
+      a.g_order[i] = s_dyn[i];
     }
 }
 

@@ -84,3 +84,23 @@ def test_feasibility_kernel_vs_oracle(ctx, catalog):
         want_k, want_c = pyoracle.compatible_available_filter(prob.catalogs[0], reqs, rq)
         assert (kept[qi] == want_k).all(), f"query {qi}"
         np.testing.assert_array_equal(cheapest[qi][want_k], want_c[want_k])
+
+
+def test_sort_spill_to_global(ctx, catalog, monkeypatch):
+    """newNodeClaims order spills from LDS to global memory past the LDS capacity (forced small here)."""
+    from kpamd import synth
+    monkeypatch.setenv("KP_SORT_CAP", "5")
+    got, want = run_both(ctx, synth.config2(catalog, n_pods=2500, seed=11))
+    check_same(got, want)
+    assert len(got["nodeclaims"]) > 5
+
+
+def test_repeated_runs_identical(ctx, catalog):
+    """kp_solve_run restores all mutable device state: repeated runs of one plan give identical results."""
+    import kpamd
+    from kpamd import synth
+    prob = synth.random_problem(catalog, 5, n_types=150, n_pods=250, n_existing=40, n_shapes=20)
+    plan = kpamd.Scheduler(ctx, prob).prepare()
+    r1, r2 = plan.run(), plan.run()
+    plan.close()
+    check_same(r1, r2)
