@@ -394,6 +394,87 @@ __device__ __forceinline__ int first_ok(const int32_t* s_ok) {
 }
 
 
+// sort.Slice(newNodeClaims, len(Pods) asc), exactly as Go's pdqsort_func would permute it, using the
+// invariant that between two sort calls at most ONE mutation happened to the (sorted) slice:
+//   mut 1: the NodeClaim at position p gained a pod (key +1);  mut 2: a NodeClaim was appended (key 1).
+// pdqsort on such input: n <= 12 -> insertionSort (a stable move); n >= 50 with choosePivot's
+// increasingHint -> partialInsertionSort performs one swap + two shifts (a stable move) and returns
+// true. Every other case (12 < n < 50 with a descent, or a non-increasing hint) replays the full
+// pdqsort on one lane. A stable move is a block shift done by the whole workgroup.
+template <int NT>
+__device__ void sort_newnodeclaims(int32_t* ord, const int32_t* npods, int n, int mut, int p, int32_t* s_ctl) {
+  const int tid = threadIdx.x;
+  // s_ctl[7]: 0 nothing, 1 shift-left block (p+1..q-1 -> p..q-2, elem -> q-1), 2 shift-right (q..n-2 -> q+1..n-1,
+  // elem -> q), 3 slow path; s_ctl[5] reused? no: use s_ctl[8..9] for q / elem
+  if (tid == 0) {
+    int mode = 0, q = 0;
+    NCSort S{ord, npods};
+    if (mut == 1 && p + 1 < n && S.Less(p + 1, p)) {
+      mode = 1;
+    } else if (mut == 2 && n >= 2 && S.Less(n - 1, n - 2)) {
+      mode = 2;
+    }
+    if (mode) {
+      bool fast = n <= 12;
+      if (!fast && n >= 50) {
+        DevPDQ<NCSort> P{S};
+        int hint;
+        P.choosePivot(0, n, &hint);  // reads/compares only; no swaps on the slice
+        fast = hint == 0;
+      }
+      if (!fast) {
+        mode = 3;
+      } else if (mode == 1) {  // first q > p with key[q] >= key[p]
+        const int K = npods[ord[p]];
+        int lo = p + 1, hi = n;
+        while (lo < hi) {
+          const int m = (lo + hi) >> 1;
+          if (npods[ord[m]] >= K) hi = m;
+          else lo = m + 1;
+        }
+        q = lo;
+      } else {  // first q with key[q] > key of the appended element (in the sorted prefix [0, n-1))
+        const int K = npods[ord[n - 1]];
+        int lo = 0, hi = n - 1;
+        while (lo < hi) {
+          const int m = (lo + hi) >> 1;
+          if (npods[ord[m]] > K) hi = m;
+          else lo = m + 1;
+        }
+        q = lo;
+      }
+    }
+    if (mode == 3) go_sort_slice(S, n);
+    s_ctl[7] = mode;
+    s_ctl[8] = q;
+    s_ctl[9] = mode == 1 ? ord[p] : (mode == 2 ? ord[n - 1] : 0);
+  }
+  __syncthreads();
+  const int mode = s_ctl[7], q = s_ctl[8], elem = s_ctl[9];
+  if (mode == 1) {
+    const int c = q - 1 - p;  // elements p+1..q-1 move left by one
+    for (int off = 0; off < c; off += NT) {
+      const int i = off + tid;
+      const int v = i < c ? ord[p + 1 + i] : 0;
+      __syncthreads();
+      if (i < c) ord[p + i] = v;
+      __syncthreads();
+    }
+    if (tid == 0) ord[q - 1] = elem;
+  } else if (mode == 2) {
+    const int c = n - 1 - q;  // elements q..n-2 move right by one (process from the top down)
+    for (int off = 0; off < c; off += NT) {
+      const int i = c - 1 - (off + tid);
+      const int v = i >= 0 ? ord[q + i] : 0;
+      __syncthreads();
+      if (i >= 0) ord[q + i + 1] = v;
+      __syncthreads();
+    }
+    if (tid == 0) ord[q] = elem;
+  }
+  __syncthreads();
+}
+
 template <int NW>
 __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
   constexpr int NT = NW * 64;
@@ -401,7 +482,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
   __shared__ WaveSlots slots[NW];
   __shared__ int32_t s_ok[NW];
   __shared__ int32_t s_wcnt[NW];
-  __shared__ int32_t s_ctl[8];
+  __shared__ int32_t s_ctl[16];
   __shared__ int32_t s_list[NT];
   __shared__ uint32_t s_scratch[NW][2 * KP_MAX_WORDS];
   __shared__ KReqs s_B;  // the popped pod's requirements, staged once per pod
@@ -420,6 +501,8 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
     s_ctl[3] = 1;
     s_ctl[4] = 0;
     s_ctl[5] = 1;
+    s_ctl[10] = 0;  // pending mutation of newNodeClaims since the last sort: 0 none, 1 +1 at s_ctl[11], 2 appended
+    s_ctl[11] = 0;
   }
   __syncthreads();
 
@@ -507,8 +590,8 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
       int32_t* ord = in_lds ? s_dyn : a.g_order;
       int32_t* npods = in_lds ? s_dyn + a.sort_cap : a.g_npods;
       // ---- sort.Slice(newNodeClaims, len(Pods) asc) -----------------------------------------------
-      if (tid == 0) go_sort_slice(NCSort{ord, npods}, s_ctl[2]);
-      __syncthreads();
+      sort_newnodeclaims<NT>(ord, npods, s_ctl[2], s_ctl[10], s_ctl[11], s_ctl);
+      if (tid == 0) s_ctl[10] = 0;
       const int n_nc = s_ctl[2];
       // ---- addToInflightNode: first NodeClaim in that order whose Add succeeds ------------------
       for (int base = 0; base < n_nc && placed == -1; base += NT) {
@@ -559,6 +642,10 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
               }
             }
             placed = ord[s_list[r0 + win]];
+            if (tid == 0) {
+              s_ctl[10] = 1;
+              s_ctl[11] = s_list[r0 + win];
+            }
           }
           __syncthreads();
           if (win >= 0) break;
@@ -665,6 +752,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
               npods[nc] = 1;
               s_ctl[5] = lds_now ? 1 : 0;
               s_ctl[2] = nc + 1;
+              s_ctl[10] = 2;
             }
             break;
           }

@@ -104,3 +104,18 @@ def test_repeated_runs_identical(ctx, catalog):
     r1, r2 = plan.run(), plan.run()
     plan.close()
     check_same(r1, r2)
+
+
+def test_config2_many_nodeclaims(ctx, catalog):
+    """>= 50 NodeClaims: exercises the ninther choosePivot / partialInsertionSort fast path of the
+    device's sort.Slice replay against the oracle's literal pdqsort."""
+    from kpamd import synth
+    got, want = run_both(ctx, synth.config2(catalog, n_pods=12000, seed=2))
+    check_same(got, want)
+    assert len(got["nodeclaims"]) >= 50
+
+
+def test_config5_many_pools(ctx, catalog):
+    from kpamd import synth
+    got, want = run_both(ctx, synth.config5(catalog, n_pods=6000, seed=5))
+    check_same(got, want)
