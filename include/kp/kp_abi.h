@@ -250,6 +250,7 @@ typedef struct kp_solve_stats {
   uint64_t attempts;        /* NodeClaim.Add / ExistingNode.CanAdd evaluations */
   uint64_t bytes_algorithmic; /* bytes the device algorithm reads+writes */
   uint64_t pops;            /* queue pops */
+  uint64_t phase_cycles[8]; /* diagnostic (KP_TIMING=1): per-phase shader cycles of the solve loop */
 } kp_solve_stats;
 
 /* ---- context ---------------------------------------------------------------------------- */

@@ -60,6 +60,9 @@ struct SolveArgs {
   int32_t* ex_fail;                  // [SL][E]
   int32_t* tmpl_ver;                 // [NT]
   int32_t* tmpl_fail;                // [SL][NT]
+  int64_t* nc_maxalloc;              // [P][NRES] max allocatable over the NodeClaim's remaining types
+  uint32_t req_res_mask;             // resources some pod shape requests (> 0)
+  int32_t timing;                    // 1: thread 0 accumulates per-phase s_memtime deltas into stats[8..15]
   // outputs
   int32_t* placement;                // [P]
   int32_t* events;                   // [P] pods in placement order

@@ -1239,9 +1239,10 @@ int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out
   const size_t o_nct = blob.reserve(sizeof(int32_t) * Pc);
   const size_t o_npods = blob.reserve(sizeof(int32_t) * Pc);
   const size_t o_order = blob.reserve(sizeof(int32_t) * Pc);
+  const size_t o_maxalloc = blob.reserve(sizeof(int64_t) * (size_t)Pc * KP_NRES);
   const size_t o_place = blob.reserve(sizeof(int32_t) * Pc);
   const size_t o_events = blob.reserve(sizeof(int32_t) * Pc);
-  const size_t o_stats = blob.reserve(sizeof(uint64_t) * 8);
+  const size_t o_stats = blob.reserve(sizeof(uint64_t) * 16);
   // failure memo (see SolveArgs): versions start at 0, memo entries at -1
   const size_t SLn = std::max<size_t>(1, C.shape_reqs.size());
   const int ncc = (int)std::min<size_t>((size_t)Pc, std::max<size_t>(1, ((size_t)256 << 20) / (4 * SLn)));
@@ -1321,6 +1322,11 @@ int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out
   a.ex_fail = (int32_t*)(base + o_exfail);
   a.tmpl_ver = (int32_t*)(base + o_tver);
   a.tmpl_fail = (int32_t*)(base + o_tfail);
+  a.nc_maxalloc = (int64_t*)(base + o_maxalloc);
+  a.req_res_mask = 0;
+  for (size_t i = 0; i < C.shape_requests.size(); i++)
+    if (C.shape_requests[i] > 0) a.req_res_mask |= 1u << (i % KP_NRES);
+  a.timing = getenv("KP_TIMING") ? 1 : 0;
   a.placement = (int32_t*)(base + o_place);
   a.events = (int32_t*)(base + o_events);
   a.stats = (uint64_t*)(base + o_stats);
@@ -1367,7 +1373,7 @@ int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out) {
   const int P = plan->P, Pc = plan->Pc, opt_stride = plan->opt_stride;
   hipStream_t st = ctx->stream;
   HIPCHK(hipMemcpyAsync(base + plan->o_mut, base + plan->o_pristine, plan->n_mut, hipMemcpyDeviceToDevice, st));
-  HIPCHK(hipMemsetAsync(base + plan->o_stats, 0, sizeof(uint64_t) * 8, st));
+  HIPCHK(hipMemsetAsync(base + plan->o_stats, 0, sizeof(uint64_t) * 16, st));
   HIPCHK(hipMemsetAsync(base + plan->o_npods, 0, sizeof(int32_t) * Pc, st));
   HIPCHK(hipMemsetAsync(base + plan->o_place, 0xFF, sizeof(int32_t) * Pc, st));
   HIPCHK(hipMemsetAsync(base + plan->o_ver, 0, plan->n_ver, st));
@@ -1377,7 +1383,7 @@ int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out) {
   HIPCHK(hipEventRecord(ctx->ev0, st));
   HIPCHK(launch_solve(a, 8, dyn, st));
   HIPCHK(hipEventRecord(ctx->ev1, st));
-  uint64_t stats[8];
+  uint64_t stats[16];
   HIPCHK(hipMemcpyAsync(stats, base + plan->o_stats, sizeof stats, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   const int n_nc = (int)stats[3];
@@ -1465,6 +1471,7 @@ int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out) {
   res->stats.bytes_algorithmic = stats[1];
   res->stats.pops = stats[2];
   res->stats.prepare_ms = plan->prepare_ms;
+  for (int i = 0; i < 8; i++) res->stats.phase_cycles[i] = stats[8 + i];
   res->stats.host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   *out = res.release();
   return KP_OK;

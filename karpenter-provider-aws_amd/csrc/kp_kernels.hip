@@ -401,6 +401,26 @@ __device__ __forceinline__ int first_ok(const int32_t* s_ok) {
 // increasingHint -> partialInsertionSort performs one swap + two shifts (a stable move) and returns
 // true. Every other case (12 < n < 50 with a descent, or a non-increasing hint) replays the full
 // pdqsort on one lane. A stable move is a block shift done by the whole workgroup.
+// Max allocatable over the remaining types X (this lane's word) for the resources in `rmask`: a
+// NodeClaim whose requests + the pod's exceed it for any resource cannot take the pod (Fits fails for
+// every remaining type), so the candidate pre-pass can skip it without an attempt.
+__device__ void store_maxalloc(const DevCatalog& Cg, uint64_t X, int T, uint32_t rmask, int64_t* dst) {
+  const int lane = LANE;
+  for (int r = 0; r < KP_NRES; r++) {
+    if (!((rmask >> r) & 1)) continue;
+    int64_t mx = INT64_MIN;
+    uint64_t m = X;
+    while (m) {
+      const int b = __builtin_ctzll(m);
+      m &= m - 1;
+      const int64_t v = Cg.alloc[(size_t)r * T + lane * 64 + b];
+      mx = v > mx ? v : mx;
+    }
+    mx = wave_max_i64(mx);
+    if (lane == 0) dst[r] = mx;
+  }
+}
+
 template <int NT>
 __device__ void sort_newnodeclaims(int32_t* ord, const int32_t* npods, int n, int mut, int p, int32_t* s_ctl) {
   const int tid = threadIdx.x;
@@ -493,6 +513,15 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
   const int lane = LANE;
   if (tid == 0) D = *a.dict;
   uint64_t bytes = 0, attempts = 0, pops = 0;
+  uint64_t tph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tlast = 0;
+  const bool timing = a.timing && tid == 0;
+#define TS(ph)                                          \
+  if (timing) {                                         \
+    const uint64_t tnow = __builtin_amdgcn_s_memtime(); \
+    tph[ph] += tnow - tlast;                            \
+    tlast = tnow;                                       \
+  }
+  if (timing) tlast = __builtin_amdgcn_s_memtime();
   // control block (thread 0 owns): 0 head, 1 len, 2 n_nc, 3 lastLen epoch, 4 n_events, 5 sort arrays in LDS, 6 pod
   if (tid == 0) {
     s_ctl[0] = 0;
@@ -535,6 +564,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
       for (int i = tid; i < (int)(sizeof(KReqs) / 8); i += NT) dst[i] = src[i];
     }
     __syncthreads();
+    TS(0);
     const KReqs* B = &s_B;
     const uint64_t b_negop = a.shape_negop[sl];
     const uint64_t b_keys = s_B.present;
@@ -585,6 +615,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
       }
     }
 
+    TS(1);
     if (placed == -1) {
       const bool in_lds = s_ctl[5] != 0;
       int32_t* ord = in_lds ? s_dyn : a.g_order;
@@ -592,6 +623,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
       // ---- sort.Slice(newNodeClaims, len(Pods) asc) -----------------------------------------------
       sort_newnodeclaims<NT>(ord, npods, s_ctl[2], s_ctl[10], s_ctl[11], s_ctl);
       if (tid == 0) s_ctl[10] = 0;
+      TS(2);
       const int n_nc = s_ctl[2];
       // ---- addToInflightNode: first NodeClaim in that order whose Add succeeds ------------------
       for (int base = 0; base < n_nc && placed == -1; base += NT) {
@@ -601,6 +633,12 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
           const int nc = ord[i];
           cand = ((tolmask >> a.tmpl_taintset[a.nc_tmpl[nc]]) & 1) &&
                  !(nc < a.ncc && a.nc_fail[(size_t)sl * a.ncc + nc] == a.nc_ver[nc]);
+          if (cand) {
+            const int64_t* rq = a.nc_requests + (size_t)nc * KP_NRES;
+            const int64_t* mx = a.nc_maxalloc + (size_t)nc * KP_NRES;
+            for (int r = 0; r < KP_NRES; r++)
+              if (((a.req_res_mask >> r) & 1) && rq[r] + preq[r] > mx[r]) cand = false;
+          }
         }
         const int n = compact_candidates<NW>(cand, i, s_list, s_wcnt);
         bytes += (uint64_t)min(NT, n_nc - base) * 12;
@@ -640,6 +678,8 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
                 npods[nc] += 1;
                 a.nc_ver[nc] += 1;
               }
+              store_maxalloc(a.cats[a.tmpl_catalog[a.nc_tmpl[nc]]], lane < D.TW ? X : 0, D.T, a.req_res_mask,
+                             a.nc_maxalloc + (size_t)nc * KP_NRES);
             }
             placed = ord[s_list[r0 + win]];
             if (tid == 0) {
@@ -653,6 +693,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
       }
     }
 
+    TS(3);
     if (placed == -1) {
       // ---- addToNewNodeClaim: templates in weight order --------------------------------------------
       for (int base = 0; base < a.n_tmpl && placed == -1; base += NT) {
@@ -712,6 +753,8 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
               if (lane < KP_NRES)
                 a.nc_requests[(size_t)nc * KP_NRES + lane] = a.tmpl_daemon[(size_t)tm * KP_NRES + lane] + preq[lane];
               if (lane == 0) a.nc_tmpl[nc] = tm;
+              store_maxalloc(a.cats[a.tmpl_catalog[tm]], lane < D.TW ? X : 0, D.T, a.req_res_mask,
+                             a.nc_maxalloc + (size_t)nc * KP_NRES);
               // subtractMax: remaining -= max capacity over the new NodeClaim's InstanceTypeOptions
               const uint32_t lim = a.tmpl_limit_present[tm];
               if (lim) {
@@ -760,6 +803,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
       }
     }
 
+    TS(4);
     // ---- bookkeeping (thread 0): placement, or Preferences.Relax + Queue.Push -------------------
     if (tid == 0) {
       if (placed != -1) {
@@ -784,7 +828,11 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
       }
     }
     __syncthreads();
+    TS(5);
   }
+#undef TS
+  if (timing)
+    for (int i = 0; i < 8; i++) a.stats[8 + i] = tph[i];
 
   if (lane == 0) {
     atomicAdd((unsigned long long*)&a.stats[0], (unsigned long long)attempts);

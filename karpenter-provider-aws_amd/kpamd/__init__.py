@@ -134,8 +134,13 @@ def read_result(lib, res, n_pods, prefix="kp_result_"):
         })
     st = abi.SolveStats()
     get("stats")(res, C.byref(st))
-    stats = {f: getattr(st, f) for f, _ in abi.SolveStats._fields_}
-    return {"placement": placement, "nodeclaims": ncs, "stats": stats}
+    return {"placement": placement, "nodeclaims": ncs, "stats": stats_dict(st)}
+
+
+def stats_dict(st):
+    d = {f: getattr(st, f) for f, _ in abi.SolveStats._fields_}
+    d["phase_cycles"] = list(st.phase_cycles)
+    return d
 
 
 def _check_generic(lib, rc):
@@ -187,7 +192,7 @@ class SolvePlan:
                 return read_result(lib, res, self.sched.problem.n_pods)
             st = abi.SolveStats()
             lib.kp_result_stats(res, C.byref(st))
-            return {"stats": {f: getattr(st, f) for f, _ in abi.SolveStats._fields_}}
+            return {"stats": stats_dict(st)}
         finally:
             lib.kp_result_destroy(res)
 
