@@ -257,6 +257,9 @@ struct DictBuilder {
     int rk = d.key(kResID), tk = d.key(kResType);
     d.dd.resid_key_bit = rk >= 0 ? 1ull << rk : 0;
     d.dd.restype_key_bit = tk >= 0 ? 1ull << tk : 0;
+    d.dd.offer_keys = d.dd.resid_key_bit | d.dd.restype_key_bit;
+    for (const char* k : {kCapType, kZone, kZoneID})
+      if (d.key(k) >= 0) d.dd.offer_keys |= 1ull << d.key(k);
     return KP_OK;
   }
 };
@@ -1240,6 +1243,7 @@ int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out
   const size_t o_npods = blob.reserve(sizeof(int32_t) * Pc);
   const size_t o_order = blob.reserve(sizeof(int32_t) * Pc);
   const size_t o_maxalloc = blob.reserve(sizeof(int64_t) * (size_t)Pc * KP_NRES);
+  const size_t o_fitj = blob.reserve(sizeof(int32_t) * (size_t)Pc * KP_NRES);
   const size_t o_place = blob.reserve(sizeof(int32_t) * Pc);
   const size_t o_events = blob.reserve(sizeof(int32_t) * Pc);
   const size_t o_stats = blob.reserve(sizeof(uint64_t) * 16);
@@ -1323,6 +1327,7 @@ int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out
   a.tmpl_ver = (int32_t*)(base + o_tver);
   a.tmpl_fail = (int32_t*)(base + o_tfail);
   a.nc_maxalloc = (int64_t*)(base + o_maxalloc);
+  a.nc_fitj = (int32_t*)(base + o_fitj);
   a.req_res_mask = 0;
   for (size_t i = 0; i < C.shape_requests.size(); i++)
     if (C.shape_requests[i] > 0) a.req_res_mask |= 1u << (i % KP_NRES);

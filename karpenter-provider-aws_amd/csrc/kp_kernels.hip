@@ -229,7 +229,8 @@ __device__ int wave_lower_bound(const int64_t* vals, int n, int64_t q, uint64_t*
 // remaining types (invariant: X already passes every key the pod did not touch). Returns the new word.
 __device__ uint64_t filter_types(const DevDict& D, const DevCatalog& Cg, const ReqView& rv, uint64_t m_v, uint64_t X,
                                  uint64_t pod_keys, const uint64_t* pvp, const int32_t* pvp_slot, const int64_t* total,
-                                 const int64_t* vint, uint32_t* scratch, uint64_t* bytes) {
+                                 const int64_t* vint, uint32_t* scratch, uint64_t* bytes, const int32_t* jstart,
+                                 int32_t* jout) {
   const int lane = LANE;
   const int TW = D.TW;
   const uint64_t negM = negop_mask(rv.present, rv.compl_, rv.nz);
@@ -264,18 +265,29 @@ __device__ uint64_t filter_types(const DevDict& D, const DevCatalog& Cg, const R
       X &= acc;
     }
   }
-  // 2) resources.Fits(total, allocatable): per requested resource, a threshold mask
+  // 2) resources.Fits(total, allocatable): per requested resource, a threshold mask. A NodeClaim's totals
+  //    only grow, so the threshold index does too: probe 64 entries past the cached index first.
   for (int r = 0; r < KP_NRES; r++) {
     const int64_t q = total[r];
-    if (q <= 0) continue;
-    const int n = Cg.fit_n[r];
-    const int j = wave_lower_bound(Cg.fit_vals + (size_t)r * D.T, n, q, &nb);
-    if (j >= n) X = 0;
-    else if (lane < TW) X &= Cg.fit_mask[((size_t)r * D.T + j) * TW + lane];
-    nb += (uint64_t)TW * 8;
+    int j = 0;
+    if (q > 0) {
+      const int n = Cg.fit_n[r];
+      const int64_t* vals = Cg.fit_vals + (size_t)r * D.T;
+      const int j0 = jstart ? jstart[r] : 0;
+      const int idx = j0 + lane;
+      const uint64_t bal = __ballot(idx < n && vals[idx] >= q);
+      nb += 512;
+      if (bal) j = j0 + __builtin_ctzll(bal);
+      else j = j0 + 64 >= n ? n : wave_lower_bound(vals + j0 + 64, n - j0 - 64, q, &nb) + j0 + 64;
+      if (j >= n) X = 0;
+      else if (lane < TW) X &= Cg.fit_mask[((size_t)r * D.T + j) * TW + lane];
+      nb += (uint64_t)TW * 8;
+    }
+    if (lane == r) jout[r] = j;
   }
-  // 3) some available offering compatible with the merged requirements
-  {
+  // 3) some available offering compatible with the merged requirements. X already satisfies the
+  //    candidate's offering keys; only a pod that constrains one of them can change the answer.
+  if (pod_keys & D.offer_keys) {
     const uint64_t cls = allowed_classes(D, Cg, rv, allowed, negM);
     uint64_t offer = 0;
     uint64_t m = cls;
@@ -401,9 +413,9 @@ __device__ __forceinline__ int first_ok(const int32_t* s_ok) {
 // increasingHint -> partialInsertionSort performs one swap + two shifts (a stable move) and returns
 // true. Every other case (12 < n < 50 with a descent, or a non-increasing hint) replays the full
 // pdqsort on one lane. A stable move is a block shift done by the whole workgroup.
-// Max allocatable over the remaining types X (this lane's word) for the resources in `rmask`: a
-// NodeClaim whose requests + the pod's exceed it for any resource cannot take the pod (Fits fails for
-// every remaining type), so the candidate pre-pass can skip it without an attempt.
+// Max allocatable over a NodeClaim's types at creation, for the resources in `rmask`. Its remaining
+// types only shrink, so this stays an upper bound: a NodeClaim whose requests + the pod's exceed it for any
+// resource cannot take the pod (Fits fails for every remaining type) and the pre-pass skips it.
 __device__ void store_maxalloc(const DevCatalog& Cg, uint64_t X, int T, uint32_t rmask, int64_t* dst) {
   const int lane = LANE;
   for (int r = 0; r < KP_NRES; r++) {
@@ -506,6 +518,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
   __shared__ int32_t s_list[NT];
   __shared__ uint32_t s_scratch[NW][2 * KP_MAX_WORDS];
   __shared__ KReqs s_B;  // the popped pod's requirements, staged once per pod
+  __shared__ int32_t s_fitj[NW][KP_NRES];
   extern __shared__ int32_t s_dyn[];  // ord[a.sort_cap], npods[a.sort_cap] while n_nc <= a.sort_cap
 
   const int tid = threadIdx.x;
@@ -660,7 +673,8 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
               for (int r = 0; r < KP_NRES; r++) total[r] = a.nc_requests[(size_t)nc * KP_NRES + r] + preq[r];
               X = lane < D.TW ? a.nc_X[(size_t)nc * D.TW + lane] : 0;
               const uint64_t* pvp = a.shape_pvp + (size_t)a.pvp_base[sl * a.n_catalogs + cat] * D.TW;
-              X = filter_types(D, a.cats[cat], rv, m_v, X, b_keys, pvp, pslot, total, a.vint, s_scratch[wave], &bytes);
+              X = filter_types(D, a.cats[cat], rv, m_v, X, b_keys, pvp, pslot, total, a.vint, s_scratch[wave], &bytes,
+                               a.nc_fitj + (size_t)nc * KP_NRES, s_fitj[wave]);
               ok = __ballot(X != 0) != 0;
               bytes += (uint64_t)D.TW * 8 + KP_NRES * 8;
             }
@@ -678,8 +692,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
                 npods[nc] += 1;
                 a.nc_ver[nc] += 1;
               }
-              store_maxalloc(a.cats[a.tmpl_catalog[a.nc_tmpl[nc]]], lane < D.TW ? X : 0, D.T, a.req_res_mask,
-                             a.nc_maxalloc + (size_t)nc * KP_NRES);
+              if (lane < KP_NRES) a.nc_fitj[(size_t)nc * KP_NRES + lane] = s_fitj[wave][lane];
             }
             placed = ord[s_list[r0 + win]];
             if (tid == 0) {
@@ -735,7 +748,8 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
                 int64_t total[KP_NRES];
                 for (int r = 0; r < KP_NRES; r++) total[r] = a.tmpl_daemon[(size_t)tm * KP_NRES + r] + preq[r];
                 const uint64_t* pvp = a.shape_pvp + (size_t)a.pvp_base[sl * a.n_catalogs + cat] * D.TW;
-                X = filter_types(D, Cg, rv, m_v, X, b_keys, pvp, pslot, total, a.vint, s_scratch[wave], &bytes);
+                X = filter_types(D, Cg, rv, m_v, X, b_keys, pvp, pslot, total, a.vint, s_scratch[wave], &bytes,
+                                 nullptr, s_fitj[wave]);
                 ok = __ballot(X != 0) != 0;
               }
             }
@@ -753,6 +767,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
               if (lane < KP_NRES)
                 a.nc_requests[(size_t)nc * KP_NRES + lane] = a.tmpl_daemon[(size_t)tm * KP_NRES + lane] + preq[lane];
               if (lane == 0) a.nc_tmpl[nc] = tm;
+              if (lane < KP_NRES) a.nc_fitj[(size_t)nc * KP_NRES + lane] = s_fitj[wave][lane];
               store_maxalloc(a.cats[a.tmpl_catalog[tm]], lane < D.TW ? X : 0, D.T, a.req_res_mask,
                              a.nc_maxalloc + (size_t)nc * KP_NRES);
               // subtractMax: remaining -= max capacity over the new NodeClaim's InstanceTypeOptions

@@ -45,6 +45,7 @@ struct DevDict {
   uint64_t single_valued;    // catalogue keys where every type has <= 1 value (complement trick allowed)
   uint64_t resid_key_bit;    // 1<<key of karpenter.k8s.aws/capacity-reservation-id (0 if absent)
   uint64_t restype_key_bit;  // 1<<key of ...capacity-reservation-type (0 if absent)
+  uint64_t offer_keys;       // keys an offering requirement can name (capacity-type, zone, zone-id, reservation)
   int8_t wkey[KP_MAX_WORDS];     // key of each value word (-1 past W)
   int32_t wofs[KP_MAX_KEYS];     // first word of key k
   int32_t nval[KP_MAX_KEYS];     // values of key k
