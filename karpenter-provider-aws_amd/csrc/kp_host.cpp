@@ -1244,6 +1244,7 @@ int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out
   const size_t o_order = blob.reserve(sizeof(int32_t) * Pc);
   const size_t o_maxalloc = blob.reserve(sizeof(int64_t) * (size_t)Pc * KP_NRES);
   const size_t o_fitj = blob.reserve(sizeof(int32_t) * (size_t)Pc * KP_NRES);
+  const size_t o_ncts = blob.reserve(sizeof(int32_t) * (size_t)Pc);
   const size_t o_place = blob.reserve(sizeof(int32_t) * Pc);
   const size_t o_events = blob.reserve(sizeof(int32_t) * Pc);
   const size_t o_stats = blob.reserve(sizeof(uint64_t) * 16);
@@ -1328,9 +1329,12 @@ int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out
   a.tmpl_fail = (int32_t*)(base + o_tfail);
   a.nc_maxalloc = (int64_t*)(base + o_maxalloc);
   a.nc_fitj = (int32_t*)(base + o_fitj);
+  a.nc_taintset = (int32_t*)(base + o_ncts);
   a.req_res_mask = 0;
   for (size_t i = 0; i < C.shape_requests.size(); i++)
     if (C.shape_requests[i] > 0) a.req_res_mask |= 1u << (i % KP_NRES);
+  for (size_t i = 0; i < C.tmpl_daemon.size(); i++)  // Fits iterates every resource of the merged requests
+    if (C.tmpl_daemon[i] > 0) a.req_res_mask |= 1u << (i % KP_NRES);
   a.timing = getenv("KP_TIMING") ? 1 : 0;
   a.placement = (int32_t*)(base + o_place);
   a.events = (int32_t*)(base + o_events);

@@ -19,6 +19,8 @@
 #include "kp_model.h"
 
 #define LANE ((int)(threadIdx.x & 63))
+#define FITV_RES 4      // requested resources whose Fits thresholds are staged in LDS
+#define FITV_CAP 1024   // distinct allocatable values per staged resource
 
 // ------------------------------------------------------------------------------------------------
 // wave helpers
@@ -228,7 +230,8 @@ __device__ int wave_lower_bound(const int64_t* vals, int n, int64_t q, uint64_t*
 // NodeClaim.Add's instance-type filter after a successful merge. X: this lane's word of the candidate's
 // remaining types (invariant: X already passes every key the pod did not touch). Returns the new word.
 __device__ uint64_t filter_types(const DevDict& D, const DevCatalog& Cg, const ReqView& rv, uint64_t m_v, uint64_t X,
-                                 uint64_t pod_keys, const uint64_t* pvp, const int32_t* pvp_slot, const int64_t* total,
+                                 uint64_t pod_keys, const uint64_t* pvp, const int32_t* pvp_slot, const int64_t* reqrow,
+                                 const int64_t* s_preq, const int64_t* const* fitv, uint32_t rmask,
                                  const int64_t* vint, uint32_t* scratch, uint64_t* bytes, const int32_t* jstart,
                                  int32_t* jout) {
   const int lane = LANE;
@@ -267,24 +270,31 @@ __device__ uint64_t filter_types(const DevDict& D, const DevCatalog& Cg, const R
   }
   // 2) resources.Fits(total, allocatable): per requested resource, a threshold mask. A NodeClaim's totals
   //    only grow, so the threshold index does too: probe 64 entries past the cached index first.
-  for (int r = 0; r < KP_NRES; r++) {
-    const int64_t q = total[r];
-    int j = 0;
-    if (q > 0) {
-      const int n = Cg.fit_n[r];
-      const int64_t* vals = Cg.fit_vals + (size_t)r * D.T;
-      const int j0 = jstart ? jstart[r] : 0;
-      const int idx = j0 + lane;
-      const uint64_t bal = __ballot(idx < n && vals[idx] >= q);
-      nb += 512;
-      if (bal) j = j0 + __builtin_ctzll(bal);
-      else j = j0 + 64 >= n ? n : wave_lower_bound(vals + j0 + 64, n - j0 - 64, q, &nb) + j0 + 64;
-      if (j >= n) X = 0;
-      else if (lane < TW) X &= Cg.fit_mask[((size_t)r * D.T + j) * TW + lane];
-      nb += (uint64_t)TW * 8;
-    }
-    if (lane == r) jout[r] = j;
+  //    Lane r holds resource r's total and cached index (one load level for all resources).
+  const int64_t q_lane = lane < KP_NRES ? reqrow[lane] + s_preq[lane] : 0;
+  const int32_t j0_lane = (lane < KP_NRES && jstart) ? jstart[lane] : 0;
+  int32_t j_lane = 0;
+  uint32_t rm = rmask;
+  while (rm) {
+    const int r = __builtin_ctz(rm);
+    rm &= rm - 1;
+    const int64_t q = __shfl(q_lane, r, 64);
+    if (q <= 0) continue;
+    const int j0 = __shfl(j0_lane, r, 64);
+    const int n = Cg.fit_n[r];
+    const int64_t* vals = fitv[r];
+    const int idx = j0 + lane;
+    const uint64_t bal = __ballot(idx < n && vals[idx] >= q);
+    nb += 512;
+    int j;
+    if (bal) j = j0 + __builtin_ctzll(bal);
+    else j = j0 + 64 >= n ? n : wave_lower_bound(vals + j0 + 64, n - j0 - 64, q, &nb) + j0 + 64;
+    if (j >= n) X = 0;
+    else if (lane < TW) X &= Cg.fit_mask[((size_t)r * D.T + j) * TW + lane];
+    nb += (uint64_t)TW * 8;
+    if (lane == r) j_lane = j;
   }
+  if (lane < KP_NRES) jout[lane] = j_lane;
   // 3) some available offering compatible with the merged requirements. X already satisfies the
   //    candidate's offering keys; only a pod that constrains one of them can change the answer.
   if (pod_keys & D.offer_keys) {
@@ -519,12 +529,36 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
   __shared__ uint32_t s_scratch[NW][2 * KP_MAX_WORDS];
   __shared__ KReqs s_B;  // the popped pod's requirements, staged once per pod
   __shared__ int32_t s_fitj[NW][KP_NRES];
+  __shared__ int64_t s_preq[KP_NRES];          // pod requests (staged per pod)
+  __shared__ int32_t s_pslot[KP_MAX_KEYS];     // PVP row of each pod key (staged per pod)
+  __shared__ const int64_t* s_fitp[KP_NRES];   // fit threshold values per resource: LDS copy or global
+  __shared__ const int64_t* s_fitg[8][KP_NRES];  // same, global, for catalogues 1..7
+  __shared__ int64_t s_fitv[FITV_RES][FITV_CAP];
   extern __shared__ int32_t s_dyn[];  // ord[a.sort_cap], npods[a.sort_cap] while n_nc <= a.sort_cap
 
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
   const int lane = LANE;
   if (tid == 0) D = *a.dict;
+  __syncthreads();
+  {  // Fits threshold tables of catalogue 0 for the first FITV_RES requested resources -> LDS
+    const DevCatalog& C0 = a.cats[0];
+    int slot = 0;
+    for (int r = 0; r < KP_NRES; r++) {
+      const int64_t* g = C0.fit_vals + (size_t)r * D.T;
+      const int n = C0.fit_n[r];
+      const bool stage = ((a.req_res_mask >> r) & 1) && slot < FITV_RES && n <= FITV_CAP;
+      if (stage) {
+        for (int i = tid; i < n; i += NT) s_fitv[slot][i] = g[i];
+        if (tid == 0) s_fitp[r] = s_fitv[slot];
+        slot++;
+      } else if (tid == 0) {
+        s_fitp[r] = g;
+      }
+      for (int c = 1; c < a.n_catalogs && c < 8; c++)
+        if (tid == 0) s_fitg[c][r] = a.cats[c].fit_vals + (size_t)r * D.T;
+    }
+  }
   uint64_t bytes = 0, attempts = 0, pops = 0;
   uint64_t tph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tlast = 0;
   const bool timing = a.timing && tid == 0;
@@ -575,15 +609,15 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
       const uint64_t* src = reinterpret_cast<const uint64_t*>(kreq_at(a.shape_reqs, sl));
       uint64_t* dst = reinterpret_cast<uint64_t*>(&s_B);
       for (int i = tid; i < (int)(sizeof(KReqs) / 8); i += NT) dst[i] = src[i];
+      if (tid < KP_NRES) s_preq[tid] = a.shape_requests[(size_t)shape * KP_NRES + tid];
+      else if (tid >= 64 && tid < 64 + KP_MAX_KEYS) s_pslot[tid - 64] = a.pvp_slot[(size_t)sl * KP_MAX_KEYS + tid - 64];
     }
     __syncthreads();
     TS(0);
     const KReqs* B = &s_B;
     const uint64_t b_negop = a.shape_negop[sl];
     const uint64_t b_keys = s_B.present;
-    const int64_t* preq = a.shape_requests + (size_t)shape * KP_NRES;
     const uint64_t tolmask = a.shape_tolerates[shape];
-    const int32_t* pslot = a.pvp_slot + (size_t)sl * KP_MAX_KEYS;
     int placed = -1;  // >= 0 NodeClaim id; <= -2 existing node; -1 not placed
 
     // ---- addToExistingNode: lowest index whose CanAdd succeeds -------------------------------
@@ -594,7 +628,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
         const int64_t* av = a.ex_available + (size_t)e * KP_NRES;
         const int64_t* rq = a.ex_requests + (size_t)e * KP_NRES;
         bool fits = true;  // Fits(Merge(requests, pod), available): CanAdd's resource check, exact
-        for (int r = 0; r < KP_NRES; r++) fits = fits && av[r] >= 0 && rq[r] + preq[r] <= av[r];
+        for (int r = 0; r < KP_NRES; r++) fits = fits && av[r] >= 0 && rq[r] + s_preq[r] <= av[r];
         cand = fits;
       }
       const int n = compact_candidates<NW>(cand, e, s_list, s_wcnt);
@@ -618,7 +652,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
         if (win >= 0) {
           if (wave == win) {
             store_merged(reinterpret_cast<KReqs*>(a.ex_reqs + (size_t)ei * sizeof(KReqs)), rv, m_v, D.W, D.KB);
-            if (lane < KP_NRES) a.ex_requests[(size_t)ei * KP_NRES + lane] += preq[lane];
+            if (lane < KP_NRES) a.ex_requests[(size_t)ei * KP_NRES + lane] += s_preq[lane];
             if (lane == 0) a.ex_ver[ei] += 1;
           }
           placed = -2 - s_list[r0 + win];
@@ -644,16 +678,17 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
         bool cand = false;
         if (i < n_nc) {
           const int nc = ord[i];
-          cand = ((tolmask >> a.tmpl_taintset[a.nc_tmpl[nc]]) & 1) &&
+          cand = ((tolmask >> a.nc_taintset[nc]) & 1) &&
                  !(nc < a.ncc && a.nc_fail[(size_t)sl * a.ncc + nc] == a.nc_ver[nc]);
           if (cand) {
             const int64_t* rq = a.nc_requests + (size_t)nc * KP_NRES;
             const int64_t* mx = a.nc_maxalloc + (size_t)nc * KP_NRES;
             for (int r = 0; r < KP_NRES; r++)
-              if (((a.req_res_mask >> r) & 1) && rq[r] + preq[r] > mx[r]) cand = false;
+              if (((a.req_res_mask >> r) & 1) && rq[r] + s_preq[r] > mx[r]) cand = false;
           }
         }
         const int n = compact_candidates<NW>(cand, i, s_list, s_wcnt);
+        TS(6);
         bytes += (uint64_t)min(NT, n_nc - base) * 12;
         for (int r0 = 0; r0 < n; r0 += NW) {
           const int li = r0 + wave;
@@ -669,11 +704,10 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
             ok = merge_compatible(D, kreq_at(a.nc_reqs, nc), B, b_negop, true, m_v, rv, &slots[wave], a.vint);
             bytes += sizeof(KReqs);
             if (ok) {
-              int64_t total[KP_NRES];
-              for (int r = 0; r < KP_NRES; r++) total[r] = a.nc_requests[(size_t)nc * KP_NRES + r] + preq[r];
               X = lane < D.TW ? a.nc_X[(size_t)nc * D.TW + lane] : 0;
               const uint64_t* pvp = a.shape_pvp + (size_t)a.pvp_base[sl * a.n_catalogs + cat] * D.TW;
-              X = filter_types(D, a.cats[cat], rv, m_v, X, b_keys, pvp, pslot, total, a.vint, s_scratch[wave], &bytes,
+              X = filter_types(D, a.cats[cat], rv, m_v, X, b_keys, pvp, s_pslot, a.nc_requests + (size_t)nc * KP_NRES,
+                               s_preq, s_fitp, a.req_res_mask, a.vint, s_scratch[wave], &bytes,
                                a.nc_fitj + (size_t)nc * KP_NRES, s_fitj[wave]);
               ok = __ballot(X != 0) != 0;
               bytes += (uint64_t)D.TW * 8 + KP_NRES * 8;
@@ -682,12 +716,13 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
           }
           if (lane == 0) s_ok[wave] = ok ? 1 : 0;
           __syncthreads();
+          TS(7);
           const int win = first_ok<NW>(s_ok);
           if (win >= 0) {
             if (wave == win) {
               store_merged(reinterpret_cast<KReqs*>(a.nc_reqs + (size_t)nc * sizeof(KReqs)), rv, m_v, D.W, D.KB);
               if (lane < D.TW) a.nc_X[(size_t)nc * D.TW + lane] = X;
-              if (lane < KP_NRES) a.nc_requests[(size_t)nc * KP_NRES + lane] += preq[lane];
+              if (lane < KP_NRES) a.nc_requests[(size_t)nc * KP_NRES + lane] += s_preq[lane];
               if (lane == 0) {
                 npods[nc] += 1;
                 a.nc_ver[nc] += 1;
@@ -745,10 +780,9 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
               attempts++;
               ok = merge_compatible(D, kreq_at(a.tmpl_reqs, tm), B, b_negop, true, m_v, rv, &slots[wave], a.vint);
               if (ok) {
-                int64_t total[KP_NRES];
-                for (int r = 0; r < KP_NRES; r++) total[r] = a.tmpl_daemon[(size_t)tm * KP_NRES + r] + preq[r];
                 const uint64_t* pvp = a.shape_pvp + (size_t)a.pvp_base[sl * a.n_catalogs + cat] * D.TW;
-                X = filter_types(D, Cg, rv, m_v, X, b_keys, pvp, pslot, total, a.vint, s_scratch[wave], &bytes,
+                X = filter_types(D, Cg, rv, m_v, X, b_keys, pvp, s_pslot, a.tmpl_daemon + (size_t)tm * KP_NRES, s_preq,
+                                 cat == 0 ? s_fitp : s_fitg[cat & 7], a.req_res_mask, a.vint, s_scratch[wave], &bytes,
                                  nullptr, s_fitj[wave]);
                 ok = __ballot(X != 0) != 0;
               }
@@ -765,8 +799,11 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
               store_merged(reinterpret_cast<KReqs*>(a.nc_reqs + (size_t)nc * sizeof(KReqs)), rv, m_v, D.W, D.KB);
               if (lane < D.TW) a.nc_X[(size_t)nc * D.TW + lane] = X;
               if (lane < KP_NRES)
-                a.nc_requests[(size_t)nc * KP_NRES + lane] = a.tmpl_daemon[(size_t)tm * KP_NRES + lane] + preq[lane];
-              if (lane == 0) a.nc_tmpl[nc] = tm;
+                a.nc_requests[(size_t)nc * KP_NRES + lane] = a.tmpl_daemon[(size_t)tm * KP_NRES + lane] + s_preq[lane];
+              if (lane == 0) {
+                a.nc_tmpl[nc] = tm;
+                a.nc_taintset[nc] = a.tmpl_taintset[tm];
+              }
               if (lane < KP_NRES) a.nc_fitj[(size_t)nc * KP_NRES + lane] = s_fitj[wave][lane];
               store_maxalloc(a.cats[a.tmpl_catalog[tm]], lane < D.TW ? X : 0, D.T, a.req_res_mask,
                              a.nc_maxalloc + (size_t)nc * KP_NRES);

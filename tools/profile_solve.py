@@ -18,10 +18,10 @@ plan = kpamd.Scheduler(ctx, prob).prepare()
 plan.run(read=False)
 r = plan.run(read=True)
 st = r["stats"]
-names = ["pop+stageB", "existing", "sort", "inflight(prepass+attempts)", "templates", "bookkeeping", "-", "-"]
+names = ["pop+stageB", "existing", "sort", "inflight-commit", "templates", "bookkeeping", "inflight-prepass", "inflight-attempts"]
 tot = sum(st["phase_cycles"]) or 1
 out = {"pods": n, "solve_kernel_ms": st["solve_kernel_ms"], "attempts": st["attempts"], "pops": st["pops"],
        "nodeclaims": len(r["nodeclaims"]), "attempts_per_pod": st["attempts"] / n,
-       "phase_share": {k: round(v / tot, 4) for k, v in zip(names, st["phase_cycles"]) if k != "-"},
+       "phase_share": {k: round(v / tot, 4) for k, v in zip(names, st["phase_cycles"]) },
        "cycles_per_pod": tot / n}
 print(json.dumps(out))
