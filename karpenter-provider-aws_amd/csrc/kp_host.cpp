@@ -221,24 +221,35 @@ struct DictBuilder {
     d.keys = order;
     d.vals.assign(order.size(), {});
     d.val_id.assign(order.size(), {});
-    int w = 0;
-    for (size_t k = 0; k < order.size(); k++) {
-      d.key_id[order[k]] = (int)k;
+    const int K = (int)order.size();
+    int w = K;  // words 0..K-1 are the keys' first words; overflow words follow
+    for (int k = 0; k < K; k++) {
+      d.key_id[order[k]] = k;
       auto& s = values[order[k]];
       d.vals[k].assign(s.begin(), s.end());
       const int nw = std::max<int>(1, (int)((s.size() + 63) / 64));
-      d.dd.wofs[k] = w;
+      d.dd.wofs[k] = k;
+      d.dd.ovf[k] = nw > 1 ? w : -1;
       d.dd.nval[k] = (int)s.size();
-      if (w + nw > KP_MAX_WORDS) return fail(KP_E_UNSUPPORTED, "label values need > %d words", KP_MAX_WORDS);
-      for (int i = 0; i < nw; i++) d.dd.wkey[w + i] = (int8_t)k;
+      d.dd.wkey[k] = (int8_t)k;
+      if (nw > 1) {
+        if (w + nw - 1 > KP_MAX_WORDS) return fail(KP_E_UNSUPPORTED, "label values need > %d words", KP_MAX_WORDS);
+        d.dd.multiword |= 1ull << k;
+        for (int i = 0; i < nw - 1; i++) {
+          d.dd.wkey[w + i] = (int8_t)k;
+          d.dd.ovfmask[k] |= 1ull << (w + i);
+        }
+        w += nw - 1;
+      }
       int b = 0;
       for (auto& v : d.vals[k]) {
-        d.val_id[k][v] = w * 64 + b;
-        d.dd.validbits[w + b / 64] |= 1ull << (b % 64);
+        const int word = b < 64 ? k : d.dd.ovf[k] + b / 64 - 1;
+        d.val_id[k][v] = word * 64 + b % 64;
+        d.dd.validbits[word] |= 1ull << (b % 64);
         b++;
       }
-      w += nw;
     }
+    d.dd.firstmask = K >= 64 ? ~0ull : ((1ull << K) - 1);
     for (int i = w; i < KP_MAX_WORDS; i++) d.dd.wkey[i] = -1;
     d.dd.K = (int)order.size();
     d.dd.W = w;
@@ -276,6 +287,7 @@ bool Within(const Dict& d, int bit, bool hg, int64_t gt, bool hl, int64_t lt) {
   return true;
 }
 int nwords(const Dict& d, int k) { return std::max(1, (d.dd.nval[k] + 63) / 64); }
+int kw(const Dict& d, int k, int i) { return i == 0 ? k : d.dd.ovf[k] + i - 1; }  // i-th word of key k
 
 KReqs Single(const Dict& d, const RawReq& r) {
   KReqs q;
@@ -328,7 +340,7 @@ void HostAdd(const Dict& d, KReqs& A, const KReqs& B) {
   for (int k = 0; k < d.dd.K; k++) {
     const uint64_t kb = 1ull << k;
     if (!(B.present & kb)) continue;
-    const int w0 = d.dd.wofs[k], nw = nwords(d, k);
+    const int nw = nwords(d, k);
     const bool bnd = k < KP_MAX_BOUND_KEYS;
     if (!(A.present & kb)) {
       A.present |= kb;
@@ -341,7 +353,7 @@ void HostAdd(const Dict& d, KReqs& A, const KReqs& B) {
         A.lt[k] = B.lt[k];
         A.minv[k] = B.minv[k];
       }
-      for (int w = w0; w < w0 + nw; w++) A.vals[w] = B.vals[w];
+      for (int i = 0; i < nw; i++) A.vals[kw(d, k, i)] = B.vals[kw(d, k, i)];
       continue;
     }
     const bool c1 = A.compl_ & kb, c2 = B.compl_ & kb;
@@ -359,10 +371,11 @@ void HostAdd(const Dict& d, KReqs& A, const KReqs& B) {
       A.compl_ &= ~kb;
       A.hgt &= ~kb;
       A.hlt &= ~kb;
-      for (int w = w0; w < w0 + nw; w++) A.vals[w] = 0;
+      for (int i = 0; i < nw; i++) A.vals[kw(d, k, i)] = 0;
       continue;
     }
-    for (int w = w0; w < w0 + nw; w++) {
+    for (int i = 0; i < nw; i++) {
+      const int w = kw(d, k, i);
       const uint64_t a = A.vals[w], b = B.vals[w];
       uint64_t v = (c1 && c2) ? (a | b) : c1 ? (b & ~a) : c2 ? (a & ~b) : (a & b);
       if (hg || hl) {
@@ -396,8 +409,8 @@ KReqs Compile(const Dict& d, const RawReqs& rs) {
   return q;
 }
 bool KeyNonEmptyVals(const Dict& d, const KReqs& q, int k) {
-  for (int w = d.dd.wofs[k]; w < d.dd.wofs[k] + nwords(d, k); w++)
-    if (q.vals[w]) return true;
+  for (int i = 0; i < nwords(d, k); i++)
+    if (q.vals[kw(d, k, i)]) return true;
   return false;
 }
 uint64_t NegOp(const Dict& d, const KReqs& q) {
@@ -475,7 +488,7 @@ int32_t CompileCatalog(const Dict& d, const vector<HostType>& types, int TW, map
                     d.keys[k].c_str());
       if (!(d.dd.wellknown & kb) && !(neg & kb)) hc.custom_nonneg[t] |= kb;
       int cnt = 0, last = -1;
-      for (int w = d.dd.wofs[k]; w < d.dd.wofs[k] + nwords(d, k); w++) {
+      for (int wi = 0, w = kw(d, k, 0); wi < nwords(d, k); wi++, w = wi < nwords(d, k) ? kw(d, k, wi) : 0) {
         uint64_t m = q.vals[w];
         while (m) {
           int b = __builtin_ctzll(m);
@@ -577,7 +590,7 @@ void HostFilterTypes(const Dict& d, const HostCat& hc, const KReqs& q, int TW, c
     if (!((q.present >> k) & 1)) continue;
     vector<uint64_t> acc(TW, 0);
     for (int w = 0; w < TW; w++) acc[w] = hc.NOKEY[(size_t)k * TW + w] | (((neg >> k) & 1) ? hc.DNE[(size_t)k * TW + w] : 0);
-    for (int w = d.dd.wofs[k]; w < d.dd.wofs[k] + nwords(d, k); w++) {
+    for (int wi = 0, w = kw(d, k, 0); wi < nwords(d, k); wi++, w = wi < nwords(d, k) ? kw(d, k, wi) : 0) {
       uint64_t m = d.dd.validbits[w];
       while (m) {
         int b = __builtin_ctzll(m);
@@ -617,7 +630,7 @@ int CountDistinct(const Dict& d, const HostCat& hc, int k, const vector<int>& ty
   std::set<int> vals;
   for (int t : types) {
     const KReqs& q = hc.treqs[t];
-    for (int w = d.dd.wofs[k]; w < d.dd.wofs[k] + nwords(d, k); w++) {
+    for (int wi = 0, w = kw(d, k, 0); wi < nwords(d, k); wi++, w = wi < nwords(d, k) ? kw(d, k, wi) : 0) {
       uint64_t m = q.vals[w];
       while (m) {
         int b = __builtin_ctzll(m);
@@ -1062,7 +1075,7 @@ int32_t CompileSolve(const kp_solve_in* in, Compiled& cp) {
         for (int k = 0; k < d.dd.K; k++) {
           if (!((q.present >> k) & 1) || !((cp.d.dd.single_valued >> k) & 1)) continue;
           vector<uint64_t> acc(hc.NOKEY.begin() + (size_t)k * TW, hc.NOKEY.begin() + (size_t)(k + 1) * TW);
-          for (int w = d.dd.wofs[k]; w < d.dd.wofs[k] + nwords(d, k); w++) {
+          for (int wi = 0, w = kw(d, k, 0); wi < nwords(d, k); wi++, w = wi < nwords(d, k) ? kw(d, k, wi) : 0) {
             uint64_t m = d.dd.validbits[w];
             while (m) {
               int b = __builtin_ctzll(m);

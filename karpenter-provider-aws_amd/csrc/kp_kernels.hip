@@ -47,8 +47,14 @@ __device__ __forceinline__ int64_t wave_max_i64(int64_t v) {
   }
   return v;
 }
-// every lane must call (uniform control flow)
-__device__ __forceinline__ uint64_t lane_bcast(uint64_t v, int src) { return __shfl(v, src, 64); }
+// broadcast lane `src` (wave-uniform) to the wave: two v_readlane, no LDS crossbar
+__device__ __forceinline__ uint64_t lane_bcast(uint64_t v, int src) {
+  const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, src);
+  const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), src);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ int64_t lane_bcast_i64(int64_t v, int src) { return (int64_t)lane_bcast((uint64_t)v, src); }
+__device__ __forceinline__ int key_word(const DevDict& D, int k, int i) { return i == 0 ? k : D.ovf[k] + i - 1; }
 
 // Requirement bounds filter (withinIntPtrs) applied to the value bits of one word.
 __device__ __forceinline__ uint64_t within_word(uint64_t v, int word, const int64_t* vint, uint64_t intok, bool hg,
@@ -77,10 +83,20 @@ __device__ __forceinline__ uint64_t negop_mask(uint64_t present, uint64_t compl_
   return present & ((compl_ & nz) | (~compl_ & ~nz));
 }
 
+// keys with at least one value bit: word k is key k's first word, so one ballot + the few overflow keys
 __device__ __forceinline__ uint64_t nz_keys(const DevDict& D, uint64_t v) {
-  const int lane = LANE;
-  const int k = lane < D.W ? (int)D.wkey[lane] : -1;
-  return wave_or((v != 0 && k >= 0) ? (1ull << k) : 0ull);
+  const uint64_t bal = __ballot(v != 0 && LANE < D.W);
+  uint64_t nz = bal & D.firstmask;
+  const uint64_t ov = bal & ~D.firstmask;
+  if (ov) {
+    uint64_t mk = D.multiword;
+    while (mk) {
+      const int k = __builtin_ctzll(mk);
+      mk &= mk - 1;
+      if (ov & D.ovfmask[k]) nz |= 1ull << k;
+    }
+  }
+  return nz;
 }
 
 // Per-wave LDS scratch holding a merged requirement set's bound slots.
@@ -255,8 +271,9 @@ __device__ uint64_t filter_types(const DevDict& D, const DevCatalog& Cg, const R
     } else {
       uint64_t acc = lane < TW ? Cg.NOKEY[(size_t)k * TW + lane] : 0;
       if (ng && lane < TW) acc |= Cg.DNE[(size_t)k * TW + lane];
-      const int w0 = D.wofs[k], nw = (D.nval[k] + 63) >> 6;
-      for (int w = w0; w < w0 + nw; w++) {
+      const int nw = (D.nval[k] + 63) >> 6;
+      for (int wi = 0; wi < nw; wi++) {
+        const int w = key_word(D, k, wi);
         uint64_t a = lane_bcast(allowed, w);
         while (a) {
           const int b = __builtin_ctzll(a);
@@ -278,9 +295,9 @@ __device__ uint64_t filter_types(const DevDict& D, const DevCatalog& Cg, const R
   while (rm) {
     const int r = __builtin_ctz(rm);
     rm &= rm - 1;
-    const int64_t q = __shfl(q_lane, r, 64);
+    const int64_t q = lane_bcast_i64(q_lane, r);
     if (q <= 0) continue;
-    const int j0 = __shfl(j0_lane, r, 64);
+    const int j0 = __builtin_amdgcn_readlane(j0_lane, r);
     const int n = Cg.fit_n[r];
     const int64_t* vals = fitv[r];
     const int idx = j0 + lane;
@@ -314,7 +331,7 @@ __device__ uint64_t filter_types(const DevDict& D, const DevCatalog& Cg, const R
   while (mk) {
     const int k = __builtin_ctzll(mk);
     mk &= mk - 1;
-    const int w0 = D.wofs[k], nw = (D.nval[k] + 63) >> 6;
+    const int nw = (D.nval[k] + 63) >> 6;
     int count = 0;
     if ((D.single_valued >> k) & 1) {
       for (int w = lane; w < 2 * nw; w += 64) scratch[w] = 0;
@@ -325,7 +342,8 @@ __device__ uint64_t filter_types(const DevDict& D, const DevCatalog& Cg, const R
         m &= m - 1;
         const uint16_t code = Cg.code[(size_t)k * D.T + lane * 64 + b];
         if (code < 0xFFFD) {
-          const int rel = (int)code - w0 * 64;
+          const int cw = code >> 6;
+          const int rel = (cw == k ? 0 : (cw - D.ovf[k] + 1) * 64) + (code & 63);  // ordinal within key k
           atomicOr(&scratch[rel >> 5], 1u << (rel & 31));
         }
       }
@@ -335,7 +353,8 @@ __device__ uint64_t filter_types(const DevDict& D, const DevCatalog& Cg, const R
       count = wave_sum(c);
       wave_sync();
     } else {
-      for (int w = w0; w < w0 + nw; w++) {
+      for (int wi = 0; wi < nw; wi++) {
+        const int w = key_word(D, k, wi);
         uint64_t vb = D.validbits[w];
         while (vb) {
           const int b = __builtin_ctzll(vb);

@@ -5,8 +5,9 @@
 //    0..KB-1 (KB <= 16) so their bound slots are dense.
 //  * Every (key, value) pair mentioned anywhere in a solve (catalogue requirements, offerings, NodePool
 //    requirements/labels, pod selectors/affinities, node labels) gets one bit. Key k owns the
-//    WORD-ALIGNED bit range [64*wofs[k], 64*wofs[k] + nval[k]); total words W <= 64, so one wave holds a
-//    whole requirement set with one 64-bit word per lane.
+//    WORD-ALIGNED bit range: its first 64 values live in word k, further values in overflow words
+//    (ovf[k]..) after the K first words; total words W <= 64, so one wave holds a whole requirement set
+//    with one 64-bit word per lane, and "which keys have values" is one __ballot.
 //  * An exact scheduling.Requirements value ("kreqs") is: key masks present/complement/has_gt/has_lt/
 //    has_min, the bound slots, and the value bitmap vals[W] (upstream Requirement{values, complement,
 //    greaterThan, lessThan, MinValues}). Value bits of complement keys hold the NotIn set.
@@ -47,7 +48,11 @@ struct DevDict {
   uint64_t restype_key_bit;  // 1<<key of ...capacity-reservation-type (0 if absent)
   uint64_t offer_keys;       // keys an offering requirement can name (capacity-type, zone, zone-id, reservation)
   int8_t wkey[KP_MAX_WORDS];     // key of each value word (-1 past W)
-  int32_t wofs[KP_MAX_KEYS];     // first word of key k
+  int32_t wofs[KP_MAX_KEYS];     // first word of key k (== k: key k's first value word is word k)
+  int32_t ovf[KP_MAX_KEYS];      // first overflow word of key k (keys with > 64 values), -1 if none
+  uint64_t firstmask;            // words 0..K-1 (first words)
+  uint64_t multiword;            // keys with overflow words
+  uint64_t ovfmask[KP_MAX_KEYS]; // overflow words of key k
   int32_t nval[KP_MAX_KEYS];     // values of key k
   uint64_t validbits[KP_MAX_WORDS];  // bits that name a value
   uint64_t vint_ok[KP_MAX_WORDS];    // bits whose value parses with strconv.Atoi
