@@ -350,6 +350,55 @@ int32_t kp_result_nodeclaim(const kp_solve_result* res, uint32_t i, kp_nodeclaim
 int32_t kp_result_stats(const kp_solve_result* res, kp_solve_stats* out);
 void kp_result_destroy(kp_solve_result* res);
 
+/* ---- Disruption: batched consolidation simulations ---------------------------------------------
+ * Cluster snapshot as the disruption controller sees it (state.Cluster nodes + their reschedulable pods),
+ * and a batch of candidate subsets. For each subset S, kp_simulate_batch computes what upstream
+ * computeConsolidation(S...) decides (docs R:website/content/en/preview/concepts/disruption.md:89-128):
+ * SimulateScheduling = Solve(pods of S, existing = every other node) + TruncateInstanceTypes(100); not all
+ * pods scheduled -> no-op; 0 NodeClaims -> delete; > 1 -> no-op; 1 -> replace if some option's worst
+ * launch price is below the summed candidate price (and, for multi-node, filterOutSameType keeps one).
+ * Spot-to-spot (feature gate, default off) -> no-op. */
+typedef struct kp_cluster_node {
+  kp_existing_node node;      /* labels, taints, available (allocatable - bound pods), requests, initialized */
+  uint32_t catalog;           /* catalogue of its instance type */
+  uint32_t instance_type;     /* index of its instance type in that catalogue */
+  const uint32_t* pods;       /* reschedulable pods on this node: indices into kp_cluster.pods */
+  uint32_t n_pods;
+  uint32_t reserved_;
+} kp_cluster_node;
+
+typedef struct kp_cluster {
+  const kp_catalog* const* catalogs;      /* device path */
+  const kp_catalog_desc* catalog_descs;   /* CPU oracle path */
+  uint32_t n_catalogs;
+  uint32_t n_nodepools;
+  const kp_nodepool* nodepools;
+  const kp_cluster_node* nodes;
+  uint32_t n_nodes;
+  uint32_t n_shapes;
+  const kp_pod_shape* shapes;
+  const kp_pod* pods;
+  uint32_t n_pods;
+  uint32_t spot_to_spot;      /* SpotToSpotConsolidation feature gate (only 0 supported) */
+} kp_cluster;
+
+enum kp_decision { KP_DECISION_NOOP = 0, KP_DECISION_DELETE = 1, KP_DECISION_REPLACE = 2 };
+
+typedef struct kp_sim_result {
+  int32_t decision;           /* enum kp_decision */
+  uint32_t replacement_nodepool;
+  double candidate_price;     /* getCandidatePrices: sum of each candidate's cheapest label-compatible offering */
+  double replacement_price;   /* REPLACE: min worst-launch price over the remaining replacement options */
+  double savings;             /* DELETE: candidate_price; REPLACE: candidate_price - replacement_price; else 0 */
+  uint32_t n_options;         /* REPLACE: replacement options left after the price filters */
+  uint32_t n_pods;            /* pods rescheduled by the simulation */
+} kp_sim_result;
+
+/* subsets in CSR form: subset i = nodes[offsets[i] .. offsets[i+1]) (indices into cluster->nodes), in
+ * candidate order. multi_node != 0 applies MultiNodeConsolidation's filterOutSameType to replacements. */
+int32_t kp_simulate_batch(kp_ctx* ctx, const kp_cluster* cluster, const uint32_t* offsets, const uint32_t* nodes,
+                          uint32_t n_subsets, int32_t multi_node, kp_sim_result* out, kp_solve_stats* stats);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1644,4 +1644,10 @@ int32_t kp_filter_compatible_available(kp_ctx* ctx, const kp_catalog* cat, const
   return KP_OK;
 }
 
+int32_t kp_simulate_batch(kp_ctx* ctx, const kp_cluster* cl, const uint32_t* offsets, const uint32_t* nodes,
+                          uint32_t n_subsets, int32_t multi_node, kp_sim_result* out, kp_solve_stats* stats) {
+  (void)ctx; (void)cl; (void)offsets; (void)nodes; (void)n_subsets; (void)multi_node; (void)out; (void)stats;
+  return fail(KP_E_UNSUPPORTED, "kp_simulate_batch: not built yet");
+}
+
 }  // extern "C"

@@ -132,6 +132,25 @@ class NodeClass(C.Structure):
                 ("reserved_", C.c_int32)]
 
 
+class ClusterNode(C.Structure):
+    _fields_ = [("node", ExistingNode), ("catalog", C.c_uint32), ("instance_type", C.c_uint32),
+                ("pods", C.POINTER(C.c_uint32)), ("n_pods", C.c_uint32), ("reserved_", C.c_uint32)]
+
+
+class Cluster(C.Structure):
+    _fields_ = [("catalogs", C.POINTER(C.c_void_p)), ("catalog_descs", C.POINTER(CatalogDesc)),
+                ("n_catalogs", C.c_uint32), ("n_nodepools", C.c_uint32), ("nodepools", C.POINTER(NodePool)),
+                ("nodes", C.POINTER(ClusterNode)), ("n_nodes", C.c_uint32), ("n_shapes", C.c_uint32),
+                ("shapes", C.POINTER(PodShape)), ("pods", C.POINTER(Pod)), ("n_pods", C.c_uint32),
+                ("spot_to_spot", C.c_uint32)]
+
+
+class SimResult(C.Structure):
+    _fields_ = [("decision", C.c_int32), ("replacement_nodepool", C.c_uint32), ("candidate_price", C.c_double),
+                ("replacement_price", C.c_double), ("savings", C.c_double), ("n_options", C.c_uint32),
+                ("n_pods", C.c_uint32)]
+
+
 class FeasibilityQuery(C.Structure):
     _fields_ = [("requirements", Requirements), ("requests", ResourceList)]
 
@@ -250,3 +269,39 @@ def build_solve_in(arena, problem, catalog_handles=None):
                  len(problem.shapes), shapes, pods_ptr, len(problem.pod_shape), problem.max_instance_types)
     arena.keep.append(si)
     return si
+
+
+def _pods_array(arena, shape, creation, uid):
+    import numpy as np
+    pods_np = np.zeros(len(shape), dtype=[("shape", "<u4"), ("r", "<u4"), ("c", "<i8"), ("u", "<u8")])
+    pods_np["shape"] = shape
+    pods_np["c"] = creation
+    pods_np["u"] = uid
+    arena.keep.append(pods_np)
+    return pods_np.ctypes.data_as(C.POINTER(Pod))
+
+
+def build_cluster(arena, cl, catalog_handles=None):
+    """kpamd.model.Cluster -> kp_cluster."""
+    descs = arena.arr(CatalogDesc, [arena.catalog_desc(c) for c in cl.catalogs]) if catalog_handles is None else None
+    handles = arena.arr(C.c_void_p, catalog_handles) if catalog_handles is not None else None
+    nps = arena.arr(NodePool, [arena.nodepool(np, np.catalog) for np in cl.nodepools])
+    nodes = []
+    for n in cl.nodes:
+        pods = arena.arr(C.c_uint32, list(n.pods))
+        nodes.append(ClusterNode(arena.existing_node(n.node), n.catalog, n.instance_type, pods, len(n.pods), 0))
+    nodes_a = arena.arr(ClusterNode, nodes)
+    shapes = arena.arr(PodShape, [arena.shape(s) for s in cl.shapes])
+    c = Cluster(handles, descs, len(cl.catalogs), len(cl.nodepools), nps, nodes_a, len(cl.nodes), len(cl.shapes),
+                shapes, _pods_array(arena, cl.pod_shape, cl.pod_creation, cl.pod_uid), len(cl.pod_shape), 0)
+    arena.keep.append(c)
+    return c
+
+
+def subsets_csr(arena, subsets):
+    import numpy as np
+    offs = np.zeros(len(subsets) + 1, dtype=np.uint32)
+    offs[1:] = np.cumsum([len(s) for s in subsets])
+    flat = np.concatenate([np.asarray(s, dtype=np.uint32) for s in subsets]) if subsets else np.zeros(1, np.uint32)
+    arena.keep.extend([offs, flat])
+    return offs.ctypes.data_as(C.POINTER(C.c_uint32)), flat.ctypes.data_as(C.POINTER(C.c_uint32))

@@ -78,6 +78,28 @@ class ExistingNode:
 
 
 @dataclass
+class ClusterNode:
+    """state.StateNode as disruption sees it: an existing node + its instance type + reschedulable pods."""
+    node: ExistingNode
+    catalog: int
+    instance_type: int
+    pods: List[int] = field(default_factory=list)   # indices into Cluster.pod_*
+
+
+@dataclass
+class Cluster:
+    catalogs: List[List[InstanceType]]
+    nodepools: List[NodePool]
+    nodes: List[ClusterNode]
+    shapes: List[PodShape]
+    pod_shape: np.ndarray
+    pod_creation: np.ndarray
+    pod_uid: np.ndarray
+    candidates: List[int] = field(default_factory=list)  # disruption-cost order
+    name: str = ""
+
+
+@dataclass
 class Problem:
     catalogs: List[List[InstanceType]]
     nodepools: List[NodePool]

@@ -864,6 +864,8 @@ struct kpo_result {
     std::vector<uint32_t> pods, options;
     uint32_t n_remaining;
     kp_resource_list requests;
+    Requirements reqs;                      // final NodeClaim requirements (consolidation needs them)
+    const std::vector<InstanceType>* cat = nullptr;
   };
   std::vector<NC> ncs;
   kp_solve_stats stats;
@@ -884,12 +886,11 @@ static std::vector<Taint> TaintsFromABI(const kp_taint* t, uint32_t n) {
   return v;
 }
 
-int32_t kpo_solve(const kp_solve_in* in, kpo_result** out) {
-  auto t0 = std::chrono::steady_clock::now();
-  if (!in || !out || (!in->catalog_descs && in->n_catalogs)) return KP_E_INVAL;
-  std::vector<std::shared_ptr<std::vector<InstanceType>>> cats;
-  for (uint32_t i = 0; i < in->n_catalogs; i++) cats.push_back(CatalogFromABI(in->catalog_descs[i]));
+using Catalogs = std::vector<std::shared_ptr<std::vector<InstanceType>>>;
 
+// Provisioner.NewScheduler + Scheduler.Solve + Results.TruncateInstanceTypes over already-converted catalogues.
+static int32_t SolveCore(const Catalogs& cats, const kp_solve_in* in, kpo_result** out) {
+  auto t0 = std::chrono::steady_clock::now();
   Scheduler s;
   // NewScheduler: templates per NodePool ordered by weight desc, name asc; options pre-filtered by the
   // template requirements with empty requests.
@@ -1027,6 +1028,8 @@ int32_t kpo_solve(const kp_solve_in* in, kpo_result** out) {
     size_t lim = in->max_instance_types ? std::min<size_t>(keyed.size(), in->max_instance_types) : keyed.size();
     for (size_t i = 0; i < lim; i++) trunc.push_back(keyed[i].second);
     bool ok = !HasMinValues(n.reqs) || SatisfiesMinValues(cat, trunc, n.reqs);
+    o.reqs = n.reqs;
+    o.cat = &cat;
     if (ok) {
       for (int t : trunc) o.options.push_back((uint32_t)t);
       for (int p : n.pods) {
@@ -1045,6 +1048,168 @@ int32_t kpo_solve(const kp_solve_in* in, kpo_result** out) {
   res->stats.bytes_algorithmic = s.counters.type_checks;  // type rows visited (SURVEY §8d counter)
   res->stats.host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   *out = res;
+  return KP_OK;
+}
+
+int32_t kpo_solve(const kp_solve_in* in, kpo_result** out) {
+  if (!in || !out || (!in->catalog_descs && in->n_catalogs)) return KP_E_INVAL;
+  Catalogs cats;
+  for (uint32_t i = 0; i < in->n_catalogs; i++) cats.push_back(CatalogFromABI(in->catalog_descs[i]));
+  return SolveCore(cats, in, out);
+}
+
+
+// ---- disruption: computeConsolidation over candidate subsets -------------
+// Offerings.Compatible(NewLabelRequirements(node labels)).Cheapest().Price (getCandidatePrices /
+// filterOutSameType); false when no offering is label-compatible.
+static bool CandidatePrice(const InstanceType& it, const Requirements& labels, double* price) {
+  bool any = false;
+  double p = 0;
+  for (auto& o : it.offerings)
+    if (Compatible(labels, o.reqs, true)) {
+      if (!any || o.price < p) p = o.price;
+      any = true;
+    }
+  *price = p;
+  return any;
+}
+// Offerings.Available().WorstLaunchPrice(reqs): capacity types in precedence reserved, spot, on-demand;
+// the most expensive compatible available offering of the first capacity type that has one.
+static double WorstLaunchPrice(const InstanceType& it, const Requirements& reqs) {
+  for (const char* ct : {"reserved", "spot", "on-demand"}) {
+    bool any = false;
+    double mx = 0;
+    for (auto& o : it.offerings) {
+      if (!o.available || !Compatible(reqs, o.reqs, true)) continue;
+      auto f = o.reqs.find(kLabelCapacityType);
+      if (f == o.reqs.end() || !Has(f->second, ct)) continue;
+      if (!any || o.price > mx) mx = o.price;
+      any = true;
+    }
+    if (any) return mx;
+  }
+  return std::numeric_limits<double>::max();
+}
+
+int32_t kpo_simulate_batch(const kp_cluster* cl, const uint32_t* offsets, const uint32_t* nodes, uint32_t n_subsets,
+                           int32_t multi_node, kp_sim_result* out, kp_solve_stats* stats) {
+  auto t0 = std::chrono::steady_clock::now();
+  if (!cl || !offsets || !out || (!cl->catalog_descs && cl->n_catalogs)) return KP_E_INVAL;
+  if (cl->spot_to_spot) return KP_E_UNSUPPORTED;
+  Catalogs cats;
+  for (uint32_t i = 0; i < cl->n_catalogs; i++) cats.push_back(CatalogFromABI(cl->catalog_descs[i]));
+  std::vector<Requirements> nodeLabels(cl->n_nodes);
+  for (uint32_t i = 0; i < cl->n_nodes; i++) nodeLabels[i] = LabelRequirements(cl->nodes[i].node.labels, cl->nodes[i].node.n_labels);
+  uint64_t attempts = 0;
+  std::vector<char> inS(cl->n_nodes, 0);
+  for (uint32_t s = 0; s < n_subsets; s++) {
+    kp_sim_result& r = out[s];
+    memset(&r, 0, sizeof r);
+    std::vector<uint32_t> cand(nodes + offsets[s], nodes + offsets[s + 1]);
+    for (uint32_t c : cand) inS[c] = 1;
+    // SimulateScheduling: pods of the candidates, every other (active) node as an existing node
+    std::vector<kp_existing_node> ex;
+    std::vector<uint32_t> exIdx;
+    for (uint32_t i = 0; i < cl->n_nodes; i++)
+      if (!inS[i]) {
+        ex.push_back(cl->nodes[i].node);
+        exIdx.push_back(i);
+      }
+    std::vector<kp_pod> pods;
+    for (uint32_t c : cand)
+      for (uint32_t j = 0; j < cl->nodes[c].n_pods; j++) pods.push_back(cl->pods[cl->nodes[c].pods[j]]);
+    for (uint32_t c : cand) inS[c] = 0;
+    r.n_pods = (uint32_t)pods.size();
+    kp_solve_in in;
+    memset(&in, 0, sizeof in);
+    in.n_catalogs = cl->n_catalogs;
+    in.catalog_descs = cl->catalog_descs;
+    in.n_nodepools = cl->n_nodepools;
+    in.nodepools = cl->nodepools;
+    in.existing = ex.data();
+    in.n_existing = (uint32_t)ex.size();
+    in.n_shapes = cl->n_shapes;
+    in.shapes = cl->shapes;
+    in.pods = pods.data();
+    in.n_pods = (uint32_t)pods.size();
+    in.max_instance_types = 100;
+    kpo_result* res = nullptr;
+    int32_t rc = SolveCore(cats, &in, &res);
+    if (rc) return rc;
+    std::unique_ptr<kpo_result> guard(res);
+    attempts += res->stats.attempts;
+    // every pod scheduled, and not onto an uninitialized node (SimulateScheduling's UninitializedNodeError)
+    bool all = true;
+    for (int32_t pl : res->placement) {
+      if (pl == -1) all = false;
+      else if (pl <= -2 && !ex[(size_t)(-2 - pl)].initialized) all = false;
+    }
+    double candPrice = 0;
+    bool priced = true;
+    for (uint32_t c : cand) {
+      const kp_cluster_node& n = cl->nodes[c];
+      double p;
+      if (!CandidatePrice((*cats[n.catalog])[n.instance_type], nodeLabels[c], &p)) priced = false;
+      candPrice += p;
+    }
+    r.candidate_price = priced ? candPrice : 0;
+    if (!all) continue;  // no-op
+    if (res->ncs.empty()) {
+      r.decision = KP_DECISION_DELETE;
+      r.savings = r.candidate_price;
+      continue;
+    }
+    if (res->ncs.size() != 1 || !priced) continue;
+    const auto& nc = res->ncs[0];
+    const auto& cat = *nc.cat;
+    bool allSpot = true;
+    for (uint32_t c : cand) {
+      auto f = nodeLabels[c].find(kLabelCapacityType);
+      if (f == nodeLabels[c].end() || f->second.complement || !f->second.values.count("spot")) allSpot = false;
+    }
+    auto ctr = nc.reqs.find(kLabelCapacityType);
+    const bool ncSpot = ctr == nc.reqs.end() || Has(ctr->second, "spot");
+    if (allSpot && ncSpot) continue;  // spot-to-spot consolidation: feature gate off
+    std::vector<int> kept;
+    for (uint32_t t : nc.options)
+      if (WorstLaunchPrice(cat[t], nc.reqs) < candPrice) kept.push_back((int)t);
+    if (HasMinValues(nc.reqs) && !SatisfiesMinValues(cat, kept, nc.reqs)) continue;
+    if (kept.empty()) continue;
+    if (multi_node) {  // filterOutSameType
+      std::map<std::string, double> prices;
+      for (uint32_t c : cand) {
+        const kp_cluster_node& n = cl->nodes[c];
+        const InstanceType& it = (*cats[n.catalog])[n.instance_type];
+        double p;
+        if (!CandidatePrice(it, nodeLabels[c], &p)) continue;
+        auto f = prices.find(it.name);
+        if (f == prices.end() || p < f->second) prices[it.name] = p;
+      }
+      double maxPrice = std::numeric_limits<double>::max();
+      for (int t : kept) {
+        auto f = prices.find(cat[t].name);
+        if (f != prices.end() && f->second < maxPrice) maxPrice = f->second;
+      }
+      std::vector<int> k2;
+      for (int t : kept)
+        if (WorstLaunchPrice(cat[t], nc.reqs) < maxPrice) k2.push_back(t);
+      if (HasMinValues(nc.reqs) && !SatisfiesMinValues(cat, k2, nc.reqs)) continue;
+      kept.swap(k2);
+      if (kept.empty()) continue;
+    }
+    double best = std::numeric_limits<double>::max();
+    for (int t : kept) best = std::min(best, WorstLaunchPrice(cat[t], nc.reqs));
+    r.decision = KP_DECISION_REPLACE;
+    r.replacement_nodepool = nc.nodepool;
+    r.replacement_price = best;
+    r.savings = candPrice - best;
+    r.n_options = (uint32_t)kept.size();
+  }
+  if (stats) {
+    memset(stats, 0, sizeof *stats);
+    stats->attempts = attempts;
+    stats->host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
   return KP_OK;
 }
 

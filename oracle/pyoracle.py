@@ -46,6 +46,8 @@ def load(path=LIB_PATH):
         "kpo_requirements_intersects": (C.c_int32, [P(abi.Requirements), P(abi.Requirements)]),
         "kpo_instance_type_resolve": (C.c_int32, [P(abi.Options), P(abi.EC2Info), P(abi.NodeClass),
                                                   P(abi.ResourceList), C.c_void_p]),
+        "kpo_simulate_batch": (C.c_int32, [P(abi.Cluster), P(C.c_uint32), P(C.c_uint32), C.c_uint32, C.c_int32,
+                                           P(abi.SimResult), P(abi.SolveStats)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -126,3 +128,23 @@ def instance_type_resolve(opts, info, nodeclass):
     rc = lib.kpo_instance_type_resolve(C.byref(opts), C.byref(info), C.byref(nodeclass), C.byref(cap), C.byref(ovh))
     assert rc == 0
     return cap, ovh
+
+
+def simulate_batch(cluster, subsets, multi_node=True):
+    """computeConsolidation for each candidate subset (list of node indices). Returns (results, stats)."""
+    lib = load()
+    arena = abi.Arena()
+    cl = abi.build_cluster(arena, cluster)
+    offs, flat = abi.subsets_csr(arena, subsets)
+    out = (abi.SimResult * max(1, len(subsets)))()
+    st = abi.SolveStats()
+    rc = lib.kpo_simulate_batch(C.byref(cl), offs, flat, len(subsets), 1 if multi_node else 0, out, C.byref(st))
+    if rc != 0:
+        raise RuntimeError(f"kpo_simulate_batch = {rc}")
+    return [sim_dict(out[i]) for i in range(len(subsets))], st
+
+
+def sim_dict(r):
+    return {"decision": r.decision, "nodepool": r.replacement_nodepool, "candidate_price": r.candidate_price,
+            "replacement_price": r.replacement_price, "savings": r.savings, "n_options": r.n_options,
+            "n_pods": r.n_pods}
