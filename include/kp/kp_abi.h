@@ -399,6 +399,18 @@ typedef struct kp_sim_result {
 int32_t kp_simulate_batch(kp_ctx* ctx, const kp_cluster* cluster, const uint32_t* offsets, const uint32_t* nodes,
                           uint32_t n_subsets, int32_t multi_node, kp_sim_result* out, kp_solve_stats* stats);
 
+/* Same, split so that one cluster snapshot serves many batches (the disruption loop re-probes one
+ * snapshot: SingleNodeConsolidation, MultiNodeConsolidation's binary search, the sweep). prepare
+ * compiles and uploads the snapshot and precomputes, per pod shape, the existing nodes it can ever use
+ * and its NodeClaimTemplate outcome; simulate runs one batch of subsets on the resident snapshot.
+ * Returns KP_E_UNSUPPORTED (the Go path then runs) for: NodePool limits, topology spread, a pod
+ * NotIn/DoesNotExist requirement on a label key some node lacks, > 65535 pods in one subset. */
+typedef struct kp_cluster_plan kp_cluster_plan;
+int32_t kp_cluster_prepare(kp_ctx* ctx, const kp_cluster* cluster, kp_cluster_plan** out);
+int32_t kp_cluster_simulate(kp_cluster_plan* plan, const uint32_t* offsets, const uint32_t* nodes, uint32_t n_subsets,
+                            int32_t multi_node, kp_sim_result* out, kp_solve_stats* stats);
+void kp_cluster_plan_destroy(kp_cluster_plan* plan);
+
 #ifdef __cplusplus
 }
 #endif

@@ -101,6 +101,101 @@ struct FeasArgs {
   double* out_cheapest;      // [Q][T] or null
 };
 
+// ---- consolidation simulations (kp_cluster_simulate) -------------------------------------------
+// One in-flight NodeClaim (a simulation with a second one is a no-op, so it stops there).
+struct SimNC {
+  KReqs reqs;
+  uint64_t X[KP_MAX_TYPE_WORDS];
+  int64_t requests[KP_NRES];
+  int64_t maxalloc[KP_NRES];
+  int32_t fitj[KP_NRES];
+  int32_t tmpl, taintset, ver, pad_;
+};
+
+// kp_sim_result as the device writes it (same layout as the ABI struct)
+struct SimOut {
+  int32_t decision;
+  uint32_t nodepool;
+  double candidate_price, replacement_price, savings;
+  uint32_t n_options, n_pods;
+};
+
+struct SimArgs {
+  const DevDict* dict;
+  const DevCatalog* cats;
+  int32_t n_catalogs;
+  int32_t SL;                        // shape-levels
+  const int64_t* vint;
+  // shapes (x relaxation levels), as in SolveArgs
+  const int32_t* shape_level_base;
+  const int32_t* shape_nlevels;
+  const int32_t* sl_shape;           // [SL] shape of a shape-level
+  const uint8_t* shape_reqs;
+  const uint64_t* shape_negop;
+  const int64_t* shape_requests;
+  const uint64_t* shape_tolerates;
+  const uint64_t* shape_pvp;
+  const int32_t* pvp_base;
+  const int32_t* pvp_slot;
+  // templates
+  int32_t n_tmpl;
+  const uint8_t* tmpl_reqs;
+  const int32_t* tmpl_taintset;
+  const int32_t* tmpl_catalog;
+  const int32_t* tmpl_nodepool;
+  const uint64_t* tmpl_X;
+  const int64_t* tmpl_daemon;
+  // existing nodes in upstream order (initialized first, then name); position e
+  int32_t E, EW;
+  const uint16_t* ex_code;           // [K][E] value bit of the node's label for key k, 0xFFFF: no label
+  const int32_t* ex_taintset;        // [E]
+  const int64_t* ex_available;       // [E][NRES]
+  const int64_t* ex_requests;        // [E][NRES]
+  const uint8_t* ex_init;            // [E]
+  // precomputed per shape-level (sim_prep_kernel / sim_usable_kernel)
+  uint64_t* usable;                  // [SL][EW] CanAdd on the snapshot: tolerated, compatible, fits
+  SimNC* tres;                       // [SL] addToNewNodeClaim outcome (tmpl -1: none)
+  // pods (all pods of the cluster)
+  const int32_t* pod_shape;          // [P]
+  const uint32_t* pod_rank;          // [P] position in byCPUAndMemoryDescending order
+  const uint32_t* rank_pod;          // [P]
+  // cluster nodes, input order
+  const int32_t* node_pos;           // [N] existing position
+  const uint32_t* node_pod_off;      // [N+1]
+  const uint32_t* node_pods;
+  const double* node_price;          // [N] cheapest label-compatible offering of its type
+  const uint8_t* node_flags;         // [N] bit0 priced, bit1 capacity-type label = spot
+  const uint32_t* node_name;         // [N] type-name id
+  const uint32_t* type_name;         // [n_catalogs][T] type-name id
+  int32_t spot_bit, od_bit, ct_key;
+  uint32_t req_res_mask;
+  int32_t RU;                        // requested resources (popcount of req_res_mask)
+  int8_t ru_res[KP_NRES];            // resource of overlay column u
+  int32_t max_types;
+  int32_t multi_node;
+  int32_t wave_lds;                  // dynamic LDS bytes per wave (bitmaps + pod queue / option sort)
+  // batch
+  int32_t n_subsets;
+  const uint32_t* sub_off;
+  const uint32_t* sub_nodes;
+  int32_t cap;                       // pods per simulation the LDS region holds
+  int32_t cap2;                      // power of two >= max(cap, 2 * sorted types)
+  // per-wave scratch (slot = global wave id)
+  int32_t n_slots;
+  uint64_t* s_pod;                   // [slot][cap] epoch<<40 | level<<32 | lastLen
+  int32_t* s_start;                  // [slot][SL] first existing position not yet known to fail
+  int64_t* s_ovl;                    // [slot][E][RU] requests of existing nodes touched by the simulation
+  SimNC* s_nc;                       // [slot]
+  int32_t* s_ncfail;                 // [slot][SL]
+  SimOut* out;                       // [n_subsets]
+  uint64_t* stats;                   // [8] attempts, bytes, pops, existing words scanned
+};
+
+hipError_t launch_sim_prep(const SimArgs& a, hipStream_t s);
+hipError_t launch_sim(const SimArgs& a, int blocks, size_t dyn_lds, hipStream_t s);
+const void* sim_kernel_ptr();
+#define SIM_WAVES 4
+
 hipError_t launch_solve(const SolveArgs& a, int nw, size_t dyn_lds, hipStream_t s);
 hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s);
 hipError_t launch_feasibility(const FeasArgs& a, hipStream_t s);

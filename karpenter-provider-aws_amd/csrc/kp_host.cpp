@@ -1644,10 +1644,406 @@ int32_t kp_filter_compatible_available(kp_ctx* ctx, const kp_catalog* cat, const
   return KP_OK;
 }
 
+// ---- consolidation: cluster snapshot + batched simulations -----------------------------------------
+}  // extern "C"
+
+struct kp_cluster_plan {
+  kp_ctx* ctx = nullptr;
+  std::unique_ptr<Compiled> cp;
+  DevBuf buf;                       // resident snapshot
+  DevBuf scratch;                   // per-wave state, grown on demand
+  size_t scratch_bytes = 0;
+  DevBuf batch;                     // subsets + results, grown on demand
+  size_t batch_bytes = 0;
+  SimArgs a;
+  int N = 0, T2 = 1, n_cu = 256;
+  vector<uint32_t> node_npods;
+  double prepare_ms = 0;
+};
+
+namespace {
+static_assert(sizeof(SimOut) == sizeof(kp_sim_result), "SimOut mirrors kp_sim_result");
+
+// Offerings.Compatible(NewLabelRequirements(node labels)).Cheapest().Price: an offering's capacity-type /
+// zone / zone-id requirement (all well-known) is compatible unless the node carries that label with a
+// different value.
+bool NodeCandidatePrice(const HostType& t, const std::map<string, string>& labels, double* price) {
+  bool any = false;
+  double p = 0;
+  auto clash = [&](const char* key, bool has, const string& v) {
+    if (!has) return false;
+    auto f = labels.find(key);
+    return f != labels.end() && f->second != v;
+  };
+  for (auto& o : t.offs) {
+    if (clash(kCapType, true, o.ct) || clash(kZone, o.has_zone, o.zone) || clash(kZoneID, o.has_zid, o.zid)) continue;
+    if (!any || o.price < p) p = o.price;
+    any = true;
+  }
+  *price = p;
+  return any;
+}
+}  // namespace
+
+extern "C" {
+
+int32_t kp_cluster_prepare(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan** out) {
+  auto t0 = std::chrono::steady_clock::now();
+  if (!ctx || !cl || !out) return fail(KP_E_INVAL, "null argument");
+  if (cl->spot_to_spot) return fail(KP_E_UNSUPPORTED, "SpotToSpotConsolidation feature gate");
+  if (cl->n_nodes && !cl->nodes) return fail(KP_E_INVAL, "null nodes");
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device));
+  auto plan = std::make_unique<kp_cluster_plan>();
+  plan->ctx = ctx;
+  plan->cp = std::make_unique<Compiled>();
+  Compiled& C = *plan->cp;
+  const int N = (int)cl->n_nodes;
+  plan->N = N;
+  vector<kp_existing_node> ex(N);
+  for (int i = 0; i < N; i++) ex[i] = cl->nodes[i].node;
+  kp_solve_in in;
+  memset(&in, 0, sizeof in);
+  in.catalogs = cl->catalogs;
+  in.n_catalogs = cl->n_catalogs;
+  in.n_nodepools = cl->n_nodepools;
+  in.nodepools = cl->nodepools;
+  in.existing = ex.data();
+  in.n_existing = (uint32_t)N;
+  in.n_shapes = cl->n_shapes;
+  in.shapes = cl->shapes;
+  in.pods = cl->pods;
+  in.n_pods = cl->n_pods;
+  in.max_instance_types = 100;
+  int32_t rc = CompileSolve(&in, C);
+  if (rc) return rc;
+  const Dict& d = C.d;
+  const int TW = C.TW, E = N, EW = (E + 63) / 64, SL = (int)C.shape_reqs.size(), NT = (int)C.tmpl_reqs.size();
+  const int T = d.dd.T, K = d.dd.K;
+  for (uint32_t lp : C.tmpl_limit_present)
+    if (lp) return fail(KP_E_UNSUPPORTED, "NodePool limits in consolidation simulations");
+  // a pod NotIn/DoesNotExist on a key some node lacks would add that key to the node's requirements
+  uint64_t all_nodes_keys = ~0ull;
+  for (auto& q : C.ex_reqs) all_nodes_keys &= q.present;
+  for (int sl = 0; sl < SL; sl++)
+    if (C.shape_negop[sl] & ~all_nodes_keys)
+      return fail(KP_E_UNSUPPORTED, "pod NotIn/DoesNotExist requirement on a label some node lacks");
+  // existing nodes: label value bit per key (node labels are single-valued In requirements)
+  vector<uint16_t> ex_code((size_t)std::max(K, 1) * std::max(E, 1), 0xFFFF);
+  vector<uint8_t> ex_init(std::max(E, 1), 0);
+  vector<int32_t> node_pos(std::max(N, 1), 0);
+  for (int e = 0; e < E; e++) {
+    const KReqs& q = C.ex_reqs[e];
+    node_pos[C.ex_input[e]] = e;
+    ex_init[e] = cl->nodes[C.ex_input[e]].node.initialized ? 1 : 0;
+    for (int k = 0; k < K; k++) {
+      if (!((q.present >> k) & 1)) continue;
+      for (int wi = 0; wi < nwords(d, k); wi++) {
+        const int w = kw(d, k, wi);
+        if (q.vals[w]) {
+          ex_code[(size_t)k * E + e] = (uint16_t)(w * 64 + __builtin_ctzll(q.vals[w]));
+          break;
+        }
+      }
+    }
+  }
+  // pods: global queue rank
+  const uint32_t P = cl->n_pods;
+  vector<uint32_t> rank(std::max<uint32_t>(P, 1)), rank_pod(std::max<uint32_t>(P, 1));
+  for (uint32_t i = 0; i < P; i++) {
+    rank[C.queue[i]] = i;
+    rank_pod[i] = (uint32_t)C.queue[i];
+  }
+  // cluster nodes: pods (CSR), candidate price, flags, type-name ids
+  std::unordered_map<string, uint32_t> names;
+  auto name_id = [&](const string& s) {
+    auto it = names.find(s);
+    if (it != names.end()) return it->second;
+    const uint32_t id = (uint32_t)names.size();
+    names[s] = id;
+    return id;
+  };
+  vector<uint32_t> node_off(N + 1, 0), node_pods;
+  vector<double> node_price(std::max(N, 1), 0);
+  vector<uint8_t> node_flags(std::max(N, 1), 0);
+  vector<uint32_t> node_name(std::max(N, 1), 0);
+  plan->node_npods.resize(N);
+  for (int i = 0; i < N; i++) {
+    const kp_cluster_node& n = cl->nodes[i];
+    if (n.catalog >= cl->n_catalogs || !cl->catalogs[n.catalog]) return fail(KP_E_INVAL, "node %d: catalogue %u", i, n.catalog);
+    const kp_catalog* cat = cl->catalogs[n.catalog];
+    if (n.instance_type >= cat->types.size()) return fail(KP_E_INVAL, "node %d: instance type %u", i, n.instance_type);
+    if (n.n_pods && !n.pods) return fail(KP_E_INVAL, "node %d: null pods", i);
+    for (uint32_t j = 0; j < n.n_pods; j++) {
+      if (n.pods[j] >= P) return fail(KP_E_INVAL, "node %d: pod %u", i, n.pods[j]);
+      node_pods.push_back(n.pods[j]);
+    }
+    node_off[i + 1] = (uint32_t)node_pods.size();
+    plan->node_npods[i] = n.n_pods;
+    std::map<string, string> labels;
+    for (uint32_t j = 0; j < n.node.n_labels; j++)
+      labels[Normalize(n.node.labels[j].key ? n.node.labels[j].key : "")] = n.node.labels[j].value ? n.node.labels[j].value : "";
+    const HostType& ht = cat->types[n.instance_type];
+    double pr = 0;
+    const bool priced = NodeCandidatePrice(ht, labels, &pr);
+    node_price[i] = pr;
+    auto ct = labels.find(kCapType);
+    node_flags[i] = (priced ? 1 : 0) | (ct != labels.end() && ct->second == "spot" ? 2 : 0);
+    node_name[i] = name_id(ht.name);
+  }
+  if (node_pods.empty()) node_pods.push_back(0);
+  vector<uint32_t> type_name((size_t)cl->n_catalogs * std::max(T, 1), 0xFFFFFFFFu);
+  for (uint32_t c = 0; c < cl->n_catalogs; c++)
+    for (size_t t = 0; t < cl->catalogs[c]->types.size(); t++)
+      type_name[(size_t)c * T + t] = name_id(cl->catalogs[c]->types[t].name);
+  vector<int32_t> sl_shape(std::max(SL, 1), 0);
+  for (uint32_t s = 0; s < cl->n_shapes; s++)
+    for (int l = 0; l < C.shape_nlevels[s]; l++) sl_shape[C.shape_level_base[s] + l] = (int32_t)s;
+  const int ctk = d.key(kCapType);
+
+  Blob blob;
+  const size_t o_dict = blob.put(&C.d.dd, 1);
+  const size_t o_vint = blob.put(C.d.vint);
+  vector<CatOffsets> coffs;
+  PutCatalogs(blob, C, coffs);
+  const size_t o_cats = blob.reserve(sizeof(DevCatalog) * coffs.size());
+  const size_t o_slb = blob.put(C.shape_level_base);
+  const size_t o_snl = blob.put(C.shape_nlevels);
+  const size_t o_sls = blob.put(sl_shape);
+  const size_t o_sreqs = blob.put(C.shape_reqs);
+  const size_t o_sneg = blob.put(C.shape_negop);
+  const size_t o_sreq = blob.put(C.shape_requests);
+  const size_t o_stol = blob.put(C.shape_tolerates);
+  const size_t o_pvp = blob.put(C.pvp);
+  const size_t o_pvpb = blob.put(C.pvp_base);
+  const size_t o_pvps = blob.put(C.pvp_slot);
+  vector<int32_t> tmpl_np(C.tmpl_nodepool.begin(), C.tmpl_nodepool.end());
+  if (tmpl_np.empty()) tmpl_np.push_back(0);
+  const size_t o_treqs = blob.put(C.tmpl_reqs);
+  const size_t o_tts = blob.put(C.tmpl_taintset);
+  const size_t o_tcat = blob.put(C.tmpl_catalog);
+  const size_t o_tnp = blob.put(tmpl_np);
+  const size_t o_tX = blob.put(C.tmpl_X);
+  const size_t o_tdm = blob.put(C.tmpl_daemon);
+  const size_t o_excode = blob.put(ex_code);
+  const size_t o_exts = blob.put(C.ex_taintset);
+  const size_t o_exav = blob.put(C.ex_available);
+  const size_t o_exrq = blob.put(C.ex_requests);
+  const size_t o_exin = blob.put(ex_init);
+  const size_t o_pshape = blob.put(C.pod_shape);
+  const size_t o_prank = blob.put(rank);
+  const size_t o_rpod = blob.put(rank_pod);
+  const size_t o_npos = blob.put(node_pos);
+  const size_t o_noff = blob.put(node_off);
+  const size_t o_npods = blob.put(node_pods);
+  const size_t o_nprice = blob.put(node_price);
+  const size_t o_nflags = blob.put(node_flags);
+  const size_t o_nname = blob.put(node_name);
+  const size_t o_tname = blob.put(type_name);
+  const size_t host_bytes = blob.host.size();
+  const size_t o_usable = blob.reserve(sizeof(uint64_t) * (size_t)std::max(SL, 1) * std::max(EW, 1));
+  const size_t o_tres = blob.reserve(sizeof(SimNC) * (size_t)std::max(SL, 1));
+  HIPCHK(hipMalloc(&plan->buf.p, blob.host.size()));
+  uint8_t* base = (uint8_t*)plan->buf.p;
+  {
+    vector<DevCatalog> dc = DevCats(base, C, coffs);
+    memcpy(blob.host.data() + o_cats, dc.data(), sizeof(DevCatalog) * dc.size());
+  }
+  HIPCHK(hipMemcpyAsync(base, blob.host.data(), host_bytes, hipMemcpyHostToDevice, ctx->stream));
+
+  SimArgs& a = plan->a;
+  memset(&a, 0, sizeof a);
+  a.dict = (const DevDict*)(base + o_dict);
+  a.cats = (const DevCatalog*)(base + o_cats);
+  a.n_catalogs = (int32_t)coffs.size();
+  a.SL = SL;
+  a.vint = (const int64_t*)(base + o_vint);
+  a.shape_level_base = (const int32_t*)(base + o_slb);
+  a.shape_nlevels = (const int32_t*)(base + o_snl);
+  a.sl_shape = (const int32_t*)(base + o_sls);
+  a.shape_reqs = base + o_sreqs;
+  a.shape_negop = (const uint64_t*)(base + o_sneg);
+  a.shape_requests = (const int64_t*)(base + o_sreq);
+  a.shape_tolerates = (const uint64_t*)(base + o_stol);
+  a.shape_pvp = (const uint64_t*)(base + o_pvp);
+  a.pvp_base = (const int32_t*)(base + o_pvpb);
+  a.pvp_slot = (const int32_t*)(base + o_pvps);
+  a.n_tmpl = NT;
+  a.tmpl_reqs = base + o_treqs;
+  a.tmpl_taintset = (const int32_t*)(base + o_tts);
+  a.tmpl_catalog = (const int32_t*)(base + o_tcat);
+  a.tmpl_nodepool = (const int32_t*)(base + o_tnp);
+  a.tmpl_X = (const uint64_t*)(base + o_tX);
+  a.tmpl_daemon = (const int64_t*)(base + o_tdm);
+  a.E = E;
+  a.EW = EW;
+  a.ex_code = (const uint16_t*)(base + o_excode);
+  a.ex_taintset = (const int32_t*)(base + o_exts);
+  a.ex_available = (const int64_t*)(base + o_exav);
+  a.ex_requests = (const int64_t*)(base + o_exrq);
+  a.ex_init = base + o_exin;
+  a.usable = (uint64_t*)(base + o_usable);
+  a.tres = (SimNC*)(base + o_tres);
+  a.pod_shape = (const int32_t*)(base + o_pshape);
+  a.pod_rank = (const uint32_t*)(base + o_prank);
+  a.rank_pod = (const uint32_t*)(base + o_rpod);
+  a.node_pos = (const int32_t*)(base + o_npos);
+  a.node_pod_off = (const uint32_t*)(base + o_noff);
+  a.node_pods = (const uint32_t*)(base + o_npods);
+  a.node_price = (const double*)(base + o_nprice);
+  a.node_flags = base + o_nflags;
+  a.node_name = (const uint32_t*)(base + o_nname);
+  a.type_name = (const uint32_t*)(base + o_tname);
+  a.ct_key = ctk;
+  a.spot_bit = ctk >= 0 ? d.bit(ctk, "spot") : -1;
+  a.od_bit = ctk >= 0 ? d.bit(ctk, "on-demand") : -1;
+  a.req_res_mask = 0;
+  for (size_t i = 0; i < C.shape_requests.size(); i++)
+    if (C.shape_requests[i] > 0) a.req_res_mask |= 1u << (i % KP_NRES);
+  for (size_t i = 0; i < C.tmpl_daemon.size(); i++)
+    if (C.tmpl_daemon[i] > 0) a.req_res_mask |= 1u << (i % KP_NRES);
+  a.RU = 0;
+  for (int r = 0; r < KP_NRES; r++)
+    if ((a.req_res_mask >> r) & 1) a.ru_res[a.RU++] = (int8_t)r;
+  a.max_types = 100;
+  (void)TW;
+  plan->T2 = 1;
+  while (plan->T2 < std::max(T, 1)) plan->T2 <<= 1;
+  int ncu = 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device) == hipSuccess && ncu > 0)
+    plan->n_cu = ncu;
+  HIPCHK(launch_sim_prep(a, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  plan->prepare_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  *out = plan.release();
+  return KP_OK;
+}
+
+void kp_cluster_plan_destroy(kp_cluster_plan* p) {
+  if (!p) return;
+  (void)hipSetDevice(p->ctx->device);
+  delete p;
+}
+
+int32_t kp_cluster_simulate(kp_cluster_plan* plan, const uint32_t* offsets, const uint32_t* nodes, uint32_t n_subsets,
+                            int32_t multi_node, kp_sim_result* out, kp_solve_stats* stats) {
+  auto t0 = std::chrono::steady_clock::now();
+  if (!plan || (n_subsets && (!offsets || !out))) return fail(KP_E_INVAL, "null argument");
+  kp_ctx* ctx = plan->ctx;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device));
+  if (stats) memset(stats, 0, sizeof *stats);
+  if (n_subsets == 0) return KP_OK;
+  if (offsets[0] != 0) return fail(KP_E_INVAL, "offsets[0] != 0");
+  const uint32_t n_flat = offsets[n_subsets];
+  if (n_flat && !nodes) return fail(KP_E_INVAL, "null nodes");
+  int cap = 1;
+  for (uint32_t s = 0; s < n_subsets; s++) {
+    if (offsets[s + 1] < offsets[s]) return fail(KP_E_INVAL, "offsets not monotone at %u", s);
+    uint64_t np = 0;
+    for (uint32_t j = offsets[s]; j < offsets[s + 1]; j++) {
+      if (nodes[j] >= (uint32_t)plan->N) return fail(KP_E_INVAL, "subset %u: node %u", s, nodes[j]);
+      np += plan->node_npods[nodes[j]];
+    }
+    if (np > 65535) return fail(KP_E_UNSUPPORTED, "subset %u reschedules %llu pods (max 65535)", s, (unsigned long long)np);
+    cap = std::max(cap, (int)np);
+  }
+  SimArgs a = plan->a;
+  int cap2 = 1;
+  while (cap2 < std::max(cap, 2 * plan->T2)) cap2 <<= 1;
+  a.cap = cap;
+  a.cap2 = cap2;
+  a.wave_lds = (int)(((size_t)16 * a.EW + (size_t)6 * cap2 + 15) & ~(size_t)15);
+  a.multi_node = multi_node ? 1 : 0;
+  hipFuncAttributes fa;
+  HIPCHK(hipFuncGetAttributes(&fa, sim_kernel_ptr()));
+  const size_t lds_wg = fa.sharedSizeBytes + (size_t)SIM_WAVES * a.wave_lds;
+  if (lds_wg > 160 * 1024) return fail(KP_E_UNSUPPORTED, "simulation LDS %zu B per workgroup (cluster or subsets too large)", lds_wg);
+  const int wg_per_cu = (int)std::max<size_t>(1, std::min<size_t>(8, (160 * 1024) / lds_wg));
+  int blocks = std::min<int>((int)((n_subsets + SIM_WAVES - 1) / SIM_WAVES), plan->n_cu * wg_per_cu);
+  blocks = std::max(blocks, 1);
+  const int slots = blocks * SIM_WAVES;
+  a.n_slots = slots;
+  a.n_subsets = (int32_t)n_subsets;
+  // per-wave scratch
+  const size_t sz_pod = sizeof(uint64_t) * (size_t)slots * cap;
+  const size_t sz_start = sizeof(int32_t) * (size_t)slots * std::max(a.SL, 1);
+  const size_t sz_ovl = sizeof(int64_t) * (size_t)slots * std::max(a.E, 1) * std::max(a.RU, 1);
+  const size_t sz_nc = sizeof(SimNC) * (size_t)slots;
+  const size_t sz_fail = sizeof(int32_t) * (size_t)slots * std::max(a.SL, 1);
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t need = al(sz_pod) + al(sz_start) + al(sz_ovl) + al(sz_nc) + al(sz_fail) + al(sizeof(uint64_t) * 8);
+  if (need > plan->scratch_bytes) {
+    if (plan->scratch.p) HIPCHK(hipFree(plan->scratch.p));
+    plan->scratch.p = nullptr;
+    HIPCHK(hipMalloc(&plan->scratch.p, need));
+    plan->scratch_bytes = need;
+  }
+  uint8_t* sb = (uint8_t*)plan->scratch.p;
+  size_t o = 0;
+  a.s_pod = (uint64_t*)(sb + o);
+  o += al(sz_pod);
+  a.s_start = (int32_t*)(sb + o);
+  o += al(sz_start);
+  a.s_ovl = (int64_t*)(sb + o);
+  o += al(sz_ovl);
+  a.s_nc = (SimNC*)(sb + o);
+  o += al(sz_nc);
+  a.s_ncfail = (int32_t*)(sb + o);
+  o += al(sz_fail);
+  a.stats = (uint64_t*)(sb + o);
+  // batch: subsets + results
+  const size_t b_off = al(sizeof(uint32_t) * (n_subsets + 1)), b_nodes = al(sizeof(uint32_t) * std::max<uint32_t>(n_flat, 1));
+  const size_t b_out = al(sizeof(SimOut) * n_subsets);
+  if (b_off + b_nodes + b_out > plan->batch_bytes) {
+    if (plan->batch.p) HIPCHK(hipFree(plan->batch.p));
+    plan->batch.p = nullptr;
+    HIPCHK(hipMalloc(&plan->batch.p, b_off + b_nodes + b_out));
+    plan->batch_bytes = b_off + b_nodes + b_out;
+  }
+  uint8_t* bb = (uint8_t*)plan->batch.p;
+  a.sub_off = (const uint32_t*)bb;
+  a.sub_nodes = (const uint32_t*)(bb + b_off);
+  a.out = (SimOut*)(bb + b_off + b_nodes);
+  hipStream_t st = ctx->stream;
+  HIPCHK(hipMemcpyAsync(bb, offsets, sizeof(uint32_t) * (n_subsets + 1), hipMemcpyHostToDevice, st));
+  if (n_flat) HIPCHK(hipMemcpyAsync(bb + b_off, nodes, sizeof(uint32_t) * n_flat, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemsetAsync(a.s_ncfail, 0xFF, sz_fail, st));
+  HIPCHK(hipMemsetAsync(a.stats, 0, sizeof(uint64_t) * 8, st));
+  HIPCHK(hipEventRecord(ctx->ev0, st));
+  HIPCHK(launch_sim(a, blocks, (size_t)SIM_WAVES * a.wave_lds, st));
+  HIPCHK(hipEventRecord(ctx->ev1, st));
+  uint64_t kst[8];
+  HIPCHK(hipMemcpyAsync(out, a.out, sizeof(SimOut) * n_subsets, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(kst, a.stats, sizeof kst, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+  for (uint32_t s = 0; s < n_subsets; s++)
+    if (out[s].n_pods == 0xFFFFFFFFu) return fail(KP_E_DEVICE, "subset %u overflowed the pod queue", s);
+  if (stats) {
+    stats->device_ms = ms;
+    stats->solve_kernel_ms = ms;
+    stats->attempts = kst[0];
+    stats->bytes_algorithmic = kst[1];
+    stats->pops = kst[2];
+    stats->phase_cycles[0] = kst[3];
+    stats->prepare_ms = plan->prepare_ms;
+    stats->host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
+  return KP_OK;
+}
+
 int32_t kp_simulate_batch(kp_ctx* ctx, const kp_cluster* cl, const uint32_t* offsets, const uint32_t* nodes,
                           uint32_t n_subsets, int32_t multi_node, kp_sim_result* out, kp_solve_stats* stats) {
-  (void)ctx; (void)cl; (void)offsets; (void)nodes; (void)n_subsets; (void)multi_node; (void)out; (void)stats;
-  return fail(KP_E_UNSUPPORTED, "kp_simulate_batch: not built yet");
+  kp_cluster_plan* plan = nullptr;
+  int32_t rc = kp_cluster_prepare(ctx, cl, &plan);
+  if (rc) return rc;
+  const double prep = plan->prepare_ms;
+  rc = kp_cluster_simulate(plan, offsets, nodes, n_subsets, multi_node, out, stats);
+  if (stats) stats->prepare_ms = prep;
+  kp_cluster_plan_destroy(plan);
+  return rc;
 }
 
 }  // extern "C"

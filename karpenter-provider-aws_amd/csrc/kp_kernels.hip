@@ -243,6 +243,54 @@ __device__ int wave_lower_bound(const int64_t* vals, int n, int64_t q, uint64_t*
   return lo;
 }
 
+// minValues over a type set (SatisfiesMinValues): for every key in `mk`, the remaining types (X: this lane's
+// word) must carry at least minv[k] distinct values of it.
+__device__ bool minvalues_ok(const DevDict& D, const DevCatalog& Cg, uint64_t mk, const int32_t* minv, uint64_t X,
+                             uint32_t* scratch) {
+  const int lane = LANE;
+  const int TW = D.TW;
+  bool ok = true;
+  while (mk) {
+    const int k = __builtin_ctzll(mk);
+    mk &= mk - 1;
+    const int nw = (D.nval[k] + 63) >> 6;
+    int count = 0;
+    if ((D.single_valued >> k) & 1) {
+      for (int w = lane; w < 2 * nw; w += 64) scratch[w] = 0;
+      wave_sync();
+      uint64_t m = lane < TW ? X : 0;
+      while (m) {
+        const int b = __builtin_ctzll(m);
+        m &= m - 1;
+        const uint16_t code = Cg.code[(size_t)k * D.T + lane * 64 + b];
+        if (code < 0xFFFD) {
+          const int cw = code >> 6;
+          const int rel = (cw == k ? 0 : (cw - D.ovf[k] + 1) * 64) + (code & 63);  // ordinal within key k
+          atomicOr(&scratch[rel >> 5], 1u << (rel & 31));
+        }
+      }
+      wave_sync();
+      int c = 0;
+      for (int w = lane; w < 2 * nw; w += 64) c += __builtin_popcount(scratch[w]);
+      count = wave_sum(c);
+      wave_sync();
+    } else {
+      for (int wi = 0; wi < nw; wi++) {
+        const int w = key_word(D, k, wi);
+        uint64_t vb = D.validbits[w];
+        while (vb) {
+          const int b = __builtin_ctzll(vb);
+          vb &= vb - 1;
+          const uint64_t hit = lane < TW ? (X & Cg.TM[(size_t)(w * 64 + b) * TW + lane]) : 0;
+          count += __ballot(hit != 0) ? 1 : 0;
+        }
+      }
+    }
+    if (count < minv[k]) ok = false;
+  }
+  return ok;
+}
+
 // NodeClaim.Add's instance-type filter after a successful merge. X: this lane's word of the candidate's
 // remaining types (invariant: X already passes every key the pod did not touch). Returns the new word.
 __device__ uint64_t filter_types(const DevDict& D, const DevCatalog& Cg, const ReqView& rv, uint64_t m_v, uint64_t X,
@@ -327,45 +375,7 @@ __device__ uint64_t filter_types(const DevDict& D, const DevCatalog& Cg, const R
     X &= offer;
   }
   // 4) minValues (relaxMinValues = false): distinct values of each minValues key over remaining types
-  uint64_t mk = rv.hmin & rv.present;
-  while (mk) {
-    const int k = __builtin_ctzll(mk);
-    mk &= mk - 1;
-    const int nw = (D.nval[k] + 63) >> 6;
-    int count = 0;
-    if ((D.single_valued >> k) & 1) {
-      for (int w = lane; w < 2 * nw; w += 64) scratch[w] = 0;
-      wave_sync();
-      uint64_t m = lane < TW ? X : 0;
-      while (m) {
-        const int b = __builtin_ctzll(m);
-        m &= m - 1;
-        const uint16_t code = Cg.code[(size_t)k * D.T + lane * 64 + b];
-        if (code < 0xFFFD) {
-          const int cw = code >> 6;
-          const int rel = (cw == k ? 0 : (cw - D.ovf[k] + 1) * 64) + (code & 63);  // ordinal within key k
-          atomicOr(&scratch[rel >> 5], 1u << (rel & 31));
-        }
-      }
-      wave_sync();
-      int c = 0;
-      for (int w = lane; w < 2 * nw; w += 64) c += __builtin_popcount(scratch[w]);
-      count = wave_sum(c);
-      wave_sync();
-    } else {
-      for (int wi = 0; wi < nw; wi++) {
-        const int w = key_word(D, k, wi);
-        uint64_t vb = D.validbits[w];
-        while (vb) {
-          const int b = __builtin_ctzll(vb);
-          vb &= vb - 1;
-          const uint64_t hit = lane < TW ? (X & Cg.TM[(size_t)(w * 64 + b) * TW + lane]) : 0;
-          count += __ballot(hit != 0) ? 1 : 0;
-        }
-      }
-    }
-    if (count < rv.minv[k]) X = 0;
-  }
+  if (!minvalues_ok(D, Cg, rv.hmin & rv.present, rv.minv, X, scratch)) X = 0;
   *bytes += nb;
   return X;
 }
@@ -1085,6 +1095,8 @@ __global__ __launch_bounds__(FEAS_WAVES * 64) void feasibility_kernel(FeasArgs a
     wave_sync();
   }
 }
+
+#include "kp_sim.hip"
 
 // ------------------------------------------------------------------------------------------------
 // launchers

@@ -4,6 +4,7 @@ The surfaces mirror the reference's plugin/operator interface for the path:
   CloudProvider.get_instance_types(nodepool)  <- R:pkg/cloudprovider/cloudprovider.go:177-193
   Scheduler(...).solve(pods)                  <- upstream scheduling.Scheduler.Solve
   compatible_available_filter(...)            <- R:pkg/providers/instance/filter/filter.go:39-64
+  ClusterPlan(...).simulate(subsets)          <- upstream disruption computeConsolidation / SimulateScheduling
 Everything computes behind the C ABI on the GPU; a missing libkp.so or HIP device raises.
 """
 import ctypes as C
@@ -55,6 +56,12 @@ def load_lib(path=LIB_PATH):
         "kp_result_nodeclaim": (C.c_int32, [C.c_void_p, C.c_uint32, P(abi.NodeClaimInfo)]),
         "kp_result_stats": (C.c_int32, [C.c_void_p, P(abi.SolveStats)]),
         "kp_result_destroy": (None, [C.c_void_p]),
+        "kp_simulate_batch": (C.c_int32, [C.c_void_p, P(abi.Cluster), P(C.c_uint32), P(C.c_uint32), C.c_uint32,
+                                          C.c_int32, P(abi.SimResult), P(abi.SolveStats)]),
+        "kp_cluster_prepare": (C.c_int32, [C.c_void_p, P(abi.Cluster), P(C.c_void_p)]),
+        "kp_cluster_simulate": (C.c_int32, [C.c_void_p, P(C.c_uint32), P(C.c_uint32), C.c_uint32, C.c_int32,
+                                            P(abi.SimResult), P(abi.SolveStats)]),
+        "kp_cluster_plan_destroy": (None, [C.c_void_p]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -224,3 +231,48 @@ def compatible_available_filter(ctx, catalog, queries):
                                                    cheapest.ctypes.data_as(C.POINTER(C.c_double)), C.byref(st)))
     bits = np.unpackbits(mask[:len(queries) * tiles].view(np.uint8), bitorder="little").reshape(len(queries), tiles * 64)
     return bits[:, :T].astype(bool), cheapest[:len(queries) * T].reshape(len(queries), T), st
+
+
+def sim_dict(r):
+    return {"decision": int(r.decision), "nodepool": int(r.replacement_nodepool), "candidate_price": r.candidate_price,
+            "replacement_price": r.replacement_price, "savings": r.savings, "n_options": int(r.n_options),
+            "n_pods": int(r.n_pods)}
+
+
+class ClusterPlan:
+    """Resident cluster snapshot for consolidation (kp_cluster_prepare); simulate() evaluates a batch of
+    candidate subsets as computeConsolidation would (kp_cluster_simulate)."""
+
+    def __init__(self, ctx, cluster, catalogs=None):
+        self.ctx = ctx
+        self.cluster = cluster
+        self.catalogs = catalogs or [Catalog(ctx, c) for c in cluster.catalogs]
+        arena = Arena()
+        cl = abi.build_cluster(arena, cluster, catalog_handles=[c.h.value for c in self.catalogs])
+        h = C.c_void_p()
+        _check(ctx.lib, ctx.lib.kp_cluster_prepare(ctx.h, C.byref(cl), C.byref(h)))
+        self.h = h
+
+    def simulate(self, subsets, multi_node=True, raw=False):
+        """subsets: list of node-index lists (candidate order). Returns (results, stats); raw=True returns
+        the kp_sim_result array instead of dicts."""
+        arena = Arena()
+        offs, flat = abi.subsets_csr(arena, subsets)
+        out = (abi.SimResult * max(1, len(subsets)))()
+        st = abi.SolveStats()
+        _check(self.ctx.lib, self.ctx.lib.kp_cluster_simulate(self.h, offs, flat, len(subsets), 1 if multi_node else 0,
+                                                              out, C.byref(st)))
+        if raw:
+            return out, stats_dict(st)
+        return [sim_dict(out[i]) for i in range(len(subsets))], stats_dict(st)
+
+    def close(self):
+        if self.h:
+            self.ctx.lib.kp_cluster_plan_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

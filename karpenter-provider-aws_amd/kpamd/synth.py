@@ -5,8 +5,8 @@ requests include pods=1 the way resources.RequestsForPods adds it.
 """
 import numpy as np
 
-from .catalog import ZONES
-from .model import ExistingNode, NodePool, PodShape, Problem
+from .catalog import ZONE_IDS, ZONES
+from .model import Cluster, ClusterNode, ExistingNode, NodePool, PodShape, Problem
 
 K = "karpenter.k8s.aws/"
 MI = 1 << 20
@@ -213,3 +213,190 @@ def random_problem(catalog, seed, n_types=120, n_pods=300, n_pools=3, n_existing
                                      bool(rng.random() < 0.9)))
     s, c, u = _pods(rng, n_pods, len(shapes))
     return Problem([cat], pools, shapes, s, c, u, existing=existing, name=f"random-{seed}")
+
+
+# ------------------------------------------------------------------------------------------------
+# config 4: a running cluster for multi-node consolidation (10k nodes, 8-40 pods per node)
+# ------------------------------------------------------------------------------------------------
+C4_CPU = [50, 100, 250, 500, 1000]
+C4_MEM = [64, 128, 256, 512, 1024, 2048]
+
+
+def node_labels(it, zone_i, capacity_type, nodepool, hostname):
+    """Labels a launched node carries: the type's single-valued requirements + offering + NodePool."""
+    labels = {r[0]: r[2][0] for r in it.requirements if r[1] == "In" and len(r[2]) == 1}
+    labels["topology.kubernetes.io/zone"] = ZONES[zone_i]
+    labels["topology.k8s.aws/zone-id"] = ZONE_IDS[zone_i]
+    labels["karpenter.sh/capacity-type"] = capacity_type
+    labels["karpenter.sh/nodepool"] = nodepool
+    labels["kubernetes.io/hostname"] = hostname
+    return labels
+
+
+def config4(catalog, n_nodes=10_000, seed=4, n_shapes=32, pods_min=8, pods_max=40, fill=(0.7, 0.98)):
+    """A cluster of n_nodes c/m/r nodes (2-16 vCPU, 3 AZ, 80% on-demand) running 8-40 pods each at
+    70-98% utilisation; 2 NodePools without limits. Candidates are sorted by disruption cost (fewer
+    pods first, then name: R:website/content/en/preview/concepts/disruption.md:101-103)."""
+    rng = np.random.default_rng(seed)
+    pools = [
+        NodePool("default", 10, 0, [("karpenter.sh/capacity-type", "In", ["on-demand", "spot"]),
+                                    (K + "instance-category", "In", ["c", "m", "r"]),
+                                    (K + "instance-generation", "Gt", ["4"])]),
+        NodePool("burst", 1, 0, [("karpenter.sh/capacity-type", "In", ["spot"]),
+                                 (K + "instance-category", "In", ["c", "m"])]),
+    ]
+
+    def req_val(it, key):
+        for r in it.requirements:
+            if r[0] == key and r[1] == "In" and len(r[2]) == 1:
+                return r[2][0]
+        return None
+
+    pool_types = []
+    for i, it in enumerate(catalog):
+        cat_ = req_val(it, K + "instance-category")
+        gen = req_val(it, K + "instance-generation")
+        cpu_n = int(req_val(it, K + "instance-cpu") or 0)
+        if cat_ in ("c", "m", "r") and gen and int(gen) > 4 and 2 <= cpu_n <= 16 \
+                and req_val(it, "kubernetes.io/arch") == "amd64" and any(o.available for o in it.offerings):
+            pool_types.append(i)
+    shapes = []
+    for i in range(n_shapes):
+        sh = PodShape(req_res(int(rng.choice(C4_CPU)), int(rng.choice(C4_MEM))))
+        if i % 8 == 7:
+            sh.node_selector = {"topology.kubernetes.io/zone": ZONES[(i // 8) % 3]}
+        elif i % 8 == 6:
+            sh.required_terms = [[("kubernetes.io/arch", "In", ["amd64"])]]
+        shapes.append(sh)
+    shape_zone = [ZONES.index(sh.node_selector["topology.kubernetes.io/zone"]) if sh.node_selector else -1
+                  for sh in shapes]
+    nodes = []
+    pod_shape, pod_creation, pod_uid = [], [], []
+    for n in range(n_nodes):
+        it = catalog[int(rng.choice(pool_types))]
+        zone_i = int(rng.integers(0, 3))
+        ct = "spot" if rng.random() < 0.2 else "on-demand"
+        name = f"node-{n:06d}"
+        labels = node_labels(it, zone_i, ct, "default", name)
+        alloc = it.allocatable()
+        frac = float(rng.uniform(*fill))
+        k = int(rng.integers(pods_min, pods_max + 1))
+        used = {"cpu": 0, "memory": 0, "pods": 0}
+        pods = []
+        for _ in range(4 * k):
+            if len(pods) >= k:
+                break
+            s_i = int(rng.integers(0, n_shapes))
+            if shape_zone[s_i] not in (-1, zone_i):
+                continue
+            rq = shapes[s_i].requests
+            if any(used[r] + rq[r] > frac * alloc[r] for r in used):
+                continue
+            for r in used:
+                used[r] += rq[r]
+            pods.append(len(pod_shape))
+            pod_shape.append(s_i)
+            pod_creation.append(1_750_000_000 + int(rng.integers(0, 86_400)))
+            pod_uid.append(int(rng.integers(0, np.iinfo(np.int64).max)))
+        avail = {r: alloc[r] - used[r] for r in used}
+        nodes.append(ClusterNode(ExistingNode(name, labels, avail, {}, [], True), 0, catalog.index(it), pods))
+    cands = sorted(range(n_nodes), key=lambda i: (len(nodes[i].pods), nodes[i].node.name))
+    return Cluster([catalog], pools, nodes, shapes, np.asarray(pod_shape, dtype=np.uint32),
+                   np.asarray(pod_creation, dtype=np.int64), np.asarray(pod_uid, dtype=np.uint64),
+                   candidates=cands, name=f"config4-{n_nodes}")
+
+
+def consolidation_subsets(cluster, n_random, seed=44, max_size=100, prefixes=True):
+    """MultiNodeConsolidation probes: every prefix candidates[0:k] (k = 2..100) and n_random random
+    subsets of 2..max_size candidates (each kept in candidate order)."""
+    rng = np.random.default_rng(seed)
+    c = cluster.candidates
+    out = [c[:k] for k in range(2, min(len(c), max_size) + 1)] if prefixes else []
+    pos = {n: i for i, n in enumerate(c)}
+    for _ in range(n_random):
+        k = int(rng.integers(2, min(len(c), max_size) + 1))
+        pick = rng.choice(len(c), size=k, replace=False)
+        out.append([c[i] for i in sorted(pick)])
+    del pos
+    return out
+
+
+def random_cluster(catalog, seed, n_nodes=60, n_types=80, n_shapes=16, n_pools=2):
+    """Randomized consolidation scenario: pools with taints / daemonsets / minValues, pods with selectors,
+    NotIn / Gt affinities and relaxable preferences on keys every node carries, spot and uninitialized
+    nodes."""
+    rng = np.random.default_rng(seed)
+    idx = np.sort(rng.choice(len(catalog), size=min(n_types, len(catalog)), replace=False))
+    cat = [catalog[i] for i in idx]
+    cat = [it for it in cat if any(o.available for o in it.offerings)
+           and any(r[0] == K + "instance-category" for r in it.requirements)]
+
+    def rand_req():
+        kind = rng.integers(0, 8)
+        if kind == 0:
+            return (K + "instance-category", "In", list(rng.choice(["c", "m", "r", "t"], size=2, replace=False)))
+        if kind == 1:
+            return (K + "instance-category", "NotIn", [str(rng.choice(["c", "m", "r", "t"]))])
+        if kind == 2:
+            return ("kubernetes.io/arch", "In", [str(rng.choice(["amd64", "arm64"]))])
+        if kind == 3:
+            return ("topology.kubernetes.io/zone", "NotIn", [str(rng.choice(ZONES))])
+        if kind == 4:
+            return ("karpenter.sh/capacity-type", "In", list(rng.choice(["spot", "on-demand"], size=int(rng.integers(1, 3)), replace=False)))
+        if kind == 5:
+            return (K + "instance-cpu", "Gt", [str(int(rng.choice([1, 2, 4])))])
+        if kind == 6:
+            return ("topology.kubernetes.io/zone", "In", list(rng.choice(ZONES, size=2, replace=False)))
+        return ("kubernetes.io/arch", "NotIn", ["arm64"])
+
+    pools = []
+    for i in range(n_pools):
+        reqs = [rand_req() for _ in range(int(rng.integers(0, 3)))]
+        if rng.random() < 0.2:
+            reqs.append((K + "instance-family", "Exists", [], int(rng.integers(2, 4))))
+        taints = [("dedicated", f"team{i}", "NoSchedule")] if rng.random() < 0.3 else []
+        daemon = {"cpu": int(rng.choice([0, 100, 250])), "memory": 64 * MI * 1000, "pods": 1000} if rng.random() < 0.5 else {}
+        pools.append(NodePool(f"pool-{i}", int(rng.integers(0, 4)), 0, reqs, taints=taints, daemon_requests=daemon))
+    shapes = []
+    for s in range(n_shapes):
+        sh = PodShape(req_res(int(rng.choice([50, 100, 250, 500, 1000])), int(rng.choice([64, 256, 512, 1024, 2048]))))
+        r = rng.random()
+        if r < 0.2:
+            sh.node_selector = {"topology.kubernetes.io/zone": str(rng.choice(ZONES))}
+        if rng.random() < 0.3:
+            sh.required_terms = [[rand_req()] for _ in range(int(rng.integers(1, 3)))]
+        if rng.random() < 0.2:
+            sh.preferred_terms = [(int(rng.integers(1, 100)), [rand_req()])]
+        if rng.random() < 0.3:
+            sh.tolerations = [("dedicated", "Exists", "", "NoSchedule")]
+        shapes.append(sh)
+    nodes, pod_shape, pod_creation, pod_uid = [], [], [], []
+    for n in range(n_nodes):
+        ti = int(rng.integers(0, len(cat)))
+        it = cat[ti]
+        zone_i = int(rng.integers(0, 3))
+        pool = pools[int(rng.integers(0, n_pools))]
+        name = f"node-{n:05d}"
+        labels = node_labels(it, zone_i, "spot" if rng.random() < 0.3 else "on-demand", pool.name, name)
+        alloc = it.allocatable()
+        frac = float(rng.uniform(0.3, 0.95))
+        used = {"cpu": 0, "memory": 0, "pods": 0}
+        pods = []
+        for _ in range(int(rng.integers(0, 30))):
+            s_i = int(rng.integers(0, n_shapes))
+            rq = shapes[s_i].requests
+            if any(used[r] + rq[r] > frac * alloc[r] for r in used):
+                continue
+            for r in used:
+                used[r] += rq[r]
+            pods.append(len(pod_shape))
+            pod_shape.append(s_i)
+            pod_creation.append(1_750_000_000 + int(rng.integers(0, 600)))
+            pod_uid.append(int(rng.integers(0, np.iinfo(np.int64).max)))
+        avail = {r: alloc[r] - used[r] for r in used}
+        nodes.append(ClusterNode(ExistingNode(name, labels, avail, {}, list(pool.taints), bool(rng.random() < 0.95)),
+                                 0, ti, pods))
+    cands = sorted(range(n_nodes), key=lambda i: (len(nodes[i].pods), nodes[i].node.name))
+    return Cluster([cat], pools, nodes, shapes, np.asarray(pod_shape, dtype=np.uint32),
+                   np.asarray(pod_creation, dtype=np.int64), np.asarray(pod_uid, dtype=np.uint64),
+                   candidates=cands, name=f"random-cluster-{seed}")
