@@ -34,6 +34,10 @@ def main():
     ap.add_argument("--pods", type=int, default=50_000)
     ap.add_argument("--cpu-sample-pods", type=int, default=10_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cluster-nodes", type=int, default=10_000)
+    ap.add_argument("--subsets", type=int, default=1_000_000)
+    ap.add_argument("--cpu-sample-sims", type=int, default=16)
+    ap.add_argument("--no-consolidation", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -123,12 +127,116 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = _cpu_baseline(cat, args.cpu_sample_pods)
+    if not args.no_consolidation:
+        line["consolidation"] = _consolidation(args, cat, ctx, dist, rank, world, barrier)
     if rank == 0:
         print(json.dumps(line), flush=True)
     plan.close()
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+CHUNK = 1 << 18  # subsets per kp_cluster_simulate call
+
+
+def _consolidation(args, cat, ctx, dist, rank, world, barrier):
+    """Config 4: multi-node consolidation sweep on a 10k-node cluster. The subsets (99 prefixes of the
+    disruption-cost order + random subsets of 2..100 candidates, generated in fixed chunks so the set
+    does not depend on N) are sharded over ranks by chunk; each rank simulates its chunks on its GPU,
+    keeps its best (savings desc, subset index asc), and one RCCL all-gather picks the global best."""
+    import numpy as np
+    import torch
+    import kpamd
+    from kpamd import disruption, synth
+
+    t0 = time.perf_counter()
+    cl = synth.config4(cat, n_nodes=args.cluster_nodes, seed=4)
+    cands = np.asarray(cl.candidates, dtype=np.uint32)
+    n_chunks = (args.subsets + CHUNK - 1) // CHUNK
+    mine = [c for c in range(n_chunks) if c % world == rank]
+    batches = []
+    if rank == 0:  # MultiNodeConsolidation's prefixes candidates[0:k], k = 2..100
+        pre = [cands[:k] for k in range(2, min(len(cands), 100) + 1)]
+        offs = np.zeros(len(pre) + 1, dtype=np.uint32)
+        offs[1:] = np.cumsum([len(p) for p in pre])
+        batches.append((-1, offs, np.concatenate(pre)))
+    for c in mine:
+        n = min(CHUNK, args.subsets - c * CHUNK)
+        offs, pos = disruption.random_subsets_csr(len(cands), n, seed=1000 + c)
+        batches.append((c, offs, cands[pos]))
+    gen_s = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    plan = kpamd.ClusterPlan(ctx, cl)
+    prep_s = time.perf_counter() - t0
+    plan.simulate_csr(batches[-1][1][:1025] if len(batches[-1][1]) > 1025 else batches[-1][1],
+                      batches[-1][2])  # warmup (untimed)
+    barrier()
+    t0 = time.perf_counter()
+    best_s, best_i, kern_ms, pops, words, n_done = -np.inf, -1, 0.0, 0, 0, 0
+    counts = np.zeros(3, dtype=np.int64)
+    for c, offs, nodes in batches:
+        res, st = plan.simulate_csr(offs, nodes)
+        base = args.subsets if c < 0 else c * CHUNK  # prefixes are indexed after the random subsets
+        s, i = disruption.best_local(res, base)
+        if i >= 0 and (s > best_s or (s == best_s and i < best_i)):
+            best_s, best_i = s, i
+        counts += np.bincount(res["decision"], minlength=3)[:3]
+        kern_ms += st["solve_kernel_ms"]
+        pops += st["pops"]
+        words += st["phase_cycles"][0]
+        n_done += len(offs) - 1
+    dev = torch.device("cuda", torch.cuda.current_device())
+    best_s, best_i = disruption.reduce_best(best_s, best_i, dist, device=dev)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    total = n_done
+    if dist is not None:
+        te = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(te, op=dist.ReduceOp.MAX)
+        tot = torch.tensor([float(n_done)], dtype=torch.float64, device=dev)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        elapsed, total = float(te.item()), int(tot.item())
+        cnt = torch.tensor(counts, device=dev)
+        dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
+        counts = cnt.cpu().numpy()
+    plan.close()
+    out = {
+        "metric": "consolidation sims/s",
+        "value": round(total / elapsed, 1),
+        "unit": "sims/s",
+        "n_gpus": world,
+        "scaling": "strong" if world > 1 else "n/a",
+        "workload": f"config4: computeConsolidation of {total} candidate subsets (99 disruption-cost prefixes + "
+                    f"random 2..100-candidate subsets) on a {args.cluster_nodes}-node cluster with "
+                    f"{len(cl.pod_shape)} pods (8-40 per node), 2 NodePools, 919 types; sharded by chunk over "
+                    f"ranks, best decision by RCCL all-gather",
+        "elapsed_s": round(elapsed, 4),
+        "sim_kernel_ms_rank0": round(kern_ms, 3),
+        "pods_rescheduled_rank0": int(pops),
+        "decisions": {"noop": int(counts[0]), "delete": int(counts[1]), "replace": int(counts[2])},
+        "best": {"savings": best_s, "subset": best_i},
+        "prepare_s": round(prep_s, 3),
+        "subset_generation_s": round(gen_s, 3),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = _cpu_baseline_sims(cl, cands, args.cpu_sample_sims)
+    return out
+
+
+def _cpu_baseline_sims(cl, cands, n):
+    import numpy as np
+    from kpamd import disruption
+    from oracle import pyoracle
+
+    offs, pos = disruption.random_subsets_csr(len(cands), n, seed=1000)
+    subs = [list(cands[pos[offs[i]:offs[i + 1]]]) for i in range(n)]
+    t0 = time.perf_counter()
+    pyoracle.simulate_batch(cl, subs)
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 3), "unit": "sims/s", "cores": 1, "kind": "port",
+            "sample": f"first {n} random subsets of chunk 0 on the same cluster, oracle computeConsolidation "
+                      f"single-threaded, {dt:.1f} s"}
 
 
 def _traffic():

@@ -266,6 +266,19 @@ class ClusterPlan:
             return out, stats_dict(st)
         return [sim_dict(out[i]) for i in range(len(subsets))], stats_dict(st)
 
+    def simulate_csr(self, offsets, nodes, multi_node=True):
+        """CSR batch (uint32 offsets[n+1], node indices) -> numpy structured array (abi.sim_dtype()), stats."""
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint32)
+        nodes = np.ascontiguousarray(nodes, dtype=np.uint32)
+        n = len(offsets) - 1
+        out = np.zeros(max(n, 1), dtype=abi.sim_dtype())
+        st = abi.SolveStats()
+        P = C.POINTER
+        _check(self.ctx.lib, self.ctx.lib.kp_cluster_simulate(
+            self.h, offsets.ctypes.data_as(P(C.c_uint32)), nodes.ctypes.data_as(P(C.c_uint32)) if len(nodes) else None,
+            n, 1 if multi_node else 0, out.ctypes.data_as(P(abi.SimResult)), C.byref(st)))
+        return out[:n], stats_dict(st)
+
     def close(self):
         if self.h:
             self.ctx.lib.kp_cluster_plan_destroy(self.h)

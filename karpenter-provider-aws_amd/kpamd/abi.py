@@ -298,6 +298,20 @@ def build_cluster(arena, cl, catalog_handles=None):
     return c
 
 
+SIM_DTYPE = None
+
+
+def sim_dtype():
+    import numpy as np
+    global SIM_DTYPE
+    if SIM_DTYPE is None:
+        SIM_DTYPE = np.dtype([("decision", "<i4"), ("nodepool", "<u4"), ("candidate_price", "<f8"),
+                              ("replacement_price", "<f8"), ("savings", "<f8"), ("n_options", "<u4"),
+                              ("n_pods", "<u4")])
+        assert SIM_DTYPE.itemsize == C.sizeof(SimResult)
+    return SIM_DTYPE
+
+
 def subsets_csr(arena, subsets):
     import numpy as np
     offs = np.zeros(len(subsets) + 1, dtype=np.uint32)

@@ -1,0 +1,122 @@
+"""Disruption-side callers of the batched simulation (kp_cluster_simulate), mirroring upstream
+pkg/controllers/disruption (sigs.k8s.io/karpenter v1.5.1, absent from the container; behaviour per SURVEY §3
+CS3 and R:website/content/en/preview/concepts/disruption.md:89-128):
+
+  SingleNodeConsolidation.compute_command   the first candidate (disruption-cost order) whose
+                                            computeConsolidation is not a no-op
+  MultiNodeConsolidation.first_n_option     firstNConsolidationOption's binary search over prefixes
+                                            candidates[0:mid+1], lo=1, hi=min(len-1, 99); every prefix
+                                            the search can touch is simulated in ONE batch, then the
+                                            search is replayed exactly over those results
+  sweep(...)                                the config-4 sweep: many subsets sharded over ranks, best
+                                            decision by (savings desc, subset index asc) across ranks
+                                            with one collective (RCCL all-gather of 16 B per rank)
+
+Decisions are kp_decision values: 0 no-op, 1 delete, 2 replace.
+"""
+import numpy as np
+
+NOOP, DELETE, REPLACE = 0, 1, 2
+
+
+class SingleNodeConsolidation:
+    def __init__(self, plan):
+        self.plan = plan
+
+    def compute_command(self, candidates):
+        """Returns (candidate, result) of the first candidate whose simulation is not a no-op, or None."""
+        if not candidates:
+            return None
+        res, _ = self.plan.simulate([[c] for c in candidates], multi_node=False)
+        for c, r in zip(candidates, res):
+            if r["decision"] != NOOP:
+                return c, r
+        return None
+
+
+class MultiNodeConsolidation:
+    MAX_CANDIDATES = 100
+
+    def __init__(self, plan):
+        self.plan = plan
+
+    @staticmethod
+    def search_prefixes(n):
+        """Every mid the binary search can evaluate (prefix length mid+1)."""
+        lo, hi = 1, min(n - 1, MultiNodeConsolidation.MAX_CANDIDATES - 1)
+        return list(range(lo, hi + 1)) if hi >= lo else []
+
+    @staticmethod
+    def replay(n, results_by_mid):
+        """firstNConsolidationOption over precomputed computeConsolidation(candidates[0:mid+1]) results."""
+        lo, hi = 1, min(n - 1, MultiNodeConsolidation.MAX_CANDIDATES - 1)
+        best = None
+        while lo <= hi:
+            mid = (lo + hi) // 2
+            r = results_by_mid[mid]
+            if r["decision"] == DELETE or (r["decision"] == REPLACE and r["n_options"] > 0):
+                best = (mid, r)
+                lo = mid + 1
+            else:
+                hi = mid - 1
+        return best
+
+    def first_n_option(self, candidates):
+        """Returns (prefix length, result) of the command firstNConsolidationOption picks, or None."""
+        mids = self.search_prefixes(len(candidates))
+        if not mids:
+            return None
+        res, _ = self.plan.simulate([candidates[:m + 1] for m in mids], multi_node=True)
+        by_mid = dict(zip(mids, res))
+        hit = self.replay(len(candidates), by_mid)
+        return None if hit is None else (hit[0] + 1, hit[1])
+
+
+def random_subsets_csr(n_candidates, n_subsets, seed, max_size=100, min_size=2):
+    """n_subsets random subsets of candidate POSITIONS (2..max_size each, distinct, ascending), CSR."""
+    rng = np.random.default_rng(seed)
+    k = rng.integers(min_size, min(max_size, n_candidates) + 1, size=n_subsets)
+    picks = rng.integers(0, n_candidates, size=(n_subsets, int(k.max())))
+    picks = np.sort(np.where(np.arange(picks.shape[1])[None, :] < k[:, None], picks, np.iinfo(np.int64).max), axis=1)
+    valid = picks != np.iinfo(np.int64).max
+    valid[:, 1:] &= picks[:, 1:] != picks[:, :-1]  # drop repeats: subsets stay sets
+    sizes = valid.sum(axis=1)
+    offs = np.zeros(n_subsets + 1, dtype=np.uint32)
+    offs[1:] = np.cumsum(sizes)
+    return offs, picks[valid].astype(np.uint32)
+
+
+def best_local(results, base_index=0):
+    """(savings, global subset index) of the best non-no-op decision in this shard; (-inf, -1) if none."""
+    dec = np.array([int(r.decision) for r in results], dtype=np.int32) if not isinstance(results, np.ndarray) else results["decision"]
+    sav = np.array([r.savings for r in results], dtype=np.float64) if not isinstance(results, np.ndarray) else results["savings"]
+    sav = np.where(dec != NOOP, sav, -np.inf)
+    if len(sav) == 0 or not np.isfinite(sav.max()):
+        return -np.inf, -1
+    i = int(np.argmax(sav))  # first index of the max: ties -> lowest subset index
+    return float(sav[i]), base_index + i
+
+
+def reduce_best(savings, index, dist=None, device=None):
+    """Cross-rank argmax of (savings, -index): one all-gather of (savings, index) per rank."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return savings, index
+    import torch
+    t = torch.tensor([savings, float(index)], dtype=torch.float64, device=device)
+    out = torch.zeros(dist.get_world_size() * 2, dtype=torch.float64, device=device)
+    dist.all_gather_into_tensor(out, t)
+    v = out.view(-1, 2).cpu().numpy()
+    best_s, best_i = -np.inf, -1
+    for s, i in v:
+        if i < 0:
+            continue
+        if s > best_s or (s == best_s and (best_i < 0 or i < best_i)):
+            best_s, best_i = float(s), int(i)
+    return best_s, best_i
+
+
+def shard(n, rank, world):
+    """Contiguous block of [0, n) for this rank."""
+    per = (n + world - 1) // world
+    lo = min(n, rank * per)
+    return lo, min(n, lo + per)

@@ -1,0 +1,112 @@
+"""Host-side consolidation logic on CPU: the oracle's computeConsolidation on hand-built clusters (known
+answers), the firstNConsolidationOption replay, subset generation, and the cross-rank best-decision
+reduction over a world_size-2 gloo group."""
+import os
+
+import numpy as np
+import pytest
+
+
+def _mini_cluster(catalog, initialized_b=True, b_pods=1):
+    """Node A: m5.large running one 500m pod; node B: m5.2xlarge with room. Both on-demand, zone 1a."""
+    from kpamd import synth
+    from kpamd.model import Cluster, ClusterNode, ExistingNode, NodePool, PodShape
+    names = [it.name for it in catalog]
+    shapes = [PodShape(synth.req_res(500, 512))]
+    pool = NodePool("default", 0, 0, [("karpenter.sh/capacity-type", "In", ["on-demand"]),
+                                      (synth.K + "instance-category", "In", ["c", "m", "r"])])
+    nodes, pods = [], []
+    for i, (tname, npods) in enumerate([("m5.large", 1), ("m5.2xlarge", b_pods)]):
+        it = catalog[names.index(tname)]
+        labels = synth.node_labels(it, 0, "on-demand", "default", f"n{i}")
+        alloc = it.allocatable()
+        mine = list(range(len(pods), len(pods) + npods))
+        pods += [0] * npods
+        used = {"cpu": 500 * npods, "memory": 512 * synth.MI * 1000 * npods, "pods": 1000 * npods}
+        avail = {r: alloc[r] - used[r] for r in used}
+        nodes.append(ClusterNode(ExistingNode(f"n{i}", labels, avail, {}, [], initialized_b or i == 0),
+                                 0, names.index(tname), mine))
+    n = len(pods)
+    return Cluster([catalog], [pool], nodes, shapes, np.zeros(n, dtype=np.uint32),
+                   np.full(n, 1_750_000_000, dtype=np.int64), np.arange(n, dtype=np.uint64), candidates=[0, 1])
+
+
+def test_delete_when_pods_fit_elsewhere(catalog):
+    from oracle import pyoracle
+    cl = _mini_cluster(catalog)
+    (r,), _ = pyoracle.simulate_batch(cl, [[0]], multi_node=False)
+    assert r["decision"] == 1 and r["n_pods"] == 1
+    assert r["savings"] == r["candidate_price"] > 0
+
+
+def test_uninitialized_destination_is_noop(catalog):
+    from oracle import pyoracle
+    cl = _mini_cluster(catalog, initialized_b=False)
+    (r,), _ = pyoracle.simulate_batch(cl, [[0]], multi_node=False)
+    assert r["decision"] == 0
+
+
+def test_replace_both_with_cheaper(catalog):
+    """Both nodes' 2 pods (1 vCPU) fit one new NodeClaim cheaper than m5.large + m5.2xlarge."""
+    from oracle import pyoracle
+    cl = _mini_cluster(catalog)
+    (r,), _ = pyoracle.simulate_batch(cl, [[0, 1]], multi_node=True)
+    assert r["decision"] == 2 and r["n_pods"] == 2
+    assert 0 < r["replacement_price"] < r["candidate_price"]
+    assert r["savings"] == pytest.approx(r["candidate_price"] - r["replacement_price"])
+    assert 1 <= r["n_options"] <= 100
+
+
+def test_first_n_replay():
+    from kpamd.disruption import DELETE, NOOP, REPLACE, MultiNodeConsolidation as M
+    n = 40
+    # prefixes up to length 13 (mid 12) succeed, longer fail -> the search settles on mid 12
+    by_mid = {m: {"decision": DELETE if m <= 12 else NOOP, "n_options": 0} for m in M.search_prefixes(n)}
+    mid, r = M.replay(n, by_mid)
+    assert mid == 12 and r["decision"] == DELETE
+    by_mid = {m: {"decision": REPLACE, "n_options": 0} for m in M.search_prefixes(n)}  # no options left
+    assert M.replay(n, by_mid) is None
+    assert M.search_prefixes(1) == [] and M.search_prefixes(300)[-1] == 99
+
+
+def test_random_subsets_csr():
+    from kpamd.disruption import random_subsets_csr
+    offs, pos = random_subsets_csr(500, 1000, seed=3)
+    assert offs[0] == 0 and len(offs) == 1001 and offs[-1] == len(pos)
+    for i in range(1000):
+        s = pos[offs[i]:offs[i + 1]]
+        assert 1 <= len(s) <= 100 and np.all(np.diff(s.astype(np.int64)) > 0) and s.max() < 500
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    from kpamd.disruption import reduce_best, shard
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # rank 0 holds savings 3.0 at subset 7, rank 1 holds 3.0 at subset 5 and its shard is [50, 100)
+        lo, hi = shard(100, rank, world)
+        s, i = (3.0, 7) if rank == 0 else (3.0, 5)
+        q.put((rank, (lo, hi), reduce_best(s, i, dist, device="cpu")))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_reduce_best_gloo_world2():
+    import multiprocessing as mp
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = [q.get(timeout=120) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+    out.sort()
+    assert out[0][1] == (0, 50) and out[1][1] == (50, 100)
+    assert out[0][2] == out[1][2] == (3.0, 5)  # tie on savings -> lowest subset index

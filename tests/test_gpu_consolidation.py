@@ -1,7 +1,12 @@
 """Batched consolidation simulations on the device (kp_cluster_simulate) vs the CPU oracle's
 computeConsolidation (oracle/oracle.cpp kpo_simulate_batch) — decision, replacement NodePool, prices,
 savings and option count must be identical for every subset."""
+import os
+import sys
+
 import pytest
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 pytestmark = pytest.mark.gpu
 
@@ -59,3 +64,34 @@ def test_repeat_and_empty(ctx, catalog):
         assert c == []
     finally:
         plan.close()
+
+
+def test_known_answers(ctx, catalog):
+    from test_consolidation_host import _mini_cluster
+    got = check(ctx, _mini_cluster(catalog), [[0], [1], [0, 1]], multi_node=True)
+    assert got[0]["decision"] == 1 and got[2]["decision"] == 2
+    got = check(ctx, _mini_cluster(catalog, initialized_b=False), [[0]], multi_node=False)
+    assert got[0]["decision"] == 0
+
+
+def test_multi_and_single_node_commands(ctx, catalog):
+    """firstNConsolidationOption / SingleNodeConsolidation driven by device batches agree with the same
+    searches driven by the oracle."""
+    import kpamd
+    from kpamd import synth
+    from kpamd.disruption import MultiNodeConsolidation, SingleNodeConsolidation
+    from oracle import pyoracle
+    cl = synth.config4(catalog, n_nodes=150, seed=12)
+    plan = kpamd.ClusterPlan(ctx, cl)
+    try:
+        multi = MultiNodeConsolidation(plan).first_n_option(cl.candidates)
+        single = SingleNodeConsolidation(plan).compute_command(cl.candidates)
+    finally:
+        plan.close()
+    mids = MultiNodeConsolidation.search_prefixes(len(cl.candidates))
+    want, _ = pyoracle.simulate_batch(cl, [cl.candidates[:m + 1] for m in mids], multi_node=True)
+    hit = MultiNodeConsolidation.replay(len(cl.candidates), dict(zip(mids, want)))
+    assert (multi is None and hit is None) or (multi[0] == hit[0] + 1 and multi[1] == hit[1])
+    want1, _ = pyoracle.simulate_batch(cl, [[c] for c in cl.candidates], multi_node=False)
+    first = next(((c, r) for c, r in zip(cl.candidates, want1) if r["decision"] != 0), None)
+    assert single == first
