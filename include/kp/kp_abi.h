@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define KP_ABI_VERSION 1
+#define KP_ABI_VERSION 2
 
 enum kp_status {
   KP_OK = 0,
@@ -176,6 +176,38 @@ typedef struct kp_preferred_term {
   kp_requirements preference;
 } kp_preferred_term;
 
+/* metav1.LabelSelector: matchLabels AND matchExpressions (In / NotIn / Exists / DoesNotExist). A nil selector
+ * (is_nil != 0) selects nothing; an empty one selects everything (metav1.LabelSelectorAsSelector). */
+enum kp_selector_operator { KP_SEL_IN = 0, KP_SEL_NOT_IN = 1, KP_SEL_EXISTS = 2, KP_SEL_DOES_NOT_EXIST = 3 };
+typedef struct kp_selector_requirement {
+  const char* key;
+  int32_t op;        /* enum kp_selector_operator */
+  uint32_t n_values;
+  const char* const* values;
+} kp_selector_requirement;
+typedef struct kp_label_selector {
+  const kp_label* match_labels;
+  uint32_t n_match_labels;
+  uint32_t n_match_expressions;
+  const kp_selector_requirement* match_expressions;
+  int32_t is_nil;
+  int32_t reserved_;
+} kp_label_selector;
+
+/* corev1.TopologySpreadConstraint (upstream scheduling.TopologyGroup of TopologyTypeSpread). */
+enum kp_when_unsatisfiable { KP_DO_NOT_SCHEDULE = 0, KP_SCHEDULE_ANYWAY = 1 };
+enum kp_inclusion_policy { KP_POLICY_UNSET = 0, KP_POLICY_HONOR = 1, KP_POLICY_IGNORE = 2 };
+typedef struct kp_topology_spread {
+  const char* topology_key;
+  int32_t max_skew;
+  int32_t min_domains;          /* <= 0: nil */
+  int32_t when_unsatisfiable;   /* ScheduleAnyway constraints are dropped one by one by Preferences.Relax */
+  int32_t node_affinity_policy; /* UNSET = Honor */
+  int32_t node_taints_policy;   /* UNSET = Ignore */
+  int32_t reserved_;
+  kp_label_selector selector;
+} kp_topology_spread;
+
 /* A pod "shape": everything the scheduler reads from a pod except its identity. */
 typedef struct kp_pod_shape {
   kp_resource_list requests;                 /* resources.RequestsForPods(pod) */
@@ -187,9 +219,21 @@ typedef struct kp_pod_shape {
   uint32_t n_preferred_terms;
   uint32_t n_tolerations;
   const kp_toleration* tolerations;
-  uint32_t n_topology_spread;                /* ABI v1: must be 0 (else KP_E_UNSUPPORTED) */
-  uint32_t reserved_;
+  uint32_t n_topology_spread;
+  uint32_t n_labels;
+  const kp_topology_spread* topology_spread; /* spec.topologySpreadConstraints, in spec order */
+  const char* namespace_;                    /* metadata.namespace (topology selectors are namespaced) */
+  const kp_label* labels;                    /* metadata.labels (matched by topology selectors) */
 } kp_pod_shape;
+
+/* A pod already bound to a node of the cluster: what upstream Topology.countDomains lists (through the
+ * kube client) to seed the domain counts of every topology group whose selector matches it. */
+typedef struct kp_bound_pod {
+  const char* namespace_;
+  const kp_label* labels;
+  uint32_t n_labels;
+  uint32_t node;  /* index into kp_solve_in.existing */
+} kp_bound_pod;
 
 typedef struct kp_pod {
   uint32_t shape;
@@ -229,6 +273,9 @@ typedef struct kp_solve_in {
   const kp_pod* pods;
   uint32_t n_pods;
   uint32_t max_instance_types;  /* scheduling.MaxInstanceTypes = 100; 0 = no truncation */
+  const kp_bound_pod* bound_pods;  /* pods running on existing nodes (topology domain counts) */
+  uint32_t n_bound_pods;
+  uint32_t reserved_;
 } kp_solve_in;
 
 typedef struct kp_nodeclaim_info {
@@ -239,6 +286,10 @@ typedef struct kp_nodeclaim_info {
   const uint32_t* pods;     /* pod indices in the order they were added */
   const uint32_t* options;  /* catalogue indices, cheapest-compatible-offering price asc then name asc */
   kp_resource_list requests;
+  /* the NodeClaim's Requirements after FinalizeScheduling (hostname placeholder removed) as upstream
+   * Requirements.NodeSelectorRequirements() renders them (Gt/Lt win over NotIn values): keys in byte order,
+   * values sorted. Owned by the result. Topology spread narrows keys here (e.g. zone In {one zone}). */
+  kp_requirements requirements;
 } kp_nodeclaim_info;
 
 typedef struct kp_solve_stats {
@@ -266,6 +317,7 @@ const char* kp_last_error(void);
 int32_t kp_abi_version(void);
 
 /* ---- catalogue ---------------------------------------------------------------------------- */
+/* ctx may be NULL for a host-only catalogue (kp_solve_validate); device entry points need a ctx one. */
 int32_t kp_catalog_upload(kp_ctx* ctx, const kp_catalog_desc* desc, uint64_t seqnum, kp_catalog** out);
 uint64_t kp_catalog_seqnum(const kp_catalog* cat);
 uint32_t kp_catalog_size(const kp_catalog* cat);
@@ -340,6 +392,9 @@ int32_t kp_filter_compatible_available(kp_ctx* ctx, const kp_catalog* cat, const
  * dictionaries -> bitsets, catalogue SoA, NodeClaimTemplates, pod queue order) and uploads it; run
  * executes Solve on the resident inputs and may be repeated (state is restored on device each run). */
 int32_t kp_solve(kp_ctx* ctx, const kp_solve_in* in, kp_solve_result** out);
+/* Host-side compile of the batch only (no device, catalogues may come from kp_catalog_upload(NULL, ...)):
+ * KP_OK when kp_solve would accept it, else the KP_E_UNSUPPORTED / KP_E_INVAL it would return. */
+int32_t kp_solve_validate(const kp_solve_in* in);
 int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out);
 int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out);
 void kp_solve_plan_destroy(kp_solve_plan* plan);

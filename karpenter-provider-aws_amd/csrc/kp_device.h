@@ -65,6 +65,35 @@ struct SolveArgs {
   int32_t* nc_taintset;              // [P] taint set of the NodeClaim's template
   uint32_t req_res_mask;             // resources some pod shape requests (> 0)
   int32_t timing;                    // 1: thread 0 accumulates per-phase s_memtime deltas into stats[8..15]
+  // topology spread (upstream Topology, TopologyTypeSpread groups). A group on a dictionary key keeps a
+  // count per value ordinal and the mask of registered domains; a hostname group a saturating u8 count per
+  // node (existing positions: hcnt_ex, NodeClaim ids: hcnt_nc).
+  int32_t n_groups;
+  const int32_t* tg_key;             // [G] dictionary key, -1: hostname
+  const int32_t* tg_row;             // [G] row of a hostname group in hcnt_*, -1 otherwise
+  const int32_t* tg_maxskew;         // [G]
+  const int32_t* tg_mindom;          // [G] minDomains, 0: nil
+  const int32_t* tg_aff;             // [G] node filter has an affinity term (NodeAffinityPolicy Honor)
+  const int32_t* tg_term_base;       // [G] its term in tg_terms
+  const uint64_t* tg_filt_tol;       // [G] bit ts: node filter admits taint set ts (NodeTaintsPolicy)
+  const uint8_t* tg_terms;           // KReqs
+  const uint64_t* tg_terms_negop;
+  int32_t* tg_cnt;                   // [G][64] (mutable)
+  uint64_t* tg_reg;                  // [G] (mutable)
+  uint8_t* hcnt_ex;                  // [GH][E] (mutable)
+  uint8_t* hcnt_nc;                  // [GH][hnc_stride] (zeroed per run)
+  int32_t hnc_stride;
+  const int32_t* shape_rec_base;     // [S] groups that select the shape's pods (Topology.Record)
+  const int32_t* shape_rec_n;        // [S]
+  const int32_t* rec_list;
+  const int32_t* sl_own_base;        // [SL] groups the shape-level owns (AddRequirements)
+  const int32_t* sl_own_n;           // [SL] (<= 8)
+  const int32_t* own_group;
+  const int32_t* own_self;           // the group's selector matches the owner pod
+  const uint64_t* own_pd;            // podDomains (strict requirements) over the key's value ordinals
+  const uint64_t* sl_topo_keys;      // [SL] dictionary keys of the owned groups
+  const int32_t* tkey_slot;          // [64] row of a topology key in ex_tcode
+  const uint8_t* ex_tcode;           // [TK][E] value ordinal of the existing node's label (0xFF: none)
   // outputs
   int32_t* placement;                // [P]
   int32_t* events;                   // [P] pods in placement order

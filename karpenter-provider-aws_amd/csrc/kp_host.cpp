@@ -682,12 +682,68 @@ struct DevBuf {
 
 }  // namespace
 
+namespace {
+// A NodeClaim's final requirements as upstream Requirements.NodeSelectorRequirements() renders them
+// (Gt, then Lt, then NotIn/Exists, then In/DoesNotExist), keys in byte order, values sorted. The hostname
+// placeholder is not part of the dictionary, as FinalizeScheduling drops it.
+struct ReqOut {
+  vector<string> keys;
+  vector<vector<string>> vals;
+  vector<vector<const char*>> ptrs;
+  vector<kp_requirement> items;
+};
+std::shared_ptr<ReqOut> DecodeReqs(const Dict& d, const KReqs& q) {
+  auto o = std::make_shared<ReqOut>();
+  vector<int> ks;
+  for (int k = 0; k < d.dd.K; k++)
+    if ((q.present >> k) & 1) ks.push_back(k);
+  std::sort(ks.begin(), ks.end(), [&](int a, int b) { return d.keys[a] < d.keys[b]; });
+  for (int k : ks) {
+    const bool bnd = k < KP_MAX_BOUND_KEYS, c = (q.compl_ >> k) & 1;
+    kp_requirement it;
+    memset(&it, 0, sizeof it);
+    vector<string> v;
+    if (c && bnd && ((q.hgt >> k) & 1)) {
+      it.op = KP_OP_GT;
+      v.push_back(std::to_string(q.gt[k]));
+    } else if (c && bnd && ((q.hlt >> k) & 1)) {
+      it.op = KP_OP_LT;
+      v.push_back(std::to_string(q.lt[k]));
+    } else {
+      for (int i = 0; i < nwords(d, k); i++) {
+        const int w = kw(d, k, i);
+        uint64_t m = q.vals[w];
+        while (m) {
+          const int b = __builtin_ctzll(m);
+          m &= m - 1;
+          v.push_back(d.vals[k][(size_t)i * 64 + b]);  // ordinal = i*64 + b; dictionary values are sorted
+        }
+      }
+      it.op = c ? (v.empty() ? KP_OP_EXISTS : KP_OP_NOT_IN) : (v.empty() ? KP_OP_DOES_NOT_EXIST : KP_OP_IN);
+    }
+    it.min_values = (bnd && ((q.hmin >> k) & 1)) ? q.minv[k] : -1;
+    o->keys.push_back(d.keys[k]);
+    o->vals.push_back(std::move(v));
+    o->items.push_back(it);
+  }
+  o->ptrs.resize(o->vals.size());
+  for (size_t i = 0; i < o->items.size(); i++) {
+    for (auto& x : o->vals[i]) o->ptrs[i].push_back(x.c_str());
+    o->items[i].key = o->keys[i].c_str();
+    o->items[i].values = o->ptrs[i].data();
+    o->items[i].n_values = (uint32_t)o->ptrs[i].size();
+  }
+  return o;
+}
+}  // namespace
+
 struct kp_solve_result {
   vector<int32_t> placement;
   struct NC {
     uint32_t nodepool, n_remaining;
     vector<uint32_t> pods, options;
     kp_resource_list requests;
+    std::shared_ptr<ReqOut> reqs;
   };
   vector<NC> ncs;
   kp_solve_stats stats;
@@ -731,7 +787,7 @@ void kp_ctx_destroy(kp_ctx* c) {
 }
 
 int32_t kp_catalog_upload(kp_ctx* ctx, const kp_catalog_desc* desc, uint64_t seqnum, kp_catalog** out) {
-  if (!ctx || !desc || !out) return fail(KP_E_INVAL, "null argument");
+  if (!desc || !out) return fail(KP_E_INVAL, "null argument");  // ctx NULL: host-only (kp_solve_validate)
   if (desc->n_types > 4096) return fail(KP_E_UNSUPPORTED, "%u instance types (max 4096)", desc->n_types);
   auto* c = new kp_catalog();
   c->ctx = ctx;
@@ -845,13 +901,345 @@ struct Compiled {
   vector<int64_t> ex_available, ex_requests;
   // pods
   vector<int32_t> pod_shape, queue;
+  // topology spread (TopologyTypeSpread groups; see SolveArgs)
+  int G = 0, GH = 0, TK = 0;
+  vector<int32_t> tg_key, tg_row, tg_maxskew, tg_mindom, tg_aff, tg_term_base, tg_nterm;
+  vector<uint64_t> tg_filt_tol, tg_reg, tg_terms_negop;
+  vector<KReqs> tg_terms;
+  vector<int32_t> tg_cnt;    // [G][64]
+  vector<uint8_t> hcnt0;     // [GH][E]
+  vector<int32_t> shape_rec_base, shape_rec_n, rec_list;
+  vector<int32_t> sl_own_base, sl_own_n, own_group, own_self;
+  vector<uint64_t> own_pd, sl_topo_keys;
+  vector<int32_t> tkey_slot;  // [64]
+  vector<uint8_t> ex_tcode;   // [TK][E]
 };
+
+// Requirements.Compatible(A, B, allowUndefinedWellKnown) on the host encoding.
+bool HostCompatible(const Dict& d, const KReqs& A, const KReqs& B, bool allow) {
+  const uint64_t negB = NegOp(d, B), negA = NegOp(d, A);
+  uint64_t undef = B.present & ~A.present & ~negB;
+  if (allow) undef &= ~d.dd.wellknown;
+  if (undef) return false;
+  KReqs m = A;
+  HostAdd(d, m, B);
+  const uint64_t shared = A.present & B.present;
+  for (int k = 0; k < d.dd.K; k++) {
+    if (!((shared >> k) & 1)) continue;
+    const bool empty = !((m.compl_ >> k) & 1) && !KeyNonEmptyVals(d, m, k);  // Len() == 0
+    if (empty && !(((negA & negB) >> k) & 1)) return false;
+  }
+  return true;
+}
+
+// Semantic canonical form of a requirement set (identity of a topology node filter).
+string KCanon(const Dict& d, const KReqs& q) {
+  string o;
+  for (int k = 0; k < d.dd.K; k++) {
+    if (!((q.present >> k) & 1)) continue;
+    const bool bnd = k < KP_MAX_BOUND_KEYS;
+    o += std::to_string(k) + ((q.compl_ >> k) & 1 ? "!" : "=");
+    for (int i = 0; i < nwords(d, k); i++) o += std::to_string(q.vals[kw(d, k, i)]) + ",";
+    if (bnd && ((q.hgt >> k) & 1)) o += ">" + std::to_string(q.gt[k]);
+    if (bnd && ((q.hlt >> k) & 1)) o += "<" + std::to_string(q.lt[k]);
+    if (bnd && ((q.hmin >> k) & 1)) o += "#" + std::to_string(q.minv[k]);
+    o += ";";
+  }
+  return o;
+}
+
+// metav1.LabelSelector.Matches (nil selects nothing)
+bool SelectorMatches(const kp_label_selector& sel, const std::map<string, string>& labels) {
+  if (sel.is_nil) return false;
+  for (uint32_t i = 0; i < sel.n_match_labels; i++) {
+    auto it = labels.find(sel.match_labels[i].key ? sel.match_labels[i].key : "");
+    if (it == labels.end() || it->second != (sel.match_labels[i].value ? sel.match_labels[i].value : "")) return false;
+  }
+  for (uint32_t i = 0; i < sel.n_match_expressions; i++) {
+    const kp_selector_requirement& r = sel.match_expressions[i];
+    auto it = labels.find(r.key ? r.key : "");
+    const bool has = it != labels.end();
+    bool in = false;
+    for (uint32_t j = 0; has && j < r.n_values && !in; j++) in = it->second == (r.values[j] ? r.values[j] : "");
+    switch (r.op) {
+      case KP_SEL_IN:
+        if (!in) return false;
+        break;
+      case KP_SEL_NOT_IN:
+        if (in) return false;
+        break;
+      case KP_SEL_EXISTS:
+        if (!has) return false;
+        break;
+      default:
+        if (has) return false;
+    }
+  }
+  return true;
+}
+string SelectorCanon(const kp_label_selector& sel) {
+  if (sel.is_nil) return "nil";
+  vector<string> parts;
+  for (uint32_t i = 0; i < sel.n_match_labels; i++)
+    parts.push_back(string(sel.match_labels[i].key) + "/0," + (sel.match_labels[i].value ? sel.match_labels[i].value : ""));
+  for (uint32_t i = 0; i < sel.n_match_expressions; i++) {
+    const kp_selector_requirement& r = sel.match_expressions[i];
+    std::set<string> vs;
+    for (uint32_t j = 0; j < r.n_values; j++) vs.insert(r.values[j] ? r.values[j] : "");
+    string x = string(r.key) + "/" + std::to_string(r.op);
+    for (auto& v : vs) x += "," + v;
+    parts.push_back(x);
+  }
+  std::sort(parts.begin(), parts.end());
+  string o;
+  for (auto& x : parts) o += x + ";";
+  return o;
+}
+std::map<string, string> LabelMap(const kp_label* l, uint32_t n) {
+  std::map<string, string> m;
+  for (uint32_t i = 0; i < n; i++) m[l[i].key ? l[i].key : ""] = l[i].value ? l[i].value : "";
+  return m;
+}
 
 struct TaintT {
   string key, value;
   int effect;
   bool operator<(const TaintT& o) const { return std::tie(key, value, effect) < std::tie(o.key, o.value, o.effect); }
 };
+
+// Topology spread groups (upstream NewTopology / TopologyGroup / countDomains / buildDomainGroups), in the
+// device encoding: one group per distinct (key, maxSkew, namespace, selector, node filter, policies) in order
+// of first appearance over the pods; dictionary-key groups keep a count per value ordinal + a registered-
+// domain mask, hostname groups a saturating u8 count per node (existing positions, then NodeClaims).
+int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector<RawReqs>>& strict_levels,
+                        const vector<vector<vector<int>>>& spread_levels, const vector<int>& np_taintset) {
+  const Dict& d = cp.d;
+  const int E = (int)cp.ex_input.size();
+  cp.tkey_slot.assign(KP_MAX_KEYS, -1);
+  cp.shape_rec_base.assign(in->n_shapes, 0);
+  cp.shape_rec_n.assign(in->n_shapes, 0);
+  const size_t SL = cp.shape_reqs.size();
+  cp.sl_own_base.assign(SL, 0);
+  cp.sl_own_n.assign(SL, 0);
+  cp.sl_topo_keys.assign(SL, 0);
+  bool any = false;
+  for (uint32_t s = 0; s < in->n_shapes; s++) any |= in->shapes[s].n_topology_spread > 0;
+  if (!any) return KP_OK;
+  vector<int> ex_pos(in->n_existing);
+  for (int e = 0; e < E; e++) ex_pos[cp.ex_input[e]] = e;
+  vector<std::map<string, string>> node_labels(in->n_existing);
+  vector<KReqs> node_reqs(in->n_existing);
+  for (uint32_t i = 0; i < in->n_existing; i++) {
+    node_labels[i] = LabelMap(in->existing[i].labels, in->existing[i].n_labels);
+    node_reqs[i] = cp.ex_reqs[ex_pos[i]];
+  }
+  // buildDomainGroups for one key: value ordinal -> taint sets of the NodePools offering it
+  std::map<int, vector<uint64_t>> domain_tsets;  // key -> [64] taint-set masks
+  auto domains_of = [&](int k) -> const vector<uint64_t>& {
+    auto it = domain_tsets.find(k);
+    if (it != domain_tsets.end()) return it->second;
+    vector<uint64_t> m(64, 0);
+    auto insert = [&](const KReqs& r, int ts) {
+      if (!((r.present >> k) & 1) || ((r.compl_ >> k) & 1)) return;  // Operator() == In
+      uint64_t v = r.vals[k];
+      while (v) {
+        const int b = __builtin_ctzll(v);
+        v &= v - 1;
+        m[b] |= 1ull << ts;
+      }
+    };
+    for (uint32_t i = 0; i < in->n_nodepools; i++) {
+      const kp_nodepool& np = in->nodepools[i];
+      const HostCat& hc = cp.cats[np.catalog];
+      if (hc.T == 0) continue;
+      RawReqs base_raw = ParseReqs(np.requirements);
+      RawReqs l = LabelReqs(np.labels, np.n_labels, false);
+      base_raw.insert(base_raw.end(), l.begin(), l.end());
+      const KReqs base = Compile(d, base_raw);
+      for (int t = 0; t < hc.T; t++) {
+        KReqs r = base;
+        HostAdd(d, r, hc.treqs[t]);
+        insert(r, np_taintset[i]);
+      }
+      insert(base, np_taintset[i]);
+    }
+    return domain_tsets[k] = m;
+  };
+  std::map<string, int> ids;
+  vector<int> g_shape;  // shape that created the group (its tolerations / filter)
+  // group identity per (shape, spread index)
+  vector<vector<int>> sgroup(in->n_shapes);
+  vector<char> seen(in->n_shapes, 0);
+  auto group_of = [&](uint32_t s, int j) -> int32_t {
+    const kp_pod_shape& sh = in->shapes[s];
+    const kp_topology_spread& t = sh.topology_spread[j];
+    const string key = t.topology_key ? t.topology_key : "";
+    const bool aff = t.node_affinity_policy != KP_POLICY_IGNORE, taint = t.node_taints_policy == KP_POLICY_HONOR;
+    // MakeTopologyNodeFilter: nodeSelector (+ the required term)
+    const KReqs filt = Compile(d, strict_levels[s][0]);
+    string id = key + "|" + std::to_string(t.max_skew) + "|" + (sh.namespace_ ? sh.namespace_ : "") + "|" +
+                SelectorCanon(t.selector) + "|" + std::to_string(aff) + std::to_string(taint) + "|[" + KCanon(d, filt) + "]";
+    if (taint)
+      for (uint32_t i = 0; i < sh.n_tolerations; i++) {
+        const kp_toleration& x = sh.tolerations[i];
+        id += string("(") + (x.key ? x.key : "") + "," + (x.value ? x.value : "") + "," + std::to_string(x.op) + "," +
+              std::to_string(x.effect) + ")";
+      }
+    auto it = ids.find(id);
+    if (it != ids.end()) return it->second;
+    const int g = cp.G++;
+    ids[id] = g;
+    g_shape.push_back((int)s);
+    int k = -1, row = -1;
+    if (key == kHostname) {
+      row = cp.GH++;
+    } else {
+      k = d.key(key);
+      if (k < 0) return fail(KP_E_INVAL, "topology key %s missing from the dictionary", key.c_str()), -1;
+      if (d.dd.nval[k] > 64) return fail(KP_E_UNSUPPORTED, "topology key %s has > 64 values", key.c_str()), -1;
+      if (cp.tkey_slot[k] < 0) cp.tkey_slot[k] = cp.TK++;
+    }
+    cp.tg_key.push_back(k);
+    cp.tg_row.push_back(row);
+    cp.tg_maxskew.push_back(t.max_skew);
+    cp.tg_mindom.push_back(t.min_domains > 0 ? t.min_domains : 0);
+    // filter: affinity terms (none when the filter is empty: everything matches)
+    cp.tg_term_base.push_back((int32_t)cp.tg_terms.size());
+    const bool nonempty = filt.present != 0;
+    cp.tg_aff.push_back(aff && nonempty ? 1 : 0);
+    cp.tg_nterm.push_back(aff && nonempty ? 1 : 0);
+    if (aff && nonempty) {
+      cp.tg_terms.push_back(filt);
+      cp.tg_terms_negop.push_back(NegOp(d, filt));
+    }
+    cp.tg_filt_tol.push_back(taint ? cp.shape_tolerates[s] : ~0ull);
+    // NewTopologyGroup: every known domain of the key, with a zero count (ForEachDomain + taint policy)
+    uint64_t reg = 0;
+    if (k >= 0) {
+      const vector<uint64_t>& dm = domains_of(k);
+      for (int b = 0; b < 64; b++)
+        if (dm[b] && (!taint || (dm[b] & cp.shape_tolerates[s]))) reg |= 1ull << b;
+    }
+    cp.tg_reg.push_back(reg);
+    for (int b = 0; b < 64; b++) cp.tg_cnt.push_back(0);
+    if (row >= 0) cp.hcnt0.resize((size_t)cp.GH * std::max(E, 1), 0);
+    // countDomains: bound pods the selector matches, on nodes the filter admits; then existing nodes' domains
+    auto filter_ok = [&](uint32_t ni) {
+      const int ts = cp.ex_taintset[ex_pos[ni]];
+      if (taint && !((cp.shape_tolerates[s] >> ts) & 1)) return false;
+      if (aff && nonempty && !HostCompatible(d, node_reqs[ni], filt, false)) return false;
+      return true;
+    };
+    const string ns = sh.namespace_ ? sh.namespace_ : "";
+    for (uint32_t b = 0; b < in->n_bound_pods; b++) {
+      const kp_bound_pod& bp = in->bound_pods[b];
+      if (ns != (bp.namespace_ ? bp.namespace_ : "")) continue;
+      if (!SelectorMatches(t.selector, LabelMap(bp.labels, bp.n_labels))) continue;
+      const uint32_t ni = bp.node;
+      if (row >= 0) {  // hostname: the node's label or, failing that, its name — one domain per node
+        if (!filter_ok(ni)) continue;
+        uint8_t& c = cp.hcnt0[(size_t)row * std::max(E, 1) + ex_pos[ni]];
+        if (c < 255) c++;
+      } else {
+        auto lv = node_labels[ni].find(key);
+        if (lv == node_labels[ni].end() || !filter_ok(ni)) continue;
+        const int ord = d.bit(k, lv->second) - k * 64;  // value ordinal (key k's values live in word k)
+        cp.tg_cnt[(size_t)g * 64 + ord]++;
+        cp.tg_reg[g] |= 1ull << ord;
+      }
+    }
+    if (k >= 0)
+      for (uint32_t ni = 0; ni < in->n_existing; ni++) {
+        auto lv = node_labels[ni].find(key);
+        if (lv == node_labels[ni].end() || !filter_ok(ni)) continue;
+        cp.tg_reg[g] |= 1ull << (d.bit(k, lv->second) - k * 64);
+      }
+    return g;
+  };
+  for (uint32_t p = 0; p < in->n_pods; p++) {  // NewTopology: Update(pod) in pod order
+    const uint32_t s = in->pods[p].shape;
+    if (seen[s]) continue;
+    seen[s] = 1;
+    const kp_pod_shape& sh = in->shapes[s];
+    for (uint32_t j = 0; j < sh.n_topology_spread; j++) {
+      const int g = group_of(s, (int)j);
+      if (g < 0) return KP_E_UNSUPPORTED;
+      sgroup[s].push_back(g);
+    }
+  }
+  if (cp.G == 0) return KP_OK;
+  if ((size_t)cp.GH * (size_t)(E + in->n_pods) > ((size_t)1 << 31))
+    return fail(KP_E_UNSUPPORTED, "%d hostname topologies x %u nodes", cp.GH, E + in->n_pods);
+  if (E == 0) cp.hcnt0.clear();
+  // recording groups per shape (TopologyGroup.selects: namespace + selector on the pod's labels)
+  for (uint32_t s = 0; s < in->n_shapes; s++) {
+    const kp_pod_shape& sh = in->shapes[s];
+    const std::map<string, string> lm = LabelMap(sh.labels, sh.n_labels);
+    const string ns = sh.namespace_ ? sh.namespace_ : "";
+    cp.shape_rec_base[s] = (int32_t)cp.rec_list.size();
+    cp.shape_rec_n[s] = 0;
+    for (int g = 0; g < cp.G; g++) {
+      const kp_pod_shape& owner = in->shapes[g_shape[g]];
+      const kp_topology_spread* spec = nullptr;
+      for (uint32_t j = 0; j < owner.n_topology_spread && !spec; j++)
+        if (sgroup[g_shape[g]].size() > j && sgroup[g_shape[g]][j] == g) spec = &owner.topology_spread[j];
+      if (!spec || ns != (owner.namespace_ ? owner.namespace_ : "") || !SelectorMatches(spec->selector, lm)) continue;
+      cp.rec_list.push_back(g);
+      cp.shape_rec_n[s]++;
+    }
+  }
+  // owned groups per shape-level: (group, self-selecting, podDomains mask over the key's value ordinals)
+  for (uint32_t s = 0; s < in->n_shapes; s++) {
+    const kp_pod_shape& sh = in->shapes[s];
+    if (!sh.n_topology_spread) continue;
+    if (sgroup[s].empty()) {  // shape without pods: no groups were created for it
+      for (uint32_t j = 0; j < sh.n_topology_spread; j++) {
+        const int g = group_of(s, (int)j);
+        if (g < 0) return KP_E_UNSUPPORTED;
+        sgroup[s].push_back(g);
+      }
+    }
+    const std::map<string, string> lm = LabelMap(sh.labels, sh.n_labels);
+    for (int l = 0; l < cp.shape_nlevels[s]; l++) {
+      const int sl = cp.shape_level_base[s] + l;
+      const vector<int>& sp = spread_levels[s][l];
+      if (sp.size() > 8) return fail(KP_E_UNSUPPORTED, "> 8 topology spread constraints on one pod");
+      cp.sl_own_base[sl] = (int32_t)cp.own_group.size();
+      cp.sl_own_n[sl] = (int32_t)sp.size();
+      const KReqs strict = Compile(d, strict_levels[s][l]);
+      for (int j : sp) {
+        const int g = sgroup[s][j];
+        cp.own_group.push_back(g);
+        cp.own_self.push_back(SelectorMatches(sh.topology_spread[j].selector, lm) ? 1 : 0);
+        const int k = cp.tg_key[g];
+        uint64_t pd = 0;
+        if (k >= 0) {
+          for (int b = 0; b < d.dd.nval[k]; b++)
+            if (Has(d, strict, k, k * 64 + b)) pd |= 1ull << b;
+          cp.sl_topo_keys[sl] |= 1ull << k;
+        }
+        cp.own_pd.push_back(pd);
+      }
+    }
+  }
+  // existing nodes: value ordinal of each topology key (0xFF: no label)
+  cp.ex_tcode.assign((size_t)std::max(cp.TK, 1) * std::max(E, 1), 0xFF);
+  for (int k = 0; k < KP_MAX_KEYS; k++) {
+    if (cp.tkey_slot[k] < 0) continue;
+    for (int e = 0; e < E; e++) {
+      auto lv = node_labels[cp.ex_input[e]].find(d.keys[k]);
+      if (lv != node_labels[cp.ex_input[e]].end())
+        cp.ex_tcode[(size_t)cp.tkey_slot[k] * E + e] = (uint8_t)(d.bit(k, lv->second) - k * 64);
+    }
+  }
+  if (cp.tg_terms.empty()) {
+    KReqs z;
+    memset(&z, 0, sizeof z);
+    cp.tg_terms.push_back(z);
+    cp.tg_terms_negop.push_back(0);
+  }
+  return KP_OK;
+}
 
 int32_t CompileSolve(const kp_solve_in* in, Compiled& cp) {
   if (in->n_catalogs == 0 || !in->catalogs) return fail(KP_E_INVAL, "no catalogues");
@@ -891,10 +1279,18 @@ int32_t CompileSolve(const kp_solve_in* in, Compiled& cp) {
                               np.taints[j].effect});
   }
   // shapes -> relaxation levels (NewPodRequirements after successive Preferences.Relax)
-  vector<vector<RawReqs>> levels(in->n_shapes);
+  vector<vector<RawReqs>> levels(in->n_shapes), strict_levels(in->n_shapes);
+  vector<vector<vector<int>>> spread_levels(in->n_shapes);  // spreads (indices into topology_spread) per level
   for (uint32_t s = 0; s < in->n_shapes; s++) {
     const kp_pod_shape& sh = in->shapes[s];
-    if (sh.n_topology_spread) return fail(KP_E_UNSUPPORTED, "topology spread constraints (ABI v1)");
+    if (sh.n_topology_spread && sh.n_required_terms > 1)
+      return fail(KP_E_UNSUPPORTED, "topology spread with > 1 required node affinity terms (relaxation re-creates groups)");
+    for (uint32_t j = 0; j < sh.n_topology_spread; j++) {
+      const kp_topology_spread& t = sh.topology_spread[j];
+      const string key = t.topology_key ? t.topology_key : "";
+      if (t.max_skew < 1 || t.max_skew > 250) return fail(KP_E_UNSUPPORTED, "topology spread maxSkew %d", t.max_skew);
+      if (key != kHostname) db.bounded[key];  // the key gets a dictionary id even if no value names it
+    }
     if (sh.n_preferred_terms > 12) return fail(KP_E_UNSUPPORTED, "> 12 preferred terms");
     RawReqs ns = LabelReqs(sh.node_selector, sh.n_node_selector, false);
     vector<RawReqs> req;
@@ -904,6 +1300,8 @@ int32_t CompileSolve(const kp_solve_in* in, Compiled& cp) {
       pref.push_back({sh.preferred_terms[j].weight, ParseReqs(sh.preferred_terms[j].preference)});
     auto byw = [](const std::pair<int, RawReqs>& a, const std::pair<int, RawReqs>& b) { return a.first > b.first; };
     std::stable_sort(pref.begin(), pref.end(), byw);  // sort.Slice on <= 12 = insertion sort (stable)
+    vector<int> spreads;
+    for (uint32_t j = 0; j < sh.n_topology_spread; j++) spreads.push_back((int)j);
     for (;;) {
       RawReqs r = ns;
       if (!pref.empty()) r.insert(r.end(), pref[0].second.begin(), pref[0].second.end());
@@ -912,9 +1310,21 @@ int32_t CompileSolve(const kp_solve_in* in, Compiled& cp) {
         if (x.key == kHostname) return fail(KP_E_UNSUPPORTED, "hostname requirement on pod");
       db.addReqs(r);
       levels[s].push_back(std::move(r));
-      if (req.size() > 1) req.erase(req.begin());
-      else if (!pref.empty()) pref.erase(pref.begin());
-      else break;
+      RawReqs strict = ns;  // NewStrictPodRequirements: without the preferred term
+      if (!req.empty()) strict.insert(strict.end(), req[0].begin(), req[0].end());
+      strict_levels[s].push_back(std::move(strict));
+      spread_levels[s].push_back(spreads);
+      if (req.size() > 1) {
+        req.erase(req.begin());
+      } else if (!pref.empty()) {
+        pref.erase(pref.begin());
+      } else {  // removeTopologySpreadScheduleAnyway: first ScheduleAnyway constraint, swapped with the last
+        size_t i = 0;
+        while (i < spreads.size() && sh.topology_spread[spreads[i]].when_unsatisfiable != KP_SCHEDULE_ANYWAY) i++;
+        if (i == spreads.size()) break;
+        spreads[i] = spreads.back();
+        spreads.pop_back();
+      }
     }
   }
   // existing nodes
@@ -975,6 +1385,8 @@ int32_t CompileSolve(const kp_solve_in* in, Compiled& cp) {
     tsets[v] = id;
     return id;
   };
+  vector<int> np_taintset(in->n_nodepools);
+  for (uint32_t i = 0; i < in->n_nodepools; i++) np_taintset[i] = tset(np_taints[i]);
   // templates: weight desc, name asc; pre-filter options with empty requests (upstream NewScheduler)
   vector<int> order(in->n_nodepools);
   for (uint32_t i = 0; i < in->n_nodepools; i++) order[i] = (int)i;
@@ -1093,6 +1505,8 @@ int32_t CompileSolve(const kp_solve_in* in, Compiled& cp) {
     }
   }
   if (cp.pvp.empty()) cp.pvp.assign(TW, 0);
+  rc = CompileTopology(in, cp, strict_levels, spread_levels, np_taintset);
+  if (rc) return rc;
   // pods: Queue order byCPUAndMemoryDescending (cpu desc, memory desc, creation asc, uid asc)
   cp.pod_shape.resize(in->n_pods);
   cp.queue.resize(in->n_pods);
@@ -1180,7 +1594,7 @@ struct kp_solve_plan {
   SolveArgs a;
   size_t o_mut = 0, n_mut = 0, o_pristine = 0, o_ver = 0, n_ver = 0, o_fail = 0, n_fail = 0;
   size_t o_stats = 0, o_npods = 0, o_place = 0, o_events = 0, o_nct = 0, o_ncrq = 0, o_opts = 0, o_nrem = 0,
-         o_nopt = 0, o_ncr = 0;
+         o_nopt = 0, o_ncr = 0, o_hcnc = 0, n_hcnc = 0;
   int opt_stride = 0, P = 0, Pc = 1;
   uint32_t max_types = 0;
   bool any_min = false;
@@ -1235,6 +1649,14 @@ int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out
   const size_t o_tlp = blob.put(C.tmpl_limit_present);
   const size_t o_exts = blob.put(C.ex_taintset);
   const size_t o_exav = blob.put(C.ex_available);
+  // topology (read-only part)
+  const size_t o_tgk = blob.put(C.tg_key), o_tgr = blob.put(C.tg_row), o_tgs = blob.put(C.tg_maxskew),
+               o_tgm = blob.put(C.tg_mindom), o_tga = blob.put(C.tg_aff), o_tgtb = blob.put(C.tg_term_base),
+               o_tgft = blob.put(C.tg_filt_tol), o_tgt = blob.put(C.tg_terms), o_tgtn = blob.put(C.tg_terms_negop),
+               o_srb = blob.put(C.shape_rec_base), o_srn = blob.put(C.shape_rec_n), o_recl = blob.put(C.rec_list),
+               o_slob = blob.put(C.sl_own_base), o_slon = blob.put(C.sl_own_n), o_owng = blob.put(C.own_group),
+               o_owns = blob.put(C.own_self), o_ownp = blob.put(C.own_pd), o_sltk = blob.put(C.sl_topo_keys),
+               o_tks = blob.put(C.tkey_slot), o_extc = blob.put(C.ex_tcode);
   // ---- mutable state: restored from a pristine device copy before every run ----
   vector<int32_t> zeros_p(Pc, 0);
   const size_t o_mut = blob.reserve(0);
@@ -1245,6 +1667,9 @@ int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out
   const size_t o_trem = blob.put(C.tmpl_remaining);
   const size_t o_exr = blob.put(C.ex_reqs);
   const size_t o_exrq = blob.put(C.ex_requests);
+  const size_t o_tgc = blob.put(C.tg_cnt);
+  const size_t o_tgreg = blob.put(C.tg_reg);
+  const size_t o_hcx = blob.put(C.hcnt0);
   const size_t n_mut = blob.host.size() - o_mut;
   const size_t host_bytes = blob.host.size();
   const size_t o_pristine = blob.reserve(n_mut);
@@ -1278,6 +1703,8 @@ int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out
   const size_t o_opts = blob.reserve(sizeof(uint32_t) * (size_t)Pc * opt_stride);
   const size_t o_nrem = blob.reserve(sizeof(uint32_t) * Pc);
   const size_t o_nopt = blob.reserve(sizeof(uint32_t) * Pc);
+  const size_t n_hcnc = (size_t)C.GH * Pc;
+  const size_t o_hcnc = blob.reserve(std::max<size_t>(n_hcnc, 1));
   const size_t total_bytes = blob.host.size();
 
   HIPCHK(hipMalloc(&plan->buf.p, total_bytes));
@@ -1349,6 +1776,34 @@ int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out
   for (size_t i = 0; i < C.tmpl_daemon.size(); i++)  // Fits iterates every resource of the merged requests
     if (C.tmpl_daemon[i] > 0) a.req_res_mask |= 1u << (i % KP_NRES);
   a.timing = getenv("KP_TIMING") ? 1 : 0;
+  a.n_groups = C.G;
+  a.tg_key = (const int32_t*)(base + o_tgk);
+  a.tg_row = (const int32_t*)(base + o_tgr);
+  a.tg_maxskew = (const int32_t*)(base + o_tgs);
+  a.tg_mindom = (const int32_t*)(base + o_tgm);
+  a.tg_aff = (const int32_t*)(base + o_tga);
+  a.tg_term_base = (const int32_t*)(base + o_tgtb);
+  a.tg_filt_tol = (const uint64_t*)(base + o_tgft);
+  a.tg_terms = base + o_tgt;
+  a.tg_terms_negop = (const uint64_t*)(base + o_tgtn);
+  a.tg_cnt = (int32_t*)(base + o_tgc);
+  a.tg_reg = (uint64_t*)(base + o_tgreg);
+  a.hcnt_ex = base + o_hcx;
+  a.hcnt_nc = base + o_hcnc;
+  a.hnc_stride = Pc;
+  a.shape_rec_base = (const int32_t*)(base + o_srb);
+  a.shape_rec_n = (const int32_t*)(base + o_srn);
+  a.rec_list = (const int32_t*)(base + o_recl);
+  a.sl_own_base = (const int32_t*)(base + o_slob);
+  a.sl_own_n = (const int32_t*)(base + o_slon);
+  a.own_group = (const int32_t*)(base + o_owng);
+  a.own_self = (const int32_t*)(base + o_owns);
+  a.own_pd = (const uint64_t*)(base + o_ownp);
+  a.sl_topo_keys = (const uint64_t*)(base + o_sltk);
+  a.tkey_slot = (const int32_t*)(base + o_tks);
+  a.ex_tcode = base + o_extc;
+  plan->o_hcnc = o_hcnc;
+  plan->n_hcnc = n_hcnc;
   a.placement = (int32_t*)(base + o_place);
   a.events = (int32_t*)(base + o_events);
   a.stats = (uint64_t*)(base + o_stats);
@@ -1400,6 +1855,7 @@ int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out) {
   HIPCHK(hipMemsetAsync(base + plan->o_place, 0xFF, sizeof(int32_t) * Pc, st));
   HIPCHK(hipMemsetAsync(base + plan->o_ver, 0, plan->n_ver, st));
   HIPCHK(hipMemsetAsync(base + plan->o_fail, 0xFF, plan->n_fail, st));
+  if (plan->n_hcnc) HIPCHK(hipMemsetAsync(base + plan->o_hcnc, 0, plan->n_hcnc, st));
   const SolveArgs& a = plan->a;
   const size_t dyn = (size_t)2 * a.sort_cap * sizeof(int32_t);
   HIPCHK(hipEventRecord(ctx->ev0, st));
@@ -1444,7 +1900,7 @@ int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out) {
     HIPCHK(hipMemcpyAsync(nopt.data(), base + plan->o_nopt, sizeof(uint32_t) * n_nc, hipMemcpyDeviceToHost, st));
   }
   vector<KReqs> fin;
-  if (plan->any_min && n_nc) {
+  if (n_nc) {
     fin.resize(n_nc);
     HIPCHK(hipMemcpyAsync(fin.data(), base + plan->o_ncr, sizeof(KReqs) * n_nc, hipMemcpyDeviceToHost, st));
   }
@@ -1475,6 +1931,7 @@ int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out) {
       if (nc.requests.milli[r]) nc.requests.present |= 1u << r;
     }
     nc.options.assign(opts.begin() + (size_t)i * opt_stride, opts.begin() + (size_t)i * opt_stride + nopt[i]);
+    nc.reqs = DecodeReqs(d, fin[i]);
     // Truncate(reqs, max): minValues must still hold on the truncated options, else the pods fail
     if (!fin.empty() && (fin[i].hmin & fin[i].present)) {
       const HostCat& hc = C.cats[C.tmpl_catalog[nct[i]]];
@@ -1497,6 +1954,13 @@ int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out) {
   res->stats.host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   *out = res.release();
   return KP_OK;
+}
+
+// Host half of kp_solve_prepare without a device: the Go shim's "can the device path take this batch" probe.
+int32_t kp_solve_validate(const kp_solve_in* in) {
+  if (!in) return fail(KP_E_INVAL, "null argument");
+  Compiled C;
+  return CompileSolve(in, C);
 }
 
 int32_t kp_solve(kp_ctx* ctx, const kp_solve_in* in, kp_solve_result** out) {
@@ -1524,6 +1988,9 @@ int32_t kp_result_nodeclaim(const kp_solve_result* r, uint32_t i, kp_nodeclaim_i
   out->pods = n.pods.data();
   out->options = n.options.data();
   out->requests = n.requests;
+  out->requirements.items = n.reqs ? n.reqs->items.data() : nullptr;
+  out->requirements.n = n.reqs ? (uint32_t)n.reqs->items.size() : 0;
+  out->requirements.reserved_ = 0;
   return KP_OK;
 }
 int32_t kp_result_stats(const kp_solve_result* r, kp_solve_stats* out) {
@@ -1692,6 +2159,9 @@ int32_t kp_cluster_prepare(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan** 
   if (!ctx || !cl || !out) return fail(KP_E_INVAL, "null argument");
   if (cl->spot_to_spot) return fail(KP_E_UNSUPPORTED, "SpotToSpotConsolidation feature gate");
   if (cl->n_nodes && !cl->nodes) return fail(KP_E_INVAL, "null nodes");
+  for (uint32_t i = 0; i < cl->n_shapes; i++)
+    if (cl->shapes[i].n_topology_spread)
+      return fail(KP_E_UNSUPPORTED, "topology spread in consolidation simulations (cluster pods are not bound pods)");
   std::lock_guard<std::mutex> lock(ctx->mu);
   HIPCHK(hipSetDevice(ctx->device));
   auto plan = std::make_unique<kp_cluster_plan>();
@@ -1828,6 +2298,14 @@ int32_t kp_cluster_prepare(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan** 
   const size_t o_excode = blob.put(ex_code);
   const size_t o_exts = blob.put(C.ex_taintset);
   const size_t o_exav = blob.put(C.ex_available);
+  // topology (read-only part)
+  const size_t o_tgk = blob.put(C.tg_key), o_tgr = blob.put(C.tg_row), o_tgs = blob.put(C.tg_maxskew),
+               o_tgm = blob.put(C.tg_mindom), o_tga = blob.put(C.tg_aff), o_tgtb = blob.put(C.tg_term_base),
+               o_tgft = blob.put(C.tg_filt_tol), o_tgt = blob.put(C.tg_terms), o_tgtn = blob.put(C.tg_terms_negop),
+               o_srb = blob.put(C.shape_rec_base), o_srn = blob.put(C.shape_rec_n), o_recl = blob.put(C.rec_list),
+               o_slob = blob.put(C.sl_own_base), o_slon = blob.put(C.sl_own_n), o_owng = blob.put(C.own_group),
+               o_owns = blob.put(C.own_self), o_ownp = blob.put(C.own_pd), o_sltk = blob.put(C.sl_topo_keys),
+               o_tks = blob.put(C.tkey_slot), o_extc = blob.put(C.ex_tcode);
   const size_t o_exrq = blob.put(C.ex_requests);
   const size_t o_exin = blob.put(ex_init);
   const size_t o_pshape = blob.put(C.pod_shape);

@@ -297,7 +297,7 @@ __device__ uint64_t filter_types(const DevDict& D, const DevCatalog& Cg, const R
                                  uint64_t pod_keys, const uint64_t* pvp, const int32_t* pvp_slot, const int64_t* reqrow,
                                  const int64_t* s_preq, const int64_t* const* fitv, uint32_t rmask,
                                  const int64_t* vint, uint32_t* scratch, uint64_t* bytes, const int32_t* jstart,
-                                 int32_t* jout) {
+                                 int32_t* jout, uint64_t generic_keys = 0) {
   const int lane = LANE;
   const int TW = D.TW;
   const uint64_t negM = negop_mask(rv.present, rv.compl_, rv.nz);
@@ -309,14 +309,14 @@ __device__ uint64_t filter_types(const DevDict& D, const DevCatalog& Cg, const R
     const int k = __builtin_ctzll(keys);
     keys &= keys - 1;
     const bool ng = (negM >> k) & 1;
-    if ((D.single_valued >> k) & 1) {
+    if (((D.single_valued & ~generic_keys) >> k) & 1) {
       // X ⊆ Pass(candidate_k) and Has_merged = Has_candidate ∧ Has_pod, so for single-valued keys
       // X ∩ ∪_{Has_merged(v)} TM[v] = X ∩ ∪_{Has_pod(v)} TM[v] (precomputed PVP row, incl. NOKEY)
       uint64_t p = lane < TW ? pvp[(size_t)pvp_slot[k] * TW + lane] : 0;
       if (ng && lane < TW) p |= Cg.DNE[(size_t)k * TW + lane];
       X &= p;
       nb += (uint64_t)TW * 8 * (ng ? 2 : 1);
-    } else {
+    } else {  // multi-valued keys, and keys narrowed by topology (Has_merged is no longer Has_pod there)
       uint64_t acc = lane < TW ? Cg.NOKEY[(size_t)k * TW + lane] : 0;
       if (ng && lane < TW) acc |= Cg.DNE[(size_t)k * TW + lane];
       const int nw = (D.nval[k] + 63) >> 6;
@@ -394,6 +394,64 @@ struct NCSort {
   }
 };
 #include "kp_pdqsort.h"
+
+// ------------------------------------------------------------------------------------------------
+// topology spread (upstream Topology.AddRequirements / TopologyGroup.nextDomainTopologySpread / Record)
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ int wave_min_i32(int v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const int w = __shfl_xor(v, o, 64);
+    v = w < v ? w : v;
+  }
+  return v;
+}
+
+// Per-pod staging of one owned group: s_tg = {group, self, key, hostname row, maxSkew, key slot}. For a
+// dictionary key, acc = registered domains d with count(d) + self - min <= maxSkew, where min is
+// domainMinCount over the registered domains podDomains admits (minDomains -> 0); the counts go to LDS.
+struct TopoOwn {
+  int32_t g, self, key, row, maxskew, slot;
+};
+
+// AddRequirements + Compatible + Add for the owned dictionary-key groups on the merged requirements of one
+// candidate (one wave): each group picks, among its acceptable domains that the candidate's requirements
+// admit (nodeDomains; Exists when the key is absent), the one with the lowest count, ties to the lowest
+// value ordinal (= byte order, the written spec for upstream's map-order tie); the key narrows to In{d}.
+__device__ bool topo_narrow(const DevDict& D, int n, const TopoOwn* own, const uint64_t* acc, const int32_t (*cnt)[64],
+                            bool allow_wk, uint64_t& m_v, ReqView& rv, const int64_t* vint) {
+  const int lane = LANE;
+  const uint64_t allowed = allowed_word(D, rv, m_v, vint);
+  uint64_t narrowed = 0, nv = m_v;
+  for (int j = 0; j < n; j++) {
+    const int k = own[j].key;
+    if (k < 0) continue;  // hostname: checked exactly by the pre-pass (a fresh node always passes)
+    const uint64_t kb = 1ull << k;
+    const bool present = (rv.present & kb) != 0;
+    if (!present && !(allow_wk && (D.wellknown & kb))) return false;  // topology key undefined on the node
+    const uint64_t aN = present ? lane_bcast(allowed, k) : D.validbits[k];
+    const uint64_t cand = acc[j] & aN;
+    if (!cand) return false;
+    const bool in = (cand >> lane) & 1;
+    const int c = in ? cnt[j][lane] : INT32_MAX;
+    const int mc = wave_min_i32(c);
+    const int d = __builtin_ctzll(__ballot(in && c == mc));
+    if (narrowed & kb) {
+      if (lane_bcast(nv, k) != (1ull << d)) return false;  // two groups on one key chose different domains
+    } else if (lane == k) {
+      nv = 1ull << d;
+    }
+    narrowed |= kb;
+  }
+  m_v = nv;
+  rv.present |= narrowed;
+  rv.compl_ &= ~narrowed;
+  rv.hgt &= ~narrowed;
+  rv.hlt &= ~narrowed;
+  rv.nz |= narrowed;
+  rv.dne &= ~narrowed;
+  return true;
+}
 
 // ------------------------------------------------------------------------------------------------
 // solve_kernel: one workgroup runs one Solve.
@@ -563,6 +621,9 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
   __shared__ const int64_t* s_fitp[KP_NRES];   // fit threshold values per resource: LDS copy or global
   __shared__ const int64_t* s_fitg[8][KP_NRES];  // same, global, for catalogues 1..7
   __shared__ int64_t s_fitv[FITV_RES][FITV_CAP];
+  __shared__ TopoOwn s_town[8];                 // owned topology groups of the popped pod (staged per pod)
+  __shared__ uint64_t s_tacc[8];
+  __shared__ int32_t s_tcnt[8][64];
   extern __shared__ int32_t s_dyn[];  // ord[a.sort_cap], npods[a.sort_cap] while n_nc <= a.sort_cap
 
   const int tid = threadIdx.x;
@@ -645,9 +706,40 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
     TS(0);
     const KReqs* B = &s_B;
     const uint64_t b_negop = a.shape_negop[sl];
-    const uint64_t b_keys = s_B.present;
     const uint64_t tolmask = a.shape_tolerates[shape];
     int placed = -1;  // >= 0 NodeClaim id; <= -2 existing node; -1 not placed
+    // ---- topology: stage the owned groups (one wave each) -----------------------------------------
+    const int own_n = a.n_groups ? a.sl_own_n[sl] : 0;
+    const uint64_t topo_keys = own_n ? a.sl_topo_keys[sl] : 0;
+    const uint64_t b_keys = s_B.present | topo_keys;  // keys whose type filter must be redone on Add
+    if (own_n) {
+      for (int j = wave; j < own_n; j += NW) {
+        const int oi = a.sl_own_base[sl] + j;
+        const int g = a.own_group[oi];
+        const int self = a.own_self[oi];
+        const int k = a.tg_key[g];
+        const int mskew = a.tg_maxskew[g];
+        uint64_t acc = 0;
+        if (k >= 0) {
+          const int c = a.tg_cnt[(size_t)g * 64 + lane];
+          const uint64_t reg = a.tg_reg[g], pd = a.own_pd[oi];
+          const bool sup = ((reg & pd) >> lane) & 1;
+          const int mn = wave_min_i32(sup ? c : INT32_MAX);
+          const int num = __builtin_popcountll(reg & pd);
+          int64_t m = num ? (int64_t)mn : (int64_t)INT32_MAX;
+          const int mind = a.tg_mindom[g];
+          if (mind > 0 && num < mind) m = 0;
+          acc = __ballot(((reg >> lane) & 1) && (int64_t)c + self - m <= mskew);
+          s_tcnt[j][lane] = c;
+          bytes += 64 * 4 + 16;
+        }
+        if (lane == 0) {
+          s_town[j] = TopoOwn{g, self, k, a.tg_row[g], mskew, k >= 0 ? a.tkey_slot[k] : -1};
+          s_tacc[j] = acc;
+        }
+      }
+      __syncthreads();
+    }
 
     // ---- addToExistingNode: lowest index whose CanAdd succeeds -------------------------------
     for (int base = 0; base < a.n_existing && placed == -1; base += NT) {
@@ -659,6 +751,17 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
         bool fits = true;  // Fits(Merge(requests, pod), available): CanAdd's resource check, exact
         for (int r = 0; r < KP_NRES; r++) fits = fits && av[r] >= 0 && rq[r] + s_preq[r] <= av[r];
         cand = fits;
+        // topology, exact: the node's domain for a dictionary key is its label value (or the key is
+        // undefined on it: incompatible); hostname: count + self <= maxSkew (min is 0 for hostname)
+        for (int j = 0; j < own_n && cand; j++) {
+          const TopoOwn& o = s_town[j];
+          if (o.key >= 0) {
+            const uint8_t code = a.ex_tcode[(size_t)o.slot * a.n_existing + e];
+            cand = code != 0xFF && ((s_tacc[j] >> code) & 1);
+          } else {
+            cand = (int)a.hcnt_ex[(size_t)o.row * a.n_existing + e] + o.self <= o.maxskew;
+          }
+        }
       }
       const int n = compact_candidates<NW>(cand, e, s_list, s_wcnt);
       bytes += (uint64_t)min(NT, a.n_existing - base) * (2 * KP_NRES * 8 + 8);
@@ -674,6 +777,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
           ok = merge_compatible(D, kreq_at(a.ex_reqs, ei), B, b_negop, false, m_v, rv, &slots[wave], a.vint);
           bytes += sizeof(KReqs);
           if (!ok && lane == 0) a.ex_fail[(size_t)sl * a.n_existing + ei] = a.ex_ver[ei];
+          if (ok && own_n) ok = topo_narrow(D, own_n, s_town, s_tacc, s_tcnt, false, m_v, rv, a.vint);  // not memoised
         }
         if (lane == 0) s_ok[wave] = ok ? 1 : 0;
         __syncthreads();
@@ -715,6 +819,9 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
             for (int r = 0; r < KP_NRES; r++)
               if (((a.req_res_mask >> r) & 1) && rq[r] + s_preq[r] > mx[r]) cand = false;
           }
+          for (int j = 0; j < own_n && cand; j++)  // hostname topologies, exact
+            if (s_town[j].key < 0)
+              cand = (int)a.hcnt_nc[(size_t)s_town[j].row * a.hnc_stride + nc] + s_town[j].self <= s_town[j].maxskew;
         }
         const int n = compact_candidates<NW>(cand, i, s_list, s_wcnt);
         TS(6);
@@ -732,16 +839,18 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
             attempts++;
             ok = merge_compatible(D, kreq_at(a.nc_reqs, nc), B, b_negop, true, m_v, rv, &slots[wave], a.vint);
             bytes += sizeof(KReqs);
+            bool memo = !ok || !own_n;  // failures after the topology step depend on the counts
+            if (ok && own_n) ok = topo_narrow(D, own_n, s_town, s_tacc, s_tcnt, true, m_v, rv, a.vint);
             if (ok) {
               X = lane < D.TW ? a.nc_X[(size_t)nc * D.TW + lane] : 0;
               const uint64_t* pvp = a.shape_pvp + (size_t)a.pvp_base[sl * a.n_catalogs + cat] * D.TW;
               X = filter_types(D, a.cats[cat], rv, m_v, X, b_keys, pvp, s_pslot, a.nc_requests + (size_t)nc * KP_NRES,
                                s_preq, s_fitp, a.req_res_mask, a.vint, s_scratch[wave], &bytes,
-                               a.nc_fitj + (size_t)nc * KP_NRES, s_fitj[wave]);
+                               a.nc_fitj + (size_t)nc * KP_NRES, s_fitj[wave], topo_keys);
               ok = __ballot(X != 0) != 0;
               bytes += (uint64_t)D.TW * 8 + KP_NRES * 8;
             }
-            if (!ok && lane == 0 && nc < a.ncc) a.nc_fail[(size_t)sl * a.ncc + nc] = a.nc_ver[nc];
+            if (!ok && memo && lane == 0 && nc < a.ncc) a.nc_fail[(size_t)sl * a.ncc + nc] = a.nc_ver[nc];
           }
           if (lane == 0) s_ok[wave] = ok ? 1 : 0;
           __syncthreads();
@@ -805,18 +914,21 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
               X = keep;
               bytes += (uint64_t)D.T * 8;
             }
+            bool memo = true;
             if (__ballot(X != 0)) {
               attempts++;
               ok = merge_compatible(D, kreq_at(a.tmpl_reqs, tm), B, b_negop, true, m_v, rv, &slots[wave], a.vint);
+              memo = !ok || !own_n;
+              if (ok && own_n) ok = topo_narrow(D, own_n, s_town, s_tacc, s_tcnt, true, m_v, rv, a.vint);
               if (ok) {
                 const uint64_t* pvp = a.shape_pvp + (size_t)a.pvp_base[sl * a.n_catalogs + cat] * D.TW;
                 X = filter_types(D, Cg, rv, m_v, X, b_keys, pvp, s_pslot, a.tmpl_daemon + (size_t)tm * KP_NRES, s_preq,
                                  cat == 0 ? s_fitp : s_fitg[cat & 7], a.req_res_mask, a.vint, s_scratch[wave], &bytes,
-                                 nullptr, s_fitj[wave]);
+                                 nullptr, s_fitj[wave], topo_keys);
                 ok = __ballot(X != 0) != 0;
               }
             }
-            if (!ok && lane == 0) a.tmpl_fail[(size_t)sl * a.n_tmpl + tm] = a.tmpl_ver[tm];
+            if (!ok && memo && lane == 0) a.tmpl_fail[(size_t)sl * a.n_tmpl + tm] = a.tmpl_ver[tm];
           }
           if (lane == 0) s_ok[wave] = ok ? 1 : 0;
           __syncthreads();
@@ -884,6 +996,42 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
       }
     }
 
+    // ---- Topology.Record: every group selecting the pod whose node filter admits the node counts it
+    //      in the node's domain (dictionary keys: only once the key is a single value) -------------
+    if (placed != -1 && a.n_groups && wave == 0) {
+      const int rn = a.shape_rec_n[shape];
+      const bool ex = placed <= -2;
+      const int idx = ex ? -2 - placed : placed;
+      const KReqs* fin = ex ? kreq_at(a.ex_reqs, idx) : kreq_at(a.nc_reqs, idx);
+      const int ts = ex ? a.ex_taintset[idx] : a.nc_taintset[idx];
+      for (int i = 0; i < rn; i++) {
+        const int g = a.rec_list[a.shape_rec_base[shape] + i];
+        bool ok = (a.tg_filt_tol[g] >> ts) & 1;
+        if (ok && a.tg_aff[g]) {  // TopologyNodeFilter.MatchesRequirements: Compatible(node reqs, term)
+          const int tb = a.tg_term_base[g];
+          uint64_t mv;
+          ReqView rv;
+          ok = merge_compatible(D, fin, kreq_at(a.tg_terms, tb), a.tg_terms_negop[tb], !ex, mv, rv, &slots[0], a.vint);
+        }
+        if (!ok) continue;
+        const int row = a.tg_row[g];
+        if (row >= 0) {
+          if (lane == 0) {
+            uint8_t* c = ex ? &a.hcnt_ex[(size_t)row * a.n_existing + idx] : &a.hcnt_nc[(size_t)row * a.hnc_stride + idx];
+            if (*c < 255) *c += 1;
+          }
+        } else {
+          const int k = a.tg_key[g];
+          const uint64_t v = fin->vals[k];
+          if (((fin->present >> k) & 1) && !((fin->compl_ >> k) & 1) && __builtin_popcountll(v) == 1 && lane == 0) {
+            const int d = __builtin_ctzll(v);
+            a.tg_cnt[(size_t)g * 64 + d] += 1;
+            a.tg_reg[g] |= 1ull << d;
+          }
+        }
+        bytes += 16;
+      }
+    }  // (the bookkeeping barrier below publishes the counts before the next pod stages them)
     TS(4);
     // ---- bookkeeping (thread 0): placement, or Preferences.Relax + Queue.Push -------------------
     if (tid == 0) {

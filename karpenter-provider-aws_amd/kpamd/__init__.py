@@ -48,6 +48,7 @@ def load_lib(path=LIB_PATH):
         "kp_filter_compatible_available": (C.c_int32, [C.c_void_p, C.c_void_p, P(abi.FeasibilityQuery), C.c_uint32,
                                                        P(C.c_uint64), P(C.c_double), P(abi.SolveStats)]),
         "kp_solve": (C.c_int32, [C.c_void_p, P(abi.SolveIn), P(C.c_void_p)]),
+        "kp_solve_validate": (C.c_int32, [P(abi.SolveIn)]),
         "kp_solve_prepare": (C.c_int32, [C.c_void_p, P(abi.SolveIn), P(C.c_void_p)]),
         "kp_solve_run": (C.c_int32, [C.c_void_p, P(C.c_void_p)]),
         "kp_solve_plan_destroy": (None, [C.c_void_p]),
@@ -122,6 +123,23 @@ class Catalog:
             pass
 
 
+def validate(problem):
+    """kp_solve_validate: host compile of the batch without a device (KP_OK or the error kp_solve would give)."""
+    lib = load_lib()
+    arena = Arena()
+    handles = []
+    for c in problem.catalogs:
+        h = C.c_void_p()
+        _check(lib, lib.kp_catalog_upload(None, C.byref(arena.catalog_desc(c)), 0, C.byref(h)))
+        handles.append(h)
+    try:
+        si = abi.build_solve_in(arena, problem, catalog_handles=[h.value for h in handles])
+        return lib.kp_solve_validate(C.byref(si))
+    finally:
+        for h in handles:
+            lib.kp_catalog_destroy(h)
+
+
 def read_result(lib, res, n_pods, prefix="kp_result_"):
     """Copy a (kp|kpo)_solve_result into plain Python: placement + NodeClaims in creation order."""
     get = lambda n: getattr(lib, prefix + n)
@@ -138,6 +156,7 @@ def read_result(lib, res, n_pods, prefix="kp_result_"):
             "pods": [int(info.pods[j]) for j in range(info.n_pods)],
             "options": [int(info.options[j]) for j in range(info.n_options)],
             "n_remaining": int(info.n_remaining),
+            "requirements": abi.read_requirements(info.requirements),
         })
     st = abi.SolveStats()
     get("stats")(res, C.byref(st))

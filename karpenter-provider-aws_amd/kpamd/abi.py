@@ -16,6 +16,17 @@ RES_NAMES = ["cpu", "memory", "ephemeral-storage", "pods", "vpc.amazonaws.com/po
              "habana.ai/gaudi", "vpc.amazonaws.com/PrivateIPv4Address"]
 RES_INDEX = {n: i for i, n in enumerate(RES_NAMES)}
 OPS = {"In": 0, "NotIn": 1, "Exists": 2, "DoesNotExist": 3, "Gt": 4, "Lt": 5}
+OP_NAMES = {v: k for k, v in OPS.items()}
+
+
+def read_requirements(r):
+    """kp_requirements -> [(key, op, [values], minValues|None)]"""
+    out = []
+    for i in range(r.n):
+        q = r.items[i]
+        vals = [q.values[j].decode() for j in range(q.n_values)]
+        out.append((q.key.decode(), OP_NAMES[q.op], vals, None if q.min_values < 0 else int(q.min_values)))
+    return out
 EFFECTS = {"": 0, "NoSchedule": 1, "PreferNoSchedule": 2, "NoExecute": 3}
 TOL_OPS = {"Equal": 0, "": 0, "Exists": 1}
 
@@ -72,12 +83,40 @@ class PreferredTerm(C.Structure):
     _fields_ = [("weight", C.c_int32), ("reserved_", C.c_int32), ("preference", Requirements)]
 
 
+SEL_OPS = {"In": 0, "NotIn": 1, "Exists": 2, "DoesNotExist": 3}
+WHEN = {"DoNotSchedule": 0, "ScheduleAnyway": 1}
+POLICY = {None: 0, "Honor": 1, "Ignore": 2}
+
+
+class SelectorRequirement(C.Structure):
+    _fields_ = [("key", C.c_char_p), ("op", C.c_int32), ("n_values", C.c_uint32), ("values", C.POINTER(C.c_char_p))]
+
+
+class LabelSelector(C.Structure):
+    _fields_ = [("match_labels", C.POINTER(Label)), ("n_match_labels", C.c_uint32),
+                ("n_match_expressions", C.c_uint32), ("match_expressions", C.POINTER(SelectorRequirement)),
+                ("is_nil", C.c_int32), ("reserved_", C.c_int32)]
+
+
+class TopologySpread(C.Structure):
+    _fields_ = [("topology_key", C.c_char_p), ("max_skew", C.c_int32), ("min_domains", C.c_int32),
+                ("when_unsatisfiable", C.c_int32), ("node_affinity_policy", C.c_int32),
+                ("node_taints_policy", C.c_int32), ("reserved_", C.c_int32), ("selector", LabelSelector)]
+
+
 class PodShape(C.Structure):
     _fields_ = [("requests", ResourceList), ("node_selector", C.POINTER(Label)), ("n_node_selector", C.c_uint32),
                 ("n_required_terms", C.c_uint32), ("required_terms", C.POINTER(Requirements)),
                 ("preferred_terms", C.POINTER(PreferredTerm)), ("n_preferred_terms", C.c_uint32),
                 ("n_tolerations", C.c_uint32), ("tolerations", C.POINTER(Toleration)),
-                ("n_topology_spread", C.c_uint32), ("reserved_", C.c_uint32)]
+                ("n_topology_spread", C.c_uint32), ("n_labels", C.c_uint32),
+                ("topology_spread", C.POINTER(TopologySpread)), ("namespace_", C.c_char_p),
+                ("labels", C.POINTER(Label))]
+
+
+class BoundPod(C.Structure):
+    _fields_ = [("namespace_", C.c_char_p), ("labels", C.POINTER(Label)), ("n_labels", C.c_uint32),
+                ("node", C.c_uint32)]
 
 
 class Pod(C.Structure):
@@ -95,13 +134,14 @@ class SolveIn(C.Structure):
                 ("n_catalogs", C.c_uint32), ("n_nodepools", C.c_uint32), ("nodepools", C.POINTER(NodePool)),
                 ("existing", C.POINTER(ExistingNode)), ("n_existing", C.c_uint32), ("n_shapes", C.c_uint32),
                 ("shapes", C.POINTER(PodShape)), ("pods", C.POINTER(Pod)), ("n_pods", C.c_uint32),
-                ("max_instance_types", C.c_uint32)]
+                ("max_instance_types", C.c_uint32), ("bound_pods", C.POINTER(BoundPod)),
+                ("n_bound_pods", C.c_uint32), ("reserved_", C.c_uint32)]
 
 
 class NodeClaimInfo(C.Structure):
     _fields_ = [("nodepool", C.c_uint32), ("n_pods", C.c_uint32), ("n_remaining", C.c_uint32),
                 ("n_options", C.c_uint32), ("pods", C.POINTER(C.c_uint32)), ("options", C.POINTER(C.c_uint32)),
-                ("requests", ResourceList)]
+                ("requests", ResourceList), ("requirements", Requirements)]
 
 
 class SolveStats(C.Structure):
@@ -241,8 +281,34 @@ class Arena:
         terms = self.arr(Requirements, [self.requirements(t) for t in sh.required_terms])
         prefs = self.arr(PreferredTerm, [PreferredTerm(int(w), 0, self.requirements(t)) for w, t in sh.preferred_terms])
         tols, ntol = self.tolerations(sh.tolerations)
+        spreads = self.arr(TopologySpread, [self.spread(t) for t in sh.topology_spread])
+        labels, nl = self.labels(sh.labels)
         return PodShape(self.resources(sh.requests), ns, nns, len(sh.required_terms), terms, prefs,
-                        len(sh.preferred_terms), ntol, tols, 0, 0)
+                        len(sh.preferred_terms), ntol, tols, len(sh.topology_spread), nl, spreads,
+                        self.s(sh.namespace), labels)
+
+    def selector(self, sel):
+        if sel is None:
+            return LabelSelector(None, 0, 0, None, 1, 0)
+        ml, nml = self.labels(sel.match_labels)
+        exprs = []
+        for key, op, values in sel.match_expressions:
+            vals = self.arr(C.c_char_p, [self.s(v) for v in values])
+            exprs.append(SelectorRequirement(self.s(key), SEL_OPS[op], len(values), vals))
+        ex = self.arr(SelectorRequirement, exprs)
+        return LabelSelector(ml, nml, len(exprs), ex, 0, 0)
+
+    def spread(self, t):
+        return TopologySpread(self.s(t.topology_key), int(t.max_skew), int(t.min_domains or 0),
+                              WHEN[t.when_unsatisfiable], POLICY[t.node_affinity_policy],
+                              POLICY[t.node_taints_policy], 0, self.selector(t.selector))
+
+    def bound_pods(self, bps):
+        out = []
+        for ns, labels, node in bps:
+            la, nl = self.labels(labels)
+            out.append(BoundPod(self.s(ns), la, nl, int(node)))
+        return self.arr(BoundPod, out), len(bps)
 
     def existing_node(self, n):
         labels, nl = self.labels(n.labels)
@@ -265,8 +331,10 @@ def build_solve_in(arena, problem, catalog_handles=None):
     pods_np["u"] = problem.pod_uid
     arena.keep.append(pods_np)
     pods_ptr = pods_np.ctypes.data_as(C.POINTER(Pod))
+    bps, nbp = arena.bound_pods(problem.bound_pods)
     si = SolveIn(handles, descs, len(problem.catalogs), len(problem.nodepools), nps, ex, len(problem.existing),
-                 len(problem.shapes), shapes, pods_ptr, len(problem.pod_shape), problem.max_instance_types)
+                 len(problem.shapes), shapes, pods_ptr, len(problem.pod_shape), problem.max_instance_types,
+                 bps, nbp, 0)
     arena.keep.append(si)
     return si
 

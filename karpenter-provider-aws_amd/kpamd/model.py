@@ -59,12 +59,34 @@ class NodePool:
 
 
 @dataclass
+class LabelSelector:
+    """metav1.LabelSelector; match_expressions are (key, "In"|"NotIn"|"Exists"|"DoesNotExist", [values])."""
+    match_labels: Dict[str, str] = field(default_factory=dict)
+    match_expressions: List[Tuple[str, str, List[str]]] = field(default_factory=list)
+
+
+@dataclass
+class TopologySpread:
+    """corev1.TopologySpreadConstraint. selector None = nil (selects nothing)."""
+    topology_key: str
+    max_skew: int = 1
+    selector: Optional[LabelSelector] = None
+    when_unsatisfiable: str = "DoNotSchedule"
+    min_domains: Optional[int] = None
+    node_affinity_policy: Optional[str] = None  # None = Honor
+    node_taints_policy: Optional[str] = None    # None = Ignore
+
+
+@dataclass
 class PodShape:
     requests: Dict[str, int]
     node_selector: Dict[str, str] = field(default_factory=dict)
     required_terms: List[List[Req]] = field(default_factory=list)
     preferred_terms: List[Tuple[int, List[Req]]] = field(default_factory=list)
     tolerations: List[Tuple[str, str, str, str]] = field(default_factory=list)  # (key, op, value, effect)
+    topology_spread: List[TopologySpread] = field(default_factory=list)
+    labels: Dict[str, str] = field(default_factory=dict)
+    namespace: str = "default"
 
 
 @dataclass
@@ -110,6 +132,7 @@ class Problem:
     existing: List[ExistingNode] = field(default_factory=list)
     max_instance_types: int = 100
     name: str = ""
+    bound_pods: List[Tuple[str, Dict[str, str], int]] = field(default_factory=list)  # (namespace, labels, existing idx)
 
     @property
     def n_pods(self):

@@ -6,7 +6,7 @@ requests include pods=1 the way resources.RequestsForPods adds it.
 import numpy as np
 
 from .catalog import ZONE_IDS, ZONES
-from .model import Cluster, ClusterNode, ExistingNode, NodePool, PodShape, Problem
+from .model import Cluster, ClusterNode, ExistingNode, LabelSelector, NodePool, PodShape, Problem, TopologySpread
 
 K = "karpenter.k8s.aws/"
 MI = 1 << 20
@@ -126,6 +126,140 @@ def config5(catalog, n_pods=1_000_000, seed=5, n_shapes=512):
         weights.append(0.25 if r <= 1 else 1.0)
     s, c, u = _pods(rng, n_pods, len(shapes), weights)
     return Problem([catalog], pools, shapes, s, c, u, name=f"config5-{n_pods}")
+
+
+# ------------------------------------------------------------------------------------------------
+# config 3: topology spread onto existing nodes
+# ------------------------------------------------------------------------------------------------
+ZONE_KEY = "topology.kubernetes.io/zone"
+HOST_KEY = "kubernetes.io/hostname"
+
+
+def _type_named(catalog, name):
+    for i, it in enumerate(catalog):
+        if it.name == name:
+            return i
+    raise KeyError(name)
+
+
+def config3(catalog, n_pods=100_000, seed=3, n_deployments=1000, n_existing=5000, prefill=0.3):
+    """100k pods of 1,000 deployments, each spread over zones (maxSkew 1) and hostnames (maxSkew 1),
+    DoNotSchedule, onto 5,000 existing m5/c5/r5 nodes (zones round-robin, ~30% of allocatable used by
+    already-bound pods of the same deployments, which seed the topology counts) plus new NodeClaims."""
+    rng = np.random.default_rng(seed)
+    sizes = rng.integers(20, 181, size=n_deployments).astype(np.float64)
+    counts = np.floor(sizes / sizes.sum() * n_pods).astype(np.int64)
+    counts[: n_pods - int(counts.sum())] += 1
+    shapes = []
+    for j in range(n_deployments):
+        app = {"app": f"dep-{j:04d}"}
+        sel = LabelSelector(match_labels=dict(app))
+        sh = PodShape(req_res(int(rng.choice([100, 250, 500, 1000, 2000])), int(rng.choice([128, 256, 512, 1024, 2048, 4096]))),
+                      labels=dict(app), namespace=f"ns-{j % 8}",
+                      topology_spread=[TopologySpread(ZONE_KEY, 1, sel), TopologySpread(HOST_KEY, 1, sel)])
+        shapes.append(sh)
+    pod_shape = np.repeat(np.arange(n_deployments, dtype=np.uint32), counts)
+    rng.shuffle(pod_shape)
+    n = len(pod_shape)
+    creation = (1_750_000_000 + rng.integers(0, 600, size=n)).astype(np.int64)
+    uid = rng.integers(0, np.iinfo(np.int64).max, size=n, dtype=np.int64).astype(np.uint64)
+    pools = [NodePool("default", 10, 0, [("kubernetes.io/os", "In", ["linux"]),
+                                         ("karpenter.sh/capacity-type", "In", ["on-demand", "spot"]),
+                                         (K + "instance-category", "In", ["c", "m", "r"]),
+                                         (K + "instance-generation", "Gt", ["4"])])]
+    kinds = [_type_named(catalog, f"{f}.{s}") for f in ("m5", "c5", "r5") for s in ("large", "xlarge", "2xlarge", "4xlarge")]
+    existing, bound = [], []
+    for e in range(n_existing):
+        ti = kinds[int(rng.integers(0, len(kinds)))]
+        it = catalog[ti]
+        name = f"node-{e:05d}"
+        labels = node_labels(it, e % 3, "on-demand", "default", name)
+        alloc = it.allocatable()
+        used = {"cpu": 0, "memory": 0, "pods": 0}
+        deps = set()
+        for _ in range(64):
+            j = int(rng.integers(0, n_deployments))
+            if j in deps:
+                continue
+            rq = shapes[j].requests
+            if any(used[r] + rq[r] > prefill * alloc[r] for r in used):
+                break
+            deps.add(j)
+            for r in used:
+                used[r] += rq[r]
+            bound.append((shapes[j].namespace, dict(shapes[j].labels), e))
+        avail = {r: alloc[r] - used[r] for r in used}
+        existing.append(ExistingNode(name, labels, avail, {}, [], True))
+    return Problem([catalog], pools, shapes, pod_shape, creation, uid, existing=existing, bound_pods=bound,
+                   name=f"config3-{n}")
+
+
+def random_topology_problem(catalog, seed, n_types=80, n_pods=240, n_existing=12, n_shapes=10, n_pools=2):
+    """Randomized topology-spread scenario: zone / hostname / capacity-type keys, maxSkew 1-3, minDomains,
+    ScheduleAnyway (relaxed away), selectors on own / other deployments / nil / expressions, node affinity
+    and taint inclusion policies, zone-restricted pools and pods, bound pods seeding the counts."""
+    rng = np.random.default_rng(seed)
+    idx = np.sort(rng.choice(len(catalog), size=min(n_types, len(catalog)), replace=False))
+    cat = [catalog[i] for i in idx]
+    cat = [it for it in cat if any(o.available for o in it.offerings)]
+    pools = []
+    for i in range(n_pools):
+        reqs = [("karpenter.sh/capacity-type", "In", ["on-demand", "spot"] if rng.random() < 0.7 else ["spot"])]
+        if rng.random() < 0.4:
+            reqs.append((ZONE_KEY, "In", list(rng.choice(ZONES, size=2, replace=False))))
+        taints = [("dedicated", f"team{i}", "NoSchedule")] if rng.random() < 0.3 else []
+        limits = {"cpu": int(rng.integers(20, 400)) * 1000} if rng.random() < 0.3 else {}
+        pools.append(NodePool(f"pool-{i}", int(rng.integers(0, 4)), 0, reqs, taints=taints, limits=limits))
+    apps = [f"app-{j}" for j in range(n_shapes)]
+    shapes = []
+    for j in range(n_shapes):
+        sh = PodShape(req_res(int(rng.choice([100, 250, 500, 1000, 2000])), int(rng.choice([128, 512, 1024, 2048]))),
+                      labels={"app": apps[j], "tier": str(rng.choice(["web", "db"]))}, namespace=str(rng.choice(["a", "b"])))
+        if rng.random() < 0.2:
+            sh.node_selector = {ZONE_KEY: str(rng.choice(ZONES))}
+        if rng.random() < 0.2:
+            sh.required_terms = [[("karpenter.sh/capacity-type", "In", [str(rng.choice(["spot", "on-demand"]))])]]
+        if rng.random() < 0.2:
+            sh.preferred_terms = [(int(rng.integers(1, 100)), [(ZONE_KEY, "In", [str(rng.choice(ZONES))])])]
+        if rng.random() < 0.3:
+            sh.tolerations = [("dedicated", "Exists", "", "NoSchedule")]
+        for _ in range(int(rng.integers(1, 3))):
+            r = rng.random()
+            if r < 0.6:
+                sel = LabelSelector(match_labels={"app": apps[j]})
+            elif r < 0.75:
+                sel = LabelSelector(match_labels={"app": apps[int(rng.integers(0, n_shapes))]})
+            elif r < 0.85:
+                sel = LabelSelector(match_expressions=[("tier", "In", ["web"]), ("app", "NotIn", [apps[0]])])
+            elif r < 0.93:
+                sel = LabelSelector(match_expressions=[("app", "Exists", [])])
+            else:
+                sel = None
+            key = str(rng.choice([ZONE_KEY, ZONE_KEY, HOST_KEY, HOST_KEY, "karpenter.sh/capacity-type"]))
+            sh.topology_spread.append(TopologySpread(
+                key, int(rng.choice([1, 1, 2, 3])), sel,
+                "ScheduleAnyway" if rng.random() < 0.25 else "DoNotSchedule",
+                int(rng.choice([2, 3, 4])) if rng.random() < 0.15 else None,
+                "Ignore" if rng.random() < 0.15 else None,
+                "Honor" if rng.random() < 0.2 else None))
+        shapes.append(sh)
+    existing, bound = [], []
+    for e in range(n_existing):
+        it = cat[int(rng.integers(0, len(cat)))]
+        name = f"node-{e:05d}"
+        labels = node_labels(it, int(rng.integers(0, 3)), str(rng.choice(["spot", "on-demand"])),
+                             pools[int(rng.integers(0, n_pools))].name, name)
+        alloc = it.allocatable()
+        frac = float(rng.uniform(0.2, 0.9))
+        avail = {k: int(v * frac) for k, v in alloc.items() if k in ("cpu", "memory", "pods")}
+        existing.append(ExistingNode(name, labels, avail, {},
+                                     [("dedicated", "team0", "NoSchedule")] if rng.random() < 0.15 else [],
+                                     bool(rng.random() < 0.9)))
+        for _ in range(int(rng.integers(0, 4))):
+            j = int(rng.integers(0, n_shapes))
+            bound.append((shapes[j].namespace, dict(shapes[j].labels), e))
+    s, c, u = _pods(rng, n_pods, len(shapes))
+    return Problem([cat], pools, shapes, s, c, u, existing=existing, bound_pods=bound, name=f"random-topology-{seed}")
 
 
 # ------------------------------------------------------------------------------------------------

@@ -69,7 +69,7 @@ static const char* kLabelOS = "kubernetes.io/os";
 static const char* kLabelWindowsBuild = "node.kubernetes.io/windows-build";
 static const char* kLabelCapacityType = "karpenter.sh/capacity-type";
 static const char* kLabelNodePool = "karpenter.sh/nodepool";
-static const char* kLabelHostname = "kubernetes.io/hostname";
+static const char* kLabelHostname = "kubernetes.io/hostname";  // corev1.LabelHostname
 static const char* kLabelZoneID = "topology.k8s.aws/zone-id";
 static const char* kLabelResID = "karpenter.k8s.aws/capacity-reservation-id";   // cloudprovider.ReservationIDLabel (R:pkg/apis/v1/doc.go:38)
 static const char* kLabelResType = "karpenter.k8s.aws/capacity-reservation-type";
@@ -648,6 +648,60 @@ struct Template {
   ResourceList remaining;
 };
 
+// ---------------------------------------------------------------------------------------------
+// metav1.LabelSelector (labels.Selector from LabelSelectorAsSelector)
+// ---------------------------------------------------------------------------------------------
+struct SelReq {
+  string key;
+  int op;
+  set<string> values;
+};
+struct Selector {
+  bool nil = true;
+  vector<SelReq> reqs;  // matchLabels become In{v}
+  bool Matches(const map<string, string>& labels) const {
+    if (nil) return false;  // labels.Nothing()
+    for (auto& r : reqs) {
+      auto it = labels.find(r.key);
+      const bool has = it != labels.end();
+      switch (r.op) {
+        case KP_SEL_IN:
+          if (!has || !r.values.count(it->second)) return false;
+          break;
+        case KP_SEL_NOT_IN:
+          if (has && r.values.count(it->second)) return false;
+          break;
+        case KP_SEL_EXISTS:
+          if (!has) return false;
+          break;
+        default:
+          if (has) return false;
+      }
+    }
+    return true;
+  }
+  string Canon() const {
+    if (nil) return "nil";
+    vector<string> parts;
+    for (auto& r : reqs) {
+      string x = r.key + "/" + std::to_string(r.op);
+      for (auto& v : r.values) x += "," + v;
+      parts.push_back(x);
+    }
+    std::sort(parts.begin(), parts.end());
+    string o;
+    for (auto& x : parts) o += x + ";";
+    return o;
+  }
+};
+
+struct Spread {
+  string key;
+  int32_t maxSkew, minDomains;  // minDomains < 0: nil
+  int when, affinityPolicy, taintsPolicy;
+  Selector sel;
+};
+
 struct PodState {
   int index;
   int shape;
@@ -660,11 +714,15 @@ struct PodState {
   Requirements node_selector;
   ResourceList requests;
   vector<Toleration> tolerations;
-  Requirements reqs;  // cached NewPodRequirements
+  vector<Spread> spreads;
+  string ns;
+  map<string, string> labels;
+  Requirements reqs;    // cached NewPodRequirements
+  Requirements strict;  // cached NewStrictPodRequirements (no preferred terms)
 };
 
 // NewPodRequirements (UP scheduling/requirements.go): nodeSelector + heaviest preferred term (treated
-// as required) + the first required term.
+// as required) + the first required term. Strict: without the preferred term.
 static Requirements PodRequirements(PodState& p) {
   Requirements r = p.node_selector;
   if (!p.preferred.empty()) {
@@ -680,10 +738,15 @@ static Requirements PodRequirements(PodState& p) {
   if (!p.required_terms.empty()) AddAll(r, p.required_terms[0]);
   return r;
 }
+static Requirements StrictPodRequirements(const PodState& p) {
+  Requirements r = p.node_selector;
+  if (!p.required_terms.empty()) AddAll(r, p.required_terms[0]);
+  return r;
+}
 
 // Preferences.Relax (UP preferences.go): first applicable of removeRequiredNodeAffinityTerm (only when
-// >1 terms), [pod affinity/anti-affinity: not modelled], removePreferredNodeAffinityTermByWeight,
-// [ScheduleAnyway spreads: ABI v1 has none].
+// >1 terms), [pod affinity/anti-affinity: not in the ABI], removePreferredNodeAffinityTerm (heaviest),
+// removeTopologySpreadScheduleAnyway (first ScheduleAnyway constraint, swap-with-last removal).
 static bool Relax(PodState& p) {
   if (p.required_terms.size() > 1) {
     p.required_terms.erase(p.required_terms.begin());
@@ -697,8 +760,236 @@ static bool Relax(PodState& p) {
     p.preferred.erase(p.preferred.begin());
     return true;
   }
+  for (size_t i = 0; i < p.spreads.size(); i++)
+    if (p.spreads[i].when == KP_SCHEDULE_ANYWAY) {
+      p.spreads[i] = p.spreads.back();
+      p.spreads.pop_back();
+      return true;
+    }
   return false;
 }
+
+static Requirement ExistsReq(const string& key) { return NewRequirement(key, KP_OP_EXISTS, {}, -1); }
+static const Requirement& GetOr(const Requirements& r, const string& key, Requirement& tmp) {
+  auto it = r.find(key);
+  if (it != r.end()) return it->second;
+  tmp = ExistsReq(key);
+  return tmp;
+}
+
+// ---------------------------------------------------------------------------------------------
+// UP Topology / TopologyGroup (topology.go, topologygroup.go, topologynodefilter.go,
+// topologydomaingroup.go) for TopologyTypeSpread. Tie-break: where upstream iterates a Go map or an
+// unsorted set (equal counts), the lexicographically smallest domain is chosen.
+// ---------------------------------------------------------------------------------------------
+struct TopologyGroup {
+  string key, id;
+  int32_t maxSkew, minDomains;
+  string ns;
+  Selector sel;
+  vector<Requirements> filter;  // TopologyNodeFilter.Requirements (ORed)
+  bool affinityHonor, taintHonor;
+  vector<Toleration> tols;
+  map<string, int32_t> domains;
+  set<int> owners;
+
+  bool Selects(const string& pns, const map<string, string>& labels) const { return pns == ns && sel.Matches(labels); }
+  bool FilterMatches(const vector<Taint>& taints, const Requirements& reqs, bool allow) const {
+    bool aff = true;
+    if (affinityHonor && !filter.empty()) {
+      aff = false;
+      for (auto& f : filter)
+        if (Compatible(reqs, f, allow)) {
+          aff = true;
+          break;
+        }
+    }
+    const bool tnt = !taintHonor || ToleratesAll(taints, tols);
+    return aff && tnt;
+  }
+  int64_t DomainMinCount(const Requirement& podDomains) const {
+    if (key == kLabelHostname) return 0;  // hostname topologies can always create a new domain
+    int64_t mn = std::numeric_limits<int32_t>::max();
+    int32_t num = 0;
+    for (auto& kv : domains)
+      if (Has(podDomains, kv.first)) {
+        num++;
+        mn = std::min<int64_t>(mn, kv.second);
+      }
+    if (minDomains >= 0 && num < minDomains) mn = 0;
+    return mn;
+  }
+  // nextDomainTopologySpread
+  Requirement NextDomain(bool self, const Requirement& podDomains, const Requirement& nodeDomains) const {
+    const int64_t mn = DomainMinCount(podDomains);
+    string minDomain;
+    bool found = false;
+    int64_t minCount = std::numeric_limits<int32_t>::max();
+    auto consider = [&](const string& d, int32_t c) {
+      const int64_t count = (int64_t)c + (self ? 1 : 0);
+      if (count - mn <= maxSkew && count < minCount) {
+        minDomain = d;
+        minCount = count;
+        found = true;
+      }
+    };
+    if (nodeDomains.Op() == KP_OP_IN) {
+      for (auto& v : nodeDomains.values) {  // sorted
+        auto it = domains.find(v);
+        if (it != domains.end()) consider(v, it->second);
+      }
+    } else {
+      for (auto& kv : domains)
+        if (Has(nodeDomains, kv.first)) consider(kv.first, kv.second);
+    }
+    if (!found) return NewRequirement(key, KP_OP_DOES_NOT_EXIST, {}, -1);
+    return NewRequirement(key, KP_OP_IN, {minDomain}, -1);
+  }
+};
+
+struct BoundPod {
+  string ns;
+  map<string, string> labels;
+  int node;  // input index of the existing node
+};
+struct NodeView {  // what countDomains reads of a node
+  string name;
+  map<string, string> labels;
+  vector<Taint> taints;
+  Requirements reqs;  // NewLabelRequirements(labels)
+};
+
+struct Topology {
+  vector<std::unique_ptr<TopologyGroup>> groups;  // creation order
+  map<string, TopologyGroup*> byId;
+  map<string, map<string, vector<vector<Taint>>>> domainGroups;  // key -> domain -> taint sets
+  vector<BoundPod> bound;
+  vector<NodeView> nodes;
+
+  static string ReqsCanon(const Requirements& r) {
+    string o;
+    for (auto& kv : r) {
+      const Requirement& q = kv.second;
+      o += kv.first + (q.complement ? "!" : "=");
+      for (auto& v : q.values) o += v + ",";
+      if (q.has_gt) o += ">" + std::to_string(q.gt);
+      if (q.has_lt) o += "<" + std::to_string(q.lt);
+      if (q.has_min) o += "#" + std::to_string(q.min_values);
+      o += ";";
+    }
+    return o;
+  }
+
+  // MakeTopologyNodeFilter + NewTopologyGroup; identity = upstream TopologyGroup.Hash fields (key, type,
+  // namespaces, selector, maxSkew, node filter).
+  std::unique_ptr<TopologyGroup> NewGroup(const PodState& p, const Spread& s) const {
+    auto g = std::make_unique<TopologyGroup>();
+    g->key = s.key;
+    g->maxSkew = s.maxSkew;
+    g->minDomains = s.minDomains;
+    g->ns = p.ns;
+    g->sel = s.sel;
+    g->affinityHonor = s.affinityPolicy != KP_POLICY_IGNORE;
+    g->taintHonor = s.taintsPolicy == KP_POLICY_HONOR;
+    g->tols = p.tolerations;
+    if (p.required_terms.empty()) {
+      g->filter.push_back(p.node_selector);
+    } else {
+      for (auto& t : p.required_terms) {
+        Requirements r = p.node_selector;
+        AddAll(r, t);
+        g->filter.push_back(r);
+      }
+    }
+    string id = s.key + "|" + std::to_string(s.maxSkew) + "|" + p.ns + "|" + s.sel.Canon() + "|" +
+                std::to_string(g->affinityHonor) + std::to_string(g->taintHonor) + "|";
+    for (auto& f : g->filter) id += "[" + ReqsCanon(f) + "]";
+    if (g->taintHonor)
+      for (auto& t : g->tols) id += "(" + t.key + "," + t.value + "," + std::to_string(t.op) + "," + std::to_string(t.effect) + ")";
+    g->id = id;
+    // domainGroup.ForEachDomain(pod, taintPolicy): register every known domain with a zero count
+    auto dg = domainGroups.find(s.key);
+    if (dg != domainGroups.end())
+      for (auto& kv : dg->second) {
+        bool ok = !g->taintHonor;
+        for (size_t i = 0; i < kv.second.size() && !ok; i++) ok = ToleratesAll(kv.second[i], p.tolerations);
+        if (ok) g->domains.emplace(kv.first, 0);
+      }
+    return g;
+  }
+
+  // countDomains: pods already running that the group selects, on nodes the filter admits; then every
+  // existing node's domain value with a zero count.
+  void CountDomains(TopologyGroup& g) const {
+    for (auto& bp : bound) {
+      if (!g.Selects(bp.ns, bp.labels)) continue;
+      const NodeView& n = nodes[(size_t)bp.node];
+      auto it = n.labels.find(g.key);
+      string domain;
+      if (it != n.labels.end()) domain = it->second;
+      else if (g.key == kLabelHostname) domain = n.name;
+      else continue;
+      if (!g.FilterMatches(n.taints, n.reqs, false)) continue;
+      g.domains[domain]++;
+    }
+    for (auto& n : nodes) {
+      if (!g.FilterMatches(n.taints, n.reqs, false)) continue;
+      auto it = n.labels.find(g.key);
+      if (it == n.labels.end()) continue;
+      g.domains.emplace(it->second, 0);
+    }
+  }
+
+  // Topology.Update: the pod stops owning every group, then owns the groups of its current spreads
+  void Update(const PodState& p) {
+    for (auto& g : groups) g->owners.erase(p.index);
+    for (auto& s : p.spreads) {
+      auto g = NewGroup(p, s);
+      auto it = byId.find(g->id);
+      TopologyGroup* tg;
+      if (it == byId.end()) {
+        CountDomains(*g);
+        tg = g.get();
+        byId[g->id] = tg;
+        groups.push_back(std::move(g));
+      } else {
+        tg = it->second;
+      }
+      tg->owners.insert(p.index);
+    }
+  }
+  void Register(const string& key, const string& domain) {
+    for (auto& g : groups)
+      if (g->key == key) g->domains.emplace(domain, 0);
+  }
+  void Unregister(const string& key, const string& domain) {
+    for (auto& g : groups)
+      if (g->key == key) g->domains.erase(domain);
+  }
+  // AddRequirements: every group the pod owns narrows its key to the chosen domain
+  bool AddRequirements(const PodState& p, const Requirements& nodeReqs, Requirements* out) const {
+    *out = nodeReqs;
+    for (auto& g : groups) {
+      if (!g->owners.count(p.index)) continue;
+      Requirement t1, t2;
+      const Requirement& podDomains = GetOr(p.strict, g->key, t1);
+      const Requirement& nodeDomains = GetOr(nodeReqs, g->key, t2);
+      Requirement d = g->NextDomain(g->Selects(p.ns, p.labels), podDomains, nodeDomains);
+      if (d.Len() == 0) return false;
+      Add(*out, d);
+    }
+    return true;
+  }
+  // Record: every group that counts the pod on a node with these requirements (single-domain keys only)
+  void Record(const PodState& p, const vector<Taint>& taints, const Requirements& reqs, bool allow) {
+    for (auto& g : groups) {
+      if (!g->Selects(p.ns, p.labels) || !g->FilterMatches(taints, reqs, allow)) continue;
+      auto it = reqs.find(g->key);
+      if (it == reqs.end() || it->second.Len() != 1) continue;
+      g->domains[*it->second.values.begin()]++;
+    }
+  }
+};
 
 struct NodeClaim {
   int id;  // creation order
@@ -707,6 +998,7 @@ struct NodeClaim {
   vector<int> options;
   ResourceList requests;
   vector<int> pods;
+  string hostname;
 };
 
 struct ExistingNode {
@@ -767,16 +1059,21 @@ struct Scheduler {
   vector<ExistingNode> existing;
   vector<std::unique_ptr<NodeClaim>> created;  // creation order
   vector<NodeClaim*> newNodeClaims;            // the slice the scheduler sorts
-  map<int, vector<int>> unused;
+  Topology topology;
+  int64_t nodeID = 0;  // hostname placeholder counter (NewNodeClaim)
   Counters counters;
 
-  // NodeClaim.Add
+  // NodeClaim.CanAdd + NodeClaim.Add
   bool NodeClaimAdd(NodeClaim& n, PodState& p) {
     counters.attempts++;
     if (!ToleratesAll(n.tmpl->taints, p.tolerations)) return false;
     Requirements ncr = n.reqs;
     if (!Compatible(ncr, p.reqs, true)) return false;
     AddAll(ncr, p.reqs);
+    Requirements topo;
+    if (!topology.AddRequirements(p, ncr, &topo)) return false;
+    if (!Compatible(ncr, topo, true)) return false;
+    AddAll(ncr, topo);
     ResourceList requests = Merge(n.requests, p.requests);
     vector<int> remaining;
     if (!FilterInstanceTypes(*n.tmpl->catalog, n.options, ncr, requests, &remaining, &counters)) return false;
@@ -784,9 +1081,11 @@ struct Scheduler {
     n.options = std::move(remaining);
     n.requests = requests;
     n.reqs = std::move(ncr);
+    topology.Record(p, n.tmpl->taints, n.reqs, true);
     return true;
   }
 
+  // ExistingNode.CanAdd + ExistingNode.Add
   bool ExistingCanAddAndAdd(ExistingNode& n, PodState& p) {
     counters.attempts++;
     if (!ToleratesAll(n.taints, p.tolerations)) return false;
@@ -795,9 +1094,14 @@ struct Scheduler {
     Requirements nr = n.reqs;
     if (!Compatible(nr, p.reqs, false)) return false;
     AddAll(nr, p.reqs);
+    Requirements topo;
+    if (!topology.AddRequirements(p, nr, &topo)) return false;
+    if (!Compatible(nr, topo, false)) return false;
+    AddAll(nr, topo);
     n.pods.push_back(p.index);
     n.requests = requests;
     n.reqs = std::move(nr);
+    topology.Record(p, n.taints, n.reqs, false);
     return true;
   }
 
@@ -826,13 +1130,22 @@ struct Scheduler {
         its.swap(f);
         if (its.empty()) continue;
       }
+      // NewNodeClaim: template + hostname In {placeholder}, registered with the hostname topologies
       auto nc = std::make_unique<NodeClaim>();
       nc->id = (int)created.size();
       nc->tmpl = &t;
-      nc->reqs = t.reqs;  // + hostname In {placeholder}: inert here (ABI v1 rejects hostname selectors)
+      char hn[64];
+      snprintf(hn, sizeof hn, "hostname-placeholder-%04lld", (long long)++nodeID);
+      nc->hostname = hn;
+      topology.Register(kLabelHostname, nc->hostname);
+      nc->reqs = t.reqs;
+      Add(nc->reqs, NewRequirement(kLabelHostname, KP_OP_IN, {nc->hostname}, -1));
       nc->options = its;
       nc->requests = t.daemon;
-      if (!NodeClaimAdd(*nc, p)) continue;
+      if (!NodeClaimAdd(*nc, p)) {
+        topology.Unregister(kLabelHostname, nc->hostname);  // NodeClaim.Destroy
+        continue;
+      }
       if (t.has_limits) {  // subtractMax over the new NodeClaim's InstanceTypeOptions
         ResourceList mx;
         for (int i : nc->options)
@@ -857,6 +1170,48 @@ struct Scheduler {
 // =============================================================================================
 using namespace oracle;
 
+// Requirements.NodeSelectorRequirements() (Gt, then Lt, then NotIn/Exists, then In/DoesNotExist), keys in
+// byte order, values sorted, the hostname placeholder dropped (NodeClaim.FinalizeScheduling).
+struct ReqOut {
+  std::vector<std::string> keys;
+  std::vector<std::vector<std::string>> vals;
+  std::vector<std::vector<const char*>> ptrs;
+  std::vector<kp_requirement> items;
+  void From(const Requirements& r) {
+    for (auto& kv : r) {
+      if (kv.first == kLabelHostname) continue;
+      const Requirement& q = kv.second;
+      kp_requirement it;
+      memset(&it, 0, sizeof it);
+      std::vector<std::string> v;
+      if (q.has_gt) {
+        it.op = KP_OP_GT;
+        v.push_back(std::to_string(q.gt));
+      } else if (q.has_lt) {
+        it.op = KP_OP_LT;
+        v.push_back(std::to_string(q.lt));
+      } else if (q.complement) {
+        it.op = q.values.empty() ? KP_OP_EXISTS : KP_OP_NOT_IN;
+        v.assign(q.values.begin(), q.values.end());
+      } else {
+        it.op = q.values.empty() ? KP_OP_DOES_NOT_EXIST : KP_OP_IN;
+        v.assign(q.values.begin(), q.values.end());
+      }
+      it.min_values = q.has_min ? q.min_values : -1;
+      keys.push_back(kv.first);
+      vals.push_back(std::move(v));
+      items.push_back(it);
+    }
+    ptrs.resize(vals.size());
+    for (size_t i = 0; i < items.size(); i++) {
+      for (auto& x : vals[i]) ptrs[i].push_back(x.c_str());
+      items[i].key = keys[i].c_str();
+      items[i].values = ptrs[i].data();
+      items[i].n_values = (uint32_t)ptrs[i].size();
+    }
+  }
+};
+
 struct kpo_result {
   std::vector<int32_t> placement;
   struct NC {
@@ -866,6 +1221,7 @@ struct kpo_result {
     kp_resource_list requests;
     Requirements reqs;                      // final NodeClaim requirements (consolidation needs them)
     const std::vector<InstanceType>* cat = nullptr;
+    std::shared_ptr<ReqOut> out;
   };
   std::vector<NC> ncs;
   kp_solve_stats stats;
@@ -873,12 +1229,7 @@ struct kpo_result {
 
 extern "C" {
 
-typedef struct kpo_nodeclaim {
-  uint32_t nodepool, n_pods, n_remaining, n_options;
-  const uint32_t* pods;
-  const uint32_t* options;
-  kp_resource_list requests;
-} kpo_nodeclaim;
+typedef kp_nodeclaim_info kpo_nodeclaim;
 
 static std::vector<Taint> TaintsFromABI(const kp_taint* t, uint32_t n) {
   std::vector<Taint> v;
@@ -920,6 +1271,59 @@ static int32_t SolveCore(const Catalogs& cats, const kp_solve_in* in, kpo_result
     t.remaining = FromABI(np.limits);
     s.templates.push_back(std::move(t));
   }
+  // Topology inputs: the node snapshot countDomains reads, the pods bound to it, and buildDomainGroups
+  // (NodePool requirements + labels, intersected with each instance type's requirements: In values).
+  Topology& topo = s.topology;
+  for (uint32_t i = 0; i < in->n_existing; i++) {
+    const kp_existing_node& e = in->existing[i];
+    NodeView v;
+    v.name = e.name ? e.name : "";
+    for (uint32_t j = 0; j < e.n_labels; j++) v.labels[e.labels[j].key] = e.labels[j].value ? e.labels[j].value : "";
+    v.taints = TaintsFromABI(e.taints, e.n_taints);
+    v.reqs = LabelRequirements(e.labels, e.n_labels);
+    topo.nodes.push_back(std::move(v));
+  }
+  for (uint32_t i = 0; i < in->n_bound_pods; i++) {
+    const kp_bound_pod& b = in->bound_pods[i];
+    if (b.node >= in->n_existing) return KP_E_INVAL;
+    BoundPod bp;
+    bp.ns = b.namespace_ ? b.namespace_ : "";
+    for (uint32_t j = 0; j < b.n_labels; j++) bp.labels[b.labels[j].key] = b.labels[j].value ? b.labels[j].value : "";
+    bp.node = (int)b.node;
+    topo.bound.push_back(std::move(bp));
+  }
+  bool anySpread = false;
+  for (uint32_t i = 0; i < in->n_shapes; i++) anySpread |= in->shapes[i].n_topology_spread > 0;
+  if (anySpread)
+    for (uint32_t i = 0; i < in->n_nodepools; i++) {
+      const kp_nodepool& np = in->nodepools[i];
+      const auto& cat = *cats[np.catalog];
+      if (cat.empty()) continue;
+      Requirements base = FromABI(np.requirements);
+      AddAll(base, LabelRequirements(np.labels, np.n_labels));
+      std::vector<Taint> taints = TaintsFromABI(np.taints, np.n_taints);
+      auto insert = [&](const Requirements& r) {
+        for (auto& kv : r)
+          if (kv.second.Op() == KP_OP_IN)
+            for (auto& v : kv.second.values) {
+              auto& lst = topo.domainGroups[kv.first][v];
+              bool dup = false;
+              for (auto& x : lst) {
+                bool same = x.size() == taints.size();
+                for (size_t k = 0; same && k < x.size(); k++)
+                  same = x[k].key == taints[k].key && x[k].value == taints[k].value && x[k].effect == taints[k].effect;
+                dup = dup || same;
+              }
+              if (!dup) lst.push_back(taints);
+            }
+      };
+      for (auto& it : cat) {
+        Requirements r = base;
+        AddAll(r, it.reqs);
+        insert(r);
+      }
+      insert(base);
+    }
   for (uint32_t i = 0; i < in->n_existing; i++) {
     const kp_existing_node& e = in->existing[i];
     ExistingNode n;
@@ -942,7 +1346,6 @@ static int32_t SolveCore(const Catalogs& cats, const kp_solve_in* in, kpo_result
     const kp_pod& p = in->pods[i];
     if (p.shape >= in->n_shapes) return KP_E_INVAL;
     const kp_pod_shape& sh = in->shapes[p.shape];
-    if (sh.n_topology_spread) return KP_E_UNSUPPORTED;
     PodState& ps = pods[i];
     ps.index = (int)i;
     ps.shape = (int)p.shape;
@@ -959,7 +1362,40 @@ static int32_t SolveCore(const Catalogs& cats, const kp_solve_in* in, kpo_result
       const kp_toleration& t = sh.tolerations[j];
       ps.tolerations.push_back({t.key ? t.key : "", t.value ? t.value : "", t.op, t.effect});
     }
+    ps.ns = sh.namespace_ ? sh.namespace_ : "";
+    for (uint32_t j = 0; j < sh.n_labels; j++) ps.labels[sh.labels[j].key] = sh.labels[j].value ? sh.labels[j].value : "";
+    for (uint32_t j = 0; j < sh.n_topology_spread; j++) {
+      const kp_topology_spread& t = sh.topology_spread[j];
+      Spread sp;
+      sp.key = t.topology_key ? t.topology_key : "";
+      sp.maxSkew = t.max_skew;
+      sp.minDomains = t.min_domains > 0 ? t.min_domains : -1;
+      sp.when = t.when_unsatisfiable;
+      sp.affinityPolicy = t.node_affinity_policy;
+      sp.taintsPolicy = t.node_taints_policy;
+      sp.sel.nil = t.selector.is_nil != 0;
+      for (uint32_t k = 0; k < t.selector.n_match_labels; k++)
+        sp.sel.reqs.push_back({t.selector.match_labels[k].key, KP_SEL_IN, {t.selector.match_labels[k].value}});
+      for (uint32_t k = 0; k < t.selector.n_match_expressions; k++) {
+        const kp_selector_requirement& e = t.selector.match_expressions[k];
+        SelReq r{e.key, e.op, {}};
+        for (uint32_t v = 0; v < e.n_values; v++) r.values.insert(e.values[v]);
+        sp.sel.reqs.push_back(r);
+      }
+      ps.spreads.push_back(sp);
+    }
     ps.reqs = PodRequirements(ps);
+    ps.strict = StrictPodRequirements(ps);
+  }
+  // NewTopology: Update(pod) for every pod of the batch, in input order; then NewExistingNode adds
+  // hostname In {HostName()} to each existing node and registers it with the hostname topologies.
+  for (auto& ps : pods) topo.Update(ps);
+  for (auto& n : s.existing) {
+    const NodeView& v = topo.nodes[(size_t)n.index];
+    auto h = v.labels.find(kLabelHostname);
+    const string host = (h == v.labels.end() || h->second.empty()) ? v.name : h->second;
+    Add(n.reqs, NewRequirement(kLabelHostname, KP_OP_IN, {host}, -1));
+    topo.Register(kLabelHostname, host);
   }
 
   // Queue (UP queue.go): byCPUAndMemoryDescending, a total order (UID tie-break).
@@ -994,7 +1430,9 @@ static int32_t SolveCore(const Catalogs& cats, const kp_solve_in* in, kpo_result
     queue.push_back(pi);
     if (relaxed) {
       lastLen.clear();
-      p.reqs = PodRequirements(p);
+      p.reqs = PodRequirements(p);  // updateCachedPodData
+      p.strict = StrictPodRequirements(p);
+      s.topology.Update(p);
     } else {
       lastLen[pi] = queue.size() - head;
     }
@@ -1030,6 +1468,8 @@ static int32_t SolveCore(const Catalogs& cats, const kp_solve_in* in, kpo_result
     bool ok = !HasMinValues(n.reqs) || SatisfiesMinValues(cat, trunc, n.reqs);
     o.reqs = n.reqs;
     o.cat = &cat;
+    o.out = std::make_shared<ReqOut>();
+    o.out->From(n.reqs);
     if (ok) {
       for (int t : trunc) o.options.push_back((uint32_t)t);
       for (int p : n.pods) {
@@ -1096,6 +1536,8 @@ int32_t kpo_simulate_batch(const kp_cluster* cl, const uint32_t* offsets, const 
   auto t0 = std::chrono::steady_clock::now();
   if (!cl || !offsets || !out || (!cl->catalog_descs && cl->n_catalogs)) return KP_E_INVAL;
   if (cl->spot_to_spot) return KP_E_UNSUPPORTED;
+  for (uint32_t i = 0; i < cl->n_shapes; i++)
+    if (cl->shapes[i].n_topology_spread) return KP_E_UNSUPPORTED;  // cluster pods are not in kp_cluster as bound pods
   Catalogs cats;
   for (uint32_t i = 0; i < cl->n_catalogs; i++) cats.push_back(CatalogFromABI(cl->catalog_descs[i]));
   std::vector<Requirements> nodeLabels(cl->n_nodes);
@@ -1229,6 +1671,9 @@ int32_t kpo_result_nodeclaim(const kpo_result* r, uint32_t i, kpo_nodeclaim* out
   out->pods = n.pods.data();
   out->options = n.options.data();
   out->requests = n.requests;
+  out->requirements.items = n.out ? n.out->items.data() : nullptr;
+  out->requirements.n = n.out ? (uint32_t)n.out->items.size() : 0;
+  out->requirements.reserved_ = 0;
   return KP_OK;
 }
 int32_t kpo_result_stats(const kpo_result* r, kp_solve_stats* out) {

@@ -10,7 +10,7 @@ pytestmark = pytest.mark.gpu
 
 
 def canon(r):
-    return [(n["nodepool"], n["pods"], n["options"], n["n_remaining"]) for n in r["nodeclaims"]]
+    return [(n["nodepool"], n["pods"], n["options"], n["n_remaining"], n["requirements"]) for n in r["nodeclaims"]]
 
 
 def check_same(got, want):
@@ -20,7 +20,7 @@ def check_same(got, want):
     g, w = canon(got), canon(want)
     assert len(g) == len(w)
     for i, (a, b) in enumerate(zip(g, w)):
-        assert a == b, f"NodeClaim {i} differs: {a[:2]} {a[3]} vs {b[:2]} {b[3]}"
+        assert a == b, f"NodeClaim {i} differs: {a[:2]} {a[3:]} vs {b[:2]} {b[3:]}"
 
 
 def run_both(ctx, prob):

@@ -1,0 +1,43 @@
+"""Topology spread on the device (solve_kernel with TopologyGroups) vs the CPU oracle — bit-exact placements,
+NodeClaims, options and final requirements (zone narrowing included). SURVEY §8a a16, config 3."""
+import pytest
+
+from test_gpu_parity import check_same, run_both
+import test_topology_oracle as kat
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_random_topology(ctx, catalog, seed):
+    from kpamd import synth
+    prob = synth.random_topology_problem(catalog, seed, n_existing=[0, 12, 30][seed % 3])
+    got, want = run_both(ctx, prob)
+    check_same(got, want)
+
+
+def test_config3_scaled(ctx, catalog):
+    from kpamd import synth
+    got, want = run_both(ctx, synth.config3(catalog, n_pods=3000, n_deployments=60, n_existing=150))
+    check_same(got, want)
+
+
+def test_topology_kats(ctx, catalog):
+    from kpamd.model import ExistingNode
+    from kpamd import synth
+    probs = [
+        kat.problem(catalog, [kat.spread_shape("a", kat.ZONE, cpu=3500)], [9]),
+        kat.problem(catalog, [kat.spread_shape("a", kat.HOST, skew=3, cpu=100)], [7]),
+        kat.problem(catalog, [kat.spread_shape("a", kat.ZONE, min_domains=4, cpu=100)], [5]),
+        kat.problem(catalog, [kat.spread_shape("a", "example.com/rack"),
+                              kat.spread_shape("b", "example.com/rack", when="ScheduleAnyway")], [3, 3]),
+    ]
+    it = catalog[synth._type_named(catalog, "m5.xlarge")]
+    alloc = it.allocatable()
+    nodes = [ExistingNode(f"n{z}", synth.node_labels(it, z, "on-demand", "default", f"n{z}"),
+                          {k: alloc[k] for k in ("cpu", "memory", "pods")}) for z in range(3)]
+    bound = [("default", {"app": "a"}, 0), ("default", {"app": "a"}, 0), ("other", {"app": "a"}, 1)]
+    probs.append(kat.problem(catalog, [kat.spread_shape("a", kat.ZONE, cpu=100)], [4], existing=nodes, bound=bound))
+    for prob in probs:
+        got, want = run_both(ctx, prob)
+        check_same(got, want)

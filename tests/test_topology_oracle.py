@@ -1,0 +1,142 @@
+"""Oracle topology spread (upstream Topology / TopologyGroup) — semantic checks on CPU.
+
+The upstream module is not in the container (parity unpinned), so these pin the oracle to the
+documented Kubernetes topologySpreadConstraints semantics the reference relies on:
+  - maxSkew against the global minimum over eligible domains; hostname minimum is always 0
+    (a new node is always a possible domain);
+  - minDomains: fewer eligible domains than minDomains -> the global minimum is 0;
+  - DoNotSchedule is a hard constraint; ScheduleAnyway is dropped by Preferences.Relax;
+  - pods already bound in the cluster seed the counts (countDomains), filtered by namespace + selector;
+  - a NodeClaim that hosts a zone-spread pod is narrowed to exactly one zone (Record counts only then).
+"""
+from collections import Counter, defaultdict
+
+import numpy as np
+import pytest
+
+from kpamd.model import LabelSelector, NodePool, PodShape, Problem, TopologySpread
+from kpamd import synth
+
+ZONE = "topology.kubernetes.io/zone"
+HOST = "kubernetes.io/hostname"
+
+
+def solve(prob):
+    from oracle import pyoracle
+    return pyoracle.solve(prob)
+
+
+def nc_zone(nc):
+    for k, op, vals, _ in nc["requirements"]:
+        if k == ZONE and op == "In":
+            return tuple(vals)
+    return None
+
+
+def one_pool(catalog, **kw):
+    return NodePool("default", 0, 0, [("kubernetes.io/os", "In", ["linux"]),
+                                      ("karpenter.sh/capacity-type", "In", ["on-demand"]),
+                                      ("karpenter.k8s.aws/instance-category", "In", ["m"])], **kw)
+
+
+def problem(catalog, shapes, counts, existing=(), bound=()):
+    ps = np.repeat(np.arange(len(shapes), dtype=np.uint32), counts)
+    n = len(ps)
+    return Problem([catalog], [one_pool(catalog)], shapes, ps, np.full(n, 1_750_000_000, dtype=np.int64),
+                   np.arange(n, dtype=np.uint64), existing=list(existing), bound_pods=list(bound))
+
+
+def spread_shape(app, key, skew=1, when="DoNotSchedule", min_domains=None, cpu=1000):
+    sel = LabelSelector(match_labels={"app": app})
+    return PodShape(synth.req_res(cpu, 1024), labels={"app": app},
+                    topology_spread=[TopologySpread(key, skew, sel, when, min_domains)])
+
+
+def test_zone_spread_balances_and_pins_zones(catalog):
+    r = solve(problem(catalog, [spread_shape("a", ZONE, cpu=3500)], [9]))
+    assert (r["placement"] >= 0).all()
+    zones = Counter()
+    for nc in r["nodeclaims"]:
+        z = nc_zone(nc)
+        assert z is not None and len(z) == 1, nc["requirements"]
+        zones[z[0]] += len(nc["pods"])
+    assert sorted(zones.values()) == [3, 3, 3]
+
+
+def test_hostname_spread_one_pod_per_node(catalog):
+    r = solve(problem(catalog, [spread_shape("a", HOST, cpu=100)], [7]))
+    assert (r["placement"] >= 0).all()
+    assert len(r["nodeclaims"]) == 7 and all(len(nc["pods"]) == 1 for nc in r["nodeclaims"])
+    r2 = solve(problem(catalog, [spread_shape("a", HOST, skew=3, cpu=100)], [7]))
+    assert sorted(len(nc["pods"]) for nc in r2["nodeclaims"]) == [1, 3, 3]
+
+
+def test_min_domains_makes_global_minimum_zero(catalog):
+    # 3 zones < minDomains 4 -> min = 0 -> count(d) + 1 <= 1: one pod per zone, the rest cannot schedule
+    r = solve(problem(catalog, [spread_shape("a", ZONE, min_domains=4, cpu=100)], [5]))
+    assert int((r["placement"] >= 0).sum()) == 3
+
+
+def test_do_not_schedule_vs_schedule_anyway(catalog):
+    # no NodePool / instance type / node has the key: no domain exists
+    hard = spread_shape("a", "example.com/rack")
+    soft = spread_shape("b", "example.com/rack", when="ScheduleAnyway")
+    r = solve(problem(catalog, [hard, soft], [3, 3]))
+    assert (r["placement"][:3] == -1).all()
+    assert (r["placement"][3:] >= 0).all()
+
+
+def test_bound_pods_seed_counts_by_selector_and_namespace(catalog):
+    from kpamd.model import ExistingNode
+    it = catalog[synth._type_named(catalog, "m5.xlarge")]
+    alloc = it.allocatable()
+    nodes = [ExistingNode(f"n{z}", synth.node_labels(it, z, "on-demand", "default", f"n{z}"),
+                          {k: alloc[k] for k in ("cpu", "memory", "pods")}) for z in range(3)]
+    # zone 0 already runs 2 pods of app a (same namespace); zone 1 one pod of app a in another namespace
+    bound = [("default", {"app": "a"}, 0), ("default", {"app": "a"}, 0), ("other", {"app": "a"}, 1)]
+    r = solve(problem(catalog, [spread_shape("a", ZONE, cpu=100)], [4], existing=nodes, bound=bound))
+    # counts start (2, 0, 0): pods go to zones 1 and 2 until they reach 2 each -> 2 + 2 placed on n1 / n2,
+    # never on n0 (count 2 + 1 - min > 1 while min < 2)
+    assert (r["placement"] <= -2).all()
+    per_node = Counter(int(-2 - p) for p in r["placement"])
+    assert per_node[0] == 0 and per_node[1] == 2 and per_node[2] == 2
+
+
+def test_config3_small_properties(catalog):
+    prob = synth.config3(catalog, n_pods=1500, n_deployments=40, n_existing=60)
+    r = solve(prob)
+    assert (r["placement"] != -1).all()
+    shape = prob.pod_shape
+    # hostname maxSkew 1: a node already running a pod of the deployment takes none, others at most one
+    bound = Counter((e, lbl["app"]) for _, lbl, e in prob.bound_pods)
+    placed = Counter()
+    for p, pl in enumerate(r["placement"]):
+        if pl <= -2:
+            placed[(int(-2 - pl), prob.shapes[shape[p]].labels["app"])] += 1
+    for key, n in placed.items():
+        assert n == 1 and bound[key] == 0, key
+    for nc in r["nodeclaims"]:
+        apps = Counter(prob.shapes[shape[p]].labels["app"] for p in nc["pods"])
+        assert max(apps.values()) == 1
+        z = nc_zone(nc)
+        assert z is not None and len(z) == 1
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_random_topology_deterministic(catalog, seed):
+    prob = synth.random_topology_problem(catalog, seed)
+    a, b = solve(prob), solve(prob)
+    assert (a["placement"] == b["placement"]).all()
+    assert [n["requirements"] for n in a["nodeclaims"]] == [n["requirements"] for n in b["nodeclaims"]]
+
+
+def test_device_host_compile_accepts_topology(catalog):
+    """kp_solve_validate (host compile of the device path, no GPU) accepts every topology scenario the GPU
+    parity tests run, and rejects what the device does not implement."""
+    import kpamd
+    for seed in range(16):
+        assert kpamd.validate(synth.random_topology_problem(catalog, seed, n_existing=[0, 12, 30][seed % 3])) == 0
+    assert kpamd.validate(synth.config3(catalog, n_pods=3000, n_deployments=60, n_existing=150)) == 0
+    bad = spread_shape("a", ZONE)
+    bad.required_terms = [[("kubernetes.io/arch", "In", ["amd64"])], [("kubernetes.io/arch", "In", ["arm64"])]]
+    assert kpamd.validate(problem(catalog, [bad], [2])) == kpamd.abi.KP_E_UNSUPPORTED
