@@ -302,6 +302,8 @@ typedef struct kp_solve_stats {
   uint64_t bytes_algorithmic; /* bytes the device algorithm reads+writes */
   uint64_t pops;            /* queue pops */
   uint64_t phase_cycles[8]; /* diagnostic (KP_TIMING=1): per-phase shader cycles of the solve loop */
+  uint64_t scanned;         /* diagnostic: in-flight NodeClaim positions the candidate pre-pass visited */
+  uint64_t cursor_starts;   /* diagnostic: sum of first-fit cursor start positions (positions skipped) */
 } kp_solve_stats;
 
 /* ---- context ---------------------------------------------------------------------------- */

@@ -92,6 +92,17 @@ struct SolveArgs {
   const int32_t* own_self;           // the group's selector matches the owner pod
   const uint64_t* own_pd;            // podDomains (strict requirements) over the key's value ordinals
   const uint64_t* sl_topo_keys;      // [SL] dictionary keys of the owned groups
+  // first-fit cursors (exact): cur_*[sl] = {k, t}: the first k candidates of the scan order were known to
+  // fail for shape-level sl at mutation time t; a mutation stack (t, position, in LDS) clamps k to the lowest
+  // position changed since (monotone stack: suffix minimum by binary search). Shape-levels that own
+  // topology groups do not use them (their outcome depends on the counts).
+  int32_t* cur_nc;                   // [SL][2] in-flight NodeClaims (positions in the sorted order)
+  int32_t* cur_ex;                   // [SL][2] existing nodes (upstream order)
+  int32_t n_tk;                      // topology keys (dictionary keys some group spreads over)
+  const int32_t* tk_keys;            // [TK]
+  uint8_t* nc_tcode;                 // [TK][hnc_stride] pinned value ordinal per NodeClaim (store_tcodes)
+  const uint8_t* ex_static_ok;       // [E] every unrequested resource fits and nothing available is negative
+  int32_t n_req_res;                 // popcount(req_res_mask)
   const int32_t* tkey_slot;          // [64] row of a topology key in ex_tcode
   const uint8_t* ex_tcode;           // [TK][E] value ordinal of the existing node's label (0xFF: none)
   // outputs

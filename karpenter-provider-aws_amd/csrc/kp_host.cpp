@@ -912,6 +912,7 @@ struct Compiled {
   vector<int32_t> sl_own_base, sl_own_n, own_group, own_self;
   vector<uint64_t> own_pd, sl_topo_keys;
   vector<int32_t> tkey_slot;  // [64]
+  vector<int32_t> tk_keys;    // [TK]
   vector<uint8_t> ex_tcode;   // [TK][E]
 };
 
@@ -1065,8 +1066,31 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
     }
     return domain_tsets[k] = m;
   };
+  // bound pods grouped by (namespace, labels): deployments repeat one label set over many pods
+  struct BoundSet {
+    string ns;
+    std::map<string, string> labels;
+    vector<uint32_t> nodes;  // input indices, one entry per bound pod
+  };
+  vector<BoundSet> bsets;
+  {
+    std::map<std::pair<string, std::map<string, string>>, int> idx;
+    for (uint32_t b = 0; b < in->n_bound_pods; b++) {
+      const kp_bound_pod& bp = in->bound_pods[b];
+      if (bp.node >= in->n_existing) return fail(KP_E_INVAL, "bound pod %u: node %u", b, bp.node);
+      auto key = std::make_pair(string(bp.namespace_ ? bp.namespace_ : ""), LabelMap(bp.labels, bp.n_labels));
+      auto it = idx.find(key);
+      if (it == idx.end()) {
+        it = idx.emplace(key, (int)bsets.size()).first;
+        bsets.push_back({key.first, key.second, {}});
+      }
+      bsets[it->second].nodes.push_back(bp.node);
+    }
+  }
   std::map<string, int> ids;
+  std::map<string, uint64_t> node_domains;
   vector<int> g_shape;  // shape that created the group (its tolerations / filter)
+  vector<const kp_topology_spread*> g_spec;
   // group identity per (shape, spread index)
   vector<vector<int>> sgroup(in->n_shapes);
   vector<char> seen(in->n_shapes, 0);
@@ -1090,6 +1114,7 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
     const int g = cp.G++;
     ids[id] = g;
     g_shape.push_back((int)s);
+    g_spec.push_back(&t);
     int k = -1, row = -1;
     if (key == kHostname) {
       row = cp.GH++;
@@ -1097,7 +1122,10 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
       k = d.key(key);
       if (k < 0) return fail(KP_E_INVAL, "topology key %s missing from the dictionary", key.c_str()), -1;
       if (d.dd.nval[k] > 64) return fail(KP_E_UNSUPPORTED, "topology key %s has > 64 values", key.c_str()), -1;
-      if (cp.tkey_slot[k] < 0) cp.tkey_slot[k] = cp.TK++;
+      if (cp.tkey_slot[k] < 0) {
+        cp.tkey_slot[k] = cp.TK++;
+        cp.tk_keys.push_back(k);
+      }
     }
     cp.tg_key.push_back(k);
     cp.tg_row.push_back(row);
@@ -1131,11 +1159,9 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
       return true;
     };
     const string ns = sh.namespace_ ? sh.namespace_ : "";
-    for (uint32_t b = 0; b < in->n_bound_pods; b++) {
-      const kp_bound_pod& bp = in->bound_pods[b];
-      if (ns != (bp.namespace_ ? bp.namespace_ : "")) continue;
-      if (!SelectorMatches(t.selector, LabelMap(bp.labels, bp.n_labels))) continue;
-      const uint32_t ni = bp.node;
+    for (auto& bs : bsets) {
+      if (ns != bs.ns || !SelectorMatches(t.selector, bs.labels)) continue;
+      for (const uint32_t ni : bs.nodes) {
       if (row >= 0) {  // hostname: the node's label or, failing that, its name — one domain per node
         if (!filter_ok(ni)) continue;
         uint8_t& c = cp.hcnt0[(size_t)row * std::max(E, 1) + ex_pos[ni]];
@@ -1147,13 +1173,23 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
         cp.tg_cnt[(size_t)g * 64 + ord]++;
         cp.tg_reg[g] |= 1ull << ord;
       }
-    }
-    if (k >= 0)
-      for (uint32_t ni = 0; ni < in->n_existing; ni++) {
-        auto lv = node_labels[ni].find(key);
-        if (lv == node_labels[ni].end() || !filter_ok(ni)) continue;
-        cp.tg_reg[g] |= 1ull << (d.bit(k, lv->second) - k * 64);
       }
+    }
+    if (k >= 0) {  // the existing nodes' domains depend only on (key, node filter): cached across groups
+      string fid = key + "|" + std::to_string(aff && nonempty) + "[" + KCanon(d, filt) + "]" +
+                   (taint ? std::to_string(cp.shape_tolerates[s]) : string("-"));
+      auto it = node_domains.find(fid);
+      if (it == node_domains.end()) {
+        uint64_t m = 0;
+        for (uint32_t ni = 0; ni < in->n_existing; ni++) {
+          auto lv = node_labels[ni].find(key);
+          if (lv == node_labels[ni].end() || !filter_ok(ni)) continue;
+          m |= 1ull << (d.bit(k, lv->second) - k * 64);
+        }
+        it = node_domains.emplace(fid, m).first;
+      }
+      cp.tg_reg[g] |= it->second;
+    }
     return g;
   };
   for (uint32_t p = 0; p < in->n_pods; p++) {  // NewTopology: Update(pod) in pod order
@@ -1171,22 +1207,40 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
   if ((size_t)cp.GH * (size_t)(E + in->n_pods) > ((size_t)1 << 31))
     return fail(KP_E_UNSUPPORTED, "%d hostname topologies x %u nodes", cp.GH, E + in->n_pods);
   if (E == 0) cp.hcnt0.clear();
-  // recording groups per shape (TopologyGroup.selects: namespace + selector on the pod's labels)
+  // recording groups per shape (TopologyGroup.selects: namespace + selector on the pod's labels); shapes are
+  // indexed by (namespace, label) so a matchLabels selector only tests the shapes carrying its first label
+  vector<std::map<string, string>> shape_labels(in->n_shapes);
+  std::map<string, vector<uint32_t>> by_label, by_ns;
   for (uint32_t s = 0; s < in->n_shapes; s++) {
     const kp_pod_shape& sh = in->shapes[s];
-    const std::map<string, string> lm = LabelMap(sh.labels, sh.n_labels);
+    shape_labels[s] = LabelMap(sh.labels, sh.n_labels);
     const string ns = sh.namespace_ ? sh.namespace_ : "";
-    cp.shape_rec_base[s] = (int32_t)cp.rec_list.size();
-    cp.shape_rec_n[s] = 0;
-    for (int g = 0; g < cp.G; g++) {
-      const kp_pod_shape& owner = in->shapes[g_shape[g]];
-      const kp_topology_spread* spec = nullptr;
-      for (uint32_t j = 0; j < owner.n_topology_spread && !spec; j++)
-        if (sgroup[g_shape[g]].size() > j && sgroup[g_shape[g]][j] == g) spec = &owner.topology_spread[j];
-      if (!spec || ns != (owner.namespace_ ? owner.namespace_ : "") || !SelectorMatches(spec->selector, lm)) continue;
-      cp.rec_list.push_back(g);
-      cp.shape_rec_n[s]++;
+    by_ns[ns].push_back(s);
+    for (auto& kv : shape_labels[s]) by_label[ns + '\x01' + kv.first + '\x01' + kv.second].push_back(s);
+  }
+  vector<vector<int>> recs(in->n_shapes);
+  static const vector<uint32_t> kNone;
+  for (int g = 0; g < cp.G; g++) {
+    const kp_pod_shape& owner = in->shapes[g_shape[g]];
+    const kp_label_selector& sel = g_spec[g]->selector;
+    const string ns = owner.namespace_ ? owner.namespace_ : "";
+    const vector<uint32_t>* cands;
+    if (sel.is_nil) continue;
+    if (sel.n_match_labels) {
+      auto it = by_label.find(ns + '\x01' + (sel.match_labels[0].key ? sel.match_labels[0].key : "") + '\x01' +
+                              (sel.match_labels[0].value ? sel.match_labels[0].value : ""));
+      cands = it == by_label.end() ? &kNone : &it->second;
+    } else {
+      auto it = by_ns.find(ns);
+      cands = it == by_ns.end() ? &kNone : &it->second;
     }
+    for (uint32_t s : *cands)
+      if (SelectorMatches(sel, shape_labels[s])) recs[s].push_back(g);
+  }
+  for (uint32_t s = 0; s < in->n_shapes; s++) {
+    cp.shape_rec_base[s] = (int32_t)cp.rec_list.size();
+    cp.shape_rec_n[s] = (int32_t)recs[s].size();
+    cp.rec_list.insert(cp.rec_list.end(), recs[s].begin(), recs[s].end());
   }
   // owned groups per shape-level: (group, self-selecting, podDomains mask over the key's value ordinals)
   for (uint32_t s = 0; s < in->n_shapes; s++) {
@@ -1656,7 +1710,22 @@ int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out
                o_srb = blob.put(C.shape_rec_base), o_srn = blob.put(C.shape_rec_n), o_recl = blob.put(C.rec_list),
                o_slob = blob.put(C.sl_own_base), o_slon = blob.put(C.sl_own_n), o_owng = blob.put(C.own_group),
                o_owns = blob.put(C.own_self), o_ownp = blob.put(C.own_pd), o_sltk = blob.put(C.sl_topo_keys),
-               o_tks = blob.put(C.tkey_slot), o_extc = blob.put(C.ex_tcode);
+               o_tks = blob.put(C.tkey_slot), o_extc = blob.put(C.ex_tcode), o_tkk = blob.put(C.tk_keys);
+  uint32_t rmask = 0;
+  for (size_t i = 0; i < C.shape_requests.size(); i++)
+    if (C.shape_requests[i] > 0) rmask |= 1u << (i % KP_NRES);
+  for (size_t i = 0; i < C.tmpl_daemon.size(); i++)
+    if (C.tmpl_daemon[i] > 0) rmask |= 1u << (i % KP_NRES);
+  vector<uint8_t> ex_static(std::max(E, 1), 0);  // unrequested resources of an existing node never change
+  for (int e = 0; e < E; e++) {
+    bool ok = true;
+    for (int r = 0; r < KP_NRES; r++) {
+      const int64_t av = C.ex_available[(size_t)e * KP_NRES + r], rq = C.ex_requests[(size_t)e * KP_NRES + r];
+      if (av < 0 || (!((rmask >> r) & 1) && rq > av)) ok = false;
+    }
+    ex_static[e] = ok ? 1 : 0;
+  }
+  const size_t o_exso = blob.put(ex_static);
   // ---- mutable state: restored from a pristine device copy before every run ----
   vector<int32_t> zeros_p(Pc, 0);
   const size_t o_mut = blob.reserve(0);
@@ -1693,6 +1762,8 @@ int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out
   const size_t o_ncver = blob.reserve(sizeof(int32_t) * Pc);
   const size_t o_exver = blob.reserve(sizeof(int32_t) * std::max(E, 1));
   const size_t o_tver = blob.reserve(sizeof(int32_t) * std::max(NT, 1));
+  const size_t o_curnc = blob.reserve(sizeof(int32_t) * 2 * SLn);  // cursors start at {0, 0} (zeroed per run)
+  const size_t o_curex = blob.reserve(sizeof(int32_t) * 2 * SLn);
   const size_t n_ver = blob.host.size() - o_ver0;
   const size_t o_fail0 = blob.reserve(0);
   const size_t o_ncfail = blob.reserve(sizeof(int32_t) * SLn * ncc);
@@ -1705,6 +1776,7 @@ int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out
   const size_t o_nopt = blob.reserve(sizeof(uint32_t) * Pc);
   const size_t n_hcnc = (size_t)C.GH * Pc;
   const size_t o_hcnc = blob.reserve(std::max<size_t>(n_hcnc, 1));
+  const size_t o_nctc = blob.reserve(std::max<size_t>((size_t)C.TK * Pc, 1));
   const size_t total_bytes = blob.host.size();
 
   HIPCHK(hipMalloc(&plan->buf.p, total_bytes));
@@ -1767,6 +1839,8 @@ int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out
   a.ex_fail = (int32_t*)(base + o_exfail);
   a.tmpl_ver = (int32_t*)(base + o_tver);
   a.tmpl_fail = (int32_t*)(base + o_tfail);
+  a.cur_nc = (int32_t*)(base + o_curnc);
+  a.cur_ex = (int32_t*)(base + o_curex);
   a.nc_maxalloc = (int64_t*)(base + o_maxalloc);
   a.nc_fitj = (int32_t*)(base + o_fitj);
   a.nc_taintset = (int32_t*)(base + o_ncts);
@@ -1775,6 +1849,7 @@ int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out
     if (C.shape_requests[i] > 0) a.req_res_mask |= 1u << (i % KP_NRES);
   for (size_t i = 0; i < C.tmpl_daemon.size(); i++)  // Fits iterates every resource of the merged requests
     if (C.tmpl_daemon[i] > 0) a.req_res_mask |= 1u << (i % KP_NRES);
+  a.n_req_res = __builtin_popcount(a.req_res_mask);
   a.timing = getenv("KP_TIMING") ? 1 : 0;
   a.n_groups = C.G;
   a.tg_key = (const int32_t*)(base + o_tgk);
@@ -1801,6 +1876,10 @@ int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out
   a.own_pd = (const uint64_t*)(base + o_ownp);
   a.sl_topo_keys = (const uint64_t*)(base + o_sltk);
   a.tkey_slot = (const int32_t*)(base + o_tks);
+  a.n_tk = C.TK;
+  a.tk_keys = (const int32_t*)(base + o_tkk);
+  a.nc_tcode = base + o_nctc;
+  a.ex_static_ok = base + o_exso;
   a.ex_tcode = base + o_extc;
   plan->o_hcnc = o_hcnc;
   plan->n_hcnc = n_hcnc;
@@ -1951,6 +2030,8 @@ int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out) {
   res->stats.pops = stats[2];
   res->stats.prepare_ms = plan->prepare_ms;
   for (int i = 0; i < 8; i++) res->stats.phase_cycles[i] = stats[8 + i];
+  res->stats.scanned = stats[5];
+  res->stats.cursor_starts = stats[6];
   res->stats.host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   *out = res.release();
   return KP_OK;
@@ -2305,7 +2386,22 @@ int32_t kp_cluster_prepare(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan** 
                o_srb = blob.put(C.shape_rec_base), o_srn = blob.put(C.shape_rec_n), o_recl = blob.put(C.rec_list),
                o_slob = blob.put(C.sl_own_base), o_slon = blob.put(C.sl_own_n), o_owng = blob.put(C.own_group),
                o_owns = blob.put(C.own_self), o_ownp = blob.put(C.own_pd), o_sltk = blob.put(C.sl_topo_keys),
-               o_tks = blob.put(C.tkey_slot), o_extc = blob.put(C.ex_tcode);
+               o_tks = blob.put(C.tkey_slot), o_extc = blob.put(C.ex_tcode), o_tkk = blob.put(C.tk_keys);
+  uint32_t rmask = 0;
+  for (size_t i = 0; i < C.shape_requests.size(); i++)
+    if (C.shape_requests[i] > 0) rmask |= 1u << (i % KP_NRES);
+  for (size_t i = 0; i < C.tmpl_daemon.size(); i++)
+    if (C.tmpl_daemon[i] > 0) rmask |= 1u << (i % KP_NRES);
+  vector<uint8_t> ex_static(std::max(E, 1), 0);  // unrequested resources of an existing node never change
+  for (int e = 0; e < E; e++) {
+    bool ok = true;
+    for (int r = 0; r < KP_NRES; r++) {
+      const int64_t av = C.ex_available[(size_t)e * KP_NRES + r], rq = C.ex_requests[(size_t)e * KP_NRES + r];
+      if (av < 0 || (!((rmask >> r) & 1) && rq > av)) ok = false;
+    }
+    ex_static[e] = ok ? 1 : 0;
+  }
+  const size_t o_exso = blob.put(ex_static);
   const size_t o_exrq = blob.put(C.ex_requests);
   const size_t o_exin = blob.put(ex_init);
   const size_t o_pshape = blob.put(C.pod_shape);

@@ -477,6 +477,20 @@ __device__ void store_merged(KReqs* dst, const ReqView& rv, uint64_t m_v, int W,
   }
 }
 
+// Pinned domain of each topology key on a NodeClaim's (merged) requirements: the value ordinal when the key
+// is In{one value}, 0xFE when it admits no value, 0xFF otherwise (multi-valued, complement or absent).
+__device__ void store_tcodes(const SolveArgs& a, const ReqView& rv, uint64_t m_v, int nc) {
+  const int lane = LANE;
+  for (int j = 0; j < a.n_tk; j++) {
+    const int k = a.tk_keys[j];
+    const uint64_t w = lane_bcast(m_v, k);
+    uint8_t code = 0xFF;
+    if (((rv.present >> k) & 1) && !((rv.compl_ >> k) & 1))
+      code = w == 0 ? 0xFE : (__builtin_popcountll(w) == 1 ? (uint8_t)__builtin_ctzll(w) : 0xFF);
+    if (lane == 0) a.nc_tcode[(size_t)j * a.hnc_stride + nc] = code;
+  }
+}
+
 // Ordered compaction of per-thread candidate flags into s_list (positions in scan order). Returns count.
 template <int NW>
 __device__ __forceinline__ int compact_candidates(bool cand, int pos, int32_t* s_list, int32_t* s_wcnt) {
@@ -493,6 +507,46 @@ __device__ __forceinline__ int compact_candidates(bool cand, int pos, int32_t* s
   if (cand) s_list[before + __builtin_popcountll(bal & ((1ull << lane) - 1))] = pos;
   __syncthreads();
   return total;
+}
+
+// Same for 4 rounds of positions per thread: round k covers pos0 + k * NT (NT = NW * 64 threads), so for a short
+// scan only round 0 is live; one barrier pair for all rounds. s_list holds 4 * NT entries; s_wcnt 4 * NW.
+template <int NW>
+__device__ __forceinline__ int compact_candidates_x4(uint32_t flags, int pos0, int32_t* s_list, int32_t* s_wcnt) {
+  constexpr int NT = NW * 64;
+  const int wave = threadIdx.x >> 6, lane = LANE;
+  uint64_t bal[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) bal[k] = __ballot((flags >> k) & 1);
+  if (lane < 4) s_wcnt[lane * NW + wave] = __builtin_popcountll(bal[lane & 3]);
+  __syncthreads();
+  int total = 0, before[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    int b = total;
+    for (int w = 0; w < NW; w++) {
+      const int c = s_wcnt[k * NW + w];
+      b += w < wave ? c : 0;
+      total += c;
+    }
+    before[k] = b;
+  }
+  const uint64_t lt = (1ull << lane) - 1;
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+    if ((flags >> k) & 1) s_list[before[k] + __builtin_popcountll(bal[k] & lt)] = pos0 + k * NT;
+  __syncthreads();
+  return total;
+}
+
+// LDS atomic min of the first scan position (round k: pos0 + k * NT) whose flag is set, one atomic per wave
+// and round (the wave's lowest lane holds its lowest position).
+template <int NT>
+__device__ __forceinline__ void first_pos_min(uint32_t flags, int pos0, int32_t* dst) {
+  for (int k = 0; k < 4; k++) {
+    const uint64_t b = __ballot((flags >> k) & 1);
+    if (b && LANE == __builtin_ctzll(b)) atomicMin(dst, pos0 + k * NT);
+  }
 }
 
 template <int NW>
@@ -528,6 +582,33 @@ __device__ void store_maxalloc(const DevCatalog& Cg, uint64_t X, int T, uint32_t
     mx = wave_max_i64(mx);
     if (lane == 0) dst[r] = mx;
   }
+}
+
+// mutation stack (LDS): entries (t, pos) with t and pos increasing bottom to top; the lowest position mutated
+// after time `stamp` is the pos of the first entry with t > stamp. On overflow the bottom half is dropped and
+// `lost` remembers the newest dropped time: a query older than it answers 0 (conservative).
+#define MSTK_CAP 512
+__device__ int mstack_query(const int32_t* stk, int n, int lost, int stamp) {
+  if (stamp < lost) return 0;
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int m = (lo + hi) >> 1;
+    if (stk[2 * m] > stamp) hi = m;
+    else lo = m + 1;
+  }
+  return lo < n ? stk[2 * lo + 1] : INT32_MAX;
+}
+__device__ void mstack_push(int32_t* stk, int32_t& n, int32_t& lost, int t, int pos) {
+  while (n > 0 && stk[2 * (n - 1) + 1] >= pos) n--;
+  if (n == MSTK_CAP) {
+    const int h = MSTK_CAP / 2;
+    lost = stk[2 * (h - 1)];
+    for (int i = 0; i < 2 * h; i++) stk[i] = stk[2 * h + i];
+    n = h;
+  }
+  stk[2 * n] = t;
+  stk[2 * n + 1] = pos;
+  n++;
 }
 
 template <int NT>
@@ -574,6 +655,8 @@ __device__ void sort_newnodeclaims(int32_t* ord, const int32_t* npods, int n, in
       }
     }
     if (mode == 3) go_sort_slice(S, n);
+    // lowest sorted position whose NodeClaim changed or moved since the last sort (cursor clamp)
+    s_ctl[16] = mode == 3 ? 0 : (mut == 1 ? p : (mut == 2 ? (mode == 2 ? q : n - 1) : -1));
     s_ctl[7] = mode;
     s_ctl[8] = q;
     s_ctl[9] = mode == 1 ? ord[p] : (mode == 2 ? ord[n - 1] : 0);
@@ -604,15 +687,16 @@ __device__ void sort_newnodeclaims(int32_t* ord, const int32_t* npods, int n, in
   __syncthreads();
 }
 
-template <int NW>
+template <int NW, bool TOPO>  // TOPO: the batch has topology spread groups (else that code compiles out)
 __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
   constexpr int NT = NW * 64;
   __shared__ DevDict D;
   __shared__ WaveSlots slots[NW];
   __shared__ int32_t s_ok[NW];
-  __shared__ int32_t s_wcnt[NW];
-  __shared__ int32_t s_ctl[16];
-  __shared__ int32_t s_list[NT];
+  __shared__ int32_t s_wcnt[4 * NW];
+  __shared__ int32_t s_ctl[32];
+  __shared__ int32_t s_stk[2][2 * MSTK_CAP];  // mutation stacks: [0] in-flight positions, [1] existing positions
+  __shared__ int32_t s_list[4 * NT];
   __shared__ uint32_t s_scratch[NW][2 * KP_MAX_WORDS];
   __shared__ KReqs s_B;  // the popped pod's requirements, staged once per pod
   __shared__ int32_t s_fitj[NW][KP_NRES];
@@ -649,7 +733,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
         if (tid == 0) s_fitg[c][r] = a.cats[c].fit_vals + (size_t)r * D.T;
     }
   }
-  uint64_t bytes = 0, attempts = 0, pops = 0;
+  uint64_t bytes = 0, attempts = 0, pops = 0, scanned = 0, starts = 0;
   uint64_t tph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tlast = 0;
   const bool timing = a.timing && tid == 0;
 #define TS(ph)                                          \
@@ -669,6 +753,15 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
     s_ctl[5] = 1;
     s_ctl[10] = 0;  // pending mutation of newNodeClaims since the last sort: 0 none, 1 +1 at s_ctl[11], 2 appended
     s_ctl[11] = 0;
+    s_ctl[12] = 0;  // in-flight mutation stack size / time / lost
+    s_ctl[13] = 0;
+    s_ctl[20] = -1;
+    s_ctl[14] = 0;  // existing-node mutation stack size / time / lost
+    s_ctl[15] = 0;
+    s_ctl[21] = -1;
+    s_ctl[17] = 0;  // existing scan start for the popped pod
+    s_ctl[22] = 0;  // in-flight cursor of the popped pod's shape-level (staged)
+    s_ctl[23] = 0;
   }
   __syncthreads();
 
@@ -701,6 +794,14 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
       for (int i = tid; i < (int)(sizeof(KReqs) / 8); i += NT) dst[i] = src[i];
       if (tid < KP_NRES) s_preq[tid] = a.shape_requests[(size_t)shape * KP_NRES + tid];
       else if (tid >= 64 && tid < 64 + KP_MAX_KEYS) s_pslot[tid - 64] = a.pvp_slot[(size_t)sl * KP_MAX_KEYS + tid - 64];
+      else if (tid == 128) {  // first-fit cursors of the shape-level (LDS stacks: no global round trips)
+        const int ce = a.n_existing ? min(a.cur_ex[2 * sl], mstack_query(s_stk[1], s_ctl[14], s_ctl[21], a.cur_ex[2 * sl + 1])) : 0;
+        s_ctl[17] = min(ce, a.n_existing);
+        s_ctl[22] = a.cur_nc[2 * sl];
+        s_ctl[23] = a.cur_nc[2 * sl + 1];
+        s_ctl[24] = INT32_MAX;  // first count-independent pass (existing / in-flight), topology shape-levels
+        s_ctl[25] = INT32_MAX;
+      }
     }
     __syncthreads();
     TS(0);
@@ -709,7 +810,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
     const uint64_t tolmask = a.shape_tolerates[shape];
     int placed = -1;  // >= 0 NodeClaim id; <= -2 existing node; -1 not placed
     // ---- topology: stage the owned groups (one wave each) -----------------------------------------
-    const int own_n = a.n_groups ? a.sl_own_n[sl] : 0;
+    const int own_n = TOPO ? a.sl_own_n[sl] : 0;
     const uint64_t topo_keys = own_n ? a.sl_topo_keys[sl] : 0;
     const uint64_t b_keys = s_B.present | topo_keys;  // keys whose type filter must be redone on Add
     if (own_n) {
@@ -742,29 +843,39 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
     }
 
     // ---- addToExistingNode: lowest index whose CanAdd succeeds -------------------------------
-    for (int base = 0; base < a.n_existing && placed == -1; base += NT) {
-      const int e = base + tid;
-      bool cand = false;
-      if (e < a.n_existing && ((tolmask >> a.ex_taintset[e]) & 1) && a.ex_fail[(size_t)sl * a.n_existing + e] != a.ex_ver[e]) {
-        const int64_t* av = a.ex_available + (size_t)e * KP_NRES;
-        const int64_t* rq = a.ex_requests + (size_t)e * KP_NRES;
-        bool fits = true;  // Fits(Merge(requests, pod), available): CanAdd's resource check, exact
-        for (int r = 0; r < KP_NRES; r++) fits = fits && av[r] >= 0 && rq[r] + s_preq[r] <= av[r];
-        cand = fits;
-        // topology, exact: the node's domain for a dictionary key is its label value (or the key is
-        // undefined on it: incompatible); hostname: count + self <= maxSkew (min is 0 for hostname)
+    for (int base = s_ctl[17]; base < a.n_existing && placed == -1; base += 4 * NT) {
+      uint32_t flags = 0, iflags = 0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {  // 4 rounds per thread: independent, so their loads overlap
+        const int ec = base + k * NT + tid;
+        if (ec >= a.n_existing) continue;
+        bool cand = a.ex_fail[(size_t)sl * a.n_existing + ec] != a.ex_ver[ec] && a.ex_static_ok[ec] &&
+                    ((tolmask >> a.ex_taintset[ec]) & 1);
+        if (cand) {  // Fits(Merge(requests, pod), available), exact: unrequested resources never change
+          const int64_t* av = a.ex_available + (size_t)ec * KP_NRES;
+          const int64_t* rq = a.ex_requests + (size_t)ec * KP_NRES;
+          for (int r = 0; r < KP_NRES; r++)
+            if ((a.req_res_mask >> r) & 1) cand &= rq[r] + s_preq[r] <= av[r];
+        }
+        // topology, exact: hostname: count + self <= maxSkew (min is 0 for hostname; the count only changes
+        // when the node takes a pod, i.e. with its version); dictionary key: the node's domain is its label
+        // value (or the key is undefined on it: incompatible), acceptable under the current counts
+        for (int j = 0; j < own_n && cand; j++)
+          if (s_town[j].key < 0)
+            cand = (int)a.hcnt_ex[(size_t)s_town[j].row * a.n_existing + ec] + s_town[j].self <= s_town[j].maxskew;
+        if (cand) iflags |= 1u << k;  // passes everything that does not depend on the zone counts
         for (int j = 0; j < own_n && cand; j++) {
           const TopoOwn& o = s_town[j];
           if (o.key >= 0) {
-            const uint8_t code = a.ex_tcode[(size_t)o.slot * a.n_existing + e];
-            cand = code != 0xFF && ((s_tacc[j] >> code) & 1);
-          } else {
-            cand = (int)a.hcnt_ex[(size_t)o.row * a.n_existing + e] + o.self <= o.maxskew;
+            const uint8_t code = a.ex_tcode[(size_t)o.slot * a.n_existing + ec];
+            cand = code != 0xFF && ((s_tacc[j] >> (code & 63)) & 1);
           }
         }
+        flags |= (cand ? 1u : 0u) << k;
       }
-      const int n = compact_candidates<NW>(cand, e, s_list, s_wcnt);
-      bytes += (uint64_t)min(NT, a.n_existing - base) * (2 * KP_NRES * 8 + 8);
+      if (own_n) first_pos_min<NT>(iflags, base + tid, &s_ctl[24]);
+      const int n = compact_candidates_x4<NW>(flags, base + tid, s_list, s_wcnt);
+      if (wave == 0) bytes += (uint64_t)min(4 * NT, a.n_existing - base) * (16 * a.n_req_res + 13);  // once
       for (int r0 = 0; r0 < n; r0 += NW) {
         const int li = r0 + wave;
         bool ok = false;
@@ -795,37 +906,69 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
       }
     }
 
+    if (tid == 0 && a.n_existing) {
+      // cursor: every position before the winner failed; with topology, before the first position that passed
+      // the count-independent checks (a zone-count failure may pass later)
+      const int cpos = own_n ? min(s_ctl[24], a.n_existing) : (placed != -1 ? -2 - placed : a.n_existing);
+      a.cur_ex[2 * sl] = cpos;
+      a.cur_ex[2 * sl + 1] = s_ctl[15];
+      if (placed != -1) mstack_push(s_stk[1], s_ctl[14], s_ctl[21], ++s_ctl[15], -2 - placed);
+    }
     TS(1);
     if (placed == -1) {
       const bool in_lds = s_ctl[5] != 0;
       int32_t* ord = in_lds ? s_dyn : a.g_order;
       int32_t* npods = in_lds ? s_dyn + a.sort_cap : a.g_npods;
       // ---- sort.Slice(newNodeClaims, len(Pods) asc) -----------------------------------------------
+      // the cursor query (one lane of wave 1) overlaps the sort (thread 0); the pending mutation's own
+      // clamp (s_ctl[16], known after the sort) is folded in below and pushed by thread 0 afterwards
+      if (tid == 64) s_ctl[19] = min(s_ctl[22], mstack_query(s_stk[0], s_ctl[12], s_ctl[20], s_ctl[23]));
       sort_newnodeclaims<NT>(ord, npods, s_ctl[2], s_ctl[10], s_ctl[11], s_ctl);
-      if (tid == 0) s_ctl[10] = 0;
-      TS(2);
       const int n_nc = s_ctl[2];
+      const int start = min(min(s_ctl[19], s_ctl[16] >= 0 ? s_ctl[16] : INT32_MAX), n_nc);
+      if (tid == 0) {
+        s_ctl[10] = 0;
+        if (s_ctl[16] >= 0) mstack_push(s_stk[0], s_ctl[12], s_ctl[20], ++s_ctl[13], s_ctl[16]);
+      }
+      TS(2);
       // ---- addToInflightNode: first NodeClaim in that order whose Add succeeds ------------------
-      for (int base = 0; base < n_nc && placed == -1; base += NT) {
-        const int i = base + tid;
-        bool cand = false;
-        if (i < n_nc) {
+      for (int base = start; base < n_nc && placed == -1; base += 4 * NT) {
+        uint32_t flags = 0, iflags = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {  // 4 rounds per thread: independent, so their loads overlap
+          const int i = base + k * NT + tid;
+          if (i >= n_nc) continue;
           const int nc = ord[i];
-          cand = ((tolmask >> a.nc_taintset[nc]) & 1) &&
-                 !(nc < a.ncc && a.nc_fail[(size_t)sl * a.ncc + nc] == a.nc_ver[nc]);
+          // memo first: most NodeClaims fail there, and the lanes that do skip the gathers below
+          bool cand = !(nc < a.ncc && a.nc_fail[(size_t)sl * a.ncc + nc] == a.nc_ver[nc]) &&
+                      ((tolmask >> a.nc_taintset[nc]) & 1);
           if (cand) {
             const int64_t* rq = a.nc_requests + (size_t)nc * KP_NRES;
             const int64_t* mx = a.nc_maxalloc + (size_t)nc * KP_NRES;
             for (int r = 0; r < KP_NRES; r++)
-              if (((a.req_res_mask >> r) & 1) && rq[r] + s_preq[r] > mx[r]) cand = false;
+              if ((a.req_res_mask >> r) & 1) cand &= rq[r] + s_preq[r] <= mx[r];
           }
-          for (int j = 0; j < own_n && cand; j++)  // hostname topologies, exact
+          for (int j = 0; j < own_n && cand; j++)  // hostname topologies, exact (count changes with the version)
             if (s_town[j].key < 0)
               cand = (int)a.hcnt_nc[(size_t)s_town[j].row * a.hnc_stride + nc] + s_town[j].self <= s_town[j].maxskew;
+          if (cand) iflags |= 1u << k;  // passes everything that does not depend on the zone counts
+          for (int j = 0; j < own_n && cand; j++) {  // a NodeClaim pinned to one domain of a key can only take it
+            const TopoOwn& o = s_town[j];
+            if (o.key >= 0) {
+              const uint8_t code = a.nc_tcode[(size_t)o.slot * a.hnc_stride + nc];
+              cand = code == 0xFF || (code < 64 && ((s_tacc[j] >> (code & 63)) & 1));
+            }
+          }
+          flags |= (cand ? 1u : 0u) << k;
         }
-        const int n = compact_candidates<NW>(cand, i, s_list, s_wcnt);
+        if (own_n) first_pos_min<NT>(iflags, base + tid, &s_ctl[25]);
+        if (tid == 0) {
+          scanned += min(4 * NT, n_nc - base);
+          if (base == start) starts += start;
+        }
+        const int n = compact_candidates_x4<NW>(flags, base + tid, s_list, s_wcnt);
         TS(6);
-        bytes += (uint64_t)min(NT, n_nc - base) * 12;
+        if (wave == 0) bytes += (uint64_t)min(4 * NT, n_nc - base) * (12 + 16 * a.n_req_res);  // counted once
         for (int r0 = 0; r0 < n; r0 += NW) {
           const int li = r0 + wave;
           bool ok = false;
@@ -859,6 +1002,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
           if (win >= 0) {
             if (wave == win) {
               store_merged(reinterpret_cast<KReqs*>(a.nc_reqs + (size_t)nc * sizeof(KReqs)), rv, m_v, D.W, D.KB);
+              if (a.n_tk) store_tcodes(a, rv, m_v, nc);
               if (lane < D.TW) a.nc_X[(size_t)nc * D.TW + lane] = X;
               if (lane < KP_NRES) a.nc_requests[(size_t)nc * KP_NRES + lane] += s_preq[lane];
               if (lane == 0) {
@@ -871,6 +1015,9 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
             if (tid == 0) {
               s_ctl[10] = 1;
               s_ctl[11] = s_list[r0 + win];
+              // cursor: all positions before the winner failed (topology: before the first count-independent pass)
+              a.cur_nc[2 * sl] = own_n ? min(s_ctl[25], s_list[r0 + win]) : s_list[r0 + win];
+              a.cur_nc[2 * sl + 1] = s_ctl[13];
             }
           }
           __syncthreads();
@@ -881,6 +1028,10 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
 
     TS(3);
     if (placed == -1) {
+      if (tid == 0) {  // every in-flight NodeClaim failed
+        a.cur_nc[2 * sl] = own_n ? min(s_ctl[25], s_ctl[2]) : s_ctl[2];
+        a.cur_nc[2 * sl + 1] = s_ctl[13];
+      }
       // ---- addToNewNodeClaim: templates in weight order --------------------------------------------
       for (int base = 0; base < a.n_tmpl && placed == -1; base += NT) {
         const int t = base + tid;
@@ -938,6 +1089,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
           if (win >= 0) {
             if (wave == win) {
               store_merged(reinterpret_cast<KReqs*>(a.nc_reqs + (size_t)nc * sizeof(KReqs)), rv, m_v, D.W, D.KB);
+              if (a.n_tk) store_tcodes(a, rv, m_v, nc);
               if (lane < D.TW) a.nc_X[(size_t)nc * D.TW + lane] = X;
               if (lane < KP_NRES)
                 a.nc_requests[(size_t)nc * KP_NRES + lane] = a.tmpl_daemon[(size_t)tm * KP_NRES + lane] + s_preq[lane];
@@ -998,7 +1150,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
 
     // ---- Topology.Record: every group selecting the pod whose node filter admits the node counts it
     //      in the node's domain (dictionary keys: only once the key is a single value) -------------
-    if (placed != -1 && a.n_groups && wave == 0) {
+    if (TOPO && placed != -1 && wave == 0) {
       const int rn = a.shape_rec_n[shape];
       const bool ex = placed <= -2;
       const int idx = ex ? -2 - placed : placed;
@@ -1071,6 +1223,8 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
     a.stats[2] = pops;
     a.stats[3] = (uint64_t)s_ctl[2];
     a.stats[4] = (uint64_t)s_ctl[4];
+    a.stats[5] = scanned;  // in-flight positions scanned by the pre-pass
+    a.stats[6] = starts;   // sum of cursor start positions
   }
   if (s_ctl[5])
     for (int i = tid; i < s_ctl[2]; i += NT) {
@@ -1250,9 +1404,9 @@ __global__ __launch_bounds__(FEAS_WAVES * 64) void feasibility_kernel(FeasArgs a
 // launchers
 // ------------------------------------------------------------------------------------------------
 hipError_t launch_solve(const SolveArgs& a, int nw, size_t dyn_lds, hipStream_t s) {
-  if (nw == 4) hipLaunchKernelGGL(solve_kernel<4>, dim3(1), dim3(4 * 64), dyn_lds, s, a);
-  else if (nw == 16) hipLaunchKernelGGL(solve_kernel<16>, dim3(1), dim3(16 * 64), dyn_lds, s, a);
-  else hipLaunchKernelGGL(solve_kernel<8>, dim3(1), dim3(8 * 64), dyn_lds, s, a);
+  (void)nw;  // 8 waves: one candidate per wave, 512 pre-pass lanes
+  if (a.n_groups) hipLaunchKernelGGL((solve_kernel<8, true>), dim3(1), dim3(8 * 64), dyn_lds, s, a);
+  else hipLaunchKernelGGL((solve_kernel<8, false>), dim3(1), dim3(8 * 64), dyn_lds, s, a);
   return hipGetLastError();
 }
 hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s) {

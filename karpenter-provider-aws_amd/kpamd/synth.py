@@ -94,7 +94,7 @@ def config5(catalog, n_pods=1_000_000, seed=5, n_shapes=512):
     pools = []
     for w in range(1, 21):
         name = f"pool-{w:02d}"
-        limits = {"cpu": int(rng.integers(2_000, 20_000)) * 1000}
+        limits = {"cpu": int(rng.integers(20_000, 200_000)) * 1000}  # ~2.2M cores in all: the burst spills by weight
         if w <= 4:
             pools.append(NodePool(name, w, 0, [(K + "instance-gpu-manufacturer", "In", ["nvidia"])],
                                   taints=[("nvidia.com/gpu", "true", "NoSchedule")], limits=limits))

@@ -1,4 +1,4 @@
-"""Diagnostic: per-phase cycle split of solve_kernel (KP_TIMING=1) on the config-2 workload."""
+"""Diagnostic: per-phase cycle split of solve_kernel (KP_TIMING=1). usage: profile_solve.py [config] [pods]"""
 import json
 import os
 import sys
@@ -9,19 +9,23 @@ sys.path.insert(0, os.path.join(REPO, "karpenter-provider-aws_amd"))
 import kpamd  # noqa: E402
 from kpamd import catalog, synth  # noqa: E402
 
-n = int(sys.argv[1]) if len(sys.argv) > 1 else 50000
+cfg = sys.argv[1] if len(sys.argv) > 1 else "2"
+n = int(sys.argv[2]) if len(sys.argv) > 2 else {"2": 50000, "3": 100000, "5": 300000}[cfg]
 lib = kpamd.load_lib()
 cat = catalog.build_catalog(lib)
-prob = synth.config2(cat, n_pods=n, seed=2)
+prob = {"2": lambda: synth.config2(cat, n_pods=n, seed=2), "3": lambda: synth.config3(cat, n_pods=n),
+        "5": lambda: synth.config5(cat, n_pods=n)}[cfg]()
 ctx = kpamd.Context(0)
 plan = kpamd.Scheduler(ctx, prob).prepare()
 plan.run(read=False)
 r = plan.run(read=True)
 st = r["stats"]
-names = ["pop+stageB", "existing", "sort", "inflight-commit", "templates", "bookkeeping", "inflight-prepass", "inflight-attempts"]
+names = ["pop+stage", "existing", "sort", "inflight-commit", "templates", "record+bookkeeping", "inflight-prepass",
+         "inflight-attempts"]
 tot = sum(st["phase_cycles"]) or 1
-out = {"pods": n, "solve_kernel_ms": st["solve_kernel_ms"], "attempts": st["attempts"], "pops": st["pops"],
-       "nodeclaims": len(r["nodeclaims"]), "attempts_per_pod": st["attempts"] / n,
-       "phase_share": {k: round(v / tot, 4) for k, v in zip(names, st["phase_cycles"]) },
-       "cycles_per_pod": tot / n}
+out = {"config": cfg, "pods": n, "solve_kernel_ms": st["solve_kernel_ms"], "attempts": st["attempts"],
+       "pops": st["pops"], "nodeclaims": len(r["nodeclaims"]), "attempts_per_pop": st["attempts"] / max(1, st["pops"]),
+       "phase_share": {k: round(v / tot, 4) for k, v in zip(names, st["phase_cycles"])},
+       "cycles_per_pop": tot / max(1, st["pops"]), "scanned_per_pop": st["scanned"] / max(1, st["pops"]),
+       "cursor_start_per_pop": st["cursor_starts"] / max(1, st["pops"])}
 print(json.dumps(out))
