@@ -11,6 +11,12 @@ synchronize on both sides, max over ranks (RCCL all-reduce of one float).
 
 cpu_baseline: the oracle (oracle/liboracle.so, single thread, kind "port") on a bounded sample of the
 same workload (the config-2 generator with fewer pods), rank 0 at N=1 only.
+
+Extra legs on the same line (the headline `value` is config 2):
+  feasibility   pods x instance-types CompatibleAvailableFilter over config 2's 50k pod rows (HBM roofline)
+  configs       config 1 (1k pods, kwok pool), config 3 (100k pods, zone + hostname topology spread onto 5k
+                existing nodes), config 5 (1M-pod burst, 20 weighted pools with limits, GPU/Neuron pools)
+  consolidation config 4 (1M candidate subsets of a 10k-node cluster, sharded over ranks)
 """
 import argparse
 import json
@@ -38,6 +44,9 @@ def main():
     ap.add_argument("--subsets", type=int, default=1_000_000)
     ap.add_argument("--cpu-sample-sims", type=int, default=16)
     ap.add_argument("--no-consolidation", action="store_true")
+    ap.add_argument("--c3-pods", type=int, default=100_000)
+    ap.add_argument("--c5-pods", type=int, default=1_000_000)
+    ap.add_argument("--quick", action="store_true", help="config 2 + feasibility only (profiling runs)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -65,17 +74,20 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
+    def max_over_ranks(x):
+        if dist is None:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
     for _ in range(args.warmup):
         plan.run(read=False)
     barrier()
     t0 = time.perf_counter()
     runs = [plan.run(read=False)["stats"] for _ in range(args.steps)]
     barrier()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(time.perf_counter() - t0)
 
     res = plan.run(read=True)  # one more run for result sanity (not timed)
     placed = int((res["placement"] != -1).sum())
@@ -120,21 +132,110 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(alg_bytes / (k_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 6),
-            "traffic": _traffic(),
+            "traffic": _traffic("solve_kernel"),
             "algorithmic_bytes_per_launch": int(alg_bytes),
             "algorithmic_bytes_per_pod": round(alg_bytes / prob.n_pods, 1),
+            "note": "single-workgroup sequential FFD: latency-bound (dependent L2 round trips + barriers per pod)",
         },
     }
+    plan.close()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = _cpu_baseline(cat, args.cpu_sample_pods)
-    if not args.no_consolidation:
+    line["feasibility"] = _feasibility(args, cat, ctx, prob, barrier, max_over_ranks, world)
+    if not args.quick:
+        cfgs = {}
+        cfgs["config1"] = _solve_leg("config1", synth.config1(cat, n_pods=1000, seed=1), ctx, barrier,
+                                     max_over_ranks, world, args.steps, 1,
+                                     None if (rank or world > 1 or args.no_cpu_baseline) else ("1", 1000))
+        cfgs["config3"] = _solve_leg("config3", synth.config3(cat, n_pods=args.c3_pods), ctx, barrier,
+                                     max_over_ranks, world, 2, 1,
+                                     None if (rank or world > 1 or args.no_cpu_baseline) else ("3", 3000))
+        cfgs["config5"] = _solve_leg("config5", synth.config5(cat, n_pods=args.c5_pods), ctx, barrier,
+                                     max_over_ranks, world, 1, 0,
+                                     None if (rank or world > 1 or args.no_cpu_baseline) else ("5", 6000))
+        line["configs"] = cfgs
+    if not args.no_consolidation and not args.quick:
         line["consolidation"] = _consolidation(args, cat, ctx, dist, rank, world, barrier)
     if rank == 0:
         print(json.dumps(line), flush=True)
-    plan.close()
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def _solve_leg(name, prob, ctx, barrier, max_over_ranks, world, steps, warmup, cpu):
+    """One more BASELINE config as a Solve leg: replicas on every rank, K timed runs on resident inputs."""
+    import kpamd
+    plan = kpamd.Scheduler(ctx, prob).prepare()
+    for _ in range(warmup):
+        plan.run(read=False)
+    barrier()
+    t0 = time.perf_counter()
+    runs = [plan.run(read=False)["stats"] for _ in range(steps)]
+    barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0)
+    res = plan.run(read=True)
+    plan.close()
+    k_ms = sum(r["solve_kernel_ms"] for r in runs) / len(runs)
+    out = {"value": round(prob.n_pods * world * steps / elapsed, 1), "unit": "pods/s", "pods": prob.n_pods,
+           "steps": steps, "ms_per_step": round(elapsed / steps * 1e3, 2), "solve_kernel_ms": round(k_ms, 2),
+           "prepare_ms": round(runs[0]["prepare_ms"], 1), "nodeclaims": len(res["nodeclaims"]),
+           "pods_on_existing": int((res["placement"] <= -2).sum()),
+           "pods_unschedulable": int((res["placement"] == -1).sum()),
+           "workload": prob.name}
+    if cpu is not None:
+        out["cpu_baseline"] = _cpu_baseline_cfg(cpu[0], cpu[1])
+    return out
+
+
+def _cpu_baseline_cfg(cfg, n):
+    """Oracle Solve, single thread, on a bounded sample of the same generator."""
+    from kpamd import catalog, synth
+    import kpamd
+    from oracle import pyoracle
+    cat = catalog.build_catalog(kpamd.load_lib())
+    prob = {"1": lambda: synth.config1(cat, n_pods=n, seed=1),
+            "3": lambda: synth.config3(cat, n_pods=n, n_deployments=max(1, n // 50), n_existing=max(1, n // 20)),
+            "5": lambda: synth.config5(cat, n_pods=n)}[cfg]()
+    t0 = time.perf_counter()
+    pyoracle.solve(prob)
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 1), "unit": "pods/s", "cores": 1, "kind": "port",
+            "sample": f"{prob.name}: same generator at {n} pods, oracle Solve single-threaded, {dt:.1f} s"}
+
+
+L2_BYTES_PER_PAIR = 208  # SURVEY §8d type row (64 B value ids + 96 B allocatable + 48 B offerings), L2/MALL-served
+ROW_BYTES = 880 + 96     # one compiled requirement row (KReqs) + its requests, read once per row
+
+
+def _feasibility(args, cat, ctx, prob, barrier, max_over_ranks, world, steps=10):
+    """pods x instance types CompatibleAvailableFilter (R:pkg/providers/instance/filter/filter.go:39-64) on the
+    device: one row per pending pod of config 2 (its NewPodRequirements + requests) against the 919-type
+    catalogue, mask + cheapest compatible available offering price per (pod, type); rows resident in HBM."""
+    import kpamd
+    catalog_h = kpamd.Catalog(ctx, cat)
+    fp = kpamd.FilterPlan(ctx, catalog_h, kpamd.pod_queries(prob), cheapest=True)
+    fp.run()
+    barrier()
+    t0 = time.perf_counter()
+    st = [fp.run() for _ in range(steps)]
+    barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0)
+    fp.close()
+    catalog_h.close()
+    k_ms = sum(x["device_ms"] for x in st) / steps
+    rows, T = prob.n_pods, len(cat)
+    pairs = rows * T
+    # compulsory HBM bytes: every row read once, every output written once (the 0.2 MB catalogue is resident)
+    alg = rows * (ROW_BYTES + 8 * T + 8 * ((T + 63) // 64))
+    ach = alg / (k_ms / 1e3) / 1e9
+    return {"metric": "pod x instance-type feasibility pairs/s", "value": round(pairs * world * steps / elapsed, 1),
+            "unit": "pairs/s", "rows": rows, "instance_types": T, "kernel_ms": round(k_ms, 4),
+            "roofline": {"bound": "hbm", "kernel": "feasibility_kernel", "achieved": round(ach, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                         "traffic": _traffic("feasibility_kernel"), "algorithmic_bytes_per_launch": alg,
+                         "bytes_per_row": ROW_BYTES + 8 * T + 8 * ((T + 63) // 64),
+                         "l2_effective_GBs": round(pairs * L2_BYTES_PER_PAIR / (k_ms / 1e3) / 1e9, 1)}}
 
 
 CHUNK = 1 << 18  # subsets per kp_cluster_simulate call
@@ -239,12 +340,12 @@ def _cpu_baseline_sims(cl, cands, n):
                       f"single-threaded, {dt:.1f} s"}
 
 
-def _traffic():
-    """HBM bytes per solve_kernel launch from the committed rocprofv3 --pmc pass (profiles/), if any."""
-    p = os.path.join(REPO, "profiles", "traffic_solve_kernel.json")
+def _traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc passes (profiles/traffic.json), if any."""
+    p = os.path.join(REPO, "profiles", "traffic.json")
     if os.path.exists(p):
         try:
-            return json.load(open(p)).get("hbm_bytes_per_launch")
+            return json.load(open(p)).get(kernel, {}).get("hbm_bytes_per_launch")
         except Exception:
             return None
     return None

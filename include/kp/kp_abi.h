@@ -389,6 +389,14 @@ int32_t kp_filter_compatible_available(kp_ctx* ctx, const kp_catalog* cat, const
                                        uint32_t n_queries, uint64_t* out_mask, double* out_cheapest,
                                        kp_solve_stats* stats);
 
+/* Same split into prepare (compile + upload the rows, resident) and run (one launch; copy-out only into
+ * non-NULL buffers) so many runs — or a benchmark — reuse resident inputs. */
+typedef struct kp_filter_plan kp_filter_plan;
+int32_t kp_filter_prepare(kp_ctx* ctx, const kp_catalog* cat, const kp_feasibility_query* queries, uint32_t n_queries,
+                          int32_t with_cheapest, kp_filter_plan** out);
+int32_t kp_filter_run(kp_filter_plan* plan, uint64_t* out_mask, double* out_cheapest, kp_solve_stats* stats);
+void kp_filter_plan_destroy(kp_filter_plan* plan);
+
 /* ---- Solve -------------------------------------------------------------------------------- */
 /* kp_solve = kp_solve_prepare + kp_solve_run + kp_solve_plan_destroy. prepare compiles the batch (string
  * dictionaries -> bitsets, catalogue SoA, NodeClaimTemplates, pod queue order) and uploads it; run

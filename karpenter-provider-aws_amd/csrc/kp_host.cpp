@@ -2082,13 +2082,30 @@ int32_t kp_result_stats(const kp_solve_result* r, kp_solve_stats* out) {
 void kp_result_destroy(kp_solve_result* r) { delete r; }
 
 // CompatibleAvailableFilter batched on the GPU.
-int32_t kp_filter_compatible_available(kp_ctx* ctx, const kp_catalog* cat, const kp_feasibility_query* queries,
-                                       uint32_t n_queries, uint64_t* out_mask, double* out_cheapest,
-                                       kp_solve_stats* stats) {
+}  // extern "C"
+
+struct kp_filter_plan {
+  kp_ctx* ctx = nullptr;
+  DevBuf buf;
+  FeasArgs fa;
+  uint32_t n_queries = 0;
+  int T = 0;
+  size_t tiles = 0, o_mask = 0, o_ch = 0;
+  bool cheapest = false;
+  double prepare_ms = 0;
+};
+
+extern "C" {
+
+// Compile the query rows against the catalogue dictionary and upload rows + catalogue SoA (resident).
+int32_t kp_filter_prepare(kp_ctx* ctx, const kp_catalog* cat, const kp_feasibility_query* queries, uint32_t n_queries,
+                          int32_t with_cheapest, kp_filter_plan** out) {
   auto t0 = std::chrono::steady_clock::now();
-  if (!ctx || !cat || (!queries && n_queries) || !out_mask) return fail(KP_E_INVAL, "null argument");
+  if (!ctx || !cat || (!queries && n_queries) || !out) return fail(KP_E_INVAL, "null argument");
   std::lock_guard<std::mutex> lock(ctx->mu);
   HIPCHK(hipSetDevice(ctx->device));
+  auto plan = std::make_unique<kp_filter_plan>();
+  plan->ctx = ctx;
   Compiled cp;
   DictBuilder db;
   vector<RawReqs> qs(n_queries);
@@ -2152,15 +2169,15 @@ int32_t kp_filter_compatible_available(kp_ctx* ctx, const kp_catalog* cat, const
   const size_t o_qr = blob.put(qrq);
   const size_t host_bytes = blob.host.size();
   const size_t tiles = (size_t)(T + 63) / 64;
-  const size_t o_mask = blob.reserve(sizeof(uint64_t) * std::max<size_t>(1, n_queries * tiles));
-  const size_t o_ch = out_cheapest ? blob.reserve(sizeof(double) * std::max<size_t>(1, (size_t)n_queries * T)) : 0;
-  DevBuf buf;
-  HIPCHK(hipMalloc(&buf.p, blob.host.size()));
-  uint8_t* base = (uint8_t*)buf.p;
+  plan->o_mask = blob.reserve(sizeof(uint64_t) * std::max<size_t>(1, n_queries * tiles));
+  plan->o_ch = with_cheapest ? blob.reserve(sizeof(double) * std::max<size_t>(1, (size_t)n_queries * T)) : 0;
+  HIPCHK(hipMalloc(&plan->buf.p, blob.host.size()));
+  uint8_t* base = (uint8_t*)plan->buf.p;
   vector<DevCatalog> dc = DevCats(base, cp, coffs);
   memcpy(blob.host.data() + o_cats, dc.data(), sizeof(DevCatalog));
   HIPCHK(hipMemcpyAsync(base, blob.host.data(), host_bytes, hipMemcpyHostToDevice, ctx->stream));
-  FeasArgs fa;
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  FeasArgs& fa = plan->fa;
   fa.dict = (const DevDict*)(base + o_dict);
   fa.cat = (const DevCatalog*)(base + o_cats);
   fa.vint = (const int64_t*)(base + o_vint);
@@ -2170,26 +2187,63 @@ int32_t kp_filter_compatible_available(kp_ctx* ctx, const kp_catalog* cat, const
   fa.pad_ = 0;
   fa.q_reqs = base + o_q;
   fa.q_requests = (const int64_t*)(base + o_qr);
-  fa.out_mask = (uint64_t*)(base + o_mask);
-  fa.out_cheapest = out_cheapest ? (double*)(base + o_ch) : nullptr;
+  fa.out_mask = (uint64_t*)(base + plan->o_mask);
+  fa.out_cheapest = with_cheapest ? (double*)(base + plan->o_ch) : nullptr;
+  plan->n_queries = n_queries;
+  plan->T = T;
+  plan->tiles = tiles;
+  plan->cheapest = with_cheapest != 0;
+  plan->prepare_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  *out = plan.release();
+  return KP_OK;
+}
+
+// One launch over the resident rows. Results are copied out only into the non-NULL buffers.
+int32_t kp_filter_run(kp_filter_plan* plan, uint64_t* out_mask, double* out_cheapest, kp_solve_stats* stats) {
+  auto t0 = std::chrono::steady_clock::now();
+  if (!plan) return fail(KP_E_INVAL, "null argument");
+  if (out_cheapest && !plan->cheapest) return fail(KP_E_INVAL, "plan was prepared without cheapest prices");
+  kp_ctx* ctx = plan->ctx;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device));
+  uint8_t* base = (uint8_t*)plan->buf.p;
+  const uint32_t n = plan->n_queries;
   HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
-  if (n_queries) HIPCHK(launch_feasibility(fa, ctx->stream));
+  if (n) HIPCHK(launch_feasibility(plan->fa, ctx->stream));
   HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));
-  if (n_queries) {
-    HIPCHK(hipMemcpyAsync(out_mask, base + o_mask, sizeof(uint64_t) * n_queries * tiles, hipMemcpyDeviceToHost, ctx->stream));
-    if (out_cheapest)
-      HIPCHK(hipMemcpyAsync(out_cheapest, base + o_ch, sizeof(double) * (size_t)n_queries * T, hipMemcpyDeviceToHost, ctx->stream));
-  }
+  if (n && out_mask)
+    HIPCHK(hipMemcpyAsync(out_mask, base + plan->o_mask, sizeof(uint64_t) * n * plan->tiles, hipMemcpyDeviceToHost, ctx->stream));
+  if (n && out_cheapest)
+    HIPCHK(hipMemcpyAsync(out_cheapest, base + plan->o_ch, sizeof(double) * (size_t)n * plan->T, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
   float ms = 0;
   HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
   if (stats) {
     memset(stats, 0, sizeof *stats);
     stats->device_ms = ms;
-    stats->attempts = (uint64_t)n_queries * T;
+    stats->attempts = (uint64_t)n * plan->T;  // (row, type) pairs evaluated
+    stats->prepare_ms = plan->prepare_ms;
     stats->host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   }
   return KP_OK;
+}
+
+void kp_filter_plan_destroy(kp_filter_plan* p) {
+  if (!p) return;
+  (void)hipSetDevice(p->ctx->device);
+  delete p;
+}
+
+int32_t kp_filter_compatible_available(kp_ctx* ctx, const kp_catalog* cat, const kp_feasibility_query* queries,
+                                       uint32_t n_queries, uint64_t* out_mask, double* out_cheapest,
+                                       kp_solve_stats* stats) {
+  if (!out_mask) return fail(KP_E_INVAL, "null argument");
+  kp_filter_plan* plan = nullptr;
+  int32_t rc = kp_filter_prepare(ctx, cat, queries, n_queries, out_cheapest != nullptr, &plan);
+  if (rc) return rc;
+  rc = kp_filter_run(plan, out_mask, out_cheapest, stats);
+  kp_filter_plan_destroy(plan);
+  return rc;
 }
 
 // ---- consolidation: cluster snapshot + batched simulations -----------------------------------------

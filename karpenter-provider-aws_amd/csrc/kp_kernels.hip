@@ -1330,6 +1330,9 @@ __global__ __launch_bounds__(FIN_THREADS) void finalize_kernel(FinalizeArgs a) {
 // feasibility_kernel: CompatibleAvailableFilter, (query, 64-type tile) per wave, lane = type.
 // ------------------------------------------------------------------------------------------------
 #define FEAS_WAVES 4
+// One wave per query row: the row's requirement set is decoded once (allowed value words, negative-operator
+// keys, compatible offering classes) and then streamed against every 64-type tile of the catalogue; lane =
+// instance type, __ballot -> mask word, per-lane min over classes -> cheapest price (64 coalesced doubles).
 __global__ __launch_bounds__(FEAS_WAVES * 64) void feasibility_kernel(FeasArgs a) {
   __shared__ DevDict D;
   __shared__ uint64_t s_allowed[FEAS_WAVES][KP_MAX_WORDS];
@@ -1338,10 +1341,7 @@ __global__ __launch_bounds__(FEAS_WAVES * 64) void feasibility_kernel(FeasArgs a
   const int wave = threadIdx.x >> 6, lane = LANE;
   const DevCatalog& Cg = *a.cat;
   const int tiles = (D.T + 63) >> 6;
-  const long total = (long)a.n_queries * tiles;
-  // items are query-major so consecutive waves share a query row (L1/L2 reuse) and stream type tiles
-  for (long item = (long)blockIdx.x * FEAS_WAVES + wave; item < total; item += (long)gridDim.x * FEAS_WAVES) {
-    const int q = (int)(item / tiles), tile = (int)(item % tiles);
+  for (long q = (long)blockIdx.x * FEAS_WAVES + wave; q < a.n_queries; q += (long)gridDim.x * FEAS_WAVES) {
     const KReqs* Q = reinterpret_cast<const KReqs*>(a.q_reqs + (size_t)q * sizeof(KReqs));
     const uint64_t v = lane < D.W ? Q->vals[lane] : 0;
     ReqView rv;
@@ -1359,41 +1359,48 @@ __global__ __launch_bounds__(FEAS_WAVES * 64) void feasibility_kernel(FeasArgs a
     const uint64_t allowed = allowed_word(D, rv, v, a.vint);
     const uint64_t cls = allowed_classes(D, Cg, rv, allowed, negQ);
     s_allowed[wave][lane] = allowed;
+    const int64_t rq_lane = lane < KP_NRES ? a.q_requests[(size_t)q * KP_NRES + lane] : 0;
+    uint32_t rmask = (uint32_t)__ballot(rq_lane > 0);
     wave_sync();
-    const int t = tile * 64 + lane;
-    bool keep = t < D.T;
-    double cheapest = __builtin_huge_val();
-    if (keep) {
-      // Compatible(q, type, WK) part (a): non-well-known type keys q does not define
-      if (a.mode_compatible && (Cg.custom_nonneg[t] & ~rv.present)) keep = false;
-      // Intersects over the shared keys
-      uint64_t keys = rv.present & D.catalog_keys;
-      while (keep && keys) {
-        const int k = __builtin_ctzll(keys);
-        keys &= keys - 1;
-        const uint16_t code = Cg.code[(size_t)k * D.T + t];
-        if (code == 0xFFFF) continue;                   // type lacks the key
-        if (code == 0xFFFE) keep = (negQ >> k) & 1;     // type DoesNotExist: only NotIn/DNE intersect
-        else if (code == 0xFFFD) keep = (s_allowed[wave][D.wofs[k]] & Cg.multi[(size_t)k * D.T + t]) != 0;
-        else keep = (s_allowed[wave][code >> 6] >> (code & 63)) & 1;
+    const uint64_t keys0 = rv.present & D.catalog_keys;
+    for (int tile = 0; tile < tiles; tile++) {
+      const int t = tile * 64 + lane;
+      bool keep = t < D.T;
+      double cheapest = __builtin_huge_val();
+      if (keep) {
+        // Compatible(q, type, WK) part (a): non-well-known type keys q does not define
+        if (a.mode_compatible && (Cg.custom_nonneg[t] & ~rv.present)) keep = false;
+        // Intersects over the shared keys
+        uint64_t keys = keys0;
+        while (keep && keys) {
+          const int k = __builtin_ctzll(keys);
+          keys &= keys - 1;
+          const uint16_t code = Cg.code[(size_t)k * D.T + t];
+          if (code == 0xFFFF) continue;                   // type lacks the key
+          if (code == 0xFFFE) keep = (negQ >> k) & 1;     // type DoesNotExist: only NotIn/DNE intersect
+          else if (code == 0xFFFD) keep = (s_allowed[wave][D.wofs[k]] & Cg.multi[(size_t)k * D.T + t]) != 0;
+          else keep = (s_allowed[wave][code >> 6] >> (code & 63)) & 1;
+        }
+        if (keep && !((Cg.nonneg[t >> 6] >> (t & 63)) & 1)) keep = false;  // Fits: negative totals never fit
+        uint32_t rm = rmask;
+        while (keep && rm) {
+          const int r = __builtin_ctz(rm);
+          rm &= rm - 1;
+          if (lane_bcast_i64(rq_lane, r) > Cg.alloc[(size_t)r * D.T + t]) keep = false;
+        }
+        uint64_t m = cls;
+        while (m) {
+          const int c = __builtin_ctzll(m);
+          m &= m - 1;
+          const double p = Cg.price[(size_t)t * D.C + c];
+          cheapest = p < cheapest ? p : cheapest;
+        }
+        if (!(cheapest < __builtin_huge_val())) keep = false;
       }
-      if (keep && !((Cg.nonneg[t >> 6] >> (t & 63)) & 1)) keep = false;  // Fits: negative totals never fit
-      for (int r = 0; r < KP_NRES && keep; r++) {
-        const int64_t qv = a.q_requests[(size_t)q * KP_NRES + r];
-        if (qv > 0 && qv > Cg.alloc[(size_t)r * D.T + t]) keep = false;
-      }
-      uint64_t m = cls;
-      while (m) {
-        const int c = __builtin_ctzll(m);
-        m &= m - 1;
-        const double p = Cg.price[(size_t)t * D.C + c];
-        cheapest = p < cheapest ? p : cheapest;
-      }
-      if (!(cheapest < __builtin_huge_val())) keep = false;
+      const uint64_t bal = __ballot(keep);
+      if (lane == 0) a.out_mask[(size_t)q * tiles + tile] = bal;
+      if (a.out_cheapest && t < D.T) a.out_cheapest[(size_t)q * D.T + t] = cheapest;
     }
-    const uint64_t bal = __ballot(keep);
-    if (lane == 0) a.out_mask[(size_t)q * tiles + tile] = bal;
-    if (a.out_cheapest && t < D.T) a.out_cheapest[(size_t)q * D.T + t] = cheapest;
     wave_sync();
   }
 }
@@ -1415,10 +1422,8 @@ hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 hipError_t launch_feasibility(const FeasArgs& a, hipStream_t s) {
-  const long tiles = (a.T + 63) / 64;
-  const long items = (long)a.n_queries * tiles;
-  long blocks = (items + FEAS_WAVES - 1) / FEAS_WAVES;
-  if (blocks > 16384) blocks = 16384;
+  long blocks = ((long)a.n_queries + FEAS_WAVES - 1) / FEAS_WAVES;
+  if (blocks > 65536) blocks = 65536;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(feasibility_kernel, dim3((unsigned)blocks), dim3(FEAS_WAVES * 64), 0, s, a);
   return hipGetLastError();

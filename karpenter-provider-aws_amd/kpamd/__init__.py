@@ -47,6 +47,10 @@ def load_lib(path=LIB_PATH):
                                                  P(abi.ResourceList), P(abi.ResourceList)]),
         "kp_filter_compatible_available": (C.c_int32, [C.c_void_p, C.c_void_p, P(abi.FeasibilityQuery), C.c_uint32,
                                                        P(C.c_uint64), P(C.c_double), P(abi.SolveStats)]),
+        "kp_filter_prepare": (C.c_int32, [C.c_void_p, C.c_void_p, P(abi.FeasibilityQuery), C.c_uint32, C.c_int32,
+                                          P(C.c_void_p)]),
+        "kp_filter_run": (C.c_int32, [C.c_void_p, P(C.c_uint64), P(C.c_double), P(abi.SolveStats)]),
+        "kp_filter_plan_destroy": (None, [C.c_void_p]),
         "kp_solve": (C.c_int32, [C.c_void_p, P(abi.SolveIn), P(C.c_void_p)]),
         "kp_solve_validate": (C.c_int32, [P(abi.SolveIn)]),
         "kp_solve_prepare": (C.c_int32, [C.c_void_p, P(abi.SolveIn), P(C.c_void_p)]),
@@ -250,6 +254,62 @@ def compatible_available_filter(ctx, catalog, queries):
                                                    cheapest.ctypes.data_as(C.POINTER(C.c_double)), C.byref(st)))
     bits = np.unpackbits(mask[:len(queries) * tiles].view(np.uint8), bitorder="little").reshape(len(queries), tiles * 64)
     return bits[:, :T].astype(bool), cheapest[:len(queries) * T].reshape(len(queries), T), st
+
+
+class FilterPlan:
+    """kp_filter_prepare / kp_filter_run: CompatibleAvailableFilter rows resident on the device."""
+
+    def __init__(self, ctx, catalog, queries, cheapest=True):
+        self.ctx = ctx
+        self.T = len(catalog.instance_types)
+        self.n = len(queries)
+        arena = Arena()
+        qs = arena.arr(abi.FeasibilityQuery, [abi.FeasibilityQuery(arena.requirements(r), arena.resources(q))
+                                              for r, q in queries])
+        h = C.c_void_p()
+        _check(ctx.lib, ctx.lib.kp_filter_prepare(ctx.h, catalog.h, qs, len(queries), 1 if cheapest else 0,
+                                                  C.byref(h)))
+        self.h = h
+
+    def run(self, read=False):
+        """One launch; read=True copies (kept bool[Q,T], cheapest f64[Q,T]) back, else results stay resident."""
+        st = abi.SolveStats()
+        lib = self.ctx.lib
+        if not read:
+            _check(lib, lib.kp_filter_run(self.h, None, None, C.byref(st)))
+            return stats_dict(st)
+        tiles = (self.T + 63) // 64
+        mask = np.zeros(max(1, self.n * tiles), dtype=np.uint64)
+        cheapest = np.zeros(max(1, self.n * self.T), dtype=np.float64)
+        _check(lib, lib.kp_filter_run(self.h, mask.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                      cheapest.ctypes.data_as(C.POINTER(C.c_double)), C.byref(st)))
+        bits = np.unpackbits(mask[:self.n * tiles].view(np.uint8), bitorder="little").reshape(self.n, tiles * 64)
+        return bits[:, :self.T].astype(bool), cheapest[:self.n * self.T].reshape(self.n, self.T), stats_dict(st)
+
+    def close(self):
+        if self.h:
+            self.ctx.lib.kp_filter_plan_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def pod_queries(problem):
+    """One CompatibleAvailableFilter row per pod: NewPodRequirements (nodeSelector + heaviest preferred term +
+    first required term) and the pod's requests."""
+    rows = []
+    for sh in problem.shapes:
+        reqs = [(k, "In", [v]) for k, v in sh.node_selector.items()]
+        if sh.preferred_terms:
+            reqs += list(max(sh.preferred_terms, key=lambda t: t[0])[1])
+        if sh.required_terms:
+            reqs += list(sh.required_terms[0])
+        rows.append((reqs, sh.requests))
+    return [rows[int(s)] for s in problem.pod_shape]
 
 
 def sim_dict(r):

@@ -119,3 +119,25 @@ def test_config5_many_pools(ctx, catalog):
     from kpamd import synth
     got, want = run_both(ctx, synth.config5(catalog, n_pods=6000, seed=5))
     check_same(got, want)
+
+
+def test_filter_plan_pod_rows(ctx, catalog):
+    """kp_filter_prepare/run over per-pod rows (the bench's feasibility leg) == the oracle, row by row."""
+    import kpamd
+    from kpamd import synth
+    from oracle import pyoracle
+    prob = synth.config2(catalog, n_pods=300, seed=9)
+    queries = kpamd.pod_queries(prob)
+    cat = kpamd.Catalog(ctx, catalog)
+    fp = kpamd.FilterPlan(ctx, cat, queries, cheapest=True)
+    kept, cheapest, st = fp.run(read=True)
+    fp.close()
+    assert st["attempts"] == len(queries) * len(catalog)
+    seen = {}
+    for qi, (reqs, rq) in enumerate(queries):
+        key = int(prob.pod_shape[qi])
+        if key not in seen:
+            seen[key] = pyoracle.compatible_available_filter(catalog, reqs, rq)
+        want_k, want_c = seen[key]
+        assert (kept[qi] == want_k).all(), f"row {qi}"
+        np.testing.assert_array_equal(cheapest[qi][want_k], want_c[want_k])
