@@ -304,6 +304,8 @@ typedef struct kp_solve_stats {
   uint64_t phase_cycles[8]; /* diagnostic (KP_TIMING=1): per-phase shader cycles of the solve loop */
   uint64_t scanned;         /* diagnostic: in-flight NodeClaim positions the candidate pre-pass visited */
   uint64_t cursor_starts;   /* diagnostic: sum of first-fit cursor start positions (positions skipped) */
+  uint64_t attempt_cycles[8]; /* diagnostic (KP_TIMING=1): wave 0's in-flight attempt split (merge, pod keys,
+                                 Fits, offerings, minValues; [5] = attempts timed) */
 } kp_solve_stats;
 
 /* ---- context ---------------------------------------------------------------------------- */

@@ -27,6 +27,7 @@ struct SolveArgs {
   const uint64_t* shape_pvp;         // rows of TW words
   const int32_t* pvp_base;           // [SL][n_catalogs] first row
   const int32_t* pvp_slot;           // [SL][64] row offset of key k (relative to base)
+  const int32_t* sl_pvp_n;           // [SL] PVP rows of catalogue 0
   // templates
   int32_t n_tmpl;
   const uint8_t* tmpl_reqs;          // [NT] KReqs

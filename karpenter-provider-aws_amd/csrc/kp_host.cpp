@@ -893,7 +893,7 @@ struct Compiled {
   vector<uint64_t> shape_negop, shape_tolerates;
   vector<int64_t> shape_requests;
   vector<uint64_t> pvp;
-  vector<int32_t> pvp_base, pvp_slot;
+  vector<int32_t> pvp_base, pvp_slot, pvp_n;  // pvp_n: rows of catalogue 0 per shape-level
   // existing (sorted)
   vector<int> ex_input;
   vector<KReqs> ex_reqs;
@@ -1538,6 +1538,7 @@ int32_t CompileSolve(const kp_solve_in* in, Compiled& cp) {
         const HostCat& hc = cp.cats[ci];
         cp.pvp_base.push_back((int32_t)(cp.pvp.size() / TW));
         int row = 0;
+        if (ci == 0) cp.pvp_n.push_back(0);
         for (int k = 0; k < d.dd.K; k++) {
           if (!((q.present >> k) & 1) || !((cp.d.dd.single_valued >> k) & 1)) continue;
           vector<uint64_t> acc(hc.NOKEY.begin() + (size_t)k * TW, hc.NOKEY.begin() + (size_t)(k + 1) * TW);
@@ -1552,6 +1553,7 @@ int32_t CompileSolve(const kp_solve_in* in, Compiled& cp) {
           }
           cp.pvp.insert(cp.pvp.end(), acc.begin(), acc.end());
           slots[k] = row++;  // same key order for every catalogue -> same relative slot
+          if (ci == 0) cp.pvp_n.back() = row;
         }
       }
       cp.pvp_slot.insert(cp.pvp_slot.end(), slots.begin(), slots.end());
@@ -1695,6 +1697,7 @@ int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out
   const size_t o_pvp = blob.put(C.pvp);
   const size_t o_pvpb = blob.put(C.pvp_base);
   const size_t o_pvps = blob.put(C.pvp_slot);
+  const size_t o_pvpn = blob.put(C.pvp_n);
   const size_t o_treqs = blob.put(C.tmpl_reqs);
   const size_t o_tts = blob.put(C.tmpl_taintset);
   const size_t o_tcat = blob.put(C.tmpl_catalog);
@@ -1754,7 +1757,7 @@ int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out
   const size_t o_ncts = blob.reserve(sizeof(int32_t) * (size_t)Pc);
   const size_t o_place = blob.reserve(sizeof(int32_t) * Pc);
   const size_t o_events = blob.reserve(sizeof(int32_t) * Pc);
-  const size_t o_stats = blob.reserve(sizeof(uint64_t) * 16);
+  const size_t o_stats = blob.reserve(sizeof(uint64_t) * 24);
   // failure memo (see SolveArgs): versions start at 0, memo entries at -1
   const size_t SLn = std::max<size_t>(1, C.shape_reqs.size());
   const int ncc = (int)std::min<size_t>((size_t)Pc, std::max<size_t>(1, ((size_t)256 << 20) / (4 * SLn)));
@@ -1810,6 +1813,7 @@ int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out
   a.shape_pvp = (const uint64_t*)(base + o_pvp);
   a.pvp_base = (const int32_t*)(base + o_pvpb);
   a.pvp_slot = (const int32_t*)(base + o_pvps);
+  a.sl_pvp_n = (const int32_t*)(base + o_pvpn);
   a.n_tmpl = NT;
   a.tmpl_reqs = base + o_treqs;
   a.tmpl_taintset = (const int32_t*)(base + o_tts);
@@ -1929,7 +1933,7 @@ int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out) {
   const int P = plan->P, Pc = plan->Pc, opt_stride = plan->opt_stride;
   hipStream_t st = ctx->stream;
   HIPCHK(hipMemcpyAsync(base + plan->o_mut, base + plan->o_pristine, plan->n_mut, hipMemcpyDeviceToDevice, st));
-  HIPCHK(hipMemsetAsync(base + plan->o_stats, 0, sizeof(uint64_t) * 16, st));
+  HIPCHK(hipMemsetAsync(base + plan->o_stats, 0, sizeof(uint64_t) * 24, st));
   HIPCHK(hipMemsetAsync(base + plan->o_npods, 0, sizeof(int32_t) * Pc, st));
   HIPCHK(hipMemsetAsync(base + plan->o_place, 0xFF, sizeof(int32_t) * Pc, st));
   HIPCHK(hipMemsetAsync(base + plan->o_ver, 0, plan->n_ver, st));
@@ -1940,7 +1944,7 @@ int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out) {
   HIPCHK(hipEventRecord(ctx->ev0, st));
   HIPCHK(launch_solve(a, 8, dyn, st));
   HIPCHK(hipEventRecord(ctx->ev1, st));
-  uint64_t stats[16];
+  uint64_t stats[24];
   HIPCHK(hipMemcpyAsync(stats, base + plan->o_stats, sizeof stats, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   const int n_nc = (int)stats[3];
@@ -2032,6 +2036,7 @@ int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out) {
   for (int i = 0; i < 8; i++) res->stats.phase_cycles[i] = stats[8 + i];
   res->stats.scanned = stats[5];
   res->stats.cursor_starts = stats[6];
+  for (int i = 0; i < 8; i++) res->stats.attempt_cycles[i] = stats[16 + i];
   res->stats.host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   *out = res.release();
   return KP_OK;

@@ -56,16 +56,29 @@ __device__ __forceinline__ uint64_t lane_bcast(uint64_t v, int src) {
 __device__ __forceinline__ int64_t lane_bcast_i64(int64_t v, int src) { return (int64_t)lane_bcast((uint64_t)v, src); }
 __device__ __forceinline__ int key_word(const DevDict& D, int k, int i) { return i == 0 ? k : D.ovf[k] + i - 1; }
 
-// Requirement bounds filter (withinIntPtrs) applied to the value bits of one word.
-__device__ __forceinline__ uint64_t within_word(uint64_t v, int word, const int64_t* vint, uint64_t intok, bool hg,
-                                                int64_t gt, bool hl, int64_t lt) {
-  if (!hg && !hl) return v;
-  uint64_t out = 0, m = v & intok;
-  while (m) {
-    const int b = __builtin_ctzll(m);
-    m &= m - 1;
-    const int64_t x = vint[word * 64 + b];
-    if ((!hg || x > gt) && (!hl || x < lt)) out |= 1ull << b;
+// withinIntPtrs over every word of the keys in bk, one wave-wide pass per word: lane b tests value bit b
+// (coalesced 512 B read of the word's parsed integers) and a ballot forms the word's mask. Returns this lane's
+// word mask (all ones when the lane's key is not in bk). Replaces a per-lane serial walk over the set bits,
+// whose dependent loads made bounded-key merges the longest chain of an attempt.
+__device__ __forceinline__ uint64_t bounds_mask(const DevDict& D, uint64_t bk, uint64_t hgt, uint64_t hlt,
+                                                const int64_t* gt, const int64_t* lt, const int64_t* vint) {
+  const int lane = LANE;
+  uint64_t out = ~0ull;
+  while (bk) {
+    const int kk = __builtin_ctzll(bk);
+    bk &= bk - 1;
+    const bool hg = (hgt >> kk) & 1, hl = (hlt >> kk) & 1;
+    const int64_t g = gt[kk], l = lt[kk];
+    uint64_t wm = 1ull << kk;
+    if ((D.multiword >> kk) & 1) wm |= D.ovfmask[kk];
+    while (wm) {
+      const int w = __builtin_ctzll(wm);
+      wm &= wm - 1;
+      const int64_t x = vint[w * 64 + lane];
+      const bool ok = ((D.vint_ok[w] >> lane) & 1) && (!hg || x > g) && (!hl || x < l);
+      const uint64_t m = __ballot(ok);
+      if (lane == w) out = m;
+    }
   }
   return out;
 }
@@ -146,16 +159,13 @@ __device__ bool merge_compatible(const DevDict& D, const KReqs* A, const KReqs* 
     if ((shared >> k) & 1) {
       const bool c1 = (aC >> k) & 1, c2 = (bC >> k) & 1;
       v = (c1 && c2) ? (a_v | b_v) : c1 ? (b_v & ~a_v) : c2 ? (a_v & ~b_v) : (a_v & b_v);
-      if ((dne >> k) & 1) {
-        v = 0;  // gt >= lt: NewRequirementWithFlexibility(key, DoesNotExist, minValues)
-      } else if (k < D.KB && (((hgt_any | hlt_any) >> k) & 1)) {
-        v = within_word(v, lane, vint, D.vint_ok[lane], (hgt_any >> k) & 1, slots->gt[k], (hlt_any >> k) & 1,
-                        slots->lt[k]);
-      }
+      if ((dne >> k) & 1) v = 0;  // gt >= lt: NewRequirementWithFlexibility(key, DoesNotExist, minValues)
     } else {
       v = ((aP >> k) & 1) ? a_v : b_v;
     }
   }
+  const uint64_t bk = (hgt_any | hlt_any) & shared & ~dne;
+  if (bk) v &= bounds_mask(D, bk, hgt_any, hlt_any, slots->gt, slots->lt, vint);
   m_v = v;
   const uint64_t compl_new = ((aC & bC) | (aC & ~bP) | (bC & ~aP)) & ~dne;
   const uint64_t nz = nz_keys(D, v);
@@ -179,15 +189,12 @@ __device__ bool merge_compatible(const DevDict& D, const KReqs* A, const KReqs* 
 // Allowed-value bits (Requirement.Has) of this lane's word under requirement set rv; absent key -> all.
 __device__ __forceinline__ uint64_t allowed_word(const DevDict& D, const ReqView& rv, uint64_t v, const int64_t* vint) {
   const int lane = LANE;
+  const uint64_t bk = (rv.hgt | rv.hlt) & rv.present & rv.compl_ & ((1ull << D.KB) - 1);
+  const uint64_t bm = bk ? bounds_mask(D, bk, rv.hgt, rv.hlt, rv.gt, rv.lt, vint) : ~0ull;
   if (lane >= D.W) return 0;
   const int k = D.wkey[lane];
   if (!((rv.present >> k) & 1)) return D.validbits[lane];
-  if ((rv.compl_ >> k) & 1) {
-    uint64_t a = ~v & D.validbits[lane];
-    if (k < D.KB && (((rv.hgt | rv.hlt) >> k) & 1))
-      a = within_word(a, lane, vint, D.vint_ok[lane], (rv.hgt >> k) & 1, rv.gt[k], (rv.hlt >> k) & 1, rv.lt[k]);
-    return a;
-  }
+  if ((rv.compl_ >> k) & 1) return ~v & D.validbits[lane] & bm;
   return v;
 }
 

@@ -170,6 +170,7 @@ def read_result(lib, res, n_pods, prefix="kp_result_"):
 def stats_dict(st):
     d = {f: getattr(st, f) for f, _ in abi.SolveStats._fields_}
     d["phase_cycles"] = list(st.phase_cycles)
+    d["attempt_cycles"] = list(st.attempt_cycles)
     return d
 
 

@@ -28,4 +28,9 @@ out = {"config": cfg, "pods": n, "solve_kernel_ms": st["solve_kernel_ms"], "atte
        "phase_share": {k: round(v / tot, 4) for k, v in zip(names, st["phase_cycles"])},
        "cycles_per_pop": tot / max(1, st["pops"]), "scanned_per_pop": st["scanned"] / max(1, st["pops"]),
        "cursor_start_per_pop": st["cursor_starts"] / max(1, st["pops"])}
+ac = st["attempt_cycles"]
+if ac[5]:
+    out["attempt_cycles_per_attempt"] = {k: round(v / ac[5], 1) for k, v in
+                                         zip(["merge", "pod-keys", "fits", "offerings", "minvalues"], ac[:5])}
+    out["attempts_timed"] = ac[5]
 print(json.dumps(out))
