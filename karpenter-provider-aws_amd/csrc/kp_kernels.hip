@@ -304,9 +304,16 @@ __device__ uint64_t filter_types(const DevDict& D, const DevCatalog& Cg, const R
                                  uint64_t pod_keys, const uint64_t* pvp, const int32_t* pvp_slot, const int64_t* reqrow,
                                  const int64_t* s_preq, const int64_t* const* fitv, uint32_t rmask,
                                  const int64_t* vint, uint32_t* scratch, uint64_t* bytes, const int32_t* jstart,
-                                 int32_t* jout, uint64_t generic_keys = 0) {
+                                 int32_t* jout, uint64_t generic_keys = 0, uint64_t* tsub = nullptr) {
   const int lane = LANE;
   const int TW = D.TW;
+  uint64_t tl = tsub ? __builtin_amdgcn_s_memtime() : 0;
+#define TSUB(i)                                        \
+  if (tsub) {                                          \
+    const uint64_t tn = __builtin_amdgcn_s_memtime(); \
+    if (lane == 0) tsub[i] += tn - tl;                 \
+    tl = tn;                                           \
+  }
   const uint64_t negM = negop_mask(rv.present, rv.compl_, rv.nz);
   const uint64_t allowed = allowed_word(D, rv, m_v, vint);
   uint64_t nb = 0;
@@ -340,6 +347,7 @@ __device__ uint64_t filter_types(const DevDict& D, const DevCatalog& Cg, const R
       X &= acc;
     }
   }
+  TSUB(1);
   // 2) resources.Fits(total, allocatable): per requested resource, a threshold mask. A NodeClaim's totals
   //    only grow, so the threshold index does too: probe 64 entries past the cached index first.
   //    Lane r holds resource r's total and cached index (one load level for all resources).
@@ -367,6 +375,7 @@ __device__ uint64_t filter_types(const DevDict& D, const DevCatalog& Cg, const R
     if (lane == r) j_lane = j;
   }
   if (lane < KP_NRES) jout[lane] = j_lane;
+  TSUB(2);
   // 3) some available offering compatible with the merged requirements. X already satisfies the
   //    candidate's offering keys; only a pod that constrains one of them can change the answer.
   if (pod_keys & D.offer_keys) {
@@ -381,8 +390,11 @@ __device__ uint64_t filter_types(const DevDict& D, const DevCatalog& Cg, const R
     nb += (uint64_t)__builtin_popcountll(cls) * TW * 8;
     X &= offer;
   }
+  TSUB(3);
   // 4) minValues (relaxMinValues = false): distinct values of each minValues key over remaining types
   if (!minvalues_ok(D, Cg, rv.hmin & rv.present, rv.minv, X, scratch)) X = 0;
+  TSUB(4);
+#undef TSUB
   *bytes += nb;
   return X;
 }
@@ -715,6 +727,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
   __shared__ TopoOwn s_town[8];                 // owned topology groups of the popped pod (staged per pod)
   __shared__ uint64_t s_tacc[8];
   __shared__ int32_t s_tcnt[8][64];
+  __shared__ uint64_t s_tsub[8];  // KP_TIMING: wave 0's attempt split (merge, pod keys, fits, offerings, minValues, n)
   extern __shared__ int32_t s_dyn[];  // ord[a.sort_cap], npods[a.sort_cap] while n_nc <= a.sort_cap
 
   const int tid = threadIdx.x;
@@ -743,6 +756,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
   uint64_t bytes = 0, attempts = 0, pops = 0, scanned = 0, starts = 0;
   uint64_t tph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tlast = 0;
   const bool timing = a.timing && tid == 0;
+  if (tid < 8) s_tsub[tid] = 0;
 #define TS(ph)                                          \
   if (timing) {                                         \
     const uint64_t tnow = __builtin_amdgcn_s_memtime(); \
@@ -987,7 +1001,10 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
             const int tm = a.nc_tmpl[nc];
             const int cat = a.tmpl_catalog[tm];
             attempts++;
+            uint64_t* tsub = (a.timing && wave == 0) ? s_tsub : nullptr;
+            const uint64_t tm0 = tsub ? __builtin_amdgcn_s_memtime() : 0;
             ok = merge_compatible(D, kreq_at(a.nc_reqs, nc), B, b_negop, true, m_v, rv, &slots[wave], a.vint);
+            if (tsub && lane == 0) tsub[0] += __builtin_amdgcn_s_memtime() - tm0;
             bytes += sizeof(KReqs);
             bool memo = !ok || !own_n;  // failures after the topology step depend on the counts
             if (ok && own_n) ok = topo_narrow(D, own_n, s_town, s_tacc, s_tcnt, true, m_v, rv, a.vint);
@@ -996,8 +1013,9 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
               const uint64_t* pvp = a.shape_pvp + (size_t)a.pvp_base[sl * a.n_catalogs + cat] * D.TW;
               X = filter_types(D, a.cats[cat], rv, m_v, X, b_keys, pvp, s_pslot, a.nc_requests + (size_t)nc * KP_NRES,
                                s_preq, s_fitp, a.req_res_mask, a.vint, s_scratch[wave], &bytes,
-                               a.nc_fitj + (size_t)nc * KP_NRES, s_fitj[wave], topo_keys);
+                               a.nc_fitj + (size_t)nc * KP_NRES, s_fitj[wave], topo_keys, tsub);
               ok = __ballot(X != 0) != 0;
+              if (tsub && lane == 0) tsub[5] += 1;  // attempts reaching filter_types (wave 0)
               bytes += (uint64_t)D.TW * 8 + KP_NRES * 8;
             }
             if (!ok && memo && lane == 0 && nc < a.ncc) a.nc_fail[(size_t)sl * a.ncc + nc] = a.nc_ver[nc];
@@ -1220,7 +1238,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
   }
 #undef TS
   if (timing)
-    for (int i = 0; i < 8; i++) a.stats[8 + i] = tph[i];
+    for (int i = 0; i < 8; i++) a.stats[8 + i] = tph[i], a.stats[16 + i] = s_tsub[i];
 
   if (lane == 0) {
     atomicAdd((unsigned long long*)&a.stats[0], (unsigned long long)attempts);
