@@ -64,6 +64,7 @@ struct SolveArgs {
   int64_t* nc_maxalloc;              // [P][NRES] max allocatable over the NodeClaim's types at creation
   int32_t* nc_fitj;                  // [P][NRES] threshold index of the last Fits per resource
   int32_t* nc_taintset;              // [P] taint set of the NodeClaim's template
+  int32_t* nc_cat;                   // [P] catalogue of the NodeClaim's template
   uint32_t req_res_mask;             // resources some pod shape requests (> 0)
   int32_t timing;                    // 1: thread 0 accumulates per-phase s_memtime deltas into stats[8..15]
   // topology spread (upstream Topology, TopologyTypeSpread groups). A group on a dictionary key keeps a

@@ -1755,6 +1755,7 @@ int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out
   const size_t o_maxalloc = blob.reserve(sizeof(int64_t) * (size_t)Pc * KP_NRES);
   const size_t o_fitj = blob.reserve(sizeof(int32_t) * (size_t)Pc * KP_NRES);
   const size_t o_ncts = blob.reserve(sizeof(int32_t) * (size_t)Pc);
+  const size_t o_nccat = blob.reserve(sizeof(int32_t) * (size_t)Pc);
   const size_t o_place = blob.reserve(sizeof(int32_t) * Pc);
   const size_t o_events = blob.reserve(sizeof(int32_t) * Pc);
   const size_t o_stats = blob.reserve(sizeof(uint64_t) * 24);
@@ -1848,6 +1849,7 @@ int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out
   a.nc_maxalloc = (int64_t*)(base + o_maxalloc);
   a.nc_fitj = (int32_t*)(base + o_fitj);
   a.nc_taintset = (int32_t*)(base + o_ncts);
+  a.nc_cat = (int32_t*)(base + o_nccat);
   a.req_res_mask = 0;
   for (size_t i = 0; i < C.shape_requests.size(); i++)
     if (C.shape_requests[i] > 0) a.req_res_mask |= 1u << (i % KP_NRES);

@@ -14,11 +14,16 @@
 // No MFMA: the path is bitwise/integer. Wave = 64 lanes everywhere.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "kp_device.h"
 #include "kp_model.h"
 
 #define LANE ((int)(threadIdx.x & 63))
+// Explicit address spaces: LDS data reached through a pointer would otherwise be read with FLAT loads (which wait
+// on the vector-memory counter too and take the long path); global rows get global_load.
+#define LDS __attribute__((address_space(3)))
+#define GLB __attribute__((address_space(1)))
 #define FITV_RES 4      // requested resources whose Fits thresholds are staged in LDS
 #define FITV_CAP 1024   // distinct allocatable values per staged resource
 
@@ -56,12 +61,22 @@ __device__ __forceinline__ uint64_t lane_bcast(uint64_t v, int src) {
 __device__ __forceinline__ int64_t lane_bcast_i64(int64_t v, int src) { return (int64_t)lane_bcast((uint64_t)v, src); }
 __device__ __forceinline__ int key_word(const DevDict& D, int k, int i) { return i == 0 ? k : D.ovf[k] + i - 1; }
 
+// Parsed integers of the value bits (vint[w*64 + b]): words w < nl from an LDS copy (the bounded keys' first
+// words, staged once per kernel), the rest from global memory.
+struct VInt {
+  const int64_t LDS* l;
+  const int64_t* g;
+  int nl;
+  __device__ __forceinline__ int64_t at(int w, int lane) const { return w < nl ? l[w * 64 + lane] : g[w * 64 + lane]; }
+};
+__device__ __forceinline__ VInt vint_global(const int64_t* g) { return VInt{nullptr, g, 0}; }
+
 // withinIntPtrs over every word of the keys in bk, one wave-wide pass per word: lane b tests value bit b
 // (coalesced 512 B read of the word's parsed integers) and a ballot forms the word's mask. Returns this lane's
 // word mask (all ones when the lane's key is not in bk). Replaces a per-lane serial walk over the set bits,
 // whose dependent loads made bounded-key merges the longest chain of an attempt.
 __device__ __forceinline__ uint64_t bounds_mask(const DevDict& D, uint64_t bk, uint64_t hgt, uint64_t hlt,
-                                                const int64_t* gt, const int64_t* lt, const int64_t* vint) {
+                                                const int64_t* gt, const int64_t* lt, const VInt& vint) {
   const int lane = LANE;
   uint64_t out = ~0ull;
   while (bk) {
@@ -74,7 +89,7 @@ __device__ __forceinline__ uint64_t bounds_mask(const DevDict& D, uint64_t bk, u
     while (wm) {
       const int w = __builtin_ctzll(wm);
       wm &= wm - 1;
-      const int64_t x = vint[w * 64 + lane];
+      const int64_t x = vint.at(w, lane);
       const bool ok = ((D.vint_ok[w] >> lane) & 1) && (!hg || x > g) && (!hl || x < l);
       const uint64_t m = __ballot(ok);
       if (lane == w) out = m;
@@ -90,6 +105,30 @@ struct ReqView {
   const int64_t* lt;
   const int32_t* minv;
 };
+
+// A catalogue descriptor staged in LDS with its small tables (offering classes, Fits threshold counts), so that a
+// filter step reads them with ds_read instead of a global round trip per field.
+#define HDR_CLS 16
+struct CatHdr {
+  DevCatalog d;
+  OfferClass cls[HDR_CLS];     // valid when D.C <= HDR_CLS
+  int32_t fit_n[KP_NRES];
+  int32_t fit_slot[KP_NRES];   // row of the kernel's LDS fit-value table holding fit_vals[r], -1: global
+};
+// one wave fills h from the global descriptor g (lanes copy words in parallel)
+__device__ __forceinline__ void hdr_fill_wave(CatHdr LDS* h, const DevCatalog* g, int C) {
+  const int lane = LANE;
+  constexpr int NWD = sizeof(DevCatalog) / 8;
+  if (lane < NWD) reinterpret_cast<uint64_t LDS*>(&h->d)[lane] = reinterpret_cast<const uint64_t*>(g)[lane];
+  const OfferClass* gc = g->cls;
+  const int32_t* gn = g->fit_n;
+  if (lane < 2 * HDR_CLS && lane < 2 * C)
+    reinterpret_cast<uint64_t LDS*>(h->cls)[lane] = reinterpret_cast<const uint64_t*>(gc)[lane];
+  if (lane < KP_NRES) {
+    h->fit_n[lane] = gn[lane];
+    h->fit_slot[lane] = -1;
+  }
+}
 
 // operator in {NotIn, DoesNotExist}: complement with values, or no complement and no values.
 __device__ __forceinline__ uint64_t negop_mask(uint64_t present, uint64_t compl_, uint64_t nz) {
@@ -119,34 +158,56 @@ struct WaveSlots {
   int32_t minv[KP_MAX_BOUND_KEYS];
 };
 
+// A candidate's requirement set as registers: key masks (wave-uniform) + this lane's value word and bound slot.
+// Loading it is one batch of independent loads, issued before anything that depends on it.
+struct CandReq {
+  uint64_t P, C, hgt, hlt, hmin, v;
+  int64_t gt, lt;
+  int32_t minv;
+};
+__device__ __forceinline__ CandReq load_cand(const DevDict& D, const KReqs* A) {
+  const int lane = LANE;
+  CandReq c;
+  c.P = A->present;
+  c.C = A->compl_;
+  c.hgt = A->hgt;
+  c.hlt = A->hlt;
+  c.hmin = A->hmin;
+  c.v = lane < D.W ? A->vals[lane] : 0;
+  const bool b = lane < D.KB;
+  c.gt = b ? A->gt[lane] : 0;
+  c.lt = b ? A->lt[lane] : 0;
+  c.minv = b ? A->minv[lane] : 0;
+  return c;
+}
+
 // Requirements.Compatible(A, B, allowUndefined) followed by A.Add(B) (= per key Requirement.Intersection).
 // On success: m_v = merged value word of this lane, rv = merged key masks, slots = merged bounds.
-__device__ bool merge_compatible(const DevDict& D, const KReqs* A, const KReqs* B, uint64_t b_negop, bool allow_wk,
-                                 uint64_t& m_v, ReqView& rv, WaveSlots* slots, const int64_t* vint) {
+__device__ __forceinline__ bool merge_compatible(const DevDict& D, const CandReq& A, const KReqs* B, uint64_t b_negop, bool allow_wk,
+                                 uint64_t& m_v, ReqView& rv, WaveSlots* slots, const VInt& vint) {
   const int lane = LANE;
   const int k = lane < D.W ? (int)D.wkey[lane] : -1;
-  const uint64_t aP = A->present, bP = B->present;
+  const uint64_t aP = A.P, bP = B->present;
   const uint64_t shared = aP & bP;
   // (a) keys the pod defines but the candidate does not: only NotIn/DoesNotExist (or well-known) pass
   uint64_t undef = bP & ~aP & ~b_negop;
   if (allow_wk) undef &= ~D.wellknown;
   if (undef) return false;
-  const uint64_t a_v = lane < D.W ? A->vals[lane] : 0;
+  const uint64_t a_v = A.v;
   const uint64_t b_v = lane < D.W ? B->vals[lane] : 0;
-  const uint64_t aC = A->compl_ & aP, bC = B->compl_ & bP;
+  const uint64_t aC = A.C & aP, bC = B->compl_ & bP;
   // bound slots: lane l < KB owns key l
   bool hg = false, hl = false, dneb = false;
   if (lane < D.KB) {
     const bool inA = (aP >> lane) & 1, inB = (bP >> lane) & 1;
-    const bool agt = inA && ((A->hgt >> lane) & 1), bgt = inB && ((B->hgt >> lane) & 1);
-    const bool alt = inA && ((A->hlt >> lane) & 1), blt = inB && ((B->hlt >> lane) & 1);
+    const bool agt = inA && ((A.hgt >> lane) & 1), bgt = inB && ((B->hgt >> lane) & 1);
+    const bool alt = inA && ((A.hlt >> lane) & 1), blt = inB && ((B->hlt >> lane) & 1);
     hg = agt || bgt;
     hl = alt || blt;
-    const int64_t g = agt && bgt ? max(A->gt[lane], B->gt[lane]) : (agt ? A->gt[lane] : (bgt ? B->gt[lane] : 0));
-    const int64_t l = alt && blt ? min(A->lt[lane], B->lt[lane]) : (alt ? A->lt[lane] : (blt ? B->lt[lane] : 0));
-    const bool amin = inA && ((A->hmin >> lane) & 1), bmin = inB && ((B->hmin >> lane) & 1);
-    const int32_t mv =
-        amin && bmin ? max(A->minv[lane], B->minv[lane]) : (amin ? A->minv[lane] : (bmin ? B->minv[lane] : 0));
+    const int64_t g = agt && bgt ? max(A.gt, B->gt[lane]) : (agt ? A.gt : (bgt ? B->gt[lane] : 0));
+    const int64_t l = alt && blt ? min(A.lt, B->lt[lane]) : (alt ? A.lt : (blt ? B->lt[lane] : 0));
+    const bool amin = inA && ((A.hmin >> lane) & 1), bmin = inB && ((B->hmin >> lane) & 1);
+    const int32_t mv = amin && bmin ? max(A.minv, B->minv[lane]) : (amin ? A.minv : (bmin ? B->minv[lane] : 0));
     dneb = inA && inB && hg && hl && g >= l;
     slots->gt[lane] = g;
     slots->lt[lane] = l;
@@ -173,7 +234,7 @@ __device__ bool merge_compatible(const DevDict& D, const KReqs* A, const KReqs* 
   rv.compl_ = compl_new;
   rv.hgt = hgt_any & compl_new;
   rv.hlt = hlt_any & compl_new;
-  rv.hmin = (A->hmin & aP) | (B->hmin & bP);
+  rv.hmin = (A.hmin & aP) | (B->hmin & bP);
   rv.nz = nz;
   rv.dne = dne;
   rv.gt = slots->gt;
@@ -185,9 +246,14 @@ __device__ bool merge_compatible(const DevDict& D, const KReqs* A, const KReqs* 
   const uint64_t negA = negop_mask(aP, aC, nzA);
   return (empty & ~(negA & b_negop)) == 0;
 }
+__device__ __forceinline__ bool merge_compatible(const DevDict& D, const KReqs* A, const KReqs* B, uint64_t b_negop,
+                                                 bool allow_wk, uint64_t& m_v, ReqView& rv, WaveSlots* slots,
+                                                 const VInt& vint) {
+  return merge_compatible(D, load_cand(D, A), B, b_negop, allow_wk, m_v, rv, slots, vint);
+}
 
 // Allowed-value bits (Requirement.Has) of this lane's word under requirement set rv; absent key -> all.
-__device__ __forceinline__ uint64_t allowed_word(const DevDict& D, const ReqView& rv, uint64_t v, const int64_t* vint) {
+__device__ __forceinline__ uint64_t allowed_word(const DevDict& D, const ReqView& rv, uint64_t v, const VInt& vint) {
   const int lane = LANE;
   const uint64_t bk = (rv.hgt | rv.hlt) & rv.present & rv.compl_ & ((1ull << D.KB) - 1);
   const uint64_t bm = bk ? bounds_mask(D, bk, rv.hgt, rv.hlt, rv.gt, rv.lt, vint) : ~0ull;
@@ -204,23 +270,30 @@ __device__ __forceinline__ bool bit_of(uint64_t allowed_lane_word, int bit) {
 }
 
 // Offering classes compatible with requirement set rv (Offerings.Compatible + reservation-key DNE test).
-__device__ uint64_t allowed_classes(const DevDict& D, const DevCatalog& Cg, const ReqView& rv, uint64_t allowed,
-                                   uint64_t negR) {
+template <class ClsP>
+__device__ uint64_t allowed_classes(const DevDict& D, ClsP cls_tab, const ReqView& rv, uint64_t allowed, uint64_t negR) {
   const bool res_ok = !(rv.present & D.resid_key_bit) || (negR & D.resid_key_bit);
   const bool rt_ok = !(rv.present & D.restype_key_bit) || (negR & D.restype_key_bit);
-  uint64_t cls = 0;
-  for (int c = 0; c < D.C; c++) {
-    const OfferClass oc = Cg.cls[c];
-    bool ok = bit_of(allowed, oc.ct_bit);
-    if (oc.zone_bit >= 0) ok = (int)ok & (int)bit_of(allowed, oc.zone_bit);
-    if (oc.zid_bit >= 0) ok = (int)ok & (int)bit_of(allowed, oc.zid_bit);
-    if (ok) cls |= 1ull << c;
+  // lane c evaluates class c: its three value bits are fetched from the owning lanes' allowed words
+  const int lane = LANE;
+  int ct_bit = 0, zone_bit = -1, zid_bit = -1;
+  if (lane < D.C) {
+    ct_bit = cls_tab[lane].ct_bit;
+    zone_bit = cls_tab[lane].zone_bit;
+    zid_bit = cls_tab[lane].zid_bit;
   }
+  const uint64_t w1 = __shfl(allowed, ct_bit >> 6, 64);
+  const uint64_t w2 = __shfl(allowed, zone_bit >= 0 ? zone_bit >> 6 : 0, 64);
+  const uint64_t w3 = __shfl(allowed, zid_bit >= 0 ? zid_bit >> 6 : 0, 64);
+  const bool ok = lane < D.C && ((w1 >> (ct_bit & 63)) & 1) && (zone_bit < 0 || ((w2 >> (zone_bit & 63)) & 1)) &&
+                  (zid_bit < 0 || ((w3 >> (zid_bit & 63)) & 1));
+  const uint64_t cls = __ballot(ok);
   return (res_ok && rt_ok) ? cls : 0;
 }
 
 // first j in [0, n) with vals[j] >= q (ascending vals), n if none; 64-ary search across the wave.
-__device__ int wave_lower_bound(const int64_t* vals, int n, int64_t q, uint64_t* bytes) {
+template <class ValP>
+__device__ int wave_lower_bound(ValP vals, int n, int64_t q, uint64_t* bytes) {
   const int lane = LANE;
   int lo = 0, hi = n;  // vals[j] < q for j < lo; answer <= hi
   while (lo < hi) {
@@ -252,7 +325,7 @@ __device__ int wave_lower_bound(const int64_t* vals, int n, int64_t q, uint64_t*
 
 // minValues over a type set (SatisfiesMinValues): for every key in `mk`, the remaining types (X: this lane's
 // word) must carry at least minv[k] distinct values of it.
-__device__ bool minvalues_ok(const DevDict& D, const DevCatalog& Cg, uint64_t mk, const int32_t* minv, uint64_t X,
+__device__ bool minvalues_ok(const DevDict& D, const uint16_t* code_tab, const uint64_t* TM, uint64_t mk, const int32_t* minv, uint64_t X,
                              uint32_t* scratch) {
   const int lane = LANE;
   const int TW = D.TW;
@@ -269,7 +342,7 @@ __device__ bool minvalues_ok(const DevDict& D, const DevCatalog& Cg, uint64_t mk
       while (m) {
         const int b = __builtin_ctzll(m);
         m &= m - 1;
-        const uint16_t code = Cg.code[(size_t)k * D.T + lane * 64 + b];
+        const uint16_t code = code_tab[(size_t)k * D.T + lane * 64 + b];
         if (code < 0xFFFD) {
           const int cw = code >> 6;
           const int rel = (cw == k ? 0 : (cw - D.ovf[k] + 1) * 64) + (code & 63);  // ordinal within key k
@@ -288,7 +361,7 @@ __device__ bool minvalues_ok(const DevDict& D, const DevCatalog& Cg, uint64_t mk
         while (vb) {
           const int b = __builtin_ctzll(vb);
           vb &= vb - 1;
-          const uint64_t hit = lane < TW ? (X & Cg.TM[(size_t)(w * 64 + b) * TW + lane]) : 0;
+          const uint64_t hit = lane < TW ? (X & TM[(size_t)(w * 64 + b) * TW + lane]) : 0;
           count += __ballot(hit != 0) ? 1 : 0;
         }
       }
@@ -298,13 +371,75 @@ __device__ bool minvalues_ok(const DevDict& D, const DevCatalog& Cg, uint64_t mk
   return ok;
 }
 
+// Row list: the type-mask rows one filter step ANDs into X, grouped (a group's rows are ORed, then ANDed into X).
+// Building it needs no global memory (LDS + scalar work), so all of its loads go out together in one batch
+// instead of one dependent round trip per key / resource / offering class. Per-wave LDS: RL_CAP row pointers.
+#define RL_CAP 16
+typedef const uint64_t GLB* RowPtr;
+struct RowBatch {
+  RowPtr LDS* rows;       // per-wave LDS
+  int n;
+  uint32_t endm;          // bit i: row i closes a group
+  uint64_t acc;
+};
+__device__ __forceinline__ void rl_flush(RowBatch& L, uint64_t& X, int TW) {
+  if (L.n == 0) return;
+  wave_sync();
+  const int lane = LANE;
+  uint64_t w[RL_CAP];
+#pragma unroll
+  for (int i = 0; i < RL_CAP; i++) {
+    w[i] = 0;
+    if (i < L.n && lane < TW) w[i] = L.rows[i][lane];
+  }
+#pragma unroll
+  for (int i = 0; i < RL_CAP; i++) {
+    if (i < L.n) {
+      L.acc |= w[i];
+      if ((L.endm >> i) & 1) {
+        X &= L.acc;
+        L.acc = 0;
+      }
+    }
+  }
+  L.n = 0;
+  L.endm = 0;
+  wave_sync();
+}
+// overflow path (more than RL_CAP rows in one step): a plain loop, kept small so that the push sites stay compact
+__device__ __forceinline__ void rl_flush_slow(RowBatch& L, uint64_t& X, int TW) {
+  wave_sync();
+  const int lane = LANE;
+#pragma unroll 1
+  for (int i = 0; i < L.n; i++) {
+    const uint64_t w = lane < TW ? L.rows[i][lane] : 0;
+    L.acc |= w;
+    if ((L.endm >> i) & 1) {
+      X &= L.acc;
+      L.acc = 0;
+    }
+  }
+  L.n = 0;
+  L.endm = 0;
+  wave_sync();
+}
+__device__ __forceinline__ void rl_push(RowBatch& L, uint64_t& X, int TW, const uint64_t* row, bool end) {
+  if (L.n == RL_CAP) rl_flush_slow(L, X, TW);
+  if (LANE == 0) L.rows[L.n] = (RowPtr)row;
+  if (end) L.endm |= 1u << L.n;
+  L.n++;
+}
+
 // NodeClaim.Add's instance-type filter after a successful merge. X: this lane's word of the candidate's
-// remaining types (invariant: X already passes every key the pod did not touch). Returns the new word.
-__device__ uint64_t filter_types(const DevDict& D, const DevCatalog& Cg, const ReqView& rv, uint64_t m_v, uint64_t X,
-                                 uint64_t pod_keys, const uint64_t* pvp, const int32_t* pvp_slot, const int64_t* reqrow,
-                                 const int64_t* s_preq, const int64_t* const* fitv, uint32_t rmask,
-                                 const int64_t* vint, uint32_t* scratch, uint64_t* bytes, const int32_t* jstart,
-                                 int32_t* jout, uint64_t generic_keys = 0, uint64_t* tsub = nullptr) {
+// remaining types (invariant: X already passes every key the pod did not touch). q_lane: lane r < NRES holds the
+// merged requests (candidate + pod) of resource r, j0_lane the candidate's cached threshold index. Returns the
+// new word; jout[r] receives the threshold index of resource r.
+__device__ __forceinline__ uint64_t filter_types(const DevDict& D, const CatHdr LDS* H, const ReqView& rv, uint64_t m_v,
+                                                 uint64_t X, uint64_t pod_keys, const uint64_t* pvp,
+                                                 const int32_t* pvp_slot, int64_t q_lane, int32_t j0_lane,
+                                                 const int64_t LDS* fitv_lds, uint32_t rmask, const VInt& vint,
+                                                 uint32_t* scratch, RowPtr LDS* rl, uint64_t* bytes, int32_t* jout,
+                                                 uint64_t generic_keys = 0, uint64_t* tsub = nullptr) {
   const int lane = LANE;
   const int TW = D.TW;
   uint64_t tl = tsub ? __builtin_amdgcn_s_memtime() : 0;
@@ -317,6 +452,8 @@ __device__ uint64_t filter_types(const DevDict& D, const DevCatalog& Cg, const R
   const uint64_t negM = negop_mask(rv.present, rv.compl_, rv.nz);
   const uint64_t allowed = allowed_word(D, rv, m_v, vint);
   uint64_t nb = 0;
+  bool zero = false;
+  RowBatch L{rl, 0, 0, 0};
   // 1) Intersects(type, merged) for the keys the pod changed
   uint64_t keys = pod_keys & D.catalog_keys;
   while (keys) {
@@ -326,13 +463,12 @@ __device__ uint64_t filter_types(const DevDict& D, const DevCatalog& Cg, const R
     if (((D.single_valued & ~generic_keys) >> k) & 1) {
       // X ⊆ Pass(candidate_k) and Has_merged = Has_candidate ∧ Has_pod, so for single-valued keys
       // X ∩ ∪_{Has_merged(v)} TM[v] = X ∩ ∪_{Has_pod(v)} TM[v] (precomputed PVP row, incl. NOKEY)
-      uint64_t p = lane < TW ? pvp[(size_t)pvp_slot[k] * TW + lane] : 0;
-      if (ng && lane < TW) p |= Cg.DNE[(size_t)k * TW + lane];
-      X &= p;
+      rl_push(L, X, TW, pvp + (size_t)pvp_slot[k] * TW, !ng);
+      if (ng) rl_push(L, X, TW, H->d.DNE + (size_t)k * TW, true);
       nb += (uint64_t)TW * 8 * (ng ? 2 : 1);
     } else {  // multi-valued keys, and keys narrowed by topology (Has_merged is no longer Has_pod there)
-      uint64_t acc = lane < TW ? Cg.NOKEY[(size_t)k * TW + lane] : 0;
-      if (ng && lane < TW) acc |= Cg.DNE[(size_t)k * TW + lane];
+      rl_push(L, X, TW, H->d.NOKEY + (size_t)k * TW, false);
+      if (ng) rl_push(L, X, TW, H->d.DNE + (size_t)k * TW, false);
       const int nw = (D.nval[k] + 63) >> 6;
       for (int wi = 0; wi < nw; wi++) {
         const int w = key_word(D, k, wi);
@@ -340,19 +476,16 @@ __device__ uint64_t filter_types(const DevDict& D, const DevCatalog& Cg, const R
         while (a) {
           const int b = __builtin_ctzll(a);
           a &= a - 1;
-          if (lane < TW) acc |= Cg.TM[(size_t)(w * 64 + b) * TW + lane];
+          rl_push(L, X, TW, H->d.TM + (size_t)(w * 64 + b) * TW, false);
           nb += (uint64_t)TW * 8;
         }
       }
-      X &= acc;
+      L.endm |= 1u << (L.n - 1);  // close the key's group (its last row)
     }
   }
   TSUB(1);
   // 2) resources.Fits(total, allocatable): per requested resource, a threshold mask. A NodeClaim's totals
   //    only grow, so the threshold index does too: probe 64 entries past the cached index first.
-  //    Lane r holds resource r's total and cached index (one load level for all resources).
-  const int64_t q_lane = lane < KP_NRES ? reqrow[lane] + s_preq[lane] : 0;
-  const int32_t j0_lane = (lane < KP_NRES && jstart) ? jstart[lane] : 0;
   int32_t j_lane = 0;
   uint32_t rm = rmask;
   while (rm) {
@@ -361,16 +494,20 @@ __device__ uint64_t filter_types(const DevDict& D, const DevCatalog& Cg, const R
     const int64_t q = lane_bcast_i64(q_lane, r);
     if (q <= 0) continue;
     const int j0 = __builtin_amdgcn_readlane(j0_lane, r);
-    const int n = Cg.fit_n[r];
-    const int64_t* vals = fitv[r];
+    const int n = H->fit_n[r];
+    const int slot = H->fit_slot[r];
     const int idx = j0 + lane;
-    const uint64_t bal = __ballot(idx < n && vals[idx] >= q);
+    uint64_t bal;
+    if (slot >= 0) bal = __ballot(idx < n && fitv_lds[slot * FITV_CAP + idx] >= q);
+    else bal = __ballot(idx < n && H->d.fit_vals[(size_t)r * D.T + idx] >= q);
     nb += 512;
     int j;
     if (bal) j = j0 + __builtin_ctzll(bal);
-    else j = j0 + 64 >= n ? n : wave_lower_bound(vals + j0 + 64, n - j0 - 64, q, &nb) + j0 + 64;
-    if (j >= n) X = 0;
-    else if (lane < TW) X &= Cg.fit_mask[((size_t)r * D.T + j) * TW + lane];
+    else if (j0 + 64 >= n) j = n;
+    else if (slot >= 0) j = wave_lower_bound(fitv_lds + slot * FITV_CAP + j0 + 64, n - j0 - 64, q, &nb) + j0 + 64;
+    else j = wave_lower_bound(H->d.fit_vals + (size_t)r * D.T + j0 + 64, n - j0 - 64, q, &nb) + j0 + 64;
+    if (j >= n) zero = true;
+    else rl_push(L, X, TW, H->d.fit_mask + ((size_t)r * D.T + j) * TW, true);
     nb += (uint64_t)TW * 8;
     if (lane == r) j_lane = j;
   }
@@ -379,20 +516,23 @@ __device__ uint64_t filter_types(const DevDict& D, const DevCatalog& Cg, const R
   // 3) some available offering compatible with the merged requirements. X already satisfies the
   //    candidate's offering keys; only a pod that constrains one of them can change the answer.
   if (pod_keys & D.offer_keys) {
-    const uint64_t cls = allowed_classes(D, Cg, rv, allowed, negM);
-    uint64_t offer = 0;
+    const uint64_t cls = D.C <= HDR_CLS ? allowed_classes(D, H->cls, rv, allowed, negM)
+                                        : allowed_classes(D, H->d.cls, rv, allowed, negM);
+    if (!cls) zero = true;
     uint64_t m = cls;
     while (m) {
       const int c = __builtin_ctzll(m);
       m &= m - 1;
-      if (lane < TW) offer |= Cg.offer_avail[(size_t)c * TW + lane];
+      rl_push(L, X, TW, H->d.offer_avail + (size_t)c * TW, m == 0);
     }
     nb += (uint64_t)__builtin_popcountll(cls) * TW * 8;
-    X &= offer;
   }
+  rl_flush(L, X, TW);
+  if (zero) X = 0;
   TSUB(3);
   // 4) minValues (relaxMinValues = false): distinct values of each minValues key over remaining types
-  if (!minvalues_ok(D, Cg, rv.hmin & rv.present, rv.minv, X, scratch)) X = 0;
+  if (rv.hmin & rv.present)
+    if (!minvalues_ok(D, H->d.code, H->d.TM, rv.hmin & rv.present, rv.minv, X, scratch)) X = 0;
   TSUB(4);
 #undef TSUB
   *bytes += nb;
@@ -438,7 +578,7 @@ struct TopoOwn {
 // admit (nodeDomains; Exists when the key is absent), the one with the lowest count, ties to the lowest
 // value ordinal (= byte order, the written spec for upstream's map-order tie); the key narrows to In{d}.
 __device__ bool topo_narrow(const DevDict& D, int n, const TopoOwn* own, const uint64_t* acc, const int32_t (*cnt)[64],
-                            bool allow_wk, uint64_t& m_v, ReqView& rv, const int64_t* vint) {
+                            bool allow_wk, uint64_t& m_v, ReqView& rv, const VInt& vint) {
   const int lane = LANE;
   const uint64_t allowed = allowed_word(D, rv, m_v, vint);
   uint64_t narrowed = 0, nv = m_v;
@@ -498,15 +638,16 @@ __device__ void store_merged(KReqs* dst, const ReqView& rv, uint64_t m_v, int W,
 
 // Pinned domain of each topology key on a NodeClaim's (merged) requirements: the value ordinal when the key
 // is In{one value}, 0xFE when it admits no value, 0xFF otherwise (multi-valued, complement or absent).
-__device__ void store_tcodes(const SolveArgs& a, const ReqView& rv, uint64_t m_v, int nc) {
+__device__ void store_tcodes(int n_tk, const int32_t* tk_keys, uint8_t* nc_tcode, int stride, const ReqView& rv,
+                             uint64_t m_v, int nc) {
   const int lane = LANE;
-  for (int j = 0; j < a.n_tk; j++) {
-    const int k = a.tk_keys[j];
+  for (int j = 0; j < n_tk; j++) {
+    const int k = tk_keys[j];
     const uint64_t w = lane_bcast(m_v, k);
     uint8_t code = 0xFF;
     if (((rv.present >> k) & 1) && !((rv.compl_ >> k) & 1))
       code = w == 0 ? 0xFE : (__builtin_popcountll(w) == 1 ? (uint8_t)__builtin_ctzll(w) : 0xFF);
-    if (lane == 0) a.nc_tcode[(size_t)j * a.hnc_stride + nc] = code;
+    if (lane == 0) nc_tcode[(size_t)j * stride + nc] = code;
   }
 }
 
@@ -586,7 +727,7 @@ __device__ __forceinline__ int first_ok(const int32_t* s_ok) {
 // Max allocatable over a NodeClaim's types at creation, for the resources in `rmask`. Its remaining
 // types only shrink, so this stays an upper bound: a NodeClaim whose requests + the pod's exceed it for any
 // resource cannot take the pod (Fits fails for every remaining type) and the pre-pass skips it.
-__device__ void store_maxalloc(const DevCatalog& Cg, uint64_t X, int T, uint32_t rmask, int64_t* dst) {
+__device__ void store_maxalloc(const int64_t* alloc, uint64_t X, int T, uint32_t rmask, int64_t* dst) {
   const int lane = LANE;
   for (int r = 0; r < KP_NRES; r++) {
     if (!((rmask >> r) & 1)) continue;
@@ -595,7 +736,7 @@ __device__ void store_maxalloc(const DevCatalog& Cg, uint64_t X, int T, uint32_t
     while (m) {
       const int b = __builtin_ctzll(m);
       m &= m - 1;
-      const int64_t v = Cg.alloc[(size_t)r * T + lane * 64 + b];
+      const int64_t v = alloc[(size_t)r * T + lane * 64 + b];
       mx = v > mx ? v : mx;
     }
     mx = wave_max_i64(mx);
@@ -721,13 +862,16 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
   __shared__ int32_t s_fitj[NW][KP_NRES];
   __shared__ int64_t s_preq[KP_NRES];          // pod requests (staged per pod)
   __shared__ int32_t s_pslot[KP_MAX_KEYS];     // PVP row of each pod key (staged per pod)
-  __shared__ const int64_t* s_fitp[KP_NRES];   // fit threshold values per resource: LDS copy or global
-  __shared__ const int64_t* s_fitg[8][KP_NRES];  // same, global, for catalogues 1..7
-  __shared__ int64_t s_fitv[FITV_RES][FITV_CAP];
+  __shared__ int64_t s_fitv[FITV_RES * FITV_CAP];   // Fits threshold values of catalogue 0 (CatHdr.fit_slot rows)
   __shared__ TopoOwn s_town[8];                 // owned topology groups of the popped pod (staged per pod)
   __shared__ uint64_t s_tacc[8];
   __shared__ int32_t s_tcnt[8][64];
-  __shared__ uint64_t s_tsub[8];  // KP_TIMING: wave 0's attempt split (merge, pod keys, fits, offerings, minValues, n)
+  __shared__ uint64_t s_tsub[8];  // KP_TIMING: wave 0's attempt split (merge, pod-key rows, Fits rows, row loads, minValues, n)
+  __shared__ int64_t s_vint[KP_MAX_BOUND_KEYS * 64];  // parsed integers of the bounded keys' first value words
+  __shared__ RowPtr s_rl[NW][RL_CAP];                 // per-wave row lists (filter_types)
+  __shared__ int32_t s_pvpb[32];                      // PVP row base of the popped pod per catalogue (staged per pod)
+  __shared__ CatHdr s_hdr[8];                         // catalogue descriptors 0..7
+  __shared__ CatHdr s_hdrw[NW];                       // per-wave descriptor of a catalogue >= 8
   extern __shared__ int32_t s_dyn[];  // ord[a.sort_cap], npods[a.sort_cap] while n_nc <= a.sort_cap
 
   const int tid = threadIdx.x;
@@ -735,24 +879,40 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
   const int lane = LANE;
   if (tid == 0) D = *a.dict;
   __syncthreads();
+  for (int i = tid; i < D.KB * 64; i += NT) s_vint[i] = a.vint[i];
+  const int ncat_lds = min(a.n_catalogs, 8);
+  for (int c = wave; c < ncat_lds; c += NW) hdr_fill_wave((CatHdr LDS*)&s_hdr[c], &a.cats[c], D.C);
+  __syncthreads();
+  // catalogue c's descriptor in LDS: catalogues >= 8 are copied into the wave's slot first (one round trip)
+  auto hdr = [&](int c) -> const CatHdr LDS* {
+    if (c < 8) return (const CatHdr LDS*)&s_hdr[c];
+    hdr_fill_wave((CatHdr LDS*)&s_hdrw[wave], &a.cats[c], D.C);
+    wave_sync();
+    return (const CatHdr LDS*)&s_hdrw[wave];
+  };
+  const VInt vi{(const int64_t LDS*)s_vint, a.vint, D.KB};
+  // the (first two) requested resources, whose pre-pass bounds are gathered unconditionally; the rest lazily.
+  // With fewer than two, the slot repeats resource 0/1 (an unrequested resource: 0 + 0 <= value, vacuous only
+  // if that value is >= 0, so such slots point at a requested one when there is one)
+  const uint32_t rmask_all = a.req_res_mask;
+  const int rr0 = rmask_all ? __builtin_ctz(rmask_all) : 0;
+  const uint32_t rm1 = rmask_all & (rmask_all - 1);
+  const int rr1 = rm1 ? __builtin_ctz(rm1) : rr0;
+  const uint32_t rr_rest = rm1 & (rm1 - 1);
   {  // Fits threshold tables of catalogue 0 for the first FITV_RES requested resources -> LDS
-    const DevCatalog& C0 = a.cats[0];
     int slot = 0;
     for (int r = 0; r < KP_NRES; r++) {
-      const int64_t* g = C0.fit_vals + (size_t)r * D.T;
-      const int n = C0.fit_n[r];
+      const int64_t* g = s_hdr[0].d.fit_vals + (size_t)r * D.T;
+      const int n = s_hdr[0].fit_n[r];
       const bool stage = ((a.req_res_mask >> r) & 1) && slot < FITV_RES && n <= FITV_CAP;
       if (stage) {
-        for (int i = tid; i < n; i += NT) s_fitv[slot][i] = g[i];
-        if (tid == 0) s_fitp[r] = s_fitv[slot];
+        for (int i = tid; i < n; i += NT) s_fitv[slot * FITV_CAP + i] = g[i];
+        if (tid == 0) s_hdr[0].fit_slot[r] = slot;
         slot++;
-      } else if (tid == 0) {
-        s_fitp[r] = g;
       }
-      for (int c = 1; c < a.n_catalogs && c < 8; c++)
-        if (tid == 0) s_fitg[c][r] = a.cats[c].fit_vals + (size_t)r * D.T;
     }
   }
+  __syncthreads();
   uint64_t bytes = 0, attempts = 0, pops = 0, scanned = 0, starts = 0;
   uint64_t tph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tlast = 0;
   const bool timing = a.timing && tid == 0;
@@ -815,6 +975,8 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
       for (int i = tid; i < (int)(sizeof(KReqs) / 8); i += NT) dst[i] = src[i];
       if (tid < KP_NRES) s_preq[tid] = a.shape_requests[(size_t)shape * KP_NRES + tid];
       else if (tid >= 64 && tid < 64 + KP_MAX_KEYS) s_pslot[tid - 64] = a.pvp_slot[(size_t)sl * KP_MAX_KEYS + tid - 64];
+      else if (tid >= 192 && tid < 192 + 32 && tid - 192 < a.n_catalogs)
+        s_pvpb[tid - 192] = a.pvp_base[sl * a.n_catalogs + tid - 192];
       else if (tid == 128) {  // first-fit cursors of the shape-level (LDS stacks: no global round trips)
         const int ce = a.n_existing ? min(a.cur_ex[2 * sl], mstack_query(s_stk[1], s_ctl[14], s_ctl[21], a.cur_ex[2 * sl + 1])) : 0;
         s_ctl[17] = min(ce, a.n_existing);
@@ -870,13 +1032,17 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
       for (int k = 0; k < 4; k++) {  // 4 rounds per thread: independent, so their loads overlap
         const int ec = base + k * NT + tid;
         if (ec >= a.n_existing) continue;
-        bool cand = a.ex_fail[(size_t)sl * a.n_existing + ec] != a.ex_ver[ec] && a.ex_static_ok[ec] &&
-                    ((tolmask >> a.ex_taintset[ec]) & 1);
-        if (cand) {  // Fits(Merge(requests, pod), available), exact: unrequested resources never change
-          const int64_t* av = a.ex_available + (size_t)ec * KP_NRES;
-          const int64_t* rq = a.ex_requests + (size_t)ec * KP_NRES;
-          for (int r = 0; r < KP_NRES; r++)
-            if ((a.req_res_mask >> r) & 1) cand &= rq[r] + s_preq[r] <= av[r];
+        const int32_t fl = a.ex_fail[(size_t)sl * a.n_existing + ec], ver = a.ex_ver[ec];
+        const uint8_t sok = a.ex_static_ok[ec];
+        const int32_t ts = a.ex_taintset[ec];
+        // Fits(Merge(requests, pod), available), exact: unrequested resources never change
+        const int64_t* av = a.ex_available + (size_t)ec * KP_NRES;
+        const int64_t* rq = a.ex_requests + (size_t)ec * KP_NRES;
+        bool cand = !rmask_all || (rq[rr0] + s_preq[rr0] <= av[rr0] && rq[rr1] + s_preq[rr1] <= av[rr1]);
+        cand = cand && fl != ver && sok && ((tolmask >> ts) & 1);
+        for (uint32_t rm = rr_rest; rm && cand; rm &= rm - 1) {
+          const int r = __builtin_ctz(rm);
+          cand = rq[r] + s_preq[r] <= av[r];
         }
         // topology, exact: hostname: count + self <= maxSkew (min is 0 for hostname; the count only changes
         // when the node takes a pod, i.e. with its version); dictionary key: the node's domain is its label
@@ -906,10 +1072,10 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
         if (li < n) {
           ei = s_list[li];
           attempts++;
-          ok = merge_compatible(D, kreq_at(a.ex_reqs, ei), B, b_negop, false, m_v, rv, &slots[wave], a.vint);
+          ok = merge_compatible(D, kreq_at(a.ex_reqs, ei), B, b_negop, false, m_v, rv, &slots[wave], vi);
           bytes += sizeof(KReqs);
           if (!ok && lane == 0) a.ex_fail[(size_t)sl * a.n_existing + ei] = a.ex_ver[ei];
-          if (ok && own_n) ok = topo_narrow(D, own_n, s_town, s_tacc, s_tcnt, false, m_v, rv, a.vint);  // not memoised
+          if (ok && own_n) ok = topo_narrow(D, own_n, s_town, s_tacc, s_tcnt, false, m_v, rv, vi);  // not memoised
         }
         if (lane == 0) s_ok[wave] = ok ? 1 : 0;
         __syncthreads();
@@ -960,14 +1126,17 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
           const int i = base + k * NT + tid;
           if (i >= n_nc) continue;
           const int nc = ord[i];
-          // memo first: most NodeClaims fail there, and the lanes that do skip the gathers below
-          bool cand = !(nc < a.ncc && a.nc_fail[(size_t)sl * a.ncc + nc] == a.nc_ver[nc]) &&
-                      ((tolmask >> a.nc_taintset[nc]) & 1);
-          if (cand) {
-            const int64_t* rq = a.nc_requests + (size_t)nc * KP_NRES;
-            const int64_t* mx = a.nc_maxalloc + (size_t)nc * KP_NRES;
-            for (int r = 0; r < KP_NRES; r++)
-              if ((a.req_res_mask >> r) & 1) cand &= rq[r] + s_preq[r] <= mx[r];
+          // every gather is issued unconditionally so they overlap (one round trip instead of a chain)
+          const int32_t fl = nc < a.ncc ? a.nc_fail[(size_t)sl * a.ncc + nc] : -2;
+          const int32_t ver = a.nc_ver[nc];
+          const int32_t ts = a.nc_taintset[nc];
+          const int64_t* rq = a.nc_requests + (size_t)nc * KP_NRES;
+          const int64_t* mx = a.nc_maxalloc + (size_t)nc * KP_NRES;
+          bool cand = !rmask_all || (rq[rr0] + s_preq[rr0] <= mx[rr0] && rq[rr1] + s_preq[rr1] <= mx[rr1]);
+          cand = cand && fl != ver && ((tolmask >> ts) & 1);
+          for (uint32_t rm = rr_rest; rm && cand; rm &= rm - 1) {
+            const int r = __builtin_ctz(rm);
+            cand = rq[r] + s_preq[r] <= mx[r];
           }
           for (int j = 0; j < own_n && cand; j++)  // hostname topologies, exact (count changes with the version)
             if (s_town[j].key < 0)
@@ -998,22 +1167,27 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
           int nc = -1;
           if (li < n) {
             nc = ord[s_list[li]];
-            const int tm = a.nc_tmpl[nc];
-            const int cat = a.tmpl_catalog[tm];
             attempts++;
             uint64_t* tsub = (a.timing && wave == 0) ? s_tsub : nullptr;
             const uint64_t tm0 = tsub ? __builtin_amdgcn_s_memtime() : 0;
-            ok = merge_compatible(D, kreq_at(a.nc_reqs, nc), B, b_negop, true, m_v, rv, &slots[wave], a.vint);
+            // one batch of independent loads: the candidate's requirements, remaining types, requests, cached
+            // threshold indices and catalogue; everything after it is LDS/ALU until filter_types' row batch
+            const CandReq cr = load_cand(D, kreq_at(a.nc_reqs, nc));
+            const int cat = a.nc_cat[nc];
+            const uint64_t X0 = lane < D.TW ? a.nc_X[(size_t)nc * D.TW + lane] : 0;
+            const int64_t rq_lane = lane < KP_NRES ? a.nc_requests[(size_t)nc * KP_NRES + lane] : 0;
+            const int32_t j0_lane = lane < KP_NRES ? a.nc_fitj[(size_t)nc * KP_NRES + lane] : 0;
+            ok = merge_compatible(D, cr, B, b_negop, true, m_v, rv, &slots[wave], vi);
             if (tsub && lane == 0) tsub[0] += __builtin_amdgcn_s_memtime() - tm0;
             bytes += sizeof(KReqs);
             bool memo = !ok || !own_n;  // failures after the topology step depend on the counts
-            if (ok && own_n) ok = topo_narrow(D, own_n, s_town, s_tacc, s_tcnt, true, m_v, rv, a.vint);
+            if (ok && own_n) ok = topo_narrow(D, own_n, s_town, s_tacc, s_tcnt, true, m_v, rv, vi);
             if (ok) {
-              X = lane < D.TW ? a.nc_X[(size_t)nc * D.TW + lane] : 0;
-              const uint64_t* pvp = a.shape_pvp + (size_t)a.pvp_base[sl * a.n_catalogs + cat] * D.TW;
-              X = filter_types(D, a.cats[cat], rv, m_v, X, b_keys, pvp, s_pslot, a.nc_requests + (size_t)nc * KP_NRES,
-                               s_preq, s_fitp, a.req_res_mask, a.vint, s_scratch[wave], &bytes,
-                               a.nc_fitj + (size_t)nc * KP_NRES, s_fitj[wave], topo_keys, tsub);
+              const int pb = cat < 32 ? s_pvpb[cat] : a.pvp_base[sl * a.n_catalogs + cat];
+              const uint64_t* pvp = a.shape_pvp + (size_t)pb * D.TW;
+              const int64_t q_lane = rq_lane + (lane < KP_NRES ? s_preq[lane] : 0);
+              X = filter_types(D, hdr(cat), rv, m_v, X0, b_keys, pvp, s_pslot, q_lane, j0_lane, (const int64_t LDS*)s_fitv,
+                               a.req_res_mask, vi, s_scratch[wave], (RowPtr LDS*)s_rl[wave], &bytes, s_fitj[wave], topo_keys, tsub);
               ok = __ballot(X != 0) != 0;
               if (tsub && lane == 0) tsub[5] += 1;  // attempts reaching filter_types (wave 0)
               bytes += (uint64_t)D.TW * 8 + KP_NRES * 8;
@@ -1027,7 +1201,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
           if (win >= 0) {
             if (wave == win) {
               store_merged(reinterpret_cast<KReqs*>(a.nc_reqs + (size_t)nc * sizeof(KReqs)), rv, m_v, D.W, D.KB);
-              if (a.n_tk) store_tcodes(a, rv, m_v, nc);
+              if (a.n_tk) store_tcodes(a.n_tk, a.tk_keys, a.nc_tcode, a.hnc_stride, rv, m_v, nc);
               if (lane < D.TW) a.nc_X[(size_t)nc * D.TW + lane] = X;
               if (lane < KP_NRES) a.nc_requests[(size_t)nc * KP_NRES + lane] += s_preq[lane];
               if (lane == 0) {
@@ -1072,7 +1246,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
           if (li < n) {
             tm = s_list[li];
             const int cat = a.tmpl_catalog[tm];
-            const DevCatalog& Cg = a.cats[cat];
+            const CatHdr LDS* H = hdr(cat);
             X = lane < D.TW ? a.tmpl_X[(size_t)tm * D.TW + lane] : 0;
             const uint32_t lim = a.tmpl_limit_present[tm];
             if (lim) {  // filterByRemainingResources: capacity <= remaining for every limited resource
@@ -1084,7 +1258,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
                 const int ty = lane * 64 + b;
                 bool viable = true;
                 for (int r = 0; r < KP_NRES; r++)
-                  if (((lim >> r) & 1) && Cg.cap[(size_t)r * D.T + ty] > rem[r]) viable = false;
+                  if (((lim >> r) & 1) && H->d.cap[(size_t)r * D.T + ty] > rem[r]) viable = false;
                 if (viable) keep |= 1ull << b;
               }
               X = keep;
@@ -1093,14 +1267,15 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
             bool memo = true;
             if (__ballot(X != 0)) {
               attempts++;
-              ok = merge_compatible(D, kreq_at(a.tmpl_reqs, tm), B, b_negop, true, m_v, rv, &slots[wave], a.vint);
+              const int64_t q_lane = lane < KP_NRES ? a.tmpl_daemon[(size_t)tm * KP_NRES + lane] + s_preq[lane] : 0;
+              ok = merge_compatible(D, kreq_at(a.tmpl_reqs, tm), B, b_negop, true, m_v, rv, &slots[wave], vi);
               memo = !ok || !own_n;
-              if (ok && own_n) ok = topo_narrow(D, own_n, s_town, s_tacc, s_tcnt, true, m_v, rv, a.vint);
+              if (ok && own_n) ok = topo_narrow(D, own_n, s_town, s_tacc, s_tcnt, true, m_v, rv, vi);
               if (ok) {
-                const uint64_t* pvp = a.shape_pvp + (size_t)a.pvp_base[sl * a.n_catalogs + cat] * D.TW;
-                X = filter_types(D, Cg, rv, m_v, X, b_keys, pvp, s_pslot, a.tmpl_daemon + (size_t)tm * KP_NRES, s_preq,
-                                 cat == 0 ? s_fitp : s_fitg[cat & 7], a.req_res_mask, a.vint, s_scratch[wave], &bytes,
-                                 nullptr, s_fitj[wave], topo_keys);
+                const int pb = cat < 32 ? s_pvpb[cat] : a.pvp_base[sl * a.n_catalogs + cat];
+                const uint64_t* pvp = a.shape_pvp + (size_t)pb * D.TW;
+                X = filter_types(D, H, rv, m_v, X, b_keys, pvp, s_pslot, q_lane, 0, (const int64_t LDS*)s_fitv, a.req_res_mask, vi,
+                                 s_scratch[wave], (RowPtr LDS*)s_rl[wave], &bytes, s_fitj[wave], topo_keys);
                 ok = __ballot(X != 0) != 0;
               }
             }
@@ -1114,21 +1289,22 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
           if (win >= 0) {
             if (wave == win) {
               store_merged(reinterpret_cast<KReqs*>(a.nc_reqs + (size_t)nc * sizeof(KReqs)), rv, m_v, D.W, D.KB);
-              if (a.n_tk) store_tcodes(a, rv, m_v, nc);
+              if (a.n_tk) store_tcodes(a.n_tk, a.tk_keys, a.nc_tcode, a.hnc_stride, rv, m_v, nc);
               if (lane < D.TW) a.nc_X[(size_t)nc * D.TW + lane] = X;
               if (lane < KP_NRES)
                 a.nc_requests[(size_t)nc * KP_NRES + lane] = a.tmpl_daemon[(size_t)tm * KP_NRES + lane] + s_preq[lane];
               if (lane == 0) {
                 a.nc_tmpl[nc] = tm;
                 a.nc_taintset[nc] = a.tmpl_taintset[tm];
+                a.nc_cat[nc] = a.tmpl_catalog[tm];
               }
               if (lane < KP_NRES) a.nc_fitj[(size_t)nc * KP_NRES + lane] = s_fitj[wave][lane];
-              store_maxalloc(a.cats[a.tmpl_catalog[tm]], lane < D.TW ? X : 0, D.T, a.req_res_mask,
+              store_maxalloc(hdr(a.tmpl_catalog[tm])->d.alloc, lane < D.TW ? X : 0, D.T, a.req_res_mask,
                              a.nc_maxalloc + (size_t)nc * KP_NRES);
               // subtractMax: remaining -= max capacity over the new NodeClaim's InstanceTypeOptions
               const uint32_t lim = a.tmpl_limit_present[tm];
               if (lim) {
-                const DevCatalog& Cg = a.cats[a.tmpl_catalog[tm]];
+                const CatHdr LDS* Hc = hdr(a.tmpl_catalog[tm]);
                 for (int r = 0; r < KP_NRES; r++) {
                   if (!((lim >> r) & 1)) continue;
                   int64_t mx = INT64_MIN;
@@ -1136,7 +1312,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
                   while (m) {
                     const int b = __builtin_ctzll(m);
                     m &= m - 1;
-                    const int64_t c = Cg.cap[(size_t)r * D.T + lane * 64 + b];
+                    const int64_t c = Hc->d.cap[(size_t)r * D.T + lane * 64 + b];
                     mx = c > mx ? c : mx;
                   }
                   mx = wave_max_i64(mx);
@@ -1188,7 +1364,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
           const int tb = a.tg_term_base[g];
           uint64_t mv;
           ReqView rv;
-          ok = merge_compatible(D, fin, kreq_at(a.tg_terms, tb), a.tg_terms_negop[tb], !ex, mv, rv, &slots[0], a.vint);
+          ok = merge_compatible(D, fin, kreq_at(a.tg_terms, tb), a.tg_terms_negop[tb], !ex, mv, rv, &slots[0], vi);
         }
         if (!ok) continue;
         const int row = a.tg_row[g];
@@ -1293,8 +1469,8 @@ __global__ __launch_bounds__(FIN_THREADS) void finalize_kernel(FinalizeArgs a) {
     rv.lt = R->lt;
     rv.minv = R->minv;
     const uint64_t negR = negop_mask(rv.present, rv.compl_, rv.nz);
-    const uint64_t allowed = allowed_word(D, rv, v, a.vint);
-    const uint64_t cls = allowed_classes(D, Cg, rv, allowed, negR);
+    const uint64_t allowed = allowed_word(D, rv, v, vint_global(a.vint));
+    const uint64_t cls = allowed_classes(D, Cg.cls, rv, allowed, negR);
     if (lane == 0) s_cls = cls;
   }
   __syncthreads();
@@ -1381,8 +1557,8 @@ __global__ __launch_bounds__(FEAS_WAVES * 64) void feasibility_kernel(FeasArgs a
     rv.lt = Q->lt;
     rv.minv = Q->minv;
     const uint64_t negQ = negop_mask(rv.present, rv.compl_, rv.nz);
-    const uint64_t allowed = allowed_word(D, rv, v, a.vint);
-    const uint64_t cls = allowed_classes(D, Cg, rv, allowed, negQ);
+    const uint64_t allowed = allowed_word(D, rv, v, vint_global(a.vint));
+    const uint64_t cls = allowed_classes(D, Cg.cls, rv, allowed, negQ);
     s_allowed[wave][lane] = allowed;
     const int64_t rq_lane = lane < KP_NRES ? a.q_requests[(size_t)q * KP_NRES + lane] : 0;
     uint32_t rmask = (uint32_t)__ballot(rq_lane > 0);
@@ -1437,8 +1613,16 @@ __global__ __launch_bounds__(FEAS_WAVES * 64) void feasibility_kernel(FeasArgs a
 // ------------------------------------------------------------------------------------------------
 hipError_t launch_solve(const SolveArgs& a, int nw, size_t dyn_lds, hipStream_t s) {
   (void)nw;  // 8 waves: one candidate per wave, 512 pre-pass lanes
-  if (a.n_groups) hipLaunchKernelGGL((solve_kernel<8, true>), dim3(1), dim3(8 * 64), dyn_lds, s, a);
-  else hipLaunchKernelGGL((solve_kernel<8, false>), dim3(1), dim3(8 * 64), dyn_lds, s, a);
+  // 4 waves (one per SIMD): the per-pod barriers and pre-pass compaction are cheaper than with 8, and 4
+  // candidates per attempt round cover the typical 2-3 attempts per pod. KP_SOLVE_WAVES=8: 8 waves.
+  static const int nw4 = !(getenv("KP_SOLVE_WAVES") && atoi(getenv("KP_SOLVE_WAVES")) == 8);
+  if (nw4) {
+    if (a.n_groups) hipLaunchKernelGGL((solve_kernel<4, true>), dim3(1), dim3(4 * 64), dyn_lds, s, a);
+    else hipLaunchKernelGGL((solve_kernel<4, false>), dim3(1), dim3(4 * 64), dyn_lds, s, a);
+  } else {
+    if (a.n_groups) hipLaunchKernelGGL((solve_kernel<8, true>), dim3(1), dim3(8 * 64), dyn_lds, s, a);
+    else hipLaunchKernelGGL((solve_kernel<8, false>), dim3(1), dim3(8 * 64), dyn_lds, s, a);
+  }
   return hipGetLastError();
 }
 hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s) {

@@ -134,7 +134,7 @@ __global__ __launch_bounds__(SIM_WAVES * 64) void sim_usable_kernel(SimArgs a) {
     const KReqs* B = reinterpret_cast<const KReqs*>(a.shape_reqs + (size_t)sl * sizeof(KReqs));
     const uint64_t v = lane < D.W ? B->vals[lane] : 0;
     const ReqView rv = stored_view(D, B, v);
-    s_allow[wave][lane] = allowed_word(D, rv, v, a.vint);
+    s_allow[wave][lane] = allowed_word(D, rv, v, vint_global(a.vint));
     wave_sync();
     const uint64_t negB = a.shape_negop[sl];
     const uint64_t tol = a.shape_tolerates[shape];
@@ -174,14 +174,20 @@ __global__ __launch_bounds__(SIM_WAVES * 64) void sim_prep_kernel(SimArgs a) {
   __shared__ int32_t s_pslot[SIM_WAVES][KP_MAX_KEYS];
   __shared__ uint32_t s_scratch[SIM_WAVES][2 * KP_MAX_WORDS];
   __shared__ int32_t s_fitj[SIM_WAVES][KP_NRES];
-  __shared__ const int64_t* s_fitg[8][KP_NRES];
+  __shared__ RowPtr s_rl[SIM_WAVES][RL_CAP];
+  __shared__ CatHdr s_hdr[8];
+  __shared__ CatHdr s_hdrw[SIM_WAVES];
   if (threadIdx.x == 0) D = *a.dict;
-  if (threadIdx.x < 8 * KP_NRES) {
-    const int c = threadIdx.x / KP_NRES, r = threadIdx.x % KP_NRES;
-    s_fitg[c][r] = c < a.n_catalogs ? a.cats[c].fit_vals + (size_t)r * a.dict->T : nullptr;
-  }
   __syncthreads();
   const int wave = threadIdx.x >> 6, lane = LANE;
+  for (int c = wave; c < min(a.n_catalogs, 8); c += SIM_WAVES) hdr_fill_wave((CatHdr LDS*)&s_hdr[c], &a.cats[c], D.C);
+  __syncthreads();
+  auto hdr = [&](int c) -> const CatHdr LDS* {
+    if (c < 8) return (const CatHdr LDS*)&s_hdr[c];
+    hdr_fill_wave((CatHdr LDS*)&s_hdrw[wave], &a.cats[c], D.C);
+    wave_sync();
+    return (const CatHdr LDS*)&s_hdrw[wave];
+  };
   uint64_t bytes = 0;
   for (int sl = blockIdx.x * SIM_WAVES + wave; sl < a.SL; sl += gridDim.x * SIM_WAVES) {
     const int shape = a.sl_shape[sl];
@@ -199,12 +205,12 @@ __global__ __launch_bounds__(SIM_WAVES * 64) void sim_prep_kernel(SimArgs a) {
       uint64_t m_v = 0;
       ReqView rv;
       bool ok = merge_compatible(D, reinterpret_cast<const KReqs*>(a.tmpl_reqs + (size_t)t * sizeof(KReqs)), &s_B[wave],
-                                 negB, true, m_v, rv, &slots[wave], a.vint);
+                                 negB, true, m_v, rv, &slots[wave], vint_global(a.vint));
       if (ok) {
         const uint64_t* pvp = a.shape_pvp + (size_t)a.pvp_base[sl * a.n_catalogs + cat] * D.TW;
-        X = filter_types(D, a.cats[cat], rv, m_v, X, s_B[wave].present, pvp, s_pslot[wave],
-                         a.tmpl_daemon + (size_t)t * KP_NRES, s_preq[wave], s_fitg[cat & 7], a.req_res_mask, a.vint,
-                         s_scratch[wave], &bytes, nullptr, s_fitj[wave]);
+        const int64_t q_lane = lane < KP_NRES ? a.tmpl_daemon[(size_t)t * KP_NRES + lane] + s_preq[wave][lane] : 0;
+        X = filter_types(D, hdr(cat), rv, m_v, X, s_B[wave].present, pvp, s_pslot[wave], q_lane, 0, nullptr,
+                         a.req_res_mask, vint_global(a.vint), s_scratch[wave], (RowPtr LDS*)s_rl[wave], &bytes, s_fitj[wave]);
         ok = __ballot(X != 0) != 0;
       }
       if (ok) {
@@ -216,7 +222,7 @@ __global__ __launch_bounds__(SIM_WAVES * 64) void sim_prep_kernel(SimArgs a) {
           out->maxalloc[lane] = INT64_MAX;
         }
         wave_sync();
-        store_maxalloc(a.cats[cat], lane < D.TW ? X : 0, D.T, a.req_res_mask, out->maxalloc);
+        store_maxalloc(a.cats[cat].alloc, lane < D.TW ? X : 0, D.T, a.req_res_mask, out->maxalloc);
         if (lane == 0) {
           out->tmpl = t;
           out->taintset = a.tmpl_taintset[t];
@@ -244,15 +250,21 @@ __global__ __launch_bounds__(NW * 64) void sim_kernel(SimArgs a) {
   __shared__ uint32_t s_scratch[NW][2 * KP_MAX_WORDS];
   __shared__ uint64_t s_mask[NW][KP_MAX_TYPE_WORDS];
   __shared__ int32_t s_fitj[NW][KP_NRES];
-  __shared__ const int64_t* s_fitg[8][KP_NRES];
+  __shared__ RowPtr s_rl[NW][RL_CAP];
+  __shared__ CatHdr s_hdr[8];
+  __shared__ CatHdr s_hdrw[NW];
   extern __shared__ uint64_t s_dyn64[];
   const int tid = threadIdx.x, wave = tid >> 6, lane = LANE;
   if (tid == 0) D = *a.dict;
-  if (tid < 8 * KP_NRES) {
-    const int c = tid / KP_NRES, r = tid % KP_NRES;
-    s_fitg[c][r] = c < a.n_catalogs ? a.cats[c].fit_vals + (size_t)r * a.dict->T : nullptr;
-  }
   __syncthreads();
+  for (int c = wave; c < min(a.n_catalogs, 8); c += NW) hdr_fill_wave((CatHdr LDS*)&s_hdr[c], &a.cats[c], D.C);
+  __syncthreads();
+  auto hdr = [&](int c) -> const CatHdr LDS* {
+    if (c < 8) return (const CatHdr LDS*)&s_hdr[c];
+    hdr_fill_wave((CatHdr LDS*)&s_hdrw[wave], &a.cats[c], D.C);
+    wave_sync();
+    return (const CatHdr LDS*)&s_hdrw[wave];
+  };
   const int EW = a.EW, SL = a.SL, cap = a.cap;
   uint8_t* wbase = reinterpret_cast<uint8_t*>(s_dyn64) + (size_t)wave * a.wave_lds;
   uint64_t* excl = reinterpret_cast<uint64_t*>(wbase);
@@ -424,13 +436,17 @@ __global__ __launch_bounds__(NW * 64) void sim_kernel(SimArgs a) {
           const int cat = a.tmpl_catalog[nc->tmpl];
           uint64_t m_v = 0, X = 0;
           ReqView rv;
-          bool ok = merge_compatible(D, &nc->reqs, sB, a.shape_negop[sl], true, m_v, rv, &slots[wave], a.vint);
+          bool ok = merge_compatible(D, &nc->reqs, sB, a.shape_negop[sl], true, m_v, rv, &slots[wave],
+                                     vint_global(a.vint));
           bytes += sizeof(KReqs);
           if (ok) {
             X = lane < D.TW ? nc->X[lane] : 0;
             const uint64_t* pvp = a.shape_pvp + (size_t)a.pvp_base[sl * a.n_catalogs + cat] * D.TW;
-            X = filter_types(D, a.cats[cat], rv, m_v, X, sB->present, pvp, s_pslot[wave], nc->requests, spreq,
-                             s_fitg[cat & 7], rmask, a.vint, s_scratch[wave], &bytes, nc->fitj, s_fitj[wave]);
+            const int64_t q_lane = lane < KP_NRES ? nc->requests[lane] + spreq[lane] : 0;
+            const int32_t j0_lane = lane < KP_NRES ? nc->fitj[lane] : 0;
+            X = filter_types(D, hdr(cat), rv, m_v, X, sB->present, pvp, s_pslot[wave], q_lane, j0_lane, nullptr,
+                             rmask, vint_global(a.vint), s_scratch[wave], (RowPtr LDS*)s_rl[wave],
+                             &bytes, s_fitj[wave]);
             ok = __ballot(X != 0) != 0;
           }
           if (ok) {
@@ -499,8 +515,8 @@ __global__ __launch_bounds__(NW * 64) void sim_kernel(SimArgs a) {
         const uint64_t v = lane < D.W ? nc->reqs.vals[lane] : 0;
         const ReqView rv = stored_view(D, &nc->reqs, v);
         const uint64_t negR = negop_mask(rv.present, rv.compl_, rv.nz);
-        const uint64_t allowed = allowed_word(D, rv, v, a.vint);
-        const uint64_t cls = allowed_classes(D, Cg, rv, allowed, negR);
+        const uint64_t allowed = allowed_word(D, rv, v, vint_global(a.vint));
+        const uint64_t cls = allowed_classes(D, Cg.cls, rv, allowed, negR);
         const bool ctp = (rv.present >> a.ct_key) & 1;
         bool ncSpot;
         if (a.spot_bit >= 0) ncSpot = !ctp || bit_of(allowed, a.spot_bit);
@@ -551,7 +567,7 @@ __global__ __launch_bounds__(NW * 64) void sim_kernel(SimArgs a) {
               atomicOr((unsigned long long*)&msk[t >> 6], 1ull << (t & 63));
             }
             wave_sync();
-            ok = minvalues_ok(D, Cg, hmin, rv.minv, lane < D.TW ? msk[lane] : 0, s_scratch[wave]);
+            ok = minvalues_ok(D, Cg.code, Cg.TM, hmin, rv.minv, lane < D.TW ? msk[lane] : 0, s_scratch[wave]);
           }
           // filterByPrice: Offerings.Available().WorstLaunchPrice(reqs) < candidate price
           double wlp[2] = {__DBL_MAX__, __DBL_MAX__};
@@ -606,7 +622,7 @@ __global__ __launch_bounds__(NW * 64) void sim_kernel(SimArgs a) {
               for (int h = 0; h < 2; h++)
                 if (keep[h]) atomicOr((unsigned long long*)&msk[tt[h] >> 6], 1ull << (tt[h] & 63));
               wave_sync();
-              if (!minvalues_ok(D, Cg, hmin, rv.minv, lane < D.TW ? msk[lane] : 0, s_scratch[wave])) ok = false;
+              if (!minvalues_ok(D, Cg.code, Cg.TM, hmin, rv.minv, lane < D.TW ? msk[lane] : 0, s_scratch[wave])) ok = false;
             }
             if (count == 0) ok = false;
             n_options = count;

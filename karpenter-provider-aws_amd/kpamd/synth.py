@@ -265,10 +265,16 @@ def random_topology_problem(catalog, seed, n_types=80, n_pods=240, n_existing=12
 # ------------------------------------------------------------------------------------------------
 # randomized parity scenarios (oracle vs device), small enough for the set-based oracle
 # ------------------------------------------------------------------------------------------------
-def random_problem(catalog, seed, n_types=120, n_pods=300, n_pools=3, n_existing=0, n_shapes=24):
+def random_problem(catalog, seed, n_types=120, n_pods=300, n_pools=3, n_existing=0, n_shapes=24, n_catalogs=1):
+    """Random scenario. n_catalogs > 1: pool i resolves GetInstanceTypes to catalogue i % n_catalogs, each a
+    different random subset of the docs catalogue (multi-NodeClass clusters)."""
     rng = np.random.default_rng(seed)
     idx = np.sort(rng.choice(len(catalog), size=min(n_types, len(catalog)), replace=False))
     cat = [catalog[i] for i in idx]
+    cats = [cat]
+    for _ in range(1, n_catalogs):
+        ix = np.sort(rng.choice(len(catalog), size=min(n_types, len(catalog)), replace=False))
+        cats.append([catalog[i] for i in ix])
     fams = sorted({r[2][0] for it in cat for r in it.requirements if r[0] == K + "instance-family" and r[2]})
 
     def rand_req(for_pool):
@@ -310,7 +316,7 @@ def random_problem(catalog, seed, n_types=120, n_pods=300, n_pools=3, n_existing
         taints = [("dedicated", f"team{i}", "NoSchedule")] if rng.random() < 0.3 else []
         limits = {"cpu": int(rng.integers(8, 200)) * 1000} if rng.random() < 0.5 else {}
         daemon = {"cpu": int(rng.choice([0, 100, 250])), "memory": 64 * MI * 1000, "pods": 1000} if rng.random() < 0.5 else {}
-        pools.append(NodePool(f"pool-{i}", int(rng.integers(0, 4)), 0, reqs, labels={"team": f"t{i % 2}"},
+        pools.append(NodePool(f"pool-{i}", int(rng.integers(0, 4)), i % n_catalogs, reqs, labels={"team": f"t{i % 2}"},
                               taints=taints, limits=limits, daemon_requests=daemon))
     shapes = []
     for s in range(n_shapes):
@@ -346,7 +352,7 @@ def random_problem(catalog, seed, n_types=120, n_pods=300, n_pools=3, n_existing
                                      [("dedicated", "team0", "NoSchedule")] if rng.random() < 0.1 else [],
                                      bool(rng.random() < 0.9)))
     s, c, u = _pods(rng, n_pods, len(shapes))
-    return Problem([cat], pools, shapes, s, c, u, existing=existing, name=f"random-{seed}")
+    return Problem(cats, pools, shapes, s, c, u, existing=existing, name=f"random-{seed}")
 
 
 # ------------------------------------------------------------------------------------------------

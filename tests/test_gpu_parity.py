@@ -53,6 +53,18 @@ def test_random_scenarios(ctx, catalog, seed):
     check_same(got, want)
 
 
+@pytest.mark.parametrize("seed,n_catalogs", [(100, 3), (105, 10)])
+def test_multi_catalog(ctx, catalog, seed, n_catalogs):
+    """Pools on different catalogues (GetInstanceTypes per NodeClass): per-catalogue Fits thresholds, PVP rows
+    and offering classes, including catalogue ids >= 8 (no LDS pointer slot)."""
+    from kpamd import synth
+    prob = synth.random_problem(catalog, seed, n_types=150, n_pods=300, n_pools=max(3, n_catalogs),
+                                n_existing=5, n_shapes=20, n_catalogs=n_catalogs)
+    got, want = run_both(ctx, prob)
+    check_same(got, want)
+    assert len({n["nodepool"] for n in got["nodeclaims"]}) > 1
+
+
 def test_config5_scaled(ctx, catalog):
     from kpamd import synth
     got, want = run_both(ctx, synth.config5(catalog, n_pods=3000, seed=5))

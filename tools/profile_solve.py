@@ -31,6 +31,6 @@ out = {"config": cfg, "pods": n, "solve_kernel_ms": st["solve_kernel_ms"], "atte
 ac = st["attempt_cycles"]
 if ac[5]:
     out["attempt_cycles_per_attempt"] = {k: round(v / ac[5], 1) for k, v in
-                                         zip(["merge", "pod-keys", "fits", "offerings", "minvalues"], ac[:5])}
+                                         zip(["merge", "pod-key-rows", "fits-rows", "offer-rows+row-loads", "minvalues"], ac[:5])}
     out["attempts_timed"] = ac[5]
 print(json.dumps(out))
