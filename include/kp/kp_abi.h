@@ -13,6 +13,10 @@
  *   kp_filter_compatible_available <- filter.CompatibleAvailableFilter
  *                             (R:pkg/providers/instance/filter/filter.go:39-64), batched: many
  *                             (requirements, requests) rows × one catalogue on the GPU.
+ *   kp_launch_select       <- instance.DefaultProvider.Create's launch-side selection
+ *                             (R:pkg/providers/instance/instance.go:117-125 Create -> filterInstanceTypes :242-270,
+ *                              getCapacityType :504-518, checkODFallback :336-355, getOverrides :392-439), batched:
+ *                             one row per NodeClaim being launched.
  *   kp_solve               <- upstream scheduling.Scheduler.Solve (sigs.k8s.io/karpenter
  *                             pkg/controllers/provisioning/scheduling/scheduler.go), reached from
  *                             R:pkg/providers/instancetype/suite_test.go:93,279 (NewProvisioner/ExpectProvisioned),
@@ -398,6 +402,61 @@ int32_t kp_filter_prepare(kp_ctx* ctx, const kp_catalog* cat, const kp_feasibili
                           int32_t with_cheapest, kp_filter_plan** out);
 int32_t kp_filter_run(kp_filter_plan* plan, uint64_t* out_mask, double* out_cheapest, kp_solve_stats* stats);
 void kp_filter_plan_destroy(kp_filter_plan* plan);
+
+/* ---- launch-side selection (instance.DefaultProvider.Create) -------------------------------------
+ * For each NodeClaim: filterInstanceTypes (R:pkg/providers/instance/instance.go:242-270) =
+ *   CompatibleAvailableFilter (R:filter.go:39-64) -> CapacityReservationTypeFilter / CapacityBlockFilter /
+ *   ReservedOfferingFilter (R:filter.go:66-274; no-ops: reserved offerings are not representable in ABI v2) ->
+ *   ExoticInstanceTypeFilter (R:filter.go:279-318) -> SpotInstanceFilter (R:filter.go:328-386), each filter that
+ *   empties the set failing the launch with InsufficientCapacityError; then InstanceTypes.Truncate(reqs,
+ *   max_types) = OrderByPrice + cut + SatisfiesMinValues (error -> CreateError "InstanceTypeFilteringFailed");
+ * getCapacityType (R:instance.go:504-518): reserved, then spot, if the requirements allow it and some remaining
+ *   type has an available compatible offering of it, else on-demand;
+ * checkODFallback (R:instance.go:336-355): on-demand launch while flexible to spot with < 5 types (a warning);
+ * getOverrides (R:instance.go:392-439): per remaining type (in truncated order) its available offerings compatible
+ *   with the requirements narrowed to the chosen capacity type, in the type's offering order, whose zone has a
+ *   subnet (subnet_zones stands for ZonalSubnetsForLaunch); launch-template grouping by AMI is AWS I/O, out of scope. */
+typedef struct kp_launch_request {
+  kp_requirements requirements;   /* NodeClaim.Spec.Requirements (minValues allowed) */
+  kp_resource_list requests;      /* NodeClaim.Spec.Resources.Requests */
+  const uint32_t* instance_types; /* the instance types Create receives: catalogue indices, any order */
+  uint32_t n_instance_types;      /* <= 1024 on the device path */
+  uint32_t reserved_;
+} kp_launch_request;
+
+enum kp_launch_status {
+  KP_LAUNCH_OK = 0,
+  KP_LAUNCH_INSUFFICIENT_CAPACITY = 1, /* a filter left no instance type (failed_filter says which) */
+  KP_LAUNCH_MINVALUES = 2              /* Truncate: the cheapest max_types types do not satisfy minValues */
+};
+enum kp_launch_filter { KP_FILTER_COMPATIBLE_AVAILABLE = 0, KP_FILTER_EXOTIC = 4, KP_FILTER_SPOT = 5 };
+
+typedef struct kp_launch_result {
+  int32_t status;             /* enum kp_launch_status */
+  int32_t capacity_type;      /* 0 on-demand, 1 spot (KP_LAUNCH_OK only) */
+  uint32_t n_types;           /* types written to out_types (after filters + Truncate) */
+  uint32_t n_overrides;       /* overrides written to out_overrides */
+  int32_t failed_filter;      /* enum kp_launch_filter when INSUFFICIENT_CAPACITY, else -1 */
+  uint32_t n_compatible;      /* types kept by CompatibleAvailableFilter */
+  uint32_t rejected_exotic;   /* types removed by ExoticInstanceTypeFilter */
+  uint32_t rejected_spot;     /* types removed by SpotInstanceFilter */
+  int32_t od_fallback_warning;/* checkODFallback would log its error */
+  int32_t reserved_;
+} kp_launch_result;
+
+/* out_types: [n][max_types] catalogue indices in launch order; out_overrides: [n][max_types * n_subnet_zones]
+ * entries (type_index << 8) | zone, zone = index into subnet_zones. max_types = 60 in the reference
+  * (maxInstanceTypes, R:instance.go:60). */
+int32_t kp_launch_select(kp_ctx* ctx, const kp_catalog* cat, const kp_launch_request* reqs, uint32_t n,
+                         const char* const* subnet_zones, uint32_t n_subnet_zones, uint32_t max_types,
+                         kp_launch_result* out, uint32_t* out_types, uint32_t* out_overrides, kp_solve_stats* stats);
+typedef struct kp_launch_plan kp_launch_plan;
+int32_t kp_launch_prepare(kp_ctx* ctx, const kp_catalog* cat, const kp_launch_request* reqs, uint32_t n,
+                          const char* const* subnet_zones, uint32_t n_subnet_zones, uint32_t max_types,
+                          kp_launch_plan** out);
+int32_t kp_launch_run(kp_launch_plan* plan, kp_launch_result* out, uint32_t* out_types, uint32_t* out_overrides,
+                      kp_solve_stats* stats);
+void kp_launch_plan_destroy(kp_launch_plan* plan);
 
 /* ---- Solve -------------------------------------------------------------------------------- */
 /* kp_solve = kp_solve_prepare + kp_solve_run + kp_solve_plan_destroy. prepare compiles the batch (string

@@ -143,6 +143,40 @@ struct FeasArgs {
   double* out_cheapest;      // [Q][T] or null
 };
 
+// ---- launch-side selection (kp_launch_select) ------------------------------------------------------
+#define LAUNCH_CAP 1024  // instance types per request on the device path
+struct LaunchOut {  // kp_launch_result as the device writes it
+  int32_t status, capacity_type;
+  uint32_t n_types, n_overrides;
+  int32_t failed_filter;
+  uint32_t n_compatible, rejected_exotic, rejected_spot;
+  int32_t od_fallback_warning, pad_;
+};
+struct LaunchArgs {
+  const DevDict* dict;
+  const DevCatalog* cat;
+  const int64_t* vint;
+  int32_t n;                  // requests
+  int32_t max_types;          // Truncate limit (0: none)
+  int32_t spot_bit, od_bit;   // dictionary value bits of karpenter.sh/capacity-type spot / on-demand (-1: absent)
+  int32_t ct_key;             // dictionary key of karpenter.sh/capacity-type
+  int32_t MO;                 // offerings per type (stride of ofs_cls)
+  uint64_t cls_spot, cls_od;  // offering classes whose capacity type is spot / on-demand
+  const uint8_t* q_reqs;      // [n] KReqs
+  const int64_t* q_requests;  // [n][NRES]
+  const uint32_t* list_off;   // [n+1] CSR of the requests' instance-type lists
+  const uint32_t* list;
+  const uint64_t* exotic;     // [TW] ExoticInstanceTypeFilter's exotic types (metal size or accelerator capacity)
+  const int8_t* cls_zone;     // [C] index of the class's zone in the subnet zones, -1: no subnet
+  const uint8_t* ofs_cls;     // [T][MO] offering classes of each type in offering order, 0xFF: end
+  uint32_t ovr_stride;        // out_overrides entries per request
+  LaunchOut* out;
+  uint32_t* out_types;        // [n][max_types]
+  uint32_t* out_overrides;    // [n][ovr_stride]
+  uint64_t* stats;            // [2]: types evaluated, algorithmic bytes
+};
+hipError_t launch_launch(const LaunchArgs& a, hipStream_t s);
+
 // ---- consolidation simulations (kp_cluster_simulate) -------------------------------------------
 // One in-flight NodeClaim (a simulation with a second one is a no-op, so it stops there).
 struct SimNC {

@@ -2091,31 +2091,11 @@ void kp_result_destroy(kp_solve_result* r) { delete r; }
 // CompatibleAvailableFilter batched on the GPU.
 }  // extern "C"
 
-struct kp_filter_plan {
-  kp_ctx* ctx = nullptr;
-  DevBuf buf;
-  FeasArgs fa;
-  uint32_t n_queries = 0;
-  int T = 0;
-  size_t tiles = 0, o_mask = 0, o_ch = 0;
-  bool cheapest = false;
-  double prepare_ms = 0;
-};
-
-extern "C" {
-
-// Compile the query rows against the catalogue dictionary and upload rows + catalogue SoA (resident).
-int32_t kp_filter_prepare(kp_ctx* ctx, const kp_catalog* cat, const kp_feasibility_query* queries, uint32_t n_queries,
-                          int32_t with_cheapest, kp_filter_plan** out) {
-  auto t0 = std::chrono::steady_clock::now();
-  if (!ctx || !cat || (!queries && n_queries) || !out) return fail(KP_E_INVAL, "null argument");
-  std::lock_guard<std::mutex> lock(ctx->mu);
-  HIPCHK(hipSetDevice(ctx->device));
-  auto plan = std::make_unique<kp_filter_plan>();
-  plan->ctx = ctx;
-  Compiled cp;
+namespace {
+// Dictionary + catalogue SoA for a batch of query rows against ONE catalogue (CompatibleAvailableFilter rows,
+// launch requests): the catalogue's labels and offerings plus the rows' requirements, compiled rows in qreqs.
+int32_t CompileQueries(const kp_catalog* cat, const vector<RawReqs>& qs, Compiled& cp, vector<KReqs>& qreqs) {
   DictBuilder db;
-  vector<RawReqs> qs(n_queries);
   for (auto& t : cat->types) {
     db.addReqs(t.reqs);
     for (auto& o : t.offs) {
@@ -2126,10 +2106,7 @@ int32_t kp_filter_prepare(kp_ctx* ctx, const kp_catalog* cat, const kp_feasibili
   }
   db.bounded[kResID];
   db.bounded[kResType];
-  for (uint32_t i = 0; i < n_queries; i++) {
-    qs[i] = ParseReqs(queries[i].requirements);
-    db.addReqs(qs[i]);
-  }
+  for (auto& q : qs) db.addReqs(q);
   int32_t rc = db.build(cp.d);
   if (rc) return rc;
   const int T = (int)cat->types.size(), TW = std::max(1, (T + 63) / 64);
@@ -2159,13 +2136,46 @@ int32_t kp_filter_prepare(kp_ctx* ctx, const kp_catalog* cat, const kp_feasibili
       if (!((cp.cats[0].NOKEY[(size_t)k * TW + t / 64] >> (t % 64)) & 1)) catalog_keys |= 1ull << k;
   cp.d.dd.catalog_keys = catalog_keys;
   cp.d.dd.single_valued = catalog_keys & ~cp.cats[0].multi_valued;
-  vector<KReqs> qreqs(std::max<uint32_t>(n_queries, 1));
+  qreqs.assign(std::max<size_t>(qs.size(), 1), KReqs{});
+  for (size_t i = 0; i < qs.size(); i++) qreqs[i] = Compile(d, qs[i]);
+  return KP_OK;
+}
+
+}  // namespace
+
+struct kp_filter_plan {
+  kp_ctx* ctx = nullptr;
+  DevBuf buf;
+  FeasArgs fa;
+  uint32_t n_queries = 0;
+  int T = 0;
+  size_t tiles = 0, o_mask = 0, o_ch = 0;
+  bool cheapest = false;
+  double prepare_ms = 0;
+};
+
+extern "C" {
+
+// Compile the query rows against the catalogue dictionary and upload rows + catalogue SoA (resident).
+int32_t kp_filter_prepare(kp_ctx* ctx, const kp_catalog* cat, const kp_feasibility_query* queries, uint32_t n_queries,
+                          int32_t with_cheapest, kp_filter_plan** out) {
+  auto t0 = std::chrono::steady_clock::now();
+  if (!ctx || !cat || (!queries && n_queries) || !out) return fail(KP_E_INVAL, "null argument");
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device));
+  auto plan = std::make_unique<kp_filter_plan>();
+  plan->ctx = ctx;
+  Compiled cp;
+  vector<RawReqs> qs(n_queries);
+  for (uint32_t i = 0; i < n_queries; i++) qs[i] = ParseReqs(queries[i].requirements);
+  vector<KReqs> qreqs;
+  int32_t rc = CompileQueries(cat, qs, cp, qreqs);
+  if (rc) return rc;
+  const int T = (int)cat->types.size();
   vector<int64_t> qrq((size_t)std::max<uint32_t>(n_queries, 1) * KP_NRES, 0);
-  for (uint32_t i = 0; i < n_queries; i++) {
-    qreqs[i] = Compile(d, qs[i]);
+  for (uint32_t i = 0; i < n_queries; i++)
     for (int r = 0; r < KP_NRES; r++)
       qrq[(size_t)i * KP_NRES + r] = (queries[i].requests.present >> r) & 1 ? queries[i].requests.milli[r] : 0;
-  }
   Blob blob;
   const size_t o_dict = blob.put(&cp.d.dd, 1);
   const size_t o_vint = blob.put(cp.d.vint);
@@ -2250,6 +2260,220 @@ int32_t kp_filter_compatible_available(kp_ctx* ctx, const kp_catalog* cat, const
   if (rc) return rc;
   rc = kp_filter_run(plan, out_mask, out_cheapest, stats);
   kp_filter_plan_destroy(plan);
+  return rc;
+}
+
+// ---- launch-side selection (instance.DefaultProvider.Create), batched over NodeClaims -----------------
+}  // extern "C"
+
+struct kp_launch_plan {
+  kp_ctx* ctx = nullptr;
+  DevBuf buf;
+  LaunchArgs la;
+  uint32_t n = 0, max_types = 0, ovr_stride = 0;
+  size_t o_out = 0, o_types = 0, o_ovr = 0, o_stats = 0;
+  double prepare_ms = 0;
+};
+static_assert(sizeof(LaunchOut) == sizeof(kp_launch_result), "LaunchOut mirrors kp_launch_result");
+
+extern "C" {
+
+int32_t kp_launch_prepare(kp_ctx* ctx, const kp_catalog* cat, const kp_launch_request* reqs, uint32_t n,
+                          const char* const* subnet_zones, uint32_t n_subnet_zones, uint32_t max_types,
+                          kp_launch_plan** out) {
+  auto t0 = std::chrono::steady_clock::now();
+  if (!ctx || !cat || (!reqs && n) || !out || (!subnet_zones && n_subnet_zones)) return fail(KP_E_INVAL, "null argument");
+  if (max_types == 0 || max_types > LAUNCH_CAP) return fail(KP_E_INVAL, "max_types %u not in [1, %d]", max_types, LAUNCH_CAP);
+  if (n_subnet_zones > 255) return fail(KP_E_UNSUPPORTED, "%u subnet zones", n_subnet_zones);
+  const int T = (int)cat->types.size();
+  for (auto& t : cat->types) {
+    std::set<std::pair<string, string>> seen;  // overrides per type <= subnet zones needs one offering per (ct, zone)
+    for (auto& o : t.offs) {
+      if (o.ct == "reserved") return fail(KP_E_UNSUPPORTED, "reserved offerings");
+      if (o.has_zone && !seen.insert({o.ct, o.zone}).second)
+        return fail(KP_E_UNSUPPORTED, "%s: two %s offerings in zone %s", t.name.c_str(), o.ct.c_str(), o.zone.c_str());
+    }
+  }
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device));
+  auto plan = std::make_unique<kp_launch_plan>();
+  plan->ctx = ctx;
+  Compiled cp;
+  vector<RawReqs> qs(n);
+  vector<uint32_t> off(n + 1, 0), list;
+  for (uint32_t i = 0; i < n; i++) {
+    qs[i] = ParseReqs(reqs[i].requirements);
+    if (reqs[i].n_instance_types > LAUNCH_CAP)
+      return fail(KP_E_UNSUPPORTED, "request %u: %u instance types", i, reqs[i].n_instance_types);
+    if (reqs[i].n_instance_types && !reqs[i].instance_types) return fail(KP_E_INVAL, "request %u: null list", i);
+    for (uint32_t j = 0; j < reqs[i].n_instance_types; j++) {
+      if (reqs[i].instance_types[j] >= (uint32_t)T) return fail(KP_E_INVAL, "request %u: type %u", i, reqs[i].instance_types[j]);
+      list.push_back(reqs[i].instance_types[j]);
+    }
+    off[i + 1] = (uint32_t)list.size();
+  }
+  if (T > 4096) return fail(KP_E_UNSUPPORTED, "%d instance types", T);
+  vector<KReqs> qreqs;
+  int32_t rc = CompileQueries(cat, qs, cp, qreqs);
+  if (rc) return rc;
+  const Dict& d = cp.d;
+  const int TW = cp.d.dd.TW, C = cp.C;
+  vector<int64_t> qrq((size_t)std::max<uint32_t>(n, 1) * KP_NRES, 0);
+  for (uint32_t i = 0; i < n; i++)
+    for (int r = 0; r < KP_NRES; r++)
+      qrq[(size_t)i * KP_NRES + r] = (reqs[i].requests.present >> r) & 1 ? reqs[i].requests.milli[r] : 0;
+  // ExoticInstanceTypeFilter's predicate (R:filter.go:295-310): a metal size or accelerator capacity
+  vector<uint64_t> exotic(TW, 0);
+  const string kSize = "karpenter.k8s.aws/instance-size";
+  for (int t = 0; t < T; t++) {
+    const HostType& ht = cat->types[t];
+    bool exo = false;
+    for (auto& r : ht.reqs)
+      if (r.key == kSize && r.op == KP_OP_IN)
+        for (auto& v : r.values)
+          if (v.find("metal") != string::npos) exo = true;
+    for (int r : {KP_RES_NEURON, KP_RES_NEURONCORE, KP_RES_AMD_GPU, KP_RES_NVIDIA_GPU, KP_RES_GAUDI})
+      if (((ht.cap_present >> r) & 1) && ht.cap[r] != 0) exo = true;
+    if (exo) exotic[t / 64] |= 1ull << (t % 64);
+  }
+  // offering classes in each type's offering order; class -> subnet zone; capacity-type class masks
+  int MO = 1;
+  for (auto& t : cat->types) MO = std::max(MO, (int)t.offs.size() + 1);
+  vector<uint8_t> ofs_cls((size_t)T * MO, 0xFF);
+  const int kct = d.key(kCapType), kz = d.key(kZone), kzid = d.key(kZoneID);
+  std::map<ClassKey, int> cls_id;
+  for (int c = 0; c < C; c++) cls_id[ClassKey{cp.classes[c].ct_bit, cp.classes[c].zone_bit, cp.classes[c].zid_bit}] = c;
+  for (int t = 0; t < T; t++) {
+    int j = 0;
+    for (auto& o : cat->types[t].offs) {
+      ClassKey ck{d.bit(kct, o.ct), o.has_zone ? d.bit(kz, o.zone) : -1, o.has_zid ? d.bit(kzid, o.zid) : -1};
+      ofs_cls[(size_t)t * MO + j++] = (uint8_t)cls_id.at(ck);
+    }
+  }
+  const int spot_bit = kct >= 0 ? d.bit(kct, "spot") : -1, od_bit = kct >= 0 ? d.bit(kct, "on-demand") : -1;
+  uint64_t cls_spot = 0, cls_od = 0;
+  vector<int8_t> cls_zone(std::max(C, 1), -1);
+  for (int c = 0; c < C; c++) {
+    if (spot_bit >= 0 && cp.classes[c].ct_bit == spot_bit) cls_spot |= 1ull << c;
+    if (od_bit >= 0 && cp.classes[c].ct_bit == od_bit) cls_od |= 1ull << c;
+    for (uint32_t z = 0; z < n_subnet_zones; z++)
+      if (kz >= 0 && cp.classes[c].zone_bit >= 0 && subnet_zones[z] && d.bit(kz, subnet_zones[z]) == cp.classes[c].zone_bit) {
+        cls_zone[c] = (int8_t)z;
+        break;
+      }
+  }
+  Blob blob;
+  const size_t o_dict = blob.put(&cp.d.dd, 1);
+  const size_t o_vint = blob.put(cp.d.vint);
+  vector<CatOffsets> coffs;
+  PutCatalogs(blob, cp, coffs);
+  const size_t o_cats = blob.reserve(sizeof(DevCatalog));
+  const size_t o_q = blob.put(qreqs);
+  const size_t o_qr = blob.put(qrq);
+  const size_t o_off = blob.put(off);
+  if (list.empty()) list.push_back(0);
+  const size_t o_list = blob.put(list);
+  const size_t o_exo = blob.put(exotic);
+  const size_t o_cz = blob.put(cls_zone);
+  const size_t o_oc = blob.put(ofs_cls);
+  const size_t host_bytes = blob.host.size();
+  const uint32_t ovr_stride = std::max<uint32_t>(1, max_types * std::max<uint32_t>(1, n_subnet_zones));
+  plan->o_out = blob.reserve(sizeof(kp_launch_result) * std::max<uint32_t>(n, 1));
+  plan->o_types = blob.reserve(sizeof(uint32_t) * (size_t)std::max<uint32_t>(n, 1) * max_types);
+  plan->o_ovr = blob.reserve(sizeof(uint32_t) * (size_t)std::max<uint32_t>(n, 1) * ovr_stride);
+  plan->o_stats = blob.reserve(sizeof(uint64_t) * 2);
+  HIPCHK(hipMalloc(&plan->buf.p, blob.host.size()));
+  uint8_t* base = (uint8_t*)plan->buf.p;
+  vector<DevCatalog> dc = DevCats(base, cp, coffs);
+  memcpy(blob.host.data() + o_cats, dc.data(), sizeof(DevCatalog));
+  HIPCHK(hipMemcpyAsync(base, blob.host.data(), host_bytes, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  LaunchArgs& la = plan->la;
+  memset(&la, 0, sizeof la);
+  la.dict = (const DevDict*)(base + o_dict);
+  la.cat = (const DevCatalog*)(base + o_cats);
+  la.vint = (const int64_t*)(base + o_vint);
+  la.n = (int32_t)n;
+  la.max_types = (int32_t)max_types;
+  la.spot_bit = spot_bit;
+  la.od_bit = od_bit;
+  la.ct_key = kct;
+  la.MO = MO;
+  la.cls_spot = cls_spot;
+  la.cls_od = cls_od;
+  la.q_reqs = base + o_q;
+  la.q_requests = (const int64_t*)(base + o_qr);
+  la.list_off = (const uint32_t*)(base + o_off);
+  la.list = (const uint32_t*)(base + o_list);
+  la.exotic = (const uint64_t*)(base + o_exo);
+  la.cls_zone = (const int8_t*)(base + o_cz);
+  la.ofs_cls = base + o_oc;
+  la.ovr_stride = ovr_stride;
+  la.out = (LaunchOut*)(base + plan->o_out);
+  la.out_types = (uint32_t*)(base + plan->o_types);
+  la.out_overrides = (uint32_t*)(base + plan->o_ovr);
+  la.stats = (uint64_t*)(base + plan->o_stats);
+  plan->n = n;
+  plan->max_types = max_types;
+  plan->ovr_stride = ovr_stride;
+  plan->prepare_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  *out = plan.release();
+  return KP_OK;
+}
+
+// One launch over the resident requests; results copied only into the non-NULL buffers (out_types:
+// [n][max_types], out_overrides: [n][max_types * n_subnet_zones]).
+int32_t kp_launch_run(kp_launch_plan* plan, kp_launch_result* out, uint32_t* out_types, uint32_t* out_overrides,
+                      kp_solve_stats* stats) {
+  auto t0 = std::chrono::steady_clock::now();
+  if (!plan) return fail(KP_E_INVAL, "null argument");
+  kp_ctx* ctx = plan->ctx;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device));
+  uint8_t* base = (uint8_t*)plan->buf.p;
+  const uint32_t n = plan->n;
+  HIPCHK(hipMemsetAsync(base + plan->o_stats, 0, sizeof(uint64_t) * 2, ctx->stream));
+  HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
+  if (n) HIPCHK(launch_launch(plan->la, ctx->stream));
+  HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));
+  uint64_t st[2] = {0, 0};
+  HIPCHK(hipMemcpyAsync(st, base + plan->o_stats, sizeof st, hipMemcpyDeviceToHost, ctx->stream));
+  if (n && out) HIPCHK(hipMemcpyAsync(out, base + plan->o_out, sizeof(kp_launch_result) * n, hipMemcpyDeviceToHost, ctx->stream));
+  if (n && out_types)
+    HIPCHK(hipMemcpyAsync(out_types, base + plan->o_types, sizeof(uint32_t) * (size_t)n * plan->max_types,
+                          hipMemcpyDeviceToHost, ctx->stream));
+  if (n && out_overrides)
+    HIPCHK(hipMemcpyAsync(out_overrides, base + plan->o_ovr, sizeof(uint32_t) * (size_t)n * plan->ovr_stride,
+                          hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+  if (stats) {
+    memset(stats, 0, sizeof *stats);
+    stats->device_ms = ms;
+    stats->attempts = st[0];           // (request, listed type) pairs evaluated
+    stats->bytes_algorithmic = st[1];
+    stats->prepare_ms = plan->prepare_ms;
+    stats->host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
+  return KP_OK;
+}
+
+void kp_launch_plan_destroy(kp_launch_plan* p) {
+  if (!p) return;
+  (void)hipSetDevice(p->ctx->device);
+  delete p;
+}
+
+int32_t kp_launch_select(kp_ctx* ctx, const kp_catalog* cat, const kp_launch_request* reqs, uint32_t n,
+                         const char* const* subnet_zones, uint32_t n_subnet_zones, uint32_t max_types,
+                         kp_launch_result* out, uint32_t* out_types, uint32_t* out_overrides, kp_solve_stats* stats) {
+  if (!out) return fail(KP_E_INVAL, "null argument");
+  kp_launch_plan* plan = nullptr;
+  int32_t rc = kp_launch_prepare(ctx, cat, reqs, n, subnet_zones, n_subnet_zones, max_types, &plan);
+  if (rc) return rc;
+  rc = kp_launch_run(plan, out, out_types, out_overrides, stats);
+  kp_launch_plan_destroy(plan);
   return rc;
 }
 

@@ -16,6 +16,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include "kp/kp_abi.h"
 #include "kp_device.h"
 #include "kp_model.h"
 
@@ -1606,6 +1607,304 @@ __global__ __launch_bounds__(FEAS_WAVES * 64) void feasibility_kernel(FeasArgs a
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// launch_kernel: instance.DefaultProvider.Create's launch-side selection (R:pkg/providers/instance/instance.go:
+// 117-125, 242-270, 336-355, 392-439, 504-518), one wave per NodeClaim request. Lane = list entry: the
+// CompatibleAvailable test and the cheapest compatible available prices per capacity type are one pass over the
+// list; the exotic and spot filters are wave reductions + an ordered compaction in LDS; Truncate is a bitonic sort
+// by (price, name) of the survivors; overrides are a wave prefix sum over the truncated entries.
+// ------------------------------------------------------------------------------------------------
+#define LAUNCH_WAVES 4
+struct LaunchWaveLds {
+  uint64_t allowed[KP_MAX_WORDS];
+  uint64_t key[LAUNCH_CAP];  // cheapest available compatible price (bits; non-negative doubles order as integers)
+  uint32_t val[LAUNCH_CAP];  // name rank << 12 | type, bit 31: exotic
+  uint64_t xm[KP_MAX_TYPE_WORDS];
+  uint32_t scratch[2 * KP_MAX_WORDS];
+};
+#define LV_ORDER(v) ((v) & 0x00FFFFFFu)
+
+// ordered compaction of the m entries in L.key/L.val keeping those whose keep() is true; returns the new count
+template <class Keep>
+__device__ int launch_compact(LaunchWaveLds& L, int m, Keep keep) {
+  const int lane = LANE;
+  int out = 0;
+  for (int base = 0; base < m; base += 64) {
+    const int i = base + lane;
+    uint64_t k = 0;
+    uint32_t v = 0;
+    bool kp = false;
+    if (i < m) {
+      k = L.key[i];
+      v = L.val[i];
+      kp = keep(k, v);
+    }
+    const uint64_t bal = __ballot(kp);
+    wave_sync();
+    if (kp) {
+      const int pos = out + __builtin_popcountll(bal & ((1ull << lane) - 1));
+      L.key[pos] = k;
+      L.val[pos] = v;
+    }
+    out += __builtin_popcountll(bal);
+    wave_sync();
+  }
+  return out;
+}
+
+__global__ __launch_bounds__(LAUNCH_WAVES * 64) void launch_kernel(LaunchArgs a) {
+  __shared__ DevDict D;
+  __shared__ LaunchWaveLds Wl[LAUNCH_WAVES];
+  if (threadIdx.x == 0) D = *a.dict;
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = LANE;
+  const DevCatalog& Cg = *a.cat;
+  LaunchWaveLds& L = Wl[wave];
+  const double INF = __builtin_huge_val();
+  uint64_t evals = 0, bytes = 0;
+  for (long q = (long)blockIdx.x * LAUNCH_WAVES + wave; q < a.n; q += (long)gridDim.x * LAUNCH_WAVES) {
+    const KReqs* Q = reinterpret_cast<const KReqs*>(a.q_reqs + (size_t)q * sizeof(KReqs));
+    const uint64_t v = lane < D.W ? Q->vals[lane] : 0;
+    ReqView rv;
+    rv.present = Q->present;
+    rv.compl_ = Q->compl_ & Q->present;
+    rv.hgt = Q->hgt;
+    rv.hlt = Q->hlt;
+    rv.hmin = Q->hmin;
+    rv.nz = nz_keys(D, v);
+    rv.dne = 0;
+    rv.gt = Q->gt;
+    rv.lt = Q->lt;
+    rv.minv = Q->minv;
+    const uint64_t negQ = negop_mask(rv.present, rv.compl_, rv.nz);
+    const uint64_t allowed = allowed_word(D, rv, v, vint_global(a.vint));
+    const uint64_t cls = allowed_classes(D, Cg.cls, rv, allowed, negQ);
+    // the same with the capacity-type key opened: getCapacityType / getOverrides pin it to one value
+    const bool ctw = a.ct_key >= 0 && lane < D.W && D.wkey[lane] == a.ct_key;
+    const uint64_t cls_noct = allowed_classes(D, Cg.cls, rv, ctw ? D.validbits[lane] : allowed, negQ);
+    L.allowed[lane] = allowed;
+    const int64_t rq_lane = lane < KP_NRES ? a.q_requests[(size_t)q * KP_NRES + lane] : 0;
+    const uint32_t rmask = (uint32_t)__ballot(rq_lane > 0);
+    const bool hasMin = (rv.hmin & rv.present) != 0;
+    // Requirements.Get(capacity-type).Has(x): an absent key is Exists
+    const bool ct_present = a.ct_key >= 0 && ((rv.present >> a.ct_key) & 1);
+    const bool ct_compl = ct_present && ((rv.compl_ >> a.ct_key) & 1);
+    const bool has_spot = a.spot_bit >= 0 ? bit_of(allowed, a.spot_bit) : (!ct_present || ct_compl);
+    const bool has_od = a.od_bit >= 0 ? bit_of(allowed, a.od_bit) : (!ct_present || ct_compl);
+    wave_sync();
+    const int lb = (int)a.list_off[q], ln = (int)(a.list_off[q + 1] - lb);
+    const uint64_t keys0 = rv.present & D.catalog_keys;
+    LaunchOut res;
+    res.status = KP_LAUNCH_OK;
+    res.capacity_type = 0;
+    res.n_types = 0;
+    res.n_overrides = 0;
+    res.failed_filter = -1;
+    res.rejected_exotic = 0;
+    res.rejected_spot = 0;
+    res.od_fallback_warning = 0;
+    res.pad_ = 0;
+    // ---- CompatibleAvailableFilter (R:filter.go:51-63) -----------------------------------------------
+    int m = 0, n_generic = 0;
+    for (int base = 0; base < ln; base += 64) {
+      const int i = base + lane;
+      bool keep = false, exo = false;
+      double cheapest = INF;
+      int t = 0;
+      if (i < ln) {
+        t = (int)a.list[lb + i];
+        keep = true;
+        if (Cg.custom_nonneg[t] & ~rv.present) keep = false;  // Compatible(part a): undefined custom keys
+        uint64_t keys = keys0;
+        while (keep && keys) {  // Intersects over the keys both define
+          const int k = __builtin_ctzll(keys);
+          keys &= keys - 1;
+          const uint16_t code = Cg.code[(size_t)k * D.T + t];
+          if (code == 0xFFFF) continue;
+          if (code == 0xFFFE) keep = (negQ >> k) & 1;
+          else if (code == 0xFFFD) keep = (L.allowed[D.wofs[k]] & Cg.multi[(size_t)k * D.T + t]) != 0;
+          else keep = (L.allowed[code >> 6] >> (code & 63)) & 1;
+        }
+        if (keep && !((Cg.nonneg[t >> 6] >> (t & 63)) & 1)) keep = false;  // Fits: negative totals never fit
+        uint32_t rm = rmask;
+        while (keep && rm) {
+          const int r = __builtin_ctz(rm);
+          rm &= rm - 1;
+          if (lane_bcast_i64(rq_lane, r) > Cg.alloc[(size_t)r * D.T + t]) keep = false;
+        }
+        for (uint64_t mm = cls; mm; mm &= mm - 1) {
+          const double p = Cg.price[(size_t)t * D.C + __builtin_ctzll(mm)];
+          cheapest = p < cheapest ? p : cheapest;
+        }
+        if (!(cheapest < INF)) keep = false;
+        exo = (a.exotic[t >> 6] >> (t & 63)) & 1;
+      }
+      const uint64_t bal = __ballot(keep);
+      if (keep) {
+        const int pos = m + __builtin_popcountll(bal & ((1ull << lane) - 1));
+        L.key[pos] = (uint64_t)__double_as_longlong(cheapest);
+        L.val[pos] = (Cg.name_rank[t] << 12) | (uint32_t)t | (exo ? 0x80000000u : 0u);
+      }
+      m += __builtin_popcountll(bal);
+      n_generic += __builtin_popcountll(__ballot(keep && !exo));
+    }
+    evals += ln;
+    bytes += (uint64_t)ln * (2 * __builtin_popcountll(keys0) + 8 * __builtin_popcount(rmask) + 8 * __builtin_popcountll(cls) + 16);
+    wave_sync();
+    res.n_compatible = (uint32_t)m;
+    if (m == 0) {
+      res.status = KP_LAUNCH_INSUFFICIENT_CAPACITY;
+      res.failed_filter = KP_FILTER_COMPATIBLE_AVAILABLE;
+    }
+    // ---- ExoticInstanceTypeFilter (R:filter.go:289-314) -------------------------------------------------
+    if (m && !hasMin && n_generic > 0 && n_generic < m) {
+      res.rejected_exotic = (uint32_t)(m - n_generic);
+      m = launch_compact(L, m, [](uint64_t, uint32_t vv) { return !(vv & 0x80000000u); });
+    }
+    // ---- SpotInstanceFilter (R:filter.go:342-382) ---------------------------------------------------------
+    if (m && !hasMin && has_od && has_spot) {
+      double od_min = INF;
+      bool any_spot = false;
+      for (int base = 0; base < m; base += 64) {
+        const int i = base + lane;
+        if (i < m) {
+          const int t = (int)(L.val[i] & 4095u);
+          for (uint64_t mm = cls & a.cls_od; mm; mm &= mm - 1) {
+            const double p = Cg.price[(size_t)t * D.C + __builtin_ctzll(mm)];
+            od_min = p < od_min ? p : od_min;
+          }
+          for (uint64_t mm = cls & a.cls_spot; mm; mm &= mm - 1)
+            if (Cg.price[(size_t)t * D.C + __builtin_ctzll(mm)] < INF) any_spot = true;
+        }
+      }
+      for (int o = 32; o >= 1; o >>= 1) {
+        const double w = __shfl_xor(od_min, o, 64);
+        od_min = w < od_min ? w : od_min;
+      }
+      any_spot = __ballot(any_spot) != 0;
+      if (od_min < INF && any_spot) {
+        const uint64_t spot_cls = cls & a.cls_spot;
+        const int m0 = m;
+        m = launch_compact(L, m, [&](uint64_t, uint32_t vv) {
+          const int t = (int)(vv & 4095u);
+          bool has = false, cheap = false;
+          for (uint64_t mm = spot_cls; mm; mm &= mm - 1) {
+            const double p = Cg.price[(size_t)t * D.C + __builtin_ctzll(mm)];
+            if (p < INF) {
+              has = true;
+              if (p <= od_min) cheap = true;
+            }
+          }
+          return cheap || !has;
+        });
+        res.rejected_spot = (uint32_t)(m0 - m);
+        if (m == 0) {
+          res.status = KP_LAUNCH_INSUFFICIENT_CAPACITY;
+          res.failed_filter = KP_FILTER_SPOT;
+        }
+      }
+    }
+    if (m) {
+      // ---- Truncate(reqs, max): OrderByPrice (price asc, name asc), cut, SatisfiesMinValues ----------------
+      int m2 = 1;
+      while (m2 < m) m2 <<= 1;
+      for (int i = m + lane; i < m2; i += 64) {
+        L.key[i] = ~0ull;
+        L.val[i] = 0x00FFFFFFu;
+      }
+      wave_sync();
+      for (int k = 2; k <= m2; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+          for (int i = lane; i < m2; i += 64) {
+            const int ixj = i ^ j;
+            if (ixj > i) {
+              const uint64_t ki = L.key[i], kj = L.key[ixj];
+              const uint32_t vi = L.val[i], vj = L.val[ixj];
+              const bool gt = ki > kj || (ki == kj && LV_ORDER(vi) > LV_ORDER(vj));
+              if (gt == ((i & k) == 0)) {
+                L.key[i] = kj;
+                L.key[ixj] = ki;
+                L.val[i] = vj;
+                L.val[ixj] = vi;
+              }
+            }
+          }
+          wave_sync();
+        }
+      }
+      const int cut = a.max_types ? min(m, a.max_types) : m;
+      bool min_ok = true;
+      if (hasMin) {
+        L.xm[lane] = 0;
+        wave_sync();
+        for (int i = lane; i < cut; i += 64) {
+          const int t = (int)(L.val[i] & 4095u);
+          atomicOr((unsigned long long*)&L.xm[t >> 6], 1ull << (t & 63));
+        }
+        wave_sync();
+        min_ok = minvalues_ok(D, Cg.code, Cg.TM, rv.hmin & rv.present, rv.minv, lane < D.TW ? L.xm[lane] : 0,
+                              L.scratch);
+      }
+      if (!min_ok) {
+        res.status = KP_LAUNCH_MINVALUES;
+      } else {
+        // ---- getCapacityType (R:instance.go:504-518) + checkODFallback (:336-355) -------------------------
+        const uint64_t spot_any_cls = cls_noct & a.cls_spot;
+        bool spot_ok = false;
+        if (has_spot)
+          for (int i = lane; i < cut; i += 64) {
+            const int t = (int)(L.val[i] & 4095u);
+            for (uint64_t mm = spot_any_cls; mm; mm &= mm - 1)
+              if (Cg.price[(size_t)t * D.C + __builtin_ctzll(mm)] < INF) spot_ok = true;
+          }
+        const bool ct_spot = has_spot && __ballot(spot_ok) != 0;
+        res.capacity_type = ct_spot ? 1 : 0;
+        res.od_fallback_warning = (!ct_spot && has_spot && cut < 5) ? 1 : 0;
+        // ---- getOverrides (R:instance.go:392-439) with the capacity type pinned -----------------------------
+        const uint64_t cls3 = cls_noct & (ct_spot ? a.cls_spot : a.cls_od);
+        uint32_t* ot = a.out_types + (size_t)q * a.max_types;
+        uint32_t* oo = a.out_overrides + (size_t)q * a.ovr_stride;
+        int novr = 0;
+        for (int base = 0; base < cut; base += 64) {
+          const int i = base + lane;
+          int t = 0, cnt = 0;
+          if (i < cut) {
+            t = (int)(L.val[i] & 4095u);
+            ot[i] = (uint32_t)t;
+            for (int j = 0; j < a.MO; j++) {
+              const int c = a.ofs_cls[(size_t)t * a.MO + j];
+              if (c == 0xFF) break;
+              if (((cls3 >> c) & 1) && Cg.price[(size_t)t * D.C + c] < INF && a.cls_zone[c] >= 0) cnt++;
+            }
+          }
+          int incl = cnt;  // inclusive wave scan
+          for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+          }
+          int pos = novr + incl - cnt;
+          if (i < cut)
+            for (int j = 0; j < a.MO; j++) {
+              const int c = a.ofs_cls[(size_t)t * a.MO + j];
+              if (c == 0xFF) break;
+              if (((cls3 >> c) & 1) && Cg.price[(size_t)t * D.C + c] < INF && a.cls_zone[c] >= 0)
+                oo[pos++] = ((uint32_t)t << 8) | (uint32_t)a.cls_zone[c];
+            }
+          novr += __shfl(incl, 63, 64);
+        }
+        res.n_types = (uint32_t)cut;
+        res.n_overrides = (uint32_t)novr;
+      }
+    }
+    if (lane == 0) a.out[q] = res;
+    wave_sync();
+  }
+  if (lane == 0) {
+    atomicAdd((unsigned long long*)&a.stats[0], (unsigned long long)evals);
+    atomicAdd((unsigned long long*)&a.stats[1], (unsigned long long)bytes);
+  }
+}
+
 #include "kp_sim.hip"
 
 // ------------------------------------------------------------------------------------------------
@@ -1628,6 +1927,13 @@ hipError_t launch_solve(const SolveArgs& a, int nw, size_t dyn_lds, hipStream_t 
 hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s) {
   if (a.n_nc == 0) return hipSuccess;
   hipLaunchKernelGGL(finalize_kernel, dim3(a.n_nc), dim3(FIN_THREADS), 0, s, a);
+  return hipGetLastError();
+}
+hipError_t launch_launch(const LaunchArgs& a, hipStream_t s) {
+  long blocks = ((long)a.n + LAUNCH_WAVES - 1) / LAUNCH_WAVES;
+  if (blocks > 65536) blocks = 65536;
+  if (blocks < 1) return hipSuccess;
+  hipLaunchKernelGGL(launch_kernel, dim3((unsigned)blocks), dim3(LAUNCH_WAVES * 64), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_feasibility(const FeasArgs& a, hipStream_t s) {

@@ -29,10 +29,6 @@
 // NotIn/DoesNotExist requirement on a key some node lacks (then ExistingNode requirements can grow a key
 // and CanAdd is no longer a function of the snapshot).
 
-#define KP_DECISION_NOOP 0
-#define KP_DECISION_DELETE 1
-#define KP_DECISION_REPLACE 2
-
 __device__ __forceinline__ void sim_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   __builtin_amdgcn_wave_barrier();

@@ -51,6 +51,14 @@ def load_lib(path=LIB_PATH):
                                           P(C.c_void_p)]),
         "kp_filter_run": (C.c_int32, [C.c_void_p, P(C.c_uint64), P(C.c_double), P(abi.SolveStats)]),
         "kp_filter_plan_destroy": (None, [C.c_void_p]),
+        "kp_launch_prepare": (C.c_int32, [C.c_void_p, C.c_void_p, P(abi.LaunchRequest), C.c_uint32, P(C.c_char_p),
+                                          C.c_uint32, C.c_uint32, P(C.c_void_p)]),
+        "kp_launch_run": (C.c_int32, [C.c_void_p, P(abi.LaunchResult), P(C.c_uint32), P(C.c_uint32),
+                                      P(abi.SolveStats)]),
+        "kp_launch_plan_destroy": (None, [C.c_void_p]),
+        "kp_launch_select": (C.c_int32, [C.c_void_p, C.c_void_p, P(abi.LaunchRequest), C.c_uint32, P(C.c_char_p),
+                                         C.c_uint32, C.c_uint32, P(abi.LaunchResult), P(C.c_uint32), P(C.c_uint32),
+                                         P(abi.SolveStats)]),
         "kp_solve": (C.c_int32, [C.c_void_p, P(abi.SolveIn), P(C.c_void_p)]),
         "kp_solve_validate": (C.c_int32, [P(abi.SolveIn)]),
         "kp_solve_prepare": (C.c_int32, [C.c_void_p, P(abi.SolveIn), P(C.c_void_p)]),
@@ -161,6 +169,7 @@ def read_result(lib, res, n_pods, prefix="kp_result_"):
             "options": [int(info.options[j]) for j in range(info.n_options)],
             "n_remaining": int(info.n_remaining),
             "requirements": abi.read_requirements(info.requirements),
+            "requests": abi.read_resources(info.requests),
         })
     st = abi.SolveStats()
     get("stats")(res, C.byref(st))
@@ -297,6 +306,64 @@ class FilterPlan:
             self.close()
         except Exception:
             pass
+
+
+MAX_LAUNCH_TYPES = 60  # maxInstanceTypes (R:pkg/providers/instance/instance.go:60)
+
+
+class LaunchPlan:
+    """kp_launch_prepare / kp_launch_run: instance.DefaultProvider.Create's launch-side selection for a batch of
+    NodeClaims (filters, Truncate, capacity type, CreateFleet overrides), requests resident on the device.
+    requests: [(requirements, requests, [catalogue indices])]; subnet_zones: zones with a launch subnet."""
+
+    def __init__(self, ctx, catalog, requests, subnet_zones, max_types=MAX_LAUNCH_TYPES):
+        self.ctx = ctx
+        self.n = len(requests)
+        self.zones = list(subnet_zones)
+        self.max_types = max_types
+        arena = Arena()
+        rq = abi.launch_requests(arena, requests)
+        zs = arena.arr(C.c_char_p, [z.encode() for z in self.zones])
+        h = C.c_void_p()
+        _check(ctx.lib, ctx.lib.kp_launch_prepare(ctx.h, catalog.h, rq, self.n, zs, len(self.zones), max_types,
+                                                  C.byref(h)))
+        self.h = h
+
+    def run(self, read=True):
+        """One launch; read=True returns ([result dict per request], stats), else (None, stats)."""
+        st = abi.SolveStats()
+        lib = self.ctx.lib
+        if not read:
+            _check(lib, lib.kp_launch_run(self.h, None, None, None, C.byref(st)))
+            return None, stats_dict(st)
+        out = (abi.LaunchResult * max(1, self.n))()
+        stride = self.max_types * max(1, len(self.zones))
+        types = np.zeros(max(1, self.n * self.max_types), dtype=np.uint32)
+        ovr = np.zeros(max(1, self.n * stride), dtype=np.uint32)
+        _check(lib, lib.kp_launch_run(self.h, out, types.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                      ovr.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(st)))
+        res = [abi.launch_result_dict(out[i], types[i * self.max_types:(i + 1) * self.max_types],
+                                      ovr[i * stride:(i + 1) * stride], self.zones) for i in range(self.n)]
+        return res, stats_dict(st)
+
+    def close(self):
+        if self.h:
+            self.ctx.lib.kp_launch_plan_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def launch_requests_from_solve(result):
+    """One launch request per NodeClaim of a Solve result: its final requirements, requests and options."""
+    reqs = []
+    for n in result["nodeclaims"]:
+        reqs.append((n["requirements"], n["requests"], n["options"]))
+    return reqs
 
 
 def pod_queries(problem):

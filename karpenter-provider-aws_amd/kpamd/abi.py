@@ -19,6 +19,11 @@ OPS = {"In": 0, "NotIn": 1, "Exists": 2, "DoesNotExist": 3, "Gt": 4, "Lt": 5}
 OP_NAMES = {v: k for k, v in OPS.items()}
 
 
+def read_resources(r):
+    """kp_resource_list -> {name: milli} (present entries only)"""
+    return {RES_NAMES[i]: int(r.milli[i]) for i in range(NUM_RES) if (r.present >> i) & 1}
+
+
 def read_requirements(r):
     """kp_requirements -> [(key, op, [values], minValues|None)]"""
     out = []
@@ -27,6 +32,8 @@ def read_requirements(r):
         vals = [q.values[j].decode() for j in range(q.n_values)]
         out.append((q.key.decode(), OP_NAMES[q.op], vals, None if q.min_values < 0 else int(q.min_values)))
     return out
+
+
 EFFECTS = {"": 0, "NoSchedule": 1, "PreferNoSchedule": 2, "NoExecute": 3}
 TOL_OPS = {"Equal": 0, "": 0, "Exists": 1}
 
@@ -194,6 +201,36 @@ class SimResult(C.Structure):
 
 class FeasibilityQuery(C.Structure):
     _fields_ = [("requirements", Requirements), ("requests", ResourceList)]
+
+
+class LaunchRequest(C.Structure):
+    _fields_ = [("requirements", Requirements), ("requests", ResourceList),
+                ("instance_types", C.POINTER(C.c_uint32)), ("n_instance_types", C.c_uint32), ("reserved_", C.c_uint32)]
+
+
+class LaunchResult(C.Structure):
+    _fields_ = [("status", C.c_int32), ("capacity_type", C.c_int32), ("n_types", C.c_uint32),
+                ("n_overrides", C.c_uint32), ("failed_filter", C.c_int32), ("n_compatible", C.c_uint32),
+                ("rejected_exotic", C.c_uint32), ("rejected_spot", C.c_uint32), ("od_fallback_warning", C.c_int32),
+                ("reserved_", C.c_int32)]
+
+
+def launch_requests(arena, requests):
+    """[(requirements, requests, [catalogue indices])] -> LaunchRequest array (buffers kept by the arena)."""
+    out = []
+    for reqs, res, types in requests:
+        lst = arena.arr(C.c_uint32, [int(t) for t in types]) if len(types) else None
+        out.append(LaunchRequest(arena.requirements(reqs), arena.resources(res), lst, len(types), 0))
+    return arena.arr(LaunchRequest, out)
+
+
+def launch_result_dict(r, types, ovr, zones):
+    return {"status": int(r.status), "capacity_type": "spot" if r.capacity_type == 1 else "on-demand",
+            "types": [int(t) for t in types[:r.n_types]] if r.status == 0 else [],
+            "overrides": [(int(o) >> 8, zones[int(o) & 0xFF]) for o in ovr[:r.n_overrides]] if r.status == 0 else [],
+            "failed_filter": int(r.failed_filter), "n_compatible": int(r.n_compatible),
+            "rejected_exotic": int(r.rejected_exotic), "rejected_spot": int(r.rejected_spot),
+            "od_fallback_warning": bool(r.od_fallback_warning)}
 
 
 # ------------------------------------------------------------------------------------------------

@@ -540,3 +540,69 @@ def random_cluster(catalog, seed, n_nodes=60, n_types=80, n_shapes=16, n_pools=2
     return Cluster([cat], pools, nodes, shapes, np.asarray(pod_shape, dtype=np.uint32),
                    np.asarray(pod_creation, dtype=np.int64), np.asarray(pod_uid, dtype=np.uint64),
                    candidates=cands, name=f"random-cluster-{seed}")
+
+
+# ------------------------------------------------------------------------------------------------
+# launch-side selection (instance.DefaultProvider.Create) requests
+# ------------------------------------------------------------------------------------------------
+def single_pod_problem(catalog, pool_reqs, requests, name="single-pod"):
+    """One pending pod on one NodePool (the reference's launch tests: R:pkg/providers/instancetype/suite_test.go)."""
+    rng = np.random.default_rng(0)
+    s, c, u = _pods(rng, 1, 1)
+    return Problem([catalog], [NodePool("default", 0, 0, list(pool_reqs))], [PodShape(dict(requests))], s, c, u,
+                   name=name)
+
+
+def random_launch_requests(catalog, n, seed):
+    """n random launch requests: NodeClaim-like requirements (capacity type, zones, categories, cpu bounds, arch,
+    minValues, GPU manufacturer), requests and instance-type lists (random subsets, the whole catalogue, empty)."""
+    rng = np.random.default_rng(seed)
+    T = len(catalog)
+    fams = sorted({r[2][0] for it in catalog for r in it.requirements if r[0] == K + "instance-family" and r[2]})
+    out = []
+    for _ in range(n):
+        reqs = []
+        k = rng.random()
+        if k < 0.25:
+            reqs.append(("karpenter.sh/capacity-type", "In", ["spot", "on-demand"]))
+        elif k < 0.45:
+            reqs.append(("karpenter.sh/capacity-type", "In", ["on-demand"]))
+        elif k < 0.6:
+            reqs.append(("karpenter.sh/capacity-type", "In", ["spot"]))
+        elif k < 0.65:
+            reqs.append(("karpenter.sh/capacity-type", "NotIn", ["spot"]))
+        if rng.random() < 0.3:
+            reqs.append(("topology.kubernetes.io/zone", "In", list(rng.choice(ZONES, size=int(rng.integers(1, 3)), replace=False))))
+        elif rng.random() < 0.1:
+            reqs.append(("topology.kubernetes.io/zone", "NotIn", [str(rng.choice(ZONES))]))
+        if rng.random() < 0.3:
+            reqs.append((K + "instance-category", "In", list(rng.choice(["c", "m", "r", "g", "p", "t", "x", "i"],
+                                                                       size=int(rng.integers(1, 4)), replace=False))))
+        if rng.random() < 0.2:
+            reqs.append((K + "instance-cpu", "Gt", [str(int(rng.choice([1, 3, 7, 15])))]))
+        if rng.random() < 0.15:
+            reqs.append((K + "instance-cpu", "Lt", [str(int(rng.choice([8, 17, 33, 97])))]))
+        if rng.random() < 0.3:
+            reqs.append(("kubernetes.io/arch", "In", [str(rng.choice(["amd64", "arm64"]))]))
+        if rng.random() < 0.1:
+            reqs.append((K + "instance-gpu-manufacturer", "In", ["nvidia"]))
+        if rng.random() < 0.1 and fams:
+            reqs.append((K + "instance-family", "In" if rng.random() < 0.7 else "NotIn",
+                         list(rng.choice(fams, size=min(len(fams), int(rng.integers(2, 12))), replace=False)),
+                         int(rng.integers(1, 5)) if rng.random() < 0.7 else None))
+        if rng.random() < 0.05:
+            reqs.append((K + "instance-size", "Exists", [], 2))
+        res = req_res(int(rng.choice(CPU_GRID + [8000, 16000])), int(rng.choice(MEM_GRID + [32768])))
+        if any(r[0] == K + "instance-gpu-manufacturer" for r in reqs) and rng.random() < 0.5:
+            res["nvidia.com/gpu"] = 1000
+        u = rng.random()
+        if u < 0.05:
+            lst = []
+        elif u < 0.15:
+            lst = list(range(T))
+        else:
+            lst = sorted(rng.choice(T, size=int(rng.integers(1, min(T, 300))), replace=False).tolist())
+            if rng.random() < 0.5:
+                rng.shuffle(lst)
+        out.append((reqs, res, [int(t) for t in lst]))
+    return out

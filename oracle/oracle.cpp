@@ -1713,8 +1713,9 @@ int32_t kpo_filter_spot(const kp_catalog_desc* cat, const kp_requirements* req, 
   Requirements reqs = FromABI(*req);
   for (size_t t = 0; t < types->size(); t++) out_kept[t] = 1;
   if (HasMinValues(reqs)) return KP_OK;
+  // Requirements.Get(key) of an absent key is Exists: Has() every value
   auto ct = reqs.find(kLabelCapacityType);
-  if (ct == reqs.end() || !Has(ct->second, "on-demand") || !Has(ct->second, "spot")) return KP_OK;
+  if (ct != reqs.end() && (!Has(ct->second, "on-demand") || !Has(ct->second, "spot"))) return KP_OK;
   double cheapestOD = std::numeric_limits<double>::max();
   bool hasSpot = false, hasOD = false;
   auto capType = [](const Offering& o) { return *o.reqs.at(kLabelCapacityType).values.begin(); };
@@ -1775,6 +1776,152 @@ int32_t kpo_filter_exotic(const kp_catalog_desc* cat, const kp_requirements* req
   }
   if (ng == 0) return KP_OK;
   for (size_t t = 0; t < n; t++) out_kept[t] = generic[t];
+  return KP_OK;
+}
+
+// ---- launch-side selection: instance.DefaultProvider.Create (R:pkg/providers/instance/instance.go:117-125) ----
+// Requirements.Get(key).Has(v): an absent key is Exists (every value).
+static bool ReqHas(const Requirements& r, const string& key, const string& v) {
+  auto f = r.find(key);
+  return f == r.end() || Has(f->second, v);
+}
+static string OfferingCapType(const Offering& o) { return *o.reqs.at(kLabelCapacityType).values.begin(); }
+static string OfferingZone(const Offering& o) {
+  auto f = o.reqs.find(kLabelZone);
+  return f == o.reqs.end() || f->second.values.empty() ? string() : *f->second.values.begin();
+}
+static bool IsExotic(const InstanceType& it) {  // R:filter.go:295-310
+  auto sz = it.reqs.find(AWSL("instance-size"));
+  if (sz != it.reqs.end() && !sz->second.complement)
+    for (auto& v : sz->second.values)
+      if (v.find("metal") != std::string::npos) return true;
+  for (int r : {KP_RES_NEURON, KP_RES_NEURONCORE, KP_RES_AMD_GPU, KP_RES_NVIDIA_GPU, KP_RES_GAUDI})
+    if (Get(it.capacity, r) != 0) return true;
+  return false;
+}
+
+// filterInstanceTypes (R:instance.go:242-270) + getCapacityType (:504-518) + checkODFallback (:336-355) +
+// getOverrides (:392-439) for one NodeClaim; reserved offerings are not representable in ABI v2, so the three
+// reservation filters (R:filter.go:66-274) are no-ops (each returns its input when no reserved offering exists).
+int32_t kpo_launch_select(const kp_catalog_desc* cat, const kp_launch_request* req, const char* const* zones,
+                          uint32_t n_zones, uint32_t max_types, kp_launch_result* out, uint32_t* out_types,
+                          uint32_t* out_overrides) {
+  auto types = CatalogFromABI(*cat);
+  const vector<InstanceType>& C = *types;
+  Requirements reqs = FromABI(req->requirements);
+  ResourceList requests = FromABI(req->requests);
+  *out = kp_launch_result{};
+  out->failed_filter = -1;
+  vector<int> its;
+  for (uint32_t i = 0; i < req->n_instance_types; i++) {
+    if (req->instance_types[i] >= C.size()) return KP_E_INVAL;
+    its.push_back((int)req->instance_types[i]);
+  }
+  // CompatibleAvailableFilter (R:filter.go:51-63)
+  vector<int> kept;
+  for (int t : its)
+    if (Compatible(reqs, C[t].reqs, true) && Fits(requests, C[t].allocatable) && HasCompatibleAvailable(C[t], reqs))
+      kept.push_back(t);
+  out->n_compatible = (uint32_t)kept.size();
+  if (kept.empty()) {
+    out->status = KP_LAUNCH_INSUFFICIENT_CAPACITY;
+    out->failed_filter = KP_FILTER_COMPATIBLE_AVAILABLE;
+    return KP_OK;
+  }
+  its = kept;
+  const bool hasMin = HasMinValues(reqs);
+  // ExoticInstanceTypeFilter (R:filter.go:289-314): keep the generic types if any
+  if (!hasMin) {
+    vector<int> generic;
+    for (int t : its)
+      if (!IsExotic(C[t])) generic.push_back(t);
+    if (!generic.empty()) {
+      out->rejected_exotic = (uint32_t)(its.size() - generic.size());
+      its = generic;
+    }
+  }
+  // SpotInstanceFilter (R:filter.go:342-382)
+  if (!hasMin && ReqHas(reqs, kLabelCapacityType, "on-demand") && ReqHas(reqs, kLabelCapacityType, "spot")) {
+    double cheapestOD = std::numeric_limits<double>::max();
+    bool hasSpot = false, hasOD = false;
+    for (int t : its)
+      for (auto& o : C[t].offerings) {
+        if (!Compatible(reqs, o.reqs, true) || !o.available) continue;
+        const string c = OfferingCapType(o);
+        if (c == "on-demand") {
+          hasOD = true;
+          if (o.price < cheapestOD) cheapestOD = o.price;
+        } else if (c == "spot") {
+          hasSpot = true;
+        }
+      }
+    if (hasOD && hasSpot) {
+      vector<int> k2;
+      for (int t : its) {
+        bool hasSpotOffering = false, keep = false;
+        for (auto& o : C[t].offerings) {
+          if (!Compatible(reqs, o.reqs, true) || !o.available) continue;
+          if (OfferingCapType(o) == "spot") {
+            hasSpotOffering = true;
+            if (o.price <= cheapestOD) {
+              keep = true;
+              break;
+            }
+          }
+        }
+        if (keep || !hasSpotOffering) k2.push_back(t);
+      }
+      out->rejected_spot = (uint32_t)(its.size() - k2.size());
+      if (k2.empty()) {
+        out->status = KP_LAUNCH_INSUFFICIENT_CAPACITY;
+        out->failed_filter = KP_FILTER_SPOT;
+        return KP_OK;
+      }
+      its = k2;
+    }
+  }
+  // InstanceTypes.Truncate(reqs, maxInstanceTypes): OrderByPrice (cheapest available compatible, then name)
+  std::sort(its.begin(), its.end(), [&](int a, int b) {
+    const double pa = CheapestPrice(C[a], reqs), pb = CheapestPrice(C[b], reqs);
+    if (pa != pb) return pa < pb;
+    return C[a].name < C[b].name;
+  });
+  if (max_types && its.size() > max_types) its.resize(max_types);
+  if (hasMin && !SatisfiesMinValues(C, its, reqs)) {
+    out->status = KP_LAUNCH_MINVALUES;
+    return KP_OK;
+  }
+  // getCapacityType: reserved (never: no reserved offerings), then spot
+  int ct = 0;
+  if (ReqHas(reqs, kLabelCapacityType, "spot")) {
+    Requirements r2 = reqs;
+    r2[kLabelCapacityType] = NewRequirement(kLabelCapacityType, KP_OP_IN, {"spot"}, -1);
+    for (int t : its)
+      if (HasCompatibleAvailable(C[t], r2)) {
+        ct = 1;
+        break;
+      }
+  }
+  out->capacity_type = ct;
+  out->od_fallback_warning = ct == 0 && ReqHas(reqs, kLabelCapacityType, "spot") && its.size() < 5;
+  // getOverrides with the capacity type pinned; zonalSubnets = subnet_zones
+  Requirements r3 = reqs;
+  r3[kLabelCapacityType] = NewRequirement(kLabelCapacityType, KP_OP_IN, {ct ? "spot" : "on-demand"}, -1);
+  uint32_t no = 0;
+  for (size_t i = 0; i < its.size(); i++) {
+    out_types[i] = (uint32_t)its[i];
+    for (auto& o : C[its[i]].offerings) {
+      if (!o.available || !Compatible(r3, o.reqs, true)) continue;
+      const string z = OfferingZone(o);
+      for (uint32_t zi = 0; zi < n_zones; zi++)
+        if (z == zones[zi]) {
+          out_overrides[no++] = ((uint32_t)its[i] << 8) | zi;
+          break;
+        }
+    }
+  }
+  out->n_types = (uint32_t)its.size();
+  out->n_overrides = no;
   return KP_OK;
 }
 

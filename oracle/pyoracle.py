@@ -41,6 +41,8 @@ def load(path=LIB_PATH):
         "kpo_filter_compatible_available": (C.c_int32, [P(abi.CatalogDesc), P(abi.FeasibilityQuery), P(C.c_uint8),
                                                         P(C.c_double)]),
         "kpo_filter_spot": (C.c_int32, [P(abi.CatalogDesc), P(abi.Requirements), P(C.c_uint8)]),
+        "kpo_launch_select": (C.c_int32, [P(abi.CatalogDesc), P(abi.LaunchRequest), P(C.c_char_p), C.c_uint32,
+                                          C.c_uint32, P(abi.LaunchResult), P(C.c_uint32), P(C.c_uint32)]),
         "kpo_filter_exotic": (C.c_int32, [P(abi.CatalogDesc), P(abi.Requirements), P(C.c_uint8)]),
         "kpo_requirements_compatible": (C.c_int32, [P(abi.Requirements), P(abi.Requirements), C.c_int32]),
         "kpo_requirements_intersects": (C.c_int32, [P(abi.Requirements), P(abi.Requirements)]),
@@ -106,6 +108,27 @@ def spot_filter(instance_types, requirements):
 
 def exotic_filter(instance_types, requirements):
     return _filter("kpo_filter_exotic", instance_types, requirements)
+
+
+def launch_select(instance_types, requests, subnet_zones, max_types=60):
+    """instance.DefaultProvider.Create's launch-side selection for each (requirements, requests, [type indices])."""
+    lib = load()
+    arena = abi.Arena()
+    desc = arena.catalog_desc(instance_types)
+    rq = abi.launch_requests(arena, requests)
+    zs = arena.arr(C.c_char_p, [z.encode() for z in subnet_zones])
+    out = []
+    stride = max_types * max(1, len(subnet_zones))
+    for i in range(len(requests)):
+        r = abi.LaunchResult()
+        types = np.zeros(max_types, dtype=np.uint32)
+        ovr = np.zeros(stride, dtype=np.uint32)
+        rc = lib.kpo_launch_select(C.byref(desc), C.byref(rq[i]), zs, len(subnet_zones), max_types, C.byref(r),
+                                   types.ctypes.data_as(C.POINTER(C.c_uint32)), ovr.ctypes.data_as(C.POINTER(C.c_uint32)))
+        if rc != 0:
+            raise RuntimeError(f"kpo_launch_select = {rc}")
+        out.append(abi.launch_result_dict(r, types, ovr, list(subnet_zones)))
+    return out
 
 
 def requirements_compatible(a, b, allow_wellknown=True):

@@ -40,3 +40,9 @@ def test_no_device_is_an_error_not_a_fallback():
         assert e.code == kpamd.abi.KP_E_DEVICE
     else:
         raise AssertionError("kp_ctx_create succeeded without a device")
+
+
+def test_launch_struct_layouts():
+    from kpamd import abi
+    assert C.sizeof(abi.LaunchResult) == 10 * 4
+    assert C.sizeof(abi.LaunchRequest) == C.sizeof(abi.Requirements) + C.sizeof(abi.ResourceList) + 8 + 8
