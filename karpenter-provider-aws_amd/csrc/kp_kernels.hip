@@ -311,8 +311,7 @@ __device__ int wave_lower_bound(ValP vals, int n, int64_t q, uint64_t* bytes) {
     const uint64_t bal = __ballot(ge);
     *bytes += 512;
     if (!bal) {
-      const int last = min(hi - 1, lo + 63 * step);
-      lo = last + 1;
+      lo = lo + min(63, (hi - 1 - lo) / step) * step + 1;  // past the last sample taken (< hi)
     } else {
       const int f = __builtin_ctzll(bal);
       if (f == 0) return lo;
@@ -431,6 +430,44 @@ __device__ __forceinline__ void rl_push(RowBatch& L, uint64_t& X, int TW, const 
   L.n++;
 }
 
+// resources.Fits(total, allocatable) as row pushes: per requested resource a threshold mask. A NodeClaim's
+// totals only grow, so the threshold index does too: probe 64 entries past the cached index first. Returns the
+// threshold indices (lane r: resource r); `zero` is set when some resource fits no type.
+__device__ __forceinline__ int32_t fits_rows(const DevDict& D, const CatHdr LDS* H, RowBatch& L, uint64_t& X,
+                                             int64_t q_lane, int32_t j0_lane, const int64_t LDS* fitv_lds,
+                                             uint32_t rmask, uint64_t& nb, bool& zero) {
+  const int lane = LANE;
+  const int TW = D.TW;
+  // 2) resources.Fits(total, allocatable): per requested resource, a threshold mask. A NodeClaim's totals
+  //    only grow, so the threshold index does too: probe 64 entries past the cached index first.
+  int32_t j_lane = 0;
+  uint32_t rm = rmask;
+  while (rm) {
+    const int r = __builtin_ctz(rm);
+    rm &= rm - 1;
+    const int64_t q = lane_bcast_i64(q_lane, r);
+    if (q <= 0) continue;
+    const int j0 = __builtin_amdgcn_readlane(j0_lane, r);
+    const int n = H->fit_n[r];
+    const int slot = H->fit_slot[r];
+    const int idx = j0 + lane;
+    uint64_t bal;
+    if (slot >= 0) bal = __ballot(idx < n && fitv_lds[slot * FITV_CAP + idx] >= q);
+    else bal = __ballot(idx < n && H->d.fit_vals[(size_t)r * D.T + idx] >= q);
+    nb += 512;
+    int j;
+    if (bal) j = j0 + __builtin_ctzll(bal);
+    else if (j0 + 64 >= n) j = n;
+    else if (slot >= 0) j = wave_lower_bound(fitv_lds + slot * FITV_CAP + j0 + 64, n - j0 - 64, q, &nb) + j0 + 64;
+    else j = wave_lower_bound(H->d.fit_vals + (size_t)r * D.T + j0 + 64, n - j0 - 64, q, &nb) + j0 + 64;
+    if (j >= n) zero = true;
+    else rl_push(L, X, TW, H->d.fit_mask + ((size_t)r * D.T + j) * TW, true);
+    nb += (uint64_t)TW * 8;
+    if (lane == r) j_lane = j;
+  }
+  return j_lane;
+}
+
 // NodeClaim.Add's instance-type filter after a successful merge. X: this lane's word of the candidate's
 // remaining types (invariant: X already passes every key the pod did not touch). q_lane: lane r < NRES holds the
 // merged requests (candidate + pod) of resource r, j0_lane the candidate's cached threshold index. Returns the
@@ -485,33 +522,8 @@ __device__ __forceinline__ uint64_t filter_types(const DevDict& D, const CatHdr 
     }
   }
   TSUB(1);
-  // 2) resources.Fits(total, allocatable): per requested resource, a threshold mask. A NodeClaim's totals
-  //    only grow, so the threshold index does too: probe 64 entries past the cached index first.
-  int32_t j_lane = 0;
-  uint32_t rm = rmask;
-  while (rm) {
-    const int r = __builtin_ctz(rm);
-    rm &= rm - 1;
-    const int64_t q = lane_bcast_i64(q_lane, r);
-    if (q <= 0) continue;
-    const int j0 = __builtin_amdgcn_readlane(j0_lane, r);
-    const int n = H->fit_n[r];
-    const int slot = H->fit_slot[r];
-    const int idx = j0 + lane;
-    uint64_t bal;
-    if (slot >= 0) bal = __ballot(idx < n && fitv_lds[slot * FITV_CAP + idx] >= q);
-    else bal = __ballot(idx < n && H->d.fit_vals[(size_t)r * D.T + idx] >= q);
-    nb += 512;
-    int j;
-    if (bal) j = j0 + __builtin_ctzll(bal);
-    else if (j0 + 64 >= n) j = n;
-    else if (slot >= 0) j = wave_lower_bound(fitv_lds + slot * FITV_CAP + j0 + 64, n - j0 - 64, q, &nb) + j0 + 64;
-    else j = wave_lower_bound(H->d.fit_vals + (size_t)r * D.T + j0 + 64, n - j0 - 64, q, &nb) + j0 + 64;
-    if (j >= n) zero = true;
-    else rl_push(L, X, TW, H->d.fit_mask + ((size_t)r * D.T + j) * TW, true);
-    nb += (uint64_t)TW * 8;
-    if (lane == r) j_lane = j;
-  }
+  // 2) resources.Fits(total, allocatable)
+  const int32_t j_lane = fits_rows(D, H, L, X, q_lane, j0_lane, fitv_lds, rmask, nb, zero);
   if (lane < KP_NRES) jout[lane] = j_lane;
   TSUB(2);
   // 3) some available offering compatible with the merged requirements. X already satisfies the
@@ -536,6 +548,25 @@ __device__ __forceinline__ uint64_t filter_types(const DevDict& D, const CatHdr 
     if (!minvalues_ok(D, H->d.code, H->d.TM, rv.hmin & rv.present, rv.minv, X, scratch)) X = 0;
   TSUB(4);
 #undef TSUB
+  *bytes += nb;
+  return X;
+}
+
+// NodeClaim.Add when the pod's shape-level was already merged into the NodeClaim: Requirement.Intersection is
+// idempotent (set ops, max/min bounds and minValues), so the merged requirements equal the NodeClaim's and its
+// remaining types pass every compatibility and offering test already; only Fits over the grown totals changes
+// (callers exclude topology-owning shape-levels and NodeClaims with minValues).
+__device__ __forceinline__ uint64_t fits_filter(const DevDict& D, const CatHdr LDS* H, uint64_t X, int64_t q_lane,
+                                                int32_t j0_lane, const int64_t LDS* fitv_lds, uint32_t rmask,
+                                                RowPtr LDS* rl, uint64_t* bytes, int32_t* jout) {
+  const int lane = LANE;
+  uint64_t nb = 0;
+  bool zero = false;
+  RowBatch L{rl, 0, 0, 0};
+  const int32_t j_lane = fits_rows(D, H, L, X, q_lane, j0_lane, fitv_lds, rmask, nb, zero);
+  if (lane < KP_NRES) jout[lane] = j_lane;
+  rl_flush(L, X, D.TW);
+  if (zero) X = 0;
   *bytes += nb;
   return X;
 }
@@ -673,7 +704,13 @@ __device__ __forceinline__ int compact_candidates(bool cand, int pos, int32_t* s
 // Same for 4 rounds of positions per thread: round k covers pos0 + k * NT (NT = NW * 64 threads), so for a short
 // scan only round 0 is live; one barrier pair for all rounds. s_list holds 4 * NT entries; s_wcnt 4 * NW.
 template <int NW>
-__device__ __forceinline__ int compact_candidates_x4(uint32_t flags, int pos0, int32_t* s_list, int32_t* s_wcnt) {
+// tags (bit k: round k's position carries LIST_TAG) mark candidates that may take the append fast path.
+#define LIST_TAG 0x40000000
+// nc_fail value: the shape-level was merged into the NodeClaim (never equal to a version)
+#define NC_MERGED 0x40000000
+#define LIST_POS(e) ((e) & (LIST_TAG - 1))
+__device__ __forceinline__ int compact_candidates_x4(uint32_t flags, int pos0, int32_t* s_list, int32_t* s_wcnt,
+                                                     uint32_t tags = 0) {
   constexpr int NT = NW * 64;
   const int wave = threadIdx.x >> 6, lane = LANE;
   uint64_t bal[4];
@@ -695,7 +732,8 @@ __device__ __forceinline__ int compact_candidates_x4(uint32_t flags, int pos0, i
   const uint64_t lt = (1ull << lane) - 1;
 #pragma unroll
   for (int k = 0; k < 4; k++)
-    if ((flags >> k) & 1) s_list[before[k] + __builtin_popcountll(bal[k] & lt)] = pos0 + k * NT;
+    if ((flags >> k) & 1)
+      s_list[before[k] + __builtin_popcountll(bal[k] & lt)] = (pos0 + k * NT) | (((tags >> k) & 1) ? LIST_TAG : 0);
   __syncthreads();
   return total;
 }
@@ -772,12 +810,58 @@ __device__ void mstack_push(int32_t* stk, int32_t& n, int32_t& lost, int t, int 
   n++;
 }
 
+// first idx in [lo, hi) whose key (npods[ord[idx]]) is >= K (strict: > K) over a non-decreasing range; hi if
+// none. One wave: 64 samples per round, so a few rounds of two dependent loads instead of a serial bisection.
+__device__ __forceinline__ int wave_key_search(const int32_t* ord, const int32_t* npods, int lo, int hi, int K,
+                                               bool strict) {
+  const int lane = LANE;
+  while (lo < hi) {
+    const int span = hi - lo;
+    const int step = span <= 64 ? 1 : (span + 63) / 64;
+    const int idx = lo + lane * step;
+    bool ge = false;
+    if (idx < hi) {
+      const int key = npods[ord[idx]];
+      ge = strict ? key > K : key >= K;
+    }
+    const uint64_t bal = __ballot(ge);
+    if (step == 1) return bal ? lo + __builtin_ctzll(bal) : hi;
+    if (!bal) {
+      lo = lo + min(63, (hi - 1 - lo) / step) * step + 1;  // past the last sample taken (< hi)
+    } else {
+      const int f = __builtin_ctzll(bal);
+      if (f == 0) return lo;
+      hi = lo + f * step;
+      lo = lo + (f - 1) * step + 1;
+    }
+  }
+  return lo;
+}
+
+// choosePivot(0, n)'s increasingHint for n >= 50, evaluated by one wave: swaps == 0 exactly when each adjacent
+// triple (i-1, i, i+1), (j-1, j, j+1), (k-1, k, k+1) is non-decreasing and so are the middles i <= j <= k
+// (every order2 then finds !Less(b, a)). Lanes 0..8 load the nine keys together.
+__device__ __forceinline__ bool wave_pivot_increasing(const int32_t* ord, const int32_t* npods, int n) {
+  const int lane = LANE;
+  const int t = lane / 3;
+  const int mid = (n / 4) * (t + 1);
+  int key = 0;
+  if (lane < 9) key = npods[ord[mid + (lane % 3) - 1]];
+  const int prev = __shfl(key, lane > 0 ? lane - 1 : 0, 64);
+  const int midkey_prev = __shfl(key, lane >= 3 ? lane - 3 : 0, 64);
+  bool bad = false;
+  if (lane < 9 && (lane % 3) != 0 && key < prev) bad = true;        // within a triple
+  if (lane < 9 && (lane % 3) == 1 && lane >= 3 && key < midkey_prev) bad = true;  // middles
+  return __ballot(bad) == 0;
+}
+
+#define DBG_SERIAL 0
 template <int NT>
 __device__ void sort_newnodeclaims(int32_t* ord, const int32_t* npods, int n, int mut, int p, int32_t* s_ctl) {
   const int tid = threadIdx.x;
   // s_ctl[7]: 0 nothing, 1 shift-left block (p+1..q-1 -> p..q-2, elem -> q-1), 2 shift-right (q..n-2 -> q+1..n-1,
-  // elem -> q), 3 slow path; s_ctl[5] reused? no: use s_ctl[8..9] for q / elem
-  if (tid == 0) {
+  // elem -> q), 3 slow path; s_ctl[8..9]: q / elem. Decided by wave 0 (lane-parallel searches).
+  if (tid < 64) {
     int mode = 0, q = 0;
     NCSort S{ord, npods};
     if (mut == 1 && p + 1 < n && S.Less(p + 1, p)) {
@@ -788,39 +872,46 @@ __device__ void sort_newnodeclaims(int32_t* ord, const int32_t* npods, int n, in
     if (mode) {
       bool fast = n <= 12;
       if (!fast && n >= 50) {
-        DevPDQ<NCSort> P{S};
-        int hint;
-        P.choosePivot(0, n, &hint);  // reads/compares only; no swaps on the slice
-        fast = hint == 0;
+        if (DBG_SERIAL) {
+          int hint = 0;
+          if (tid == 0) {
+            DevPDQ<NCSort> P{S};
+            P.choosePivot(0, n, &hint);
+          }
+          hint = __shfl(hint, 0, 64);
+          const bool f2 = wave_pivot_increasing(ord, npods, n);
+          if (tid == 0 && f2 != (hint == 0)) printf("HINT MISMATCH n=%d p=%d mut=%d\n", n, p, mut);
+          fast = hint == 0;
+        } else {
+          fast = wave_pivot_increasing(ord, npods, n);
+        }
       }
       if (!fast) {
         mode = 3;
       } else if (mode == 1) {  // first q > p with key[q] >= key[p]
-        const int K = npods[ord[p]];
-        int lo = p + 1, hi = n;
-        while (lo < hi) {
-          const int m = (lo + hi) >> 1;
-          if (npods[ord[m]] >= K) hi = m;
-          else lo = m + 1;
+        q = wave_key_search(ord, npods, p + 1, n, npods[ord[p]], false);
+        if (DBG_SERIAL && tid == 0) {
+          const int K = npods[ord[p]];
+          int lo = p + 1, hi = n;
+          while (lo < hi) { const int m = (lo + hi) >> 1; if (npods[ord[m]] >= K) hi = m; else lo = m + 1; }
+          if (lo != q) {
+            printf("Q1 MISMATCH n=%d p=%d q=%d lo=%d K=%d\n", n, p, q, lo, K);
+            for (int i = p; i < n; i++) printf("k[%d]=%d ", i, npods[ord[i]]);
+            printf("\n");
+          }
         }
-        q = lo;
       } else {  // first q with key[q] > key of the appended element (in the sorted prefix [0, n-1))
-        const int K = npods[ord[n - 1]];
-        int lo = 0, hi = n - 1;
-        while (lo < hi) {
-          const int m = (lo + hi) >> 1;
-          if (npods[ord[m]] > K) hi = m;
-          else lo = m + 1;
-        }
-        q = lo;
+        q = wave_key_search(ord, npods, 0, n - 1, npods[ord[n - 1]], true);
       }
     }
-    if (mode == 3) go_sort_slice(S, n);
-    // lowest sorted position whose NodeClaim changed or moved since the last sort (cursor clamp)
-    s_ctl[16] = mode == 3 ? 0 : (mut == 1 ? p : (mut == 2 ? (mode == 2 ? q : n - 1) : -1));
-    s_ctl[7] = mode;
-    s_ctl[8] = q;
-    s_ctl[9] = mode == 1 ? ord[p] : (mode == 2 ? ord[n - 1] : 0);
+    if (tid == 0) {
+      if (mode == 3) go_sort_slice(S, n);
+      // lowest sorted position whose NodeClaim changed or moved since the last sort (cursor clamp)
+      s_ctl[16] = mode == 3 ? 0 : (mut == 1 ? p : (mut == 2 ? (mode == 2 ? q : n - 1) : -1));
+      s_ctl[7] = mode;
+      s_ctl[8] = q;
+      s_ctl[9] = mode == 1 ? ord[p] : (mode == 2 ? ord[n - 1] : 0);
+    }
   }
   __syncthreads();
   const int mode = s_ctl[7], q = s_ctl[8], elem = s_ctl[9];
@@ -844,6 +935,15 @@ __device__ void sort_newnodeclaims(int32_t* ord, const int32_t* npods, int n, in
       __syncthreads();
     }
     if (tid == 0) ord[q] = elem;
+  }
+  __syncthreads();
+  if (DBG_SERIAL && tid == 0) {
+    for (int i = 1; i < n; i++)
+      if (npods[ord[i]] < npods[ord[i - 1]]) {
+        if (s_ctl[30] != 12345) printf("UNSORTED after mode=%d mut=%d p=%d q=%d n=%d at %d\n", mode, mut, p, q, n, i);
+        s_ctl[30] = 12345;
+        break;
+      }
   }
   __syncthreads();
 }
@@ -1121,7 +1221,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
       TS(2);
       // ---- addToInflightNode: first NodeClaim in that order whose Add succeeds ------------------
       for (int base = start; base < n_nc && placed == -1; base += 4 * NT) {
-        uint32_t flags = 0, iflags = 0;
+        uint32_t flags = 0, iflags = 0, tflags = 0;
 #pragma unroll
         for (int k = 0; k < 4; k++) {  // 4 rounds per thread: independent, so their loads overlap
           const int i = base + k * NT + tid;
@@ -1143,6 +1243,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
             if (s_town[j].key < 0)
               cand = (int)a.hcnt_nc[(size_t)s_town[j].row * a.hnc_stride + nc] + s_town[j].self <= s_town[j].maxskew;
           if (cand) iflags |= 1u << k;  // passes everything that does not depend on the zone counts
+          if (cand && !own_n && fl >= NC_MERGED) tflags |= 1u << k;  // shape-level already merged: append path
           for (int j = 0; j < own_n && cand; j++) {  // a NodeClaim pinned to one domain of a key can only take it
             const TopoOwn& o = s_town[j];
             if (o.key >= 0) {
@@ -1157,17 +1258,20 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
           scanned += min(4 * NT, n_nc - base);
           if (base == start) starts += start;
         }
-        const int n = compact_candidates_x4<NW>(flags, base + tid, s_list, s_wcnt);
+        const int n = compact_candidates_x4<NW>(flags, base + tid, s_list, s_wcnt, tflags);
         TS(6);
         if (wave == 0) bytes += (uint64_t)min(4 * NT, n_nc - base) * (12 + 16 * a.n_req_res);  // counted once
-        for (int r0 = 0; r0 < n; r0 += NW) {
+        // a round whose first candidate takes the append path evaluates it alone (it is the likely winner and
+        // costs a fraction of a full attempt, which the other waves would make the round wait for)
+        for (int r0 = 0, width = NW; r0 < n; r0 += width) {
+          width = (s_list[r0] & LIST_TAG) ? 1 : NW;
           const int li = r0 + wave;
-          bool ok = false;
+          bool ok = false, fast = false;
           uint64_t m_v = 0, X = 0;
           ReqView rv;
           int nc = -1;
-          if (li < n) {
-            nc = ord[s_list[li]];
+          if (wave < width && li < n) {
+            nc = ord[LIST_POS(s_list[li])];
             attempts++;
             uint64_t* tsub = (a.timing && wave == 0) ? s_tsub : nullptr;
             const uint64_t tm0 = tsub ? __builtin_amdgcn_s_memtime() : 0;
@@ -1178,12 +1282,21 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
             const uint64_t X0 = lane < D.TW ? a.nc_X[(size_t)nc * D.TW + lane] : 0;
             const int64_t rq_lane = lane < KP_NRES ? a.nc_requests[(size_t)nc * KP_NRES + lane] : 0;
             const int32_t j0_lane = lane < KP_NRES ? a.nc_fitj[(size_t)nc * KP_NRES + lane] : 0;
-            ok = merge_compatible(D, cr, B, b_negop, true, m_v, rv, &slots[wave], vi);
+            fast = (s_list[li] & LIST_TAG) && !(cr.hmin & cr.P);
+            if (fast) {
+              const int64_t q_lane = rq_lane + (lane < KP_NRES ? s_preq[lane] : 0);
+              X = fits_filter(D, hdr(cat), X0, q_lane, j0_lane, (const int64_t LDS*)s_fitv, a.req_res_mask,
+                              (RowPtr LDS*)s_rl[wave], &bytes, s_fitj[wave]);
+              ok = __ballot(X != 0) != 0;
+              bytes += (uint64_t)D.TW * 8 + KP_NRES * 8 + 8;
+            } else {
+              ok = merge_compatible(D, cr, B, b_negop, true, m_v, rv, &slots[wave], vi);
+              bytes += sizeof(KReqs);
+            }
             if (tsub && lane == 0) tsub[0] += __builtin_amdgcn_s_memtime() - tm0;
-            bytes += sizeof(KReqs);
             bool memo = !ok || !own_n;  // failures after the topology step depend on the counts
             if (ok && own_n) ok = topo_narrow(D, own_n, s_town, s_tacc, s_tcnt, true, m_v, rv, vi);
-            if (ok) {
+            if (ok && !fast) {
               const int pb = cat < 32 ? s_pvpb[cat] : a.pvp_base[sl * a.n_catalogs + cat];
               const uint64_t* pvp = a.shape_pvp + (size_t)pb * D.TW;
               const int64_t q_lane = rq_lane + (lane < KP_NRES ? s_preq[lane] : 0);
@@ -1195,14 +1308,17 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
             }
             if (!ok && memo && lane == 0 && nc < a.ncc) a.nc_fail[(size_t)sl * a.ncc + nc] = a.nc_ver[nc];
           }
-          if (lane == 0) s_ok[wave] = ok ? 1 : 0;
+          if (lane == 0 && wave < width) s_ok[wave] = ok ? 1 : 0;
           __syncthreads();
           TS(7);
-          const int win = first_ok<NW>(s_ok);
+          const int win = width == 1 ? (s_ok[0] ? 0 : -1) : first_ok<NW>(s_ok);
           if (win >= 0) {
             if (wave == win) {
-              store_merged(reinterpret_cast<KReqs*>(a.nc_reqs + (size_t)nc * sizeof(KReqs)), rv, m_v, D.W, D.KB);
-              if (a.n_tk) store_tcodes(a.n_tk, a.tk_keys, a.nc_tcode, a.hnc_stride, rv, m_v, nc);
+              if (!fast) {  // the append path leaves the requirements as they are
+                store_merged(reinterpret_cast<KReqs*>(a.nc_reqs + (size_t)nc * sizeof(KReqs)), rv, m_v, D.W, D.KB);
+                if (a.n_tk) store_tcodes(a.n_tk, a.tk_keys, a.nc_tcode, a.hnc_stride, rv, m_v, nc);
+              }
+              if (lane == 0 && !own_n && nc < a.ncc) a.nc_fail[(size_t)sl * a.ncc + nc] = NC_MERGED;
               if (lane < D.TW) a.nc_X[(size_t)nc * D.TW + lane] = X;
               if (lane < KP_NRES) a.nc_requests[(size_t)nc * KP_NRES + lane] += s_preq[lane];
               if (lane == 0) {
@@ -1211,12 +1327,13 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
               }
               if (lane < KP_NRES) a.nc_fitj[(size_t)nc * KP_NRES + lane] = s_fitj[wave][lane];
             }
-            placed = ord[s_list[r0 + win]];
+            const int wpos = LIST_POS(s_list[r0 + win]);
+            placed = ord[wpos];
             if (tid == 0) {
               s_ctl[10] = 1;
-              s_ctl[11] = s_list[r0 + win];
+              s_ctl[11] = wpos;
               // cursor: all positions before the winner failed (topology: before the first count-independent pass)
-              a.cur_nc[2 * sl] = own_n ? min(s_ctl[25], s_list[r0 + win]) : s_list[r0 + win];
+              a.cur_nc[2 * sl] = own_n ? min(s_ctl[25], wpos) : wpos;
               a.cur_nc[2 * sl + 1] = s_ctl[13];
             }
           }
@@ -1300,6 +1417,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
                 a.nc_cat[nc] = a.tmpl_catalog[tm];
               }
               if (lane < KP_NRES) a.nc_fitj[(size_t)nc * KP_NRES + lane] = s_fitj[wave][lane];
+              if (lane == 0 && !own_n && nc < a.ncc) a.nc_fail[(size_t)sl * a.ncc + nc] = NC_MERGED;
               store_maxalloc(hdr(a.tmpl_catalog[tm])->d.alloc, lane < D.TW ? X : 0, D.T, a.req_res_mask,
                              a.nc_maxalloc + (size_t)nc * KP_NRES);
               // subtractMax: remaining -= max capacity over the new NodeClaim's InstanceTypeOptions
