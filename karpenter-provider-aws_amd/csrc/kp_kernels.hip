@@ -40,6 +40,14 @@ __device__ __forceinline__ uint64_t wave_or(uint64_t v) {
   for (int o = 32; o >= 1; o >>= 1) v |= __shfl_xor(v, o, 64);
   return v;
 }
+// cooperative copy of a plain descriptor into LDS, one 32-bit word per thread (a single thread's copy of the
+// ~2.6 KB DevDict is hundreds of serial loads: microseconds per workgroup)
+template <class S>
+__device__ __forceinline__ void block_copy(S& dst, const S* src) {
+  static_assert(sizeof(S) % 4 == 0, "descriptor size");
+  for (int i = threadIdx.x; i < (int)(sizeof(S) / 4); i += blockDim.x)
+    reinterpret_cast<uint32_t*>(&dst)[i] = reinterpret_cast<const uint32_t*>(src)[i];
+}
 __device__ __forceinline__ int wave_sum(int v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -978,7 +986,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
   const int lane = LANE;
-  if (tid == 0) D = *a.dict;
+  block_copy(D, a.dict);
   __syncthreads();
   for (int i = tid; i < D.KB * 64; i += NT) s_vint[i] = a.vint[i];
   const int ncat_lds = min(a.n_catalogs, 8);
@@ -1565,10 +1573,8 @@ __global__ __launch_bounds__(FIN_THREADS) void finalize_kernel(FinalizeArgs a) {
   __shared__ uint32_t s_idx[FIN_MAX_T];
   __shared__ uint32_t s_cnt;
   const int nc = blockIdx.x;
-  if (threadIdx.x == 0) {
-    D = *a.dict;
-    s_cnt = 0;
-  }
+  block_copy(D, a.dict);
+  if (threadIdx.x == 0) s_cnt = 0;
   __syncthreads();
   const int tm = a.nc_tmpl[nc];
   const DevCatalog& Cg = a.cats[a.tmpl_catalog[tm]];
@@ -1647,23 +1653,30 @@ __global__ __launch_bounds__(FIN_THREADS) void finalize_kernel(FinalizeArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// feasibility_kernel: CompatibleAvailableFilter, (query, 64-type tile) per wave, lane = type.
+// feasibility_kernel: CompatibleAvailableFilter, one query row per wave, lane = type.
 // ------------------------------------------------------------------------------------------------
 #define FEAS_WAVES 4
+#define FEAS_NT 8  // 64-type tiles per lane batch (measured: 4 and 16 are slower)
 // One wave per query row: the row's requirement set is decoded once (allowed value words, negative-operator
-// keys, compatible offering classes) and then streamed against every 64-type tile of the catalogue; lane =
-// instance type, __ballot -> mask word, per-lane min over classes -> cheapest price (64 coalesced doubles).
+// keys, compatible offering classes), then the lane evaluates its types t = tile*64 + lane of FEAS_NT tiles at
+// once. Every catalogue gather of one step (a key's codes, a resource's allocatable, a class's prices) is one
+// batch of FEAS_NT independent loads, so a row costs ~(keys + resources + classes) L2 round trips instead of
+// that many per tile. Outputs: __ballot -> mask word per tile, cheapest price per (row, type) (coalesced).
 __global__ __launch_bounds__(FEAS_WAVES * 64) void feasibility_kernel(FeasArgs a) {
   __shared__ DevDict D;
   __shared__ uint64_t s_allowed[FEAS_WAVES][KP_MAX_WORDS];
-  if (threadIdx.x == 0) D = *a.dict;
+  block_copy(D, a.dict);
   __syncthreads();
-  const int wave = threadIdx.x >> 6, lane = LANE;
-  const DevCatalog& Cg = *a.cat;
-  const int tiles = (D.T + 63) >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = LANE;
+  // by value: the catalogue pointers live in SGPRs; through a generic reference every field access after an
+  // output store was re-read with a FLAT load (which waits for the outstanding stores)
+  const DevCatalog Cg = *a.cat;
+  const int T = D.T, C = D.C;
+  const int tiles = (T + 63) >> 6;
   for (long q = (long)blockIdx.x * FEAS_WAVES + wave; q < a.n_queries; q += (long)gridDim.x * FEAS_WAVES) {
     const KReqs* Q = reinterpret_cast<const KReqs*>(a.q_reqs + (size_t)q * sizeof(KReqs));
     const uint64_t v = lane < D.W ? Q->vals[lane] : 0;
+    const int64_t rq_lane = lane < KP_NRES ? a.q_requests[(size_t)q * KP_NRES + lane] : 0;
     ReqView rv;
     rv.present = Q->present;
     rv.compl_ = Q->compl_ & Q->present;
@@ -1679,47 +1692,108 @@ __global__ __launch_bounds__(FEAS_WAVES * 64) void feasibility_kernel(FeasArgs a
     const uint64_t allowed = allowed_word(D, rv, v, vint_global(a.vint));
     const uint64_t cls = allowed_classes(D, Cg.cls, rv, allowed, negQ);
     s_allowed[wave][lane] = allowed;
-    const int64_t rq_lane = lane < KP_NRES ? a.q_requests[(size_t)q * KP_NRES + lane] : 0;
-    uint32_t rmask = (uint32_t)__ballot(rq_lane > 0);
+    const uint32_t rmask = (uint32_t)__ballot(rq_lane > 0);
     wave_sync();
     const uint64_t keys0 = rv.present & D.catalog_keys;
-    for (int tile = 0; tile < tiles; tile++) {
-      const int t = tile * 64 + lane;
-      bool keep = t < D.T;
-      double cheapest = __builtin_huge_val();
-      if (keep) {
-        // Compatible(q, type, WK) part (a): non-well-known type keys q does not define
-        if (a.mode_compatible && (Cg.custom_nonneg[t] & ~rv.present)) keep = false;
-        // Intersects over the shared keys
-        uint64_t keys = keys0;
-        while (keep && keys) {
-          const int k = __builtin_ctzll(keys);
-          keys &= keys - 1;
-          const uint16_t code = Cg.code[(size_t)k * D.T + t];
-          if (code == 0xFFFF) continue;                   // type lacks the key
-          if (code == 0xFFFE) keep = (negQ >> k) & 1;     // type DoesNotExist: only NotIn/DNE intersect
-          else if (code == 0xFFFD) keep = (s_allowed[wave][D.wofs[k]] & Cg.multi[(size_t)k * D.T + t]) != 0;
-          else keep = (s_allowed[wave][code >> 6] >> (code & 63)) & 1;
-        }
-        if (keep && !((Cg.nonneg[t >> 6] >> (t & 63)) & 1)) keep = false;  // Fits: negative totals never fit
-        uint32_t rm = rmask;
-        while (keep && rm) {
-          const int r = __builtin_ctz(rm);
-          rm &= rm - 1;
-          if (lane_bcast_i64(rq_lane, r) > Cg.alloc[(size_t)r * D.T + t]) keep = false;
-        }
-        uint64_t m = cls;
-        while (m) {
-          const int c = __builtin_ctzll(m);
-          m &= m - 1;
-          const double p = Cg.price[(size_t)t * D.C + c];
-          cheapest = p < cheapest ? p : cheapest;
-        }
-        if (!(cheapest < __builtin_huge_val())) keep = false;
+    for (int c0 = 0; c0 < tiles; c0 += FEAS_NT) {
+      int tt[FEAS_NT];
+      uint32_t alive = 0;
+#pragma unroll
+      for (int i = 0; i < FEAS_NT; i++) {
+        const int t = (c0 + i) * 64 + lane;
+        const bool ok = c0 + i < tiles && t < T;
+        tt[i] = ok ? t : 0;
+        alive |= (uint32_t)ok << i;
       }
-      const uint64_t bal = __ballot(keep);
-      if (lane == 0) a.out_mask[(size_t)q * tiles + tile] = bal;
-      if (a.out_cheapest && t < D.T) a.out_cheapest[(size_t)q * D.T + t] = cheapest;
+      const uint32_t valid = alive;
+      // Fits: negative totals never fit (one uniform word per tile)
+#pragma unroll
+      for (int i = 0; i < FEAS_NT; i++)
+        if (c0 + i < tiles && !((Cg.nonneg[c0 + i] >> lane) & 1)) alive &= ~(1u << i);
+      // Compatible(q, type, WK) part (a): non-well-known type keys q does not define
+      if (a.mode_compatible) {
+        uint64_t cn[FEAS_NT];
+#pragma unroll
+        for (int i = 0; i < FEAS_NT; i++) cn[i] = Cg.custom_nonneg[tt[i]];
+#pragma unroll
+        for (int i = 0; i < FEAS_NT; i++)
+          if (cn[i] & ~rv.present) alive &= ~(1u << i);
+      }
+      // Intersects over the shared keys: one batch of code gathers per key
+      uint64_t keys = keys0;
+      while (keys) {
+        const int k = __builtin_ctzll(keys);
+        keys &= keys - 1;
+        const uint16_t* ck = Cg.code + (size_t)k * T;
+        uint32_t code[FEAS_NT];
+#pragma unroll
+        for (int i = 0; i < FEAS_NT; i++) code[i] = ck[tt[i]];
+        uint32_t multi_need = 0;
+#pragma unroll
+        for (int i = 0; i < FEAS_NT; i++) {
+          const uint32_t c = code[i];
+          bool pass;
+          if (c == 0xFFFFu) pass = true;                      // type lacks the key
+          else if (c == 0xFFFEu) pass = (negQ >> k) & 1;      // type DoesNotExist: only NotIn/DNE intersect
+          else if (c == 0xFFFDu) { pass = true; multi_need |= 1u << i; }
+          else pass = (s_allowed[wave][c >> 6] >> (c & 63)) & 1;
+          if (!pass) alive &= ~(1u << i);
+        }
+        multi_need &= alive;
+        if (__ballot(multi_need != 0)) {
+          const uint64_t aw = s_allowed[wave][D.wofs[k]];
+          const uint64_t* mk = Cg.multi + (size_t)k * T;
+          uint64_t mv[FEAS_NT];
+#pragma unroll
+          for (int i = 0; i < FEAS_NT; i++) mv[i] = (multi_need >> i) & 1 ? mk[tt[i]] : ~0ull;
+#pragma unroll
+          for (int i = 0; i < FEAS_NT; i++)
+            if ((aw & mv[i]) == 0) alive &= ~(1u << i);
+        }
+      }
+      // Fits on the requested resources
+      uint32_t rm = rmask;
+      while (rm) {
+        const int r = __builtin_ctz(rm);
+        rm &= rm - 1;
+        const int64_t need = lane_bcast_i64(rq_lane, r);
+        const int64_t* ar = Cg.alloc + (size_t)r * T;
+        int64_t al[FEAS_NT];
+#pragma unroll
+        for (int i = 0; i < FEAS_NT; i++) al[i] = ar[tt[i]];
+#pragma unroll
+        for (int i = 0; i < FEAS_NT; i++)
+          if (need > al[i]) alive &= ~(1u << i);
+      }
+      // cheapest compatible available offering (per-lane min over the row's classes)
+      double cheapest[FEAS_NT];
+#pragma unroll
+      for (int i = 0; i < FEAS_NT; i++) cheapest[i] = __builtin_huge_val();
+      uint64_t m = cls;
+      while (m) {
+        const int c = __builtin_ctzll(m);
+        m &= m - 1;
+        double p[FEAS_NT];
+#pragma unroll
+        for (int i = 0; i < FEAS_NT; i++) p[i] = Cg.price[(size_t)tt[i] * C + c];
+#pragma unroll
+        for (int i = 0; i < FEAS_NT; i++) cheapest[i] = p[i] < cheapest[i] ? p[i] : cheapest[i];
+      }
+      uint64_t myword = 0;
+#pragma unroll
+      for (int i = 0; i < FEAS_NT; i++) {
+        const bool keep = ((alive >> i) & 1) && cheapest[i] < __builtin_huge_val();
+        const uint64_t bal = __ballot(keep);
+        if (lane == i) myword = bal;
+      }
+      const int nt = min(FEAS_NT, tiles - c0);
+      if (lane < nt) a.out_mask[(size_t)q * tiles + c0 + lane] = myword;
+      if (a.out_cheapest) {
+        double* oc = a.out_cheapest + (size_t)q * T;
+#pragma unroll
+        for (int i = 0; i < FEAS_NT; i++)
+          if ((valid >> i) & 1) oc[tt[i]] = cheapest[i];
+      }
     }
     wave_sync();
   }
@@ -1773,7 +1847,7 @@ __device__ int launch_compact(LaunchWaveLds& L, int m, Keep keep) {
 __global__ __launch_bounds__(LAUNCH_WAVES * 64) void launch_kernel(LaunchArgs a) {
   __shared__ DevDict D;
   __shared__ LaunchWaveLds Wl[LAUNCH_WAVES];
-  if (threadIdx.x == 0) D = *a.dict;
+  block_copy(D, a.dict);
   __syncthreads();
   const int wave = threadIdx.x >> 6, lane = LANE;
   const DevCatalog& Cg = *a.cat;

@@ -120,7 +120,7 @@ __device__ void wave_bitonic_kv(uint64_t* k, uint32_t* v, int n2) {
 __global__ __launch_bounds__(SIM_WAVES * 64) void sim_usable_kernel(SimArgs a) {
   __shared__ DevDict D;
   __shared__ uint64_t s_allow[SIM_WAVES][KP_MAX_WORDS];
-  if (threadIdx.x == 0) D = *a.dict;
+  block_copy(D, a.dict);
   __syncthreads();
   const int wave = threadIdx.x >> 6, lane = LANE;
   const long items = (long)a.SL * a.EW;
@@ -173,7 +173,7 @@ __global__ __launch_bounds__(SIM_WAVES * 64) void sim_prep_kernel(SimArgs a) {
   __shared__ RowPtr s_rl[SIM_WAVES][RL_CAP];
   __shared__ CatHdr s_hdr[8];
   __shared__ CatHdr s_hdrw[SIM_WAVES];
-  if (threadIdx.x == 0) D = *a.dict;
+  block_copy(D, a.dict);
   __syncthreads();
   const int wave = threadIdx.x >> 6, lane = LANE;
   for (int c = wave; c < min(a.n_catalogs, 8); c += SIM_WAVES) hdr_fill_wave((CatHdr LDS*)&s_hdr[c], &a.cats[c], D.C);
@@ -251,7 +251,7 @@ __global__ __launch_bounds__(NW * 64) void sim_kernel(SimArgs a) {
   __shared__ CatHdr s_hdrw[NW];
   extern __shared__ uint64_t s_dyn64[];
   const int tid = threadIdx.x, wave = tid >> 6, lane = LANE;
-  if (tid == 0) D = *a.dict;
+  block_copy(D, a.dict);
   __syncthreads();
   for (int c = wave; c < min(a.n_catalogs, 8); c += NW) hdr_fill_wave((CatHdr LDS*)&s_hdr[c], &a.cats[c], D.C);
   __syncthreads();

@@ -77,12 +77,14 @@ def test_config2_medium(ctx, catalog):
     check_same(got, want)
 
 
-def test_feasibility_kernel_vs_oracle(ctx, catalog):
-    """CompatibleAvailableFilter over the full catalogue for randomized (requirements, requests) rows."""
+@pytest.mark.parametrize("n_types", [37, 919])
+def test_feasibility_kernel_vs_oracle(ctx, catalog, n_types):
+    """CompatibleAvailableFilter for randomized (requirements, requests) rows: one partial 64-type tile (37) and
+    the full catalogue (15 tiles: two lane batches of the kernel)."""
     import kpamd
     from kpamd import synth
     from oracle import pyoracle
-    prob = synth.random_problem(catalog, 99, n_types=919, n_pods=10, n_shapes=40)
+    prob = synth.random_problem(catalog, 99, n_types=n_types, n_pods=10, n_shapes=40)
     rng = np.random.default_rng(3)
     queries = []
     for sh in prob.shapes:
