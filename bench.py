@@ -245,7 +245,7 @@ def _consolidation(args, cat, ctx, dist, rank, world, barrier):
     """Config 4: multi-node consolidation sweep on a 10k-node cluster. The subsets (99 prefixes of the
     disruption-cost order + random subsets of 2..100 candidates, generated in fixed chunks so the set
     does not depend on N) are sharded over ranks by chunk; each rank simulates its chunks on its GPU,
-    keeps its best (savings desc, subset index asc), and one RCCL all-gather picks the global best."""
+    keeps its best (savings desc, subset index asc), and an RCCL argmax all-reduce (MAX savings, then MIN subset index) picks the global best."""
     import numpy as np
     import torch
     import kpamd
@@ -311,7 +311,7 @@ def _consolidation(args, cat, ctx, dist, rank, world, barrier):
         "workload": f"config4: computeConsolidation of {total} candidate subsets (99 disruption-cost prefixes + "
                     f"random 2..100-candidate subsets) on a {args.cluster_nodes}-node cluster with "
                     f"{len(cl.pod_shape)} pods (8-40 per node), 2 NodePools, 919 types; sharded by chunk over "
-                    f"ranks, best decision by RCCL all-gather",
+                    f"ranks, best decision by RCCL argmax all-reduce (MAX savings, MIN index)",
         "elapsed_s": round(elapsed, 4),
         "sim_kernel_ms_rank0": round(kern_ms, 3),
         "pods_rescheduled_rank0": int(pops),

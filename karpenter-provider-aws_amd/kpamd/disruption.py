@@ -10,7 +10,7 @@ CS3 and R:website/content/en/preview/concepts/disruption.md:89-128):
                                             search is replayed exactly over those results
   sweep(...)                                the config-4 sweep: many subsets sharded over ranks, best
                                             decision by (savings desc, subset index asc) across ranks
-                                            with one collective (RCCL all-gather of 16 B per rank)
+                                            with two scalar RCCL all-reduces (MAX savings, MIN index)
 
 Decisions are kp_decision values: 0 no-op, 1 delete, 2 replace.
 """
@@ -98,21 +98,21 @@ def best_local(results, base_index=0):
 
 
 def reduce_best(savings, index, dist=None, device=None):
-    """Cross-rank argmax of (savings, -index): one all-gather of (savings, index) per rank."""
+    """Cross-rank argmax of (savings, -index) as two scalar all-reduces (RCCL over xGMI on the GPU path):
+    MAX of the savings, then MIN of the subset index among the ranks holding that maximum. Exact (no packing of
+    the f64 savings into a key) and deterministic: ties go to the lowest global subset index."""
     if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
         return savings, index
     import torch
-    t = torch.tensor([savings, float(index)], dtype=torch.float64, device=device)
-    out = torch.zeros(dist.get_world_size() * 2, dtype=torch.float64, device=device)
-    dist.all_gather_into_tensor(out, t)
-    v = out.view(-1, 2).cpu().numpy()
-    best_s, best_i = -np.inf, -1
-    for s, i in v:
-        if i < 0:
-            continue
-        if s > best_s or (s == best_s and (best_i < 0 or i < best_i)):
-            best_s, best_i = float(s), int(i)
-    return best_s, best_i
+    s = torch.tensor([savings if index >= 0 else -np.inf], dtype=torch.float64, device=device)
+    dist.all_reduce(s, op=dist.ReduceOp.MAX)
+    best_s = float(s.item())
+    if not np.isfinite(best_s):
+        return -np.inf, -1
+    mine = index >= 0 and savings == best_s
+    i = torch.tensor([index if mine else np.iinfo(np.int64).max], dtype=torch.int64, device=device)
+    dist.all_reduce(i, op=dist.ReduceOp.MIN)
+    return best_s, int(i.item())
 
 
 def shard(n, rank, world):

@@ -88,7 +88,12 @@ def _worker(rank, world, port, q):
         # rank 0 holds savings 3.0 at subset 7, rank 1 holds 3.0 at subset 5 and its shard is [50, 100)
         lo, hi = shard(100, rank, world)
         s, i = (3.0, 7) if rank == 0 else (3.0, 5)
-        q.put((rank, (lo, hi), reduce_best(s, i, dist, device="cpu")))
+        tie = reduce_best(s, i, dist, device="cpu")
+        # strict winner on rank 0 at a higher index; rank 1 without any decision
+        s, i = (4.5, 70) if rank == 0 else (-np.inf, -1)
+        win = reduce_best(s, i, dist, device="cpu")
+        none = reduce_best(-np.inf, -1, dist, device="cpu")
+        q.put((rank, (lo, hi), tie, win, none))
     finally:
         dist.destroy_process_group()
 
@@ -110,3 +115,5 @@ def test_reduce_best_gloo_world2():
     out.sort()
     assert out[0][1] == (0, 50) and out[1][1] == (50, 100)
     assert out[0][2] == out[1][2] == (3.0, 5)  # tie on savings -> lowest subset index
+    assert out[0][3] == out[1][3] == (4.5, 70)
+    assert out[0][4] == out[1][4] == (-np.inf, -1)
