@@ -54,11 +54,19 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
 
+    # KP_BENCH_BACKEND=gloo rehearses N ranks on a box with fewer GPUs (ranks share GPU local % count); the
+    # driver's multi-GPU runs use the default: RCCL ("nccl"), one rank per GPU
+    backend = os.environ.get("KP_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     dist = None
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     import kpamd
     from kpamd import catalog, synth
@@ -238,7 +246,7 @@ def _feasibility(args, cat, ctx, prob, barrier, max_over_ranks, world, steps=10)
                          "l2_effective_GBs": round(pairs * L2_BYTES_PER_PAIR / (k_ms / 1e3) / 1e9, 1)}}
 
 
-CHUNK = 1 << 18  # subsets per kp_cluster_simulate call
+CHUNK = 1 << 16  # subsets per kp_cluster_simulate call (1M subsets: 16 chunks, contiguous ranges per rank)
 
 
 def _consolidation(args, cat, ctx, dist, rank, world, barrier):
@@ -255,7 +263,8 @@ def _consolidation(args, cat, ctx, dist, rank, world, barrier):
     cl = synth.config4(cat, n_nodes=args.cluster_nodes, seed=4)
     cands = np.asarray(cl.candidates, dtype=np.uint32)
     n_chunks = (args.subsets + CHUNK - 1) // CHUNK
-    mine = [c for c in range(n_chunks) if c % world == rank]
+    lo, hi = disruption.shard(n_chunks, rank, world)  # contiguous chunk range: balanced for N in 1, 2, 4, 8
+    mine = list(range(lo, hi))
     batches = []
     if rank == 0:  # MultiNodeConsolidation's prefixes candidates[0:k], k = 2..100
         pre = [cands[:k] for k in range(2, min(len(cands), 100) + 1)]
@@ -270,8 +279,9 @@ def _consolidation(args, cat, ctx, dist, rank, world, barrier):
     t0 = time.perf_counter()
     plan = kpamd.ClusterPlan(ctx, cl)
     prep_s = time.perf_counter() - t0
-    plan.simulate_csr(batches[-1][1][:1025] if len(batches[-1][1]) > 1025 else batches[-1][1],
-                      batches[-1][2])  # warmup (untimed)
+    if batches:  # warmup (untimed); a rank may hold no chunk when ranks outnumber chunks
+        plan.simulate_csr(batches[-1][1][:1025] if len(batches[-1][1]) > 1025 else batches[-1][1],
+                          batches[-1][2])
     barrier()
     t0 = time.perf_counter()
     best_s, best_i, kern_ms, pops, words, n_done = -np.inf, -1, 0.0, 0, 0, 0
