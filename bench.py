@@ -48,6 +48,7 @@ def main():
     ap.add_argument("--c5-pods", type=int, default=1_000_000)
     ap.add_argument("--quick", action="store_true", help="config 2 + feasibility only (profiling runs)")
     args = ap.parse_args()
+    t_start = time.perf_counter()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -149,21 +150,31 @@ def main():
     plan.close()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = _cpu_baseline(cat, args.cpu_sample_pods)
+    def progress(msg):  # stderr progress per leg (rank 0): long runs keep writing
+        if rank == 0:
+            print(f"[bench] {msg} ({time.perf_counter() - t_start:.1f} s)", file=sys.stderr, flush=True)
+
+    progress(f"config2 solve done: {value:.0f} pods/s")
     line["feasibility"] = _feasibility(args, cat, ctx, prob, barrier, max_over_ranks, world)
+    progress("feasibility done")
     if not args.quick:
         cfgs = {}
         cfgs["config1"] = _solve_leg("config1", synth.config1(cat, n_pods=1000, seed=1), ctx, barrier,
                                      max_over_ranks, world, args.steps, 1,
                                      None if (rank or world > 1 or args.no_cpu_baseline) else ("1", 1000))
+        progress("config1 done")
         cfgs["config3"] = _solve_leg("config3", synth.config3(cat, n_pods=args.c3_pods), ctx, barrier,
                                      max_over_ranks, world, 2, 1,
                                      None if (rank or world > 1 or args.no_cpu_baseline) else ("3", 3000))
+        progress("config3 done")
         cfgs["config5"] = _solve_leg("config5", synth.config5(cat, n_pods=args.c5_pods), ctx, barrier,
                                      max_over_ranks, world, 1, 0,
                                      None if (rank or world > 1 or args.no_cpu_baseline) else ("5", 6000))
         line["configs"] = cfgs
     if not args.no_consolidation and not args.quick:
+        progress("config5 done")
         line["consolidation"] = _consolidation(args, cat, ctx, dist, rank, world, barrier)
+        progress("consolidation done")
     if rank == 0:
         print(json.dumps(line), flush=True)
     ctx.close()
