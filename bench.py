@@ -282,10 +282,16 @@ def _consolidation(args, cat, ctx, dist, rank, world, barrier):
         offs = np.zeros(len(pre) + 1, dtype=np.uint32)
         offs[1:] = np.cumsum([len(p) for p in pre])
         batches.append((-1, offs, np.concatenate(pre)))
-    for c in mine:
-        n = min(CHUNK, args.subsets - c * CHUNK)
-        offs, pos = disruption.random_subsets_csr(len(cands), n, seed=1000 + c)
-        batches.append((c, offs, cands[pos]))
+    if mine:  # this rank's chunks (fixed seeds per chunk) concatenated into ONE launch: no per-chunk tails
+        offs_l, nodes_l, base = [], [], 0
+        for c in mine:
+            n = min(CHUNK, args.subsets - c * CHUNK)
+            offs, pos = disruption.random_subsets_csr(len(cands), n, seed=1000 + c)
+            offs_l.append(offs[:-1] + base)
+            nodes_l.append(cands[pos])
+            base += int(offs[-1])
+        offs_l.append(np.array([base], dtype=np.uint32))
+        batches.append((mine[0], np.concatenate(offs_l).astype(np.uint32), np.concatenate(nodes_l)))
     gen_s = time.perf_counter() - t0
     t0 = time.perf_counter()
     plan = kpamd.ClusterPlan(ctx, cl)
