@@ -447,6 +447,7 @@ struct HostCat {
   vector<uint64_t> fit_mask;          // [R][T][TW]
   vector<uint64_t> offer_avail;       // [C][TW]
   vector<double> price;               // [T][C]
+  vector<double> price_cm;            // [C][T]
   vector<uint32_t> name_rank;         // [T]
   vector<uint16_t> code;              // [K][T]
   vector<uint64_t> multi;             // [K][T]
@@ -574,6 +575,9 @@ int32_t CompileCatalog(const Dict& d, const vector<HostType>& types, int TW, map
       double& p = hc.price[(size_t)t * C + c];
       if (o.price < p) p = o.price;
     }
+  hc.price_cm.assign((size_t)C * T, std::numeric_limits<double>::infinity());
+  for (int t = 0; t < T; t++)
+    for (int c = 0; c < C; c++) hc.price_cm[(size_t)c * T + t] = hc.price[(size_t)t * C + c];
   vector<int> idx(T);
   for (int t = 0; t < T; t++) idx[t] = t;
   std::sort(idx.begin(), idx.end(), [&](int a, int b) { return types[a].name < types[b].name; });
@@ -1584,7 +1588,7 @@ int32_t CompileSolve(const kp_solve_in* in, Compiled& cp) {
 
 // Lays out dict + catalogues in `blob`; fills `catoffs` with the device DevCatalog array offset.
 struct CatOffsets {
-  size_t TM, DNE, NOKEY, alloc, cap, nonneg, fit_vals, fit_n, fit_mask, cls, offer, price, rank, code, multi, custom;
+  size_t TM, DNE, NOKEY, alloc, cap, nonneg, fit_vals, fit_n, fit_mask, cls, offer, price, price_cm, rank, code, multi, custom;
 };
 
 void PutCatalogs(Blob& blob, const Compiled& cp, vector<CatOffsets>& offs) {
@@ -1602,6 +1606,7 @@ void PutCatalogs(Blob& blob, const Compiled& cp, vector<CatOffsets>& offs) {
     o.cls = blob.put(cp.classes);
     o.offer = blob.put(hc.offer_avail);
     o.price = blob.put(hc.price);
+    o.price_cm = blob.put(hc.price_cm);
     o.rank = blob.put(hc.name_rank);
     o.code = blob.put(hc.code);
     o.multi = blob.put(hc.multi);
@@ -1627,6 +1632,7 @@ vector<DevCatalog> DevCats(uint8_t* base, const Compiled& cp, const vector<CatOf
     c.cls = (const OfferClass*)(base + o.cls);
     c.offer_avail = (const uint64_t*)(base + o.offer);
     c.price = (const double*)(base + o.price);
+    c.price_cm = (const double*)(base + o.price_cm);
     c.name_rank = (const uint32_t*)(base + o.rank);
     c.code = (const uint16_t*)(base + o.code);
     c.multi = (const uint64_t*)(base + o.multi);

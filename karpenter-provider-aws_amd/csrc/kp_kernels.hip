@@ -1608,7 +1608,7 @@ __global__ __launch_bounds__(FIN_THREADS) void finalize_kernel(FinalizeArgs a) {
     while (m) {
       const int c = __builtin_ctzll(m);
       m &= m - 1;
-      const double q = Cg.price[(size_t)t * D.C + c];
+      const double q = Cg.price_cm[(size_t)c * D.T + t];
       p = q < p ? q : p;
     }
     const uint32_t slot = atomicAdd(&s_cnt, 1u);
@@ -1657,6 +1657,9 @@ __global__ __launch_bounds__(FIN_THREADS) void finalize_kernel(FinalizeArgs a) {
 // ------------------------------------------------------------------------------------------------
 #define FEAS_WAVES 4
 #define FEAS_NT 8  // 64-type tiles per lane batch (measured: 4 and 16 are slower)
+#ifndef FEAS_MAX_BLOCKS
+#define FEAS_MAX_BLOCKS 65536
+#endif
 // One wave per query row: the row's requirement set is decoded once (allowed value words, negative-operator
 // keys, compatible offering classes), then the lane evaluates its types t = tile*64 + lane of FEAS_NT tiles at
 // once. Every catalogue gather of one step (a key's codes, a resource's allocatable, a class's prices) is one
@@ -1671,7 +1674,7 @@ __global__ __launch_bounds__(FEAS_WAVES * 64) void feasibility_kernel(FeasArgs a
   // by value: the catalogue pointers live in SGPRs; through a generic reference every field access after an
   // output store was re-read with a FLAT load (which waits for the outstanding stores)
   const DevCatalog Cg = *a.cat;
-  const int T = D.T, C = D.C;
+  const int T = D.T;
   const int tiles = (T + 63) >> 6;
   for (long q = (long)blockIdx.x * FEAS_WAVES + wave; q < a.n_queries; q += (long)gridDim.x * FEAS_WAVES) {
     const KReqs* Q = reinterpret_cast<const KReqs*>(a.q_reqs + (size_t)q * sizeof(KReqs));
@@ -1773,9 +1776,10 @@ __global__ __launch_bounds__(FEAS_WAVES * 64) void feasibility_kernel(FeasArgs a
       while (m) {
         const int c = __builtin_ctzll(m);
         m &= m - 1;
+        const double* pc = Cg.price_cm + (size_t)c * T;
         double p[FEAS_NT];
 #pragma unroll
-        for (int i = 0; i < FEAS_NT; i++) p[i] = Cg.price[(size_t)tt[i] * C + c];
+        for (int i = 0; i < FEAS_NT; i++) p[i] = pc[tt[i]];
 #pragma unroll
         for (int i = 0; i < FEAS_NT; i++) cheapest[i] = p[i] < cheapest[i] ? p[i] : cheapest[i];
       }
@@ -2130,7 +2134,7 @@ hipError_t launch_launch(const LaunchArgs& a, hipStream_t s) {
 }
 hipError_t launch_feasibility(const FeasArgs& a, hipStream_t s) {
   long blocks = ((long)a.n_queries + FEAS_WAVES - 1) / FEAS_WAVES;
-  if (blocks > 65536) blocks = 65536;
+  if (blocks > FEAS_MAX_BLOCKS) blocks = FEAS_MAX_BLOCKS;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(feasibility_kernel, dim3((unsigned)blocks), dim3(FEAS_WAVES * 64), 0, s, a);
   return hipGetLastError();
