@@ -331,6 +331,22 @@ uint64_t kp_catalog_seqnum(const kp_catalog* cat);
 uint32_t kp_catalog_size(const kp_catalog* cat);
 void kp_catalog_destroy(kp_catalog* cat);
 
+/* Offering availability / price change on a resident catalogue: the UnavailableOfferings.MarkUnavailable ->
+ * SeqNum bump -> InjectOfferings rebuild of the reference (R:pkg/cache/unavailableofferings.go:66-92,
+ * R:pkg/providers/instancetype/offering/offering.go:68-147, cache key R:offering.go:189-207) without re-parsing
+ * the types. An update names an existing offering by (type index, capacity type, zone): every offering of that
+ * type with that capacity type and zone (NULL zone: the offerings without a zone requirement) takes `available`
+ * and, when price is not NaN, `price`. All-or-nothing: KP_E_INVAL (nothing changed) if any update names no
+ * offering. On success the catalogue's seqnum becomes `seqnum`. */
+typedef struct kp_offering_update {
+  uint32_t type;              /* index into the uploaded types */
+  int32_t available;          /* 0: ICE / unavailable, 1: available */
+  const char* capacity_type;
+  const char* zone;
+  double price;               /* NaN: keep */
+} kp_offering_update;
+int32_t kp_catalog_update_offerings(kp_catalog* cat, const kp_offering_update* updates, uint32_t n, uint64_t seqnum);
+
 /* EC2 facts the reference reads from ec2types.InstanceTypeInfo (+ the static tables it joins). */
 typedef struct kp_ec2_info {
   const char* name;
@@ -402,6 +418,10 @@ int32_t kp_filter_prepare(kp_ctx* ctx, const kp_catalog* cat, const kp_feasibili
                           int32_t with_cheapest, kp_filter_plan** out);
 int32_t kp_filter_run(kp_filter_plan* plan, uint64_t* out_mask, double* out_cheapest, kp_solve_stats* stats);
 void kp_filter_plan_destroy(kp_filter_plan* plan);
+/* Re-apply the catalogue's current offerings to a prepared plan: only the offering section of the resident
+ * catalogue (available-class masks, per-(type, class) prices; ~C*T*16 bytes) is rebuilt and copied to the
+ * device, the rows stay resident. `cat` must be the catalogue the plan was prepared on (KP_E_INVAL otherwise). */
+int32_t kp_filter_refresh(kp_filter_plan* plan, const kp_catalog* cat);
 
 /* ---- launch-side selection (instance.DefaultProvider.Create) -------------------------------------
  * For each NodeClaim: filterInstanceTypes (R:pkg/providers/instance/instance.go:242-270) =

@@ -17,6 +17,7 @@
 #include <memory>
 #include <mutex>
 #include <set>
+#include <stdexcept>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -447,7 +448,7 @@ struct HostCat {
   vector<uint64_t> fit_mask;          // [R][T][TW]
   vector<uint64_t> offer_avail;       // [C][TW]
   vector<double> price;               // [T][C]
-  vector<double> price_cm;            // [C][T]
+  vector<double> price_cm;            // [C][S]
   vector<uint32_t> name_rank;         // [T]
   vector<uint16_t> code;              // [K][T]
   vector<uint64_t> multi;             // [K][T]
@@ -459,6 +460,30 @@ struct ClassKey {
   int ct, zone, zid;
   bool operator<(const ClassKey& o) const { return std::tie(ct, zone, zid) < std::tie(o.ct, o.zone, o.zid); }
 };
+
+// Offering section of a compiled catalogue: available classes per type, cheapest price per (type, class), and the
+// class-major copy (offering.go:115-147 createOfferings: Available = !ICE && hasPrice && zone offered). Also the
+// whole of an ICE refresh (kp_filter_refresh): availability and price are the only inputs an ICE mark changes.
+void FillOfferings(const Dict& d, const vector<HostType>& types, int TW, const map<ClassKey, int>& classes,
+                   HostCat& hc) {
+  const int T = hc.T, S = hc.S;
+  const int C = (int)classes.size();
+  hc.offer_avail.assign((size_t)C * TW, 0);
+  hc.price.assign((size_t)T * C, std::numeric_limits<double>::infinity());
+  const int kct = d.key(kCapType), kz = d.key(kZone), kzid = d.key(kZoneID);
+  for (int t = 0; t < T; t++)
+    for (auto& o : types[t].offs) {
+      ClassKey ck{d.bit(kct, o.ct), o.has_zone ? d.bit(kz, o.zone) : -1, o.has_zid ? d.bit(kzid, o.zid) : -1};
+      const int c = classes.at(ck);
+      if (!o.available) continue;
+      hc.offer_avail[(size_t)c * TW + t / 64] |= 1ull << (t % 64);
+      double& p = hc.price[(size_t)t * C + c];
+      if (o.price < p) p = o.price;
+    }
+  hc.price_cm.assign((size_t)C * S, std::numeric_limits<double>::infinity());  // row stride S (= D.T)
+  for (int t = 0; t < T; t++)
+    for (int c = 0; c < C; c++) hc.price_cm[(size_t)c * S + t] = hc.price[(size_t)t * C + c];
+}
 
 int32_t CompileCatalog(const Dict& d, const vector<HostType>& types, int TW, map<ClassKey, int>& classes, HostCat& hc) {
   const int T = (int)types.size(), K = d.dd.K, NB = d.dd.W * 64;
@@ -561,23 +586,7 @@ int32_t CompileCatalog(const Dict& d, const vector<HostType>& types, int TW, map
       std::copy(acc.begin(), acc.end(), hc.fit_mask.begin() + ((size_t)r * S + j) * TW);
     }
   }
-  // offerings
-  const int C = (int)classes.size();
-  hc.offer_avail.assign((size_t)C * TW, 0);
-  hc.price.assign((size_t)T * C, std::numeric_limits<double>::infinity());
-  const int kct = d.key(kCapType), kz = d.key(kZone), kzid = d.key(kZoneID);
-  for (int t = 0; t < T; t++)
-    for (auto& o : types[t].offs) {
-      ClassKey ck{d.bit(kct, o.ct), o.has_zone ? d.bit(kz, o.zone) : -1, o.has_zid ? d.bit(kzid, o.zid) : -1};
-      const int c = classes.at(ck);
-      if (!o.available) continue;
-      hc.offer_avail[(size_t)c * TW + t / 64] |= 1ull << (t % 64);
-      double& p = hc.price[(size_t)t * C + c];
-      if (o.price < p) p = o.price;
-    }
-  hc.price_cm.assign((size_t)C * T, std::numeric_limits<double>::infinity());
-  for (int t = 0; t < T; t++)
-    for (int c = 0; c < C; c++) hc.price_cm[(size_t)c * T + t] = hc.price[(size_t)t * C + c];
+  FillOfferings(d, types, TW, classes, hc);
   vector<int> idx(T);
   for (int t = 0; t < T; t++) idx[t] = t;
   std::sort(idx.begin(), idx.end(), [&](int a, int b) { return types[a].name < types[b].name; });
@@ -823,6 +832,32 @@ int32_t kp_catalog_upload(kp_ctx* ctx, const kp_catalog_desc* desc, uint64_t seq
 uint64_t kp_catalog_seqnum(const kp_catalog* c) { return c ? c->seqnum : 0; }
 uint32_t kp_catalog_size(const kp_catalog* c) { return c ? (uint32_t)c->types.size() : 0; }
 void kp_catalog_destroy(kp_catalog* c) { delete c; }
+
+// UnavailableOfferings.MarkUnavailable + SeqNum bump (R:pkg/cache/unavailableofferings.go:66-92) on the uploaded
+// offerings; the next prepare (or kp_filter_refresh) rebuilds Available exactly as createOfferings does
+// (R:offering.go:115-147). Validated in full before anything changes.
+int32_t kp_catalog_update_offerings(kp_catalog* c, const kp_offering_update* ups, uint32_t n, uint64_t seqnum) {
+  if (!c || (!ups && n)) return fail(KP_E_INVAL, "null argument");
+  auto match = [](const HostOffering& o, const kp_offering_update& u) {
+    if (o.ct != (u.capacity_type ? u.capacity_type : "")) return false;
+    return u.zone ? (o.has_zone && o.zone == u.zone) : !o.has_zone;
+  };
+  for (uint32_t i = 0; i < n; i++) {
+    if (ups[i].type >= c->types.size())
+      return fail(KP_E_INVAL, "update %u: type %u of %zu", i, ups[i].type, c->types.size());
+    bool any = false;
+    for (auto& o : c->types[ups[i].type].offs) any = any || match(o, ups[i]);
+    if (!any) return fail(KP_E_INVAL, "update %u names no offering of type %u", i, ups[i].type);
+  }
+  for (uint32_t i = 0; i < n; i++)
+    for (auto& o : c->types[ups[i].type].offs)
+      if (match(o, ups[i])) {
+        o.available = ups[i].available != 0;
+        if (!std::isnan(ups[i].price)) o.price = ups[i].price;
+      }
+  c->seqnum = seqnum;
+  return KP_OK;
+}
 
 // instancetype.NewInstanceType capacity + Overhead.Total() for the AL2023 family (R:types.go:313-598).
 int32_t kp_instance_type_resolve(const kp_options* opts, const kp_ec2_info* info, const kp_nodeclass* nc,
@@ -2158,6 +2193,9 @@ struct kp_filter_plan {
   size_t tiles = 0, o_mask = 0, o_ch = 0;
   bool cheapest = false;
   double prepare_ms = 0;
+  const kp_catalog* cat = nullptr;  // kp_filter_refresh: catalogue, compiled form and its offering offsets
+  Compiled cp;
+  CatOffsets coff{};
 };
 
 extern "C" {
@@ -2216,6 +2254,9 @@ int32_t kp_filter_prepare(kp_ctx* ctx, const kp_catalog* cat, const kp_feasibili
   plan->T = T;
   plan->tiles = tiles;
   plan->cheapest = with_cheapest != 0;
+  plan->cat = cat;
+  plan->coff = coffs[0];
+  plan->cp = std::move(cp);
   plan->prepare_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   *out = plan.release();
   return KP_OK;
@@ -2248,6 +2289,35 @@ int32_t kp_filter_run(kp_filter_plan* plan, uint64_t* out_mask, double* out_chea
     stats->prepare_ms = plan->prepare_ms;
     stats->host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   }
+  return KP_OK;
+}
+
+// ICE refresh of a prepared plan: FillOfferings over the catalogue's current offerings with the plan's own class
+// ids, then only the offering arrays are copied over their resident copies.
+int32_t kp_filter_refresh(kp_filter_plan* plan, const kp_catalog* cat) {
+  if (!plan || !cat) return fail(KP_E_INVAL, "null argument");
+  if (cat != plan->cat || (int)cat->types.size() != plan->T)
+    return fail(KP_E_INVAL, "kp_filter_refresh: the plan was prepared on another catalogue");
+  kp_ctx* ctx = plan->ctx;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device));
+  Compiled& cp = plan->cp;
+  map<ClassKey, int> classes;
+  for (int c = 0; c < cp.C; c++) classes[{cp.classes[c].ct_bit, cp.classes[c].zone_bit, cp.classes[c].zid_bit}] = c;
+  HostCat& hc = cp.cats[0];
+  try {
+    FillOfferings(cp.d, cat->types, cp.TW, classes, hc);
+  } catch (const std::out_of_range&) {
+    return fail(KP_E_INVAL, "kp_filter_refresh: an offering outside the plan's offering classes");
+  }
+  uint8_t* base = (uint8_t*)plan->buf.p;
+  HIPCHK(hipMemcpyAsync(base + plan->coff.offer, hc.offer_avail.data(), hc.offer_avail.size() * sizeof(uint64_t),
+                        hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipMemcpyAsync(base + plan->coff.price, hc.price.data(), hc.price.size() * sizeof(double),
+                        hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipMemcpyAsync(base + plan->coff.price_cm, hc.price_cm.data(), hc.price_cm.size() * sizeof(double),
+                        hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
   return KP_OK;
 }
 

@@ -73,7 +73,7 @@ struct DevCatalog {
   const OfferClass* cls;    // [C]
   const uint64_t* offer_avail;  // [C][TW] types with an AVAILABLE offering of class c
   const double* price;      // [T][C] price of type t's offering of class c (+inf when none/unavailable)
-  const double* price_cm;   // [C][T] the same prices class-major (lane = type gathers coalesce)
+  const double* price_cm;   // [C][D.T] the same prices class-major (lane = type gathers coalesce)
   const uint32_t* name_rank;    // [T] rank of the type name in byte order
   const uint16_t* code;     // [K][T] single-valued code: bit index | 0xFFFE = DNE | 0xFFFF = no key
   const uint64_t* multi;    // [K][T] first-word value mask for multi-valued keys (multi_valued only)

@@ -43,6 +43,7 @@ def load_lib(path=LIB_PATH):
         "kp_catalog_seqnum": (C.c_uint64, [C.c_void_p]),
         "kp_catalog_size": (C.c_uint32, [C.c_void_p]),
         "kp_catalog_destroy": (None, [C.c_void_p]),
+        "kp_catalog_update_offerings": (C.c_int32, [C.c_void_p, P(abi.OfferingUpdate), C.c_uint32, C.c_uint64]),
         "kp_instance_type_resolve": (C.c_int32, [P(abi.Options), P(abi.EC2Info), P(abi.NodeClass),
                                                  P(abi.ResourceList), P(abi.ResourceList)]),
         "kp_filter_compatible_available": (C.c_int32, [C.c_void_p, C.c_void_p, P(abi.FeasibilityQuery), C.c_uint32,
@@ -51,6 +52,7 @@ def load_lib(path=LIB_PATH):
                                           P(C.c_void_p)]),
         "kp_filter_run": (C.c_int32, [C.c_void_p, P(C.c_uint64), P(C.c_double), P(abi.SolveStats)]),
         "kp_filter_plan_destroy": (None, [C.c_void_p]),
+        "kp_filter_refresh": (C.c_int32, [C.c_void_p, C.c_void_p]),
         "kp_launch_prepare": (C.c_int32, [C.c_void_p, C.c_void_p, P(abi.LaunchRequest), C.c_uint32, P(C.c_char_p),
                                           C.c_uint32, C.c_uint32, P(C.c_void_p)]),
         "kp_launch_run": (C.c_int32, [C.c_void_p, P(abi.LaunchResult), P(C.c_uint32), P(C.c_uint32),
@@ -122,6 +124,25 @@ class Catalog:
         h = C.c_void_p()
         _check(ctx.lib, ctx.lib.kp_catalog_upload(ctx.h, C.byref(desc), seqnum, C.byref(h)))
         self.h = h
+
+    def update_offerings(self, updates, seqnum):
+        """kp_catalog_update_offerings: UnavailableOfferings.MarkUnavailable + SeqNum bump
+        (R:pkg/cache/unavailableofferings.go:66-92). updates: (type index, capacity type, zone, available[, price]);
+        the matching offerings of self.instance_types change with the device-side catalogue (all or nothing)."""
+        ups = [abi.OfferingUpdate(int(u[0]), 1 if u[3] else 0, u[1].encode() if u[1] is not None else None,
+                                  u[2].encode() if u[2] is not None else None,
+                                  float(u[4]) if len(u) > 4 and u[4] is not None else float("nan")) for u in updates]
+        arr = (abi.OfferingUpdate * max(1, len(ups)))(*ups)
+        _check(self.ctx.lib, self.ctx.lib.kp_catalog_update_offerings(self.h, arr, len(ups), seqnum))
+        for u in updates:
+            for o in self.instance_types[u[0]].offerings:
+                if o.capacity_type == u[1] and o.zone == u[2]:
+                    o.available = bool(u[3])
+                    if len(u) > 4 and u[4] is not None:
+                        o.price = float(u[4])
+
+    def seqnum(self):
+        return self.ctx.lib.kp_catalog_seqnum(self.h)
 
     def close(self):
         if self.h:
@@ -295,6 +316,10 @@ class FilterPlan:
                                       cheapest.ctypes.data_as(C.POINTER(C.c_double)), C.byref(st)))
         bits = np.unpackbits(mask[:self.n * tiles].view(np.uint8), bitorder="little").reshape(self.n, tiles * 64)
         return bits[:, :self.T].astype(bool), cheapest[:self.n * self.T].reshape(self.n, self.T), stats_dict(st)
+
+    def refresh(self, catalog):
+        """kp_filter_refresh: re-apply the catalogue's current offerings (ICE / price) to the resident plan."""
+        _check(self.ctx.lib, self.ctx.lib.kp_filter_refresh(self.h, catalog.h))
 
     def close(self):
         if self.h:

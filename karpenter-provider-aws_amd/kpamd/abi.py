@@ -69,6 +69,11 @@ class Offering(C.Structure):
                 ("price", C.c_double), ("available", C.c_int32), ("reservation_capacity", C.c_int32)]
 
 
+class OfferingUpdate(C.Structure):
+    _fields_ = [("type", C.c_uint32), ("available", C.c_int32), ("capacity_type", C.c_char_p), ("zone", C.c_char_p),
+                ("price", C.c_double)]
+
+
 class InstanceType(C.Structure):
     _fields_ = [("name", C.c_char_p), ("requirements", Requirements), ("capacity", ResourceList),
                 ("overhead", ResourceList), ("offerings", C.POINTER(Offering)), ("n_offerings", C.c_uint32),

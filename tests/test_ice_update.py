@@ -1,0 +1,131 @@
+"""ICE / price updates on a resident catalogue (kp_catalog_update_offerings, kp_filter_refresh).
+
+Reference: UnavailableOfferings.MarkUnavailable bumps SeqNum (R:pkg/cache/unavailableofferings.go:66-92), which
+changes the offering cache key (R:pkg/providers/instancetype/offering/offering.go:189-207) so InjectOfferings
+rebuilds every offering with Available = !ICE && hasPrice && zone offered (R:offering.go:115-147). The expected
+state after an update is therefore a catalogue built from scratch with the same ICE set
+(`catalog.build_catalog(unavailable=...)`, the restatement of createOfferings); the device plan refreshed in place
+must give bit-identical filter results to a plan prepared on that rebuilt catalogue.
+"""
+import copy
+import ctypes as C
+import math
+
+import numpy as np
+import pytest
+
+# (capacity type, type index, zone) marks; type indices into the 919-type catalogue
+MARKS = [("spot", 0, "test-zone-1a"), ("on-demand", 0, "test-zone-1b"), ("spot", 5, "test-zone-1c"),
+         ("on-demand", 17, "test-zone-1a"), ("spot", 17, "test-zone-1a"), ("on-demand", 300, "test-zone-1c")]
+
+
+def _host_catalog(lib, its):
+    from kpamd import abi
+    arena = abi.Arena()
+    h = C.c_void_p()
+    assert lib.kp_catalog_upload(None, C.byref(arena.catalog_desc(its)), 7, C.byref(h)) == 0
+    return h, arena
+
+
+def _updates(marks, avail=False, price=None):
+    from kpamd import abi
+    ups = [abi.OfferingUpdate(t, 1 if avail else 0, ct.encode(), z.encode(), math.nan if price is None else price)
+           for ct, t, z in marks]
+    return (abi.OfferingUpdate * len(ups))(*ups), len(ups)
+
+
+def test_update_struct_layout():
+    from kpamd import abi
+    assert C.sizeof(abi.OfferingUpdate) == 4 + 4 + 8 + 8 + 8
+
+
+def test_update_host_catalogue_and_seqnum(lib, catalog):
+    h, _ = _host_catalog(lib, catalog)
+    try:
+        arr, n = _updates(MARKS)
+        assert lib.kp_catalog_update_offerings(h, arr, n, 8) == 0
+        assert lib.kp_catalog_seqnum(h) == 8
+        assert lib.kp_catalog_update_offerings(h, arr, 0, 9) == 0  # empty update still bumps the seqnum
+        assert lib.kp_catalog_seqnum(h) == 9
+    finally:
+        lib.kp_catalog_destroy(h)
+
+
+@pytest.mark.parametrize("bad", [("spot", 919, "test-zone-1a"), ("spot", 3, "no-such-zone"),
+                                 ("reserved", 3, "test-zone-1a")])
+def test_update_rejects_unknown_offering_all_or_nothing(lib, catalog, bad):
+    import kpamd
+    h, _ = _host_catalog(lib, catalog)
+    try:
+        arr, n = _updates(MARKS[:2] + [bad])
+        assert lib.kp_catalog_update_offerings(h, arr, n, 8) == kpamd.abi.KP_E_INVAL
+        assert lib.kp_catalog_seqnum(h) == 7  # nothing applied
+    finally:
+        lib.kp_catalog_destroy(h)
+
+
+def test_oracle_ice_marks_equal_rebuilt_catalogue(lib, catalog):
+    """The update semantics (flip Available of the named offerings) == createOfferings with the ICE set."""
+    from kpamd import catalog as kc
+    from oracle import pyoracle
+    names = [it.name for it in catalog]
+    rebuilt = kc.build_catalog(lib, unavailable=frozenset((ct, names[t], z) for ct, t, z in MARKS))
+    flipped = copy.deepcopy(catalog)
+    for ct, t, z in MARKS:
+        for o in flipped[t].offerings:
+            if o.capacity_type == ct and o.zone == z:
+                o.available = False
+    for a, b in zip(rebuilt, flipped):
+        assert [(o.capacity_type, o.zone, o.price, o.available) for o in a.offerings] == \
+               [(o.capacity_type, o.zone, o.price, o.available) for o in b.offerings]
+    reqs = [("topology.kubernetes.io/zone", "In", ["test-zone-1a"])]
+    k1, c1 = pyoracle.compatible_available_filter(rebuilt, reqs, {"cpu": 100})
+    k2, c2 = pyoracle.compatible_available_filter(flipped, reqs, {"cpu": 100})
+    assert (k1 == k2).all() and not k1[17]  # both zone-1a offerings of type 17 are ICE'd
+    np.testing.assert_array_equal(c1[k1], c2[k2])
+
+
+@pytest.mark.gpu
+def test_filter_refresh_equals_rebuilt_plan(ctx, lib, catalog):
+    """Resident plan + ICE marks + kp_filter_refresh == plan prepared on the rebuilt catalogue, and both == the
+    oracle; then un-marking with new prices restores / reprices exactly."""
+    import kpamd
+    from kpamd import catalog as kc
+    from kpamd import synth
+    from oracle import pyoracle
+    prob = synth.config2(catalog, n_pods=400, seed=21)
+    queries = kpamd.pod_queries(prob)
+    queries.append(([("topology.kubernetes.io/zone", "In", ["test-zone-1a"])], {"cpu": 100}))
+    its = copy.deepcopy(catalog)
+    cat = kpamd.Catalog(ctx, its, seqnum=1)
+    fp = kpamd.FilterPlan(ctx, cat, queries, cheapest=True)
+    k0, c0, _ = fp.run(read=True)
+    cat.update_offerings([(t, ct, z, False) for ct, t, z in MARKS], seqnum=2)
+    assert cat.seqnum() == 2
+    fp.refresh(cat)
+    k1, c1, _ = fp.run(read=True)
+    names = [it.name for it in catalog]
+    rebuilt = kc.build_catalog(lib, unavailable=frozenset((ct, names[t], z) for ct, t, z in MARKS))
+    cat2 = kpamd.Catalog(ctx, rebuilt)
+    fp2 = kpamd.FilterPlan(ctx, cat2, queries, cheapest=True)
+    k2, c2, _ = fp2.run(read=True)
+    assert (k1 == k2).all()
+    np.testing.assert_array_equal(c1, c2)
+    assert not (k0 == k1).all()  # the marks changed something (query -1 lost type 17)
+    want_k, want_c = pyoracle.compatible_available_filter(rebuilt, queries[-1][0], queries[-1][1])
+    assert (k1[-1] == want_k).all()
+    np.testing.assert_array_equal(c1[-1][want_k], want_c[want_k])
+    # clear the marks and reprice one offering: the refreshed plan follows the new prices
+    cat.update_offerings([(t, ct, z, True) for ct, t, z in MARKS] + [(5, "spot", "test-zone-1c", True, 0.0001)],
+                         seqnum=3)
+    fp.refresh(cat)
+    k3, c3, _ = fp.run(read=True)
+    assert (k3 == k0).all()
+    want_k, want_c = pyoracle.compatible_available_filter(its, queries[0][0], queries[0][1])
+    assert (k3[0] == want_k).all()
+    np.testing.assert_array_equal(c3[0][want_k], want_c[want_k])
+    # a plan refreshes only from the catalogue it was prepared on
+    with pytest.raises(kpamd.KPError):
+        fp.refresh(cat2)
+    for x in (fp, fp2, cat, cat2):
+        x.close()
