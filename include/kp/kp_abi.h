@@ -476,6 +476,8 @@ int32_t kp_launch_prepare(kp_ctx* ctx, const kp_catalog* cat, const kp_launch_re
                           kp_launch_plan** out);
 int32_t kp_launch_run(kp_launch_plan* plan, kp_launch_result* out, uint32_t* out_types, uint32_t* out_overrides,
                       kp_solve_stats* stats);
+/* ICE / price refresh of a prepared launch plan from its catalogue (see kp_filter_refresh). */
+int32_t kp_launch_refresh(kp_launch_plan* plan, const kp_catalog* cat);
 void kp_launch_plan_destroy(kp_launch_plan* plan);
 
 /* ---- Solve -------------------------------------------------------------------------------- */

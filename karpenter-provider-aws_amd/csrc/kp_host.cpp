@@ -2184,6 +2184,29 @@ int32_t CompileQueries(const kp_catalog* cat, const vector<RawReqs>& qs, Compile
 
 }  // namespace
 
+// Shared by kp_filter_refresh / kp_launch_refresh: rebuild the offering section of a plan's compiled catalogue
+// from the catalogue's current offerings (class ids as compiled) and copy it over the resident arrays.
+static int32_t RefreshOfferings(kp_ctx* ctx, const kp_catalog* cat, Compiled& cp, const CatOffsets& coff, uint8_t* base) {
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device));
+  map<ClassKey, int> classes;
+  for (int c = 0; c < cp.C; c++) classes[{cp.classes[c].ct_bit, cp.classes[c].zone_bit, cp.classes[c].zid_bit}] = c;
+  HostCat& hc = cp.cats[0];
+  try {
+    FillOfferings(cp.d, cat->types, cp.TW, classes, hc);
+  } catch (const std::out_of_range&) {
+    return fail(KP_E_INVAL, "refresh: an offering outside the plan's offering classes");
+  }
+  HIPCHK(hipMemcpyAsync(base + coff.offer, hc.offer_avail.data(), hc.offer_avail.size() * sizeof(uint64_t),
+                        hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipMemcpyAsync(base + coff.price, hc.price.data(), hc.price.size() * sizeof(double),
+                        hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipMemcpyAsync(base + coff.price_cm, hc.price_cm.data(), hc.price_cm.size() * sizeof(double),
+                        hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return KP_OK;
+}
+
 struct kp_filter_plan {
   kp_ctx* ctx = nullptr;
   DevBuf buf;
@@ -2298,27 +2321,7 @@ int32_t kp_filter_refresh(kp_filter_plan* plan, const kp_catalog* cat) {
   if (!plan || !cat) return fail(KP_E_INVAL, "null argument");
   if (cat != plan->cat || (int)cat->types.size() != plan->T)
     return fail(KP_E_INVAL, "kp_filter_refresh: the plan was prepared on another catalogue");
-  kp_ctx* ctx = plan->ctx;
-  std::lock_guard<std::mutex> lock(ctx->mu);
-  HIPCHK(hipSetDevice(ctx->device));
-  Compiled& cp = plan->cp;
-  map<ClassKey, int> classes;
-  for (int c = 0; c < cp.C; c++) classes[{cp.classes[c].ct_bit, cp.classes[c].zone_bit, cp.classes[c].zid_bit}] = c;
-  HostCat& hc = cp.cats[0];
-  try {
-    FillOfferings(cp.d, cat->types, cp.TW, classes, hc);
-  } catch (const std::out_of_range&) {
-    return fail(KP_E_INVAL, "kp_filter_refresh: an offering outside the plan's offering classes");
-  }
-  uint8_t* base = (uint8_t*)plan->buf.p;
-  HIPCHK(hipMemcpyAsync(base + plan->coff.offer, hc.offer_avail.data(), hc.offer_avail.size() * sizeof(uint64_t),
-                        hipMemcpyHostToDevice, ctx->stream));
-  HIPCHK(hipMemcpyAsync(base + plan->coff.price, hc.price.data(), hc.price.size() * sizeof(double),
-                        hipMemcpyHostToDevice, ctx->stream));
-  HIPCHK(hipMemcpyAsync(base + plan->coff.price_cm, hc.price_cm.data(), hc.price_cm.size() * sizeof(double),
-                        hipMemcpyHostToDevice, ctx->stream));
-  HIPCHK(hipStreamSynchronize(ctx->stream));
-  return KP_OK;
+  return RefreshOfferings(plan->ctx, cat, plan->cp, plan->coff, (uint8_t*)plan->buf.p);
 }
 
 void kp_filter_plan_destroy(kp_filter_plan* p) {
@@ -2349,6 +2352,9 @@ struct kp_launch_plan {
   uint32_t n = 0, max_types = 0, ovr_stride = 0;
   size_t o_out = 0, o_types = 0, o_ovr = 0, o_stats = 0;
   double prepare_ms = 0;
+  const kp_catalog* cat = nullptr;  // kp_launch_refresh
+  Compiled cp;
+  CatOffsets coff{};
 };
 static_assert(sizeof(LaunchOut) == sizeof(kp_launch_result), "LaunchOut mirrors kp_launch_result");
 
@@ -2492,6 +2498,9 @@ int32_t kp_launch_prepare(kp_ctx* ctx, const kp_catalog* cat, const kp_launch_re
   plan->n = n;
   plan->max_types = max_types;
   plan->ovr_stride = ovr_stride;
+  plan->cat = cat;
+  plan->coff = coffs[0];
+  plan->cp = std::move(cp);
   plan->prepare_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   *out = plan.release();
   return KP_OK;
@@ -2533,6 +2542,14 @@ int32_t kp_launch_run(kp_launch_plan* plan, kp_launch_result* out, uint32_t* out
     stats->host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   }
   return KP_OK;
+}
+
+// ICE refresh of a prepared launch plan (same offering section as kp_filter_refresh; the offering -> class map and
+// the subnet-zone classes do not change with availability or price).
+int32_t kp_launch_refresh(kp_launch_plan* plan, const kp_catalog* cat) {
+  if (!plan || !cat) return fail(KP_E_INVAL, "null argument");
+  if (cat != plan->cat) return fail(KP_E_INVAL, "kp_launch_refresh: the plan was prepared on another catalogue");
+  return RefreshOfferings(plan->ctx, cat, plan->cp, plan->coff, (uint8_t*)plan->buf.p);
 }
 
 void kp_launch_plan_destroy(kp_launch_plan* p) {

@@ -53,6 +53,7 @@ def load_lib(path=LIB_PATH):
         "kp_filter_run": (C.c_int32, [C.c_void_p, P(C.c_uint64), P(C.c_double), P(abi.SolveStats)]),
         "kp_filter_plan_destroy": (None, [C.c_void_p]),
         "kp_filter_refresh": (C.c_int32, [C.c_void_p, C.c_void_p]),
+        "kp_launch_refresh": (C.c_int32, [C.c_void_p, C.c_void_p]),
         "kp_launch_prepare": (C.c_int32, [C.c_void_p, C.c_void_p, P(abi.LaunchRequest), C.c_uint32, P(C.c_char_p),
                                           C.c_uint32, C.c_uint32, P(C.c_void_p)]),
         "kp_launch_run": (C.c_int32, [C.c_void_p, P(abi.LaunchResult), P(C.c_uint32), P(C.c_uint32),
@@ -370,6 +371,10 @@ class LaunchPlan:
         res = [abi.launch_result_dict(out[i], types[i * self.max_types:(i + 1) * self.max_types],
                                       ovr[i * stride:(i + 1) * stride], self.zones) for i in range(self.n)]
         return res, stats_dict(st)
+
+    def refresh(self, catalog):
+        """kp_launch_refresh: re-apply the catalogue's current offerings (ICE / price) to the resident plan."""
+        _check(self.ctx.lib, self.ctx.lib.kp_launch_refresh(self.h, catalog.h))
 
     def close(self):
         if self.h:

@@ -129,3 +129,32 @@ def test_filter_refresh_equals_rebuilt_plan(ctx, lib, catalog):
         fp.refresh(cat2)
     for x in (fp, fp2, cat, cat2):
         x.close()
+
+
+@pytest.mark.gpu
+def test_launch_refresh_equals_rebuilt_catalogue(ctx, lib, catalog):
+    """Launch-side selection after ICE marks (the reference's ICE fallback, R:pkg/providers/instancetype/
+    suite_test.go:2059-2092): a resident launch plan refreshed in place == the oracle on the rebuilt catalogue."""
+    import kpamd
+    from kpamd import catalog as kc
+    from kpamd import synth
+    from oracle import pyoracle
+    marks = [("spot", t, "test-zone-1a") for t in range(0, len(catalog), 2)] + \
+            [("on-demand", t, "test-zone-1b") for t in range(0, len(catalog), 3)]
+    reqs = synth.random_launch_requests(catalog, 200, seed=311)
+    its = copy.deepcopy(catalog)
+    cat = kpamd.Catalog(ctx, its, seqnum=1)
+    plan = kpamd.LaunchPlan(ctx, cat, reqs, kc.ZONES)
+    before, _ = plan.run(read=True)
+    cat.update_offerings([(t, ct, z, False) for ct, t, z in marks], seqnum=2)
+    plan.refresh(cat)
+    got, _ = plan.run(read=True)
+    names = [it.name for it in catalog]
+    rebuilt = kc.build_catalog(lib, unavailable=frozenset((ct, names[t], z) for ct, t, z in marks))
+    want = pyoracle.launch_select(rebuilt, reqs, kc.ZONES, max_types=60)
+    assert len(got) == len(want)
+    for i, (g, w) in enumerate(zip(got, want)):
+        assert g == w, f"request {i}: device {g} vs oracle {w}"
+    assert got != before  # the marks moved some launches (overrides or capacity type)
+    plan.close()
+    cat.close()
