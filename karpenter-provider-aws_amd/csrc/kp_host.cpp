@@ -449,6 +449,7 @@ struct HostCat {
   vector<uint64_t> offer_avail;       // [C][TW]
   vector<double> price;               // [T][C]
   vector<double> price_cm;            // [C][S]
+  vector<double> price_sub;           // [2^C][S] (C <= KP_SUB_MAX_C)
   vector<uint32_t> name_rank;         // [T]
   vector<uint16_t> code;              // [K][T]
   vector<uint64_t> multi;             // [K][T]
@@ -483,6 +484,17 @@ void FillOfferings(const Dict& d, const vector<HostType>& types, int TW, const m
   hc.price_cm.assign((size_t)C * S, std::numeric_limits<double>::infinity());  // row stride S (= D.T)
   for (int t = 0; t < T; t++)
     for (int c = 0; c < C; c++) hc.price_cm[(size_t)c * S + t] = hc.price[(size_t)t * C + c];
+  // cheapest over a row's compatible class set in one gather: min over each subset m, built from m & (m - 1)
+  hc.price_sub.clear();
+  if (C <= KP_SUB_MAX_C) {
+    hc.price_sub.assign((size_t)S << C, std::numeric_limits<double>::infinity());
+    for (size_t m = 1; m < ((size_t)1 << C); m++) {
+      const int c = __builtin_ctzll(m);
+      const double* prev = &hc.price_sub[(m & (m - 1)) * S];
+      double* cur = &hc.price_sub[m * S];
+      for (int t = 0; t < T; t++) cur[t] = std::min(prev[t], hc.price[(size_t)t * C + c]);
+    }
+  }
 }
 
 int32_t CompileCatalog(const Dict& d, const vector<HostType>& types, int TW, map<ClassKey, int>& classes, HostCat& hc) {
@@ -1623,7 +1635,7 @@ int32_t CompileSolve(const kp_solve_in* in, Compiled& cp) {
 
 // Lays out dict + catalogues in `blob`; fills `catoffs` with the device DevCatalog array offset.
 struct CatOffsets {
-  size_t TM, DNE, NOKEY, alloc, cap, nonneg, fit_vals, fit_n, fit_mask, cls, offer, price, price_cm, rank, code, multi, custom;
+  size_t TM, DNE, NOKEY, alloc, cap, nonneg, fit_vals, fit_n, fit_mask, cls, offer, price, price_cm, price_sub, rank, code, multi, custom;
 };
 
 void PutCatalogs(Blob& blob, const Compiled& cp, vector<CatOffsets>& offs) {
@@ -1642,6 +1654,7 @@ void PutCatalogs(Blob& blob, const Compiled& cp, vector<CatOffsets>& offs) {
     o.offer = blob.put(hc.offer_avail);
     o.price = blob.put(hc.price);
     o.price_cm = blob.put(hc.price_cm);
+    o.price_sub = blob.put(hc.price_sub);
     o.rank = blob.put(hc.name_rank);
     o.code = blob.put(hc.code);
     o.multi = blob.put(hc.multi);
@@ -1668,6 +1681,7 @@ vector<DevCatalog> DevCats(uint8_t* base, const Compiled& cp, const vector<CatOf
     c.offer_avail = (const uint64_t*)(base + o.offer);
     c.price = (const double*)(base + o.price);
     c.price_cm = (const double*)(base + o.price_cm);
+    c.price_sub = cp.cats[i].price_sub.empty() ? nullptr : (const double*)(base + o.price_sub);
     c.name_rank = (const uint32_t*)(base + o.rank);
     c.code = (const uint16_t*)(base + o.code);
     c.multi = (const uint64_t*)(base + o.multi);
@@ -2202,6 +2216,8 @@ static int32_t RefreshOfferings(kp_ctx* ctx, const kp_catalog* cat, Compiled& cp
   HIPCHK(hipMemcpyAsync(base + coff.price, hc.price.data(), hc.price.size() * sizeof(double),
                         hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(hipMemcpyAsync(base + coff.price_cm, hc.price_cm.data(), hc.price_cm.size() * sizeof(double),
+                        hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipMemcpyAsync(base + coff.price_sub, hc.price_sub.data(), hc.price_sub.size() * sizeof(double),
                         hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
   return KP_OK;

@@ -1773,6 +1773,12 @@ __global__ __launch_bounds__(FEAS_WAVES * 64) void feasibility_kernel(FeasArgs a
 #pragma unroll
       for (int i = 0; i < FEAS_NT; i++) cheapest[i] = __builtin_huge_val();
       uint64_t m = cls;
+      if (Cg.price_sub) {  // one gather: the min over the row's class set is precomputed per subset
+        const double* ps = Cg.price_sub + (size_t)cls * T;
+#pragma unroll
+        for (int i = 0; i < FEAS_NT; i++) cheapest[i] = ps[tt[i]];
+        m = 0;
+      }
       while (m) {
         const int c = __builtin_ctzll(m);
         m &= m - 1;

@@ -22,6 +22,7 @@
 #define KP_MAX_WORDS 64
 #define KP_MAX_TYPE_WORDS 64
 #define KP_MAX_CLASSES 64
+#define KP_SUB_MAX_C 6  // class-subset price table up to 2^6 x T doubles (470 KB at T = 919)
 #define KP_NRES 12
 
 struct KReqs {
@@ -74,6 +75,7 @@ struct DevCatalog {
   const uint64_t* offer_avail;  // [C][TW] types with an AVAILABLE offering of class c
   const double* price;      // [T][C] price of type t's offering of class c (+inf when none/unavailable)
   const double* price_cm;   // [C][D.T] the same prices class-major (lane = type gathers coalesce)
+  const double* price_sub;  // [2^C][D.T] min price over each class subset (C <= KP_SUB_MAX_C), else null
   const uint32_t* name_rank;    // [T] rank of the type name in byte order
   const uint16_t* code;     // [K][T] single-valued code: bit index | 0xFFFE = DNE | 0xFFFF = no key
   const uint64_t* multi;    // [K][T] first-word value mask for multi-valued keys (multi_valued only)
