@@ -455,6 +455,7 @@ struct HostCat {
   vector<uint64_t> multi;             // [K][T]
   vector<uint64_t> custom_nonneg;     // [T]
   uint64_t multi_valued = 0;
+  uint64_t custom_any = 0;            // OR of custom_nonneg
 };
 
 struct ClassKey {
@@ -524,7 +525,10 @@ int32_t CompileCatalog(const Dict& d, const vector<HostType>& types, int TW, map
       if ((q.compl_ & kb) || (q.hgt & kb) || (q.hlt & kb))
         return fail(KP_E_UNSUPPORTED, "instance type %s: requirement %s is not In/DoesNotExist", types[t].name.c_str(),
                     d.keys[k].c_str());
-      if (!(d.dd.wellknown & kb) && !(neg & kb)) hc.custom_nonneg[t] |= kb;
+      if (!(d.dd.wellknown & kb) && !(neg & kb)) {
+        hc.custom_nonneg[t] |= kb;
+        hc.custom_any |= kb;
+      }
       int cnt = 0, last = -1;
       for (int wi = 0, w = kw(d, k, 0); wi < nwords(d, k); wi++, w = wi < nwords(d, k) ? kw(d, k, wi) : 0) {
         uint64_t m = q.vals[w];
@@ -1687,6 +1691,7 @@ vector<DevCatalog> DevCats(uint8_t* base, const Compiled& cp, const vector<CatOf
     c.multi = (const uint64_t*)(base + o.multi);
     c.custom_nonneg = (const uint64_t*)(base + o.custom);
     c.multi_valued = cp.cats[i].multi_valued;
+    c.custom_any = cp.cats[i].custom_any;
     out.push_back(c);
   }
   return out;

@@ -1714,7 +1714,7 @@ __global__ __launch_bounds__(FEAS_WAVES * 64) void feasibility_kernel(FeasArgs a
       for (int i = 0; i < FEAS_NT; i++)
         if (c0 + i < tiles && !((Cg.nonneg[c0 + i] >> lane) & 1)) alive &= ~(1u << i);
       // Compatible(q, type, WK) part (a): non-well-known type keys q does not define
-      if (a.mode_compatible) {
+      if (a.mode_compatible && (Cg.custom_any & ~rv.present)) {  // skipped when no type has such a key
         uint64_t cn[FEAS_NT];
 #pragma unroll
         for (int i = 0; i < FEAS_NT; i++) cn[i] = Cg.custom_nonneg[tt[i]];

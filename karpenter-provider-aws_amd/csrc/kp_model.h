@@ -81,4 +81,5 @@ struct DevCatalog {
   const uint64_t* multi;    // [K][T] first-word value mask for multi-valued keys (multi_valued only)
   const uint64_t* custom_nonneg; // [T] key mask of non-well-known keys the type has with a non-NotIn/DNE op
   uint64_t multi_valued;    // keys where some type has > 1 value
+  uint64_t custom_any;      // OR of custom_nonneg over the types (0: the per-type test is vacuous)
 };
