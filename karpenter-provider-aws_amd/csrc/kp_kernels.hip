@@ -1655,7 +1655,7 @@ __global__ __launch_bounds__(FIN_THREADS) void finalize_kernel(FinalizeArgs a) {
 // ------------------------------------------------------------------------------------------------
 // feasibility_kernel: CompatibleAvailableFilter, one query row per wave, lane = type.
 // ------------------------------------------------------------------------------------------------
-#define FEAS_WAVES 4
+#define FEAS_WAVES 8
 #define FEAS_NT 8  // 64-type tiles per lane batch (measured: 4 and 16 are slower)
 #ifndef FEAS_MAX_BLOCKS
 #define FEAS_MAX_BLOCKS 65536
