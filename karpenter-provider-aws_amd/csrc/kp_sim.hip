@@ -526,7 +526,9 @@ __global__ __launch_bounds__(NW * 64) void sim_kernel(SimArgs a) {
             const int t = ch * 64 + lane;
             const bool has = (wd >> lane) & 1;
             double p = __builtin_huge_val();
-            if (has) {
+            if (has && Cg.price_sub) {  // min over the compatible class set in one gather
+              p = Cg.price_sub[(size_t)cls * D.T + t];
+            } else if (has) {
               uint64_t m = cls;
               while (m) {
                 const int c = __builtin_ctzll(m);
