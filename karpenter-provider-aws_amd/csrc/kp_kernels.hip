@@ -1605,6 +1605,10 @@ __global__ __launch_bounds__(FIN_THREADS) void finalize_kernel(FinalizeArgs a) {
     if (!((xw >> (t & 63)) & 1)) continue;
     double p = __builtin_huge_val();
     uint64_t m = cls;
+    if (Cg.price_sub) {  // min over the compatible class set in one gather
+      p = Cg.price_sub[(size_t)cls * D.T + t];
+      m = 0;
+    }
     while (m) {
       const int c = __builtin_ctzll(m);
       m &= m - 1;
