@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define KP_ABI_VERSION 2
+#define KP_ABI_VERSION 3
 
 enum kp_status {
   KP_OK = 0,
@@ -310,6 +310,10 @@ typedef struct kp_solve_stats {
   uint64_t cursor_starts;   /* diagnostic: sum of first-fit cursor start positions (positions skipped) */
   uint64_t attempt_cycles[8]; /* diagnostic (KP_TIMING=1): wave 0's in-flight attempt split (merge, pod keys,
                                  Fits, offerings, minValues; [5] = attempts timed) */
+  double catalog_ms;        /* part of prepare_ms spent compiling the catalogue half (dictionary, catalogue SoA,
+                               NodeClaimTemplates); 0 when it came resident from the kp_ctx cache */
+  uint32_t catalog_cached;  /* 1: the catalogue half was resident (same catalogues + seqnums + NodePools) */
+  uint32_t reserved_;
 } kp_solve_stats;
 
 /* ---- context ---------------------------------------------------------------------------- */

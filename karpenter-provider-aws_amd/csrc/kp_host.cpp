@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdarg>
@@ -158,17 +159,28 @@ struct HostType {
 
 }  // namespace
 
+namespace {
+struct SolveBase;
+}
+
 struct kp_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
   kp_options opts;
   std::mutex mu;
+  // resident compiled catalogues + templates of recent Solves (most recent last), see SolveBase
+  vector<std::shared_ptr<SolveBase>> bases;
+  uint64_t base_hits = 0, base_misses = 0;
+  // per-Solve device arena handed back by kp_solve_plan_destroy and reused by the next kp_solve_prepare
+  void* spare = nullptr;
+  size_t spare_bytes = 0;
 };
 
 struct kp_catalog {
   kp_ctx* ctx;
   uint64_t seqnum;
+  uint64_t uid;  // process-unique identity (a new upload never reuses one, unlike its address)
   vector<HostType> types;
 };
 
@@ -681,8 +693,11 @@ bool HostMinValuesOK(const Dict& d, const HostCat& hc, const KReqs& q, const vec
 // ------------------------------------------------------------------------------------------------
 // device buffer arena: everything of one solve in one allocation
 // ------------------------------------------------------------------------------------------------
+// Host image of one device allocation: put()/reserve() lay out host-initialised regions (uploaded in one copy),
+// reserve_dev() appends device-only regions after them (no host backing, nothing to zero or copy).
 struct Blob {
   vector<uint8_t> host;
+  size_t dev_end = 0;  // > 0 once device-only regions were appended
   template <class T>
   size_t put(const T* p, size_t n) {
     size_t off = (host.size() + 255) & ~(size_t)255;
@@ -699,13 +714,32 @@ struct Blob {
     host.resize(off + bytes);
     return off;
   }
+  size_t reserve_dev(size_t bytes) {
+    size_t off = (std::max(host.size(), dev_end) + 255) & ~(size_t)255;
+    dev_end = off + bytes;
+    return off;
+  }
+  size_t total() const { return std::max(host.size(), dev_end); }
 };
 
 struct DevBuf {
   void* p = nullptr;
   size_t n = 0;
-  ~DevBuf() {
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { reset(); }
+  void reset() {
     if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  hipError_t alloc(size_t bytes) {
+    reset();
+    hipError_t e = hipMalloc(&p, std::max<size_t>(bytes, 1));
+    if (e == hipSuccess) n = bytes;
+    else p = nullptr;
+    return e;
   }
 };
 
@@ -807,6 +841,8 @@ int32_t kp_ctx_create(const kp_options* opts, kp_ctx** out) {
 void kp_ctx_destroy(kp_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
+  c->bases.clear();
+  if (c->spare) (void)hipFree(c->spare);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->ev2) (void)hipEventDestroy(c->ev2);
@@ -818,9 +854,11 @@ void kp_ctx_destroy(kp_ctx* c) {
 int32_t kp_catalog_upload(kp_ctx* ctx, const kp_catalog_desc* desc, uint64_t seqnum, kp_catalog** out) {
   if (!desc || !out) return fail(KP_E_INVAL, "null argument");  // ctx NULL: host-only (kp_solve_validate)
   if (desc->n_types > 4096) return fail(KP_E_UNSUPPORTED, "%u instance types (max 4096)", desc->n_types);
+  static std::atomic<uint64_t> next_uid{1};
   auto* c = new kp_catalog();
   c->ctx = ctx;
   c->seqnum = seqnum;
+  c->uid = next_uid.fetch_add(1);
   for (uint32_t i = 0; i < desc->n_types; i++) {
     const kp_instance_type& t = desc->types[i];
     HostType h;
@@ -854,6 +892,9 @@ void kp_catalog_destroy(kp_catalog* c) { delete c; }
 // (R:offering.go:115-147). Validated in full before anything changes.
 int32_t kp_catalog_update_offerings(kp_catalog* c, const kp_offering_update* ups, uint32_t n, uint64_t seqnum) {
   if (!c || (!ups && n)) return fail(KP_E_INVAL, "null argument");
+  // serialized with every prepare / refresh / run of the catalogue's context (they read c->types)
+  std::unique_lock<std::mutex> lock;
+  if (c->ctx) lock = std::unique_lock<std::mutex>(c->ctx->mu);
   auto match = [](const HostOffering& o, const kp_offering_update& u) {
     if (o.ct != (u.capacity_type ? u.capacity_type : "")) return false;
     return u.zone ? (o.has_zone && o.zone == u.zone) : !o.has_zone;
@@ -930,18 +971,44 @@ int32_t kp_instance_type_resolve(const kp_options* opts, const kp_ec2_info* info
 // ==================================================================================================
 namespace {
 
-struct Compiled {
+struct TaintT {
+  string key, value;
+  int effect;
+  bool operator<(const TaintT& o) const { return std::tie(key, value, effect) < std::tie(o.key, o.value, o.effect); }
+};
+
+// The part of a Solve's compiled form that depends only on the catalogues (identity + seqnum) and the NodePools:
+// the string dictionary, every catalogue SoA, the offering classes and the NodeClaimTemplates (upstream
+// NewScheduler's per-template pre-filter). It is built on a cache miss and kept resident (host + device) in the
+// kp_ctx across Solves, keyed by that fingerprint (R:pkg/providers/instancetype/instancetype.go:225-237 cacheKey:
+// the reference likewise rebuilds its InstanceType list only when a seqnum changes). A Solve whose pods or nodes
+// name a label key or value the dictionary lacks triggers a rebuild that adds them (the dictionary only grows).
+struct SolveBase {
   Dict d;
   int TW = 1, C = 0;
   vector<HostCat> cats;
   vector<OfferClass> classes;
-  // templates (ordered)
-  vector<int> tmpl_nodepool;
+  // templates (weight desc, name asc; pools whose requirements filter out every type are skipped)
+  vector<int> tmpl_nodepool;          // index into kp_solve_in.nodepools
   vector<KReqs> tmpl_reqs;
   vector<int32_t> tmpl_taintset, tmpl_catalog;
   vector<uint64_t> tmpl_X;
-  vector<int64_t> tmpl_daemon, tmpl_remaining;
+  vector<int64_t> tmpl_daemon;
+  vector<vector<TaintT>> tsets;       // the NodePools' taint sets in id order
+  vector<int> np_taintset;            // per input NodePool
+  string key;                         // cache fingerprint
+  // device copy (Solve plans): dict, parsed integers, catalogue SoA + descriptors, templates
+  DevBuf dev;
+  bool on_device = false;
+  size_t o_dict = 0, o_vint = 0, o_cats = 0, o_treqs = 0, o_tts = 0, o_tcat = 0, o_tX = 0, o_tdm = 0;
+  double build_ms = 0;
+};
+
+struct Compiled {
+  std::shared_ptr<SolveBase> B = std::make_shared<SolveBase>();
+  bool base_hit = false;              // the base came from the ctx cache
   vector<uint32_t> tmpl_limit_present;
+  vector<int64_t> tmpl_remaining;
   // shapes
   vector<int32_t> shape_level_base, shape_nlevels;
   vector<KReqs> shape_reqs;
@@ -1057,19 +1124,13 @@ std::map<string, string> LabelMap(const kp_label* l, uint32_t n) {
   return m;
 }
 
-struct TaintT {
-  string key, value;
-  int effect;
-  bool operator<(const TaintT& o) const { return std::tie(key, value, effect) < std::tie(o.key, o.value, o.effect); }
-};
-
 // Topology spread groups (upstream NewTopology / TopologyGroup / countDomains / buildDomainGroups), in the
 // device encoding: one group per distinct (key, maxSkew, namespace, selector, node filter, policies) in order
 // of first appearance over the pods; dictionary-key groups keep a count per value ordinal + a registered-
 // domain mask, hostname groups a saturating u8 count per node (existing positions, then NodeClaims).
 int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector<RawReqs>>& strict_levels,
                         const vector<vector<vector<int>>>& spread_levels, const vector<int>& np_taintset) {
-  const Dict& d = cp.d;
+  const Dict& d = cp.B->d;
   const int E = (int)cp.ex_input.size();
   cp.tkey_slot.assign(KP_MAX_KEYS, -1);
   cp.shape_rec_base.assign(in->n_shapes, 0);
@@ -1106,7 +1167,7 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
     };
     for (uint32_t i = 0; i < in->n_nodepools; i++) {
       const kp_nodepool& np = in->nodepools[i];
-      const HostCat& hc = cp.cats[np.catalog];
+      const HostCat& hc = cp.B->cats[np.catalog];
       if (hc.T == 0) continue;
       RawReqs base_raw = ParseReqs(np.requirements);
       RawReqs l = LabelReqs(np.labels, np.n_labels, false);
@@ -1350,28 +1411,74 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
   return KP_OK;
 }
 
-int32_t CompileSolve(const kp_solve_in* in, Compiled& cp) {
-  if (in->n_catalogs == 0 || !in->catalogs) return fail(KP_E_INVAL, "no catalogues");
-  vector<const kp_catalog*> cats(in->catalogs, in->catalogs + in->n_catalogs);
-  DictBuilder db;
-  int maxT = 1;
-  for (auto* c : cats) {
-    if (!c) return fail(KP_E_INVAL, "null catalogue");
-    maxT = std::max(maxT, (int)c->types.size());
-    for (auto& t : c->types) {
-      db.addReqs(t.reqs);
-      for (auto& o : t.offs) {
-        db.addLabel(kCapType, o.ct);
-        if (o.has_zone) db.addLabel(kZone, o.zone);
-        if (o.has_zid) db.addLabel(kZoneID, o.zid);
-      }
-    }
+// Inputs of one Solve that are not part of its SolveBase: the pods' relaxation levels, node labels, spread keys.
+struct SolveRaw {
+  vector<RawReqs> np_reqs;                        // per input NodePool (requirements + labels + nodepool key)
+  vector<vector<TaintT>> np_taints;
+  vector<vector<RawReqs>> levels, strict_levels;  // per shape: NewPodRequirements after successive Relax
+  vector<vector<vector<int>>> spread_levels;      // spreads (indices into topology_spread) per level
+  std::set<string> topo_keys;                     // non-hostname spread keys (need a dictionary id)
+  vector<RawReqs> ex_labels;                      // per input existing node (hostname dropped)
+};
+
+void KeyReqs(string& o, const RawReqs& rs) {
+  for (auto& r : rs) {
+    o += r.key + '\x01' + std::to_string(r.op) + '\x01' + std::to_string(r.minv);
+    for (auto& v : r.values) o += '\x02' + v;
+    o += '\x03';
   }
-  db.bounded[kResID];
-  db.bounded[kResType];
-  // NodePools
-  vector<RawReqs> np_reqs(in->n_nodepools);
-  vector<vector<TaintT>> np_taints(in->n_nodepools);
+  o += '\x04';
+}
+
+// Fingerprint of everything a SolveBase depends on: catalogue identities + seqnums, the NodePools.
+string BaseKey(const kp_solve_in* in, const SolveRaw& raw) {
+  string k;
+  for (uint32_t c = 0; c < in->n_catalogs; c++) {
+    const kp_catalog* cat = in->catalogs[c];
+    k += std::to_string(cat->uid) + ":" + std::to_string(cat->seqnum) + ":" + std::to_string(cat->types.size()) + ";";
+  }
+  for (uint32_t i = 0; i < in->n_nodepools; i++) {
+    const kp_nodepool& np = in->nodepools[i];
+    k += string(np.name ? np.name : "") + '\x05' + std::to_string(np.weight) + '\x05' + std::to_string(np.catalog);
+    KeyReqs(k, raw.np_reqs[i]);
+    for (auto& t : raw.np_taints[i]) k += t.key + '\x01' + t.value + '\x01' + std::to_string(t.effect) + '\x02';
+    for (int r = 0; r < KP_NRES; r++)
+      if ((np.daemon_requests.present >> r) & 1) k += std::to_string(r) + "=" + std::to_string(np.daemon_requests.milli[r]) + ",";
+    k += '\x06';
+  }
+  return k;
+}
+
+// Every key / value / bound slot the requirement set needs is already in the dictionary.
+bool Covers(const Dict& d, const RawReqs& rs) {
+  for (auto& r : rs) {
+    const int k = d.key(r.key);
+    if (k < 0) return false;
+    if ((r.op == KP_OP_GT || r.op == KP_OP_LT || r.minv >= 0) && k >= d.dd.KB) return false;
+    if (r.op == KP_OP_IN || r.op == KP_OP_NOT_IN)
+      for (auto& v : r.values)
+        if (d.bit(k, v) < 0) return false;
+  }
+  return true;
+}
+bool BaseCovers(const SolveBase& b, const SolveRaw& raw) {
+  for (auto& lv : raw.levels)
+    for (auto& r : lv)
+      if (!Covers(b.d, r)) return false;
+  for (auto& l : raw.ex_labels)
+    if (!Covers(b.d, l)) return false;
+  for (auto& k : raw.topo_keys)
+    if (b.d.key(k) < 0) return false;
+  return true;
+}
+
+// Parse the NodePools, shapes (relaxation levels) and node labels of a Solve.
+int32_t ParseSolve(const kp_solve_in* in, SolveRaw& raw) {
+  if (in->n_catalogs == 0 || !in->catalogs) return fail(KP_E_INVAL, "no catalogues");
+  for (uint32_t c = 0; c < in->n_catalogs; c++)
+    if (!in->catalogs[c]) return fail(KP_E_INVAL, "null catalogue");
+  raw.np_reqs.resize(in->n_nodepools);
+  raw.np_taints.resize(in->n_nodepools);
   for (uint32_t i = 0; i < in->n_nodepools; i++) {
     const kp_nodepool& np = in->nodepools[i];
     if (np.catalog >= in->n_catalogs) return fail(KP_E_INVAL, "nodepool %u: catalogue %u", i, np.catalog);
@@ -1381,15 +1488,14 @@ int32_t CompileSolve(const kp_solve_in* in, Compiled& cp) {
     r.push_back({kNodePool, KP_OP_IN, {np.name ? np.name : ""}, -1});
     for (auto& x : r)
       if (x.key == kHostname) return fail(KP_E_UNSUPPORTED, "hostname requirement on nodepool");
-    db.addReqs(r);
-    np_reqs[i] = std::move(r);
+    raw.np_reqs[i] = std::move(r);
     for (uint32_t j = 0; j < np.n_taints; j++)
-      np_taints[i].push_back({np.taints[j].key ? np.taints[j].key : "", np.taints[j].value ? np.taints[j].value : "",
-                              np.taints[j].effect});
+      raw.np_taints[i].push_back({np.taints[j].key ? np.taints[j].key : "", np.taints[j].value ? np.taints[j].value : "",
+                                  np.taints[j].effect});
   }
-  // shapes -> relaxation levels (NewPodRequirements after successive Preferences.Relax)
-  vector<vector<RawReqs>> levels(in->n_shapes), strict_levels(in->n_shapes);
-  vector<vector<vector<int>>> spread_levels(in->n_shapes);  // spreads (indices into topology_spread) per level
+  raw.levels.assign(in->n_shapes, {});
+  raw.strict_levels.assign(in->n_shapes, {});
+  raw.spread_levels.assign(in->n_shapes, {});
   for (uint32_t s = 0; s < in->n_shapes; s++) {
     const kp_pod_shape& sh = in->shapes[s];
     if (sh.n_topology_spread && sh.n_required_terms > 1)
@@ -1398,7 +1504,7 @@ int32_t CompileSolve(const kp_solve_in* in, Compiled& cp) {
       const kp_topology_spread& t = sh.topology_spread[j];
       const string key = t.topology_key ? t.topology_key : "";
       if (t.max_skew < 1 || t.max_skew > 250) return fail(KP_E_UNSUPPORTED, "topology spread maxSkew %d", t.max_skew);
-      if (key != kHostname) db.bounded[key];  // the key gets a dictionary id even if no value names it
+      if (key != kHostname) raw.topo_keys.insert(key);  // the key gets a dictionary id even if no value names it
     }
     if (sh.n_preferred_terms > 12) return fail(KP_E_UNSUPPORTED, "> 12 preferred terms");
     RawReqs ns = LabelReqs(sh.node_selector, sh.n_node_selector, false);
@@ -1417,12 +1523,11 @@ int32_t CompileSolve(const kp_solve_in* in, Compiled& cp) {
       if (!req.empty()) r.insert(r.end(), req[0].begin(), req[0].end());
       for (auto& x : r)
         if (x.key == kHostname) return fail(KP_E_UNSUPPORTED, "hostname requirement on pod");
-      db.addReqs(r);
-      levels[s].push_back(std::move(r));
+      raw.levels[s].push_back(std::move(r));
       RawReqs strict = ns;  // NewStrictPodRequirements: without the preferred term
       if (!req.empty()) strict.insert(strict.end(), req[0].begin(), req[0].end());
-      strict_levels[s].push_back(std::move(strict));
-      spread_levels[s].push_back(spreads);
+      raw.strict_levels[s].push_back(std::move(strict));
+      raw.spread_levels[s].push_back(spreads);
       if (req.size() > 1) {
         req.erase(req.begin());
       } else if (!pref.empty()) {
@@ -1436,18 +1541,44 @@ int32_t CompileSolve(const kp_solve_in* in, Compiled& cp) {
       }
     }
   }
-  // existing nodes
-  for (uint32_t i = 0; i < in->n_existing; i++) {
-    const kp_existing_node& e = in->existing[i];
-    for (auto& r : LabelReqs(e.labels, e.n_labels, true)) db.addLabel(r.key, r.values[0]);
+  raw.ex_labels.resize(in->n_existing);
+  for (uint32_t i = 0; i < in->n_existing; i++)
+    raw.ex_labels[i] = LabelReqs(in->existing[i].labels, in->existing[i].n_labels, true);
+  return KP_OK;
+}
+
+// Dictionary (catalogues, NodePools + the values `raw` names), catalogue SoA, offering classes, templates.
+int32_t BuildBase(const kp_solve_in* in, const SolveRaw& raw, SolveBase& b) {
+  auto t0 = std::chrono::steady_clock::now();
+  vector<const kp_catalog*> cats(in->catalogs, in->catalogs + in->n_catalogs);
+  DictBuilder db;
+  int maxT = 1;
+  for (auto* c : cats) {
+    maxT = std::max(maxT, (int)c->types.size());
+    for (auto& t : c->types) {
+      db.addReqs(t.reqs);
+      for (auto& o : t.offs) {
+        db.addLabel(kCapType, o.ct);
+        if (o.has_zone) db.addLabel(kZone, o.zone);
+        if (o.has_zid) db.addLabel(kZoneID, o.zid);
+      }
+    }
   }
-  int32_t rc = db.build(cp.d);
+  db.bounded[kResID];
+  db.bounded[kResType];
+  for (auto& r : raw.np_reqs) db.addReqs(r);
+  for (auto& lv : raw.levels)
+    for (auto& r : lv) db.addReqs(r);
+  for (auto& k : raw.topo_keys) db.bounded[k];
+  for (auto& l : raw.ex_labels)
+    for (auto& r : l) db.addLabel(r.key, r.values[0]);
+  int32_t rc = db.build(b.d);
   if (rc) return rc;
-  const Dict& d = cp.d;
+  const Dict& d = b.d;
   const int TW = (maxT + 63) / 64;
-  cp.TW = TW;
-  cp.d.dd.TW = TW;
-  cp.d.dd.T = maxT;
+  b.TW = TW;
+  b.d.dd.TW = TW;
+  b.d.dd.T = maxT;
   // offering classes
   map<ClassKey, int> classes;
   for (auto* c : cats)
@@ -1460,61 +1591,59 @@ int32_t CompileSolve(const kp_solve_in* in, Compiled& cp) {
         }
       }
   if (classes.size() > KP_MAX_CLASSES) return fail(KP_E_UNSUPPORTED, "%zu offering classes", classes.size());
-  cp.C = (int)classes.size();
-  cp.classes.resize(cp.C);
-  for (auto& kv : classes) cp.classes[kv.second] = {kv.first.ct, kv.first.zone, kv.first.zid, 0};
-  cp.d.dd.C = cp.C;
-  cp.cats.resize(cats.size());
+  b.C = (int)classes.size();
+  b.classes.resize(b.C);
+  for (auto& kv : classes) b.classes[kv.second] = {kv.first.ct, kv.first.zone, kv.first.zid, 0};
+  b.d.dd.C = b.C;
+  b.cats.resize(cats.size());
   uint64_t catalog_keys = 0, multi = 0;
   for (size_t i = 0; i < cats.size(); i++) {
-    rc = CompileCatalog(d, cats[i]->types, TW, classes, cp.cats[i]);
+    rc = CompileCatalog(d, cats[i]->types, TW, classes, b.cats[i]);
     if (rc) return rc;
-    multi |= cp.cats[i].multi_valued;
+    multi |= b.cats[i].multi_valued;
     for (int k = 0; k < d.dd.K; k++) {
-      bool any = false;
-      for (int w = 0; w < TW && !any; w++) any = ~cp.cats[i].NOKEY[(size_t)k * TW + w] != 0;
-      // NOKEY covers every type only if no type has the key; mask padding bits
+      // NOKEY covers every type only if no type has the key (padding bits masked)
       bool all = true;
-      for (int t = 0; t < cp.cats[i].T && all; t++)
-        if (!((cp.cats[i].NOKEY[(size_t)k * TW + t / 64] >> (t % 64)) & 1)) all = false;
+      for (int t = 0; t < b.cats[i].T && all; t++)
+        if (!((b.cats[i].NOKEY[(size_t)k * TW + t / 64] >> (t % 64)) & 1)) all = false;
       if (!all) catalog_keys |= 1ull << k;
-      (void)any;
     }
   }
-  cp.d.dd.catalog_keys = catalog_keys;
-  cp.d.dd.single_valued = catalog_keys & ~multi;
-  for (auto& hc : cp.cats) hc.multi_valued = multi;
-  // taint sets
+  b.d.dd.catalog_keys = catalog_keys;
+  b.d.dd.single_valued = catalog_keys & ~multi;
+  for (auto& hc : b.cats) hc.multi_valued = multi;
+  // the NodePools' taint sets (ids 0.. in input order; a Solve's nodes add theirs after these)
   map<vector<TaintT>, int> tsets;
-  auto tset = [&](vector<TaintT> v) {
+  b.np_taintset.resize(in->n_nodepools);
+  for (uint32_t i = 0; i < in->n_nodepools; i++) {
+    vector<TaintT> v = raw.np_taints[i];
     std::sort(v.begin(), v.end());
     auto it = tsets.find(v);
-    if (it != tsets.end()) return it->second;
-    int id = (int)tsets.size();
-    tsets[v] = id;
-    return id;
-  };
-  vector<int> np_taintset(in->n_nodepools);
-  for (uint32_t i = 0; i < in->n_nodepools; i++) np_taintset[i] = tset(np_taints[i]);
+    if (it == tsets.end()) {
+      it = tsets.emplace(v, (int)b.tsets.size()).first;
+      b.tsets.push_back(v);
+    }
+    b.np_taintset[i] = it->second;
+  }
   // templates: weight desc, name asc; pre-filter options with empty requests (upstream NewScheduler)
   vector<int> order(in->n_nodepools);
   for (uint32_t i = 0; i < in->n_nodepools; i++) order[i] = (int)i;
-  std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
-    const kp_nodepool &x = in->nodepools[a], &y = in->nodepools[b];
-    if (x.weight != y.weight) return x.weight > y.weight;
-    return strcmp(x.name ? x.name : "", y.name ? y.name : "") < 0;
+  std::stable_sort(order.begin(), order.end(), [&](int x, int y) {
+    const kp_nodepool &p = in->nodepools[x], &q = in->nodepools[y];
+    if (p.weight != q.weight) return p.weight > q.weight;
+    return strcmp(p.name ? p.name : "", q.name ? q.name : "") < 0;
   });
   for (int i : order) {
     const kp_nodepool& np = in->nodepools[i];
-    KReqs q = Compile(d, np_reqs[i]);
-    const HostCat& hc = cp.cats[np.catalog];
+    KReqs q = Compile(d, raw.np_reqs[i]);
+    const HostCat& hc = b.cats[np.catalog];
     vector<uint64_t> X(TW, 0);
     for (int t = 0; t < hc.T; t++) X[t / 64] |= 1ull << (t % 64);
     int64_t zero[KP_NRES] = {0};
     HostFilterTypes(d, hc, q, TW, zero, X);
-    const uint64_t cls = HostAllowedClasses(d, q, cp.classes);
+    const uint64_t cls = HostAllowedClasses(d, q, b.classes);
     vector<uint64_t> offer(TW, 0);
-    for (int c = 0; c < cp.C; c++)
+    for (int c = 0; c < b.C; c++)
       if ((cls >> c) & 1)
         for (int w = 0; w < TW; w++) offer[w] |= hc.offer_avail[(size_t)c * TW + w];
     bool any = false;
@@ -1526,29 +1655,50 @@ int32_t CompileSolve(const kp_solve_in* in, Compiled& cp) {
       if (!HostMinValuesOK(d, hc, q, ts)) any = false;
     }
     if (!any) continue;  // "skipping, nodepool requirements filtered out all instance types"
-    cp.tmpl_nodepool.push_back(i);
-    cp.tmpl_reqs.push_back(q);
-    cp.tmpl_taintset.push_back(tset(np_taints[i]));
-    cp.tmpl_catalog.push_back((int32_t)np.catalog);
-    cp.tmpl_X.insert(cp.tmpl_X.end(), X.begin(), X.end());
-    for (int r = 0; r < KP_NRES; r++) {
-      cp.tmpl_daemon.push_back((np.daemon_requests.present >> r) & 1 ? np.daemon_requests.milli[r] : 0);
-      cp.tmpl_remaining.push_back((np.limits.present >> r) & 1 ? np.limits.milli[r] : 0);
-    }
-    cp.tmpl_limit_present.push_back(np.limits.present);
+    b.tmpl_nodepool.push_back(i);
+    b.tmpl_reqs.push_back(q);
+    b.tmpl_taintset.push_back(b.np_taintset[i]);
+    b.tmpl_catalog.push_back((int32_t)np.catalog);
+    b.tmpl_X.insert(b.tmpl_X.end(), X.begin(), X.end());
+    for (int r = 0; r < KP_NRES; r++)
+      b.tmpl_daemon.push_back((np.daemon_requests.present >> r) & 1 ? np.daemon_requests.milli[r] : 0);
+  }
+  b.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return KP_OK;
+}
+
+// Per-Solve half on a SolveBase: taint sets, limits, existing nodes, shapes (levels, PVP rows), topology, queue.
+int32_t CompilePerCall(const kp_solve_in* in, const SolveRaw& raw, Compiled& cp) {
+  const SolveBase& b = *cp.B;
+  const Dict& d = b.d;
+  const int TW = b.TW;
+  map<vector<TaintT>, int> tsets;
+  for (size_t i = 0; i < b.tsets.size(); i++) tsets[b.tsets[i]] = (int)i;
+  auto tset = [&](vector<TaintT> v) {
+    std::sort(v.begin(), v.end());
+    auto it = tsets.find(v);
+    if (it != tsets.end()) return it->second;
+    int id = (int)tsets.size();
+    tsets[v] = id;
+    return id;
+  };
+  for (int np : b.tmpl_nodepool) {
+    const kp_nodepool& p = in->nodepools[np];
+    for (int r = 0; r < KP_NRES; r++) cp.tmpl_remaining.push_back((p.limits.present >> r) & 1 ? p.limits.milli[r] : 0);
+    cp.tmpl_limit_present.push_back(p.limits.present);
   }
   // existing nodes: initialized first, then by name
   vector<int> ex(in->n_existing);
   for (uint32_t i = 0; i < in->n_existing; i++) ex[i] = (int)i;
-  std::stable_sort(ex.begin(), ex.end(), [&](int a, int b) {
-    const kp_existing_node &x = in->existing[a], &y = in->existing[b];
-    if ((x.initialized != 0) != (y.initialized != 0)) return x.initialized != 0;
-    return strcmp(x.name ? x.name : "", y.name ? y.name : "") < 0;
+  std::stable_sort(ex.begin(), ex.end(), [&](int x, int y) {
+    const kp_existing_node &p = in->existing[x], &q = in->existing[y];
+    if ((p.initialized != 0) != (q.initialized != 0)) return p.initialized != 0;
+    return strcmp(p.name ? p.name : "", q.name ? q.name : "") < 0;
   });
   for (int i : ex) {
     const kp_existing_node& e = in->existing[i];
     cp.ex_input.push_back(i);
-    cp.ex_reqs.push_back(Compile(d, LabelReqs(e.labels, e.n_labels, true)));
+    cp.ex_reqs.push_back(Compile(d, raw.ex_labels[i]));
     vector<TaintT> ts;
     for (uint32_t j = 0; j < e.n_taints; j++)
       ts.push_back({e.taints[j].key ? e.taints[j].key : "", e.taints[j].value ? e.taints[j].value : "", e.taints[j].effect});
@@ -1564,7 +1714,7 @@ int32_t CompileSolve(const kp_solve_in* in, Compiled& cp) {
   for (uint32_t s = 0; s < in->n_shapes; s++) {
     const kp_pod_shape& sh = in->shapes[s];
     cp.shape_level_base.push_back(sl);
-    cp.shape_nlevels.push_back((int32_t)levels[s].size());
+    cp.shape_nlevels.push_back((int32_t)raw.levels[s].size());
     for (int r = 0; r < KP_NRES; r++) cp.shape_requests.push_back((sh.requests.present >> r) & 1 ? sh.requests.milli[r] : 0);
     uint64_t tol = 0;
     for (auto& kv : tsets) {
@@ -1584,26 +1734,26 @@ int32_t CompileSolve(const kp_solve_in* in, Compiled& cp) {
       if (all) tol |= 1ull << kv.second;
     }
     cp.shape_tolerates.push_back(tol);
-    for (auto& lv : levels[s]) {
+    for (auto& lv : raw.levels[s]) {
       KReqs q = Compile(d, lv);
       cp.shape_reqs.push_back(q);
       cp.shape_negop.push_back(NegOp(d, q));
       vector<int32_t> slots(KP_MAX_KEYS, 0);
-      for (size_t ci = 0; ci < cp.cats.size(); ci++) {
-        const HostCat& hc = cp.cats[ci];
+      for (size_t ci = 0; ci < b.cats.size(); ci++) {
+        const HostCat& hc = b.cats[ci];
         cp.pvp_base.push_back((int32_t)(cp.pvp.size() / TW));
         int row = 0;
         if (ci == 0) cp.pvp_n.push_back(0);
         for (int k = 0; k < d.dd.K; k++) {
-          if (!((q.present >> k) & 1) || !((cp.d.dd.single_valued >> k) & 1)) continue;
+          if (!((q.present >> k) & 1) || !((d.dd.single_valued >> k) & 1)) continue;
           vector<uint64_t> acc(hc.NOKEY.begin() + (size_t)k * TW, hc.NOKEY.begin() + (size_t)(k + 1) * TW);
           for (int wi = 0, w = kw(d, k, 0); wi < nwords(d, k); wi++, w = wi < nwords(d, k) ? kw(d, k, wi) : 0) {
             uint64_t m = d.dd.validbits[w];
             while (m) {
-              int b = __builtin_ctzll(m);
+              int bb = __builtin_ctzll(m);
               m &= m - 1;
-              if (Has(d, q, k, w * 64 + b))
-                for (int x = 0; x < TW; x++) acc[x] |= hc.TM[(size_t)(w * 64 + b) * TW + x];
+              if (Has(d, q, k, w * 64 + bb))
+                for (int x = 0; x < TW; x++) acc[x] |= hc.TM[(size_t)(w * 64 + bb) * TW + x];
             }
           }
           cp.pvp.insert(cp.pvp.end(), acc.begin(), acc.end());
@@ -1616,7 +1766,7 @@ int32_t CompileSolve(const kp_solve_in* in, Compiled& cp) {
     }
   }
   if (cp.pvp.empty()) cp.pvp.assign(TW, 0);
-  rc = CompileTopology(in, cp, strict_levels, spread_levels, np_taintset);
+  int32_t rc = CompileTopology(in, cp, raw.strict_levels, raw.spread_levels, b.np_taintset);
   if (rc) return rc;
   // pods: Queue order byCPUAndMemoryDescending (cpu desc, memory desc, creation asc, uid asc)
   cp.pod_shape.resize(in->n_pods);
@@ -1626,14 +1776,67 @@ int32_t CompileSolve(const kp_solve_in* in, Compiled& cp) {
     cp.pod_shape[p] = (int32_t)in->pods[p].shape;
     cp.queue[p] = (int32_t)p;
   }
-  std::sort(cp.queue.begin(), cp.queue.end(), [&](int a, int b) {
-    const int64_t* ra = &cp.shape_requests[(size_t)cp.pod_shape[a] * KP_NRES];
-    const int64_t* rb = &cp.shape_requests[(size_t)cp.pod_shape[b] * KP_NRES];
-    if (ra[KP_RES_CPU] != rb[KP_RES_CPU]) return ra[KP_RES_CPU] > rb[KP_RES_CPU];
-    if (ra[KP_RES_MEMORY] != rb[KP_RES_MEMORY]) return ra[KP_RES_MEMORY] > rb[KP_RES_MEMORY];
-    if (in->pods[a].creation_unix != in->pods[b].creation_unix) return in->pods[a].creation_unix < in->pods[b].creation_unix;
-    return in->pods[a].uid_key < in->pods[b].uid_key;
+  // sort keys gathered once (cpu, memory of the pod's shape): the comparator then touches one array
+  struct QKey {
+    int64_t cpu, mem, creation;
+    uint64_t uid;
+  };
+  vector<QKey> qk(in->n_pods);
+  for (uint32_t p = 0; p < in->n_pods; p++) {
+    const int64_t* r = &cp.shape_requests[(size_t)cp.pod_shape[p] * KP_NRES];
+    qk[p] = {r[KP_RES_CPU], r[KP_RES_MEMORY], in->pods[p].creation_unix, in->pods[p].uid_key};
+  }
+  std::sort(cp.queue.begin(), cp.queue.end(), [&](int x, int y) {
+    const QKey &p = qk[x], &q = qk[y];
+    if (p.cpu != q.cpu) return p.cpu > q.cpu;
+    if (p.mem != q.mem) return p.mem > q.mem;
+    if (p.creation != q.creation) return p.creation < q.creation;
+    return p.uid < q.uid;
   });
+  return KP_OK;
+}
+
+// Compile a Solve. With a ctx, the SolveBase comes from (and goes to) the ctx cache when its fingerprint matches
+// and its dictionary covers the batch; without one (kp_solve_validate) it is always built.
+int32_t CompileSolve(const kp_solve_in* in, Compiled& cp, kp_ctx* cache = nullptr) {
+  SolveRaw raw;
+  int32_t rc = ParseSolve(in, raw);
+  if (rc) return rc;
+  const string key = BaseKey(in, raw);
+  if (cache) {
+    for (size_t i = 0; i < cache->bases.size(); i++) {
+      auto& b = cache->bases[i];
+      if (b->key != key || !BaseCovers(*b, raw)) continue;
+      cp.B = b;
+      cp.base_hit = true;
+      rc = CompilePerCall(in, raw, cp);
+      if (rc == KP_OK) {
+        std::rotate(cache->bases.begin() + i, cache->bases.begin() + i + 1, cache->bases.end());  // most recent last
+        cache->base_hits++;
+        return KP_OK;
+      }
+      if (rc != KP_E_UNSUPPORTED) return rc;
+      break;  // the cached dictionary's extra values may exceed a per-key limit: rebuild for this batch alone
+    }
+  }
+  Compiled fresh;
+  rc = BuildBase(in, raw, *fresh.B);
+  if (rc) return rc;
+  fresh.B->key = key;
+  rc = CompilePerCall(in, raw, fresh);
+  if (rc) return rc;
+  cp = std::move(fresh);
+  if (cache) {
+    cache->base_misses++;
+    for (size_t i = 0; i < cache->bases.size(); i++)
+      if (cache->bases[i]->key == key) {
+        cache->bases.erase(cache->bases.begin() + i);
+        break;
+      }
+    cache->bases.push_back(cp.B);
+    constexpr size_t kMaxBases = 4;
+    if (cache->bases.size() > kMaxBases) cache->bases.erase(cache->bases.begin());
+  }
   return KP_OK;
 }
 
@@ -1643,7 +1846,7 @@ struct CatOffsets {
 };
 
 void PutCatalogs(Blob& blob, const Compiled& cp, vector<CatOffsets>& offs) {
-  for (auto& hc : cp.cats) {
+  for (auto& hc : cp.B->cats) {
     CatOffsets o;
     o.TM = blob.put(hc.TM);
     o.DNE = blob.put(hc.DNE);
@@ -1654,7 +1857,7 @@ void PutCatalogs(Blob& blob, const Compiled& cp, vector<CatOffsets>& offs) {
     o.fit_vals = blob.put(hc.fit_vals);
     o.fit_n = blob.put(hc.fit_n);
     o.fit_mask = blob.put(hc.fit_mask);
-    o.cls = blob.put(cp.classes);
+    o.cls = blob.put(cp.B->classes);
     o.offer = blob.put(hc.offer_avail);
     o.price = blob.put(hc.price);
     o.price_cm = blob.put(hc.price_cm);
@@ -1685,13 +1888,13 @@ vector<DevCatalog> DevCats(uint8_t* base, const Compiled& cp, const vector<CatOf
     c.offer_avail = (const uint64_t*)(base + o.offer);
     c.price = (const double*)(base + o.price);
     c.price_cm = (const double*)(base + o.price_cm);
-    c.price_sub = cp.cats[i].price_sub.empty() ? nullptr : (const double*)(base + o.price_sub);
+    c.price_sub = cp.B->cats[i].price_sub.empty() ? nullptr : (const double*)(base + o.price_sub);
     c.name_rank = (const uint32_t*)(base + o.rank);
     c.code = (const uint16_t*)(base + o.code);
     c.multi = (const uint64_t*)(base + o.multi);
     c.custom_nonneg = (const uint64_t*)(base + o.custom);
-    c.multi_valued = cp.cats[i].multi_valued;
-    c.custom_any = cp.cats[i].custom_any;
+    c.multi_valued = cp.B->cats[i].multi_valued;
+    c.custom_any = cp.B->cats[i].custom_any;
     out.push_back(c);
   }
   return out;
@@ -1706,8 +1909,9 @@ extern "C" {
 struct kp_solve_plan {
   kp_ctx* ctx = nullptr;
   std::unique_ptr<Compiled> cp;
-  DevBuf buf;
+  DevBuf buf;  // per-Solve arena (the catalogue / template part lives in cp->B->dev, shared through the ctx cache)
   SolveArgs a;
+  double catalog_ms = 0;  // SolveBase build time when this prepare missed the cache, else 0
   size_t o_mut = 0, n_mut = 0, o_pristine = 0, o_ver = 0, n_ver = 0, o_fail = 0, n_fail = 0;
   size_t o_stats = 0, o_npods = 0, o_place = 0, o_events = 0, o_nct = 0, o_ncrq = 0, o_opts = 0, o_nrem = 0,
          o_nopt = 0, o_ncr = 0, o_hcnc = 0, n_hcnc = 0;
@@ -1721,6 +1925,36 @@ extern "C" {
 
 // Compile the batch (dictionary, bitsets, catalogue SoA, templates, shapes, queue order) and upload it:
 // after this the whole Solve input is resident in HBM.
+// Upload a SolveBase once (dict, parsed integers, catalogue SoA + descriptors, templates); later Solves on the same
+// catalogues and NodePools point their kernels at this copy.
+static int32_t EnsureBaseOnDevice(kp_ctx* ctx, SolveBase& B) {
+  if (B.on_device) return KP_OK;
+  Compiled view;
+  view.B = std::shared_ptr<SolveBase>(&B, [](SolveBase*) {});  // non-owning: PutCatalogs / DevCats read B
+  Blob blob;
+  B.o_dict = blob.put(&B.d.dd, 1);
+  B.o_vint = blob.put(B.d.vint);
+  vector<CatOffsets> coffs;
+  PutCatalogs(blob, view, coffs);
+  B.o_cats = blob.reserve(sizeof(DevCatalog) * coffs.size());
+  B.o_treqs = blob.put(B.tmpl_reqs);
+  B.o_tts = blob.put(B.tmpl_taintset);
+  B.o_tcat = blob.put(B.tmpl_catalog);
+  B.o_tX = blob.put(B.tmpl_X);
+  B.o_tdm = blob.put(B.tmpl_daemon);
+  HIPCHK(B.dev.alloc(blob.total()));
+  uint8_t* base = (uint8_t*)B.dev.p;
+  vector<DevCatalog> dc = DevCats(base, view, coffs);
+  memcpy(blob.host.data() + B.o_cats, dc.data(), sizeof(DevCatalog) * dc.size());
+  HIPCHK(hipMemcpyAsync(base, blob.host.data(), blob.host.size(), hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  B.on_device = true;
+  return KP_OK;
+}
+
+// Compile the batch and upload it. The catalogue half (SolveBase: dictionary, catalogue SoA, templates) is taken
+// from the ctx cache when the catalogues (identity + seqnum) and NodePools match and the dictionary covers the
+// batch; only the per-Solve half (shapes, existing nodes, topology, queue order) is compiled and uploaded.
 int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out) {
   auto t0 = std::chrono::steady_clock::now();
   if (!ctx || !in || !out) return fail(KP_E_INVAL, "null argument");
@@ -1730,23 +1964,21 @@ int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out
   plan->ctx = ctx;
   plan->cp = std::make_unique<Compiled>();
   Compiled& C = *plan->cp;
-  int32_t rc = CompileSolve(in, C);
+  int32_t rc = CompileSolve(in, C, ctx);
   if (rc) return rc;
-  const Dict& d = C.d;
-  const int TW = C.TW, P = (int)in->n_pods, NT = (int)C.tmpl_reqs.size(), E = (int)C.ex_reqs.size();
+  plan->catalog_ms = C.base_hit ? 0 : C.B->build_ms;
+  rc = EnsureBaseOnDevice(ctx, *C.B);
+  if (rc) return rc;
+  const Dict& d = C.B->d;
+  const int TW = C.B->TW, P = (int)in->n_pods, NT = (int)C.B->tmpl_reqs.size(), E = (int)C.ex_reqs.size();
   const int Pc = std::max(P, 1);
   plan->P = P;
   plan->Pc = Pc;
   plan->max_types = in->max_instance_types;
-  for (auto& q : C.tmpl_reqs) plan->any_min |= q.hmin != 0;
+  for (auto& q : C.B->tmpl_reqs) plan->any_min |= q.hmin != 0;
   for (auto& q : C.shape_reqs) plan->any_min |= q.hmin != 0;
 
   Blob blob;
-  const size_t o_dict = blob.put(&C.d.dd, 1);
-  const size_t o_vint = blob.put(C.d.vint);
-  vector<CatOffsets> coffs;
-  PutCatalogs(blob, C, coffs);
-  const size_t o_cats = blob.reserve(sizeof(DevCatalog) * coffs.size());
   const size_t o_pod_shape = blob.put(C.pod_shape);
   const size_t o_slb = blob.put(C.shape_level_base);
   const size_t o_snl = blob.put(C.shape_nlevels);
@@ -1758,11 +1990,6 @@ int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out
   const size_t o_pvpb = blob.put(C.pvp_base);
   const size_t o_pvps = blob.put(C.pvp_slot);
   const size_t o_pvpn = blob.put(C.pvp_n);
-  const size_t o_treqs = blob.put(C.tmpl_reqs);
-  const size_t o_tts = blob.put(C.tmpl_taintset);
-  const size_t o_tcat = blob.put(C.tmpl_catalog);
-  const size_t o_tX = blob.put(C.tmpl_X);
-  const size_t o_tdm = blob.put(C.tmpl_daemon);
   const size_t o_tlp = blob.put(C.tmpl_limit_present);
   const size_t o_exts = blob.put(C.ex_taintset);
   const size_t o_exav = blob.put(C.ex_available);
@@ -1777,8 +2004,8 @@ int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out
   uint32_t rmask = 0;
   for (size_t i = 0; i < C.shape_requests.size(); i++)
     if (C.shape_requests[i] > 0) rmask |= 1u << (i % KP_NRES);
-  for (size_t i = 0; i < C.tmpl_daemon.size(); i++)
-    if (C.tmpl_daemon[i] > 0) rmask |= 1u << (i % KP_NRES);
+  for (size_t i = 0; i < C.B->tmpl_daemon.size(); i++)
+    if (C.B->tmpl_daemon[i] > 0) rmask |= 1u << (i % KP_NRES);
   vector<uint8_t> ex_static(std::max(E, 1), 0);  // unrequested resources of an existing node never change
   for (int e = 0; e < E; e++) {
     bool ok = true;
@@ -1804,61 +2031,69 @@ int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out
   const size_t o_hcx = blob.put(C.hcnt0);
   const size_t n_mut = blob.host.size() - o_mut;
   const size_t host_bytes = blob.host.size();
-  const size_t o_pristine = blob.reserve(n_mut);
+  const size_t o_pristine = blob.reserve_dev(n_mut);
   // ---- device-only regions ----
-  const size_t o_ncr = blob.reserve(sizeof(KReqs) * Pc);
-  const size_t o_ncX = blob.reserve(sizeof(uint64_t) * (size_t)Pc * TW);
-  const size_t o_ncrq = blob.reserve(sizeof(int64_t) * (size_t)Pc * KP_NRES);
-  const size_t o_nct = blob.reserve(sizeof(int32_t) * Pc);
-  const size_t o_npods = blob.reserve(sizeof(int32_t) * Pc);
-  const size_t o_order = blob.reserve(sizeof(int32_t) * Pc);
-  const size_t o_maxalloc = blob.reserve(sizeof(int64_t) * (size_t)Pc * KP_NRES);
-  const size_t o_fitj = blob.reserve(sizeof(int32_t) * (size_t)Pc * KP_NRES);
-  const size_t o_ncts = blob.reserve(sizeof(int32_t) * (size_t)Pc);
-  const size_t o_nccat = blob.reserve(sizeof(int32_t) * (size_t)Pc);
-  const size_t o_place = blob.reserve(sizeof(int32_t) * Pc);
-  const size_t o_events = blob.reserve(sizeof(int32_t) * Pc);
-  const size_t o_stats = blob.reserve(sizeof(uint64_t) * 24);
+  const size_t o_ncr = blob.reserve_dev(sizeof(KReqs) * Pc);
+  const size_t o_ncX = blob.reserve_dev(sizeof(uint64_t) * (size_t)Pc * TW);
+  const size_t o_ncrq = blob.reserve_dev(sizeof(int64_t) * (size_t)Pc * KP_NRES);
+  const size_t o_nct = blob.reserve_dev(sizeof(int32_t) * Pc);
+  const size_t o_npods = blob.reserve_dev(sizeof(int32_t) * Pc);
+  const size_t o_order = blob.reserve_dev(sizeof(int32_t) * Pc);
+  const size_t o_maxalloc = blob.reserve_dev(sizeof(int64_t) * (size_t)Pc * KP_NRES);
+  const size_t o_fitj = blob.reserve_dev(sizeof(int32_t) * (size_t)Pc * KP_NRES);
+  const size_t o_ncts = blob.reserve_dev(sizeof(int32_t) * (size_t)Pc);
+  const size_t o_nccat = blob.reserve_dev(sizeof(int32_t) * (size_t)Pc);
+  const size_t o_place = blob.reserve_dev(sizeof(int32_t) * Pc);
+  const size_t o_events = blob.reserve_dev(sizeof(int32_t) * Pc);
+  const size_t o_stats = blob.reserve_dev(sizeof(uint64_t) * 24);
   // failure memo (see SolveArgs): versions start at 0, memo entries at -1
   const size_t SLn = std::max<size_t>(1, C.shape_reqs.size());
   const int ncc = (int)std::min<size_t>((size_t)Pc, std::max<size_t>(1, ((size_t)256 << 20) / (4 * SLn)));
-  const size_t o_ver0 = blob.reserve(0);
-  const size_t o_ncver = blob.reserve(sizeof(int32_t) * Pc);
-  const size_t o_exver = blob.reserve(sizeof(int32_t) * std::max(E, 1));
-  const size_t o_tver = blob.reserve(sizeof(int32_t) * std::max(NT, 1));
-  const size_t o_curnc = blob.reserve(sizeof(int32_t) * 2 * SLn);  // cursors start at {0, 0} (zeroed per run)
-  const size_t o_curex = blob.reserve(sizeof(int32_t) * 2 * SLn);
-  const size_t n_ver = blob.host.size() - o_ver0;
-  const size_t o_fail0 = blob.reserve(0);
-  const size_t o_ncfail = blob.reserve(sizeof(int32_t) * SLn * ncc);
-  const size_t o_exfail = blob.reserve(sizeof(int32_t) * SLn * std::max(E, 1));
-  const size_t o_tfail = blob.reserve(sizeof(int32_t) * SLn * std::max(NT, 1));
-  const size_t n_fail = blob.host.size() - o_fail0;
+  const size_t o_ver0 = blob.reserve_dev(0);
+  const size_t o_ncver = blob.reserve_dev(sizeof(int32_t) * Pc);
+  const size_t o_exver = blob.reserve_dev(sizeof(int32_t) * std::max(E, 1));
+  const size_t o_tver = blob.reserve_dev(sizeof(int32_t) * std::max(NT, 1));
+  const size_t o_curnc = blob.reserve_dev(sizeof(int32_t) * 2 * SLn);  // cursors start at {0, 0} (zeroed per run)
+  const size_t o_curex = blob.reserve_dev(sizeof(int32_t) * 2 * SLn);
+  const size_t n_ver = blob.total() - o_ver0;
+  const size_t o_fail0 = blob.reserve_dev(0);
+  const size_t o_ncfail = blob.reserve_dev(sizeof(int32_t) * SLn * ncc);
+  const size_t o_exfail = blob.reserve_dev(sizeof(int32_t) * SLn * std::max(E, 1));
+  const size_t o_tfail = blob.reserve_dev(sizeof(int32_t) * SLn * std::max(NT, 1));
+  const size_t n_fail = blob.total() - o_fail0;
   const int opt_stride = in->max_instance_types ? (int)in->max_instance_types : std::max(1, d.dd.T);
-  const size_t o_opts = blob.reserve(sizeof(uint32_t) * (size_t)Pc * opt_stride);
-  const size_t o_nrem = blob.reserve(sizeof(uint32_t) * Pc);
-  const size_t o_nopt = blob.reserve(sizeof(uint32_t) * Pc);
+  const size_t o_opts = blob.reserve_dev(sizeof(uint32_t) * (size_t)Pc * opt_stride);
+  const size_t o_nrem = blob.reserve_dev(sizeof(uint32_t) * Pc);
+  const size_t o_nopt = blob.reserve_dev(sizeof(uint32_t) * Pc);
   const size_t n_hcnc = (size_t)C.GH * Pc;
-  const size_t o_hcnc = blob.reserve(std::max<size_t>(n_hcnc, 1));
-  const size_t o_nctc = blob.reserve(std::max<size_t>((size_t)C.TK * Pc, 1));
-  const size_t total_bytes = blob.host.size();
+  const size_t o_hcnc = blob.reserve_dev(std::max<size_t>(n_hcnc, 1));
+  const size_t o_nctc = blob.reserve_dev(std::max<size_t>((size_t)C.TK * Pc, 1));
+  const size_t total_bytes = blob.total();
 
-  HIPCHK(hipMalloc(&plan->buf.p, total_bytes));
-  uint8_t* base = (uint8_t*)plan->buf.p;
-  {
-    vector<DevCatalog> dc = DevCats(base, C, coffs);
-    memcpy(blob.host.data() + o_cats, dc.data(), sizeof(DevCatalog) * dc.size());
+  // the per-Solve arena: reuse the ctx's spare allocation when it is large enough
+  if (ctx->spare && ctx->spare_bytes >= total_bytes) {
+    plan->buf.p = ctx->spare;
+    plan->buf.n = ctx->spare_bytes;
+    ctx->spare = nullptr;
+    ctx->spare_bytes = 0;
+  } else {
+    if (ctx->spare) HIPCHK(hipFree(ctx->spare));
+    ctx->spare = nullptr;
+    ctx->spare_bytes = 0;
+    HIPCHK(plan->buf.alloc(total_bytes));
   }
+  uint8_t* base = (uint8_t*)plan->buf.p;
+  uint8_t* cbase = (uint8_t*)C.B->dev.p;
   HIPCHK(hipMemcpyAsync(base, blob.host.data(), host_bytes, hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(hipMemcpyAsync(base + o_pristine, base + o_mut, n_mut, hipMemcpyDeviceToDevice, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
 
   SolveArgs& a = plan->a;
   memset(&a, 0, sizeof a);
-  a.dict = (const DevDict*)(base + o_dict);
-  a.cats = (const DevCatalog*)(base + o_cats);
-  a.n_catalogs = (int32_t)coffs.size();
-  a.vint = (const int64_t*)(base + o_vint);
+  a.dict = (const DevDict*)(cbase + C.B->o_dict);
+  a.cats = (const DevCatalog*)(cbase + C.B->o_cats);
+  a.n_catalogs = (int32_t)C.B->cats.size();
+  a.vint = (const int64_t*)(cbase + C.B->o_vint);
   a.n_pods = P;
   a.pod_shape = (const int32_t*)(base + o_pod_shape);
   a.pod_level = (int32_t*)(base + o_pod_level);
@@ -1876,11 +2111,11 @@ int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out
   a.pvp_slot = (const int32_t*)(base + o_pvps);
   a.sl_pvp_n = (const int32_t*)(base + o_pvpn);
   a.n_tmpl = NT;
-  a.tmpl_reqs = base + o_treqs;
-  a.tmpl_taintset = (const int32_t*)(base + o_tts);
-  a.tmpl_catalog = (const int32_t*)(base + o_tcat);
-  a.tmpl_X = (const uint64_t*)(base + o_tX);
-  a.tmpl_daemon = (const int64_t*)(base + o_tdm);
+  a.tmpl_reqs = cbase + C.B->o_treqs;
+  a.tmpl_taintset = (const int32_t*)(cbase + C.B->o_tts);
+  a.tmpl_catalog = (const int32_t*)(cbase + C.B->o_tcat);
+  a.tmpl_X = (const uint64_t*)(cbase + C.B->o_tX);
+  a.tmpl_daemon = (const int64_t*)(cbase + C.B->o_tdm);
   a.tmpl_limit_present = (const uint32_t*)(base + o_tlp);
   a.tmpl_remaining = (int64_t*)(base + o_trem);
   a.n_existing = E;
@@ -1913,8 +2148,8 @@ int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out
   a.req_res_mask = 0;
   for (size_t i = 0; i < C.shape_requests.size(); i++)
     if (C.shape_requests[i] > 0) a.req_res_mask |= 1u << (i % KP_NRES);
-  for (size_t i = 0; i < C.tmpl_daemon.size(); i++)  // Fits iterates every resource of the merged requests
-    if (C.tmpl_daemon[i] > 0) a.req_res_mask |= 1u << (i % KP_NRES);
+  for (size_t i = 0; i < C.B->tmpl_daemon.size(); i++)  // Fits iterates every resource of the merged requests
+    if (C.B->tmpl_daemon[i] > 0) a.req_res_mask |= 1u << (i % KP_NRES);
   a.n_req_res = __builtin_popcount(a.req_res_mask);
   a.timing = getenv("KP_TIMING") ? 1 : 0;
   a.n_groups = C.G;
@@ -1978,7 +2213,16 @@ int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out
 
 void kp_solve_plan_destroy(kp_solve_plan* p) {
   if (!p) return;
-  (void)hipSetDevice(p->ctx->device);
+  kp_ctx* ctx = p->ctx;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  (void)hipSetDevice(ctx->device);
+  if (p->buf.p && p->buf.n >= ctx->spare_bytes) {  // keep the larger arena for the next prepare
+    if (ctx->spare) (void)hipFree(ctx->spare);
+    ctx->spare = p->buf.p;
+    ctx->spare_bytes = p->buf.n;
+    p->buf.p = nullptr;
+    p->buf.n = 0;
+  }
   delete p;
 }
 
@@ -1990,7 +2234,7 @@ int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out) {
   std::lock_guard<std::mutex> lock(ctx->mu);
   HIPCHK(hipSetDevice(ctx->device));
   const Compiled& C = *plan->cp;
-  const Dict& d = C.d;
+  const Dict& d = C.B->d;
   uint8_t* base = (uint8_t*)plan->buf.p;
   const int P = plan->P, Pc = plan->Pc, opt_stride = plan->opt_stride;
   hipStream_t st = ctx->stream;
@@ -2068,7 +2312,7 @@ int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out) {
   }
   for (int i = 0; i < n_nc; i++) {
     auto& nc = res->ncs[i];
-    nc.nodepool = (uint32_t)C.tmpl_nodepool[nct[i]];
+    nc.nodepool = (uint32_t)C.B->tmpl_nodepool[nct[i]];
     nc.n_remaining = nrem[i];
     memset(&nc.requests, 0, sizeof nc.requests);
     for (int r = 0; r < KP_NRES; r++) {
@@ -2079,7 +2323,7 @@ int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out) {
     nc.reqs = DecodeReqs(d, fin[i]);
     // Truncate(reqs, max): minValues must still hold on the truncated options, else the pods fail
     if (!fin.empty() && (fin[i].hmin & fin[i].present)) {
-      const HostCat& hc = C.cats[C.tmpl_catalog[nct[i]]];
+      const HostCat& hc = C.B->cats[C.B->tmpl_catalog[nct[i]]];
       vector<int> ts(nc.options.begin(), nc.options.end());
       if (!HostMinValuesOK(d, hc, fin[i], ts)) {
         for (uint32_t p : nc.pods) res->placement[p] = -1;
@@ -2095,6 +2339,8 @@ int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out) {
   res->stats.bytes_algorithmic = stats[1];
   res->stats.pops = stats[2];
   res->stats.prepare_ms = plan->prepare_ms;
+  res->stats.catalog_ms = plan->catalog_ms;
+  res->stats.catalog_cached = plan->cp->base_hit ? 1 : 0;
   for (int i = 0; i < 8; i++) res->stats.phase_cycles[i] = stats[8 + i];
   res->stats.scanned = stats[5];
   res->stats.cursor_starts = stats[6];
@@ -2167,13 +2413,13 @@ int32_t CompileQueries(const kp_catalog* cat, const vector<RawReqs>& qs, Compile
   db.bounded[kResID];
   db.bounded[kResType];
   for (auto& q : qs) db.addReqs(q);
-  int32_t rc = db.build(cp.d);
+  int32_t rc = db.build(cp.B->d);
   if (rc) return rc;
   const int T = (int)cat->types.size(), TW = std::max(1, (T + 63) / 64);
-  cp.d.dd.T = T;
-  cp.d.dd.TW = TW;
+  cp.B->d.dd.T = T;
+  cp.B->d.dd.TW = TW;
   map<ClassKey, int> classes;
-  const Dict& d = cp.d;
+  const Dict& d = cp.B->d;
   for (auto& t : cat->types)
     for (auto& o : t.offs) {
       ClassKey ck{d.bit(d.key(kCapType), o.ct), o.has_zone ? d.bit(d.key(kZone), o.zone) : -1, o.has_zid ? d.bit(d.key(kZoneID), o.zid) : -1};
@@ -2183,19 +2429,19 @@ int32_t CompileQueries(const kp_catalog* cat, const vector<RawReqs>& qs, Compile
       }
     }
   if (classes.size() > KP_MAX_CLASSES) return fail(KP_E_UNSUPPORTED, "%zu offering classes", classes.size());
-  cp.C = (int)classes.size();
-  cp.d.dd.C = cp.C;
-  cp.classes.resize(cp.C);
-  for (auto& kv : classes) cp.classes[kv.second] = {kv.first.ct, kv.first.zone, kv.first.zid, 0};
-  cp.cats.resize(1);
-  rc = CompileCatalog(d, cat->types, TW, classes, cp.cats[0]);
+  cp.B->C = (int)classes.size();
+  cp.B->d.dd.C = cp.B->C;
+  cp.B->classes.resize(cp.B->C);
+  for (auto& kv : classes) cp.B->classes[kv.second] = {kv.first.ct, kv.first.zone, kv.first.zid, 0};
+  cp.B->cats.resize(1);
+  rc = CompileCatalog(d, cat->types, TW, classes, cp.B->cats[0]);
   if (rc) return rc;
   uint64_t catalog_keys = 0;
   for (int k = 0; k < d.dd.K; k++)
     for (int t = 0; t < T; t++)
-      if (!((cp.cats[0].NOKEY[(size_t)k * TW + t / 64] >> (t % 64)) & 1)) catalog_keys |= 1ull << k;
-  cp.d.dd.catalog_keys = catalog_keys;
-  cp.d.dd.single_valued = catalog_keys & ~cp.cats[0].multi_valued;
+      if (!((cp.B->cats[0].NOKEY[(size_t)k * TW + t / 64] >> (t % 64)) & 1)) catalog_keys |= 1ull << k;
+  cp.B->d.dd.catalog_keys = catalog_keys;
+  cp.B->d.dd.single_valued = catalog_keys & ~cp.B->cats[0].multi_valued;
   qreqs.assign(std::max<size_t>(qs.size(), 1), KReqs{});
   for (size_t i = 0; i < qs.size(); i++) qreqs[i] = Compile(d, qs[i]);
   return KP_OK;
@@ -2209,10 +2455,12 @@ static int32_t RefreshOfferings(kp_ctx* ctx, const kp_catalog* cat, Compiled& cp
   std::lock_guard<std::mutex> lock(ctx->mu);
   HIPCHK(hipSetDevice(ctx->device));
   map<ClassKey, int> classes;
-  for (int c = 0; c < cp.C; c++) classes[{cp.classes[c].ct_bit, cp.classes[c].zone_bit, cp.classes[c].zid_bit}] = c;
-  HostCat& hc = cp.cats[0];
+  for (int c = 0; c < cp.B->C; c++) classes[{cp.B->classes[c].ct_bit, cp.B->classes[c].zone_bit, cp.B->classes[c].zid_bit}] = c;
+  HostCat hc;  // filled aside: the plan's host copy changes only once the device copy did
+  hc.T = cp.B->cats[0].T;
+  hc.S = cp.B->cats[0].S;
   try {
-    FillOfferings(cp.d, cat->types, cp.TW, classes, hc);
+    FillOfferings(cp.B->d, cat->types, cp.B->TW, classes, hc);
   } catch (const std::out_of_range&) {
     return fail(KP_E_INVAL, "refresh: an offering outside the plan's offering classes");
   }
@@ -2225,6 +2473,11 @@ static int32_t RefreshOfferings(kp_ctx* ctx, const kp_catalog* cat, Compiled& cp
   HIPCHK(hipMemcpyAsync(base + coff.price_sub, hc.price_sub.data(), hc.price_sub.size() * sizeof(double),
                         hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
+  HostCat& dst = cp.B->cats[0];
+  dst.offer_avail.swap(hc.offer_avail);
+  dst.price.swap(hc.price);
+  dst.price_cm.swap(hc.price_cm);
+  dst.price_sub.swap(hc.price_sub);
   return KP_OK;
 }
 
@@ -2238,6 +2491,7 @@ struct kp_filter_plan {
   bool cheapest = false;
   double prepare_ms = 0;
   const kp_catalog* cat = nullptr;  // kp_filter_refresh: catalogue, compiled form and its offering offsets
+  uint64_t seqnum = 0;              // catalogue seqnum the resident offerings reflect
   Compiled cp;
   CatOffsets coff{};
 };
@@ -2265,8 +2519,8 @@ int32_t kp_filter_prepare(kp_ctx* ctx, const kp_catalog* cat, const kp_feasibili
     for (int r = 0; r < KP_NRES; r++)
       qrq[(size_t)i * KP_NRES + r] = (queries[i].requests.present >> r) & 1 ? queries[i].requests.milli[r] : 0;
   Blob blob;
-  const size_t o_dict = blob.put(&cp.d.dd, 1);
-  const size_t o_vint = blob.put(cp.d.vint);
+  const size_t o_dict = blob.put(&cp.B->d.dd, 1);
+  const size_t o_vint = blob.put(cp.B->d.vint);
   vector<CatOffsets> coffs;
   PutCatalogs(blob, cp, coffs);
   const size_t o_cats = blob.reserve(sizeof(DevCatalog));
@@ -2299,6 +2553,7 @@ int32_t kp_filter_prepare(kp_ctx* ctx, const kp_catalog* cat, const kp_feasibili
   plan->tiles = tiles;
   plan->cheapest = with_cheapest != 0;
   plan->cat = cat;
+  plan->seqnum = cat->seqnum;
   plan->coff = coffs[0];
   plan->cp = std::move(cp);
   plan->prepare_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -2313,6 +2568,9 @@ int32_t kp_filter_run(kp_filter_plan* plan, uint64_t* out_mask, double* out_chea
   if (out_cheapest && !plan->cheapest) return fail(KP_E_INVAL, "plan was prepared without cheapest prices");
   kp_ctx* ctx = plan->ctx;
   std::lock_guard<std::mutex> lock(ctx->mu);
+  if (plan->cat->seqnum != plan->seqnum)  // R:instancetype.go:225-237: a changed seqnum invalidates the offerings
+    return fail(KP_E_INVAL, "stale plan: catalogue seqnum %llu, plan built at %llu (kp_filter_refresh)",
+                (unsigned long long)plan->cat->seqnum, (unsigned long long)plan->seqnum);
   HIPCHK(hipSetDevice(ctx->device));
   uint8_t* base = (uint8_t*)plan->buf.p;
   const uint32_t n = plan->n_queries;
@@ -2342,7 +2600,9 @@ int32_t kp_filter_refresh(kp_filter_plan* plan, const kp_catalog* cat) {
   if (!plan || !cat) return fail(KP_E_INVAL, "null argument");
   if (cat != plan->cat || (int)cat->types.size() != plan->T)
     return fail(KP_E_INVAL, "kp_filter_refresh: the plan was prepared on another catalogue");
-  return RefreshOfferings(plan->ctx, cat, plan->cp, plan->coff, (uint8_t*)plan->buf.p);
+  const int32_t rc = RefreshOfferings(plan->ctx, cat, plan->cp, plan->coff, (uint8_t*)plan->buf.p);
+  if (rc == KP_OK) plan->seqnum = cat->seqnum;
+  return rc;
 }
 
 void kp_filter_plan_destroy(kp_filter_plan* p) {
@@ -2374,6 +2634,8 @@ struct kp_launch_plan {
   size_t o_out = 0, o_types = 0, o_ovr = 0, o_stats = 0;
   double prepare_ms = 0;
   const kp_catalog* cat = nullptr;  // kp_launch_refresh
+  uint64_t seqnum = 0;              // catalogue seqnum the resident offerings reflect
+  int T = 0;
   Compiled cp;
   CatOffsets coff{};
 };
@@ -2419,8 +2681,8 @@ int32_t kp_launch_prepare(kp_ctx* ctx, const kp_catalog* cat, const kp_launch_re
   vector<KReqs> qreqs;
   int32_t rc = CompileQueries(cat, qs, cp, qreqs);
   if (rc) return rc;
-  const Dict& d = cp.d;
-  const int TW = cp.d.dd.TW, C = cp.C;
+  const Dict& d = cp.B->d;
+  const int TW = cp.B->d.dd.TW, C = cp.B->C;
   vector<int64_t> qrq((size_t)std::max<uint32_t>(n, 1) * KP_NRES, 0);
   for (uint32_t i = 0; i < n; i++)
     for (int r = 0; r < KP_NRES; r++)
@@ -2445,7 +2707,7 @@ int32_t kp_launch_prepare(kp_ctx* ctx, const kp_catalog* cat, const kp_launch_re
   vector<uint8_t> ofs_cls((size_t)T * MO, 0xFF);
   const int kct = d.key(kCapType), kz = d.key(kZone), kzid = d.key(kZoneID);
   std::map<ClassKey, int> cls_id;
-  for (int c = 0; c < C; c++) cls_id[ClassKey{cp.classes[c].ct_bit, cp.classes[c].zone_bit, cp.classes[c].zid_bit}] = c;
+  for (int c = 0; c < C; c++) cls_id[ClassKey{cp.B->classes[c].ct_bit, cp.B->classes[c].zone_bit, cp.B->classes[c].zid_bit}] = c;
   for (int t = 0; t < T; t++) {
     int j = 0;
     for (auto& o : cat->types[t].offs) {
@@ -2457,17 +2719,17 @@ int32_t kp_launch_prepare(kp_ctx* ctx, const kp_catalog* cat, const kp_launch_re
   uint64_t cls_spot = 0, cls_od = 0;
   vector<int8_t> cls_zone(std::max(C, 1), -1);
   for (int c = 0; c < C; c++) {
-    if (spot_bit >= 0 && cp.classes[c].ct_bit == spot_bit) cls_spot |= 1ull << c;
-    if (od_bit >= 0 && cp.classes[c].ct_bit == od_bit) cls_od |= 1ull << c;
+    if (spot_bit >= 0 && cp.B->classes[c].ct_bit == spot_bit) cls_spot |= 1ull << c;
+    if (od_bit >= 0 && cp.B->classes[c].ct_bit == od_bit) cls_od |= 1ull << c;
     for (uint32_t z = 0; z < n_subnet_zones; z++)
-      if (kz >= 0 && cp.classes[c].zone_bit >= 0 && subnet_zones[z] && d.bit(kz, subnet_zones[z]) == cp.classes[c].zone_bit) {
+      if (kz >= 0 && cp.B->classes[c].zone_bit >= 0 && subnet_zones[z] && d.bit(kz, subnet_zones[z]) == cp.B->classes[c].zone_bit) {
         cls_zone[c] = (int8_t)z;
         break;
       }
   }
   Blob blob;
-  const size_t o_dict = blob.put(&cp.d.dd, 1);
-  const size_t o_vint = blob.put(cp.d.vint);
+  const size_t o_dict = blob.put(&cp.B->d.dd, 1);
+  const size_t o_vint = blob.put(cp.B->d.vint);
   vector<CatOffsets> coffs;
   PutCatalogs(blob, cp, coffs);
   const size_t o_cats = blob.reserve(sizeof(DevCatalog));
@@ -2520,6 +2782,8 @@ int32_t kp_launch_prepare(kp_ctx* ctx, const kp_catalog* cat, const kp_launch_re
   plan->max_types = max_types;
   plan->ovr_stride = ovr_stride;
   plan->cat = cat;
+  plan->seqnum = cat->seqnum;
+  plan->T = T;
   plan->coff = coffs[0];
   plan->cp = std::move(cp);
   plan->prepare_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -2535,6 +2799,9 @@ int32_t kp_launch_run(kp_launch_plan* plan, kp_launch_result* out, uint32_t* out
   if (!plan) return fail(KP_E_INVAL, "null argument");
   kp_ctx* ctx = plan->ctx;
   std::lock_guard<std::mutex> lock(ctx->mu);
+  if (plan->cat->seqnum != plan->seqnum)
+    return fail(KP_E_INVAL, "stale plan: catalogue seqnum %llu, plan built at %llu (kp_launch_refresh)",
+                (unsigned long long)plan->cat->seqnum, (unsigned long long)plan->seqnum);
   HIPCHK(hipSetDevice(ctx->device));
   uint8_t* base = (uint8_t*)plan->buf.p;
   const uint32_t n = plan->n;
@@ -2569,8 +2836,11 @@ int32_t kp_launch_run(kp_launch_plan* plan, kp_launch_result* out, uint32_t* out
 // the subnet-zone classes do not change with availability or price).
 int32_t kp_launch_refresh(kp_launch_plan* plan, const kp_catalog* cat) {
   if (!plan || !cat) return fail(KP_E_INVAL, "null argument");
-  if (cat != plan->cat) return fail(KP_E_INVAL, "kp_launch_refresh: the plan was prepared on another catalogue");
-  return RefreshOfferings(plan->ctx, cat, plan->cp, plan->coff, (uint8_t*)plan->buf.p);
+  if (cat != plan->cat || (int)cat->types.size() != plan->T)
+    return fail(KP_E_INVAL, "kp_launch_refresh: the plan was prepared on another catalogue");
+  const int32_t rc = RefreshOfferings(plan->ctx, cat, plan->cp, plan->coff, (uint8_t*)plan->buf.p);
+  if (rc == KP_OK) plan->seqnum = cat->seqnum;
+  return rc;
 }
 
 void kp_launch_plan_destroy(kp_launch_plan* p) {
@@ -2667,8 +2937,8 @@ int32_t kp_cluster_prepare(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan** 
   in.max_instance_types = 100;
   int32_t rc = CompileSolve(&in, C);
   if (rc) return rc;
-  const Dict& d = C.d;
-  const int TW = C.TW, E = N, EW = (E + 63) / 64, SL = (int)C.shape_reqs.size(), NT = (int)C.tmpl_reqs.size();
+  const Dict& d = C.B->d;
+  const int TW = C.B->TW, E = N, EW = (E + 63) / 64, SL = (int)C.shape_reqs.size(), NT = (int)C.B->tmpl_reqs.size();
   const int T = d.dd.T, K = d.dd.K;
   for (uint32_t lp : C.tmpl_limit_present)
     if (lp) return fail(KP_E_UNSUPPORTED, "NodePool limits in consolidation simulations");
@@ -2752,8 +3022,8 @@ int32_t kp_cluster_prepare(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan** 
   const int ctk = d.key(kCapType);
 
   Blob blob;
-  const size_t o_dict = blob.put(&C.d.dd, 1);
-  const size_t o_vint = blob.put(C.d.vint);
+  const size_t o_dict = blob.put(&C.B->d.dd, 1);
+  const size_t o_vint = blob.put(C.B->d.vint);
   vector<CatOffsets> coffs;
   PutCatalogs(blob, C, coffs);
   const size_t o_cats = blob.reserve(sizeof(DevCatalog) * coffs.size());
@@ -2767,14 +3037,14 @@ int32_t kp_cluster_prepare(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan** 
   const size_t o_pvp = blob.put(C.pvp);
   const size_t o_pvpb = blob.put(C.pvp_base);
   const size_t o_pvps = blob.put(C.pvp_slot);
-  vector<int32_t> tmpl_np(C.tmpl_nodepool.begin(), C.tmpl_nodepool.end());
+  vector<int32_t> tmpl_np(C.B->tmpl_nodepool.begin(), C.B->tmpl_nodepool.end());
   if (tmpl_np.empty()) tmpl_np.push_back(0);
-  const size_t o_treqs = blob.put(C.tmpl_reqs);
-  const size_t o_tts = blob.put(C.tmpl_taintset);
-  const size_t o_tcat = blob.put(C.tmpl_catalog);
+  const size_t o_treqs = blob.put(C.B->tmpl_reqs);
+  const size_t o_tts = blob.put(C.B->tmpl_taintset);
+  const size_t o_tcat = blob.put(C.B->tmpl_catalog);
   const size_t o_tnp = blob.put(tmpl_np);
-  const size_t o_tX = blob.put(C.tmpl_X);
-  const size_t o_tdm = blob.put(C.tmpl_daemon);
+  const size_t o_tX = blob.put(C.B->tmpl_X);
+  const size_t o_tdm = blob.put(C.B->tmpl_daemon);
   const size_t o_excode = blob.put(ex_code);
   const size_t o_exts = blob.put(C.ex_taintset);
   const size_t o_exav = blob.put(C.ex_available);
@@ -2789,8 +3059,8 @@ int32_t kp_cluster_prepare(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan** 
   uint32_t rmask = 0;
   for (size_t i = 0; i < C.shape_requests.size(); i++)
     if (C.shape_requests[i] > 0) rmask |= 1u << (i % KP_NRES);
-  for (size_t i = 0; i < C.tmpl_daemon.size(); i++)
-    if (C.tmpl_daemon[i] > 0) rmask |= 1u << (i % KP_NRES);
+  for (size_t i = 0; i < C.B->tmpl_daemon.size(); i++)
+    if (C.B->tmpl_daemon[i] > 0) rmask |= 1u << (i % KP_NRES);
   vector<uint8_t> ex_static(std::max(E, 1), 0);  // unrequested resources of an existing node never change
   for (int e = 0; e < E; e++) {
     bool ok = true;
@@ -2873,8 +3143,8 @@ int32_t kp_cluster_prepare(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan** 
   a.req_res_mask = 0;
   for (size_t i = 0; i < C.shape_requests.size(); i++)
     if (C.shape_requests[i] > 0) a.req_res_mask |= 1u << (i % KP_NRES);
-  for (size_t i = 0; i < C.tmpl_daemon.size(); i++)
-    if (C.tmpl_daemon[i] > 0) a.req_res_mask |= 1u << (i % KP_NRES);
+  for (size_t i = 0; i < C.B->tmpl_daemon.size(); i++)
+    if (C.B->tmpl_daemon[i] > 0) a.req_res_mask |= 1u << (i % KP_NRES);
   a.RU = 0;
   for (int r = 0; r < KP_NRES; r++)
     if ((a.req_res_mask >> r) & 1) a.ru_res[a.RU++] = (int8_t)r;

@@ -219,14 +219,26 @@ class Scheduler:
         self.problem = problem
         self.catalogs = catalogs or [Catalog(ctx, c) for c in problem.catalogs]
 
-    def solve(self):
+    def solve_in(self):
+        """The kp_solve_in of this batch (marshalled once; the C ABI owns nothing of it)."""
+        if getattr(self, "_si", None) is None:
+            self._arena = Arena()
+            self._si = abi.build_solve_in(self._arena, self.problem, catalog_handles=[c.h.value for c in self.catalogs])
+        return self._si
+
+    def solve(self, read=True):
+        """kp_solve: compile the per-Solve half (the catalogue half comes resident from the ctx cache after the first
+        Solve on these catalogues + NodePools), upload, run, copy the results back. read=False returns stats only."""
         lib = self.ctx.lib
-        arena = Arena()
-        si = abi.build_solve_in(arena, self.problem, catalog_handles=[c.h.value for c in self.catalogs])
+        si = self.solve_in()
         res = C.c_void_p()
         _check(lib, lib.kp_solve(self.ctx.h, C.byref(si), C.byref(res)))
         try:
-            return read_result(lib, res, self.problem.n_pods)
+            if read:
+                return read_result(lib, res, self.problem.n_pods)
+            st = abi.SolveStats()
+            lib.kp_result_stats(res, C.byref(st))
+            return {"stats": stats_dict(st)}
         finally:
             lib.kp_result_destroy(res)
 

@@ -160,7 +160,8 @@ class SolveStats(C.Structure):
     _fields_ = [("device_ms", C.c_double), ("host_ms", C.c_double), ("prepare_ms", C.c_double),
                 ("solve_kernel_ms", C.c_double), ("finalize_kernel_ms", C.c_double), ("attempts", C.c_uint64),
                 ("bytes_algorithmic", C.c_uint64), ("pops", C.c_uint64), ("phase_cycles", C.c_uint64 * 8),
-                ("scanned", C.c_uint64), ("cursor_starts", C.c_uint64), ("attempt_cycles", C.c_uint64 * 8)]
+                ("scanned", C.c_uint64), ("cursor_starts", C.c_uint64), ("attempt_cycles", C.c_uint64 * 8),
+                ("catalog_ms", C.c_double), ("catalog_cached", C.c_uint32), ("reserved_", C.c_uint32)]
 
 
 class Options(C.Structure):

@@ -5,7 +5,9 @@ CS3 and R:website/content/en/preview/concepts/disruption.md:89-128):
   SingleNodeConsolidation.compute_command   the first candidate (disruption-cost order) whose
                                             computeConsolidation is not a no-op
   MultiNodeConsolidation.first_n_option     firstNConsolidationOption's binary search over prefixes
-                                            candidates[0:mid+1], lo=1, hi=min(len-1, 99); every prefix
+                                            candidates[0:mid+1], lo=1, hi = len-1 if len <= 100 else 100
+                                            (ComputeCommand passes max = Clamp(len, 0, MaxParallel=100) and
+                                            firstN lowers it to len-1 only when len <= max); every prefix
                                             the search can touch is simulated in ONE batch, then the
                                             search is replayed exactly over those results
   sweep(...)                                the config-4 sweep: many subsets sharded over ranks, best
@@ -35,21 +37,31 @@ class SingleNodeConsolidation:
 
 
 class MultiNodeConsolidation:
-    MAX_CANDIDATES = 100
+    MAX_PARALLEL = 100  # upstream MultiNodeConsolidation MaxParallel
 
     def __init__(self, plan):
         self.plan = plan
 
     @staticmethod
+    def search_hi(n):
+        """firstNConsolidationOption's initial max: ComputeCommand passes Clamp(n, 0, 100); if n <= max it becomes
+        n - 1 (so with more than 100 candidates the search can reach the 101-candidate prefix)."""
+        mx = min(max(n, 0), MultiNodeConsolidation.MAX_PARALLEL)
+        return n - 1 if n <= mx else mx
+
+    @staticmethod
     def search_prefixes(n):
         """Every mid the binary search can evaluate (prefix length mid+1)."""
-        lo, hi = 1, min(n - 1, MultiNodeConsolidation.MAX_CANDIDATES - 1)
-        return list(range(lo, hi + 1)) if hi >= lo else []
+        if n < 2:
+            return []
+        return list(range(1, MultiNodeConsolidation.search_hi(n) + 1))
 
     @staticmethod
     def replay(n, results_by_mid):
         """firstNConsolidationOption over precomputed computeConsolidation(candidates[0:mid+1]) results."""
-        lo, hi = 1, min(n - 1, MultiNodeConsolidation.MAX_CANDIDATES - 1)
+        if n < 2:
+            return None
+        lo, hi = 1, MultiNodeConsolidation.search_hi(n)
         best = None
         while lo <= hi:
             mid = (lo + hi) // 2

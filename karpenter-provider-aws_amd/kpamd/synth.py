@@ -606,3 +606,46 @@ def random_launch_requests(catalog, n, seed):
                 rng.shuffle(lst)
         out.append((reqs, res, [int(t) for t in lst]))
     return out
+
+
+# ------------------------------------------------------------------------------------------------
+# feasibility rows: distinct (requirements, requests) queries (SURVEY §8d unit = one (pod shape, type) pair)
+# ------------------------------------------------------------------------------------------------
+def distinct_queries(catalog, n, seed=8):
+    """n pairwise-distinct CompatibleAvailableFilter rows, the requirement mixes of deployments in a large cluster:
+    zone / capacity-type / category / arch / cpu bounds / GPU / family constraints and cpu-memory(-GPU) requests.
+    Distinctness is exact (a row repeats no other row's requirements + requests)."""
+    rng = np.random.default_rng(seed)
+    fams = sorted({r[2][0] for it in catalog for r in it.requirements if r[0] == K + "instance-family" and r[2]})
+    cats = ["c", "m", "r", "t", "g", "p", "x", "i", "z", "d"]
+    seen, out = set(), []
+    while len(out) < n:
+        reqs = []
+        if rng.random() < 0.35:
+            reqs.append(("topology.kubernetes.io/zone", "In", sorted(rng.choice(ZONES, size=int(rng.integers(1, 3)), replace=False).tolist())))
+        if rng.random() < 0.5:
+            reqs.append(("karpenter.sh/capacity-type", "In", sorted(rng.choice(["spot", "on-demand"], size=int(rng.integers(1, 3)), replace=False).tolist())))
+        if rng.random() < 0.5:
+            reqs.append((K + "instance-category", "In" if rng.random() < 0.8 else "NotIn",
+                         sorted(rng.choice(cats, size=int(rng.integers(1, 4)), replace=False).tolist())))
+        if rng.random() < 0.3:
+            reqs.append(("kubernetes.io/arch", "In", [str(rng.choice(["amd64", "arm64"]))]))
+        if rng.random() < 0.3:
+            reqs.append((K + "instance-cpu", "Gt", [str(int(rng.choice([1, 3, 7, 15, 31])))]))
+        if rng.random() < 0.2:
+            reqs.append((K + "instance-cpu", "Lt", [str(int(rng.choice([8, 17, 33, 65, 97])))]))
+        if rng.random() < 0.15:
+            reqs.append((K + "instance-generation", "Gt", [str(int(rng.integers(2, 7)))]))
+        if rng.random() < 0.1 and fams:
+            reqs.append((K + "instance-family", "In", sorted(rng.choice(fams, size=int(rng.integers(2, 16)), replace=False).tolist())))
+        if rng.random() < 0.1:
+            reqs.append((K + "instance-gpu-manufacturer", "DoesNotExist", []))
+        res = req_res(int(rng.integers(1, 400)) * 50, int(rng.integers(1, 512)) * 64)
+        if rng.random() < 0.05:
+            res["nvidia.com/gpu"] = 1000 * int(rng.choice([1, 2, 4]))
+        key = (tuple((k, op, tuple(v)) for k, op, v in reqs), tuple(sorted(res.items())))
+        if key in seen:
+            continue
+        seen.add(key)
+        out.append((reqs, res))
+    return out

@@ -66,7 +66,8 @@ def test_first_n_replay():
     assert mid == 12 and r["decision"] == DELETE
     by_mid = {m: {"decision": REPLACE, "n_options": 0} for m in M.search_prefixes(n)}  # no options left
     assert M.replay(n, by_mid) is None
-    assert M.search_prefixes(1) == [] and M.search_prefixes(300)[-1] == 99
+    assert M.search_prefixes(1) == [] and M.search_prefixes(300)[-1] == 100  # prefix of 101 candidates
+    assert M.search_prefixes(100)[-1] == 99 and M.search_prefixes(101)[-1] == 100 and M.search_prefixes(2) == [1]
 
 
 def test_random_subsets_csr():

@@ -102,6 +102,8 @@ def test_filter_refresh_equals_rebuilt_plan(ctx, lib, catalog):
     k0, c0, _ = fp.run(read=True)
     cat.update_offerings([(t, ct, z, False) for ct, t, z in MARKS], seqnum=2)
     assert cat.seqnum() == 2
+    with pytest.raises(kpamd.KPError, match="stale plan"):  # offerings changed: the plan must be refreshed first
+        fp.run(read=True)
     fp.refresh(cat)
     k1, c1, _ = fp.run(read=True)
     names = [it.name for it in catalog]
@@ -147,6 +149,8 @@ def test_launch_refresh_equals_rebuilt_catalogue(ctx, lib, catalog):
     plan = kpamd.LaunchPlan(ctx, cat, reqs, kc.ZONES)
     before, _ = plan.run(read=True)
     cat.update_offerings([(t, ct, z, False) for ct, t, z in marks], seqnum=2)
+    with pytest.raises(kpamd.KPError, match="stale plan"):
+        plan.run(read=True)
     plan.refresh(cat)
     got, _ = plan.run(read=True)
     names = [it.name for it in catalog]
@@ -157,4 +161,41 @@ def test_launch_refresh_equals_rebuilt_catalogue(ctx, lib, catalog):
         assert g == w, f"request {i}: device {g} vs oracle {w}"
     assert got != before  # the marks moved some launches (overrides or capacity type)
     plan.close()
+    cat.close()
+
+
+@pytest.mark.gpu
+def test_solve_catalogue_resident_across_seqnums(ctx, lib, catalog):
+    """The Solve's compiled catalogue half stays resident in the kp_ctx across Solves (same catalogue identity,
+    seqnum and NodePools: catalog_cached = 1) and is rebuilt when an ICE mark bumps the seqnum
+    (R:pkg/providers/instancetype/instancetype.go:225-237 cacheKey; R:pkg/cache/unavailableofferings.go:66-92);
+    every Solve equals the oracle on the catalogue as it is at that moment."""
+    import kpamd
+    from kpamd import catalog as kc
+    from kpamd import synth
+    from oracle import pyoracle
+    its = copy.deepcopy(catalog)
+    cat = kpamd.Catalog(ctx, its, seqnum=1)
+    prob = synth.config2(its, n_pods=600, seed=23)
+    sched = kpamd.Scheduler(ctx, prob, catalogs=[cat])
+    first = sched.solve()
+    second = sched.solve()
+    assert second["stats"]["catalog_cached"] == 1
+    want = pyoracle.solve(prob)
+    for got in (first, second):
+        assert (got["placement"] == want["placement"]).all()
+        assert [(n["nodepool"], n["pods"], n["options"]) for n in got["nodeclaims"]] == \
+            [(n["nodepool"], n["pods"], n["options"]) for n in want["nodeclaims"]]
+    marks = [("spot", t, z) for t in range(0, len(its), 2) for z in kc.ZONES[:2]] + \
+            [("on-demand", t, "test-zone-1a") for t in range(len(its))]
+    cat.update_offerings([(t, ct, z, False) for ct, t, z in marks], seqnum=2)
+    third = sched.solve()
+    assert third["stats"]["catalog_cached"] == 0
+    names = [it.name for it in catalog]
+    rebuilt = kc.build_catalog(lib, unavailable=frozenset((ct, names[t], z) for ct, t, z in marks))
+    want = pyoracle.solve(synth.config2(rebuilt, n_pods=600, seed=23))
+    assert (third["placement"] == want["placement"]).all()
+    assert [(n["nodepool"], n["pods"], n["options"]) for n in third["nodeclaims"]] == \
+        [(n["nodepool"], n["pods"], n["options"]) for n in want["nodeclaims"]]
+    assert [n["options"] for n in third["nodeclaims"]] != [n["options"] for n in first["nodeclaims"]]
     cat.close()
