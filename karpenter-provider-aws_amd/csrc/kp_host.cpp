@@ -2418,6 +2418,7 @@ int32_t CompileQueries(const kp_catalog* cat, const vector<RawReqs>& qs, Compile
   const int T = (int)cat->types.size(), TW = std::max(1, (T + 63) / 64);
   cp.B->d.dd.T = T;
   cp.B->d.dd.TW = TW;
+  cp.B->TW = TW;  // FillOfferings (kp_*_refresh) lays the offering masks out with it
   map<ClassKey, int> classes;
   const Dict& d = cp.B->d;
   for (auto& t : cat->types)

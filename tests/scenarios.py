@@ -1,0 +1,184 @@
+"""Reference provisioning scenarios — TEST INFRASTRUCTURE.
+
+The reference's behavioural tests drive Scheduler.Solve end to end: ExpectProvisioned (Solve + the launch of each
+NodeClaim through CloudProvider.Create) against the fake EC2 API, whose CreateFleet fails the capacity pools listed in
+InsufficientCapacityPools; the instance provider then marks those offerings unavailable (the ICE cache) and the next
+ExpectProvisioned solves again on the re-injected offerings. This module restates that loop over either backend:
+
+  backend "device"  Solve on the GPU (kp_solve), launch selection on the GPU (kp_launch_prepare/run), ICE marks
+                    through kp_catalog_update_offerings on the resident catalogue
+  backend "oracle"  the CPU restatement (oracle/liboracle.so) for all three
+
+Sources restated here:
+  fake CreateFleet            R:pkg/fake/ec2api.go:137-199 (ICE'd overrides skipped and reported; an instance is
+                              created from Overrides[0] when any override was not ICE'd)
+  ICE cache                   R:pkg/cache/unavailableofferings.go:66-92 (MarkUnavailable per (type, zone, capacity type))
+  fake 16-type catalogue      R:pkg/fake/zz_generated.describe_instance_types.go (offering zones extracted to
+                              tests/golden/fake_offerings.tsv by tests/golden/make_fake_catalog.py; EC2 facts from the
+                              committed docs-derived table karpenter-provider-aws_amd/data/ec2_instance_types.tsv)
+  fake.MakeInstances          R:pkg/fake/utils.go:185-214 (uniform 2 vCPU / 8 GiB types, 3 ENIs x 10 IPv4, named from
+                              the static price table, offered in test-zone-1a only: MakeInstanceOfferings :238-249)
+  test pricing                R:pkg/providers/pricing/pricing.go:156-170 (spot falls back to the type's default price
+                              until the first spot update; after UpdateSpotPricing only the zones in the history price)
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+K = "karpenter.k8s.aws/"
+
+
+def _fake_offering_zones():
+    zones = {}
+    for line in open(os.path.join(HERE, "golden", "fake_offerings.tsv")):
+        if line.startswith("#") or line.startswith("instance_type"):
+            continue
+        t, z = line.rstrip("\n").split("\t")
+        zones.setdefault(t, []).append(z)
+    return zones
+
+
+def _resolve(lib, row, zones, spot_price, offering_zones):
+    from kpamd import abi, catalog
+    from kpamd.model import InstanceType
+    arena = abi.Arena()
+    opts = catalog.default_options()
+    nc = catalog.nodeclass(arena)
+    info = catalog.ec2_info(arena, row)
+    cap, ovh = abi.ResourceList(), abi.ResourceList()
+    assert lib.kp_instance_type_resolve(C.byref(opts), C.byref(info), C.byref(nc), C.byref(cap), C.byref(ovh)) == 0
+    reqs = catalog.compute_requirements(row, offering_zones=offering_zones)
+    priced = {(row["name"], z): spot_price.get((row["name"], z), 0.0) for z in catalog.ZONES}
+    offs = catalog.create_offerings(row, reqs, priced, catalog.ZONES, catalog.ZONE_IDS)
+    for o in offs:  # a spot offering without a spot price has no price (createOfferings: hasPrice false)
+        if o.capacity_type == "spot" and (row["name"], o.zone) not in spot_price:
+            o.available = False
+    return InstanceType(row["name"], reqs, catalog.resource_dict(cap), catalog.resource_dict(ovh), offs)
+
+
+def fake_catalog(lib):
+    """The 16-type fake EC2 catalogue with its offering zones; on-demand prices from the static table, spot = the
+    default price (no spot update in the instancetype suite)."""
+    from kpamd import catalog
+    zones = _fake_offering_zones()
+    rows = [r for r in catalog.load_ec2_table() if r["name"] in zones]
+    out = []
+    for r in rows:
+        z = [x for x in zones[r["name"]] if x in catalog.ZONES]
+        spot = {(r["name"], x): r["od_price"] for x in z}
+        out.append(_resolve(lib, r, catalog.ZONES, spot, z))
+    return out
+
+
+def uniform_instances(lib, names, vcpus, spot_prices):
+    """fake.MakeInstances() narrowed by MakeUniqueInstancesAndFamilies, with per-type vCPU overrides, offered in
+    test-zone-1a only, spot priced by UpdateSpotPricing in test-zone-1a (R:pkg/cloudprovider/suite_test.go:352-377)."""
+    from kpamd import catalog
+    table = {r["name"]: r for r in catalog.load_ec2_table()}
+    out = []
+    for name, v, sp in zip(names, vcpus, spot_prices):
+        base = table[name]
+        row = dict(base)
+        row.update(vcpu=v, memory_mib=8192, arch="amd64", max_enis=3, ipv4_per_eni=10, gpu_name="", gpu_manufacturer="",
+                   gpu_count=0, gpu_memory_mib="", accel_name="", accel_manufacturer="", accel_count=0, neuron_devices=0,
+                   neuron_cores_per_device=0, efa=0, local_nvme_gb="")
+        out.append(_resolve(lib, row, catalog.ZONES, {(name, "test-zone-1a"): sp}, ["test-zone-1a"]))
+    return out
+
+
+def pods_of(shapes_counts, seed=0):
+    """(shape index per pod, creation, uid): distinct creation seconds keep the queue order = submission order
+    among equal requests."""
+    shape = np.concatenate([np.full(n, i, dtype=np.uint32) for i, n in enumerate(shapes_counts)]) \
+        if shapes_counts else np.zeros(0, dtype=np.uint32)
+    n = len(shape)
+    creation = (1_750_000_000 + np.arange(n)).astype(np.int64)
+    uid = np.arange(1, n + 1, dtype=np.uint64)
+    return shape, creation, uid
+
+
+class Env:
+    """One test environment: a catalogue (resident on the device for backend "device"), the fake EC2 API's
+    InsufficientCapacityPools, and ExpectProvisioned."""
+
+    def __init__(self, backend, types, ctx=None, ice_pools=()):
+        self.backend = backend
+        self.types = types
+        self.ice = set(ice_pools)  # (capacity type, instance type name, zone)
+        self.ctx = ctx
+        self.seq = 1
+        self.cat = None
+        if backend == "device":
+            import kpamd
+            self.cat = kpamd.Catalog(ctx, types, seqnum=self.seq)
+        self.names = [t.name for t in types]
+
+    def close(self):
+        if self.cat is not None:
+            self.cat.close()
+            self.cat = None
+
+    def _solve(self, prob):
+        if self.backend == "device":
+            import kpamd
+            return kpamd.Scheduler(self.ctx, prob, catalogs=[self.cat]).solve()
+        from oracle import pyoracle
+        return pyoracle.solve(prob)
+
+    def _launch(self, reqs):
+        from kpamd import catalog
+        if not reqs:
+            return []
+        if self.backend == "device":
+            import kpamd
+            plan = kpamd.LaunchPlan(self.ctx, self.cat, reqs, catalog.ZONES)
+            try:
+                out, _ = plan.run(read=True)
+            finally:
+                plan.close()
+            return out
+        from oracle import pyoracle
+        return pyoracle.launch_select(self.types, reqs, catalog.ZONES)
+
+    def mark_unavailable(self, pools):
+        """UnavailableOfferings.MarkUnavailable for each (capacity type, type name, zone): SeqNum bump + re-inject."""
+        if not pools:
+            return
+        idx = {n: i for i, n in enumerate(self.names)}
+        self.seq += 1
+        if self.backend == "device":
+            self.cat.update_offerings([(idx[t], ct, z, False) for ct, t, z in pools], seqnum=self.seq)
+        else:
+            for ct, t, z in pools:
+                for o in self.types[idx[t]].offerings:
+                    if o.capacity_type == ct and o.zone == z:
+                        o.available = False
+
+    def provision(self, pools, shapes, counts):
+        """ExpectProvisioned: Solve, then Create every NodeClaim through the fake CreateFleet. Returns the launched
+        nodes [{"type", "zone", "capacity_type", "pods", "overrides"}] and, per pod, the index of its node or None."""
+        import kpamd
+        from kpamd.model import Problem
+        s, c, u = pods_of(counts)
+        prob = Problem([self.types], pools, shapes, s, c, u, name="scenario")
+        res = self._solve(prob)
+        launches = self._launch(kpamd.launch_requests_from_solve(res))
+        nodes, pod_node, iced = [], [None] * prob.n_pods, []
+        for nc, lr in zip(res["nodeclaims"], launches):
+            if lr["status"] != 0:
+                continue
+            ct = lr["capacity_type"]
+            overrides = [(self.names[t], z) for t, z in lr["overrides"]]
+            hit = [(ct, t, z) for t, z in overrides if (ct, t, z) in self.ice]
+            iced += hit
+            if len(hit) == len(overrides):  # every override ICE'd: CreateFleet fails, the pods stay pending
+                continue
+            t0, z0 = overrides[0]  # the fake builds the instance from Overrides[0] (R:pkg/fake/ec2api.go:188-199)
+            for p in nc["pods"]:
+                pod_node[p] = len(nodes)
+            nodes.append({"type": t0, "zone": z0, "capacity_type": ct, "pods": list(nc["pods"]),
+                          "overrides": overrides, "options": [self.names[t] for t in nc["options"]]})
+        self.mark_unavailable(sorted(set(iced)))
+        return nodes, pod_node

@@ -16,7 +16,8 @@ import pytest
 
 # (capacity type, type index, zone) marks; type indices into the 919-type catalogue
 MARKS = [("spot", 0, "test-zone-1a"), ("on-demand", 0, "test-zone-1b"), ("spot", 5, "test-zone-1c"),
-         ("on-demand", 17, "test-zone-1a"), ("spot", 17, "test-zone-1a"), ("on-demand", 300, "test-zone-1c")]
+         ("on-demand", 17, "test-zone-1a"), ("spot", 17, "test-zone-1a"), ("on-demand", 300, "test-zone-1c"),
+         ("spot", 700, "test-zone-1b"), ("on-demand", 900, "test-zone-1a"), ("spot", 900, "test-zone-1a")]
 
 
 def _host_catalog(lib, its):
