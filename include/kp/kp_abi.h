@@ -314,6 +314,9 @@ typedef struct kp_solve_stats {
                                NodeClaimTemplates); 0 when it came resident from the kp_ctx cache */
   uint32_t catalog_cached;  /* 1: the catalogue half was resident (same catalogues + seqnums + NodePools) */
   uint32_t reserved_;
+  uint64_t fast_pods;       /* pods placed by solve_kernel's single-wave fast lane (no requirement merge) */
+  uint64_t fast_cycles[6];  /* diagnostic (KP_TIMING=1): fast-lane cycles: pop, stage, sort, pre-pass, attempts, commit */
+  uint64_t slow_sorts;      /* sort.Slice replays that ran the literal pdqsort (no stable-move shortcut) */
 } kp_solve_stats;
 
 /* ---- context ---------------------------------------------------------------------------- */

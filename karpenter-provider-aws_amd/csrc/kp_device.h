@@ -110,7 +110,8 @@ struct SolveArgs {
   // outputs
   int32_t* placement;                // [P]
   int32_t* events;                   // [P] pods in placement order
-  uint64_t* stats;                   // [8]: attempts, bytes, pops, n_nc, n_events
+  uint64_t* stats;                   // [32]: attempts, bytes, pops, n_nc, n_events, scanned, starts; [8..15] phases,
+                                     // [16..23] attempt split, [24] fast-lane pods, [25..30] fast-lane cycles
 };
 
 struct FinalizeArgs {

@@ -2045,7 +2045,7 @@ int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out
   const size_t o_nccat = blob.reserve_dev(sizeof(int32_t) * (size_t)Pc);
   const size_t o_place = blob.reserve_dev(sizeof(int32_t) * Pc);
   const size_t o_events = blob.reserve_dev(sizeof(int32_t) * Pc);
-  const size_t o_stats = blob.reserve_dev(sizeof(uint64_t) * 24);
+  const size_t o_stats = blob.reserve_dev(sizeof(uint64_t) * 32);
   // failure memo (see SolveArgs): versions start at 0, memo entries at -1
   const size_t SLn = std::max<size_t>(1, C.shape_reqs.size());
   const int ncc = (int)std::min<size_t>((size_t)Pc, std::max<size_t>(1, ((size_t)256 << 20) / (4 * SLn)));
@@ -2239,7 +2239,7 @@ int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out) {
   const int P = plan->P, Pc = plan->Pc, opt_stride = plan->opt_stride;
   hipStream_t st = ctx->stream;
   HIPCHK(hipMemcpyAsync(base + plan->o_mut, base + plan->o_pristine, plan->n_mut, hipMemcpyDeviceToDevice, st));
-  HIPCHK(hipMemsetAsync(base + plan->o_stats, 0, sizeof(uint64_t) * 24, st));
+  HIPCHK(hipMemsetAsync(base + plan->o_stats, 0, sizeof(uint64_t) * 32, st));
   HIPCHK(hipMemsetAsync(base + plan->o_npods, 0, sizeof(int32_t) * Pc, st));
   HIPCHK(hipMemsetAsync(base + plan->o_place, 0xFF, sizeof(int32_t) * Pc, st));
   HIPCHK(hipMemsetAsync(base + plan->o_ver, 0, plan->n_ver, st));
@@ -2250,9 +2250,11 @@ int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out) {
   HIPCHK(hipEventRecord(ctx->ev0, st));
   HIPCHK(launch_solve(a, 8, dyn, st));
   HIPCHK(hipEventRecord(ctx->ev1, st));
-  uint64_t stats[24];
+  uint64_t stats[32];
   HIPCHK(hipMemcpyAsync(stats, base + plan->o_stats, sizeof stats, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  if (stats[7]) return fail(KP_E_DEVICE, "solve_kernel exceeded its Queue.Pop bound (%llu pops): aborted",
+                            (unsigned long long)stats[2]);
   const int n_nc = (int)stats[3];
   FinalizeArgs f;
   f.dict = a.dict;
@@ -2345,6 +2347,9 @@ int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out) {
   res->stats.scanned = stats[5];
   res->stats.cursor_starts = stats[6];
   for (int i = 0; i < 8; i++) res->stats.attempt_cycles[i] = stats[16 + i];
+  res->stats.fast_pods = stats[24];
+  res->stats.slow_sorts = stats[31];
+  for (int i = 0; i < 6; i++) res->stats.fast_cycles[i] = stats[25 + i];
   res->stats.host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   *out = res.release();
   return KP_OK;

@@ -21,6 +21,9 @@
 #include "kp_model.h"
 
 #define LANE ((int)(threadIdx.x & 63))
+#ifndef FASTLANE
+#define FASTLANE 1  // solve_kernel: wave-0 fast lane for merge-free placements (0 = full path only)
+#endif
 // Explicit address spaces: LDS data reached through a pointer would otherwise be read with FLAT loads (which wait
 // on the vector-memory counter too and take the long path); global rows get global_load.
 #define LDS __attribute__((address_space(3)))
@@ -390,24 +393,33 @@ struct RowBatch {
   uint32_t endm;          // bit i: row i closes a group
   uint64_t acc;
 };
+// Rows are loaded four at a time (one batch of independent loads per group): a step with few rows (the usual
+// 3-6) executes one group instead of a fully unrolled RL_CAP-slot body.
 __device__ __forceinline__ void rl_flush(RowBatch& L, uint64_t& X, int TW) {
   if (L.n == 0) return;
   wave_sync();
   const int lane = LANE;
-  uint64_t w[RL_CAP];
-#pragma unroll
-  for (int i = 0; i < RL_CAP; i++) {
-    w[i] = 0;
-    if (i < L.n && lane < TW) w[i] = L.rows[i][lane];
-  }
-#pragma unroll
-  for (int i = 0; i < RL_CAP; i++) {
-    if (i < L.n) {
-      L.acc |= w[i];
-      if ((L.endm >> i) & 1) {
-        X &= L.acc;
-        L.acc = 0;
-      }
+  const bool lv = lane < TW;
+  for (int g = 0; g < L.n; g += 4) {
+    const int m = L.n - g;
+    const uint64_t w0 = lv ? L.rows[g][lane] : 0;
+    const uint64_t w1 = (m > 1 && lv) ? L.rows[g + 1][lane] : 0;
+    const uint64_t w2 = (m > 2 && lv) ? L.rows[g + 2][lane] : 0;
+    const uint64_t w3 = (m > 3 && lv) ? L.rows[g + 3][lane] : 0;
+    const uint32_t e = L.endm >> g;
+    L.acc |= w0;
+    if (e & 1) X &= L.acc, L.acc = 0;
+    if (m > 1) {
+      L.acc |= w1;
+      if (e & 2) X &= L.acc, L.acc = 0;
+    }
+    if (m > 2) {
+      L.acc |= w2;
+      if (e & 4) X &= L.acc, L.acc = 0;
+    }
+    if (m > 3) {
+      L.acc |= w3;
+      if (e & 8) X &= L.acc, L.acc = 0;
     }
   }
   L.n = 0;
@@ -560,6 +572,50 @@ __device__ __forceinline__ uint64_t filter_types(const DevDict& D, const CatHdr 
   return X;
 }
 
+// fits_filter for at most 4 requested resources (the fast lane): the threshold probes, then the (up to 4) mask
+// rows as one batch of independent loads, ANDed into X. Same result and threshold indices as fits_filter.
+__device__ __forceinline__ uint64_t fits_lean(const DevDict& D, const CatHdr LDS* H, uint64_t X, int64_t q_lane,
+                                              int32_t j0_lane, const int64_t LDS* fitv_lds, const int8_t* rr, int nr,
+                                              uint64_t& nb, int32_t LDS* jout) {
+  const int lane = LANE;
+  const int TW = D.TW;
+  const uint64_t GLB* rowp[4] = {nullptr, nullptr, nullptr, nullptr};
+  bool zero = false;
+  int32_t j_lane = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    if (k >= nr) break;
+    const int r = rr[k];
+    const int64_t q = lane_bcast_i64(q_lane, r);
+    if (q <= 0) continue;
+    const int j0 = __builtin_amdgcn_readlane(j0_lane, r);
+    const int n = H->fit_n[r];
+    const int slot = H->fit_slot[r];
+    const int idx = j0 + lane;
+    uint64_t bal;
+    if (slot >= 0) bal = __ballot(idx < n && fitv_lds[slot * FITV_CAP + idx] >= q);
+    else bal = __ballot(idx < n && H->d.fit_vals[(size_t)r * D.T + idx] >= q);
+    nb += 512;
+    int j;
+    if (bal) j = j0 + __builtin_ctzll(bal);
+    else if (j0 + 64 >= n) j = n;
+    else if (slot >= 0) j = wave_lower_bound(fitv_lds + slot * FITV_CAP + j0 + 64, n - j0 - 64, q, &nb) + j0 + 64;
+    else j = wave_lower_bound(H->d.fit_vals + (size_t)r * D.T + j0 + 64, n - j0 - 64, q, &nb) + j0 + 64;
+    if (j >= n) zero = true;
+    else rowp[k] = (const uint64_t GLB*)(H->d.fit_mask + ((size_t)r * D.T + j) * TW);
+    nb += (uint64_t)TW * 8;
+    if (lane == r) j_lane = j;
+  }
+  if (lane < KP_NRES) jout[lane] = j_lane;
+  if (zero) return 0;
+  const bool lv = lane < TW;
+  const uint64_t w0 = (rowp[0] && lv) ? rowp[0][lane] : ~0ull;
+  const uint64_t w1 = (rowp[1] && lv) ? rowp[1][lane] : ~0ull;
+  const uint64_t w2 = (rowp[2] && lv) ? rowp[2][lane] : ~0ull;
+  const uint64_t w3 = (rowp[3] && lv) ? rowp[3][lane] : ~0ull;
+  return X & w0 & w1 & w2 & w3;
+}
+
 // NodeClaim.Add when the pod's shape-level was already merged into the NodeClaim: Requirement.Intersection is
 // idempotent (set ops, max/min bounds and minValues), so the merged requirements equal the NodeClaim's and its
 // remaining types pass every compatibility and offering test already; only Fits over the grown totals changes
@@ -582,6 +638,21 @@ __device__ __forceinline__ uint64_t fits_filter(const DevDict& D, const CatHdr L
 // ------------------------------------------------------------------------------------------------
 // Go sort.Slice (pdqsort_func) over the in-flight NodeClaims by len(Pods), executed by one lane.
 // ------------------------------------------------------------------------------------------------
+// P: int32_t LDS* (sort arrays in LDS) or int32_t GLB* (spilled to global memory); typed pointers keep the
+// accesses ds_* / global_* instead of FLAT (which waits on both counters and takes the long path for LDS).
+typedef int32_t LDS* LdsI32;
+typedef int32_t GLB* GlbI32;
+template <class P>
+struct NCSortT {
+  P ord;  // newNodeClaims (NodeClaim ids)
+  P key;  // len(Pods) per NodeClaim id
+  __device__ bool Less(int i, int j) const { return key[ord[i]] < key[ord[j]]; }
+  __device__ void Swap(int i, int j) const {
+    const int32_t t = ord[i];
+    ord[i] = ord[j];
+    ord[j] = t;
+  }
+};
 struct NCSort {
   int32_t* ord;        // newNodeClaims (NodeClaim ids)
   const int32_t* key;  // len(Pods) per NodeClaim id
@@ -659,7 +730,7 @@ __device__ __forceinline__ const KReqs* kreq_at(const uint8_t* base, size_t i) {
   return reinterpret_cast<const KReqs*>(base + i * sizeof(KReqs));
 }
 
-__device__ void store_merged(KReqs* dst, const ReqView& rv, uint64_t m_v, int W, int KB) {
+__device__ __forceinline__ void store_merged(KReqs* dst, const ReqView& rv, uint64_t m_v, int W, int KB) {
   const int lane = LANE;
   if (lane < W) dst->vals[lane] = m_v;
   if (lane < KB) {
@@ -678,7 +749,7 @@ __device__ void store_merged(KReqs* dst, const ReqView& rv, uint64_t m_v, int W,
 
 // Pinned domain of each topology key on a NodeClaim's (merged) requirements: the value ordinal when the key
 // is In{one value}, 0xFE when it admits no value, 0xFF otherwise (multi-valued, complement or absent).
-__device__ void store_tcodes(int n_tk, const int32_t* tk_keys, uint8_t* nc_tcode, int stride, const ReqView& rv,
+__device__ __forceinline__ void store_tcodes(int n_tk, const int32_t* tk_keys, uint8_t* nc_tcode, int stride, const ReqView& rv,
                              uint64_t m_v, int nc) {
   const int lane = LANE;
   for (int j = 0; j < n_tk; j++) {
@@ -774,7 +845,7 @@ __device__ __forceinline__ int first_ok(const int32_t* s_ok) {
 // Max allocatable over a NodeClaim's types at creation, for the resources in `rmask`. Its remaining
 // types only shrink, so this stays an upper bound: a NodeClaim whose requests + the pod's exceed it for any
 // resource cannot take the pod (Fits fails for every remaining type) and the pre-pass skips it.
-__device__ void store_maxalloc(const int64_t* alloc, uint64_t X, int T, uint32_t rmask, int64_t* dst) {
+__device__ __forceinline__ void store_maxalloc(const int64_t* alloc, uint64_t X, int T, uint32_t rmask, int64_t* dst) {
   const int lane = LANE;
   for (int r = 0; r < KP_NRES; r++) {
     if (!((rmask >> r) & 1)) continue;
@@ -795,7 +866,7 @@ __device__ void store_maxalloc(const int64_t* alloc, uint64_t X, int T, uint32_t
 // after time `stamp` is the pos of the first entry with t > stamp. On overflow the bottom half is dropped and
 // `lost` remembers the newest dropped time: a query older than it answers 0 (conservative).
 #define MSTK_CAP 512
-__device__ int mstack_query(const int32_t* stk, int n, int lost, int stamp) {
+__device__ __forceinline__ int mstack_query(const int32_t LDS* stk, int n, int lost, int stamp) {
   if (stamp < lost) return 0;
   int lo = 0, hi = n;
   while (lo < hi) {
@@ -805,23 +876,53 @@ __device__ int mstack_query(const int32_t* stk, int n, int lost, int stamp) {
   }
   return lo < n ? stk[2 * lo + 1] : INT32_MAX;
 }
-__device__ void mstack_push(int32_t* stk, int32_t& n, int32_t& lost, int t, int pos) {
+// one lane; n_ / lost_: the stack's size and lost-time words (LDS control block)
+__device__ __forceinline__ void mstack_push(int32_t LDS* stk, int32_t LDS* n_, int32_t LDS* lost_, int t, int pos) {
+  int n = *n_;
   while (n > 0 && stk[2 * (n - 1) + 1] >= pos) n--;
   if (n == MSTK_CAP) {
     const int h = MSTK_CAP / 2;
-    lost = stk[2 * (h - 1)];
+    *lost_ = stk[2 * (h - 1)];
     for (int i = 0; i < 2 * h; i++) stk[i] = stk[2 * h + i];
     n = h;
   }
   stk[2 * n] = t;
   stk[2 * n + 1] = pos;
-  n++;
+  *n_ = n + 1;
+}
+
+// mstack_query by one wave: 64 stack entries per step (two dependent LDS reads for a full stack instead of nine).
+__device__ __forceinline__ int mstack_query_wave(const int32_t LDS* stk, int n, int lost, int stamp) {
+  if (stamp < lost) return 0;
+  const int lane = LANE;
+  int lo = 0, hi = n;  // answer: first entry with t > stamp, in [lo, hi]
+  while (hi - lo > 64) {
+    const int step = (hi - lo + 63) / 64;
+    const int idx = lo + lane * step;
+    const uint64_t bal = __ballot(idx < hi && stk[2 * idx] > stamp);
+    if (!bal) {
+      lo = lo + min(63, (hi - 1 - lo) / step) * step + 1;
+    } else {
+      const int f = __builtin_ctzll(bal);
+      if (f == 0) {
+        hi = lo;
+        break;
+      }
+      hi = lo + f * step;
+      lo = lo + (f - 1) * step + 1;
+    }
+  }
+  if (hi > lo) {
+    const uint64_t bal = __ballot(lo + lane < hi && stk[2 * (lo + lane)] > stamp);
+    lo = bal ? lo + __builtin_ctzll(bal) : hi;
+  }
+  return lo < n ? stk[2 * lo + 1] : INT32_MAX;
 }
 
 // first idx in [lo, hi) whose key (npods[ord[idx]]) is >= K (strict: > K) over a non-decreasing range; hi if
 // none. One wave: 64 samples per round, so a few rounds of two dependent loads instead of a serial bisection.
-__device__ __forceinline__ int wave_key_search(const int32_t* ord, const int32_t* npods, int lo, int hi, int K,
-                                               bool strict) {
+template <class P>
+__device__ __forceinline__ int wave_key_search(P ord, P npods, int lo, int hi, int K, bool strict) {
   const int lane = LANE;
   while (lo < hi) {
     const int span = hi - lo;
@@ -849,7 +950,8 @@ __device__ __forceinline__ int wave_key_search(const int32_t* ord, const int32_t
 // choosePivot(0, n)'s increasingHint for n >= 50, evaluated by one wave: swaps == 0 exactly when each adjacent
 // triple (i-1, i, i+1), (j-1, j, j+1), (k-1, k, k+1) is non-decreasing and so are the middles i <= j <= k
 // (every order2 then finds !Less(b, a)). Lanes 0..8 load the nine keys together.
-__device__ __forceinline__ bool wave_pivot_increasing(const int32_t* ord, const int32_t* npods, int n) {
+template <class P>
+__device__ __forceinline__ bool wave_pivot_increasing(P ord, P npods, int n) {
   const int lane = LANE;
   const int t = lane / 3;
   const int mid = (n / 4) * (t + 1);
@@ -863,15 +965,54 @@ __device__ __forceinline__ bool wave_pivot_increasing(const int32_t* ord, const 
   return __ballot(bad) == 0;
 }
 
+// The literal pdqsort replay (no stable-move shortcut) by wave 0: when keys < 2^11 and ids < 2^20 the wave packs
+// (len(Pods) << 20 | id) into ord so that lane 0's comparisons read one word instead of the ord -> npods chain, then
+// unpacks; Less compares the key field only, so the permutation is the one pdqsort_func gives on (ord, npods).
+template <class P>
+struct NCSortPacked {
+  P v;
+  __device__ bool Less(int i, int j) const { return ((uint32_t)v[i] >> 20) < ((uint32_t)v[j] >> 20); }
+  __device__ void Swap(int i, int j) const {
+    const int32_t t = v[i];
+    v[i] = v[j];
+    v[j] = t;
+  }
+};
+template <class P>
+__device__ void slow_sort_wave(P ord, P npods, int n) {
+  const int lane = LANE;
+  int kmax = 0, imax = 0;
+  for (int i = lane; i < n; i += 64) {
+    const int id = ord[i];
+    kmax = max(kmax, npods[id]);
+    imax = max(imax, id);
+  }
+  kmax = -wave_min_i32(-kmax);
+  imax = -wave_min_i32(-imax);
+  if (kmax < 2048 && imax < (1 << 20)) {
+    for (int i = lane; i < n; i += 64) {
+      const int id = ord[i];
+      ord[i] = (npods[id] << 20) | id;
+    }
+    wave_sync();
+    if (lane == 0) go_sort_slice(NCSortPacked<P>{ord}, n);
+    wave_sync();
+    for (int i = lane; i < n; i += 64) ord[i] &= (1 << 20) - 1;
+  } else {
+    if (lane == 0) go_sort_slice(NCSortT<P>{ord, npods}, n);
+  }
+  wave_sync();
+}
+
 #define DBG_SERIAL 0
-template <int NT>
-__device__ void sort_newnodeclaims(int32_t* ord, const int32_t* npods, int n, int mut, int p, int32_t* s_ctl) {
+template <int NT, class P>
+__device__ void sort_newnodeclaims(P ord, P npods, int n, int mut, int p, int32_t* s_ctl, uint64_t* slow = nullptr) {
   const int tid = threadIdx.x;
   // s_ctl[7]: 0 nothing, 1 shift-left block (p+1..q-1 -> p..q-2, elem -> q-1), 2 shift-right (q..n-2 -> q+1..n-1,
   // elem -> q), 3 slow path; s_ctl[8..9]: q / elem. Decided by wave 0 (lane-parallel searches).
   if (tid < 64) {
     int mode = 0, q = 0;
-    NCSort S{ord, npods};
+    NCSortT<P> S{ord, npods};
     if (mut == 1 && p + 1 < n && S.Less(p + 1, p)) {
       mode = 1;
     } else if (mut == 2 && n >= 2 && S.Less(n - 1, n - 2)) {
@@ -883,8 +1024,8 @@ __device__ void sort_newnodeclaims(int32_t* ord, const int32_t* npods, int n, in
         if (DBG_SERIAL) {
           int hint = 0;
           if (tid == 0) {
-            DevPDQ<NCSort> P{S};
-            P.choosePivot(0, n, &hint);
+            DevPDQ<NCSortT<P>> PQ{S};
+            PQ.choosePivot(0, n, &hint);
           }
           hint = __shfl(hint, 0, 64);
           const bool f2 = wave_pivot_increasing(ord, npods, n);
@@ -912,8 +1053,11 @@ __device__ void sort_newnodeclaims(int32_t* ord, const int32_t* npods, int n, in
         q = wave_key_search(ord, npods, 0, n - 1, npods[ord[n - 1]], true);
       }
     }
+    if (mode == 3) {
+      slow_sort_wave(ord, npods, n);
+      if (tid == 0 && slow) slow[0] += 1;
+    }
     if (tid == 0) {
-      if (mode == 3) go_sort_slice(S, n);
       // lowest sorted position whose NodeClaim changed or moved since the last sort (cursor clamp)
       s_ctl[16] = mode == 3 ? 0 : (mut == 1 ? p : (mut == 2 ? (mode == 2 ? q : n - 1) : -1));
       s_ctl[7] = mode;
@@ -954,6 +1098,62 @@ __device__ void sort_newnodeclaims(int32_t* ord, const int32_t* npods, int n, in
       }
   }
   __syncthreads();
+}
+
+// sort_newnodeclaims executed by ONE wave (the fast lane): the same decisions (stable move when pdqsort would
+// perform one, else the literal pdqsort on lane 0), block shifts by 64 lanes with wave-level ordering only.
+// Returns the lowest sorted position whose NodeClaim changed or moved (-1: none), as s_ctl[16] would hold.
+// max_shift: a stable move shifting more than this many entries (or a literal pdqsort) is left undone and -2 is
+// returned, so that the caller hands the pod to the full path (256 lanes per shift step, pdqsort included).
+template <class P>
+__device__ __forceinline__ int sort_newnodeclaims_wave(P ord, P npods, int n, int mut, int p, int max_shift,
+                                                       uint64_t* slow = nullptr) {
+  const int lane = LANE;
+  int mode = 0, q = 0;
+  NCSortT<P> S{ord, npods};
+  if (mut == 1 && p + 1 < n && S.Less(p + 1, p)) {
+    mode = 1;
+  } else if (mut == 2 && n >= 2 && S.Less(n - 1, n - 2)) {
+    mode = 2;
+  }
+  if (mode) {
+    bool fast = n <= 12;
+    if (!fast && n >= 50) fast = wave_pivot_increasing(ord, npods, n);
+    if (!fast) mode = 3;
+    else if (mode == 1) q = wave_key_search(ord, npods, p + 1, n, npods[ord[p]], false);
+    else q = wave_key_search(ord, npods, 0, n - 1, npods[ord[n - 1]], true);
+  }
+  if ((mode == 3 && n > max_shift) || (mode == 1 && q - 1 - p > max_shift) || (mode == 2 && n - 1 - q > max_shift))
+    return -2;
+  const int low = mode == 3 ? 0 : (mut == 1 ? p : (mut == 2 ? (mode == 2 ? q : n - 1) : -1));
+  if (mode == 3) {
+    slow_sort_wave(ord, npods, n);
+    if (lane == 0 && slow) slow[0] += 1;
+  } else if (mode == 1) {
+    const int elem = ord[p];
+    const int c = q - 1 - p;  // elements p+1..q-1 move left by one
+    for (int off = 0; off < c; off += 64) {
+      const int i = off + lane;
+      const int v = i < c ? ord[p + 1 + i] : 0;
+      wave_sync();
+      if (i < c) ord[p + i] = v;
+    }
+    wave_sync();
+    if (lane == 0) ord[q - 1] = elem;
+  } else if (mode == 2) {
+    const int elem = ord[n - 1];
+    const int c = n - 1 - q;  // elements q..n-2 move right by one (top block first)
+    for (int off = 0; off < c; off += 64) {
+      const int i = c - 1 - (off + lane);
+      const int v = i >= 0 ? ord[q + i] : 0;
+      wave_sync();
+      if (i >= 0) ord[q + i + 1] = v;
+    }
+    wave_sync();
+    if (lane == 0) ord[q] = elem;
+  }
+  wave_sync();
+  return low;
 }
 
 template <int NW, bool TOPO>  // TOPO: the batch has topology spread groups (else that code compiles out)
@@ -1008,6 +1208,12 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
   const uint32_t rm1 = rmask_all & (rmask_all - 1);
   const int rr1 = rm1 ? __builtin_ctz(rm1) : rr0;
   const uint32_t rr_rest = rm1 & (rm1 - 1);
+  int8_t rr_list[4] = {0, 0, 0, 0};  // the requested resources in order (fits_lean), when there are <= 4
+  int n_rr = 0;
+  for (uint32_t m = rmask_all; m; m &= m - 1) {
+    if (n_rr < 4) rr_list[n_rr] = (int8_t)__builtin_ctz(m);
+    n_rr++;
+  }
   {  // Fits threshold tables of catalogue 0 for the first FITV_RES requested resources -> LDS
     int slot = 0;
     for (int r = 0; r < KP_NRES; r++) {
@@ -1022,7 +1228,9 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
     }
   }
   __syncthreads();
-  uint64_t bytes = 0, attempts = 0, pops = 0, scanned = 0, starts = 0;
+  uint64_t bytes = 0, attempts = 0, pops = 0, scanned = 0, starts = 0, fpods = 0;
+  const uint64_t pop_cap = (uint64_t)a.n_pods * 64 + 65536;  // Queue.Pop bound for the runaway guard
+  uint64_t fcyc[6] = {0, 0, 0, 0, 0, 0};  // fast-lane cycles (KP_TIMING, lane 0 of wave 0)
   uint64_t tph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tlast = 0;
   const bool timing = a.timing && tid == 0;
   if (tid < 8) s_tsub[tid] = 0;
@@ -1052,15 +1260,234 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
     s_ctl[17] = 0;  // existing scan start for the popped pod
     s_ctl[22] = 0;  // in-flight cursor of the popped pod's shape-level (staged)
     s_ctl[23] = 0;
+    s_ctl[26] = 0;  // 1: the fast lane popped s_ctl[6] and hands it to the full path
   }
   __syncthreads();
 
+  // fast lane's prefetched Queue window (wave 0): lane i holds queue entry qw_head + i (ring order)
+  int qw_head = 0, qw_n = 0, qw_next = -1, qw_pod = 0, qw_shape = 0, qw_sl = 0, qw_lastlen = 0, qw_epoch = 0;
   for (;;) {
+    // ---- fast lane: wave 0 alone places every pod whose placement needs no requirement merge ----------------
+    // The pod owns/feeds no topology group, every existing node is known to fail it (first-fit cursor), and the
+    // first in-flight NodeClaim (sort order) that passes the pre-checks already carries the pod's shape-level
+    // (NC_MERGED) without minValues: NodeClaim.Add is then Fits over the remaining types, evaluated in order
+    // until one succeeds. The steps, decisions and state writes are the full path's (below), done by one wave
+    // without workgroup barriers. Any other situation hands the popped pod to the full path (s_ctl[26]).
+    if (FASTLANE && wave == 0) {
+      uint64_t ft = a.timing ? __builtin_amdgcn_s_memtime() : 0;
+#define FT(i)                                                \
+  if (a.timing) {                                            \
+    const uint64_t tn_ = __builtin_amdgcn_s_memtime();       \
+    if (lane == 0) fcyc[i] += tn_ - ft;                      \
+    ft = tn_;                                                \
+  }
+      for (;;) {
+        const int len = s_ctl[1];
+        const int head = s_ctl[0];
+        if (len <= 0 || pops > pop_cap) break;
+        // Queue.Pop from the prefetched window: entries [qw_head, qw_head + qw_n) of the ring were in the queue when
+        // the window was read, and nothing rewrites a queued entry (pushes go to the tail) or its pod's level and
+        // lastLen stamps while it waits, so lane i's copy of entry qw_head + i stays exact.
+        int off = head - qw_head;
+        if (off < 0) off += a.n_pods;
+        if (off != qw_next || off >= qw_n) {  // exhausted, or the ring wrapped onto re-pushed entries
+          qw_head = head;
+          qw_n = min(64, len);
+          off = 0;
+          int qi = head + lane;
+          if (qi >= a.n_pods) qi -= a.n_pods;
+          if (lane < qw_n) {
+            qw_pod = a.queue[qi];
+            qw_shape = a.pod_shape[qw_pod];
+            qw_sl = a.shape_level_base[qw_shape] + a.pod_level[qw_pod];
+            qw_lastlen = a.lastlen[qw_pod];
+            qw_epoch = a.lastlen_epoch[qw_pod];
+          }
+        }
+        qw_next = off + 1;  // only the fast lane pops: the next pop reads the following entry
+        const int pod = __builtin_amdgcn_readlane(qw_pod, off);
+        if (__builtin_amdgcn_readlane(qw_epoch, off) == s_ctl[3] && __builtin_amdgcn_readlane(qw_lastlen, off) == len)
+          break;  // the full path's pop sees the same queue and ends the Solve
+        const int shape = __builtin_amdgcn_readlane(qw_shape, off);
+        const int sl = __builtin_amdgcn_readlane(qw_sl, off);
+        // stage: one batch of independent loads (eligibility, requests, tolerations, both first-fit cursors)
+        const int own = TOPO ? a.sl_own_n[sl] + a.shape_rec_n[shape] : 0;
+        const int ce0 = a.n_existing ? a.cur_ex[2 * sl] : 0, ce1 = a.n_existing ? a.cur_ex[2 * sl + 1] : 0;
+        const int64_t preq_lane = lane < KP_NRES ? a.shape_requests[(size_t)shape * KP_NRES + lane] : 0;
+        const uint64_t tolmask = a.shape_tolerates[shape];
+        const int cur = a.cur_nc[2 * sl], stamp = a.cur_nc[2 * sl + 1];
+        wave_sync();
+        if (lane == 0) {
+          s_ctl[0] = head + 1 == a.n_pods ? 0 : head + 1;
+          s_ctl[1] = len - 1;
+        }
+        bool eligible = own == 0;
+        if (a.n_existing) eligible = eligible && min(ce0, mstack_query_wave((LdsI32)s_stk[1], s_ctl[14], s_ctl[21], ce1)) >= a.n_existing;
+        FT(0);
+        if (!eligible) {
+          wave_sync();
+          if (lane == 0) {
+            s_ctl[6] = pod;
+            s_ctl[26] = 1;
+          }
+          break;
+        }
+        const int64_t pr0 = lane_bcast_i64(preq_lane, rr0), pr1 = lane_bcast_i64(preq_lane, rr1);
+        if (a.n_existing && lane == 0) {  // addToExistingNode: every position fails (cursor == n_existing)
+          a.cur_ex[2 * sl] = a.n_existing;
+          a.cur_ex[2 * sl + 1] = s_ctl[15];
+        }
+        FT(1);
+        // sort.Slice(newNodeClaims) replay + first-fit start (sort arrays in LDS; spilled ones: the full path)
+        if (s_ctl[5] == 0) {
+          wave_sync();
+          if (lane == 0) {
+            s_ctl[6] = pod;
+            s_ctl[26] = 1;
+          }
+          break;
+        }
+        const LdsI32 ord = (LdsI32)s_dyn;
+        const LdsI32 npods = (LdsI32)(s_dyn + a.sort_cap);
+        const int c19 = min(cur, mstack_query_wave((LdsI32)s_stk[0], s_ctl[12], s_ctl[20], stamp));
+        const int n_nc = s_ctl[2];
+        const int low = sort_newnodeclaims_wave(ord, npods, n_nc, s_ctl[10], s_ctl[11], 256, &a.stats[31]);
+        if (low == -2) {  // a long shift: the full path sorts (the pending mutation is still in s_ctl[10..11])
+          wave_sync();
+          if (lane == 0) {
+            s_ctl[6] = pod;
+            s_ctl[26] = 1;
+          }
+          break;
+        }
+        const int start = min(min(c19, low >= 0 ? low : INT32_MAX), n_nc);
+        if (lane == 0) {
+          s_ctl[10] = 0;
+          if (low >= 0) mstack_push((LdsI32)s_stk[0], (LdsI32)&s_ctl[12], (LdsI32)&s_ctl[20], ++s_ctl[13], low);
+        }
+        wave_sync();
+        FT(2);
+        // addToInflightNode: pre-checks 64 positions at a time, then the append-path attempts in order. A long scan
+        // is the full path's (512-lane pre-pass).
+        int placed = -1, wpos = -1;
+        bool bail = n_nc - start > 2 * 64;
+        if (lane == 0 && !bail) starts += start;
+        for (int base = start; base < n_nc && placed == -1 && !bail; base += 64) {
+          const int i = base + lane;
+          bool cand = false, tag = false;
+          int nc = 0;
+          if (i < n_nc) {
+            nc = ord[i];
+            // every gather issued unconditionally: one round trip
+            const int32_t fl = nc < a.ncc ? a.nc_fail[(size_t)sl * a.ncc + nc] : -2;
+            const int32_t ver = a.nc_ver[nc];
+            const int32_t ts = a.nc_taintset[nc];
+            const int64_t* rq = a.nc_requests + (size_t)nc * KP_NRES;
+            const int64_t* mx = a.nc_maxalloc + (size_t)nc * KP_NRES;
+            bool fit = !rmask_all || (rq[rr0] + pr0 <= mx[rr0] && rq[rr1] + pr1 <= mx[rr1]);
+            for (uint32_t rm = rr_rest; rm; rm &= rm - 1) {
+              const int r = __builtin_ctz(rm);
+              fit = fit & (rq[r] + lane_bcast_i64(preq_lane, r) <= mx[r]);
+            }
+            cand = fit && fl != ver && ((tolmask >> ts) & 1);
+            tag = cand && fl >= NC_MERGED;
+          }
+          // speculative loads of the first position's NodeClaim (the usual winner): they overlap the pre-checks
+          const int nc0 = __builtin_amdgcn_readlane(nc, 0);
+          const KReqs* cr0 = kreq_at(a.nc_reqs, nc0);
+          const uint64_t hm0 = cr0->hmin & cr0->present;
+          const int cat0 = a.nc_cat[nc0];
+          const uint64_t X00 = lane < D.TW ? a.nc_X[(size_t)nc0 * D.TW + lane] : 0;
+          const int64_t rq0 = lane < KP_NRES ? a.nc_requests[(size_t)nc0 * KP_NRES + lane] : 0;
+          const int32_t j00 = lane < KP_NRES ? a.nc_fitj[(size_t)nc0 * KP_NRES + lane] : 0;
+          if (lane == 0) scanned += min(64, n_nc - base);
+          if (lane == 0) bytes += (uint64_t)min(64, n_nc - base) * (12 + 16 * a.n_req_res);
+          uint64_t cm = __ballot(cand);
+          const uint64_t tm = __ballot(tag);
+          FT(3);
+          while (cm) {
+            const int l = __builtin_ctzll(cm);
+            cm &= cm - 1;
+            if (!((tm >> l) & 1)) {  // needs the merge: the full path evaluates it
+              bail = true;
+              break;
+            }
+            const int ncx = __shfl(nc, l, 64);
+            attempts++;
+            uint64_t hm = hm0, X0 = X00;
+            int cat = cat0;
+            int64_t rq_lane = rq0;
+            int32_t j0_lane = j00;
+            if (l != 0) {
+              const KReqs* cr = kreq_at(a.nc_reqs, ncx);
+              hm = cr->hmin & cr->present;
+              cat = a.nc_cat[ncx];
+              X0 = lane < D.TW ? a.nc_X[(size_t)ncx * D.TW + lane] : 0;
+              rq_lane = lane < KP_NRES ? a.nc_requests[(size_t)ncx * KP_NRES + lane] : 0;
+              j0_lane = lane < KP_NRES ? a.nc_fitj[(size_t)ncx * KP_NRES + lane] : 0;
+            }
+            if (hm) {  // minValues on the NodeClaim: the full path re-filters it
+              bail = true;
+              break;
+            }
+            const int64_t q_lane = rq_lane + preq_lane;
+            const uint64_t X = n_rr <= 4 ? fits_lean(D, hdr(cat), X0, q_lane, j0_lane, (const int64_t LDS*)s_fitv, rr_list,
+                                                     n_rr, bytes, (int32_t LDS*)s_fitj[0])
+                                         : fits_filter(D, hdr(cat), X0, q_lane, j0_lane, (const int64_t LDS*)s_fitv,
+                                                       a.req_res_mask, (RowPtr LDS*)s_rl[0], &bytes, s_fitj[0]);
+            bytes += (uint64_t)D.TW * 8 + KP_NRES * 8 + 8;
+            if (__ballot(X != 0)) {
+              if (lane < D.TW) a.nc_X[(size_t)ncx * D.TW + lane] = X;
+              if (lane < KP_NRES) {
+                a.nc_requests[(size_t)ncx * KP_NRES + lane] = q_lane;
+                a.nc_fitj[(size_t)ncx * KP_NRES + lane] = s_fitj[0][lane];
+              }
+              if (lane == 0) {
+                npods[ncx] += 1;
+                a.nc_ver[ncx] += 1;
+              }
+              placed = ncx;
+              wpos = base + l;
+              break;
+            }
+            if (lane == 0 && ncx < a.ncc) a.nc_fail[(size_t)sl * a.ncc + ncx] = a.nc_ver[ncx];
+          }
+        }
+        wave_sync();
+        FT(4);
+        if (placed == -1) {  // templates, a merge, minValues or a long scan: the full path takes over this pod
+          if (lane == 0) {
+            s_ctl[6] = pod;
+            s_ctl[26] = 1;
+          }
+          break;
+        }
+        pops++;
+        fpods++;
+        if (lane == 0) {
+          s_ctl[10] = 1;
+          s_ctl[11] = wpos;
+          a.cur_nc[2 * sl] = wpos;
+          a.cur_nc[2 * sl + 1] = s_ctl[13];
+          a.placement[pod] = placed;
+          a.events[s_ctl[4]++] = pod;
+        }
+        wave_sync();
+        FT(5);
+      }
+#undef FT
+    }
+    __syncthreads();
     // ---- Queue.Pop: stop when the head pod was last pushed at the current queue length ----------
     if (tid == 0) {
       const int len = s_ctl[1];
       int pod = -1;
-      if (len > 0) {
+      if (pops > pop_cap) {  // runaway guard (a correct Solve stays far below): end the launch, report it
+        a.stats[7] = 1;
+      } else if (s_ctl[26]) {  // popped by the fast lane
+        pod = s_ctl[6];
+        s_ctl[26] = 0;
+      } else if (len > 0) {
         const int head = s_ctl[0];
         const int p = a.queue[head];
         if (!(a.lastlen_epoch[p] == s_ctl[3] && a.lastlen[p] == len)) {
@@ -1087,7 +1514,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
       else if (tid >= 192 && tid < 192 + 32 && tid - 192 < a.n_catalogs)
         s_pvpb[tid - 192] = a.pvp_base[sl * a.n_catalogs + tid - 192];
       else if (tid == 128) {  // first-fit cursors of the shape-level (LDS stacks: no global round trips)
-        const int ce = a.n_existing ? min(a.cur_ex[2 * sl], mstack_query(s_stk[1], s_ctl[14], s_ctl[21], a.cur_ex[2 * sl + 1])) : 0;
+        const int ce = a.n_existing ? min(a.cur_ex[2 * sl], mstack_query((LdsI32)s_stk[1], s_ctl[14], s_ctl[21], a.cur_ex[2 * sl + 1])) : 0;
         s_ctl[17] = min(ce, a.n_existing);
         s_ctl[22] = a.cur_nc[2 * sl];
         s_ctl[23] = a.cur_nc[2 * sl + 1];
@@ -1208,23 +1635,24 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
       const int cpos = own_n ? min(s_ctl[24], a.n_existing) : (placed != -1 ? -2 - placed : a.n_existing);
       a.cur_ex[2 * sl] = cpos;
       a.cur_ex[2 * sl + 1] = s_ctl[15];
-      if (placed != -1) mstack_push(s_stk[1], s_ctl[14], s_ctl[21], ++s_ctl[15], -2 - placed);
+      if (placed != -1) mstack_push((LdsI32)s_stk[1], (LdsI32)&s_ctl[14], (LdsI32)&s_ctl[21], ++s_ctl[15], -2 - placed);
     }
     TS(1);
     if (placed == -1) {
       const bool in_lds = s_ctl[5] != 0;
-      int32_t* ord = in_lds ? s_dyn : a.g_order;
-      int32_t* npods = in_lds ? s_dyn + a.sort_cap : a.g_npods;
       // ---- sort.Slice(newNodeClaims, len(Pods) asc) -----------------------------------------------
       // the cursor query (one lane of wave 1) overlaps the sort (thread 0); the pending mutation's own
       // clamp (s_ctl[16], known after the sort) is folded in below and pushed by thread 0 afterwards
-      if (tid == 64) s_ctl[19] = min(s_ctl[22], mstack_query(s_stk[0], s_ctl[12], s_ctl[20], s_ctl[23]));
-      sort_newnodeclaims<NT>(ord, npods, s_ctl[2], s_ctl[10], s_ctl[11], s_ctl);
+      if (tid == 64) s_ctl[19] = min(s_ctl[22], mstack_query((LdsI32)s_stk[0], s_ctl[12], s_ctl[20], s_ctl[23]));
+      if (in_lds)
+        sort_newnodeclaims<NT>((LdsI32)s_dyn, (LdsI32)(s_dyn + a.sort_cap), s_ctl[2], s_ctl[10], s_ctl[11], s_ctl, &a.stats[31]);
+      else
+        sort_newnodeclaims<NT>((GlbI32)a.g_order, (GlbI32)a.g_npods, s_ctl[2], s_ctl[10], s_ctl[11], s_ctl, &a.stats[31]);
       const int n_nc = s_ctl[2];
       const int start = min(min(s_ctl[19], s_ctl[16] >= 0 ? s_ctl[16] : INT32_MAX), n_nc);
       if (tid == 0) {
         s_ctl[10] = 0;
-        if (s_ctl[16] >= 0) mstack_push(s_stk[0], s_ctl[12], s_ctl[20], ++s_ctl[13], s_ctl[16]);
+        if (s_ctl[16] >= 0) mstack_push((LdsI32)s_stk[0], (LdsI32)&s_ctl[12], (LdsI32)&s_ctl[20], ++s_ctl[13], s_ctl[16]);
       }
       TS(2);
       // ---- addToInflightNode: first NodeClaim in that order whose Add succeeds ------------------
@@ -1234,7 +1662,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
         for (int k = 0; k < 4; k++) {  // 4 rounds per thread: independent, so their loads overlap
           const int i = base + k * NT + tid;
           if (i >= n_nc) continue;
-          const int nc = ord[i];
+          const int nc = in_lds ? ((LdsI32)s_dyn)[i] : ((GlbI32)a.g_order)[i];
           // every gather is issued unconditionally so they overlap (one round trip instead of a chain)
           const int32_t fl = nc < a.ncc ? a.nc_fail[(size_t)sl * a.ncc + nc] : -2;
           const int32_t ver = a.nc_ver[nc];
@@ -1279,7 +1707,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
           ReqView rv;
           int nc = -1;
           if (wave < width && li < n) {
-            nc = ord[LIST_POS(s_list[li])];
+            nc = in_lds ? ((LdsI32)s_dyn)[LIST_POS(s_list[li])] : ((GlbI32)a.g_order)[LIST_POS(s_list[li])];
             attempts++;
             uint64_t* tsub = (a.timing && wave == 0) ? s_tsub : nullptr;
             const uint64_t tm0 = tsub ? __builtin_amdgcn_s_memtime() : 0;
@@ -1330,13 +1758,14 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
               if (lane < D.TW) a.nc_X[(size_t)nc * D.TW + lane] = X;
               if (lane < KP_NRES) a.nc_requests[(size_t)nc * KP_NRES + lane] += s_preq[lane];
               if (lane == 0) {
-                npods[nc] += 1;
+                if (in_lds) ((LdsI32)(s_dyn + a.sort_cap))[nc] += 1;
+                else ((GlbI32)a.g_npods)[nc] += 1;
                 a.nc_ver[nc] += 1;
               }
               if (lane < KP_NRES) a.nc_fitj[(size_t)nc * KP_NRES + lane] = s_fitj[wave][lane];
             }
             const int wpos = LIST_POS(s_list[r0 + win]);
-            placed = ord[wpos];
+            placed = in_lds ? ((LdsI32)s_dyn)[wpos] : ((GlbI32)a.g_order)[wpos];
             if (tid == 0) {
               s_ctl[10] = 1;
               s_ctl[11] = wpos;
@@ -1553,6 +1982,8 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
     a.stats[4] = (uint64_t)s_ctl[4];
     a.stats[5] = scanned;  // in-flight positions scanned by the pre-pass
     a.stats[6] = starts;   // sum of cursor start positions
+    a.stats[24] = fpods;
+    for (int i = 0; i < 6; i++) a.stats[25 + i] = fcyc[i];
   }
   if (s_ctl[5])
     for (int i = tid; i < s_ctl[2]; i += NT) {

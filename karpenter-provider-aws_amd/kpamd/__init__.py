@@ -202,6 +202,7 @@ def stats_dict(st):
     d = {f: getattr(st, f) for f, _ in abi.SolveStats._fields_}
     d["phase_cycles"] = list(st.phase_cycles)
     d["attempt_cycles"] = list(st.attempt_cycles)
+    d["fast_cycles"] = list(st.fast_cycles)
     return d
 
 

@@ -16,9 +16,9 @@ cat = catalog.build_catalog(lib)
 prob = {"2": lambda: synth.config2(cat, n_pods=n, seed=2), "3": lambda: synth.config3(cat, n_pods=n),
         "5": lambda: synth.config5(cat, n_pods=n)}[cfg]()
 ctx = kpamd.Context(0)
-plan = kpamd.Scheduler(ctx, prob).prepare()
-plan.run(read=False)
-r = plan.run(read=True)
+sched = kpamd.Scheduler(ctx, prob)
+sched.solve(read=False)
+r = sched.solve(read=True)
 st = r["stats"]
 names = ["pop+stage", "existing", "sort", "inflight-commit", "templates", "record+bookkeeping", "inflight-prepass",
          "inflight-attempts"]
@@ -33,4 +33,10 @@ if ac[5]:
     out["attempt_cycles_per_attempt"] = {k: round(v / ac[5], 1) for k, v in
                                          zip(["merge", "pod-key-rows", "fits-rows", "offer-rows+row-loads", "minvalues"], ac[:5])}
     out["attempts_timed"] = ac[5]
+out["fast_pods"] = st["fast_pods"]
+out["slow_sorts"] = st["slow_sorts"]
+fc = st["fast_cycles"]
+if sum(fc):
+    out["fast_cycles_per_fast_pod"] = {k: round(v / max(1, st["fast_pods"]), 1) for k, v in
+                                       zip(["pop", "stage", "sort", "prepass", "attempts", "commit"], fc)}
 print(json.dumps(out))
