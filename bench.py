@@ -284,14 +284,18 @@ def _feasibility(args, cat, ctx, prob, barrier, max_over_ranks, world, steps=10)
     return out
 
 
-CHUNK = 1 << 16  # subsets per kp_cluster_simulate call (1M subsets: 16 chunks, contiguous ranges per rank)
+CHUNK = 1 << 16  # subsets per generation chunk (1M subsets: 16 chunks, contiguous chunk ranges per rank)
 
 
 def _consolidation(args, cat, ctx, dist, rank, world, barrier):
-    """Config 4: multi-node consolidation sweep on a 10k-node cluster. The subsets (99 prefixes of the
-    disruption-cost order + random subsets of 2..100 candidates, generated in fixed chunks so the set
-    does not depend on N) are sharded over ranks by chunk; each rank simulates its chunks on its GPU,
-    keeps its best (savings desc, subset index asc), and an RCCL argmax all-reduce (MAX savings, then MIN subset index) picks the global best."""
+    """Config 4: multi-node consolidation on a 10k-node cluster packed near capacity (delete, replace and no-op
+    decisions all occur). Timed, per rank:
+      sweep     this rank's contiguous chunk range of the 1M random candidate subsets (2..100 candidates, fixed seed
+                per chunk, so the set does not depend on N) through kp_consolidate_argmin: simulation, device argmax,
+                and one RCCL all-gather of the ranks' records inside libkp (comm NULL at N=1)
+      firstN    rank 0: every prefix firstNConsolidationOption can probe (candidates[0:mid+1], mid = 1..100),
+                simulated in one batch, then the binary search replayed (MultiNodeConsolidation's command)
+    value = all ranks' subsets / the slowest rank's time."""
     import numpy as np
     import torch
     import kpamd
@@ -302,96 +306,133 @@ def _consolidation(args, cat, ctx, dist, rank, world, barrier):
     cands = np.asarray(cl.candidates, dtype=np.uint32)
     n_chunks = (args.subsets + CHUNK - 1) // CHUNK
     lo, hi = disruption.shard(n_chunks, rank, world)  # contiguous chunk range: balanced for N in 1, 2, 4, 8
-    mine = list(range(lo, hi))
-    batches = []
-    if rank == 0:  # every prefix firstNConsolidationOption can probe: candidates[0:mid+1], mid = 1..100
-        pre = [cands[:m + 1] for m in disruption.MultiNodeConsolidation.search_prefixes(len(cands))]
-        offs = np.zeros(len(pre) + 1, dtype=np.uint32)
-        offs[1:] = np.cumsum([len(p) for p in pre])
-        batches.append((-1, offs, np.concatenate(pre)))
-    if mine:  # this rank's chunks (fixed seeds per chunk) concatenated into ONE launch: no per-chunk tails
-        offs_l, nodes_l, base = [], [], 0
-        for c in mine:
-            n = min(CHUNK, args.subsets - c * CHUNK)
-            offs, pos = disruption.random_subsets_csr(len(cands), n, seed=1000 + c)
-            offs_l.append(offs[:-1] + base)
-            nodes_l.append(cands[pos])
-            base += int(offs[-1])
-        offs_l.append(np.array([base], dtype=np.uint32))
-        batches.append((mine[0], np.concatenate(offs_l).astype(np.uint32), np.concatenate(nodes_l)))
+    offs_l, nodes_l, base = [], [], 0
+    for c in range(lo, hi):  # this rank's chunks concatenated into ONE launch
+        n = min(CHUNK, args.subsets - c * CHUNK)
+        offs, pos = disruption.random_subsets_csr(len(cands), n, seed=1000 + c)
+        offs_l.append(offs[:-1] + base)
+        nodes_l.append(cands[pos])
+        base += int(offs[-1])
+    offs_l.append(np.array([base], dtype=np.uint32))
+    sw_offs = np.concatenate(offs_l).astype(np.uint32)
+    sw_nodes = np.concatenate(nodes_l) if nodes_l else np.zeros(0, dtype=np.uint32)
+    base_index = lo * CHUNK
+    mids = disruption.MultiNodeConsolidation.search_prefixes(len(cands))
+    pre = [cands[:m + 1] for m in mids]
+    pre_offs = np.zeros(len(pre) + 1, dtype=np.uint32)
+    pre_offs[1:] = np.cumsum([len(p) for p in pre])
+    pre_nodes = np.concatenate(pre)
     gen_s = time.perf_counter() - t0
     t0 = time.perf_counter()
     plan = kpamd.ClusterPlan(ctx, cl)
+    comm = None
+    if dist is not None:  # the RCCL communicator lives in libkp: rank 0's unique id, shared over torch.distributed
+        uid = [kpamd.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = kpamd.Comm(ctx, uid[0], world, rank)
     prep_s = time.perf_counter() - t0
-    if batches:  # warmup (untimed); a rank may hold no chunk when ranks outnumber chunks
-        plan.simulate_csr(batches[-1][1][:1025] if len(batches[-1][1]) > 1025 else batches[-1][1],
-                          batches[-1][2])
+    warm = min(len(sw_offs) - 1, 1024)  # warmup (untimed) on the first subsets
+    plan.argmin(sw_offs[:warm + 1], sw_nodes, base_index=base_index, comm=comm)
     barrier()
     t0 = time.perf_counter()
-    best_s, best_i, kern_ms, pops, words, n_done = -np.inf, -1, 0.0, 0, 0, 0
-    counts = np.zeros(3, dtype=np.int64)
-    for c, offs, nodes in batches:
-        res, st = plan.simulate_csr(offs, nodes)
-        base = args.subsets if c < 0 else c * CHUNK  # prefixes are indexed after the random subsets
-        s, i = disruption.best_local(res, base)
-        if i >= 0 and (s > best_s or (s == best_s and i < best_i)):
-            best_s, best_i = s, i
-        counts += np.bincount(res["decision"], minlength=3)[:3]
-        kern_ms += st["solve_kernel_ms"]
-        pops += st["pops"]
-        words += st["phase_cycles"][0]
-        n_done += len(offs) - 1
-    dev = torch.device("cuda", torch.cuda.current_device())
-    best_s, best_i = disruption.reduce_best(best_s, best_i, dist, device=dev)
+    choice, st = disruption.sweep(plan, sw_offs, sw_nodes, base_index=base_index, comm=comm)
+    first_n = None
+    if rank == 0:
+        pres, pst = plan.simulate_csr(pre_offs, pre_nodes)
+        hit = disruption.MultiNodeConsolidation.replay(len(cands), dict(zip(mids, [kpamd.sim_dict(r) for r in pres])))
+        first_n = None if hit is None else {"candidates": hit[0] + 1, "decision": int(hit[1]["decision"]),
+                                            "savings": hit[1]["savings"]}
     barrier()
     elapsed = time.perf_counter() - t0
+    n_done = len(sw_offs) - 1 + (len(pre) if rank == 0 else 0)
     total = n_done
+    dev = torch.device("cuda", torch.cuda.current_device())
     if dist is not None:
         te = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(te, op=dist.ReduceOp.MAX)
         tot = torch.tensor([float(n_done)], dtype=torch.float64, device=dev)
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         elapsed, total = float(te.item()), int(tot.item())
-        cnt = torch.tensor(counts, device=dev)
-        dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
-        counts = cnt.cpu().numpy()
-    plan.close()
     out = {
         "metric": "consolidation sims/s",
         "value": round(total / elapsed, 1),
         "unit": "sims/s",
         "n_gpus": world,
         "scaling": "strong" if world > 1 else "n/a",
-        "workload": f"config4: computeConsolidation of {total} candidate subsets (99 disruption-cost prefixes + "
-                    f"random 2..100-candidate subsets) on a {args.cluster_nodes}-node cluster with "
-                    f"{len(cl.pod_shape)} pods (8-40 per node), 2 NodePools, 919 types; sharded by chunk over "
-                    f"ranks, best decision by RCCL argmax all-reduce (MAX savings, MIN index)",
+        "workload": f"config4: computeConsolidation of {total} candidate subsets ({args.subsets} random subsets of "
+                    f"2..100 candidates + {len(pre)} firstNConsolidationOption prefixes) on a {args.cluster_nodes}-node "
+                    f"cluster packed near capacity ({len(cl.pod_shape)} pods), 2 NodePools, 919 types; subsets sharded "
+                    f"by chunk over ranks, best decision by kp_consolidate_argmin (device argmax + RCCL all-gather)",
         "elapsed_s": round(elapsed, 4),
-        "sim_kernel_ms_rank0": round(kern_ms, 3),
-        "pods_rescheduled_rank0": int(pops),
-        "decisions": {"noop": int(counts[0]), "delete": int(counts[1]), "replace": int(counts[2])},
-        "best": {"savings": best_s, "subset": best_i},
+        "sim_kernel_ms_rank0": round(st["solve_kernel_ms"], 3),
+        "pods_rescheduled_rank0": int(st["pops"]),
+        "decisions": {"noop": choice["counts"][0], "delete": choice["counts"][1], "replace": choice["counts"][2]},
+        "best": {"subset": choice["subset"], "decision": choice["result"]["decision"],
+                 "savings": choice["result"]["savings"]},
+        "first_n": first_n,
         "prepare_s": round(prep_s, 3),
         "subset_generation_s": round(gen_s, 3),
     }
+    if rank == 0 and world == 1:  # sims/s by decision class: the first chunk's subsets regrouped by their decision
+        n0 = min(CHUNK, len(sw_offs) - 1)
+        _, res0, _ = plan.argmin(sw_offs[:n0 + 1], sw_nodes, read_all=True)
+        by = {}
+        for cls, name in ((0, "noop"), (1, "delete"), (2, "replace")):
+            idx = np.nonzero(res0["decision"] == cls)[0]
+            if len(idx) < 64:
+                continue
+            sub = [sw_nodes[sw_offs[i]:sw_offs[i + 1]] for i in idx]
+            o = np.zeros(len(sub) + 1, dtype=np.uint32)
+            o[1:] = np.cumsum([len(x) for x in sub])
+            flat = np.concatenate(sub)
+            t1 = time.perf_counter()
+            plan.argmin(o, flat)
+            torch.cuda.synchronize()
+            by[name] = {"subsets": int(len(idx)), "sims_per_s": round(len(idx) / (time.perf_counter() - t1), 1)}
+        out["by_decision"] = by
+    if comm is not None:
+        comm.close()
+    plan.close()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = _cpu_baseline_sims(cl, cands, args.cpu_sample_sims)
     return out
 
 
-def _cpu_baseline_sims(cl, cands, n):
-    import numpy as np
+def _sims_worker(arg):
+    """One process of the all-threads CPU baseline: the oracle simulates its share of the sample subsets."""
+    n_nodes, subs = arg
+    import kpamd
+    from kpamd import catalog, synth
+    from oracle import pyoracle
+    cl = synth.config4(catalog.build_catalog(kpamd.load_lib()), n_nodes=n_nodes, seed=4)
+    t0 = time.perf_counter()
+    pyoracle.simulate_batch(cl, subs)
+    return time.perf_counter() - t0
+
+
+def _cpu_baseline_sims(cl, cands, n, procs=16):
+    """computeConsolidation on the CPU oracle: one thread over n subsets of chunk 0, and `procs` processes (the box's
+    CPU share; sims parallelize per subset) over procs * n subsets; rate = subsets / the slowest process's time."""
+    import multiprocessing as mp
     from kpamd import disruption
     from oracle import pyoracle
 
-    offs, pos = disruption.random_subsets_csr(len(cands), n, seed=1000)
-    subs = [list(cands[pos[offs[i]:offs[i + 1]]]) for i in range(n)]
+    offs, pos = disruption.random_subsets_csr(len(cands), n * procs, seed=1000)
+    subs = [[int(x) for x in cands[pos[offs[i]:offs[i + 1]]]] for i in range(n * procs)]
     t0 = time.perf_counter()
-    pyoracle.simulate_batch(cl, subs)
+    pyoracle.simulate_batch(cl, subs[:n])
     dt = time.perf_counter() - t0
-    return {"value": round(n / dt, 3), "unit": "sims/s", "cores": 1, "kind": "port",
-            "sample": f"first {n} random subsets of chunk 0 on the same cluster, oracle computeConsolidation "
-                      f"single-threaded, {dt:.1f} s"}
+    out = {"value": round(n / dt, 3), "unit": "sims/s", "cores": 1, "kind": "port",
+           "sample": f"first {n} random subsets of chunk 0 on the same cluster, oracle computeConsolidation "
+                     f"single-threaded, {dt:.1f} s"}
+    try:
+        with mp.get_context("spawn").Pool(procs) as pool:
+            times = pool.map(_sims_worker, [(len(cl.nodes), subs[i::procs]) for i in range(procs)])
+        out["all_threads"] = {"value": round(len(subs) / max(times), 3), "unit": "sims/s", "cores": procs,
+                              "sample": f"{len(subs)} subsets over {procs} oracle processes (max {max(times):.1f} s)"}
+    except Exception as e:  # the single-thread figure stands on its own
+        out["all_threads"] = {"error": str(e)[:200]}
+    return out
 
 
 def _traffic(kernel):

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define KP_ABI_VERSION 3
+#define KP_ABI_VERSION 4
 
 enum kp_status {
   KP_OK = 0,
@@ -565,6 +565,36 @@ int32_t kp_cluster_prepare(kp_ctx* ctx, const kp_cluster* cluster, kp_cluster_pl
 int32_t kp_cluster_simulate(kp_cluster_plan* plan, const uint32_t* offsets, const uint32_t* nodes, uint32_t n_subsets,
                             int32_t multi_node, kp_sim_result* out, kp_solve_stats* stats);
 void kp_cluster_plan_destroy(kp_cluster_plan* plan);
+
+/* ---- Multi-GPU consolidation: RCCL over xGMI -----------------------------------------------------------------
+ * One rank per GPU (one process per GPU, or one thread per GPU/kp_ctx in a single process): rank 0 calls
+ * kp_comm_unique_id and hands the 128 bytes to every rank out of band; each rank calls kp_comm_init on its own
+ * kp_ctx (collective: it returns once all n_ranks joined). SURVEY §8e: the subsets of a sweep shard by contiguous
+ * index range; the snapshot is replicated (each rank prepares its own kp_cluster_plan from the same kp_cluster). */
+#define KP_COMM_ID_BYTES 128
+typedef struct kp_comm kp_comm;
+int32_t kp_comm_unique_id(uint8_t* id /* KP_COMM_ID_BYTES */);
+int32_t kp_comm_init(kp_ctx* ctx, const uint8_t* id, int32_t n_ranks, int32_t rank, kp_comm** out);
+void kp_comm_destroy(kp_comm* comm);
+
+typedef struct kp_choice {
+  int64_t subset;         /* global subset index of the best decision; -1: every subset of every rank is a no-op */
+  uint64_t counts[3];     /* no-op / delete / replace decisions over all ranks' subsets */
+  uint64_t overflowed;    /* subsets whose pods overflowed the device queue (kp_consolidate_argmin then fails) */
+  kp_sim_result result;   /* computeConsolidation(subset) (decision, prices, savings, ...) */
+} kp_choice;
+
+/* The consolidation sweep step of one rank: simulate this rank's subsets (global indices base_index + i), reduce them
+ * on the device to the best non-no-op decision (max savings, ties to the lowest global subset index), then one
+ * RCCL all-gather of the ranks' 80-byte records over xGMI; every rank returns the same choice. comm NULL: this GPU
+ * alone (n_ranks = 1). out (optional, n_subsets entries): the per-subset results, as kp_cluster_simulate.
+ * Replaces the multi-node sweep the reference runs serially on one CPU (disruption.md:89-128). */
+int32_t kp_consolidate_argmin(kp_cluster_plan* plan, kp_comm* comm, const uint32_t* offsets, const uint32_t* nodes,
+                              uint32_t n_subsets, uint64_t base_index, int32_t multi_node, kp_sim_result* out,
+                              kp_choice* best, kp_solve_stats* stats);
+/* The reduction kp_consolidate_argmin applies to the gathered per-rank records (host-only; exposed for callers that
+ * reduce over another transport, and for tests): counts are summed, the best record wins. */
+int32_t kp_choice_reduce(const kp_choice* per_rank, uint32_t n, kp_choice* out);
 
 #ifdef __cplusplus
 }

@@ -268,6 +268,20 @@ struct SimArgs {
   uint64_t* stats;                   // [8] attempts, bytes, pops, existing words scanned
 };
 
+// kp_consolidate_argmin: per-block partial bests, and the record each rank contributes to the all-gather
+struct ArgmaxPart {
+  double savings;
+  int64_t index;  // -1: no non-no-op decision in the range
+  uint64_t counts[4];  // no-op, delete, replace, pod-queue overflows
+};
+struct CommBest {
+  int64_t index;  // global subset index, -1: every decision of the rank was a no-op
+  uint64_t counts[4];  // no-op, delete, replace, pod-queue overflows
+  SimOut rec;
+};
+hipError_t launch_argmax(const SimOut* out, int n, ArgmaxPart* part, int n_parts, int64_t base, CommBest* dst,
+                         hipStream_t s);
+
 hipError_t launch_sim_prep(const SimArgs& a, hipStream_t s);
 hipError_t launch_sim(const SimArgs& a, int blocks, size_t dyn_lds, hipStream_t s);
 const void* sim_kernel_ptr();

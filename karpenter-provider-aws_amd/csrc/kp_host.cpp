@@ -5,6 +5,7 @@
 // copies results back. There is no CPU fallback: without a HIP device every compute entry point returns
 // KP_E_DEVICE (the Go shim's own CPU path is the fallback).
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <atomic>
@@ -3174,15 +3175,10 @@ void kp_cluster_plan_destroy(kp_cluster_plan* p) {
   delete p;
 }
 
-int32_t kp_cluster_simulate(kp_cluster_plan* plan, const uint32_t* offsets, const uint32_t* nodes, uint32_t n_subsets,
-                            int32_t multi_node, kp_sim_result* out, kp_solve_stats* stats) {
-  auto t0 = std::chrono::steady_clock::now();
-  if (!plan || (n_subsets && (!offsets || !out))) return fail(KP_E_INVAL, "null argument");
+// One batch on the resident snapshot, results left on the device (a_out.out); the caller holds ctx->mu.
+static int32_t SimLaunchLocked(kp_cluster_plan* plan, const uint32_t* offsets, const uint32_t* nodes, uint32_t n_subsets,
+                               int32_t multi_node, SimArgs& a_out) {
   kp_ctx* ctx = plan->ctx;
-  std::lock_guard<std::mutex> lock(ctx->mu);
-  HIPCHK(hipSetDevice(ctx->device));
-  if (stats) memset(stats, 0, sizeof *stats);
-  if (n_subsets == 0) return KP_OK;
   if (offsets[0] != 0) return fail(KP_E_INVAL, "offsets[0] != 0");
   const uint32_t n_flat = offsets[n_subsets];
   if (n_flat && !nodes) return fail(KP_E_INVAL, "null nodes");
@@ -3197,7 +3193,8 @@ int32_t kp_cluster_simulate(kp_cluster_plan* plan, const uint32_t* offsets, cons
     if (np > 65535) return fail(KP_E_UNSUPPORTED, "subset %u reschedules %llu pods (max 65535)", s, (unsigned long long)np);
     cap = std::max(cap, (int)np);
   }
-  SimArgs a = plan->a;
+  SimArgs& a = a_out;
+  a = plan->a;
   int cap2 = 1;
   while (cap2 < std::max(cap, 2 * plan->T2)) cap2 <<= 1;
   a.cap = cap;
@@ -3262,6 +3259,22 @@ int32_t kp_cluster_simulate(kp_cluster_plan* plan, const uint32_t* offsets, cons
   HIPCHK(hipEventRecord(ctx->ev0, st));
   HIPCHK(launch_sim(a, blocks, (size_t)SIM_WAVES * a.wave_lds, st));
   HIPCHK(hipEventRecord(ctx->ev1, st));
+  return KP_OK;
+}
+
+int32_t kp_cluster_simulate(kp_cluster_plan* plan, const uint32_t* offsets, const uint32_t* nodes, uint32_t n_subsets,
+                            int32_t multi_node, kp_sim_result* out, kp_solve_stats* stats) {
+  auto t0 = std::chrono::steady_clock::now();
+  if (!plan || (n_subsets && (!offsets || !out))) return fail(KP_E_INVAL, "null argument");
+  kp_ctx* ctx = plan->ctx;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device));
+  if (stats) memset(stats, 0, sizeof *stats);
+  if (n_subsets == 0) return KP_OK;
+  SimArgs a;
+  int32_t rc = SimLaunchLocked(plan, offsets, nodes, n_subsets, multi_node, a);
+  if (rc) return rc;
+  hipStream_t st = ctx->stream;
   uint64_t kst[8];
   HIPCHK(hipMemcpyAsync(out, a.out, sizeof(SimOut) * n_subsets, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(kst, a.stats, sizeof kst, hipMemcpyDeviceToHost, st));
@@ -3293,6 +3306,154 @@ int32_t kp_simulate_batch(kp_ctx* ctx, const kp_cluster* cl, const uint32_t* off
   if (stats) stats->prepare_ms = prep;
   kp_cluster_plan_destroy(plan);
   return rc;
+}
+
+}  // extern "C"
+
+// ==================================================================================================
+// Multi-GPU consolidation: RCCL communicator + the sweep's argmin (kp_consolidate_argmin)
+// ==================================================================================================
+static_assert(sizeof(kp_choice) == sizeof(CommBest), "kp_choice mirrors CommBest (the all-gathered record)");
+
+struct kp_comm {
+  kp_ctx* ctx = nullptr;
+  ncclComm_t comm = nullptr;
+  int n_ranks = 1, rank = 0;
+  DevBuf buf;  // [0]: this rank's record, [1..n_ranks]: the gathered records
+};
+
+namespace {
+int32_t nccl_fail(ncclResult_t r, const char* what) {
+  return fail(KP_E_DEVICE, "%s: %s", what, ncclGetErrorString(r));
+}
+// (savings desc, global index asc) over the records holding a decision (index >= 0)
+bool Better(const kp_choice& x, const kp_choice& best) {
+  if (x.subset < 0) return false;
+  if (best.subset < 0) return true;
+  if (x.result.savings != best.result.savings) return x.result.savings > best.result.savings;
+  return x.subset < best.subset;
+}
+}  // namespace
+
+extern "C" {
+
+int32_t kp_choice_reduce(const kp_choice* per_rank, uint32_t n, kp_choice* out) {
+  if (!out || (!per_rank && n)) return fail(KP_E_INVAL, "null argument");
+  kp_choice best;
+  memset(&best, 0, sizeof best);
+  best.subset = -1;
+  uint64_t counts[3] = {0, 0, 0}, overflowed = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    for (int k = 0; k < 3; k++) counts[k] += per_rank[i].counts[k];
+    overflowed += per_rank[i].overflowed;
+    if (Better(per_rank[i], best)) best = per_rank[i];
+  }
+  for (int k = 0; k < 3; k++) best.counts[k] = counts[k];
+  best.overflowed = overflowed;
+  if (best.subset < 0) memset(&best.result, 0, sizeof best.result);
+  *out = best;
+  return KP_OK;
+}
+
+int32_t kp_comm_unique_id(uint8_t* id) {
+  if (!id) return fail(KP_E_INVAL, "null argument");
+  ncclUniqueId u;
+  ncclResult_t r = ncclGetUniqueId(&u);
+  if (r != ncclSuccess) return nccl_fail(r, "ncclGetUniqueId");
+  static_assert(sizeof(u) == KP_COMM_ID_BYTES, "ncclUniqueId size");
+  memcpy(id, &u, sizeof u);
+  return KP_OK;
+}
+
+int32_t kp_comm_init(kp_ctx* ctx, const uint8_t* id, int32_t n_ranks, int32_t rank, kp_comm** out) {
+  if (!ctx || !id || !out) return fail(KP_E_INVAL, "null argument");
+  if (n_ranks < 1 || rank < 0 || rank >= n_ranks) return fail(KP_E_INVAL, "rank %d of %d", rank, n_ranks);
+  HIPCHK(hipSetDevice(ctx->device));
+  auto c = std::make_unique<kp_comm>();
+  c->ctx = ctx;
+  c->n_ranks = n_ranks;
+  c->rank = rank;
+  ncclUniqueId u;
+  memcpy(&u, id, sizeof u);
+  ncclResult_t r = ncclCommInitRank(&c->comm, n_ranks, u, rank);
+  if (r != ncclSuccess) return nccl_fail(r, "ncclCommInitRank");
+  HIPCHK(c->buf.alloc(sizeof(CommBest) * (size_t)(n_ranks + 1)));
+  *out = c.release();
+  return KP_OK;
+}
+
+void kp_comm_destroy(kp_comm* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->ctx->device);
+  if (c->comm) (void)ncclCommDestroy(c->comm);
+  delete c;
+}
+
+int32_t kp_consolidate_argmin(kp_cluster_plan* plan, kp_comm* comm, const uint32_t* offsets, const uint32_t* nodes,
+                              uint32_t n_subsets, uint64_t base_index, int32_t multi_node, kp_sim_result* out,
+                              kp_choice* best, kp_solve_stats* stats) {
+  auto t0 = std::chrono::steady_clock::now();
+  if (!plan || !best || (n_subsets && !offsets)) return fail(KP_E_INVAL, "null argument");
+  if (comm && comm->ctx->device != plan->ctx->device) return fail(KP_E_INVAL, "comm and plan are on different GPUs");
+  kp_ctx* ctx = plan->ctx;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device));
+  if (stats) memset(stats, 0, sizeof *stats);
+  hipStream_t st = ctx->stream;
+  // this rank's record slot: its own buffer without a comm
+  DevBuf solo;
+  CommBest* mine;
+  if (comm) {
+    mine = (CommBest*)comm->buf.p;
+  } else {
+    HIPCHK(solo.alloc(sizeof(CommBest)));
+    mine = (CommBest*)solo.p;
+  }
+  SimArgs a;
+  memset(&a, 0, sizeof a);
+  float ms = 0;
+  uint64_t kst[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  DevBuf parts;
+  const int n_parts = (int)std::min<uint32_t>(std::max<uint32_t>((n_subsets + 4095) / 4096, 1), 1024);
+  HIPCHK(parts.alloc(sizeof(ArgmaxPart) * n_parts));
+  if (n_subsets) {
+    int32_t rc = SimLaunchLocked(plan, offsets, nodes, n_subsets, multi_node, a);
+    if (rc) return rc;
+    if (out) HIPCHK(hipMemcpyAsync(out, a.out, sizeof(SimOut) * n_subsets, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(kst, a.stats, sizeof kst, hipMemcpyDeviceToHost, st));
+  }
+  HIPCHK(launch_argmax(n_subsets ? a.out : nullptr, (int)n_subsets, (ArgmaxPart*)parts.p, n_parts,
+                       (int64_t)base_index, mine, st));
+  const int nr = comm ? comm->n_ranks : 1;
+  vector<CommBest> recs(nr);
+  if (comm) {  // one collective: every rank's 80-byte record to every rank (RCCL over xGMI)
+    CommBest* gathered = mine + 1;
+    ncclResult_t r = ncclAllGather(mine, gathered, sizeof(CommBest), ncclUint8, comm->comm, st);
+    if (r != ncclSuccess) return nccl_fail(r, "ncclAllGather");
+    HIPCHK(hipMemcpyAsync(recs.data(), gathered, sizeof(CommBest) * nr, hipMemcpyDeviceToHost, st));
+  } else {
+    HIPCHK(hipMemcpyAsync(recs.data(), mine, sizeof(CommBest), hipMemcpyDeviceToHost, st));
+  }
+  HIPCHK(hipStreamSynchronize(st));
+  if (n_subsets) HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+  for (int i = 0; i < nr; i++)
+    if (recs[i].counts[3]) return fail(KP_E_DEVICE, "rank %d: %llu subsets overflowed the pod queue", i,
+                                       (unsigned long long)recs[i].counts[3]);
+  vector<kp_choice> ch(nr);
+  memcpy(ch.data(), recs.data(), sizeof(kp_choice) * nr);
+  int32_t rc = kp_choice_reduce(ch.data(), (uint32_t)nr, best);
+  if (rc) return rc;
+  if (stats) {
+    stats->device_ms = ms;
+    stats->solve_kernel_ms = ms;
+    stats->attempts = kst[0];
+    stats->bytes_algorithmic = kst[1];
+    stats->pops = kst[2];
+    stats->phase_cycles[0] = kst[3];
+    stats->prepare_ms = plan->prepare_ms;
+    stats->host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
+  return KP_OK;
 }
 
 }  // extern "C"

@@ -677,3 +677,91 @@ hipError_t launch_sim(const SimArgs& a, int blocks, size_t dyn_lds, hipStream_t 
   return hipGetLastError();
 }
 const void* sim_kernel_ptr() { return reinterpret_cast<const void*>(sim_kernel<SIM_WAVES>); }
+
+// ------------------------------------------------------------------------------------------------
+// Best decision of a simulated batch (kp_consolidate_argmin): max savings over non-no-op decisions, ties to the
+// lowest subset index, plus the decision counts. Two stages: blocks reduce contiguous ranges, one block the partials.
+// ------------------------------------------------------------------------------------------------
+#define ARGMAX_THREADS 256
+__device__ __forceinline__ bool better(double s, int64_t i, double bs, int64_t bi) {
+  return i >= 0 && (bi < 0 || s > bs || (s == bs && i < bi));
+}
+__global__ __launch_bounds__(ARGMAX_THREADS) void argmax_kernel(const SimOut* out, int n, ArgmaxPart* part) {
+  __shared__ double s_s[ARGMAX_THREADS];
+  __shared__ int64_t s_i[ARGMAX_THREADS];
+  __shared__ unsigned long long s_cnt[4];
+  const int tid = threadIdx.x;
+  if (tid < 4) s_cnt[tid] = 0;
+  __syncthreads();
+  const int per = (n + gridDim.x - 1) / gridDim.x;
+  const int lo = blockIdx.x * per, hi = min(n, lo + per);
+  double bs = 0;
+  int64_t bi = -1;
+  unsigned long long c[4] = {0, 0, 0, 0};
+  for (int i = lo + tid; i < hi; i += ARGMAX_THREADS) {
+    const SimOut o = out[i];
+    const int d = o.decision;
+    c[d == KP_DECISION_DELETE ? 1 : (d == KP_DECISION_REPLACE ? 2 : 0)]++;
+    if (o.n_pods == 0xFFFFFFFFu) c[3]++;  // overflowed the pod queue (an error on the host)
+    if (d != KP_DECISION_NOOP && better(o.savings, i, bs, bi)) bs = o.savings, bi = i;
+  }
+  s_s[tid] = bs;
+  s_i[tid] = bi;
+  for (int k = 0; k < 4; k++) atomicAdd(&s_cnt[k], c[k]);
+  __syncthreads();
+  for (int w = ARGMAX_THREADS / 2; w > 0; w >>= 1) {
+    if (tid < w && better(s_s[tid + w], s_i[tid + w], s_s[tid], s_i[tid])) {
+      s_s[tid] = s_s[tid + w];
+      s_i[tid] = s_i[tid + w];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    part[blockIdx.x].savings = s_s[0];
+    part[blockIdx.x].index = s_i[0];
+    for (int k = 0; k < 4; k++) part[blockIdx.x].counts[k] = s_cnt[k];
+  }
+}
+// one block: partials -> the record this rank contributes to the all-gather
+__global__ __launch_bounds__(ARGMAX_THREADS) void argmax_final_kernel(const ArgmaxPart* part, int np, const SimOut* out,
+                                                                     int64_t base, CommBest* dst) {
+  __shared__ double s_s[ARGMAX_THREADS];
+  __shared__ int64_t s_i[ARGMAX_THREADS];
+  __shared__ unsigned long long s_cnt[4];
+  const int tid = threadIdx.x;
+  if (tid < 4) s_cnt[tid] = 0;
+  __syncthreads();
+  double bs = 0;
+  int64_t bi = -1;
+  unsigned long long c[4] = {0, 0, 0, 0};
+  for (int i = tid; i < np; i += ARGMAX_THREADS) {
+    if (better(part[i].savings, part[i].index, bs, bi)) bs = part[i].savings, bi = part[i].index;
+    for (int k = 0; k < 4; k++) c[k] += part[i].counts[k];
+  }
+  s_s[tid] = bs;
+  s_i[tid] = bi;
+  for (int k = 0; k < 4; k++) atomicAdd(&s_cnt[k], c[k]);
+  __syncthreads();
+  for (int w = ARGMAX_THREADS / 2; w > 0; w >>= 1) {
+    if (tid < w && better(s_s[tid + w], s_i[tid + w], s_s[tid], s_i[tid])) {
+      s_s[tid] = s_s[tid + w];
+      s_i[tid] = s_i[tid + w];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    dst->index = s_i[0] >= 0 ? base + s_i[0] : -1;
+    if (s_i[0] >= 0) dst->rec = out[s_i[0]];
+    else memset(&dst->rec, 0, sizeof(SimOut));
+    for (int k = 0; k < 4; k++) dst->counts[k] = s_cnt[k];
+  }
+}
+hipError_t launch_argmax(const SimOut* out, int n, ArgmaxPart* part, int n_parts, int64_t base, CommBest* dst,
+                         hipStream_t s) {
+  if (n > 0) hipLaunchKernelGGL(argmax_kernel, dim3(n_parts), dim3(ARGMAX_THREADS), 0, s, out, n, part);
+  else hipMemsetAsync(part, 0xFF, sizeof(ArgmaxPart) * n_parts, s);  // index -1 everywhere (counts fixed below)
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(argmax_final_kernel, dim3(1), dim3(ARGMAX_THREADS), 0, s, part, n > 0 ? n_parts : 0, out, base, dst);
+  return hipGetLastError();
+}

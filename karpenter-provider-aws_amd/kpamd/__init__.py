@@ -78,6 +78,13 @@ def load_lib(path=LIB_PATH):
         "kp_cluster_simulate": (C.c_int32, [C.c_void_p, P(C.c_uint32), P(C.c_uint32), C.c_uint32, C.c_int32,
                                             P(abi.SimResult), P(abi.SolveStats)]),
         "kp_cluster_plan_destroy": (None, [C.c_void_p]),
+        "kp_comm_unique_id": (C.c_int32, [C.c_char_p]),
+        "kp_comm_init": (C.c_int32, [C.c_void_p, C.c_char_p, C.c_int32, C.c_int32, P(C.c_void_p)]),
+        "kp_comm_destroy": (None, [C.c_void_p]),
+        "kp_consolidate_argmin": (C.c_int32, [C.c_void_p, C.c_void_p, P(C.c_uint32), P(C.c_uint32), C.c_uint32,
+                                              C.c_uint64, C.c_int32, P(abi.SimResult), P(abi.Choice),
+                                              P(abi.SolveStats)]),
+        "kp_choice_reduce": (C.c_int32, [P(abi.Choice), C.c_uint32, P(abi.Choice)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -469,6 +476,23 @@ class ClusterPlan:
             n, 1 if multi_node else 0, out.ctypes.data_as(P(abi.SimResult)), C.byref(st)))
         return out[:n], stats_dict(st)
 
+    def argmin(self, offsets, nodes, base_index=0, comm=None, multi_node=True, read_all=False):
+        """kp_consolidate_argmin: this rank's subsets (CSR, global indices base_index + i) simulated, reduced on the
+        device and across ranks (RCCL all-gather when comm is a Comm). Returns (choice dict, per-subset results
+        or None, stats)."""
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint32)
+        nodes = np.ascontiguousarray(nodes, dtype=np.uint32)
+        n = len(offsets) - 1
+        out = np.zeros(max(n, 1), dtype=abi.sim_dtype()) if read_all else None
+        ch = abi.Choice()
+        st = abi.SolveStats()
+        P = C.POINTER
+        _check(self.ctx.lib, self.ctx.lib.kp_consolidate_argmin(
+            self.h, comm.h if comm is not None else None, offsets.ctypes.data_as(P(C.c_uint32)),
+            nodes.ctypes.data_as(P(C.c_uint32)) if len(nodes) else None, n, int(base_index), 1 if multi_node else 0,
+            out.ctypes.data_as(P(abi.SimResult)) if out is not None else None, C.byref(ch), C.byref(st)))
+        return choice_dict(ch), (out[:n] if out is not None else None), stats_dict(st)
+
     def close(self):
         if self.h:
             self.ctx.lib.kp_cluster_plan_destroy(self.h)
@@ -479,3 +503,46 @@ class ClusterPlan:
             self.close()
         except Exception:
             pass
+
+
+def choice_dict(ch):
+    return {"subset": int(ch.subset), "counts": [int(x) for x in ch.counts], "overflowed": int(ch.overflowed),
+            "result": sim_dict(ch.result)}
+
+
+def comm_unique_id(lib=None):
+    """kp_comm_unique_id (rank 0): 128 bytes every rank passes to Comm."""
+    lib = lib or load_lib()
+    buf = C.create_string_buffer(abi.COMM_ID_BYTES)
+    _check(lib, lib.kp_comm_unique_id(buf))
+    return buf.raw
+
+
+class Comm:
+    """kp_comm: one rank of the RCCL communicator over the node's GPUs (kp_comm_init is collective)."""
+
+    def __init__(self, ctx, uid, n_ranks, rank):
+        self.ctx = ctx
+        h = C.c_void_p()
+        _check(ctx.lib, ctx.lib.kp_comm_init(ctx.h, bytes(uid), n_ranks, rank, C.byref(h)))
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self.ctx.lib.kp_comm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def choice_reduce(records, lib=None):
+    """kp_choice_reduce over per-rank kp_choice records (the all-gather's host step)."""
+    lib = lib or load_lib()
+    arr = (abi.Choice * max(1, len(records)))(*records)
+    out = abi.Choice()
+    _check(lib, lib.kp_choice_reduce(arr, len(records), C.byref(out)))
+    return out

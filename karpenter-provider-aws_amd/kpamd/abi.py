@@ -206,6 +206,14 @@ class SimResult(C.Structure):
                 ("n_pods", C.c_uint32)]
 
 
+class Choice(C.Structure):
+    """kp_choice: the sweep's best decision over all ranks (kp_consolidate_argmin / kp_choice_reduce)."""
+    _fields_ = [("subset", C.c_int64), ("counts", C.c_uint64 * 3), ("overflowed", C.c_uint64), ("result", SimResult)]
+
+
+COMM_ID_BYTES = 128
+
+
 class FeasibilityQuery(C.Structure):
     _fields_ = [("requirements", Requirements), ("requests", ResourceList)]
 

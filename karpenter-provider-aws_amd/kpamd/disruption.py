@@ -10,9 +10,11 @@ CS3 and R:website/content/en/preview/concepts/disruption.md:89-128):
                                             firstN lowers it to len-1 only when len <= max); every prefix
                                             the search can touch is simulated in ONE batch, then the
                                             search is replayed exactly over those results
-  sweep(...)                                the config-4 sweep: many subsets sharded over ranks, best
-                                            decision by (savings desc, subset index asc) across ranks
-                                            with two scalar RCCL all-reduces (MAX savings, MIN index)
+  sweep(...)                                the config-4 sweep: this rank's contiguous share of the subsets
+                                            through kp_consolidate_argmin (simulation, device argmax, one
+                                            RCCL all-gather of the ranks' records inside libkp)
+  local_choice(...)                         a rank's kp_choice record from per-subset results on the host
+                                            (what the device argmax produces; CPU tests and other transports)
 
 Decisions are kp_decision values: 0 no-op, 1 delete, 2 replace.
 """
@@ -132,3 +134,39 @@ def shard(n, rank, world):
     per = (n + world - 1) // world
     lo = min(n, rank * per)
     return lo, min(n, lo + per)
+
+
+def local_choice(results, base_index=0):
+    """kp_choice record of one rank from its per-subset results (dicts or the simulate_csr structured array): the
+    best non-no-op decision (savings desc, global subset index asc) and the decision counts."""
+    from . import abi
+    ch = abi.Choice()
+    ch.subset = -1
+    dec = [int(r["decision"]) for r in results]
+    for k in range(3):
+        ch.counts[k] = sum(1 for d in dec if d == k)
+    s, i = best_local(results if isinstance(results, np.ndarray) else _as_struct(results), base_index)
+    if i >= 0:
+        r = results[i - base_index]
+        ch.subset = i
+        ch.result = abi.SimResult(int(r["decision"]), int(r["nodepool"]), float(r["candidate_price"]),
+                                  float(r["replacement_price"]), float(r["savings"]), int(r["n_options"]),
+                                  int(r["n_pods"]))
+    return ch
+
+
+def _as_struct(results):
+    from . import abi
+    out = np.zeros(len(results), dtype=abi.sim_dtype())
+    for j, r in enumerate(results):
+        out[j]["decision"] = r["decision"]
+        out[j]["savings"] = r["savings"]
+    return out
+
+
+def sweep(plan, offsets, nodes, base_index=0, comm=None, multi_node=True):
+    """The config-4 sweep step of one rank: kp_consolidate_argmin over this rank's CSR subsets (global indices
+    base_index + i); with a Comm the best decision is reduced across ranks inside libkp (RCCL all-gather).
+    Returns (choice, stats)."""
+    ch, _, st = plan.argmin(offsets, nodes, base_index=base_index, comm=comm, multi_node=multi_node)
+    return ch, st

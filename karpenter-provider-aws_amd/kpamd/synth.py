@@ -358,8 +358,8 @@ def random_problem(catalog, seed, n_types=120, n_pods=300, n_pools=3, n_existing
 # ------------------------------------------------------------------------------------------------
 # config 4: a running cluster for multi-node consolidation (10k nodes, 8-40 pods per node)
 # ------------------------------------------------------------------------------------------------
-C4_CPU = [50, 100, 250, 500, 1000]
-C4_MEM = [64, 128, 256, 512, 1024, 2048]
+C4_CPU = [250, 500, 1000, 2000]
+C4_MEM = [256, 512, 1024, 2048, 4096]
 
 
 def node_labels(it, zone_i, capacity_type, nodepool, hostname):
@@ -373,10 +373,14 @@ def node_labels(it, zone_i, capacity_type, nodepool, hostname):
     return labels
 
 
-def config4(catalog, n_nodes=10_000, seed=4, n_shapes=32, pods_min=8, pods_max=40, fill=(0.7, 0.98)):
-    """A cluster of n_nodes c/m/r nodes (2-16 vCPU, 3 AZ, 80% on-demand) running 8-40 pods each at
-    70-98% utilisation; 2 NodePools without limits. Candidates are sorted by disruption cost (fewer
-    pods first, then name: R:website/content/en/preview/concepts/disruption.md:101-103)."""
+def config4(catalog, n_nodes=10_000, seed=4, n_shapes=32, pods_min=8, pods_max=40, fill=(0.97, 1.0), topup=True,
+            loose=0.004, loose_fill=(0.4, 0.8)):
+    """A cluster of n_nodes c/m/r nodes (2-16 vCPU, 3 AZ, 80% on-demand) running 8-40 pods each: a random start,
+    then topped up with the largest shapes that fit, to 97-100% of the binding resource (0.4% of the nodes stay
+    40-80% used: the cluster's usable slack), so that the displaced pods of a candidate subset often exceed the remaining
+    slack: the sweep then sees delete, replace and no-op decisions (at 70-98% fill every subset was a delete);
+    2 NodePools without limits. Candidates are sorted by disruption cost (fewer pods first, then name:
+    R:website/content/en/preview/concepts/disruption.md:101-103)."""
     rng = np.random.default_rng(seed)
     pools = [
         NodePool("default", 10, 0, [("karpenter.sh/capacity-type", "In", ["on-demand", "spot"]),
@@ -410,6 +414,7 @@ def config4(catalog, n_nodes=10_000, seed=4, n_shapes=32, pods_min=8, pods_max=4
         shapes.append(sh)
     shape_zone = [ZONES.index(sh.node_selector["topology.kubernetes.io/zone"]) if sh.node_selector else -1
                   for sh in shapes]
+    topup_order = sorted(range(n_shapes), key=lambda i: (-shapes[i].requests["cpu"], -shapes[i].requests["memory"], i))
     nodes = []
     pod_shape, pod_creation, pod_uid = [], [], []
     for n in range(n_nodes):
@@ -419,7 +424,8 @@ def config4(catalog, n_nodes=10_000, seed=4, n_shapes=32, pods_min=8, pods_max=4
         name = f"node-{n:06d}"
         labels = node_labels(it, zone_i, ct, "default", name)
         alloc = it.allocatable()
-        frac = float(rng.uniform(*fill))
+        is_loose = rng.random() < loose  # an underutilised node (no top-up): the cluster's usable slack
+        frac = float(rng.uniform(*(loose_fill if is_loose else fill)))
         k = int(rng.integers(pods_min, pods_max + 1))
         used = {"cpu": 0, "memory": 0, "pods": 0}
         pods = []
@@ -438,6 +444,18 @@ def config4(catalog, n_nodes=10_000, seed=4, n_shapes=32, pods_min=8, pods_max=4
             pod_shape.append(s_i)
             pod_creation.append(1_750_000_000 + int(rng.integers(0, 86_400)))
             pod_uid.append(int(rng.integers(0, np.iinfo(np.int64).max)))
+        if topup and not is_loose:  # pack the rest: the largest shapes that still fit under frac, up to pods_max pods
+            for s_i in topup_order:
+                if shape_zone[s_i] not in (-1, zone_i):
+                    continue
+                rq = shapes[s_i].requests
+                while len(pods) < pods_max and not any(used[r] + rq[r] > frac * alloc[r] for r in used):
+                    for r in used:
+                        used[r] += rq[r]
+                    pods.append(len(pod_shape))
+                    pod_shape.append(s_i)
+                    pod_creation.append(1_750_000_000 + int(rng.integers(0, 86_400)))
+                    pod_uid.append(int(rng.integers(0, np.iinfo(np.int64).max)))
         avail = {r: alloc[r] - used[r] for r in used}
         nodes.append(ClusterNode(ExistingNode(name, labels, avail, {}, [], True), 0, catalog.index(it), pods))
     cands = sorted(range(n_nodes), key=lambda i: (len(nodes[i].pods), nodes[i].node.name))

@@ -1,0 +1,76 @@
+"""Full-size parity fixtures (oracle results at BASELINE.json's sizes), generated in this container by the CPU oracle
+(oracle/liboracle.so) on the committed generators, for the -m gpu tests in tests/test_fullsize_parity.py:
+
+  config2-50000   Solve of config 2 at 50k pods: digest of the placement array and of the NodeClaims
+                  (nodepool, pods in add order, options after OrderByPrice + Truncate, requirements)
+  config3-100000  Solve of config 3 at 100k pods (zone + hostname spread onto 5k existing nodes): same digests
+  config4-10000   computeConsolidation on the 10k-node config-4 cluster for every firstNConsolidationOption prefix
+                  (candidates[0:mid+1], mid = 1..100) and 200 random subsets: every decision field
+
+Run from the repo root: python tests/golden/make_fullsize_digests.py  (about 6 minutes)
+"""
+import hashlib
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "karpenter-provider-aws_amd"))
+
+OUT = os.path.join(HERE, "fullsize_digests.json")
+
+
+def solve_digest(res):
+    """Stable digest of a Solve result (the device path returns the same structure)."""
+    import numpy as np
+    pl = hashlib.sha256(np.asarray(res["placement"], dtype=np.int32).tobytes()).hexdigest()
+    h = hashlib.sha256()
+    for n in res["nodeclaims"]:
+        h.update(json.dumps([n["nodepool"], n["pods"], n["options"], n["n_remaining"], n["requirements"]],
+                            sort_keys=True).encode())
+    return {"placement_sha256": pl, "nodeclaims_sha256": h.hexdigest(), "nodeclaims": len(res["nodeclaims"]),
+            "placed": int((np.asarray(res["placement"]) != -1).sum()),
+            "on_existing": int((np.asarray(res["placement"]) <= -2).sum())}
+
+
+def config4_subsets(cl):
+    import numpy as np
+    from kpamd import disruption
+    cands = np.asarray(cl.candidates, dtype=np.uint32)
+    pre = [[int(x) for x in cands[:m + 1]] for m in disruption.MultiNodeConsolidation.search_prefixes(len(cands))]
+    offs, pos = disruption.random_subsets_csr(len(cands), 200, seed=4242)
+    rnd = [[int(x) for x in cands[pos[offs[i]:offs[i + 1]]]] for i in range(200)]
+    return pre, rnd
+
+
+def sim_record(r):
+    return [int(r["decision"]), int(r["nodepool"]), float(r["candidate_price"]).hex(), float(r["replacement_price"]).hex(),
+            float(r["savings"]).hex(), int(r["n_options"]), int(r["n_pods"])]
+
+
+def main():
+    import kpamd
+    from kpamd import catalog, synth
+    from oracle import pyoracle
+    cat = catalog.build_catalog(kpamd.load_lib())
+    out = {}
+    for name, mk in (("config2-50000", lambda: synth.config2(cat, n_pods=50_000, seed=2)),
+                     ("config3-100000", lambda: synth.config3(cat, n_pods=100_000))):
+        t = time.time()
+        out[name] = solve_digest(pyoracle.solve(mk()))
+        print(name, out[name], f"{time.time() - t:.1f}s", flush=True)
+    t = time.time()
+    cl = synth.config4(cat, n_nodes=10_000, seed=4)
+    pre, rnd = config4_subsets(cl)
+    res, _ = pyoracle.simulate_batch(cl, pre + rnd)
+    out["config4-10000"] = {"prefixes": [sim_record(r) for r in res[:len(pre)]],
+                            "random": [sim_record(r) for r in res[len(pre):]], "random_seed": 4242}
+    print("config4", len(res), f"{time.time() - t:.1f}s", flush=True)
+    json.dump(out, open(OUT, "w"), indent=0)
+
+
+if __name__ == "__main__":
+    main()

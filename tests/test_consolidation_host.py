@@ -118,3 +118,59 @@ def test_reduce_best_gloo_world2():
     assert out[0][2] == out[1][2] == (3.0, 5)  # tie on savings -> lowest subset index
     assert out[0][3] == out[1][3] == (4.5, 70)
     assert out[0][4] == out[1][4] == (-np.inf, -1)
+
+
+def _sweep_worker(rank, world, port, q):
+    """One rank of the sweep on the CPU-validated path: the oracle simulates this rank's contiguous share of the
+    subsets, the rank's kp_choice record goes through a gloo all-gather, and libkp's kp_choice_reduce picks the
+    best (the host step of kp_consolidate_argmin)."""
+    import torch.distributed as dist
+    import kpamd
+    from kpamd import abi, catalog, disruption, synth
+    from oracle import pyoracle
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cat = catalog.build_catalog(kpamd.load_lib())
+        cl = synth.config4(cat, n_nodes=80, seed=44)
+        subs = synth.consolidation_subsets(cl, 40, seed=7, max_size=30)
+        lo, hi = disruption.shard(len(subs), rank, world)
+        res, _ = pyoracle.simulate_batch(cl, subs[lo:hi]) if hi > lo else ([], None)
+        rec = disruption.local_choice(res, base_index=lo)
+        raw = bytes(memoryview(rec))
+        gathered = [None] * world
+        dist.all_gather_object(gathered, raw)
+        recs = [abi.Choice.from_buffer_copy(g) for g in gathered]
+        best = kpamd.choice_reduce(recs)
+        q.put((rank, kpamd.choice_dict(best)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sweep_argmin_gloo_world2():
+    """World-size 2 sweep (gloo): each rank simulates real subsets of a config-4 cluster; the reduced best over the
+    ranks equals the N=1 best over all subsets (savings desc, lowest global index), counts summed."""
+    import multiprocessing as mp
+    import socket
+    import kpamd
+    from kpamd import catalog, disruption, synth
+    from oracle import pyoracle
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_sweep_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = dict(q.get(timeout=300) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    cat = catalog.build_catalog(kpamd.load_lib())
+    cl = synth.config4(cat, n_nodes=80, seed=44)
+    subs = synth.consolidation_subsets(cl, 40, seed=7, max_size=30)
+    res, _ = pyoracle.simulate_batch(cl, subs)
+    want = kpamd.choice_dict(kpamd.choice_reduce([disruption.local_choice(res, 0)]))
+    assert out[0] == out[1] == want
+    assert want["subset"] >= 0 and sum(want["counts"]) == len(subs)

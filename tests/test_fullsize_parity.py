@@ -1,0 +1,59 @@
+"""Device parity at BASELINE.json's full sizes, against oracle results committed as fixtures
+(tests/golden/fullsize_digests.json, generated in this container by tests/golden/make_fullsize_digests.py from the
+same generators and seeds): the headline config 2 at 50k pods, config 3 at 100k pods onto 5k existing nodes, and
+config 4's 10k-node cluster on every firstNConsolidationOption prefix plus 200 random candidate subsets.
+
+The -m "not gpu" test checks the fixture is consistent with the generators (counts and shapes)."""
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "golden"))
+
+
+@pytest.fixture(scope="module")
+def digests():
+    return json.load(open(os.path.join(HERE, "golden", "fullsize_digests.json")))
+
+
+def test_fixture_shape(digests):
+    assert digests["config2-50000"]["placed"] == 50_000
+    assert digests["config3-100000"]["on_existing"] > 0
+    c4 = digests["config4-10000"]
+    assert len(c4["prefixes"]) == 100 and len(c4["random"]) == 200
+    decisions = {r[0] for r in c4["random"]}
+    assert decisions >= {1, 2}, "the near-capacity cluster yields deletes and replacements"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["config2-50000", "config3-100000"])
+def test_solve_fullsize(ctx, catalog, digests, name):
+    import kpamd
+    import make_fullsize_digests as mk
+    from kpamd import synth
+    prob = synth.config2(catalog, n_pods=50_000, seed=2) if name.startswith("config2") else \
+        synth.config3(catalog, n_pods=100_000)
+    got = mk.solve_digest(kpamd.Scheduler(ctx, prob).solve())
+    assert got == digests[name]
+
+
+@pytest.mark.gpu
+def test_consolidation_fullsize(ctx, catalog, digests):
+    import kpamd
+    import make_fullsize_digests as mk
+    from kpamd import synth
+    cl = synth.config4(catalog, n_nodes=10_000, seed=4)
+    pre, rnd = mk.config4_subsets(cl)
+    plan = kpamd.ClusterPlan(ctx, cl)
+    try:
+        res, _ = plan.simulate(pre + rnd)
+    finally:
+        plan.close()
+    want = digests["config4-10000"]
+    got = [mk.sim_record(r) for r in res]
+    assert got[:len(pre)] == want["prefixes"]
+    assert got[len(pre):] == want["random"]

@@ -5,6 +5,7 @@ import os
 import sys
 
 import pytest
+import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
@@ -95,3 +96,32 @@ def test_multi_and_single_node_commands(ctx, catalog):
     want1, _ = pyoracle.simulate_batch(cl, [[c] for c in cl.candidates], multi_node=False)
     first = next(((c, r) for c, r in zip(cl.candidates, want1) if r["decision"] != 0), None)
     assert single == first
+
+
+@pytest.mark.gpu
+def test_consolidate_argmin_device(ctx, catalog):
+    """kp_consolidate_argmin: the device argmax over a batch (+ the RCCL all-gather on a one-rank communicator)
+    equals the host reduction of the per-subset results and of the oracle's (savings desc, lowest global index)."""
+    import kpamd
+    from kpamd import disruption, synth
+    from oracle import pyoracle
+    cl = synth.config4(catalog, n_nodes=120, seed=4)
+    subs = synth.consolidation_subsets(cl, 300, seed=5)
+    offs = np.zeros(len(subs) + 1, dtype=np.uint32)
+    offs[1:] = np.cumsum([len(s) for s in subs])
+    flat = np.concatenate([np.asarray(s, dtype=np.uint32) for s in subs])
+    plan = kpamd.ClusterPlan(ctx, cl)
+    comm = kpamd.Comm(ctx, kpamd.comm_unique_id(), 1, 0)
+    try:
+        ch, res, _ = plan.argmin(offs, flat, base_index=1000, read_all=True)
+        ch2, _, _ = plan.argmin(offs, flat, base_index=1000, comm=comm)
+        empty, _, _ = plan.argmin(np.zeros(1, dtype=np.uint32), np.zeros(0, dtype=np.uint32), base_index=7, comm=comm)
+    finally:
+        comm.close()
+        plan.close()
+    host = kpamd.choice_dict(kpamd.choice_reduce([disruption.local_choice(res, 1000)]))
+    assert ch == ch2 == host
+    want, _ = pyoracle.simulate_batch(cl, subs)
+    oracle = kpamd.choice_dict(kpamd.choice_reduce([disruption.local_choice(want, 1000)]))
+    assert ch == oracle
+    assert empty["subset"] == -1 and empty["counts"] == [0, 0, 0]
