@@ -30,10 +30,10 @@ def check(ctx, cluster, subsets, multi_node=True):
 
 def test_config4_small(ctx, catalog):
     from kpamd import synth
-    cl = synth.config4(catalog, n_nodes=120, seed=4)
+    cl = synth.config4(catalog, n_nodes=120, seed=4, loose=0.05)
     got = check(ctx, cl, synth.consolidation_subsets(cl, 30, seed=5))
     kinds = {r["decision"] for r in got}
-    assert {0, 1}.issubset(kinds)
+    assert {0, 1, 2}.issubset(kinds)
 
 
 def test_config4_single_node(ctx, catalog):
