@@ -431,9 +431,14 @@ def pod_queries(problem):
 
 
 def sim_dict(r):
-    return {"decision": int(r.decision), "nodepool": int(r.replacement_nodepool), "candidate_price": r.candidate_price,
-            "replacement_price": r.replacement_price, "savings": r.savings, "n_options": int(r.n_options),
-            "n_pods": int(r.n_pods)}
+    """kp_sim_result (ctypes struct or a record of abi.sim_dtype()) -> dict."""
+    if isinstance(r, np.void):
+        g, np_key = (lambda k: r[k]), "nodepool"
+    else:
+        g, np_key = (lambda k: getattr(r, k)), "replacement_nodepool"
+    return {"decision": int(g("decision")), "nodepool": int(g(np_key)),
+            "candidate_price": float(g("candidate_price")), "replacement_price": float(g("replacement_price")),
+            "savings": float(g("savings")), "n_options": int(g("n_options")), "n_pods": int(g("n_pods"))}
 
 
 class ClusterPlan:
