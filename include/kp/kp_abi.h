@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define KP_ABI_VERSION 4
+#define KP_ABI_VERSION 5
 
 enum kp_status {
   KP_OK = 0,
@@ -387,6 +387,26 @@ typedef struct kp_ec2_info {
   int32_t reserved2_;
 } kp_ec2_info;
 
+/* One kubelet eviction-signal value (memory.available / nodefs.available): a quantity or a percentage of the
+ * node's capacity (R:pkg/providers/instancetype/types.go:571-598, computeEvictionSignal / mustParsePercentage). */
+typedef struct kp_eviction_value {
+  int32_t set;                   /* 0: the key is absent from the map */
+  int32_t is_percent;            /* 1: "<p>%" (percent holds p; 100 disables the threshold) */
+  double percent;
+  int64_t milli;                 /* quantity in milli-units (resource.Quantity.MilliValue) when !is_percent */
+} kp_eviction_value;
+
+/* EC2NodeClass.spec.kubelet overrides (R:pkg/apis/v1/ec2nodeclass.go KubeletConfiguration). Resource maps carry
+ * the keys the user set (present bits); eviction maps are nil unless has_* is set. */
+typedef struct kp_kubelet {
+  kp_resource_list kube_reserved;
+  kp_resource_list system_reserved;
+  int32_t has_eviction_hard;
+  int32_t has_eviction_soft;
+  kp_eviction_value hard_memory_available, hard_nodefs_available;
+  kp_eviction_value soft_memory_available, soft_nodefs_available;
+} kp_kubelet;
+
 /* EC2NodeClass subset that changes results (AL2023 family; kubelet overrides). */
 typedef struct kp_nodeclass {
   const char* region;
@@ -396,6 +416,7 @@ typedef struct kp_nodeclass {
   int32_t max_pods;              /* < 0: nil */
   int32_t pods_per_core;         /* <= 0: nil */
   int32_t reserved_;
+  const kp_kubelet* kubelet;     /* NULL: no kubelet block (defaults) */
 } kp_nodeclass;
 
 /* instancetype.NewInstanceType capacity + Overhead.Total() for the AL2023 family (R:types.go:123-155,
@@ -403,6 +424,15 @@ typedef struct kp_nodeclass {
  * stays with the caller (kpamd/catalog.py mirrors it). */
 int32_t kp_instance_type_resolve(const kp_options* opts, const kp_ec2_info* info, const kp_nodeclass* nc,
                                  kp_resource_list* capacity, kp_resource_list* overhead);
+
+/* The three InstanceTypeOverhead lists NewInstanceType builds (R:types.go:145-149): kubeReservedResources
+ * (R:types.go:500-533, overrides win), systemReservedResources (R:types.go:494-498) and evictionThreshold
+ * (R:types.go:535-564: defaults, then the max over evictionHard and evictionSoft — soft honoured for AL2023's
+ * EvictionSoftEnabled — of each signal, assigned over the defaults). kp_instance_type_resolve's overhead is
+ * their sum (Overhead.Total()). */
+int32_t kp_instance_type_overhead(const kp_options* opts, const kp_ec2_info* info, const kp_nodeclass* nc,
+                                  kp_resource_list* kube_reserved, kp_resource_list* system_reserved,
+                                  kp_resource_list* eviction_threshold);
 
 /* ---- feasibility (CompatibleAvailableFilter, batched) ------------------------------------- */
 typedef struct kp_feasibility_query {

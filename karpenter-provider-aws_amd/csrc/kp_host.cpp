@@ -917,51 +917,110 @@ int32_t kp_catalog_update_offerings(kp_catalog* c, const kp_offering_update* ups
   return KP_OK;
 }
 
-// instancetype.NewInstanceType capacity + Overhead.Total() for the AL2023 family (R:types.go:313-598).
-int32_t kp_instance_type_resolve(const kp_options* opts, const kp_ec2_info* info, const kp_nodeclass* nc,
-                                 kp_resource_list* capacity, kp_resource_list* overhead) {
-  if (!opts || !info || !capacity || !overhead) return fail(KP_E_INVAL, "null argument");
-  auto mi = [](int64_t x) { return x * 1048576ll * 1000ll; };
-  auto eniPods = [&](int reserved) -> int64_t {  // ENILimitedPods (R:types.go:461-475)
-    int64_t usable = std::max<int64_t>((int64_t)info->max_enis - reserved, 0);
-    return usable == 0 ? 0 : usable * ((int64_t)info->ipv4_per_eni - 1) + 2;
-  };
-  memset(capacity, 0, sizeof *capacity);
-  memset(overhead, 0, sizeof *overhead);
-  auto set = [](kp_resource_list* l, int r, int64_t v) {
-    l->milli[r] = v;
-    l->present |= 1u << r;
-  };
-  set(capacity, KP_RES_CPU, (int64_t)info->vcpu * 1000);
+namespace {
+int64_t EniLimitedPods(const kp_ec2_info* info, int reserved) {  // ENILimitedPods (R:types.go:461-475)
+  int64_t usable = std::max<int64_t>((int64_t)info->max_enis - reserved, 0);
+  return usable == 0 ? 0 : usable * ((int64_t)info->ipv4_per_eni - 1) + 2;
+}
+void SetRes(kp_resource_list* l, int r, int64_t v) {
+  l->milli[r] = v;
+  l->present |= 1u << r;
+}
+int64_t MemoryBytes(const kp_options* opts, const kp_ec2_info* info) {  // memory() (R:types.go:337-347)
   int64_t mib = info->memory_mib;
-  if (info->arch && strcmp(info->arch, "arm64") == 0) mib -= 64;  // Graviton CMA (R:types.go:339-342)
+  if (info->arch && strcmp(info->arch, "arm64") == 0) mib -= 64;  // Graviton CMA
   const int64_t ovMiB = (int64_t)std::ceil((double)(mib * 1048576ll) * opts->vm_memory_overhead_percent / 1024 / 1024);
-  set(capacity, KP_RES_MEMORY, mi(mib - ovMiB));
-  const int64_t storage = 20ll << 30;  // AL2023 default /dev/xvda, no BDMs (R:amifamily/al2023.go:98-108)
-  set(capacity, KP_RES_EPHEMERAL_STORAGE, storage * 1000);
-  int64_t pods = (nc && nc->max_pods >= 0) ? nc->max_pods : eniPods(opts->reserved_enis);
-  if (nc && nc->pods_per_core > 0) pods = std::min<int64_t>((int64_t)nc->pods_per_core * info->vcpu, pods);
-  set(capacity, KP_RES_PODS, pods * 1000);
-  set(capacity, KP_RES_POD_ENI, (info->in_limits_table && info->trunking) ? (int64_t)info->branch_enis * 1000 : 0);
-  const string gm = info->gpu_manufacturer ? info->gpu_manufacturer : "";
-  set(capacity, KP_RES_NVIDIA_GPU, gm == "nvidia" ? info->gpu_count * 1000ll : 0);
-  set(capacity, KP_RES_AMD_GPU, gm == "amd" ? info->gpu_count * 1000ll : 0);
-  set(capacity, KP_RES_NEURON, (int64_t)info->neuron_devices * 1000);
-  set(capacity, KP_RES_NEURONCORE, (int64_t)info->neuron_devices * info->neuron_cores_per_device * 1000);
-  set(capacity, KP_RES_GAUDI, gm == "habana" ? info->gpu_count * 1000ll : 0);
-  set(capacity, KP_RES_EFA, (int64_t)info->efa * 1000);
-  // kube-reserved (AL2023 UsesENILimitedMemoryOverhead) + eviction threshold (R:types.go:492-551)
-  int64_t cpuOverhead = 0;
+  return (mib - ovMiB) * 1048576ll;
+}
+constexpr int64_t kStorageBytes = 20ll << 30;  // AL2023 default /dev/xvda, no BDMs (R:amifamily/al2023.go:98-108)
+
+// computeEvictionSignal (R:types.go:571-598) in milli-units: a percentage p of the capacity (100% disables the
+// threshold) as ceil(capacity / 100 * p) whole units, else the quantity itself.
+int64_t EvictionSignalMilli(int64_t capacity_units, const kp_eviction_value& v) {
+  if (!v.is_percent) return v.milli;
+  const double p = v.percent == 100.0 ? 0.0 : v.percent;
+  return (int64_t)std::ceil((double)capacity_units / 100 * p) * 1000;
+}
+}  // namespace
+
+int32_t kp_instance_type_overhead(const kp_options* opts, const kp_ec2_info* info, const kp_nodeclass* nc,
+                                  kp_resource_list* kube, kp_resource_list* sys, kp_resource_list* ev) {
+  if (!opts || !info || !kube || !sys || !ev) return fail(KP_E_INVAL, "null argument");
+  const kp_kubelet* kl = nc ? nc->kubelet : nullptr;
+  memset(kube, 0, sizeof *kube);
+  memset(sys, 0, sizeof *sys);
+  memset(ev, 0, sizeof *ev);
+  // kubeReservedResources: AL2023 UsesENILimitedMemoryOverhead -> memory from ENILimitedPods(info, 0); the CPU
+  // ranges accumulate with a truncation per range; then the user's keys replace the computed ones (lo.Assign)
+  SetRes(kube, KP_RES_MEMORY, (11 * EniLimitedPods(info, 0) + 255) * 1048576ll * 1000ll);
+  SetRes(kube, KP_RES_EPHEMERAL_STORAGE, (1ll << 30) * 1000);
   const struct {
     int64_t s, e;
     double p;
   } rg[4] = {{0, 1000, 0.06}, {1000, 2000, 0.01}, {2000, 4000, 0.005}, {4000, 1ll << 31, 0.0025}};
-  const int64_t cpuM = capacity->milli[KP_RES_CPU];
+  const int64_t cpuM = (int64_t)info->vcpu * 1000;
+  int64_t cpuOverhead = 0;
   for (auto& x : rg)
     if (cpuM >= x.s) cpuOverhead += (int64_t)((double)(cpuM < x.e ? cpuM - x.s : x.e - x.s) * x.p);
-  set(overhead, KP_RES_CPU, cpuOverhead);
-  set(overhead, KP_RES_MEMORY, mi(11 * eniPods(0) + 255) + mi(100));
-  set(overhead, KP_RES_EPHEMERAL_STORAGE, (1ll << 30) * 1000 + (int64_t)std::ceil((double)storage / 100 * 10) * 1000);
+  SetRes(kube, KP_RES_CPU, cpuOverhead);
+  if (kl)
+    for (int r = 0; r < KP_NUM_RESOURCES; r++)
+      if (kl->kube_reserved.present & (1u << r)) SetRes(kube, r, kl->kube_reserved.milli[r]);
+  // systemReservedResources: exactly the user's map
+  if (kl)
+    for (int r = 0; r < KP_NUM_RESOURCES; r++)
+      if (kl->system_reserved.present & (1u << r)) SetRes(sys, r, kl->system_reserved.milli[r]);
+  // evictionThreshold: defaults, then MaxResources over the signal maps (hard, then soft), assigned over them
+  SetRes(ev, KP_RES_MEMORY, 100ll * 1048576ll * 1000ll);
+  SetRes(ev, KP_RES_EPHEMERAL_STORAGE, (int64_t)std::ceil((double)kStorageBytes / 100 * 10) * 1000);
+  if (kl) {
+    const int64_t memBytes = MemoryBytes(opts, info);
+    kp_resource_list ov{};
+    auto fold = [&](const kp_eviction_value& mem, const kp_eviction_value& fs) {
+      if (mem.set) {
+        const int64_t v = EvictionSignalMilli(memBytes, mem);
+        if (!(ov.present & (1u << KP_RES_MEMORY)) || v > ov.milli[KP_RES_MEMORY]) SetRes(&ov, KP_RES_MEMORY, v);
+      }
+      if (fs.set) {
+        const int64_t v = EvictionSignalMilli(kStorageBytes, fs);
+        if (!(ov.present & (1u << KP_RES_EPHEMERAL_STORAGE)) || v > ov.milli[KP_RES_EPHEMERAL_STORAGE])
+          SetRes(&ov, KP_RES_EPHEMERAL_STORAGE, v);
+      }
+    };
+    if (kl->has_eviction_hard) fold(kl->hard_memory_available, kl->hard_nodefs_available);
+    if (kl->has_eviction_soft) fold(kl->soft_memory_available, kl->soft_nodefs_available);  // AL2023: enabled
+    for (int r = 0; r < KP_NUM_RESOURCES; r++)
+      if (ov.present & (1u << r)) SetRes(ev, r, ov.milli[r]);
+  }
+  return KP_OK;
+}
+
+// instancetype.NewInstanceType capacity + Overhead.Total() for the AL2023 family (R:types.go:123-155, 313-598).
+int32_t kp_instance_type_resolve(const kp_options* opts, const kp_ec2_info* info, const kp_nodeclass* nc,
+                                 kp_resource_list* capacity, kp_resource_list* overhead) {
+  if (!opts || !info || !capacity || !overhead) return fail(KP_E_INVAL, "null argument");
+  memset(capacity, 0, sizeof *capacity);
+  memset(overhead, 0, sizeof *overhead);
+  SetRes(capacity, KP_RES_CPU, (int64_t)info->vcpu * 1000);
+  SetRes(capacity, KP_RES_MEMORY, MemoryBytes(opts, info) * 1000);
+  SetRes(capacity, KP_RES_EPHEMERAL_STORAGE, kStorageBytes * 1000);
+  int64_t pods = (nc && nc->max_pods >= 0) ? nc->max_pods : EniLimitedPods(info, opts->reserved_enis);
+  if (nc && nc->pods_per_core > 0) pods = std::min<int64_t>((int64_t)nc->pods_per_core * info->vcpu, pods);
+  SetRes(capacity, KP_RES_PODS, pods * 1000);
+  SetRes(capacity, KP_RES_POD_ENI, (info->in_limits_table && info->trunking) ? (int64_t)info->branch_enis * 1000 : 0);
+  const string gm = info->gpu_manufacturer ? info->gpu_manufacturer : "";
+  SetRes(capacity, KP_RES_NVIDIA_GPU, gm == "nvidia" ? info->gpu_count * 1000ll : 0);
+  SetRes(capacity, KP_RES_AMD_GPU, gm == "amd" ? info->gpu_count * 1000ll : 0);
+  SetRes(capacity, KP_RES_NEURON, (int64_t)info->neuron_devices * 1000);
+  SetRes(capacity, KP_RES_NEURONCORE, (int64_t)info->neuron_devices * info->neuron_cores_per_device * 1000);
+  SetRes(capacity, KP_RES_GAUDI, gm == "habana" ? info->gpu_count * 1000ll : 0);
+  SetRes(capacity, KP_RES_EFA, (int64_t)info->efa * 1000);
+  kp_resource_list parts[3];
+  int32_t rc = kp_instance_type_overhead(opts, info, nc, &parts[0], &parts[1], &parts[2]);
+  if (rc != KP_OK) return rc;
+  for (auto& l : parts)  // InstanceTypeOverhead.Total(): resources.Merge of the three lists
+    for (int r = 0; r < KP_NUM_RESOURCES; r++)
+      if (l.present & (1u << r)) SetRes(overhead, r, overhead->milli[r] + l.milli[r]);
   return KP_OK;
 }
 

@@ -46,6 +46,8 @@ def load_lib(path=LIB_PATH):
         "kp_catalog_update_offerings": (C.c_int32, [C.c_void_p, P(abi.OfferingUpdate), C.c_uint32, C.c_uint64]),
         "kp_instance_type_resolve": (C.c_int32, [P(abi.Options), P(abi.EC2Info), P(abi.NodeClass),
                                                  P(abi.ResourceList), P(abi.ResourceList)]),
+        "kp_instance_type_overhead": (C.c_int32, [P(abi.Options), P(abi.EC2Info), P(abi.NodeClass),
+                                                  P(abi.ResourceList), P(abi.ResourceList), P(abi.ResourceList)]),
         "kp_filter_compatible_available": (C.c_int32, [C.c_void_p, C.c_void_p, P(abi.FeasibilityQuery), C.c_uint32,
                                                        P(C.c_uint64), P(C.c_double), P(abi.SolveStats)]),
         "kp_filter_prepare": (C.c_int32, [C.c_void_p, C.c_void_p, P(abi.FeasibilityQuery), C.c_uint32, C.c_int32,

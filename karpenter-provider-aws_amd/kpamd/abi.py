@@ -181,10 +181,21 @@ class EC2Info(C.Structure):
                 ("branch_enis", C.c_int32), ("in_limits_table", C.c_int32), ("reserved2_", C.c_int32)]
 
 
+class EvictionValue(C.Structure):
+    _fields_ = [("set", C.c_int32), ("is_percent", C.c_int32), ("percent", C.c_double), ("milli", C.c_int64)]
+
+
+class Kubelet(C.Structure):
+    _fields_ = [("kube_reserved", ResourceList), ("system_reserved", ResourceList),
+                ("has_eviction_hard", C.c_int32), ("has_eviction_soft", C.c_int32),
+                ("hard_memory_available", EvictionValue), ("hard_nodefs_available", EvictionValue),
+                ("soft_memory_available", EvictionValue), ("soft_nodefs_available", EvictionValue)]
+
+
 class NodeClass(C.Structure):
     _fields_ = [("region", C.c_char_p), ("zones", C.POINTER(C.c_char_p)), ("zone_ids", C.POINTER(C.c_char_p)),
                 ("n_zones", C.c_uint32), ("max_pods", C.c_int32), ("pods_per_core", C.c_int32),
-                ("reserved_", C.c_int32)]
+                ("reserved_", C.c_int32), ("kubelet", C.POINTER(Kubelet))]
 
 
 class ClusterNode(C.Structure):

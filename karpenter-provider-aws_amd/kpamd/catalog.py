@@ -159,8 +159,58 @@ def ec2_info(arena, row):
     return i
 
 
-def nodeclass(arena, zones=ZONES, zone_ids=ZONE_IDS, max_pods=None, pods_per_core=None):
+_SUFFIX = {"": 1, "k": 10**3, "M": 10**6, "G": 10**9, "T": 10**12, "P": 10**15, "E": 10**18,
+           "Ki": 2**10, "Mi": 2**20, "Gi": 2**30, "Ti": 2**40, "Pi": 2**50, "Ei": 2**60}
+
+
+def parse_quantity(q):
+    """resource.MustParse(q).MilliValue() for the plain forms kubelet maps use ("2", "80m", "1.5", "20Gi",
+    "500Mi", "1G", "1e3"), exact (rational arithmetic, rounded up like MilliValue)."""
+    from fractions import Fraction
+    q = str(q).strip()
+    if q.endswith("m") and not q.endswith("Mi"):
+        return -(-Fraction(q[:-1]) // 1)
+    for suf in sorted(_SUFFIX, key=len, reverse=True):
+        if suf and q.endswith(suf):
+            return -(-(Fraction(q[:-len(suf)]) * _SUFFIX[suf] * 1000) // 1)
+    return -(-(Fraction(q) * 1000) // 1)
+
+
+EVICTION_SIGNALS = {"memory.available": "memory_available", "nodefs.available": "nodefs_available"}
+
+
+def _eviction_value(v):
+    ev = abi.EvictionValue()
+    ev.set = 1
+    if str(v).endswith("%"):
+        ev.is_percent, ev.percent = 1, float(str(v).strip("%"))  # strconv.ParseFloat(strings.Trim(v, "%"))
+    else:
+        ev.milli = parse_quantity(v)
+    return ev
+
+
+def kubelet(arena, kube_reserved=None, system_reserved=None, eviction_hard=None, eviction_soft=None):
+    """EC2NodeClass.spec.kubelet resource/eviction maps -> kp_kubelet (string quantities as the CRD holds them).
+    A None eviction map is nil; {} is an empty, non-nil map."""
+    k = abi.Kubelet()
+    k.kube_reserved = arena.resources({r: parse_quantity(v) for r, v in (kube_reserved or {}).items()})
+    k.system_reserved = arena.resources({r: parse_quantity(v) for r, v in (system_reserved or {}).items()})
+    for which, m in (("hard", eviction_hard), ("soft", eviction_soft)):
+        if m is None:
+            continue
+        setattr(k, f"has_eviction_{which}", 1)
+        for sig, v in m.items():
+            if sig in EVICTION_SIGNALS:  # other signals (imagefs, pid) do not enter the overhead
+                setattr(k, f"{which}_{EVICTION_SIGNALS[sig]}", _eviction_value(v))
+    arena.keep.append(k)
+    return k
+
+
+def nodeclass(arena, zones=ZONES, zone_ids=ZONE_IDS, max_pods=None, pods_per_core=None, kubelet_cfg=None):
+    """kp_nodeclass; kubelet_cfg: dict of kubelet(...) keyword arguments, or None for no kubelet block."""
     nc = abi.NodeClass()
+    if kubelet_cfg is not None:
+        nc.kubelet = C.pointer(kubelet(arena, **kubelet_cfg))
     nc.region = arena.s(REGION)
     nc.zones = arena.arr(C.c_char_p, [arena.s(z) for z in zones])
     nc.zone_ids = arena.arr(C.c_char_p, [arena.s(z) for z in zone_ids])
@@ -202,12 +252,12 @@ def spot_price_table(rows, zones=ZONES, seed=SPOT_SEED):
 
 
 def build_catalog(lib, rows=None, opts=None, max_pods=None, pods_per_core=None, zones=ZONES, zone_ids=ZONE_IDS,
-                  unavailable=frozenset()):
+                  unavailable=frozenset(), kubelet_cfg=None):
     """GetInstanceTypes for one EC2NodeClass: NewInstanceType for every row, then InjectOfferings."""
     rows = load_ec2_table() if rows is None else rows
     arena = abi.Arena()
     opts = opts or default_options()
-    nc = nodeclass(arena, zones, zone_ids, max_pods, pods_per_core)
+    nc = nodeclass(arena, zones, zone_ids, max_pods, pods_per_core, kubelet_cfg)
     spot = spot_price_table(rows, zones)
     out = []
     for r in rows:

@@ -1991,12 +1991,41 @@ int32_t kpo_instance_type_resolve(const kp_options* opts, const kp_ec2_info* inf
       kube[KP_RES_CPU] = Get(kube, KP_RES_CPU) + (int64_t)(r * rg.pct);
     }
   }
-  // evictionThreshold: memory 100Mi, ephemeral ceil(storage/100*10)
+  const kp_kubelet* kl = nc ? nc->kubelet : nullptr;
+  ResourceList sys;
+  if (kl) {  // lo.Assign(computed, kubeReserved); systemReserved is the map as given
+    ResourceList kr = FromABI(kl->kube_reserved), sr = FromABI(kl->system_reserved);
+    for (auto& kv : kr) kube[kv.first] = kv.second;
+    sys = sr;
+  }
+  // evictionThreshold: memory 100Mi, ephemeral ceil(storage/100*10); signal maps (evictionHard, then evictionSoft —
+  // EvictionSoftEnabled for AL2023) each give a temp list, MaxResources'd together, then assigned over the defaults
   ResourceList ev;
   ev[KP_RES_MEMORY] = Mi(100);
   ev[KP_RES_EPHEMERAL_STORAGE] = (int64_t)std::ceil((double)storageBytes / 100 * 10) * 1000;
+  if (kl) {
+    auto signal = [](double capacityUnits, const kp_eviction_value& v) -> int64_t {  // computeEvictionSignal
+      if (!v.is_percent) return v.milli;
+      double p = v.percent;
+      if (p == 100) p = 0;  // mustParsePercentage: 100% disables the threshold
+      return (int64_t)std::ceil(capacityUnits / 100 * p) * 1000;
+    };
+    const double memUnits = (double)(mib - ovMiB) * 1048576.0, fsUnits = (double)storageBytes;
+    std::vector<std::pair<const kp_eviction_value*, const kp_eviction_value*>> maps;
+    if (kl->has_eviction_hard) maps.push_back({&kl->hard_memory_available, &kl->hard_nodefs_available});
+    if (kl->has_eviction_soft) maps.push_back({&kl->soft_memory_available, &kl->soft_nodefs_available});
+    ResourceList override_;
+    for (auto& m : maps) {
+      ResourceList temp;
+      if (m.first->set) temp[KP_RES_MEMORY] = signal(memUnits, *m.first);
+      if (m.second->set) temp[KP_RES_EPHEMERAL_STORAGE] = signal(fsUnits, *m.second);
+      for (auto& kv : temp)  // resources.MaxResources
+        if (!override_.count(kv.first) || kv.second > override_[kv.first]) override_[kv.first] = kv.second;
+    }
+    for (auto& kv : override_) ev[kv.first] = kv.second;
+  }
   overhead->kube_reserved = ToABI(kube);
-  overhead->system_reserved = ToABI(ResourceList{});
+  overhead->system_reserved = ToABI(sys);
   overhead->eviction_threshold = ToABI(ev);
   return KP_OK;
 }
