@@ -317,6 +317,9 @@ typedef struct kp_solve_stats {
   uint64_t fast_pods;       /* pods placed by solve_kernel's single-wave fast lane (no requirement merge) */
   uint64_t fast_cycles[6];  /* diagnostic (KP_TIMING=1): fast-lane cycles: pop, stage, sort, pre-pass, attempts, commit */
   uint64_t slow_sorts;      /* sort.Slice replays that ran the literal pdqsort (no stable-move shortcut) */
+  uint64_t fast_bails[8];   /* pods the fast lane handed to the full path: ineligible (topology / existing nodes),
+                               spilled sort arrays, long sort shift, long scan, requirement merge, minValues,
+                               no in-flight NodeClaim took it, reserved */
 } kp_solve_stats;
 
 /* ---- context ---------------------------------------------------------------------------- */
@@ -526,6 +529,14 @@ int32_t kp_solve(kp_ctx* ctx, const kp_solve_in* in, kp_solve_result** out);
  * KP_OK when kp_solve would accept it, else the KP_E_UNSUPPORTED / KP_E_INVAL it would return. */
 int32_t kp_solve_validate(const kp_solve_in* in);
 int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out);
+/* kp_solve_prepare as a collective over a communicator (kp_comm_init; NULL = this process alone): the per-Solve
+ * table of template options per (shape-level, NodePool template) — addToNewNodeClaim's Compatible + Add +
+ * filterInstanceTypesByRequirements for a fresh NodeClaim, SURVEY §8e "feasibility precompute" — is computed in
+ * shape-level row ranges, one per rank, and all-gathered (ncclAllGather over xGMI); solve_kernel then reads one
+ * entry per template attempt instead of re-filtering the template's types. Every rank passes the same batch; each
+ * can then run the Solve (replicas) or only the committing rank does. */
+struct kp_comm;
+int32_t kp_solve_prepare_comm(kp_ctx* ctx, const kp_solve_in* in, struct kp_comm* comm, kp_solve_plan** out);
 int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out);
 void kp_solve_plan_destroy(kp_solve_plan* plan);
 uint32_t kp_result_nodeclaim_count(const kp_solve_result* res);

@@ -5,6 +5,10 @@
 
 #include "kp_model.h"
 
+#define KP_SOLVE_STATS 40
+// why the fast lane handed a popped pod to the full path (stats[32 + FB_*])
+enum { FB_INELIGIBLE = 0, FB_SPILLED = 1, FB_SHIFT = 2, FB_SCAN = 3, FB_MERGE = 4, FB_MINVALUES = 5, FB_NONE = 6 };
+
 struct SolveArgs {
   const DevDict* dict;
   const DevCatalog* cats;
@@ -107,12 +111,42 @@ struct SolveArgs {
   int32_t n_req_res;                 // popcount(req_res_mask)
   const int32_t* tkey_slot;          // [64] row of a topology key in ex_tcode
   const uint8_t* ex_tcode;           // [TK][E] value ordinal of the existing node's label (0xFF: none)
+  // precomputed template options per (shape-level, template) (tmpl_feas_kernel), or null
+  const uint64_t* tfeas;             // [SL][NT] entries of tfeas_words
+  int32_t tfeas_words;
   // outputs
   int32_t* placement;                // [P]
   int32_t* events;                   // [P] pods in placement order
-  uint64_t* stats;                   // [32]: attempts, bytes, pops, n_nc, n_events, scanned, starts; [8..15] phases,
-                                     // [16..23] attempt split, [24] fast-lane pods, [25..30] fast-lane cycles
+  uint64_t* stats;                   // [KP_SOLVE_STATS]: attempts, bytes, pops, n_nc, n_events, scanned, starts; [7] runaway;
+                                     // [8..15] phases, [16..23] attempt split, [24] fast-lane pods, [25..30] fast-lane
+                                     // cycles, [31] literal pdqsorts, [32..39] fast-lane hand-offs by reason (FB_*)
 };
+
+// tmpl_feas_kernel: rows [row_lo, row_hi) of shape-levels x every template
+struct TfeasArgs {
+  const DevDict* dict;
+  const DevCatalog* cats;
+  int32_t n_catalogs;
+  const int64_t* vint;
+  int32_t n_tmpl;
+  const uint8_t* tmpl_reqs;
+  const int32_t* tmpl_catalog;
+  const uint64_t* tmpl_X;
+  const int64_t* tmpl_daemon;
+  const uint8_t* shape_reqs;         // [SL] KReqs
+  const uint64_t* shape_negop;       // [SL]
+  const int32_t* sl_shape;           // [SL] shape of the shape-level
+  const int64_t* shape_requests;     // [S][NRES]
+  const uint64_t* shape_pvp;
+  const int32_t* pvp_base;
+  const int32_t* pvp_slot;
+  const int32_t* sl_own_n;
+  uint32_t req_res_mask;
+  int32_t row_lo, row_hi;
+  int32_t words;                     // u64 per entry: TW + KP_NRES / 2 + 1
+  uint64_t* out;                     // [SL][NT] entries (this call writes rows [row_lo, row_hi))
+};
+hipError_t launch_tmpl_feas(const TfeasArgs& a, hipStream_t s);
 
 struct FinalizeArgs {
   const DevDict* dict;

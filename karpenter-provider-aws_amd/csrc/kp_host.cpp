@@ -1966,6 +1966,13 @@ extern "C" {
 
 }  // extern "C"
 
+struct kp_comm {
+  kp_ctx* ctx = nullptr;
+  ncclComm_t comm = nullptr;
+  int n_ranks = 1, rank = 0;
+  DevBuf buf;  // [0]: this rank's record, [1..n_ranks]: the gathered records
+};
+
 struct kp_solve_plan {
   kp_ctx* ctx = nullptr;
   std::unique_ptr<Compiled> cp;
@@ -2015,7 +2022,15 @@ static int32_t EnsureBaseOnDevice(kp_ctx* ctx, SolveBase& B) {
 // Compile the batch and upload it. The catalogue half (SolveBase: dictionary, catalogue SoA, templates) is taken
 // from the ctx cache when the catalogues (identity + seqnum) and NodePools match and the dictionary covers the
 // batch; only the per-Solve half (shapes, existing nodes, topology, queue order) is compiled and uploaded.
+static int32_t SolvePrepare(kp_ctx* ctx, const kp_solve_in* in, kp_comm* comm, kp_solve_plan** out);
 int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out) {
+  return SolvePrepare(ctx, in, nullptr, out);
+}
+int32_t kp_solve_prepare_comm(kp_ctx* ctx, const kp_solve_in* in, kp_comm* comm, kp_solve_plan** out) {
+  if (comm && comm->ctx != ctx) return fail(KP_E_INVAL, "communicator belongs to another context");
+  return SolvePrepare(ctx, in, comm, out);
+}
+static int32_t SolvePrepare(kp_ctx* ctx, const kp_solve_in* in, kp_comm* comm, kp_solve_plan** out) {
   auto t0 = std::chrono::steady_clock::now();
   if (!ctx || !in || !out) return fail(KP_E_INVAL, "null argument");
   std::lock_guard<std::mutex> lock(ctx->mu);
@@ -2076,6 +2091,11 @@ int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out
     ex_static[e] = ok ? 1 : 0;
   }
   const size_t o_exso = blob.put(ex_static);
+  // shape of each shape-level (tmpl_feas_kernel)
+  vector<int32_t> sl_shape(std::max<size_t>(1, C.shape_reqs.size()), 0);
+  for (size_t sh = 0; sh < C.shape_level_base.size(); sh++)
+    for (int l = 0; l < C.shape_nlevels[sh]; l++) sl_shape[(size_t)C.shape_level_base[sh] + l] = (int32_t)sh;
+  const size_t o_slsh = blob.put(sl_shape);
   // ---- mutable state: restored from a pristine device copy before every run ----
   vector<int32_t> zeros_p(Pc, 0);
   const size_t o_mut = blob.reserve(0);
@@ -2105,7 +2125,7 @@ int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out
   const size_t o_nccat = blob.reserve_dev(sizeof(int32_t) * (size_t)Pc);
   const size_t o_place = blob.reserve_dev(sizeof(int32_t) * Pc);
   const size_t o_events = blob.reserve_dev(sizeof(int32_t) * Pc);
-  const size_t o_stats = blob.reserve_dev(sizeof(uint64_t) * 32);
+  const size_t o_stats = blob.reserve_dev(sizeof(uint64_t) * KP_SOLVE_STATS);
   // failure memo (see SolveArgs): versions start at 0, memo entries at -1
   const size_t SLn = std::max<size_t>(1, C.shape_reqs.size());
   const int ncc = (int)std::min<size_t>((size_t)Pc, std::max<size_t>(1, ((size_t)256 << 20) / (4 * SLn)));
@@ -2128,6 +2148,15 @@ int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out
   const size_t n_hcnc = (size_t)C.GH * Pc;
   const size_t o_hcnc = blob.reserve_dev(std::max<size_t>(n_hcnc, 1));
   const size_t o_nctc = blob.reserve_dev(std::max<size_t>((size_t)C.TK * Pc, 1));
+  // template options per (shape-level, template): rows split evenly over the communicator's ranks (padded so that
+  // every rank contributes the same byte count to the all-gather)
+  const int SLi = (int)C.shape_reqs.size();
+  const int n_ranks = comm ? comm->n_ranks : 1, my_rank = comm ? comm->rank : 0;
+  const bool tfeas_on = NT > 0 && SLi > 0 && !getenv("KP_NO_TFEAS");
+  const int tf_words = TW + KP_NRES / 2 + 1;
+  const int rows_per_rank = (SLi + n_ranks - 1) / n_ranks;
+  const size_t tf_bytes = tfeas_on ? (size_t)rows_per_rank * n_ranks * NT * tf_words * sizeof(uint64_t) : 0;
+  const size_t o_tfeas = blob.reserve_dev(std::max<size_t>(tf_bytes, 8));
   const size_t total_bytes = blob.total();
 
   // the per-Solve arena: reuse the ctx's spare allocation when it is large enough
@@ -2247,6 +2276,42 @@ int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out
   a.placement = (int32_t*)(base + o_place);
   a.events = (int32_t*)(base + o_events);
   a.stats = (uint64_t*)(base + o_stats);
+  if (tfeas_on) {  // this rank's rows of the template-options table, then one all-gather (RCCL) of every rank's rows
+    TfeasArgs f;
+    memset(&f, 0, sizeof f);
+    f.dict = a.dict;
+    f.cats = a.cats;
+    f.n_catalogs = a.n_catalogs;
+    f.vint = a.vint;
+    f.n_tmpl = NT;
+    f.tmpl_reqs = a.tmpl_reqs;
+    f.tmpl_catalog = a.tmpl_catalog;
+    f.tmpl_X = a.tmpl_X;
+    f.tmpl_daemon = a.tmpl_daemon;
+    f.shape_reqs = a.shape_reqs;
+    f.shape_negop = a.shape_negop;
+    f.sl_shape = (const int32_t*)(base + o_slsh);
+    f.shape_requests = a.shape_requests;
+    f.shape_pvp = a.shape_pvp;
+    f.pvp_base = a.pvp_base;
+    f.pvp_slot = a.pvp_slot;
+    f.sl_own_n = a.sl_own_n;
+    f.req_res_mask = a.req_res_mask;
+    f.row_lo = std::min(SLi, my_rank * rows_per_rank);
+    f.row_hi = std::min(SLi, (my_rank + 1) * rows_per_rank);
+    f.words = tf_words;
+    f.out = (uint64_t*)(base + o_tfeas);
+    HIPCHK(launch_tmpl_feas(f, ctx->stream));
+    if (comm && n_ranks > 1) {
+      const size_t chunk = (size_t)rows_per_rank * NT * tf_words * sizeof(uint64_t);
+      ncclResult_t r = ncclAllGather(base + o_tfeas + chunk * my_rank, base + o_tfeas, chunk, ncclUint8, comm->comm,
+                                     ctx->stream);
+      if (r != ncclSuccess) return fail(KP_E_DEVICE, "ncclAllGather: %s", ncclGetErrorString(r));
+    }
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    a.tfeas = (const uint64_t*)(base + o_tfeas);
+    a.tfeas_words = tf_words;
+  }
 
   plan->o_ver = o_ver0;
   plan->n_ver = n_ver;
@@ -2299,7 +2364,7 @@ int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out) {
   const int P = plan->P, Pc = plan->Pc, opt_stride = plan->opt_stride;
   hipStream_t st = ctx->stream;
   HIPCHK(hipMemcpyAsync(base + plan->o_mut, base + plan->o_pristine, plan->n_mut, hipMemcpyDeviceToDevice, st));
-  HIPCHK(hipMemsetAsync(base + plan->o_stats, 0, sizeof(uint64_t) * 32, st));
+  HIPCHK(hipMemsetAsync(base + plan->o_stats, 0, sizeof(uint64_t) * KP_SOLVE_STATS, st));
   HIPCHK(hipMemsetAsync(base + plan->o_npods, 0, sizeof(int32_t) * Pc, st));
   HIPCHK(hipMemsetAsync(base + plan->o_place, 0xFF, sizeof(int32_t) * Pc, st));
   HIPCHK(hipMemsetAsync(base + plan->o_ver, 0, plan->n_ver, st));
@@ -2310,7 +2375,7 @@ int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out) {
   HIPCHK(hipEventRecord(ctx->ev0, st));
   HIPCHK(launch_solve(a, 8, dyn, st));
   HIPCHK(hipEventRecord(ctx->ev1, st));
-  uint64_t stats[32];
+  uint64_t stats[KP_SOLVE_STATS];
   HIPCHK(hipMemcpyAsync(stats, base + plan->o_stats, sizeof stats, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   if (stats[7]) return fail(KP_E_DEVICE, "solve_kernel exceeded its Queue.Pop bound (%llu pops): aborted",
@@ -2410,6 +2475,7 @@ int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out) {
   res->stats.fast_pods = stats[24];
   res->stats.slow_sorts = stats[31];
   for (int i = 0; i < 6; i++) res->stats.fast_cycles[i] = stats[25 + i];
+  for (int i = 0; i < 8; i++) res->stats.fast_bails[i] = stats[32 + i];
   res->stats.host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   *out = res.release();
   return KP_OK;
@@ -3374,12 +3440,6 @@ int32_t kp_simulate_batch(kp_ctx* ctx, const kp_cluster* cl, const uint32_t* off
 // ==================================================================================================
 static_assert(sizeof(kp_choice) == sizeof(CommBest), "kp_choice mirrors CommBest (the all-gathered record)");
 
-struct kp_comm {
-  kp_ctx* ctx = nullptr;
-  ncclComm_t comm = nullptr;
-  int n_ranks = 1, rank = 0;
-  DevBuf buf;  // [0]: this rank's record, [1..n_ranks]: the gathered records
-};
 
 namespace {
 int32_t nccl_fail(ncclResult_t r, const char* what) {

@@ -24,6 +24,12 @@
 #ifndef FASTLANE
 #define FASTLANE 1  // solve_kernel: wave-0 fast lane for merge-free placements (0 = full path only)
 #endif
+#ifndef FT_FINE
+#define FT_FINE 0  // diagnostic: finer fast-lane probes (FTF) in place of the full path's attempt split
+#endif
+#ifndef FAST_SCAN_MAX
+#define FAST_SCAN_MAX 512  // longest first-fit scan (positions) the fast lane takes on; longer: the 4-wave pre-pass
+#endif
 // Explicit address spaces: LDS data reached through a pointer would otherwise be read with FLAT loads (which wait
 // on the vector-memory counter too and take the long path); global rows get global_load.
 #define LDS __attribute__((address_space(3)))
@@ -34,6 +40,15 @@
 // ------------------------------------------------------------------------------------------------
 // wave helpers
 // ------------------------------------------------------------------------------------------------
+// wave-uniform value made provably uniform (SGPR): values read from LDS or global memory at a uniform address are
+// uniform in fact, but where the compiler cannot prove it the loop and branches around them become divergent code
+__device__ __forceinline__ int U(int x) { return __builtin_amdgcn_readfirstlane(x); }
+// the value's load has completed here (the compiler places the wait at this point, not at a later join)
+#define READY(x) asm volatile("" ::"v"(x))
+__device__ __forceinline__ uint64_t U64(uint64_t x) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(x >> 32)) << 32) |
+         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+}
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -497,7 +512,8 @@ __device__ __forceinline__ uint64_t filter_types(const DevDict& D, const CatHdr 
                                                  const int32_t* pvp_slot, int64_t q_lane, int32_t j0_lane,
                                                  const int64_t LDS* fitv_lds, uint32_t rmask, const VInt& vint,
                                                  uint32_t* scratch, RowPtr LDS* rl, uint64_t* bytes, int32_t* jout,
-                                                 uint64_t generic_keys = 0, uint64_t* tsub = nullptr) {
+                                                 uint64_t generic_keys = 0, uint64_t* tsub = nullptr,
+                                                 bool min_check = true) {
   const int lane = LANE;
   const int TW = D.TW;
   uint64_t tl = tsub ? __builtin_amdgcn_s_memtime() : 0;
@@ -564,7 +580,7 @@ __device__ __forceinline__ uint64_t filter_types(const DevDict& D, const CatHdr 
   if (zero) X = 0;
   TSUB(3);
   // 4) minValues (relaxMinValues = false): distinct values of each minValues key over remaining types
-  if (rv.hmin & rv.present)
+  if (min_check && (rv.hmin & rv.present))
     if (!minvalues_ok(D, H->d.code, H->d.TM, rv.hmin & rv.present, rv.minv, X, scratch)) X = 0;
   TSUB(4);
 #undef TSUB
@@ -579,6 +595,26 @@ __device__ __forceinline__ uint64_t fits_lean(const DevDict& D, const CatHdr LDS
                                               uint64_t& nb, int32_t LDS* jout) {
   const int lane = LANE;
   const int TW = D.TW;
+  // threshold indices unchanged for every requested resource (q_r <= fit_vals_r[j0_r], one LDS probe per lane):
+  // X already lies in those rows (it was ANDed with them when j0 was stored), so X is the answer without loads
+  {
+    bool same = true;
+    bool in_rr = false;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      if (k < nr && rr[k] == lane) in_rr = true;
+    if (in_rr && q_lane > 0) {
+      const int n = H->fit_n[lane];
+      const int slot = H->fit_slot[lane];
+      same = j0_lane < n && slot >= 0 && fitv_lds[slot * FITV_CAP + j0_lane] >= q_lane;
+    }
+    const uint64_t act = __ballot(in_rr && q_lane > 0);
+    if (__ballot(!same) == 0) {
+      nb += (uint64_t)__popcll(act) * (512 + (uint64_t)TW * 8);  // the algorithm's probe + row bytes, as below
+      if (lane < KP_NRES) jout[lane] = in_rr && q_lane > 0 ? j0_lane : 0;
+      return X;
+    }
+  }
   const uint64_t GLB* rowp[4] = {nullptr, nullptr, nullptr, nullptr};
   bool zero = false;
   int32_t j_lane = 0;
@@ -897,11 +933,12 @@ __device__ __forceinline__ int mstack_query_wave(const int32_t LDS* stk, int n, 
   const int lane = LANE;
   int lo = 0, hi = n;  // answer: first entry with t > stamp, in [lo, hi]
   while (hi - lo > 64) {
-    const int step = (hi - lo + 63) / 64;
+    const int step = (hi - lo + 63) >> 6;
     const int idx = lo + lane * step;
-    const uint64_t bal = __ballot(idx < hi && stk[2 * idx] > stamp);
+    const bool in = idx < hi;
+    const uint64_t bal = __ballot(in && stk[2 * idx] > stamp);
     if (!bal) {
-      lo = lo + min(63, (hi - 1 - lo) / step) * step + 1;
+      lo = lo + (__popcll(__ballot(in)) - 1) * step + 1;  // past the last sample taken (< hi)
     } else {
       const int f = __builtin_ctzll(bal);
       if (f == 0) {
@@ -926,7 +963,7 @@ __device__ __forceinline__ int wave_key_search(P ord, P npods, int lo, int hi, i
   const int lane = LANE;
   while (lo < hi) {
     const int span = hi - lo;
-    const int step = span <= 64 ? 1 : (span + 63) / 64;
+    const int step = span <= 64 ? 1 : (span + 63) >> 6;
     const int idx = lo + lane * step;
     bool ge = false;
     if (idx < hi) {
@@ -936,7 +973,7 @@ __device__ __forceinline__ int wave_key_search(P ord, P npods, int lo, int hi, i
     const uint64_t bal = __ballot(ge);
     if (step == 1) return bal ? lo + __builtin_ctzll(bal) : hi;
     if (!bal) {
-      lo = lo + min(63, (hi - 1 - lo) / step) * step + 1;  // past the last sample taken (< hi)
+      lo = lo + (__popcll(__ballot(idx < hi)) - 1) * step + 1;  // past the last sample taken (< hi)
     } else {
       const int f = __builtin_ctzll(bal);
       if (f == 0) return lo;
@@ -1156,22 +1193,450 @@ __device__ __forceinline__ int sort_newnodeclaims_wave(P ord, P npods, int n, in
   return low;
 }
 
+
+// sort.Slice replay after NodeClaim.Add at sorted position p (pending mutation 1), the common case in one batch:
+// lanes read ord[p..p+63] and, for pdqsort's choosePivot, the nine sampled positions, then their keys (two dependent
+// LDS reads in all). When pdqsort would do a stable move (n <= 12: insertion sort; n >= 50 with increasingHint:
+// partialInsertionSort) and the moved NodeClaim's new place is within the window, the ids already in registers
+// are written back shifted. Returns the cursor clamp (p), or -2: the general replay (sort_newnodeclaims_wave).
+__device__ __forceinline__ int sort_mut1_window(LdsI32 ord, LdsI32 npods, int n, int p) {
+  const int lane = LANE;
+  const int i = p + lane;
+  const int t = lane / 3;
+  const int pidx = (n / 4) * (t + 1) + (lane % 3) - 1;  // choosePivot's samples (lanes 0..8, n >= 50)
+  const bool piv = lane < 9 && n >= 50;
+  const int id = i < n ? ord[i] : 0;
+  const int pid = piv ? ord[pidx] : 0;
+  const int key = i < n ? npods[id] : INT32_MAX;
+  const int pkey = piv ? npods[pid] : 0;
+  const int K = __builtin_amdgcn_readfirstlane(key);  // npods of the mutated NodeClaim (position p)
+  const uint64_t less = __ballot(lane > 0 && i < n && key < K);
+  if (!((less >> 1) & 1)) return p;  // Less(p + 1, p) false: sort.Slice leaves the order as it is
+  if (n > 12) {
+    if (n < 50) return -2;
+    const int prev = __shfl(pkey, lane > 0 ? lane - 1 : 0, 64);
+    const int midprev = __shfl(pkey, lane >= 3 ? lane - 3 : 0, 64);
+    const bool bad = piv && (((lane % 3) != 0 && pkey < prev) || ((lane % 3) == 1 && lane >= 3 && pkey < midprev));
+    if (__ballot(bad)) return -2;  // not increasingHint: the literal pdqsort
+  }
+  const uint64_t ge = __ballot(lane > 0 && (i >= n || key >= K));
+  if (!ge) return -2;  // the tie run continues past the window
+  const int q = __builtin_ctzll(ge);  // elements p+1 .. p+q-1 move left by one, the mutated one lands at p+q-1
+  wave_sync();
+  if (lane >= 1 && lane < q) ord[i - 1] = id;
+  const int elem = __builtin_amdgcn_readfirstlane(id);
+  if (lane == 0) ord[p + q - 1] = elem;
+  wave_sync();
+  return p;
+}
+
+// mutation stack push (mstack_push) with the stack's size / lost time / clock in registers (uniform)
+__device__ __forceinline__ void mstack_push_reg(int32_t LDS* stk, int& n, int& lost, int t, int pos) {
+  const int lane = LANE;
+  while (n > 0 && stk[2 * (n - 1) + 1] >= pos) n--;
+  if (n == MSTK_CAP) {
+    const int h = MSTK_CAP / 2;
+    lost = stk[2 * (h - 1)];
+    for (int i = lane; i < 2 * h; i += 64) {
+      const int v = stk[2 * h + i];
+      wave_sync();
+      stk[i] = v;
+    }
+    wave_sync();
+    n = h;
+  }
+  if (lane == 0) {
+    stk[2 * n] = t;
+    stk[2 * n + 1] = pos;
+  }
+  n++;
+  wave_sync();
+}
+
+// ---- solve_kernel's fast lane (wave 0), compiled as its own function ------------------------------------------
+// State shared with the kernel lives in LDS at file scope (one solve workgroup per CU); the kernel arguments are
+// read through the kernarg segment (scalar loads), so the lane's registers are allocated for this loop alone
+// instead of inheriting the full path's pressure (whose spills and copies dominated the per-pod instruction count).
+#define KARG __attribute__((address_space(4)))
+__shared__ DevDict g_D;
+__shared__ int32_t g_ctl[32];
+__shared__ int32_t g_stk[2][2 * MSTK_CAP];  // mutation stacks: [0] in-flight positions, [1] existing positions
+__shared__ int64_t g_fitv[FITV_RES * FITV_CAP];  // Fits threshold values of catalogue 0 (CatHdr.fit_slot rows)
+__shared__ CatHdr g_hdr[8];                      // catalogue descriptors 0..7
+__shared__ int32_t fl_fitj[KP_NRES];             // the fast lane's per-wave scratch (wave 0)
+__shared__ RowPtr fl_rl[RL_CAP];
+__shared__ CatHdr fl_hdrw;
+struct FastState {
+  int32_t qw_head, qw_n, qw_next, reserved_;
+  int32_t qw_pod[64], qw_shape[64], qw_sl[64], qw_lastlen[64], qw_epoch[64];  // lane i: queue entry qw_head + i
+  uint64_t bytes, attempts, scanned, starts, fpods;
+  uint64_t fcyc[16];  // [0..5] phases; [6..13] finer probes (FT_FINE builds, exported in place of stats[16..23])
+  uint32_t fbail[8];
+};
+__shared__ FastState g_fast;
+
+// Places popped pods while they need no requirement merge; returns the number placed. A pod it cannot place is
+// handed to the full path through g_ctl[6] / g_ctl[26]. Called by wave 0 only.
+template <bool TOPO>
+__device__ __noinline__ int fast_lane(uint64_t kargs, int32_t LDS* s_dyn_arg, uint64_t pops_in_arg) {
+  // a callee's arguments arrive in VGPRs and count as divergent: made provably uniform here, or every value and
+  // branch that depends on them (the whole pod loop) would be compiled as divergent control flow
+  int32_t LDS* s_dyn = (int32_t LDS*)(uintptr_t)__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)s_dyn_arg);
+  const uint64_t pops_in = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(pops_in_arg >> 32)) << 32) |
+                           (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)pops_in_arg);
+  // the kernel's argument block (the kernarg segment pointer is only defined in the kernel itself: it passes it);
+  // readfirstlane makes it provably uniform, so field reads are scalar loads
+  const uint32_t klo = __builtin_amdgcn_readfirstlane((uint32_t)kargs);
+  const uint32_t khi = __builtin_amdgcn_readfirstlane((uint32_t)(kargs >> 32));
+  const KARG SolveArgs* A = (const KARG SolveArgs*)(((uint64_t)khi << 32) | klo);
+  const DevDict& D = g_D;
+  int32_t LDS* s_ctl = (int32_t LDS*)g_ctl;
+  auto& s_stk = g_stk;
+  FastState LDS* S = (FastState LDS*)&g_fast;
+  const int lane = LANE;
+  auto hdr = [&](int c) -> const CatHdr LDS* {
+    if (c < 8) return (const CatHdr LDS*)&g_hdr[c];
+    hdr_fill_wave((CatHdr LDS*)&fl_hdrw, &A->cats[c], D.C);
+    wave_sync();
+    return (const CatHdr LDS*)&fl_hdrw;
+  };
+  const uint32_t rmask_all = A->req_res_mask;
+  const int rr0 = rmask_all ? __builtin_ctz(rmask_all) : 0;
+  const uint32_t rm1 = rmask_all & (rmask_all - 1);
+  const int rr1 = rm1 ? __builtin_ctz(rm1) : rr0;
+  const uint32_t rr_rest = rm1 & (rm1 - 1);
+  int8_t rr_list[4] = {0, 0, 0, 0};
+  int n_rr = 0;
+  for (uint32_t m = rmask_all; m; m &= m - 1) {
+    if (n_rr < 4) rr_list[n_rr] = (int8_t)__builtin_ctz(m);
+    n_rr++;
+  }
+  const uint64_t pop_cap = (uint64_t)A->n_pods * 64 + 65536;
+  // control state in registers for the loop; written back on exit
+  int q_head = U(s_ctl[0]), q_len = U(s_ctl[1]), n_ev = U(s_ctl[4]), mut = U(s_ctl[10]), mut_p = U(s_ctl[11]);
+  int stk_n = U(s_ctl[12]), stk_t = U(s_ctl[13]), stk_lost = U(s_ctl[20]);  // in-flight mutation stack
+  const int n_nc_all = U(s_ctl[2]), epoch = U(s_ctl[3]);
+  const bool in_lds = U(s_ctl[5]) != 0;
+  int qw_head = U(S->qw_head), qw_n = U(S->qw_n), qw_next = U(S->qw_next);
+  int qw_pod = S->qw_pod[lane], qw_shape = S->qw_shape[lane], qw_sl = S->qw_sl[lane], qw_lastlen = S->qw_lastlen[lane],
+      qw_epoch = S->qw_epoch[lane];
+  uint64_t bytes = 0, attempts = 0, scanned = 0, starts = 0, fcyc[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  int pops = 0, handoff = -1, fb = -1;
+    const bool tmg = A->timing != 0;
+    uint64_t ft = tmg ? __builtin_amdgcn_s_memtime() : 0;
+#define FTF(i)                                               \
+  if (FT_FINE && tmg) {                                      \
+    const uint64_t tn_ = __builtin_amdgcn_s_memtime();       \
+    fcyc[i] += tn_ - ft;                                     \
+    ft = tn_;                                                \
+  }
+#define FT(i)                                                \
+if (A->timing) {                                            \
+  const uint64_t tn_ = __builtin_amdgcn_s_memtime();       \
+  fcyc[i] += tn_ - ft;                      \
+  ft = tn_;                                                \
+}
+    // next pod's stage data, loaded while the current pod is placed (window offset pf_off; -1: none)
+    int pf_off = -1, pf_own = 0, pf_ce0 = 0, pf_ce1 = 0, pf_cur = 0, pf_stamp = 0, prev_sl = -1;
+    int a_cur_prev_pos = 0, a_cur_prev_stamp = 0, a_cex_prev_stamp = 0;  // cursors the previous pod stored
+    int64_t pf_preq = 0;
+    uint64_t pf_tol = 0;
+    for (;;) {
+      // the argument block re-derived per pod (opaque to the optimiser): its fields are scalar-loaded where they are
+      // used instead of being held in registers across the whole loop (which spilled SGPRs into VGPR lanes)
+      uint32_t klo_i = klo, khi_i = khi;
+      asm volatile("" : "+s"(klo_i), "+s"(khi_i));
+      const KARG SolveArgs* A = (const KARG SolveArgs*)(((uint64_t)khi_i << 32) | klo_i);
+      const int len = q_len;
+      const int head = q_head;
+      if (len <= 0 || pops_in + pops > pop_cap) break;
+      // Queue.Pop from the prefetched window: entries [qw_head, qw_head + qw_n) of the ring were in the queue when
+      // the window was read, and nothing rewrites a queued entry (pushes go to the tail) or its pod's level and
+      // lastLen stamps while it waits, so lane i's copy of entry qw_head + i stays exact.
+      int off = head - qw_head;
+      if (off < 0) off += A->n_pods;
+      if (off != qw_next || off >= qw_n) {  // exhausted, or the ring wrapped onto re-pushed entries
+        qw_head = head;
+        qw_n = min(64, len);
+        off = 0;
+        pf_off = -1;
+        int qi = head + lane;
+        if (qi >= A->n_pods) qi -= A->n_pods;
+        if (lane < qw_n) {
+          qw_pod = A->queue[qi];
+          qw_shape = A->pod_shape[qw_pod];
+          qw_sl = A->shape_level_base[qw_shape] + A->pod_level[qw_pod];
+          qw_lastlen = A->lastlen[qw_pod];
+          qw_epoch = A->lastlen_epoch[qw_pod];
+        }
+        // wait for the window here, in the rare branch: at the join the compiler would otherwise wait for every
+        // outstanding vector-memory operation (the previous pod's stores included) on the common path too
+        READY(qw_pod);
+        READY(qw_shape);
+        READY(qw_sl);
+        READY(qw_lastlen);
+        READY(qw_epoch);
+      }
+      qw_next = off + 1;  // only the fast lane pops: the next pop reads the following entry
+      const int pod = __builtin_amdgcn_readlane(qw_pod, off);
+      if (__builtin_amdgcn_readlane(qw_epoch, off) == epoch && __builtin_amdgcn_readlane(qw_lastlen, off) == len)
+        break;  // the full path's pop sees the same queue and ends the Solve
+      FTF(6);
+      const int shape = __builtin_amdgcn_readlane(qw_shape, off);
+      const int sl = __builtin_amdgcn_readlane(qw_sl, off);
+      // stage: one batch of independent loads (eligibility, requests, tolerations, both first-fit cursors),
+      // issued by the previous pod when this entry was next in the window
+      int own, ce0, ce1, cur, stamp;
+      int64_t preq_lane;
+      uint64_t tolmask;
+      if (pf_off == off) {
+        own = U(pf_own), ce0 = U(pf_ce0), ce1 = U(pf_ce1), cur = U(pf_cur), stamp = U(pf_stamp), preq_lane = pf_preq,
+        tolmask = U64(pf_tol);
+        if (sl == prev_sl) {  // the previous pod (same shape-level) advanced both cursors after the loads
+          cur = a_cur_prev_pos;
+          stamp = a_cur_prev_stamp;
+          ce0 = A->n_existing;
+          ce1 = a_cex_prev_stamp;
+        }
+      } else {
+        own = U(TOPO ? A->sl_own_n[sl] + A->shape_rec_n[shape] : 0);
+        ce0 = U(A->n_existing ? A->cur_ex[2 * sl] : 0), ce1 = U(A->n_existing ? A->cur_ex[2 * sl + 1] : 0);
+        preq_lane = lane < KP_NRES ? A->shape_requests[(size_t)shape * KP_NRES + lane] : 0;
+        tolmask = U64(A->shape_tolerates[shape]);
+        cur = U(A->cur_nc[2 * sl]), stamp = U(A->cur_nc[2 * sl + 1]);
+        READY(preq_lane);
+      }
+      pf_off = -1;
+      if (off + 1 < qw_n) {  // the next entry's stage loads: in flight while this pod is sorted and placed
+        const int nshape = __builtin_amdgcn_readlane(qw_shape, off + 1);
+        const int nsl = __builtin_amdgcn_readlane(qw_sl, off + 1);
+        pf_own = TOPO ? A->sl_own_n[nsl] + A->shape_rec_n[nshape] : 0;
+        pf_ce0 = A->n_existing ? A->cur_ex[2 * nsl] : 0, pf_ce1 = A->n_existing ? A->cur_ex[2 * nsl + 1] : 0;
+        pf_preq = lane < KP_NRES ? A->shape_requests[(size_t)nshape * KP_NRES + lane] : 0;
+        pf_tol = A->shape_tolerates[nshape];
+        pf_cur = A->cur_nc[2 * nsl], pf_stamp = A->cur_nc[2 * nsl + 1];
+        pf_off = off + 1;
+      }
+      prev_sl = sl;
+      FTF(7);
+      q_head = head + 1 == A->n_pods ? 0 : head + 1;
+      q_len = len - 1;
+      bool eligible = own == 0;
+      if (A->n_existing) eligible = eligible && min(ce0, mstack_query_wave((LdsI32)s_stk[1], U(s_ctl[14]), U(s_ctl[21]), ce1)) >= A->n_existing;
+      FT(0);
+      if (!eligible) {
+        handoff = pod;
+        fb = FB_INELIGIBLE;
+        break;
+      }
+      const int64_t pr0 = lane_bcast_i64(preq_lane, rr0), pr1 = lane_bcast_i64(preq_lane, rr1);
+      a_cex_prev_stamp = U(s_ctl[15]);
+      if (A->n_existing && lane == 0) {  // addToExistingNode: every position fails (cursor == n_existing)
+        A->cur_ex[2 * sl] = A->n_existing;
+        A->cur_ex[2 * sl + 1] = a_cex_prev_stamp;
+      }
+      FT(1);
+      // sort.Slice(newNodeClaims) replay + first-fit start (sort arrays in LDS; spilled ones: the full path)
+      if (!in_lds) {
+        handoff = pod;
+        fb = FB_SPILLED;
+        break;
+      }
+      const LdsI32 ord = (LdsI32)s_dyn;
+      const LdsI32 npods = (LdsI32)(s_dyn + A->sort_cap);
+      const int c19 = min(cur, mstack_query_wave((LdsI32)s_stk[0], stk_n, stk_lost, stamp));
+      const int n_nc = n_nc_all;
+      FTF(8);
+      int low = mut == 0 ? -1 : (mut == 1 ? sort_mut1_window(ord, npods, n_nc, mut_p) : -2);
+      if (low == -2) low = sort_newnodeclaims_wave(ord, npods, n_nc, mut, mut_p, 256, &A->stats[31]);
+      if (low == -2) {  // a long shift: the full path sorts (the pending mutation is still in s_ctl[10..11])
+        handoff = pod;
+        fb = FB_SHIFT;
+        break;
+      }
+      FTF(9);
+      const int start = min(min(c19, low >= 0 ? low : INT32_MAX), n_nc);
+      mut = 0;
+      if (low >= 0) mstack_push_reg((int32_t LDS*)s_stk[0], stk_n, stk_lost, ++stk_t, low);
+      wave_sync();
+      FT(2);
+      // addToInflightNode: pre-checks 64 positions at a time, then the append-path attempts in order. A long scan
+      // is the full path's (512-lane pre-pass).
+      int placed = -1, wpos = -1, why = FB_NONE;
+      bool bail = n_nc - start > FAST_SCAN_MAX;
+      if (bail) why = FB_SCAN;
+      if (lane == 0 && !bail) starts += start;
+      for (int base = start; base < n_nc && placed == -1 && !bail; base += 64) {
+        const int i = base + lane;
+        bool cand = false, tag = false;
+        int nc = 0;
+        int32_t ver = 0;
+        if (i < n_nc) {
+          nc = ord[i];
+          // every gather issued unconditionally: one round trip
+          const int32_t fl = nc < A->ncc ? A->nc_fail[(size_t)sl * A->ncc + nc] : -2;
+          ver = A->nc_ver[nc];
+          const int32_t ts = A->nc_taintset[nc];
+          const int64_t* rq = A->nc_requests + (size_t)nc * KP_NRES;
+          const int64_t* mx = A->nc_maxalloc + (size_t)nc * KP_NRES;
+          bool fit = !rmask_all || (rq[rr0] + pr0 <= mx[rr0] && rq[rr1] + pr1 <= mx[rr1]);
+          for (uint32_t rm = rr_rest; rm; rm &= rm - 1) {
+            const int r = __builtin_ctz(rm);
+            fit = fit & (rq[r] + lane_bcast_i64(preq_lane, r) <= mx[r]);
+          }
+          cand = fit && fl != ver && ((tolmask >> ts) & 1);
+          tag = cand && fl >= NC_MERGED;
+        }
+        // speculative loads of the first position's NodeClaim (the usual winner): they overlap the pre-checks
+        const int nc0 = __builtin_amdgcn_readlane(nc, 0);
+        const KReqs* cr0 = kreq_at(A->nc_reqs, nc0);
+        const uint64_t hm0 = cr0->hmin & cr0->present;
+        const int cat0 = A->nc_cat[nc0];
+        const uint64_t X00 = lane < D.TW ? A->nc_X[(size_t)nc0 * D.TW + lane] : 0;
+        const int64_t rq0 = lane < KP_NRES ? A->nc_requests[(size_t)nc0 * KP_NRES + lane] : 0;
+        const int32_t j00 = lane < KP_NRES ? A->nc_fitj[(size_t)nc0 * KP_NRES + lane] : 0;
+        if (lane == 0) scanned += min(64, n_nc - base);
+        if (lane == 0) bytes += (uint64_t)min(64, n_nc - base) * (12 + 16 * A->n_req_res);
+        uint64_t cm = __ballot(cand);
+        const uint64_t tm = __ballot(tag);
+        // the next pod's prefetch was issued before these gathers, so it has landed: take it off the outstanding
+        // list now rather than at the next pod's stage, where the wait would cover this pod's stores as well
+        READY(pf_own);
+        READY(pf_ce0);
+        READY(pf_ce1);
+        READY(pf_preq);
+        READY(pf_tol);
+        READY(pf_cur);
+        READY(pf_stamp);
+        FT(3);
+        while (cm) {
+          const int l = __builtin_ctzll(cm);
+          cm &= cm - 1;
+          if (!((tm >> l) & 1)) {  // needs the merge: the full path evaluates it
+            bail = true;
+            why = FB_MERGE;
+            break;
+          }
+          const int ncx = __builtin_amdgcn_readlane(nc, l);
+          const int32_t verx = __builtin_amdgcn_readlane(ver, l);  // NodeClaim's version (no reload after stores)
+          attempts++;
+          uint64_t hm = hm0, X0 = X00;
+          int cat = cat0;
+          int64_t rq_lane = rq0;
+          int32_t j0_lane = j00;
+          if (l != 0) {
+            const KReqs* cr = kreq_at(A->nc_reqs, ncx);
+            hm = cr->hmin & cr->present;
+            cat = A->nc_cat[ncx];
+            X0 = lane < D.TW ? A->nc_X[(size_t)ncx * D.TW + lane] : 0;
+            rq_lane = lane < KP_NRES ? A->nc_requests[(size_t)ncx * KP_NRES + lane] : 0;
+            j0_lane = lane < KP_NRES ? A->nc_fitj[(size_t)ncx * KP_NRES + lane] : 0;
+          }
+          if (hm) {  // minValues on the NodeClaim: the full path re-filters it
+            bail = true;
+            why = FB_MINVALUES;
+            break;
+          }
+          FTF(10);
+          const int64_t q_lane = rq_lane + preq_lane;
+          const uint64_t X = n_rr <= 4 ? fits_lean(D, hdr(cat), X0, q_lane, j0_lane, (const int64_t LDS*)g_fitv, rr_list,
+                                                   n_rr, bytes, (int32_t LDS*)fl_fitj)
+                                       : fits_filter(D, hdr(cat), X0, q_lane, j0_lane, (const int64_t LDS*)g_fitv,
+                                                     A->req_res_mask, (RowPtr LDS*)fl_rl, &bytes, fl_fitj);
+          bytes += (uint64_t)D.TW * 8 + KP_NRES * 8 + 8;
+          FTF(11);
+          if (__ballot(X != 0)) {
+            if (lane < D.TW) A->nc_X[(size_t)ncx * D.TW + lane] = X;
+            if (lane < KP_NRES) {
+              A->nc_requests[(size_t)ncx * KP_NRES + lane] = q_lane;
+              A->nc_fitj[(size_t)ncx * KP_NRES + lane] = fl_fitj[lane];
+            }
+            if (lane == 0) {
+              npods[ncx] += 1;
+              A->nc_ver[ncx] = verx + 1;
+            }
+            placed = ncx;
+            wpos = base + l;
+            FTF(12);
+            break;
+          }
+          if (lane == 0 && ncx < A->ncc) A->nc_fail[(size_t)sl * A->ncc + ncx] = verx;
+        }
+      }
+      wave_sync();
+      FT(4);
+      if (placed == -1) {  // templates, a merge, minValues or a long scan: the full path takes over this pod
+        handoff = pod;
+        fb = why;
+        break;
+      }
+      pops++;
+      a_cur_prev_pos = wpos;
+      a_cur_prev_stamp = stk_t;
+      mut = 1;
+      mut_p = wpos;
+      if (lane == 0) {
+        A->cur_nc[2 * sl] = wpos;
+        A->cur_nc[2 * sl + 1] = a_cur_prev_stamp;
+        A->placement[pod] = placed;
+        A->events[n_ev] = pod;
+      }
+      n_ev++;
+      FT(5);
+    }
+#undef FT
+#undef FTF
+  
+  // write back: control block, window, counters, hand-off
+  if (lane == 0) {
+    s_ctl[0] = q_head;
+    s_ctl[1] = q_len;
+    s_ctl[4] = n_ev;
+    s_ctl[10] = mut;
+    s_ctl[11] = mut_p;
+    s_ctl[12] = stk_n;
+    s_ctl[13] = stk_t;
+    s_ctl[20] = stk_lost;
+    if (handoff >= 0) {
+      s_ctl[6] = handoff;
+      s_ctl[26] = 1;
+    }
+    S->qw_head = qw_head;
+    S->qw_n = qw_n;
+    S->qw_next = qw_next;
+    S->bytes += bytes;
+    S->attempts += attempts;
+    S->scanned += scanned;
+    S->starts += starts;
+    S->fpods += pops;
+    for (int i = 0; i < 14; i++) S->fcyc[i] += fcyc[i];
+    if (fb >= 0) S->fbail[fb] += 1;
+  }
+  S->qw_pod[lane] = qw_pod;
+  S->qw_shape[lane] = qw_shape;
+  S->qw_sl[lane] = qw_sl;
+  S->qw_lastlen[lane] = qw_lastlen;
+  S->qw_epoch[lane] = qw_epoch;
+  wave_sync();
+  return pops;
+}
+
 template <int NW, bool TOPO>  // TOPO: the batch has topology spread groups (else that code compiles out)
 __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
   constexpr int NT = NW * 64;
-  __shared__ DevDict D;
+  DevDict& D = g_D;
   __shared__ WaveSlots slots[NW];
   __shared__ int32_t s_ok[NW];
   __shared__ int32_t s_wcnt[4 * NW];
-  __shared__ int32_t s_ctl[32];
-  __shared__ int32_t s_stk[2][2 * MSTK_CAP];  // mutation stacks: [0] in-flight positions, [1] existing positions
+  int32_t (&s_ctl)[32] = g_ctl;
+  auto& s_stk = g_stk;  // mutation stacks: [0] in-flight positions, [1] existing positions
   __shared__ int32_t s_list[4 * NT];
   __shared__ uint32_t s_scratch[NW][2 * KP_MAX_WORDS];
   __shared__ KReqs s_B;  // the popped pod's requirements, staged once per pod
   __shared__ int32_t s_fitj[NW][KP_NRES];
   __shared__ int64_t s_preq[KP_NRES];          // pod requests (staged per pod)
   __shared__ int32_t s_pslot[KP_MAX_KEYS];     // PVP row of each pod key (staged per pod)
-  __shared__ int64_t s_fitv[FITV_RES * FITV_CAP];   // Fits threshold values of catalogue 0 (CatHdr.fit_slot rows)
+  auto& s_fitv = g_fitv;  // Fits threshold values of catalogue 0 (CatHdr.fit_slot rows)
   __shared__ TopoOwn s_town[8];                 // owned topology groups of the popped pod (staged per pod)
   __shared__ uint64_t s_tacc[8];
   __shared__ int32_t s_tcnt[8][64];
@@ -1179,7 +1644,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
   __shared__ int64_t s_vint[KP_MAX_BOUND_KEYS * 64];  // parsed integers of the bounded keys' first value words
   __shared__ RowPtr s_rl[NW][RL_CAP];                 // per-wave row lists (filter_types)
   __shared__ int32_t s_pvpb[32];                      // PVP row base of the popped pod per catalogue (staged per pod)
-  __shared__ CatHdr s_hdr[8];                         // catalogue descriptors 0..7
+  auto& s_hdr = g_hdr;  // catalogue descriptors 0..7
   __shared__ CatHdr s_hdrw[NW];                       // per-wave descriptor of a catalogue >= 8
   extern __shared__ int32_t s_dyn[];  // ord[a.sort_cap], npods[a.sort_cap] while n_nc <= a.sort_cap
 
@@ -1228,9 +1693,8 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
     }
   }
   __syncthreads();
-  uint64_t bytes = 0, attempts = 0, pops = 0, scanned = 0, starts = 0, fpods = 0;
+  uint64_t bytes = 0, attempts = 0, pops = 0, scanned = 0, starts = 0;
   const uint64_t pop_cap = (uint64_t)a.n_pods * 64 + 65536;  // Queue.Pop bound for the runaway guard
-  uint64_t fcyc[6] = {0, 0, 0, 0, 0, 0};  // fast-lane cycles (KP_TIMING, lane 0 of wave 0)
   uint64_t tph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tlast = 0;
   const bool timing = a.timing && tid == 0;
   if (tid < 8) s_tsub[tid] = 0;
@@ -1261,11 +1725,15 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
     s_ctl[22] = 0;  // in-flight cursor of the popped pod's shape-level (staged)
     s_ctl[23] = 0;
     s_ctl[26] = 0;  // 1: the fast lane popped s_ctl[6] and hands it to the full path
+    g_fast.qw_head = 0;  // the fast lane's Queue window (empty) and counters
+    g_fast.qw_n = 0;
+    g_fast.qw_next = -1;
+    g_fast.bytes = g_fast.attempts = g_fast.scanned = g_fast.starts = g_fast.fpods = 0;
+    for (int i = 0; i < 16; i++) g_fast.fcyc[i] = 0;
+    for (int i = 0; i < 8; i++) g_fast.fbail[i] = 0;
   }
   __syncthreads();
 
-  // fast lane's prefetched Queue window (wave 0): lane i holds queue entry qw_head + i (ring order)
-  int qw_head = 0, qw_n = 0, qw_next = -1, qw_pod = 0, qw_shape = 0, qw_sl = 0, qw_lastlen = 0, qw_epoch = 0;
   for (;;) {
     // ---- fast lane: wave 0 alone places every pod whose placement needs no requirement merge ----------------
     // The pod owns/feeds no topology group, every existing node is known to fail it (first-fit cursor), and the
@@ -1273,210 +1741,8 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
     // (NC_MERGED) without minValues: NodeClaim.Add is then Fits over the remaining types, evaluated in order
     // until one succeeds. The steps, decisions and state writes are the full path's (below), done by one wave
     // without workgroup barriers. Any other situation hands the popped pod to the full path (s_ctl[26]).
-    if (FASTLANE && wave == 0) {
-      uint64_t ft = a.timing ? __builtin_amdgcn_s_memtime() : 0;
-#define FT(i)                                                \
-  if (a.timing) {                                            \
-    const uint64_t tn_ = __builtin_amdgcn_s_memtime();       \
-    if (lane == 0) fcyc[i] += tn_ - ft;                      \
-    ft = tn_;                                                \
-  }
-      for (;;) {
-        const int len = s_ctl[1];
-        const int head = s_ctl[0];
-        if (len <= 0 || pops > pop_cap) break;
-        // Queue.Pop from the prefetched window: entries [qw_head, qw_head + qw_n) of the ring were in the queue when
-        // the window was read, and nothing rewrites a queued entry (pushes go to the tail) or its pod's level and
-        // lastLen stamps while it waits, so lane i's copy of entry qw_head + i stays exact.
-        int off = head - qw_head;
-        if (off < 0) off += a.n_pods;
-        if (off != qw_next || off >= qw_n) {  // exhausted, or the ring wrapped onto re-pushed entries
-          qw_head = head;
-          qw_n = min(64, len);
-          off = 0;
-          int qi = head + lane;
-          if (qi >= a.n_pods) qi -= a.n_pods;
-          if (lane < qw_n) {
-            qw_pod = a.queue[qi];
-            qw_shape = a.pod_shape[qw_pod];
-            qw_sl = a.shape_level_base[qw_shape] + a.pod_level[qw_pod];
-            qw_lastlen = a.lastlen[qw_pod];
-            qw_epoch = a.lastlen_epoch[qw_pod];
-          }
-        }
-        qw_next = off + 1;  // only the fast lane pops: the next pop reads the following entry
-        const int pod = __builtin_amdgcn_readlane(qw_pod, off);
-        if (__builtin_amdgcn_readlane(qw_epoch, off) == s_ctl[3] && __builtin_amdgcn_readlane(qw_lastlen, off) == len)
-          break;  // the full path's pop sees the same queue and ends the Solve
-        const int shape = __builtin_amdgcn_readlane(qw_shape, off);
-        const int sl = __builtin_amdgcn_readlane(qw_sl, off);
-        // stage: one batch of independent loads (eligibility, requests, tolerations, both first-fit cursors)
-        const int own = TOPO ? a.sl_own_n[sl] + a.shape_rec_n[shape] : 0;
-        const int ce0 = a.n_existing ? a.cur_ex[2 * sl] : 0, ce1 = a.n_existing ? a.cur_ex[2 * sl + 1] : 0;
-        const int64_t preq_lane = lane < KP_NRES ? a.shape_requests[(size_t)shape * KP_NRES + lane] : 0;
-        const uint64_t tolmask = a.shape_tolerates[shape];
-        const int cur = a.cur_nc[2 * sl], stamp = a.cur_nc[2 * sl + 1];
-        wave_sync();
-        if (lane == 0) {
-          s_ctl[0] = head + 1 == a.n_pods ? 0 : head + 1;
-          s_ctl[1] = len - 1;
-        }
-        bool eligible = own == 0;
-        if (a.n_existing) eligible = eligible && min(ce0, mstack_query_wave((LdsI32)s_stk[1], s_ctl[14], s_ctl[21], ce1)) >= a.n_existing;
-        FT(0);
-        if (!eligible) {
-          wave_sync();
-          if (lane == 0) {
-            s_ctl[6] = pod;
-            s_ctl[26] = 1;
-          }
-          break;
-        }
-        const int64_t pr0 = lane_bcast_i64(preq_lane, rr0), pr1 = lane_bcast_i64(preq_lane, rr1);
-        if (a.n_existing && lane == 0) {  // addToExistingNode: every position fails (cursor == n_existing)
-          a.cur_ex[2 * sl] = a.n_existing;
-          a.cur_ex[2 * sl + 1] = s_ctl[15];
-        }
-        FT(1);
-        // sort.Slice(newNodeClaims) replay + first-fit start (sort arrays in LDS; spilled ones: the full path)
-        if (s_ctl[5] == 0) {
-          wave_sync();
-          if (lane == 0) {
-            s_ctl[6] = pod;
-            s_ctl[26] = 1;
-          }
-          break;
-        }
-        const LdsI32 ord = (LdsI32)s_dyn;
-        const LdsI32 npods = (LdsI32)(s_dyn + a.sort_cap);
-        const int c19 = min(cur, mstack_query_wave((LdsI32)s_stk[0], s_ctl[12], s_ctl[20], stamp));
-        const int n_nc = s_ctl[2];
-        const int low = sort_newnodeclaims_wave(ord, npods, n_nc, s_ctl[10], s_ctl[11], 256, &a.stats[31]);
-        if (low == -2) {  // a long shift: the full path sorts (the pending mutation is still in s_ctl[10..11])
-          wave_sync();
-          if (lane == 0) {
-            s_ctl[6] = pod;
-            s_ctl[26] = 1;
-          }
-          break;
-        }
-        const int start = min(min(c19, low >= 0 ? low : INT32_MAX), n_nc);
-        if (lane == 0) {
-          s_ctl[10] = 0;
-          if (low >= 0) mstack_push((LdsI32)s_stk[0], (LdsI32)&s_ctl[12], (LdsI32)&s_ctl[20], ++s_ctl[13], low);
-        }
-        wave_sync();
-        FT(2);
-        // addToInflightNode: pre-checks 64 positions at a time, then the append-path attempts in order. A long scan
-        // is the full path's (512-lane pre-pass).
-        int placed = -1, wpos = -1;
-        bool bail = n_nc - start > 2 * 64;
-        if (lane == 0 && !bail) starts += start;
-        for (int base = start; base < n_nc && placed == -1 && !bail; base += 64) {
-          const int i = base + lane;
-          bool cand = false, tag = false;
-          int nc = 0;
-          if (i < n_nc) {
-            nc = ord[i];
-            // every gather issued unconditionally: one round trip
-            const int32_t fl = nc < a.ncc ? a.nc_fail[(size_t)sl * a.ncc + nc] : -2;
-            const int32_t ver = a.nc_ver[nc];
-            const int32_t ts = a.nc_taintset[nc];
-            const int64_t* rq = a.nc_requests + (size_t)nc * KP_NRES;
-            const int64_t* mx = a.nc_maxalloc + (size_t)nc * KP_NRES;
-            bool fit = !rmask_all || (rq[rr0] + pr0 <= mx[rr0] && rq[rr1] + pr1 <= mx[rr1]);
-            for (uint32_t rm = rr_rest; rm; rm &= rm - 1) {
-              const int r = __builtin_ctz(rm);
-              fit = fit & (rq[r] + lane_bcast_i64(preq_lane, r) <= mx[r]);
-            }
-            cand = fit && fl != ver && ((tolmask >> ts) & 1);
-            tag = cand && fl >= NC_MERGED;
-          }
-          // speculative loads of the first position's NodeClaim (the usual winner): they overlap the pre-checks
-          const int nc0 = __builtin_amdgcn_readlane(nc, 0);
-          const KReqs* cr0 = kreq_at(a.nc_reqs, nc0);
-          const uint64_t hm0 = cr0->hmin & cr0->present;
-          const int cat0 = a.nc_cat[nc0];
-          const uint64_t X00 = lane < D.TW ? a.nc_X[(size_t)nc0 * D.TW + lane] : 0;
-          const int64_t rq0 = lane < KP_NRES ? a.nc_requests[(size_t)nc0 * KP_NRES + lane] : 0;
-          const int32_t j00 = lane < KP_NRES ? a.nc_fitj[(size_t)nc0 * KP_NRES + lane] : 0;
-          if (lane == 0) scanned += min(64, n_nc - base);
-          if (lane == 0) bytes += (uint64_t)min(64, n_nc - base) * (12 + 16 * a.n_req_res);
-          uint64_t cm = __ballot(cand);
-          const uint64_t tm = __ballot(tag);
-          FT(3);
-          while (cm) {
-            const int l = __builtin_ctzll(cm);
-            cm &= cm - 1;
-            if (!((tm >> l) & 1)) {  // needs the merge: the full path evaluates it
-              bail = true;
-              break;
-            }
-            const int ncx = __shfl(nc, l, 64);
-            attempts++;
-            uint64_t hm = hm0, X0 = X00;
-            int cat = cat0;
-            int64_t rq_lane = rq0;
-            int32_t j0_lane = j00;
-            if (l != 0) {
-              const KReqs* cr = kreq_at(a.nc_reqs, ncx);
-              hm = cr->hmin & cr->present;
-              cat = a.nc_cat[ncx];
-              X0 = lane < D.TW ? a.nc_X[(size_t)ncx * D.TW + lane] : 0;
-              rq_lane = lane < KP_NRES ? a.nc_requests[(size_t)ncx * KP_NRES + lane] : 0;
-              j0_lane = lane < KP_NRES ? a.nc_fitj[(size_t)ncx * KP_NRES + lane] : 0;
-            }
-            if (hm) {  // minValues on the NodeClaim: the full path re-filters it
-              bail = true;
-              break;
-            }
-            const int64_t q_lane = rq_lane + preq_lane;
-            const uint64_t X = n_rr <= 4 ? fits_lean(D, hdr(cat), X0, q_lane, j0_lane, (const int64_t LDS*)s_fitv, rr_list,
-                                                     n_rr, bytes, (int32_t LDS*)s_fitj[0])
-                                         : fits_filter(D, hdr(cat), X0, q_lane, j0_lane, (const int64_t LDS*)s_fitv,
-                                                       a.req_res_mask, (RowPtr LDS*)s_rl[0], &bytes, s_fitj[0]);
-            bytes += (uint64_t)D.TW * 8 + KP_NRES * 8 + 8;
-            if (__ballot(X != 0)) {
-              if (lane < D.TW) a.nc_X[(size_t)ncx * D.TW + lane] = X;
-              if (lane < KP_NRES) {
-                a.nc_requests[(size_t)ncx * KP_NRES + lane] = q_lane;
-                a.nc_fitj[(size_t)ncx * KP_NRES + lane] = s_fitj[0][lane];
-              }
-              if (lane == 0) {
-                npods[ncx] += 1;
-                a.nc_ver[ncx] += 1;
-              }
-              placed = ncx;
-              wpos = base + l;
-              break;
-            }
-            if (lane == 0 && ncx < a.ncc) a.nc_fail[(size_t)sl * a.ncc + ncx] = a.nc_ver[ncx];
-          }
-        }
-        wave_sync();
-        FT(4);
-        if (placed == -1) {  // templates, a merge, minValues or a long scan: the full path takes over this pod
-          if (lane == 0) {
-            s_ctl[6] = pod;
-            s_ctl[26] = 1;
-          }
-          break;
-        }
-        pops++;
-        fpods++;
-        if (lane == 0) {
-          s_ctl[10] = 1;
-          s_ctl[11] = wpos;
-          a.cur_nc[2 * sl] = wpos;
-          a.cur_nc[2 * sl + 1] = s_ctl[13];
-          a.placement[pod] = placed;
-          a.events[s_ctl[4]++] = pod;
-        }
-        wave_sync();
-        FT(5);
-      }
-#undef FT
-    }
+    if (FASTLANE && wave == 0)
+      pops += fast_lane<TOPO>((uint64_t)__builtin_amdgcn_kernarg_segment_ptr(), (int32_t LDS*)s_dyn, pops);
     __syncthreads();
     // ---- Queue.Pop: stop when the head pod was last pushed at the current queue length ----------
     if (tid == 0) {
@@ -1826,7 +2092,18 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
               ok = merge_compatible(D, kreq_at(a.tmpl_reqs, tm), B, b_negop, true, m_v, rv, &slots[wave], vi);
               memo = !ok || !own_n;
               if (ok && own_n) ok = topo_narrow(D, own_n, s_town, s_tacc, s_tcnt, true, m_v, rv, vi);
-              if (ok) {
+              if (ok && a.tfeas && !own_n) {
+                // the template's types for this shape-level, precomputed (tmpl_feas_kernel, row-sharded over ranks):
+                // filter_types is a per-type filter, so (options after the limits) ∩ (filtered template) is the
+                // filtered set; minValues is a property of the set and is checked on the intersection
+                const uint64_t* e = a.tfeas + ((size_t)sl * a.n_tmpl + tm) * a.tfeas_words;
+                X &= lane < D.TW ? e[lane] : 0;
+                if (lane < KP_NRES) s_fitj[wave][lane] = reinterpret_cast<const int32_t*>(e + D.TW)[lane];
+                if (rv.hmin & rv.present)
+                  if (!minvalues_ok(D, H->d.code, H->d.TM, rv.hmin & rv.present, rv.minv, X, s_scratch[wave])) X = 0;
+                bytes += (uint64_t)D.TW * 8 + KP_NRES * 4;
+                ok = __ballot(X != 0) != 0;
+              } else if (ok) {
                 const int pb = cat < 32 ? s_pvpb[cat] : a.pvp_base[sl * a.n_catalogs + cat];
                 const uint64_t* pvp = a.shape_pvp + (size_t)pb * D.TW;
                 X = filter_types(D, H, rv, m_v, X, b_keys, pvp, s_pslot, q_lane, 0, (const int64_t LDS*)s_fitv, a.req_res_mask, vi,
@@ -1980,16 +2257,92 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
     a.stats[2] = pops;
     a.stats[3] = (uint64_t)s_ctl[2];
     a.stats[4] = (uint64_t)s_ctl[4];
-    a.stats[5] = scanned;  // in-flight positions scanned by the pre-pass
-    a.stats[6] = starts;   // sum of cursor start positions
-    a.stats[24] = fpods;
-    for (int i = 0; i < 6; i++) a.stats[25 + i] = fcyc[i];
+    a.stats[5] = scanned + g_fast.scanned;  // in-flight positions scanned by the pre-pass
+    a.stats[6] = starts + g_fast.starts;    // sum of cursor start positions
+    atomicAdd((unsigned long long*)&a.stats[0], (unsigned long long)g_fast.attempts);
+    atomicAdd((unsigned long long*)&a.stats[1], (unsigned long long)g_fast.bytes);
+    a.stats[24] = g_fast.fpods;
+    for (int i = 0; i < 7; i++) a.stats[32 + i] = g_fast.fbail[i];
+    for (int i = 0; i < 6; i++) a.stats[25 + i] = g_fast.fcyc[i];
+    if (FT_FINE && timing)
+      for (int i = 0; i < 8; i++) a.stats[16 + i] = g_fast.fcyc[6 + i];
   }
   if (s_ctl[5])
     for (int i = tid; i < s_ctl[2]; i += NT) {
       a.g_npods[i] = s_dyn[a.sort_cap + i];
       a.g_order[i] = s_dyn[i];
     }
+}
+
+// ------------------------------------------------------------------------------------------------
+// tmpl_feas_kernel: for each (shape-level, NodePool template) pair of a row range, the template's InstanceTypeOptions
+// a new NodeClaim for that shape-level would start from (addToNewNodeClaim: Compatible + Add of the requirements,
+// then filterInstanceTypesByRequirements over the template's types with the daemon + pod requests), without the
+// NodePool limits and minValues, which solve_kernel applies at use. Entry (tfeas_words u64): the type mask, the Fits
+// threshold indices (int32 x KP_NRES), and a word: 1 compatible / 0 incompatible / -1 not precomputed (shape-levels
+// that own topology groups narrow the requirements by the current counts first). One wave per pair. Row ranges are
+// what the ranks of a kp_comm split between them before one ncclAllGather of the table.
+// ------------------------------------------------------------------------------------------------
+#define TF_WAVES 4
+__global__ __launch_bounds__(TF_WAVES * 64) void tmpl_feas_kernel(TfeasArgs a) {
+  __shared__ DevDict D;
+  __shared__ WaveSlots slots[TF_WAVES];
+  __shared__ uint32_t s_scratch[TF_WAVES][2 * KP_MAX_WORDS];
+  __shared__ RowPtr s_rl[TF_WAVES][RL_CAP];
+  __shared__ int32_t s_fitj[TF_WAVES][KP_NRES];
+  __shared__ CatHdr s_hdr[TF_WAVES];
+  __shared__ int64_t s_vint[KP_MAX_BOUND_KEYS * 64];
+  block_copy(D, a.dict);
+  __syncthreads();
+  for (int i = threadIdx.x; i < D.KB * 64; i += TF_WAVES * 64) s_vint[i] = a.vint[i];
+  __syncthreads();
+  const VInt vi{(const int64_t LDS*)s_vint, a.vint, D.KB};
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = LANE;
+  const int NTm = a.n_tmpl, TW = D.TW;
+  const long first = (long)a.row_lo * NTm, last = (long)a.row_hi * NTm;
+  for (long pr = first + (long)blockIdx.x * TF_WAVES + wave; pr < last; pr += (long)gridDim.x * TF_WAVES) {
+    const int sl = (int)(pr / NTm), t = (int)(pr % NTm);
+    uint64_t* e = a.out + (size_t)pr * a.words;
+    int32_t* ej = reinterpret_cast<int32_t*>(e + TW);
+    if (a.sl_own_n[sl] > 0) {
+      if (lane == 0) e[TW + KP_NRES / 2] = (uint64_t)(int64_t)-1;
+      continue;
+    }
+    const int shape = a.sl_shape[sl];
+    const int cat = a.tmpl_catalog[t];
+    hdr_fill_wave((CatHdr LDS*)&s_hdr[wave], &a.cats[cat], D.C);
+    wave_sync();
+    const CatHdr LDS* H = (const CatHdr LDS*)&s_hdr[wave];
+    const KReqs* B = kreq_at(a.shape_reqs, sl);
+    uint64_t m_v = 0;
+    ReqView rv;
+    const bool ok = merge_compatible(D, kreq_at(a.tmpl_reqs, t), B, a.shape_negop[sl], true, m_v, rv, &slots[wave], vi);
+    uint64_t X = 0;
+    int32_t j_lane = 0;
+    if (ok) {
+      X = lane < TW ? a.tmpl_X[(size_t)t * TW + lane] : 0;
+      const uint64_t* pvp = a.shape_pvp + (size_t)a.pvp_base[sl * a.n_catalogs + cat] * TW;
+      const int64_t q_lane = lane < KP_NRES ? a.tmpl_daemon[(size_t)t * KP_NRES + lane] +
+                                                  a.shape_requests[(size_t)shape * KP_NRES + lane]
+                                            : 0;
+      uint64_t bytes = 0;
+      X = filter_types(D, H, rv, m_v, X, B->present, pvp, a.pvp_slot + (size_t)sl * KP_MAX_KEYS, q_lane, 0, nullptr,
+                       a.req_res_mask, vi, s_scratch[wave], (RowPtr LDS*)s_rl[wave], &bytes, s_fitj[wave], 0, nullptr,
+                       false);
+      j_lane = lane < KP_NRES ? s_fitj[wave][lane] : 0;
+    }
+    if (lane < TW) e[lane] = X;
+    if (lane < KP_NRES) ej[lane] = j_lane;
+    if (lane == 0) e[TW + KP_NRES / 2] = ok ? 1 : 0;
+  }
+}
+
+hipError_t launch_tmpl_feas(const TfeasArgs& a, hipStream_t s) {
+  const long pairs = (long)(a.row_hi - a.row_lo) * a.n_tmpl;
+  if (pairs <= 0) return hipSuccess;
+  const int blocks = (int)std::min<long>((pairs + TF_WAVES - 1) / TF_WAVES, 4096);
+  hipLaunchKernelGGL(tmpl_feas_kernel, dim3(blocks), dim3(TF_WAVES * 64), 0, s, a);
+  return hipGetLastError();
 }
 
 // ------------------------------------------------------------------------------------------------

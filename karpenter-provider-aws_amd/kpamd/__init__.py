@@ -67,6 +67,7 @@ def load_lib(path=LIB_PATH):
         "kp_solve": (C.c_int32, [C.c_void_p, P(abi.SolveIn), P(C.c_void_p)]),
         "kp_solve_validate": (C.c_int32, [P(abi.SolveIn)]),
         "kp_solve_prepare": (C.c_int32, [C.c_void_p, P(abi.SolveIn), P(C.c_void_p)]),
+        "kp_solve_prepare_comm": (C.c_int32, [C.c_void_p, P(abi.SolveIn), C.c_void_p, P(C.c_void_p)]),
         "kp_solve_run": (C.c_int32, [C.c_void_p, P(C.c_void_p)]),
         "kp_solve_plan_destroy": (None, [C.c_void_p]),
         "kp_result_nodeclaim_count": (C.c_uint32, [C.c_void_p]),
@@ -212,6 +213,7 @@ def stats_dict(st):
     d["phase_cycles"] = list(st.phase_cycles)
     d["attempt_cycles"] = list(st.attempt_cycles)
     d["fast_cycles"] = list(st.fast_cycles)
+    d["fast_bails"] = list(st.fast_bails)
     return d
 
 
@@ -252,19 +254,24 @@ class Scheduler:
         finally:
             lib.kp_result_destroy(res)
 
-    def prepare(self):
-        """kp_solve_prepare: compile + upload once; returns a SolvePlan whose run() repeats Solve."""
-        return SolvePlan(self)
+    def prepare(self, comm=None):
+        """kp_solve_prepare: compile + upload once; returns a SolvePlan whose run() repeats Solve. With a Comm,
+        kp_solve_prepare_comm: a collective whose template-options table is row-sharded over the ranks and
+        all-gathered (every rank passes the same batch)."""
+        return SolvePlan(self, comm)
 
 
 class SolvePlan:
-    def __init__(self, sched):
+    def __init__(self, sched, comm=None):
         self.sched = sched
         lib = sched.ctx.lib
         arena = Arena()
         si = abi.build_solve_in(arena, sched.problem, catalog_handles=[c.h.value for c in sched.catalogs])
         h = C.c_void_p()
-        _check(lib, lib.kp_solve_prepare(sched.ctx.h, C.byref(si), C.byref(h)))
+        if comm is None:
+            _check(lib, lib.kp_solve_prepare(sched.ctx.h, C.byref(si), C.byref(h)))
+        else:
+            _check(lib, lib.kp_solve_prepare_comm(sched.ctx.h, C.byref(si), comm.h, C.byref(h)))
         self.h = h
 
     def run(self, read=True):
