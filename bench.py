@@ -80,6 +80,12 @@ def main():
     cat = catalog.build_catalog(lib)
     prob = synth.config2(cat, n_pods=args.pods, seed=2)
     ctx = kpamd.Context(local)
+    kcomm = None
+    if dist is not None and backend == "nccl":  # libkp's RCCL communicator (one rank per GPU): rank 0's unique id
+        # shared over torch.distributed; a gloo rehearsal shares GPUs between ranks, which RCCL does not allow
+        uid = [kpamd.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        kcomm = kpamd.Comm(ctx, uid[0], world, rank)
     sched = kpamd.Scheduler(ctx, prob)
     sched.solve_in()  # the caller's marshalled batch (Go: the []*v1.Pod it passes to Solve), built once
 
@@ -95,16 +101,16 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    cold = sched.solve(read=False)["stats"]  # first Solve on this ctx: compiles the catalogue half (cache miss)
+    cold = _solve_step(sched, kcomm)["stats"]  # first Solve on this ctx: compiles the catalogue half (cache miss)
     for _ in range(args.warmup):
-        sched.solve(read=False)
+        _solve_step(sched, kcomm)
     barrier()
     t0 = time.perf_counter()
-    runs = [sched.solve(read=False)["stats"] for _ in range(args.steps)]
+    runs = [_solve_step(sched, kcomm)["stats"] for _ in range(args.steps)]
     barrier()
     elapsed = max_over_ranks(time.perf_counter() - t0)
 
-    res = sched.solve(read=True)  # one more Solve for result sanity (not timed)
+    res = _solve_step(sched, kcomm, read=True)  # one more Solve for result sanity (not timed)
     placed = int((res["placement"] != -1).sum())
     mean = lambda k: sum(r[k] for r in runs) / len(runs)
     k_ms, f_ms, dev_ms = mean("solve_kernel_ms"), mean("finalize_kernel_ms"), mean("device_ms")
@@ -131,7 +137,9 @@ def main():
                         "3 weighted NodePools; step = whole kp_solve call (per-Solve compile + upload + kernels + "
                         "result copy-back)",
             "pods": prob.n_pods, "instance_types": len(cat), "nodepools": len(prob.nodepools),
-            "parallelism": f"replicas x{world} (Solve is sequential FFD; one workgroup per Solve)",
+            "parallelism": f"replicas x{world} (Solve is sequential FFD; one workgroup per Solve)" +
+                           ("; each Solve's template-options table row-sharded over the ranks + ncclAllGather"
+                            if world > 1 else ""),
         },
         "per_solve_prepare_ms": round(mean("prepare_ms"), 3),
         "run_host_ms": round(mean("host_ms"), 3),
@@ -168,44 +176,58 @@ def main():
     if not args.quick:
         cfgs = {}
         cfgs["config1"] = _solve_leg("config1", synth.config1(cat, n_pods=1000, seed=1), ctx, barrier,
-                                     max_over_ranks, world, args.steps, 1,
+                                     max_over_ranks, world, args.steps, 1, kcomm,
                                      None if (rank or world > 1 or args.no_cpu_baseline) else ("1", 1000))
         progress("config1 done")
         cfgs["config3"] = _solve_leg("config3", synth.config3(cat, n_pods=args.c3_pods), ctx, barrier,
-                                     max_over_ranks, world, 2, 1,
+                                     max_over_ranks, world, 2, 1, kcomm,
                                      None if (rank or world > 1 or args.no_cpu_baseline) else ("3", 3000))
         progress("config3 done")
         cfgs["config5"] = _solve_leg("config5", synth.config5(cat, n_pods=args.c5_pods), ctx, barrier,
-                                     max_over_ranks, world, 1, 0,
+                                     max_over_ranks, world, 1, 0, kcomm,
                                      None if (rank or world > 1 or args.no_cpu_baseline) else ("5", 6000))
         line["configs"] = cfgs
     if not args.no_consolidation and not args.quick:
         progress("config5 done")
-        line["consolidation"] = _consolidation(args, cat, ctx, dist, rank, world, barrier)
+        line["consolidation"] = _consolidation(args, cat, ctx, dist, rank, world, barrier, kcomm)
         progress("consolidation done")
     if rank == 0:
         print(json.dumps(line), flush=True)
+    if kcomm is not None:
+        kcomm.close()
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
 
 
-def _solve_leg(name, prob, ctx, barrier, max_over_ranks, world, steps, warmup, cpu):
+def _solve_step(sched, kcomm, read=False):
+    """One whole Solve through the C ABI: kp_solve (one process), or with N ranks kp_solve_prepare_comm (the
+    template-options table row-sharded over the ranks and all-gathered) + kp_solve_run + destroy."""
+    if kcomm is None:
+        return sched.solve(read=read)
+    plan = sched.prepare(kcomm)
+    try:
+        return plan.run(read=read)
+    finally:
+        plan.close()
+
+
+def _solve_leg(name, prob, ctx, barrier, max_over_ranks, world, steps, warmup, kcomm, cpu):
     """One more BASELINE config as a Solve leg: replicas on every rank, K timed whole kp_solve calls (the catalogue
     half resident after the first). value counts every pod the batch submits; placed_pods_per_s counts the pods
     the Solve placed (existing nodes + new NodeClaims; limits or taints can leave pods unschedulable)."""
     import kpamd
     sched = kpamd.Scheduler(ctx, prob)
     sched.solve_in()
-    sched.solve(read=False)
+    _solve_step(sched, kcomm)
     for _ in range(warmup):
-        sched.solve(read=False)
+        _solve_step(sched, kcomm)
     barrier()
     t0 = time.perf_counter()
-    runs = [sched.solve(read=False)["stats"] for _ in range(steps)]
+    runs = [_solve_step(sched, kcomm)["stats"] for _ in range(steps)]
     barrier()
     elapsed = max_over_ranks(time.perf_counter() - t0)
-    res = sched.solve(read=True)
+    res = _solve_step(sched, kcomm, read=True)
     k_ms = sum(r["solve_kernel_ms"] for r in runs) / len(runs)
     placed = int((res["placement"] != -1).sum())
     out = {"value": round(prob.n_pods * world * steps / elapsed, 1), "unit": "pods/s", "pods": prob.n_pods,
@@ -287,7 +309,7 @@ def _feasibility(args, cat, ctx, prob, barrier, max_over_ranks, world, steps=10)
 CHUNK = 1 << 16  # subsets per generation chunk (1M subsets: 16 chunks, contiguous chunk ranges per rank)
 
 
-def _consolidation(args, cat, ctx, dist, rank, world, barrier):
+def _consolidation(args, cat, ctx, dist, rank, world, barrier, kcomm):
     """Config 4: multi-node consolidation on a 10k-node cluster packed near capacity (delete, replace and no-op
     decisions all occur). Timed, per rank:
       sweep     this rank's contiguous chunk range of the 1M random candidate subsets (2..100 candidates, fixed seed
@@ -325,11 +347,7 @@ def _consolidation(args, cat, ctx, dist, rank, world, barrier):
     gen_s = time.perf_counter() - t0
     t0 = time.perf_counter()
     plan = kpamd.ClusterPlan(ctx, cl)
-    comm = None
-    if dist is not None:  # the RCCL communicator lives in libkp: rank 0's unique id, shared over torch.distributed
-        uid = [kpamd.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        comm = kpamd.Comm(ctx, uid[0], world, rank)
+    comm = kcomm  # the RCCL communicator lives in libkp (None at N=1)
     prep_s = time.perf_counter() - t0
     warm = min(len(sw_offs) - 1, 1024)  # warmup (untimed) on the first subsets
     plan.argmin(sw_offs[:warm + 1], sw_nodes, base_index=base_index, comm=comm)
@@ -390,8 +408,6 @@ def _consolidation(args, cat, ctx, dist, rank, world, barrier):
             torch.cuda.synchronize()
             by[name] = {"subsets": int(len(idx)), "sims_per_s": round(len(idx) / (time.perf_counter() - t1), 1)}
         out["by_decision"] = by
-    if comm is not None:
-        comm.close()
     plan.close()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = _cpu_baseline_sims(cl, cands, args.cpu_sample_sims)

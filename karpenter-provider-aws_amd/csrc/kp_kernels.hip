@@ -1695,6 +1695,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
   __syncthreads();
   uint64_t bytes = 0, attempts = 0, pops = 0, scanned = 0, starts = 0;
   const uint64_t pop_cap = (uint64_t)a.n_pods * 64 + 65536;  // Queue.Pop bound for the runaway guard
+  int fl_fail = 0, fl_skip = 0;  // fast-lane backoff (wave 0)
   uint64_t tph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tlast = 0;
   const bool timing = a.timing && tid == 0;
   if (tid < 8) s_tsub[tid] = 0;
@@ -1741,8 +1742,18 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
     // (NC_MERGED) without minValues: NodeClaim.Add is then Fits over the remaining types, evaluated in order
     // until one succeeds. The steps, decisions and state writes are the full path's (below), done by one wave
     // without workgroup barriers. Any other situation hands the popped pod to the full path (s_ctl[26]).
-    if (FASTLANE && wave == 0)
-      pops += fast_lane<TOPO>((uint64_t)__builtin_amdgcn_kernarg_segment_ptr(), (int32_t LDS*)s_dyn, pops);
+    if (FASTLANE && wave == 0) {
+      // the call costs a few thousand cycles (register saves): after calls that placed nothing (topology-owning
+      // or unschedulable pods), skip it for a growing number of pops; results do not depend on which path places
+      if (fl_skip > 0) {
+        fl_skip--;
+      } else {
+        const int placed_fast = fast_lane<TOPO>((uint64_t)__builtin_amdgcn_kernarg_segment_ptr(), (int32_t LDS*)s_dyn, pops);
+        pops += placed_fast;
+        fl_fail = placed_fast ? 0 : fl_fail + 1;
+        fl_skip = fl_fail >= 2 ? min(1 << min(fl_fail - 2, 6), 64) : 0;
+      }
+    }
     __syncthreads();
     // ---- Queue.Pop: stop when the head pod was last pushed at the current queue length ----------
     if (tid == 0) {
