@@ -550,17 +550,19 @@ void kp_result_destroy(kp_solve_result* res);
  * Cluster snapshot as the disruption controller sees it (state.Cluster nodes + their reschedulable pods),
  * and a batch of candidate subsets. For each subset S, kp_simulate_batch computes what upstream
  * computeConsolidation(S...) decides (docs R:website/content/en/preview/concepts/disruption.md:89-128):
- * SimulateScheduling = Solve(pods of S, existing = every other node) + TruncateInstanceTypes(100); not all
- * pods scheduled -> no-op; 0 NodeClaims -> delete; > 1 -> no-op; 1 -> replace if some option's worst
- * launch price is below the summed candidate price (and, for multi-node, filterOutSameType keeps one).
- * Spot-to-spot (feature gate, default off) -> no-op. */
+ * SimulateScheduling = Solve(pending pods + pods of the deleting nodes + pods of S, existing = every node that is
+ * neither in S nor deleting) + TruncateInstanceTypes(100), with the NodePools' remaining limits; a pod of S placed
+ * on an uninitialized node is an error (pods of deleting nodes are exempt); not all non-pending pods scheduled ->
+ * no-op; 0 NodeClaims -> delete; > 1 -> no-op; 1 -> replace if some option's worst launch price is below the
+ * summed candidate price (and, for multi-node, filterOutSameType keeps one). Spot-to-spot (feature gate, default
+ * off) -> no-op. Subsets must not name deleting nodes. */
 typedef struct kp_cluster_node {
   kp_existing_node node;      /* labels, taints, available (allocatable - bound pods), requests, initialized */
   uint32_t catalog;           /* catalogue of its instance type */
   uint32_t instance_type;     /* index of its instance type in that catalogue */
   const uint32_t* pods;       /* reschedulable pods on this node: indices into kp_cluster.pods */
   uint32_t n_pods;
-  uint32_t reserved_;
+  uint32_t deleting;          /* MarkedForDeletion: never a destination; its pods join every simulation */
 } kp_cluster_node;
 
 typedef struct kp_cluster {
@@ -576,6 +578,10 @@ typedef struct kp_cluster {
   const kp_pod* pods;
   uint32_t n_pods;
   uint32_t spot_to_spot;      /* SpotToSpotConsolidation feature gate (only 0 supported) */
+  const uint32_t* pending_pods;  /* provisionable pods not bound to any node (indices into pods): they join every
+                                    simulation, but their own scheduling errors do not block a decision */
+  uint32_t n_pending;
+  uint32_t reserved_;
 } kp_cluster;
 
 enum kp_decision { KP_DECISION_NOOP = 0, KP_DECISION_DELETE = 1, KP_DECISION_REPLACE = 2 };

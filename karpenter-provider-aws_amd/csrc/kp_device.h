@@ -256,6 +256,8 @@ struct SimArgs {
   const int32_t* tmpl_nodepool;
   const uint64_t* tmpl_X;
   const int64_t* tmpl_daemon;
+  const uint32_t* tmpl_limit_present;  // [NT] NodePool limits: filterByRemainingResources for the new NodeClaim
+  const int64_t* tmpl_remaining;       // [NT][NRES]
   // existing nodes in upstream order (initialized first, then name); position e
   int32_t E, EW;
   const uint16_t* ex_code;           // [K][E] value bit of the node's label for key k, 0xFFFF: no label
@@ -266,6 +268,11 @@ struct SimArgs {
   // precomputed per shape-level (sim_prep_kernel / sim_usable_kernel)
   uint64_t* usable;                  // [SL][EW] CanAdd on the snapshot: tolerated, compatible, fits
   SimNC* tres;                       // [SL] addToNewNodeClaim outcome (tmpl -1: none)
+  // pods every simulation schedules besides those of S: the deleting nodes' and the pending ones
+  const uint64_t* base_excl;         // [EW] deleting nodes (never destinations)
+  const uint32_t* base_keys;         // [n_base] their queue ranks
+  int32_t n_base;
+  const uint8_t* pod_kind;           // [P] 0 on a node, 1 on a deleting node, 2 pending
   // pods (all pods of the cluster)
   const int32_t* pod_shape;          // [P]
   const uint32_t* pod_rank;          // [P] position in byCPUAndMemoryDescending order

@@ -3007,6 +3007,8 @@ struct kp_cluster_plan {
   SimArgs a;
   int N = 0, T2 = 1, n_cu = 256;
   vector<uint32_t> node_npods;
+  vector<uint8_t> deleting;         // [N] MarkedForDeletion
+  int n_base = 0;                   // pending + deleting-node pods in every simulation
   double prepare_ms = 0;
 };
 
@@ -3072,8 +3074,6 @@ int32_t kp_cluster_prepare(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan** 
   const Dict& d = C.B->d;
   const int TW = C.B->TW, E = N, EW = (E + 63) / 64, SL = (int)C.shape_reqs.size(), NT = (int)C.B->tmpl_reqs.size();
   const int T = d.dd.T, K = d.dd.K;
-  for (uint32_t lp : C.tmpl_limit_present)
-    if (lp) return fail(KP_E_UNSUPPORTED, "NodePool limits in consolidation simulations");
   // a pod NotIn/DoesNotExist on a key some node lacks would add that key to the node's requirements
   uint64_t all_nodes_keys = ~0ull;
   for (auto& q : C.ex_reqs) all_nodes_keys &= q.present;
@@ -3144,6 +3144,33 @@ int32_t kp_cluster_prepare(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan** 
     node_name[i] = name_id(ht.name);
   }
   if (node_pods.empty()) node_pods.push_back(0);
+  // pods every simulation schedules besides those of S (SimulateScheduling: pending pods and the pods of nodes
+  // already being deleted), and the deleting nodes, which are never destinations
+  if (cl->n_pending && !cl->pending_pods) return fail(KP_E_INVAL, "null pending_pods");
+  vector<uint8_t> pod_kind(std::max<uint32_t>(P, 1), 0);
+  vector<uint32_t> base_keys;
+  vector<uint64_t> base_excl(std::max(EW, 1), 0);
+  plan->deleting.assign(N, 0);
+  for (uint32_t j = 0; j < cl->n_pending; j++) {
+    const uint32_t p = cl->pending_pods[j];
+    if (p >= P) return fail(KP_E_INVAL, "pending pod %u", p);
+    if (pod_kind[p]) return fail(KP_E_INVAL, "pod %u listed twice", p);
+    pod_kind[p] = 2;
+    base_keys.push_back(rank[p]);
+  }
+  for (int i = 0; i < N; i++) {
+    if (!cl->nodes[i].deleting) continue;
+    plan->deleting[i] = 1;
+    const int e = node_pos[i];
+    base_excl[e >> 6] |= 1ull << (e & 63);
+    for (uint32_t j = node_off[i]; j < node_off[i + 1]; j++) {
+      if (pod_kind[node_pods[j]]) return fail(KP_E_INVAL, "pod %u listed twice", node_pods[j]);
+      pod_kind[node_pods[j]] = 1;
+      base_keys.push_back(rank[node_pods[j]]);
+    }
+  }
+  plan->n_base = (int)base_keys.size();
+  if (base_keys.empty()) base_keys.push_back(0);
   vector<uint32_t> type_name((size_t)cl->n_catalogs * std::max(T, 1), 0xFFFFFFFFu);
   for (uint32_t c = 0; c < cl->n_catalogs; c++)
     for (size_t t = 0; t < cl->catalogs[c]->types.size(); t++)
@@ -3215,6 +3242,11 @@ int32_t kp_cluster_prepare(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan** 
   const size_t o_nflags = blob.put(node_flags);
   const size_t o_nname = blob.put(node_name);
   const size_t o_tname = blob.put(type_name);
+  const size_t o_pkind = blob.put(pod_kind);
+  const size_t o_bkeys = blob.put(base_keys);
+  const size_t o_bexcl = blob.put(base_excl);
+  const size_t o_tlp = blob.put(C.tmpl_limit_present);
+  const size_t o_trem = blob.put(C.tmpl_remaining);
   const size_t host_bytes = blob.host.size();
   const size_t o_usable = blob.reserve(sizeof(uint64_t) * (size_t)std::max(SL, 1) * std::max(EW, 1));
   const size_t o_tres = blob.reserve(sizeof(SimNC) * (size_t)std::max(SL, 1));
@@ -3250,6 +3282,12 @@ int32_t kp_cluster_prepare(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan** 
   a.tmpl_nodepool = (const int32_t*)(base + o_tnp);
   a.tmpl_X = (const uint64_t*)(base + o_tX);
   a.tmpl_daemon = (const int64_t*)(base + o_tdm);
+  a.tmpl_limit_present = (const uint32_t*)(base + o_tlp);
+  a.tmpl_remaining = (const int64_t*)(base + o_trem);
+  a.pod_kind = base + o_pkind;
+  a.base_keys = (const uint32_t*)(base + o_bkeys);
+  a.base_excl = (const uint64_t*)(base + o_bexcl);
+  a.n_base = plan->n_base;
   a.E = E;
   a.EW = EW;
   a.ex_code = (const uint16_t*)(base + o_excode);
@@ -3308,11 +3346,13 @@ static int32_t SimLaunchLocked(kp_cluster_plan* plan, const uint32_t* offsets, c
   const uint32_t n_flat = offsets[n_subsets];
   if (n_flat && !nodes) return fail(KP_E_INVAL, "null nodes");
   int cap = 1;
+  const bool any_deleting = plan->n_base > 0;
   for (uint32_t s = 0; s < n_subsets; s++) {
     if (offsets[s + 1] < offsets[s]) return fail(KP_E_INVAL, "offsets not monotone at %u", s);
-    uint64_t np = 0;
+    uint64_t np = (uint64_t)plan->n_base;  // every simulation also schedules the pending and deleting-node pods
     for (uint32_t j = offsets[s]; j < offsets[s + 1]; j++) {
       if (nodes[j] >= (uint32_t)plan->N) return fail(KP_E_INVAL, "subset %u: node %u", s, nodes[j]);
+      if (any_deleting && plan->deleting[nodes[j]]) return fail(KP_E_INVAL, "subset %u: node %u is being deleted", s, nodes[j]);
       np += plan->node_npods[nodes[j]];
     }
     if (np > 65535) return fail(KP_E_UNSUPPORTED, "subset %u reschedules %llu pods (max 65535)", s, (unsigned long long)np);

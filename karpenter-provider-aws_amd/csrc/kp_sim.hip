@@ -197,6 +197,22 @@ __global__ __launch_bounds__(SIM_WAVES * 64) void sim_prep_kernel(SimArgs a) {
       if (!((tol >> a.tmpl_taintset[t]) & 1)) continue;
       const int cat = a.tmpl_catalog[t];
       uint64_t X = lane < D.TW ? a.tmpl_X[(size_t)t * D.TW + lane] : 0;
+      const uint32_t lim = a.tmpl_limit_present[t];
+      if (lim) {  // filterByRemainingResources: every limited resource's capacity within the NodePool's remaining
+        const int64_t* rem = a.tmpl_remaining + (size_t)t * KP_NRES;
+        const int64_t* capv = a.cats[cat].cap;
+        uint64_t m = X, keep = 0;
+        while (m) {
+          const int b = __builtin_ctzll(m);
+          m &= m - 1;
+          const int ty = lane * 64 + b;
+          bool viable = true;
+          for (int r = 0; r < KP_NRES; r++)
+            if (((lim >> r) & 1) && capv[(size_t)r * D.T + ty] > rem[r]) viable = false;
+          if (viable) keep |= 1ull << b;
+        }
+        X = keep;
+      }
       if (!__ballot(X != 0)) continue;
       uint64_t m_v = 0;
       ReqView rv;
@@ -285,16 +301,17 @@ __global__ __launch_bounds__(NW * 64) void sim_kernel(SimArgs a) {
     const uint32_t s0 = a.sub_off[sim];
     const int ns = (int)(a.sub_off[sim + 1] - s0);
     for (int w = lane; w < EW; w += 64) {
-      excl[w] = 0;
+      excl[w] = a.base_excl[w];  // deleting nodes are never destinations
       dirty[w] = 0;
     }
+    for (int i = lane; i < a.n_base; i += 64) keys[i] = a.base_keys[i];  // pending + deleting-node pods
     wave_sync();
     // ---- exclusions, candidate prices, pods of S ------------------------------------------------
     for (int i = lane; i < ns; i += 64) {
       const int pos = a.node_pos[a.sub_nodes[s0 + i]];
       atomicOr((unsigned long long*)&excl[pos >> 6], 1ull << (pos & 63));
     }
-    int n = 0;
+    int n = a.n_base;
     bool overflow = false;
     for (int i0 = 0; i0 < ns; i0 += 64) {
       const int i = i0 + lane;
@@ -345,6 +362,13 @@ __global__ __launch_bounds__(NW * 64) void sim_kernel(SimArgs a) {
     sim_sync();
 
     // ---- the Solve loop -------------------------------------------------------------------------
+    // need: pods that must schedule (all but the pending ones: AllNonPendingPodsScheduled)
+    int need = 0;
+    for (int i0 = 0; i0 < n; i0 += 64) {
+      const int i = i0 + lane;
+      const bool req = i < n && a.pod_kind[a.rank_pod[keys[i]]] != 2;
+      need += __builtin_popcountll(__ballot(req));
+    }
     int head = 0, len = overflow ? 0 : n, n_nc = 0, placed_cnt = 0;
     uint32_t epoch = 1;
     bool abort = overflow;
@@ -357,6 +381,7 @@ __global__ __launch_bounds__(NW * 64) void sim_kernel(SimArgs a) {
       pops++;
       const int lvl = (int)((ent >> 32) & 0xFF);
       const int gid = (int)a.rank_pod[keys[i]];
+      const int kind = a.pod_kind[gid];
       const int shape = a.pod_shape[gid];
       const int sl = a.shape_level_base[shape] + lvl;
       stage_shape(a, sl, shape, sB, spreq, s_pslot[wave]);
@@ -406,8 +431,8 @@ __global__ __launch_bounds__(NW * 64) void sim_kernel(SimArgs a) {
       if (lane == 0) sstart[sl] = st;
       if (placed <= -2) {
         const int e = -2 - placed;
-        if (!a.ex_init[e]) {
-          abort = true;  // SimulateScheduling: relied on an uninitialized node
+        if (!a.ex_init[e] && kind == 0) {
+          abort = true;  // SimulateScheduling: a candidate pod relied on an uninitialized node
         } else {
           const bool first = !((dirty[e >> 6] >> (e & 63)) & 1);
           if (lane < a.RU) {
@@ -476,7 +501,7 @@ __global__ __launch_bounds__(NW * 64) void sim_kernel(SimArgs a) {
       }
       if (abort) break;
       if (placed != -1) {
-        placed_cnt++;
+        if (kind != 2) placed_cnt++;
       } else {  // Preferences.Relax + Queue.Push
         const bool relaxed = lvl + 1 < a.shape_nlevels[shape];
         int tail = head + len;
@@ -501,7 +526,7 @@ __global__ __launch_bounds__(NW * 64) void sim_kernel(SimArgs a) {
     int decision = KP_DECISION_NOOP, nodepool = 0, n_options = 0;
     double repl = 0, savings = 0;
     const double candReported = priced ? candPrice : 0.0;
-    if (!abort && placed_cnt == n) {
+    if (!abort && placed_cnt == need) {
       if (n_nc == 0) {
         decision = KP_DECISION_DELETE;
         savings = candReported;

@@ -201,7 +201,7 @@ class NodeClass(C.Structure):
 
 class ClusterNode(C.Structure):
     _fields_ = [("node", ExistingNode), ("catalog", C.c_uint32), ("instance_type", C.c_uint32),
-                ("pods", C.POINTER(C.c_uint32)), ("n_pods", C.c_uint32), ("reserved_", C.c_uint32)]
+                ("pods", C.POINTER(C.c_uint32)), ("n_pods", C.c_uint32), ("deleting", C.c_uint32)]
 
 
 class Cluster(C.Structure):
@@ -209,7 +209,8 @@ class Cluster(C.Structure):
                 ("n_catalogs", C.c_uint32), ("n_nodepools", C.c_uint32), ("nodepools", C.POINTER(NodePool)),
                 ("nodes", C.POINTER(ClusterNode)), ("n_nodes", C.c_uint32), ("n_shapes", C.c_uint32),
                 ("shapes", C.POINTER(PodShape)), ("pods", C.POINTER(Pod)), ("n_pods", C.c_uint32),
-                ("spot_to_spot", C.c_uint32)]
+                ("spot_to_spot", C.c_uint32), ("pending_pods", C.POINTER(C.c_uint32)), ("n_pending", C.c_uint32),
+                ("reserved_", C.c_uint32)]
 
 
 class SimResult(C.Structure):
@@ -422,11 +423,14 @@ def build_cluster(arena, cl, catalog_handles=None):
     nodes = []
     for n in cl.nodes:
         pods = arena.arr(C.c_uint32, list(n.pods))
-        nodes.append(ClusterNode(arena.existing_node(n.node), n.catalog, n.instance_type, pods, len(n.pods), 0))
+        nodes.append(ClusterNode(arena.existing_node(n.node), n.catalog, n.instance_type, pods, len(n.pods),
+                                 1 if n.deleting else 0))
     nodes_a = arena.arr(ClusterNode, nodes)
     shapes = arena.arr(PodShape, [arena.shape(s) for s in cl.shapes])
+    pending = list(cl.pending)
     c = Cluster(handles, descs, len(cl.catalogs), len(cl.nodepools), nps, nodes_a, len(cl.nodes), len(cl.shapes),
-                shapes, _pods_array(arena, cl.pod_shape, cl.pod_creation, cl.pod_uid), len(cl.pod_shape), 0)
+                shapes, _pods_array(arena, cl.pod_shape, cl.pod_creation, cl.pod_uid), len(cl.pod_shape), 0,
+                arena.arr(C.c_uint32, pending) if pending else None, len(pending), 0)
     arena.keep.append(c)
     return c
 

@@ -106,6 +106,7 @@ class ClusterNode:
     catalog: int
     instance_type: int
     pods: List[int] = field(default_factory=list)   # indices into Cluster.pod_*
+    deleting: bool = False                           # MarkedForDeletion: its pods join every simulation
 
 
 @dataclass
@@ -119,6 +120,7 @@ class Cluster:
     pod_uid: np.ndarray
     candidates: List[int] = field(default_factory=list)  # disruption-cost order
     name: str = ""
+    pending: List[int] = field(default_factory=list)  # provisionable pods bound to no node (indices into pod_*)
 
 
 @dataclass

@@ -667,3 +667,37 @@ def distinct_queries(catalog, n, seed=8):
         seen.add(key)
         out.append((reqs, res))
     return out
+
+
+def with_disruption_state(cluster, seed, n_deleting=3, n_pending=6, cpu_limit_m=None):
+    """A copy of a consolidation cluster with the rest of SimulateScheduling's inputs: n_deleting nodes marked for
+    deletion (dropped from the candidates; their pods join every simulation), n_pending provisionable pods bound to
+    no node (shapes of the cluster, a quarter of them oversized so they cannot schedule), and optionally a remaining
+    cpu limit on every NodePool (kp_nodepool limits are remaining limits)."""
+    import copy
+    rng = np.random.default_rng(seed)
+    cl = copy.deepcopy(cluster)
+    order = rng.permutation(len(cl.nodes))[:n_deleting]
+    for i in order:
+        cl.nodes[int(i)].deleting = True
+    dele = {int(i) for i in order}
+    cl.candidates = [c for c in cl.candidates if c not in dele]
+    n0 = len(cl.pod_shape)
+    shapes = list(cl.shapes)
+    new_shape = []
+    for j in range(n_pending):
+        if j % 4 == 3:  # fits no node and no instance type: a pending pod whose error must not block the decision
+            shapes.append(PodShape(req_res(10_000_000, 64)))
+            new_shape.append(len(shapes) - 1)
+        else:
+            new_shape.append(int(rng.integers(0, len(cluster.shapes))))
+    cl.shapes = shapes
+    cl.pod_shape = np.concatenate([cl.pod_shape, np.asarray(new_shape, dtype=cl.pod_shape.dtype)])
+    cl.pod_creation = np.concatenate([cl.pod_creation, (1_750_000_000 + rng.integers(0, 600, size=n_pending)).astype(np.int64)])
+    cl.pod_uid = np.concatenate([cl.pod_uid, rng.integers(0, np.iinfo(np.int64).max, size=n_pending, dtype=np.int64).astype(np.uint64)])
+    cl.pending = list(range(n0, n0 + n_pending))
+    if cpu_limit_m is not None:
+        for np_ in cl.nodepools:
+            np_.limits = {"cpu": int(cpu_limit_m)}
+    cl.name = f"{cluster.name}+disruption-state"
+    return cl

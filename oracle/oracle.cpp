@@ -1548,18 +1548,36 @@ int32_t kpo_simulate_batch(const kp_cluster* cl, const uint32_t* offsets, const 
     kp_sim_result& r = out[s];
     memset(&r, 0, sizeof r);
     std::vector<uint32_t> cand(nodes + offsets[s], nodes + offsets[s + 1]);
-    for (uint32_t c : cand) inS[c] = 1;
-    // SimulateScheduling: pods of the candidates, every other (active) node as an existing node
+    for (uint32_t c : cand) {
+      if (cl->nodes[c].deleting) return KP_E_INVAL;  // candidates never include nodes already being deleted
+      inS[c] = 1;
+    }
+    // SimulateScheduling: the pending pods, the pods of the deleting nodes and of the candidates; every node that
+    // is neither a candidate nor deleting is an existing node. kind: 0 candidate pod, 1 deleting-node pod, 2 pending
     std::vector<kp_existing_node> ex;
     std::vector<uint32_t> exIdx;
     for (uint32_t i = 0; i < cl->n_nodes; i++)
-      if (!inS[i]) {
+      if (!inS[i] && !cl->nodes[i].deleting) {
         ex.push_back(cl->nodes[i].node);
         exIdx.push_back(i);
       }
     std::vector<kp_pod> pods;
+    std::vector<int> kind;
+    for (uint32_t j = 0; j < cl->n_pending; j++) {
+      pods.push_back(cl->pods[cl->pending_pods[j]]);
+      kind.push_back(2);
+    }
+    for (uint32_t i = 0; i < cl->n_nodes; i++)
+      if (cl->nodes[i].deleting)
+        for (uint32_t j = 0; j < cl->nodes[i].n_pods; j++) {
+          pods.push_back(cl->pods[cl->nodes[i].pods[j]]);
+          kind.push_back(1);
+        }
     for (uint32_t c : cand)
-      for (uint32_t j = 0; j < cl->nodes[c].n_pods; j++) pods.push_back(cl->pods[cl->nodes[c].pods[j]]);
+      for (uint32_t j = 0; j < cl->nodes[c].n_pods; j++) {
+        pods.push_back(cl->pods[cl->nodes[c].pods[j]]);
+        kind.push_back(0);
+      }
     for (uint32_t c : cand) inS[c] = 0;
     r.n_pods = (uint32_t)pods.size();
     kp_solve_in in;
@@ -1580,11 +1598,14 @@ int32_t kpo_simulate_batch(const kp_cluster* cl, const uint32_t* offsets, const 
     if (rc) return rc;
     std::unique_ptr<kpo_result> guard(res);
     attempts += res->stats.attempts;
-    // every pod scheduled, and not onto an uninitialized node (SimulateScheduling's UninitializedNodeError)
+    // AllNonPendingPodsScheduled: every pod that was not pending scheduled; a candidate pod on an uninitialized
+    // node is SimulateScheduling's UninitializedNodeError (pods of deleting nodes are exempt)
     bool all = true;
-    for (int32_t pl : res->placement) {
+    for (size_t p = 0; p < res->placement.size(); p++) {
+      const int32_t pl = res->placement[p];
+      if (kind[p] == 2) continue;
       if (pl == -1) all = false;
-      else if (pl <= -2 && !ex[(size_t)(-2 - pl)].initialized) all = false;
+      else if (kind[p] == 0 && pl <= -2 && !ex[(size_t)(-2 - pl)].initialized) all = false;
     }
     double candPrice = 0;
     bool priced = true;

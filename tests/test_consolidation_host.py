@@ -57,6 +57,61 @@ def test_replace_both_with_cheaper(catalog):
     assert 1 <= r["n_options"] <= 100
 
 
+def _with_pending(cl, requests):
+    """Append one provisionable pod bound to no node (a new shape with these requests)."""
+    from kpamd import synth
+    from kpamd.model import PodShape
+    cl.shapes = list(cl.shapes) + [PodShape(synth.req_res(*requests))]
+    cl.pod_shape = np.append(cl.pod_shape, np.uint32(len(cl.shapes) - 1))
+    cl.pod_creation = np.append(cl.pod_creation, np.int64(1_750_000_100))
+    cl.pod_uid = np.append(cl.pod_uid, np.uint64(len(cl.pod_uid)))
+    cl.pending = list(cl.pending) + [len(cl.pod_shape) - 1]
+    return cl
+
+
+def test_pending_pod_error_does_not_block(catalog):
+    """A pending pod that fits nowhere joins the simulation, but only non-pending pods must schedule
+    (AllNonPendingPodsScheduled): the delete stands, and the simulation counts both pods."""
+    from oracle import pyoracle
+    cl = _with_pending(_mini_cluster(catalog), (10_000_000, 64))
+    (r,), _ = pyoracle.simulate_batch(cl, [[0]], multi_node=False)
+    assert r["decision"] == 1 and r["n_pods"] == 2
+
+
+def test_pending_pod_needing_a_nodeclaim(catalog):
+    """A pending pod that needs a new NodeClaim makes the result carry one: no longer a delete."""
+    from oracle import pyoracle
+    cl = _mini_cluster(catalog)
+    (r0,), _ = pyoracle.simulate_batch(cl, [[0]], multi_node=False)
+    assert r0["decision"] == 1
+    cl = _with_pending(cl, (7_000, 1024))  # larger than node B's room
+    (r,), _ = pyoracle.simulate_batch(cl, [[0]], multi_node=False)
+    assert r["decision"] != 1 and r["n_pods"] == 2
+
+
+def test_deleting_node_pods_join(catalog):
+    """A node marked for deletion is no destination and its pods reschedule in every simulation; a subset naming
+    it is an error."""
+    from oracle import pyoracle
+    cl = _mini_cluster(catalog, b_pods=2)
+    cl.nodes[1].deleting = True  # B: its two pods join, and A's pod has nowhere left but a new NodeClaim
+    (r,), _ = pyoracle.simulate_batch(cl, [[0]], multi_node=False)
+    assert r["n_pods"] == 3 and r["decision"] != 1
+    with pytest.raises(RuntimeError):
+        pyoracle.simulate_batch(cl, [[1]], multi_node=False)
+
+
+def test_nodepool_limits_in_simulation(catalog):
+    """kp_nodepool limits are the remaining limits: with no cpu left the replacement NodeClaim cannot be created."""
+    from oracle import pyoracle
+    cl = _mini_cluster(catalog)
+    (r,), _ = pyoracle.simulate_batch(cl, [[0, 1]], multi_node=True)
+    assert r["decision"] == 2
+    cl.nodepools[0].limits = {"cpu": 0}
+    (r,), _ = pyoracle.simulate_batch(cl, [[0, 1]], multi_node=True)
+    assert r["decision"] == 0
+
+
 def test_first_n_replay():
     from kpamd.disruption import DELETE, NOOP, REPLACE, MultiNodeConsolidation as M
     n = 40

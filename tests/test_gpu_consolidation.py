@@ -125,3 +125,26 @@ def test_consolidate_argmin_device(ctx, catalog):
     oracle = kpamd.choice_dict(kpamd.choice_reduce([disruption.local_choice(want, 1000)]))
     assert ch == oracle
     assert empty["subset"] == -1 and empty["counts"] == [0, 0, 0]
+
+
+@pytest.mark.parametrize("limit", [None, 16000, 4000])
+def test_disruption_state_config4(ctx, catalog, limit):
+    """Deleting nodes, pending pods (some unschedulable) and remaining NodePool limits (SimulateScheduling's
+    other inputs) on a near-capacity config-4 cluster: device == oracle."""
+    from kpamd import synth
+    base = synth.config4(catalog, n_nodes=120, seed=4, loose=0.05)
+    cl = synth.with_disruption_state(base, 7, cpu_limit_m=limit)
+    subs = [[c for c in s if not cl.nodes[c].deleting] for s in synth.consolidation_subsets(base, 30, seed=5)]
+    got = check(ctx, cl, [s for s in subs if s])
+    assert {r["n_pods"] for r in got} != {0}
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_disruption_state_random(ctx, catalog, seed):
+    from kpamd import synth
+    base = synth.random_cluster(catalog, 100 + seed, n_nodes=40)
+    cl = synth.with_disruption_state(base, seed, n_deleting=2, n_pending=4, cpu_limit_m=[None, 8000][seed % 2])
+    subs = synth.consolidation_subsets(cl, 20, seed=seed, max_size=min(20, len(cl.candidates)))
+    subs += [[c] for c in cl.candidates[:10]]
+    check(ctx, cl, subs, multi_node=bool(seed % 2))
+
