@@ -291,6 +291,7 @@ struct SimArgs {
   int8_t ru_res[KP_NRES];            // resource of overlay column u
   int32_t max_types;
   int32_t multi_node;
+  int32_t spot_to_spot;              // SpotToSpotConsolidation feature gate
   int32_t wave_lds;                  // dynamic LDS bytes per wave (bitmaps + pod queue / option sort)
   // batch
   int32_t n_subsets;

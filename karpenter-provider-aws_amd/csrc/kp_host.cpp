@@ -3041,7 +3041,6 @@ extern "C" {
 int32_t kp_cluster_prepare(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan** out) {
   auto t0 = std::chrono::steady_clock::now();
   if (!ctx || !cl || !out) return fail(KP_E_INVAL, "null argument");
-  if (cl->spot_to_spot) return fail(KP_E_UNSUPPORTED, "SpotToSpotConsolidation feature gate");
   if (cl->n_nodes && !cl->nodes) return fail(KP_E_INVAL, "null nodes");
   for (uint32_t i = 0; i < cl->n_shapes; i++)
     if (cl->shapes[i].n_topology_spread)
@@ -3319,6 +3318,7 @@ int32_t kp_cluster_prepare(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan** 
   for (int r = 0; r < KP_NRES; r++)
     if ((a.req_res_mask >> r) & 1) a.ru_res[a.RU++] = (int8_t)r;
   a.max_types = 100;
+  a.spot_to_spot = cl->spot_to_spot ? 1 : 0;
   (void)TW;
   plan->T2 = 1;
   while (plan->T2 < std::max(T, 1)) plan->T2 <<= 1;

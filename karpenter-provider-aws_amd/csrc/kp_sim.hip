@@ -542,7 +542,10 @@ __global__ __launch_bounds__(NW * 64) void sim_kernel(SimArgs a) {
         bool ncSpot;
         if (a.spot_bit >= 0) ncSpot = !ctp || bit_of(allowed, a.spot_bit);
         else ncSpot = !ctp || ((rv.compl_ >> a.ct_key) & 1);
-        if (!(allSpot && ncSpot)) {  // spot-to-spot needs the (off) feature gate
+        // spot-to-spot (every candidate spot, the replacement may launch spot): only with the feature gate, on
+        // the replacement narrowed to spot offerings, and a single candidate needs 15 cheaper options
+        const bool s2s = allSpot && ncSpot;
+        if (!s2s || a.spot_to_spot) {
           // TruncateInstanceTypes: OrderByPrice (cheapest compatible offering, then name) + cut
           const uint64_t Xl = lane < D.TW ? nc->X[lane] : 0;
           int cnt = 0;
@@ -600,7 +603,7 @@ __global__ __launch_bounds__(NW * 64) void sim_kernel(SimArgs a) {
             if (q >= lim) continue;
             const int t = (int)(fidx[q] & 4095u);
             tt[h] = t;
-            for (int pass = 0; pass < 2; pass++) {  // capacity-type precedence: spot, on-demand
+            for (int pass = 0; pass < (s2s ? 1 : 2); pass++) {  // capacity-type precedence: spot, on-demand
               const int ctb = pass == 0 ? a.spot_bit : a.od_bit;
               if (ctb < 0) continue;
               bool any = false;
@@ -649,6 +652,18 @@ __global__ __launch_bounds__(NW * 64) void sim_kernel(SimArgs a) {
             }
             if (count == 0) ok = false;
             n_options = count;
+          }
+          if (ok && s2s && ns == 1) {  // MinInstanceTypesForSpotToSpotConsolidation, then the launch keeps 15
+            if (n_options < 15) {
+              ok = false;
+            } else {  // the first 15 (100 with minValues) kept options in price order
+              const int L = hmin ? 100 : 15;
+              const uint64_t lt = (1ull << lane) - 1;
+              const uint64_t b0 = __ballot(keep[0]), b1 = __ballot(keep[1]);
+              keep[0] = keep[0] && __popcll(b0 & lt) < L;
+              keep[1] = keep[1] && __popcll(b0) + __popcll(b1 & lt) < L;
+              n_options = min(n_options, L);
+            }
           }
           if (ok) {
             double b = __DBL_MAX__;

@@ -429,7 +429,8 @@ def build_cluster(arena, cl, catalog_handles=None):
     shapes = arena.arr(PodShape, [arena.shape(s) for s in cl.shapes])
     pending = list(cl.pending)
     c = Cluster(handles, descs, len(cl.catalogs), len(cl.nodepools), nps, nodes_a, len(cl.nodes), len(cl.shapes),
-                shapes, _pods_array(arena, cl.pod_shape, cl.pod_creation, cl.pod_uid), len(cl.pod_shape), 0,
+                shapes, _pods_array(arena, cl.pod_shape, cl.pod_creation, cl.pod_uid), len(cl.pod_shape),
+                1 if cl.spot_to_spot else 0,
                 arena.arr(C.c_uint32, pending) if pending else None, len(pending), 0)
     arena.keep.append(c)
     return c

@@ -121,6 +121,7 @@ class Cluster:
     candidates: List[int] = field(default_factory=list)  # disruption-cost order
     name: str = ""
     pending: List[int] = field(default_factory=list)  # provisionable pods bound to no node (indices into pod_*)
+    spot_to_spot: bool = False                         # SpotToSpotConsolidation feature gate
 
 
 @dataclass

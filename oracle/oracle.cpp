@@ -1515,8 +1515,9 @@ static bool CandidatePrice(const InstanceType& it, const Requirements& labels, d
 }
 // Offerings.Available().WorstLaunchPrice(reqs): capacity types in precedence reserved, spot, on-demand;
 // the most expensive compatible available offering of the first capacity type that has one.
-static double WorstLaunchPrice(const InstanceType& it, const Requirements& reqs) {
+static double WorstLaunchPrice(const InstanceType& it, const Requirements& reqs, bool spot_only = false) {
   for (const char* ct : {"reserved", "spot", "on-demand"}) {
+    if (spot_only && std::string(ct) != "spot") continue;  // requirements narrowed to capacity-type In {spot}
     bool any = false;
     double mx = 0;
     for (auto& o : it.offerings) {
@@ -1535,7 +1536,6 @@ int32_t kpo_simulate_batch(const kp_cluster* cl, const uint32_t* offsets, const 
                            int32_t multi_node, kp_sim_result* out, kp_solve_stats* stats) {
   auto t0 = std::chrono::steady_clock::now();
   if (!cl || !offsets || !out || (!cl->catalog_descs && cl->n_catalogs)) return KP_E_INVAL;
-  if (cl->spot_to_spot) return KP_E_UNSUPPORTED;
   for (uint32_t i = 0; i < cl->n_shapes; i++)
     if (cl->shapes[i].n_topology_spread) return KP_E_UNSUPPORTED;  // cluster pods are not in kp_cluster as bound pods
   Catalogs cats;
@@ -1632,10 +1632,15 @@ int32_t kpo_simulate_batch(const kp_cluster* cl, const uint32_t* offsets, const 
     }
     auto ctr = nc.reqs.find(kLabelCapacityType);
     const bool ncSpot = ctr == nc.reqs.end() || Has(ctr->second, "spot");
-    if (allSpot && ncSpot) continue;  // spot-to-spot consolidation: feature gate off
+    // spot-to-spot consolidation (every candidate spot, the replacement may launch spot): only with the feature
+    // gate; the replacement's requirements are narrowed to capacity-type In {spot} (its options keep only spot
+    // offerings), and a single candidate needs MinInstanceTypesForSpotToSpotConsolidation = 15 cheaper options,
+    // after which the launch keeps the cheapest 15 (100 with minValues) — disruption.md:110-128
+    const bool s2s = allSpot && ncSpot;
+    if (s2s && !cl->spot_to_spot) continue;
     std::vector<int> kept;
     for (uint32_t t : nc.options)
-      if (WorstLaunchPrice(cat[t], nc.reqs) < candPrice) kept.push_back((int)t);
+      if (WorstLaunchPrice(cat[t], nc.reqs, s2s) < candPrice) kept.push_back((int)t);
     if (HasMinValues(nc.reqs) && !SatisfiesMinValues(cat, kept, nc.reqs)) continue;
     if (kept.empty()) continue;
     if (multi_node) {  // filterOutSameType
@@ -1655,13 +1660,17 @@ int32_t kpo_simulate_batch(const kp_cluster* cl, const uint32_t* offsets, const 
       }
       std::vector<int> k2;
       for (int t : kept)
-        if (WorstLaunchPrice(cat[t], nc.reqs) < maxPrice) k2.push_back(t);
+        if (WorstLaunchPrice(cat[t], nc.reqs, s2s) < maxPrice) k2.push_back(t);
       if (HasMinValues(nc.reqs) && !SatisfiesMinValues(cat, k2, nc.reqs)) continue;
       kept.swap(k2);
       if (kept.empty()) continue;
     }
+    if (s2s && cand.size() == 1) {
+      if (kept.size() < 15) continue;
+      kept.resize(std::min<size_t>(kept.size(), HasMinValues(nc.reqs) ? 100 : 15));  // kept is in price order
+    }
     double best = std::numeric_limits<double>::max();
-    for (int t : kept) best = std::min(best, WorstLaunchPrice(cat[t], nc.reqs));
+    for (int t : kept) best = std::min(best, WorstLaunchPrice(cat[t], nc.reqs, s2s));
     r.decision = KP_DECISION_REPLACE;
     r.replacement_nodepool = nc.nodepool;
     r.replacement_price = best;

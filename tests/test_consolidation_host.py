@@ -112,6 +112,36 @@ def test_nodepool_limits_in_simulation(catalog):
     assert r["decision"] == 0
 
 
+def _spot_cluster(catalog):
+    """One spot m5.2xlarge running one 500m pod and no other node: removing it needs a replacement; the pool
+    allows spot and on-demand."""
+    from kpamd import synth
+    from kpamd.model import Cluster, ClusterNode, ExistingNode, NodePool, PodShape
+    names = [it.name for it in catalog]
+    shapes = [PodShape(synth.req_res(500, 512))]
+    pool = NodePool("default", 0, 0, [("karpenter.sh/capacity-type", "In", ["on-demand", "spot"]),
+                                      (synth.K + "instance-category", "In", ["c", "m", "r"])])
+    it = catalog[names.index("m5.2xlarge")]
+    labels = synth.node_labels(it, 0, "spot", "default", "n0")
+    alloc = it.allocatable()
+    avail = {r: alloc[r] - u for r, u in (("cpu", 500), ("memory", 512 * synth.MI * 1000), ("pods", 1000))}
+    nodes = [ClusterNode(ExistingNode("n0", labels, avail, {}, [], True), 0, names.index("m5.2xlarge"), [0])]
+    return Cluster([catalog], [pool], nodes, shapes, np.zeros(1, dtype=np.uint32),
+                   np.full(1, 1_750_000_000, dtype=np.int64), np.arange(1, dtype=np.uint64), candidates=[0])
+
+
+def test_spot_to_spot_gate(catalog):
+    """All-spot candidates with a spot-capable replacement: no-op with the SpotToSpotConsolidation gate off;
+    with it on, a replacement among >= 15 cheaper spot options, and the launch keeps 15 (disruption.md:110-128)."""
+    from oracle import pyoracle
+    cl = _spot_cluster(catalog)
+    (r,), _ = pyoracle.simulate_batch(cl, [[0]], multi_node=False)
+    assert r["decision"] == 0
+    cl.spot_to_spot = True
+    (r,), _ = pyoracle.simulate_batch(cl, [[0]], multi_node=False)
+    assert r["decision"] == 2 and r["n_options"] == 15 and 0 < r["replacement_price"] < r["candidate_price"]
+
+
 def test_first_n_replay():
     from kpamd.disruption import DELETE, NOOP, REPLACE, MultiNodeConsolidation as M
     n = 40

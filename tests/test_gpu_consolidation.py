@@ -148,3 +148,32 @@ def test_disruption_state_random(ctx, catalog, seed):
     subs += [[c] for c in cl.candidates[:10]]
     check(ctx, cl, subs, multi_node=bool(seed % 2))
 
+
+@pytest.mark.parametrize("seed", range(4))
+def test_spot_to_spot_random(ctx, catalog, seed):
+    """SpotToSpotConsolidation gate on: randomized clusters (30 % spot nodes), single- and multi-node, device ==
+    oracle."""
+    from kpamd import synth
+    cl = synth.random_cluster(catalog, 200 + seed, n_nodes=40)
+    cl.spot_to_spot = True
+    spot = [c for c in cl.candidates if dict(cl.nodes[c].node.labels).get("karpenter.sh/capacity-type") == "spot"]
+    subs = [[c] for c in spot[:15]] + [spot[i:i + 3] for i in range(0, max(0, len(spot) - 2), 2)]
+    subs += synth.consolidation_subsets(cl, 10, seed=seed, max_size=min(10, len(cl.candidates)))
+    check(ctx, cl, [s for s in subs if s], multi_node=bool(seed % 2))
+
+
+@pytest.mark.parametrize("multi_node", [False, True])
+def test_spot_to_spot_config4(ctx, catalog, multi_node):
+    """Near-capacity config-4 cluster, gate on, spot-only candidate subsets (single nodes and triples): spot-to-spot
+    replacements occur (15 options for a single node, all cheaper spot options for several) and device == oracle."""
+    from kpamd import synth
+    cl = synth.config4(catalog, n_nodes=200, seed=11)
+    cl.spot_to_spot = True
+    spot = [c for c in cl.candidates if dict(cl.nodes[c].node.labels).get("karpenter.sh/capacity-type") == "spot"]
+    rng = np.random.default_rng(1)
+    subs = [[c] for c in spot[:30]]
+    subs += [sorted(rng.choice(spot, 3, replace=False).tolist(), key=cl.candidates.index) for _ in range(20)]
+    got = check(ctx, cl, subs, multi_node=multi_node)
+    repl = [r for r in got if r["decision"] == 2]
+    assert repl and any(r["n_options"] == 15 for r in repl)
+
