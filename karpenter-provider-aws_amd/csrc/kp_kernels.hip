@@ -1266,6 +1266,9 @@ __shared__ CatHdr g_hdr[8];                      // catalogue descriptors 0..7
 __shared__ int32_t fl_fitj[KP_NRES];             // the fast lane's per-wave scratch (wave 0)
 __shared__ RowPtr fl_rl[RL_CAP];
 __shared__ CatHdr fl_hdrw;
+__shared__ KReqs fl_B;                           // the popped pod's requirements (staged on its first merge)
+__shared__ WaveSlots fl_slots;
+__shared__ uint32_t fl_scratch[2 * KP_MAX_WORDS];
 struct FastState {
   int32_t qw_head, qw_n, qw_next, reserved_;
   int32_t qw_pod[64], qw_shape[64], qw_sl[64], qw_lastlen[64], qw_epoch[64];  // lane i: queue entry qw_head + i
@@ -1463,6 +1466,7 @@ if (A->timing) {                                            \
       // addToInflightNode: pre-checks 64 positions at a time, then the append-path attempts in order. A long scan
       // is the full path's (512-lane pre-pass).
       int placed = -1, wpos = -1, why = FB_NONE;
+      bool b_staged = false;
       bool bail = n_nc - start > FAST_SCAN_MAX;
       if (bail) why = FB_SCAN;
       if (lane == 0 && !bail) starts += start;
@@ -1512,11 +1516,7 @@ if (A->timing) {                                            \
         while (cm) {
           const int l = __builtin_ctzll(cm);
           cm &= cm - 1;
-          if (!((tm >> l) & 1)) {  // needs the merge: the full path evaluates it
-            bail = true;
-            why = FB_MERGE;
-            break;
-          }
+          const bool tagged = (tm >> l) & 1;  // the NodeClaim already carries this shape-level (append path)
           const int ncx = __builtin_amdgcn_readlane(nc, l);
           const int32_t verx = __builtin_amdgcn_readlane(ver, l);  // NodeClaim's version (no reload after stores)
           attempts++;
@@ -1532,20 +1532,49 @@ if (A->timing) {                                            \
             rq_lane = lane < KP_NRES ? A->nc_requests[(size_t)ncx * KP_NRES + lane] : 0;
             j0_lane = lane < KP_NRES ? A->nc_fitj[(size_t)ncx * KP_NRES + lane] : 0;
           }
-          if (hm) {  // minValues on the NodeClaim: the full path re-filters it
-            bail = true;
-            why = FB_MINVALUES;
-            break;
-          }
           FTF(10);
           const int64_t q_lane = rq_lane + preq_lane;
-          const uint64_t X = n_rr <= 4 ? fits_lean(D, hdr(cat), X0, q_lane, j0_lane, (const int64_t LDS*)g_fitv, rr_list,
-                                                   n_rr, bytes, (int32_t LDS*)fl_fitj)
-                                       : fits_filter(D, hdr(cat), X0, q_lane, j0_lane, (const int64_t LDS*)g_fitv,
-                                                     A->req_res_mask, (RowPtr LDS*)fl_rl, &bytes, fl_fitj);
-          bytes += (uint64_t)D.TW * 8 + KP_NRES * 8 + 8;
+          // append path (merged before, no minValues): Fits over the remaining types; otherwise NodeClaim.Add in
+          // full, as the full path's attempt: Compatible + Add of the requirements, then the type filter
+          const bool full_add = !tagged || hm;
+          uint64_t X = 0, m_v = 0;
+          ReqView rv;
+          if (!full_add) {
+            X = n_rr <= 4 ? fits_lean(D, hdr(cat), X0, q_lane, j0_lane, (const int64_t LDS*)g_fitv, rr_list, n_rr, bytes,
+                                      (int32_t LDS*)fl_fitj)
+                          : fits_filter(D, hdr(cat), X0, q_lane, j0_lane, (const int64_t LDS*)g_fitv, A->req_res_mask,
+                                        (RowPtr LDS*)fl_rl, &bytes, fl_fitj);
+            bytes += (uint64_t)D.TW * 8 + KP_NRES * 8 + 8;
+          } else {
+            if (!b_staged) {  // the pod's requirement set, once per pod
+              constexpr int NQ = (int)(sizeof(KReqs) / 8);
+              const uint64_t* src = reinterpret_cast<const uint64_t*>(A->shape_reqs + (size_t)sl * sizeof(KReqs));
+              uint64_t* dstB = reinterpret_cast<uint64_t*>(&fl_B);
+              for (int i = lane; i < NQ; i += 64) dstB[i] = src[i];
+              wave_sync();
+              b_staged = true;
+            }
+            const CandReq crx = load_cand(D, kreq_at(A->nc_reqs, ncx));
+            const VInt vig = vint_global(A->vint);
+            bool mok = merge_compatible(D, crx, (const KReqs*)&fl_B, A->shape_negop[sl], true, m_v, rv,
+                                        (WaveSlots*)&fl_slots, vig);
+            bytes += sizeof(KReqs);
+            if (mok) {
+              const int pb = A->pvp_base[sl * A->n_catalogs + cat];
+              const uint64_t* pvp = A->shape_pvp + (size_t)pb * D.TW;
+              X = filter_types(D, hdr(cat), rv, m_v, X0, fl_B.present, pvp, A->pvp_slot + (size_t)sl * KP_MAX_KEYS,
+                               q_lane, j0_lane, (const int64_t LDS*)g_fitv, A->req_res_mask, vig, (uint32_t*)fl_scratch,
+                               (RowPtr LDS*)fl_rl, &bytes, fl_fitj);
+              bytes += (uint64_t)D.TW * 8 + KP_NRES * 8;
+            }
+          }
           FTF(11);
           if (__ballot(X != 0)) {
+            if (full_add) {
+              store_merged(reinterpret_cast<KReqs*>(A->nc_reqs + (size_t)ncx * sizeof(KReqs)), rv, m_v, D.W, D.KB);
+              if (TOPO && A->n_tk) store_tcodes(A->n_tk, A->tk_keys, A->nc_tcode, A->hnc_stride, rv, m_v, ncx);
+              if (lane == 0 && ncx < A->ncc) A->nc_fail[(size_t)sl * A->ncc + ncx] = NC_MERGED;
+            }
             if (lane < D.TW) A->nc_X[(size_t)ncx * D.TW + lane] = X;
             if (lane < KP_NRES) {
               A->nc_requests[(size_t)ncx * KP_NRES + lane] = q_lane;
