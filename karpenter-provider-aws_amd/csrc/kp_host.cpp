@@ -3206,29 +3206,6 @@ int32_t kp_cluster_prepare(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan** 
   const size_t o_excode = blob.put(ex_code);
   const size_t o_exts = blob.put(C.ex_taintset);
   const size_t o_exav = blob.put(C.ex_available);
-  // topology (read-only part)
-  const size_t o_tgk = blob.put(C.tg_key), o_tgr = blob.put(C.tg_row), o_tgs = blob.put(C.tg_maxskew),
-               o_tgm = blob.put(C.tg_mindom), o_tga = blob.put(C.tg_aff), o_tgtb = blob.put(C.tg_term_base),
-               o_tgft = blob.put(C.tg_filt_tol), o_tgt = blob.put(C.tg_terms), o_tgtn = blob.put(C.tg_terms_negop),
-               o_srb = blob.put(C.shape_rec_base), o_srn = blob.put(C.shape_rec_n), o_recl = blob.put(C.rec_list),
-               o_slob = blob.put(C.sl_own_base), o_slon = blob.put(C.sl_own_n), o_owng = blob.put(C.own_group),
-               o_owns = blob.put(C.own_self), o_ownp = blob.put(C.own_pd), o_sltk = blob.put(C.sl_topo_keys),
-               o_tks = blob.put(C.tkey_slot), o_extc = blob.put(C.ex_tcode), o_tkk = blob.put(C.tk_keys);
-  uint32_t rmask = 0;
-  for (size_t i = 0; i < C.shape_requests.size(); i++)
-    if (C.shape_requests[i] > 0) rmask |= 1u << (i % KP_NRES);
-  for (size_t i = 0; i < C.B->tmpl_daemon.size(); i++)
-    if (C.B->tmpl_daemon[i] > 0) rmask |= 1u << (i % KP_NRES);
-  vector<uint8_t> ex_static(std::max(E, 1), 0);  // unrequested resources of an existing node never change
-  for (int e = 0; e < E; e++) {
-    bool ok = true;
-    for (int r = 0; r < KP_NRES; r++) {
-      const int64_t av = C.ex_available[(size_t)e * KP_NRES + r], rq = C.ex_requests[(size_t)e * KP_NRES + r];
-      if (av < 0 || (!((rmask >> r) & 1) && rq > av)) ok = false;
-    }
-    ex_static[e] = ok ? 1 : 0;
-  }
-  const size_t o_exso = blob.put(ex_static);
   const size_t o_exrq = blob.put(C.ex_requests);
   const size_t o_exin = blob.put(ex_init);
   const size_t o_pshape = blob.put(C.pod_shape);
