@@ -823,6 +823,12 @@ template <int NW>
 #define LIST_TAG 0x40000000
 // nc_fail value: the shape-level was merged into the NodeClaim (never equal to a version)
 #define NC_MERGED 0x40000000
+// Failure memo value of a permanent failure. NodeClaim.Add / ExistingNode.CanAdd failures are monotone: the
+// candidate's requirements only narrow (Add intersects), its remaining types only shrink and its requests only
+// grow, so once the pod's shape-level fails (taints, Compatible, the type filter, Fits, minValues) it fails for the
+// rest of the Solve. The one exception is Compatible's undefined-key rule (the pod requires a custom key the
+// candidate does not define yet, and a later merge may define it): such failures keep the candidate's version.
+#define NC_NEVER (-3)
 #define LIST_POS(e) ((e) & (LIST_TAG - 1))
 __device__ __forceinline__ int compact_candidates_x4(uint32_t flags, int pos0, int32_t* s_list, int32_t* s_wcnt,
                                                      uint32_t tags = 0) {
@@ -1488,7 +1494,7 @@ if (A->timing) {                                            \
             const int r = __builtin_ctz(rm);
             fit = fit & (rq[r] + lane_bcast_i64(preq_lane, r) <= mx[r]);
           }
-          cand = fit && fl != ver && ((tolmask >> ts) & 1);
+          cand = fit && fl != ver && fl != NC_NEVER && ((tolmask >> ts) & 1);
           tag = cand && fl >= NC_MERGED;
         }
         // speculative loads of the first position's NodeClaim (the usual winner): they overlap the pre-checks
@@ -1539,6 +1545,7 @@ if (A->timing) {                                            \
           const bool full_add = !tagged || hm;
           uint64_t X = 0, m_v = 0;
           ReqView rv;
+          bool perm = true;  // a failure here is permanent (NC_NEVER) unless it is Compatible's undefined-key rule
           if (!full_add) {
             X = n_rr <= 4 ? fits_lean(D, hdr(cat), X0, q_lane, j0_lane, (const int64_t LDS*)g_fitv, rr_list, n_rr, bytes,
                                       (int32_t LDS*)fl_fitj)
@@ -1556,8 +1563,10 @@ if (A->timing) {                                            \
             }
             const CandReq crx = load_cand(D, kreq_at(A->nc_reqs, ncx));
             const VInt vig = vint_global(A->vint);
-            bool mok = merge_compatible(D, crx, (const KReqs*)&fl_B, A->shape_negop[sl], true, m_v, rv,
+            const uint64_t b_negop = A->shape_negop[sl];
+            bool mok = merge_compatible(D, crx, (const KReqs*)&fl_B, b_negop, true, m_v, rv,
                                         (WaveSlots*)&fl_slots, vig);
+            if (!mok) perm = (fl_B.present & ~crx.P & ~b_negop & ~D.wellknown) == 0;
             bytes += sizeof(KReqs);
             if (mok) {
               const int pb = A->pvp_base[sl * A->n_catalogs + cat];
@@ -1589,7 +1598,7 @@ if (A->timing) {                                            \
             FTF(12);
             break;
           }
-          if (lane == 0 && ncx < A->ncc) A->nc_fail[(size_t)sl * A->ncc + ncx] = verx;
+          if (lane == 0 && ncx < A->ncc) A->nc_fail[(size_t)sl * A->ncc + ncx] = perm ? NC_NEVER : verx;
         }
       }
       wave_sync();
@@ -1881,7 +1890,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
         const int64_t* av = a.ex_available + (size_t)ec * KP_NRES;
         const int64_t* rq = a.ex_requests + (size_t)ec * KP_NRES;
         bool cand = !rmask_all || (rq[rr0] + s_preq[rr0] <= av[rr0] && rq[rr1] + s_preq[rr1] <= av[rr1]);
-        cand = cand && fl != ver && sok && ((tolmask >> ts) & 1);
+        cand = cand && fl != ver && fl != NC_NEVER && sok && ((tolmask >> ts) & 1);
         for (uint32_t rm = rr_rest; rm && cand; rm &= rm - 1) {
           const int r = __builtin_ctz(rm);
           cand = rq[r] + s_preq[r] <= av[r];
@@ -1914,9 +1923,11 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
         if (li < n) {
           ei = s_list[li];
           attempts++;
-          ok = merge_compatible(D, kreq_at(a.ex_reqs, ei), B, b_negop, false, m_v, rv, &slots[wave], vi);
+          const KReqs* er = kreq_at(a.ex_reqs, ei);
+          ok = merge_compatible(D, er, B, b_negop, false, m_v, rv, &slots[wave], vi);
           bytes += sizeof(KReqs);
-          if (!ok && lane == 0) a.ex_fail[(size_t)sl * a.n_existing + ei] = a.ex_ver[ei];
+          if (!ok && lane == 0)  // permanent unless the undefined-key rule failed (no well-known exemption here)
+            a.ex_fail[(size_t)sl * a.n_existing + ei] = (B->present & ~er->present & ~b_negop) == 0 ? NC_NEVER : a.ex_ver[ei];
           if (ok && own_n) ok = topo_narrow(D, own_n, s_town, s_tacc, s_tcnt, false, m_v, rv, vi);  // not memoised
         }
         if (lane == 0) s_ok[wave] = ok ? 1 : 0;
@@ -1976,7 +1987,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
           const int64_t* rq = a.nc_requests + (size_t)nc * KP_NRES;
           const int64_t* mx = a.nc_maxalloc + (size_t)nc * KP_NRES;
           bool cand = !rmask_all || (rq[rr0] + s_preq[rr0] <= mx[rr0] && rq[rr1] + s_preq[rr1] <= mx[rr1]);
-          cand = cand && fl != ver && ((tolmask >> ts) & 1);
+          cand = cand && fl != ver && fl != NC_NEVER && ((tolmask >> ts) & 1);
           for (uint32_t rm = rr_rest; rm && cand; rm &= rm - 1) {
             const int r = __builtin_ctz(rm);
             cand = rq[r] + s_preq[r] <= mx[r];
@@ -2008,7 +2019,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
         for (int r0 = 0, width = NW; r0 < n; r0 += width) {
           width = (s_list[r0] & LIST_TAG) ? 1 : NW;
           const int li = r0 + wave;
-          bool ok = false, fast = false;
+          bool ok = false, fast = false, perm = true;
           uint64_t m_v = 0, X = 0;
           ReqView rv;
           int nc = -1;
@@ -2033,6 +2044,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
               bytes += (uint64_t)D.TW * 8 + KP_NRES * 8 + 8;
             } else {
               ok = merge_compatible(D, cr, B, b_negop, true, m_v, rv, &slots[wave], vi);
+              if (!ok) perm = (B->present & ~cr.P & ~b_negop & ~D.wellknown) == 0;
               bytes += sizeof(KReqs);
             }
             if (tsub && lane == 0) tsub[0] += __builtin_amdgcn_s_memtime() - tm0;
@@ -2048,7 +2060,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
               if (tsub && lane == 0) tsub[5] += 1;  // attempts reaching filter_types (wave 0)
               bytes += (uint64_t)D.TW * 8 + KP_NRES * 8;
             }
-            if (!ok && memo && lane == 0 && nc < a.ncc) a.nc_fail[(size_t)sl * a.ncc + nc] = a.nc_ver[nc];
+            if (!ok && memo && lane == 0 && nc < a.ncc) a.nc_fail[(size_t)sl * a.ncc + nc] = perm ? NC_NEVER : a.nc_ver[nc];
           }
           if (lane == 0 && wave < width) s_ok[wave] = ok ? 1 : 0;
           __syncthreads();
