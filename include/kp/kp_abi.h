@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define KP_ABI_VERSION 5
+#define KP_ABI_VERSION 6
 
 enum kp_status {
   KP_OK = 0,
@@ -212,6 +212,15 @@ typedef struct kp_topology_spread {
   kp_label_selector selector;
 } kp_topology_spread;
 
+/* A container port with hostPort != 0, as upstream scheduling.GetHostPorts reads it (HostPortUsage). Two entries
+ * conflict when protocol and port are equal and either IP is unspecified (0.0.0.0 / ::) or both IPs are equal. */
+enum kp_protocol { KP_PROTO_TCP = 0, KP_PROTO_UDP = 1, KP_PROTO_SCTP = 2 };
+typedef struct kp_host_port {
+  const char* ip;     /* hostIP; NULL or "" = 0.0.0.0 (corev1 default) */
+  int32_t port;       /* hostPort, 1..65535 */
+  int32_t protocol;   /* enum kp_protocol; corev1 default TCP */
+} kp_host_port;
+
 /* A pod "shape": everything the scheduler reads from a pod except its identity. */
 typedef struct kp_pod_shape {
   kp_resource_list requests;                 /* resources.RequestsForPods(pod) */
@@ -228,6 +237,14 @@ typedef struct kp_pod_shape {
   const kp_topology_spread* topology_spread; /* spec.topologySpreadConstraints, in spec order */
   const char* namespace_;                    /* metadata.namespace (topology selectors are namespaced) */
   const kp_label* labels;                    /* metadata.labels (matched by topology selectors) */
+  /* ABI v6 */
+  const kp_host_port* host_ports;            /* GetHostPorts(pod): NodeClaim.Add / ExistingNode.CanAdd conflicts */
+  uint32_t n_host_ports;
+  uint32_t n_volume_requirements;
+  /* VolumeTopology.Inject: the topology requirements of the pod's volumes (PV node affinity / StorageClass
+   * allowedTopologies, resolved by the caller), appended to every required node-affinity term (one term is
+   * created when the pod has none) before scheduling. */
+  const kp_requirement* volume_requirements;
 } kp_pod_shape;
 
 /* A pod already bound to a node of the cluster: what upstream Topology.countDomains lists (through the
@@ -257,6 +274,10 @@ typedef struct kp_existing_node {
   kp_resource_list requests;   /* initial requests: daemonset pods expected but not yet bound */
   int32_t initialized;
   int32_t reserved_;
+  /* ABI v6: HostPortUsage of the pods bound to the node (in a kp_cluster: every bound pod, reschedulable or not) */
+  const kp_host_port* host_ports;
+  uint32_t n_host_ports;
+  uint32_t reserved2_;
 } kp_existing_node;
 
 typedef struct kp_ctx kp_ctx;

@@ -111,6 +111,13 @@ struct SolveArgs {
   int32_t n_req_res;                 // popcount(req_res_mask)
   const int32_t* tkey_slot;          // [64] row of a topology key in ex_tcode
   const uint8_t* ex_tcode;           // [TK][E] value ordinal of the existing node's label (0xFF: none)
+  // host ports (upstream HostPortUsage, one bit per distinct port entry of the batch): a candidate conflicts when
+  // its used bits meet the pod's conflict mask; a placement ORs in the pod's add mask (used bits only grow)
+  int32_t hp_any;                    // some shape or existing node names a host port
+  const uint64_t* shape_hp_conf;     // [S]
+  const uint64_t* shape_hp_add;      // [S]
+  uint64_t* ex_hp;                   // [E] (mutable)
+  uint64_t* nc_hp;                   // [P] set when the NodeClaim is created
   // precomputed template options per (shape-level, template) (tmpl_feas_kernel), or null
   const uint64_t* tfeas;             // [SL][NT] entries of tfeas_words
   int32_t tfeas_words;
@@ -221,6 +228,7 @@ struct SimNC {
   int64_t maxalloc[KP_NRES];
   int32_t fitj[KP_NRES];
   int32_t tmpl, taintset, ver, pad_;
+  uint64_t hp;  // used host-port bits
 };
 
 // kp_sim_result as the device writes it (same layout as the ABI struct)
@@ -265,6 +273,12 @@ struct SimArgs {
   const int64_t* ex_available;       // [E][NRES]
   const int64_t* ex_requests;        // [E][NRES]
   const uint8_t* ex_init;            // [E]
+  // host ports (see SolveArgs): static used bits per node; touched nodes keep theirs in s_ovlhp
+  int32_t hp_any;
+  const uint64_t* shape_hp_conf;     // [S]
+  const uint64_t* shape_hp_add;      // [S]
+  const uint64_t* ex_hp;             // [E]
+  uint64_t* s_ovlhp;                 // [slot][E] (valid where the node is touched)
   // precomputed per shape-level (sim_prep_kernel / sim_usable_kernel)
   uint64_t* usable;                  // [SL][EW] CanAdd on the snapshot: tolerated, compatible, fits
   SimNC* tres;                       // [SL] addToNewNodeClaim outcome (tmpl -1: none)

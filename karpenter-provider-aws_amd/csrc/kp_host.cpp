@@ -7,7 +7,10 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <arpa/inet.h>
+
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -141,6 +144,42 @@ RawReqs LabelReqs(const kp_label* l, uint32_t n, bool drop_hostname) {
     out.push_back({k, KP_OP_IN, {l[i].value ? l[i].value : ""}, -1});
   }
   return out;
+}
+
+// scheduling.GetHostPorts entries in a canonical form: (protocol, port) group + 16-byte IP (IPv4 as ::ffff:a.b.c.d,
+// the form net.ParseIP returns, so IP.Equal of a v4 and its v4-in-v6 spelling holds). Entries with hostPort 0 are
+// skipped, as GetHostPorts skips them; an unparsable IP is KP_E_INVAL (the API server validates hostIP).
+struct HostPortKey {
+  int proto, port;
+  std::array<uint8_t, 16> ip;
+  bool unspec;
+};
+bool ParseHostPorts(const kp_host_port* hp, uint32_t n, vector<HostPortKey>* out, string* err) {
+  for (uint32_t i = 0; i < n; i++) {
+    if (hp[i].port == 0) continue;
+    if (hp[i].port < 0 || hp[i].port > 65535 || hp[i].protocol < KP_PROTO_TCP || hp[i].protocol > KP_PROTO_SCTP) {
+      *err = "host port " + std::to_string(hp[i].port) + "/" + std::to_string(hp[i].protocol);
+      return false;
+    }
+    HostPortKey k;
+    k.proto = hp[i].protocol;
+    k.port = hp[i].port;
+    k.ip.fill(0);
+    const string ip = hp[i].ip && hp[i].ip[0] ? hp[i].ip : "0.0.0.0";
+    uint8_t v4[4];
+    if (inet_pton(AF_INET, ip.c_str(), v4) == 1) {
+      k.ip[10] = k.ip[11] = 0xFF;
+      memcpy(&k.ip[12], v4, 4);
+    } else if (inet_pton(AF_INET6, ip.c_str(), k.ip.data()) != 1) {
+      *err = "host IP '" + ip + "'";
+      return false;
+    }
+    static const uint8_t v4z[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0xFF, 0xFF, 0, 0, 0, 0};
+    static const uint8_t v6z[16] = {0};
+    k.unspec = memcmp(k.ip.data(), v4z, 16) == 0 || memcmp(k.ip.data(), v6z, 16) == 0;
+    out->push_back(k);
+  }
+  return true;
 }
 
 struct HostOffering {
@@ -1081,6 +1120,9 @@ struct Compiled {
   vector<KReqs> ex_reqs;
   vector<int32_t> ex_taintset;
   vector<int64_t> ex_available, ex_requests;
+  // host ports (HostPortUsage): conflict / add masks per shape over the batch's port bits, used bits per node
+  vector<uint64_t> shape_hp_conf, shape_hp_add, ex_hp;
+  bool hp_any = false;
   // pods
   vector<int32_t> pod_shape, queue;
   // topology spread (TopologyTypeSpread groups; see SolveArgs)
@@ -1188,6 +1230,59 @@ std::map<string, string> LabelMap(const kp_label* l, uint32_t n) {
 // device encoding: one group per distinct (key, maxSkew, namespace, selector, node filter, policies) in order
 // of first appearance over the pods; dictionary-key groups keep a count per value ordinal + a registered-
 // domain mask, hostname groups a saturating u8 count per node (existing positions, then NodeClaims).
+// HostPortUsage.Conflicts as bit masks. Bits: U(g) per (protocol, port) group g some unspecified-IP entry names,
+// S(g, ip) per specific entry. An entry (g, unspecified) conflicts with every used bit of g and adds U(g); an
+// entry (g, ip) conflicts with U(g) and S(g, ip) and adds S(g, ip) — HostPort.Matches (same protocol and port, and
+// an unspecified IP on either side or equal IPs). A node's used bits only grow, so a conflict is permanent.
+int32_t EncodeHostPorts(const vector<vector<HostPortKey>>& shapes, const vector<vector<HostPortKey>>& nodes,
+                        Compiled& cp) {
+  std::map<std::pair<int, int>, int> ubit;                               // group -> U bit
+  std::map<std::pair<std::pair<int, int>, std::array<uint8_t, 16>>, int> sbit;  // (group, ip) -> S bit
+  std::map<std::pair<int, int>, uint64_t> gmask;                         // every bit of a group
+  int nb = 0;
+  auto visit = [&](const vector<HostPortKey>& v) {
+    for (auto& k : v) {
+      const auto g = std::make_pair(k.proto, k.port);
+      if (k.unspec) {
+        if (!ubit.count(g)) ubit[g] = nb++;
+      } else if (!sbit.count({g, k.ip})) {
+        sbit[{g, k.ip}] = nb++;
+      }
+    }
+  };
+  for (auto& v : shapes) visit(v);
+  for (auto& v : nodes) visit(v);
+  if (nb > 64) return fail(KP_E_UNSUPPORTED, "%d distinct host port entries (max 64)", nb);
+  for (auto& kv : ubit) gmask[kv.first] |= 1ull << kv.second;
+  for (auto& kv : sbit) gmask[kv.first.first] |= 1ull << kv.second;
+  auto masks = [&](const vector<HostPortKey>& v, uint64_t* conf, uint64_t* add) {
+    *conf = *add = 0;
+    for (auto& k : v) {
+      const auto g = std::make_pair(k.proto, k.port);
+      auto u = ubit.find(g);
+      const uint64_t ub = u == ubit.end() ? 0 : 1ull << u->second;
+      if (k.unspec) {
+        *conf |= gmask[g];
+        *add |= ub;
+      } else {
+        const uint64_t sb = 1ull << sbit[{g, k.ip}];
+        *conf |= ub | sb;
+        *add |= sb;
+      }
+    }
+  };
+  cp.shape_hp_conf.assign(shapes.size(), 0);
+  cp.shape_hp_add.assign(shapes.size(), 0);
+  for (size_t i = 0; i < shapes.size(); i++) masks(shapes[i], &cp.shape_hp_conf[i], &cp.shape_hp_add[i]);
+  cp.ex_hp.assign(nodes.size(), 0);
+  for (size_t i = 0; i < nodes.size(); i++) {
+    uint64_t c;
+    masks(nodes[i], &c, &cp.ex_hp[i]);
+  }
+  cp.hp_any = nb > 0;
+  return KP_OK;
+}
+
 int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector<RawReqs>>& strict_levels,
                         const vector<vector<vector<int>>>& spread_levels, const vector<int>& np_taintset) {
   const Dict& d = cp.B->d;
@@ -1570,6 +1665,12 @@ int32_t ParseSolve(const kp_solve_in* in, SolveRaw& raw) {
     RawReqs ns = LabelReqs(sh.node_selector, sh.n_node_selector, false);
     vector<RawReqs> req;
     for (uint32_t j = 0; j < sh.n_required_terms; j++) req.push_back(ParseReqs(sh.required_terms[j]));
+    if (sh.n_volume_requirements) {  // VolumeTopology.Inject: appended to every required term (one created if none)
+      RawReqs v = ParseReqs(kp_requirements{sh.volume_requirements, sh.n_volume_requirements, 0});
+      if (req.empty()) req.push_back(v);
+      else
+        for (auto& t : req) t.insert(t.end(), v.begin(), v.end());
+    }
     vector<std::pair<int, RawReqs>> pref;
     for (uint32_t j = 0; j < sh.n_preferred_terms; j++)
       pref.push_back({sh.preferred_terms[j].weight, ParseReqs(sh.preferred_terms[j].preference)});
@@ -1826,6 +1927,20 @@ int32_t CompilePerCall(const kp_solve_in* in, const SolveRaw& raw, Compiled& cp)
     }
   }
   if (cp.pvp.empty()) cp.pvp.assign(TW, 0);
+  {  // host ports: shapes, then the existing nodes in upstream order
+    vector<vector<HostPortKey>> hs(in->n_shapes), hn;
+    string err;
+    for (uint32_t s2 = 0; s2 < in->n_shapes; s2++)
+      if (!ParseHostPorts(in->shapes[s2].host_ports, in->shapes[s2].n_host_ports, &hs[s2], &err))
+        return fail(KP_E_INVAL, "shape %u: %s", s2, err.c_str());
+    for (int i : cp.ex_input) {
+      hn.emplace_back();
+      if (!ParseHostPorts(in->existing[i].host_ports, in->existing[i].n_host_ports, &hn.back(), &err))
+        return fail(KP_E_INVAL, "existing node %d: %s", i, err.c_str());
+    }
+    const int32_t hrc = EncodeHostPorts(hs, hn, cp);
+    if (hrc) return hrc;
+  }
   int32_t rc = CompileTopology(in, cp, raw.strict_levels, raw.spread_levels, b.np_taintset);
   if (rc) return rc;
   // pods: Queue order byCPUAndMemoryDescending (cpu desc, memory desc, creation asc, uid asc)
@@ -2068,6 +2183,7 @@ static int32_t SolvePrepare(kp_ctx* ctx, const kp_solve_in* in, kp_comm* comm, k
   const size_t o_tlp = blob.put(C.tmpl_limit_present);
   const size_t o_exts = blob.put(C.ex_taintset);
   const size_t o_exav = blob.put(C.ex_available);
+  const size_t o_shpc = blob.put(C.shape_hp_conf), o_shpa = blob.put(C.shape_hp_add);
   // topology (read-only part)
   const size_t o_tgk = blob.put(C.tg_key), o_tgr = blob.put(C.tg_row), o_tgs = blob.put(C.tg_maxskew),
                o_tgm = blob.put(C.tg_mindom), o_tga = blob.put(C.tg_aff), o_tgtb = blob.put(C.tg_term_base),
@@ -2109,6 +2225,7 @@ static int32_t SolvePrepare(kp_ctx* ctx, const kp_solve_in* in, kp_comm* comm, k
   const size_t o_tgc = blob.put(C.tg_cnt);
   const size_t o_tgreg = blob.put(C.tg_reg);
   const size_t o_hcx = blob.put(C.hcnt0);
+  const size_t o_exhp = blob.put(C.ex_hp);
   const size_t n_mut = blob.host.size() - o_mut;
   const size_t host_bytes = blob.host.size();
   const size_t o_pristine = blob.reserve_dev(n_mut);
@@ -2123,6 +2240,7 @@ static int32_t SolvePrepare(kp_ctx* ctx, const kp_solve_in* in, kp_comm* comm, k
   const size_t o_fitj = blob.reserve_dev(sizeof(int32_t) * (size_t)Pc * KP_NRES);
   const size_t o_ncts = blob.reserve_dev(sizeof(int32_t) * (size_t)Pc);
   const size_t o_nccat = blob.reserve_dev(sizeof(int32_t) * (size_t)Pc);
+  const size_t o_nchp = blob.reserve_dev(C.hp_any ? sizeof(uint64_t) * (size_t)Pc : 8);
   const size_t o_place = blob.reserve_dev(sizeof(int32_t) * Pc);
   const size_t o_events = blob.reserve_dev(sizeof(int32_t) * Pc);
   const size_t o_stats = blob.reserve_dev(sizeof(uint64_t) * KP_SOLVE_STATS);
@@ -2234,6 +2352,11 @@ static int32_t SolvePrepare(kp_ctx* ctx, const kp_solve_in* in, kp_comm* comm, k
   a.nc_fitj = (int32_t*)(base + o_fitj);
   a.nc_taintset = (int32_t*)(base + o_ncts);
   a.nc_cat = (int32_t*)(base + o_nccat);
+  a.hp_any = C.hp_any ? 1 : 0;
+  a.shape_hp_conf = (const uint64_t*)(base + o_shpc);
+  a.shape_hp_add = (const uint64_t*)(base + o_shpa);
+  a.ex_hp = (uint64_t*)(base + o_exhp);
+  a.nc_hp = (uint64_t*)(base + o_nchp);
   a.req_res_mask = 0;
   for (size_t i = 0; i < C.shape_requests.size(); i++)
     if (C.shape_requests[i] > 0) a.req_res_mask |= 1u << (i % KP_NRES);
@@ -3223,6 +3346,7 @@ int32_t kp_cluster_prepare(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan** 
   const size_t o_bexcl = blob.put(base_excl);
   const size_t o_tlp = blob.put(C.tmpl_limit_present);
   const size_t o_trem = blob.put(C.tmpl_remaining);
+  const size_t o_shpc = blob.put(C.shape_hp_conf), o_shpa = blob.put(C.shape_hp_add), o_exhp = blob.put(C.ex_hp);
   const size_t host_bytes = blob.host.size();
   const size_t o_usable = blob.reserve(sizeof(uint64_t) * (size_t)std::max(SL, 1) * std::max(EW, 1));
   const size_t o_tres = blob.reserve(sizeof(SimNC) * (size_t)std::max(SL, 1));
@@ -3271,6 +3395,10 @@ int32_t kp_cluster_prepare(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan** 
   a.ex_available = (const int64_t*)(base + o_exav);
   a.ex_requests = (const int64_t*)(base + o_exrq);
   a.ex_init = base + o_exin;
+  a.hp_any = C.hp_any ? 1 : 0;
+  a.shape_hp_conf = (const uint64_t*)(base + o_shpc);
+  a.shape_hp_add = (const uint64_t*)(base + o_shpa);
+  a.ex_hp = (const uint64_t*)(base + o_exhp);
   a.usable = (uint64_t*)(base + o_usable);
   a.tres = (SimNC*)(base + o_tres);
   a.pod_shape = (const int32_t*)(base + o_pshape);
@@ -3359,8 +3487,9 @@ static int32_t SimLaunchLocked(kp_cluster_plan* plan, const uint32_t* offsets, c
   const size_t sz_ovl = sizeof(int64_t) * (size_t)slots * std::max(a.E, 1) * std::max(a.RU, 1);
   const size_t sz_nc = sizeof(SimNC) * (size_t)slots;
   const size_t sz_fail = sizeof(int32_t) * (size_t)slots * std::max(a.SL, 1);
+  const size_t sz_ovlhp = a.hp_any ? sizeof(uint64_t) * (size_t)slots * std::max(a.E, 1) : 8;
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-  const size_t need = al(sz_pod) + al(sz_start) + al(sz_ovl) + al(sz_nc) + al(sz_fail) + al(sizeof(uint64_t) * 8);
+  const size_t need = al(sz_pod) + al(sz_start) + al(sz_ovl) + al(sz_nc) + al(sz_fail) + al(sz_ovlhp) + al(sizeof(uint64_t) * 8);
   if (need > plan->scratch_bytes) {
     if (plan->scratch.p) HIPCHK(hipFree(plan->scratch.p));
     plan->scratch.p = nullptr;
@@ -3379,6 +3508,8 @@ static int32_t SimLaunchLocked(kp_cluster_plan* plan, const uint32_t* offsets, c
   o += al(sz_nc);
   a.s_ncfail = (int32_t*)(sb + o);
   o += al(sz_fail);
+  a.s_ovlhp = (uint64_t*)(sb + o);
+  o += al(sz_ovlhp);
   a.stats = (uint64_t*)(sb + o);
   // batch: subsets + results
   const size_t b_off = al(sizeof(uint32_t) * (n_subsets + 1)), b_nodes = al(sizeof(uint32_t) * std::max<uint32_t>(n_flat, 1));

@@ -1408,7 +1408,7 @@ if (A->timing) {                                            \
           ce1 = a_cex_prev_stamp;
         }
       } else {
-        own = U(TOPO ? A->sl_own_n[sl] + A->shape_rec_n[shape] : 0);
+        own = U((TOPO ? A->sl_own_n[sl] + A->shape_rec_n[shape] : 0) + (A->hp_any && A->shape_hp_conf[shape] ? 1 : 0));
         ce0 = U(A->n_existing ? A->cur_ex[2 * sl] : 0), ce1 = U(A->n_existing ? A->cur_ex[2 * sl + 1] : 0);
         preq_lane = lane < KP_NRES ? A->shape_requests[(size_t)shape * KP_NRES + lane] : 0;
         tolmask = U64(A->shape_tolerates[shape]);
@@ -1419,7 +1419,7 @@ if (A->timing) {                                            \
       if (off + 1 < qw_n) {  // the next entry's stage loads: in flight while this pod is sorted and placed
         const int nshape = __builtin_amdgcn_readlane(qw_shape, off + 1);
         const int nsl = __builtin_amdgcn_readlane(qw_sl, off + 1);
-        pf_own = TOPO ? A->sl_own_n[nsl] + A->shape_rec_n[nshape] : 0;
+        pf_own = (TOPO ? A->sl_own_n[nsl] + A->shape_rec_n[nshape] : 0) + (A->hp_any && A->shape_hp_conf[nshape] ? 1 : 0);
         pf_ce0 = A->n_existing ? A->cur_ex[2 * nsl] : 0, pf_ce1 = A->n_existing ? A->cur_ex[2 * nsl + 1] : 0;
         pf_preq = lane < KP_NRES ? A->shape_requests[(size_t)nshape * KP_NRES + lane] : 0;
         pf_tol = A->shape_tolerates[nshape];
@@ -1842,6 +1842,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
     const KReqs* B = &s_B;
     const uint64_t b_negop = a.shape_negop[sl];
     const uint64_t tolmask = a.shape_tolerates[shape];
+    const uint64_t hpc = a.hp_any ? a.shape_hp_conf[shape] : 0, hpa = a.hp_any ? a.shape_hp_add[shape] : 0;
     int placed = -1;  // >= 0 NodeClaim id; <= -2 existing node; -1 not placed
     // ---- topology: stage the owned groups (one wave each) -----------------------------------------
     const int own_n = TOPO ? a.sl_own_n[sl] : 0;
@@ -1891,6 +1892,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
         const int64_t* rq = a.ex_requests + (size_t)ec * KP_NRES;
         bool cand = !rmask_all || (rq[rr0] + s_preq[rr0] <= av[rr0] && rq[rr1] + s_preq[rr1] <= av[rr1]);
         cand = cand && fl != ver && fl != NC_NEVER && sok && ((tolmask >> ts) & 1);
+        if (hpc) cand = cand && !(a.ex_hp[ec] & hpc);  // HostPortUsage.Conflicts (permanent: used bits only grow)
         for (uint32_t rm = rr_rest; rm && cand; rm &= rm - 1) {
           const int r = __builtin_ctz(rm);
           cand = rq[r] + s_preq[r] <= av[r];
@@ -1938,6 +1940,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
             store_merged(reinterpret_cast<KReqs*>(a.ex_reqs + (size_t)ei * sizeof(KReqs)), rv, m_v, D.W, D.KB);
             if (lane < KP_NRES) a.ex_requests[(size_t)ei * KP_NRES + lane] += s_preq[lane];
             if (lane == 0) a.ex_ver[ei] += 1;
+            if (lane == 0 && hpa) a.ex_hp[ei] |= hpa;
           }
           placed = -2 - s_list[r0 + win];
         }
@@ -1988,6 +1991,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
           const int64_t* mx = a.nc_maxalloc + (size_t)nc * KP_NRES;
           bool cand = !rmask_all || (rq[rr0] + s_preq[rr0] <= mx[rr0] && rq[rr1] + s_preq[rr1] <= mx[rr1]);
           cand = cand && fl != ver && fl != NC_NEVER && ((tolmask >> ts) & 1);
+          if (hpc) cand = cand && !(a.nc_hp[nc] & hpc);
           for (uint32_t rm = rr_rest; rm && cand; rm &= rm - 1) {
             const int r = __builtin_ctz(rm);
             cand = rq[r] + s_preq[r] <= mx[r];
@@ -2075,6 +2079,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
               if (lane == 0 && !own_n && nc < a.ncc) a.nc_fail[(size_t)sl * a.ncc + nc] = NC_MERGED;
               if (lane < D.TW) a.nc_X[(size_t)nc * D.TW + lane] = X;
               if (lane < KP_NRES) a.nc_requests[(size_t)nc * KP_NRES + lane] += s_preq[lane];
+              if (lane == 0 && hpa) a.nc_hp[nc] |= hpa;
               if (lane == 0) {
                 if (in_lds) ((LdsI32)(s_dyn + a.sort_cap))[nc] += 1;
                 else ((GlbI32)a.g_npods)[nc] += 1;
@@ -2181,6 +2186,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
                 a.nc_tmpl[nc] = tm;
                 a.nc_taintset[nc] = a.tmpl_taintset[tm];
                 a.nc_cat[nc] = a.tmpl_catalog[tm];
+                if (a.hp_any) a.nc_hp[nc] = hpa;  // a template's HostPortUsage is empty
               }
               if (lane < KP_NRES) a.nc_fitj[(size_t)nc * KP_NRES + lane] = s_fitj[wave][lane];
               if (lane == 0 && !own_n && nc < a.ncc) a.nc_fail[(size_t)sl * a.ncc + nc] = NC_MERGED;

@@ -137,6 +137,7 @@ __global__ __launch_bounds__(SIM_WAVES * 64) void sim_usable_kernel(SimArgs a) {
     const int e = w * 64 + lane;
     bool ok = e < a.E;
     if (ok) ok = (tol >> a.ex_taintset[e]) & 1;
+    if (ok && a.hp_any) ok = !(a.ex_hp[e] & a.shape_hp_conf[shape]);  // HostPortUsage.Conflicts
     for (int r = 0; r < KP_NRES && ok; r++) {  // Fits(Merge(requests, pod), available)
       const int64_t av = a.ex_available[(size_t)e * KP_NRES + r];
       ok = av >= 0 && a.ex_requests[(size_t)e * KP_NRES + r] + a.shape_requests[(size_t)shape * KP_NRES + r] <= av;
@@ -239,6 +240,7 @@ __global__ __launch_bounds__(SIM_WAVES * 64) void sim_prep_kernel(SimArgs a) {
           out->tmpl = t;
           out->taintset = a.tmpl_taintset[t];
           out->ver = 0;
+          out->hp = a.hp_any ? a.shape_hp_add[shape] : 0;
         }
         won = t;
       }
@@ -289,6 +291,7 @@ __global__ __launch_bounds__(NW * 64) void sim_kernel(SimArgs a) {
   uint64_t* spod = a.s_pod + (size_t)slot * cap;
   int32_t* sstart = a.s_start + (size_t)slot * SL;
   int64_t* ovl = a.s_ovl + (size_t)slot * a.E * a.RU;
+  uint64_t* ovlhp = a.hp_any ? a.s_ovlhp + (size_t)slot * a.E : nullptr;
   SimNC* nc = a.s_nc + slot;
   int32_t* ncfail = a.s_ncfail + (size_t)slot * SL;
   KReqs* sB = &s_B[wave];
@@ -386,6 +389,7 @@ __global__ __launch_bounds__(NW * 64) void sim_kernel(SimArgs a) {
       const int sl = a.shape_level_base[shape] + lvl;
       stage_shape(a, sl, shape, sB, spreq, s_pslot[wave]);
       sim_sync();
+      const uint64_t hpc = a.hp_any ? a.shape_hp_conf[shape] : 0, hpa = a.hp_any ? a.shape_hp_add[shape] : 0;
       int placed = -1;  // 0: the NodeClaim; <= -2: existing position -2-placed
       // addToExistingNode
       int st = sstart[sl];
@@ -410,6 +414,7 @@ __global__ __launch_bounds__(NW * 64) void sim_kernel(SimArgs a) {
             const int r = a.ru_res[u];
             fits = fits && ovl[(size_t)e * a.RU + u] + spreq[r] <= a.ex_available[(size_t)e * KP_NRES + r];
           }
+          if (hpc) fits = fits && !(ovlhp[e] & hpc);  // ports the simulation's pods took on the node
           if (fits) {
             found = b;
             break;
@@ -440,6 +445,7 @@ __global__ __launch_bounds__(NW * 64) void sim_kernel(SimArgs a) {
             const int64_t prev = first ? a.ex_requests[(size_t)e * KP_NRES + r] : ovl[(size_t)e * a.RU + lane];
             ovl[(size_t)e * a.RU + lane] = prev + spreq[r];
           }
+          if (ovlhp && lane == 0) ovlhp[e] = (first ? a.ex_hp[e] : ovlhp[e]) | hpa;
           wave_sync();
           if (lane == 0) dirty[e >> 6] |= 1ull << (e & 63);
         }
@@ -448,7 +454,7 @@ __global__ __launch_bounds__(NW * 64) void sim_kernel(SimArgs a) {
       // addToInflightNode (at most one NodeClaim exists)
       if (placed == -1 && n_nc == 1) {
         const uint64_t tol = a.shape_tolerates[shape];
-        bool cand = ((tol >> nc->taintset) & 1) && ncfail[sl] != nc->ver;
+        bool cand = ((tol >> nc->taintset) & 1) && ncfail[sl] != nc->ver && !(nc->hp & hpc);
         if (cand)
           for (int r = 0; r < KP_NRES; r++)
             if (((rmask >> r) & 1) && nc->requests[r] + spreq[r] > nc->maxalloc[r]) cand = false;
@@ -478,6 +484,7 @@ __global__ __launch_bounds__(NW * 64) void sim_kernel(SimArgs a) {
               nc->fitj[lane] = s_fitj[wave][lane];
             }
             if (lane == 0) nc->ver = ++vcount;
+            if (lane == 0) nc->hp |= hpa;
             placed = 0;
           } else if (lane == 0) {
             ncfail[sl] = nc->ver;

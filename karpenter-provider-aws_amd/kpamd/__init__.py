@@ -25,11 +25,12 @@ class KPError(RuntimeError):
         self.code = code
 
 
-def load_lib(path=LIB_PATH):
+def load_lib(path=None):
     """Load libkp.so (built in-tree by __graft_entry__.build()). Raises if absent — no fallback."""
     global _LIB
     if _LIB is not None:
         return _LIB
+    path = path or os.environ.get("KP_LIB") or LIB_PATH  # KP_LIB: a diagnostic build (tools/), same ABI
     if not os.path.exists(path):
         raise KPError(abi.KP_E_DEVICE, f"{path} missing: run __graft_entry__.build()")
     lib = C.CDLL(path)

@@ -116,6 +116,13 @@ class TopologySpread(C.Structure):
                 ("node_taints_policy", C.c_int32), ("reserved_", C.c_int32), ("selector", LabelSelector)]
 
 
+class HostPort(C.Structure):
+    _fields_ = [("ip", C.c_char_p), ("port", C.c_int32), ("protocol", C.c_int32)]
+
+
+PROTOCOLS = {"TCP": 0, "UDP": 1, "SCTP": 2, "": 0, None: 0}
+
+
 class PodShape(C.Structure):
     _fields_ = [("requests", ResourceList), ("node_selector", C.POINTER(Label)), ("n_node_selector", C.c_uint32),
                 ("n_required_terms", C.c_uint32), ("required_terms", C.POINTER(Requirements)),
@@ -123,7 +130,8 @@ class PodShape(C.Structure):
                 ("n_tolerations", C.c_uint32), ("tolerations", C.POINTER(Toleration)),
                 ("n_topology_spread", C.c_uint32), ("n_labels", C.c_uint32),
                 ("topology_spread", C.POINTER(TopologySpread)), ("namespace_", C.c_char_p),
-                ("labels", C.POINTER(Label))]
+                ("labels", C.POINTER(Label)), ("host_ports", C.POINTER(HostPort)), ("n_host_ports", C.c_uint32),
+                ("n_volume_requirements", C.c_uint32), ("volume_requirements", C.POINTER(Requirement))]
 
 
 class BoundPod(C.Structure):
@@ -138,7 +146,8 @@ class Pod(C.Structure):
 class ExistingNode(C.Structure):
     _fields_ = [("name", C.c_char_p), ("labels", C.POINTER(Label)), ("n_labels", C.c_uint32),
                 ("n_taints", C.c_uint32), ("taints", C.POINTER(Taint)), ("available", ResourceList),
-                ("requests", ResourceList), ("initialized", C.c_int32), ("reserved_", C.c_int32)]
+                ("requests", ResourceList), ("initialized", C.c_int32), ("reserved_", C.c_int32),
+                ("host_ports", C.POINTER(HostPort)), ("n_host_ports", C.c_uint32), ("reserved2_", C.c_uint32)]
 
 
 class SolveIn(C.Structure):
@@ -349,9 +358,17 @@ class Arena:
         tols, ntol = self.tolerations(sh.tolerations)
         spreads = self.arr(TopologySpread, [self.spread(t) for t in sh.topology_spread])
         labels, nl = self.labels(sh.labels)
+        hps, nhp = self.host_ports(getattr(sh, "host_ports", None))
+        vol = list(getattr(sh, "volume_requirements", None) or [])
+        vreqs = self.arr(Requirement, [self.requirement(r) for r in vol])
         return PodShape(self.resources(sh.requests), ns, nns, len(sh.required_terms), terms, prefs,
                         len(sh.preferred_terms), ntol, tols, len(sh.topology_spread), nl, spreads,
-                        self.s(sh.namespace), labels)
+                        self.s(sh.namespace), labels, hps, nhp, len(vol), vreqs)
+
+    def host_ports(self, hps):
+        """[(hostIP, hostPort, protocol)] -> kp_host_port[] (hostIP None/"" = 0.0.0.0, protocol None = TCP)."""
+        hps = list(hps or [])
+        return self.arr(HostPort, [HostPort(self.s(ip or ""), int(port), PROTOCOLS[proto]) for ip, port, proto in hps]), len(hps)
 
     def selector(self, sel):
         if sel is None:
@@ -376,11 +393,12 @@ class Arena:
             out.append(BoundPod(self.s(ns), la, nl, int(node)))
         return self.arr(BoundPod, out), len(bps)
 
-    def existing_node(self, n):
+    def existing_node(self, n, extra_ports=()):
         labels, nl = self.labels(n.labels)
         taints, nt = self.taints(n.taints)
+        hps, nhp = self.host_ports(list(getattr(n, "host_ports", None) or []) + list(extra_ports))
         return ExistingNode(self.s(n.name), labels, nl, nt, taints, self.resources(n.available),
-                            self.resources(n.requests), 1 if n.initialized else 0, 0)
+                            self.resources(n.requests), 1 if n.initialized else 0, 0, hps, nhp, 0)
 
 
 def build_solve_in(arena, problem, catalog_handles=None):
@@ -423,7 +441,9 @@ def build_cluster(arena, cl, catalog_handles=None):
     nodes = []
     for n in cl.nodes:
         pods = arena.arr(C.c_uint32, list(n.pods))
-        nodes.append(ClusterNode(arena.existing_node(n.node), n.catalog, n.instance_type, pods, len(n.pods),
+        # the node's HostPortUsage: its own entries plus those of every pod bound to it (kp_cluster convention)
+        used = [hp for p in n.pods for hp in (getattr(cl.shapes[int(cl.pod_shape[p])], "host_ports", None) or [])]
+        nodes.append(ClusterNode(arena.existing_node(n.node, used), n.catalog, n.instance_type, pods, len(n.pods),
                                  1 if n.deleting else 0))
     nodes_a = arena.arr(ClusterNode, nodes)
     shapes = arena.arr(PodShape, [arena.shape(s) for s in cl.shapes])

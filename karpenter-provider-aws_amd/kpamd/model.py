@@ -87,6 +87,8 @@ class PodShape:
     topology_spread: List[TopologySpread] = field(default_factory=list)
     labels: Dict[str, str] = field(default_factory=dict)
     namespace: str = "default"
+    host_ports: List[Tuple[str, int, str]] = field(default_factory=list)  # GetHostPorts: (hostIP, hostPort, protocol)
+    volume_requirements: List[Req] = field(default_factory=list)         # VolumeTopology.Inject input
 
 
 @dataclass
@@ -97,6 +99,7 @@ class ExistingNode:
     requests: Dict[str, int] = field(default_factory=dict)
     taints: List[Tuple[str, str, str]] = field(default_factory=list)
     initialized: bool = True
+    host_ports: List[Tuple[str, int, str]] = field(default_factory=list)  # HostPortUsage of its bound pods
 
 
 @dataclass

@@ -33,6 +33,8 @@
  * (queue order, in-flight order, relaxation order) are "parity unpinned": no Go toolchain and no
  * upstream module here, so this file IS the written spec for them.
  */
+#include <arpa/inet.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -702,6 +704,50 @@ struct Spread {
   Selector sel;
 };
 
+// UP scheduling.HostPort / GetHostPorts / HostPortUsage (hostportusage.go): hostIP "" -> 0.0.0.0, protocol "" -> TCP,
+// hostPort 0 skipped; Matches = same protocol and port, and an unspecified IP on either side or equal IPs
+// (net.IP.Equal: an IPv4 address equals its v4-in-v6 form).
+struct HostPort {
+  int proto, port;
+  unsigned char ip[16];  // net.ParseIP form: IPv4 as ::ffff:a.b.c.d
+  bool IsUnspecified() const {
+    static const unsigned char z[16] = {0};
+    static const unsigned char z4[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0xFF, 0xFF, 0, 0, 0, 0};
+    return !memcmp(ip, z, 16) || !memcmp(ip, z4, 16);
+  }
+  bool Matches(const HostPort& r) const {
+    if (proto != r.proto || port != r.port) return false;
+    if (IsUnspecified() || r.IsUnspecified()) return true;
+    return !memcmp(ip, r.ip, 16);
+  }
+};
+static bool GetHostPorts(const kp_host_port* hp, uint32_t n, vector<HostPort>* out) {
+  for (uint32_t i = 0; i < n; i++) {
+    if (hp[i].port == 0) continue;
+    HostPort h;
+    h.proto = hp[i].protocol;
+    h.port = hp[i].port;
+    memset(h.ip, 0, 16);
+    const char* ip = hp[i].ip && hp[i].ip[0] ? hp[i].ip : "0.0.0.0";
+    unsigned char v4[4];
+    if (inet_pton(AF_INET, ip, v4) == 1) {
+      h.ip[10] = h.ip[11] = 0xFF;
+      memcpy(h.ip + 12, v4, 4);
+    } else if (inet_pton(AF_INET6, ip, h.ip) != 1) {
+      return false;
+    }
+    out->push_back(h);
+  }
+  return true;
+}
+// HostPortUsage.Conflicts(pod, ports): any new entry matching an entry another pod reserved
+static bool HostPortsConflict(const vector<HostPort>& reserved, const vector<HostPort>& ports) {
+  for (auto& n : ports)
+    for (auto& e : reserved)
+      if (n.Matches(e)) return true;
+  return false;
+}
+
 struct PodState {
   int index;
   int shape;
@@ -717,6 +763,7 @@ struct PodState {
   vector<Spread> spreads;
   string ns;
   map<string, string> labels;
+  vector<HostPort> hostPorts;
   Requirements reqs;    // cached NewPodRequirements
   Requirements strict;  // cached NewStrictPodRequirements (no preferred terms)
 };
@@ -999,6 +1046,7 @@ struct NodeClaim {
   ResourceList requests;
   vector<int> pods;
   string hostname;
+  vector<HostPort> hostPortUsage;
 };
 
 struct ExistingNode {
@@ -1009,6 +1057,7 @@ struct ExistingNode {
   vector<Taint> taints;
   ResourceList available, requests;
   vector<int> pods;
+  vector<HostPort> hostPortUsage;
 };
 
 static bool SatisfiesMinValues(const vector<InstanceType>& cat, const vector<int>& its, const Requirements& reqs) {
@@ -1067,6 +1116,7 @@ struct Scheduler {
   bool NodeClaimAdd(NodeClaim& n, PodState& p) {
     counters.attempts++;
     if (!ToleratesAll(n.tmpl->taints, p.tolerations)) return false;
+    if (HostPortsConflict(n.hostPortUsage, p.hostPorts)) return false;
     Requirements ncr = n.reqs;
     if (!Compatible(ncr, p.reqs, true)) return false;
     AddAll(ncr, p.reqs);
@@ -1081,6 +1131,7 @@ struct Scheduler {
     n.options = std::move(remaining);
     n.requests = requests;
     n.reqs = std::move(ncr);
+    n.hostPortUsage.insert(n.hostPortUsage.end(), p.hostPorts.begin(), p.hostPorts.end());
     topology.Record(p, n.tmpl->taints, n.reqs, true);
     return true;
   }
@@ -1089,6 +1140,7 @@ struct Scheduler {
   bool ExistingCanAddAndAdd(ExistingNode& n, PodState& p) {
     counters.attempts++;
     if (!ToleratesAll(n.taints, p.tolerations)) return false;
+    if (HostPortsConflict(n.hostPortUsage, p.hostPorts)) return false;
     ResourceList requests = Merge(n.requests, p.requests);
     if (!Fits(requests, n.available)) return false;
     Requirements nr = n.reqs;
@@ -1101,6 +1153,7 @@ struct Scheduler {
     n.pods.push_back(p.index);
     n.requests = requests;
     n.reqs = std::move(nr);
+    n.hostPortUsage.insert(n.hostPortUsage.end(), p.hostPorts.begin(), p.hostPorts.end());
     topology.Record(p, n.taints, n.reqs, false);
     return true;
   }
@@ -1334,6 +1387,7 @@ static int32_t SolveCore(const Catalogs& cats, const kp_solve_in* in, kpo_result
     n.taints = TaintsFromABI(e.taints, e.n_taints);
     n.available = FromABI(e.available);
     n.requests = FromABI(e.requests);
+    if (!GetHostPorts(e.host_ports, e.n_host_ports, &n.hostPortUsage)) return KP_E_INVAL;
     s.existing.push_back(std::move(n));
   }
   std::stable_sort(s.existing.begin(), s.existing.end(), [](const ExistingNode& a, const ExistingNode& b) {
@@ -1356,6 +1410,12 @@ static int32_t SolveCore(const Catalogs& cats, const kp_solve_in* in, kpo_result
     ps.mem = Get(ps.requests, KP_RES_MEMORY);
     ps.node_selector = LabelRequirements(sh.node_selector, sh.n_node_selector);
     for (uint32_t j = 0; j < sh.n_required_terms; j++) ps.required_terms.push_back(FromABI(sh.required_terms[j]));
+    if (sh.n_volume_requirements) {  // UP VolumeTopology.Inject: appended to every required term (one if none)
+      const Requirements vol = FromABI(kp_requirements{sh.volume_requirements, sh.n_volume_requirements, 0});
+      if (ps.required_terms.empty()) ps.required_terms.push_back(Requirements());
+      for (auto& t : ps.required_terms) AddAll(t, vol);
+    }
+    if (!GetHostPorts(sh.host_ports, sh.n_host_ports, &ps.hostPorts)) return KP_E_INVAL;
     for (uint32_t j = 0; j < sh.n_preferred_terms; j++)
       ps.preferred.push_back({sh.preferred_terms[j].weight, FromABI(sh.preferred_terms[j].preference)});
     for (uint32_t j = 0; j < sh.n_tolerations; j++) {

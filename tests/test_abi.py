@@ -23,7 +23,7 @@ def test_all_declared_symbols_exported():
 
 def test_abi_version_and_struct_sizes():
     lib = kpamd.load_lib()
-    assert lib.kp_abi_version() == 5
+    assert lib.kp_abi_version() == 6
     from kpamd import abi
     assert C.sizeof(abi.ResourceList) == 12 * 8 + 8
     assert C.sizeof(abi.Offering) == 5 * 8 + 8 + 8
@@ -46,3 +46,22 @@ def test_launch_struct_layouts():
     from kpamd import abi
     assert C.sizeof(abi.LaunchResult) == 10 * 4
     assert C.sizeof(abi.LaunchRequest) == C.sizeof(abi.Requirements) + C.sizeof(abi.ResourceList) + 8 + 8
+
+
+def test_struct_sizes_match_the_c_header(tmp_path):
+    """ctypes mirrors of the ABI structs have the sizes gcc gives the header's structs (ABI v6 host ports, volumes)."""
+    import shutil
+    import subprocess
+    from kpamd import abi
+    if not shutil.which("gcc"):
+        return
+    pairs = {"kp_pod_shape": abi.PodShape, "kp_existing_node": abi.ExistingNode, "kp_host_port": abi.HostPort,
+             "kp_cluster_node": abi.ClusterNode, "kp_solve_in": abi.SolveIn, "kp_topology_spread": abi.TopologySpread,
+             "kp_nodepool": abi.NodePool, "kp_cluster": abi.Cluster}
+    src = tmp_path / "sz.c"
+    src.write_text('#include <stdio.h>\n#include "kp/kp_abi.h"\nint main(void){\n' +
+                   "".join(f'printf("%zu\\n", sizeof({k}));\n' for k in pairs) + "return 0;}\n")
+    exe = tmp_path / "sz"
+    subprocess.check_call(["gcc", "-I", os.path.dirname(os.path.dirname(HDR)), str(src), "-o", str(exe)])
+    got = [int(x) for x in subprocess.check_output([str(exe)]).split()]
+    assert got == [C.sizeof(t) for t in pairs.values()], dict(zip(pairs, got))
