@@ -17,6 +17,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <deque>
 #include <limits>
 #include <map>
 #include <memory>
@@ -208,7 +209,7 @@ struct kp_ctx {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
   kp_options opts;
-  std::mutex mu;
+  std::recursive_mutex mu;  // recursive: the general simulation path runs whole Solves under the cluster plan's lock
   // resident compiled catalogues + templates of recent Solves (most recent last), see SolveBase
   vector<std::shared_ptr<SolveBase>> bases;
   uint64_t base_hits = 0, base_misses = 0;
@@ -850,6 +851,8 @@ struct kp_solve_result {
   };
   vector<NC> ncs;
   kp_solve_stats stats;
+  vector<KReqs> fin;     // per NodeClaim: final requirements (device encoding), for in-library callers
+  vector<int> nc_cat;    // per NodeClaim: catalogue of its template
 };
 
 extern "C" {
@@ -933,8 +936,8 @@ void kp_catalog_destroy(kp_catalog* c) { delete c; }
 int32_t kp_catalog_update_offerings(kp_catalog* c, const kp_offering_update* ups, uint32_t n, uint64_t seqnum) {
   if (!c || (!ups && n)) return fail(KP_E_INVAL, "null argument");
   // serialized with every prepare / refresh / run of the catalogue's context (they read c->types)
-  std::unique_lock<std::mutex> lock;
-  if (c->ctx) lock = std::unique_lock<std::mutex>(c->ctx->mu);
+  std::unique_lock<std::recursive_mutex> lock;
+  if (c->ctx) lock = std::unique_lock<std::recursive_mutex>(c->ctx->mu);
   auto match = [](const HostOffering& o, const kp_offering_update& u) {
     if (o.ct != (u.capacity_type ? u.capacity_type : "")) return false;
     return u.zone ? (o.has_zone && o.zone == u.zone) : !o.has_zone;
@@ -2148,7 +2151,7 @@ int32_t kp_solve_prepare_comm(kp_ctx* ctx, const kp_solve_in* in, kp_comm* comm,
 static int32_t SolvePrepare(kp_ctx* ctx, const kp_solve_in* in, kp_comm* comm, kp_solve_plan** out) {
   auto t0 = std::chrono::steady_clock::now();
   if (!ctx || !in || !out) return fail(KP_E_INVAL, "null argument");
-  std::lock_guard<std::mutex> lock(ctx->mu);
+  std::lock_guard<std::recursive_mutex> lock(ctx->mu);
   HIPCHK(hipSetDevice(ctx->device));
   auto plan = std::make_unique<kp_solve_plan>();
   plan->ctx = ctx;
@@ -2462,7 +2465,7 @@ static int32_t SolvePrepare(kp_ctx* ctx, const kp_solve_in* in, kp_comm* comm, k
 void kp_solve_plan_destroy(kp_solve_plan* p) {
   if (!p) return;
   kp_ctx* ctx = p->ctx;
-  std::lock_guard<std::mutex> lock(ctx->mu);
+  std::lock_guard<std::recursive_mutex> lock(ctx->mu);
   (void)hipSetDevice(ctx->device);
   if (p->buf.p && p->buf.n >= ctx->spare_bytes) {  // keep the larger arena for the next prepare
     if (ctx->spare) (void)hipFree(ctx->spare);
@@ -2479,7 +2482,7 @@ int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out) {
   auto t0 = std::chrono::steady_clock::now();
   if (!plan || !out) return fail(KP_E_INVAL, "null argument");
   kp_ctx* ctx = plan->ctx;
-  std::lock_guard<std::mutex> lock(ctx->mu);
+  std::lock_guard<std::recursive_mutex> lock(ctx->mu);
   HIPCHK(hipSetDevice(ctx->device));
   const Compiled& C = *plan->cp;
   const Dict& d = C.B->d;
@@ -2560,8 +2563,11 @@ int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out) {
       res->placement[p] = -2 - C.ex_input[-2 - t];
     }
   }
+  res->fin = fin;
+  res->nc_cat.resize(n_nc);
   for (int i = 0; i < n_nc; i++) {
     auto& nc = res->ncs[i];
+    res->nc_cat[i] = C.B->tmpl_catalog[nct[i]];
     nc.nodepool = (uint32_t)C.B->tmpl_nodepool[nct[i]];
     nc.n_remaining = nrem[i];
     memset(&nc.requests, 0, sizeof nc.requests);
@@ -2707,7 +2713,7 @@ int32_t CompileQueries(const kp_catalog* cat, const vector<RawReqs>& qs, Compile
 // Shared by kp_filter_refresh / kp_launch_refresh: rebuild the offering section of a plan's compiled catalogue
 // from the catalogue's current offerings (class ids as compiled) and copy it over the resident arrays.
 static int32_t RefreshOfferings(kp_ctx* ctx, const kp_catalog* cat, Compiled& cp, const CatOffsets& coff, uint8_t* base) {
-  std::lock_guard<std::mutex> lock(ctx->mu);
+  std::lock_guard<std::recursive_mutex> lock(ctx->mu);
   HIPCHK(hipSetDevice(ctx->device));
   map<ClassKey, int> classes;
   for (int c = 0; c < cp.B->C; c++) classes[{cp.B->classes[c].ct_bit, cp.B->classes[c].zone_bit, cp.B->classes[c].zid_bit}] = c;
@@ -2758,7 +2764,7 @@ int32_t kp_filter_prepare(kp_ctx* ctx, const kp_catalog* cat, const kp_feasibili
                           int32_t with_cheapest, kp_filter_plan** out) {
   auto t0 = std::chrono::steady_clock::now();
   if (!ctx || !cat || (!queries && n_queries) || !out) return fail(KP_E_INVAL, "null argument");
-  std::lock_guard<std::mutex> lock(ctx->mu);
+  std::lock_guard<std::recursive_mutex> lock(ctx->mu);
   HIPCHK(hipSetDevice(ctx->device));
   auto plan = std::make_unique<kp_filter_plan>();
   plan->ctx = ctx;
@@ -2822,7 +2828,7 @@ int32_t kp_filter_run(kp_filter_plan* plan, uint64_t* out_mask, double* out_chea
   if (!plan) return fail(KP_E_INVAL, "null argument");
   if (out_cheapest && !plan->cheapest) return fail(KP_E_INVAL, "plan was prepared without cheapest prices");
   kp_ctx* ctx = plan->ctx;
-  std::lock_guard<std::mutex> lock(ctx->mu);
+  std::lock_guard<std::recursive_mutex> lock(ctx->mu);
   if (plan->cat->seqnum != plan->seqnum)  // R:instancetype.go:225-237: a changed seqnum invalidates the offerings
     return fail(KP_E_INVAL, "stale plan: catalogue seqnum %llu, plan built at %llu (kp_filter_refresh)",
                 (unsigned long long)plan->cat->seqnum, (unsigned long long)plan->seqnum);
@@ -2914,7 +2920,7 @@ int32_t kp_launch_prepare(kp_ctx* ctx, const kp_catalog* cat, const kp_launch_re
         return fail(KP_E_UNSUPPORTED, "%s: two %s offerings in zone %s", t.name.c_str(), o.ct.c_str(), o.zone.c_str());
     }
   }
-  std::lock_guard<std::mutex> lock(ctx->mu);
+  std::lock_guard<std::recursive_mutex> lock(ctx->mu);
   HIPCHK(hipSetDevice(ctx->device));
   auto plan = std::make_unique<kp_launch_plan>();
   plan->ctx = ctx;
@@ -3053,7 +3059,7 @@ int32_t kp_launch_run(kp_launch_plan* plan, kp_launch_result* out, uint32_t* out
   auto t0 = std::chrono::steady_clock::now();
   if (!plan) return fail(KP_E_INVAL, "null argument");
   kp_ctx* ctx = plan->ctx;
-  std::lock_guard<std::mutex> lock(ctx->mu);
+  std::lock_guard<std::recursive_mutex> lock(ctx->mu);
   if (plan->cat->seqnum != plan->seqnum)
     return fail(KP_E_INVAL, "stale plan: catalogue seqnum %llu, plan built at %llu (kp_launch_refresh)",
                 (unsigned long long)plan->cat->seqnum, (unsigned long long)plan->seqnum);
@@ -3119,8 +3125,123 @@ int32_t kp_launch_select(kp_ctx* ctx, const kp_catalog* cat, const kp_launch_req
 // ---- consolidation: cluster snapshot + batched simulations -----------------------------------------
 }  // extern "C"
 
+// Owned deep copy of a kp_cluster (strings and nested arrays), kept by a cluster plan whose simulations run as
+// whole Solves (the general path): the caller's buffers are not retained past kp_cluster_prepare.
+struct OwnedCluster {
+  std::deque<string> strs;
+  vector<std::unique_ptr<uint8_t[]>> blocks;
+  kp_cluster cl;
+  vector<const kp_catalog*> cats;
+  const char* S(const char* x) {
+    if (!x) return nullptr;
+    strs.emplace_back(x);
+    return strs.back().c_str();
+  }
+  template <class T>
+  T* A(const T* src, size_t n) {
+    if (!src || !n) return nullptr;
+    blocks.emplace_back(new uint8_t[sizeof(T) * n]);
+    T* d = reinterpret_cast<T*>(blocks.back().get());
+    memcpy((void*)d, (const void*)src, sizeof(T) * n);
+    return d;
+  }
+  void Reqs(kp_requirements& r) {
+    kp_requirement* it = A(r.items, r.n);
+    for (uint32_t i = 0; it && i < r.n; i++) {
+      it[i].key = S(it[i].key);
+      const char** v = (const char**)A(it[i].values, it[i].n_values);
+      for (uint32_t j = 0; v && j < it[i].n_values; j++) v[j] = S(v[j]);
+      it[i].values = v;
+    }
+    r.items = it;
+  }
+  const kp_label* Labels(const kp_label* l, uint32_t n) {
+    kp_label* o = A(l, n);
+    for (uint32_t i = 0; o && i < n; i++) o[i].key = S(o[i].key), o[i].value = S(o[i].value);
+    return o;
+  }
+  const kp_taint* Taints(const kp_taint* t, uint32_t n) {
+    kp_taint* o = A(t, n);
+    for (uint32_t i = 0; o && i < n; i++) o[i].key = S(o[i].key), o[i].value = S(o[i].value);
+    return o;
+  }
+  const kp_host_port* Ports(const kp_host_port* h, uint32_t n) {
+    kp_host_port* o = A(h, n);
+    for (uint32_t i = 0; o && i < n; i++) o[i].ip = S(o[i].ip);
+    return o;
+  }
+  void Selector(kp_label_selector& s) {
+    s.match_labels = Labels(s.match_labels, s.n_match_labels);
+    kp_selector_requirement* e = A(s.match_expressions, s.n_match_expressions);
+    for (uint32_t i = 0; e && i < s.n_match_expressions; i++) {
+      e[i].key = S(e[i].key);
+      const char** v = (const char**)A(e[i].values, e[i].n_values);
+      for (uint32_t j = 0; v && j < e[i].n_values; j++) v[j] = S(v[j]);
+      e[i].values = v;
+    }
+    s.match_expressions = e;
+  }
+  void Node(kp_existing_node& n) {
+    n.name = S(n.name);
+    n.labels = Labels(n.labels, n.n_labels);
+    n.taints = Taints(n.taints, n.n_taints);
+    n.host_ports = Ports(n.host_ports, n.n_host_ports);
+  }
+  explicit OwnedCluster(const kp_cluster* in) {
+    cl = *in;
+    cats.assign(in->catalogs, in->catalogs + in->n_catalogs);
+    cl.catalogs = cats.data();
+    cl.catalog_descs = nullptr;
+    kp_nodepool* np = A(in->nodepools, in->n_nodepools);
+    for (uint32_t i = 0; np && i < in->n_nodepools; i++) {
+      np[i].name = S(np[i].name);
+      Reqs(np[i].requirements);
+      np[i].labels = Labels(np[i].labels, np[i].n_labels);
+      np[i].taints = Taints(np[i].taints, np[i].n_taints);
+    }
+    cl.nodepools = np;
+    kp_cluster_node* nd = A(in->nodes, in->n_nodes);
+    for (uint32_t i = 0; nd && i < in->n_nodes; i++) {
+      Node(nd[i].node);
+      nd[i].pods = A(nd[i].pods, nd[i].n_pods);
+    }
+    cl.nodes = nd;
+    kp_pod_shape* sh = A(in->shapes, in->n_shapes);
+    for (uint32_t i = 0; sh && i < in->n_shapes; i++) {
+      kp_pod_shape& x = sh[i];
+      x.node_selector = Labels(x.node_selector, x.n_node_selector);
+      kp_requirements* rt = A(x.required_terms, x.n_required_terms);
+      for (uint32_t j = 0; rt && j < x.n_required_terms; j++) Reqs(rt[j]);
+      x.required_terms = rt;
+      kp_preferred_term* pt = A(x.preferred_terms, x.n_preferred_terms);
+      for (uint32_t j = 0; pt && j < x.n_preferred_terms; j++) Reqs(pt[j].preference);
+      x.preferred_terms = pt;
+      kp_toleration* tl = A(x.tolerations, x.n_tolerations);
+      for (uint32_t j = 0; tl && j < x.n_tolerations; j++) tl[j].key = S(tl[j].key), tl[j].value = S(tl[j].value);
+      x.tolerations = tl;
+      kp_topology_spread* ts = A(x.topology_spread, x.n_topology_spread);
+      for (uint32_t j = 0; ts && j < x.n_topology_spread; j++) {
+        ts[j].topology_key = S(ts[j].topology_key);
+        Selector(ts[j].selector);
+      }
+      x.topology_spread = ts;
+      x.namespace_ = S(x.namespace_);
+      x.labels = Labels(x.labels, x.n_labels);
+      x.host_ports = Ports(x.host_ports, x.n_host_ports);
+      kp_requirements vr{x.volume_requirements, x.n_volume_requirements, 0};
+      Reqs(vr);
+      x.volume_requirements = vr.items;
+    }
+    cl.shapes = sh;
+    cl.pods = A(in->pods, in->n_pods);
+    cl.pending_pods = A(in->pending_pods, in->n_pending);
+  }
+};
+
 struct kp_cluster_plan {
   kp_ctx* ctx = nullptr;
+  std::unique_ptr<OwnedCluster> general;  // set: simulations run as whole Solves (kp_solve on this device)
+  double general_ms = 0;                  // device time of the last general batch (solve + finalize kernels)
   std::unique_ptr<Compiled> cp;
   DevBuf buf;                       // resident snapshot
   DevBuf scratch;                   // per-wave state, grown on demand
@@ -3161,14 +3282,47 @@ bool NodeCandidatePrice(const HostType& t, const std::map<string, string>& label
 
 extern "C" {
 
+// A cluster plan for the general path: the cluster is validated by a host compile (every node existing, every pod
+// pending) and kept as an owned copy; nothing is uploaded until a batch runs.
+static int32_t PrepareGeneral(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan** out,
+                              std::chrono::steady_clock::time_point t0) {
+  for (uint32_t i = 0; i < cl->n_catalogs; i++)
+    if (!cl->catalogs || !cl->catalogs[i]) return fail(KP_E_INVAL, "catalogue %u is null", i);
+  vector<kp_existing_node> ex(cl->n_nodes);
+  for (uint32_t i = 0; i < cl->n_nodes; i++) ex[i] = cl->nodes[i].node;
+  kp_solve_in in;
+  memset(&in, 0, sizeof in);
+  in.catalogs = cl->catalogs;
+  in.n_catalogs = cl->n_catalogs;
+  in.n_nodepools = cl->n_nodepools;
+  in.nodepools = cl->nodepools;
+  in.existing = ex.data();
+  in.n_existing = cl->n_nodes;
+  in.n_shapes = cl->n_shapes;
+  in.shapes = cl->shapes;
+  in.pods = cl->pods;
+  in.n_pods = cl->n_pods;
+  in.max_instance_types = 100;
+  Compiled C;
+  int32_t rc = CompileSolve(&in, C);
+  if (rc) return rc;
+  auto plan = std::make_unique<kp_cluster_plan>();
+  plan->ctx = ctx;
+  plan->N = (int)cl->n_nodes;
+  plan->general = std::make_unique<OwnedCluster>(cl);
+  plan->prepare_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  *out = plan.release();
+  return KP_OK;
+}
+
 int32_t kp_cluster_prepare(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan** out) {
   auto t0 = std::chrono::steady_clock::now();
   if (!ctx || !cl || !out) return fail(KP_E_INVAL, "null argument");
   if (cl->n_nodes && !cl->nodes) return fail(KP_E_INVAL, "null nodes");
-  for (uint32_t i = 0; i < cl->n_shapes; i++)
-    if (cl->shapes[i].n_topology_spread)
-      return fail(KP_E_UNSUPPORTED, "topology spread in consolidation simulations (cluster pods are not bound pods)");
-  std::lock_guard<std::mutex> lock(ctx->mu);
+  bool topo = false;
+  for (uint32_t i = 0; i < cl->n_shapes; i++) topo |= cl->shapes[i].n_topology_spread > 0;
+  if (topo) return PrepareGeneral(ctx, cl, out, t0);
+  std::lock_guard<std::recursive_mutex> lock(ctx->mu);
   HIPCHK(hipSetDevice(ctx->device));
   auto plan = std::make_unique<kp_cluster_plan>();
   plan->ctx = ctx;
@@ -3200,8 +3354,8 @@ int32_t kp_cluster_prepare(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan** 
   uint64_t all_nodes_keys = ~0ull;
   for (auto& q : C.ex_reqs) all_nodes_keys &= q.present;
   for (int sl = 0; sl < SL; sl++)
-    if (C.shape_negop[sl] & ~all_nodes_keys)
-      return fail(KP_E_UNSUPPORTED, "pod NotIn/DoesNotExist requirement on a label some node lacks");
+    if (C.shape_negop[sl] & ~all_nodes_keys)  // CanAdd is then not a function of the snapshot: whole Solves
+      return PrepareGeneral(ctx, cl, out, t0);
   // existing nodes: label value bit per key (node labels are single-valued In requirements)
   vector<uint16_t> ex_code((size_t)std::max(K, 1) * std::max(E, 1), 0xFFFF);
   vector<uint8_t> ex_init(std::max(E, 1), 0);
@@ -3444,9 +3598,232 @@ void kp_cluster_plan_destroy(kp_cluster_plan* p) {
 }
 
 // One batch on the resident snapshot, results left on the device (a_out.out); the caller holds ctx->mu.
+// ---- general simulations: each subset's SimulateScheduling as a whole Solve on the device -----------------------
+// Used for clusters the batched sim kernels do not model (topology spread; pod NotIn/DoesNotExist on a label key
+// some node lacks). Per subset: the pending pods, the deleting nodes' pods and the subset's pods are scheduled onto
+// every other node (existing), with every pod still bound to one of those nodes as a bound pod (Topology.countDomains
+// skips the pods being scheduled), then computeConsolidation's decision is taken on the Solve result exactly as the
+// batched kernel takes it (sim_kernel's decision; disruption.md:89-128).
+namespace {
+bool OfferAdmits(const Dict& d, const KReqs& R, const HostOffering& o) {
+  auto admits = [&](const char* key, bool has, const string& v) {
+    if (!has) return true;
+    const int k = d.key(key);
+    if (k < 0 || !((R.present >> k) & 1)) return true;  // undefined well-known key: allowed
+    const int b = d.bit(k, v);
+    if (b < 0) return ((R.compl_ >> k) & 1) != 0;
+    return Has(d, R, k, b);
+  };
+  return admits(kCapType, true, o.ct) && admits(kZone, o.has_zone, o.zone) && admits(kZoneID, o.has_zid, o.zid);
+}
+// Offerings.Available().Compatible(reqs).WorstLaunchPrice: capacity types in precedence reserved, spot, on-demand
+double WorstLaunch(const Dict& d, const KReqs& R, const HostType& t, bool spot_only) {
+  for (const char* ct : {"reserved", "spot", "on-demand"}) {
+    if (spot_only && strcmp(ct, "spot") != 0) continue;
+    bool any = false;
+    double mx = 0;
+    for (auto& o : t.offs) {
+      if (!o.available || o.ct != ct || !OfferAdmits(d, R, o)) continue;
+      if (!any || o.price > mx) mx = o.price;
+      any = true;
+    }
+    if (any) return mx;
+  }
+  return std::numeric_limits<double>::max();
+}
+}  // namespace
+
+static int32_t SolvePrepare(kp_ctx* ctx, const kp_solve_in* in, kp_comm* comm, kp_solve_plan** out);
+
+static int32_t GeneralSimLocked(kp_cluster_plan* plan, const uint32_t* offsets, const uint32_t* nodes,
+                                uint32_t n_subsets, int32_t multi_node, SimArgs& a) {
+  kp_ctx* ctx = plan->ctx;
+  const kp_cluster& cl = plan->general->cl;
+  const int N = (int)cl.n_nodes;
+  if (offsets[0] != 0) return fail(KP_E_INVAL, "offsets[0] != 0");
+  if (offsets[n_subsets] && !nodes) return fail(KP_E_INVAL, "null nodes");
+  vector<std::map<string, string>> labels(N);
+  for (int i = 0; i < N; i++)
+    for (uint32_t j = 0; j < cl.nodes[i].node.n_labels; j++) {
+      const kp_label& l = cl.nodes[i].node.labels[j];
+      labels[i][Normalize(l.key ? l.key : "")] = l.value ? l.value : "";
+    }
+  vector<SimOut> outs(n_subsets);
+  vector<char> inS(N, 0);
+  uint64_t attempts = 0, pops = 0, bytes = 0;
+  double dev_ms = 0;
+  for (uint32_t s = 0; s < n_subsets; s++) {
+    if (offsets[s + 1] < offsets[s]) return fail(KP_E_INVAL, "offsets not monotone at %u", s);
+    vector<uint32_t> cand(nodes + offsets[s], nodes + offsets[s + 1]);
+    for (uint32_t c : cand) {
+      if (c >= (uint32_t)N) return fail(KP_E_INVAL, "subset %u: node %u", s, c);
+      if (cl.nodes[c].deleting) return fail(KP_E_INVAL, "subset %u: node %u is being deleted", s, c);
+      inS[c] = 1;
+    }
+    vector<kp_existing_node> ex;
+    vector<int> exNode;
+    for (int i = 0; i < N; i++)
+      if (!inS[i] && !cl.nodes[i].deleting) {
+        ex.push_back(cl.nodes[i].node);
+        exNode.push_back(i);
+      }
+    vector<kp_pod> pods;
+    vector<int> kind;  // 0 candidate pod, 1 deleting-node pod, 2 pending
+    for (uint32_t j = 0; j < cl.n_pending; j++) {
+      if (cl.pending_pods[j] >= cl.n_pods) return fail(KP_E_INVAL, "pending pod %u", cl.pending_pods[j]);
+      pods.push_back(cl.pods[cl.pending_pods[j]]);
+      kind.push_back(2);
+    }
+    for (int i = 0; i < N; i++)
+      if (cl.nodes[i].deleting)
+        for (uint32_t j = 0; j < cl.nodes[i].n_pods; j++) {
+          pods.push_back(cl.pods[cl.nodes[i].pods[j]]);
+          kind.push_back(1);
+        }
+    for (uint32_t c : cand)
+      for (uint32_t j = 0; j < cl.nodes[c].n_pods; j++) {
+        pods.push_back(cl.pods[cl.nodes[c].pods[j]]);
+        kind.push_back(0);
+      }
+    vector<kp_bound_pod> bound;
+    for (size_t e = 0; e < exNode.size(); e++) {
+      const kp_cluster_node& n = cl.nodes[exNode[e]];
+      for (uint32_t j = 0; j < n.n_pods; j++) {
+        const uint32_t p = n.pods[j];
+        if (p >= cl.n_pods || cl.pods[p].shape >= cl.n_shapes) return fail(KP_E_INVAL, "node %d: pod %u", exNode[e], p);
+        const kp_pod_shape& sh = cl.shapes[cl.pods[p].shape];
+        bound.push_back({sh.namespace_, sh.labels, sh.n_labels, (uint32_t)e});
+      }
+    }
+    for (uint32_t c : cand) inS[c] = 0;
+    SimOut& r = outs[s];
+    memset(&r, 0, sizeof r);
+    r.n_pods = (uint32_t)pods.size();
+    double candPrice = 0;
+    bool priced = true, allSpot = true;
+    for (uint32_t c : cand) {
+      const kp_cluster_node& n = cl.nodes[c];
+      double p = 0;
+      if (!NodeCandidatePrice(cl.catalogs[n.catalog]->types[n.instance_type], labels[c], &p)) priced = false;
+      candPrice += p;
+      auto f = labels[c].find(kCapType);
+      if (f == labels[c].end() || f->second != "spot") allSpot = false;
+    }
+    r.candidate_price = priced ? candPrice : 0;
+    kp_solve_in in;
+    memset(&in, 0, sizeof in);
+    in.catalogs = cl.catalogs;
+    in.n_catalogs = cl.n_catalogs;
+    in.n_nodepools = cl.n_nodepools;
+    in.nodepools = cl.nodepools;
+    in.existing = ex.data();
+    in.n_existing = (uint32_t)ex.size();
+    in.n_shapes = cl.n_shapes;
+    in.shapes = cl.shapes;
+    in.pods = pods.data();
+    in.n_pods = (uint32_t)pods.size();
+    in.max_instance_types = 100;
+    in.bound_pods = bound.data();
+    in.n_bound_pods = (uint32_t)bound.size();
+    kp_solve_plan* sp = nullptr;
+    int32_t rc = SolvePrepare(ctx, &in, nullptr, &sp);
+    if (rc) return rc;
+    std::unique_ptr<kp_solve_plan, void (*)(kp_solve_plan*)> spg(sp, kp_solve_plan_destroy);
+    kp_solve_result* res = nullptr;
+    rc = kp_solve_run(sp, &res);
+    if (rc) return rc;
+    std::unique_ptr<kp_solve_result, void (*)(kp_solve_result*)> rg(res, kp_result_destroy);
+    attempts += res->stats.attempts;
+    pops += res->stats.pops;
+    bytes += res->stats.bytes_algorithmic;
+    dev_ms += res->stats.device_ms;
+    // AllNonPendingPodsScheduled; a candidate pod on an uninitialized node is an error (deleting-node pods exempt)
+    bool all = true;
+    for (size_t p = 0; p < pods.size() && all; p++) {
+      const int32_t pl = res->placement[p];
+      if (kind[p] == 2) continue;
+      if (pl == -1) all = false;
+      else if (kind[p] == 0 && pl <= -2 && !ex[(size_t)(-2 - pl)].initialized) all = false;
+    }
+    if (!all) continue;  // no-op
+    if (res->ncs.empty()) {
+      r.decision = KP_DECISION_DELETE;
+      r.savings = r.candidate_price;
+      continue;
+    }
+    if (res->ncs.size() != 1 || !priced) continue;
+    const Dict& d = sp->cp->B->d;
+    const KReqs& R = res->fin[0];
+    const int ci = res->nc_cat[0];
+    const vector<HostType>& types = cl.catalogs[ci]->types;
+    const HostCat& hc = sp->cp->B->cats[ci];
+    const int kct = d.key(kCapType), bspot = kct >= 0 ? d.bit(kct, "spot") : -1;
+    const bool ncSpot = kct < 0 || !((R.present >> kct) & 1) || (bspot >= 0 ? Has(d, R, kct, bspot) : ((R.compl_ >> kct) & 1));
+    const bool s2s = allSpot && ncSpot;  // spot-to-spot: only behind the feature gate
+    if (s2s && !cl.spot_to_spot) continue;
+    const bool hasMin = (R.hmin & R.present) != 0;
+    vector<int> kept;
+    for (uint32_t t : res->ncs[0].options)
+      if (WorstLaunch(d, R, types[t], s2s) < candPrice) kept.push_back((int)t);
+    if (hasMin && !HostMinValuesOK(d, hc, R, kept)) continue;
+    if (kept.empty()) continue;
+    if (multi_node) {  // filterOutSameType
+      std::map<string, double> prices;
+      for (uint32_t c : cand) {
+        const kp_cluster_node& n = cl.nodes[c];
+        const HostType& it = cl.catalogs[n.catalog]->types[n.instance_type];
+        double p = 0;
+        if (!NodeCandidatePrice(it, labels[c], &p)) continue;
+        auto f = prices.find(it.name);
+        if (f == prices.end() || p < f->second) prices[it.name] = p;
+      }
+      double maxPrice = std::numeric_limits<double>::max();
+      for (int t : kept) {
+        auto f = prices.find(types[t].name);
+        if (f != prices.end() && f->second < maxPrice) maxPrice = f->second;
+      }
+      vector<int> k2;
+      for (int t : kept)
+        if (WorstLaunch(d, R, types[t], s2s) < maxPrice) k2.push_back(t);
+      if (hasMin && !HostMinValuesOK(d, hc, R, k2)) continue;
+      kept.swap(k2);
+      if (kept.empty()) continue;
+    }
+    if (s2s && cand.size() == 1) {
+      if (kept.size() < 15) continue;
+      kept.resize(std::min<size_t>(kept.size(), hasMin ? 100 : 15));
+    }
+    double best = std::numeric_limits<double>::max();
+    for (int t : kept) best = std::min(best, WorstLaunch(d, R, types[t], s2s));
+    r.decision = KP_DECISION_REPLACE;
+    r.nodepool = res->ncs[0].nodepool;
+    r.replacement_price = best;
+    r.savings = candPrice - best;
+    r.n_options = (uint32_t)kept.size();
+  }
+  // results and counters in device buffers, as the batched kernel leaves them
+  const size_t need = sizeof(SimOut) * std::max<uint32_t>(n_subsets, 1) + 256 + sizeof(uint64_t) * 8;
+  if (need > plan->batch_bytes) {
+    if (plan->batch.p) HIPCHK(hipFree(plan->batch.p));
+    plan->batch.p = nullptr;
+    HIPCHK(hipMalloc(&plan->batch.p, need));
+    plan->batch_bytes = need;
+  }
+  a = SimArgs{};
+  a.out = (SimOut*)plan->batch.p;
+  a.stats = (uint64_t*)((uint8_t*)plan->batch.p + ((sizeof(SimOut) * std::max<uint32_t>(n_subsets, 1) + 255) & ~(size_t)255));
+  uint64_t st[8] = {attempts, bytes, pops, 0, 0, 0, 0, 0};
+  if (n_subsets) HIPCHK(hipMemcpyAsync(a.out, outs.data(), sizeof(SimOut) * n_subsets, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipMemcpyAsync(a.stats, st, sizeof st, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  plan->general_ms = dev_ms;
+  return KP_OK;
+}
+
 static int32_t SimLaunchLocked(kp_cluster_plan* plan, const uint32_t* offsets, const uint32_t* nodes, uint32_t n_subsets,
                                int32_t multi_node, SimArgs& a_out) {
   kp_ctx* ctx = plan->ctx;
+  if (plan->general) return GeneralSimLocked(plan, offsets, nodes, n_subsets, multi_node, a_out);
   if (offsets[0] != 0) return fail(KP_E_INVAL, "offsets[0] != 0");
   const uint32_t n_flat = offsets[n_subsets];
   if (n_flat && !nodes) return fail(KP_E_INVAL, "null nodes");
@@ -3540,7 +3917,7 @@ int32_t kp_cluster_simulate(kp_cluster_plan* plan, const uint32_t* offsets, cons
   auto t0 = std::chrono::steady_clock::now();
   if (!plan || (n_subsets && (!offsets || !out))) return fail(KP_E_INVAL, "null argument");
   kp_ctx* ctx = plan->ctx;
-  std::lock_guard<std::mutex> lock(ctx->mu);
+  std::lock_guard<std::recursive_mutex> lock(ctx->mu);
   HIPCHK(hipSetDevice(ctx->device));
   if (stats) memset(stats, 0, sizeof *stats);
   if (n_subsets == 0) return KP_OK;
@@ -3552,8 +3929,8 @@ int32_t kp_cluster_simulate(kp_cluster_plan* plan, const uint32_t* offsets, cons
   HIPCHK(hipMemcpyAsync(out, a.out, sizeof(SimOut) * n_subsets, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(kst, a.stats, sizeof kst, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
-  float ms = 0;
-  HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+  float ms = (float)plan->general_ms;
+  if (!plan->general) HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
   for (uint32_t s = 0; s < n_subsets; s++)
     if (out[s].n_pods == 0xFFFFFFFFu) return fail(KP_E_DEVICE, "subset %u overflowed the pod queue", s);
   if (stats) {
@@ -3663,7 +4040,7 @@ int32_t kp_consolidate_argmin(kp_cluster_plan* plan, kp_comm* comm, const uint32
   if (!plan || !best || (n_subsets && !offsets)) return fail(KP_E_INVAL, "null argument");
   if (comm && comm->ctx->device != plan->ctx->device) return fail(KP_E_INVAL, "comm and plan are on different GPUs");
   kp_ctx* ctx = plan->ctx;
-  std::lock_guard<std::mutex> lock(ctx->mu);
+  std::lock_guard<std::recursive_mutex> lock(ctx->mu);
   HIPCHK(hipSetDevice(ctx->device));
   if (stats) memset(stats, 0, sizeof *stats);
   hipStream_t st = ctx->stream;
@@ -3702,7 +4079,8 @@ int32_t kp_consolidate_argmin(kp_cluster_plan* plan, kp_comm* comm, const uint32
     HIPCHK(hipMemcpyAsync(recs.data(), mine, sizeof(CommBest), hipMemcpyDeviceToHost, st));
   }
   HIPCHK(hipStreamSynchronize(st));
-  if (n_subsets) HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+  if (n_subsets && plan->general) ms = (float)plan->general_ms;
+  else if (n_subsets) HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
   for (int i = 0; i < nr; i++)
     if (recs[i].counts[3]) return fail(KP_E_DEVICE, "rank %d: %llu subsets overflowed the pod queue", i,
                                        (unsigned long long)recs[i].counts[3]);

@@ -1596,8 +1596,6 @@ int32_t kpo_simulate_batch(const kp_cluster* cl, const uint32_t* offsets, const 
                            int32_t multi_node, kp_sim_result* out, kp_solve_stats* stats) {
   auto t0 = std::chrono::steady_clock::now();
   if (!cl || !offsets || !out || (!cl->catalog_descs && cl->n_catalogs)) return KP_E_INVAL;
-  for (uint32_t i = 0; i < cl->n_shapes; i++)
-    if (cl->shapes[i].n_topology_spread) return KP_E_UNSUPPORTED;  // cluster pods are not in kp_cluster as bound pods
   Catalogs cats;
   for (uint32_t i = 0; i < cl->n_catalogs; i++) cats.push_back(CatalogFromABI(cl->catalog_descs[i]));
   std::vector<Requirements> nodeLabels(cl->n_nodes);
@@ -1639,6 +1637,16 @@ int32_t kpo_simulate_batch(const kp_cluster* cl, const uint32_t* offsets, const 
         kind.push_back(0);
       }
     for (uint32_t c : cand) inS[c] = 0;
+    // Topology.countDomains lists every pod bound to a node except the pods being scheduled: the pods of the
+    // remaining nodes are the bound pods (their shape's namespace and labels)
+    std::vector<kp_bound_pod> bound;
+    for (size_t e = 0; e < exIdx.size(); e++) {
+      const kp_cluster_node& n = cl->nodes[exIdx[e]];
+      for (uint32_t j = 0; j < n.n_pods; j++) {
+        const kp_pod_shape& sh = cl->shapes[cl->pods[n.pods[j]].shape];
+        bound.push_back({sh.namespace_, sh.labels, sh.n_labels, (uint32_t)e});
+      }
+    }
     r.n_pods = (uint32_t)pods.size();
     kp_solve_in in;
     memset(&in, 0, sizeof in);
@@ -1653,6 +1661,8 @@ int32_t kpo_simulate_batch(const kp_cluster* cl, const uint32_t* offsets, const 
     in.pods = pods.data();
     in.n_pods = (uint32_t)pods.size();
     in.max_instance_types = 100;
+    in.bound_pods = bound.data();
+    in.n_bound_pods = (uint32_t)bound.size();
     kpo_result* res = nullptr;
     int32_t rc = SolveCore(cats, &in, &res);
     if (rc) return rc;
