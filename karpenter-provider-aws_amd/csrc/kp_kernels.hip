@@ -1331,6 +1331,7 @@ __device__ __noinline__ int fast_lane(uint64_t kargs, int32_t LDS* s_dyn_arg, ui
       qw_epoch = S->qw_epoch[lane];
   uint64_t bytes = 0, attempts = 0, scanned = 0, starts = 0, fcyc[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   int pops = 0, handoff = -1, fb = -1;
+  int n_buf = 0, buf_pod = 0, buf_pl = 0;  // placements not yet written (lane i: the i-th)
     const bool tmg = A->timing != 0;
     uint64_t ft = tmg ? __builtin_amdgcn_s_memtime() : 0;
 #define FTF(i)                                               \
@@ -1479,10 +1480,18 @@ if (A->timing) {                                            \
       for (int base = start; base < n_nc && placed == -1 && !bail; base += 64) {
         const int i = base + lane;
         bool cand = false, tag = false;
-        int nc = 0;
+        const int nc = i < n_nc ? ord[i] : 0;
         int32_t ver = 0;
+        // speculative loads of the first position's NodeClaim (the usual winner), issued ahead of the pre-check
+        // gathers (and outside their lane-divergent block) so that the two round trips overlap
+        const int nc0 = __builtin_amdgcn_readlane(nc, 0);
+        const KReqs* cr0 = kreq_at(A->nc_reqs, nc0);
+        const uint64_t hm0 = cr0->hmin & cr0->present;
+        const int cat0 = A->nc_cat[nc0];
+        const uint64_t X00 = lane < D.TW ? A->nc_X[(size_t)nc0 * D.TW + lane] : 0;
+        const int64_t rq0 = lane < KP_NRES ? A->nc_requests[(size_t)nc0 * KP_NRES + lane] : 0;
+        const int32_t j00 = lane < KP_NRES ? A->nc_fitj[(size_t)nc0 * KP_NRES + lane] : 0;
         if (i < n_nc) {
-          nc = ord[i];
           // every gather issued unconditionally: one round trip
           const int32_t fl = nc < A->ncc ? A->nc_fail[(size_t)sl * A->ncc + nc] : -2;
           ver = A->nc_ver[nc];
@@ -1497,14 +1506,6 @@ if (A->timing) {                                            \
           cand = fit && fl != ver && fl != NC_NEVER && ((tolmask >> ts) & 1);
           tag = cand && fl >= NC_MERGED;
         }
-        // speculative loads of the first position's NodeClaim (the usual winner): they overlap the pre-checks
-        const int nc0 = __builtin_amdgcn_readlane(nc, 0);
-        const KReqs* cr0 = kreq_at(A->nc_reqs, nc0);
-        const uint64_t hm0 = cr0->hmin & cr0->present;
-        const int cat0 = A->nc_cat[nc0];
-        const uint64_t X00 = lane < D.TW ? A->nc_X[(size_t)nc0 * D.TW + lane] : 0;
-        const int64_t rq0 = lane < KP_NRES ? A->nc_requests[(size_t)nc0 * KP_NRES + lane] : 0;
-        const int32_t j00 = lane < KP_NRES ? A->nc_fitj[(size_t)nc0 * KP_NRES + lane] : 0;
         if (lane == 0) scanned += min(64, n_nc - base);
         if (lane == 0) bytes += (uint64_t)min(64, n_nc - base) * (12 + 16 * A->n_req_res);
         uint64_t cm = __ballot(cand);
@@ -1584,10 +1585,15 @@ if (A->timing) {                                            \
               if (TOPO && A->n_tk) store_tcodes(A->n_tk, A->tk_keys, A->nc_tcode, A->hnc_stride, rv, m_v, ncx);
               if (lane == 0 && ncx < A->ncc) A->nc_fail[(size_t)sl * A->ncc + ncx] = NC_MERGED;
             }
-            if (lane < D.TW) A->nc_X[(size_t)ncx * D.TW + lane] = X;
-            if (lane < KP_NRES) {
-              A->nc_requests[(size_t)ncx * KP_NRES + lane] = q_lane;
-              A->nc_fitj[(size_t)ncx * KP_NRES + lane] = fl_fitj[lane];
+            // the remaining types and threshold indices are stored only when they changed (the append path
+            // usually leaves both as they were): fewer vector-memory operations ahead of the next pod's loads
+            const int32_t fj = lane < KP_NRES ? fl_fitj[lane] : 0;
+            if (__ballot(lane < D.TW && X != X0)) {
+              if (lane < D.TW) A->nc_X[(size_t)ncx * D.TW + lane] = X;
+            }
+            if (lane < KP_NRES) A->nc_requests[(size_t)ncx * KP_NRES + lane] = q_lane;
+            if (__ballot(lane < KP_NRES && fj != j0_lane)) {
+              if (lane < KP_NRES) A->nc_fitj[(size_t)ncx * KP_NRES + lane] = fj;
             }
             if (lane == 0) {
               npods[ncx] += 1;
@@ -1616,12 +1622,26 @@ if (A->timing) {                                            \
       if (lane == 0) {
         A->cur_nc[2 * sl] = wpos;
         A->cur_nc[2 * sl + 1] = a_cur_prev_stamp;
-        A->placement[pod] = placed;
-        A->events[n_ev] = pod;
       }
-      n_ev++;
+      // placement / events: buffered one pod per lane, written 64 at a time (nothing reads them before the
+      // fast lane returns)
+      if (lane == n_buf) {
+        buf_pod = pod;
+        buf_pl = placed;
+      }
+      if (++n_buf == 64) {
+        A->placement[buf_pod] = buf_pl;
+        A->events[n_ev + lane] = buf_pod;
+        n_ev += 64;
+        n_buf = 0;
+      }
       FT(5);
     }
+    if (lane < n_buf) {
+      A->placement[buf_pod] = buf_pl;
+      A->events[n_ev + lane] = buf_pod;
+    }
+    n_ev += n_buf;
 #undef FT
 #undef FTF
   
