@@ -212,6 +212,19 @@ typedef struct kp_topology_spread {
   kp_label_selector selector;
 } kp_topology_spread;
 
+/* corev1.PodAffinityTerm (ABI v6): anti-affinity on the hostname key (upstream TopologyGroup of
+ * TopologyTypePodAntiAffinity, and the inverse groups bound pods' required terms create). Other topology keys, pod
+ * affinity and namespaceSelector return KP_E_UNSUPPORTED. */
+typedef struct kp_pod_affinity_term {
+  const char* topology_key;
+  kp_label_selector selector;
+  const char* const* namespaces;  /* n_namespaces == 0: the pod's own namespace */
+  uint32_t n_namespaces;
+  int32_t weight;                 /* preferred terms: WeightedPodAffinityTerm.weight */
+  int32_t has_namespace_selector; /* != 0: namespaceSelector set (unsupported) */
+  int32_t reserved_;
+} kp_pod_affinity_term;
+
 /* A container port with hostPort != 0, as upstream scheduling.GetHostPorts reads it (HostPortUsage). Two entries
  * conflict when protocol and port are equal and either IP is unspecified (0.0.0.0 / ::) or both IPs are equal. */
 enum kp_protocol { KP_PROTO_TCP = 0, KP_PROTO_UDP = 1, KP_PROTO_SCTP = 2 };
@@ -245,6 +258,16 @@ typedef struct kp_pod_shape {
    * allowedTopologies, resolved by the caller), appended to every required node-affinity term (one term is
    * created when the pod has none) before scheduling. */
   const kp_requirement* volume_requirements;
+  /* podAntiAffinity required / preferred terms and podAffinity (required / preferred: unsupported). Preferred
+   * terms act as required until Preferences.Relax removes them, heaviest first. */
+  const kp_pod_affinity_term* required_anti_affinity;
+  const kp_pod_affinity_term* preferred_anti_affinity;
+  const kp_pod_affinity_term* required_affinity;   /* podAffinity: KP_E_UNSUPPORTED when present */
+  const kp_pod_affinity_term* preferred_affinity;
+  uint32_t n_required_anti_affinity;
+  uint32_t n_preferred_anti_affinity;
+  uint32_t n_required_affinity;
+  uint32_t n_preferred_affinity;
 } kp_pod_shape;
 
 /* A pod already bound to a node of the cluster: what upstream Topology.countDomains lists (through the
@@ -254,6 +277,11 @@ typedef struct kp_bound_pod {
   const kp_label* labels;
   uint32_t n_labels;
   uint32_t node;  /* index into kp_solve_in.existing */
+  /* ABI v6: its required podAntiAffinity terms (Topology.updateInverseAntiAffinity: pods the selector selects
+   * avoid the bound pod's domain) */
+  const kp_pod_affinity_term* anti_affinity;
+  uint32_t n_anti_affinity;
+  uint32_t reserved_;
 } kp_bound_pod;
 
 typedef struct kp_pod {

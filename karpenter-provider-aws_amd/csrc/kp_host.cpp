@@ -1233,6 +1233,19 @@ std::map<string, string> LabelMap(const kp_label* l, uint32_t n) {
 // device encoding: one group per distinct (key, maxSkew, namespace, selector, node filter, policies) in order
 // of first appearance over the pods; dictionary-key groups keep a count per value ordinal + a registered-
 // domain mask, hostname groups a saturating u8 count per node (existing positions, then NodeClaims).
+// A pod's podAntiAffinity terms in one list: required terms, then preferred ones (spec order).
+const kp_pod_affinity_term* AntiTermAt(const kp_pod_shape& sh, int a) {
+  return a < (int)sh.n_required_anti_affinity ? &sh.required_anti_affinity[a]
+                                              : &sh.preferred_anti_affinity[a - (int)sh.n_required_anti_affinity];
+}
+int32_t CheckAntiTerm(const kp_pod_affinity_term& t, const char* who, uint32_t i) {
+  if (t.has_namespace_selector) return fail(KP_E_UNSUPPORTED, "%s %u: pod anti-affinity namespaceSelector", who, i);
+  if (!t.topology_key || string(t.topology_key) != kHostname)
+    return fail(KP_E_UNSUPPORTED, "%s %u: pod anti-affinity on topology key %s (hostname only)", who, i,
+                t.topology_key ? t.topology_key : "");
+  return KP_OK;
+}
+
 // HostPortUsage.Conflicts as bit masks. Bits: U(g) per (protocol, port) group g some unspecified-IP entry names,
 // S(g, ip) per specific entry. An entry (g, unspecified) conflicts with every used bit of g and adds U(g); an
 // entry (g, ip) conflicts with U(g) and S(g, ip) and adds S(g, ip) — HostPort.Matches (same protocol and port, and
@@ -1298,7 +1311,16 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
   cp.sl_own_n.assign(SL, 0);
   cp.sl_topo_keys.assign(SL, 0);
   bool any = false;
-  for (uint32_t s = 0; s < in->n_shapes; s++) any |= in->shapes[s].n_topology_spread > 0;
+  for (uint32_t s = 0; s < in->n_shapes; s++)
+    any |= in->shapes[s].n_topology_spread + in->shapes[s].n_required_anti_affinity +
+               in->shapes[s].n_preferred_anti_affinity > 0;
+  for (uint32_t b = 0; b < in->n_bound_pods; b++) {
+    for (uint32_t j = 0; j < in->bound_pods[b].n_anti_affinity; j++) {
+      const int32_t rc = CheckAntiTerm(in->bound_pods[b].anti_affinity[j], "bound pod", b);
+      if (rc) return rc;
+    }
+    any |= in->bound_pods[b].n_anti_affinity > 0;
+  }
   if (!any) return KP_OK;
   vector<int> ex_pos(in->n_existing);
   for (int e = 0; e < E; e++) ex_pos[cp.ex_input[e]] = e;
@@ -1365,6 +1387,9 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
   std::map<string, uint64_t> node_domains;
   vector<int> g_shape;  // shape that created the group (its tolerations / filter)
   vector<const kp_topology_spread*> g_spec;
+  vector<const kp_label_selector*> g_sel;   // every group: its selector
+  vector<std::set<string>> g_nss;           // namespaces it selects in (spread: the owner's)
+  vector<char> g_inverse;                   // inverse anti-affinity group (bound pods own it; never recorded)
   // group identity per (shape, spread index)
   vector<vector<int>> sgroup(in->n_shapes);
   vector<char> seen(in->n_shapes, 0);
@@ -1389,6 +1414,9 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
     ids[id] = g;
     g_shape.push_back((int)s);
     g_spec.push_back(&t);
+    g_sel.push_back(&t.selector);
+    g_nss.push_back({sh.namespace_ ? sh.namespace_ : ""});
+    g_inverse.push_back(0);
     int k = -1, row = -1;
     if (key == kHostname) {
       row = cp.GH++;
@@ -1466,6 +1494,52 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
     }
     return g;
   };
+  // TopologyTypePodAntiAffinity on the hostname key, as a hostname row whose acceptance test is count == 0 (the
+  // pre-pass test count + self <= maxSkew with self = 0, maxSkew = 0); no node filter; identity = (type, key,
+  // namespaces, selector). countDomains: bound pods it selects, per node. inverse: a bound pod's own required term
+  // (updateInverseAntiAffinity): its counts are the owners' nodes, it constrains the pods it selects, and no
+  // placement records into it.
+  auto nss_of = [](const kp_pod_affinity_term& t, const char* pod_ns) {
+    std::set<string> n;
+    for (uint32_t i = 0; i < t.n_namespaces; i++) n.insert(t.namespaces[i] ? t.namespaces[i] : "");
+    if (n.empty()) n.insert(pod_ns ? pod_ns : "");
+    return n;
+  };
+  auto anti_group = [&](const kp_pod_affinity_term& t, const std::set<string>& nss, bool inverse) -> int {
+    string id = string(inverse ? "inv|" : "anti|") + (t.topology_key ? t.topology_key : "") + "|";
+    for (auto& n : nss) id += n + ",";
+    id += "|" + SelectorCanon(t.selector);
+    auto it = ids.find(id);
+    if (it != ids.end()) return it->second;
+    const int g = cp.G++;
+    ids[id] = g;
+    g_shape.push_back(-1);
+    g_spec.push_back(nullptr);
+    g_sel.push_back(&t.selector);
+    g_nss.push_back(nss);
+    g_inverse.push_back(inverse ? 1 : 0);
+    const int row = cp.GH++;
+    cp.tg_key.push_back(-1);
+    cp.tg_row.push_back(row);
+    cp.tg_maxskew.push_back(0);
+    cp.tg_mindom.push_back(0);
+    cp.tg_term_base.push_back((int32_t)cp.tg_terms.size());
+    cp.tg_aff.push_back(0);
+    cp.tg_nterm.push_back(0);
+    cp.tg_filt_tol.push_back(~0ull);
+    cp.tg_reg.push_back(0);
+    for (int b = 0; b < 64; b++) cp.tg_cnt.push_back(0);
+    cp.hcnt0.resize((size_t)cp.GH * std::max(E, 1), 0);
+    if (!inverse)
+      for (auto& bs : bsets) {
+        if (!nss.count(bs.ns) || !SelectorMatches(t.selector, bs.labels)) continue;
+        for (const uint32_t ni : bs.nodes) {
+          uint8_t& c = cp.hcnt0[(size_t)row * std::max(E, 1) + ex_pos[ni]];
+          if (c < 255) c++;
+        }
+      }
+    return g;
+  };
   for (uint32_t p = 0; p < in->n_pods; p++) {  // NewTopology: Update(pod) in pod order
     const uint32_t s = in->pods[p].shape;
     if (seen[s]) continue;
@@ -1475,6 +1549,21 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
       const int g = group_of(s, (int)j);
       if (g < 0) return KP_E_UNSUPPORTED;
       sgroup[s].push_back(g);
+    }
+    for (uint32_t a = 0; a < sh.n_required_anti_affinity + sh.n_preferred_anti_affinity; a++) {
+      const kp_pod_affinity_term& t = *AntiTermAt(sh, (int)a);
+      sgroup[s].push_back(anti_group(t, nss_of(t, sh.namespace_), false));
+    }
+  }
+  vector<int> inverse_groups;  // updateInverseAffinities: after the batch's groups
+  for (uint32_t b = 0; b < in->n_bound_pods; b++) {
+    const kp_bound_pod& bp = in->bound_pods[b];
+    for (uint32_t j = 0; j < bp.n_anti_affinity; j++) {
+      const kp_pod_affinity_term& t = bp.anti_affinity[j];
+      const int g = anti_group(t, nss_of(t, bp.namespace_), true);
+      if (std::find(inverse_groups.begin(), inverse_groups.end(), g) == inverse_groups.end()) inverse_groups.push_back(g);
+      uint8_t& c = cp.hcnt0[(size_t)cp.tg_row[g] * std::max(E, 1) + ex_pos[bp.node]];
+      if (c < 255) c++;
     }
   }
   if (cp.G == 0) return KP_OK;
@@ -1494,22 +1583,23 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
   }
   vector<vector<int>> recs(in->n_shapes);
   static const vector<uint32_t> kNone;
+  vector<vector<int>> inv_owned(in->n_shapes);  // inverse groups that select each shape
   for (int g = 0; g < cp.G; g++) {
-    const kp_pod_shape& owner = in->shapes[g_shape[g]];
-    const kp_label_selector& sel = g_spec[g]->selector;
-    const string ns = owner.namespace_ ? owner.namespace_ : "";
-    const vector<uint32_t>* cands;
+    const kp_label_selector& sel = *g_sel[g];
     if (sel.is_nil) continue;
-    if (sel.n_match_labels) {
-      auto it = by_label.find(ns + '\x01' + (sel.match_labels[0].key ? sel.match_labels[0].key : "") + '\x01' +
-                              (sel.match_labels[0].value ? sel.match_labels[0].value : ""));
-      cands = it == by_label.end() ? &kNone : &it->second;
-    } else {
-      auto it = by_ns.find(ns);
-      cands = it == by_ns.end() ? &kNone : &it->second;
+    for (const string& ns : g_nss[g]) {
+      const vector<uint32_t>* cands;
+      if (sel.n_match_labels) {
+        auto it = by_label.find(ns + '\x01' + (sel.match_labels[0].key ? sel.match_labels[0].key : "") + '\x01' +
+                                (sel.match_labels[0].value ? sel.match_labels[0].value : ""));
+        cands = it == by_label.end() ? &kNone : &it->second;
+      } else {
+        auto it = by_ns.find(ns);
+        cands = it == by_ns.end() ? &kNone : &it->second;
+      }
+      for (uint32_t s : *cands)
+        if (SelectorMatches(sel, shape_labels[s])) (g_inverse[g] ? inv_owned[s] : recs[s]).push_back(g);
     }
-    for (uint32_t s : *cands)
-      if (SelectorMatches(sel, shape_labels[s])) recs[s].push_back(g);
   }
   for (uint32_t s = 0; s < in->n_shapes; s++) {
     cp.shape_rec_base[s] = (int32_t)cp.rec_list.size();
@@ -1519,26 +1609,33 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
   // owned groups per shape-level: (group, self-selecting, podDomains mask over the key's value ordinals)
   for (uint32_t s = 0; s < in->n_shapes; s++) {
     const kp_pod_shape& sh = in->shapes[s];
-    if (!sh.n_topology_spread) continue;
-    if (sgroup[s].empty()) {  // shape without pods: no groups were created for it
+    const uint32_t n_terms = sh.n_topology_spread + sh.n_required_anti_affinity + sh.n_preferred_anti_affinity;
+    if (!n_terms && inv_owned[s].empty()) continue;
+    if (sgroup[s].empty() && n_terms) {  // shape without pods: no groups were created for it
       for (uint32_t j = 0; j < sh.n_topology_spread; j++) {
         const int g = group_of(s, (int)j);
         if (g < 0) return KP_E_UNSUPPORTED;
         sgroup[s].push_back(g);
       }
+      for (uint32_t a = 0; a < sh.n_required_anti_affinity + sh.n_preferred_anti_affinity; a++) {
+        const kp_pod_affinity_term& t = *AntiTermAt(sh, (int)a);
+        sgroup[s].push_back(anti_group(t, nss_of(t, sh.namespace_), false));
+      }
     }
     const std::map<string, string> lm = LabelMap(sh.labels, sh.n_labels);
     for (int l = 0; l < cp.shape_nlevels[s]; l++) {
       const int sl = cp.shape_level_base[s] + l;
-      const vector<int>& sp = spread_levels[s][l];
-      if (sp.size() > 8) return fail(KP_E_UNSUPPORTED, "> 8 topology spread constraints on one pod");
+      vector<int> sp = spread_levels[s][l];  // term ids, then the inverse groups selecting the shape (as -1 - g)
+      for (int g : inv_owned[s]) sp.push_back(-1 - g);
+      if (sp.size() > 8) return fail(KP_E_UNSUPPORTED, "> 8 topology constraints (spread / anti-affinity) on one pod");
       cp.sl_own_base[sl] = (int32_t)cp.own_group.size();
       cp.sl_own_n[sl] = (int32_t)sp.size();
       const KReqs strict = Compile(d, strict_levels[s][l]);
       for (int j : sp) {
-        const int g = sgroup[s][j];
+        const int g = j < 0 ? -1 - j : sgroup[s][j];
         cp.own_group.push_back(g);
-        cp.own_self.push_back(SelectorMatches(sh.topology_spread[j].selector, lm) ? 1 : 0);
+        // self: the spread's selector matches the pod (count + 1); anti-affinity accepts count == 0 only
+        cp.own_self.push_back(j >= 0 && j < (int)sh.n_topology_spread && SelectorMatches(sh.topology_spread[j].selector, lm) ? 1 : 0);
         const int k = cp.tg_key[g];
         uint64_t pd = 0;
         if (k >= 0) {
@@ -1574,7 +1671,8 @@ struct SolveRaw {
   vector<RawReqs> np_reqs;                        // per input NodePool (requirements + labels + nodepool key)
   vector<vector<TaintT>> np_taints;
   vector<vector<RawReqs>> levels, strict_levels;  // per shape: NewPodRequirements after successive Relax
-  vector<vector<vector<int>>> spread_levels;      // spreads (indices into topology_spread) per level
+  vector<vector<vector<int>>> spread_levels;      // per level: topology terms (j < n_topology_spread: spread j;
+                                                  // n_topology_spread + a: anti-affinity term a of AntiTerms)
   std::set<string> topo_keys;                     // non-hostname spread keys (need a dictionary id)
   vector<RawReqs> ex_labels;                      // per input existing node (hostname dropped)
 };
@@ -1665,6 +1763,12 @@ int32_t ParseSolve(const kp_solve_in* in, SolveRaw& raw) {
       if (key != kHostname) raw.topo_keys.insert(key);  // the key gets a dictionary id even if no value names it
     }
     if (sh.n_preferred_terms > 12) return fail(KP_E_UNSUPPORTED, "> 12 preferred terms");
+    if (sh.n_required_affinity || sh.n_preferred_affinity) return fail(KP_E_UNSUPPORTED, "shape %u: pod affinity", s);
+    if (sh.n_preferred_anti_affinity > 12) return fail(KP_E_UNSUPPORTED, "> 12 preferred anti-affinity terms");
+    for (uint32_t j = 0; j < sh.n_required_anti_affinity + sh.n_preferred_anti_affinity; j++) {
+      const int32_t rc = CheckAntiTerm(*AntiTermAt(sh, (int)j), "shape", s);
+      if (rc) return rc;
+    }
     RawReqs ns = LabelReqs(sh.node_selector, sh.n_node_selector, false);
     vector<RawReqs> req;
     for (uint32_t j = 0; j < sh.n_required_terms; j++) req.push_back(ParseReqs(sh.required_terms[j]));
@@ -1681,6 +1785,13 @@ int32_t ParseSolve(const kp_solve_in* in, SolveRaw& raw) {
     std::stable_sort(pref.begin(), pref.end(), byw);  // sort.Slice on <= 12 = insertion sort (stable)
     vector<int> spreads;
     for (uint32_t j = 0; j < sh.n_topology_spread; j++) spreads.push_back((int)j);
+    // preferred anti-affinity terms: removePreferredPodAntiAffinityTerm drops the heaviest first (sort.Slice by
+    // weight desc on <= 12 terms: insertion sort, stable)
+    vector<int> apref;
+    for (uint32_t a = 0; a < sh.n_preferred_anti_affinity; a++) apref.push_back((int)a);
+    std::stable_sort(apref.begin(), apref.end(), [&](int x, int y) {
+      return sh.preferred_anti_affinity[x].weight > sh.preferred_anti_affinity[y].weight;
+    });
     for (;;) {
       RawReqs r = ns;
       if (!pref.empty()) r.insert(r.end(), pref[0].second.begin(), pref[0].second.end());
@@ -1691,9 +1802,14 @@ int32_t ParseSolve(const kp_solve_in* in, SolveRaw& raw) {
       RawReqs strict = ns;  // NewStrictPodRequirements: without the preferred term
       if (!req.empty()) strict.insert(strict.end(), req[0].begin(), req[0].end());
       raw.strict_levels[s].push_back(std::move(strict));
-      raw.spread_levels[s].push_back(spreads);
+      vector<int> terms = spreads;  // spreads, required anti-affinity terms, remaining preferred ones
+      for (uint32_t a = 0; a < sh.n_required_anti_affinity; a++) terms.push_back((int)(sh.n_topology_spread + a));
+      for (int a : apref) terms.push_back((int)(sh.n_topology_spread + sh.n_required_anti_affinity) + a);
+      raw.spread_levels[s].push_back(terms);
       if (req.size() > 1) {
         req.erase(req.begin());
+      } else if (!apref.empty()) {
+        apref.erase(apref.begin());
       } else if (!pref.empty()) {
         pref.erase(pref.begin());
       } else {  // removeTopologySpreadScheduleAnyway: first ScheduleAnyway constraint, swapped with the last
@@ -3181,6 +3297,17 @@ struct OwnedCluster {
     }
     s.match_expressions = e;
   }
+  const kp_pod_affinity_term* Terms(const kp_pod_affinity_term* t, uint32_t n) {
+    kp_pod_affinity_term* o = A(t, n);
+    for (uint32_t i = 0; o && i < n; i++) {
+      o[i].topology_key = S(o[i].topology_key);
+      Selector(o[i].selector);
+      const char** v = (const char**)A(o[i].namespaces, o[i].n_namespaces);
+      for (uint32_t j = 0; v && j < o[i].n_namespaces; j++) v[j] = S(v[j]);
+      o[i].namespaces = v;
+    }
+    return o;
+  }
   void Node(kp_existing_node& n) {
     n.name = S(n.name);
     n.labels = Labels(n.labels, n.n_labels);
@@ -3231,6 +3358,10 @@ struct OwnedCluster {
       kp_requirements vr{x.volume_requirements, x.n_volume_requirements, 0};
       Reqs(vr);
       x.volume_requirements = vr.items;
+      x.required_anti_affinity = Terms(x.required_anti_affinity, x.n_required_anti_affinity);
+      x.preferred_anti_affinity = Terms(x.preferred_anti_affinity, x.n_preferred_anti_affinity);
+      x.required_affinity = Terms(x.required_affinity, x.n_required_affinity);
+      x.preferred_affinity = Terms(x.preferred_affinity, x.n_preferred_affinity);
     }
     cl.shapes = sh;
     cl.pods = A(in->pods, in->n_pods);
@@ -3320,7 +3451,9 @@ int32_t kp_cluster_prepare(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan** 
   if (!ctx || !cl || !out) return fail(KP_E_INVAL, "null argument");
   if (cl->n_nodes && !cl->nodes) return fail(KP_E_INVAL, "null nodes");
   bool topo = false;
-  for (uint32_t i = 0; i < cl->n_shapes; i++) topo |= cl->shapes[i].n_topology_spread > 0;
+  for (uint32_t i = 0; i < cl->n_shapes; i++)
+    topo |= cl->shapes[i].n_topology_spread > 0 || cl->shapes[i].n_required_anti_affinity > 0 ||
+            cl->shapes[i].n_preferred_anti_affinity > 0;
   if (topo) return PrepareGeneral(ctx, cl, out, t0);
   std::lock_guard<std::recursive_mutex> lock(ctx->mu);
   HIPCHK(hipSetDevice(ctx->device));
@@ -3692,7 +3825,8 @@ static int32_t GeneralSimLocked(kp_cluster_plan* plan, const uint32_t* offsets, 
         const uint32_t p = n.pods[j];
         if (p >= cl.n_pods || cl.pods[p].shape >= cl.n_shapes) return fail(KP_E_INVAL, "node %d: pod %u", exNode[e], p);
         const kp_pod_shape& sh = cl.shapes[cl.pods[p].shape];
-        bound.push_back({sh.namespace_, sh.labels, sh.n_labels, (uint32_t)e});
+        bound.push_back({sh.namespace_, sh.labels, sh.n_labels, (uint32_t)e, sh.required_anti_affinity,
+                         sh.n_required_anti_affinity, 0});
       }
     }
     for (uint32_t c : cand) inS[c] = 0;

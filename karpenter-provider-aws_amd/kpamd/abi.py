@@ -116,6 +116,12 @@ class TopologySpread(C.Structure):
                 ("node_taints_policy", C.c_int32), ("reserved_", C.c_int32), ("selector", LabelSelector)]
 
 
+class PodAffinityTerm(C.Structure):
+    _fields_ = [("topology_key", C.c_char_p), ("selector", LabelSelector), ("namespaces", C.POINTER(C.c_char_p)),
+                ("n_namespaces", C.c_uint32), ("weight", C.c_int32), ("has_namespace_selector", C.c_int32),
+                ("reserved_", C.c_int32)]
+
+
 class HostPort(C.Structure):
     _fields_ = [("ip", C.c_char_p), ("port", C.c_int32), ("protocol", C.c_int32)]
 
@@ -131,12 +137,18 @@ class PodShape(C.Structure):
                 ("n_topology_spread", C.c_uint32), ("n_labels", C.c_uint32),
                 ("topology_spread", C.POINTER(TopologySpread)), ("namespace_", C.c_char_p),
                 ("labels", C.POINTER(Label)), ("host_ports", C.POINTER(HostPort)), ("n_host_ports", C.c_uint32),
-                ("n_volume_requirements", C.c_uint32), ("volume_requirements", C.POINTER(Requirement))]
+                ("n_volume_requirements", C.c_uint32), ("volume_requirements", C.POINTER(Requirement)),
+                ("required_anti_affinity", C.POINTER(PodAffinityTerm)),
+                ("preferred_anti_affinity", C.POINTER(PodAffinityTerm)),
+                ("required_affinity", C.POINTER(PodAffinityTerm)), ("preferred_affinity", C.POINTER(PodAffinityTerm)),
+                ("n_required_anti_affinity", C.c_uint32), ("n_preferred_anti_affinity", C.c_uint32),
+                ("n_required_affinity", C.c_uint32), ("n_preferred_affinity", C.c_uint32)]
 
 
 class BoundPod(C.Structure):
     _fields_ = [("namespace_", C.c_char_p), ("labels", C.POINTER(Label)), ("n_labels", C.c_uint32),
-                ("node", C.c_uint32)]
+                ("node", C.c_uint32), ("anti_affinity", C.POINTER(PodAffinityTerm)), ("n_anti_affinity", C.c_uint32),
+                ("reserved_", C.c_uint32)]
 
 
 class Pod(C.Structure):
@@ -361,9 +373,23 @@ class Arena:
         hps, nhp = self.host_ports(getattr(sh, "host_ports", None))
         vol = list(getattr(sh, "volume_requirements", None) or [])
         vreqs = self.arr(Requirement, [self.requirement(r) for r in vol])
+        ra, nra = self.affinity_terms(getattr(sh, "required_anti_affinity", None))
+        pa, npa = self.affinity_terms(getattr(sh, "preferred_anti_affinity", None))
+        rf, nrf = self.affinity_terms(getattr(sh, "required_affinity", None))
+        pf, npf = self.affinity_terms(getattr(sh, "preferred_affinity", None))
         return PodShape(self.resources(sh.requests), ns, nns, len(sh.required_terms), terms, prefs,
                         len(sh.preferred_terms), ntol, tols, len(sh.topology_spread), nl, spreads,
-                        self.s(sh.namespace), labels, hps, nhp, len(vol), vreqs)
+                        self.s(sh.namespace), labels, hps, nhp, len(vol), vreqs, ra, pa, rf, pf, nra, npa, nrf, npf)
+
+    def affinity_terms(self, terms):
+        """[model.PodAffinityTerm] -> kp_pod_affinity_term[]."""
+        terms = list(terms or [])
+        out = []
+        for t in terms:
+            nss = self.arr(C.c_char_p, [self.s(n) for n in (t.namespaces or [])])
+            out.append(PodAffinityTerm(self.s(t.topology_key), self.selector(t.selector), nss, len(t.namespaces or []),
+                                       int(t.weight), 1 if t.namespace_selector else 0, 0))
+        return self.arr(PodAffinityTerm, out), len(terms)
 
     def host_ports(self, hps):
         """[(hostIP, hostPort, protocol)] -> kp_host_port[] (hostIP None/"" = 0.0.0.0, protocol None = TCP)."""
@@ -388,9 +414,11 @@ class Arena:
 
     def bound_pods(self, bps):
         out = []
-        for ns, labels, node in bps:
+        for bp in bps:  # (namespace, labels, existing idx[, required anti-affinity terms])
+            ns, labels, node = bp[0], bp[1], bp[2]
             la, nl = self.labels(labels)
-            out.append(BoundPod(self.s(ns), la, nl, int(node)))
+            aa, naa = self.affinity_terms(bp[3] if len(bp) > 3 else None)
+            out.append(BoundPod(self.s(ns), la, nl, int(node), aa, naa, 0))
         return self.arr(BoundPod, out), len(bps)
 
     def existing_node(self, n, extra_ports=()):

@@ -78,6 +78,16 @@ class TopologySpread:
 
 
 @dataclass
+class PodAffinityTerm:
+    """corev1.PodAffinityTerm (+ weight for a WeightedPodAffinityTerm). namespaces empty = the pod's namespace."""
+    topology_key: str
+    selector: Optional[LabelSelector] = None
+    namespaces: List[str] = field(default_factory=list)
+    weight: int = 0
+    namespace_selector: bool = False
+
+
+@dataclass
 class PodShape:
     requests: Dict[str, int]
     node_selector: Dict[str, str] = field(default_factory=dict)
@@ -89,6 +99,10 @@ class PodShape:
     namespace: str = "default"
     host_ports: List[Tuple[str, int, str]] = field(default_factory=list)  # GetHostPorts: (hostIP, hostPort, protocol)
     volume_requirements: List[Req] = field(default_factory=list)         # VolumeTopology.Inject input
+    required_anti_affinity: List[PodAffinityTerm] = field(default_factory=list)
+    preferred_anti_affinity: List[PodAffinityTerm] = field(default_factory=list)
+    required_affinity: List[PodAffinityTerm] = field(default_factory=list)   # unsupported on the device path
+    preferred_affinity: List[PodAffinityTerm] = field(default_factory=list)
 
 
 @dataclass

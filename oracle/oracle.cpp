@@ -703,6 +703,35 @@ struct Spread {
   int when, affinityPolicy, taintsPolicy;
   Selector sel;
 };
+// corev1.PodAffinityTerm of a podAntiAffinity (TopologyTypePodAntiAffinity)
+struct AntiTerm {
+  string key;
+  Selector sel;
+  set<string> namespaces;  // buildNamespaceList: the term's namespaces, else the pod's own
+  int32_t weight;
+};
+static Selector SelectorFromABI(const kp_label_selector& s) {
+  Selector o;
+  o.nil = s.is_nil != 0;
+  for (uint32_t k = 0; k < s.n_match_labels; k++)
+    o.reqs.push_back({s.match_labels[k].key, KP_SEL_IN, {s.match_labels[k].value ? s.match_labels[k].value : ""}});
+  for (uint32_t k = 0; k < s.n_match_expressions; k++) {
+    const kp_selector_requirement& e = s.match_expressions[k];
+    SelReq r{e.key, e.op, {}};
+    for (uint32_t v = 0; v < e.n_values; v++) r.values.insert(e.values[v] ? e.values[v] : "");
+    o.reqs.push_back(r);
+  }
+  return o;
+}
+static AntiTerm AntiFromABI(const kp_pod_affinity_term& t, const string& podNs) {
+  AntiTerm a;
+  a.key = t.topology_key ? t.topology_key : "";
+  a.sel = SelectorFromABI(t.selector);
+  for (uint32_t i = 0; i < t.n_namespaces; i++) a.namespaces.insert(t.namespaces[i] ? t.namespaces[i] : "");
+  if (a.namespaces.empty()) a.namespaces.insert(podNs);
+  a.weight = t.weight;
+  return a;
+}
 
 // UP scheduling.HostPort / GetHostPorts / HostPortUsage (hostportusage.go): hostIP "" -> 0.0.0.0, protocol "" -> TCP,
 // hostPort 0 skipped; Matches = same protocol and port, and an unspecified IP on either side or equal IPs
@@ -761,6 +790,7 @@ struct PodState {
   ResourceList requests;
   vector<Toleration> tolerations;
   vector<Spread> spreads;
+  vector<AntiTerm> antiRequired, antiPreferred;  // podAntiAffinity (preferred: relaxed heaviest first)
   string ns;
   map<string, string> labels;
   vector<HostPort> hostPorts;
@@ -799,6 +829,13 @@ static bool Relax(PodState& p) {
     p.required_terms.erase(p.required_terms.begin());
     return true;
   }
+  // removePreferredPodAffinityTerm: pod affinity is not supported (the batch is refused)
+  if (!p.antiPreferred.empty()) {  // removePreferredPodAntiAffinityTerm: sort.Slice by weight desc (<= 12: stable)
+    std::stable_sort(p.antiPreferred.begin(), p.antiPreferred.end(),
+                     [](const AntiTerm& a, const AntiTerm& b) { return a.weight > b.weight; });
+    p.antiPreferred.erase(p.antiPreferred.begin());
+    return true;
+  }
   if (!p.preferred.empty()) {
     std::stable_sort(p.preferred.begin(), p.preferred.end(),
                      [](const std::pair<int, Requirements>& a, const std::pair<int, Requirements>& b) {
@@ -831,6 +868,8 @@ static const Requirement& GetOr(const Requirements& r, const string& key, Requir
 // ---------------------------------------------------------------------------------------------
 struct TopologyGroup {
   string key, id;
+  int type = 0;  // 0 TopologyTypeSpread, 2 TopologyTypePodAntiAffinity
+  set<string> nss;  // anti-affinity: the term's namespaces
   int32_t maxSkew, minDomains;
   string ns;
   Selector sel;
@@ -840,7 +879,9 @@ struct TopologyGroup {
   map<string, int32_t> domains;
   set<int> owners;
 
-  bool Selects(const string& pns, const map<string, string>& labels) const { return pns == ns && sel.Matches(labels); }
+  bool Selects(const string& pns, const map<string, string>& labels) const {
+    return (type == 2 ? nss.count(pns) > 0 : pns == ns) && sel.Matches(labels);
+  }
   bool FilterMatches(const vector<Taint>& taints, const Requirements& reqs, bool allow) const {
     bool aff = true;
     if (affinityHonor && !filter.empty()) {
@@ -866,8 +907,17 @@ struct TopologyGroup {
     if (minDomains >= 0 && num < minDomains) mn = 0;
     return mn;
   }
+  // nextDomainAntiAffinity: every known domain the pod admits whose count is zero
+  Requirement NextDomainAnti(const Requirement& podDomains) const {
+    vector<string> options;
+    for (auto& kv : domains)
+      if (Has(podDomains, kv.first) && kv.second == 0) options.push_back(kv.first);
+    if (options.empty()) return NewRequirement(key, KP_OP_DOES_NOT_EXIST, {}, -1);
+    return NewRequirement(key, KP_OP_IN, options, -1);
+  }
   // nextDomainTopologySpread
   Requirement NextDomain(bool self, const Requirement& podDomains, const Requirement& nodeDomains) const {
+    if (type == 2) return NextDomainAnti(podDomains);
     const int64_t mn = DomainMinCount(podDomains);
     string minDomain;
     bool found = false;
@@ -898,6 +948,7 @@ struct BoundPod {
   string ns;
   map<string, string> labels;
   int node;  // input index of the existing node
+  vector<AntiTerm> anti;  // its required podAntiAffinity terms (inverse groups)
 };
 struct NodeView {  // what countDomains reads of a node
   string name;
@@ -965,6 +1016,48 @@ struct Topology {
     return g;
   }
 
+  // NewTopologyGroup(TopologyTypePodAntiAffinity, ...): no node filter, every known domain registered; identity =
+  // (type, key, namespaces, selector)
+  std::unique_ptr<TopologyGroup> NewAntiGroup(const AntiTerm& t) const {
+    auto g = std::make_unique<TopologyGroup>();
+    g->type = 2;
+    g->key = t.key;
+    g->maxSkew = std::numeric_limits<int32_t>::max();
+    g->minDomains = -1;
+    g->sel = t.sel;
+    g->nss = t.namespaces;
+    g->affinityHonor = false;
+    g->taintHonor = false;
+    string id = "anti|" + t.key + "|";
+    for (auto& n : t.namespaces) id += n + ",";
+    g->id = id + "|" + t.sel.Canon();
+    auto dg = domainGroups.find(t.key);
+    if (dg != domainGroups.end())
+      for (auto& kv : dg->second) g->domains.emplace(kv.first, 0);
+    return g;
+  }
+  vector<std::unique_ptr<TopologyGroup>> inverse;  // updateInverseAntiAffinity: bound pods' required terms
+  map<string, TopologyGroup*> inverseById;
+  void BuildInverse() {
+    for (auto& bp : bound)
+      for (auto& t : bp.anti) {
+        auto g = NewAntiGroup(t);
+        TopologyGroup* tg;
+        auto it = inverseById.find(g->id);
+        if (it == inverseById.end()) {
+          tg = g.get();
+          inverseById[g->id] = tg;
+          inverse.push_back(std::move(g));
+        } else {
+          tg = it->second;
+        }
+        const NodeView& n = nodes[(size_t)bp.node];
+        auto lv = n.labels.find(t.key);
+        if (lv != n.labels.end()) tg->domains[lv->second]++;
+        else if (t.key == kLabelHostname) tg->domains[n.name]++;
+      }
+  }
+
   // countDomains: pods already running that the group selects, on nodes the filter admits; then every
   // existing node's domain value with a zero count.
   void CountDomains(TopologyGroup& g) const {
@@ -990,8 +1083,11 @@ struct Topology {
   // Topology.Update: the pod stops owning every group, then owns the groups of its current spreads
   void Update(const PodState& p) {
     for (auto& g : groups) g->owners.erase(p.index);
-    for (auto& s : p.spreads) {
-      auto g = NewGroup(p, s);
+    vector<std::unique_ptr<TopologyGroup>> fresh;
+    for (auto& s : p.spreads) fresh.push_back(NewGroup(p, s));
+    for (auto& t : p.antiRequired) fresh.push_back(NewAntiGroup(t));
+    for (auto& t : p.antiPreferred) fresh.push_back(NewAntiGroup(t));
+    for (auto& g : fresh) {
       auto it = byId.find(g->id);
       TopologyGroup* tg;
       if (it == byId.end()) {
@@ -1005,19 +1101,27 @@ struct Topology {
       tg->owners.insert(p.index);
     }
   }
-  void Register(const string& key, const string& domain) {
+  void Register(const string& key, const string& domain) {  // topologies and inverseTopologies alike
     for (auto& g : groups)
+      if (g->key == key) g->domains.emplace(domain, 0);
+    for (auto& g : inverse)
       if (g->key == key) g->domains.emplace(domain, 0);
   }
   void Unregister(const string& key, const string& domain) {
     for (auto& g : groups)
       if (g->key == key) g->domains.erase(domain);
+    for (auto& g : inverse)
+      if (g->key == key) g->domains.erase(domain);
   }
   // AddRequirements: every group the pod owns narrows its key to the chosen domain
   bool AddRequirements(const PodState& p, const Requirements& nodeReqs, Requirements* out) const {
     *out = nodeReqs;
-    for (auto& g : groups) {
-      if (!g->owners.count(p.index)) continue;
+    vector<const TopologyGroup*> matching;  // getMatchingTopologies: owned groups, then inverse groups selecting p
+    for (auto& g : groups)
+      if (g->owners.count(p.index)) matching.push_back(g.get());
+    for (auto& g : inverse)
+      if (g->Selects(p.ns, p.labels)) matching.push_back(g.get());
+    for (const TopologyGroup* g : matching) {
       Requirement t1, t2;
       const Requirement& podDomains = GetOr(p.strict, g->key, t1);
       const Requirement& nodeDomains = GetOr(nodeReqs, g->key, t2);
@@ -1032,6 +1136,11 @@ struct Topology {
     for (auto& g : groups) {
       if (!g->Selects(p.ns, p.labels) || !g->FilterMatches(taints, reqs, allow)) continue;
       auto it = reqs.find(g->key);
+      if (g->type == 2) {  // anti-affinity blocks every domain the node could be in: Record(domains.Values()...)
+        if (it != reqs.end())
+          for (auto& v : it->second.values) g->domains[v]++;
+        continue;
+      }
       if (it == reqs.end() || it->second.Len() != 1) continue;
       g->domains[*it->second.values.begin()]++;
     }
@@ -1343,10 +1452,17 @@ static int32_t SolveCore(const Catalogs& cats, const kp_solve_in* in, kpo_result
     bp.ns = b.namespace_ ? b.namespace_ : "";
     for (uint32_t j = 0; j < b.n_labels; j++) bp.labels[b.labels[j].key] = b.labels[j].value ? b.labels[j].value : "";
     bp.node = (int)b.node;
+    for (uint32_t j = 0; j < b.n_anti_affinity; j++) {
+      if (b.anti_affinity[j].has_namespace_selector) return KP_E_UNSUPPORTED;
+      bp.anti.push_back(AntiFromABI(b.anti_affinity[j], bp.ns));
+    }
     topo.bound.push_back(std::move(bp));
   }
   bool anySpread = false;
-  for (uint32_t i = 0; i < in->n_shapes; i++) anySpread |= in->shapes[i].n_topology_spread > 0;
+  for (uint32_t i = 0; i < in->n_shapes; i++)
+    anySpread |= in->shapes[i].n_topology_spread > 0 || in->shapes[i].n_required_anti_affinity > 0 ||
+                 in->shapes[i].n_preferred_anti_affinity > 0;
+  for (uint32_t i = 0; i < in->n_bound_pods; i++) anySpread |= in->bound_pods[i].n_anti_affinity > 0;
   if (anySpread)
     for (uint32_t i = 0; i < in->n_nodepools; i++) {
       const kp_nodepool& np = in->nodepools[i];
@@ -1424,6 +1540,15 @@ static int32_t SolveCore(const Catalogs& cats, const kp_solve_in* in, kpo_result
     }
     ps.ns = sh.namespace_ ? sh.namespace_ : "";
     for (uint32_t j = 0; j < sh.n_labels; j++) ps.labels[sh.labels[j].key] = sh.labels[j].value ? sh.labels[j].value : "";
+    if (sh.n_required_affinity || sh.n_preferred_affinity) return KP_E_UNSUPPORTED;  // podAffinity: not restated
+    for (uint32_t j = 0; j < sh.n_required_anti_affinity; j++) {
+      if (sh.required_anti_affinity[j].has_namespace_selector) return KP_E_UNSUPPORTED;
+      ps.antiRequired.push_back(AntiFromABI(sh.required_anti_affinity[j], ps.ns));
+    }
+    for (uint32_t j = 0; j < sh.n_preferred_anti_affinity; j++) {
+      if (sh.preferred_anti_affinity[j].has_namespace_selector) return KP_E_UNSUPPORTED;
+      ps.antiPreferred.push_back(AntiFromABI(sh.preferred_anti_affinity[j], ps.ns));
+    }
     for (uint32_t j = 0; j < sh.n_topology_spread; j++) {
       const kp_topology_spread& t = sh.topology_spread[j];
       Spread sp;
@@ -1450,6 +1575,7 @@ static int32_t SolveCore(const Catalogs& cats, const kp_solve_in* in, kpo_result
   // NewTopology: Update(pod) for every pod of the batch, in input order; then NewExistingNode adds
   // hostname In {HostName()} to each existing node and registers it with the hostname topologies.
   for (auto& ps : pods) topo.Update(ps);
+  topo.BuildInverse();  // updateInverseAffinities: after the batch's own groups
   for (auto& n : s.existing) {
     const NodeView& v = topo.nodes[(size_t)n.index];
     auto h = v.labels.find(kLabelHostname);
@@ -1644,7 +1770,8 @@ int32_t kpo_simulate_batch(const kp_cluster* cl, const uint32_t* offsets, const 
       const kp_cluster_node& n = cl->nodes[exIdx[e]];
       for (uint32_t j = 0; j < n.n_pods; j++) {
         const kp_pod_shape& sh = cl->shapes[cl->pods[n.pods[j]].shape];
-        bound.push_back({sh.namespace_, sh.labels, sh.n_labels, (uint32_t)e});
+        bound.push_back({sh.namespace_, sh.labels, sh.n_labels, (uint32_t)e, sh.required_anti_affinity,
+                         sh.n_required_anti_affinity, 0});
       }
     }
     r.n_pods = (uint32_t)pods.size();

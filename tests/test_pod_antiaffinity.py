@@ -1,0 +1,194 @@
+"""Pod anti-affinity on the hostname key (ABI v6): upstream TopologyGroup of TopologyTypePodAntiAffinity
+(nextDomainAntiAffinity: only domains whose count is zero; Topology.Record counts every selected pod on its node),
+the inverse groups a bound pod's required terms create (Topology.updateInverseAntiAffinity: pods the selector selects
+avoid the bound pod's node), and Preferences.Relax's removePreferredPodAntiAffinityTerm (heaviest first, before the
+preferred node-affinity terms). Docs: R:website/content/en/preview/concepts/scheduling.md:395-428 (the anti-affinity
+example "avoid running on any node with a pod labeled app=inflate": one replica per node). Other topology keys, pod
+affinity and namespaceSelector return KP_E_UNSUPPORTED (the Go path runs).
+
+Known answers on the CPU oracle, device == oracle under -m gpu (Solve and consolidation simulations). Parity
+unpinned beyond the written semantics (upstream core is not in the container)."""
+import copy
+import os
+import sys
+
+import numpy as np
+import pytest
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from test_hostports_volumes import POOL_REQS, small_problem  # noqa: E402
+
+HOST = "kubernetes.io/hostname"
+
+
+def anti(app, weight=0, key=HOST, namespaces=()):
+    from kpamd.model import LabelSelector, PodAffinityTerm
+    return PodAffinityTerm(key, LabelSelector({"app": app}), list(namespaces), weight)
+
+
+def shape(app, cpu_m=500, mem_mi=512, req=(), pref=(), **kw):
+    from kpamd import synth
+    from kpamd.model import PodShape
+    return PodShape(synth.req_res(cpu_m, mem_mi), labels={"app": app}, required_anti_affinity=list(req),
+                    preferred_anti_affinity=list(pref), **kw)
+
+
+def oracle(prob):
+    from oracle import pyoracle
+    return pyoracle.solve(prob)
+
+
+def m5_node(catalog, name="node-a"):
+    from kpamd import synth
+    from kpamd.model import ExistingNode
+    it = catalog[[i for i, t in enumerate(catalog) if t.name == "m5.xlarge"][0]]
+    return ExistingNode(name, synth.node_labels(it, 0, "on-demand", "default", name), it.allocatable())
+
+
+# ---- oracle known answers (CPU) -------------------------------------------------------------------------------
+def test_one_replica_per_node(catalog):
+    r = oracle(small_problem(catalog, [shape("web", req=[anti("web")])], [5]))
+    assert len(r["nodeclaims"]) == 5
+    assert sorted(r["placement"].tolist()) == [0, 1, 2, 3, 4]
+
+
+def test_selector_not_matching_itself(catalog):
+    r = oracle(small_problem(catalog, [shape("web", req=[anti("db")])], [5]))
+    assert len(r["nodeclaims"]) == 1
+
+
+def test_other_pods_share(catalog):
+    # web pods spread one per node; db pods (no terms) fill in beside them
+    r = oracle(small_problem(catalog, [shape("web", 1000, 1024, req=[anti("web")]), shape("db", 250, 256)], [3, 6]))
+    pl = r["placement"].tolist()
+    assert len(set(pl[:3])) == 3
+    assert set(pl[3:]) <= set(pl[:3])
+
+
+def test_existing_node_with_selected_pod(catalog):
+    node = m5_node(catalog)
+    prob = small_problem(catalog, [shape("web", req=[anti("web")]), shape("api")], [1, 1], existing=[node])
+    prob.bound_pods = [("default", {"app": "web"}, 0)]
+    pl = oracle(prob)["placement"].tolist()
+    assert pl[0] >= 0   # a web pod already runs on node-a
+    assert pl[1] == -2  # no terms: the existing node
+
+
+def test_inverse_anti_affinity_of_a_bound_pod(catalog):
+    # the bound pod on node-a refuses company from app=web: a web pod without terms of its own avoids node-a
+    node = m5_node(catalog)
+    prob = small_problem(catalog, [shape("web"), shape("api")], [1, 1], existing=[node])
+    prob.bound_pods = [("default", {"app": "cache"}, 0, [anti("web")])]
+    pl = oracle(prob)["placement"].tolist()
+    assert pl[0] >= 0 and pl[1] == -2
+
+
+def test_namespaces(catalog):
+    # the term selects app=web in namespace "other" only: default-namespace web pods are not counted
+    r = oracle(small_problem(catalog, [shape("web", req=[anti("web", namespaces=["other"])])], [4]))
+    assert len(r["nodeclaims"]) == 1
+
+
+def test_preferred_term_relaxed_when_it_cannot_hold(catalog):
+    # a cpu limit allows two NodeClaims: the third web pod fails with its preferred term, which Relax drops, and
+    # it then joins one of the two
+    from kpamd.model import NodePool
+    prob = small_problem(catalog, [shape("web", 1000, 1024, pref=[anti("web", 50)])], [3])
+    prob.nodepools = [NodePool("default", 0, 0, list(POOL_REQS) +
+                               [("karpenter.k8s.aws/instance-cpu", "In", ["4"])], limits={"cpu": 8000})]
+    pl = oracle(prob)["placement"].tolist()
+    assert pl[0] != pl[1] and pl[2] in (pl[0], pl[1])
+
+
+def test_unsupported_variants(catalog):
+    import kpamd
+    from kpamd.model import LabelSelector, PodAffinityTerm
+    zone = small_problem(catalog, [shape("web", req=[anti("web", key="topology.kubernetes.io/zone")])], [2])
+    assert kpamd.validate(zone) == kpamd.abi.KP_E_UNSUPPORTED
+    aff = small_problem(catalog, [shape("web", required_affinity=[PodAffinityTerm(HOST, LabelSelector({"app": "x"}))])], [2])
+    assert kpamd.validate(aff) == kpamd.abi.KP_E_UNSUPPORTED
+    nss = small_problem(catalog, [shape("web", req=[PodAffinityTerm(HOST, LabelSelector({"app": "web"}),
+                                                                    namespace_selector=True)])], [2])
+    assert kpamd.validate(nss) == kpamd.abi.KP_E_UNSUPPORTED
+    assert kpamd.validate(small_problem(catalog, [shape("web", req=[anti("web")])], [2])) == 0
+
+
+# ---- randomized (oracle on CPU, device under -m gpu) --------------------------------------------------------------
+def add_anti(prob, seed, p=0.4):
+    rng = np.random.default_rng(seed)
+    prob = copy.deepcopy(prob)
+    apps = [f"app-{i}" for i in range(4)]
+    for i, sh in enumerate(prob.shapes):
+        sh.labels = dict(sh.labels or {}, app=apps[i % 4])
+        if rng.random() < p:
+            sh.required_anti_affinity = [anti(str(rng.choice(apps)))]
+        if rng.random() < 0.2:
+            sh.preferred_anti_affinity = [anti(str(rng.choice(apps)), int(rng.integers(1, 100)))
+                                          for _ in range(int(rng.integers(1, 3)))]
+    bound = []
+    for e in range(len(prob.existing)):
+        for _ in range(int(rng.integers(0, 3))):
+            terms = [anti(str(rng.choice(apps)))] if rng.random() < 0.3 else []
+            bound.append(("default", {"app": str(rng.choice(apps))}, e, terms))
+    prob.bound_pods = bound
+    return prob
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_random_oracle_and_host_compile(catalog, seed):
+    import kpamd
+    from kpamd import synth
+    prob = add_anti(synth.random_problem(catalog, 500 + seed, n_types=120, n_pods=200, n_pools=3,
+                                         n_existing=[0, 10][seed % 2], n_shapes=14), seed)
+    r = oracle(prob)
+    assert len(r["placement"]) == prob.n_pods
+    assert kpamd.validate(prob) == 0
+
+
+@pytest.mark.gpu
+def test_gpu_known_answers(ctx, catalog):
+    import kpamd
+    from test_gpu_parity import check_same
+    from kpamd.model import NodePool
+    node = m5_node(catalog)
+    probs = [small_problem(catalog, [shape("web", req=[anti("web")])], [5]),
+             small_problem(catalog, [shape("web", 1000, 1024, req=[anti("web")]), shape("db", 250, 256)], [3, 6])]
+    p = small_problem(catalog, [shape("web", req=[anti("web")]), shape("api")], [1, 1], existing=[node])
+    p.bound_pods = [("default", {"app": "web"}, 0)]
+    probs.append(p)
+    p = small_problem(catalog, [shape("web"), shape("api")], [1, 1], existing=[m5_node(catalog)])
+    p.bound_pods = [("default", {"app": "cache"}, 0, [anti("web")])]
+    probs.append(p)
+    p = small_problem(catalog, [shape("web", 1000, 1024, pref=[anti("web", 50)])], [3])
+    p.nodepools = [NodePool("default", 0, 0, list(POOL_REQS) + [("karpenter.k8s.aws/instance-cpu", "In", ["4"])],
+                            limits={"cpu": 8000})]
+    probs.append(p)
+    for prob in probs:
+        check_same(kpamd.Scheduler(ctx, prob).solve(), oracle(prob))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(8))
+def test_gpu_random_anti_affinity(ctx, catalog, seed):
+    import kpamd
+    from kpamd import synth
+    from test_gpu_parity import check_same
+    prob = add_anti(synth.random_problem(catalog, 600 + seed, n_types=150, n_pods=300, n_pools=3,
+                                         n_existing=[0, 6, 30][seed % 3], n_shapes=18), seed)
+    check_same(kpamd.Scheduler(ctx, prob).solve(), oracle(prob))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(3))
+def test_gpu_consolidation_anti_affinity(ctx, catalog, seed):
+    from kpamd import synth
+    from test_gpu_consolidation import check
+    cl = synth.random_cluster(catalog, 70 + seed, n_nodes=[20, 30, 40][seed])
+    rng = np.random.default_rng(seed)
+    for i, sh in enumerate(cl.shapes):
+        sh.labels = {"app": f"app-{i % 4}"}
+        if rng.random() < 0.4:
+            sh.required_anti_affinity = [anti(f"app-{int(rng.integers(0, 4))}")]
+    subs = synth.consolidation_subsets(cl, 15, seed=seed, max_size=min(12, len(cl.nodes)))
+    subs += [[c] for c in cl.candidates[:10]]
+    check(ctx, cl, subs, multi_node=bool(seed % 2))
