@@ -212,9 +212,9 @@ typedef struct kp_topology_spread {
   kp_label_selector selector;
 } kp_topology_spread;
 
-/* corev1.PodAffinityTerm (ABI v6): anti-affinity on the hostname key (upstream TopologyGroup of
- * TopologyTypePodAntiAffinity, and the inverse groups bound pods' required terms create). Other topology keys, pod
- * affinity and namespaceSelector return KP_E_UNSUPPORTED. */
+/* corev1.PodAffinityTerm (ABI v6): pod affinity / anti-affinity on the hostname key (upstream TopologyGroup of
+ * TopologyTypePodAffinity / TopologyTypePodAntiAffinity, and the inverse groups bound pods' required anti-affinity
+ * terms create). Other topology keys and namespaceSelector return KP_E_UNSUPPORTED. */
 typedef struct kp_pod_affinity_term {
   const char* topology_key;
   kp_label_selector selector;
@@ -258,11 +258,11 @@ typedef struct kp_pod_shape {
    * allowedTopologies, resolved by the caller), appended to every required node-affinity term (one term is
    * created when the pod has none) before scheduling. */
   const kp_requirement* volume_requirements;
-  /* podAntiAffinity required / preferred terms and podAffinity (required / preferred: unsupported). Preferred
-   * terms act as required until Preferences.Relax removes them, heaviest first. */
+  /* podAntiAffinity and podAffinity required / preferred terms. Preferred terms act as required until
+   * Preferences.Relax removes them, heaviest first (affinity terms before anti-affinity terms). */
   const kp_pod_affinity_term* required_anti_affinity;
   const kp_pod_affinity_term* preferred_anti_affinity;
-  const kp_pod_affinity_term* required_affinity;   /* podAffinity: KP_E_UNSUPPORTED when present */
+  const kp_pod_affinity_term* required_affinity;
   const kp_pod_affinity_term* preferred_affinity;
   uint32_t n_required_anti_affinity;
   uint32_t n_preferred_anti_affinity;

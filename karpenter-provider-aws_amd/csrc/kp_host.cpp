@@ -1234,14 +1234,29 @@ std::map<string, string> LabelMap(const kp_label* l, uint32_t n) {
 // of first appearance over the pods; dictionary-key groups keep a count per value ordinal + a registered-
 // domain mask, hostname groups a saturating u8 count per node (existing positions, then NodeClaims).
 // A pod's podAntiAffinity terms in one list: required terms, then preferred ones (spec order).
-const kp_pod_affinity_term* AntiTermAt(const kp_pod_shape& sh, int a) {
-  return a < (int)sh.n_required_anti_affinity ? &sh.required_anti_affinity[a]
-                                              : &sh.preferred_anti_affinity[a - (int)sh.n_required_anti_affinity];
+// A pod's inter-pod terms in one list: required anti-affinity, preferred anti-affinity, required affinity, preferred
+// affinity (spec order within each). *aff: the term is a podAffinity term.
+uint32_t PodTermCount(const kp_pod_shape& sh) {
+  return sh.n_required_anti_affinity + sh.n_preferred_anti_affinity + sh.n_required_affinity + sh.n_preferred_affinity;
+}
+const kp_pod_affinity_term* PodTermAt(const kp_pod_shape& sh, int a, bool* aff = nullptr) {
+  const uint32_t n[4] = {sh.n_required_anti_affinity, sh.n_preferred_anti_affinity, sh.n_required_affinity,
+                         sh.n_preferred_affinity};
+  const kp_pod_affinity_term* p[4] = {sh.required_anti_affinity, sh.preferred_anti_affinity, sh.required_affinity,
+                                      sh.preferred_affinity};
+  for (int i = 0; i < 4; i++) {
+    if (a < (int)n[i]) {
+      if (aff) *aff = i >= 2;
+      return &p[i][a];
+    }
+    a -= (int)n[i];
+  }
+  return nullptr;
 }
 int32_t CheckAntiTerm(const kp_pod_affinity_term& t, const char* who, uint32_t i) {
-  if (t.has_namespace_selector) return fail(KP_E_UNSUPPORTED, "%s %u: pod anti-affinity namespaceSelector", who, i);
+  if (t.has_namespace_selector) return fail(KP_E_UNSUPPORTED, "%s %u: pod (anti-)affinity namespaceSelector", who, i);
   if (!t.topology_key || string(t.topology_key) != kHostname)
-    return fail(KP_E_UNSUPPORTED, "%s %u: pod anti-affinity on topology key %s (hostname only)", who, i,
+    return fail(KP_E_UNSUPPORTED, "%s %u: pod (anti-)affinity on topology key %s (hostname only)", who, i,
                 t.topology_key ? t.topology_key : "");
   return KP_OK;
 }
@@ -1312,8 +1327,7 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
   cp.sl_topo_keys.assign(SL, 0);
   bool any = false;
   for (uint32_t s = 0; s < in->n_shapes; s++)
-    any |= in->shapes[s].n_topology_spread + in->shapes[s].n_required_anti_affinity +
-               in->shapes[s].n_preferred_anti_affinity > 0;
+    any |= in->shapes[s].n_topology_spread + PodTermCount(in->shapes[s]) > 0;
   for (uint32_t b = 0; b < in->n_bound_pods; b++) {
     for (uint32_t j = 0; j < in->bound_pods[b].n_anti_affinity; j++) {
       const int32_t rc = CheckAntiTerm(in->bound_pods[b].anti_affinity[j], "bound pod", b);
@@ -1505,8 +1519,10 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
     if (n.empty()) n.insert(pod_ns ? pod_ns : "");
     return n;
   };
-  auto anti_group = [&](const kp_pod_affinity_term& t, const std::set<string>& nss, bool inverse) -> int {
-    string id = string(inverse ? "inv|" : "anti|") + (t.topology_key ? t.topology_key : "") + "|";
+  // TopologyTypePodAffinity (aff): the same hostname row with maxSkew = -1, whose pre-pass test is count > 0, or,
+  // while no domain has a count (tg_reg bit 0 clear), the self-selecting pod's bootstrap (nextDomainAffinity).
+  auto anti_group = [&](const kp_pod_affinity_term& t, const std::set<string>& nss, bool inverse, bool aff = false) -> int {
+    string id = string(inverse ? "inv|" : aff ? "aff|" : "anti|") + (t.topology_key ? t.topology_key : "") + "|";
     for (auto& n : nss) id += n + ",";
     id += "|" + SelectorCanon(t.selector);
     auto it = ids.find(id);
@@ -1521,7 +1537,7 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
     const int row = cp.GH++;
     cp.tg_key.push_back(-1);
     cp.tg_row.push_back(row);
-    cp.tg_maxskew.push_back(0);
+    cp.tg_maxskew.push_back(aff ? -1 : 0);
     cp.tg_mindom.push_back(0);
     cp.tg_term_base.push_back((int32_t)cp.tg_terms.size());
     cp.tg_aff.push_back(0);
@@ -1536,6 +1552,7 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
         for (const uint32_t ni : bs.nodes) {
           uint8_t& c = cp.hcnt0[(size_t)row * std::max(E, 1) + ex_pos[ni]];
           if (c < 255) c++;
+          cp.tg_reg[g] = 1;  // hostname rows: bit 0 = some domain has a count (affinity bootstrap)
         }
       }
     return g;
@@ -1550,9 +1567,10 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
       if (g < 0) return KP_E_UNSUPPORTED;
       sgroup[s].push_back(g);
     }
-    for (uint32_t a = 0; a < sh.n_required_anti_affinity + sh.n_preferred_anti_affinity; a++) {
-      const kp_pod_affinity_term& t = *AntiTermAt(sh, (int)a);
-      sgroup[s].push_back(anti_group(t, nss_of(t, sh.namespace_), false));
+    for (uint32_t a = 0; a < PodTermCount(sh); a++) {
+      bool aff = false;
+      const kp_pod_affinity_term& t = *PodTermAt(sh, (int)a, &aff);
+      sgroup[s].push_back(anti_group(t, nss_of(t, sh.namespace_), false, aff));
     }
   }
   vector<int> inverse_groups;  // updateInverseAffinities: after the batch's groups
@@ -1564,6 +1582,7 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
       if (std::find(inverse_groups.begin(), inverse_groups.end(), g) == inverse_groups.end()) inverse_groups.push_back(g);
       uint8_t& c = cp.hcnt0[(size_t)cp.tg_row[g] * std::max(E, 1) + ex_pos[bp.node]];
       if (c < 255) c++;
+      cp.tg_reg[g] = 1;
     }
   }
   if (cp.G == 0) return KP_OK;
@@ -1609,7 +1628,7 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
   // owned groups per shape-level: (group, self-selecting, podDomains mask over the key's value ordinals)
   for (uint32_t s = 0; s < in->n_shapes; s++) {
     const kp_pod_shape& sh = in->shapes[s];
-    const uint32_t n_terms = sh.n_topology_spread + sh.n_required_anti_affinity + sh.n_preferred_anti_affinity;
+    const uint32_t n_terms = sh.n_topology_spread + PodTermCount(sh);
     if (!n_terms && inv_owned[s].empty()) continue;
     if (sgroup[s].empty() && n_terms) {  // shape without pods: no groups were created for it
       for (uint32_t j = 0; j < sh.n_topology_spread; j++) {
@@ -1617,9 +1636,10 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
         if (g < 0) return KP_E_UNSUPPORTED;
         sgroup[s].push_back(g);
       }
-      for (uint32_t a = 0; a < sh.n_required_anti_affinity + sh.n_preferred_anti_affinity; a++) {
-        const kp_pod_affinity_term& t = *AntiTermAt(sh, (int)a);
-        sgroup[s].push_back(anti_group(t, nss_of(t, sh.namespace_), false));
+      for (uint32_t a = 0; a < PodTermCount(sh); a++) {
+        bool aff = false;
+        const kp_pod_affinity_term& t = *PodTermAt(sh, (int)a, &aff);
+        sgroup[s].push_back(anti_group(t, nss_of(t, sh.namespace_), false, aff));
       }
     }
     const std::map<string, string> lm = LabelMap(sh.labels, sh.n_labels);
@@ -1634,8 +1654,13 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
       for (int j : sp) {
         const int g = j < 0 ? -1 - j : sgroup[s][j];
         cp.own_group.push_back(g);
-        // self: the spread's selector matches the pod (count + 1); anti-affinity accepts count == 0 only
-        cp.own_self.push_back(j >= 0 && j < (int)sh.n_topology_spread && SelectorMatches(sh.topology_spread[j].selector, lm) ? 1 : 0);
+        // self: the spread's / affinity term's selector matches the pod (spread: count + 1; affinity: it may
+        // bootstrap); anti-affinity accepts count == 0 only
+        bool aff = false;
+        const kp_pod_affinity_term* pt = j >= (int)sh.n_topology_spread ? PodTermAt(sh, j - (int)sh.n_topology_spread, &aff) : nullptr;
+        cp.own_self.push_back(j >= 0 && j < (int)sh.n_topology_spread ? (SelectorMatches(sh.topology_spread[j].selector, lm) ? 1 : 0)
+                              : (pt && aff && nss_of(*pt, sh.namespace_).count(sh.namespace_ ? sh.namespace_ : "") &&
+                                 SelectorMatches(pt->selector, lm)) ? 1 : 0);
         const int k = cp.tg_key[g];
         uint64_t pd = 0;
         if (k >= 0) {
@@ -1763,10 +1788,10 @@ int32_t ParseSolve(const kp_solve_in* in, SolveRaw& raw) {
       if (key != kHostname) raw.topo_keys.insert(key);  // the key gets a dictionary id even if no value names it
     }
     if (sh.n_preferred_terms > 12) return fail(KP_E_UNSUPPORTED, "> 12 preferred terms");
-    if (sh.n_required_affinity || sh.n_preferred_affinity) return fail(KP_E_UNSUPPORTED, "shape %u: pod affinity", s);
-    if (sh.n_preferred_anti_affinity > 12) return fail(KP_E_UNSUPPORTED, "> 12 preferred anti-affinity terms");
-    for (uint32_t j = 0; j < sh.n_required_anti_affinity + sh.n_preferred_anti_affinity; j++) {
-      const int32_t rc = CheckAntiTerm(*AntiTermAt(sh, (int)j), "shape", s);
+    if (sh.n_preferred_anti_affinity > 12 || sh.n_preferred_affinity > 12)
+      return fail(KP_E_UNSUPPORTED, "> 12 preferred pod (anti-)affinity terms");
+    for (uint32_t j = 0; j < PodTermCount(sh); j++) {
+      const int32_t rc = CheckAntiTerm(*PodTermAt(sh, (int)j), "shape", s);
       if (rc) return rc;
     }
     RawReqs ns = LabelReqs(sh.node_selector, sh.n_node_selector, false);
@@ -1787,11 +1812,17 @@ int32_t ParseSolve(const kp_solve_in* in, SolveRaw& raw) {
     for (uint32_t j = 0; j < sh.n_topology_spread; j++) spreads.push_back((int)j);
     // preferred anti-affinity terms: removePreferredPodAntiAffinityTerm drops the heaviest first (sort.Slice by
     // weight desc on <= 12 terms: insertion sort, stable)
-    vector<int> apref;
+    vector<int> apref, fpref;  // removePreferredPodAffinityTerm, then removePreferredPodAntiAffinityTerm
     for (uint32_t a = 0; a < sh.n_preferred_anti_affinity; a++) apref.push_back((int)a);
     std::stable_sort(apref.begin(), apref.end(), [&](int x, int y) {
       return sh.preferred_anti_affinity[x].weight > sh.preferred_anti_affinity[y].weight;
     });
+    for (uint32_t a = 0; a < sh.n_preferred_affinity; a++) fpref.push_back((int)a);
+    std::stable_sort(fpref.begin(), fpref.end(), [&](int x, int y) {
+      return sh.preferred_affinity[x].weight > sh.preferred_affinity[y].weight;
+    });
+    const int nS = (int)sh.n_topology_spread, nRA = (int)sh.n_required_anti_affinity,
+              nPA = (int)sh.n_preferred_anti_affinity, nRF = (int)sh.n_required_affinity;
     for (;;) {
       RawReqs r = ns;
       if (!pref.empty()) r.insert(r.end(), pref[0].second.begin(), pref[0].second.end());
@@ -1802,12 +1833,16 @@ int32_t ParseSolve(const kp_solve_in* in, SolveRaw& raw) {
       RawReqs strict = ns;  // NewStrictPodRequirements: without the preferred term
       if (!req.empty()) strict.insert(strict.end(), req[0].begin(), req[0].end());
       raw.strict_levels[s].push_back(std::move(strict));
-      vector<int> terms = spreads;  // spreads, required anti-affinity terms, remaining preferred ones
-      for (uint32_t a = 0; a < sh.n_required_anti_affinity; a++) terms.push_back((int)(sh.n_topology_spread + a));
-      for (int a : apref) terms.push_back((int)(sh.n_topology_spread + sh.n_required_anti_affinity) + a);
+      vector<int> terms = spreads;  // spreads, required anti-affinity terms, remaining preferred ones, affinity alike
+      for (int a = 0; a < nRA; a++) terms.push_back(nS + a);
+      for (int a : apref) terms.push_back(nS + nRA + a);
+      for (int a = 0; a < nRF; a++) terms.push_back(nS + nRA + nPA + a);
+      for (int a : fpref) terms.push_back(nS + nRA + nPA + nRF + a);
       raw.spread_levels[s].push_back(terms);
       if (req.size() > 1) {
         req.erase(req.begin());
+      } else if (!fpref.empty()) {
+        fpref.erase(fpref.begin());
       } else if (!apref.empty()) {
         apref.erase(apref.begin());
       } else if (!pref.empty()) {
@@ -3452,8 +3487,7 @@ int32_t kp_cluster_prepare(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan** 
   if (cl->n_nodes && !cl->nodes) return fail(KP_E_INVAL, "null nodes");
   bool topo = false;
   for (uint32_t i = 0; i < cl->n_shapes; i++)
-    topo |= cl->shapes[i].n_topology_spread > 0 || cl->shapes[i].n_required_anti_affinity > 0 ||
-            cl->shapes[i].n_preferred_anti_affinity > 0;
+    topo |= cl->shapes[i].n_topology_spread > 0 || PodTermCount(cl->shapes[i]) > 0;
   if (topo) return PrepareGeneral(ctx, cl, out, t0);
   std::lock_guard<std::recursive_mutex> lock(ctx->mu);
   HIPCHK(hipSetDevice(ctx->device));

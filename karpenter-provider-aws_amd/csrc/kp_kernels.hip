@@ -1889,8 +1889,11 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
           s_tcnt[j][lane] = c;
           bytes += 64 * 4 + 16;
         }
+        // pod affinity (hostname row, maxSkew -1): self = the pod may bootstrap (it selects itself and no domain
+        // has a count yet, tg_reg bit 0)
+        const int self_eff = (k < 0 && mskew < 0) ? (self && !(a.tg_reg[g] & 1)) : self;
         if (lane == 0) {
-          s_town[j] = TopoOwn{g, self, k, a.tg_row[g], mskew, k >= 0 ? a.tkey_slot[k] : -1};
+          s_town[j] = TopoOwn{g, self_eff, k, a.tg_row[g], mskew, k >= 0 ? a.tkey_slot[k] : -1};
           s_tacc[j] = acc;
         }
       }
@@ -1921,8 +1924,10 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
         // when the node takes a pod, i.e. with its version); dictionary key: the node's domain is its label
         // value (or the key is undefined on it: incompatible), acceptable under the current counts
         for (int j = 0; j < own_n && cand; j++)
-          if (s_town[j].key < 0)
-            cand = (int)a.hcnt_ex[(size_t)s_town[j].row * a.n_existing + ec] + s_town[j].self <= s_town[j].maxskew;
+          if (s_town[j].key < 0) {
+            const int c = (int)a.hcnt_ex[(size_t)s_town[j].row * a.n_existing + ec];
+            cand = s_town[j].maxskew >= 0 ? c + s_town[j].self <= s_town[j].maxskew : (c > 0 || s_town[j].self);
+          }
         if (cand) iflags |= 1u << k;  // passes everything that does not depend on the zone counts
         for (int j = 0; j < own_n && cand; j++) {
           const TopoOwn& o = s_town[j];
@@ -2017,8 +2022,10 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
             cand = rq[r] + s_preq[r] <= mx[r];
           }
           for (int j = 0; j < own_n && cand; j++)  // hostname topologies, exact (count changes with the version)
-            if (s_town[j].key < 0)
-              cand = (int)a.hcnt_nc[(size_t)s_town[j].row * a.hnc_stride + nc] + s_town[j].self <= s_town[j].maxskew;
+            if (s_town[j].key < 0) {
+              const int c = (int)a.hcnt_nc[(size_t)s_town[j].row * a.hnc_stride + nc];
+              cand = s_town[j].maxskew >= 0 ? c + s_town[j].self <= s_town[j].maxskew : (c > 0 || s_town[j].self);
+            }
           if (cand) iflags |= 1u << k;  // passes everything that does not depend on the zone counts
           if (cand && !own_n && fl >= NC_MERGED) tflags |= 1u << k;  // shape-level already merged: append path
           for (int j = 0; j < own_n && cand; j++) {  // a NodeClaim pinned to one domain of a key can only take it
@@ -2169,6 +2176,8 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
               ok = merge_compatible(D, kreq_at(a.tmpl_reqs, tm), B, b_negop, true, m_v, rv, &slots[wave], vi);
               memo = !ok || !own_n;
               if (ok && own_n) ok = topo_narrow(D, own_n, s_town, s_tacc, s_tcnt, true, m_v, rv, vi);
+              for (int j = 0; j < own_n && ok; j++)  // a fresh node has no count: pod affinity only by bootstrap
+                if (s_town[j].key < 0 && s_town[j].maxskew < 0 && !s_town[j].self) ok = false;
               if (ok && a.tfeas && !own_n) {
                 // the template's types for this shape-level, precomputed (tmpl_feas_kernel, row-sharded over ranks):
                 // filter_types is a per-type filter, so (options after the limits) ∩ (filtered template) is the
@@ -2283,6 +2292,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
           if (lane == 0) {
             uint8_t* c = ex ? &a.hcnt_ex[(size_t)row * a.n_existing + idx] : &a.hcnt_nc[(size_t)row * a.hnc_stride + idx];
             if (*c < 255) *c += 1;
+            a.tg_reg[g] = 1;  // hostname rows: some domain has a count (ends pod-affinity bootstrap)
           }
         } else {
           const int k = a.tg_key[g];

@@ -791,6 +791,7 @@ struct PodState {
   vector<Toleration> tolerations;
   vector<Spread> spreads;
   vector<AntiTerm> antiRequired, antiPreferred;  // podAntiAffinity (preferred: relaxed heaviest first)
+  vector<AntiTerm> affRequired, affPreferred;    // podAffinity (same term shape)
   string ns;
   map<string, string> labels;
   vector<HostPort> hostPorts;
@@ -829,7 +830,12 @@ static bool Relax(PodState& p) {
     p.required_terms.erase(p.required_terms.begin());
     return true;
   }
-  // removePreferredPodAffinityTerm: pod affinity is not supported (the batch is refused)
+  if (!p.affPreferred.empty()) {  // removePreferredPodAffinityTerm: sort.Slice by weight desc (<= 12: stable)
+    std::stable_sort(p.affPreferred.begin(), p.affPreferred.end(),
+                     [](const AntiTerm& a, const AntiTerm& b) { return a.weight > b.weight; });
+    p.affPreferred.erase(p.affPreferred.begin());
+    return true;
+  }
   if (!p.antiPreferred.empty()) {  // removePreferredPodAntiAffinityTerm: sort.Slice by weight desc (<= 12: stable)
     std::stable_sort(p.antiPreferred.begin(), p.antiPreferred.end(),
                      [](const AntiTerm& a, const AntiTerm& b) { return a.weight > b.weight; });
@@ -868,7 +874,7 @@ static const Requirement& GetOr(const Requirements& r, const string& key, Requir
 // ---------------------------------------------------------------------------------------------
 struct TopologyGroup {
   string key, id;
-  int type = 0;  // 0 TopologyTypeSpread, 2 TopologyTypePodAntiAffinity
+  int type = 0;  // 0 TopologyTypeSpread, 1 TopologyTypePodAffinity, 2 TopologyTypePodAntiAffinity
   set<string> nss;  // anti-affinity: the term's namespaces
   int32_t maxSkew, minDomains;
   string ns;
@@ -880,7 +886,7 @@ struct TopologyGroup {
   set<int> owners;
 
   bool Selects(const string& pns, const map<string, string>& labels) const {
-    return (type == 2 ? nss.count(pns) > 0 : pns == ns) && sel.Matches(labels);
+    return (type != 0 ? nss.count(pns) > 0 : pns == ns) && sel.Matches(labels);
   }
   bool FilterMatches(const vector<Taint>& taints, const Requirements& reqs, bool allow) const {
     bool aff = true;
@@ -915,9 +921,32 @@ struct TopologyGroup {
     if (options.empty()) return NewRequirement(key, KP_OP_DOES_NOT_EXIST, {}, -1);
     return NewRequirement(key, KP_OP_IN, options, -1);
   }
+  // nextDomainAffinity: the known domains the pod admits that hold a selected pod; none and the pod selects itself:
+  // bootstrap with the first domain of podDomains ∩ nodeDomains and the first of podDomains (upstream iterates a
+  // map there: the lexicographically smallest, as everywhere in this oracle)
+  Requirement NextDomainAffinity(bool self, const Requirement& podDomains, const Requirement& nodeDomains) const {
+    vector<string> options;
+    for (auto& kv : domains)
+      if (Has(podDomains, kv.first) && kv.second > 0) options.push_back(kv.first);
+    if (options.empty() && self) {
+      for (auto& kv : domains)
+        if (Has(podDomains, kv.first) && Has(nodeDomains, kv.first)) {
+          options.push_back(kv.first);
+          break;
+        }
+      for (auto& kv : domains)
+        if (Has(podDomains, kv.first)) {
+          if (std::find(options.begin(), options.end(), kv.first) == options.end()) options.push_back(kv.first);
+          break;
+        }
+    }
+    if (options.empty()) return NewRequirement(key, KP_OP_DOES_NOT_EXIST, {}, -1);
+    return NewRequirement(key, KP_OP_IN, options, -1);
+  }
   // nextDomainTopologySpread
   Requirement NextDomain(bool self, const Requirement& podDomains, const Requirement& nodeDomains) const {
     if (type == 2) return NextDomainAnti(podDomains);
+    if (type == 1) return NextDomainAffinity(self, podDomains, nodeDomains);
     const int64_t mn = DomainMinCount(podDomains);
     string minDomain;
     bool found = false;
@@ -1018,9 +1047,9 @@ struct Topology {
 
   // NewTopologyGroup(TopologyTypePodAntiAffinity, ...): no node filter, every known domain registered; identity =
   // (type, key, namespaces, selector)
-  std::unique_ptr<TopologyGroup> NewAntiGroup(const AntiTerm& t) const {
+  std::unique_ptr<TopologyGroup> NewAntiGroup(const AntiTerm& t, int type = 2) const {
     auto g = std::make_unique<TopologyGroup>();
-    g->type = 2;
+    g->type = type;
     g->key = t.key;
     g->maxSkew = std::numeric_limits<int32_t>::max();
     g->minDomains = -1;
@@ -1028,7 +1057,7 @@ struct Topology {
     g->nss = t.namespaces;
     g->affinityHonor = false;
     g->taintHonor = false;
-    string id = "anti|" + t.key + "|";
+    string id = (type == 1 ? "aff|" : "anti|") + t.key + "|";
     for (auto& n : t.namespaces) id += n + ",";
     g->id = id + "|" + t.sel.Canon();
     auto dg = domainGroups.find(t.key);
@@ -1087,6 +1116,8 @@ struct Topology {
     for (auto& s : p.spreads) fresh.push_back(NewGroup(p, s));
     for (auto& t : p.antiRequired) fresh.push_back(NewAntiGroup(t));
     for (auto& t : p.antiPreferred) fresh.push_back(NewAntiGroup(t));
+    for (auto& t : p.affRequired) fresh.push_back(NewAntiGroup(t, 1));
+    for (auto& t : p.affPreferred) fresh.push_back(NewAntiGroup(t, 1));
     for (auto& g : fresh) {
       auto it = byId.find(g->id);
       TopologyGroup* tg;
@@ -1461,7 +1492,8 @@ static int32_t SolveCore(const Catalogs& cats, const kp_solve_in* in, kpo_result
   bool anySpread = false;
   for (uint32_t i = 0; i < in->n_shapes; i++)
     anySpread |= in->shapes[i].n_topology_spread > 0 || in->shapes[i].n_required_anti_affinity > 0 ||
-                 in->shapes[i].n_preferred_anti_affinity > 0;
+                 in->shapes[i].n_preferred_anti_affinity > 0 || in->shapes[i].n_required_affinity > 0 ||
+                 in->shapes[i].n_preferred_affinity > 0;
   for (uint32_t i = 0; i < in->n_bound_pods; i++) anySpread |= in->bound_pods[i].n_anti_affinity > 0;
   if (anySpread)
     for (uint32_t i = 0; i < in->n_nodepools; i++) {
@@ -1540,7 +1572,14 @@ static int32_t SolveCore(const Catalogs& cats, const kp_solve_in* in, kpo_result
     }
     ps.ns = sh.namespace_ ? sh.namespace_ : "";
     for (uint32_t j = 0; j < sh.n_labels; j++) ps.labels[sh.labels[j].key] = sh.labels[j].value ? sh.labels[j].value : "";
-    if (sh.n_required_affinity || sh.n_preferred_affinity) return KP_E_UNSUPPORTED;  // podAffinity: not restated
+    for (uint32_t j = 0; j < sh.n_required_affinity; j++) {
+      if (sh.required_affinity[j].has_namespace_selector) return KP_E_UNSUPPORTED;
+      ps.affRequired.push_back(AntiFromABI(sh.required_affinity[j], ps.ns));
+    }
+    for (uint32_t j = 0; j < sh.n_preferred_affinity; j++) {
+      if (sh.preferred_affinity[j].has_namespace_selector) return KP_E_UNSUPPORTED;
+      ps.affPreferred.push_back(AntiFromABI(sh.preferred_affinity[j], ps.ns));
+    }
     for (uint32_t j = 0; j < sh.n_required_anti_affinity; j++) {
       if (sh.required_anti_affinity[j].has_namespace_selector) return KP_E_UNSUPPORTED;
       ps.antiRequired.push_back(AntiFromABI(sh.required_anti_affinity[j], ps.ns));

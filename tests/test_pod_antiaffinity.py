@@ -1,10 +1,12 @@
-"""Pod anti-affinity on the hostname key (ABI v6): upstream TopologyGroup of TopologyTypePodAntiAffinity
+"""Pod anti-affinity and pod affinity on the hostname key (ABI v6): upstream TopologyGroup of TopologyTypePodAntiAffinity
 (nextDomainAntiAffinity: only domains whose count is zero; Topology.Record counts every selected pod on its node),
 the inverse groups a bound pod's required terms create (Topology.updateInverseAntiAffinity: pods the selector selects
-avoid the bound pod's node), and Preferences.Relax's removePreferredPodAntiAffinityTerm (heaviest first, before the
-preferred node-affinity terms). Docs: R:website/content/en/preview/concepts/scheduling.md:395-428 (the anti-affinity
-example "avoid running on any node with a pod labeled app=inflate": one replica per node). Other topology keys, pod
-affinity and namespaceSelector return KP_E_UNSUPPORTED (the Go path runs).
+avoid the bound pod's node), TopologyTypePodAffinity (nextDomainAffinity: a node holding a selected pod, or — while no
+domain has one and the pod selects itself — any node: the bootstrap), and Preferences.Relax's
+removePreferredPodAffinityTerm / removePreferredPodAntiAffinityTerm (heaviest first, before the preferred
+node-affinity terms). Docs: R:website/content/en/preview/concepts/scheduling.md:395-428 (the anti-affinity
+example "avoid running on any node with a pod labeled app=inflate": one replica per node). Other topology keys and
+namespaceSelector return KP_E_UNSUPPORTED (the Go path runs).
 
 Known answers on the CPU oracle, device == oracle under -m gpu (Solve and consolidation simulations). Parity
 unpinned beyond the written semantics (upstream core is not in the container)."""
@@ -100,12 +102,41 @@ def test_preferred_term_relaxed_when_it_cannot_hold(catalog):
     assert pl[0] != pl[1] and pl[2] in (pl[0], pl[1])
 
 
+def aff(app, weight=0):
+    from kpamd.model import LabelSelector, PodAffinityTerm
+    return PodAffinityTerm(HOST, LabelSelector({"app": app}), [], weight)
+
+
+def test_affinity_colocates_with_a_bound_pod(catalog):
+    node = m5_node(catalog)
+    prob = small_problem(catalog, [shape("web", required_affinity=[aff("cache")])], [2], existing=[node])
+    prob.bound_pods = [("default", {"app": "cache"}, 0)]
+    assert oracle(prob)["placement"].tolist() == [-2, -2]
+
+
+def test_affinity_bootstrap_and_follow(catalog):
+    # self-selecting: the first pod bootstraps (any node), the others must join a node holding one
+    r = oracle(small_problem(catalog, [shape("web", required_affinity=[aff("web")])], [3]))
+    assert r["placement"].tolist() == [0, 0, 0]
+
+
+def test_affinity_without_target_fails(catalog):
+    r = oracle(small_problem(catalog, [shape("web", required_affinity=[aff("cache")])], [2]))
+    assert r["placement"].tolist() == [-1, -1]
+
+
+def test_preferred_affinity_relaxed(catalog):
+    r = oracle(small_problem(catalog, [shape("web", preferred_affinity=[aff("cache", 10)])], [2]))
+    assert r["placement"].tolist() == [0, 0]
+
+
 def test_unsupported_variants(catalog):
     import kpamd
     from kpamd.model import LabelSelector, PodAffinityTerm
     zone = small_problem(catalog, [shape("web", req=[anti("web", key="topology.kubernetes.io/zone")])], [2])
     assert kpamd.validate(zone) == kpamd.abi.KP_E_UNSUPPORTED
-    aff = small_problem(catalog, [shape("web", required_affinity=[PodAffinityTerm(HOST, LabelSelector({"app": "x"}))])], [2])
+    aff = small_problem(catalog, [shape("web", required_affinity=[
+        PodAffinityTerm("topology.kubernetes.io/zone", LabelSelector({"app": "x"}))])], [2])
     assert kpamd.validate(aff) == kpamd.abi.KP_E_UNSUPPORTED
     nss = small_problem(catalog, [shape("web", req=[PodAffinityTerm(HOST, LabelSelector({"app": "web"}),
                                                                     namespace_selector=True)])], [2])
@@ -125,6 +156,10 @@ def add_anti(prob, seed, p=0.4):
         if rng.random() < 0.2:
             sh.preferred_anti_affinity = [anti(str(rng.choice(apps)), int(rng.integers(1, 100)))
                                           for _ in range(int(rng.integers(1, 3)))]
+        if rng.random() < 0.15:
+            sh.required_affinity = [aff(str(rng.choice(apps)))]
+        if rng.random() < 0.15:
+            sh.preferred_affinity = [aff(str(rng.choice(apps)), int(rng.integers(1, 100)))]
     bound = []
     for e in range(len(prob.existing)):
         for _ in range(int(rng.integers(0, 3))):
@@ -163,6 +198,11 @@ def test_gpu_known_answers(ctx, catalog):
     p.nodepools = [NodePool("default", 0, 0, list(POOL_REQS) + [("karpenter.k8s.aws/instance-cpu", "In", ["4"])],
                             limits={"cpu": 8000})]
     probs.append(p)
+    p = small_problem(catalog, [shape("web", required_affinity=[aff("cache")])], [2], existing=[m5_node(catalog)])
+    p.bound_pods = [("default", {"app": "cache"}, 0)]
+    probs += [p, small_problem(catalog, [shape("web", required_affinity=[aff("web")])], [3]),
+              small_problem(catalog, [shape("web", required_affinity=[aff("cache")])], [2]),
+              small_problem(catalog, [shape("web", preferred_affinity=[aff("cache", 10)])], [2])]
     for prob in probs:
         check_same(kpamd.Scheduler(ctx, prob).solve(), oracle(prob))
 
@@ -189,6 +229,8 @@ def test_gpu_consolidation_anti_affinity(ctx, catalog, seed):
         sh.labels = {"app": f"app-{i % 4}"}
         if rng.random() < 0.4:
             sh.required_anti_affinity = [anti(f"app-{int(rng.integers(0, 4))}")]
+        elif rng.random() < 0.2:
+            sh.preferred_affinity = [aff(f"app-{int(rng.integers(0, 4))}", 5)]
     subs = synth.consolidation_subsets(cl, 15, seed=seed, max_size=min(12, len(cl.nodes)))
     subs += [[c] for c in cl.candidates[:10]]
     check(ctx, cl, subs, multi_node=bool(seed % 2))
