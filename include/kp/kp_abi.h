@@ -212,9 +212,9 @@ typedef struct kp_topology_spread {
   kp_label_selector selector;
 } kp_topology_spread;
 
-/* corev1.PodAffinityTerm (ABI v6): pod affinity / anti-affinity on the hostname key (upstream TopologyGroup of
- * TopologyTypePodAffinity / TopologyTypePodAntiAffinity, and the inverse groups bound pods' required anti-affinity
- * terms create). Other topology keys and namespaceSelector return KP_E_UNSUPPORTED. */
+/* corev1.PodAffinityTerm (ABI v6): pod affinity / anti-affinity on the hostname or a label key (upstream
+ * TopologyGroup of TopologyTypePodAffinity / TopologyTypePodAntiAffinity, and the inverse groups bound pods' required
+ * anti-affinity terms create). namespaceSelector returns KP_E_UNSUPPORTED. */
 typedef struct kp_pod_affinity_term {
   const char* topology_key;
   kp_label_selector selector;

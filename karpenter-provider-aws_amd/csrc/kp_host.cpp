@@ -1255,9 +1255,7 @@ const kp_pod_affinity_term* PodTermAt(const kp_pod_shape& sh, int a, bool* aff =
 }
 int32_t CheckAntiTerm(const kp_pod_affinity_term& t, const char* who, uint32_t i) {
   if (t.has_namespace_selector) return fail(KP_E_UNSUPPORTED, "%s %u: pod (anti-)affinity namespaceSelector", who, i);
-  if (!t.topology_key || string(t.topology_key) != kHostname)
-    return fail(KP_E_UNSUPPORTED, "%s %u: pod (anti-)affinity on topology key %s (hostname only)", who, i,
-                t.topology_key ? t.topology_key : "");
+  if (!t.topology_key || !t.topology_key[0]) return fail(KP_E_INVAL, "%s %u: pod (anti-)affinity without topologyKey", who, i);
   return KP_OK;
 }
 
@@ -1521,6 +1519,22 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
   };
   // TopologyTypePodAffinity (aff): the same hostname row with maxSkew = -1, whose pre-pass test is count > 0, or,
   // while no domain has a count (tg_reg bit 0 clear), the self-selecting pod's bootstrap (nextDomainAffinity).
+  // one bound pod counted in group g on input node ni: hostname rows count per node (bit 0 of tg_reg: some domain
+  // has a count); dictionary keys count per value ordinal of the node's label (none: not counted)
+  auto record_bound = [&](int g, uint32_t ni) {
+    if (cp.tg_row[g] >= 0) {
+      uint8_t& c = cp.hcnt0[(size_t)cp.tg_row[g] * std::max(E, 1) + ex_pos[ni]];
+      if (c < 255) c++;
+      cp.tg_reg[g] |= 1;
+    } else {
+      const int k = cp.tg_key[g];
+      auto lv = node_labels[ni].find(d.keys[k]);
+      if (lv == node_labels[ni].end()) return;
+      const int ord = d.bit(k, lv->second) - k * 64;
+      cp.tg_cnt[(size_t)g * 64 + ord]++;
+      cp.tg_reg[g] |= 1ull << ord;
+    }
+  };
   auto anti_group = [&](const kp_pod_affinity_term& t, const std::set<string>& nss, bool inverse, bool aff = false) -> int {
     string id = string(inverse ? "inv|" : aff ? "aff|" : "anti|") + (t.topology_key ? t.topology_key : "") + "|";
     for (auto& n : nss) id += n + ",";
@@ -1534,8 +1548,20 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
     g_sel.push_back(&t.selector);
     g_nss.push_back(nss);
     g_inverse.push_back(inverse ? 1 : 0);
-    const int row = cp.GH++;
-    cp.tg_key.push_back(-1);
+    const string key = t.topology_key ? t.topology_key : "";
+    int k = -1, row = -1;
+    if (key == kHostname) {
+      row = cp.GH++;
+    } else {  // a dictionary key: counts per value ordinal, registered domains = every known value (no taint policy)
+      k = d.key(key);
+      if (k < 0) return fail(KP_E_INVAL, "topology key %s missing from the dictionary", key.c_str()), -1;
+      if (d.dd.nval[k] > 64) return fail(KP_E_UNSUPPORTED, "topology key %s has > 64 values", key.c_str()), -1;
+      if (cp.tkey_slot[k] < 0) {
+        cp.tkey_slot[k] = cp.TK++;
+        cp.tk_keys.push_back(k);
+      }
+    }
+    cp.tg_key.push_back(k);
     cp.tg_row.push_back(row);
     cp.tg_maxskew.push_back(aff ? -1 : 0);
     cp.tg_mindom.push_back(0);
@@ -1543,17 +1569,23 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
     cp.tg_aff.push_back(0);
     cp.tg_nterm.push_back(0);
     cp.tg_filt_tol.push_back(~0ull);
-    cp.tg_reg.push_back(0);
+    uint64_t reg = 0;
+    if (k >= 0) {
+      const vector<uint64_t>& dm = domains_of(k);
+      for (int b = 0; b < 64; b++)
+        if (dm[b]) reg |= 1ull << b;
+      for (uint32_t ni = 0; ni < in->n_existing; ni++) {
+        auto lv = node_labels[ni].find(key);
+        if (lv != node_labels[ni].end()) reg |= 1ull << (d.bit(k, lv->second) - k * 64);
+      }
+    }
+    cp.tg_reg.push_back(reg);
     for (int b = 0; b < 64; b++) cp.tg_cnt.push_back(0);
-    cp.hcnt0.resize((size_t)cp.GH * std::max(E, 1), 0);
+    if (row >= 0) cp.hcnt0.resize((size_t)cp.GH * std::max(E, 1), 0);
     if (!inverse)
       for (auto& bs : bsets) {
         if (!nss.count(bs.ns) || !SelectorMatches(t.selector, bs.labels)) continue;
-        for (const uint32_t ni : bs.nodes) {
-          uint8_t& c = cp.hcnt0[(size_t)row * std::max(E, 1) + ex_pos[ni]];
-          if (c < 255) c++;
-          cp.tg_reg[g] = 1;  // hostname rows: bit 0 = some domain has a count (affinity bootstrap)
-        }
+        for (const uint32_t ni : bs.nodes) record_bound(g, ni);
       }
     return g;
   };
@@ -1570,7 +1602,9 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
     for (uint32_t a = 0; a < PodTermCount(sh); a++) {
       bool aff = false;
       const kp_pod_affinity_term& t = *PodTermAt(sh, (int)a, &aff);
-      sgroup[s].push_back(anti_group(t, nss_of(t, sh.namespace_), false, aff));
+      const int g = anti_group(t, nss_of(t, sh.namespace_), false, aff);
+      if (g < 0) return KP_E_UNSUPPORTED;
+      sgroup[s].push_back(g);
     }
   }
   vector<int> inverse_groups;  // updateInverseAffinities: after the batch's groups
@@ -1579,10 +1613,9 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
     for (uint32_t j = 0; j < bp.n_anti_affinity; j++) {
       const kp_pod_affinity_term& t = bp.anti_affinity[j];
       const int g = anti_group(t, nss_of(t, bp.namespace_), true);
+      if (g < 0) return KP_E_UNSUPPORTED;
       if (std::find(inverse_groups.begin(), inverse_groups.end(), g) == inverse_groups.end()) inverse_groups.push_back(g);
-      uint8_t& c = cp.hcnt0[(size_t)cp.tg_row[g] * std::max(E, 1) + ex_pos[bp.node]];
-      if (c < 255) c++;
-      cp.tg_reg[g] = 1;
+      record_bound(g, bp.node);
     }
   }
   if (cp.G == 0) return KP_OK;
@@ -1639,7 +1672,9 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
       for (uint32_t a = 0; a < PodTermCount(sh); a++) {
         bool aff = false;
         const kp_pod_affinity_term& t = *PodTermAt(sh, (int)a, &aff);
-        sgroup[s].push_back(anti_group(t, nss_of(t, sh.namespace_), false, aff));
+        const int g = anti_group(t, nss_of(t, sh.namespace_), false, aff);
+        if (g < 0) return KP_E_UNSUPPORTED;
+        sgroup[s].push_back(g);
       }
     }
     const std::map<string, string> lm = LabelMap(sh.labels, sh.n_labels);
@@ -1791,8 +1826,10 @@ int32_t ParseSolve(const kp_solve_in* in, SolveRaw& raw) {
     if (sh.n_preferred_anti_affinity > 12 || sh.n_preferred_affinity > 12)
       return fail(KP_E_UNSUPPORTED, "> 12 preferred pod (anti-)affinity terms");
     for (uint32_t j = 0; j < PodTermCount(sh); j++) {
-      const int32_t rc = CheckAntiTerm(*PodTermAt(sh, (int)j), "shape", s);
+      const kp_pod_affinity_term& t = *PodTermAt(sh, (int)j);
+      const int32_t rc = CheckAntiTerm(t, "shape", s);
       if (rc) return rc;
+      if (t.topology_key != string(kHostname)) raw.topo_keys.insert(t.topology_key);
     }
     RawReqs ns = LabelReqs(sh.node_selector, sh.n_node_selector, false);
     vector<RawReqs> req;
@@ -1856,6 +1893,11 @@ int32_t ParseSolve(const kp_solve_in* in, SolveRaw& raw) {
       }
     }
   }
+  for (uint32_t b = 0; b < in->n_bound_pods; b++)  // inverse anti-affinity keys need a dictionary id too
+    for (uint32_t j = 0; j < in->bound_pods[b].n_anti_affinity; j++) {
+      const char* k = in->bound_pods[b].anti_affinity[j].topology_key;
+      if (k && k[0] && string(k) != kHostname) raw.topo_keys.insert(k);
+    }
   raw.ex_labels.resize(in->n_existing);
   for (uint32_t i = 0; i < in->n_existing; i++)
     raw.ex_labels[i] = LabelReqs(in->existing[i].labels, in->existing[i].n_labels, true);

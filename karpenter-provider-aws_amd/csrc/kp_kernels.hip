@@ -738,14 +738,23 @@ __device__ bool topo_narrow(const DevDict& D, int n, const TopoOwn* own, const u
     const uint64_t aN = present ? lane_bcast(allowed, k) : D.validbits[k];
     const uint64_t cand = acc[j] & aN;
     if (!cand) return false;
-    const bool in = (cand >> lane) & 1;
-    const int c = in ? cnt[j][lane] : INT32_MAX;
-    const int mc = wave_min_i32(c);
-    const int d = __builtin_ctzll(__ballot(in && c == mc));
-    if (narrowed & kb) {
-      if (lane_bcast(nv, k) != (1ull << d)) return false;  // two groups on one key chose different domains
+    uint64_t pick;
+    if (own[j].maxskew > 0) {  // spread: the lowest count, ties to the lowest ordinal
+      const bool in = (cand >> lane) & 1;
+      const int c = in ? cnt[j][lane] : INT32_MAX;
+      const int mc = wave_min_i32(c);
+      pick = 1ull << __builtin_ctzll(__ballot(in && c == mc));
+    } else if (own[j].maxskew < 0 && own[j].self) {  // pod-affinity bootstrap: the first domain the node admits
+      pick = cand & (0 - cand);
+    } else {  // pod (anti-)affinity: every acceptable domain (requirements.Add intersects)
+      pick = cand;
+    }
+    if (narrowed & kb) {  // groups on one key intersect (empty: Compatible fails)
+      const uint64_t both = lane_bcast(nv, k) & pick;
+      if (!both) return false;
+      if (lane == k) nv = both;
     } else if (lane == k) {
-      nv = 1ull << d;
+      nv = pick;
     }
     narrowed |= kb;
   }
@@ -1876,6 +1885,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
         const int k = a.tg_key[g];
         const int mskew = a.tg_maxskew[g];
         uint64_t acc = 0;
+        bool boot = false;  // pod affinity on a dictionary key: TopoOwn.self = bootstrap
         if (k >= 0) {
           const int c = a.tg_cnt[(size_t)g * 64 + lane];
           const uint64_t reg = a.tg_reg[g], pd = a.own_pd[oi];
@@ -1885,13 +1895,21 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
           int64_t m = num ? (int64_t)mn : (int64_t)INT32_MAX;
           const int mind = a.tg_mindom[g];
           if (mind > 0 && num < mind) m = 0;
-          acc = __ballot(((reg >> lane) & 1) && (int64_t)c + self - m <= mskew);
+          if (mskew > 0) {  // spread: count + self - min <= maxSkew
+            acc = __ballot(((reg >> lane) & 1) && (int64_t)c + self - m <= mskew);
+          } else if (mskew == 0) {  // pod anti-affinity: known domains without a selected pod
+            acc = __ballot(((reg >> lane) & 1) && c == 0);
+          } else {  // pod affinity: known domains the pod admits that hold one; none: the self-selecting bootstrap
+            acc = __ballot(sup && c > 0);
+            boot = !acc && self;
+            if (boot) acc = reg & pd;
+          }
           s_tcnt[j][lane] = c;
           bytes += 64 * 4 + 16;
         }
         // pod affinity (hostname row, maxSkew -1): self = the pod may bootstrap (it selects itself and no domain
         // has a count yet, tg_reg bit 0)
-        const int self_eff = (k < 0 && mskew < 0) ? (self && !(a.tg_reg[g] & 1)) : self;
+        const int self_eff = mskew >= 0 ? self : k < 0 ? (self && !(a.tg_reg[g] & 1)) : (boot ? 1 : 0);
         if (lane == 0) {
           s_town[j] = TopoOwn{g, self_eff, k, a.tg_row[g], mskew, k >= 0 ? a.tkey_slot[k] : -1};
           s_tacc[j] = acc;
@@ -2297,7 +2315,12 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
         } else {
           const int k = a.tg_key[g];
           const uint64_t v = fin->vals[k];
-          if (((fin->present >> k) & 1) && !((fin->compl_ >> k) & 1) && __builtin_popcountll(v) == 1 && lane == 0) {
+          if (a.tg_maxskew[g] == 0) {  // pod anti-affinity: Record(domains.Values()...), every value of the key
+            if (((fin->present >> k) & 1) && lane == 0) {
+              for (uint64_t m = v; m; m &= m - 1) a.tg_cnt[(size_t)g * 64 + __builtin_ctzll(m)] += 1;
+              a.tg_reg[g] |= v;
+            }
+          } else if (((fin->present >> k) & 1) && !((fin->compl_ >> k) & 1) && __builtin_popcountll(v) == 1 && lane == 0) {
             const int d = __builtin_ctzll(v);
             a.tg_cnt[(size_t)g * 64 + d] += 1;
             a.tg_reg[g] |= 1ull << d;

@@ -1,12 +1,12 @@
-"""Pod anti-affinity and pod affinity on the hostname key (ABI v6): upstream TopologyGroup of TopologyTypePodAntiAffinity
+"""Pod anti-affinity and pod affinity on the hostname and on label keys such as the zone (ABI v6): upstream TopologyGroup of TopologyTypePodAntiAffinity
 (nextDomainAntiAffinity: only domains whose count is zero; Topology.Record counts every selected pod on its node),
 the inverse groups a bound pod's required terms create (Topology.updateInverseAntiAffinity: pods the selector selects
 avoid the bound pod's node), TopologyTypePodAffinity (nextDomainAffinity: a node holding a selected pod, or — while no
 domain has one and the pod selects itself — any node: the bootstrap), and Preferences.Relax's
 removePreferredPodAffinityTerm / removePreferredPodAntiAffinityTerm (heaviest first, before the preferred
 node-affinity terms). Docs: R:website/content/en/preview/concepts/scheduling.md:395-428 (the anti-affinity
-example "avoid running on any node with a pod labeled app=inflate": one replica per node). Other topology keys and
-namespaceSelector return KP_E_UNSUPPORTED (the Go path runs).
+example "avoid running on any node with a pod labeled app=inflate": one replica per node). A namespaceSelector
+returns KP_E_UNSUPPORTED (the Go path runs).
 
 Known answers on the CPU oracle, device == oracle under -m gpu (Solve and consolidation simulations). Parity
 unpinned beyond the written semantics (upstream core is not in the container)."""
@@ -130,14 +130,40 @@ def test_preferred_affinity_relaxed(catalog):
     assert r["placement"].tolist() == [0, 0]
 
 
+ZONE = "topology.kubernetes.io/zone"
+
+
+def zaff(app, weight=0):
+    from kpamd.model import LabelSelector, PodAffinityTerm
+    return PodAffinityTerm(ZONE, LabelSelector({"app": app}), [], weight)
+
+
+def zone_of(r, nc):
+    return [q[2] for q in r["nodeclaims"][nc]["requirements"] if q[0] == ZONE]
+
+
+def test_zone_anti_affinity(catalog):
+    # pods pinned to a zone each: one per zone, a second pod for zone 1a has no zone left
+    shapes = [shape("web", req=[anti("web", key=ZONE)], node_selector={ZONE: z})
+              for z in ("test-zone-1a", "test-zone-1b", "test-zone-1c", "test-zone-1a")]
+    pl = oracle(small_problem(catalog, shapes, [1, 1, 1, 1]))["placement"].tolist()
+    assert len(set(pl[:3])) == 3 and min(pl[:3]) >= 0 and pl[3] == -1
+    # unpinned: the first NodeClaim may launch in any zone, and Topology.Record blocks every zone it could be in
+    # (for anti-affinity upstream records all of the node's possible domains), so the second pod has none left
+    pl = oracle(small_problem(catalog, [shape("web", req=[anti("web", key=ZONE)])], [2]))["placement"].tolist()
+    assert pl == [0, -1]
+
+
+def test_zone_affinity_follows_the_first(catalog):
+    # the self-selecting bootstrap pins the first NodeClaim to the lowest zone; the rest follow into that zone
+    r = oracle(small_problem(catalog, [shape("web", required_affinity=[zaff("web")]), shape("api", required_affinity=[zaff("web")])], [2, 2]))
+    zs = {tuple(zone_of(r, nc)[0]) for nc in set(r["placement"].tolist())}
+    assert zs == {("test-zone-1a",)}
+
+
 def test_unsupported_variants(catalog):
     import kpamd
     from kpamd.model import LabelSelector, PodAffinityTerm
-    zone = small_problem(catalog, [shape("web", req=[anti("web", key="topology.kubernetes.io/zone")])], [2])
-    assert kpamd.validate(zone) == kpamd.abi.KP_E_UNSUPPORTED
-    aff = small_problem(catalog, [shape("web", required_affinity=[
-        PodAffinityTerm("topology.kubernetes.io/zone", LabelSelector({"app": "x"}))])], [2])
-    assert kpamd.validate(aff) == kpamd.abi.KP_E_UNSUPPORTED
     nss = small_problem(catalog, [shape("web", req=[PodAffinityTerm(HOST, LabelSelector({"app": "web"}),
                                                                     namespace_selector=True)])], [2])
     assert kpamd.validate(nss) == kpamd.abi.KP_E_UNSUPPORTED
@@ -152,12 +178,12 @@ def add_anti(prob, seed, p=0.4):
     for i, sh in enumerate(prob.shapes):
         sh.labels = dict(sh.labels or {}, app=apps[i % 4])
         if rng.random() < p:
-            sh.required_anti_affinity = [anti(str(rng.choice(apps)))]
+            sh.required_anti_affinity = [anti(str(rng.choice(apps)), key=str(rng.choice([HOST, HOST, ZONE])))]
         if rng.random() < 0.2:
             sh.preferred_anti_affinity = [anti(str(rng.choice(apps)), int(rng.integers(1, 100)))
                                           for _ in range(int(rng.integers(1, 3)))]
         if rng.random() < 0.15:
-            sh.required_affinity = [aff(str(rng.choice(apps)))]
+            sh.required_affinity = [aff(str(rng.choice(apps))) if rng.random() < 0.6 else zaff(str(rng.choice(apps)))]
         if rng.random() < 0.15:
             sh.preferred_affinity = [aff(str(rng.choice(apps)), int(rng.integers(1, 100)))]
     bound = []
@@ -202,7 +228,13 @@ def test_gpu_known_answers(ctx, catalog):
     p.bound_pods = [("default", {"app": "cache"}, 0)]
     probs += [p, small_problem(catalog, [shape("web", required_affinity=[aff("web")])], [3]),
               small_problem(catalog, [shape("web", required_affinity=[aff("cache")])], [2]),
-              small_problem(catalog, [shape("web", preferred_affinity=[aff("cache", 10)])], [2])]
+              small_problem(catalog, [shape("web", preferred_affinity=[aff("cache", 10)])], [2]),
+              small_problem(catalog, [shape("web", req=[anti("web", key=ZONE)], node_selector={ZONE: z})
+                                      for z in ("test-zone-1a", "test-zone-1b", "test-zone-1c", "test-zone-1a")],
+                            [1, 1, 1, 1]),
+              small_problem(catalog, [shape("web", req=[anti("web", key=ZONE)])], [2]),
+              small_problem(catalog, [shape("web", required_affinity=[zaff("web")]),
+                                      shape("api", required_affinity=[zaff("web")])], [2, 2])]
     for prob in probs:
         check_same(kpamd.Scheduler(ctx, prob).solve(), oracle(prob))
 
