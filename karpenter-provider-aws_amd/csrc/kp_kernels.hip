@@ -24,6 +24,10 @@
 #ifndef FASTLANE
 #define FASTLANE 1  // solve_kernel: wave-0 fast lane for merge-free placements (0 = full path only)
 #endif
+#ifndef FL_NOTIME
+#define FL_NOTIME 1  // the fast lane's per-phase s_memtime probes are compiled out (their registers cost 3.7 % even
+                     // when KP_TIMING is off); the diagnostic build (tools/build_fine.sh) turns them back on
+#endif
 #ifndef FT_FINE
 #define FT_FINE 0  // diagnostic: finer fast-lane probes (FTF) in place of the full path's attempt split
 #endif
@@ -1342,6 +1346,7 @@ __device__ __noinline__ int fast_lane(uint64_t kargs, int32_t LDS* s_dyn_arg, ui
   int pops = 0, handoff = -1, fb = -1;
   int n_buf = 0, buf_pod = 0, buf_pl = 0;  // placements not yet written (lane i: the i-th)
     const bool tmg = A->timing != 0;
+#define FL_HAS_EX (A->n_existing != 0)
     uint64_t ft = tmg ? __builtin_amdgcn_s_memtime() : 0;
 #define FTF(i)                                               \
   if (FT_FINE && tmg) {                                      \
@@ -1350,7 +1355,7 @@ __device__ __noinline__ int fast_lane(uint64_t kargs, int32_t LDS* s_dyn_arg, ui
     ft = tn_;                                                \
   }
 #define FT(i)                                                \
-if (A->timing) {                                            \
+if (!FL_NOTIME && tmg) {                                    \
   const uint64_t tn_ = __builtin_amdgcn_s_memtime();       \
   fcyc[i] += tn_ - ft;                      \
   ft = tn_;                                                \
@@ -1419,7 +1424,7 @@ if (A->timing) {                                            \
         }
       } else {
         own = U((TOPO ? A->sl_own_n[sl] + A->shape_rec_n[shape] : 0) + (A->hp_any && A->shape_hp_conf[shape] ? 1 : 0));
-        ce0 = U(A->n_existing ? A->cur_ex[2 * sl] : 0), ce1 = U(A->n_existing ? A->cur_ex[2 * sl + 1] : 0);
+        ce0 = U(FL_HAS_EX ? A->cur_ex[2 * sl] : 0), ce1 = U(FL_HAS_EX ? A->cur_ex[2 * sl + 1] : 0);
         preq_lane = lane < KP_NRES ? A->shape_requests[(size_t)shape * KP_NRES + lane] : 0;
         tolmask = U64(A->shape_tolerates[shape]);
         cur = U(A->cur_nc[2 * sl]), stamp = U(A->cur_nc[2 * sl + 1]);
@@ -1430,7 +1435,7 @@ if (A->timing) {                                            \
         const int nshape = __builtin_amdgcn_readlane(qw_shape, off + 1);
         const int nsl = __builtin_amdgcn_readlane(qw_sl, off + 1);
         pf_own = (TOPO ? A->sl_own_n[nsl] + A->shape_rec_n[nshape] : 0) + (A->hp_any && A->shape_hp_conf[nshape] ? 1 : 0);
-        pf_ce0 = A->n_existing ? A->cur_ex[2 * nsl] : 0, pf_ce1 = A->n_existing ? A->cur_ex[2 * nsl + 1] : 0;
+        pf_ce0 = FL_HAS_EX ? A->cur_ex[2 * nsl] : 0, pf_ce1 = FL_HAS_EX ? A->cur_ex[2 * nsl + 1] : 0;
         pf_preq = lane < KP_NRES ? A->shape_requests[(size_t)nshape * KP_NRES + lane] : 0;
         pf_tol = A->shape_tolerates[nshape];
         pf_cur = A->cur_nc[2 * nsl], pf_stamp = A->cur_nc[2 * nsl + 1];
@@ -1441,7 +1446,7 @@ if (A->timing) {                                            \
       q_head = head + 1 == A->n_pods ? 0 : head + 1;
       q_len = len - 1;
       bool eligible = own == 0;
-      if (A->n_existing) eligible = eligible && min(ce0, mstack_query_wave((LdsI32)s_stk[1], U(s_ctl[14]), U(s_ctl[21]), ce1)) >= A->n_existing;
+      if (FL_HAS_EX) eligible = eligible && min(ce0, mstack_query_wave((LdsI32)s_stk[1], U(s_ctl[14]), U(s_ctl[21]), ce1)) >= A->n_existing;
       FT(0);
       if (!eligible) {
         handoff = pod;
@@ -1450,7 +1455,7 @@ if (A->timing) {                                            \
       }
       const int64_t pr0 = lane_bcast_i64(preq_lane, rr0), pr1 = lane_bcast_i64(preq_lane, rr1);
       a_cex_prev_stamp = U(s_ctl[15]);
-      if (A->n_existing && lane == 0) {  // addToExistingNode: every position fails (cursor == n_existing)
+      if (FL_HAS_EX && lane == 0) {  // addToExistingNode: every position fails (cursor == n_existing)
         A->cur_ex[2 * sl] = A->n_existing;
         A->cur_ex[2 * sl + 1] = a_cex_prev_stamp;
       }
@@ -1653,6 +1658,7 @@ if (A->timing) {                                            \
     n_ev += n_buf;
 #undef FT
 #undef FTF
+#undef FL_HAS_EX
   
   // write back: control block, window, counters, hand-off
   if (lane == 0) {

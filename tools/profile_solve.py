@@ -1,4 +1,5 @@
-"""Diagnostic: per-phase cycle split of solve_kernel (KP_TIMING=1). usage: profile_solve.py [config] [pods]"""
+"""Diagnostic: per-phase cycle split of solve_kernel (KP_TIMING=1). usage: profile_solve.py [config] [pods]
+The fast lane's phases need the diagnostic build: KP_LIB=tools/fine/libkp.so (tools/build_fine.sh)."""
 import json
 import os
 import sys
