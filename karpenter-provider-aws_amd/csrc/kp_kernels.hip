@@ -24,6 +24,26 @@
 #ifndef FASTLANE
 #define FASTLANE 1  // solve_kernel: wave-0 fast lane for merge-free placements (0 = full path only)
 #endif
+#ifndef FL_SPLIT
+#define FL_SPLIT 0  // variant under measurement: the fast lane's full NodeClaim.Add as a separate (noinline) function
+#endif
+#ifndef FL_CNT32
+#define FL_CNT32 1  // the fast lane's byte model as 32-bit event counts converted on exit (same totals; the 64-bit
+                    // accumulators cost 2.8 % of the loop)
+#endif
+#if FL_CNT32
+#define FL_CNT32_APP (n_app++)
+#define FL_CNT32_SCAN(x) (n_scan += (uint32_t)(x))
+#else
+#define FL_CNT32_APP ((void)0)
+#define FL_CNT32_SCAN(x) ((void)0)
+#endif
+#ifndef FL_NOBYTES
+#define FL_NOBYTES 0  // variant under measurement: no algorithmic-byte accounting in the fast lane
+#endif
+#ifndef FL_NOGUARD
+#define FL_NOGUARD 0  // variant under measurement: no runaway guard in the fast lane's loop
+#endif
 #ifndef FL_NOTIME
 #define FL_NOTIME 1  // the fast lane's per-phase s_memtime probes are compiled out (their registers cost 3.7 % even
                      // when KP_TIMING is off); the diagnostic build (tools/build_fine.sh) turns them back on
@@ -592,11 +612,25 @@ __device__ __forceinline__ uint64_t filter_types(const DevDict& D, const CatHdr 
   return X;
 }
 
+// Algorithmic-byte accounting of fits_lean: bytes directly (uint64_t), or event counts the caller converts once
+// (NbUnits: 512-byte threshold probes, TW-word mask rows, lower-bound bytes / 8), which keeps the hot loop's
+// registers free of 64-bit accumulators.
+struct NbUnits {
+  uint32_t probes, rows, lb8;
+};
+__device__ __forceinline__ void nb_probe(uint64_t& nb, uint32_t n, int) { nb += 512ull * n; }
+__device__ __forceinline__ void nb_probe(NbUnits& nb, uint32_t n, int) { nb.probes += n; }
+__device__ __forceinline__ void nb_row(uint64_t& nb, uint32_t n, int TW) { nb += (uint64_t)TW * 8 * n; }
+__device__ __forceinline__ void nb_row(NbUnits& nb, uint32_t n, int) { nb.rows += n; }
+__device__ __forceinline__ void nb_lb(uint64_t& nb, uint64_t b) { nb += b; }
+__device__ __forceinline__ void nb_lb(NbUnits& nb, uint64_t b) { nb.lb8 += (uint32_t)(b >> 3); }
+
 // fits_filter for at most 4 requested resources (the fast lane): the threshold probes, then the (up to 4) mask
 // rows as one batch of independent loads, ANDed into X. Same result and threshold indices as fits_filter.
+template <class NB>
 __device__ __forceinline__ uint64_t fits_lean(const DevDict& D, const CatHdr LDS* H, uint64_t X, int64_t q_lane,
                                               int32_t j0_lane, const int64_t LDS* fitv_lds, const int8_t* rr, int nr,
-                                              uint64_t& nb, int32_t LDS* jout) {
+                                              NB& nb, int32_t LDS* jout) {
   const int lane = LANE;
   const int TW = D.TW;
   // threshold indices unchanged for every requested resource (q_r <= fit_vals_r[j0_r], one LDS probe per lane):
@@ -614,7 +648,8 @@ __device__ __forceinline__ uint64_t fits_lean(const DevDict& D, const CatHdr LDS
     }
     const uint64_t act = __ballot(in_rr && q_lane > 0);
     if (__ballot(!same) == 0) {
-      nb += (uint64_t)__popcll(act) * (512 + (uint64_t)TW * 8);  // the algorithm's probe + row bytes, as below
+      nb_probe(nb, (uint32_t)__popcll(act), TW);  // the algorithm's probe + row bytes, as below
+      nb_row(nb, (uint32_t)__popcll(act), TW);
       if (lane < KP_NRES) jout[lane] = in_rr && q_lane > 0 ? j0_lane : 0;
       return X;
     }
@@ -635,15 +670,19 @@ __device__ __forceinline__ uint64_t fits_lean(const DevDict& D, const CatHdr LDS
     uint64_t bal;
     if (slot >= 0) bal = __ballot(idx < n && fitv_lds[slot * FITV_CAP + idx] >= q);
     else bal = __ballot(idx < n && H->d.fit_vals[(size_t)r * D.T + idx] >= q);
-    nb += 512;
+    nb_probe(nb, 1, TW);
     int j;
     if (bal) j = j0 + __builtin_ctzll(bal);
     else if (j0 + 64 >= n) j = n;
-    else if (slot >= 0) j = wave_lower_bound(fitv_lds + slot * FITV_CAP + j0 + 64, n - j0 - 64, q, &nb) + j0 + 64;
-    else j = wave_lower_bound(H->d.fit_vals + (size_t)r * D.T + j0 + 64, n - j0 - 64, q, &nb) + j0 + 64;
+    else {
+      uint64_t lb = 0;
+      if (slot >= 0) j = wave_lower_bound(fitv_lds + slot * FITV_CAP + j0 + 64, n - j0 - 64, q, &lb) + j0 + 64;
+      else j = wave_lower_bound(H->d.fit_vals + (size_t)r * D.T + j0 + 64, n - j0 - 64, q, &lb) + j0 + 64;
+      nb_lb(nb, lb);
+    }
     if (j >= n) zero = true;
     else rowp[k] = (const uint64_t GLB*)(H->d.fit_mask + ((size_t)r * D.T + j) * TW);
-    nb += (uint64_t)TW * 8;
+    nb_row(nb, 1, TW);
     if (lane == r) j_lane = j;
   }
   if (lane < KP_NRES) jout[lane] = j_lane;
@@ -1297,6 +1336,64 @@ struct FastState {
 };
 __shared__ FastState g_fast;
 
+// NodeClaim.Add in full for the fast lane (Compatible + Add of the requirements, the type filter, minValues) as its
+// own function: the merge is the rare attempt, and inlined its registers burden every pod's append path. On
+// success the merged requirements (and topology codes) are stored and the memo marks the shape-level merged.
+// Returns this lane's word of the remaining types (0 everywhere: failed); fl_io[0] = permanent failure,
+// fl_io[1] = algorithmic bytes read.
+__shared__ uint64_t fl_io[2];
+template <bool TOPO>
+__device__ __noinline__ uint64_t fl_full_add(uint64_t kargs, int sl_a, int cat_a, int ncx_a, uint64_t X0, int64_t q_lane,
+                                             int32_t j0_lane, int staged_a) {
+  const uint32_t klo = __builtin_amdgcn_readfirstlane((uint32_t)kargs);
+  const uint32_t khi = __builtin_amdgcn_readfirstlane((uint32_t)(kargs >> 32));
+  const KARG SolveArgs* A = (const KARG SolveArgs*)(((uint64_t)khi << 32) | klo);
+  const int sl = U(sl_a), cat = U(cat_a), ncx = U(ncx_a);
+  const DevDict& D = g_D;
+  const int lane = LANE;
+  uint64_t nb = 0;
+  if (!U(staged_a)) {  // the pod's requirement set, once per pod
+    constexpr int NQ = (int)(sizeof(KReqs) / 8);
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(A->shape_reqs + (size_t)sl * sizeof(KReqs));
+    uint64_t* dstB = reinterpret_cast<uint64_t*>(&fl_B);
+    for (int i = lane; i < NQ; i += 64) dstB[i] = src[i];
+    wave_sync();
+  }
+  auto hdr = [&](int c) -> const CatHdr LDS* {
+    if (c < 8) return (const CatHdr LDS*)&g_hdr[c];
+    hdr_fill_wave((CatHdr LDS*)&fl_hdrw, &A->cats[c], D.C);
+    wave_sync();
+    return (const CatHdr LDS*)&fl_hdrw;
+  };
+  const CandReq crx = load_cand(D, kreq_at(A->nc_reqs, ncx));
+  const VInt vig = vint_global(A->vint);
+  const uint64_t b_negop = A->shape_negop[sl];
+  uint64_t m_v = 0, X = 0;
+  ReqView rv;
+  const bool mok = merge_compatible(D, crx, (const KReqs*)&fl_B, b_negop, true, m_v, rv, (WaveSlots*)&fl_slots, vig);
+  const bool perm = mok || (fl_B.present & ~crx.P & ~b_negop & ~D.wellknown) == 0;
+  nb += sizeof(KReqs);
+  if (mok) {
+    const int pb = A->pvp_base[sl * A->n_catalogs + cat];
+    const uint64_t* pvp = A->shape_pvp + (size_t)pb * D.TW;
+    X = filter_types(D, hdr(cat), rv, m_v, X0, fl_B.present, pvp, A->pvp_slot + (size_t)sl * KP_MAX_KEYS, q_lane,
+                     j0_lane, (const int64_t LDS*)g_fitv, A->req_res_mask, vig, (uint32_t*)fl_scratch,
+                     (RowPtr LDS*)fl_rl, &nb, fl_fitj);
+    nb += (uint64_t)D.TW * 8 + KP_NRES * 8;
+    if (__ballot(X != 0)) {
+      store_merged(reinterpret_cast<KReqs*>(A->nc_reqs + (size_t)ncx * sizeof(KReqs)), rv, m_v, D.W, D.KB);
+      if (TOPO && A->n_tk) store_tcodes(A->n_tk, A->tk_keys, A->nc_tcode, A->hnc_stride, rv, m_v, ncx);
+      if (lane == 0 && ncx < A->ncc) A->nc_fail[(size_t)sl * A->ncc + ncx] = NC_MERGED;
+    }
+  }
+  if (lane == 0) {
+    fl_io[0] = perm ? 1 : 0;
+    fl_io[1] = nb;
+  }
+  wave_sync();
+  return X;
+}
+
 // Places popped pods while they need no requirement merge; returns the number placed. A pod it cannot place is
 // handed to the full path through g_ctl[6] / g_ctl[26]. Called by wave 0 only.
 template <bool TOPO>
@@ -1345,6 +1442,13 @@ __device__ __noinline__ int fast_lane(uint64_t kargs, int32_t LDS* s_dyn_arg, ui
   uint64_t bytes = 0, attempts = 0, scanned = 0, starts = 0, fcyc[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   int pops = 0, handoff = -1, fb = -1;
   int n_buf = 0, buf_pod = 0, buf_pl = 0;  // placements not yet written (lane i: the i-th)
+#if FL_CNT32
+  NbUnits fnb{0, 0, 0};  // append-path byte model as event counts, converted on exit
+  uint32_t n_app = 0, n_scan = 0;
+#define FL_NB fnb
+#else
+#define FL_NB bytes
+#endif
     const bool tmg = A->timing != 0;
 #define FL_HAS_EX (A->n_existing != 0)
     uint64_t ft = tmg ? __builtin_amdgcn_s_memtime() : 0;
@@ -1373,7 +1477,7 @@ if (!FL_NOTIME && tmg) {                                    \
       const KARG SolveArgs* A = (const KARG SolveArgs*)(((uint64_t)khi_i << 32) | klo_i);
       const int len = q_len;
       const int head = q_head;
-      if (len <= 0 || pops_in + pops > pop_cap) break;
+      if (len <= 0 || (!FL_NOGUARD && pops_in + pops > pop_cap)) break;
       // Queue.Pop from the prefetched window: entries [qw_head, qw_head + qw_n) of the ring were in the queue when
       // the window was read, and nothing rewrites a queued entry (pushes go to the tail) or its pod's level and
       // lastLen stamps while it waits, so lane i's copy of entry qw_head + i stays exact.
@@ -1521,7 +1625,8 @@ if (!FL_NOTIME && tmg) {                                    \
           tag = cand && fl >= NC_MERGED;
         }
         if (lane == 0) scanned += min(64, n_nc - base);
-        if (lane == 0) bytes += (uint64_t)min(64, n_nc - base) * (12 + 16 * A->n_req_res);
+        if (!FL_CNT32 && lane == 0) bytes += (uint64_t)min(64, n_nc - base) * (12 + 16 * A->n_req_res);
+        FL_CNT32_SCAN(min(64, n_nc - base));
         uint64_t cm = __ballot(cand);
         const uint64_t tm = __ballot(tag);
         // the next pod's prefetch was issued before these gathers, so it has landed: take it off the outstanding
@@ -1562,11 +1667,17 @@ if (!FL_NOTIME && tmg) {                                    \
           ReqView rv;
           bool perm = true;  // a failure here is permanent (NC_NEVER) unless it is Compatible's undefined-key rule
           if (!full_add) {
-            X = n_rr <= 4 ? fits_lean(D, hdr(cat), X0, q_lane, j0_lane, (const int64_t LDS*)g_fitv, rr_list, n_rr, bytes,
+            X = n_rr <= 4 ? fits_lean(D, hdr(cat), X0, q_lane, j0_lane, (const int64_t LDS*)g_fitv, rr_list, n_rr, FL_NB,
                                       (int32_t LDS*)fl_fitj)
                           : fits_filter(D, hdr(cat), X0, q_lane, j0_lane, (const int64_t LDS*)g_fitv, A->req_res_mask,
                                         (RowPtr LDS*)fl_rl, &bytes, fl_fitj);
-            bytes += (uint64_t)D.TW * 8 + KP_NRES * 8 + 8;
+            if (FL_CNT32) FL_CNT32_APP;
+            else bytes += (uint64_t)D.TW * 8 + KP_NRES * 8 + 8;
+          } else if (FL_SPLIT) {
+            X = fl_full_add<TOPO>(((uint64_t)khi_i << 32) | klo_i, sl, cat, ncx, X0, q_lane, j0_lane, b_staged ? 1 : 0);
+            b_staged = true;
+            perm = fl_io[0] != 0;
+            bytes += fl_io[1];
           } else {
             if (!b_staged) {  // the pod's requirement set, once per pod
               constexpr int NQ = (int)(sizeof(KReqs) / 8);
@@ -1594,7 +1705,7 @@ if (!FL_NOTIME && tmg) {                                    \
           }
           FTF(11);
           if (__ballot(X != 0)) {
-            if (full_add) {
+            if (full_add && !FL_SPLIT) {
               store_merged(reinterpret_cast<KReqs*>(A->nc_reqs + (size_t)ncx * sizeof(KReqs)), rv, m_v, D.W, D.KB);
               if (TOPO && A->n_tk) store_tcodes(A->n_tk, A->tk_keys, A->nc_tcode, A->hnc_stride, rv, m_v, ncx);
               if (lane == 0 && ncx < A->ncc) A->nc_fail[(size_t)sl * A->ncc + ncx] = NC_MERGED;
@@ -1659,6 +1770,7 @@ if (!FL_NOTIME && tmg) {                                    \
 #undef FT
 #undef FTF
 #undef FL_HAS_EX
+#undef FL_NB
   
   // write back: control block, window, counters, hand-off
   if (lane == 0) {
@@ -1677,7 +1789,13 @@ if (!FL_NOTIME && tmg) {                                    \
     S->qw_head = qw_head;
     S->qw_n = qw_n;
     S->qw_next = qw_next;
+#if FL_CNT32
+    bytes += (uint64_t)fnb.probes * 512 + (uint64_t)fnb.rows * D.TW * 8 + (uint64_t)fnb.lb8 * 8 +
+             (uint64_t)n_app * ((uint64_t)D.TW * 8 + KP_NRES * 8 + 8) + (uint64_t)n_scan * (12 + 16 * A->n_req_res);
+#endif
+#if !FL_NOBYTES
     S->bytes += bytes;
+#endif
     S->attempts += attempts;
     S->scanned += scanned;
     S->starts += starts;
