@@ -24,6 +24,9 @@
 #ifndef FASTLANE
 #define FASTLANE 1  // solve_kernel: wave-0 fast lane for merge-free placements (0 = full path only)
 #endif
+#ifndef FL_NI
+#define FL_NI 0  // variant under measurement: the append attempt's rare paths out of line
+#endif
 #ifndef FL_SPLIT
 #define FL_SPLIT 0  // variant under measurement: the fast lane's full NodeClaim.Add as a separate (noinline) function
 #endif
@@ -1336,12 +1339,34 @@ struct FastState {
 };
 __shared__ FastState g_fast;
 
+__shared__ uint64_t fl_io[2];  // results of the fast lane's out-of-line helpers
+// Rare paths of the fast lane's append attempt as calls (FL_NI): a catalogue id >= 8 (descriptor copied to LDS)
+// and more than 4 requested resources (fits_filter); inlined, their registers weigh on every pod.
+__device__ __noinline__ void fl_hdr_fill(uint64_t cats_a, int c_a, int C_a) {
+  const DevCatalog* cats = (const DevCatalog*)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(cats_a >> 32)) << 32) |
+                                               (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)cats_a));
+  hdr_fill_wave((CatHdr LDS*)&fl_hdrw, &cats[U(c_a)], U(C_a));
+  wave_sync();
+}
+__device__ __noinline__ uint64_t fl_fits_filter(int cat_a, uint64_t X0, int64_t q_lane, int32_t j0_lane, uint32_t rmask_a,
+                                                uint64_t cats_a) {
+  const int cat = U(cat_a);
+  const DevDict& D = g_D;
+  if (cat >= 8) fl_hdr_fill(cats_a, cat, D.C);
+  const CatHdr LDS* H = cat < 8 ? (const CatHdr LDS*)&g_hdr[cat] : (const CatHdr LDS*)&fl_hdrw;
+  uint64_t nb = 0;
+  const uint64_t X = fits_filter(D, H, X0, q_lane, j0_lane, (const int64_t LDS*)g_fitv, (uint32_t)U((int)rmask_a),
+                                 (RowPtr LDS*)fl_rl, &nb, fl_fitj);
+  if (LANE == 0) fl_io[1] = nb;
+  wave_sync();
+  return X;
+}
+
 // NodeClaim.Add in full for the fast lane (Compatible + Add of the requirements, the type filter, minValues) as its
 // own function: the merge is the rare attempt, and inlined its registers burden every pod's append path. On
 // success the merged requirements (and topology codes) are stored and the memo marks the shape-level merged.
 // Returns this lane's word of the remaining types (0 everywhere: failed); fl_io[0] = permanent failure,
 // fl_io[1] = algorithmic bytes read.
-__shared__ uint64_t fl_io[2];
 template <bool TOPO>
 __device__ __noinline__ uint64_t fl_full_add(uint64_t kargs, int sl_a, int cat_a, int ncx_a, uint64_t X0, int64_t q_lane,
                                              int32_t j0_lane, int staged_a) {
@@ -1667,10 +1692,20 @@ if (!FL_NOTIME && tmg) {                                    \
           ReqView rv;
           bool perm = true;  // a failure here is permanent (NC_NEVER) unless it is Compatible's undefined-key rule
           if (!full_add) {
+#if FL_NI
+            if (n_rr <= 4 && cat < 8) {
+              X = fits_lean(D, (const CatHdr LDS*)&g_hdr[cat], X0, q_lane, j0_lane, (const int64_t LDS*)g_fitv, rr_list,
+                            n_rr, FL_NB, (int32_t LDS*)fl_fitj);
+            } else {
+              X = fl_fits_filter(cat, X0, q_lane, j0_lane, A->req_res_mask, (uint64_t)(uintptr_t)A->cats);
+              bytes += fl_io[1];
+            }
+#else
             X = n_rr <= 4 ? fits_lean(D, hdr(cat), X0, q_lane, j0_lane, (const int64_t LDS*)g_fitv, rr_list, n_rr, FL_NB,
                                       (int32_t LDS*)fl_fitj)
                           : fits_filter(D, hdr(cat), X0, q_lane, j0_lane, (const int64_t LDS*)g_fitv, A->req_res_mask,
                                         (RowPtr LDS*)fl_rl, &bytes, fl_fitj);
+#endif
             if (FL_CNT32) FL_CNT32_APP;
             else bytes += (uint64_t)D.TW * 8 + KP_NRES * 8 + 8;
           } else if (FL_SPLIT) {
