@@ -25,7 +25,8 @@
 #define FASTLANE 1  // solve_kernel: wave-0 fast lane for merge-free placements (0 = full path only)
 #endif
 #ifndef FL_NI
-#define FL_NI 0  // variant under measurement: the append attempt's rare paths out of line
+#define FL_NI 1  // the append attempt's rare Fits paths (>4 resource rows, catalogue >= 8) out of line: frees
+                 // registers in the append loop (config 2 kernel 211.6 -> 206.4 ms, same algorithmic bytes)
 #endif
 #ifndef FL_SPLIT
 #define FL_SPLIT 0  // variant under measurement: the fast lane's full NodeClaim.Add as a separate (noinline) function
