@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define KP_ABI_VERSION 6
+#define KP_ABI_VERSION 7
 
 enum kp_status {
   KP_OK = 0,
@@ -139,7 +139,10 @@ typedef struct kp_offering {
   const char* reservation_type; /* capacity-reservation-type In {type}; NULL: DoesNotExist (R:offering.go:137) */
   double price;
   int32_t available;
-  int32_t reservation_capacity; /* reserved offerings: device path returns KP_E_UNSUPPORTED in ABI v1 */
+  int32_t reservation_capacity; /* Offering.ReservationCapacity (R:offering.go:178): read by ReservedOfferingFilter.
+                                   Filter and launch plans take reserved offerings (ABI v7); a Solve / cluster plan
+                                   over a catalogue holding an offering with a reservation id or type returns
+                                   KP_E_UNSUPPORTED (the ReservationManager's accounting is not modelled) */
 } kp_offering;
 
 /* cloudprovider.InstanceType after InjectOfferings. */
@@ -515,12 +518,13 @@ int32_t kp_filter_refresh(kp_filter_plan* plan, const kp_catalog* cat);
 /* ---- launch-side selection (instance.DefaultProvider.Create) -------------------------------------
  * For each NodeClaim: filterInstanceTypes (R:pkg/providers/instance/instance.go:242-270) =
  *   CompatibleAvailableFilter (R:filter.go:39-64) -> CapacityReservationTypeFilter / CapacityBlockFilter /
- *   ReservedOfferingFilter (R:filter.go:66-274; no-ops: reserved offerings are not representable in ABI v2) ->
+ *   ReservedOfferingFilter (R:filter.go:66-274: they replace a type's offerings; offerings equal in every label form
+ *   one class, so a replaced slice keeps whole classes) ->
  *   ExoticInstanceTypeFilter (R:filter.go:279-318) -> SpotInstanceFilter (R:filter.go:328-386), each filter that
  *   empties the set failing the launch with InsufficientCapacityError; then InstanceTypes.Truncate(reqs,
  *   max_types) = OrderByPrice + cut + SatisfiesMinValues (error -> CreateError "InstanceTypeFilteringFailed");
  * getCapacityType (R:instance.go:504-518): reserved, then spot, if the requirements allow it and some remaining
- *   type has an available compatible offering of it, else on-demand;
+ *   type has an available compatible offering of it (in its replaced offering slice), else on-demand;
  * checkODFallback (R:instance.go:336-355): on-demand launch while flexible to spot with < 5 types (a warning);
  * getOverrides (R:instance.go:392-439): per remaining type (in truncated order) its available offerings compatible
  *   with the requirements narrowed to the chosen capacity type, in the type's offering order, whose zone has a
@@ -542,7 +546,7 @@ enum kp_launch_filter { KP_FILTER_COMPATIBLE_AVAILABLE = 0, KP_FILTER_EXOTIC = 4
 
 typedef struct kp_launch_result {
   int32_t status;             /* enum kp_launch_status */
-  int32_t capacity_type;      /* 0 on-demand, 1 spot (KP_LAUNCH_OK only) */
+  int32_t capacity_type;      /* 0 on-demand, 1 spot, 2 reserved (KP_LAUNCH_OK only) */
   uint32_t n_types;           /* types written to out_types (after filters + Truncate) */
   uint32_t n_overrides;       /* overrides written to out_overrides */
   int32_t failed_filter;      /* enum kp_launch_filter when INSUFFICIENT_CAPACITY, else -1 */
@@ -550,6 +554,9 @@ typedef struct kp_launch_result {
   uint32_t rejected_exotic;   /* types removed by ExoticInstanceTypeFilter */
   uint32_t rejected_spot;     /* types removed by SpotInstanceFilter */
   int32_t od_fallback_warning;/* checkODFallback would log its error */
+  int32_t reservation_type;   /* capacity_type 2: getCapacityReservationType (R:instance.go:520-530), 0 default,
+                                 1 capacity-block, -1 none; else -1 */
+  uint32_t rejected_reservation; /* types removed by the three reservation filters */
   int32_t reserved_;
 } kp_launch_result;
 

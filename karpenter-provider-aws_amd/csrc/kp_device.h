@@ -192,7 +192,9 @@ struct LaunchOut {  // kp_launch_result as the device writes it
   uint32_t n_types, n_overrides;
   int32_t failed_filter;
   uint32_t n_compatible, rejected_exotic, rejected_spot;
-  int32_t od_fallback_warning, pad_;
+  int32_t od_fallback_warning, reservation_type;
+  uint32_t rejected_reservation;
+  int32_t pad_;
 };
 struct LaunchArgs {
   const DevDict* dict;
@@ -204,6 +206,11 @@ struct LaunchArgs {
   int32_t ct_key;             // dictionary key of karpenter.sh/capacity-type
   int32_t MO;                 // offerings per type (stride of ofs_cls)
   uint64_t cls_spot, cls_od;  // offering classes whose capacity type is spot / on-demand
+  int32_t res_bit, pad0_;     // dictionary value bit of karpenter.sh/capacity-type reserved (-1: absent)
+  uint64_t cls_res;           // offering classes whose capacity type is reserved
+  uint64_t cls_rt0, cls_rt1;  // classes whose capacity-reservation-type is default / capacity-block
+  const double* price_all;    // [T][C] cheapest offering of each class, any availability (CapacityBlockFilter)
+  const int32_t* rcap;        // [T][C] greatest reservation capacity over the class's available offerings
   const uint8_t* q_reqs;      // [n] KReqs
   const int64_t* q_requests;  // [n][NRES]
   const uint32_t* list_off;   // [n+1] CSR of the requests' instance-type lists

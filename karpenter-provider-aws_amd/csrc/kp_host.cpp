@@ -188,6 +188,9 @@ struct HostOffering {
   bool has_zone, has_zid;
   double price;
   bool available;
+  string rid, rt;  // capacity-reservation-id / -type In {..}; DoesNotExist when !has_rid / !has_rt
+  bool has_rid = false, has_rt = false;
+  int32_t rcap = 0;  // ReservationCapacity
 };
 struct HostType {
   string name;
@@ -223,6 +226,7 @@ struct kp_catalog {
   uint64_t seqnum;
   uint64_t uid;  // process-unique identity (a new upload never reuses one, unlike its address)
   vector<HostType> types;
+  bool reservations = false;  // some offering carries a capacity-reservation id or type
 };
 
 namespace {
@@ -512,9 +516,21 @@ struct HostCat {
 };
 
 struct ClassKey {
-  int ct, zone, zid;
-  bool operator<(const ClassKey& o) const { return std::tie(ct, zone, zid) < std::tie(o.ct, o.zone, o.zid); }
+  int ct, zone, zid, rid = -1, rt = -1;
+  bool operator<(const ClassKey& o) const {
+    return std::tie(ct, zone, zid, rid, rt) < std::tie(o.ct, o.zone, o.zid, o.rid, o.rt);
+  }
 };
+// An offering's class: its label values as dictionary bits (-1: no such requirement / DoesNotExist).
+ClassKey ClassOf(const Dict& d, const HostOffering& o) {
+  return {d.bit(d.key(kCapType), o.ct), o.has_zone ? d.bit(d.key(kZone), o.zone) : -1,
+          o.has_zid ? d.bit(d.key(kZoneID), o.zid) : -1, o.has_rid ? d.bit(d.key(kResID), o.rid) : -1,
+          o.has_rt ? d.bit(d.key(kResType), o.rt) : -1};
+}
+OfferClass ClassOfKey(const ClassKey& k) {
+  return {(int16_t)k.ct, (int16_t)k.zone, (int16_t)k.zid, (int16_t)k.rid, (int16_t)k.rt, {0, 0, 0}};
+}
+ClassKey KeyOfClass(const OfferClass& c) { return {c.ct_bit, c.zone_bit, c.zid_bit, c.rid_bit, c.rt_bit}; }
 
 // Offering section of a compiled catalogue: available classes per type, cheapest price per (type, class), and the
 // class-major copy (offering.go:115-147 createOfferings: Available = !ICE && hasPrice && zone offered). Also the
@@ -525,11 +541,9 @@ void FillOfferings(const Dict& d, const vector<HostType>& types, int TW, const m
   const int C = (int)classes.size();
   hc.offer_avail.assign((size_t)C * TW, 0);
   hc.price.assign((size_t)T * C, std::numeric_limits<double>::infinity());
-  const int kct = d.key(kCapType), kz = d.key(kZone), kzid = d.key(kZoneID);
   for (int t = 0; t < T; t++)
     for (auto& o : types[t].offs) {
-      ClassKey ck{d.bit(kct, o.ct), o.has_zone ? d.bit(kz, o.zone) : -1, o.has_zid ? d.bit(kzid, o.zid) : -1};
-      const int c = classes.at(ck);
+      const int c = classes.at(ClassOf(d, o));
       if (!o.available) continue;
       hc.offer_avail[(size_t)c * TW + t / 64] |= 1ull << (t % 64);
       double& p = hc.price[(size_t)t * C + c];
@@ -694,15 +708,18 @@ void HostFilterTypes(const Dict& d, const HostCat& hc, const KReqs& q, int TW, c
 
 uint64_t HostAllowedClasses(const Dict& d, const KReqs& q, const vector<OfferClass>& cls) {
   const uint64_t neg = NegOp(d, q);
+  // a reservation key the offering does not carry is DoesNotExist: compatible when the query leaves the key out or
+  // admits its absence (NotIn / DoesNotExist)
   const bool res_ok = !(q.present & d.dd.resid_key_bit) || (neg & d.dd.resid_key_bit);
   const bool rt_ok = !(q.present & d.dd.restype_key_bit) || (neg & d.dd.restype_key_bit);
-  if (!res_ok || !rt_ok) return 0;
   uint64_t m = 0;
   auto keyof = [&](int bit) { return (int)d.dd.wkey[bit / 64]; };
   for (size_t c = 0; c < cls.size(); c++) {
     bool ok = Has(d, q, keyof(cls[c].ct_bit), cls[c].ct_bit);
     if (cls[c].zone_bit >= 0) ok = ok && Has(d, q, keyof(cls[c].zone_bit), cls[c].zone_bit);
     if (cls[c].zid_bit >= 0) ok = ok && Has(d, q, keyof(cls[c].zid_bit), cls[c].zid_bit);
+    ok = ok && (cls[c].rid_bit >= 0 ? Has(d, q, keyof(cls[c].rid_bit), cls[c].rid_bit) : res_ok);
+    ok = ok && (cls[c].rt_bit >= 0 ? Has(d, q, keyof(cls[c].rt_bit), cls[c].rt_bit) : rt_ok);
     if (ok) m |= 1ull << c;
   }
   return m;
@@ -914,12 +931,15 @@ int32_t kp_catalog_upload(kp_ctx* ctx, const kp_catalog_desc* desc, uint64_t seq
     h.cap_present = t.capacity.present;
     for (uint32_t j = 0; j < t.n_offerings; j++) {
       const kp_offering& o = t.offerings[j];
-      if (o.reservation_id || o.reservation_type) {
-        delete c;
-        return fail(KP_E_UNSUPPORTED, "reserved offerings (ABI v1)");
-      }
       h.offs.push_back({o.capacity_type ? o.capacity_type : "", o.zone ? o.zone : "", o.zone_id ? o.zone_id : "",
                         o.zone != nullptr, o.zone_id != nullptr, o.price, o.available != 0});
+      HostOffering& ho = h.offs.back();
+      ho.has_rid = o.reservation_id != nullptr;
+      ho.has_rt = o.reservation_type != nullptr;
+      if (ho.has_rid) ho.rid = o.reservation_id;
+      if (ho.has_rt) ho.rt = o.reservation_type;
+      ho.rcap = o.reservation_capacity;
+      c->reservations = c->reservations || ho.has_rid || ho.has_rt;
     }
     c->types.push_back(std::move(h));
   }
@@ -1911,6 +1931,8 @@ int32_t BuildBase(const kp_solve_in* in, const SolveRaw& raw, SolveBase& b) {
   DictBuilder db;
   int maxT = 1;
   for (auto* c : cats) {
+    if (c->reservations)  // NodeClaim.Add's reserveOfferings (upstream ReservationManager) is not modelled
+      return fail(KP_E_UNSUPPORTED, "capacity-reservation offerings in a Solve / cluster catalogue");
     maxT = std::max(maxT, (int)c->types.size());
     for (auto& t : c->types) {
       db.addReqs(t.reqs);
@@ -1941,7 +1963,7 @@ int32_t BuildBase(const kp_solve_in* in, const SolveRaw& raw, SolveBase& b) {
   for (auto* c : cats)
     for (auto& t : c->types)
       for (auto& o : t.offs) {
-        ClassKey ck{d.bit(d.key(kCapType), o.ct), o.has_zone ? d.bit(d.key(kZone), o.zone) : -1, o.has_zid ? d.bit(d.key(kZoneID), o.zid) : -1};
+        const ClassKey ck = ClassOf(d, o);
         if (!classes.count(ck)) {
           int id = (int)classes.size();
           classes[ck] = id;
@@ -1950,7 +1972,7 @@ int32_t BuildBase(const kp_solve_in* in, const SolveRaw& raw, SolveBase& b) {
   if (classes.size() > KP_MAX_CLASSES) return fail(KP_E_UNSUPPORTED, "%zu offering classes", classes.size());
   b.C = (int)classes.size();
   b.classes.resize(b.C);
-  for (auto& kv : classes) b.classes[kv.second] = {kv.first.ct, kv.first.zone, kv.first.zid, 0};
+  for (auto& kv : classes) b.classes[kv.second] = ClassOfKey(kv.first);
   b.d.dd.C = b.C;
   b.cats.resize(cats.size());
   uint64_t catalog_keys = 0, multi = 0;
@@ -2861,6 +2883,8 @@ int32_t CompileQueries(const kp_catalog* cat, const vector<RawReqs>& qs, Compile
       db.addLabel(kCapType, o.ct);
       db.addLabel(kZone, o.zone);
       if (o.has_zid) db.addLabel(kZoneID, o.zid);
+      if (o.has_rid) db.addLabel(kResID, o.rid);
+      if (o.has_rt) db.addLabel(kResType, o.rt);
     }
   }
   db.bounded[kResID];
@@ -2876,7 +2900,7 @@ int32_t CompileQueries(const kp_catalog* cat, const vector<RawReqs>& qs, Compile
   const Dict& d = cp.B->d;
   for (auto& t : cat->types)
     for (auto& o : t.offs) {
-      ClassKey ck{d.bit(d.key(kCapType), o.ct), o.has_zone ? d.bit(d.key(kZone), o.zone) : -1, o.has_zid ? d.bit(d.key(kZoneID), o.zid) : -1};
+      const ClassKey ck = ClassOf(d, o);
       if (!classes.count(ck)) {
         int id = (int)classes.size();
         classes[ck] = id;
@@ -2886,7 +2910,7 @@ int32_t CompileQueries(const kp_catalog* cat, const vector<RawReqs>& qs, Compile
   cp.B->C = (int)classes.size();
   cp.B->d.dd.C = cp.B->C;
   cp.B->classes.resize(cp.B->C);
-  for (auto& kv : classes) cp.B->classes[kv.second] = {kv.first.ct, kv.first.zone, kv.first.zid, 0};
+  for (auto& kv : classes) cp.B->classes[kv.second] = ClassOfKey(kv.first);
   cp.B->cats.resize(1);
   rc = CompileCatalog(d, cat->types, TW, classes, cp.B->cats[0]);
   if (rc) return rc;
@@ -2909,7 +2933,7 @@ static int32_t RefreshOfferings(kp_ctx* ctx, const kp_catalog* cat, Compiled& cp
   std::lock_guard<std::recursive_mutex> lock(ctx->mu);
   HIPCHK(hipSetDevice(ctx->device));
   map<ClassKey, int> classes;
-  for (int c = 0; c < cp.B->C; c++) classes[{cp.B->classes[c].ct_bit, cp.B->classes[c].zone_bit, cp.B->classes[c].zid_bit}] = c;
+  for (int c = 0; c < cp.B->C; c++) classes[KeyOfClass(cp.B->classes[c])] = c;
   HostCat hc;  // filled aside: the plan's host copy changes only once the device copy did
   hc.T = cp.B->cats[0].T;
   hc.S = cp.B->cats[0].S;
@@ -3080,12 +3104,29 @@ int32_t kp_filter_compatible_available(kp_ctx* ctx, const kp_catalog* cat, const
 // ---- launch-side selection (instance.DefaultProvider.Create), batched over NodeClaims -----------------
 }  // extern "C"
 
+// Launch-side reservation tables per (type, class): the cheapest offering at any availability (CapacityBlockFilter
+// reads unavailable offerings too, R:filter.go:177-189) and the greatest ReservationCapacity over the available
+// offerings (ReservedOfferingFilter, R:filter.go:247-251).
+static void FillReservationTables(const Dict& d, const vector<HostType>& types, const map<ClassKey, int>& cls_id, int C,
+                                  vector<double>& price_all, vector<int32_t>& rcap) {
+  const size_t T = types.size();
+  price_all.assign(std::max<size_t>(T * C, 1), std::numeric_limits<double>::infinity());
+  rcap.assign(std::max<size_t>(T * C, 1), INT32_MIN);
+  for (size_t t = 0; t < T; t++)
+    for (auto& o : types[t].offs) {
+      const int c = cls_id.at(ClassOf(d, o));
+      double& p = price_all[t * C + c];
+      if (o.price < p) p = o.price;
+      if (o.available) rcap[t * C + c] = std::max(rcap[t * C + c], o.rcap);
+    }
+}
+
 struct kp_launch_plan {
   kp_ctx* ctx = nullptr;
   DevBuf buf;
   LaunchArgs la;
   uint32_t n = 0, max_types = 0, ovr_stride = 0;
-  size_t o_out = 0, o_types = 0, o_ovr = 0, o_stats = 0;
+  size_t o_out = 0, o_types = 0, o_ovr = 0, o_stats = 0, o_pall = 0, o_rcap = 0;
   double prepare_ms = 0;
   const kp_catalog* cat = nullptr;  // kp_launch_refresh
   uint64_t seqnum = 0;              // catalogue seqnum the resident offerings reflect
@@ -3106,10 +3147,12 @@ int32_t kp_launch_prepare(kp_ctx* ctx, const kp_catalog* cat, const kp_launch_re
   if (n_subnet_zones > 255) return fail(KP_E_UNSUPPORTED, "%u subnet zones", n_subnet_zones);
   const int T = (int)cat->types.size();
   for (auto& t : cat->types) {
-    std::set<std::pair<string, string>> seen;  // overrides per type <= subnet zones needs one offering per (ct, zone)
+    // overrides per type <= subnet zones: one offering per (capacity type, zone), except reserved ones, which the
+    // ReservedOfferingFilter narrows to one per zone (then one per (zone, reservation) keeps classes single)
+    std::set<std::tuple<string, string, string, string>> seen;
     for (auto& o : t.offs) {
-      if (o.ct == "reserved") return fail(KP_E_UNSUPPORTED, "reserved offerings");
-      if (o.has_zone && !seen.insert({o.ct, o.zone}).second)
+      const bool res = o.ct == "reserved";
+      if (o.has_zone && !seen.insert({o.ct, o.zone, res ? o.rid : "", res ? o.rt : ""}).second)
         return fail(KP_E_UNSUPPORTED, "%s: two %s offerings in zone %s", t.name.c_str(), o.ct.c_str(), o.zone.c_str());
     }
   }
@@ -3159,17 +3202,26 @@ int32_t kp_launch_prepare(kp_ctx* ctx, const kp_catalog* cat, const kp_launch_re
   int MO = 1;
   for (auto& t : cat->types) MO = std::max(MO, (int)t.offs.size() + 1);
   vector<uint8_t> ofs_cls((size_t)T * MO, 0xFF);
-  const int kct = d.key(kCapType), kz = d.key(kZone), kzid = d.key(kZoneID);
+  const int kct = d.key(kCapType), kz = d.key(kZone);
   std::map<ClassKey, int> cls_id;
-  for (int c = 0; c < C; c++) cls_id[ClassKey{cp.B->classes[c].ct_bit, cp.B->classes[c].zone_bit, cp.B->classes[c].zid_bit}] = c;
+  for (int c = 0; c < C; c++) cls_id[KeyOfClass(cp.B->classes[c])] = c;
   for (int t = 0; t < T; t++) {
     int j = 0;
-    for (auto& o : cat->types[t].offs) {
-      ClassKey ck{d.bit(kct, o.ct), o.has_zone ? d.bit(kz, o.zone) : -1, o.has_zid ? d.bit(kzid, o.zid) : -1};
-      ofs_cls[(size_t)t * MO + j++] = (uint8_t)cls_id.at(ck);
-    }
+    for (auto& o : cat->types[t].offs) ofs_cls[(size_t)t * MO + j++] = (uint8_t)cls_id.at(ClassOf(d, o));
   }
   const int spot_bit = kct >= 0 ? d.bit(kct, "spot") : -1, od_bit = kct >= 0 ? d.bit(kct, "on-demand") : -1;
+  const int res_bit = kct >= 0 ? d.bit(kct, "reserved") : -1, krt = d.key(kResType);
+  const int rt0_bit = krt >= 0 ? d.bit(krt, "default") : -1, rt1_bit = krt >= 0 ? d.bit(krt, "capacity-block") : -1;
+  uint64_t cls_res = 0, cls_rt0 = 0, cls_rt1 = 0;
+  for (int c = 0; c < C; c++) {
+    const OfferClass& oc = cp.B->classes[c];
+    if (res_bit >= 0 && oc.ct_bit == res_bit) cls_res |= 1ull << c;
+    if (rt0_bit >= 0 && oc.rt_bit == rt0_bit) cls_rt0 |= 1ull << c;
+    if (rt1_bit >= 0 && oc.rt_bit == rt1_bit) cls_rt1 |= 1ull << c;
+  }
+  vector<double> price_all;
+  vector<int32_t> rcap;
+  FillReservationTables(d, cat->types, cls_id, C, price_all, rcap);
   uint64_t cls_spot = 0, cls_od = 0;
   vector<int8_t> cls_zone(std::max(C, 1), -1);
   for (int c = 0; c < C; c++) {
@@ -3195,6 +3247,8 @@ int32_t kp_launch_prepare(kp_ctx* ctx, const kp_catalog* cat, const kp_launch_re
   const size_t o_exo = blob.put(exotic);
   const size_t o_cz = blob.put(cls_zone);
   const size_t o_oc = blob.put(ofs_cls);
+  plan->o_pall = blob.put(price_all);
+  plan->o_rcap = blob.put(rcap);
   const size_t host_bytes = blob.host.size();
   const uint32_t ovr_stride = std::max<uint32_t>(1, max_types * std::max<uint32_t>(1, n_subnet_zones));
   plan->o_out = blob.reserve(sizeof(kp_launch_result) * std::max<uint32_t>(n, 1));
@@ -3220,6 +3274,12 @@ int32_t kp_launch_prepare(kp_ctx* ctx, const kp_catalog* cat, const kp_launch_re
   la.MO = MO;
   la.cls_spot = cls_spot;
   la.cls_od = cls_od;
+  la.res_bit = res_bit;
+  la.cls_res = cls_res;
+  la.cls_rt0 = cls_rt0;
+  la.cls_rt1 = cls_rt1;
+  la.price_all = (const double*)(base + plan->o_pall);
+  la.rcap = (const int32_t*)(base + plan->o_rcap);
   la.q_reqs = base + o_q;
   la.q_requests = (const int64_t*)(base + o_qr);
   la.list_off = (const uint32_t*)(base + o_off);
@@ -3292,9 +3352,24 @@ int32_t kp_launch_refresh(kp_launch_plan* plan, const kp_catalog* cat) {
   if (!plan || !cat) return fail(KP_E_INVAL, "null argument");
   if (cat != plan->cat || (int)cat->types.size() != plan->T)
     return fail(KP_E_INVAL, "kp_launch_refresh: the plan was prepared on another catalogue");
-  const int32_t rc = RefreshOfferings(plan->ctx, cat, plan->cp, plan->coff, (uint8_t*)plan->buf.p);
-  if (rc == KP_OK) plan->seqnum = cat->seqnum;
-  return rc;
+  int32_t rc = RefreshOfferings(plan->ctx, cat, plan->cp, plan->coff, (uint8_t*)plan->buf.p);
+  if (rc != KP_OK) return rc;
+  {  // the reservation tables follow availability and price too
+    std::lock_guard<std::recursive_mutex> lock(plan->ctx->mu);
+    map<ClassKey, int> cls_id;
+    for (int c = 0; c < plan->cp.B->C; c++) cls_id[KeyOfClass(plan->cp.B->classes[c])] = c;
+    vector<double> price_all;
+    vector<int32_t> rcap;
+    FillReservationTables(plan->cp.B->d, cat->types, cls_id, plan->cp.B->C, price_all, rcap);
+    uint8_t* base = (uint8_t*)plan->buf.p;
+    HIPCHK(hipMemcpyAsync(base + plan->o_pall, price_all.data(), price_all.size() * sizeof(double),
+                          hipMemcpyHostToDevice, plan->ctx->stream));
+    HIPCHK(hipMemcpyAsync(base + plan->o_rcap, rcap.data(), rcap.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+                          plan->ctx->stream));
+    HIPCHK(hipStreamSynchronize(plan->ctx->stream));
+  }
+  plan->seqnum = cat->seqnum;
+  return KP_OK;
 }
 
 void kp_launch_plan_destroy(kp_launch_plan* p) {

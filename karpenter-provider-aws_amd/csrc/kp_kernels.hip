@@ -177,7 +177,9 @@ __device__ __forceinline__ void hdr_fill_wave(CatHdr LDS* h, const DevCatalog* g
   if (lane < NWD) reinterpret_cast<uint64_t LDS*>(&h->d)[lane] = reinterpret_cast<const uint64_t*>(g)[lane];
   const OfferClass* gc = g->cls;
   const int32_t* gn = g->fit_n;
-  if (lane < 2 * HDR_CLS && lane < 2 * C)
+  constexpr int CW = sizeof(OfferClass) / 8;
+  static_assert(CW * HDR_CLS <= 64, "one wave copies the class table");
+  if (lane < CW * HDR_CLS && lane < CW * C)
     reinterpret_cast<uint64_t LDS*>(h->cls)[lane] = reinterpret_cast<const uint64_t*>(gc)[lane];
   if (lane < KP_NRES) {
     h->fit_n[lane] = gn[lane];
@@ -324,26 +326,38 @@ __device__ __forceinline__ bool bit_of(uint64_t allowed_lane_word, int bit) {
   return (w >> (bit & 63)) & 1;
 }
 
-// Offering classes compatible with requirement set rv (Offerings.Compatible + reservation-key DNE test).
-template <class ClsP>
+// Offering classes compatible with requirement set rv (Offerings.Compatible): a reservation key the class does not
+// carry is DoesNotExist, compatible when rv leaves the key out or admits its absence.
+// RES = false (Solve, consolidation: their catalogues hold no reservation classes) skips the reservation bits.
+template <bool RES = false, class ClsP>
 __device__ uint64_t allowed_classes(const DevDict& D, ClsP cls_tab, const ReqView& rv, uint64_t allowed, uint64_t negR) {
   const bool res_ok = !(rv.present & D.resid_key_bit) || (negR & D.resid_key_bit);
   const bool rt_ok = !(rv.present & D.restype_key_bit) || (negR & D.restype_key_bit);
-  // lane c evaluates class c: its three value bits are fetched from the owning lanes' allowed words
+  // lane c evaluates class c: its value bits are fetched from the owning lanes' allowed words
   const int lane = LANE;
-  int ct_bit = 0, zone_bit = -1, zid_bit = -1;
+  int ct_bit = 0, zone_bit = -1, zid_bit = -1, rid_bit = -1, rt_bit = -1;
   if (lane < D.C) {
     ct_bit = cls_tab[lane].ct_bit;
     zone_bit = cls_tab[lane].zone_bit;
     zid_bit = cls_tab[lane].zid_bit;
+    if (RES) {
+      rid_bit = cls_tab[lane].rid_bit;
+      rt_bit = cls_tab[lane].rt_bit;
+    }
   }
   const uint64_t w1 = __shfl(allowed, ct_bit >> 6, 64);
   const uint64_t w2 = __shfl(allowed, zone_bit >= 0 ? zone_bit >> 6 : 0, 64);
   const uint64_t w3 = __shfl(allowed, zid_bit >= 0 ? zid_bit >> 6 : 0, 64);
-  const bool ok = lane < D.C && ((w1 >> (ct_bit & 63)) & 1) && (zone_bit < 0 || ((w2 >> (zone_bit & 63)) & 1)) &&
-                  (zid_bit < 0 || ((w3 >> (zid_bit & 63)) & 1));
-  const uint64_t cls = __ballot(ok);
-  return (res_ok && rt_ok) ? cls : 0;
+  bool ok = lane < D.C && ((w1 >> (ct_bit & 63)) & 1) && (zone_bit < 0 || ((w2 >> (zone_bit & 63)) & 1)) &&
+            (zid_bit < 0 || ((w3 >> (zid_bit & 63)) & 1));
+  if (RES && __ballot(rid_bit >= 0 || rt_bit >= 0)) {  // reservation classes (launch / filter plans only)
+    const uint64_t w4 = __shfl(allowed, rid_bit >= 0 ? rid_bit >> 6 : 0, 64);
+    const uint64_t w5 = __shfl(allowed, rt_bit >= 0 ? rt_bit >> 6 : 0, 64);
+    ok = ok && (rid_bit < 0 ? res_ok : ((w4 >> (rid_bit & 63)) & 1)) && (rt_bit < 0 ? rt_ok : ((w5 >> (rt_bit & 63)) & 1));
+  } else {
+    ok = ok && res_ok && rt_ok;
+  }
+  return __ballot(ok);
 }
 
 // first j in [0, n) with vals[j] >= q (ascending vals), n if none; 64-ary search across the wave.
@@ -2752,7 +2766,7 @@ __global__ __launch_bounds__(FEAS_WAVES * 64) void feasibility_kernel(FeasArgs a
     rv.minv = Q->minv;
     const uint64_t negQ = negop_mask(rv.present, rv.compl_, rv.nz);
     const uint64_t allowed = allowed_word(D, rv, v, vint_global(a.vint));
-    const uint64_t cls = allowed_classes(D, Cg.cls, rv, allowed, negQ);
+    const uint64_t cls = allowed_classes<true>(D, Cg.cls, rv, allowed, negQ);
     s_allowed[wave][lane] = allowed;
     const uint32_t rmask = (uint32_t)__ballot(rq_lane > 0);
     wave_sync();
@@ -2939,10 +2953,10 @@ __global__ __launch_bounds__(LAUNCH_WAVES * 64) void launch_kernel(LaunchArgs a)
     rv.minv = Q->minv;
     const uint64_t negQ = negop_mask(rv.present, rv.compl_, rv.nz);
     const uint64_t allowed = allowed_word(D, rv, v, vint_global(a.vint));
-    const uint64_t cls = allowed_classes(D, Cg.cls, rv, allowed, negQ);
+    const uint64_t cls = allowed_classes<true>(D, Cg.cls, rv, allowed, negQ);
     // the same with the capacity-type key opened: getCapacityType / getOverrides pin it to one value
     const bool ctw = a.ct_key >= 0 && lane < D.W && D.wkey[lane] == a.ct_key;
-    const uint64_t cls_noct = allowed_classes(D, Cg.cls, rv, ctw ? D.validbits[lane] : allowed, negQ);
+    const uint64_t cls_noct = allowed_classes<true>(D, Cg.cls, rv, ctw ? D.validbits[lane] : allowed, negQ);
     L.allowed[lane] = allowed;
     const int64_t rq_lane = lane < KP_NRES ? a.q_requests[(size_t)q * KP_NRES + lane] : 0;
     const uint32_t rmask = (uint32_t)__ballot(rq_lane > 0);
@@ -2964,6 +2978,8 @@ __global__ __launch_bounds__(LAUNCH_WAVES * 64) void launch_kernel(LaunchArgs a)
     res.rejected_exotic = 0;
     res.rejected_spot = 0;
     res.od_fallback_warning = 0;
+    res.reservation_type = -1;
+    res.rejected_reservation = 0;
     res.pad_ = 0;
     // ---- CompatibleAvailableFilter (R:filter.go:51-63) -----------------------------------------------
     int m = 0, n_generic = 0;
@@ -3017,13 +3033,170 @@ __global__ __launch_bounds__(LAUNCH_WAVES * 64) void launch_kernel(LaunchArgs a)
       res.status = KP_LAUNCH_INSUFFICIENT_CAPACITY;
       res.failed_filter = KP_FILTER_COMPATIBLE_AVAILABLE;
     }
+    // ---- CapacityReservationType / CapacityBlock / ReservedOffering filters (R:filter.go:66-274) -----------
+    // Each replaces a kept type's offering slice. As class sets: every remaining type keeps the classes in M
+    // (the first two filters narrow all survivors alike), and after the third (rof) type t keeps rof_pick(t).
+    uint64_t M = ~0ull;
+    bool rof = false;
+    const bool has_res = a.res_bit >= 0 ? bit_of(allowed, a.res_bit) : (!ct_present || ct_compl);
+    const uint64_t res_cand = cls & a.cls_res;  // compatible reserved classes
+    // ReservedOfferingFilter's choice for type t: per zone, the available compatible reserved class in M with the
+    // greatest reservation capacity (the first in offering order on ties)
+    auto rof_pick = [&](int t) -> uint64_t {
+      const uint64_t cand = res_cand & M;
+      uint64_t pick = 0;
+      for (int j = 0; j < a.MO && cand; j++) {
+        const int c = a.ofs_cls[(size_t)t * a.MO + j];
+        if (c == 0xFF) break;
+        if (!((cand >> c) & 1) || !(Cg.price[(size_t)t * D.C + c] < INF)) continue;
+        const int z = Cg.cls[c].zone_bit;
+        int cur = -1;
+        for (uint64_t pp = pick; pp; pp &= pp - 1)
+          if (Cg.cls[__builtin_ctzll(pp)].zone_bit == z) {
+            cur = __builtin_ctzll(pp);
+            break;
+          }
+        if (cur < 0) pick |= 1ull << c;
+        else if (a.rcap[(size_t)t * D.C + c] > a.rcap[(size_t)t * D.C + cur]) pick = (pick & ~(1ull << cur)) | (1ull << c);
+      }
+      return pick;
+    };
+    auto om_of = [&](int t) -> uint64_t { return rof ? rof_pick(t) : M; };
+    if (m && has_res && res_cand) {
+      // CapacityReservationTypeFilter (R:filter.go:80-144): the partition with the cheapest available compatible
+      // reserved offering (ties: default before capacity-block)
+      double pmin[2] = {INF, INF};
+      for (int i = lane; i < m; i += 64) {
+        const int t = (int)(L.val[i] & 4095u);
+        for (uint64_t mm = res_cand & (a.cls_rt0 | a.cls_rt1); mm; mm &= mm - 1) {
+          const int c = __builtin_ctzll(mm);
+          const double p = Cg.price[(size_t)t * D.C + c];
+          const int k = ((a.cls_rt1 >> c) & 1) ? 1 : 0;
+          pmin[k] = p < pmin[k] ? p : pmin[k];
+        }
+      }
+      for (int o = 32; o >= 1; o >>= 1)
+        for (int k = 0; k < 2; k++) {
+          const double w = __shfl_xor(pmin[k], o, 64);
+          pmin[k] = w < pmin[k] ? w : pmin[k];
+        }
+      const uint64_t selm = res_cand & (pmin[1] < pmin[0] ? a.cls_rt1 : a.cls_rt0);
+      auto in_part = [&](int t) {
+        for (uint64_t mm = selm; mm; mm &= mm - 1)
+          if (Cg.price[(size_t)t * D.C + __builtin_ctzll(mm)] < INF) return true;
+        return false;
+      };
+      if (pmin[0] < INF || pmin[1] < INF) {  // the selected partition has types
+        const int m0 = m;
+        m = launch_compact(L, m, [&](uint64_t, uint32_t vv) { return in_part((int)(vv & 4095u)); });
+        M = a.cls_res & (pmin[1] < pmin[0] ? a.cls_rt1 : a.cls_rt0);
+        res.rejected_reservation += (uint32_t)(m0 - m);
+      }
+      // CapacityBlockFilter (R:filter.go:160-225): when the first offering of the first type is a capacity block,
+      // keep the one type whose cheapest capacity-block offering (any availability) is the cheapest
+      bool should = false;
+      {
+        const int t0 = (int)(L.val[0] & 4095u);
+        for (int j = 0; j < a.MO; j++) {
+          const int c = a.ofs_cls[(size_t)t0 * a.MO + j];
+          if (c == 0xFF) break;
+          if ((M >> c) & 1) {
+            should = (a.cls_rt1 >> c) & 1;
+            break;
+          }
+        }
+      }
+      if (should) {
+        const uint64_t cb = M & a.cls_res & a.cls_rt1;
+        double best_p = INF;
+        int best_i = -1, best_c = -1;
+        for (int base = 0; base < m; base += 64) {
+          const int i = base + lane;
+          double p = INF;
+          int sc = -1;
+          if (i < m) {
+            const int t = (int)(L.val[i] & 4095u);
+            for (int j = 0; j < a.MO; j++) {
+              const int c = a.ofs_cls[(size_t)t * a.MO + j];
+              if (c == 0xFF) break;
+              if (!((cb >> c) & 1)) continue;
+              const double pc = a.price_all[(size_t)t * D.C + c];
+              if (sc < 0 || pc < p) {
+                p = pc;
+                sc = c;
+              }
+            }
+          }
+          // first entry with the smallest price in this chunk
+          double wp = sc >= 0 ? p : INF;
+          int wi = sc >= 0 ? i : INT32_MAX;
+          for (int o = 32; o >= 1; o >>= 1) {
+            const double op = __shfl_xor(wp, o, 64);
+            const int oi = __shfl_xor(wi, o, 64);
+            if (op < wp || (op == wp && oi < wi)) {
+              wp = op;
+              wi = oi;
+            }
+          }
+          const int wc = __shfl(sc, wi == INT32_MAX ? 0 : (wi & 63), 64);
+          if (wi != INT32_MAX && (best_i < 0 || wp < best_p)) {
+            best_p = wp;
+            best_i = wi;
+            best_c = wc;
+          }
+        }
+        if (best_i >= 0) {
+          const uint64_t k = L.key[best_i];
+          const uint32_t vv = L.val[best_i];
+          wave_sync();
+          if (lane == 0) {
+            L.key[0] = k;
+            L.val[0] = vv;
+          }
+          wave_sync();
+          res.rejected_reservation += (uint32_t)(m - 1);
+          m = 1;
+          M = 1ull << best_c;
+        }
+      }
+      // ReservedOfferingFilter (R:filter.go:241-274): types without an available compatible reserved offering are
+      // rejected, unless that rejects all
+      int n_keep = 0;
+      for (int i = lane; i < m; i += 64) n_keep += rof_pick((int)(L.val[i] & 4095u)) != 0;
+      for (int o = 32; o >= 1; o >>= 1) n_keep += __shfl_xor(n_keep, o, 64);
+      if (n_keep > 0) {
+        const int m0 = m;
+        m = launch_compact(L, m, [&](uint64_t, uint32_t vv) { return rof_pick((int)(vv & 4095u)) != 0; });
+        rof = true;
+        res.rejected_reservation += (uint32_t)(m0 - m);
+      }
+      if (M != ~0ull || rof) {  // OrderByPrice reads the replaced slices
+        for (int i = lane; i < m; i += 64) {
+          const int t = (int)(L.val[i] & 4095u);
+          double cheapest = INF;
+          for (uint64_t mm = cls & om_of(t); mm; mm &= mm - 1) {
+            const double p = Cg.price[(size_t)t * D.C + __builtin_ctzll(mm)];
+            cheapest = p < cheapest ? p : cheapest;
+          }
+          L.key[i] = (uint64_t)__double_as_longlong(cheapest);
+        }
+        wave_sync();
+      }
+    }
+    const bool sliced = M != ~0ull || rof;  // every remaining type holds reserved offerings only
     // ---- ExoticInstanceTypeFilter (R:filter.go:289-314) -------------------------------------------------
+    if (m && !hasMin) {
+      int ng = 0;  // n_generic of the list the reservation filters left
+      for (int i = lane; i < m; i += 64) ng += !(L.val[i] & 0x80000000u);
+      for (int o = 32; o >= 1; o >>= 1) ng += __shfl_xor(ng, o, 64);
+      n_generic = ng;
+    }
     if (m && !hasMin && n_generic > 0 && n_generic < m) {
       res.rejected_exotic = (uint32_t)(m - n_generic);
       m = launch_compact(L, m, [](uint64_t, uint32_t vv) { return !(vv & 0x80000000u); });
     }
-    // ---- SpotInstanceFilter (R:filter.go:342-382) ---------------------------------------------------------
-    if (m && !hasMin && has_od && has_spot) {
+    // ---- SpotInstanceFilter (R:filter.go:342-382): a no-op over reserved-only slices (no on-demand offering) ----
+    if (m && !hasMin && has_od && has_spot && !sliced) {
       double od_min = INF;
       bool any_spot = false;
       for (int base = 0; base < m; base += 64) {
@@ -3056,6 +3229,9 @@ __global__ __launch_bounds__(LAUNCH_WAVES * 64) void launch_kernel(LaunchArgs a)
               if (p <= od_min) cheap = true;
             }
           }
+          // types with an available compatible reserved offering are always kept (R:filter.go:368-371)
+          for (uint64_t mm = res_cand; mm; mm &= mm - 1)
+            if (Cg.price[(size_t)t * D.C + __builtin_ctzll(mm)] < INF) return true;
           return cheap || !has;
         });
         res.rejected_spot = (uint32_t)(m0 - m);
@@ -3110,32 +3286,51 @@ __global__ __launch_bounds__(LAUNCH_WAVES * 64) void launch_kernel(LaunchArgs a)
         res.status = KP_LAUNCH_MINVALUES;
       } else {
         // ---- getCapacityType (R:instance.go:504-518) + checkODFallback (:336-355) -------------------------
-        const uint64_t spot_any_cls = cls_noct & a.cls_spot;
-        bool spot_ok = false;
-        if (has_spot)
-          for (int i = lane; i < cut; i += 64) {
-            const int t = (int)(L.val[i] & 4095u);
-            for (uint64_t mm = spot_any_cls; mm; mm &= mm - 1)
+        // reserved first (R:instance.go:506), then spot, over the (replaced) offering slices
+        bool res_ok = false, spot_ok = false;
+        for (int i = lane; i < cut; i += 64) {
+          const int t = (int)(L.val[i] & 4095u);
+          const uint64_t om = om_of(t) & cls_noct;
+          if (has_res)
+            for (uint64_t mm = om & a.cls_res; mm; mm &= mm - 1)
+              if (Cg.price[(size_t)t * D.C + __builtin_ctzll(mm)] < INF) res_ok = true;
+          if (has_spot)
+            for (uint64_t mm = om & a.cls_spot; mm; mm &= mm - 1)
               if (Cg.price[(size_t)t * D.C + __builtin_ctzll(mm)] < INF) spot_ok = true;
+        }
+        const bool ct_res = has_res && __ballot(res_ok) != 0;
+        const bool ct_spot = !ct_res && has_spot && __ballot(spot_ok) != 0;
+        res.capacity_type = ct_res ? 2 : ct_spot ? 1 : 0;
+        res.od_fallback_warning = (!ct_res && !ct_spot && has_spot && cut < 5) ? 1 : 0;
+        if (ct_res) {  // getCapacityReservationType: the first offering of the first type
+          const int t0 = (int)(L.val[0] & 4095u);
+          const uint64_t om0 = om_of(t0);
+          for (int j = 0; j < a.MO; j++) {
+            const int c = a.ofs_cls[(size_t)t0 * a.MO + j];
+            if (c == 0xFF) break;
+            if ((om0 >> c) & 1) {
+              res.reservation_type = ((a.cls_rt0 >> c) & 1) ? 0 : ((a.cls_rt1 >> c) & 1) ? 1 : -1;
+              break;
+            }
           }
-        const bool ct_spot = has_spot && __ballot(spot_ok) != 0;
-        res.capacity_type = ct_spot ? 1 : 0;
-        res.od_fallback_warning = (!ct_spot && has_spot && cut < 5) ? 1 : 0;
+        }
         // ---- getOverrides (R:instance.go:392-439) with the capacity type pinned -----------------------------
-        const uint64_t cls3 = cls_noct & (ct_spot ? a.cls_spot : a.cls_od);
+        const uint64_t cls3 = cls_noct & (ct_res ? a.cls_res : ct_spot ? a.cls_spot : a.cls_od);
         uint32_t* ot = a.out_types + (size_t)q * a.max_types;
         uint32_t* oo = a.out_overrides + (size_t)q * a.ovr_stride;
         int novr = 0;
         for (int base = 0; base < cut; base += 64) {
           const int i = base + lane;
           int t = 0, cnt = 0;
+          uint64_t c3 = 0;
           if (i < cut) {
             t = (int)(L.val[i] & 4095u);
             ot[i] = (uint32_t)t;
+            c3 = cls3 & om_of(t);
             for (int j = 0; j < a.MO; j++) {
               const int c = a.ofs_cls[(size_t)t * a.MO + j];
               if (c == 0xFF) break;
-              if (((cls3 >> c) & 1) && Cg.price[(size_t)t * D.C + c] < INF && a.cls_zone[c] >= 0) cnt++;
+              if (((c3 >> c) & 1) && Cg.price[(size_t)t * D.C + c] < INF && a.cls_zone[c] >= 0) cnt++;
             }
           }
           int incl = cnt;  // inclusive wave scan
@@ -3148,7 +3343,7 @@ __global__ __launch_bounds__(LAUNCH_WAVES * 64) void launch_kernel(LaunchArgs a)
             for (int j = 0; j < a.MO; j++) {
               const int c = a.ofs_cls[(size_t)t * a.MO + j];
               if (c == 0xFF) break;
-              if (((cls3 >> c) & 1) && Cg.price[(size_t)t * D.C + c] < INF && a.cls_zone[c] >= 0)
+              if (((c3 >> c) & 1) && Cg.price[(size_t)t * D.C + c] < INF && a.cls_zone[c] >= 0 && pos < (int)a.ovr_stride)
                 oo[pos++] = ((uint32_t)t << 8) | (uint32_t)a.cls_zone[c];
             }
           novr += __shfl(incl, 63, 64);

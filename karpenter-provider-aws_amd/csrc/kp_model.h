@@ -33,10 +33,12 @@ struct KReqs {
   uint64_t vals[KP_MAX_WORDS];
 };
 
-// Offering class = one (capacity-type, zone, zone-id) signature (R:offering.go:133-143).
-struct OfferClass {
-  int32_t ct_bit, zone_bit, zid_bit;  // global value bits; zid_bit < 0: offering has no zone-id requirement
-  int32_t pad_;
+// Offering class = one (capacity-type, zone, zone-id, reservation id, reservation type) signature
+// (R:offering.go:133-143, 165-183).
+struct OfferClass {  // 16 bytes: two words per class in the LDS catalogue header
+  int16_t ct_bit, zone_bit, zid_bit;  // global value bits (< 64 * KP_MAX_WORDS); zid_bit < 0: no zone-id requirement
+  int16_t rid_bit, rt_bit;            // capacity-reservation-id / -type value bits; < 0: DoesNotExist
+  int16_t pad_[3];
 };
 
 // Everything the device needs about the dictionary + one catalogue, for one solve.

@@ -261,7 +261,7 @@ class LaunchResult(C.Structure):
     _fields_ = [("status", C.c_int32), ("capacity_type", C.c_int32), ("n_types", C.c_uint32),
                 ("n_overrides", C.c_uint32), ("failed_filter", C.c_int32), ("n_compatible", C.c_uint32),
                 ("rejected_exotic", C.c_uint32), ("rejected_spot", C.c_uint32), ("od_fallback_warning", C.c_int32),
-                ("reserved_", C.c_int32)]
+                ("reservation_type", C.c_int32), ("rejected_reservation", C.c_uint32), ("reserved_", C.c_int32)]
 
 
 def launch_requests(arena, requests):
@@ -274,12 +274,14 @@ def launch_requests(arena, requests):
 
 
 def launch_result_dict(r, types, ovr, zones):
-    return {"status": int(r.status), "capacity_type": "spot" if r.capacity_type == 1 else "on-demand",
+    return {"status": int(r.status), "capacity_type": ("on-demand", "spot", "reserved")[int(r.capacity_type)],
             "types": [int(t) for t in types[:r.n_types]] if r.status == 0 else [],
             "overrides": [(int(o) >> 8, zones[int(o) & 0xFF]) for o in ovr[:r.n_overrides]] if r.status == 0 else [],
             "failed_filter": int(r.failed_filter), "n_compatible": int(r.n_compatible),
             "rejected_exotic": int(r.rejected_exotic), "rejected_spot": int(r.rejected_spot),
-            "od_fallback_warning": bool(r.od_fallback_warning)}
+            "od_fallback_warning": bool(r.od_fallback_warning),
+            "reservation_type": {0: "default", 1: "capacity-block"}.get(int(r.reservation_type)),
+            "rejected_reservation": int(r.rejected_reservation)}
 
 
 # ------------------------------------------------------------------------------------------------

@@ -383,6 +383,7 @@ struct Offering {
   Requirements reqs;
   double price;
   bool available;
+  int32_t reservation_capacity = 0;  // Offering.ReservationCapacity (R:offering.go:178)
 };
 struct InstanceType {
   string name;
@@ -414,6 +415,7 @@ static std::shared_ptr<vector<InstanceType>> CatalogFromABI(const kp_catalog_des
       if (o.zone_id) Add(of.reqs, NewRequirement(kLabelZoneID, KP_OP_IN, {o.zone_id}, -1));
       of.price = o.price;
       of.available = o.available != 0;
+      of.reservation_capacity = o.reservation_capacity;
       it.offerings.push_back(std::move(of));
     }
     out->push_back(std::move(it));
@@ -2066,9 +2068,156 @@ static bool IsExotic(const InstanceType& it) {  // R:filter.go:295-310
   return false;
 }
 
+// A launch's working list: each instance type with its current offering list (indices into the catalogue's
+// offerings). The reservation filters replace a type's offering slice (R:filter.go:107-116, 196-200, 253-257);
+// everything after them reads the replaced slices. Where the reference returns map values (lo.Values: random
+// order) this keeps list / offering order.
+struct WorkType {
+  int t;
+  vector<int> offs;
+};
+static string OfferingResType(const Offering& o) {  // Requirements.Get(capacity-reservation-type).Any(); "" for DNE
+  auto f = o.reqs.find(kLabelResType);
+  return f == o.reqs.end() || f->second.complement || f->second.values.empty() ? string() : *f->second.values.begin();
+}
+static int ResTypeIndex(const string& rt) {  // v1.CapacityReservationType("").Values() order = priority order
+  return rt == "default" ? 0 : rt == "capacity-block" ? 1 : -1;
+}
+
+// CapacityReservationTypeFilter (R:filter.go:66-144): the partition (default / capacity-block) holding the
+// cheapest available compatible reserved offering (ties: priority default < capacity-block); its types keep only
+// their reserved offerings of that type, the rest are rejected; an empty selected partition keeps everything.
+// A reserved offering without a reservation type (the reference panics) belongs to no partition.
+static void FilterCapacityReservationType(const vector<InstanceType>& C, const Requirements& reqs, vector<WorkType>& W) {
+  if (!ReqHas(reqs, kLabelCapacityType, "reserved")) return;
+  double cheapest[2] = {std::numeric_limits<double>::max(), std::numeric_limits<double>::max()};
+  vector<char> member[2] = {vector<char>(W.size(), 0), vector<char>(W.size(), 0)};
+  for (size_t i = 0; i < W.size(); i++)
+    for (int oi : W[i].offs) {
+      const Offering& o = C[W[i].t].offerings[oi];
+      if (!o.available || !Compatible(reqs, o.reqs, true) || OfferingCapType(o) != "reserved") continue;
+      const int p = ResTypeIndex(OfferingResType(o));
+      if (p < 0) continue;
+      if (o.price < cheapest[p]) cheapest[p] = o.price;
+      member[p][i] = 1;
+    }
+  const int sel = cheapest[1] < cheapest[0] ? 1 : 0;
+  vector<WorkType> kept;
+  for (size_t i = 0; i < W.size(); i++)
+    if (member[sel][i]) {
+      WorkType w{W[i].t, {}};
+      for (int oi : W[i].offs) {
+        const Offering& o = C[W[i].t].offerings[oi];
+        if (OfferingCapType(o) == "reserved" && ResTypeIndex(OfferingResType(o)) == sel) w.offs.push_back(oi);
+      }
+      kept.push_back(std::move(w));
+    }
+  if (!kept.empty()) W = std::move(kept);
+}
+
+// CapacityBlockFilter (R:filter.go:146-225): applies when the first offering of the first type carries the
+// capacity-block reservation type (every offering carries the key: DoesNotExist on non-reserved ones,
+// R:offering.go:136-137); keeps the single type whose cheapest capacity-block offering (any availability) is the
+// cheapest, with only that offering.
+static void FilterCapacityBlock(const vector<InstanceType>& C, const Requirements& reqs, vector<WorkType>& W) {
+  if (!ReqHas(reqs, kLabelCapacityType, "reserved")) return;
+  bool should = false;
+  for (auto& w : W)
+    if (!w.offs.empty()) {
+      should = ResTypeIndex(OfferingResType(C[w.t].offerings[w.offs[0]])) == 1;
+      break;
+    }
+  if (!should) return;
+  int sel_w = -1;
+  double sel_price = 0;
+  for (size_t i = 0; i < W.size(); i++) {
+    int so = -1;
+    for (int oi : W[i].offs) {
+      const Offering& o = C[W[i].t].offerings[oi];
+      if (OfferingCapType(o) != "reserved" || ResTypeIndex(OfferingResType(o)) != 1) continue;
+      if (so < 0 || C[W[i].t].offerings[so].price > o.price) so = oi;
+    }
+    if (so >= 0 && (sel_w < 0 || sel_price > C[W[i].t].offerings[so].price)) {
+      W[i].offs = {so};
+      sel_w = (int)i;
+      sel_price = C[W[i].t].offerings[so].price;
+    }
+  }
+  W = {W[sel_w]};
+}
+
+// ReservedOfferingFilter (R:filter.go:227-274): per type, one available compatible reserved offering per zone (the
+// greatest ReservationCapacity, the first on ties); types without one are rejected unless that rejects all.
+static void FilterReservedOffering(const vector<InstanceType>& C, const Requirements& reqs, vector<WorkType>& W) {
+  if (!ReqHas(reqs, kLabelCapacityType, "reserved")) return;
+  vector<WorkType> kept;
+  for (auto& w : W) {
+    vector<std::pair<string, int>> zonal;  // zone -> offering, in first-seen order
+    for (int oi : w.offs) {
+      const Offering& o = C[w.t].offerings[oi];
+      if (!o.available || !Compatible(reqs, o.reqs, true) || OfferingCapType(o) != "reserved") continue;
+      const string z = OfferingZone(o);
+      auto f = std::find_if(zonal.begin(), zonal.end(), [&](const std::pair<string, int>& e) { return e.first == z; });
+      if (f == zonal.end()) zonal.push_back({z, oi});
+      else if (o.reservation_capacity > C[w.t].offerings[f->second].reservation_capacity) f->second = oi;
+    }
+    if (zonal.empty()) continue;
+    WorkType k{w.t, {}};
+    for (auto& e : zonal) k.offs.push_back(e.second);
+    std::sort(k.offs.begin(), k.offs.end());
+    kept.push_back(std::move(k));
+  }
+  if (!kept.empty()) W = std::move(kept);
+}
+
+static bool WorkHasCompatibleAvailable(const vector<InstanceType>& C, const WorkType& w, const Requirements& reqs,
+                                       const char* ct = nullptr) {
+  for (int oi : w.offs) {
+    const Offering& o = C[w.t].offerings[oi];
+    if (o.available && Compatible(reqs, o.reqs, true) && (!ct || OfferingCapType(o) == ct)) return true;
+  }
+  return false;
+}
+static double WorkCheapest(const vector<InstanceType>& C, const WorkType& w, const Requirements& reqs) {
+  double p = std::numeric_limits<double>::max();
+  for (int oi : w.offs) {
+    const Offering& o = C[w.t].offerings[oi];
+    if (o.available && Compatible(reqs, o.reqs, true) && o.price < p) p = o.price;
+  }
+  return p;
+}
+
+// One reservation filter over the whole catalogue (in order, every offering): which 0 CapacityReservationType,
+// 1 CapacityBlock, 2 ReservedOffering. out_kept[t]: the type is in the returned list; out_offering_kept[flat
+// offering index]: the offering is in its type's (replaced) slice. Pinned by R:filter_test.go:130-396.
+int32_t kpo_filter_reservation(const kp_catalog_desc* cat, const kp_requirements* req, int32_t which, uint8_t* out_kept,
+                               uint8_t* out_offering_kept) {
+  auto types = CatalogFromABI(*cat);
+  const vector<InstanceType>& C = *types;
+  Requirements reqs = FromABI(*req);
+  vector<WorkType> W;
+  for (size_t t = 0; t < C.size(); t++) {
+    WorkType w{(int)t, {}};
+    for (size_t j = 0; j < C[t].offerings.size(); j++) w.offs.push_back((int)j);
+    W.push_back(std::move(w));
+  }
+  if (which == 0) FilterCapacityReservationType(C, reqs, W);
+  else if (which == 1) FilterCapacityBlock(C, reqs, W);
+  else if (which == 2) FilterReservedOffering(C, reqs, W);
+  else return KP_E_INVAL;
+  vector<size_t> first(C.size() + 1, 0);
+  for (size_t t = 0; t < C.size(); t++) first[t + 1] = first[t] + C[t].offerings.size();
+  std::fill(out_kept, out_kept + C.size(), 0);
+  std::fill(out_offering_kept, out_offering_kept + first[C.size()], 0);
+  for (auto& w : W) {
+    out_kept[w.t] = 1;
+    for (int oi : w.offs) out_offering_kept[first[w.t] + oi] = 1;
+  }
+  return KP_OK;
+}
+
 // filterInstanceTypes (R:instance.go:242-270) + getCapacityType (:504-518) + checkODFallback (:336-355) +
-// getOverrides (:392-439) for one NodeClaim; reserved offerings are not representable in ABI v2, so the three
-// reservation filters (R:filter.go:66-274) are no-ops (each returns its input when no reserved offering exists).
+// getOverrides (:392-439) + getCapacityReservationType (:520-530) for one NodeClaim.
 int32_t kpo_launch_select(const kp_catalog_desc* cat, const kp_launch_request* req, const char* const* zones,
                           uint32_t n_zones, uint32_t max_types, kp_launch_result* out, uint32_t* out_types,
                           uint32_t* out_overrides) {
@@ -2078,40 +2227,52 @@ int32_t kpo_launch_select(const kp_catalog_desc* cat, const kp_launch_request* r
   ResourceList requests = FromABI(req->requests);
   *out = kp_launch_result{};
   out->failed_filter = -1;
-  vector<int> its;
+  out->reservation_type = -1;
+  vector<WorkType> W;
   for (uint32_t i = 0; i < req->n_instance_types; i++) {
     if (req->instance_types[i] >= C.size()) return KP_E_INVAL;
-    its.push_back((int)req->instance_types[i]);
+    const int t = (int)req->instance_types[i];
+    // CompatibleAvailableFilter (R:filter.go:51-63)
+    if (!(Compatible(reqs, C[t].reqs, true) && Fits(requests, C[t].allocatable) && HasCompatibleAvailable(C[t], reqs)))
+      continue;
+    WorkType w{t, {}};
+    for (size_t j = 0; j < C[t].offerings.size(); j++) w.offs.push_back((int)j);
+    W.push_back(std::move(w));
   }
-  // CompatibleAvailableFilter (R:filter.go:51-63)
-  vector<int> kept;
-  for (int t : its)
-    if (Compatible(reqs, C[t].reqs, true) && Fits(requests, C[t].allocatable) && HasCompatibleAvailable(C[t], reqs))
-      kept.push_back(t);
-  out->n_compatible = (uint32_t)kept.size();
-  if (kept.empty()) {
+  out->n_compatible = (uint32_t)W.size();
+  if (W.empty()) {
     out->status = KP_LAUNCH_INSUFFICIENT_CAPACITY;
     out->failed_filter = KP_FILTER_COMPATIBLE_AVAILABLE;
     return KP_OK;
   }
-  its = kept;
+  // the reservation filters never empty the list (each keeps its input rather than nothing)
+  size_t n0 = W.size();
+  FilterCapacityReservationType(C, reqs, W);
+  out->rejected_reservation = (uint32_t)(n0 - W.size());
+  n0 = W.size();
+  FilterCapacityBlock(C, reqs, W);
+  out->rejected_reservation += (uint32_t)(n0 - W.size());
+  n0 = W.size();
+  FilterReservedOffering(C, reqs, W);
+  out->rejected_reservation += (uint32_t)(n0 - W.size());
   const bool hasMin = HasMinValues(reqs);
   // ExoticInstanceTypeFilter (R:filter.go:289-314): keep the generic types if any
   if (!hasMin) {
-    vector<int> generic;
-    for (int t : its)
-      if (!IsExotic(C[t])) generic.push_back(t);
+    vector<WorkType> generic;
+    for (auto& w : W)
+      if (!IsExotic(C[w.t])) generic.push_back(w);
     if (!generic.empty()) {
-      out->rejected_exotic = (uint32_t)(its.size() - generic.size());
-      its = generic;
+      out->rejected_exotic = (uint32_t)(W.size() - generic.size());
+      W = std::move(generic);
     }
   }
   // SpotInstanceFilter (R:filter.go:342-382)
   if (!hasMin && ReqHas(reqs, kLabelCapacityType, "on-demand") && ReqHas(reqs, kLabelCapacityType, "spot")) {
     double cheapestOD = std::numeric_limits<double>::max();
     bool hasSpot = false, hasOD = false;
-    for (int t : its)
-      for (auto& o : C[t].offerings) {
+    for (auto& w : W)
+      for (int oi : w.offs) {
+        const Offering& o = C[w.t].offerings[oi];
         if (!Compatible(reqs, o.reqs, true) || !o.available) continue;
         const string c = OfferingCapType(o);
         if (c == "on-demand") {
@@ -2122,12 +2283,18 @@ int32_t kpo_launch_select(const kp_catalog_desc* cat, const kp_launch_request* r
         }
       }
     if (hasOD && hasSpot) {
-      vector<int> k2;
-      for (int t : its) {
+      vector<WorkType> k2;
+      for (auto& w : W) {
         bool hasSpotOffering = false, keep = false;
-        for (auto& o : C[t].offerings) {
+        for (int oi : w.offs) {
+          const Offering& o = C[w.t].offerings[oi];
           if (!Compatible(reqs, o.reqs, true) || !o.available) continue;
-          if (OfferingCapType(o) == "spot") {
+          const string c = OfferingCapType(o);
+          if (c == "reserved") {  // modelled as free: always kept (R:filter.go:368-371)
+            keep = true;
+            break;
+          }
+          if (c == "spot") {
             hasSpotOffering = true;
             if (o.price <= cheapestOD) {
               keep = true;
@@ -2135,58 +2302,73 @@ int32_t kpo_launch_select(const kp_catalog_desc* cat, const kp_launch_request* r
             }
           }
         }
-        if (keep || !hasSpotOffering) k2.push_back(t);
+        if (keep || !hasSpotOffering) k2.push_back(w);
       }
-      out->rejected_spot = (uint32_t)(its.size() - k2.size());
+      out->rejected_spot = (uint32_t)(W.size() - k2.size());
       if (k2.empty()) {
         out->status = KP_LAUNCH_INSUFFICIENT_CAPACITY;
         out->failed_filter = KP_FILTER_SPOT;
         return KP_OK;
       }
-      its = k2;
+      W = std::move(k2);
     }
   }
   // InstanceTypes.Truncate(reqs, maxInstanceTypes): OrderByPrice (cheapest available compatible, then name)
-  std::sort(its.begin(), its.end(), [&](int a, int b) {
-    const double pa = CheapestPrice(C[a], reqs), pb = CheapestPrice(C[b], reqs);
+  std::stable_sort(W.begin(), W.end(), [&](const WorkType& a, const WorkType& b) {
+    const double pa = WorkCheapest(C, a, reqs), pb = WorkCheapest(C, b, reqs);
     if (pa != pb) return pa < pb;
-    return C[a].name < C[b].name;
+    return C[a.t].name < C[b.t].name;
   });
-  if (max_types && its.size() > max_types) its.resize(max_types);
-  if (hasMin && !SatisfiesMinValues(C, its, reqs)) {
-    out->status = KP_LAUNCH_MINVALUES;
-    return KP_OK;
+  if (max_types && W.size() > max_types) W.resize(max_types);
+  if (hasMin) {
+    vector<int> its;
+    for (auto& w : W) its.push_back(w.t);
+    if (!SatisfiesMinValues(C, its, reqs)) {
+      out->status = KP_LAUNCH_MINVALUES;
+      return KP_OK;
+    }
   }
-  // getCapacityType: reserved (never: no reserved offerings), then spot
+  // getCapacityType: reserved, then spot, when the requirements allow it and a remaining type has an available
+  // offering compatible with the requirements pinned to it
   int ct = 0;
-  if (ReqHas(reqs, kLabelCapacityType, "spot")) {
+  const char* ct_names[3] = {"on-demand", "spot", "reserved"};
+  for (int cand : {2, 1}) {
+    if (!ReqHas(reqs, kLabelCapacityType, ct_names[cand])) continue;
     Requirements r2 = reqs;
-    r2[kLabelCapacityType] = NewRequirement(kLabelCapacityType, KP_OP_IN, {"spot"}, -1);
-    for (int t : its)
-      if (HasCompatibleAvailable(C[t], r2)) {
-        ct = 1;
+    r2[kLabelCapacityType] = NewRequirement(kLabelCapacityType, KP_OP_IN, {ct_names[cand]}, -1);
+    for (auto& w : W)
+      if (WorkHasCompatibleAvailable(C, w, r2)) {
+        ct = cand;
         break;
       }
+    if (ct) break;
   }
   out->capacity_type = ct;
-  out->od_fallback_warning = ct == 0 && ReqHas(reqs, kLabelCapacityType, "spot") && its.size() < 5;
+  out->od_fallback_warning = ct == 0 && ReqHas(reqs, kLabelCapacityType, "spot") && W.size() < 5;
+  if (ct == 2)  // getCapacityReservationType: the first offering (of the first type) carrying the key
+    for (auto& w : W)
+      if (!w.offs.empty()) {
+        out->reservation_type = ResTypeIndex(OfferingResType(C[w.t].offerings[w.offs[0]]));
+        break;
+      }
   // getOverrides with the capacity type pinned; zonalSubnets = subnet_zones
   Requirements r3 = reqs;
-  r3[kLabelCapacityType] = NewRequirement(kLabelCapacityType, KP_OP_IN, {ct ? "spot" : "on-demand"}, -1);
+  r3[kLabelCapacityType] = NewRequirement(kLabelCapacityType, KP_OP_IN, {ct_names[ct]}, -1);
   uint32_t no = 0;
-  for (size_t i = 0; i < its.size(); i++) {
-    out_types[i] = (uint32_t)its[i];
-    for (auto& o : C[its[i]].offerings) {
+  for (size_t i = 0; i < W.size(); i++) {
+    out_types[i] = (uint32_t)W[i].t;
+    for (int oi : W[i].offs) {
+      const Offering& o = C[W[i].t].offerings[oi];
       if (!o.available || !Compatible(r3, o.reqs, true)) continue;
       const string z = OfferingZone(o);
       for (uint32_t zi = 0; zi < n_zones; zi++)
         if (z == zones[zi]) {
-          out_overrides[no++] = ((uint32_t)its[i] << 8) | zi;
+          out_overrides[no++] = ((uint32_t)W[i].t << 8) | zi;
           break;
         }
     }
   }
-  out->n_types = (uint32_t)its.size();
+  out->n_types = (uint32_t)W.size();
   out->n_overrides = no;
   return KP_OK;
 }

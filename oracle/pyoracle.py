@@ -44,6 +44,8 @@ def load(path=LIB_PATH):
         "kpo_launch_select": (C.c_int32, [P(abi.CatalogDesc), P(abi.LaunchRequest), P(C.c_char_p), C.c_uint32,
                                           C.c_uint32, P(abi.LaunchResult), P(C.c_uint32), P(C.c_uint32)]),
         "kpo_filter_exotic": (C.c_int32, [P(abi.CatalogDesc), P(abi.Requirements), P(C.c_uint8)]),
+        "kpo_filter_reservation": (C.c_int32, [P(abi.CatalogDesc), P(abi.Requirements), C.c_int32, P(C.c_uint8),
+                                               P(C.c_uint8)]),
         "kpo_requirements_compatible": (C.c_int32, [P(abi.Requirements), P(abi.Requirements), C.c_int32]),
         "kpo_requirements_intersects": (C.c_int32, [P(abi.Requirements), P(abi.Requirements)]),
         "kpo_instance_type_resolve": (C.c_int32, [P(abi.Options), P(abi.EC2Info), P(abi.NodeClass),
@@ -108,6 +110,27 @@ def spot_filter(instance_types, requirements):
 
 def exotic_filter(instance_types, requirements):
     return _filter("kpo_filter_exotic", instance_types, requirements)
+
+
+def reservation_filter(instance_types, requirements, which):
+    """CapacityReservationType ("type") / CapacityBlock ("block") / ReservedOffering ("offering") filter:
+    (kept type flags, per type the indices of its offerings in the replaced slice)."""
+    lib = load()
+    arena = abi.Arena()
+    desc = arena.catalog_desc(instance_types)
+    reqs = arena.requirements(requirements)
+    n_off = sum(len(t.offerings) for t in instance_types)
+    kept = np.zeros(max(1, len(instance_types)), dtype=np.uint8)
+    okept = np.zeros(max(1, n_off), dtype=np.uint8)
+    rc = lib.kpo_filter_reservation(C.byref(desc), C.byref(reqs), {"type": 0, "block": 1, "offering": 2}[which],
+                                    kept.ctypes.data_as(C.POINTER(C.c_uint8)), okept.ctypes.data_as(C.POINTER(C.c_uint8)))
+    if rc != 0:
+        raise RuntimeError(f"kpo_filter_reservation = {rc}")
+    offs, i = [], 0
+    for t in instance_types:
+        offs.append([j for j in range(len(t.offerings)) if okept[i + j]])
+        i += len(t.offerings)
+    return kept[:len(instance_types)].astype(bool), offs
 
 
 def launch_select(instance_types, requests, subnet_zones, max_types=60):

@@ -23,7 +23,7 @@ def test_all_declared_symbols_exported():
 
 def test_abi_version_and_struct_sizes():
     lib = kpamd.load_lib()
-    assert lib.kp_abi_version() == 6
+    assert lib.kp_abi_version() == 7
     from kpamd import abi
     assert C.sizeof(abi.ResourceList) == 12 * 8 + 8
     assert C.sizeof(abi.Offering) == 5 * 8 + 8 + 8
@@ -44,7 +44,7 @@ def test_no_device_is_an_error_not_a_fallback():
 
 def test_launch_struct_layouts():
     from kpamd import abi
-    assert C.sizeof(abi.LaunchResult) == 10 * 4
+    assert C.sizeof(abi.LaunchResult) == 12 * 4
     assert C.sizeof(abi.LaunchRequest) == C.sizeof(abi.Requirements) + C.sizeof(abi.ResourceList) + 8 + 8
 
 

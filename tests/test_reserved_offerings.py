@@ -1,0 +1,264 @@
+"""Reserved (capacity-reservation) offerings on the launch path.
+
+Oracle pins: the CapacityReservationType / CapacityBlock / ReservedOffering filter cases of
+R:pkg/providers/instance/filter/filter_test.go:130-396, transcribed as data below (kept / rejected names and the
+offerings a kept type retains). Device: kp_launch_select (launch_kernel) against the oracle's launch selection,
+bit-exact, on catalogues carrying reservations (R:pkg/providers/instancetype/offering/offering.go:151-186 builds
+them: capacity type reserved, the reservation id and type labels, ReservationCapacity), gpu-marked.
+"""
+import dataclasses
+
+import numpy as np
+import pytest
+
+from kpamd.model import InstanceType, Offering
+
+CT = "karpenter.sh/capacity-type"
+Z = "topology.kubernetes.io/zone"
+K = "karpenter.k8s.aws/"
+RTYPES = ["default", "capacity-block"]  # v1.CapacityReservationType("").Values(), priority order
+
+
+def off(ct, avail, price=0.0, zone=None, rt=None, rid=None, cap=0):
+    return Offering(ct, zone, None, float(price), bool(avail), rid, rt, int(cap))
+
+
+def it(name, *offs):
+    return InstanceType(name, [], {}, {}, list(offs))
+
+
+def run(which, types, reqs):
+    from oracle import pyoracle
+    kept, offs = pyoracle.reservation_filter(types, reqs, which)
+    return ({t.name for t, k in zip(types, kept) if k}, {t.name for t, k in zip(types, kept) if not k},
+            {t.name: [t.offerings[j] for j in o] for t, k, o in zip(types, kept, offs) if k})
+
+
+# ---- CapacityReservationTypeFilter (R:filter_test.go:130-255) ----------------------------------------------
+@pytest.mark.parametrize("sel", RTYPES)
+def test_crt_prioritizes_cheapest_type(sel):
+    kept_types = [it(f"cheap-instance-{sel}", off("reserved", True, 5.0, "zone-1a", rt=sel)),
+                  it(f"expensive-instance-{sel}", off("reserved", True, 10.0, "zone-1a", rt=sel))]
+    rejected = [it(f"expensive-instance-{t}", off("reserved", True, 10.0, "zone-1a", rt=t),
+                   off("reserved", False, 1.0, "zone-1a", rt=t), off("reserved", True, 1.0, "zone-1b", rt=t))
+                for t in RTYPES if t != sel]
+    kept, rej, _ = run("type", kept_types + rejected, [(CT, "In", ["reserved"]), (Z, "In", ["zone-1a"])])
+    assert kept == {t.name for t in kept_types} and rej == {t.name for t in rejected}
+
+
+def test_crt_breaks_ties_by_priority():
+    kept, rej, _ = run("type", [it("default", off("reserved", True, 5.0, rt="default")),
+                                it("capacity-block", off("reserved", True, 5.0, rt="capacity-block"))],
+                       [(CT, "In", ["reserved"])])
+    assert kept == {"default"} and rej == {"capacity-block"}
+
+
+@pytest.mark.parametrize("sel", RTYPES)
+def test_crt_removes_other_type_offerings(sel):
+    types = [it("pin-instance", off("reserved", True, 1.0, rt=sel)),
+             it("filter-instance", *[off("reserved", True, 5.0, rt=t) for t in RTYPES])]
+    kept, rej, offs = run("type", types, [(CT, "In", ["reserved"])])
+    assert kept == {"pin-instance", "filter-instance"} and not rej
+    for name in kept:
+        assert len(offs[name]) == 1
+        assert offs[name][0].capacity_type == "reserved" and offs[name][0].reservation_type == sel
+
+
+def test_crt_not_compatible_with_reserved():
+    types = [it(f"{t}-instance", off("on-demand", True), off("reserved", True, 1.0, rt=t)) for t in RTYPES]
+    kept, rej, offs = run("type", types, [(CT, "NotIn", ["reserved"])])
+    assert kept == {t.name for t in types} and not rej
+    assert all(len(o) == 2 for o in offs.values())
+
+
+# ---- CapacityBlockFilter (R:filter_test.go:257-320) ----------------------------------------------------------
+def test_cb_selects_cheapest_capacity_block():
+    types = [it("cheap-instance", off("reserved", True, 1.0, rt="capacity-block"), off("reserved", True, 10.0, rt="capacity-block")),
+             it("expensive-instance", off("reserved", True, 2.0, rt="capacity-block"),
+                off("reserved", True, 10.0, rt="capacity-block"))]
+    kept, rej, offs = run("block", types, [(CT, "Exists", [])])
+    assert kept == {"cheap-instance"} and rej == {"expensive-instance"}
+    assert [o.price for o in offs["cheap-instance"]] == [1.0]
+
+
+def test_cb_ignores_other_reservation_types():
+    types = [it("cheap-instance", off("reserved", True, 1.0, rt="default"), off("reserved", True, 10.0, rt="default")),
+             it("expensive-instance", off("reserved", True, 2.0, rt="default"), off("reserved", True, 10.0, rt="default"))]
+    kept, rej, _ = run("block", types, [(CT, "Exists", [])])
+    assert kept == {"cheap-instance", "expensive-instance"} and not rej
+
+
+def test_cb_not_compatible_with_reserved():
+    types = [it("cheap-instance", off("reserved", True, 1.0, rt="capacity-block"), off("on-demand", True, 1.0, rt="capacity-block")),
+             it("expensive-instance", off("reserved", True, 2.0, rt="capacity-block"),
+                off("on-demand", True, 2.0, rt="capacity-block"))]
+    kept, rej, _ = run("block", types, [(CT, "NotIn", ["reserved"])])
+    assert kept == {"cheap-instance", "expensive-instance"} and not rej
+
+
+# ---- ReservedOfferingFilter (R:filter_test.go:322-396) -------------------------------------------------------
+def test_rof_no_available_reserved_offerings():
+    types = [it("non-reserved-instance", off("on-demand", True), off("spot", True)),
+             it("reserved-instance", off("on-demand", True), off("spot", True), off("reserved", False))]
+    kept, rej, _ = run("offering", types, [(CT, "Exists", [])])
+    assert kept == {"non-reserved-instance", "reserved-instance"} and not rej
+
+
+def test_rof_one_offering_per_zone():
+    types = [it("non-reserved-instance", off("on-demand", True), off("spot", True)),
+             it("reserved-instance-a", off("on-demand", True), off("spot", True),
+                off("reserved", True, zone="1", rid="kept", cap=5), off("reserved", True, zone="2", rid="kept", cap=6),
+                off("reserved", True, zone="2", rid="rejected", cap=5)),
+             it("reserved-instance-b", off("on-demand", True), off("spot", True),
+                off("reserved", True, zone="1", rid="kept", cap=1), off("reserved", False, zone="1", rid="rejected", cap=2))]
+    kept, rej, offs = run("offering", types, [(CT, "Exists", [])])
+    assert kept == {"reserved-instance-a", "reserved-instance-b"} and rej == {"non-reserved-instance"}
+    assert len(offs["reserved-instance-a"]) == 2
+    assert all(o.reservation_id == "kept" for v in offs.values() for o in v)
+
+
+def test_rof_not_compatible_with_reserved():
+    types = [it("non-reserved-instance", off("on-demand", True), off("spot", True)),
+             it("reserved-instance", off("on-demand", True), off("spot", True), off("reserved", True, zone="1"))]
+    kept, rej, offs = run("offering", types, [(CT, "NotIn", ["reserved"])])
+    assert kept == {"non-reserved-instance", "reserved-instance"} and not rej
+    assert sorted(len(o) for o in offs.values()) == [2, 3]
+
+
+# ---- launch-level behaviour (oracle) ---------------------------------------------------------------------------
+def test_launch_prefers_reserved_then_reports_type():
+    """getCapacityType: reserved first (R:instance.go:504-518); getCapacityReservationType on the kept slices;
+    overrides only from the reserved offering ReservedOfferingFilter kept per zone."""
+    from oracle import pyoracle
+    types = [InstanceType("m5.large", [(CT, "In", ["on-demand", "spot", "reserved"])], {"cpu": 2000}, {},
+                          [off("on-demand", True, 0.1, "zone-1a"), off("spot", True, 0.03, "zone-1a"),
+                           off("reserved", True, 1e-8, "zone-1a", rt="default", rid="cr-a", cap=2),
+                           off("reserved", True, 1e-8, "zone-1a", rt="default", rid="cr-b", cap=3)]),
+             InstanceType("m5.xlarge", [(CT, "In", ["on-demand", "spot"])], {"cpu": 4000}, {},
+                          [off("on-demand", True, 0.2, "zone-1a"), off("spot", True, 0.05, "zone-1a")])]
+    reqs = [([(CT, "In", ["on-demand", "spot", "reserved"])], {"cpu": 1000}, [0, 1]),
+            ([(CT, "In", ["on-demand", "spot"])], {"cpu": 1000}, [0, 1])]
+    r = pyoracle.launch_select(types, reqs, ["zone-1a"])
+    assert r[0]["capacity_type"] == "reserved" and r[0]["reservation_type"] == "default"
+    assert r[0]["types"] == [0] and r[0]["rejected_reservation"] == 1
+    assert r[0]["overrides"] == [(0, "zone-1a")]  # cr-b (capacity 3) only
+    assert r[1]["capacity_type"] == "spot" and r[1]["reservation_type"] is None
+
+
+# ---- device vs oracle ------------------------------------------------------------------------------------------
+def reserved_catalogue(catalog, n_types, seed):
+    """The first n_types docs types; 18 random ones get 1-3 capacity reservations each (offering.go:151-186: price =
+    OD / 1e7, Available = capacity != 0, the type's requirements gain reserved / the ids / the types,
+    types.go:172,223-229). Every reservation is an offering class of its own: <= 54 of the device's 64 classes."""
+    from kpamd import catalog as cmod
+    rng = np.random.default_rng(seed)
+    out, nres = [], 0
+    with_res = set(rng.choice(n_types, size=18, replace=False).tolist())
+    for i, t in enumerate(catalog[:n_types]):
+        offs = list(t.offerings)
+        reqs = list(t.requirements)
+        if i in with_res:
+            od = min([o.price for o in offs if o.capacity_type == "on-demand"] or [1.0])
+            ids, rts = [], []
+            for _ in range(int(rng.integers(1, 4))):
+                nres += 1
+                cap = int(rng.choice([0, 1, 2, 5, 9]))
+                rt = RTYPES[int(rng.random() < 0.3)]
+                rid = f"cr-{nres:05d}"
+                price = od / 1e7 * (1 + int(rng.integers(0, 3)))  # ties and orderings between partitions
+                offs.append(Offering("reserved", str(rng.choice(cmod.ZONES)), None, price, cap != 0, rid, rt, cap))
+                ids.append(rid)
+                rts.append(rt)
+            reqs = [r for r in reqs if r[0] not in (CT, K + "capacity-reservation-id", K + "capacity-reservation-type")]
+            reqs += [(CT, "In", ["on-demand", "spot", "reserved"]), (K + "capacity-reservation-id", "In", ids),
+                     (K + "capacity-reservation-type", "In", sorted(set(rts)))]
+        out.append(dataclasses.replace(t, requirements=reqs, offerings=offs))
+    return out
+
+
+def reserved_requests(cat, n, seed):
+    from kpamd import synth
+    rng = np.random.default_rng(seed + 1)
+    out = []
+    for reqs, res, types in synth.random_launch_requests(cat, n, seed=seed):
+        reqs = [r for r in reqs if r[0] != CT]
+        k = rng.random()
+        if k < 0.3:
+            reqs.append((CT, "In", ["reserved"]))
+        elif k < 0.55:
+            reqs.append((CT, "In", ["reserved", "on-demand", "spot"]))
+        elif k < 0.65:
+            reqs.append((CT, "In", ["reserved", "spot"]))
+        elif k < 0.75:
+            reqs.append((CT, "NotIn", ["reserved"]))
+        if rng.random() < 0.15:
+            reqs.append((K + "capacity-reservation-type", "In", [str(rng.choice(RTYPES))]))
+        if rng.random() < 0.05:
+            reqs.append((K + "capacity-reservation-type", "DoesNotExist", []))
+        out.append((reqs, res, types))
+    return out
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_oracle_launch_random_reserved_smoke(catalog, seed):
+    """CPU: the oracle runs the whole chain on reserved catalogues and picks reserved capacity somewhere."""
+    from oracle import pyoracle
+    from kpamd import catalog as cmod
+    cat = reserved_catalogue(catalog, 300, seed)
+    r = pyoracle.launch_select(cat, reserved_requests(cat, 80, 40 + seed), cmod.ZONES)
+    cts = {x["capacity_type"] for x in r if x["status"] == 0}
+    assert "reserved" in cts and ("on-demand" in cts or "spot" in cts)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(4))
+def test_device_launch_reserved_matches_oracle(ctx, catalog, seed):
+    import kpamd
+    from kpamd import catalog as cmod
+    from oracle import pyoracle
+    cat = reserved_catalogue(catalog, 400 if seed < 2 else len(catalog), seed)
+    reqs = reserved_requests(cat, 250, 40 + seed)
+    zones = [cmod.ZONES, cmod.ZONES[:2], cmod.ZONES, cmod.ZONES[1:]][seed]
+    ch = kpamd.Catalog(ctx, cat)
+    plan = kpamd.LaunchPlan(ctx, ch, reqs, zones)
+    got, _ = plan.run(read=True)
+    plan.close()
+    ch.close()
+    want = pyoracle.launch_select(cat, reqs, zones)
+    for i, (g, w) in enumerate(zip(got, want)):
+        assert g == w, f"request {i}: device {g} vs oracle {w}"
+    assert sum(g["capacity_type"] == "reserved" for g in got) > 0
+    assert sum(g["rejected_reservation"] > 0 for g in got) > 0
+
+
+@pytest.mark.gpu
+def test_device_launch_reserved_kat(ctx):
+    import kpamd
+    types = [InstanceType("m5.large", [(CT, "In", ["on-demand", "spot", "reserved"])], {"cpu": 2000}, {},
+                          [off("on-demand", True, 0.1, "zone-1a"), off("spot", True, 0.03, "zone-1a"),
+                           off("reserved", True, 1e-8, "zone-1a", rt="default", rid="cr-a", cap=2),
+                           off("reserved", True, 1e-8, "zone-1a", rt="default", rid="cr-b", cap=3)]),
+             InstanceType("m5.xlarge", [(CT, "In", ["on-demand", "spot"])], {"cpu": 4000}, {},
+                          [off("on-demand", True, 0.2, "zone-1a"), off("spot", True, 0.05, "zone-1a")])]
+    reqs = [([(CT, "In", ["on-demand", "spot", "reserved"])], {"cpu": 1000}, [0, 1]),
+            ([(CT, "In", ["on-demand", "spot"])], {"cpu": 1000}, [0, 1])]
+    ch = kpamd.Catalog(ctx, types)
+    plan = kpamd.LaunchPlan(ctx, ch, reqs, ["zone-1a"])
+    got, _ = plan.run(read=True)
+    plan.close()
+    ch.close()
+    assert got[0]["capacity_type"] == "reserved" and got[0]["reservation_type"] == "default"
+    assert got[0]["overrides"] == [(0, "zone-1a")] and got[0]["rejected_reservation"] == 1
+    assert got[1]["capacity_type"] == "spot"
+
+
+@pytest.mark.gpu
+def test_solve_refuses_reservations(ctx, catalog):
+    """NodeClaim.Add's reservation accounting (upstream ReservationManager) is not modelled: a Solve over a
+    catalogue with reservation offerings is KP_E_UNSUPPORTED (the shim keeps the Go path for it)."""
+    import kpamd
+    from kpamd import synth
+    cat = reserved_catalogue(catalog, 200, 0)
+    prob = synth.config2(cat, n_pods=50, seed=2)
+    with pytest.raises(kpamd.KPError, match="reservation"):
+        kpamd.Scheduler(ctx, prob).solve()
