@@ -262,3 +262,24 @@ def test_solve_refuses_reservations(ctx, catalog):
     prob = synth.config2(cat, n_pods=50, seed=2)
     with pytest.raises(kpamd.KPError, match="reservation"):
         kpamd.Scheduler(ctx, prob).solve()
+
+
+@pytest.mark.gpu
+def test_device_compatible_available_with_reservations(ctx, catalog):
+    """CompatibleAvailableFilter rows over reservation classes (feasibility_kernel): kept masks and the cheapest
+    compatible available price equal the oracle's, including queries pinning a reservation type or DoesNotExist."""
+    import kpamd
+    from oracle import pyoracle
+    cat = reserved_catalogue(catalog, 300, 7)
+    queries = [(r, q) for r, q, _ in reserved_requests(cat, 40, 77)]
+    ch = kpamd.Catalog(ctx, cat)
+    kept, cheapest, _ = kpamd.compatible_available_filter(ctx, ch, queries)
+    ch.close()
+    n_res_kept = 0
+    for i, (r, q) in enumerate(queries):
+        wk, wc = pyoracle.compatible_available_filter(cat, r, q)
+        assert (kept[i] == wk).all(), f"query {i}"
+        assert np.array_equal(np.where(wk, cheapest[i], 0), np.where(wk, wc, 0)), f"query {i}"
+        if any(x == (CT, "In", ["reserved"]) for x in r):
+            n_res_kept += int(wk.sum())
+    assert n_res_kept > 0
