@@ -406,6 +406,12 @@ typedef struct kp_offering_update {
   const char* capacity_type;
   const char* zone;
   double price;               /* NaN: keep */
+  /* ABI v7: capacity reservations (capacityreservation.Provider.MarkUnavailable / GetAvailableInstanceCount,
+   * R:pkg/providers/instance/instance.go:470-484): a non-NULL reservation_id narrows the match to that
+   * reservation's offerings; reservation_capacity >= 0 sets ReservationCapacity (-1: keep). */
+  const char* reservation_id;
+  int32_t reservation_capacity;
+  int32_t reserved_;
 } kp_offering_update;
 int32_t kp_catalog_update_offerings(kp_catalog* cat, const kp_offering_update* updates, uint32_t n, uint64_t seqnum);
 

@@ -960,6 +960,7 @@ int32_t kp_catalog_update_offerings(kp_catalog* c, const kp_offering_update* ups
   if (c->ctx) lock = std::unique_lock<std::recursive_mutex>(c->ctx->mu);
   auto match = [](const HostOffering& o, const kp_offering_update& u) {
     if (o.ct != (u.capacity_type ? u.capacity_type : "")) return false;
+    if (u.reservation_id && !(o.has_rid && o.rid == u.reservation_id)) return false;
     return u.zone ? (o.has_zone && o.zone == u.zone) : !o.has_zone;
   };
   for (uint32_t i = 0; i < n; i++) {
@@ -974,6 +975,7 @@ int32_t kp_catalog_update_offerings(kp_catalog* c, const kp_offering_update* ups
       if (match(o, ups[i])) {
         o.available = ups[i].available != 0;
         if (!std::isnan(ups[i].price)) o.price = ups[i].price;
+        if (ups[i].reservation_capacity >= 0) o.rcap = ups[i].reservation_capacity;
       }
   c->seqnum = seqnum;
   return KP_OK;

@@ -139,19 +139,26 @@ class Catalog:
 
     def update_offerings(self, updates, seqnum):
         """kp_catalog_update_offerings: UnavailableOfferings.MarkUnavailable + SeqNum bump
-        (R:pkg/cache/unavailableofferings.go:66-92). updates: (type index, capacity type, zone, available[, price]);
-        the matching offerings of self.instance_types change with the device-side catalogue (all or nothing)."""
+        (R:pkg/cache/unavailableofferings.go:66-92). updates: (type index, capacity type, zone, available[, price
+        [, reservation id[, reservation capacity]]]); the matching offerings of self.instance_types change with the
+        device-side catalogue (all or nothing)."""
+        def opt(u, i):
+            return u[i] if len(u) > i else None
         ups = [abi.OfferingUpdate(int(u[0]), 1 if u[3] else 0, u[1].encode() if u[1] is not None else None,
                                   u[2].encode() if u[2] is not None else None,
-                                  float(u[4]) if len(u) > 4 and u[4] is not None else float("nan")) for u in updates]
+                                  float(u[4]) if opt(u, 4) is not None else float("nan"),
+                                  opt(u, 5).encode() if opt(u, 5) is not None else None,
+                                  int(opt(u, 6)) if opt(u, 6) is not None else -1, 0) for u in updates]
         arr = (abi.OfferingUpdate * max(1, len(ups)))(*ups)
         _check(self.ctx.lib, self.ctx.lib.kp_catalog_update_offerings(self.h, arr, len(ups), seqnum))
         for u in updates:
             for o in self.instance_types[u[0]].offerings:
-                if o.capacity_type == u[1] and o.zone == u[2]:
+                if o.capacity_type == u[1] and o.zone == u[2] and (opt(u, 5) is None or o.reservation_id == opt(u, 5)):
                     o.available = bool(u[3])
-                    if len(u) > 4 and u[4] is not None:
+                    if opt(u, 4) is not None:
                         o.price = float(u[4])
+                    if opt(u, 6) is not None and int(opt(u, 6)) >= 0:
+                        o.reservation_capacity = int(opt(u, 6))
 
     def seqnum(self):
         return self.ctx.lib.kp_catalog_seqnum(self.h)

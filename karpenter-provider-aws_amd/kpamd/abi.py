@@ -71,7 +71,8 @@ class Offering(C.Structure):
 
 class OfferingUpdate(C.Structure):
     _fields_ = [("type", C.c_uint32), ("available", C.c_int32), ("capacity_type", C.c_char_p), ("zone", C.c_char_p),
-                ("price", C.c_double)]
+                ("price", C.c_double), ("reservation_id", C.c_char_p), ("reservation_capacity", C.c_int32),
+                ("reserved_", C.c_int32)]
 
 
 class InstanceType(C.Structure):

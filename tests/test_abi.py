@@ -58,7 +58,8 @@ def test_struct_sizes_match_the_c_header(tmp_path):
     pairs = {"kp_pod_shape": abi.PodShape, "kp_existing_node": abi.ExistingNode, "kp_host_port": abi.HostPort,
              "kp_cluster_node": abi.ClusterNode, "kp_solve_in": abi.SolveIn, "kp_topology_spread": abi.TopologySpread,
              "kp_nodepool": abi.NodePool, "kp_cluster": abi.Cluster,
-             "kp_pod_affinity_term": abi.PodAffinityTerm, "kp_bound_pod": abi.BoundPod}
+             "kp_pod_affinity_term": abi.PodAffinityTerm, "kp_bound_pod": abi.BoundPod,
+             "kp_offering": abi.Offering, "kp_offering_update": abi.OfferingUpdate, "kp_launch_result": abi.LaunchResult}
     src = tmp_path / "sz.c"
     src.write_text('#include <stdio.h>\n#include "kp/kp_abi.h"\nint main(void){\n' +
                    "".join(f'printf("%zu\\n", sizeof({k}));\n' for k in pairs) + "return 0;}\n")

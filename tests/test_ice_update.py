@@ -37,7 +37,7 @@ def _updates(marks, avail=False, price=None):
 
 def test_update_struct_layout():
     from kpamd import abi
-    assert C.sizeof(abi.OfferingUpdate) == 4 + 4 + 8 + 8 + 8
+    assert C.sizeof(abi.OfferingUpdate) == 4 + 4 + 8 + 8 + 8 + 8 + 4 + 4
 
 
 def test_update_host_catalogue_and_seqnum(lib, catalog):

@@ -283,3 +283,33 @@ def test_device_compatible_available_with_reservations(ctx, catalog):
         if any(x == (CT, "In", ["reserved"]) for x in r):
             n_res_kept += int(wk.sum())
     assert n_res_kept > 0
+
+
+@pytest.mark.gpu
+def test_device_launch_reservation_updates_refresh(ctx, catalog):
+    """Reservation ICE / capacity updates by id (kp_offering_update.reservation_id / reservation_capacity) on a
+    prepared launch plan: kp_launch_refresh re-applies availability, prices and the capacity table; the result equals
+    the oracle on the updated catalogue."""
+    import kpamd
+    from kpamd import catalog as cmod
+    from oracle import pyoracle
+    cat = reserved_catalogue(catalog, 400, 3)
+    reqs = reserved_requests(cat, 150, 53)
+    ch = kpamd.Catalog(ctx, cat)
+    plan = kpamd.LaunchPlan(ctx, ch, reqs, cmod.ZONES)
+    ups, k = [], 0
+    for ti, t in enumerate(ch.instance_types):
+        for o in t.offerings:
+            if o.reservation_id:
+                cap = [0, 7, 1][k % 3]
+                k += 1
+                ups.append((ti, "reserved", o.zone, cap != 0, None, o.reservation_id, cap))
+    ch.update_offerings(ups, ch.seqnum() + 1)
+    plan.refresh(ch)
+    got, _ = plan.run(read=True)
+    plan.close()
+    want = pyoracle.launch_select(ch.instance_types, reqs, cmod.ZONES)
+    ch.close()
+    for i, (g, w) in enumerate(zip(got, want)):
+        assert g == w, f"request {i}: device {g} vs oracle {w}"
+    assert sum(g["capacity_type"] == "reserved" for g in got) > 0
