@@ -10,6 +10,7 @@
 Synthetic pricing: on-demand from the static us-east-1 table; spot = OD × U(0.3, 0.7)
 per (type, zone) from splitmix64(seed=20250704), in table order then zone order.
 """
+from dataclasses import dataclass
 import ctypes as C
 import os
 import re
@@ -64,8 +65,20 @@ class SplitMix64:
         return (self.next() >> 11) * (1.0 / (1 << 53))
 
 
-def compute_requirements(row, region=REGION, zones=ZONES, zone_ids=ZONE_IDS, offering_zones=None):
-    """computeRequirements (R:types.go:158-292) for the AL2023 family, no capacity reservations."""
+@dataclass
+class CapacityReservation:
+    """EC2NodeClass.status.capacityReservations entry (the fields createOfferings / computeRequirements read) plus the
+    capacity reservation provider's available instance count (R:offering.go:165-170)."""
+    id: str
+    instance_type: str
+    availability_zone: str
+    reservation_type: str = "default"  # default | capacity-block
+    available_count: int = 1
+
+
+def compute_requirements(row, region=REGION, zones=ZONES, zone_ids=ZONE_IDS, offering_zones=None, reservations=()):
+    """computeRequirements (R:types.go:158-292) for the AL2023 family; reservations = the type's capacity
+    reservations (reserved capacity type, reservation id / type In, R:types.go:172-174,223-232)."""
     name = row["name"]
     offering_zones = zones if offering_zones is None else offering_zones
     available = [z for z in zones if z in set(offering_zones)]
@@ -77,7 +90,8 @@ def compute_requirements(row, region=REGION, zones=ZONES, zone_ids=ZONE_IDS, off
         "topology.kubernetes.io/zone": ("topology.kubernetes.io/zone", "In", available),
         "topology.kubernetes.io/region": ("topology.kubernetes.io/region", "In", [region]),
         "node.kubernetes.io/windows-build": DNE("node.kubernetes.io/windows-build"),
-        "karpenter.sh/capacity-type": ("karpenter.sh/capacity-type", "In", ["on-demand", "spot"]),
+        "karpenter.sh/capacity-type": ("karpenter.sh/capacity-type", "In",
+                                       ["on-demand", "spot"] + (["reserved"] if reservations else [])),
         K + "instance-cpu": (K + "instance-cpu", "In", [str(row["vcpu"])]),
         K + "instance-memory": (K + "instance-memory", "In", [str(row["memory_mib"])]),
         K + "instance-hypervisor": (K + "instance-hypervisor", "In", [row["hypervisor"]]),
@@ -93,8 +107,13 @@ def compute_requirements(row, region=REGION, zones=ZONES, zone_ids=ZONE_IDS, off
     ids = [zid for z, zid in zip(zones, zone_ids) if z in set(available) and zid]
     if ids:
         reqs["topology.k8s.aws/zone-id"] = ("topology.k8s.aws/zone-id", "In", ids)
-    reqs[K + "capacity-reservation-id"] = DNE(K + "capacity-reservation-id")
-    reqs[K + "capacity-reservation-type"] = DNE(K + "capacity-reservation-type")
+    if reservations:
+        reqs[K + "capacity-reservation-id"] = (K + "capacity-reservation-id", "In", [cr.id for cr in reservations])
+        reqs[K + "capacity-reservation-type"] = (K + "capacity-reservation-type", "In",
+                                                 sorted({cr.reservation_type for cr in reservations}))
+    else:
+        reqs[K + "capacity-reservation-id"] = DNE(K + "capacity-reservation-id")
+        reqs[K + "capacity-reservation-type"] = DNE(K + "capacity-reservation-type")
 
     def ins(k, v):
         reqs[K + k] = (K + k, "In", [v])
@@ -224,8 +243,10 @@ def resource_dict(rl):
     return {abi.RES_NAMES[i]: int(rl.milli[i]) for i in range(abi.NUM_RES) if rl.present & (1 << i)}
 
 
-def create_offerings(row, reqs, spot_prices, zones=ZONES, zone_ids=ZONE_IDS, unavailable=frozenset()):
-    """createOfferings (R:offering.go:101-150): zones × {on-demand, spot}; Available = !ICE ∧ hasPrice ∧ zone∈itZones."""
+def create_offerings(row, reqs, spot_prices, zones=ZONES, zone_ids=ZONE_IDS, unavailable=frozenset(), reservations=()):
+    """createOfferings (R:offering.go:101-186): zones × {on-demand, spot}, Available = !ICE ∧ hasPrice ∧
+    zone∈itZones; then one reserved offering per capacity reservation of the type (price = OD / 1e7, 0 without an OD
+    price; Available = available count != 0 ∧ zone∈itZones; ReservationCapacity = the count)."""
     it_zones = set(next(r for r in reqs if r[0] == "topology.kubernetes.io/zone")[2])
     zid = dict(zip(zones, zone_ids))
     out = []
@@ -238,6 +259,11 @@ def create_offerings(row, reqs, spot_prices, zones=ZONES, zone_ids=ZONE_IDS, una
                 price, has = (spot_prices[(row["name"], z)], True) if od >= 0 else (0.0, False)
             ice = (ct, row["name"], z) in unavailable or ct in unavailable or z in unavailable
             out.append(Offering(ct, z, zid.get(z), price, (not ice) and has and z in it_zones))
+    for cr in reservations:
+        out.append(Offering("reserved", cr.availability_zone, zid.get(cr.availability_zone),
+                            od / 10_000_000.0 if od >= 0 else 0.0,
+                            cr.available_count != 0 and cr.availability_zone in it_zones,
+                            cr.id, cr.reservation_type, int(cr.available_count)))
     return out
 
 
@@ -252,8 +278,9 @@ def spot_price_table(rows, zones=ZONES, seed=SPOT_SEED):
 
 
 def build_catalog(lib, rows=None, opts=None, max_pods=None, pods_per_core=None, zones=ZONES, zone_ids=ZONE_IDS,
-                  unavailable=frozenset(), kubelet_cfg=None):
-    """GetInstanceTypes for one EC2NodeClass: NewInstanceType for every row, then InjectOfferings."""
+                  unavailable=frozenset(), kubelet_cfg=None, capacity_reservations=()):
+    """GetInstanceTypes for one EC2NodeClass: NewInstanceType for every row, then InjectOfferings
+    (capacity_reservations: the NodeClass's reservations, ReservedCapacity feature gate on)."""
     rows = load_ec2_table() if rows is None else rows
     arena = abi.Arena()
     opts = opts or default_options()
@@ -266,9 +293,10 @@ def build_catalog(lib, rows=None, opts=None, max_pods=None, pods_per_core=None, 
         rc = lib.kp_instance_type_resolve(C.byref(opts), C.byref(info), C.byref(nc), C.byref(cap), C.byref(ovh))
         if rc != 0:
             raise RuntimeError(f"kp_instance_type_resolve({r['name']}) = {rc}")
-        reqs = compute_requirements(r, zones=zones, zone_ids=zone_ids)
+        crs = [cr for cr in capacity_reservations if cr.instance_type == r["name"]]  # R:types.go:117-119
+        reqs = compute_requirements(r, zones=zones, zone_ids=zone_ids, reservations=crs)
         out.append(InstanceType(r["name"], reqs, resource_dict(cap), resource_dict(ovh),
-                                create_offerings(r, reqs, spot, zones, zone_ids, unavailable)))
+                                create_offerings(r, reqs, spot, zones, zone_ids, unavailable, crs)))
     return out
 
 

@@ -147,33 +147,43 @@ def test_launch_prefers_reserved_then_reports_type():
 
 # ---- device vs oracle ------------------------------------------------------------------------------------------
 def reserved_catalogue(catalog, n_types, seed):
-    """The first n_types docs types; 18 random ones get 1-3 capacity reservations each (offering.go:151-186: price =
-    OD / 1e7, Available = capacity != 0, the type's requirements gain reserved / the ids / the types,
-    types.go:172,223-229). Every reservation is an offering class of its own: <= 54 of the device's 64 classes."""
+    """The first n_types docs types through kpamd.catalog.build_catalog with 18 random types holding 1-3 capacity
+    reservations each (offering.go:151-186: price OD / 1e7, Available = count != 0, ReservationCapacity = count;
+    types.go:172,223-232: the type's requirements gain reserved / the ids / the types). Every reservation is an
+    offering class of its own: <= 54 of the device's 64 classes. `catalog` only fixes the library (lib)."""
     from kpamd import catalog as cmod
+    import kpamd
     rng = np.random.default_rng(seed)
-    out, nres = [], 0
-    with_res = set(rng.choice(n_types, size=18, replace=False).tolist())
-    for i, t in enumerate(catalog[:n_types]):
-        offs = list(t.offerings)
-        reqs = list(t.requirements)
-        if i in with_res:
-            od = min([o.price for o in offs if o.capacity_type == "on-demand"] or [1.0])
-            ids, rts = [], []
-            for _ in range(int(rng.integers(1, 4))):
-                nres += 1
-                cap = int(rng.choice([0, 1, 2, 5, 9]))
-                rt = RTYPES[int(rng.random() < 0.3)]
-                rid = f"cr-{nres:05d}"
-                price = od / 1e7 * (1 + int(rng.integers(0, 3)))  # ties and orderings between partitions
-                offs.append(Offering("reserved", str(rng.choice(cmod.ZONES)), None, price, cap != 0, rid, rt, cap))
-                ids.append(rid)
-                rts.append(rt)
-            reqs = [r for r in reqs if r[0] not in (CT, K + "capacity-reservation-id", K + "capacity-reservation-type")]
-            reqs += [(CT, "In", ["on-demand", "spot", "reserved"]), (K + "capacity-reservation-id", "In", ids),
-                     (K + "capacity-reservation-type", "In", sorted(set(rts)))]
-        out.append(dataclasses.replace(t, requirements=reqs, offerings=offs))
-    return out
+    rows = cmod.load_ec2_table()[:n_types]
+    crs = []
+    for i in sorted(rng.choice(n_types, size=18, replace=False).tolist()):
+        for _ in range(int(rng.integers(1, 4))):
+            crs.append(cmod.CapacityReservation(f"cr-{len(crs) + 1:05d}", rows[i]["name"], str(rng.choice(cmod.ZONES)),
+                                                RTYPES[int(rng.random() < 0.3)], int(rng.choice([0, 1, 2, 5, 9]))))
+    return cmod.build_catalog(kpamd.load_lib(), rows=rows, capacity_reservations=crs)
+
+
+def test_catalogue_reservations_kat(catalog):
+    """createOfferings / computeRequirements with reservations (R:offering.go:151-186, R:types.go:172,223-232)."""
+    from kpamd import catalog as cmod
+    import kpamd
+    rows = [r for r in cmod.load_ec2_table() if r["name"] in ("m5.large", "c5.xlarge")]
+    crs = [cmod.CapacityReservation("cr-1", "m5.large", cmod.ZONES[0], "default", 3),
+           cmod.CapacityReservation("cr-2", "m5.large", cmod.ZONES[1], "capacity-block", 0)]
+    cat = {t.name: t for t in cmod.build_catalog(kpamd.load_lib(), rows=rows, capacity_reservations=crs)}
+    m5, c5 = cat["m5.large"], cat["c5.xlarge"]
+    req = {r[0]: r for r in m5.requirements}
+    assert req[CT][2] == ["on-demand", "spot", "reserved"]
+    assert req[K + "capacity-reservation-id"] == (K + "capacity-reservation-id", "In", ["cr-1", "cr-2"])
+    assert req[K + "capacity-reservation-type"][1:] == ("In", ["capacity-block", "default"])
+    res = [o for o in m5.offerings if o.capacity_type == "reserved"]
+    od = next(o.price for o in m5.offerings if o.capacity_type == "on-demand")
+    assert [(o.reservation_id, o.zone, o.available, o.reservation_capacity) for o in res] == \
+        [("cr-1", cmod.ZONES[0], True, 3), ("cr-2", cmod.ZONES[1], False, 0)]
+    assert all(o.price == od / 10_000_000.0 for o in res)
+    creq = {r[0]: r for r in c5.requirements}
+    assert creq[CT][2] == ["on-demand", "spot"] and creq[K + "capacity-reservation-id"][1] == "DoesNotExist"
+    assert not any(o.capacity_type == "reserved" for o in c5.offerings)
 
 
 def reserved_requests(cat, n, seed):
