@@ -2143,6 +2143,7 @@ static void FilterCapacityBlock(const vector<InstanceType>& C, const Requirement
       sel_price = C[W[i].t].offerings[so].price;
     }
   }
+  if (sel_w < 0) return;  // no reserved capacity-block offering at all (the reference dereferences nil here)
   W = {W[sel_w]};
 }
 
