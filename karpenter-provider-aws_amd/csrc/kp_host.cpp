@@ -2171,23 +2171,36 @@ int32_t CompilePerCall(const kp_solve_in* in, const SolveRaw& raw, Compiled& cp)
     cp.pod_shape[p] = (int32_t)in->pods[p].shape;
     cp.queue[p] = (int32_t)p;
   }
-  // sort keys gathered once (cpu, memory of the pod's shape): the comparator then touches one array
+  // (cpu desc, memory desc) depends on the shape only: rank the shapes once, then sort the keys themselves
+  // (rank, creation, uid, pod) in place, so the comparator reads contiguous memory instead of gathering per pod
+  vector<int32_t> sorder(in->n_shapes), srank(in->n_shapes);
+  for (uint32_t s2 = 0; s2 < in->n_shapes; s2++) sorder[s2] = (int32_t)s2;
+  auto req_of = [&](int s2, int r) { return cp.shape_requests[(size_t)s2 * KP_NRES + r]; };
+  std::sort(sorder.begin(), sorder.end(), [&](int x, int y) {
+    if (req_of(x, KP_RES_CPU) != req_of(y, KP_RES_CPU)) return req_of(x, KP_RES_CPU) > req_of(y, KP_RES_CPU);
+    return req_of(x, KP_RES_MEMORY) > req_of(y, KP_RES_MEMORY);
+  });
+  for (uint32_t i = 0, r = 0; i < in->n_shapes; i++) {  // equal (cpu, memory) share a rank
+    if (i > 0 && (req_of(sorder[i], KP_RES_CPU) != req_of(sorder[i - 1], KP_RES_CPU) ||
+                  req_of(sorder[i], KP_RES_MEMORY) != req_of(sorder[i - 1], KP_RES_MEMORY)))
+      r = i;
+    srank[sorder[i]] = (int32_t)r;
+  }
   struct QKey {
-    int64_t cpu, mem, creation;
+    int32_t rank, pod;
+    int64_t creation;
     uint64_t uid;
   };
   vector<QKey> qk(in->n_pods);
-  for (uint32_t p = 0; p < in->n_pods; p++) {
-    const int64_t* r = &cp.shape_requests[(size_t)cp.pod_shape[p] * KP_NRES];
-    qk[p] = {r[KP_RES_CPU], r[KP_RES_MEMORY], in->pods[p].creation_unix, in->pods[p].uid_key};
-  }
-  std::sort(cp.queue.begin(), cp.queue.end(), [&](int x, int y) {
-    const QKey &p = qk[x], &q = qk[y];
-    if (p.cpu != q.cpu) return p.cpu > q.cpu;
-    if (p.mem != q.mem) return p.mem > q.mem;
+  for (uint32_t p = 0; p < in->n_pods; p++)
+    qk[p] = {srank[cp.pod_shape[p]], (int32_t)p, in->pods[p].creation_unix, in->pods[p].uid_key};
+  std::sort(qk.begin(), qk.end(), [](const QKey& p, const QKey& q) {
+    if (p.rank != q.rank) return p.rank < q.rank;
     if (p.creation != q.creation) return p.creation < q.creation;
-    return p.uid < q.uid;
+    if (p.uid != q.uid) return p.uid < q.uid;
+    return p.pod < q.pod;
   });
+  for (uint32_t p = 0; p < in->n_pods; p++) cp.queue[p] = qk[p].pod;
   return KP_OK;
 }
 
