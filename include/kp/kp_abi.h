@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define KP_ABI_VERSION 7
+#define KP_ABI_VERSION 8
 
 enum kp_status {
   KP_OK = 0,
@@ -684,7 +684,25 @@ void kp_cluster_plan_destroy(kp_cluster_plan* plan);
 typedef struct kp_comm kp_comm;
 int32_t kp_comm_unique_id(uint8_t* id /* KP_COMM_ID_BYTES */);
 int32_t kp_comm_init(kp_ctx* ctx, const uint8_t* id, int32_t n_ranks, int32_t rank, kp_comm** out);
+/* Single-process multi-GPU (the Karpenter controller is one leader-elected process): one kp_ctx per GPU, created by
+ * the caller, and one call that builds their n communicators at once (ncclCommInitAll; rank i = ctxs[i], distinct
+ * GPUs). Each rank is then driven by its own OS thread (one goroutine per GPU, runtime.LockOSThread): every
+ * collective entry point (kp_solve_prepare_comm, kp_consolidate_argmin) must be called by all n threads for the
+ * same step. out: n communicators. No unique-id transport is needed. */
+int32_t kp_comm_init_all(kp_ctx* const* ctxs, int32_t n, kp_comm** out);
+/* A communicator whose exchange step is a caller-supplied host all-gather: fn(user, rank, send, recv, bytes) must
+ * block until every rank contributed `bytes` and fill recv with n_ranks * bytes in rank order, returning 0 (non-zero:
+ * the step fails with KP_E_DEVICE). For transports other than RCCL (a gRPC stream between controller replicas, Go
+ * channels between goroutines, a test harness); the records exchanged are small (status words, 88-byte choices, and
+ * the template-options table only when it is sharded). */
+typedef int32_t (*kp_allgather_fn)(void* user, int32_t rank, const void* send, void* recv, size_t bytes);
+int32_t kp_comm_init_host(kp_ctx* ctx, int32_t n_ranks, int32_t rank, kp_allgather_fn fn, void* user, kp_comm** out);
+int32_t kp_comm_rank(const kp_comm* comm, int32_t* rank, int32_t* n_ranks);
 void kp_comm_destroy(kp_comm* comm);
+/* Collective steps never leave a peer waiting: a rank whose local part fails still takes part in the exchange with
+ * a failure record (kp_choice.subset = KP_CHOICE_FAILED, counts[0] = its error code; a status word in
+ * kp_solve_prepare_comm), and then every rank returns an error. */
+#define KP_CHOICE_FAILED (-2)
 
 typedef struct kp_choice {
   int64_t subset;         /* global subset index of the best decision; -1: every subset of every rank is a no-op */

@@ -967,7 +967,15 @@ int32_t kp_catalog_update_offerings(kp_catalog* c, const kp_offering_update* ups
     if (ups[i].type >= c->types.size())
       return fail(KP_E_INVAL, "update %u: type %u of %zu", i, ups[i].type, c->types.size());
     bool any = false;
-    for (auto& o : c->types[ups[i].type].offs) any = any || match(o, ups[i]);
+    for (auto& o : c->types[ups[i].type].offs) {
+      if (!match(o, ups[i])) continue;
+      any = true;
+      // a reserved offering is Available only with capacity left (R:offering.go:178 ReservationCapacity != 0 &&
+      // zone in itZones): an update giving capacity 0 with available set names a state upstream cannot reach
+      if ((o.has_rid || o.ct == "reserved") && ups[i].reservation_capacity == 0 && ups[i].available)
+        return fail(KP_E_INVAL, "update %u: reserved offering of type %u available with reservation capacity 0", i,
+                    ups[i].type);
+    }
     if (!any) return fail(KP_E_INVAL, "update %u names no offering of type %u", i, ups[i].type);
   }
   for (uint32_t i = 0; i < n; i++)
@@ -2314,12 +2322,69 @@ extern "C" {
 
 }  // extern "C"
 
+// A communicator of n_ranks kp_ctx (one per GPU): RCCL (kp_comm_init / kp_comm_init_all), or a caller-supplied host
+// all-gather (kp_comm_init_host). Its settings are read once here, so that every rank takes the same decisions.
 struct kp_comm {
   kp_ctx* ctx = nullptr;
-  ncclComm_t comm = nullptr;
+  ncclComm_t comm = nullptr;        // RCCL transport (null: host transport)
+  kp_allgather_fn host_fn = nullptr;
+  void* host_user = nullptr;
   int n_ranks = 1, rank = 0;
+  bool no_tfeas = false;            // KP_NO_TFEAS at init: no template-options table
+  uint64_t tfeas_shard_min = 0;     // shard the table over the ranks from this many (shape-level, template) pairs
   DevBuf buf;  // [0]: this rank's record, [1..n_ranks]: the gathered records
 };
+
+namespace {
+// All-gather of `bytes` per rank over host buffers (recv: n_ranks * bytes in rank order), through the comm's
+// transport. Every rank of a collective step calls this exactly once per step, whatever its local outcome: a rank
+// that failed locally sends a record saying so (the callers' status / KP_CHOICE_FAILED records), so no peer is left
+// waiting in the collective.
+int32_t CommExchange(kp_comm* c, const void* send, void* recv, size_t bytes) {
+  if (c->host_fn) {
+    if (c->host_fn(c->host_user, c->rank, send, recv, bytes) != 0)
+      return fail(KP_E_DEVICE, "host all-gather callback failed (rank %d)", c->rank);
+    return KP_OK;
+  }
+  hipStream_t st = c->ctx->stream;
+  if (c->buf.n < bytes * (size_t)(c->n_ranks + 1)) {
+    c->buf.reset();
+    HIPCHK(c->buf.alloc(bytes * (size_t)(c->n_ranks + 1)));
+  }
+  uint8_t* dev = (uint8_t*)c->buf.p;
+  HIPCHK(hipMemcpyAsync(dev, send, bytes, hipMemcpyHostToDevice, st));
+  ncclResult_t r = ncclAllGather(dev, dev + bytes, bytes, ncclUint8, c->comm, st);
+  if (r != ncclSuccess) return fail(KP_E_DEVICE, "ncclAllGather: %s", ncclGetErrorString(r));
+  HIPCHK(hipMemcpyAsync(recv, dev + bytes, bytes * (size_t)c->n_ranks, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  return KP_OK;
+}
+// Device-to-device all-gather (the template-options table): RCCL directly, or staged through the host transport.
+int32_t CommAllGatherDev(kp_comm* c, const void* send, void* recv, size_t bytes) {
+  hipStream_t st = c->ctx->stream;
+  if (!c->host_fn) {
+    ncclResult_t r = ncclAllGather(send, recv, bytes, ncclUint8, c->comm, st);
+    if (r != ncclSuccess) return fail(KP_E_DEVICE, "ncclAllGather: %s", ncclGetErrorString(r));
+    HIPCHK(hipStreamSynchronize(st));
+    return KP_OK;
+  }
+  vector<uint8_t> hs(bytes), hr(bytes * (size_t)c->n_ranks);
+  const hipError_t e = hipMemcpyAsync(hs.data(), send, bytes, hipMemcpyDeviceToHost, st);
+  const hipError_t e2 = e == hipSuccess ? hipStreamSynchronize(st) : e;
+  int32_t rc = CommExchange(c, hs.data(), hr.data(), bytes);  // reached even when the copy failed
+  if (e2 != hipSuccess) return fail(KP_E_DEVICE, "all-gather staging: %s", hipGetErrorString(e2));
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(recv, hr.data(), hr.size(), hipMemcpyHostToDevice, st));
+  HIPCHK(hipStreamSynchronize(st));
+  return KP_OK;
+}
+void CommReadSettings(kp_comm* c) {
+  c->no_tfeas = getenv("KP_NO_TFEAS") != nullptr;
+  // the table costs ~10 us per 1k pairs on one GPU and an all-gather tens of us: shard only tables worth it
+  c->tfeas_shard_min = 1u << 20;
+  if (const char* e = getenv("KP_TFEAS_SHARD_MIN")) c->tfeas_shard_min = strtoull(e, nullptr, 10);
+}
+}  // namespace
 
 struct kp_solve_plan {
   kp_ctx* ctx = nullptr;
@@ -2378,12 +2443,52 @@ int32_t kp_solve_prepare_comm(kp_ctx* ctx, const kp_solve_in* in, kp_comm* comm,
   if (comm && comm->ctx != ctx) return fail(KP_E_INVAL, "communicator belongs to another context");
   return SolvePrepare(ctx, in, comm, out);
 }
+static int32_t SolvePrepareLocal(kp_ctx* ctx, const kp_solve_in* in, kp_comm* comm,
+                                 std::unique_ptr<kp_solve_plan>& plan, size_t& gather_chunk, size_t& gather_off);
 static int32_t SolvePrepare(kp_ctx* ctx, const kp_solve_in* in, kp_comm* comm, kp_solve_plan** out) {
   auto t0 = std::chrono::steady_clock::now();
   if (!ctx || !in || !out) return fail(KP_E_INVAL, "null argument");
   std::lock_guard<std::recursive_mutex> lock(ctx->mu);
+  std::unique_ptr<kp_solve_plan> plan;
+  size_t chunk = 0, off = 0;
+  int32_t rc = SolvePrepareLocal(ctx, in, comm, plan, chunk, off);
+  if (comm && comm->n_ranks > 1) {
+    // every rank reaches this exchange, failed or not: (status, table chunk bytes) of each rank; the all-gather of
+    // the table follows only when every rank prepared and all agree on its size
+    const string err = g_err;
+    int64_t mine[2] = {rc, (int64_t)chunk};
+    vector<int64_t> all(2 * (size_t)comm->n_ranks);
+    int32_t xrc = CommExchange(comm, mine, all.data(), sizeof mine);
+    if (xrc) return xrc;
+    if (rc) {
+      g_err = err;
+      return rc;
+    }
+    for (int i = 0; i < comm->n_ranks; i++) {
+      if (all[2 * i]) return fail(KP_E_DEVICE, "rank %d failed to prepare the Solve (error %lld)", i, (long long)all[2 * i]);
+      if (all[2 * i + 1] != (int64_t)chunk)
+        return fail(KP_E_INVAL, "ranks disagree on the template-options table (%lld vs %zu bytes): every rank must "
+                    "pass the same batch", (long long)all[2 * i + 1], chunk);
+    }
+    if (chunk) {
+      uint8_t* tab = (uint8_t*)plan->buf.p + off;
+      rc = CommAllGatherDev(comm, tab + chunk * comm->rank, tab, chunk);
+      if (rc) return rc;
+    }
+  } else if (rc) {
+    return rc;
+  }
+  plan->prepare_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  *out = plan.release();
+  return KP_OK;
+}
+// Everything of a prepare that involves only this rank: compile, upload, this rank's rows of the template table.
+// gather_chunk > 0: the table rows [rank * chunk, (rank + 1) * chunk) bytes at gather_off still need the all-gather.
+static int32_t SolvePrepareLocal(kp_ctx* ctx, const kp_solve_in* in, kp_comm* comm,
+                                 std::unique_ptr<kp_solve_plan>& plan, size_t& gather_chunk, size_t& gather_off) {
+  gather_chunk = gather_off = 0;
   HIPCHK(hipSetDevice(ctx->device));
-  auto plan = std::make_unique<kp_solve_plan>();
+  plan = std::make_unique<kp_solve_plan>();
   plan->ctx = ctx;
   plan->cp = std::make_unique<Compiled>();
   Compiled& C = *plan->cp;
@@ -2502,8 +2607,10 @@ static int32_t SolvePrepare(kp_ctx* ctx, const kp_solve_in* in, kp_comm* comm, k
   // template options per (shape-level, template): rows split evenly over the communicator's ranks (padded so that
   // every rank contributes the same byte count to the all-gather)
   const int SLi = (int)C.shape_reqs.size();
-  const int n_ranks = comm ? comm->n_ranks : 1, my_rank = comm ? comm->rank : 0;
-  const bool tfeas_on = NT > 0 && SLi > 0 && !getenv("KP_NO_TFEAS");
+  const bool tfeas_on = NT > 0 && SLi > 0 && !(comm ? comm->no_tfeas : getenv("KP_NO_TFEAS") != nullptr);
+  // shard the rows over the ranks only when the table is large enough to repay the all-gather (kp_comm settings)
+  const bool shard = tfeas_on && comm && comm->n_ranks > 1 && (uint64_t)SLi * NT >= comm->tfeas_shard_min;
+  const int n_ranks = shard ? comm->n_ranks : 1, my_rank = shard ? comm->rank : 0;
   const int tf_words = TW + KP_NRES / 2 + 1;
   const int rows_per_rank = (SLi + n_ranks - 1) / n_ranks;
   const size_t tf_bytes = tfeas_on ? (size_t)rows_per_rank * n_ranks * NT * tf_words * sizeof(uint64_t) : 0;
@@ -2658,13 +2765,11 @@ static int32_t SolvePrepare(kp_ctx* ctx, const kp_solve_in* in, kp_comm* comm, k
     f.words = tf_words;
     f.out = (uint64_t*)(base + o_tfeas);
     HIPCHK(launch_tmpl_feas(f, ctx->stream));
-    if (comm && n_ranks > 1) {
-      const size_t chunk = (size_t)rows_per_rank * NT * tf_words * sizeof(uint64_t);
-      ncclResult_t r = ncclAllGather(base + o_tfeas + chunk * my_rank, base + o_tfeas, chunk, ncclUint8, comm->comm,
-                                     ctx->stream);
-      if (r != ncclSuccess) return fail(KP_E_DEVICE, "ncclAllGather: %s", ncclGetErrorString(r));
-    }
     HIPCHK(hipStreamSynchronize(ctx->stream));
+    if (shard) {  // the all-gather of every rank's rows follows in SolvePrepare, after the ranks' status exchange
+      gather_chunk = (size_t)rows_per_rank * NT * tf_words * sizeof(uint64_t);
+      gather_off = o_tfeas;
+    }
     a.tfeas = (const uint64_t*)(base + o_tfeas);
     a.tfeas_words = tf_words;
   }
@@ -2687,8 +2792,6 @@ static int32_t SolvePrepare(kp_ctx* ctx, const kp_solve_in* in, kp_comm* comm, k
   plan->o_nopt = o_nopt;
   plan->o_ncr = o_ncr;
   plan->opt_stride = opt_stride;
-  plan->prepare_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  *out = plan.release();
   return KP_OK;
 }
 
@@ -4287,6 +4390,9 @@ int32_t kp_choice_reduce(const kp_choice* per_rank, uint32_t n, kp_choice* out) 
   memset(&best, 0, sizeof best);
   best.subset = -1;
   uint64_t counts[3] = {0, 0, 0}, overflowed = 0;
+  for (uint32_t i = 0; i < n; i++)
+    if (per_rank[i].subset == KP_CHOICE_FAILED)
+      return fail(KP_E_DEVICE, "rank %u failed its step of the sweep (error %lld)", i, (long long)per_rank[i].counts[0]);
   for (uint32_t i = 0; i < n; i++) {
     for (int k = 0; k < 3; k++) counts[k] += per_rank[i].counts[k];
     overflowed += per_rank[i].overflowed;
@@ -4322,7 +4428,60 @@ int32_t kp_comm_init(kp_ctx* ctx, const uint8_t* id, int32_t n_ranks, int32_t ra
   ncclResult_t r = ncclCommInitRank(&c->comm, n_ranks, u, rank);
   if (r != ncclSuccess) return nccl_fail(r, "ncclCommInitRank");
   HIPCHK(c->buf.alloc(sizeof(CommBest) * (size_t)(n_ranks + 1)));
+  CommReadSettings(c.get());
   *out = c.release();
+  return KP_OK;
+}
+
+int32_t kp_comm_init_all(kp_ctx* const* ctxs, int32_t n, kp_comm** out) {
+  if (!ctxs || !out || n < 1) return fail(KP_E_INVAL, "null argument");
+  vector<int> devs(n);
+  for (int i = 0; i < n; i++) {
+    if (!ctxs[i]) return fail(KP_E_INVAL, "null context %d", i);
+    devs[i] = ctxs[i]->device;
+    for (int j = 0; j < i; j++)
+      if (devs[j] == devs[i]) return fail(KP_E_INVAL, "contexts %d and %d share GPU %d (RCCL: one rank per GPU)", j, i, devs[i]);
+  }
+  vector<ncclComm_t> comms(n, nullptr);
+  ncclResult_t r = ncclCommInitAll(comms.data(), n, devs.data());
+  if (r != ncclSuccess) return nccl_fail(r, "ncclCommInitAll");
+  vector<std::unique_ptr<kp_comm>> cs(n);
+  for (int i = 0; i < n; i++) {
+    cs[i] = std::make_unique<kp_comm>();
+    cs[i]->ctx = ctxs[i];
+    cs[i]->comm = comms[i];
+    cs[i]->n_ranks = n;
+    cs[i]->rank = i;
+    CommReadSettings(cs[i].get());
+  }
+  for (int i = 0; i < n; i++) {
+    if (hipSetDevice(devs[i]) != hipSuccess || cs[i]->buf.alloc(sizeof(CommBest) * (size_t)(n + 1)) != hipSuccess) {
+      for (int j = 0; j < n; j++) (void)ncclCommDestroy(comms[j]);
+      return fail(KP_E_NOMEM, "communicator buffer on GPU %d", devs[i]);
+    }
+  }
+  for (int i = 0; i < n; i++) out[i] = cs[i].release();
+  return KP_OK;
+}
+
+int32_t kp_comm_init_host(kp_ctx* ctx, int32_t n_ranks, int32_t rank, kp_allgather_fn fn, void* user, kp_comm** out) {
+  if (!ctx || !fn || !out) return fail(KP_E_INVAL, "null argument");
+  if (n_ranks < 1 || rank < 0 || rank >= n_ranks) return fail(KP_E_INVAL, "rank %d of %d", rank, n_ranks);
+  auto c = std::make_unique<kp_comm>();
+  c->ctx = ctx;
+  c->host_fn = fn;
+  c->host_user = user;
+  c->n_ranks = n_ranks;
+  c->rank = rank;
+  CommReadSettings(c.get());
+  *out = c.release();
+  return KP_OK;
+}
+
+int32_t kp_comm_rank(const kp_comm* c, int32_t* rank, int32_t* n_ranks) {
+  if (!c) return fail(KP_E_INVAL, "null argument");
+  if (rank) *rank = c->rank;
+  if (n_ranks) *n_ranks = c->n_ranks;
   return KP_OK;
 }
 
@@ -4341,49 +4500,56 @@ int32_t kp_consolidate_argmin(kp_cluster_plan* plan, kp_comm* comm, const uint32
   if (comm && comm->ctx->device != plan->ctx->device) return fail(KP_E_INVAL, "comm and plan are on different GPUs");
   kp_ctx* ctx = plan->ctx;
   std::lock_guard<std::recursive_mutex> lock(ctx->mu);
-  HIPCHK(hipSetDevice(ctx->device));
   if (stats) memset(stats, 0, sizeof *stats);
   hipStream_t st = ctx->stream;
-  // this rank's record slot: its own buffer without a comm
-  DevBuf solo;
-  CommBest* mine;
-  if (comm) {
-    mine = (CommBest*)comm->buf.p;
-  } else {
-    HIPCHK(solo.alloc(sizeof(CommBest)));
-    mine = (CommBest*)solo.p;
-  }
-  SimArgs a;
-  memset(&a, 0, sizeof a);
   float ms = 0;
   uint64_t kst[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  DevBuf parts;
-  const int n_parts = (int)std::min<uint32_t>(std::max<uint32_t>((n_subsets + 4095) / 4096, 1), 1024);
-  HIPCHK(parts.alloc(sizeof(ArgmaxPart) * n_parts));
-  if (n_subsets) {
-    int32_t rc = SimLaunchLocked(plan, offsets, nodes, n_subsets, multi_node, a);
-    if (rc) return rc;
-    if (out) HIPCHK(hipMemcpyAsync(out, a.out, sizeof(SimOut) * n_subsets, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(kst, a.stats, sizeof kst, hipMemcpyDeviceToHost, st));
+  CommBest mine;  // this rank's record (host)
+  memset(&mine, 0, sizeof mine);
+  DevBuf rec, parts;
+  // the local step: simulation + device argmax into one record; any failure becomes a KP_CHOICE_FAILED record so that
+  // the collective below is still reached by every rank
+  auto local = [&]() -> int32_t {
+    HIPCHK(hipSetDevice(ctx->device));
+    SimArgs a;
+    memset(&a, 0, sizeof a);
+    const int n_parts = (int)std::min<uint32_t>(std::max<uint32_t>((n_subsets + 4095) / 4096, 1), 1024);
+    HIPCHK(parts.alloc(sizeof(ArgmaxPart) * n_parts));
+    HIPCHK(rec.alloc(sizeof(CommBest)));
+    if (n_subsets) {
+      int32_t rc = SimLaunchLocked(plan, offsets, nodes, n_subsets, multi_node, a);
+      if (rc) return rc;
+      if (out) HIPCHK(hipMemcpyAsync(out, a.out, sizeof(SimOut) * n_subsets, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipMemcpyAsync(kst, a.stats, sizeof kst, hipMemcpyDeviceToHost, st));
+    }
+    HIPCHK(launch_argmax(n_subsets ? a.out : nullptr, (int)n_subsets, (ArgmaxPart*)parts.p, n_parts,
+                         (int64_t)base_index, (CommBest*)rec.p, st));
+    HIPCHK(hipMemcpyAsync(&mine, rec.p, sizeof mine, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (n_subsets && plan->general) ms = (float)plan->general_ms;
+    else if (n_subsets) HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    return KP_OK;
+  };
+  const int32_t lrc = local();
+  if (lrc) {
+    memset(&mine, 0, sizeof mine);
+    mine.index = KP_CHOICE_FAILED;
+    mine.counts[0] = (uint64_t)(int64_t)lrc;
   }
-  HIPCHK(launch_argmax(n_subsets ? a.out : nullptr, (int)n_subsets, (ArgmaxPart*)parts.p, n_parts,
-                       (int64_t)base_index, mine, st));
   const int nr = comm ? comm->n_ranks : 1;
   vector<CommBest> recs(nr);
-  if (comm) {  // one collective: every rank's 80-byte record to every rank (RCCL over xGMI)
-    CommBest* gathered = mine + 1;
-    ncclResult_t r = ncclAllGather(mine, gathered, sizeof(CommBest), ncclUint8, comm->comm, st);
-    if (r != ncclSuccess) return nccl_fail(r, "ncclAllGather");
-    HIPCHK(hipMemcpyAsync(recs.data(), gathered, sizeof(CommBest) * nr, hipMemcpyDeviceToHost, st));
+  if (comm && nr > 1) {  // one collective: every rank's 88-byte record to every rank (RCCL over xGMI)
+    const string err = g_err;
+    int32_t rc = CommExchange(comm, &mine, recs.data(), sizeof mine);
+    if (rc) return rc;
+    g_err = err;
   } else {
-    HIPCHK(hipMemcpyAsync(recs.data(), mine, sizeof(CommBest), hipMemcpyDeviceToHost, st));
+    recs[0] = mine;
   }
-  HIPCHK(hipStreamSynchronize(st));
-  if (n_subsets && plan->general) ms = (float)plan->general_ms;
-  else if (n_subsets) HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+  if (lrc) return lrc;
   for (int i = 0; i < nr; i++)
-    if (recs[i].counts[3]) return fail(KP_E_DEVICE, "rank %d: %llu subsets overflowed the pod queue", i,
-                                       (unsigned long long)recs[i].counts[3]);
+    if (recs[i].index != KP_CHOICE_FAILED && recs[i].counts[3])
+      return fail(KP_E_DEVICE, "rank %d: %llu subsets overflowed the pod queue", i, (unsigned long long)recs[i].counts[3]);
   vector<kp_choice> ch(nr);
   memcpy(ch.data(), recs.data(), sizeof(kp_choice) * nr);
   int32_t rc = kp_choice_reduce(ch.data(), (uint32_t)nr, best);

@@ -3062,7 +3062,7 @@ __global__ __launch_bounds__(LAUNCH_WAVES * 64) void launch_kernel(LaunchArgs a)
       return pick;
     };
     auto om_of = [&](int t) -> uint64_t { return rof ? rof_pick(t) : M; };
-    if (m && has_res && res_cand) {
+    if (m && has_res) {  // (no compatible reserved class: CapacityReservationType is a no-op, CapacityBlock may still apply)
       // CapacityReservationTypeFilter (R:filter.go:80-144): the partition with the cheapest available compatible
       // reserved offering (ties: default before capacity-block)
       double pmin[2] = {INF, INF};

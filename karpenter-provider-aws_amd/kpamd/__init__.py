@@ -85,6 +85,10 @@ def load_lib(path=None):
         "kp_comm_unique_id": (C.c_int32, [C.c_char_p]),
         "kp_comm_init": (C.c_int32, [C.c_void_p, C.c_char_p, C.c_int32, C.c_int32, P(C.c_void_p)]),
         "kp_comm_destroy": (None, [C.c_void_p]),
+        "kp_comm_init_all": (C.c_int32, [P(C.c_void_p), C.c_int32, P(C.c_void_p)]),
+        "kp_comm_init_host": (C.c_int32, [C.c_void_p, C.c_int32, C.c_int32, abi.AllGatherFn, C.c_void_p,
+                                          P(C.c_void_p)]),
+        "kp_comm_rank": (C.c_int32, [C.c_void_p, P(C.c_int32), P(C.c_int32)]),
         "kp_consolidate_argmin": (C.c_int32, [C.c_void_p, C.c_void_p, P(C.c_uint32), P(C.c_uint32), C.c_uint32,
                                               C.c_uint64, C.c_int32, P(abi.SimResult), P(abi.Choice),
                                               P(abi.SolveStats)]),
@@ -541,13 +545,49 @@ def comm_unique_id(lib=None):
 
 
 class Comm:
-    """kp_comm: one rank of the RCCL communicator over the node's GPUs (kp_comm_init is collective)."""
+    """kp_comm: one rank of a communicator over the node's GPUs. Comm(ctx, uid, n, rank) is one rank of an RCCL
+    communicator (kp_comm_init, collective, one process per GPU); Comm.init_all(ctxs) builds the n RCCL ranks of one
+    process (kp_comm_init_all, one thread per GPU); Comm.host(ctx, n, rank, allgather) uses a host all-gather
+    (kp_comm_init_host): allgather(rank, data: bytes) -> list of n bytes objects, blocking until every rank sent."""
 
-    def __init__(self, ctx, uid, n_ranks, rank):
+    def __init__(self, ctx, uid=None, n_ranks=1, rank=0, _handle=None):
         self.ctx = ctx
+        self._cb = None
+        if _handle is not None:
+            self.h = _handle
+            return
         h = C.c_void_p()
         _check(ctx.lib, ctx.lib.kp_comm_init(ctx.h, bytes(uid), n_ranks, rank, C.byref(h)))
         self.h = h
+
+    @classmethod
+    def init_all(cls, ctxs):
+        lib = ctxs[0].lib
+        hs = (C.c_void_p * len(ctxs))(*[c.h for c in ctxs])
+        out = (C.c_void_p * len(ctxs))()
+        _check(lib, lib.kp_comm_init_all(hs, len(ctxs), out))
+        return [cls(c, _handle=C.c_void_p(out[i])) for i, c in enumerate(ctxs)]
+
+    @classmethod
+    def host(cls, ctx, n_ranks, rank, allgather):
+        def fn(_user, r, send, recv, nbytes):
+            try:
+                parts = allgather(int(r), C.string_at(send, nbytes))
+                C.memmove(recv, b"".join(parts), nbytes * n_ranks)
+                return 0
+            except Exception:  # the library turns a non-zero return into KP_E_DEVICE
+                return 1
+        cb = abi.AllGatherFn(fn)
+        h = C.c_void_p()
+        _check(ctx.lib, ctx.lib.kp_comm_init_host(ctx.h, n_ranks, rank, cb, None, C.byref(h)))
+        c = cls(ctx, _handle=h)
+        c._cb = cb  # keep the trampoline alive as long as the communicator
+        return c
+
+    def rank(self):
+        r, n = C.c_int32(), C.c_int32()
+        _check(self.ctx.lib, self.ctx.lib.kp_comm_rank(self.h, C.byref(r), C.byref(n)))
+        return r.value, n.value
 
     def close(self):
         if self.h:
@@ -559,6 +599,39 @@ class Comm:
             self.close()
         except Exception:
             pass
+
+
+class ThreadAllGather:
+    """In-process host all-gather for n threads (one per kp_ctx): the exchange step of Comm.host when the ranks
+    are threads of one process (the one-goroutine-per-GPU pattern; tests run it on one GPU)."""
+
+    def __init__(self, n):
+        import threading
+        self.n = n
+        self.slots = [None] * n
+        self.b1 = threading.Barrier(n)
+        self.b2 = threading.Barrier(n)
+
+    def __call__(self, rank, data):
+        self.slots[rank] = data
+        self.b1.wait(timeout=120)
+        out = list(self.slots)
+        self.b2.wait(timeout=120)
+        return out
+
+
+def torch_allgather(group=None):
+    """Host all-gather over torch.distributed (e.g. gloo across processes) for Comm.host."""
+    import torch
+    import torch.distributed as dist
+
+    def ag(rank, data):
+        n = dist.get_world_size(group)
+        t = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+        parts = [torch.empty_like(t) for _ in range(n)]
+        dist.all_gather(parts, t, group=group)
+        return [bytes(p.numpy().tobytes()) for p in parts]
+    return ag
 
 
 def choice_reduce(records, lib=None):

@@ -247,6 +247,8 @@ class Choice(C.Structure):
 
 
 COMM_ID_BYTES = 128
+CHOICE_FAILED = -2  # kp_choice.subset of a rank whose step failed
+AllGatherFn = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_size_t)
 
 
 class FeasibilityQuery(C.Structure):

@@ -23,7 +23,7 @@ def test_all_declared_symbols_exported():
 
 def test_abi_version_and_struct_sizes():
     lib = kpamd.load_lib()
-    assert lib.kp_abi_version() == 7
+    assert lib.kp_abi_version() == 8
     from kpamd import abi
     assert C.sizeof(abi.ResourceList) == 12 * 8 + 8
     assert C.sizeof(abi.Offering) == 5 * 8 + 8 + 8
@@ -53,13 +53,20 @@ def test_struct_sizes_match_the_c_header(tmp_path):
     import shutil
     import subprocess
     from kpamd import abi
+    import pytest
     if not shutil.which("gcc"):
-        return
+        pytest.skip("gcc not available")
     pairs = {"kp_pod_shape": abi.PodShape, "kp_existing_node": abi.ExistingNode, "kp_host_port": abi.HostPort,
              "kp_cluster_node": abi.ClusterNode, "kp_solve_in": abi.SolveIn, "kp_topology_spread": abi.TopologySpread,
              "kp_nodepool": abi.NodePool, "kp_cluster": abi.Cluster,
              "kp_pod_affinity_term": abi.PodAffinityTerm, "kp_bound_pod": abi.BoundPod,
-             "kp_offering": abi.Offering, "kp_offering_update": abi.OfferingUpdate, "kp_launch_result": abi.LaunchResult}
+             "kp_offering": abi.Offering, "kp_offering_update": abi.OfferingUpdate, "kp_launch_result": abi.LaunchResult,
+             "kp_solve_stats": abi.SolveStats, "kp_nodeclass": abi.NodeClass, "kp_kubelet": abi.Kubelet,
+             "kp_eviction_value": abi.EvictionValue, "kp_choice": abi.Choice, "kp_sim_result": abi.SimResult,
+             "kp_options": abi.Options, "kp_ec2_info": abi.EC2Info, "kp_nodeclaim_info": abi.NodeClaimInfo,
+             "kp_launch_request": abi.LaunchRequest, "kp_feasibility_query": abi.FeasibilityQuery,
+             "kp_instance_type": abi.InstanceType, "kp_preferred_term": abi.PreferredTerm,
+             "kp_label_selector": abi.LabelSelector, "kp_pod": abi.Pod}
     src = tmp_path / "sz.c"
     src.write_text('#include <stdio.h>\n#include "kp/kp_abi.h"\nint main(void){\n' +
                    "".join(f'printf("%zu\\n", sizeof({k}));\n' for k in pairs) + "return 0;}\n")

@@ -65,6 +65,29 @@ def test_update_rejects_unknown_offering_all_or_nothing(lib, catalog, bad):
         lib.kp_catalog_destroy(h)
 
 
+def test_update_reserved_capacity_zero_cannot_be_available(lib):
+    """R:offering.go:178: a reserved offering's Available is ReservationCapacity != 0 && zone in itZones, so an update
+    that sets capacity 0 while marking it available is refused (all or nothing); capacity 0 + unavailable applies."""
+    import kpamd
+    from kpamd import abi, catalog as catmod
+    rows = [r for r in catmod.load_ec2_table() if r["name"] in ("m5.large", "c5.xlarge")]
+    crs = [catmod.CapacityReservation("cr-1", "m5.large", "test-zone-1a", available_count=3)]
+    its = catmod.build_catalog(lib, rows=rows, capacity_reservations=crs)
+    t = next(i for i, it in enumerate(its) if it.name == "m5.large")
+    h, _ = _host_catalog(lib, its)
+    try:
+        def up(avail, cap):
+            return (abi.OfferingUpdate * 1)(abi.OfferingUpdate(t, avail, b"reserved", b"test-zone-1a", math.nan, b"cr-1",
+                                                                cap, 0))
+        assert lib.kp_catalog_update_offerings(h, up(1, 0), 1, 8) == kpamd.abi.KP_E_INVAL
+        assert lib.kp_catalog_seqnum(h) == 7
+        assert lib.kp_catalog_update_offerings(h, up(0, 0), 1, 8) == 0
+        assert lib.kp_catalog_update_offerings(h, up(1, 2), 1, 9) == 0
+        assert lib.kp_catalog_seqnum(h) == 9
+    finally:
+        lib.kp_catalog_destroy(h)
+
+
 def test_oracle_ice_marks_equal_rebuilt_catalogue(lib, catalog):
     """The update semantics (flip Available of the named offerings) == createOfferings with the ICE set."""
     from kpamd import catalog as kc

@@ -241,6 +241,39 @@ def test_device_launch_reserved_matches_oracle(ctx, catalog, seed):
     assert sum(g["rejected_reservation"] > 0 for g in got) > 0
 
 
+def _cb_first_types():
+    """The first type's first offering is a capacity block in a zone the request excludes: no reserved offering is
+    compatible, yet CapacityBlockFilter's shouldFilter (R:filter.go:204-220) looks only at that first offering and the
+    requirement admitting reserved, so it applies."""
+    return [InstanceType("cb-first", [(CT, "In", ["on-demand", "reserved"])], {"cpu": 2000}, {},
+                         [off("reserved", True, 0.5, "zone-1a", rt="capacity-block", rid="cr-cb", cap=1),
+                          off("on-demand", True, 0.2, "zone-1b")]),
+            InstanceType("plain", [(CT, "In", ["on-demand"])], {"cpu": 2000}, {}, [off("on-demand", True, 0.1, "zone-1b")])]
+
+
+def test_oracle_capacity_block_without_compatible_reservation():
+    kept, rej, offs = run("block", _cb_first_types(), [(CT, "In", ["on-demand", "reserved"]), (Z, "In", ["zone-1b"])])
+    assert kept == {"cb-first"} and rej == {"plain"}
+    assert [o.reservation_type for o in offs["cb-first"]] == ["capacity-block"]
+
+
+@pytest.mark.gpu
+def test_device_launch_capacity_block_without_compatible_reservation(ctx):
+    import kpamd
+    from oracle import pyoracle
+    types = _cb_first_types()
+    reqs = [([(CT, "In", ["on-demand", "reserved"]), (Z, "In", ["zone-1b"])], {"cpu": 1000}, [0, 1]),
+            ([(CT, "In", ["on-demand"]), (Z, "In", ["zone-1b"])], {"cpu": 1000}, [0, 1])]
+    ch = kpamd.Catalog(ctx, types)
+    plan = kpamd.LaunchPlan(ctx, ch, reqs, ["zone-1a", "zone-1b"])
+    got, _ = plan.run(read=True)
+    plan.close()
+    ch.close()
+    want = pyoracle.launch_select(types, reqs, ["zone-1a", "zone-1b"])
+    assert got == want
+    assert got[0]["types"] == [0] and got[0]["rejected_reservation"] == 1 and len(got[1]["types"]) == 2
+
+
 @pytest.mark.gpu
 def test_device_launch_reserved_kat(ctx):
     import kpamd
