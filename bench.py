@@ -328,17 +328,8 @@ def _consolidation(args, cat, ctx, dist, rank, world, barrier, kcomm):
     cands = np.asarray(cl.candidates, dtype=np.uint32)
     n_chunks = (args.subsets + CHUNK - 1) // CHUNK
     lo, hi = disruption.shard(n_chunks, rank, world)  # contiguous chunk range: balanced for N in 1, 2, 4, 8
-    offs_l, nodes_l, base = [], [], 0
-    for c in range(lo, hi):  # this rank's chunks concatenated into ONE launch
-        n = min(CHUNK, args.subsets - c * CHUNK)
-        offs, pos = disruption.random_subsets_csr(len(cands), n, seed=1000 + c)
-        offs_l.append(offs[:-1] + base)
-        nodes_l.append(cands[pos])
-        base += int(offs[-1])
-    offs_l.append(np.array([base], dtype=np.uint32))
-    sw_offs = np.concatenate(offs_l).astype(np.uint32)
-    sw_nodes = np.concatenate(nodes_l) if nodes_l else np.zeros(0, dtype=np.uint32)
-    base_index = lo * CHUNK
+    # this rank's chunks concatenated into ONE launch
+    sw_offs, sw_nodes, base_index = disruption.sweep_subsets(cands, args.subsets, lo, hi)
     mids = disruption.MultiNodeConsolidation.search_prefixes(len(cands))
     pre = [cands[:m + 1] for m in mids]
     pre_offs = np.zeros(len(pre) + 1, dtype=np.uint32)

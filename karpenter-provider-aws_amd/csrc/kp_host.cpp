@@ -3077,6 +3077,60 @@ static int32_t RefreshOfferings(kp_ctx* ctx, const kp_catalog* cat, Compiled& cp
   return KP_OK;
 }
 
+// Which catalogue columns feasibility_lds_kernel stages in LDS for this batch: the codes of the keys the rows name
+// (most read), the allocatable of the resources they request, then the class-major prices, while they fit beside
+// the kernel's static LDS; a column that does not fit is gathered from global memory. Without any: the
+// global-gather kernel.
+static int32_t FeasStageLds(kp_ctx* ctx, const DevDict& dd, const vector<KReqs>& qreqs, const vector<int64_t>& qrq,
+                            uint32_t n_queries, FeasArgs& fa) {
+  fa.lds_bytes = 0;
+  fa.lds_keys = 0;
+  fa.lds_res = 0;
+  fa.price_lds = 0;
+  if (getenv("KP_FEAS_GLOBAL") || n_queries == 0) return KP_OK;  // measurement hook: the global-gather kernel
+  hipFuncAttributes attr;
+  HIPCHK(hipFuncGetAttributes(&attr, feasibility_lds_kernel_ptr()));
+  const long budget = 160 * 1024 - (long)attr.sharedSizeBytes - 256;
+  const long T = dd.T, tiles = (T + 63) / 64;
+  uint64_t keys = 0;
+  uint32_t res = 0;
+  for (uint32_t i = 0; i < n_queries; i++) {
+    keys |= qreqs[i].present;
+    for (int r = 0; r < KP_NRES; r++)
+      if (qrq[(size_t)i * KP_NRES + r] > 0) res |= 1u << r;
+  }
+  keys &= dd.catalog_keys;
+  long used = tiles * 8;
+  if (getenv("KP_FEAS_NO_KEYS")) keys = 0;  // measurement hooks: leave a column family in global memory
+  if (getenv("KP_FEAS_NO_RES")) res = 0;
+  for (uint64_t m = keys; m; m &= m - 1)
+    if (used + (2 * T + 7) / 8 * 8 <= budget) {  // codes rows padded to 8 B so the total stays a multiple of 8
+      fa.lds_keys |= 1ull << __builtin_ctzll(m);
+      used += (2 * T + 7) / 8 * 8;
+    }
+  for (uint32_t m = res; m; m &= m - 1)
+    if (used + 8 * T <= budget) {
+      fa.lds_res |= 1u << __builtin_ctz(m);
+      used += 8 * T;
+    }
+  if (used + 8 * T * dd.C <= budget && !getenv("KP_FEAS_NO_PRICE")) {
+    fa.price_lds = 1;
+    used += 8 * T * dd.C;
+  }
+  if (!fa.lds_keys && !fa.lds_res && !fa.price_lds) return KP_OK;
+  // the kernel lays codes rows back to back: size them exactly (+ alignment slack)
+  const long n_k = __builtin_popcountll(fa.lds_keys);
+  used = (fa.price_lds ? 8 * T * dd.C : 0) + 8 * T * __builtin_popcount(fa.lds_res) + 8 * tiles + 2 * T * n_k + 16;
+  if (used > budget) return fail(KP_E_INVAL, "feasibility LDS plan %ld B exceeds %ld B", used, budget);
+  int ncu = 256;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || ncu <= 0) ncu = 256;
+  fa.lds_bytes = (int32_t)((used + 15) & ~15L);
+  fa.blocks = (int32_t)std::min<long>(ncu, ((long)n_queries + 15) / 16);
+  if (const char* e = getenv("KP_FEAS_BLOCKS")) fa.blocks = std::max(1, atoi(e));
+  HIPCHK(hipFuncSetAttribute(feasibility_lds_kernel_ptr(), hipFuncAttributeMaxDynamicSharedMemorySize, fa.lds_bytes));
+  return KP_OK;
+}
+
 struct kp_filter_plan {
   kp_ctx* ctx = nullptr;
   DevBuf buf;
@@ -3144,6 +3198,8 @@ int32_t kp_filter_prepare(kp_ctx* ctx, const kp_catalog* cat, const kp_feasibili
   fa.q_requests = (const int64_t*)(base + o_qr);
   fa.out_mask = (uint64_t*)(base + plan->o_mask);
   fa.out_cheapest = with_cheapest ? (double*)(base + plan->o_ch) : nullptr;
+  rc = FeasStageLds(ctx, cp.B->d.dd, qreqs, qrq, n_queries, fa);
+  if (rc) return rc;
   plan->n_queries = n_queries;
   plan->T = T;
   plan->tiles = tiles;

@@ -2882,6 +2882,164 @@ __global__ __launch_bounds__(FEAS_WAVES * 64) void feasibility_kernel(FeasArgs a
   }
 }
 
+// feasibility_lds_kernel: the same filter with the catalogue columns a batch reads staged in LDS. One persistent
+// workgroup of 16 waves per CU copies the single-value codes of the keys the rows name, the allocatable of the
+// resources they request and the class-major prices into LDS (~120 KB at T = 919), once; then every (row, type) test
+// is LDS reads + ALU, and the kernel streams what HBM must carry: each row's requirements in, its mask words and
+// one f64 cheapest price per type out. Per row the wave decodes the requirement set once (allowed value words in
+// LDS, compatible offering classes), then walks the types two 64-type tiles at a time (independent LDS reads in
+// flight), ballot -> mask word (kept in lane `tile` and stored coalesced at the end of the row).
+#define FEAS2_WAVES 16
+#define FEAS2_TB 2  // tiles per step
+__global__ __launch_bounds__(FEAS2_WAVES * 64) void feasibility_lds_kernel(FeasArgs a) {
+  __shared__ DevDict D;
+  __shared__ uint64_t s_allowed[FEAS2_WAVES][KP_MAX_WORDS];
+  __shared__ int64_t s_vint[KP_MAX_BOUND_KEYS * 64];
+  extern __shared__ __attribute__((aligned(16))) uint64_t s_cat2[];
+  block_copy(D, a.dict);
+  __syncthreads();
+  const DevCatalog Cg = *a.cat;
+  const int T = D.T, tiles = (T + 63) >> 6, C = D.C;
+  const int tid = threadIdx.x;
+  constexpr int NT = FEAS2_WAVES * 64;
+  const uint64_t lds_keys = a.lds_keys;
+  const uint32_t lds_res = a.lds_res;
+  const int n_k = __builtin_popcountll(lds_keys), n_r = __builtin_popcount(lds_res);
+  double LDS* s_price = (double LDS*)s_cat2;                                              // [C][T]
+  int64_t LDS* s_alloc = (int64_t LDS*)(s_cat2 + (a.price_lds ? (size_t)C * T : 0));       // [n_r][T]
+  uint64_t LDS* s_nonneg = (uint64_t LDS*)(s_alloc + (size_t)n_r * T);                     // [tiles]
+  uint16_t LDS* s_code = (uint16_t LDS*)(s_nonneg + tiles);                                // [n_k][T]
+  if (a.price_lds)
+    for (int i = tid; i < C * T; i += NT) s_price[i] = Cg.price_cm[i];
+  {
+    int s = 0;
+    for (uint32_t rm = lds_res; rm; rm &= rm - 1, s++) {
+      const int64_t* src = Cg.alloc + (size_t)__builtin_ctz(rm) * T;
+      for (int i = tid; i < T; i += NT) s_alloc[(size_t)s * T + i] = src[i];
+    }
+    s = 0;
+    for (uint64_t km = lds_keys; km; km &= km - 1, s++) {
+      const uint16_t* src = Cg.code + (size_t)__builtin_ctzll(km) * T;
+      for (int i = tid; i < T; i += NT) s_code[(size_t)s * T + i] = src[i];
+    }
+  }
+  for (int i = tid; i < tiles; i += NT) s_nonneg[i] = Cg.nonneg[i];
+  for (int i = tid; i < D.KB * 64; i += NT) s_vint[i] = a.vint[i];
+  __syncthreads();
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = LANE;
+  const VInt vi{(const int64_t LDS*)s_vint, a.vint, D.KB};
+  const bool custom_on = a.mode_compatible && Cg.custom_any;
+  for (long q = (long)blockIdx.x * FEAS2_WAVES + wave; q < a.n_queries; q += (long)gridDim.x * FEAS2_WAVES) {
+    const KReqs* Q = reinterpret_cast<const KReqs*>(a.q_reqs + (size_t)q * sizeof(KReqs));
+    const uint64_t v = lane < D.W ? Q->vals[lane] : 0;
+    const int64_t rq_lane = lane < KP_NRES ? a.q_requests[(size_t)q * KP_NRES + lane] : 0;
+    ReqView rv;
+    rv.present = Q->present;
+    rv.compl_ = Q->compl_ & Q->present;
+    rv.hgt = Q->hgt;
+    rv.hlt = Q->hlt;
+    rv.hmin = Q->hmin;
+    rv.nz = nz_keys(D, v);
+    rv.dne = 0;
+    rv.gt = Q->gt;
+    rv.lt = Q->lt;
+    rv.minv = Q->minv;
+    const uint64_t negQ = negop_mask(rv.present, rv.compl_, rv.nz);
+    const uint64_t allowed = allowed_word(D, rv, v, vi);
+    const uint64_t cls = allowed_classes<true>(D, Cg.cls, rv, allowed, negQ);
+    uint64_t LDS* al_w = (uint64_t LDS*)s_allowed[wave];
+    al_w[lane] = allowed;
+    const uint32_t rmask = (uint32_t)__ballot(rq_lane > 0);
+    wave_sync();
+    const uint64_t keys0 = rv.present & D.catalog_keys;
+    const bool custom = custom_on && (Cg.custom_any & ~rv.present);
+    double* oc = a.out_cheapest ? a.out_cheapest + (size_t)q * T : nullptr;
+    uint64_t myword = 0;
+    for (int tile0 = 0; tile0 < tiles; tile0 += FEAS2_TB) {
+      int tt[FEAS2_TB];
+      bool valid[FEAS2_TB], alive[FEAS2_TB];
+#pragma unroll
+      for (int i = 0; i < FEAS2_TB; i++) {
+        const int t = (tile0 + i) * 64 + lane;
+        valid[i] = tile0 + i < tiles && t < T;
+        tt[i] = valid[i] ? t : 0;
+        alive[i] = valid[i] && ((s_nonneg[min(tile0 + i, tiles - 1)] >> lane) & 1);
+      }
+      if (custom) {  // Compatible(q, type, WK) part (a): non-well-known type keys q does not define
+#pragma unroll
+        for (int i = 0; i < FEAS2_TB; i++) alive[i] = alive[i] && !(Cg.custom_nonneg[tt[i]] & ~rv.present);
+      }
+      // Intersects over the shared keys
+      for (uint64_t keys = keys0; keys; keys &= keys - 1) {
+        const int k = __builtin_ctzll(keys);
+        const bool staged = (lds_keys >> k) & 1;
+        const int slot = __builtin_popcountll(lds_keys & ((1ull << k) - 1));
+        uint32_t code[FEAS2_TB];
+#pragma unroll
+        for (int i = 0; i < FEAS2_TB; i++)
+          code[i] = staged ? s_code[(size_t)slot * T + tt[i]] : Cg.code[(size_t)k * T + tt[i]];
+#pragma unroll
+        for (int i = 0; i < FEAS2_TB; i++) {
+          const uint32_t c = code[i];
+          bool pass;
+          if (c == 0xFFFFu) pass = true;                   // type lacks the key
+          else if (c == 0xFFFEu) pass = (negQ >> k) & 1;   // type DoesNotExist: only NotIn/DNE intersect
+          else if (c == 0xFFFDu) pass = !alive[i] || (al_w[D.wofs[k]] & Cg.multi[(size_t)k * T + tt[i]]) != 0;
+          else pass = (al_w[c >> 6] >> (c & 63)) & 1;
+          alive[i] = alive[i] && pass;
+        }
+      }
+      // Fits on the requested resources
+      for (uint32_t rm = rmask; rm; rm &= rm - 1) {
+        const int r = __builtin_ctz(rm);
+        const int64_t need = lane_bcast_i64(rq_lane, r);
+        const bool staged = (lds_res >> r) & 1;
+        const int slot = __builtin_popcount(lds_res & ((1u << r) - 1));
+#pragma unroll
+        for (int i = 0; i < FEAS2_TB; i++) {
+          const int64_t al = staged ? s_alloc[(size_t)slot * T + tt[i]] : Cg.alloc[(size_t)r * T + tt[i]];
+          alive[i] = alive[i] && need <= al;
+        }
+      }
+      // cheapest compatible available offering: min over the row's classes
+      double ch[FEAS2_TB];
+#pragma unroll
+      for (int i = 0; i < FEAS2_TB; i++) ch[i] = __builtin_huge_val();
+      if (a.price_lds) {
+        for (uint64_t m = cls; m; m &= m - 1) {
+          const int c = __builtin_ctzll(m);
+#pragma unroll
+          for (int i = 0; i < FEAS2_TB; i++) {
+            const double p = s_price[(size_t)c * T + tt[i]];
+            ch[i] = p < ch[i] ? p : ch[i];
+          }
+        }
+      } else if (Cg.price_sub) {
+#pragma unroll
+        for (int i = 0; i < FEAS2_TB; i++) ch[i] = Cg.price_sub[(size_t)cls * T + tt[i]];
+      } else {
+        for (uint64_t m = cls; m; m &= m - 1) {
+          const int c = __builtin_ctzll(m);
+#pragma unroll
+          for (int i = 0; i < FEAS2_TB; i++) {
+            const double p = Cg.price_cm[(size_t)c * T + tt[i]];
+            ch[i] = p < ch[i] ? p : ch[i];
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < FEAS2_TB; i++) {
+        const uint64_t bal = __ballot(alive[i] && ch[i] < __builtin_huge_val());
+        if (lane == tile0 + i) myword = bal;
+        if (oc && valid[i]) oc[tt[i]] = ch[i];
+      }
+    }
+    if (lane < tiles) a.out_mask[(size_t)q * tiles + lane] = myword;
+    wave_sync();
+  }
+}
+const void* feasibility_lds_kernel_ptr() { return (const void*)feasibility_lds_kernel; }
+
 // ------------------------------------------------------------------------------------------------
 // launch_kernel: instance.DefaultProvider.Create's launch-side selection (R:pkg/providers/instance/instance.go:
 // 117-125, 242-270, 336-355, 392-439, 504-518), one wave per NodeClaim request. Lane = list entry: the
@@ -3393,6 +3551,11 @@ hipError_t launch_launch(const LaunchArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 hipError_t launch_feasibility(const FeasArgs& a, hipStream_t s) {
+  if (a.lds_bytes > 0) {
+    hipLaunchKernelGGL(feasibility_lds_kernel, dim3((unsigned)max(1, a.blocks)), dim3(FEAS2_WAVES * 64),
+                       (size_t)a.lds_bytes, s, a);
+    return hipGetLastError();
+  }
   long blocks = ((long)a.n_queries + FEAS_WAVES - 1) / FEAS_WAVES;
   if (blocks > FEAS_MAX_BLOCKS) blocks = FEAS_MAX_BLOCKS;
   if (blocks < 1) blocks = 1;

@@ -100,6 +100,28 @@ def random_subsets_csr(n_candidates, n_subsets, seed, max_size=100, min_size=2):
     return offs, picks[valid].astype(np.uint32)
 
 
+SWEEP_CHUNK = 1 << 16  # subsets per generation chunk of the config-4 sweep (chunk c uses seed 1000 + c)
+
+
+def sweep_subsets(candidates, n_subsets, chunk_lo=0, chunk_hi=None):
+    """The config-4 sweep's random candidate subsets (2..100 candidates each), chunks [chunk_lo, chunk_hi) of
+    SWEEP_CHUNK subsets concatenated into one CSR over cluster node indices; the set does not depend on how the
+    chunks are split over ranks. Returns (offsets, nodes, global index of the first subset)."""
+    cands = np.asarray(candidates, dtype=np.uint32)
+    n_chunks = (n_subsets + SWEEP_CHUNK - 1) // SWEEP_CHUNK
+    chunk_hi = n_chunks if chunk_hi is None else chunk_hi
+    offs_l, nodes_l, base = [], [], 0
+    for c in range(chunk_lo, chunk_hi):
+        n = min(SWEEP_CHUNK, n_subsets - c * SWEEP_CHUNK)
+        offs, pos = random_subsets_csr(len(cands), n, seed=1000 + c)
+        offs_l.append(offs[:-1] + base)
+        nodes_l.append(cands[pos])
+        base += int(offs[-1])
+    offs_l.append(np.array([base], dtype=np.uint32))
+    return (np.concatenate(offs_l).astype(np.uint32),
+            np.concatenate(nodes_l) if nodes_l else np.zeros(0, dtype=np.uint32), chunk_lo * SWEEP_CHUNK)
+
+
 def best_local(results, base_index=0):
     """(savings, global subset index) of the best non-no-op decision in this shard; (-inf, -1) if none."""
     dec = np.array([int(r.decision) for r in results], dtype=np.int32) if not isinstance(results, np.ndarray) else results["decision"]

@@ -1189,7 +1189,17 @@ struct NodeClaim {
   vector<int> pods;
   string hostname;
   vector<HostPort> hostPortUsage;
+  // max allocatable per resource over `options` (missing = 0): a checker-side shortcut, not part of the restated
+  // algorithm. If the merged requests exceed it on some resource, no option Fits, so filterInstanceTypesByRequirements
+  // returns nothing and NodeClaim.Add fails whatever the requirement checks say; the outcome is unchanged.
+  int64_t maxalloc[KP_NUM_RESOURCES] = {};
 };
+
+static void SetMaxAlloc(NodeClaim& n) {
+  for (int r = 0; r < KP_NUM_RESOURCES; r++) n.maxalloc[r] = INT64_MIN;
+  for (int t : n.options)
+    for (int r = 0; r < KP_NUM_RESOURCES; r++) n.maxalloc[r] = std::max(n.maxalloc[r], Get((*n.tmpl->catalog)[t].allocatable, r));
+}
 
 struct ExistingNode {
   int index;  // input index
@@ -1259,6 +1269,8 @@ struct Scheduler {
     counters.attempts++;
     if (!ToleratesAll(n.tmpl->taints, p.tolerations)) return false;
     if (HostPortsConflict(n.hostPortUsage, p.hostPorts)) return false;
+    for (auto& kv : p.requests)  // no remaining option can fit (see NodeClaim.maxalloc)
+      if (kv.second > 0 && Get(n.requests, kv.first) + kv.second > n.maxalloc[kv.first]) return false;
     Requirements ncr = n.reqs;
     if (!Compatible(ncr, p.reqs, true)) return false;
     AddAll(ncr, p.reqs);
@@ -1271,6 +1283,7 @@ struct Scheduler {
     if (!FilterInstanceTypes(*n.tmpl->catalog, n.options, ncr, requests, &remaining, &counters)) return false;
     n.pods.push_back(p.index);
     n.options = std::move(remaining);
+    SetMaxAlloc(n);
     n.requests = requests;
     n.reqs = std::move(ncr);
     n.hostPortUsage.insert(n.hostPortUsage.end(), p.hostPorts.begin(), p.hostPorts.end());
@@ -1336,6 +1349,7 @@ struct Scheduler {
       nc->reqs = t.reqs;
       Add(nc->reqs, NewRequirement(kLabelHostname, KP_OP_IN, {nc->hostname}, -1));
       nc->options = its;
+      SetMaxAlloc(*nc);
       nc->requests = t.daemon;
       if (!NodeClaimAdd(*nc, p)) {
         topology.Unregister(kLabelHostname, nc->hostname);  // NodeClaim.Destroy

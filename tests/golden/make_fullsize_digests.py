@@ -4,10 +4,13 @@
   config2-50000   Solve of config 2 at 50k pods: digest of the placement array and of the NodeClaims
                   (nodepool, pods in add order, options after OrderByPrice + Truncate, requirements)
   config3-100000  Solve of config 3 at 100k pods (zone + hostname spread onto 5k existing nodes): same digests
+  config5-100000  Solve of config 5 (20 weighted pools, GPU/Neuron pools) at 100k pods: 17.5k NodeClaims, so the
+                  device's newNodeClaims order spills past its 8,192-entry LDS capacity on its own
   config4-10000   computeConsolidation on the 10k-node config-4 cluster for every firstNConsolidationOption prefix
                   (candidates[0:mid+1], mid = 1..100) and 200 random subsets: every decision field
 
-Run from the repo root: python tests/golden/make_fullsize_digests.py  (about 6 minutes)
+Run from the repo root: python tests/golden/make_fullsize_digests.py [name ...]  (all: about 8 minutes); names given
+regenerate only those entries.
 """
 import hashlib
 import json
@@ -51,17 +54,30 @@ def sim_record(r):
             float(r["savings"]).hex(), int(r["n_options"]), int(r["n_pods"])]
 
 
+def _solves():
+    from kpamd import synth
+    return {"config2-50000": lambda cat: synth.config2(cat, n_pods=50_000, seed=2),
+            "config3-100000": lambda cat: synth.config3(cat, n_pods=100_000),
+            "config5-100000": lambda cat: synth.config5(cat, n_pods=100_000)}
+
+
 def main():
     import kpamd
     from kpamd import catalog, synth
     from oracle import pyoracle
     cat = catalog.build_catalog(kpamd.load_lib())
-    out = {}
-    for name, mk in (("config2-50000", lambda: synth.config2(cat, n_pods=50_000, seed=2)),
-                     ("config3-100000", lambda: synth.config3(cat, n_pods=100_000))):
+    SOLVES = {k: (lambda f: lambda: f(cat))(f) for k, f in _solves().items()}
+    only = set(sys.argv[1:])
+    out = json.load(open(OUT)) if os.path.exists(OUT) and only else {}
+    for name, mk in SOLVES.items():
+        if only and name not in only:
+            continue
         t = time.time()
         out[name] = solve_digest(pyoracle.solve(mk()))
         print(name, out[name], f"{time.time() - t:.1f}s", flush=True)
+    if only and "config4-10000" not in only:
+        json.dump(out, open(OUT, "w"), indent=0)
+        return
     t = time.time()
     cl = synth.config4(cat, n_nodes=10_000, seed=4)
     pre, rnd = config4_subsets(cl)

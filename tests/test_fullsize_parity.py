@@ -1,6 +1,7 @@
 """Device parity at BASELINE.json's full sizes, against oracle results committed as fixtures
 (tests/golden/fullsize_digests.json, generated in this container by tests/golden/make_fullsize_digests.py from the
 same generators and seeds): the headline config 2 at 50k pods, config 3 at 100k pods onto 5k existing nodes, and
+config 5 at 100k pods (17.5k NodeClaims: the newNodeClaims order spills past the device's LDS capacity by itself),
 config 4's 10k-node cluster on every firstNConsolidationOption prefix plus 200 random candidate subsets.
 
 The -m "not gpu" test checks the fixture is consistent with the generators (counts and shapes)."""
@@ -23,6 +24,7 @@ def digests():
 def test_fixture_shape(digests):
     assert digests["config2-50000"]["placed"] == 50_000
     assert digests["config3-100000"]["on_existing"] > 0
+    assert digests["config5-100000"]["nodeclaims"] > 2 * 8192, "past the device's LDS sort capacity without forcing it"
     c4 = digests["config4-10000"]
     assert len(c4["prefixes"]) == 100 and len(c4["random"]) == 200
     decisions = {r[0] for r in c4["random"]}
@@ -30,15 +32,16 @@ def test_fixture_shape(digests):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["config2-50000", "config3-100000"])
+@pytest.mark.parametrize("name", ["config2-50000", "config3-100000", "config5-100000"])
 def test_solve_fullsize(ctx, catalog, digests, name):
     import kpamd
     import make_fullsize_digests as mk
-    from kpamd import synth
-    prob = synth.config2(catalog, n_pods=50_000, seed=2) if name.startswith("config2") else \
-        synth.config3(catalog, n_pods=100_000)
-    got = mk.solve_digest(kpamd.Scheduler(ctx, prob).solve())
+    prob = mk._solves()[name](catalog)
+    res = kpamd.Scheduler(ctx, prob).solve()
+    got = mk.solve_digest(res)
     assert got == digests[name]
+    if name.startswith("config5"):
+        assert len(res["nodeclaims"]) > 8192
 
 
 @pytest.mark.gpu

@@ -155,3 +155,31 @@ def test_filter_plan_pod_rows(ctx, catalog):
         want_k, want_c = seen[key]
         assert (kept[qi] == want_k).all(), f"row {qi}"
         np.testing.assert_array_equal(cheapest[qi][want_k], want_c[want_k])
+
+
+def test_feasibility_lds_staged_equals_global(ctx, catalog, monkeypatch):
+    """feasibility_lds_kernel (catalogue columns staged in LDS) == feasibility_kernel (global gathers, KP_FEAS_GLOBAL)
+    bit for bit on pairwise-distinct rows (the bench's roofline leg: Gt/Lt bounds, NotIn, zones, capacity types), and
+    both == the oracle on a sample of rows."""
+    import kpamd
+    from kpamd import synth
+    from oracle import pyoracle
+    queries = synth.distinct_queries(catalog, 3000)
+    cat = kpamd.Catalog(ctx, catalog)
+    try:
+        fp = kpamd.FilterPlan(ctx, cat, queries, cheapest=True)
+        k1, c1, _ = fp.run(read=True)
+        fp.close()
+        monkeypatch.setenv("KP_FEAS_GLOBAL", "1")
+        fp = kpamd.FilterPlan(ctx, cat, queries, cheapest=True)
+        k2, c2, _ = fp.run(read=True)
+        fp.close()
+    finally:
+        cat.close()
+    assert (k1 == k2).all()
+    np.testing.assert_array_equal(c1, c2)
+    assert k1.any() and not k1.all()
+    for qi in range(0, len(queries), 97):
+        want_k, want_c = pyoracle.compatible_available_filter(catalog, *queries[qi])
+        assert (k1[qi] == want_k).all(), f"row {qi}"
+        np.testing.assert_array_equal(c1[qi][want_k], want_c[want_k])

@@ -77,7 +77,8 @@ def test_argmin_two_ranks_one_process(ctx2, catalog):
     from kpamd import synth
     cl = synth.config4(catalog, n_nodes=150, seed=4)
     subs = synth.consolidation_subsets(cl, 400, seed=6)
-    halves = [(0, 230), (230, 400)]
+    n = len(subs)
+    halves = [(0, n * 3 // 5), (n * 3 // 5, n)]
     ag = kpamd.ThreadAllGather(2)
     comms = [kpamd.Comm.host(ctx2[r], 2, r, ag) for r in range(2)]
     plans = [kpamd.ClusterPlan(ctx2[r], cl) for r in range(2)]

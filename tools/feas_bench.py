@@ -1,0 +1,33 @@
+"""Feasibility leg probe: median device time of kp_filter_run over pairwise-distinct rows (the bench's roofline leg),
+per variant given on the command line as NAME=ENV1=V1,ENV2=V2 (plans are prepared after setting the env)."""
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "karpenter-provider-aws_amd"))
+import kpamd  # noqa: E402
+from kpamd import catalog, synth  # noqa: E402
+
+rows = int(os.environ.get("FEAS_ROWS", "50000"))
+lib = kpamd.load_lib()
+cat = catalog.build_catalog(lib)
+ctx = kpamd.Context(0)
+ch = kpamd.Catalog(ctx, cat)
+qs = synth.distinct_queries(cat, rows)
+out = {}
+KNOBS = ("KP_FEAS_GLOBAL", "KP_FEAS_NO_KEYS", "KP_FEAS_NO_RES", "KP_FEAS_NO_PRICE", "KP_FEAS_BLOCKS")
+for spec in sys.argv[1:] or ["lds"]:
+    name, _, envs = spec.partition("=")
+    for k in KNOBS:
+        os.environ.pop(k, None)
+    for kv in filter(None, envs.split(",")):
+        k, _, v = kv.partition("=")
+        os.environ[k] = v
+    for cheapest in (True, False):
+        fp = kpamd.FilterPlan(ctx, ch, qs, cheapest=cheapest)
+        fp.run()
+        ms = sorted(fp.run()["device_ms"] for _ in range(int(os.environ.get("FEAS_REPS", "10"))))
+        fp.close()
+        out[f"{name}{'' if cheapest else '_nocheapest'}"] = round(ms[len(ms) // 2], 4)
+print(json.dumps(out), flush=True)
