@@ -364,8 +364,10 @@ typedef struct kp_solve_stats {
                                  Fits, offerings, minValues; [5] = attempts timed) */
   double catalog_ms;        /* part of prepare_ms spent compiling the catalogue half (dictionary, catalogue SoA,
                                NodeClaimTemplates); 0 when it came resident from the kp_ctx cache */
-  uint32_t catalog_cached;  /* 1: the catalogue half was resident (same catalogues + seqnums + NodePools) */
-  uint32_t reserved_;
+  uint32_t catalog_cached;  /* 1: the catalogue half was resident (same catalogues + NodePools; seqnums equal, or
+                               re-applied in place: catalog_refreshed) */
+  uint32_t catalog_refreshed; /* 1: the catalogues' seqnums had changed (ICE marks, prices) and the resident half's
+                                 offerings and template options were re-applied in place, not recompiled */
   uint64_t fast_pods;       /* pods placed by solve_kernel's single-wave fast lane (no requirement merge) */
   uint64_t fast_cycles[6];  /* diagnostic (KP_TIMING=1): fast-lane cycles: pop, stage, sort, pre-pass, attempts, commit */
   uint64_t slow_sorts;      /* sort.Slice replays that ran the literal pdqsort (no stable-move shortcut) */
@@ -600,6 +602,13 @@ int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out
 struct kp_comm;
 int32_t kp_solve_prepare_comm(kp_ctx* ctx, const kp_solve_in* in, struct kp_comm* comm, kp_solve_plan** out);
 int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out);
+/* A prepared plan after kp_catalog_update_offerings (UnavailableOfferings.MarkUnavailable + SeqNum,
+ * R:pkg/cache/unavailableofferings.go:66-92): re-applies the catalogues' current availability and prices to the
+ * resident catalogue half (offering masks, class prices and subset minima, the NodeClaimTemplates' options) and the
+ * plan's template-options table, in place. kp_solve_run refuses a plan whose catalogues changed until this ran.
+ * KP_E_INVAL when the update changed which NodePools keep any instance type (prepare again). A new kp_solve on the
+ * same catalogues does the same on its own (stats.catalog_refreshed). */
+int32_t kp_solve_refresh(kp_solve_plan* plan);
 void kp_solve_plan_destroy(kp_solve_plan* plan);
 uint32_t kp_result_nodeclaim_count(const kp_solve_result* res);
 /* out[p] for every input pod: >= 0 new NodeClaim index; -1 pod error; <= -2 existing node -(2+i) */
@@ -673,6 +682,10 @@ typedef struct kp_cluster_plan kp_cluster_plan;
 int32_t kp_cluster_prepare(kp_ctx* ctx, const kp_cluster* cluster, kp_cluster_plan** out);
 int32_t kp_cluster_simulate(kp_cluster_plan* plan, const uint32_t* offsets, const uint32_t* nodes, uint32_t n_subsets,
                             int32_t multi_node, kp_sim_result* out, kp_solve_stats* stats);
+/* kp_solve_refresh for a cluster snapshot: after kp_catalog_update_offerings the catalogues' availability and
+ * prices, the templates' options and the candidates' prices are re-applied in place and the per shape-level template
+ * outcomes recomputed; kp_cluster_simulate / kp_consolidate_argmin refuse the plan until then. */
+int32_t kp_cluster_refresh(kp_cluster_plan* plan);
 void kp_cluster_plan_destroy(kp_cluster_plan* plan);
 
 /* ---- Multi-GPU consolidation: RCCL over xGMI -----------------------------------------------------------------

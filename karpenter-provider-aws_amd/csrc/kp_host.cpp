@@ -1115,6 +1115,11 @@ struct TaintT {
 // kp_ctx across Solves, keyed by that fingerprint (R:pkg/providers/instancetype/instancetype.go:225-237 cacheKey:
 // the reference likewise rebuilds its InstanceType list only when a seqnum changes). A Solve whose pods or nodes
 // name a label key or value the dictionary lacks triggers a rebuild that adds them (the dictionary only grows).
+// Device offsets of one catalogue's arrays inside an upload blob.
+struct CatOffsets {
+  size_t TM, DNE, NOKEY, alloc, cap, nonneg, fit_vals, fit_n, fit_mask, cls, offer, price, price_cm, price_sub, rank, code, multi, custom;
+};
+
 struct SolveBase {
   Dict d;
   int TW = 1, C = 0;
@@ -1128,17 +1133,29 @@ struct SolveBase {
   vector<int64_t> tmpl_daemon;
   vector<vector<TaintT>> tsets;       // the NodePools' taint sets in id order
   vector<int> np_taintset;            // per input NodePool
-  string key;                         // cache fingerprint
+  // the NodePools as the templates need them (input order; np_order = weight desc, name asc), so that an ICE update
+  // can rebuild the templates' options without the caller's kp_solve_in
+  vector<KReqs> np_q;
+  vector<int32_t> np_catalog;
+  vector<int> np_order;
+  vector<int64_t> np_daemon;          // [n_nodepools][NRES]
+  vector<const kp_catalog*> catalogs; // the catalogues compiled in (caller-owned, they outlive every plan on them)
+  vector<uint64_t> seqnums;           // their seqnums the offering arrays reflect
+  string ident;                       // cache fingerprint without the seqnums
+  string key;                         // cache fingerprint: ident + seqnums
+  uint64_t version = 0;               // bumped by every in-place offering refresh (RefreshOfferings)
   // device copy (Solve plans): dict, parsed integers, catalogue SoA + descriptors, templates
   DevBuf dev;
   bool on_device = false;
   size_t o_dict = 0, o_vint = 0, o_cats = 0, o_treqs = 0, o_tts = 0, o_tcat = 0, o_tX = 0, o_tdm = 0;
+  vector<CatOffsets> coffs;
   double build_ms = 0;
 };
 
 struct Compiled {
   std::shared_ptr<SolveBase> B = std::make_shared<SolveBase>();
   bool base_hit = false;              // the base came from the ctx cache
+  bool base_refreshed = false;        // ... after an in-place offering refresh (a new catalogue seqnum)
   vector<uint32_t> tmpl_limit_present;
   vector<int64_t> tmpl_remaining;
   // shapes
@@ -1776,12 +1793,23 @@ void KeyReqs(string& o, const RawReqs& rs) {
   o += '\x04';
 }
 
-// Fingerprint of everything a SolveBase depends on: catalogue identities + seqnums, the NodePools.
-string BaseKey(const kp_solve_in* in, const SolveRaw& raw) {
+// The catalogues' seqnums as they are now, and that part of a cache fingerprint.
+vector<uint64_t> SeqnumsOf(const vector<const kp_catalog*>& cats) {
+  vector<uint64_t> v;
+  for (auto* c : cats) v.push_back(c->seqnum);
+  return v;
+}
+string SeqKey(const vector<uint64_t>& seqs) {
+  string k = "#";
+  for (uint64_t q : seqs) k += std::to_string(q) + ";";
+  return k;
+}
+// Fingerprint of everything a SolveBase depends on but the seqnums: catalogue identities, the NodePools.
+string BaseIdent(const kp_solve_in* in, const SolveRaw& raw) {
   string k;
   for (uint32_t c = 0; c < in->n_catalogs; c++) {
     const kp_catalog* cat = in->catalogs[c];
-    k += std::to_string(cat->uid) + ":" + std::to_string(cat->seqnum) + ":" + std::to_string(cat->types.size()) + ";";
+    k += std::to_string(cat->uid) + ":" + std::to_string(cat->types.size()) + ";";
   }
   for (uint32_t i = 0; i < in->n_nodepools; i++) {
     const kp_nodepool& np = in->nodepools[i];
@@ -1935,6 +1963,40 @@ int32_t ParseSolve(const kp_solve_in* in, SolveRaw& raw) {
 }
 
 // Dictionary (catalogues, NodePools + the values `raw` names), catalogue SoA, offering classes, templates.
+// The NodeClaimTemplates' InstanceTypeOptions (upstream NewScheduler's pre-filter: the pool's requirements, empty
+// requests, a compatible available offering, minValues); pools that keep no type are skipped. Depends on the
+// offerings' availability, so an ICE update re-runs it (RefreshOfferings).
+void BuildTemplates(const SolveBase& b, vector<int>& tnp, vector<uint64_t>& tX) {
+  const Dict& d = b.d;
+  const int TW = b.TW;
+  tnp.clear();
+  tX.clear();
+  for (int i : b.np_order) {
+    const KReqs& q = b.np_q[i];
+    const HostCat& hc = b.cats[b.np_catalog[i]];
+    vector<uint64_t> X(TW, 0);
+    for (int t = 0; t < hc.T; t++) X[t / 64] |= 1ull << (t % 64);
+    int64_t zero[KP_NRES] = {0};
+    HostFilterTypes(d, hc, q, TW, zero, X);
+    const uint64_t cls = HostAllowedClasses(d, q, b.classes);
+    vector<uint64_t> offer(TW, 0);
+    for (int c = 0; c < b.C; c++)
+      if ((cls >> c) & 1)
+        for (int w = 0; w < TW; w++) offer[w] |= hc.offer_avail[(size_t)c * TW + w];
+    bool any = false;
+    for (int w = 0; w < TW; w++) any |= (X[w] &= offer[w]) != 0;
+    if (any && q.hmin) {
+      vector<int> ts;
+      for (int t = 0; t < hc.T; t++)
+        if ((X[t / 64] >> (t % 64)) & 1) ts.push_back(t);
+      if (!HostMinValuesOK(d, hc, q, ts)) any = false;
+    }
+    if (!any) continue;  // "skipping, nodepool requirements filtered out all instance types"
+    tnp.push_back(i);
+    tX.insert(tX.end(), X.begin(), X.end());
+  }
+}
+
 int32_t BuildBase(const kp_solve_in* in, const SolveRaw& raw, SolveBase& b) {
   auto t0 = std::chrono::steady_clock::now();
   vector<const kp_catalog*> cats(in->catalogs, in->catalogs + in->n_catalogs);
@@ -2022,35 +2084,23 @@ int32_t BuildBase(const kp_solve_in* in, const SolveRaw& raw, SolveBase& b) {
     if (p.weight != q.weight) return p.weight > q.weight;
     return strcmp(p.name ? p.name : "", q.name ? q.name : "") < 0;
   });
-  for (int i : order) {
+  b.np_order = order;
+  for (uint32_t i = 0; i < in->n_nodepools; i++) {
     const kp_nodepool& np = in->nodepools[i];
-    KReqs q = Compile(d, raw.np_reqs[i]);
-    const HostCat& hc = b.cats[np.catalog];
-    vector<uint64_t> X(TW, 0);
-    for (int t = 0; t < hc.T; t++) X[t / 64] |= 1ull << (t % 64);
-    int64_t zero[KP_NRES] = {0};
-    HostFilterTypes(d, hc, q, TW, zero, X);
-    const uint64_t cls = HostAllowedClasses(d, q, b.classes);
-    vector<uint64_t> offer(TW, 0);
-    for (int c = 0; c < b.C; c++)
-      if ((cls >> c) & 1)
-        for (int w = 0; w < TW; w++) offer[w] |= hc.offer_avail[(size_t)c * TW + w];
-    bool any = false;
-    for (int w = 0; w < TW; w++) any |= (X[w] &= offer[w]) != 0;
-    if (any && q.hmin) {
-      vector<int> ts;
-      for (int t = 0; t < hc.T; t++)
-        if ((X[t / 64] >> (t % 64)) & 1) ts.push_back(t);
-      if (!HostMinValuesOK(d, hc, q, ts)) any = false;
-    }
-    if (!any) continue;  // "skipping, nodepool requirements filtered out all instance types"
-    b.tmpl_nodepool.push_back(i);
-    b.tmpl_reqs.push_back(q);
-    b.tmpl_taintset.push_back(b.np_taintset[i]);
-    b.tmpl_catalog.push_back((int32_t)np.catalog);
-    b.tmpl_X.insert(b.tmpl_X.end(), X.begin(), X.end());
+    b.np_q.push_back(Compile(d, raw.np_reqs[i]));
+    b.np_catalog.push_back((int32_t)np.catalog);
     for (int r = 0; r < KP_NRES; r++)
-      b.tmpl_daemon.push_back((np.daemon_requests.present >> r) & 1 ? np.daemon_requests.milli[r] : 0);
+      b.np_daemon.push_back((np.daemon_requests.present >> r) & 1 ? np.daemon_requests.milli[r] : 0);
+  }
+  b.catalogs = cats;
+  b.seqnums = SeqnumsOf(cats);
+  BuildTemplates(b, b.tmpl_nodepool, b.tmpl_X);
+  for (int i : b.tmpl_nodepool) {
+    b.tmpl_reqs.push_back(b.np_q[i]);
+    b.tmpl_taintset.push_back(b.np_taintset[i]);
+    b.tmpl_catalog.push_back(b.np_catalog[i]);
+    b.tmpl_daemon.insert(b.tmpl_daemon.end(), b.np_daemon.begin() + (size_t)i * KP_NRES,
+                         b.np_daemon.begin() + (size_t)(i + 1) * KP_NRES);
   }
   b.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return KP_OK;
@@ -2212,32 +2262,99 @@ int32_t CompilePerCall(const kp_solve_in* in, const SolveRaw& raw, Compiled& cp)
   return KP_OK;
 }
 
+// An ICE update (kp_catalog_update_offerings: availability, prices; never new offering classes) re-applied to a
+// SolveBase in place: the offering arrays of every catalogue (FillOfferings with the base's class ids) and the
+// templates' options (BuildTemplates), host side, then the same regions of the resident device copy. Returns 0 when
+// done (version bumped), 1 when the base must be rebuilt instead (an offering of an unknown class, or the set of
+// templates changed: a NodePool whose types all became unavailable, or the reverse), < 0 on a device error.
+// Plans prepared on the base before the refresh see it through `version` (kp_solve_run refuses them until
+// kp_solve_refresh).
+int32_t RefreshOfferings(kp_ctx* ctx, SolveBase& b) {
+  map<ClassKey, int> classes;
+  for (int c = 0; c < b.C; c++) classes[KeyOfClass(b.classes[c])] = c;
+  for (auto* cat : b.catalogs)
+    for (auto& t : cat->types)
+      for (auto& o : t.offs)
+        if (!classes.count(ClassOf(b.d, o))) return 1;
+  vector<HostCat> saved;
+  for (size_t i = 0; i < b.cats.size(); i++) {
+    saved.push_back(HostCat());
+    saved.back().offer_avail.swap(b.cats[i].offer_avail);
+    saved.back().price.swap(b.cats[i].price);
+    saved.back().price_cm.swap(b.cats[i].price_cm);
+    saved.back().price_sub.swap(b.cats[i].price_sub);
+    FillOfferings(b.d, b.catalogs[i]->types, b.TW, classes, b.cats[i]);
+  }
+  vector<int> tnp;
+  vector<uint64_t> tX;
+  BuildTemplates(b, tnp, tX);
+  if (tnp != b.tmpl_nodepool) {  // restore: the caller rebuilds a fresh base (other plans may share this one)
+    for (size_t i = 0; i < b.cats.size(); i++) {
+      b.cats[i].offer_avail.swap(saved[i].offer_avail);
+      b.cats[i].price.swap(saved[i].price);
+      b.cats[i].price_cm.swap(saved[i].price_cm);
+      b.cats[i].price_sub.swap(saved[i].price_sub);
+    }
+    return 1;
+  }
+  b.tmpl_X.swap(tX);
+  b.seqnums = SeqnumsOf(b.catalogs);
+  b.key = b.ident + SeqKey(b.seqnums);
+  b.version++;
+  if (b.on_device && ctx) {
+    uint8_t* base = (uint8_t*)b.dev.p;
+    hipStream_t st = ctx->stream;
+    for (size_t i = 0; i < b.cats.size(); i++) {
+      const HostCat& hc = b.cats[i];
+      const CatOffsets& o = b.coffs[i];
+      HIPCHK(hipMemcpyAsync(base + o.offer, hc.offer_avail.data(), hc.offer_avail.size() * 8, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(base + o.price, hc.price.data(), hc.price.size() * 8, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(base + o.price_cm, hc.price_cm.data(), hc.price_cm.size() * 8, hipMemcpyHostToDevice, st));
+      if (!hc.price_sub.empty())
+        HIPCHK(hipMemcpyAsync(base + o.price_sub, hc.price_sub.data(), hc.price_sub.size() * 8, hipMemcpyHostToDevice, st));
+    }
+    HIPCHK(hipMemcpyAsync(base + b.o_tX, b.tmpl_X.data(), b.tmpl_X.size() * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
+  return 0;
+}
+
 // Compile a Solve. With a ctx, the SolveBase comes from (and goes to) the ctx cache when its fingerprint matches
 // and its dictionary covers the batch; without one (kp_solve_validate) it is always built.
 int32_t CompileSolve(const kp_solve_in* in, Compiled& cp, kp_ctx* cache = nullptr) {
   SolveRaw raw;
   int32_t rc = ParseSolve(in, raw);
   if (rc) return rc;
-  const string key = BaseKey(in, raw);
+  const string ident = BaseIdent(in, raw);
+  const string key = ident + SeqKey(SeqnumsOf(vector<const kp_catalog*>(in->catalogs, in->catalogs + in->n_catalogs)));
   if (cache) {
-    for (size_t i = 0; i < cache->bases.size(); i++) {
-      auto& b = cache->bases[i];
-      if (b->key != key || !BaseCovers(*b, raw)) continue;
-      cp.B = b;
-      cp.base_hit = true;
-      rc = CompilePerCall(in, raw, cp);
-      if (rc == KP_OK) {
-        std::rotate(cache->bases.begin() + i, cache->bases.begin() + i + 1, cache->bases.end());  // most recent last
-        cache->base_hits++;
-        return KP_OK;
+    for (int pass = 0; pass < 2; pass++)  // the exact fingerprint; then one whose catalogues only changed seqnum
+      for (size_t i = 0; i < cache->bases.size(); i++) {
+        auto& b = cache->bases[i];
+        if ((pass == 0 ? b->key != key : b->ident != ident) || !BaseCovers(*b, raw)) continue;
+        if (pass == 1) {  // an ICE update: re-apply the offerings in place (host + device) instead of a rebuild
+          rc = RefreshOfferings(cache, *b);
+          if (rc < 0) return rc;
+          if (rc > 0) break;  // the templates changed: rebuild
+          cp.base_refreshed = true;
+        }
+        cp.B = b;
+        cp.base_hit = true;
+        rc = CompilePerCall(in, raw, cp);
+        if (rc == KP_OK) {
+          std::rotate(cache->bases.begin() + i, cache->bases.begin() + i + 1, cache->bases.end());  // most recent last
+          cache->base_hits++;
+          return KP_OK;
+        }
+        if (rc != KP_E_UNSUPPORTED) return rc;
+        pass = 2;  // the cached dictionary's extra values may exceed a per-key limit: rebuild for this batch alone
+        break;
       }
-      if (rc != KP_E_UNSUPPORTED) return rc;
-      break;  // the cached dictionary's extra values may exceed a per-key limit: rebuild for this batch alone
-    }
   }
   Compiled fresh;
   rc = BuildBase(in, raw, *fresh.B);
   if (rc) return rc;
+  fresh.B->ident = ident;
   fresh.B->key = key;
   rc = CompilePerCall(in, raw, fresh);
   if (rc) return rc;
@@ -2257,9 +2374,6 @@ int32_t CompileSolve(const kp_solve_in* in, Compiled& cp, kp_ctx* cache = nullpt
 }
 
 // Lays out dict + catalogues in `blob`; fills `catoffs` with the device DevCatalog array offset.
-struct CatOffsets {
-  size_t TM, DNE, NOKEY, alloc, cap, nonneg, fit_vals, fit_n, fit_mask, cls, offer, price, price_cm, price_sub, rank, code, multi, custom;
-};
 
 void PutCatalogs(Blob& blob, const Compiled& cp, vector<CatOffsets>& offs) {
   for (auto& hc : cp.B->cats) {
@@ -2399,6 +2513,9 @@ struct kp_solve_plan {
   uint32_t max_types = 0;
   bool any_min = false;
   double prepare_ms = 0;
+  uint64_t base_version = 0;  // SolveBase::version the plan's derived data (template-options table) reflects
+  TfeasArgs tf;               // the table's launch over every row (kp_solve_refresh recomputes it locally)
+  bool tfeas_on = false;
 };
 
 extern "C" {
@@ -2416,6 +2533,7 @@ static int32_t EnsureBaseOnDevice(kp_ctx* ctx, SolveBase& B) {
   B.o_vint = blob.put(B.d.vint);
   vector<CatOffsets> coffs;
   PutCatalogs(blob, view, coffs);
+  B.coffs = coffs;
   B.o_cats = blob.reserve(sizeof(DevCatalog) * coffs.size());
   B.o_treqs = blob.put(B.tmpl_reqs);
   B.o_tts = blob.put(B.tmpl_taintset);
@@ -2764,6 +2882,10 @@ static int32_t SolvePrepareLocal(kp_ctx* ctx, const kp_solve_in* in, kp_comm* co
     f.row_hi = std::min(SLi, (my_rank + 1) * rows_per_rank);
     f.words = tf_words;
     f.out = (uint64_t*)(base + o_tfeas);
+    plan->tf = f;
+    plan->tf.row_lo = 0;
+    plan->tf.row_hi = SLi;
+    plan->tfeas_on = true;
     HIPCHK(launch_tmpl_feas(f, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     if (shard) {  // the all-gather of every rank's rows follows in SolvePrepare, after the ranks' status exchange
@@ -2792,6 +2914,35 @@ static int32_t SolvePrepareLocal(kp_ctx* ctx, const kp_solve_in* in, kp_comm* co
   plan->o_nopt = o_nopt;
   plan->o_ncr = o_ncr;
   plan->opt_stride = opt_stride;
+  plan->base_version = C.B->version;
+  return KP_OK;
+}
+
+// kp_solve_run on a plan whose catalogues changed since its data was derived would place pods on stale offerings
+static int32_t SolvePlanStale(const kp_solve_plan* plan) {
+  const SolveBase& B = *plan->cp->B;
+  if (plan->base_version != B.version || SeqnumsOf(B.catalogs) != B.seqnums)
+    return fail(KP_E_INVAL, "stale plan: a catalogue's seqnum changed since it was prepared (kp_solve_refresh)");
+  return KP_OK;
+}
+
+int32_t kp_solve_refresh(kp_solve_plan* plan) {
+  if (!plan) return fail(KP_E_INVAL, "null argument");
+  kp_ctx* ctx = plan->ctx;
+  std::lock_guard<std::recursive_mutex> lock(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device));
+  SolveBase& B = *plan->cp->B;
+  if (SeqnumsOf(B.catalogs) != B.seqnums) {
+    int32_t rc = RefreshOfferings(ctx, B);
+    if (rc < 0) return rc;
+    if (rc > 0)
+      return fail(KP_E_INVAL, "the offering update changed which NodePools keep instance types: prepare the Solve again");
+  }
+  if (plan->base_version != B.version && plan->tfeas_on) {  // the table derives from the templates' options
+    HIPCHK(launch_tmpl_feas(plan->tf, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+  }
+  plan->base_version = B.version;
   return KP_OK;
 }
 
@@ -2816,6 +2967,7 @@ int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out) {
   if (!plan || !out) return fail(KP_E_INVAL, "null argument");
   kp_ctx* ctx = plan->ctx;
   std::lock_guard<std::recursive_mutex> lock(ctx->mu);
+  if (int32_t rc = SolvePlanStale(plan)) return rc;
   HIPCHK(hipSetDevice(ctx->device));
   const Compiled& C = *plan->cp;
   const Dict& d = C.B->d;
@@ -2930,6 +3082,7 @@ int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out) {
   res->stats.prepare_ms = plan->prepare_ms;
   res->stats.catalog_ms = plan->catalog_ms;
   res->stats.catalog_cached = plan->cp->base_hit ? 1 : 0;
+  res->stats.catalog_refreshed = plan->cp->base_refreshed ? 1 : 0;
   for (int i = 0; i < 8; i++) res->stats.phase_cycles[i] = stats[8 + i];
   res->stats.scanned = stats[5];
   res->stats.cursor_starts = stats[6];
@@ -3711,6 +3864,15 @@ struct kp_cluster_plan {
   vector<uint8_t> deleting;         // [N] MarkedForDeletion
   int n_base = 0;                   // pending + deleting-node pods in every simulation
   double prepare_ms = 0;
+  // kp_cluster_refresh: where the offering-dependent parts live in the snapshot, and what they derive from
+  vector<CatOffsets> coffs;
+  size_t o_tX = 0, o_nprice = 0, o_nflags = 0;
+  struct NodeOffer {
+    uint32_t cat, type;
+    std::map<string, string> labels;  // the capacity-type / zone / zone-id labels (NodeCandidatePrice)
+  };
+  vector<NodeOffer> node_offer;
+  vector<uint8_t> node_flags;
 };
 
 namespace {
@@ -3876,6 +4038,12 @@ int32_t kp_cluster_prepare(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan** 
     auto ct = labels.find(kCapType);
     node_flags[i] = (priced ? 1 : 0) | (ct != labels.end() && ct->second == "spot" ? 2 : 0);
     node_name[i] = name_id(ht.name);
+    kp_cluster_plan::NodeOffer no{n.catalog, n.instance_type, {}};
+    for (const char* k : {kCapType, kZone, kZoneID}) {
+      auto f = labels.find(k);
+      if (f != labels.end()) no.labels[k] = f->second;
+    }
+    plan->node_offer.push_back(std::move(no));
   }
   if (node_pods.empty()) node_pods.push_back(0);
   // pods every simulation schedules besides those of S (SimulateScheduling: pending pods and the pods of nodes
@@ -4042,10 +4210,54 @@ int32_t kp_cluster_prepare(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan** 
   int ncu = 0;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device) == hipSuccess && ncu > 0)
     plan->n_cu = ncu;
+  plan->coffs = coffs;
+  plan->o_tX = o_tX;
+  plan->o_nprice = o_nprice;
+  plan->o_nflags = o_nflags;
+  plan->node_flags = node_flags;
   HIPCHK(launch_sim_prep(a, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
   plan->prepare_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   *out = plan.release();
+  return KP_OK;
+}
+
+// ICE refresh of a resident snapshot (kp_cluster_refresh, see kp_solve_refresh): the catalogues' offering arrays,
+// the templates' options, the candidates' prices, then sim_prep_kernel again (its per shape-level template
+// outcomes read the options and prices). A general-path plan compiles every simulation from the live catalogues.
+int32_t kp_cluster_refresh(kp_cluster_plan* plan) {
+  if (!plan) return fail(KP_E_INVAL, "null argument");
+  if (plan->general) return KP_OK;
+  kp_ctx* ctx = plan->ctx;
+  std::lock_guard<std::recursive_mutex> lock(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device));
+  SolveBase& B = *plan->cp->B;
+  if (SeqnumsOf(B.catalogs) == B.seqnums) return KP_OK;
+  int32_t rc = RefreshOfferings(nullptr, B);  // host side; the snapshot's own device copy is written below
+  if (rc < 0) return rc;
+  if (rc > 0) return fail(KP_E_INVAL, "the offering update changed which NodePools keep instance types: prepare again");
+  uint8_t* base = (uint8_t*)plan->buf.p;
+  hipStream_t st = ctx->stream;
+  for (size_t i = 0; i < B.cats.size(); i++) {
+    const HostCat& hc = B.cats[i];
+    const CatOffsets& o = plan->coffs[i];
+    HIPCHK(hipMemcpyAsync(base + o.offer, hc.offer_avail.data(), hc.offer_avail.size() * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(base + o.price, hc.price.data(), hc.price.size() * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(base + o.price_cm, hc.price_cm.data(), hc.price_cm.size() * 8, hipMemcpyHostToDevice, st));
+    if (!hc.price_sub.empty())
+      HIPCHK(hipMemcpyAsync(base + o.price_sub, hc.price_sub.data(), hc.price_sub.size() * 8, hipMemcpyHostToDevice, st));
+  }
+  HIPCHK(hipMemcpyAsync(base + plan->o_tX, B.tmpl_X.data(), B.tmpl_X.size() * 8, hipMemcpyHostToDevice, st));
+  vector<double> price(std::max<size_t>(plan->node_offer.size(), 1), 0);
+  for (size_t i = 0; i < plan->node_offer.size(); i++) {
+    const auto& no = plan->node_offer[i];
+    const bool priced = NodeCandidatePrice(B.catalogs[no.cat]->types[no.type], no.labels, &price[i]);
+    plan->node_flags[i] = (uint8_t)((plan->node_flags[i] & ~1) | (priced ? 1 : 0));
+  }
+  HIPCHK(hipMemcpyAsync(base + plan->o_nprice, price.data(), price.size() * 8, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(base + plan->o_nflags, plan->node_flags.data(), plan->node_flags.size(), hipMemcpyHostToDevice, st));
+  HIPCHK(launch_sim_prep(plan->a, st));
+  HIPCHK(hipStreamSynchronize(st));
   return KP_OK;
 }
 
@@ -4283,6 +4495,8 @@ static int32_t SimLaunchLocked(kp_cluster_plan* plan, const uint32_t* offsets, c
                                int32_t multi_node, SimArgs& a_out) {
   kp_ctx* ctx = plan->ctx;
   if (plan->general) return GeneralSimLocked(plan, offsets, nodes, n_subsets, multi_node, a_out);
+  if (SeqnumsOf(plan->cp->B->catalogs) != plan->cp->B->seqnums)
+    return fail(KP_E_INVAL, "stale plan: a catalogue's seqnum changed since it was prepared (kp_cluster_refresh)");
   if (offsets[0] != 0) return fail(KP_E_INVAL, "offsets[0] != 0");
   const uint32_t n_flat = offsets[n_subsets];
   if (n_flat && !nodes) return fail(KP_E_INVAL, "null nodes");

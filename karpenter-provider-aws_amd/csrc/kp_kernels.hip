@@ -2886,15 +2886,22 @@ __global__ __launch_bounds__(FEAS_WAVES * 64) void feasibility_kernel(FeasArgs a
 // workgroup of 16 waves per CU copies the single-value codes of the keys the rows name, the allocatable of the
 // resources they request and the class-major prices into LDS (~120 KB at T = 919), once; then every (row, type) test
 // is LDS reads + ALU, and the kernel streams what HBM must carry: each row's requirements in, its mask words and
-// one f64 cheapest price per type out. Per row the wave decodes the requirement set once (allowed value words in
-// LDS, compatible offering classes), then walks the types two 64-type tiles at a time (independent LDS reads in
-// flight), ballot -> mask word (kept in lane `tile` and stored coalesced at the end of the row).
+// one f64 cheapest price per type out.
+// Per row the wave decodes the requirement set once into its allowed-value words in LDS, plus two sentinel words:
+// word 64 = all ones (the code of "type lacks the key") and word 65 = the row's NotIn/DoesNotExist keys (the code
+// of "type has the key DoesNotExist" is 65 * 64 + k, remapped at staging), so that for a single-valued key one
+// ds_read of the code and one of the allowed word decide a type, branch-free. Loops run key-outer / tile-inner:
+// a lane keeps its types' verdicts as one bit per 64-type tile, the tile loop's LDS reads are independent (in
+// flight together), and the scalar key walk is paid once per key instead of once per tile.
 #define FEAS2_WAVES 16
-#define FEAS2_TB 2  // tiles per step
+#define FEAS2_AW 68  // allowed words per wave: 64 value words + the two sentinel words (+ pad)
+#define FEAS2_CODE_NOKEY (64 * 64)
+#define FEAS2_CODE_DNE (65 * 64)
 __global__ __launch_bounds__(FEAS2_WAVES * 64) void feasibility_lds_kernel(FeasArgs a) {
   __shared__ DevDict D;
-  __shared__ uint64_t s_allowed[FEAS2_WAVES][KP_MAX_WORDS];
+  __shared__ uint64_t s_allowed[FEAS2_WAVES][FEAS2_AW];
   __shared__ int64_t s_vint[KP_MAX_BOUND_KEYS * 64];
+  __shared__ OfferClass s_cls[KP_MAX_CLASSES];
   extern __shared__ __attribute__((aligned(16))) uint64_t s_cat2[];
   block_copy(D, a.dict);
   __syncthreads();
@@ -2919,16 +2926,22 @@ __global__ __launch_bounds__(FEAS2_WAVES * 64) void feasibility_lds_kernel(FeasA
     }
     s = 0;
     for (uint64_t km = lds_keys; km; km &= km - 1, s++) {
-      const uint16_t* src = Cg.code + (size_t)__builtin_ctzll(km) * T;
-      for (int i = tid; i < T; i += NT) s_code[(size_t)s * T + i] = src[i];
+      const int k = __builtin_ctzll(km);
+      const uint16_t* src = Cg.code + (size_t)k * T;
+      for (int i = tid; i < T; i += NT) {
+        const uint32_t c = src[i];
+        s_code[(size_t)s * T + i] = (uint16_t)(c == 0xFFFFu ? FEAS2_CODE_NOKEY : c == 0xFFFEu ? FEAS2_CODE_DNE + k : c);
+      }
     }
   }
   for (int i = tid; i < tiles; i += NT) s_nonneg[i] = Cg.nonneg[i];
   for (int i = tid; i < D.KB * 64; i += NT) s_vint[i] = a.vint[i];
+  for (int i = tid; i < C; i += NT) s_cls[i] = Cg.cls[i];
   __syncthreads();
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = LANE;
   const VInt vi{(const int64_t LDS*)s_vint, a.vint, D.KB};
   const bool custom_on = a.mode_compatible && Cg.custom_any;
+  uint64_t LDS* al_w = (uint64_t LDS*)s_allowed[wave];
   for (long q = (long)blockIdx.x * FEAS2_WAVES + wave; q < a.n_queries; q += (long)gridDim.x * FEAS2_WAVES) {
     const KReqs* Q = reinterpret_cast<const KReqs*>(a.q_reqs + (size_t)q * sizeof(KReqs));
     const uint64_t v = lane < D.W ? Q->vals[lane] : 0;
@@ -2946,93 +2959,90 @@ __global__ __launch_bounds__(FEAS2_WAVES * 64) void feasibility_lds_kernel(FeasA
     rv.minv = Q->minv;
     const uint64_t negQ = negop_mask(rv.present, rv.compl_, rv.nz);
     const uint64_t allowed = allowed_word(D, rv, v, vi);
-    const uint64_t cls = allowed_classes<true>(D, Cg.cls, rv, allowed, negQ);
-    uint64_t LDS* al_w = (uint64_t LDS*)s_allowed[wave];
+    const uint64_t cls = allowed_classes<true>(D, (const OfferClass LDS*)s_cls, rv, allowed, negQ);
     al_w[lane] = allowed;
+    if (lane == 0) al_w[64] = ~0ull;
+    if (lane == 1) al_w[65] = negQ;
     const uint32_t rmask = (uint32_t)__ballot(rq_lane > 0);
     wave_sync();
     const uint64_t keys0 = rv.present & D.catalog_keys;
-    const bool custom = custom_on && (Cg.custom_any & ~rv.present);
+    // this lane's types t = i * 64 + lane: bit i of `alive` while type t passes
+    uint64_t alive = 0;
+    for (int i = 0; i < tiles; i++)
+      if (i * 64 + lane < T && ((s_nonneg[i] >> lane) & 1)) alive |= 1ull << i;
+    if (custom_on && (Cg.custom_any & ~rv.present))  // Compatible(q, type, WK) (a): non-well-known type keys q lacks
+      for (int i = 0; i < tiles; i++)
+        if ((alive >> i) & 1)
+          if (Cg.custom_nonneg[i * 64 + lane] & ~rv.present) alive &= ~(1ull << i);
+    // Intersects over the shared keys: staged single-valued keys (sentinel codes), branch-free
+    const uint64_t ks = keys0 & lds_keys & ~Cg.multi_valued;
+    for (uint64_t km = ks; km; km &= km - 1) {
+      const int k = __builtin_ctzll(km);
+      const uint16_t LDS* ck = s_code + (size_t)__builtin_popcountll(lds_keys & ((1ull << k) - 1)) * T;
+      uint64_t fail = 0;
+#pragma unroll 4
+      for (int i = 0; i < tiles; i++) {
+        const uint32_t c = ck[min(i * 64 + lane, T - 1)];
+        fail |= (uint64_t)(((al_w[c >> 6] >> (c & 63)) & 1) ^ 1) << i;
+      }
+      alive &= ~fail;
+    }
+    // keys read from global memory or multi-valued (a type with several values: Intersects if any is allowed)
+    for (uint64_t km = keys0 & ~ks; km; km &= km - 1) {
+      const int k = __builtin_ctzll(km);
+      const bool staged = (lds_keys >> k) & 1;
+      const uint16_t LDS* ck = s_code + (size_t)__builtin_popcountll(lds_keys & ((1ull << k) - 1)) * T;
+      const uint64_t aw = al_w[D.wofs[k]];
+      for (int i = 0; i < tiles; i++) {
+        if (!((alive >> i) & 1)) continue;
+        const int t = i * 64 + lane;
+        uint32_t c = staged ? (uint32_t)ck[t] : (uint32_t)Cg.code[(size_t)k * T + t];
+        if (!staged) c = c == 0xFFFFu ? FEAS2_CODE_NOKEY : c == 0xFFFEu ? FEAS2_CODE_DNE + k : c;
+        const bool pass = c == 0xFFFDu ? (aw & Cg.multi[(size_t)k * T + t]) != 0 : ((al_w[c >> 6] >> (c & 63)) & 1);
+        if (!pass) alive &= ~(1ull << i);
+      }
+    }
+    // Fits on the requested resources
+    for (uint32_t rm = rmask; rm; rm &= rm - 1) {
+      const int r = __builtin_ctz(rm);
+      const int64_t need = lane_bcast_i64(rq_lane, r);
+      const bool staged = (lds_res >> r) & 1;
+      const int64_t LDS* sa = s_alloc + (size_t)__builtin_popcount(lds_res & ((1u << r) - 1)) * T;
+      const int64_t* ga = Cg.alloc + (size_t)r * T;
+      uint64_t fail = 0;
+#pragma unroll 4
+      for (int i = 0; i < tiles; i++) {
+        const int t = min(i * 64 + lane, T - 1);
+        const int64_t al = staged ? sa[t] : ga[t];
+        fail |= (uint64_t)(need > al) << i;
+      }
+      alive &= ~fail;
+    }
+    // cheapest compatible available offering per type (min over the row's classes), mask words, output stream
     double* oc = a.out_cheapest ? a.out_cheapest + (size_t)q * T : nullptr;
+    const double* ps = (!a.price_lds && Cg.price_sub) ? Cg.price_sub + (size_t)cls * T : nullptr;
     uint64_t myword = 0;
-    for (int tile0 = 0; tile0 < tiles; tile0 += FEAS2_TB) {
-      int tt[FEAS2_TB];
-      bool valid[FEAS2_TB], alive[FEAS2_TB];
-#pragma unroll
-      for (int i = 0; i < FEAS2_TB; i++) {
-        const int t = (tile0 + i) * 64 + lane;
-        valid[i] = tile0 + i < tiles && t < T;
-        tt[i] = valid[i] ? t : 0;
-        alive[i] = valid[i] && ((s_nonneg[min(tile0 + i, tiles - 1)] >> lane) & 1);
-      }
-      if (custom) {  // Compatible(q, type, WK) part (a): non-well-known type keys q does not define
-#pragma unroll
-        for (int i = 0; i < FEAS2_TB; i++) alive[i] = alive[i] && !(Cg.custom_nonneg[tt[i]] & ~rv.present);
-      }
-      // Intersects over the shared keys
-      for (uint64_t keys = keys0; keys; keys &= keys - 1) {
-        const int k = __builtin_ctzll(keys);
-        const bool staged = (lds_keys >> k) & 1;
-        const int slot = __builtin_popcountll(lds_keys & ((1ull << k) - 1));
-        uint32_t code[FEAS2_TB];
-#pragma unroll
-        for (int i = 0; i < FEAS2_TB; i++)
-          code[i] = staged ? s_code[(size_t)slot * T + tt[i]] : Cg.code[(size_t)k * T + tt[i]];
-#pragma unroll
-        for (int i = 0; i < FEAS2_TB; i++) {
-          const uint32_t c = code[i];
-          bool pass;
-          if (c == 0xFFFFu) pass = true;                   // type lacks the key
-          else if (c == 0xFFFEu) pass = (negQ >> k) & 1;   // type DoesNotExist: only NotIn/DNE intersect
-          else if (c == 0xFFFDu) pass = !alive[i] || (al_w[D.wofs[k]] & Cg.multi[(size_t)k * T + tt[i]]) != 0;
-          else pass = (al_w[c >> 6] >> (c & 63)) & 1;
-          alive[i] = alive[i] && pass;
-        }
-      }
-      // Fits on the requested resources
-      for (uint32_t rm = rmask; rm; rm &= rm - 1) {
-        const int r = __builtin_ctz(rm);
-        const int64_t need = lane_bcast_i64(rq_lane, r);
-        const bool staged = (lds_res >> r) & 1;
-        const int slot = __builtin_popcount(lds_res & ((1u << r) - 1));
-#pragma unroll
-        for (int i = 0; i < FEAS2_TB; i++) {
-          const int64_t al = staged ? s_alloc[(size_t)slot * T + tt[i]] : Cg.alloc[(size_t)r * T + tt[i]];
-          alive[i] = alive[i] && need <= al;
-        }
-      }
-      // cheapest compatible available offering: min over the row's classes
-      double ch[FEAS2_TB];
-#pragma unroll
-      for (int i = 0; i < FEAS2_TB; i++) ch[i] = __builtin_huge_val();
+#pragma unroll 2
+    for (int i = 0; i < tiles; i++) {
+      const int t = i * 64 + lane;
+      const int tc = min(t, T - 1);
+      double ch = __builtin_huge_val();
       if (a.price_lds) {
         for (uint64_t m = cls; m; m &= m - 1) {
-          const int c = __builtin_ctzll(m);
-#pragma unroll
-          for (int i = 0; i < FEAS2_TB; i++) {
-            const double p = s_price[(size_t)c * T + tt[i]];
-            ch[i] = p < ch[i] ? p : ch[i];
-          }
+          const double p = s_price[(size_t)__builtin_ctzll(m) * T + tc];
+          ch = p < ch ? p : ch;
         }
-      } else if (Cg.price_sub) {
-#pragma unroll
-        for (int i = 0; i < FEAS2_TB; i++) ch[i] = Cg.price_sub[(size_t)cls * T + tt[i]];
+      } else if (ps) {
+        ch = ps[tc];
       } else {
         for (uint64_t m = cls; m; m &= m - 1) {
-          const int c = __builtin_ctzll(m);
-#pragma unroll
-          for (int i = 0; i < FEAS2_TB; i++) {
-            const double p = Cg.price_cm[(size_t)c * T + tt[i]];
-            ch[i] = p < ch[i] ? p : ch[i];
-          }
+          const double p = Cg.price_cm[(size_t)__builtin_ctzll(m) * T + tc];
+          ch = p < ch ? p : ch;
         }
       }
-#pragma unroll
-      for (int i = 0; i < FEAS2_TB; i++) {
-        const uint64_t bal = __ballot(alive[i] && ch[i] < __builtin_huge_val());
-        if (lane == tile0 + i) myword = bal;
-        if (oc && valid[i]) oc[tt[i]] = ch[i];
-      }
+      const uint64_t bal = __ballot(((alive >> i) & 1) && ch < __builtin_huge_val());
+      if (lane == i) myword = bal;
+      if (oc && t < T) oc[t] = ch;
     }
     if (lane < tiles) a.out_mask[(size_t)q * tiles + lane] = myword;
     wave_sync();

@@ -70,6 +70,8 @@ def load_lib(path=None):
         "kp_solve_prepare": (C.c_int32, [C.c_void_p, P(abi.SolveIn), P(C.c_void_p)]),
         "kp_solve_prepare_comm": (C.c_int32, [C.c_void_p, P(abi.SolveIn), C.c_void_p, P(C.c_void_p)]),
         "kp_solve_run": (C.c_int32, [C.c_void_p, P(C.c_void_p)]),
+        "kp_solve_refresh": (C.c_int32, [C.c_void_p]),
+        "kp_cluster_refresh": (C.c_int32, [C.c_void_p]),
         "kp_solve_plan_destroy": (None, [C.c_void_p]),
         "kp_result_nodeclaim_count": (C.c_uint32, [C.c_void_p]),
         "kp_result_pod_placements": (C.c_int32, [C.c_void_p, P(C.c_int32), C.c_uint32]),
@@ -299,6 +301,10 @@ class SolvePlan:
         finally:
             lib.kp_result_destroy(res)
 
+    def refresh(self):
+        """kp_solve_refresh: re-apply the catalogues' current offerings (after update_offerings) in place."""
+        _check(self.sched.ctx.lib, self.sched.ctx.lib.kp_solve_refresh(self.h))
+
     def close(self):
         if self.h:
             self.sched.ctx.lib.kp_solve_plan_destroy(self.h)
@@ -475,6 +481,10 @@ class ClusterPlan:
         h = C.c_void_p()
         _check(ctx.lib, ctx.lib.kp_cluster_prepare(ctx.h, C.byref(cl), C.byref(h)))
         self.h = h
+
+    def refresh(self):
+        """kp_cluster_refresh: re-apply the catalogues' current offerings (after update_offerings) in place."""
+        _check(self.ctx.lib, self.ctx.lib.kp_cluster_refresh(self.h))
 
     def simulate(self, subsets, multi_node=True, raw=False):
         """subsets: list of node-index lists (candidate order). Returns (results, stats); raw=True returns

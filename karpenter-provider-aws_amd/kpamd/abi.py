@@ -183,7 +183,7 @@ class SolveStats(C.Structure):
                 ("solve_kernel_ms", C.c_double), ("finalize_kernel_ms", C.c_double), ("attempts", C.c_uint64),
                 ("bytes_algorithmic", C.c_uint64), ("pops", C.c_uint64), ("phase_cycles", C.c_uint64 * 8),
                 ("scanned", C.c_uint64), ("cursor_starts", C.c_uint64), ("attempt_cycles", C.c_uint64 * 8),
-                ("catalog_ms", C.c_double), ("catalog_cached", C.c_uint32), ("reserved_", C.c_uint32),
+                ("catalog_ms", C.c_double), ("catalog_cached", C.c_uint32), ("catalog_refreshed", C.c_uint32),
                 ("fast_pods", C.c_uint64), ("fast_cycles", C.c_uint64 * 6), ("slow_sorts", C.c_uint64),
                 ("fast_bails", C.c_uint64 * 8)]
 

@@ -191,7 +191,8 @@ def test_launch_refresh_equals_rebuilt_catalogue(ctx, lib, catalog):
 @pytest.mark.gpu
 def test_solve_catalogue_resident_across_seqnums(ctx, lib, catalog):
     """The Solve's compiled catalogue half stays resident in the kp_ctx across Solves (same catalogue identity,
-    seqnum and NodePools: catalog_cached = 1) and is rebuilt when an ICE mark bumps the seqnum
+    seqnum and NodePools: catalog_cached = 1) and has its offerings re-applied in place when an ICE mark bumps the
+    seqnum (catalog_refreshed = 1)
     (R:pkg/providers/instancetype/instancetype.go:225-237 cacheKey; R:pkg/cache/unavailableofferings.go:66-92);
     every Solve equals the oracle on the catalogue as it is at that moment."""
     import kpamd
@@ -214,7 +215,7 @@ def test_solve_catalogue_resident_across_seqnums(ctx, lib, catalog):
             [("on-demand", t, "test-zone-1a") for t in range(len(its))]
     cat.update_offerings([(t, ct, z, False) for ct, t, z in marks], seqnum=2)
     third = sched.solve()
-    assert third["stats"]["catalog_cached"] == 0
+    assert third["stats"]["catalog_cached"] == 1 and third["stats"]["catalog_refreshed"] == 1
     names = [it.name for it in catalog]
     rebuilt = kc.build_catalog(lib, unavailable=frozenset((ct, names[t], z) for ct, t, z in marks))
     want = pyoracle.solve(synth.config2(rebuilt, n_pods=600, seed=23))
@@ -223,3 +224,81 @@ def test_solve_catalogue_resident_across_seqnums(ctx, lib, catalog):
         [(n["nodepool"], n["pods"], n["options"]) for n in want["nodeclaims"]]
     assert [n["options"] for n in third["nodeclaims"]] != [n["options"] for n in first["nodeclaims"]]
     cat.close()
+
+
+def _marks(its):
+    from kpamd import catalog as kc
+    return [("spot", t, z) for t in range(0, len(its), 2) for z in kc.ZONES[:2]] + \
+        [("on-demand", t, "test-zone-1a") for t in range(len(its))] + [("on-demand", t, "test-zone-1b") for t in range(0, len(its), 3)]
+
+
+def _canon(res):
+    return (res["placement"].tolist(), [(n["nodepool"], n["pods"], n["options"], n["n_remaining"], n["requirements"])
+                                        for n in res["nodeclaims"]])
+
+
+@pytest.mark.gpu
+def test_solve_plan_refresh_equals_rebuilt_catalogue(ctx, lib, catalog):
+    """kp_solve_refresh (R:pkg/cache/unavailableofferings.go:66-92 SeqNum): a prepared plan refuses to run once its
+    catalogue's seqnum moved; refreshed in place (offering masks, class prices, template options, the per-Solve
+    template table) it equals the oracle on a catalogue rebuilt with those offerings unavailable, and a second
+    Solve on the ctx reuses the refreshed half."""
+    import kpamd
+    from kpamd import catalog as kc
+    from kpamd import synth
+    from oracle import pyoracle
+    its = copy.deepcopy(catalog)
+    cat = kpamd.Catalog(ctx, its, seqnum=1)
+    prob = synth.config5(its, n_pods=3000)
+    sched = kpamd.Scheduler(ctx, prob, catalogs=[cat])
+    plan = sched.prepare()
+    before = plan.run()
+    marks = _marks(its)
+    cat.update_offerings([(t, ct, z, False) for ct, t, z in marks], seqnum=2)
+    with pytest.raises(kpamd.KPError) as e:
+        plan.run()
+    assert e.value.code == kpamd.abi.KP_E_INVAL
+    plan.refresh()
+    after = plan.run()
+    plan.close()
+    names = [it.name for it in catalog]
+    rebuilt = kc.build_catalog(lib, unavailable=frozenset((ct, names[t], z) for ct, t, z in marks))
+    want = pyoracle.solve(synth.config5(rebuilt, n_pods=3000))
+    assert _canon(after) == _canon(want)
+    assert _canon(after) != _canon(before)
+    again = sched.solve()
+    assert again["stats"]["catalog_cached"] == 1 and again["stats"]["catalog_refreshed"] == 0
+    assert _canon(again) == _canon(want)
+    cat.close()
+
+
+@pytest.mark.gpu
+def test_cluster_plan_refresh_equals_rebuilt_catalogue(ctx, lib, catalog):
+    """kp_cluster_refresh: a resident consolidation snapshot after ICE marks equals the oracle's
+    computeConsolidation on the rebuilt catalogue; before the refresh it refuses to simulate."""
+    import kpamd
+    from kpamd import catalog as kc
+    from kpamd import synth
+    from oracle import pyoracle
+    its = copy.deepcopy(catalog)
+    cl = synth.config4(its, n_nodes=150, seed=4)
+    cat = kpamd.Catalog(ctx, cl.catalogs[0], seqnum=1)
+    plan = kpamd.ClusterPlan(ctx, cl, catalogs=[cat])
+    subs = synth.consolidation_subsets(cl, 60, seed=5)
+    before, _ = plan.simulate(subs)
+    marks = _marks(its)
+    cat.update_offerings([(t, ct, z, False) for ct, t, z in marks], seqnum=2)
+    with pytest.raises(kpamd.KPError):
+        plan.simulate(subs)
+    plan.refresh()
+    after, _ = plan.simulate(subs)
+    plan.close()
+    cat.close()
+    names = [it.name for it in catalog]
+    rebuilt = kc.build_catalog(lib, unavailable=frozenset((ct, names[t], z) for ct, t, z in marks))
+    cl2 = copy.copy(cl)
+    cl2.catalogs = [rebuilt]
+    want, _ = pyoracle.simulate_batch(cl2, subs)
+    fields = ("decision", "nodepool", "candidate_price", "replacement_price", "savings", "n_options", "n_pods")
+    assert [tuple(r[f] for f in fields) for r in after] == [tuple(r[f] for f in fields) for r in want]
+    assert [tuple(r[f] for f in fields) for r in after] != [tuple(r[f] for f in fields) for r in before]
