@@ -162,6 +162,7 @@ def main():
             "algorithmic_bytes_per_launch": int(alg_bytes),
             "algorithmic_bytes_per_pod": round(alg_bytes / prob.n_pods, 1),
             "note": "single-workgroup sequential FFD: latency-bound (dependent L2 round trips + barriers per pod)",
+            "latency": _latency_roofline(k_ms, prob.n_pods),
         },
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -353,15 +354,16 @@ def _consolidation(args, cat, ctx, dist, rank, world, barrier, kcomm):
                                             "savings": hit[1]["savings"]}
     barrier()
     elapsed = time.perf_counter() - t0
+    elapsed_incl = elapsed + prep_s
     n_done = len(sw_offs) - 1 + (len(pre) if rank == 0 else 0)
     total = n_done
     dev = torch.device("cuda", torch.cuda.current_device())
     if dist is not None:
-        te = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        te = torch.tensor([elapsed, elapsed_incl], dtype=torch.float64, device=dev)
         dist.all_reduce(te, op=dist.ReduceOp.MAX)
         tot = torch.tensor([float(n_done)], dtype=torch.float64, device=dev)
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        elapsed, total = float(te.item()), int(tot.item())
+        elapsed, elapsed_incl, total = float(te[0].item()), float(te[1].item()), int(tot.item())
     out = {
         "metric": "consolidation sims/s",
         "value": round(total / elapsed, 1),
@@ -372,6 +374,9 @@ def _consolidation(args, cat, ctx, dist, rank, world, barrier, kcomm):
                     f"2..100 candidates + {len(pre)} firstNConsolidationOption prefixes) on a {args.cluster_nodes}-node "
                     f"cluster packed near capacity ({len(cl.pod_shape)} pods), 2 NodePools, 919 types; subsets sharded "
                     f"by chunk over ranks, best decision by kp_consolidate_argmin (device argmax + RCCL all-gather)",
+        # the disruption controller rebuilds its snapshot every pass: the rate with kp_cluster_prepare inside
+        "sims_per_s_incl_prepare": round(total / elapsed_incl, 1),
+        "elapsed_incl_prepare_s": round(elapsed_incl, 4),
         "elapsed_s": round(elapsed, 4),
         "sim_kernel_ms_rank0": round(st["solve_kernel_ms"], 3),
         "pods_rescheduled_rank0": int(st["pops"]),
@@ -440,6 +445,26 @@ def _cpu_baseline_sims(cl, cands, n, procs=16):
     except Exception as e:  # the single-thread figure stands on its own
         out["all_threads"] = {"error": str(e)[:200]}
     return out
+
+
+CLOCK_GHZ = 2.4  # MI355X peak engine clock (MI355X_MICROARCH.md chip table)
+
+
+def _latency_roofline(kernel_ms, pods):
+    """The Solve kernel's own bound: one wave issues the whole first-fit loop, so its floor is the issue time of the
+    instructions it executes per pod (SQ_ACTIVE_INST_ANY: cycles the waves were issuing; SQ counters from a separate
+    rocprofv3 --pmc pass of the same build, tools/pmc_sq.sh -> profiles/latency.json). frac = floor / measured."""
+    p = os.path.join(REPO, "profiles", "latency.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        lat = json.load(open(p))
+        cyc = kernel_ms * 1e-3 * CLOCK_GHZ * 1e9 / pods
+        floor = float(lat["issue_cycles_per_pod"])
+        return {"cycles_per_pod": round(cyc, 1), "issue_floor_cycles": round(floor, 1), "frac": round(floor / cyc, 4),
+                "instructions_per_pod": lat.get("instructions_per_pod"), "source": lat.get("source")}
+    except Exception:
+        return None
 
 
 def _traffic(kernel):

@@ -217,16 +217,28 @@ typedef struct kp_topology_spread {
 
 /* corev1.PodAffinityTerm (ABI v6): pod affinity / anti-affinity on the hostname or a label key (upstream
  * TopologyGroup of TopologyTypePodAffinity / TopologyTypePodAntiAffinity, and the inverse groups bound pods' required
- * anti-affinity terms create). namespaceSelector returns KP_E_UNSUPPORTED. */
+ * anti-affinity terms create). The namespaces a term selects (upstream Topology.buildNamespaceList): no namespaces
+ * and no namespaceSelector -> the pod's own namespace; else `namespaces` plus every namespace of
+ * kp_solve_in.namespaces / kp_cluster.namespaces whose labels namespace_selector matches (ABI v8; an empty
+ * selector matches them all). */
 typedef struct kp_pod_affinity_term {
   const char* topology_key;
   kp_label_selector selector;
-  const char* const* namespaces;  /* n_namespaces == 0: the pod's own namespace */
+  const char* const* namespaces;  /* n_namespaces == 0 and no namespace selector: the pod's own namespace */
   uint32_t n_namespaces;
   int32_t weight;                 /* preferred terms: WeightedPodAffinityTerm.weight */
-  int32_t has_namespace_selector; /* != 0: namespaceSelector set (unsupported) */
+  int32_t has_namespace_selector; /* != 0: namespaceSelector set (namespace_selector) */
   int32_t reserved_;
+  kp_label_selector namespace_selector;
 } kp_pod_affinity_term;
+
+/* A namespace of the cluster and its labels (ABI v8): what a namespaceSelector lists (corev1.NamespaceList). */
+typedef struct kp_namespace {
+  const char* name;
+  const kp_label* labels;
+  uint32_t n_labels;
+  uint32_t reserved_;
+} kp_namespace;
 
 /* A container port with hostPort != 0, as upstream scheduling.GetHostPorts reads it (HostPortUsage). Two entries
  * conflict when protocol and port are equal and either IP is unspecified (0.0.0.0 / ::) or both IPs are equal. */
@@ -331,7 +343,8 @@ typedef struct kp_solve_in {
   uint32_t max_instance_types;  /* scheduling.MaxInstanceTypes = 100; 0 = no truncation */
   const kp_bound_pod* bound_pods;  /* pods running on existing nodes (topology domain counts) */
   uint32_t n_bound_pods;
-  uint32_t reserved_;
+  uint32_t n_namespaces;           /* ABI v8: the cluster's namespaces (pod affinity namespaceSelector) */
+  const kp_namespace* namespaces;
 } kp_solve_in;
 
 typedef struct kp_nodeclaim_info {
@@ -652,7 +665,8 @@ typedef struct kp_cluster {
   const uint32_t* pending_pods;  /* provisionable pods not bound to any node (indices into pods): they join every
                                     simulation, but their own scheduling errors do not block a decision */
   uint32_t n_pending;
-  uint32_t reserved_;
+  uint32_t n_namespaces;         /* ABI v8: the cluster's namespaces (pod affinity namespaceSelector) */
+  const kp_namespace* namespaces;
 } kp_cluster;
 
 enum kp_decision { KP_DECISION_NOOP = 0, KP_DECISION_DELETE = 1, KP_DECISION_REPLACE = 2 };

@@ -183,13 +183,8 @@ struct FeasArgs {
   const int64_t* q_requests; // [Q][NRES]
   uint64_t* out_mask;        // [Q][tiles]
   double* out_cheapest;      // [Q][T] or null
-  // catalogue columns staged in LDS once per workgroup (feasibility_lds_kernel; lds_bytes 0: feasibility_kernel's
-  // global gathers). Rows of the LDS tables in key / resource order of the masks: slot(k) = popc(lds_keys below k).
-  int32_t lds_bytes;         // dynamic LDS per workgroup
-  int32_t blocks;            // persistent grid (one workgroup per CU)
-  uint64_t lds_keys;         // keys whose single-value codes [T] u16 are staged
-  uint32_t lds_res;          // resources whose allocatable [T] i64 is staged
-  int32_t price_lds;         // class-major prices [C][T] f64 staged
+  int32_t bits;              // 1: feasibility_bits_kernel (bitsets over the catalogue), 0: feasibility_kernel
+  int32_t blocks;            // its grid (rows are strided over the waves)
 };
 
 // ---- launch-side selection (kp_launch_select) ------------------------------------------------------
@@ -360,4 +355,4 @@ const void* sim_kernel_ptr();
 hipError_t launch_solve(const SolveArgs& a, int nw, size_t dyn_lds, hipStream_t s);
 hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s);
 hipError_t launch_feasibility(const FeasArgs& a, hipStream_t s);
-const void* feasibility_lds_kernel_ptr();
+

@@ -1301,7 +1301,6 @@ const kp_pod_affinity_term* PodTermAt(const kp_pod_shape& sh, int a, bool* aff =
   return nullptr;
 }
 int32_t CheckAntiTerm(const kp_pod_affinity_term& t, const char* who, uint32_t i) {
-  if (t.has_namespace_selector) return fail(KP_E_UNSUPPORTED, "%s %u: pod (anti-)affinity namespaceSelector", who, i);
   if (!t.topology_key || !t.topology_key[0]) return fail(KP_E_INVAL, "%s %u: pod (anti-)affinity without topologyKey", who, i);
   return KP_OK;
 }
@@ -1558,10 +1557,22 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
   // namespaces, selector). countDomains: bound pods it selects, per node. inverse: a bound pod's own required term
   // (updateInverseAntiAffinity): its counts are the owners' nodes, it constrains the pods it selects, and no
   // placement records into it.
-  auto nss_of = [](const kp_pod_affinity_term& t, const char* pod_ns) {
+  // the namespaces a term selects (upstream Topology.buildNamespaceList): none given and no namespaceSelector -> the
+  // pod's own; else the listed ones plus every cluster namespace whose labels the namespaceSelector matches
+  auto nss_of = [&](const kp_pod_affinity_term& t, const char* pod_ns) {
     std::set<string> n;
     for (uint32_t i = 0; i < t.n_namespaces; i++) n.insert(t.namespaces[i] ? t.namespaces[i] : "");
-    if (n.empty()) n.insert(pod_ns ? pod_ns : "");
+    if (t.has_namespace_selector) {
+      for (uint32_t i = 0; i < in->n_namespaces; i++) {
+        const kp_namespace& ns = in->namespaces[i];
+        std::map<string, string> labels;
+        for (uint32_t j = 0; j < ns.n_labels; j++)
+          labels[ns.labels[j].key ? ns.labels[j].key : ""] = ns.labels[j].value ? ns.labels[j].value : "";
+        if (SelectorMatches(t.namespace_selector, labels)) n.insert(ns.name ? ns.name : "");
+      }
+    } else if (n.empty()) {
+      n.insert(pod_ns ? pod_ns : "");
+    }
     return n;
   };
   // TopologyTypePodAffinity (aff): the same hostname row with maxSkew = -1, whose pre-pass test is count > 0, or,
@@ -3230,60 +3241,6 @@ static int32_t RefreshOfferings(kp_ctx* ctx, const kp_catalog* cat, Compiled& cp
   return KP_OK;
 }
 
-// Which catalogue columns feasibility_lds_kernel stages in LDS for this batch: the codes of the keys the rows name
-// (most read), the allocatable of the resources they request, then the class-major prices, while they fit beside
-// the kernel's static LDS; a column that does not fit is gathered from global memory. Without any: the
-// global-gather kernel.
-static int32_t FeasStageLds(kp_ctx* ctx, const DevDict& dd, const vector<KReqs>& qreqs, const vector<int64_t>& qrq,
-                            uint32_t n_queries, FeasArgs& fa) {
-  fa.lds_bytes = 0;
-  fa.lds_keys = 0;
-  fa.lds_res = 0;
-  fa.price_lds = 0;
-  if (getenv("KP_FEAS_GLOBAL") || n_queries == 0) return KP_OK;  // measurement hook: the global-gather kernel
-  hipFuncAttributes attr;
-  HIPCHK(hipFuncGetAttributes(&attr, feasibility_lds_kernel_ptr()));
-  const long budget = 160 * 1024 - (long)attr.sharedSizeBytes - 256;
-  const long T = dd.T, tiles = (T + 63) / 64;
-  uint64_t keys = 0;
-  uint32_t res = 0;
-  for (uint32_t i = 0; i < n_queries; i++) {
-    keys |= qreqs[i].present;
-    for (int r = 0; r < KP_NRES; r++)
-      if (qrq[(size_t)i * KP_NRES + r] > 0) res |= 1u << r;
-  }
-  keys &= dd.catalog_keys;
-  long used = tiles * 8;
-  if (getenv("KP_FEAS_NO_KEYS")) keys = 0;  // measurement hooks: leave a column family in global memory
-  if (getenv("KP_FEAS_NO_RES")) res = 0;
-  for (uint64_t m = keys; m; m &= m - 1)
-    if (used + (2 * T + 7) / 8 * 8 <= budget) {  // codes rows padded to 8 B so the total stays a multiple of 8
-      fa.lds_keys |= 1ull << __builtin_ctzll(m);
-      used += (2 * T + 7) / 8 * 8;
-    }
-  for (uint32_t m = res; m; m &= m - 1)
-    if (used + 8 * T <= budget) {
-      fa.lds_res |= 1u << __builtin_ctz(m);
-      used += 8 * T;
-    }
-  if (used + 8 * T * dd.C <= budget && !getenv("KP_FEAS_NO_PRICE")) {
-    fa.price_lds = 1;
-    used += 8 * T * dd.C;
-  }
-  if (!fa.lds_keys && !fa.lds_res && !fa.price_lds) return KP_OK;
-  // the kernel lays codes rows back to back: size them exactly (+ alignment slack)
-  const long n_k = __builtin_popcountll(fa.lds_keys);
-  used = (fa.price_lds ? 8 * T * dd.C : 0) + 8 * T * __builtin_popcount(fa.lds_res) + 8 * tiles + 2 * T * n_k + 16;
-  if (used > budget) return fail(KP_E_INVAL, "feasibility LDS plan %ld B exceeds %ld B", used, budget);
-  int ncu = 256;
-  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || ncu <= 0) ncu = 256;
-  fa.lds_bytes = (int32_t)((used + 15) & ~15L);
-  fa.blocks = (int32_t)std::min<long>(ncu, ((long)n_queries + 15) / 16);
-  if (const char* e = getenv("KP_FEAS_BLOCKS")) fa.blocks = std::max(1, atoi(e));
-  HIPCHK(hipFuncSetAttribute(feasibility_lds_kernel_ptr(), hipFuncAttributeMaxDynamicSharedMemorySize, fa.lds_bytes));
-  return KP_OK;
-}
-
 struct kp_filter_plan {
   kp_ctx* ctx = nullptr;
   DevBuf buf;
@@ -3351,8 +3308,9 @@ int32_t kp_filter_prepare(kp_ctx* ctx, const kp_catalog* cat, const kp_feasibili
   fa.q_requests = (const int64_t*)(base + o_qr);
   fa.out_mask = (uint64_t*)(base + plan->o_mask);
   fa.out_cheapest = with_cheapest ? (double*)(base + plan->o_ch) : nullptr;
-  rc = FeasStageLds(ctx, cp.B->d.dd, qreqs, qrq, n_queries, fa);
-  if (rc) return rc;
+  // the bitset kernel (KP_FEAS_GLOBAL: the per-type global-gather kernel, kept as its cross-check)
+  fa.bits = getenv("KP_FEAS_GLOBAL") ? 0 : 1;
+  fa.blocks = (int32_t)std::min<uint32_t>(std::max<uint32_t>((n_queries + 7) / 8, 1), 8192);
   plan->n_queries = n_queries;
   plan->T = T;
   plan->tiles = tiles;
@@ -3781,6 +3739,7 @@ struct OwnedCluster {
     for (uint32_t i = 0; o && i < n; i++) {
       o[i].topology_key = S(o[i].topology_key);
       Selector(o[i].selector);
+      Selector(o[i].namespace_selector);
       const char** v = (const char**)A(o[i].namespaces, o[i].n_namespaces);
       for (uint32_t j = 0; v && j < o[i].n_namespaces; j++) v[j] = S(v[j]);
       o[i].namespaces = v;
@@ -3845,6 +3804,9 @@ struct OwnedCluster {
     cl.shapes = sh;
     cl.pods = A(in->pods, in->n_pods);
     cl.pending_pods = A(in->pending_pods, in->n_pending);
+    kp_namespace* ns = A(in->namespaces, in->n_namespaces);
+    for (uint32_t i = 0; ns && i < in->n_namespaces; i++) ns[i].name = S(ns[i].name), ns[i].labels = Labels(ns[i].labels, ns[i].n_labels);
+    cl.namespaces = ns;
   }
 };
 
@@ -3922,6 +3884,8 @@ static int32_t PrepareGeneral(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan
   in.pods = cl->pods;
   in.n_pods = cl->n_pods;
   in.max_instance_types = 100;
+  in.namespaces = cl->namespaces;
+  in.n_namespaces = cl->n_namespaces;
   Compiled C;
   int32_t rc = CompileSolve(&in, C);
   if (rc) return rc;
@@ -3965,6 +3929,8 @@ int32_t kp_cluster_prepare(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan** 
   in.pods = cl->pods;
   in.n_pods = cl->n_pods;
   in.max_instance_types = 100;
+  in.namespaces = cl->namespaces;
+  in.n_namespaces = cl->n_namespaces;
   int32_t rc = CompileSolve(&in, C);
   if (rc) return rc;
   const Dict& d = C.B->d;
@@ -4396,6 +4362,8 @@ static int32_t GeneralSimLocked(kp_cluster_plan* plan, const uint32_t* offsets, 
     in.max_instance_types = 100;
     in.bound_pods = bound.data();
     in.n_bound_pods = (uint32_t)bound.size();
+    in.namespaces = cl.namespaces;
+    in.n_namespaces = cl.n_namespaces;
     kp_solve_plan* sp = nullptr;
     int32_t rc = SolvePrepare(ctx, &in, nullptr, &sp);
     if (rc) return rc;

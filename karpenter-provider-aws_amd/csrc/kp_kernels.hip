@@ -153,6 +153,34 @@ __device__ __forceinline__ uint64_t bounds_mask(const DevDict& D, uint64_t bk, u
   return out;
 }
 
+// bounds_mask with the bound slots held by the lanes (lane k: key k's gt / lt) and the parsed integers of the staged
+// words in LDS: no generic (FLAT) loads, whose waits would also cover every outstanding global load and store.
+__device__ __forceinline__ uint64_t bounds_mask_lanes(const DevDict& D, uint64_t bk, uint64_t hgt, uint64_t hlt,
+                                                      int64_t gt_lane, int64_t lt_lane, const int64_t LDS* vl, int nl,
+                                                      const GLB int64_t* vg) {
+  const int lane = LANE;
+  uint64_t out = ~0ull;
+  while (bk) {
+    const int kk = __builtin_ctzll(bk);
+    bk &= bk - 1;
+    const bool hg = (hgt >> kk) & 1, hl = (hlt >> kk) & 1;
+    const int64_t g = lane_bcast_i64(gt_lane, kk), l = lane_bcast_i64(lt_lane, kk);
+    uint64_t wm = 1ull << kk;
+    if ((D.multiword >> kk) & 1) wm |= D.ovfmask[kk];
+    while (wm) {
+      const int w = __builtin_ctzll(wm);
+      wm &= wm - 1;
+      int64_t x;
+      if (w < nl) x = vl[w * 64 + lane];
+      else x = vg[w * 64 + lane];
+      const bool ok = ((D.vint_ok[w] >> lane) & 1) && (!hg || x > g) && (!hl || x < l);
+      const uint64_t m = __ballot(ok);
+      if (lane == w) out = m;
+    }
+  }
+  return out;
+}
+
 // Key masks + bound slots of one requirement set; values stay in registers (one word per lane).
 struct ReqView {
   uint64_t present, compl_, hgt, hlt, hmin, nz, dne;
@@ -2882,173 +2910,158 @@ __global__ __launch_bounds__(FEAS_WAVES * 64) void feasibility_kernel(FeasArgs a
   }
 }
 
-// feasibility_lds_kernel: the same filter with the catalogue columns a batch reads staged in LDS. One persistent
-// workgroup of 16 waves per CU copies the single-value codes of the keys the rows name, the allocatable of the
-// resources they request and the class-major prices into LDS (~120 KB at T = 919), once; then every (row, type) test
-// is LDS reads + ALU, and the kernel streams what HBM must carry: each row's requirements in, its mask words and
-// one f64 cheapest price per type out.
-// Per row the wave decodes the requirement set once into its allowed-value words in LDS, plus two sentinel words:
-// word 64 = all ones (the code of "type lacks the key") and word 65 = the row's NotIn/DoesNotExist keys (the code
-// of "type has the key DoesNotExist" is 65 * 64 + k, remapped at staging), so that for a single-valued key one
-// ds_read of the code and one of the allowed word decide a type, branch-free. Loops run key-outer / tile-inner:
-// a lane keeps its types' verdicts as one bit per 64-type tile, the tile loop's LDS reads are independent (in
-// flight together), and the scalar key walk is paid once per key instead of once per tile.
-#define FEAS2_WAVES 16
-#define FEAS2_AW 68  // allowed words per wave: 64 value words + the two sentinel words (+ pad)
-#define FEAS2_CODE_NOKEY (64 * 64)
-#define FEAS2_CODE_DNE (65 * 64)
-__global__ __launch_bounds__(FEAS2_WAVES * 64) void feasibility_lds_kernel(FeasArgs a) {
+// feasibility_bits_kernel: the same filter, each row evaluated as bitsets over the whole catalogue. One wave per row;
+// lane l < TW holds the row's verdict for types 64 l .. 64 l + 63 as one word, built from the catalogue's type-set
+// rows (L2-resident): per key, NOKEY | (NotIn/DoesNotExist ? DNE) | the union of TM rows of the key's allowed values
+// (for a single-valued key, when fewer, the complement: valued types minus the union over its excluded values);
+// Fits as one threshold row per requested resource (fit_mask at the first allocatable >= the request); an available
+// compatible offering as the union of the row's classes' offer_avail rows. The mask words are the lanes' words: no
+// per-type work. The cheapest compatible available price per type is the row price_sub[cls] of the precomputed
+// per-class-subset minima (a row copy, L2 -> HBM), or the min over the classes' price rows when C > KP_SUB_MAX_C.
+// The next row's header loads are issued before this row is evaluated.
+#define FEASB_WAVES 8
+__global__ __launch_bounds__(FEASB_WAVES * 64) void feasibility_bits_kernel(FeasArgs a) {
   __shared__ DevDict D;
-  __shared__ uint64_t s_allowed[FEAS2_WAVES][FEAS2_AW];
   __shared__ int64_t s_vint[KP_MAX_BOUND_KEYS * 64];
   __shared__ OfferClass s_cls[KP_MAX_CLASSES];
-  extern __shared__ __attribute__((aligned(16))) uint64_t s_cat2[];
   block_copy(D, a.dict);
-  __syncthreads();
-  const DevCatalog Cg = *a.cat;
-  const int T = D.T, tiles = (T + 63) >> 6, C = D.C;
   const int tid = threadIdx.x;
-  constexpr int NT = FEAS2_WAVES * 64;
-  const uint64_t lds_keys = a.lds_keys;
-  const uint32_t lds_res = a.lds_res;
-  const int n_k = __builtin_popcountll(lds_keys), n_r = __builtin_popcount(lds_res);
-  double LDS* s_price = (double LDS*)s_cat2;                                              // [C][T]
-  int64_t LDS* s_alloc = (int64_t LDS*)(s_cat2 + (a.price_lds ? (size_t)C * T : 0));       // [n_r][T]
-  uint64_t LDS* s_nonneg = (uint64_t LDS*)(s_alloc + (size_t)n_r * T);                     // [tiles]
-  uint16_t LDS* s_code = (uint16_t LDS*)(s_nonneg + tiles);                                // [n_k][T]
-  if (a.price_lds)
-    for (int i = tid; i < C * T; i += NT) s_price[i] = Cg.price_cm[i];
-  {
-    int s = 0;
-    for (uint32_t rm = lds_res; rm; rm &= rm - 1, s++) {
-      const int64_t* src = Cg.alloc + (size_t)__builtin_ctz(rm) * T;
-      for (int i = tid; i < T; i += NT) s_alloc[(size_t)s * T + i] = src[i];
-    }
-    s = 0;
-    for (uint64_t km = lds_keys; km; km &= km - 1, s++) {
-      const int k = __builtin_ctzll(km);
-      const uint16_t* src = Cg.code + (size_t)k * T;
-      for (int i = tid; i < T; i += NT) {
-        const uint32_t c = src[i];
-        s_code[(size_t)s * T + i] = (uint16_t)(c == 0xFFFFu ? FEAS2_CODE_NOKEY : c == 0xFFFEu ? FEAS2_CODE_DNE + k : c);
-      }
-    }
-  }
-  for (int i = tid; i < tiles; i += NT) s_nonneg[i] = Cg.nonneg[i];
+  constexpr int NT = FEASB_WAVES * 64;
+  const DevCatalog Cd = *a.cat;
+  const GLB uint64_t* TM = (const GLB uint64_t*)Cd.TM;
+  const GLB uint64_t* DNE = (const GLB uint64_t*)Cd.DNE;
+  const GLB uint64_t* NOKEY = (const GLB uint64_t*)Cd.NOKEY;
+  const GLB uint64_t* fit_mask = (const GLB uint64_t*)Cd.fit_mask;
+  const GLB int64_t* fit_vals = (const GLB int64_t*)Cd.fit_vals;
+  const GLB int32_t* fit_n = (const GLB int32_t*)Cd.fit_n;
+  const GLB uint64_t* offer = (const GLB uint64_t*)Cd.offer_avail;
+  const GLB double* price_sub = (const GLB double*)Cd.price_sub;
+  const GLB double* price_cm = (const GLB double*)Cd.price_cm;
+  const GLB uint64_t* custom = (const GLB uint64_t*)Cd.custom_nonneg;
+  __syncthreads();
+  const int T = D.T, TW = D.TW, C = D.C;
   for (int i = tid; i < D.KB * 64; i += NT) s_vint[i] = a.vint[i];
-  for (int i = tid; i < C; i += NT) s_cls[i] = Cg.cls[i];
+  for (int i = tid; i < C; i += NT) s_cls[i] = Cd.cls[i];
   __syncthreads();
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = LANE;
-  const VInt vi{(const int64_t LDS*)s_vint, a.vint, D.KB};
-  const bool custom_on = a.mode_compatible && Cg.custom_any;
-  uint64_t LDS* al_w = (uint64_t LDS*)s_allowed[wave];
-  for (long q = (long)blockIdx.x * FEAS2_WAVES + wave; q < a.n_queries; q += (long)gridDim.x * FEAS2_WAVES) {
-    const KReqs* Q = reinterpret_cast<const KReqs*>(a.q_reqs + (size_t)q * sizeof(KReqs));
-    const uint64_t v = lane < D.W ? Q->vals[lane] : 0;
-    const int64_t rq_lane = lane < KP_NRES ? a.q_requests[(size_t)q * KP_NRES + lane] : 0;
+  const bool lw = lane < TW;  // this lane holds a type word
+  const uint64_t nonneg = lw ? ((const GLB uint64_t*)Cd.nonneg)[lane] : 0;
+  struct RowHdr {
+    uint64_t hw, v;
+    int64_t rq, gt, lt;
+  };
+  auto load_row = [&](long q) {
+    RowHdr h;
+    const GLB KReqs* Q = reinterpret_cast<const GLB KReqs*>((const GLB uint8_t*)a.q_reqs + (size_t)q * sizeof(KReqs));
+    h.hw = lane < 6 ? reinterpret_cast<const GLB uint64_t*>(Q)[lane] : 0;
+    h.v = lane < D.W ? Q->vals[lane] : 0;
+    h.rq = lane < KP_NRES ? ((const GLB int64_t*)a.q_requests)[(size_t)q * KP_NRES + lane] : 0;
+    h.gt = lane < KP_MAX_BOUND_KEYS ? Q->gt[lane] : 0;
+    h.lt = lane < KP_MAX_BOUND_KEYS ? Q->lt[lane] : 0;
+    return h;
+  };
+  const long q_stride = (long)gridDim.x * FEASB_WAVES;
+  long q = (long)blockIdx.x * FEASB_WAVES + wave;
+  RowHdr nxt = q < a.n_queries ? load_row(q) : RowHdr{0, 0, 0, 0, 0};
+  for (; q < a.n_queries; q += q_stride) {
+    const RowHdr cur = nxt;
+    if (q + q_stride < a.n_queries) nxt = load_row(q + q_stride);
+    const uint64_t v = cur.v;
     ReqView rv;
-    rv.present = Q->present;
-    rv.compl_ = Q->compl_ & Q->present;
-    rv.hgt = Q->hgt;
-    rv.hlt = Q->hlt;
-    rv.hmin = Q->hmin;
+    rv.present = lane_bcast(cur.hw, 0);
+    rv.compl_ = lane_bcast(cur.hw, 1) & rv.present;
+    rv.hgt = lane_bcast(cur.hw, 2);
+    rv.hlt = lane_bcast(cur.hw, 3);
+    rv.hmin = lane_bcast(cur.hw, 4);
     rv.nz = nz_keys(D, v);
     rv.dne = 0;
-    rv.gt = Q->gt;
-    rv.lt = Q->lt;
-    rv.minv = Q->minv;
+    rv.gt = rv.lt = nullptr;  // the bounds stay in the lanes (bounds_mask_lanes)
+    rv.minv = nullptr;        // minValues plays no part in CompatibleAvailableFilter
     const uint64_t negQ = negop_mask(rv.present, rv.compl_, rv.nz);
-    const uint64_t allowed = allowed_word(D, rv, v, vi);
+    uint64_t allowed;  // allowed_word() with the lane-held bounds
+    {
+      const uint64_t bk = (rv.hgt | rv.hlt) & rv.present & rv.compl_ & ((1ull << D.KB) - 1);
+      const uint64_t bm = bk ? bounds_mask_lanes(D, bk, rv.hgt, rv.hlt, cur.gt, cur.lt, (const int64_t LDS*)s_vint, D.KB,
+                                                 (const GLB int64_t*)a.vint)
+                             : ~0ull;
+      const int k = lane < D.W ? (int)D.wkey[lane] : 0;
+      allowed = lane >= D.W ? 0
+                : !((rv.present >> k) & 1) ? D.validbits[lane]
+                : ((rv.compl_ >> k) & 1)   ? (~v & D.validbits[lane] & bm)
+                                            : v;
+    }
     const uint64_t cls = allowed_classes<true>(D, (const OfferClass LDS*)s_cls, rv, allowed, negQ);
-    al_w[lane] = allowed;
-    if (lane == 0) al_w[64] = ~0ull;
-    if (lane == 1) al_w[65] = negQ;
-    const uint32_t rmask = (uint32_t)__ballot(rq_lane > 0);
-    wave_sync();
-    const uint64_t keys0 = rv.present & D.catalog_keys;
-    // this lane's types t = i * 64 + lane: bit i of `alive` while type t passes
-    uint64_t alive = 0;
-    for (int i = 0; i < tiles; i++)
-      if (i * 64 + lane < T && ((s_nonneg[i] >> lane) & 1)) alive |= 1ull << i;
-    if (custom_on && (Cg.custom_any & ~rv.present))  // Compatible(q, type, WK) (a): non-well-known type keys q lacks
-      for (int i = 0; i < tiles; i++)
-        if ((alive >> i) & 1)
-          if (Cg.custom_nonneg[i * 64 + lane] & ~rv.present) alive &= ~(1ull << i);
-    // Intersects over the shared keys: staged single-valued keys (sentinel codes), branch-free
-    const uint64_t ks = keys0 & lds_keys & ~Cg.multi_valued;
-    for (uint64_t km = ks; km; km &= km - 1) {
-      const int k = __builtin_ctzll(km);
-      const uint16_t LDS* ck = s_code + (size_t)__builtin_popcountll(lds_keys & ((1ull << k) - 1)) * T;
-      uint64_t fail = 0;
-#pragma unroll 4
-      for (int i = 0; i < tiles; i++) {
-        const uint32_t c = ck[min(i * 64 + lane, T - 1)];
-        fail |= (uint64_t)(((al_w[c >> 6] >> (c & 63)) & 1) ^ 1) << i;
-      }
-      alive &= ~fail;
+    const uint32_t rmask = (uint32_t)__ballot(cur.rq > 0);
+    uint64_t pass = nonneg;
+    // Compatible(q, type, WK) part (a): types with a non-well-known key q does not define (rare: per-type loads)
+    if (a.mode_compatible && (Cd.custom_any & ~rv.present) && __ballot(lw && pass)) {
+      uint64_t keep = 0;
+      if (lw)
+        for (uint64_t m = pass; m; m &= m - 1) {
+          const int b = __builtin_ctzll(m);
+          if (!(custom[lane * 64 + b] & ~rv.present)) keep |= 1ull << b;
+        }
+      pass = keep;
     }
-    // keys read from global memory or multi-valued (a type with several values: Intersects if any is allowed)
-    for (uint64_t km = keys0 & ~ks; km; km &= km - 1) {
+    // Intersects over the shared keys, one key's type set at a time
+    for (uint64_t km = rv.present & D.catalog_keys; km; km &= km - 1) {
       const int k = __builtin_ctzll(km);
-      const bool staged = (lds_keys >> k) & 1;
-      const uint16_t LDS* ck = s_code + (size_t)__builtin_popcountll(lds_keys & ((1ull << k) - 1)) * T;
-      const uint64_t aw = al_w[D.wofs[k]];
-      for (int i = 0; i < tiles; i++) {
-        if (!((alive >> i) & 1)) continue;
-        const int t = i * 64 + lane;
-        uint32_t c = staged ? (uint32_t)ck[t] : (uint32_t)Cg.code[(size_t)k * T + t];
-        if (!staged) c = c == 0xFFFFu ? FEAS2_CODE_NOKEY : c == 0xFFFEu ? FEAS2_CODE_DNE + k : c;
-        const bool pass = c == 0xFFFDu ? (aw & Cg.multi[(size_t)k * T + t]) != 0 : ((al_w[c >> 6] >> (c & 63)) & 1);
-        if (!pass) alive &= ~(1ull << i);
+      uint64_t acc = lw ? NOKEY[(size_t)k * TW + lane] | (((negQ >> k) & 1) ? DNE[(size_t)k * TW + lane] : 0) : 0;
+      // the key's value words: allowed (A) and excluded (E) value bits
+      int nA = 0, nE = 0;
+      uint64_t wm = 1ull << k;
+      if ((D.multiword >> k) & 1) wm |= D.ovfmask[k];
+      for (uint64_t m = wm; m; m &= m - 1) {
+        const int w = __builtin_ctzll(m);
+        const uint64_t aw = lane_bcast(allowed, w);
+        nA += __builtin_popcountll(aw & D.validbits[w]);
+        nE += __builtin_popcountll(~aw & D.validbits[w]);
       }
+      const bool compl_walk = ((D.single_valued >> k) & 1) && nE < nA;
+      uint64_t u = 0;
+      for (uint64_t m = wm; m; m &= m - 1) {
+        const int w = __builtin_ctzll(m);
+        const uint64_t aw = lane_bcast(allowed, w);
+        for (uint64_t bits = (compl_walk ? ~aw : aw) & D.validbits[w]; bits; bits &= bits - 1)
+          u |= lw ? TM[(size_t)(w * 64 + __builtin_ctzll(bits)) * TW + lane] : 0;
+      }
+      if (compl_walk) {  // valued types (single-valued key: not NOKEY, not DNE) outside the excluded values' union
+        const uint64_t nk = lw ? NOKEY[(size_t)k * TW + lane] | DNE[(size_t)k * TW + lane] : ~0ull;
+        u = ~nk & ~u;
+      }
+      pass &= acc | u;
     }
-    // Fits on the requested resources
+    // Fits on the requested resources: the threshold row of the first allocatable >= the request
     for (uint32_t rm = rmask; rm; rm &= rm - 1) {
       const int r = __builtin_ctz(rm);
-      const int64_t need = lane_bcast_i64(rq_lane, r);
-      const bool staged = (lds_res >> r) & 1;
-      const int64_t LDS* sa = s_alloc + (size_t)__builtin_popcount(lds_res & ((1u << r) - 1)) * T;
-      const int64_t* ga = Cg.alloc + (size_t)r * T;
-      uint64_t fail = 0;
-#pragma unroll 4
-      for (int i = 0; i < tiles; i++) {
-        const int t = min(i * 64 + lane, T - 1);
-        const int64_t al = staged ? sa[t] : ga[t];
-        fail |= (uint64_t)(need > al) << i;
-      }
-      alive &= ~fail;
+      const int64_t need = lane_bcast_i64(cur.rq, r);
+      uint64_t nb = 0;
+      const int n = fit_n[r];
+      const int j = wave_lower_bound(fit_vals + (size_t)r * T, n, need, &nb);
+      pass &= (j < n && lw) ? fit_mask[((size_t)r * T + j) * TW + lane] : 0;
     }
-    // cheapest compatible available offering per type (min over the row's classes), mask words, output stream
-    double* oc = a.out_cheapest ? a.out_cheapest + (size_t)q * T : nullptr;
-    const double* ps = (!a.price_lds && Cg.price_sub) ? Cg.price_sub + (size_t)cls * T : nullptr;
-    uint64_t myword = 0;
-#pragma unroll 2
-    for (int i = 0; i < tiles; i++) {
-      const int t = i * 64 + lane;
-      const int tc = min(t, T - 1);
-      double ch = __builtin_huge_val();
-      if (a.price_lds) {
-        for (uint64_t m = cls; m; m &= m - 1) {
-          const double p = s_price[(size_t)__builtin_ctzll(m) * T + tc];
-          ch = p < ch ? p : ch;
-        }
-      } else if (ps) {
-        ch = ps[tc];
+    // an available offering of a compatible class
+    uint64_t av = 0;
+    for (uint64_t m = cls; m; m &= m - 1) av |= lw ? offer[(size_t)__builtin_ctzll(m) * TW + lane] : 0;
+    pass &= av;
+    if (lw) ((GLB uint64_t*)a.out_mask)[(size_t)q * TW + lane] = pass;
+    // cheapest compatible available offering price per type
+    if (a.out_cheapest) {
+      GLB double* oc = (GLB double*)a.out_cheapest + (size_t)q * T;
+      if (price_sub) {
+        const GLB double* ps = price_sub + (size_t)cls * T;
+        for (int t = lane; t < T; t += 64) oc[t] = ps[t];
       } else {
-        for (uint64_t m = cls; m; m &= m - 1) {
-          const double p = Cg.price_cm[(size_t)__builtin_ctzll(m) * T + tc];
-          ch = p < ch ? p : ch;
+        for (int t = lane; t < T; t += 64) {
+          double ch = __builtin_huge_val();
+          for (uint64_t m = cls; m; m &= m - 1) ch = fmin(ch, price_cm[(size_t)__builtin_ctzll(m) * T + t]);
+          oc[t] = ch;
         }
       }
-      const uint64_t bal = __ballot(((alive >> i) & 1) && ch < __builtin_huge_val());
-      if (lane == i) myword = bal;
-      if (oc && t < T) oc[t] = ch;
     }
-    if (lane < tiles) a.out_mask[(size_t)q * tiles + lane] = myword;
-    wave_sync();
   }
 }
-const void* feasibility_lds_kernel_ptr() { return (const void*)feasibility_lds_kernel; }
+const void* feasibility_bits_kernel_ptr() { return (const void*)feasibility_bits_kernel; }
 
 // ------------------------------------------------------------------------------------------------
 // launch_kernel: instance.DefaultProvider.Create's launch-side selection (R:pkg/providers/instance/instance.go:
@@ -3561,9 +3574,8 @@ hipError_t launch_launch(const LaunchArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 hipError_t launch_feasibility(const FeasArgs& a, hipStream_t s) {
-  if (a.lds_bytes > 0) {
-    hipLaunchKernelGGL(feasibility_lds_kernel, dim3((unsigned)max(1, a.blocks)), dim3(FEAS2_WAVES * 64),
-                       (size_t)a.lds_bytes, s, a);
+  if (a.bits) {
+    hipLaunchKernelGGL(feasibility_bits_kernel, dim3((unsigned)max(1, a.blocks)), dim3(FEASB_WAVES * 64), 0, s, a);
     return hipGetLastError();
   }
   long blocks = ((long)a.n_queries + FEAS_WAVES - 1) / FEAS_WAVES;

@@ -120,7 +120,11 @@ class TopologySpread(C.Structure):
 class PodAffinityTerm(C.Structure):
     _fields_ = [("topology_key", C.c_char_p), ("selector", LabelSelector), ("namespaces", C.POINTER(C.c_char_p)),
                 ("n_namespaces", C.c_uint32), ("weight", C.c_int32), ("has_namespace_selector", C.c_int32),
-                ("reserved_", C.c_int32)]
+                ("reserved_", C.c_int32), ("namespace_selector", LabelSelector)]
+
+
+class Namespace(C.Structure):
+    _fields_ = [("name", C.c_char_p), ("labels", C.POINTER(Label)), ("n_labels", C.c_uint32), ("reserved_", C.c_uint32)]
 
 
 class HostPort(C.Structure):
@@ -169,7 +173,7 @@ class SolveIn(C.Structure):
                 ("existing", C.POINTER(ExistingNode)), ("n_existing", C.c_uint32), ("n_shapes", C.c_uint32),
                 ("shapes", C.POINTER(PodShape)), ("pods", C.POINTER(Pod)), ("n_pods", C.c_uint32),
                 ("max_instance_types", C.c_uint32), ("bound_pods", C.POINTER(BoundPod)),
-                ("n_bound_pods", C.c_uint32), ("reserved_", C.c_uint32)]
+                ("n_bound_pods", C.c_uint32), ("n_namespaces", C.c_uint32), ("namespaces", C.POINTER(Namespace))]
 
 
 class NodeClaimInfo(C.Structure):
@@ -232,7 +236,7 @@ class Cluster(C.Structure):
                 ("nodes", C.POINTER(ClusterNode)), ("n_nodes", C.c_uint32), ("n_shapes", C.c_uint32),
                 ("shapes", C.POINTER(PodShape)), ("pods", C.POINTER(Pod)), ("n_pods", C.c_uint32),
                 ("spot_to_spot", C.c_uint32), ("pending_pods", C.POINTER(C.c_uint32)), ("n_pending", C.c_uint32),
-                ("reserved_", C.c_uint32)]
+                ("n_namespaces", C.c_uint32), ("namespaces", C.POINTER(Namespace))]
 
 
 class SimResult(C.Structure):
@@ -392,9 +396,18 @@ class Arena:
         out = []
         for t in terms:
             nss = self.arr(C.c_char_p, [self.s(n) for n in (t.namespaces or [])])
+            nsel = t.namespace_selector
             out.append(PodAffinityTerm(self.s(t.topology_key), self.selector(t.selector), nss, len(t.namespaces or []),
-                                       int(t.weight), 1 if t.namespace_selector else 0, 0))
+                                       int(t.weight), 0 if nsel is None else 1, 0, self.selector(nsel)))
         return self.arr(PodAffinityTerm, out), len(terms)
+
+    def namespaces(self, nss):
+        """{name: labels} -> kp_namespace[] (sorted by name)."""
+        out = []
+        for name in sorted(nss or {}):
+            lab, nl = self.labels(nss[name])
+            out.append(Namespace(self.s(name), lab, nl, 0))
+        return self.arr(Namespace, out), len(out)
 
     def host_ports(self, hps):
         """[(hostIP, hostPort, protocol)] -> kp_host_port[] (hostIP None/"" = 0.0.0.0, protocol None = TCP)."""
@@ -449,9 +462,10 @@ def build_solve_in(arena, problem, catalog_handles=None):
     arena.keep.append(pods_np)
     pods_ptr = pods_np.ctypes.data_as(C.POINTER(Pod))
     bps, nbp = arena.bound_pods(problem.bound_pods)
+    nsa, nns = arena.namespaces(getattr(problem, "namespaces", None))
     si = SolveIn(handles, descs, len(problem.catalogs), len(problem.nodepools), nps, ex, len(problem.existing),
                  len(problem.shapes), shapes, pods_ptr, len(problem.pod_shape), problem.max_instance_types,
-                 bps, nbp, 0)
+                 bps, nbp, nns, nsa if nns else None)
     arena.keep.append(si)
     return si
 
@@ -481,10 +495,11 @@ def build_cluster(arena, cl, catalog_handles=None):
     nodes_a = arena.arr(ClusterNode, nodes)
     shapes = arena.arr(PodShape, [arena.shape(s) for s in cl.shapes])
     pending = list(cl.pending)
+    nsa, nns = arena.namespaces(getattr(cl, "namespaces", None))
     c = Cluster(handles, descs, len(cl.catalogs), len(cl.nodepools), nps, nodes_a, len(cl.nodes), len(cl.shapes),
                 shapes, _pods_array(arena, cl.pod_shape, cl.pod_creation, cl.pod_uid), len(cl.pod_shape),
                 1 if cl.spot_to_spot else 0,
-                arena.arr(C.c_uint32, pending) if pending else None, len(pending), 0)
+                arena.arr(C.c_uint32, pending) if pending else None, len(pending), nns, nsa if nns else None)
     arena.keep.append(c)
     return c
 

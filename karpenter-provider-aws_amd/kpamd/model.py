@@ -79,12 +79,14 @@ class TopologySpread:
 
 @dataclass
 class PodAffinityTerm:
-    """corev1.PodAffinityTerm (+ weight for a WeightedPodAffinityTerm). namespaces empty = the pod's namespace."""
+    """corev1.PodAffinityTerm (+ weight for a WeightedPodAffinityTerm). namespaces empty and no namespace_selector =
+    the pod's namespace; a namespace_selector (LabelSelector; empty = every namespace) adds the problem's namespaces
+    whose labels it matches (Problem.namespaces / Cluster.namespaces)."""
     topology_key: str
     selector: Optional[LabelSelector] = None
     namespaces: List[str] = field(default_factory=list)
     weight: int = 0
-    namespace_selector: bool = False
+    namespace_selector: Optional[LabelSelector] = None
 
 
 @dataclass
@@ -139,6 +141,7 @@ class Cluster:
     name: str = ""
     pending: List[int] = field(default_factory=list)  # provisionable pods bound to no node (indices into pod_*)
     spot_to_spot: bool = False                         # SpotToSpotConsolidation feature gate
+    namespaces: Dict[str, Dict[str, str]] = field(default_factory=dict)  # cluster namespaces: name -> labels
 
 
 @dataclass
@@ -153,6 +156,7 @@ class Problem:
     max_instance_types: int = 100
     name: str = ""
     bound_pods: List[Tuple[str, Dict[str, str], int]] = field(default_factory=list)  # (namespace, labels, existing idx)
+    namespaces: Dict[str, Dict[str, str]] = field(default_factory=dict)  # cluster namespaces: name -> labels
 
     @property
     def n_pods(self):

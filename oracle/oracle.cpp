@@ -725,12 +725,33 @@ static Selector SelectorFromABI(const kp_label_selector& s) {
   }
   return o;
 }
-static AntiTerm AntiFromABI(const kp_pod_affinity_term& t, const string& podNs) {
+// The cluster's namespaces (kp_solve_in.namespaces) a namespaceSelector lists.
+struct NamespaceList {
+  vector<std::pair<string, map<string, string>>> items;
+};
+static NamespaceList NamespacesFromABI(const kp_namespace* ns, uint32_t n) {
+  NamespaceList o;
+  for (uint32_t i = 0; i < n; i++) {
+    map<string, string> l;
+    for (uint32_t j = 0; j < ns[i].n_labels; j++) l[ns[i].labels[j].key] = ns[i].labels[j].value ? ns[i].labels[j].value : "";
+    o.items.push_back({ns[i].name ? ns[i].name : "", l});
+  }
+  return o;
+}
+// UP Topology.buildNamespaceList: no namespaces and no namespaceSelector -> the pod's own namespace; otherwise the
+// term's namespaces plus every namespace the namespaceSelector selects (kubeClient.List with its LabelSelector)
+static AntiTerm AntiFromABI(const kp_pod_affinity_term& t, const string& podNs, const NamespaceList& nsl) {
   AntiTerm a;
   a.key = t.topology_key ? t.topology_key : "";
   a.sel = SelectorFromABI(t.selector);
   for (uint32_t i = 0; i < t.n_namespaces; i++) a.namespaces.insert(t.namespaces[i] ? t.namespaces[i] : "");
-  if (a.namespaces.empty()) a.namespaces.insert(podNs);
+  if (t.has_namespace_selector) {
+    const Selector ns = SelectorFromABI(t.namespace_selector);
+    for (auto& item : nsl.items)
+      if (ns.Matches(item.second)) a.namespaces.insert(item.first);
+  } else if (a.namespaces.empty()) {
+    a.namespaces.insert(podNs);
+  }
   a.weight = t.weight;
   return a;
 }
@@ -1450,6 +1471,7 @@ using Catalogs = std::vector<std::shared_ptr<std::vector<InstanceType>>>;
 
 // Provisioner.NewScheduler + Scheduler.Solve + Results.TruncateInstanceTypes over already-converted catalogues.
 static int32_t SolveCore(const Catalogs& cats, const kp_solve_in* in, kpo_result** out) {
+  const NamespaceList nsl = NamespacesFromABI(in->namespaces, in->n_namespaces);
   auto t0 = std::chrono::steady_clock::now();
   Scheduler s;
   // NewScheduler: templates per NodePool ordered by weight desc, name asc; options pre-filtered by the
@@ -1500,8 +1522,7 @@ static int32_t SolveCore(const Catalogs& cats, const kp_solve_in* in, kpo_result
     for (uint32_t j = 0; j < b.n_labels; j++) bp.labels[b.labels[j].key] = b.labels[j].value ? b.labels[j].value : "";
     bp.node = (int)b.node;
     for (uint32_t j = 0; j < b.n_anti_affinity; j++) {
-      if (b.anti_affinity[j].has_namespace_selector) return KP_E_UNSUPPORTED;
-      bp.anti.push_back(AntiFromABI(b.anti_affinity[j], bp.ns));
+      bp.anti.push_back(AntiFromABI(b.anti_affinity[j], bp.ns, nsl));
     }
     topo.bound.push_back(std::move(bp));
   }
@@ -1589,20 +1610,16 @@ static int32_t SolveCore(const Catalogs& cats, const kp_solve_in* in, kpo_result
     ps.ns = sh.namespace_ ? sh.namespace_ : "";
     for (uint32_t j = 0; j < sh.n_labels; j++) ps.labels[sh.labels[j].key] = sh.labels[j].value ? sh.labels[j].value : "";
     for (uint32_t j = 0; j < sh.n_required_affinity; j++) {
-      if (sh.required_affinity[j].has_namespace_selector) return KP_E_UNSUPPORTED;
-      ps.affRequired.push_back(AntiFromABI(sh.required_affinity[j], ps.ns));
+      ps.affRequired.push_back(AntiFromABI(sh.required_affinity[j], ps.ns, nsl));
     }
     for (uint32_t j = 0; j < sh.n_preferred_affinity; j++) {
-      if (sh.preferred_affinity[j].has_namespace_selector) return KP_E_UNSUPPORTED;
-      ps.affPreferred.push_back(AntiFromABI(sh.preferred_affinity[j], ps.ns));
+      ps.affPreferred.push_back(AntiFromABI(sh.preferred_affinity[j], ps.ns, nsl));
     }
     for (uint32_t j = 0; j < sh.n_required_anti_affinity; j++) {
-      if (sh.required_anti_affinity[j].has_namespace_selector) return KP_E_UNSUPPORTED;
-      ps.antiRequired.push_back(AntiFromABI(sh.required_anti_affinity[j], ps.ns));
+      ps.antiRequired.push_back(AntiFromABI(sh.required_anti_affinity[j], ps.ns, nsl));
     }
     for (uint32_t j = 0; j < sh.n_preferred_anti_affinity; j++) {
-      if (sh.preferred_anti_affinity[j].has_namespace_selector) return KP_E_UNSUPPORTED;
-      ps.antiPreferred.push_back(AntiFromABI(sh.preferred_anti_affinity[j], ps.ns));
+      ps.antiPreferred.push_back(AntiFromABI(sh.preferred_anti_affinity[j], ps.ns, nsl));
     }
     for (uint32_t j = 0; j < sh.n_topology_spread; j++) {
       const kp_topology_spread& t = sh.topology_spread[j];
@@ -1845,6 +1862,8 @@ int32_t kpo_simulate_batch(const kp_cluster* cl, const uint32_t* offsets, const 
     in.max_instance_types = 100;
     in.bound_pods = bound.data();
     in.n_bound_pods = (uint32_t)bound.size();
+    in.namespaces = cl->namespaces;
+    in.n_namespaces = cl->n_namespaces;
     kpo_result* res = nullptr;
     int32_t rc = SolveCore(cats, &in, &res);
     if (rc) return rc;

@@ -5,8 +5,9 @@ avoid the bound pod's node), TopologyTypePodAffinity (nextDomainAffinity: a node
 domain has one and the pod selects itself — any node: the bootstrap), and Preferences.Relax's
 removePreferredPodAffinityTerm / removePreferredPodAntiAffinityTerm (heaviest first, before the preferred
 node-affinity terms). Docs: R:website/content/en/preview/concepts/scheduling.md:395-428 (the anti-affinity
-example "avoid running on any node with a pod labeled app=inflate": one replica per node). A namespaceSelector
-returns KP_E_UNSUPPORTED (the Go path runs).
+example "avoid running on any node with a pod labeled app=inflate": one replica per node). A namespaceSelector adds
+the cluster namespaces whose labels it matches (upstream Topology.buildNamespaceList; ABI v8: kp_solve_in.namespaces),
+docs R:website/content/en/preview/concepts/scheduling.md:394-428.
 
 Known answers on the CPU oracle, device == oracle under -m gpu (Solve and consolidation simulations). Parity
 unpinned beyond the written semantics (upstream core is not in the container)."""
@@ -161,12 +162,58 @@ def test_zone_affinity_follows_the_first(catalog):
     assert zs == {("test-zone-1a",)}
 
 
-def test_unsupported_variants(catalog):
-    import kpamd
+NAMESPACES = {"team-a": {"team": "a", "env": "prod"}, "team-b": {"team": "b", "env": "prod"},
+              "sandbox": {"env": "dev"}, "default": {}}
+
+
+def nsanti(app, nsel, namespaces=(), key=HOST, weight=0):
+    """An anti-affinity term with a namespaceSelector (LabelSelector; {} = every namespace)."""
     from kpamd.model import LabelSelector, PodAffinityTerm
-    nss = small_problem(catalog, [shape("web", req=[PodAffinityTerm(HOST, LabelSelector({"app": "web"}),
-                                                                    namespace_selector=True)])], [2])
-    assert kpamd.validate(nss) == kpamd.abi.KP_E_UNSUPPORTED
+    sel = LabelSelector(dict(nsel)) if isinstance(nsel, dict) else nsel
+    return PodAffinityTerm(key, LabelSelector({"app": app}), list(namespaces), weight, namespace_selector=sel)
+
+
+def _ns_problem(catalog, term, bound_ns, pod_ns="default"):
+    """node-a runs one bound app=web pod in namespace bound_ns; a new pod (namespace pod_ns) carries `term`."""
+    node = m5_node(catalog)
+    sh = shape("api", req=[term])
+    sh.namespace = pod_ns
+    prob = small_problem(catalog, [sh], [1], existing=[node])
+    prob.bound_pods = [(bound_ns, {"app": "web"}, 0)]
+    prob.namespaces = dict(NAMESPACES)
+    return prob
+
+
+@pytest.mark.parametrize("nsel,bound_ns,avoids", [
+    ({"team": "a"}, "team-a", True),      # the selector picks team-a, where the web pod runs: node-a is avoided
+    ({"team": "b"}, "team-a", False),     # picks team-b only: the team-a pod is not counted
+    ({}, "sandbox", True),                # an empty selector selects every namespace
+    ({"env": "prod"}, "sandbox", False),  # prod namespaces only
+])
+def test_namespace_selector(catalog, nsel, bound_ns, avoids):
+    pl = oracle(_ns_problem(catalog, nsanti("web", nsel), bound_ns))["placement"].tolist()
+    assert (pl[0] >= 0) == avoids and (pl[0] == -2) == (not avoids)
+
+
+def test_namespace_selector_adds_to_listed_namespaces(catalog):
+    # namespaces ["sandbox"] plus the selector's team-b: a web pod in sandbox is counted, one in team-a is not
+    assert oracle(_ns_problem(catalog, nsanti("web", {"team": "b"}, ["sandbox"]), "sandbox"))["placement"][0] >= 0
+    assert oracle(_ns_problem(catalog, nsanti("web", {"team": "b"}, ["sandbox"]), "team-a"))["placement"][0] == -2
+
+
+def test_namespace_selector_expressions_and_own_namespace(catalog):
+    # a selector given: the pod's own namespace is not implied (upstream buildNamespaceList)
+    from kpamd.model import LabelSelector
+    sel = LabelSelector({}, [("team", "In", ["a", "b"])])
+    assert oracle(_ns_problem(catalog, nsanti("web", sel), "default", pod_ns="default"))["placement"][0] == -2
+    assert oracle(_ns_problem(catalog, nsanti("web", sel), "team-b"))["placement"][0] >= 0
+    sel = LabelSelector({}, [("team", "DoesNotExist", [])])
+    assert oracle(_ns_problem(catalog, nsanti("web", sel), "sandbox"))["placement"][0] >= 0
+
+
+def test_namespace_selector_host_compile(catalog):
+    import kpamd
+    assert kpamd.validate(_ns_problem(catalog, nsanti("web", {"team": "a"}), "team-a")) == 0
     assert kpamd.validate(small_problem(catalog, [shape("web", req=[anti("web")])], [2])) == 0
 
 
@@ -174,6 +221,7 @@ def test_unsupported_variants(catalog):
 def add_anti(prob, seed, p=0.4):
     rng = np.random.default_rng(seed)
     prob = copy.deepcopy(prob)
+    prob.namespaces = dict(NAMESPACES)
     apps = [f"app-{i}" for i in range(4)]
     for i, sh in enumerate(prob.shapes):
         sh.labels = dict(sh.labels or {}, app=apps[i % 4])
@@ -192,6 +240,15 @@ def add_anti(prob, seed, p=0.4):
             terms = [anti(str(rng.choice(apps)))] if rng.random() < 0.3 else []
             bound.append(("default", {"app": str(rng.choice(apps))}, e, terms))
     prob.bound_pods = bound
+    # namespaces and namespaceSelectors (a separate stream: the draws above stay as they were)
+    r2 = np.random.default_rng(seed + 1000)
+    nss, sels = sorted(NAMESPACES), [{"team": "a"}, {}, {"env": "prod"}, {"team": "b"}]
+    for sh in prob.shapes:
+        sh.namespace = str(r2.choice(nss))
+        sh.required_anti_affinity = [nsanti(t.selector.match_labels["app"], sels[int(r2.integers(len(sels)))],
+                                            key=t.topology_key) if r2.random() < 0.5 else t
+                                     for t in (sh.required_anti_affinity or [])]
+    prob.bound_pods = [(str(r2.choice(nss)), lab, e, terms) for _, lab, e, terms in prob.bound_pods]
     return prob
 
 
@@ -266,3 +323,16 @@ def test_gpu_consolidation_anti_affinity(ctx, catalog, seed):
     subs = synth.consolidation_subsets(cl, 15, seed=seed, max_size=min(12, len(cl.nodes)))
     subs += [[c] for c in cl.candidates[:10]]
     check(ctx, cl, subs, multi_node=bool(seed % 2))
+
+
+@pytest.mark.gpu
+def test_gpu_namespace_selector(ctx, catalog):
+    """namespaceSelector on the device (host compile resolves the namespaces) == the oracle."""
+    import kpamd
+    from kpamd.model import LabelSelector
+    from test_gpu_parity import check_same
+    cases = [({"team": "a"}, "team-a"), ({"team": "b"}, "team-a"), ({}, "sandbox"), ({"env": "prod"}, "sandbox"),
+             (LabelSelector({}, [("team", "In", ["a", "b"])]), "team-b")]
+    for nsel, bound_ns in cases:
+        prob = _ns_problem(catalog, nsanti("web", nsel), bound_ns)
+        check_same(kpamd.Scheduler(ctx, prob).solve(), oracle(prob))

@@ -16,7 +16,7 @@ ctx = kpamd.Context(0)
 ch = kpamd.Catalog(ctx, cat)
 qs = synth.distinct_queries(cat, rows)
 out = {}
-KNOBS = ("KP_FEAS_GLOBAL", "KP_FEAS_NO_KEYS", "KP_FEAS_NO_RES", "KP_FEAS_NO_PRICE", "KP_FEAS_BLOCKS")
+KNOBS = ("KP_FEAS_GLOBAL", "KP_FEAS_NO_KEYS", "KP_FEAS_NO_RES", "KP_FEAS_NO_PRICE", "KP_FEAS_BLOCKS", "KP_FEAS_DBG")
 for spec in sys.argv[1:] or ["lds"]:
     name, _, envs = spec.partition("=")
     for k in KNOBS:
@@ -27,7 +27,10 @@ for spec in sys.argv[1:] or ["lds"]:
     for cheapest in (True, False):
         fp = kpamd.FilterPlan(ctx, ch, qs, cheapest=cheapest)
         fp.run()
-        ms = sorted(fp.run()["device_ms"] for _ in range(int(os.environ.get("FEAS_REPS", "10"))))
+        sts = [fp.run() for _ in range(int(os.environ.get("FEAS_REPS", "10")))]
+        ms = sorted(x["device_ms"] for x in sts)
+        if os.environ.get("KP_TIMING"):
+            out[f"{name}{'' if cheapest else '_nocheapest'}_phases"] = sts[-1]["phase_cycles"][:4]
         fp.close()
         out[f"{name}{'' if cheapest else '_nocheapest'}"] = round(ms[len(ms) // 2], 4)
 print(json.dumps(out), flush=True)

@@ -15,4 +15,14 @@ for f in glob.glob('gpurun_out/pmc_*/**/*counter_collection.csv', recursive=True
 pops = 50000  # one launch
 for k, v in sorted(acc.items()):
     print(f"{k:22s} {v:16.0f} per_pop {v / pops:10.1f}")
+# the latency roofline bench.py reads (profiles/latency.json): SQ cycle counters count 4-cycle units summed over the
+# workgroup's waves (SQ_WAVE_CYCLES per pod = the measured wall cycles per pod), so the issue floor is 4 x ACTIVE_INST_ANY
+import json
+ins = sum(acc.get(k, 0) for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM", "SQ_INSTS_SMEM",
+                                  "SQ_INSTS_BRANCH")) / pops
+json.dump({"issue_cycles_per_pod": round(4 * acc["SQ_ACTIVE_INST_ANY"] / pops, 1), "instructions_per_pod": round(ins, 1),
+           "wave_cycles_per_pod": round(4 * acc["SQ_WAVE_CYCLES"] / pops / max(1, acc.get("SQ_WAVES", 4)) , 1),
+           "wait_cycles_per_pod": round(4 * acc["SQ_WAIT_ANY"] / pops, 1),
+           "source": "tools/pmc_sq.sh: rocprofv3 --pmc SQ counters over one config-2 Solve (50k pods)"},
+          open("gpurun_out/latency.json", "w"), indent=1)
 PY
