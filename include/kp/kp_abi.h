@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define KP_ABI_VERSION 8
+#define KP_ABI_VERSION 9
 
 enum kp_status {
   KP_OK = 0,
@@ -345,7 +345,16 @@ typedef struct kp_solve_in {
   uint32_t n_bound_pods;
   uint32_t n_namespaces;           /* ABI v8: the cluster's namespaces (pod affinity namespaceSelector) */
   const kp_namespace* namespaces;
+  /* ABI v9: capacity reservations inside the Solve (upstream NodeClaim.Add reserveOfferings + ReservationManager,
+   * designed in R:designs/odcr.md:248-256): KP_RESERVED_FALLBACK (0, the scheduler's default) never fails an Add for
+   * want of reservation capacity; KP_RESERVED_STRICT (1, the provisioner's DisableReservedCapacityFallback) fails an
+   * Add whose NodeClaim is compatible with reserved offerings it cannot reserve, and does not relax the pod then. */
+  uint32_t reserved_offering_mode;
+  uint32_t reserved2_;
 } kp_solve_in;
+
+#define KP_RESERVED_FALLBACK 0
+#define KP_RESERVED_STRICT 1
 
 typedef struct kp_nodeclaim_info {
   uint32_t nodepool;        /* index into kp_solve_in.nodepools */
@@ -387,6 +396,8 @@ typedef struct kp_solve_stats {
   uint64_t fast_bails[8];   /* pods the fast lane handed to the full path: ineligible (topology / existing nodes),
                                spilled sort arrays, long sort shift, long scan, requirement merge, minValues,
                                no in-flight NodeClaim took it, reserved */
+  uint64_t reserved_offering_errors; /* ABI v9: pops whose addToNewNodeClaim failed on a ReservedOfferingError (strict
+                                        mode; upstream Results.ReservedOfferingErrors: deferred, not relaxed) */
 } kp_solve_stats;
 
 /* ---- context ---------------------------------------------------------------------------- */

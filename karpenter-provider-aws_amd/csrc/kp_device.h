@@ -5,7 +5,7 @@
 
 #include "kp_model.h"
 
-#define KP_SOLVE_STATS 40
+#define KP_SOLVE_STATS 48
 // why the fast lane handed a popped pod to the full path (stats[32 + FB_*])
 enum { FB_INELIGIBLE = 0, FB_SPILLED = 1, FB_SHIFT = 2, FB_SCAN = 3, FB_MERGE = 4, FB_MINVALUES = 5, FB_NONE = 6 };
 
@@ -126,7 +126,16 @@ struct SolveArgs {
   int32_t* events;                   // [P] pods in placement order
   uint64_t* stats;                   // [KP_SOLVE_STATS]: attempts, bytes, pops, n_nc, n_events, scanned, starts; [7] runaway;
                                      // [8..15] phases, [16..23] attempt split, [24] fast-lane pods, [25..30] fast-lane
-                                     // cycles, [31] literal pdqsorts, [32..39] fast-lane hand-offs by reason (FB_*)
+                                     // cycles, [31] literal pdqsorts, [32..39] fast-lane hand-offs by reason (FB_*),
+                                     // [40] pops whose addToNewNodeClaim failed on a ReservedOfferingError
+  // capacity reservations (upstream ReservationManager + NodeClaim.reserveOfferings): res_mode 0 none, 1 fallback,
+  // 2 strict. A reservation id is one offering class (res_cls); its remaining capacity lives in LDS during the Solve,
+  // starting from res_cap0; nc_held[nc] = the classes NodeClaim nc holds (zeroed per run)
+  int32_t res_mode;
+  int32_t res_pad_;
+  uint64_t res_cls;
+  uint64_t* nc_held;                 // [P]
+  int32_t res_cap0[KP_MAX_CLASSES];
 };
 
 // tmpl_feas_kernel: rows [row_lo, row_hi) of shape-levels x every template
@@ -169,6 +178,7 @@ struct FinalizeArgs {
   uint32_t* out_options;     // [n_nc][opt_stride]
   uint32_t* out_n_remaining; // [n_nc]
   uint32_t* out_n_options;   // [n_nc]
+  const uint64_t* nc_held;   // [n_nc] reservation classes held (FinalizeScheduling: reservation-id In {..}), or null
 };
 
 struct FeasArgs {

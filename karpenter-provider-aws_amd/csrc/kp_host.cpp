@@ -1150,7 +1150,41 @@ struct SolveBase {
   size_t o_dict = 0, o_vint = 0, o_cats = 0, o_treqs = 0, o_tts = 0, o_tcat = 0, o_tX = 0, o_tdm = 0;
   vector<CatOffsets> coffs;
   double build_ms = 0;
+  // capacity reservations (NewReservationManager): the reserved offering classes (one per reservation id) and the
+  // least ReservationCapacity the NodePools' catalogues report for each
+  uint64_t res_cls = 0;
+  vector<int32_t> res_cap0;
 };
+
+// NewReservationManager's starting capacities (UP reservationmanager.go: the least ReservationCapacity any NodePool's
+// instance types report for an id). Requires one class per reservation id (a reservation is one type in one zone).
+int32_t ReservationTables(SolveBase& b) {
+  b.res_cls = 0;
+  b.res_cap0.assign(KP_MAX_CLASSES, 0);
+  const int ct = b.d.key(kCapType), res = ct >= 0 ? b.d.bit(ct, "reserved") : -1;
+  if (res < 0) return KP_OK;
+  map<int, int> rid_class;
+  for (int c = 0; c < b.C; c++) {
+    if (b.classes[c].ct_bit != res) continue;
+    if (b.classes[c].rid_bit < 0) return fail(KP_E_UNSUPPORTED, "reserved offering class without a reservation id");
+    if (!rid_class.emplace(b.classes[c].rid_bit, c).second)
+      return fail(KP_E_UNSUPPORTED, "one capacity reservation in two offering classes");
+    b.res_cls |= 1ull << c;
+    b.res_cap0[c] = INT32_MAX;
+  }
+  if (!b.res_cls) return KP_OK;
+  map<ClassKey, int> classes;
+  for (int c = 0; c < b.C; c++) classes[KeyOfClass(b.classes[c])] = c;
+  for (int np = 0; np < (int)b.np_catalog.size(); np++)
+    for (auto& t : b.catalogs[b.np_catalog[np]]->types)
+      for (auto& o : t.offs) {
+        const int c = classes.at(ClassOf(b.d, o));
+        if ((b.res_cls >> c) & 1) b.res_cap0[c] = std::min(b.res_cap0[c], std::max(o.rcap, 0));
+      }
+  for (int c = 0; c < b.C; c++)
+    if (b.res_cap0[c] == INT32_MAX) b.res_cap0[c] = 0;  // only in catalogues no NodePool uses
+  return KP_OK;
+}
 
 struct Compiled {
   std::shared_ptr<SolveBase> B = std::make_shared<SolveBase>();
@@ -2014,8 +2048,6 @@ int32_t BuildBase(const kp_solve_in* in, const SolveRaw& raw, SolveBase& b) {
   DictBuilder db;
   int maxT = 1;
   for (auto* c : cats) {
-    if (c->reservations)  // NodeClaim.Add's reserveOfferings (upstream ReservationManager) is not modelled
-      return fail(KP_E_UNSUPPORTED, "capacity-reservation offerings in a Solve / cluster catalogue");
     maxT = std::max(maxT, (int)c->types.size());
     for (auto& t : c->types) {
       db.addReqs(t.reqs);
@@ -2023,6 +2055,8 @@ int32_t BuildBase(const kp_solve_in* in, const SolveRaw& raw, SolveBase& b) {
         db.addLabel(kCapType, o.ct);
         if (o.has_zone) db.addLabel(kZone, o.zone);
         if (o.has_zid) db.addLabel(kZoneID, o.zid);
+        if (o.has_rid) db.addLabel(kResID, o.rid);
+        if (o.has_rt) db.addLabel(kResType, o.rt);
       }
     }
   }
@@ -2105,6 +2139,9 @@ int32_t BuildBase(const kp_solve_in* in, const SolveRaw& raw, SolveBase& b) {
   }
   b.catalogs = cats;
   b.seqnums = SeqnumsOf(cats);
+  rc = ReservationTables(b);
+  if (rc) return rc;
+  b.d.dd.res_any = b.res_cls ? 1 : 0;
   BuildTemplates(b, b.tmpl_nodepool, b.tmpl_X);
   for (int i : b.tmpl_nodepool) {
     b.tmpl_reqs.push_back(b.np_q[i]);
@@ -2309,6 +2346,7 @@ int32_t RefreshOfferings(kp_ctx* ctx, SolveBase& b) {
     return 1;
   }
   b.tmpl_X.swap(tX);
+  if (ReservationTables(b)) return 1;  // (reservation classes are fixed by the dictionary: cannot fail here)
   b.seqnums = SeqnumsOf(b.catalogs);
   b.key = b.ident + SeqKey(b.seqnums);
   b.version++;
@@ -2519,7 +2557,7 @@ struct kp_solve_plan {
   double catalog_ms = 0;  // SolveBase build time when this prepare missed the cache, else 0
   size_t o_mut = 0, n_mut = 0, o_pristine = 0, o_ver = 0, n_ver = 0, o_fail = 0, n_fail = 0;
   size_t o_stats = 0, o_npods = 0, o_place = 0, o_events = 0, o_nct = 0, o_ncrq = 0, o_opts = 0, o_nrem = 0,
-         o_nopt = 0, o_ncr = 0, o_hcnc = 0, n_hcnc = 0;
+         o_nopt = 0, o_ncr = 0, o_hcnc = 0, n_hcnc = 0, o_held = 0;
   int opt_stride = 0, P = 0, Pc = 1;
   uint32_t max_types = 0;
   bool any_min = false;
@@ -2720,6 +2758,7 @@ static int32_t SolvePrepareLocal(kp_ctx* ctx, const kp_solve_in* in, kp_comm* co
   const size_t o_tver = blob.reserve_dev(sizeof(int32_t) * std::max(NT, 1));
   const size_t o_curnc = blob.reserve_dev(sizeof(int32_t) * 2 * SLn);  // cursors start at {0, 0} (zeroed per run)
   const size_t o_curex = blob.reserve_dev(sizeof(int32_t) * 2 * SLn);
+  const size_t o_held = blob.reserve_dev(C.B->res_cls ? sizeof(uint64_t) * (size_t)Pc : 8);
   const size_t n_ver = blob.total() - o_ver0;
   const size_t o_fail0 = blob.reserve_dev(0);
   const size_t o_ncfail = blob.reserve_dev(sizeof(int32_t) * SLn * ncc);
@@ -2868,6 +2907,11 @@ static int32_t SolvePrepareLocal(kp_ctx* ctx, const kp_solve_in* in, kp_comm* co
   a.placement = (int32_t*)(base + o_place);
   a.events = (int32_t*)(base + o_events);
   a.stats = (uint64_t*)(base + o_stats);
+  a.res_mode = !C.B->res_cls ? 0 : in->reserved_offering_mode == KP_RESERVED_STRICT ? 2 : 1;
+  a.res_cls = C.B->res_cls;
+  a.nc_held = (uint64_t*)(base + o_held);
+  for (int c = 0; c < KP_MAX_CLASSES; c++) a.res_cap0[c] = C.B->res_cap0.empty() ? 0 : C.B->res_cap0[c];
+  plan->o_held = o_held;
   if (tfeas_on) {  // this rank's rows of the template-options table, then one all-gather (RCCL) of every rank's rows
     TfeasArgs f;
     memset(&f, 0, sizeof f);
@@ -2953,6 +2997,7 @@ int32_t kp_solve_refresh(kp_solve_plan* plan) {
     HIPCHK(launch_tmpl_feas(plan->tf, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
   }
+  for (int c = 0; c < KP_MAX_CLASSES; c++) plan->a.res_cap0[c] = B.res_cap0.empty() ? 0 : B.res_cap0[c];
   plan->base_version = B.version;
   return KP_OK;
 }
@@ -3017,6 +3062,7 @@ int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out) {
   f.out_options = (uint32_t*)(base + plan->o_opts);
   f.out_n_remaining = (uint32_t*)(base + plan->o_nrem);
   f.out_n_options = (uint32_t*)(base + plan->o_nopt);
+  f.nc_held = a.res_mode ? a.nc_held : nullptr;
   HIPCHK(hipEventRecord(ctx->ev2, st));
   HIPCHK(launch_finalize(f, st));
   HIPCHK(hipEventRecord(ctx->ev3, st));
@@ -3038,11 +3084,30 @@ int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out) {
     HIPCHK(hipMemcpyAsync(nopt.data(), base + plan->o_nopt, sizeof(uint32_t) * n_nc, hipMemcpyDeviceToHost, st));
   }
   vector<KReqs> fin;
+  vector<uint64_t> held;
   if (n_nc) {
     fin.resize(n_nc);
     HIPCHK(hipMemcpyAsync(fin.data(), base + plan->o_ncr, sizeof(KReqs) * n_nc, hipMemcpyDeviceToHost, st));
+    if (a.res_mode) {
+      held.resize(n_nc);
+      HIPCHK(hipMemcpyAsync(held.data(), base + plan->o_held, sizeof(uint64_t) * n_nc, hipMemcpyDeviceToHost, st));
+    }
   }
   HIPCHK(hipStreamSynchronize(st));
+  // FinalizeScheduling: a NodeClaim holding reservations launches only into them (reservation-id In {held ids}; the
+  // held classes are compatible with its requirements, so the intersection is exactly that set)
+  for (int i = 0; i < (int)held.size(); i++) {
+    if (!held[i]) continue;
+    const int k = d.key(kResID);
+    KReqs& q = fin[i];
+    for (int wi = 0; wi < nwords(d, k); wi++) q.vals[kw(d, k, wi)] = 0;
+    for (uint64_t m = held[i]; m; m &= m - 1) {
+      const int bit = C.B->classes[__builtin_ctzll(m)].rid_bit;
+      q.vals[bit / 64] |= 1ull << (bit % 64);
+    }
+    q.present |= 1ull << k;
+    q.compl_ &= ~(1ull << k);
+  }
   float ms_solve = 0, ms_fin = 0;
   HIPCHK(hipEventElapsedTime(&ms_solve, ctx->ev0, ctx->ev1));
   HIPCHK(hipEventElapsedTime(&ms_fin, ctx->ev2, ctx->ev3));
@@ -3102,6 +3167,7 @@ int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out) {
   res->stats.slow_sorts = stats[31];
   for (int i = 0; i < 6; i++) res->stats.fast_cycles[i] = stats[25 + i];
   for (int i = 0; i < 8; i++) res->stats.fast_bails[i] = stats[32 + i];
+  res->stats.reserved_offering_errors = stats[40];
   res->stats.host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   *out = res.release();
   return KP_OK;
@@ -3902,6 +3968,9 @@ int32_t kp_cluster_prepare(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan** 
   auto t0 = std::chrono::steady_clock::now();
   if (!ctx || !cl || !out) return fail(KP_E_INVAL, "null argument");
   if (cl->n_nodes && !cl->nodes) return fail(KP_E_INVAL, "null nodes");
+  for (uint32_t i = 0; i < cl->n_catalogs; i++)  // SimulateScheduling's reservation accounting is not modelled
+    if (cl->catalogs && cl->catalogs[i] && cl->catalogs[i]->reservations)
+      return fail(KP_E_UNSUPPORTED, "capacity-reservation offerings in a cluster catalogue");
   bool topo = false;
   for (uint32_t i = 0; i < cl->n_shapes; i++)
     topo |= cl->shapes[i].n_topology_spread > 0 || PodTermCount(cl->shapes[i]) > 0;

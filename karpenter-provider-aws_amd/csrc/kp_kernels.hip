@@ -359,6 +359,7 @@ __device__ __forceinline__ bool bit_of(uint64_t allowed_lane_word, int bit) {
 // RES = false (Solve, consolidation: their catalogues hold no reservation classes) skips the reservation bits.
 template <bool RES = false, class ClsP>
 __device__ uint64_t allowed_classes(const DevDict& D, ClsP cls_tab, const ReqView& rv, uint64_t allowed, uint64_t negR) {
+  if (!RES && D.res_any) return allowed_classes<true>(D, cls_tab, rv, allowed, negR);  // Solve over reservations
   const bool res_ok = !(rv.present & D.resid_key_bit) || (negR & D.resid_key_bit);
   const bool rt_ok = !(rv.present & D.restype_key_bit) || (negR & D.restype_key_bit);
   // lane c evaluates class c: its value bits are fetched from the owning lanes' allowed words
@@ -656,6 +657,38 @@ __device__ __forceinline__ uint64_t filter_types(const DevDict& D, const CatHdr 
 #undef TSUB
   *bytes += nb;
   return X;
+}
+
+// NodeClaim.reserveOfferings (upstream nodeclaim.go; design R:designs/odcr.md:248-256) on a wave: M = the reserved
+// classes (one per reservation id) compatible with the NodeClaim's new requirements (rv, m_v) that offer an available
+// offering among its remaining types X; the held set becomes (held ∩ M) ∪ {c ∈ M \ held : capacity left}. Strict mode
+// (ReservedOfferingModeStrict) fails when that is empty while M or held is not: returns ~0 then.
+__device__ uint64_t reserve_classes(const DevDict& D, const CatHdr LDS* H, const ReqView& rv, uint64_t m_v, uint64_t X,
+                                    uint64_t res_cls, uint64_t held, const int32_t LDS* cap, bool strict, const VInt& vint) {
+  const int lane = LANE;
+  const uint64_t negM = negop_mask(rv.present, rv.compl_, rv.nz);
+  const uint64_t allowed = allowed_word(D, rv, m_v, vint);
+  uint64_t cls = (D.C <= HDR_CLS ? allowed_classes<true>(D, H->cls, rv, allowed, negM)
+                                 : allowed_classes<true>(D, H->d.cls, rv, allowed, negM)) & res_cls;
+  uint64_t M = 0;
+  while (cls) {
+    const int c = __builtin_ctzll(cls);
+    cls &= cls - 1;
+    const uint64_t row = lane < D.TW ? H->d.offer_avail[(size_t)c * D.TW + lane] : 0;
+    if (__ballot((row & X) != 0)) M |= 1ull << c;
+  }
+  const uint64_t free = __ballot(lane < D.C && cap[lane] > 0);
+  const uint64_t nh = (held & M) | (M & ~held & free);
+  return strict && !nh && (M | held) ? ~0ull : nh;
+}
+
+// A reservation commit on the wave: capacity of the newly held classes down, of the released ones up.
+__device__ __forceinline__ void reserve_commit(int32_t LDS* cap, uint64_t held, uint64_t nh) {
+  const int lane = LANE;
+  if (lane < 64) {
+    if (((nh & ~held) >> lane) & 1) cap[lane] -= 1;
+    if (((held & ~nh) >> lane) & 1) cap[lane] += 1;
+  }
 }
 
 // Algorithmic-byte accounting of fits_lean: bytes directly (uint64_t), or event counts the caller converts once
@@ -1916,6 +1949,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
   auto& s_hdr = g_hdr;  // catalogue descriptors 0..7
   __shared__ CatHdr s_hdrw[NW];                       // per-wave descriptor of a catalogue >= 8
   extern __shared__ int32_t s_dyn[];  // ord[a.sort_cap], npods[a.sort_cap] while n_nc <= a.sort_cap
+  __shared__ int32_t s_rcap[KP_MAX_CLASSES];  // remaining capacity per reservation class (ReservationManager)
 
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
@@ -1923,6 +1957,8 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
   block_copy(D, a.dict);
   __syncthreads();
   for (int i = tid; i < D.KB * 64; i += NT) s_vint[i] = a.vint[i];
+  if (tid < KP_MAX_CLASSES) s_rcap[tid] = a.res_cap0[tid];
+  const bool res_strict = a.res_mode == 2;
   const int ncat_lds = min(a.n_catalogs, 8);
   for (int c = wave; c < ncat_lds; c += NW) hdr_fill_wave((CatHdr LDS*)&s_hdr[c], &a.cats[c], D.C);
   __syncthreads();
@@ -2011,7 +2047,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
     // (NC_MERGED) without minValues: NodeClaim.Add is then Fits over the remaining types, evaluated in order
     // until one succeeds. The steps, decisions and state writes are the full path's (below), done by one wave
     // without workgroup barriers. Any other situation hands the popped pod to the full path (s_ctl[26]).
-    if (FASTLANE && wave == 0) {
+    if (FASTLANE && wave == 0 && !a.res_mode) {  // (reservation accounting runs on the full path only)
       // the call costs a few thousand cycles (register saves): after calls that placed nothing (topology-owning
       // or unschedulable pods), skip it for a growing number of pops; results do not depend on which path places
       if (fl_skip > 0) {
@@ -2066,6 +2102,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
         s_ctl[23] = a.cur_nc[2 * sl + 1];
         s_ctl[24] = INT32_MAX;  // first count-independent pass (existing / in-flight), topology shape-levels
         s_ctl[25] = INT32_MAX;
+        s_ctl[27] = 0;  // addToNewNodeClaim met a ReservedOfferingError
       }
     }
     __syncthreads();
@@ -2214,7 +2251,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
       else
         sort_newnodeclaims<NT>((GlbI32)a.g_order, (GlbI32)a.g_npods, s_ctl[2], s_ctl[10], s_ctl[11], s_ctl, &a.stats[31]);
       const int n_nc = s_ctl[2];
-      const int start = min(min(s_ctl[19], s_ctl[16] >= 0 ? s_ctl[16] : INT32_MAX), n_nc);
+      const int start = res_strict ? 0 : min(min(s_ctl[19], s_ctl[16] >= 0 ? s_ctl[16] : INT32_MAX), n_nc);
       if (tid == 0) {
         s_ctl[10] = 0;
         if (s_ctl[16] >= 0) mstack_push((LdsI32)s_stk[0], (LdsI32)&s_ctl[12], (LdsI32)&s_ctl[20], ++s_ctl[13], s_ctl[16]);
@@ -2247,7 +2284,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
               cand = s_town[j].maxskew >= 0 ? c + s_town[j].self <= s_town[j].maxskew : (c > 0 || s_town[j].self);
             }
           if (cand) iflags |= 1u << k;  // passes everything that does not depend on the zone counts
-          if (cand && !own_n && fl >= NC_MERGED) tflags |= 1u << k;  // shape-level already merged: append path
+          if (cand && !own_n && fl >= NC_MERGED && !a.res_mode) tflags |= 1u << k;  // shape-level already merged: append path
           for (int j = 0; j < own_n && cand; j++) {  // a NodeClaim pinned to one domain of a key can only take it
             const TopoOwn& o = s_town[j];
             if (o.key >= 0) {
@@ -2271,7 +2308,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
           width = (s_list[r0] & LIST_TAG) ? 1 : NW;
           const int li = r0 + wave;
           bool ok = false, fast = false, perm = true;
-          uint64_t m_v = 0, X = 0;
+          uint64_t m_v = 0, X = 0, held = 0, nh = 0;
           ReqView rv;
           int nc = -1;
           if (wave < width && li < n) {
@@ -2311,6 +2348,11 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
               if (tsub && lane == 0) tsub[5] += 1;  // attempts reaching filter_types (wave 0)
               bytes += (uint64_t)D.TW * 8 + KP_NRES * 8;
             }
+            if (ok && a.res_mode) {  // reserveOfferings: a strict failure depends on the capacities (not memoised)
+              held = a.nc_held[nc];
+              nh = reserve_classes(D, hdr(cat), rv, m_v, X, a.res_cls, held, (const int32_t LDS*)s_rcap, res_strict, vi);
+              if (nh == ~0ull) ok = memo = false;
+            }
             if (!ok && memo && lane == 0 && nc < a.ncc) a.nc_fail[(size_t)sl * a.ncc + nc] = perm ? NC_NEVER : a.nc_ver[nc];
           }
           if (lane == 0 && wave < width) s_ok[wave] = ok ? 1 : 0;
@@ -2333,6 +2375,10 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
                 a.nc_ver[nc] += 1;
               }
               if (lane < KP_NRES) a.nc_fitj[(size_t)nc * KP_NRES + lane] = s_fitj[wave][lane];
+              if (a.res_mode) {
+                reserve_commit((int32_t LDS*)s_rcap, held, nh);
+                if (lane == 0) a.nc_held[nc] = nh;
+              }
             }
             const int wpos = LIST_POS(s_list[r0 + win]);
             placed = in_lds ? ((LdsI32)s_dyn)[wpos] : ((GlbI32)a.g_order)[wpos];
@@ -2365,7 +2411,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
         for (int r0 = 0; r0 < n; r0 += NW) {
           const int li = r0 + wave;
           bool ok = false;
-          uint64_t m_v = 0, X = 0;
+          uint64_t m_v = 0, X = 0, nh = 0;
           ReqView rv;
           int tm = -1;
           if (li < n) {
@@ -2416,6 +2462,13 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
                                  s_scratch[wave], (RowPtr LDS*)s_rl[wave], &bytes, s_fitj[wave], topo_keys);
                 ok = __ballot(X != 0) != 0;
               }
+              if (ok && a.res_mode) {  // a new NodeClaim holds nothing yet
+                nh = reserve_classes(D, H, rv, m_v, X, a.res_cls, 0, (const int32_t LDS*)s_rcap, res_strict, vi);
+                if (nh == ~0ull) {
+                  ok = memo = false;
+                  if (lane == 0) s_ctl[27] = 1;  // ReservedOfferingError: the pod is not relaxed
+                }
+              }
             }
             if (!ok && memo && lane == 0) a.tmpl_fail[(size_t)sl * a.n_tmpl + tm] = a.tmpl_ver[tm];
           }
@@ -2439,6 +2492,10 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
               }
               if (lane < KP_NRES) a.nc_fitj[(size_t)nc * KP_NRES + lane] = s_fitj[wave][lane];
               if (lane == 0 && !own_n && nc < a.ncc) a.nc_fail[(size_t)sl * a.ncc + nc] = NC_MERGED;
+              if (a.res_mode) {
+                reserve_commit((int32_t LDS*)s_rcap, 0, nh);
+                if (lane == 0) a.nc_held[nc] = nh;
+              }
               store_maxalloc(hdr(a.tmpl_catalog[tm])->d.alloc, lane < D.TW ? X : 0, D.T, a.req_res_mask,
                              a.nc_maxalloc + (size_t)nc * KP_NRES);
               // subtractMax: remaining -= max capacity over the new NodeClaim's InstanceTypeOptions
@@ -2539,7 +2596,9 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
         a.events[s_ctl[4]++] = pod;
       } else {
         a.placement[pod] = -1;
-        const bool relaxed = lvl + 1 < a.shape_nlevels[shape];
+        const bool res_err = s_ctl[27] != 0;  // a ReservedOfferingError is not relaxed (upstream trySchedule)
+        if (res_err) a.stats[40] += 1;
+        const bool relaxed = !res_err && lvl + 1 < a.shape_nlevels[shape];
         if (relaxed) a.pod_level[pod] = lvl + 1;
         int len = s_ctl[1];
         int tail = s_ctl[0] + len;
@@ -2692,7 +2751,9 @@ __global__ __launch_bounds__(FIN_THREADS) void finalize_kernel(FinalizeArgs a) {
     rv.minv = R->minv;
     const uint64_t negR = negop_mask(rv.present, rv.compl_, rv.nz);
     const uint64_t allowed = allowed_word(D, rv, v, vint_global(a.vint));
-    const uint64_t cls = allowed_classes(D, Cg.cls, rv, allowed, negR);
+    uint64_t cls = allowed_classes(D, Cg.cls, rv, allowed, negR);
+    const uint64_t held = a.nc_held ? a.nc_held[nc] : 0;
+    if (held) cls &= held;  // FinalizeScheduling: reservation-id In {held ids}
     if (lane == 0) s_cls = cls;
   }
   __syncthreads();

@@ -43,7 +43,7 @@ struct OfferClass {  // 16 bytes: two words per class in the LDS catalogue heade
 
 // Everything the device needs about the dictionary + one catalogue, for one solve.
 struct DevDict {
-  int32_t K, W, KB, T, TW, C, R_used, pad0_;
+  int32_t K, W, KB, T, TW, C, R_used, res_any;  // res_any: some offering class is a capacity reservation
   uint64_t wellknown;        // key mask: AllowUndefinedWellKnownLabels
   uint64_t catalog_keys;     // keys some type carries
   uint64_t single_valued;    // catalogue keys where every type has <= 1 value (complement trick allowed)

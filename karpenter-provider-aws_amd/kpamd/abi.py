@@ -173,7 +173,8 @@ class SolveIn(C.Structure):
                 ("existing", C.POINTER(ExistingNode)), ("n_existing", C.c_uint32), ("n_shapes", C.c_uint32),
                 ("shapes", C.POINTER(PodShape)), ("pods", C.POINTER(Pod)), ("n_pods", C.c_uint32),
                 ("max_instance_types", C.c_uint32), ("bound_pods", C.POINTER(BoundPod)),
-                ("n_bound_pods", C.c_uint32), ("n_namespaces", C.c_uint32), ("namespaces", C.POINTER(Namespace))]
+                ("n_bound_pods", C.c_uint32), ("n_namespaces", C.c_uint32), ("namespaces", C.POINTER(Namespace)),
+                ("reserved_offering_mode", C.c_uint32), ("reserved2_", C.c_uint32)]
 
 
 class NodeClaimInfo(C.Structure):
@@ -189,7 +190,7 @@ class SolveStats(C.Structure):
                 ("scanned", C.c_uint64), ("cursor_starts", C.c_uint64), ("attempt_cycles", C.c_uint64 * 8),
                 ("catalog_ms", C.c_double), ("catalog_cached", C.c_uint32), ("catalog_refreshed", C.c_uint32),
                 ("fast_pods", C.c_uint64), ("fast_cycles", C.c_uint64 * 6), ("slow_sorts", C.c_uint64),
-                ("fast_bails", C.c_uint64 * 8)]
+                ("fast_bails", C.c_uint64 * 8), ("reserved_offering_errors", C.c_uint64)]
 
 
 class Options(C.Structure):
@@ -465,7 +466,7 @@ def build_solve_in(arena, problem, catalog_handles=None):
     nsa, nns = arena.namespaces(getattr(problem, "namespaces", None))
     si = SolveIn(handles, descs, len(problem.catalogs), len(problem.nodepools), nps, ex, len(problem.existing),
                  len(problem.shapes), shapes, pods_ptr, len(problem.pod_shape), problem.max_instance_types,
-                 bps, nbp, nns, nsa if nns else None)
+                 bps, nbp, nns, nsa if nns else None, getattr(problem, "reserved_offering_mode", 0), 0)
     arena.keep.append(si)
     return si
 

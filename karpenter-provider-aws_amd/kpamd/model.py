@@ -157,6 +157,7 @@ class Problem:
     name: str = ""
     bound_pods: List[Tuple[str, Dict[str, str], int]] = field(default_factory=list)  # (namespace, labels, existing idx)
     namespaces: Dict[str, Dict[str, str]] = field(default_factory=dict)  # cluster namespaces: name -> labels
+    reserved_offering_mode: int = 0  # 0 fallback (scheduler default), 1 strict (provisioner: DisableReservedCapacityFallback)
 
     @property
     def n_pods(self):

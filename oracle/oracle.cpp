@@ -1210,6 +1210,7 @@ struct NodeClaim {
   vector<int> pods;
   string hostname;
   vector<HostPort> hostPortUsage;
+  set<string> reserved;  // NodeClaim.reservedOfferings, by reservation id (an id names one offering of one type)
   // max allocatable per resource over `options` (missing = 0): a checker-side shortcut, not part of the restated
   // algorithm. If the merged requests exceed it on some resource, no option Fits, so filterInstanceTypesByRequirements
   // returns nothing and NodeClaim.Add fails whatever the requirement checks say; the outcome is unchanged.
@@ -1252,8 +1253,39 @@ static bool SatisfiesMinValues(const vector<InstanceType>& cat, const vector<int
 }
 
 struct Counters {
-  uint64_t attempts = 0, type_checks = 0, pops = 0;
+  uint64_t attempts = 0, type_checks = 0, pops = 0, reserved_errors = 0;
 };
+
+// UP ReservationManager (scheduling/reservationmanager.go), the design of R:designs/odcr.md:248-256: the scheduler
+// counts the simulated NodeClaims that launch into a capacity reservation and stops at its ReservationCapacity.
+// capacity starts at the least ReservationCapacity any NodePool's instance types report for the id (two NodePools may
+// have listed the reservation at different times); Reserve is idempotent per (hostname, id); Release gives it back.
+struct ReservationManager {
+  map<string, int64_t> capacity;
+  map<string, set<string>> held;  // hostname -> reservation ids
+  void Track(const string& id, int64_t cap) {
+    auto it = capacity.find(id);
+    if (it == capacity.end() || cap < it->second) capacity[id] = cap;
+  }
+  bool Reserve(const string& host, const string& id) {
+    auto& h = held[host];
+    if (h.count(id)) return true;
+    int64_t& c = capacity.at(id);
+    if (c <= 0) return false;
+    c--;
+    h.insert(id);
+    return true;
+  }
+  void Release(const string& host, const string& id) {
+    auto& h = held[host];
+    if (h.erase(id)) capacity.at(id)++;
+  }
+};
+
+static string OfferingResID(const Offering& o) {  // Offering.ReservationID(): the id of a reserved offering
+  auto it = o.reqs.find(kLabelResID);
+  return it == o.reqs.end() || it->second.values.empty() ? string() : *it->second.values.begin();
+}
 
 // filterInstanceTypesByRequirements (UP nodeclaim.go) with relaxMinValues = false.
 static bool FilterInstanceTypes(const vector<InstanceType>& cat, const vector<int>& its, const Requirements& reqs,
@@ -1284,6 +1316,31 @@ struct Scheduler {
   Topology topology;
   int64_t nodeID = 0;  // hostname placeholder counter (NewNodeClaim)
   Counters counters;
+  ReservationManager rm;
+  bool strict = false;       // ReservedOfferingModeStrict (the provisioner's DisableReservedCapacityFallback)
+  bool reservedErr = false;  // the last NodeClaim.Add failed with a ReservedOfferingError
+
+  // NodeClaim.reserveOfferings (UP nodeclaim.go): every available reserved offering of a remaining type that is
+  // compatible with the NodeClaim's new requirements is reserved for its hostname when capacity allows. Strict mode
+  // fails the Add when some were compatible but none could be reserved, or when the NodeClaim held reservations and
+  // now holds none. A failing call reserved nothing new (the failure means the reserved set is empty).
+  bool ReserveOfferings(NodeClaim& n, const Requirements& ncr, const vector<int>& its, set<string>* out) {
+    if (rm.capacity.empty()) return true;
+    bool compatible = false;
+    for (int t : its)
+      for (auto& o : (*n.tmpl->catalog)[t].offerings) {
+        if (!o.available || *o.reqs.at(kLabelCapacityType).values.begin() != "reserved") continue;
+        if (!Compatible(ncr, o.reqs, true)) continue;
+        compatible = true;
+        const string id = OfferingResID(o);
+        if (rm.Reserve(n.hostname, id)) out->insert(id);
+      }
+    if (strict && out->empty() && (compatible || !n.reserved.empty())) {
+      reservedErr = true;
+      return false;
+    }
+    return true;
+  }
 
   // NodeClaim.CanAdd + NodeClaim.Add
   bool NodeClaimAdd(NodeClaim& n, PodState& p) {
@@ -1302,6 +1359,11 @@ struct Scheduler {
     ResourceList requests = Merge(n.requests, p.requests);
     vector<int> remaining;
     if (!FilterInstanceTypes(*n.tmpl->catalog, n.options, ncr, requests, &remaining, &counters)) return false;
+    set<string> reserved;
+    if (!ReserveOfferings(n, ncr, remaining, &reserved)) return false;
+    for (auto& id : n.reserved)  // the offerings the narrower NodeClaim no longer reserves go back
+      if (!reserved.count(id)) rm.Release(n.hostname, id);
+    n.reserved.swap(reserved);
     n.pods.push_back(p.index);
     n.options = std::move(remaining);
     SetMaxAlloc(n);
@@ -1334,7 +1396,9 @@ struct Scheduler {
     return true;
   }
 
+  bool anyReservedErr = false;  // addToNewNodeClaim's error for the pod holds a ReservedOfferingError
   bool add(PodState& p) {
+    anyReservedErr = false;
     for (auto& n : existing)
       if (ExistingCanAddAndAdd(n, p)) return true;
     struct LS {
@@ -1372,7 +1436,9 @@ struct Scheduler {
       nc->options = its;
       SetMaxAlloc(*nc);
       nc->requests = t.daemon;
+      reservedErr = false;
       if (!NodeClaimAdd(*nc, p)) {
+        anyReservedErr |= reservedErr;
         topology.Unregister(kLabelHostname, nc->hostname);  // NodeClaim.Destroy
         continue;
       }
@@ -1502,6 +1568,12 @@ static int32_t SolveCore(const Catalogs& cats, const kp_solve_in* in, kpo_result
     t.remaining = FromABI(np.limits);
     s.templates.push_back(std::move(t));
   }
+  // NewReservationManager over the NodePools' instance types
+  s.strict = in->reserved_offering_mode == KP_RESERVED_STRICT;
+  for (uint32_t i = 0; i < in->n_nodepools; i++)
+    for (auto& it : *cats[in->nodepools[i].catalog])
+      for (auto& o : it.offerings)
+        if (*o.reqs.at(kLabelCapacityType).values.begin() == "reserved") s.rm.Track(OfferingResID(o), o.reservation_capacity);
   // Topology inputs: the node snapshot countDomains reads, the pods bound to it, and buildDomainGroups
   // (NodePool requirements + labels, intersected with each instance type's requirements: In values).
   Topology& topo = s.topology;
@@ -1684,7 +1756,9 @@ static int32_t SolveCore(const Catalogs& cats, const kp_solve_in* in, kpo_result
       continue;
     }
     errored[pi] = 1;
-    bool relaxed = Relax(p);
+    // a ReservedOfferingError is not relaxed: the pod waits for capacity another NodeClaim may release
+    if (s.anyReservedErr) s.counters.reserved_errors++;
+    bool relaxed = !s.anyReservedErr && Relax(p);
     queue.push_back(pi);
     if (relaxed) {
       lastLen.clear();
@@ -1709,6 +1783,8 @@ static int32_t SolveCore(const Catalogs& cats, const kp_solve_in* in, kpo_result
   // re-checked on the truncated list, failures turn the NodeClaim's pods into errors.
   for (auto& ncp : s.created) {
     NodeClaim& n = *ncp;
+    if (!n.reserved.empty())  // FinalizeScheduling: launch only into the reservations the NodeClaim holds
+      Add(n.reqs, NewRequirement(kLabelResID, KP_OP_IN, vector<string>(n.reserved.begin(), n.reserved.end()), -1));
     kpo_result::NC o;
     o.nodepool = (uint32_t)n.tmpl->nodepool;
     o.n_remaining = (uint32_t)n.options.size();
@@ -1743,6 +1819,7 @@ static int32_t SolveCore(const Catalogs& cats, const kp_solve_in* in, kpo_result
   memset(&res->stats, 0, sizeof(res->stats));
   res->stats.attempts = s.counters.attempts;
   res->stats.pops = s.counters.pops;
+  res->stats.reserved_offering_errors = s.counters.reserved_errors;
   res->stats.bytes_algorithmic = s.counters.type_checks;  // type rows visited (SURVEY §8d counter)
   res->stats.host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   *out = res;

@@ -296,15 +296,16 @@ def test_device_launch_reserved_kat(ctx):
 
 
 @pytest.mark.gpu
-def test_solve_refuses_reservations(ctx, catalog):
-    """NodeClaim.Add's reservation accounting (upstream ReservationManager) is not modelled: a Solve over a
-    catalogue with reservation offerings is KP_E_UNSUPPORTED (the shim keeps the Go path for it)."""
+def test_cluster_refuses_reservations(ctx, catalog):
+    """SimulateScheduling's reservation accounting is not modelled: a consolidation cluster over a catalogue with
+    reservation offerings is KP_E_UNSUPPORTED (the shim keeps the Go path for it). A Solve takes them (ABI v9,
+    tests/test_reserved_solve.py)."""
     import kpamd
     from kpamd import synth
     cat = reserved_catalogue(catalog, 200, 0)
-    prob = synth.config2(cat, n_pods=50, seed=2)
+    cl = synth.random_cluster(cat, 0, n_nodes=10)
     with pytest.raises(kpamd.KPError, match="reservation"):
-        kpamd.Scheduler(ctx, prob).solve()
+        kpamd.ClusterPlan(ctx, cl)
 
 
 @pytest.mark.gpu
