@@ -9,6 +9,16 @@
 // why the fast lane handed a popped pod to the full path (stats[32 + FB_*])
 enum { FB_INELIGIBLE = 0, FB_SPILLED = 1, FB_SHIFT = 2, FB_SCAN = 3, FB_MERGE = 4, FB_MINVALUES = 5, FB_NONE = 6 };
 
+// The in-flight pre-check's view of one NodeClaim in one 64-byte line (one gather per candidate position instead of
+// one per field): headroom = max allocatable over its types at creation minus its requests, for the first four
+// requested resources (req_res_mask bit order; more are checked from nc_requests / nc_maxalloc), the exact failure
+// memo's version, the taint set of its template.
+struct NcHead {
+  int64_t room[4];
+  int32_t ver, taintset;
+  int32_t pad_[6];
+};
+
 struct SolveArgs {
   const DevDict* dict;
   const DevCatalog* cats;
@@ -59,7 +69,7 @@ struct SolveArgs {
   // exact failure memo: outcome of Add/CanAdd depends only on (candidate state, pod shape-level), so a
   // recorded failure stays valid while the candidate's version is unchanged
   int32_t ncc;                       // NodeClaim ids < ncc are memoised
-  int32_t* nc_ver;                   // [P]
+  NcHead* nc_head;                   // [P] pre-check record (version, taint set, headroom), written at creation
   int32_t* nc_fail;                  // [SL][ncc]
   int32_t* ex_ver;                   // [E]
   int32_t* ex_fail;                  // [SL][E]
@@ -67,7 +77,6 @@ struct SolveArgs {
   int32_t* tmpl_fail;                // [SL][NT]
   int64_t* nc_maxalloc;              // [P][NRES] max allocatable over the NodeClaim's types at creation
   int32_t* nc_fitj;                  // [P][NRES] threshold index of the last Fits per resource
-  int32_t* nc_taintset;              // [P] taint set of the NodeClaim's template
   int32_t* nc_cat;                   // [P] catalogue of the NodeClaim's template
   uint32_t req_res_mask;             // resources some pod shape requests (> 0)
   int32_t timing;                    // 1: thread 0 accumulates per-phase s_memtime deltas into stats[8..15]

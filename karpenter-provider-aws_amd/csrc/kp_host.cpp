@@ -2743,7 +2743,7 @@ static int32_t SolvePrepareLocal(kp_ctx* ctx, const kp_solve_in* in, kp_comm* co
   const size_t o_order = blob.reserve_dev(sizeof(int32_t) * Pc);
   const size_t o_maxalloc = blob.reserve_dev(sizeof(int64_t) * (size_t)Pc * KP_NRES);
   const size_t o_fitj = blob.reserve_dev(sizeof(int32_t) * (size_t)Pc * KP_NRES);
-  const size_t o_ncts = blob.reserve_dev(sizeof(int32_t) * (size_t)Pc);
+  const size_t o_nchead = blob.reserve_dev(sizeof(NcHead) * (size_t)Pc + 64);
   const size_t o_nccat = blob.reserve_dev(sizeof(int32_t) * (size_t)Pc);
   const size_t o_nchp = blob.reserve_dev(C.hp_any ? sizeof(uint64_t) * (size_t)Pc : 8);
   const size_t o_place = blob.reserve_dev(sizeof(int32_t) * Pc);
@@ -2753,7 +2753,6 @@ static int32_t SolvePrepareLocal(kp_ctx* ctx, const kp_solve_in* in, kp_comm* co
   const size_t SLn = std::max<size_t>(1, C.shape_reqs.size());
   const int ncc = (int)std::min<size_t>((size_t)Pc, std::max<size_t>(1, ((size_t)256 << 20) / (4 * SLn)));
   const size_t o_ver0 = blob.reserve_dev(0);
-  const size_t o_ncver = blob.reserve_dev(sizeof(int32_t) * Pc);
   const size_t o_exver = blob.reserve_dev(sizeof(int32_t) * std::max(E, 1));
   const size_t o_tver = blob.reserve_dev(sizeof(int32_t) * std::max(NT, 1));
   const size_t o_curnc = blob.reserve_dev(sizeof(int32_t) * 2 * SLn);  // cursors start at {0, 0} (zeroed per run)
@@ -2848,7 +2847,7 @@ static int32_t SolvePrepareLocal(kp_ctx* ctx, const kp_solve_in* in, kp_comm* co
   a.sort_cap = 8192;  // newNodeClaims order lives in LDS (64 KiB) up to this many NodeClaims, then spills
   if (const char* e = getenv("KP_SORT_CAP")) a.sort_cap = std::max(1, std::min(8192, atoi(e)));  // test hook
   a.ncc = ncc;
-  a.nc_ver = (int32_t*)(base + o_ncver);
+  a.nc_head = (NcHead*)(((uintptr_t)(base + o_nchead) + 63) & ~(uintptr_t)63);
   a.nc_fail = (int32_t*)(base + o_ncfail);
   a.ex_ver = (int32_t*)(base + o_exver);
   a.ex_fail = (int32_t*)(base + o_exfail);
@@ -2858,7 +2857,6 @@ static int32_t SolvePrepareLocal(kp_ctx* ctx, const kp_solve_in* in, kp_comm* co
   a.cur_ex = (int32_t*)(base + o_curex);
   a.nc_maxalloc = (int64_t*)(base + o_maxalloc);
   a.nc_fitj = (int32_t*)(base + o_fitj);
-  a.nc_taintset = (int32_t*)(base + o_ncts);
   a.nc_cat = (int32_t*)(base + o_nccat);
   a.hp_any = C.hp_any ? 1 : 0;
   a.shape_hp_conf = (const uint64_t*)(base + o_shpc);

@@ -1018,8 +1018,13 @@ __device__ __forceinline__ int first_ok(const int32_t* s_ok) {
 // Max allocatable over a NodeClaim's types at creation, for the resources in `rmask`. Its remaining
 // types only shrink, so this stays an upper bound: a NodeClaim whose requests + the pod's exceed it for any
 // resource cannot take the pod (Fits fails for every remaining type) and the pre-pass skips it.
-__device__ __forceinline__ void store_maxalloc(const int64_t* alloc, uint64_t X, int T, uint32_t rmask, int64_t* dst) {
+// With `head`, the new NodeClaim's pre-check record is written as well: headroom = max allocatable - requests (q_lane:
+// lane r holds the requests of resource r) for the first four requested resources (INT64_MAX past them), version 0.
+__device__ __forceinline__ void store_maxalloc(const int64_t* alloc, uint64_t X, int T, uint32_t rmask, int64_t* dst,
+                                               NcHead* head = nullptr, int64_t q_lane = 0, int32_t taintset = 0) {
   const int lane = LANE;
+  int64_t room0 = INT64_MAX, room1 = INT64_MAX, room2 = INT64_MAX, room3 = INT64_MAX;
+  int k = 0;
   for (int r = 0; r < KP_NRES; r++) {
     if (!((rmask >> r) & 1)) continue;
     int64_t mx = INT64_MIN;
@@ -1032,7 +1037,42 @@ __device__ __forceinline__ void store_maxalloc(const int64_t* alloc, uint64_t X,
     }
     mx = wave_max_i64(mx);
     if (lane == 0) dst[r] = mx;
+    if (head) {
+      const int64_t room = mx - lane_bcast_i64(q_lane, r);
+      if (k == 0) room0 = room;
+      else if (k == 1) room1 = room;
+      else if (k == 2) room2 = room;
+      else if (k == 3) room3 = room;
+    }
+    k++;
   }
+  if (head && lane == 0) {
+    head->room[0] = room0;
+    head->room[1] = room1;
+    head->room[2] = room2;
+    head->room[3] = room3;
+    head->ver = 0;
+    head->taintset = taintset;
+  }
+}
+
+// The k-th (k < 4) set bit of a requested-resource mask, -1 past its last; and the pre-check record as three 16-byte
+// loads (headroom 0-1, headroom 2-3 when more than two resources are requested, version + taint set).
+__device__ __forceinline__ int kth_res(uint32_t m, int k) {
+  for (int i = 0; i < k && m; i++) m &= m - 1;
+  return m ? __builtin_ctz(m) : -1;
+}
+struct HeadView {
+  int64_t r0, r1, r2, r3;
+  int32_t ver, ts;
+};
+__device__ __forceinline__ int64_t i64_of(int lo, int hi) { return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo); }
+__device__ __forceinline__ HeadView load_head(const NcHead* h, bool four) {
+  const int4* p = reinterpret_cast<const int4*>(h);
+  const int4 a = p[0], c = p[2];
+  int4 b = make_int4(-1, 0x7FFFFFFF, -1, 0x7FFFFFFF);
+  if (four) b = p[1];
+  return HeadView{i64_of(a.x, a.y), i64_of(a.z, a.w), i64_of(b.x, b.y), i64_of(b.z, b.w), c.x, c.y};
 }
 
 // mutation stack (LDS): entries (t, pos) with t and pos increasing bottom to top; the lowest position mutated
@@ -1241,23 +1281,42 @@ __device__ void sort_newnodeclaims(P ord, P npods, int n, int mut, int p, int32_
   }
   __syncthreads();
   const int mode = s_ctl[7], q = s_ctl[8], elem = s_ctl[9];
+  // shifts: SH_PER entries per thread between two barriers (a spilled order array shifts thousands of entries in
+  // global memory: the loads of a step are in flight together)
+  constexpr int SH_PER = 8;
   if (mode == 1) {
     const int c = q - 1 - p;  // elements p+1..q-1 move left by one
-    for (int off = 0; off < c; off += NT) {
-      const int i = off + tid;
-      const int v = i < c ? ord[p + 1 + i] : 0;
+    for (int off = 0; off < c; off += NT * SH_PER) {
+      int v[SH_PER];
+#pragma unroll
+      for (int j = 0; j < SH_PER; j++) {
+        const int i = off + j * NT + tid;
+        v[j] = i < c ? ord[p + 1 + i] : 0;
+      }
       __syncthreads();
-      if (i < c) ord[p + i] = v;
+#pragma unroll
+      for (int j = 0; j < SH_PER; j++) {
+        const int i = off + j * NT + tid;
+        if (i < c) ord[p + i] = v[j];
+      }
       __syncthreads();
     }
     if (tid == 0) ord[q - 1] = elem;
   } else if (mode == 2) {
     const int c = n - 1 - q;  // elements q..n-2 move right by one (process from the top down)
-    for (int off = 0; off < c; off += NT) {
-      const int i = c - 1 - (off + tid);
-      const int v = i >= 0 ? ord[q + i] : 0;
+    for (int off = 0; off < c; off += NT * SH_PER) {
+      int v[SH_PER];
+#pragma unroll
+      for (int j = 0; j < SH_PER; j++) {
+        const int i = c - 1 - (off + j * NT + tid);
+        v[j] = i >= 0 ? ord[q + i] : 0;
+      }
       __syncthreads();
-      if (i >= 0) ord[q + i + 1] = v;
+#pragma unroll
+      for (int j = 0; j < SH_PER; j++) {
+        const int i = c - 1 - (off + j * NT + tid);
+        if (i >= 0) ord[q + i + 1] = v[j];
+      }
       __syncthreads();
     }
     if (tid == 0) ord[q] = elem;
@@ -1531,6 +1590,11 @@ __device__ __noinline__ int fast_lane(uint64_t kargs, int32_t LDS* s_dyn_arg, ui
     if (n_rr < 4) rr_list[n_rr] = (int8_t)__builtin_ctz(m);
     n_rr++;
   }
+  // the pre-check record holds the first four requested resources' headroom; more come from requests / maxalloc
+  const int rk2 = kth_res(rmask_all, 2), rk3 = kth_res(rmask_all, 3);
+  uint32_t rr_b4 = rr_rest;
+  for (int i = 0; i < 2 && rr_b4; i++) rr_b4 &= rr_b4 - 1;
+  const bool four = rk2 >= 0;
   const uint64_t pop_cap = (uint64_t)A->n_pods * 64 + 65536;
   // control state in registers for the loop; written back on exit
   int q_head = U(s_ctl[0]), q_len = U(s_ctl[1]), n_ev = U(s_ctl[4]), mut = U(s_ctl[10]), mut_p = U(s_ctl[11]);
@@ -1658,7 +1722,8 @@ if (!FL_NOTIME && tmg) {                                    \
         fb = FB_INELIGIBLE;
         break;
       }
-      const int64_t pr0 = lane_bcast_i64(preq_lane, rr0), pr1 = lane_bcast_i64(preq_lane, rr1);
+      const int64_t pr0 = rmask_all ? lane_bcast_i64(preq_lane, rr0) : 0, pr1 = rm1 ? lane_bcast_i64(preq_lane, rr1) : 0;
+      const int64_t pr2 = rk2 >= 0 ? lane_bcast_i64(preq_lane, rk2) : 0, pr3 = rk3 >= 0 ? lane_bcast_i64(preq_lane, rk3) : 0;
       a_cex_prev_stamp = U(s_ctl[15]);
       if (FL_HAS_EX && lane == 0) {  // addToExistingNode: every position fails (cursor == n_existing)
         A->cur_ex[2 * sl] = A->n_existing;
@@ -1701,6 +1766,7 @@ if (!FL_NOTIME && tmg) {                                    \
         bool cand = false, tag = false;
         const int nc = i < n_nc ? ord[i] : 0;
         int32_t ver = 0;
+        HeadView hv{0, 0, 0, 0, 0, 0};
         // speculative loads of the first position's NodeClaim (the usual winner), issued ahead of the pre-check
         // gathers (and outside their lane-divergent block) so that the two round trips overlap
         const int nc0 = __builtin_amdgcn_readlane(nc, 0);
@@ -1713,14 +1779,17 @@ if (!FL_NOTIME && tmg) {                                    \
         if (i < n_nc) {
           // every gather issued unconditionally: one round trip
           const int32_t fl = nc < A->ncc ? A->nc_fail[(size_t)sl * A->ncc + nc] : -2;
-          ver = A->nc_ver[nc];
-          const int32_t ts = A->nc_taintset[nc];
-          const int64_t* rq = A->nc_requests + (size_t)nc * KP_NRES;
-          const int64_t* mx = A->nc_maxalloc + (size_t)nc * KP_NRES;
-          bool fit = !rmask_all || (rq[rr0] + pr0 <= mx[rr0] && rq[rr1] + pr1 <= mx[rr1]);
-          for (uint32_t rm = rr_rest; rm; rm &= rm - 1) {
-            const int r = __builtin_ctz(rm);
-            fit = fit & (rq[r] + lane_bcast_i64(preq_lane, r) <= mx[r]);
+          hv = load_head(A->nc_head + nc, four);
+          ver = hv.ver;
+          const int32_t ts = hv.ts;
+          bool fit = hv.r0 >= pr0 && hv.r1 >= pr1 && hv.r2 >= pr2 && hv.r3 >= pr3;
+          if (rr_b4) {  // a fifth requested resource and beyond
+            const int64_t* rq = A->nc_requests + (size_t)nc * KP_NRES;
+            const int64_t* mx = A->nc_maxalloc + (size_t)nc * KP_NRES;
+            for (uint32_t rm = rr_b4; rm; rm &= rm - 1) {
+              const int r = __builtin_ctz(rm);
+              fit = fit & (rq[r] + lane_bcast_i64(preq_lane, r) <= mx[r]);
+            }
           }
           cand = fit && fl != ver && fl != NC_NEVER && ((tolmask >> ts) & 1);
           tag = cand && fl >= NC_MERGED;
@@ -1831,9 +1900,16 @@ if (!FL_NOTIME && tmg) {                                    \
             if (__ballot(lane < KP_NRES && fj != j0_lane)) {
               if (lane < KP_NRES) A->nc_fitj[(size_t)ncx * KP_NRES + lane] = fj;
             }
-            if (lane == 0) {
-              npods[ncx] += 1;
-              A->nc_ver[ncx] = verx + 1;
+            if (lane == 0) npods[ncx] += 1;
+            if (lane == l) {  // the pre-check record, from this lane's copy: headroom minus the pod, version + 1
+              int4* hp = reinterpret_cast<int4*>(A->nc_head + ncx);
+              const int64_t n0 = hv.r0 - pr0, n1 = hv.r1 - pr1;
+              hp[0] = make_int4((int)n0, (int)(n0 >> 32), (int)n1, (int)(n1 >> 32));
+              if (four) {
+                const int64_t n2 = hv.r2 - pr2, n3 = hv.r3 - pr3;
+                hp[1] = make_int4((int)n2, (int)(n2 >> 32), (int)n3, (int)(n3 >> 32));
+              }
+              A->nc_head[ncx].ver = verx + 1;
             }
             placed = ncx;
             wpos = base + l;
@@ -1984,6 +2060,10 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
     if (n_rr < 4) rr_list[n_rr] = (int8_t)__builtin_ctz(m);
     n_rr++;
   }
+  const int rk2 = kth_res(rmask_all, 2), rk3 = kth_res(rmask_all, 3);  // pre-check record: resources 0..3
+  uint32_t rr_b4 = rr_rest;
+  for (int i = 0; i < 2 && rr_b4; i++) rr_b4 &= rr_b4 - 1;
+  const bool four = rk2 >= 0;
   {  // Fits threshold tables of catalogue 0 for the first FITV_RES requested resources -> LDS
     int slot = 0;
     for (int r = 0; r < KP_NRES; r++) {
@@ -2251,6 +2331,8 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
       else
         sort_newnodeclaims<NT>((GlbI32)a.g_order, (GlbI32)a.g_npods, s_ctl[2], s_ctl[10], s_ctl[11], s_ctl, &a.stats[31]);
       const int n_nc = s_ctl[2];
+      const int64_t p0 = rmask_all ? s_preq[rr0] : 0, p1 = rm1 ? s_preq[rr1] : 0;  // the pod, per record slot
+      const int64_t p2 = rk2 >= 0 ? s_preq[rk2] : 0, p3 = rk3 >= 0 ? s_preq[rk3] : 0;
       const int start = res_strict ? 0 : min(min(s_ctl[19], s_ctl[16] >= 0 ? s_ctl[16] : INT32_MAX), n_nc);
       if (tid == 0) {
         s_ctl[10] = 0;
@@ -2267,16 +2349,17 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
           const int nc = in_lds ? ((LdsI32)s_dyn)[i] : ((GlbI32)a.g_order)[i];
           // every gather is issued unconditionally so they overlap (one round trip instead of a chain)
           const int32_t fl = nc < a.ncc ? a.nc_fail[(size_t)sl * a.ncc + nc] : -2;
-          const int32_t ver = a.nc_ver[nc];
-          const int32_t ts = a.nc_taintset[nc];
-          const int64_t* rq = a.nc_requests + (size_t)nc * KP_NRES;
-          const int64_t* mx = a.nc_maxalloc + (size_t)nc * KP_NRES;
-          bool cand = !rmask_all || (rq[rr0] + s_preq[rr0] <= mx[rr0] && rq[rr1] + s_preq[rr1] <= mx[rr1]);
-          cand = cand && fl != ver && fl != NC_NEVER && ((tolmask >> ts) & 1);
+          const HeadView hv = load_head(a.nc_head + nc, four);
+          bool cand = hv.r0 >= p0 && hv.r1 >= p1 && hv.r2 >= p2 && hv.r3 >= p3;
+          cand = cand && fl != hv.ver && fl != NC_NEVER && ((tolmask >> hv.ts) & 1);
           if (hpc) cand = cand && !(a.nc_hp[nc] & hpc);
-          for (uint32_t rm = rr_rest; rm && cand; rm &= rm - 1) {
-            const int r = __builtin_ctz(rm);
-            cand = rq[r] + s_preq[r] <= mx[r];
+          if (rr_b4 && cand) {
+            const int64_t* rq = a.nc_requests + (size_t)nc * KP_NRES;
+            const int64_t* mx = a.nc_maxalloc + (size_t)nc * KP_NRES;
+            for (uint32_t rm = rr_b4; rm && cand; rm &= rm - 1) {
+              const int r = __builtin_ctz(rm);
+              cand = rq[r] + s_preq[r] <= mx[r];
+            }
           }
           for (int j = 0; j < own_n && cand; j++)  // hostname topologies, exact (count changes with the version)
             if (s_town[j].key < 0) {
@@ -2353,7 +2436,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
               nh = reserve_classes(D, hdr(cat), rv, m_v, X, a.res_cls, held, (const int32_t LDS*)s_rcap, res_strict, vi);
               if (nh == ~0ull) ok = memo = false;
             }
-            if (!ok && memo && lane == 0 && nc < a.ncc) a.nc_fail[(size_t)sl * a.ncc + nc] = perm ? NC_NEVER : a.nc_ver[nc];
+            if (!ok && memo && lane == 0 && nc < a.ncc) a.nc_fail[(size_t)sl * a.ncc + nc] = perm ? NC_NEVER : a.nc_head[nc].ver;
           }
           if (lane == 0 && wave < width) s_ok[wave] = ok ? 1 : 0;
           __syncthreads();
@@ -2372,7 +2455,12 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
               if (lane == 0) {
                 if (in_lds) ((LdsI32)(s_dyn + a.sort_cap))[nc] += 1;
                 else ((GlbI32)a.g_npods)[nc] += 1;
-                a.nc_ver[nc] += 1;
+                NcHead* h = a.nc_head + nc;
+                h->ver += 1;
+                h->room[0] -= p0;
+                h->room[1] -= p1;
+                h->room[2] -= p2;
+                h->room[3] -= p3;
               }
               if (lane < KP_NRES) a.nc_fitj[(size_t)nc * KP_NRES + lane] = s_fitj[wave][lane];
               if (a.res_mode) {
@@ -2486,7 +2574,6 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
                 a.nc_requests[(size_t)nc * KP_NRES + lane] = a.tmpl_daemon[(size_t)tm * KP_NRES + lane] + s_preq[lane];
               if (lane == 0) {
                 a.nc_tmpl[nc] = tm;
-                a.nc_taintset[nc] = a.tmpl_taintset[tm];
                 a.nc_cat[nc] = a.tmpl_catalog[tm];
                 if (a.hp_any) a.nc_hp[nc] = hpa;  // a template's HostPortUsage is empty
               }
@@ -2497,7 +2584,9 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
                 if (lane == 0) a.nc_held[nc] = nh;
               }
               store_maxalloc(hdr(a.tmpl_catalog[tm])->d.alloc, lane < D.TW ? X : 0, D.T, a.req_res_mask,
-                             a.nc_maxalloc + (size_t)nc * KP_NRES);
+                             a.nc_maxalloc + (size_t)nc * KP_NRES, a.nc_head + nc,
+                             lane < KP_NRES ? a.tmpl_daemon[(size_t)tm * KP_NRES + lane] + s_preq[lane] : 0,
+                             a.tmpl_taintset[tm]);
               // subtractMax: remaining -= max capacity over the new NodeClaim's InstanceTypeOptions
               const uint32_t lim = a.tmpl_limit_present[tm];
               if (lim) {
@@ -2553,7 +2642,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
       const bool ex = placed <= -2;
       const int idx = ex ? -2 - placed : placed;
       const KReqs* fin = ex ? kreq_at(a.ex_reqs, idx) : kreq_at(a.nc_reqs, idx);
-      const int ts = ex ? a.ex_taintset[idx] : a.nc_taintset[idx];
+      const int ts = ex ? a.ex_taintset[idx] : a.nc_head[idx].taintset;
       for (int i = 0; i < rn; i++) {
         const int g = a.rec_list[a.shape_rec_base[shape] + i];
         bool ok = (a.tg_filt_tol[g] >> ts) & 1;
