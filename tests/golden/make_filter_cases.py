@@ -1,8 +1,9 @@
 """Transcribes the kept/rejected expectations of R:pkg/providers/instance/filter/filter_test.go:47-629
 into data (tests/golden/filter_cases.json). Instance types are built the way the test helpers build them
 (makeInstanceType/makeOffering/withZone/withPrice, R:filter_test.go:633-743): empty overhead, capacity only
-what withResource sets, offerings with only capacity-type (+zone/price when given). Reserved-capacity
-filters (CapacityReservationType/CapacityBlock/ReservedOffering) are SURVEY §8f "next" and not included.
+what withResource sets, offerings with only capacity-type (+zone/price when given). The reserved-capacity
+filters' cases (CapacityReservationType / CapacityBlock / ReservedOffering, R:filter_test.go:130-396) are transcribed
+in tests/test_reserved_offerings.py instead (they need reservation ids / types on the offerings).
 """
 import json
 import os

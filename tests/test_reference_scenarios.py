@@ -9,6 +9,7 @@ fake CreateFleet with InsufficientCapacityPools, ICE marks, re-Solve (tests/scen
   ICE fallback to smaller instances   R:pkg/providers/instancetype/suite_test.go:2059-2092
   ICE cache expiry                    R:pkg/providers/instancetype/suite_test.go:2093-2111
   on-demand when spot is ICE'd        R:pkg/providers/instancetype/suite_test.go:2139-2174
+  ICE'd type stays listed             R:pkg/providers/instancetype/suite_test.go:2175-2226 (no available offering left)
   capacity type                       R:pkg/providers/instancetype/suite_test.go:2229-2244 (default on-demand; spot when
                                       flexible to both)
 """
@@ -186,6 +187,33 @@ def test_on_demand_when_spot_unavailable(backend, mk, lib):
     assert pod_node == [None]
     nodes, pod_node = env.provision(pool, shape, [1])
     assert pod_node == [0] and nodes[0]["capacity_type"] == "on-demand"
+
+
+@pytest.mark.parametrize("backend", BACKENDS)
+def test_all_instance_types_listed_after_ice(backend, mk, lib):
+    """m5.xlarge's on-demand and spot pools in test-zone-1a/1b ICE'd; four pods pinned to each (capacity type, zone)
+    try it and stay pending; GetInstanceTypes still returns m5.xlarge, with no available offering
+    (R:suite_test.go:2175-2226). Device backend: the resident catalogue after the four ICE marks answers
+    CompatibleAvailableFilter with nothing for m5.xlarge."""
+    import numpy as np
+    import scenarios
+    types = scenarios.fake_catalog(lib)
+    pools = [(ct, "m5.xlarge", z) for ct in ("on-demand", "spot") for z in ("test-zone-1a", "test-zone-1b")]
+    env = mk(backend, types, ice=pools)
+    pool = [NodePool("default", 0, 0, [(IT, "In", ["m5.xlarge"]), (CT, "In", ["spot", "on-demand"])])]
+    for ct in ("on-demand", "spot"):
+        for z in ("test-zone-1a", "test-zone-1b"):
+            _, pod_node = env.provision(pool, [PodShape(rq(1000), node_selector={CT: ct, ZONE: z})], [1])
+            assert pod_node == [None]
+    listed = env.cat.instance_types if backend == "device" else types
+    names = [t.name for t in listed]
+    assert "m5.xlarge" in names
+    m5x = listed[names.index("m5.xlarge")]
+    assert [o for o in m5x.offerings if o.available] == []
+    if backend == "device":
+        import kpamd
+        kept, _, _ = kpamd.compatible_available_filter(env.ctx, env.cat, [([], {"cpu": 1000})])
+        assert not kept[0][names.index("m5.xlarge")] and kept[0].sum() > 0
 
 
 @pytest.mark.parametrize("backend", BACKENDS)
