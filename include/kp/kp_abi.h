@@ -502,13 +502,24 @@ typedef struct kp_nodeclass {
   uint32_t n_zones;
   int32_t max_pods;              /* < 0: nil */
   int32_t pods_per_core;         /* <= 0: nil */
-  int32_t reserved_;
+  int32_t ami_family;            /* ABI v9: KP_AMI_* (EC2NodeClass.AMIFamily(); 0 = AL2023, the default alias) */
   const kp_kubelet* kubelet;     /* NULL: no kubelet block (defaults) */
 } kp_nodeclass;
 
-/* instancetype.NewInstanceType capacity + Overhead.Total() for the AL2023 family (R:types.go:123-155,
- * 313-598). The label half (computeRequirements, R:types.go:158-292) is plain string marshalling and
- * stays with the caller (kpamd/catalog.py mirrors it). */
+/* AMI families (R:pkg/providers/amifamily): their FeatureFlags (R:resolver.go:110-117, bottlerocket.go:126-132,
+ * windows.go:101-108) and default ephemeral block device (al2023.go:98-108, al2.go:107-116, bottlerocket.go:95-112,
+ * windows.go:88-99, custom.go:48-58) shape pods, kube-reserved memory, eviction and ephemeral storage. */
+#define KP_AMI_AL2023 0
+#define KP_AMI_AL2 1
+#define KP_AMI_BOTTLEROCKET 2
+#define KP_AMI_WINDOWS2019 3
+#define KP_AMI_WINDOWS2022 4
+#define KP_AMI_CUSTOM 5
+
+/* instancetype.NewInstanceType capacity + Overhead.Total() (R:types.go:123-155, 313-598) for the nodeclass's AMI
+ * family: Windows families add vpc.amazonaws.com/PrivateIPv4Address (IPv4 addresses per ENI - 1, types in the VPC
+ * limits table, amd64 only: R:types.go:151-153, 477-484). The label half (computeRequirements, R:types.go:158-292)
+ * is plain string marshalling and stays with the caller (kpamd/catalog.py mirrors it). */
 int32_t kp_instance_type_resolve(const kp_options* opts, const kp_ec2_info* info, const kp_nodeclass* nc,
                                  kp_resource_list* capacity, kp_resource_list* overhead);
 

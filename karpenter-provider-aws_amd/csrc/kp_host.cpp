@@ -998,13 +998,35 @@ void SetRes(kp_resource_list* l, int r, int64_t v) {
   l->milli[r] = v;
   l->present |= 1u << r;
 }
+struct FamilyFlags;
+int64_t PodsOf(const kp_options* opts, const kp_ec2_info* info, const kp_nodeclass* nc);
 int64_t MemoryBytes(const kp_options* opts, const kp_ec2_info* info) {  // memory() (R:types.go:337-347)
   int64_t mib = info->memory_mib;
   if (info->arch && strcmp(info->arch, "arm64") == 0) mib -= 64;  // Graviton CMA
   const int64_t ovMiB = (int64_t)std::ceil((double)(mib * 1048576ll) * opts->vm_memory_overhead_percent / 1024 / 1024);
   return (mib - ovMiB) * 1048576ll;
 }
-constexpr int64_t kStorageBytes = 20ll << 30;  // AL2023 default /dev/xvda, no BDMs (R:amifamily/al2023.go:98-108)
+// An AMI family's FeatureFlags and its default ephemeral volume (no blockDeviceMappings on the nodeclass):
+// DefaultFamily (AL2023, AL2, Custom) R:amifamily/resolver.go:110-117; Bottlerocket :126-132 (/dev/xvdb, DefaultEBS);
+// Windows windows.go:101-108 (/dev/sda1, 50Gi); the others DefaultEBS 20Gi (resolver.go:39-43).
+struct FamilyFlags {
+  bool eni_memory, pods_per_core, eviction_soft, eni_density, windows;
+  int64_t storage_bytes;
+};
+FamilyFlags Family(const kp_nodeclass* nc) {
+  const int f = nc ? nc->ami_family : KP_AMI_AL2023;
+  if (f == KP_AMI_BOTTLEROCKET) return {false, false, false, true, false, 20ll << 30};
+  if (f == KP_AMI_WINDOWS2019 || f == KP_AMI_WINDOWS2022) return {false, true, true, false, true, 50ll << 30};
+  return {true, true, true, true, false, 20ll << 30};
+}
+
+// pods() (R:types.go:553-569): maxPods, else ENI-limited when the family supports it, else 110; then podsPerCore
+int64_t PodsOf(const kp_options* opts, const kp_ec2_info* info, const kp_nodeclass* nc) {
+  const FamilyFlags fam = Family(nc);
+  int64_t pods = (nc && nc->max_pods >= 0) ? nc->max_pods : fam.eni_density ? EniLimitedPods(info, opts->reserved_enis) : 110;
+  if (nc && nc->pods_per_core > 0 && fam.pods_per_core) pods = std::min<int64_t>((int64_t)nc->pods_per_core * info->vcpu, pods);
+  return pods;
+}
 
 // computeEvictionSignal (R:types.go:571-598) in milli-units: a percentage p of the capacity (100% disables the
 // threshold) as ceil(capacity / 100 * p) whole units, else the quantity itself.
@@ -1022,9 +1044,11 @@ int32_t kp_instance_type_overhead(const kp_options* opts, const kp_ec2_info* inf
   memset(kube, 0, sizeof *kube);
   memset(sys, 0, sizeof *sys);
   memset(ev, 0, sizeof *ev);
-  // kubeReservedResources: AL2023 UsesENILimitedMemoryOverhead -> memory from ENILimitedPods(info, 0); the CPU
-  // ranges accumulate with a truncation per range; then the user's keys replace the computed ones (lo.Assign)
-  SetRes(kube, KP_RES_MEMORY, (11 * EniLimitedPods(info, 0) + 255) * 1048576ll * 1000ll);
+  const FamilyFlags fam = Family(nc);
+  const int64_t kStorageBytes = fam.storage_bytes;
+  // kubeReservedResources: UsesENILimitedMemoryOverhead -> memory from ENILimitedPods(info, 0), else from pods(); the
+  // CPU ranges accumulate with a truncation per range; then the user's keys replace the computed ones (lo.Assign)
+  SetRes(kube, KP_RES_MEMORY, (11 * (fam.eni_memory ? EniLimitedPods(info, 0) : PodsOf(opts, info, nc)) + 255) * 1048576ll * 1000ll);
   SetRes(kube, KP_RES_EPHEMERAL_STORAGE, (1ll << 30) * 1000);
   const struct {
     int64_t s, e;
@@ -1060,14 +1084,14 @@ int32_t kp_instance_type_overhead(const kp_options* opts, const kp_ec2_info* inf
       }
     };
     if (kl->has_eviction_hard) fold(kl->hard_memory_available, kl->hard_nodefs_available);
-    if (kl->has_eviction_soft) fold(kl->soft_memory_available, kl->soft_nodefs_available);  // AL2023: enabled
+    if (kl->has_eviction_soft && fam.eviction_soft) fold(kl->soft_memory_available, kl->soft_nodefs_available);
     for (int r = 0; r < KP_NUM_RESOURCES; r++)
       if (ov.present & (1u << r)) SetRes(ev, r, ov.milli[r]);
   }
   return KP_OK;
 }
 
-// instancetype.NewInstanceType capacity + Overhead.Total() for the AL2023 family (R:types.go:123-155, 313-598).
+// instancetype.NewInstanceType capacity + Overhead.Total() for the nodeclass's AMI family (R:types.go:123-155, 313-598).
 int32_t kp_instance_type_resolve(const kp_options* opts, const kp_ec2_info* info, const kp_nodeclass* nc,
                                  kp_resource_list* capacity, kp_resource_list* overhead) {
   if (!opts || !info || !capacity || !overhead) return fail(KP_E_INVAL, "null argument");
@@ -1075,10 +1099,9 @@ int32_t kp_instance_type_resolve(const kp_options* opts, const kp_ec2_info* info
   memset(overhead, 0, sizeof *overhead);
   SetRes(capacity, KP_RES_CPU, (int64_t)info->vcpu * 1000);
   SetRes(capacity, KP_RES_MEMORY, MemoryBytes(opts, info) * 1000);
-  SetRes(capacity, KP_RES_EPHEMERAL_STORAGE, kStorageBytes * 1000);
-  int64_t pods = (nc && nc->max_pods >= 0) ? nc->max_pods : EniLimitedPods(info, opts->reserved_enis);
-  if (nc && nc->pods_per_core > 0) pods = std::min<int64_t>((int64_t)nc->pods_per_core * info->vcpu, pods);
-  SetRes(capacity, KP_RES_PODS, pods * 1000);
+  const FamilyFlags fam = Family(nc);
+  SetRes(capacity, KP_RES_EPHEMERAL_STORAGE, fam.storage_bytes * 1000);
+  SetRes(capacity, KP_RES_PODS, PodsOf(opts, info, nc) * 1000);
   SetRes(capacity, KP_RES_POD_ENI, (info->in_limits_table && info->trunking) ? (int64_t)info->branch_enis * 1000 : 0);
   const string gm = info->gpu_manufacturer ? info->gpu_manufacturer : "";
   SetRes(capacity, KP_RES_NVIDIA_GPU, gm == "nvidia" ? info->gpu_count * 1000ll : 0);
@@ -1087,6 +1110,9 @@ int32_t kp_instance_type_resolve(const kp_options* opts, const kp_ec2_info* info
   SetRes(capacity, KP_RES_NEURONCORE, (int64_t)info->neuron_devices * info->neuron_cores_per_device * 1000);
   SetRes(capacity, KP_RES_GAUDI, gm == "habana" ? info->gpu_count * 1000ll : 0);
   SetRes(capacity, KP_RES_EFA, (int64_t)info->efa * 1000);
+  // Windows: the os requirement is windows only for amd64 types (getOS), which then get PrivateIPv4Address
+  if (fam.windows && info->arch && strcmp(info->arch, "amd64") == 0)
+    SetRes(capacity, KP_RES_PRIVATE_IPV4, info->in_limits_table ? ((int64_t)info->ipv4_per_eni - 1) * 1000 : 0);
   kp_resource_list parts[3];
   int32_t rc = kp_instance_type_overhead(opts, info, nc, &parts[0], &parts[1], &parts[2]);
   if (rc != KP_OK) return rc;

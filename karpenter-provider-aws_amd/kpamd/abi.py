@@ -223,7 +223,11 @@ class Kubelet(C.Structure):
 class NodeClass(C.Structure):
     _fields_ = [("region", C.c_char_p), ("zones", C.POINTER(C.c_char_p)), ("zone_ids", C.POINTER(C.c_char_p)),
                 ("n_zones", C.c_uint32), ("max_pods", C.c_int32), ("pods_per_core", C.c_int32),
-                ("reserved_", C.c_int32), ("kubelet", C.POINTER(Kubelet))]
+                ("ami_family", C.c_int32), ("kubelet", C.POINTER(Kubelet))]
+
+
+AMI_FAMILIES = {"AL2023": 0, "AL2": 1, "Bottlerocket": 2, "Windows2019": 3, "Windows2022": 4, "Custom": 5}
+WINDOWS_BUILDS = {"Windows2019": "10.0.17763", "Windows2022": "10.0.20348"}  # R:pkg/apis/v1/labels.go:111-112
 
 
 class ClusterNode(C.Structure):

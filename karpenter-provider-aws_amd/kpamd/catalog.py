@@ -76,9 +76,11 @@ class CapacityReservation:
     available_count: int = 1
 
 
-def compute_requirements(row, region=REGION, zones=ZONES, zone_ids=ZONE_IDS, offering_zones=None, reservations=()):
-    """computeRequirements (R:types.go:158-292) for the AL2023 family; reservations = the type's capacity
-    reservations (reserved capacity type, reservation id / type In, R:types.go:172-174,223-232)."""
+def compute_requirements(row, region=REGION, zones=ZONES, zone_ids=ZONE_IDS, offering_zones=None, reservations=(),
+                         ami_family="AL2023"):
+    """computeRequirements (R:types.go:158-292); reservations = the type's capacity reservations (reserved capacity
+    type, reservation id / type In, R:types.go:172-174,223-232). Windows families: os In {windows} for amd64 types, no
+    value otherwise (getOS, :294-302), windows-build In {the family's build} (:274-277)."""
     name = row["name"]
     offering_zones = zones if offering_zones is None else offering_zones
     available = [z for z in zones if z in set(offering_zones)]
@@ -86,10 +88,13 @@ def compute_requirements(row, region=REGION, zones=ZONES, zone_ids=ZONE_IDS, off
     reqs = {
         "node.kubernetes.io/instance-type": ("node.kubernetes.io/instance-type", "In", [name]),
         "kubernetes.io/arch": ("kubernetes.io/arch", "In", [row["arch"]]),
-        "kubernetes.io/os": ("kubernetes.io/os", "In", ["linux"]),
+        "kubernetes.io/os": ("kubernetes.io/os", "In", ["linux"]) if ami_family not in abi.WINDOWS_BUILDS else
+                            ("kubernetes.io/os", "In", ["windows"]) if row["arch"] == "amd64" else
+                            ("kubernetes.io/os", "DoesNotExist", []),
         "topology.kubernetes.io/zone": ("topology.kubernetes.io/zone", "In", available),
         "topology.kubernetes.io/region": ("topology.kubernetes.io/region", "In", [region]),
-        "node.kubernetes.io/windows-build": DNE("node.kubernetes.io/windows-build"),
+        "node.kubernetes.io/windows-build": DNE("node.kubernetes.io/windows-build") if ami_family not in abi.WINDOWS_BUILDS
+                                            else ("node.kubernetes.io/windows-build", "In", [abi.WINDOWS_BUILDS[ami_family]]),
         "karpenter.sh/capacity-type": ("karpenter.sh/capacity-type", "In",
                                        ["on-demand", "spot"] + (["reserved"] if reservations else [])),
         K + "instance-cpu": (K + "instance-cpu", "In", [str(row["vcpu"])]),
@@ -225,9 +230,12 @@ def kubelet(arena, kube_reserved=None, system_reserved=None, eviction_hard=None,
     return k
 
 
-def nodeclass(arena, zones=ZONES, zone_ids=ZONE_IDS, max_pods=None, pods_per_core=None, kubelet_cfg=None):
-    """kp_nodeclass; kubelet_cfg: dict of kubelet(...) keyword arguments, or None for no kubelet block."""
+def nodeclass(arena, zones=ZONES, zone_ids=ZONE_IDS, max_pods=None, pods_per_core=None, kubelet_cfg=None,
+              ami_family="AL2023"):
+    """kp_nodeclass; kubelet_cfg: dict of kubelet(...) keyword arguments, or None for no kubelet block; ami_family:
+    a key of abi.AMI_FAMILIES (EC2NodeClass.AMIFamily())."""
     nc = abi.NodeClass()
+    nc.ami_family = abi.AMI_FAMILIES[ami_family]
     if kubelet_cfg is not None:
         nc.kubelet = C.pointer(kubelet(arena, **kubelet_cfg))
     nc.region = arena.s(REGION)
@@ -278,13 +286,13 @@ def spot_price_table(rows, zones=ZONES, seed=SPOT_SEED):
 
 
 def build_catalog(lib, rows=None, opts=None, max_pods=None, pods_per_core=None, zones=ZONES, zone_ids=ZONE_IDS,
-                  unavailable=frozenset(), kubelet_cfg=None, capacity_reservations=()):
+                  unavailable=frozenset(), kubelet_cfg=None, capacity_reservations=(), ami_family="AL2023"):
     """GetInstanceTypes for one EC2NodeClass: NewInstanceType for every row, then InjectOfferings
     (capacity_reservations: the NodeClass's reservations, ReservedCapacity feature gate on)."""
     rows = load_ec2_table() if rows is None else rows
     arena = abi.Arena()
     opts = opts or default_options()
-    nc = nodeclass(arena, zones, zone_ids, max_pods, pods_per_core, kubelet_cfg)
+    nc = nodeclass(arena, zones, zone_ids, max_pods, pods_per_core, kubelet_cfg, ami_family)
     spot = spot_price_table(rows, zones)
     out = []
     for r in rows:
@@ -294,7 +302,7 @@ def build_catalog(lib, rows=None, opts=None, max_pods=None, pods_per_core=None, 
         if rc != 0:
             raise RuntimeError(f"kp_instance_type_resolve({r['name']}) = {rc}")
         crs = [cr for cr in capacity_reservations if cr.instance_type == r["name"]]  # R:types.go:117-119
-        reqs = compute_requirements(r, zones=zones, zone_ids=zone_ids, reservations=crs)
+        reqs = compute_requirements(r, zones=zones, zone_ids=zone_ids, reservations=crs, ami_family=ami_family)
         out.append(InstanceType(r["name"], reqs, resource_dict(cap), resource_dict(ovh),
                                 create_offerings(r, reqs, spot, zones, zone_ids, unavailable, crs)))
     return out

@@ -2492,7 +2492,25 @@ int32_t kpo_requirements_intersects(const kp_requirements* a, const kp_requireme
   return Intersects(FromABI(*a), FromABI(*b)) ? 1 : 0;
 }
 
-// ---- catalogue: NewInstanceType (R:types.go:123-598), AL2023 family ----------------------------
+// ---- catalogue: NewInstanceType (R:types.go:123-598) per AMI family ------------------------------
+// FeatureFlags: DefaultFamily (AL2023, AL2, Custom) R:pkg/providers/amifamily/resolver.go:110-117, Bottlerocket
+// bottlerocket.go:126-132, Windows windows.go:101-108; default ephemeral volume (no blockDeviceMappings): the family's
+// EphemeralBlockDevice in its DefaultBlockDeviceMappings, else DefaultEBS (20Gi) (R:types.go:350-388).
+struct AMIFamilyFlags {
+  bool UsesENILimitedMemoryOverhead, PodsPerCoreEnabled, EvictionSoftEnabled, SupportsENILimitedPodDensity, Windows;
+  int64_t EphemeralGi;
+};
+static AMIFamilyFlags FamilyOf(const kp_nodeclass* nc) {
+  switch (nc ? nc->ami_family : KP_AMI_AL2023) {
+    case KP_AMI_BOTTLEROCKET:
+      return {false, false, false, true, false, 20};  // /dev/xvdb: DefaultEBS
+    case KP_AMI_WINDOWS2019:
+    case KP_AMI_WINDOWS2022:
+      return {false, true, true, false, true, 50};  // /dev/sda1: 50Gi
+    default:
+      return {true, true, true, true, false, 20};  // AL2023 / AL2 /dev/xvda DefaultEBS; Custom: none -> DefaultEBS
+  }
+}
 typedef struct kpo_overhead {
   kp_resource_list kube_reserved, system_reserved, eviction_threshold;
 } kpo_overhead;
@@ -2515,14 +2533,17 @@ int32_t kpo_instance_type_resolve(const kp_options* opts, const kp_ec2_info* inf
   double bytes = (double)(mib * 1048576ll);
   int64_t ovMiB = (int64_t)std::ceil(bytes * opts->vm_memory_overhead_percent / 1024 / 1024);
   cap[KP_RES_MEMORY] = Mi(mib - ovMiB);
-  // ephemeralStorage(): no BDMs -> AL2023 default /dev/xvda 20Gi (R:amifamily/al2023.go:98-108, resolver.go:39-43)
-  int64_t storageBytes = 20ll * 1073741824ll;
+  const AMIFamilyFlags fam = FamilyOf(nc);
+  // ephemeralStorage(): no BDMs -> the family's default ephemeral volume
+  int64_t storageBytes = fam.EphemeralGi * 1073741824ll;
   cap[KP_RES_EPHEMERAL_STORAGE] = storageBytes * 1000;
-  // pods(): maxPods, else ENI-limited (AL2023 SupportsENILimitedPodDensity), then podsPerCore cap
+  // pods(): maxPods, else ENI-limited (SupportsENILimitedPodDensity), else 110; then podsPerCore (PodsPerCoreEnabled)
   int64_t pods;
   if (nc && nc->max_pods >= 0) pods = nc->max_pods;
-  else pods = ENILimitedPods(info, opts->reserved_enis);
-  if (nc && nc->pods_per_core > 0) pods = std::min<int64_t>((int64_t)nc->pods_per_core * info->vcpu, pods);
+  else if (fam.SupportsENILimitedPodDensity) pods = ENILimitedPods(info, opts->reserved_enis);
+  else pods = 110;
+  if (nc && nc->pods_per_core > 0 && fam.PodsPerCoreEnabled)
+    pods = std::min<int64_t>((int64_t)nc->pods_per_core * info->vcpu, pods);
   cap[KP_RES_PODS] = pods * 1000;
   cap[KP_RES_POD_ENI] = (info->in_limits_table && info->trunking) ? (int64_t)info->branch_enis * 1000 : 0;
   std::string gm = info->gpu_manufacturer ? info->gpu_manufacturer : "";
@@ -2532,11 +2553,15 @@ int32_t kpo_instance_type_resolve(const kp_options* opts, const kp_ec2_info* inf
   cap[KP_RES_NEURONCORE] = (int64_t)info->neuron_devices * info->neuron_cores_per_device * 1000;
   cap[KP_RES_GAUDI] = (gm == "habana" ? info->gpu_count : 0) * 1000ll;
   cap[KP_RES_EFA] = (int64_t)info->efa * 1000;
+  // R:types.go:151-153: types compatible with os In {windows} (getOS: Windows families, amd64) get PrivateIPv4Address
+  // = the VPC limits table's IPv4 addresses per interface - 1, 0 when the table lacks the type (:477-484)
+  if (fam.Windows && info->arch && std::string(info->arch) == "amd64")
+    cap[KP_RES_PRIVATE_IPV4] = info->in_limits_table ? ((int64_t)info->ipv4_per_eni - 1) * 1000 : 0;
   *capacity = ToABI(cap);
 
-  // kubeReservedResources (memory uses ENILimitedPods(ctx, info, 0) for AL2023)
+  // kubeReservedResources: memory from ENILimitedPods(ctx, info, 0) when UsesENILimitedMemoryOverhead, else pods()
   ResourceList kube;
-  kube[KP_RES_MEMORY] = Mi(11 * ENILimitedPods(info, 0) + 255);
+  kube[KP_RES_MEMORY] = Mi(11 * (fam.UsesENILimitedMemoryOverhead ? ENILimitedPods(info, 0) : pods) + 255);
   kube[KP_RES_EPHEMERAL_STORAGE] = 1073741824ll * 1000;
   struct R {
     int64_t start, end;
@@ -2572,7 +2597,7 @@ int32_t kpo_instance_type_resolve(const kp_options* opts, const kp_ec2_info* inf
     const double memUnits = (double)(mib - ovMiB) * 1048576.0, fsUnits = (double)storageBytes;
     std::vector<std::pair<const kp_eviction_value*, const kp_eviction_value*>> maps;
     if (kl->has_eviction_hard) maps.push_back({&kl->hard_memory_available, &kl->hard_nodefs_available});
-    if (kl->has_eviction_soft) maps.push_back({&kl->soft_memory_available, &kl->soft_nodefs_available});
+    if (kl->has_eviction_soft && fam.EvictionSoftEnabled) maps.push_back({&kl->soft_memory_available, &kl->soft_nodefs_available});
     ResourceList override_;
     for (auto& m : maps) {
       ResourceList temp;

@@ -40,16 +40,16 @@ def _fake_offering_zones():
     return zones
 
 
-def _resolve(lib, row, zones, spot_price, offering_zones):
+def _resolve(lib, row, zones, spot_price, offering_zones, ami_family="AL2023"):
     from kpamd import abi, catalog
     from kpamd.model import InstanceType
     arena = abi.Arena()
     opts = catalog.default_options()
-    nc = catalog.nodeclass(arena)
+    nc = catalog.nodeclass(arena, ami_family=ami_family)
     info = catalog.ec2_info(arena, row)
     cap, ovh = abi.ResourceList(), abi.ResourceList()
     assert lib.kp_instance_type_resolve(C.byref(opts), C.byref(info), C.byref(nc), C.byref(cap), C.byref(ovh)) == 0
-    reqs = catalog.compute_requirements(row, offering_zones=offering_zones)
+    reqs = catalog.compute_requirements(row, offering_zones=offering_zones, ami_family=ami_family)
     priced = {(row["name"], z): spot_price.get((row["name"], z), 0.0) for z in catalog.ZONES}
     offs = catalog.create_offerings(row, reqs, priced, catalog.ZONES, catalog.ZONE_IDS)
     for o in offs:  # a spot offering without a spot price has no price (createOfferings: hasPrice false)
@@ -58,17 +58,17 @@ def _resolve(lib, row, zones, spot_price, offering_zones):
     return InstanceType(row["name"], reqs, catalog.resource_dict(cap), catalog.resource_dict(ovh), offs)
 
 
-def fake_catalog(lib):
+def fake_catalog(lib, ami_family="AL2023", extra_rows=()):
     """The 16-type fake EC2 catalogue with its offering zones; on-demand prices from the static table, spot = the
-    default price (no spot update in the instancetype suite)."""
+    default price (no spot update in the instancetype suite). extra_rows: more (row, offering zones) pairs."""
     from kpamd import catalog
     zones = _fake_offering_zones()
-    rows = [r for r in catalog.load_ec2_table() if r["name"] in zones]
+    rows = [(r, zones[r["name"]]) for r in catalog.load_ec2_table() if r["name"] in zones] + list(extra_rows)
     out = []
-    for r in rows:
-        z = [x for x in zones[r["name"]] if x in catalog.ZONES]
+    for r, rz in rows:
+        z = [x for x in rz if x in catalog.ZONES]
         spot = {(r["name"], x): r["od_price"] for x in z}
-        out.append(_resolve(lib, r, catalog.ZONES, spot, z))
+        out.append(_resolve(lib, r, catalog.ZONES, spot, z, ami_family))
     return out
 
 

@@ -5,8 +5,9 @@ VMMemoryOverheadPercent 0, :1176-1180). Each KAT runs on the product (kp_instanc
 no GPU) and on the oracle restatement (kpo_instance_type_resolve); the product's kp_instance_type_resolve overhead
 must equal the sum of the three lists (Overhead.Total()).
 
-Not transcribed: "should ignore eviction threshold when using Bottlerocket AMI" (:1397-1430) — the catalogue is
-the AL2023 family only."""
+AMI families (ABI v9 kp_nodeclass.ami_family): Bottlerocket ignores evictionSoft (:1397-1430); max-pods and the
+kube-reserved memory per family on t3.large, with maxPods 10 (:1626-1670) and with reservedENIs 1 (:1697-1744);
+Windows sets pods to 110 when the family has no ENI-limited density (:979-1001)."""
 import ctypes as C
 
 import pytest
@@ -29,10 +30,11 @@ def _opts(vm_overhead):
     return o
 
 
-def product(lib, kubelet_cfg, vm_overhead=None):
+def product(lib, kubelet_cfg, vm_overhead=None, family="AL2023", name="m5.xlarge", max_pods=None, reserved_enis=0):
     arena = abi.Arena()
-    opts, info = _opts(vm_overhead), _info(arena)
-    nc = catalog.nodeclass(arena, kubelet_cfg=kubelet_cfg)
+    opts, info = _opts(vm_overhead), _info(arena, name)
+    opts.reserved_enis = reserved_enis
+    nc = catalog.nodeclass(arena, kubelet_cfg=kubelet_cfg, ami_family=family, max_pods=max_pods)
     kube, sys_, ev = abi.ResourceList(), abi.ResourceList(), abi.ResourceList()
     assert lib.kp_instance_type_overhead(C.byref(opts), C.byref(info), C.byref(nc), C.byref(kube), C.byref(sys_),
                                          C.byref(ev)) == 0
@@ -47,11 +49,13 @@ def product(lib, kubelet_cfg, vm_overhead=None):
     return parts, catalog.resource_dict(cap)
 
 
-def oracle(kubelet_cfg, vm_overhead=None):
+def oracle(kubelet_cfg, vm_overhead=None, family="AL2023", name="m5.xlarge", max_pods=None, reserved_enis=0):
     from oracle import pyoracle
     arena = abi.Arena()
-    nc = catalog.nodeclass(arena, kubelet_cfg=kubelet_cfg)
-    cap, ovh = pyoracle.instance_type_resolve(_opts(vm_overhead), _info(arena), nc)
+    nc = catalog.nodeclass(arena, kubelet_cfg=kubelet_cfg, ami_family=family, max_pods=max_pods)
+    opts = _opts(vm_overhead)
+    opts.reserved_enis = reserved_enis
+    cap, ovh = pyoracle.instance_type_resolve(opts, _info(arena, name), nc)
     return [catalog.resource_dict(x) for x in (ovh.kube_reserved, ovh.system_reserved, ovh.eviction_threshold)], \
         catalog.resource_dict(cap)
 
@@ -59,8 +63,8 @@ def oracle(kubelet_cfg, vm_overhead=None):
 BACKENDS = ["product", "oracle"]
 
 
-def run(backend, lib, cfg, vm_overhead=None):
-    return product(lib, cfg, vm_overhead) if backend == "product" else oracle(cfg, vm_overhead)
+def run(backend, lib, cfg, vm_overhead=None, **kw):
+    return product(lib, cfg, vm_overhead, **kw) if backend == "product" else oracle(cfg, vm_overhead, **kw)
 
 
 def q(d, k):
@@ -166,3 +170,63 @@ def test_parse_quantity():
     assert catalog.parse_quantity("2") == 2000 and catalog.parse_quantity("80m") == 80
     assert catalog.parse_quantity("20Gi") == 20 * GI * 1000 and catalog.parse_quantity("1.5") == 1500
     assert catalog.parse_quantity("1G") == 10**12 and catalog.parse_quantity("500Mi") == 500 * MI * 1000
+
+
+# ---- AMI families -------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("backend", BACKENDS)
+def test_bottlerocket_ignores_eviction_soft(backend, lib):
+    """R:suite_test.go:1397-1430: Bottlerocket's EvictionSoftEnabled is false, so evictionHard alone sets it."""
+    cfg = dict(SYS_KUBE, eviction_hard={"memory.available": "1Gi"}, eviction_soft={"memory.available": "10Gi"})
+    (_, _, ev), _ = run(backend, lib, cfg, family="Bottlerocket")
+    assert q(ev, "memory") == 1 * GI * 1000
+    (_, _, ev2), _ = run(backend, lib, cfg, family="AL2023")  # the default family takes the larger soft signal
+    assert q(ev2, "memory") == 10 * GI * 1000
+
+
+FAMILY_MAXPODS = [("AL2", 10, 640), ("AL2023", 10, 640), ("Bottlerocket", 10, 365), ("Windows2019", 10, 365),
+                  ("Windows2022", 10, 365), ("Custom", 10, 640)]  # R:suite_test.go:1664-1669 (11 * pods + 255 Mi)
+FAMILY_RESERVED_ENIS = [("AL2", 24, 640), ("AL2023", 24, 640), ("Bottlerocket", 24, 519), ("Windows2019", 110, 1465),
+                        ("Windows2022", 110, 1465), ("Custom", 24, 640)]  # R:suite_test.go:1738-1743
+
+
+@pytest.mark.parametrize("backend", BACKENDS)
+@pytest.mark.parametrize("family,pods,mem_mi", FAMILY_MAXPODS)
+def test_family_max_pods_and_kube_reserved_memory(backend, lib, family, pods, mem_mi):
+    """t3.large (3 ENIs x 12 IPv4), kubelet maxPods 10: pods 10 everywhere; kube-reserved memory from the ENI-limited
+    count (35) for the families with UsesENILimitedMemoryOverhead, from pods() otherwise (R:suite_test.go:1626-1670)."""
+    (kube, _, _), cap = run(backend, lib, {}, family=family, name="t3.large", max_pods=10)
+    assert q(cap, "pods") == pods * 1000
+    assert q(kube, "memory") == mem_mi * MI * 1000
+
+
+@pytest.mark.parametrize("backend", BACKENDS)
+@pytest.mark.parametrize("family,pods,mem_mi", FAMILY_RESERVED_ENIS)
+def test_family_reserved_enis(backend, lib, family, pods, mem_mi):
+    """reservedENIs 1: (3 - 1) * (12 - 1) + 2 = 24 pods where ENI-limited density applies, 110 on Windows
+    (R:suite_test.go:1697-1744)."""
+    (kube, _, _), cap = run(backend, lib, {}, family=family, name="t3.large", reserved_enis=1)
+    assert q(cap, "pods") == pods * 1000
+    assert q(kube, "memory") == mem_mi * MI * 1000
+
+
+@pytest.mark.parametrize("backend", BACKENDS)
+def test_windows_pods_110_and_private_ipv4(backend, lib):
+    """R:suite_test.go:979-1001: a Windows nodeclass without maxPods gives every type 110 pods; amd64 types in the VPC
+    limits table get PrivateIPv4Address = IPv4 per interface - 1 (R:types.go:151-153, 477-484), 50Gi root volume."""
+    for name in ("m5.xlarge", "t3.large", "c6g.large"):
+        _, cap = run(backend, lib, {}, family="Windows2022", name=name)
+        assert q(cap, "pods") == 110 * 1000
+        rows = {r["name"]: r for r in catalog.load_ec2_table()}
+        r = rows[name]
+        want = (r["ipv4_per_eni"] - 1) * 1000 if r["arch"] == "amd64" and r["eni_source"] == "vpclimits" else 0
+        assert q(cap, "vpc.amazonaws.com/PrivateIPv4Address") == want
+        assert q(cap, "ephemeral-storage") == 50 * GI * 1000
+
+
+def test_product_equals_oracle_every_family(lib):
+    """Capacity and the three overhead lists, product == oracle, for every docs type and every AMI family."""
+    rows = catalog.load_ec2_table()
+    for family in abi.AMI_FAMILIES:
+        for r in rows[::7]:
+            assert product(lib, dict(SYS_KUBE, eviction_soft={"memory.available": "5%"}), family=family, name=r["name"]) == \
+                oracle(dict(SYS_KUBE, eviction_soft={"memory.available": "5%"}), family=family, name=r["name"]), (family, r["name"])

@@ -10,6 +10,8 @@ fake CreateFleet with InsufficientCapacityPools, ICE marks, re-Solve (tests/scen
   ICE cache expiry                    R:pkg/providers/instancetype/suite_test.go:2093-2111
   on-demand when spot is ICE'd        R:pkg/providers/instancetype/suite_test.go:2139-2174
   ICE'd type stays listed             R:pkg/providers/instancetype/suite_test.go:2175-2226 (no available offering left)
+  Windows PrivateIPv4Address          R:pkg/providers/instancetype/suite_test.go:639-706 (launched on a type the VPC
+                                      limits table advertises; not scheduled on one it does not)
   capacity type                       R:pkg/providers/instancetype/suite_test.go:2229-2244 (default on-demand; spot when
                                       flexible to both)
 """
@@ -226,3 +228,48 @@ def test_capacity_type(backend, cts, want, mk, lib):
     env = mk(backend, types)
     nodes, pod_node = env.provision([NodePool("default", 0, 0, [(CT, "In", cts)])], [PodShape(rq())], [1])
     assert pod_node == [0] and nodes[0]["capacity_type"] == want
+
+
+PIP = "vpc.amazonaws.com/PrivateIPv4Address"
+
+
+def _test_type_row():
+    """The reference's fabricated "test" type (R:suite_test.go:657-680): 2 vCPU, 8 GiB, x86_64, 3 ENIs x 10 IPv4, absent
+    from the VPC limits table (so PrivateIPv4Address capacity 0), offered in test-zone-1a."""
+    from kpamd import catalog
+    base = dict(next(r for r in catalog.load_ec2_table() if r["name"] == "m5.large"))
+    base.update(name="test", vcpu=2, memory_mib=8192, arch="amd64", max_enis=3, ipv4_per_eni=10, eni_source="ec2",
+                trunking=0, branch_enis=0, gpu_name="", gpu_manufacturer="", gpu_count=0, gpu_memory_mib="",
+                accel_name="", accel_manufacturer="", accel_count=0, neuron_devices=0, neuron_cores_per_device=0,
+                efa=0, local_nvme_gb="")
+    return base
+
+
+@pytest.mark.parametrize("backend", BACKENDS)
+def test_windows_private_ipv4_launch(backend, mk, lib):
+    """windows2022 nodeclass, a pod requesting one vpc.amazonaws.com/PrivateIPv4Address: scheduled, on a type the limits
+    table advertises (IPv4PerInterface != 0) (R:suite_test.go:639-654)."""
+    import scenarios
+    from kpamd import catalog
+    types = scenarios.fake_catalog(lib, ami_family="Windows2022")
+    env = mk(backend, types)
+    nodes, pod_node = env.provision([NodePool("default", 0, 0, OD_POOL)], [PodShape(rq(**{PIP: 1000}))], [1])
+    assert pod_node == [0]
+    row = {r["name"]: r for r in catalog.load_ec2_table()}[nodes[0]["type"]]
+    assert row["eni_source"] == "vpclimits" and row["ipv4_per_eni"] > 0
+    it = next(t for t in types if t.name == nodes[0]["type"])
+    assert ("kubernetes.io/os", "In", ["windows"]) in [tuple(r[:3]) for r in it.requirements]
+
+
+@pytest.mark.parametrize("backend", BACKENDS)
+def test_windows_private_ipv4_not_advertised(backend, mk, lib):
+    """The "test" type has IPv4 addresses but is not in the limits table: a pod requesting PrivateIPv4Address on a NodePool
+    restricted to it stays pending (R:suite_test.go:655-706)."""
+    import scenarios
+    types = scenarios.fake_catalog(lib, ami_family="Windows2022", extra_rows=[(_test_type_row(), ["test-zone-1a"])])
+    env = mk(backend, types)
+    pool = [NodePool("default", 0, 0, OD_POOL + [(IT, "In", ["test"])])]
+    _, pod_node = env.provision(pool, [PodShape(rq(**{PIP: 1000}))], [1])
+    assert pod_node == [None]
+    _, pod_node = env.provision(pool, [PodShape(rq())], [1])  # the type itself is launchable
+    assert pod_node == [0]
