@@ -89,7 +89,9 @@ struct SolveArgs {
   const int32_t* tg_maxskew;         // [G]
   const int32_t* tg_mindom;          // [G] minDomains, 0: nil
   const int32_t* tg_aff;             // [G] node filter has an affinity term (NodeAffinityPolicy Honor)
-  const int32_t* tg_term_base;       // [G] its term in tg_terms
+  const int32_t* tg_term_base;       // [G] its first term in tg_terms
+  const int32_t* tg_nterm;           // [G] its terms (ORed: MakeTopologyNodeFilter over the required terms)
+  int32_t* tg_live;                  // [G] 1: the group exists (mutable: a relaxation's Topology.Update makes it)
   const uint64_t* tg_filt_tol;       // [G] bit ts: node filter admits taint set ts (NodeTaintsPolicy)
   const uint8_t* tg_terms;           // KReqs
   const uint64_t* tg_terms_negop;

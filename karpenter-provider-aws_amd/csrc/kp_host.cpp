@@ -1241,6 +1241,7 @@ struct Compiled {
   vector<uint64_t> tg_filt_tol, tg_reg, tg_terms_negop;
   vector<KReqs> tg_terms;
   vector<int32_t> tg_cnt;    // [G][64]
+  vector<int32_t> tg_live;   // [G] 1: the group exists (NewTopology, or a Topology.Update made it); Record skips others
   vector<uint8_t> hcnt0;     // [GH][E]
   vector<int32_t> shape_rec_base, shape_rec_n, rec_list;
   vector<int32_t> sl_own_base, sl_own_n, own_group, own_self;
@@ -1419,7 +1420,8 @@ int32_t EncodeHostPorts(const vector<vector<HostPortKey>>& shapes, const vector<
 }
 
 int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector<RawReqs>>& strict_levels,
-                        const vector<vector<vector<int>>>& spread_levels, const vector<int>& np_taintset) {
+                        const vector<vector<vector<int>>>& spread_levels, const vector<int>& np_taintset,
+                        const vector<vector<vector<RawReqs>>>& filter_levels) {
   const Dict& d = cp.B->d;
   const int E = (int)cp.ex_input.size();
   cp.tkey_slot.assign(KP_MAX_KEYS, -1);
@@ -1511,15 +1513,23 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
   // group identity per (shape, spread index)
   vector<vector<int>> sgroup(in->n_shapes);
   vector<char> seen(in->n_shapes, 0);
-  auto group_of = [&](uint32_t s, int j) -> int32_t {
+  // A spread group at relaxation level l of shape s. MakeTopologyNodeFilter: the nodeSelector with each remaining
+  // required node-affinity term (ORed); relaxing a term (Preferences.removeRequiredNodeAffinityTerm) changes the
+  // filter and so the group identity: Topology.Update then makes a new group, counted from the cluster alone, which
+  // exists (is live: records count into it) from that first relaxation on (upstream Topology.Update).
+  auto group_of = [&](uint32_t s, int j, int l, bool live) -> int32_t {
     const kp_pod_shape& sh = in->shapes[s];
     const kp_topology_spread& t = sh.topology_spread[j];
     const string key = t.topology_key ? t.topology_key : "";
     const bool aff = t.node_affinity_policy != KP_POLICY_IGNORE, taint = t.node_taints_policy == KP_POLICY_HONOR;
-    // MakeTopologyNodeFilter: nodeSelector (+ the required term)
-    const KReqs filt = Compile(d, strict_levels[s][0]);
+    vector<KReqs> filts;
+    for (auto& fr : filter_levels[s][l]) filts.push_back(Compile(d, fr));
+    bool nonempty = true;  // an empty term admits every node: the filter is vacuous
+    for (auto& f : filts) nonempty = nonempty && f.present != 0;
+    string fcanon;
+    for (auto& f : filts) fcanon += "[" + KCanon(d, f) + "]";
     string id = key + "|" + std::to_string(t.max_skew) + "|" + (sh.namespace_ ? sh.namespace_ : "") + "|" +
-                SelectorCanon(t.selector) + "|" + std::to_string(aff) + std::to_string(taint) + "|[" + KCanon(d, filt) + "]";
+                SelectorCanon(t.selector) + "|" + std::to_string(aff) + std::to_string(taint) + "|" + fcanon;
     if (taint)
       for (uint32_t i = 0; i < sh.n_tolerations; i++) {
         const kp_toleration& x = sh.tolerations[i];
@@ -1527,9 +1537,13 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
               std::to_string(x.effect) + ")";
       }
     auto it = ids.find(id);
-    if (it != ids.end()) return it->second;
+    if (it != ids.end()) {
+      if (live) cp.tg_live[it->second] = 1;
+      return it->second;
+    }
     const int g = cp.G++;
     ids[id] = g;
+    cp.tg_live.push_back(live ? 1 : 0);
     g_shape.push_back((int)s);
     g_spec.push_back(&t);
     g_sel.push_back(&t.selector);
@@ -1551,15 +1565,15 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
     cp.tg_row.push_back(row);
     cp.tg_maxskew.push_back(t.max_skew);
     cp.tg_mindom.push_back(t.min_domains > 0 ? t.min_domains : 0);
-    // filter: affinity terms (none when the filter is empty: everything matches)
+    // filter: affinity terms, ORed (none when a term is empty: everything matches)
     cp.tg_term_base.push_back((int32_t)cp.tg_terms.size());
-    const bool nonempty = filt.present != 0;
     cp.tg_aff.push_back(aff && nonempty ? 1 : 0);
-    cp.tg_nterm.push_back(aff && nonempty ? 1 : 0);
-    if (aff && nonempty) {
-      cp.tg_terms.push_back(filt);
-      cp.tg_terms_negop.push_back(NegOp(d, filt));
-    }
+    cp.tg_nterm.push_back(aff && nonempty ? (int32_t)filts.size() : 0);
+    if (aff && nonempty)
+      for (auto& f : filts) {
+        cp.tg_terms.push_back(f);
+        cp.tg_terms_negop.push_back(NegOp(d, f));
+      }
     cp.tg_filt_tol.push_back(taint ? cp.shape_tolerates[s] : ~0ull);
     // NewTopologyGroup: every known domain of the key, with a zero count (ForEachDomain + taint policy)
     uint64_t reg = 0;
@@ -1575,8 +1589,10 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
     auto filter_ok = [&](uint32_t ni) {
       const int ts = cp.ex_taintset[ex_pos[ni]];
       if (taint && !((cp.shape_tolerates[s] >> ts) & 1)) return false;
-      if (aff && nonempty && !HostCompatible(d, node_reqs[ni], filt, false)) return false;
-      return true;
+      if (!(aff && nonempty)) return true;
+      for (auto& f : filts)
+        if (HostCompatible(d, node_reqs[ni], f, false)) return true;
+      return false;
     };
     const string ns = sh.namespace_ ? sh.namespace_ : "";
     for (auto& bs : bsets) {
@@ -1585,7 +1601,7 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
       if (row >= 0) {  // hostname: the node's label or, failing that, its name — one domain per node
         if (!filter_ok(ni)) continue;
         uint8_t& c = cp.hcnt0[(size_t)row * std::max(E, 1) + ex_pos[ni]];
-        if (c < 255) c++;
+        if (c < 254) c++;  // (255: an unregistered domain, below)
       } else {
         auto lv = node_labels[ni].find(key);
         if (lv == node_labels[ni].end() || !filter_ok(ni)) continue;
@@ -1596,8 +1612,7 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
       }
     }
     if (k >= 0) {  // the existing nodes' domains depend only on (key, node filter): cached across groups
-      string fid = key + "|" + std::to_string(aff && nonempty) + "[" + KCanon(d, filt) + "]" +
-                   (taint ? std::to_string(cp.shape_tolerates[s]) : string("-"));
+      string fid = key + "|" + std::to_string(aff && nonempty) + fcanon + (taint ? std::to_string(cp.shape_tolerates[s]) : string("-"));
       auto it = node_domains.find(fid);
       if (it == node_domains.end()) {
         uint64_t m = 0;
@@ -1609,6 +1624,21 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
         it = node_domains.emplace(fid, m).first;
       }
       cp.tg_reg[g] |= it->second;
+    }
+    if (row >= 0 && !live && E) {
+      // a hostname group a relaxation creates (Topology.Update after NewTopology): its domains are only what
+      // countDomains registers, the filter-matching nodes with a hostname label and the nodes of the pods it counted
+      // (NewTopology's Register of every existing node came before it). An unregistered node holds 255: the spread
+      // test fails on it until a Record registers it; the NodeClaims created before the group get 255 on the device
+      // when the group comes to exist.
+      vector<char> counted(in->n_existing, 0);
+      for (auto& bs : bsets)
+        if (ns == bs.ns && SelectorMatches(t.selector, bs.labels))
+          for (const uint32_t ni : bs.nodes) counted[ni] = 1;
+      for (uint32_t ni = 0; ni < in->n_existing; ni++) {
+        const bool reg = filter_ok(ni) && (node_labels[ni].count(kHostname) || counted[ni]);
+        if (!reg) cp.hcnt0[(size_t)row * E + ex_pos[ni]] = 255;
+      }
     }
     return g;
   };
@@ -1642,7 +1672,7 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
   auto record_bound = [&](int g, uint32_t ni) {
     if (cp.tg_row[g] >= 0) {
       uint8_t& c = cp.hcnt0[(size_t)cp.tg_row[g] * std::max(E, 1) + ex_pos[ni]];
-      if (c < 255) c++;
+      if (c < 254) c++;
       cp.tg_reg[g] |= 1;
     } else {
       const int k = cp.tg_key[g];
@@ -1661,6 +1691,7 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
     if (it != ids.end()) return it->second;
     const int g = cp.G++;
     ids[id] = g;
+    cp.tg_live.push_back(1);
     g_shape.push_back(-1);
     g_spec.push_back(nullptr);
     g_sel.push_back(&t.selector);
@@ -1713,7 +1744,7 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
     seen[s] = 1;
     const kp_pod_shape& sh = in->shapes[s];
     for (uint32_t j = 0; j < sh.n_topology_spread; j++) {
-      const int g = group_of(s, (int)j);
+      const int g = group_of(s, (int)j, 0, true);
       if (g < 0) return KP_E_UNSUPPORTED;
       sgroup[s].push_back(g);
     }
@@ -1783,7 +1814,7 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
     if (!n_terms && inv_owned[s].empty()) continue;
     if (sgroup[s].empty() && n_terms) {  // shape without pods: no groups were created for it
       for (uint32_t j = 0; j < sh.n_topology_spread; j++) {
-        const int g = group_of(s, (int)j);
+        const int g = group_of(s, (int)j, 0, false);
         if (g < 0) return KP_E_UNSUPPORTED;
         sgroup[s].push_back(g);
       }
@@ -1805,7 +1836,9 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
       cp.sl_own_n[sl] = (int32_t)sp.size();
       const KReqs strict = Compile(d, strict_levels[s][l]);
       for (int j : sp) {
-        const int g = j < 0 ? -1 - j : sgroup[s][j];
+        // spreads: the level's group (a relaxed required term makes another one, live once a pod relaxes to it)
+        const int g = j < 0 ? -1 - j : j < (int)sh.n_topology_spread ? group_of(s, j, l, false) : sgroup[s][j];
+        if (g < 0) return KP_E_UNSUPPORTED;
         cp.own_group.push_back(g);
         // self: the spread's / affinity term's selector matches the pod (spread: count + 1; affinity: it may
         // bootstrap); anti-affinity accepts count == 0 only
@@ -1851,6 +1884,8 @@ struct SolveRaw {
   vector<vector<RawReqs>> levels, strict_levels;  // per shape: NewPodRequirements after successive Relax
   vector<vector<vector<int>>> spread_levels;      // per level: topology terms (j < n_topology_spread: spread j;
                                                   // n_topology_spread + a: anti-affinity term a of AntiTerms)
+  vector<vector<vector<RawReqs>>> filter_levels;  // per level: MakeTopologyNodeFilter's terms (nodeSelector + each
+                                                  // remaining required term; the nodeSelector alone when none)
   std::set<string> topo_keys;                     // non-hostname spread keys (need a dictionary id)
   vector<RawReqs> ex_labels;                      // per input existing node (hostname dropped)
 };
@@ -1941,10 +1976,9 @@ int32_t ParseSolve(const kp_solve_in* in, SolveRaw& raw) {
   raw.levels.assign(in->n_shapes, {});
   raw.strict_levels.assign(in->n_shapes, {});
   raw.spread_levels.assign(in->n_shapes, {});
+  raw.filter_levels.assign(in->n_shapes, {});
   for (uint32_t s = 0; s < in->n_shapes; s++) {
     const kp_pod_shape& sh = in->shapes[s];
-    if (sh.n_topology_spread && sh.n_required_terms > 1)
-      return fail(KP_E_UNSUPPORTED, "topology spread with > 1 required node affinity terms (relaxation re-creates groups)");
     for (uint32_t j = 0; j < sh.n_topology_spread; j++) {
       const kp_topology_spread& t = sh.topology_spread[j];
       const string key = t.topology_key ? t.topology_key : "";
@@ -1999,6 +2033,13 @@ int32_t ParseSolve(const kp_solve_in* in, SolveRaw& raw) {
       RawReqs strict = ns;  // NewStrictPodRequirements: without the preferred term
       if (!req.empty()) strict.insert(strict.end(), req[0].begin(), req[0].end());
       raw.strict_levels[s].push_back(std::move(strict));
+      vector<RawReqs> filt;
+      for (auto& t : req) {
+        filt.push_back(ns);
+        filt.back().insert(filt.back().end(), t.begin(), t.end());
+      }
+      if (filt.empty()) filt.push_back(ns);
+      raw.filter_levels[s].push_back(std::move(filt));
       vector<int> terms = spreads;  // spreads, required anti-affinity terms, remaining preferred ones, affinity alike
       for (int a = 0; a < nRA; a++) terms.push_back(nS + a);
       for (int a : apref) terms.push_back(nS + nRA + a);
@@ -2293,7 +2334,7 @@ int32_t CompilePerCall(const kp_solve_in* in, const SolveRaw& raw, Compiled& cp)
     const int32_t hrc = EncodeHostPorts(hs, hn, cp);
     if (hrc) return hrc;
   }
-  int32_t rc = CompileTopology(in, cp, raw.strict_levels, raw.spread_levels, b.np_taintset);
+  int32_t rc = CompileTopology(in, cp, raw.strict_levels, raw.spread_levels, b.np_taintset, raw.filter_levels);
   if (rc) return rc;
   // pods: Queue order byCPUAndMemoryDescending (cpu desc, memory desc, creation asc, uid asc)
   cp.pod_shape.resize(in->n_pods);
@@ -2719,6 +2760,7 @@ static int32_t SolvePrepareLocal(kp_ctx* ctx, const kp_solve_in* in, kp_comm* co
   const size_t o_tgk = blob.put(C.tg_key), o_tgr = blob.put(C.tg_row), o_tgs = blob.put(C.tg_maxskew),
                o_tgm = blob.put(C.tg_mindom), o_tga = blob.put(C.tg_aff), o_tgtb = blob.put(C.tg_term_base),
                o_tgft = blob.put(C.tg_filt_tol), o_tgt = blob.put(C.tg_terms), o_tgtn = blob.put(C.tg_terms_negop),
+               o_tgnt = blob.put(C.tg_nterm),
                o_srb = blob.put(C.shape_rec_base), o_srn = blob.put(C.shape_rec_n), o_recl = blob.put(C.rec_list),
                o_slob = blob.put(C.sl_own_base), o_slon = blob.put(C.sl_own_n), o_owng = blob.put(C.own_group),
                o_owns = blob.put(C.own_self), o_ownp = blob.put(C.own_pd), o_sltk = blob.put(C.sl_topo_keys),
@@ -2754,6 +2796,7 @@ static int32_t SolvePrepareLocal(kp_ctx* ctx, const kp_solve_in* in, kp_comm* co
   const size_t o_exr = blob.put(C.ex_reqs);
   const size_t o_exrq = blob.put(C.ex_requests);
   const size_t o_tgc = blob.put(C.tg_cnt);
+  const size_t o_tglv = blob.put(C.tg_live);
   const size_t o_tgreg = blob.put(C.tg_reg);
   const size_t o_hcx = blob.put(C.hcnt0);
   const size_t o_exhp = blob.put(C.ex_hp);
@@ -2907,6 +2950,8 @@ static int32_t SolvePrepareLocal(kp_ctx* ctx, const kp_solve_in* in, kp_comm* co
   a.tg_terms = base + o_tgt;
   a.tg_terms_negop = (const uint64_t*)(base + o_tgtn);
   a.tg_cnt = (int32_t*)(base + o_tgc);
+  a.tg_live = (int32_t*)(base + o_tglv);
+  a.tg_nterm = (const int32_t*)(base + o_tgnt);
   a.tg_reg = (uint64_t*)(base + o_tgreg);
   a.hcnt_ex = base + o_hcx;
   a.hcnt_nc = base + o_hcnc;

@@ -2645,19 +2645,22 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
       const int ts = ex ? a.ex_taintset[idx] : a.nc_head[idx].taintset;
       for (int i = 0; i < rn; i++) {
         const int g = a.rec_list[a.shape_rec_base[shape] + i];
-        bool ok = (a.tg_filt_tol[g] >> ts) & 1;
-        if (ok && a.tg_aff[g]) {  // TopologyNodeFilter.MatchesRequirements: Compatible(node reqs, term)
-          const int tb = a.tg_term_base[g];
-          uint64_t mv;
-          ReqView rv;
-          ok = merge_compatible(D, fin, kreq_at(a.tg_terms, tb), a.tg_terms_negop[tb], !ex, mv, rv, &slots[0], vi);
+        bool ok = a.tg_live[g] && ((a.tg_filt_tol[g] >> ts) & 1);
+        if (ok && a.tg_aff[g]) {  // TopologyNodeFilter.MatchesRequirements: Compatible(node reqs, some term)
+          const int tb = a.tg_term_base[g], nt = a.tg_nterm[g];
+          ok = false;
+          for (int ti = 0; ti < nt && !ok; ti++) {
+            uint64_t mv;
+            ReqView rv;
+            ok = merge_compatible(D, fin, kreq_at(a.tg_terms, tb + ti), a.tg_terms_negop[tb + ti], !ex, mv, rv, &slots[0], vi);
+          }
         }
         if (!ok) continue;
         const int row = a.tg_row[g];
         if (row >= 0) {
           if (lane == 0) {
             uint8_t* c = ex ? &a.hcnt_ex[(size_t)row * a.n_existing + idx] : &a.hcnt_nc[(size_t)row * a.hnc_stride + idx];
-            if (*c < 255) *c += 1;
+            *c = *c == 255 ? 1 : *c < 254 ? *c + 1 : 254;  // 255: an unregistered domain (Record registers it)
             a.tg_reg[g] = 1;  // hostname rows: some domain has a count (ends pod-affinity bootstrap)
           }
         } else {
@@ -2689,6 +2692,19 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
         if (res_err) a.stats[40] += 1;
         const bool relaxed = !res_err && lvl + 1 < a.shape_nlevels[shape];
         if (relaxed) a.pod_level[pod] = lvl + 1;
+        if (TOPO && relaxed) {  // Topology.Update: the groups the relaxed pod owns now exist from here on
+          const int nsl = sl + 1;
+          for (int i = 0; i < a.sl_own_n[nsl]; i++) {
+            const int g = a.own_group[a.sl_own_base[nsl] + i];
+            if (a.tg_live[g]) continue;
+            a.tg_live[g] = 1;
+            // a new hostname group: the NodeClaims created before it were never registered with it (Register runs
+            // at NodeClaim creation over the groups that exist then)
+            const int row = a.tg_row[g];
+            if (row >= 0)
+              for (int x = 0; x < s_ctl[2]; x++) a.hcnt_nc[(size_t)row * a.hnc_stride + x] = 255;
+          }
+        }
         int len = s_ctl[1];
         int tail = s_ctl[0] + len;
         if (tail >= a.n_pods) tail -= a.n_pods;

@@ -194,10 +194,13 @@ def config3(catalog, n_pods=100_000, seed=3, n_deployments=1000, n_existing=5000
                    name=f"config3-{n}")
 
 
-def random_topology_problem(catalog, seed, n_types=80, n_pods=240, n_existing=12, n_shapes=10, n_pools=2):
+def random_topology_problem(catalog, seed, n_types=80, n_pods=240, n_existing=12, n_shapes=10, n_pools=2,
+                            multi_terms=0.0):
     """Randomized topology-spread scenario: zone / hostname / capacity-type keys, maxSkew 1-3, minDomains,
     ScheduleAnyway (relaxed away), selectors on own / other deployments / nil / expressions, node affinity
-    and taint inclusion policies, zone-restricted pools and pods, bound pods seeding the counts."""
+    and taint inclusion policies, zone-restricted pools and pods, bound pods seeding the counts.
+    multi_terms: the share of shapes with 2-3 required node-affinity terms, the first often unsatisfiable, so that
+    relaxation removes terms and re-creates the shapes' spread groups (Topology.Update)."""
     rng = np.random.default_rng(seed)
     idx = np.sort(rng.choice(len(catalog), size=min(n_types, len(catalog)), replace=False))
     cat = [catalog[i] for i in idx]
@@ -219,6 +222,16 @@ def random_topology_problem(catalog, seed, n_types=80, n_pods=240, n_existing=12
             sh.node_selector = {ZONE_KEY: str(rng.choice(ZONES))}
         if rng.random() < 0.2:
             sh.required_terms = [[("karpenter.sh/capacity-type", "In", [str(rng.choice(["spot", "on-demand"]))])]]
+        if multi_terms and rng.random() < multi_terms:
+            pool_terms = [[(K + "instance-category", "In", ["x"])],  # no such type: relaxed away
+                          [("karpenter.sh/capacity-type", "In", [str(rng.choice(["spot", "on-demand"]))])],
+                          [(ZONE_KEY, "In", [str(rng.choice(ZONES))])],
+                          [(K + "instance-category", "In", ["c", "m"])],
+                          [(ZONE_KEY, "NotIn", [str(rng.choice(ZONES))]), (K + "instance-generation", "Gt", ["3"])]]
+            pick = rng.choice(len(pool_terms), size=int(rng.integers(2, 4)), replace=False)
+            if rng.random() < 0.6 and 0 not in pick:
+                pick[0] = 0
+            sh.required_terms = [pool_terms[int(i)] for i in pick]
         if rng.random() < 0.2:
             sh.preferred_terms = [(int(rng.integers(1, 100)), [(ZONE_KEY, "In", [str(rng.choice(ZONES))])])]
         if rng.random() < 0.3:

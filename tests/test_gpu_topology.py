@@ -41,3 +41,27 @@ def test_topology_kats(ctx, catalog):
     for prob in probs:
         got, want = run_both(ctx, prob)
         check_same(got, want)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_topology_multi_terms(ctx, catalog, seed):
+    """Spread pods with 2-3 required node-affinity terms: relaxation re-creates their groups (per-level groups, live
+    from the first relaxation, hostname groups registering only later NodeClaims and countDomains' nodes)."""
+    from kpamd import synth
+    prob = synth.random_topology_problem(catalog, 100 + seed, n_existing=[0, 12, 30][seed % 3], multi_terms=0.5)
+    got, want = run_both(ctx, prob)
+    check_same(got, want)
+
+
+def test_multi_term_kats(ctx, catalog):
+    from kpamd import synth
+    from kpamd.model import PodShape
+    a = kat.spread_shape("a", kat.ZONE, cpu=3500)
+    a.required_terms = [kat.CAT_X, kat.OD]
+    b = kat.spread_shape("a", kat.ZONE, cpu=3600)
+    c = PodShape(synth.req_res(500, 1024), labels={"app": "a"})
+    h = kat.spread_shape("a", kat.HOST, cpu=400)
+    h.required_terms = [kat.CAT_X, kat.OD]
+    for prob in [kat.problem(catalog, [a], [9]), kat.problem(catalog, [b, a], [2, 3]), kat.problem(catalog, [c, h], [2, 2])]:
+        got, want = run_both(ctx, prob)
+        check_same(got, want)

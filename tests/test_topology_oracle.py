@@ -132,11 +132,67 @@ def test_random_topology_deterministic(catalog, seed):
 
 def test_device_host_compile_accepts_topology(catalog):
     """kp_solve_validate (host compile of the device path, no GPU) accepts every topology scenario the GPU
-    parity tests run, and rejects what the device does not implement."""
+    parity tests run (spread with several required node-affinity terms included), and rejects what the device does
+    not implement (a spread maxSkew past 250)."""
     import kpamd
     for seed in range(16):
         assert kpamd.validate(synth.random_topology_problem(catalog, seed, n_existing=[0, 12, 30][seed % 3])) == 0
+        assert kpamd.validate(synth.random_topology_problem(catalog, 100 + seed, multi_terms=0.5)) == 0
     assert kpamd.validate(synth.config3(catalog, n_pods=3000, n_deployments=60, n_existing=150)) == 0
-    bad = spread_shape("a", ZONE)
-    bad.required_terms = [[("kubernetes.io/arch", "In", ["amd64"])], [("kubernetes.io/arch", "In", ["arm64"])]]
+    two = spread_shape("a", ZONE)
+    two.required_terms = [[("kubernetes.io/arch", "In", ["amd64"])], [("kubernetes.io/arch", "In", ["arm64"])]]
+    assert kpamd.validate(problem(catalog, [two], [2])) == 0
+    bad = spread_shape("a", ZONE, skew=251)
     assert kpamd.validate(problem(catalog, [bad], [2])) == kpamd.abi.KP_E_UNSUPPORTED
+
+
+# ---- spread with several required node-affinity terms: relaxation re-creates the groups (Topology.Update) --------
+CAT_X = [("karpenter.k8s.aws/instance-category", "In", ["x"])]  # no type has it: relaxed away
+OD = [("karpenter.sh/capacity-type", "In", ["on-demand"])]
+
+
+def test_spread_with_required_terms_relaxes(catalog):
+    """MakeTopologyNodeFilter ORs the required terms; the first term here matches no type, so Preferences.Relax drops
+    it (removeRequiredNodeAffinityTerm) and the pods schedule under the second, still zone-spread (skew 1)."""
+    a = spread_shape("a", ZONE, cpu=3500)
+    a.required_terms = [CAT_X, OD]
+    r = solve(problem(catalog, [a], [9]))
+    assert (r["placement"] >= 0).all()
+    zones = Counter(nc_zone(nc) for nc in r["nodeclaims"] for _ in nc["pods"])
+    assert sorted(zones.values()) == [3, 3, 3]
+    for nc in r["nodeclaims"]:
+        assert ("karpenter.sh/capacity-type", "In", ["on-demand"], None) in nc["requirements"]
+
+
+def test_relaxed_group_counts_from_cluster_only(catalog):
+    """The group a relaxation creates counts the cluster (countDomains), not the pods this Solve placed before it
+    existed: two app=a pods (bigger, first) spread to zones a and b; then three app=a pods whose first required term
+    fails relax to a new group (other node filter) that starts from zero counts, so the first of them joins the zone-a
+    NodeClaim (with the earlier pods counted it would have opened zone c), the next the zone-b one, the last opens zone
+    c. Upstream Topology.Update; parity unpinned beyond this written semantics."""
+    b = spread_shape("a", ZONE, cpu=3600)
+    a = spread_shape("a", ZONE, cpu=3500)
+    a.required_terms = [CAT_X, OD]
+    r = solve(problem(catalog, [b, a], [2, 3]))
+    assert list(r["placement"]) == [0, 1, 0, 1, 2]
+    assert [nc_zone(nc) for nc in r["nodeclaims"]] == [("test-zone-1a",), ("test-zone-1b",), ("test-zone-1c",)]
+
+
+def test_relaxed_hostname_group_registers_new_nodeclaims_only(catalog):
+    """A hostname spread group created by a relaxation has not registered the NodeClaims made before it (Register runs
+    at NodeClaim creation): the relaxed pods cannot join them and open their own."""
+    b = PodShape(synth.req_res(500, 1024), labels={"app": "a"})
+    a = spread_shape("a", HOST, cpu=400)
+    a.required_terms = [CAT_X, OD]
+    r = solve(problem(catalog, [b, a], [2, 2]))
+    assert (r["placement"] >= 0).all()
+    assert r["placement"][0] == r["placement"][1] == 0  # b pods share one NodeClaim
+    assert r["placement"][2] != 0 and r["placement"][3] != 0 and r["placement"][2] != r["placement"][3]
+
+
+def test_random_multi_term_topology_runs(catalog):
+    for seed in range(4):
+        prob = synth.random_topology_problem(catalog, 100 + seed, multi_terms=0.5)
+        assert any(len(sh.required_terms) > 1 and sh.topology_spread for sh in prob.shapes)
+        r = solve(prob)
+        assert len(r["placement"]) == prob.n_pods
