@@ -140,9 +140,10 @@ typedef struct kp_offering {
   double price;
   int32_t available;
   int32_t reservation_capacity; /* Offering.ReservationCapacity (R:offering.go:178): read by ReservedOfferingFilter.
-                                   Filter and launch plans take reserved offerings (ABI v7); a Solve / cluster plan
-                                   over a catalogue holding an offering with a reservation id or type returns
-                                   KP_E_UNSUPPORTED (the ReservationManager's accounting is not modelled) */
+                                   Filter and launch plans take reserved offerings (ABI v7), Solve plans too (ABI
+                                   v9: NodeClaim.reserveOfferings against each reservation's capacity, see
+                                   kp_solve_in.reserved_offering_mode); a cluster plan over a catalogue holding an
+                                   offering with a reservation id or type returns KP_E_UNSUPPORTED */
 } kp_offering;
 
 /* cloudprovider.InstanceType after InjectOfferings. */
@@ -494,7 +495,7 @@ typedef struct kp_kubelet {
   kp_eviction_value soft_memory_available, soft_nodefs_available;
 } kp_kubelet;
 
-/* EC2NodeClass subset that changes results (AL2023 family; kubelet overrides). */
+/* EC2NodeClass subset that changes results (AMI family, kubelet overrides). */
 typedef struct kp_nodeclass {
   const char* region;
   const char* const* zones;      /* subnet zones (ZoneInfo) */
@@ -712,8 +713,10 @@ int32_t kp_simulate_batch(kp_ctx* ctx, const kp_cluster* cluster, const uint32_t
  * snapshot: SingleNodeConsolidation, MultiNodeConsolidation's binary search, the sweep). prepare
  * compiles and uploads the snapshot and precomputes, per pod shape, the existing nodes it can ever use
  * and its NodeClaimTemplate outcome; simulate runs one batch of subsets on the resident snapshot.
- * Returns KP_E_UNSUPPORTED (the Go path then runs) for: NodePool limits, topology spread, a pod
- * NotIn/DoesNotExist requirement on a label key some node lacks, > 65535 pods in one subset. */
+ * NodePool limits, pending pods, deleting nodes, spot-to-spot and host ports run in the batched kernels; topology
+ * spread, pod (anti-)affinity and a pod NotIn/DoesNotExist requirement on a label key some node lacks take the general
+ * path (each subset a whole device Solve). Returns KP_E_UNSUPPORTED (the Go path then runs) for > 65535 pods in one
+ * subset and for catalogues holding capacity reservations. */
 typedef struct kp_cluster_plan kp_cluster_plan;
 int32_t kp_cluster_prepare(kp_ctx* ctx, const kp_cluster* cluster, kp_cluster_plan** out);
 int32_t kp_cluster_simulate(kp_cluster_plan* plan, const uint32_t* offsets, const uint32_t* nodes, uint32_t n_subsets,
