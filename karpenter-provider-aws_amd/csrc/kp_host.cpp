@@ -1767,6 +1767,29 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
       record_bound(g, bp.node);
     }
   }
+  // every other group a shape-level owns, before the recording lists are built: the groups of shapes without pods,
+  // and the spread groups of relaxed levels (a relaxation makes them exist; records must reach them from then on)
+  for (uint32_t s = 0; s < in->n_shapes; s++) {
+    const kp_pod_shape& sh = in->shapes[s];
+    const uint32_t n_terms = sh.n_topology_spread + PodTermCount(sh);
+    if (sgroup[s].empty() && n_terms) {  // shape without pods: no groups were created for it
+      for (uint32_t j = 0; j < sh.n_topology_spread; j++) {
+        const int g = group_of(s, (int)j, 0, false);
+        if (g < 0) return KP_E_UNSUPPORTED;
+        sgroup[s].push_back(g);
+      }
+      for (uint32_t a = 0; a < PodTermCount(sh); a++) {
+        bool aff = false;
+        const kp_pod_affinity_term& t = *PodTermAt(sh, (int)a, &aff);
+        const int g = anti_group(t, nss_of(t, sh.namespace_), false, aff);
+        if (g < 0) return KP_E_UNSUPPORTED;
+        sgroup[s].push_back(g);
+      }
+    }
+    for (int l = 1; l < cp.shape_nlevels[s]; l++)
+      for (int j : spread_levels[s][l])
+        if (j < (int)sh.n_topology_spread && group_of(s, j, l, false) < 0) return KP_E_UNSUPPORTED;
+  }
   if (cp.G == 0) return KP_OK;
   if ((size_t)cp.GH * (size_t)(E + in->n_pods) > ((size_t)1 << 31))
     return fail(KP_E_UNSUPPORTED, "%d hostname topologies x %u nodes", cp.GH, E + in->n_pods);
@@ -1812,20 +1835,6 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
     const kp_pod_shape& sh = in->shapes[s];
     const uint32_t n_terms = sh.n_topology_spread + PodTermCount(sh);
     if (!n_terms && inv_owned[s].empty()) continue;
-    if (sgroup[s].empty() && n_terms) {  // shape without pods: no groups were created for it
-      for (uint32_t j = 0; j < sh.n_topology_spread; j++) {
-        const int g = group_of(s, (int)j, 0, false);
-        if (g < 0) return KP_E_UNSUPPORTED;
-        sgroup[s].push_back(g);
-      }
-      for (uint32_t a = 0; a < PodTermCount(sh); a++) {
-        bool aff = false;
-        const kp_pod_affinity_term& t = *PodTermAt(sh, (int)a, &aff);
-        const int g = anti_group(t, nss_of(t, sh.namespace_), false, aff);
-        if (g < 0) return KP_E_UNSUPPORTED;
-        sgroup[s].push_back(g);
-      }
-    }
     const std::map<string, string> lm = LabelMap(sh.labels, sh.n_labels);
     for (int l = 0; l < cp.shape_nlevels[s]; l++) {
       const int sl = cp.shape_level_base[s] + l;

@@ -223,7 +223,7 @@ def random_topology_problem(catalog, seed, n_types=80, n_pods=240, n_existing=12
         if rng.random() < 0.2:
             sh.required_terms = [[("karpenter.sh/capacity-type", "In", [str(rng.choice(["spot", "on-demand"]))])]]
         if multi_terms and rng.random() < multi_terms:
-            pool_terms = [[(K + "instance-category", "In", ["x"])],  # no such type: relaxed away
+            pool_terms = [[(K + "instance-category", "In", ["x"])],  # x1 / x2 only: often unsatisfiable, relaxed away
                           [("karpenter.sh/capacity-type", "In", [str(rng.choice(["spot", "on-demand"]))])],
                           [(ZONE_KEY, "In", [str(rng.choice(ZONES))])],
                           [(K + "instance-category", "In", ["c", "m"])],

@@ -147,7 +147,7 @@ def test_device_host_compile_accepts_topology(catalog):
 
 
 # ---- spread with several required node-affinity terms: relaxation re-creates the groups (Topology.Update) --------
-CAT_X = [("karpenter.k8s.aws/instance-category", "In", ["x"])]  # no type has it: relaxed away
+CAT_X = [("karpenter.k8s.aws/instance-category", "In", ["x"])]  # the pool allows category m only: relaxed away
 OD = [("karpenter.sh/capacity-type", "In", ["on-demand"])]
 
 
