@@ -199,7 +199,7 @@ struct FeasArgs {
   int32_t T;
   int32_t n_queries;
   int32_t mode_compatible;   // 1: Compatible(q, type, WK) (CompatibleAvailableFilter); 0: type.Intersects(q)
-  int32_t pad_;
+  int32_t pad_;              // bits kernel: bit 0 = write the cheapest-price stream with non-temporal stores
   const uint8_t* q_reqs;     // [Q] KReqs
   const int64_t* q_requests; // [Q][NRES]
   uint64_t* out_mask;        // [Q][tiles]

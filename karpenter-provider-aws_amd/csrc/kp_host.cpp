@@ -3455,6 +3455,8 @@ int32_t kp_filter_prepare(kp_ctx* ctx, const kp_catalog* cat, const kp_feasibili
   // the bitset kernel (KP_FEAS_GLOBAL: the per-type global-gather kernel, kept as its cross-check)
   fa.bits = getenv("KP_FEAS_GLOBAL") ? 0 : 1;
   fa.blocks = (int32_t)std::min<uint32_t>(std::max<uint32_t>((n_queries + 7) / 8, 1), 8192);
+  if (const char* e = getenv("KP_FEAS_BLOCKS")) fa.blocks = std::max(1, std::min(65535, atoi(e)));  // measurement knob
+  fa.pad_ = getenv("KP_FEAS_TEMPORAL") ? 0 : 1;  // bit 0: the cheapest-price stream as non-temporal stores
   plan->n_queries = n_queries;
   plan->T = T;
   plan->tiles = tiles;

@@ -3086,7 +3086,20 @@ __global__ __launch_bounds__(FEAS_WAVES * 64) void feasibility_kernel(FeasArgs a
 // per-class-subset minima (a row copy, L2 -> HBM), or the min over the classes' price rows when C > KP_SUB_MAX_C.
 // The next row's header loads are issued before this row is evaluated.
 #define FEASB_WAVES 8
+#ifndef FEASB_CP
+#define FEASB_CP 8  // cheapest-row copy: loads in flight per lane before their stores (measured: 16 is slower)
+#endif
+#ifndef FEASB_EARLY
+#define FEASB_EARLY 0  // variant under measurement: the cheapest-row copy before the key / Fits / offering evaluation
+#endif
+#ifndef FEASB_MINW
+#define FEASB_MINW 8  // waves per SIMD the register budget must allow (measured: 0.1574 -> 0.1245 ms on 50k rows)
+#endif
+#if FEASB_MINW
+__global__ __launch_bounds__(FEASB_WAVES * 64, FEASB_MINW) void feasibility_bits_kernel(FeasArgs a) {
+#else
 __global__ __launch_bounds__(FEASB_WAVES * 64) void feasibility_bits_kernel(FeasArgs a) {
+#endif
   __shared__ DevDict D;
   __shared__ int64_t s_vint[KP_MAX_BOUND_KEYS * 64];
   __shared__ OfferClass s_cls[KP_MAX_CLASSES];
@@ -3157,6 +3170,42 @@ __global__ __launch_bounds__(FEASB_WAVES * 64) void feasibility_bits_kernel(Feas
                                             : v;
     }
     const uint64_t cls = allowed_classes<true>(D, (const OfferClass LDS*)s_cls, rv, allowed, negQ);
+    // cheapest compatible available offering price per type
+    auto cheapest_row = [&]() {
+      if (!a.out_cheapest) return;
+      GLB double* oc = (GLB double*)a.out_cheapest + (size_t)q * T;
+      if (price_sub) {  // a row copy: FEASB_CP loads in flight per lane before their stores (the pointers may alias)
+        const GLB double* ps = price_sub + (size_t)cls * T;
+        for (int t0 = 0; t0 < T; t0 += 64 * FEASB_CP) {
+          double vv[FEASB_CP];
+#pragma unroll
+          for (int i = 0; i < FEASB_CP; i++) {
+            const int t = t0 + i * 64 + lane;
+            vv[i] = t < T ? ps[t] : 0.0;
+          }
+          if (a.pad_ & 1) {
+#pragma unroll
+            for (int i = 0; i < FEASB_CP; i++) {
+              const int t = t0 + i * 64 + lane;
+              if (t < T) __builtin_nontemporal_store(vv[i], (double*)&oc[t]);
+            }
+          } else {
+#pragma unroll
+            for (int i = 0; i < FEASB_CP; i++) {
+              const int t = t0 + i * 64 + lane;
+              if (t < T) oc[t] = vv[i];
+            }
+          }
+        }
+      } else {
+        for (int t = lane; t < T; t += 64) {
+          double ch = __builtin_huge_val();
+          for (uint64_t m = cls; m; m &= m - 1) ch = fmin(ch, price_cm[(size_t)__builtin_ctzll(m) * T + t]);
+          oc[t] = ch;
+        }
+      }
+    };
+    if (FEASB_EARLY) cheapest_row();
     const uint32_t rmask = (uint32_t)__ballot(cur.rq > 0);
     uint64_t pass = nonneg;
     // Compatible(q, type, WK) part (a): types with a non-well-known key q does not define (rare: per-type loads)
@@ -3211,20 +3260,7 @@ __global__ __launch_bounds__(FEASB_WAVES * 64) void feasibility_bits_kernel(Feas
     for (uint64_t m = cls; m; m &= m - 1) av |= lw ? offer[(size_t)__builtin_ctzll(m) * TW + lane] : 0;
     pass &= av;
     if (lw) ((GLB uint64_t*)a.out_mask)[(size_t)q * TW + lane] = pass;
-    // cheapest compatible available offering price per type
-    if (a.out_cheapest) {
-      GLB double* oc = (GLB double*)a.out_cheapest + (size_t)q * T;
-      if (price_sub) {
-        const GLB double* ps = price_sub + (size_t)cls * T;
-        for (int t = lane; t < T; t += 64) oc[t] = ps[t];
-      } else {
-        for (int t = lane; t < T; t += 64) {
-          double ch = __builtin_huge_val();
-          for (uint64_t m = cls; m; m &= m - 1) ch = fmin(ch, price_cm[(size_t)__builtin_ctzll(m) * T + t]);
-          oc[t] = ch;
-        }
-      }
-    }
+    if (!FEASB_EARLY) cheapest_row();
   }
 }
 const void* feasibility_bits_kernel_ptr() { return (const void*)feasibility_bits_kernel; }
