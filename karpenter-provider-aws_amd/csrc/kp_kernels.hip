@@ -2342,11 +2342,35 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
       // ---- addToInflightNode: first NodeClaim in that order whose Add succeeds ------------------
       for (int base = start; base < n_nc && placed == -1; base += 4 * NT) {
         uint32_t flags = 0, iflags = 0, tflags = 0;
+        // 4 rounds per thread: independent, so their loads overlap. A spilled order (thousands of NodeClaims, long
+        // scans bound by the gathers' cache-line traffic) first filters on the headroom of the first two requested
+        // resources (one 16-byte load per position) and gathers the memo and the rest of the record for survivors.
+        int ncs[4];
+        uint32_t room_ok = 0;
+        int64_t r0s[4], r1s[4];
 #pragma unroll
-        for (int k = 0; k < 4; k++) {  // 4 rounds per thread: independent, so their loads overlap
+        for (int k = 0; k < 4; k++) {
           const int i = base + k * NT + tid;
-          if (i >= n_nc) continue;
-          const int nc = in_lds ? ((LdsI32)s_dyn)[i] : ((GlbI32)a.g_order)[i];
+          ncs[k] = i >= n_nc ? -1 : in_lds ? ((LdsI32)s_dyn)[i] : ((GlbI32)a.g_order)[i];
+        }
+        if (!in_lds) {
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            r0s[k] = r1s[k] = 0;
+            if (ncs[k] < 0) continue;
+            const int4 h = reinterpret_cast<const int4*>(a.nc_head + ncs[k])[0];
+            r0s[k] = i64_of(h.x, h.y);
+            r1s[k] = i64_of(h.z, h.w);
+          }
+#pragma unroll
+          for (int k = 0; k < 4; k++)
+            if (ncs[k] >= 0 && r0s[k] >= p0 && r1s[k] >= p1) room_ok |= 1u << k;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const int i = base + k * NT + tid;
+          if (i >= n_nc || (!in_lds && !((room_ok >> k) & 1))) continue;
+          const int nc = ncs[k];
           // every gather is issued unconditionally so they overlap (one round trip instead of a chain)
           const int32_t fl = nc < a.ncc ? a.nc_fail[(size_t)sl * a.ncc + nc] : -2;
           const HeadView hv = load_head(a.nc_head + nc, four);

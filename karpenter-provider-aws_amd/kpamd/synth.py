@@ -50,8 +50,9 @@ def config1(catalog, n_pods=1000, seed=1):
     return Problem([catalog], [np_], shapes, s, c, u, name=f"config1-{n_pods}")
 
 
-def config2(catalog, n_pods=50_000, seed=2, n_shapes=256):
-    """50k pods from 256 deployment shapes with mixed nodeSelector / node affinity / tolerations."""
+def config2(catalog, n_pods=50_000, seed=2, n_shapes=256, burst=False):
+    """50k pods from 256 deployment shapes with mixed nodeSelector / node affinity / tolerations. burst: each
+    deployment's pods are created within 2 s of its own start (ReplicaSet bursts) instead of uniformly over 600 s."""
     rng = np.random.default_rng(seed)
     shapes = []
     for i in range(n_shapes):
@@ -75,6 +76,10 @@ def config2(catalog, n_pods=50_000, seed=2, n_shapes=256):
             sh.node_selector = {"karpenter.sh/nodepool": "dedicated"}
         shapes.append(sh)
     s, c, u = _pods(rng, n_pods, len(shapes))
+    if burst:
+        brng = np.random.default_rng(seed + 1000)
+        start = brng.integers(0, 600, size=len(shapes))
+        c = (1_750_000_000 + start[s] + brng.integers(0, 2, size=n_pods)).astype(np.int64)
     pools = [
         NodePool("general", 10, 0, [("kubernetes.io/os", "In", ["linux"]),
                                     ("karpenter.sh/capacity-type", "In", ["on-demand", "spot"]),
