@@ -57,6 +57,8 @@ struct SolveArgs {
   const int32_t* ex_taintset;        // [E]
   const int64_t* ex_available;       // [E][NRES]
   int64_t* ex_requests;              // [E][NRES] (mutable)
+  int64_t* ex_room;                  // [4][E] available - requests of the first four requested resources (mutable;
+                                     // INT64_MAX past the requested ones)
   // in-flight NodeClaims (capacity n_pods)
   uint8_t* nc_reqs;                  // [P] KReqs
   uint64_t* nc_X;                    // [P][TW]

@@ -2804,6 +2804,18 @@ static int32_t SolvePrepareLocal(kp_ctx* ctx, const kp_solve_in* in, kp_comm* co
   const size_t o_trem = blob.put(C.tmpl_remaining);
   const size_t o_exr = blob.put(C.ex_reqs);
   const size_t o_exrq = blob.put(C.ex_requests);
+  // headroom rows of the existing nodes for the first four requested resources (req_res_mask order)
+  vector<int64_t> ex_room((size_t)4 * std::max(E, 1), INT64_MAX);
+  {
+    int k = 0;
+    for (int r = 0; r < KP_NRES && k < 4; r++) {
+      if (!((rmask >> r) & 1)) continue;
+      for (int e = 0; e < E; e++)
+        ex_room[(size_t)k * E + e] = C.ex_available[(size_t)e * KP_NRES + r] - C.ex_requests[(size_t)e * KP_NRES + r];
+      k++;
+    }
+  }
+  const size_t o_exroom = blob.put(ex_room);
   const size_t o_tgc = blob.put(C.tg_cnt);
   const size_t o_tglv = blob.put(C.tg_live);
   const size_t o_tgreg = blob.put(C.tg_reg);
@@ -2915,6 +2927,7 @@ static int32_t SolvePrepareLocal(kp_ctx* ctx, const kp_solve_in* in, kp_comm* co
   a.ex_taintset = (const int32_t*)(base + o_exts);
   a.ex_available = (const int64_t*)(base + o_exav);
   a.ex_requests = (int64_t*)(base + o_exrq);
+  a.ex_room = (int64_t*)(base + o_exroom);
   a.nc_reqs = base + o_ncr;
   a.nc_X = (uint64_t*)(base + o_ncX);
   a.nc_requests = (int64_t*)(base + o_ncrq);

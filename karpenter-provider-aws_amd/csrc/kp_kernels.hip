@@ -2238,6 +2238,8 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
     }
 
     // ---- addToExistingNode: lowest index whose CanAdd succeeds -------------------------------
+    const int64_t ep0 = rmask_all ? s_preq[rr0] : 0, ep1 = rm1 ? s_preq[rr1] : 0;  // the pod, per headroom row
+    const int64_t ep2 = rk2 >= 0 ? s_preq[rk2] : 0, ep3 = rk3 >= 0 ? s_preq[rk3] : 0;
     for (int base = s_ctl[17]; base < a.n_existing && placed == -1; base += 4 * NT) {
       uint32_t flags = 0, iflags = 0;
 #pragma unroll
@@ -2247,15 +2249,20 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
         const int32_t fl = a.ex_fail[(size_t)sl * a.n_existing + ec], ver = a.ex_ver[ec];
         const uint8_t sok = a.ex_static_ok[ec];
         const int32_t ts = a.ex_taintset[ec];
-        // Fits(Merge(requests, pod), available), exact: unrequested resources never change
-        const int64_t* av = a.ex_available + (size_t)ec * KP_NRES;
-        const int64_t* rq = a.ex_requests + (size_t)ec * KP_NRES;
-        bool cand = !rmask_all || (rq[rr0] + s_preq[rr0] <= av[rr0] && rq[rr1] + s_preq[rr1] <= av[rr1]);
+        // Fits(Merge(requests, pod), available), exact: unrequested resources never change. The headroom rows
+        // (available - requests of the first four requested resources, [4][E]) coalesce across the positions.
+        const size_t En = (size_t)a.n_existing;
+        bool cand = a.ex_room[ec] >= ep0 && a.ex_room[En + ec] >= ep1;
+        if (four) cand = cand && a.ex_room[2 * En + ec] >= ep2 && a.ex_room[3 * En + ec] >= ep3;
         cand = cand && fl != ver && fl != NC_NEVER && sok && ((tolmask >> ts) & 1);
         if (hpc) cand = cand && !(a.ex_hp[ec] & hpc);  // HostPortUsage.Conflicts (permanent: used bits only grow)
-        for (uint32_t rm = rr_rest; rm && cand; rm &= rm - 1) {
-          const int r = __builtin_ctz(rm);
-          cand = rq[r] + s_preq[r] <= av[r];
+        if (rr_b4 && cand) {  // a fifth requested resource and beyond
+          const int64_t* av = a.ex_available + (size_t)ec * KP_NRES;
+          const int64_t* rq = a.ex_requests + (size_t)ec * KP_NRES;
+          for (uint32_t rm = rr_b4; rm && cand; rm &= rm - 1) {
+            const int r = __builtin_ctz(rm);
+            cand = rq[r] + s_preq[r] <= av[r];
+          }
         }
         // topology, exact: hostname: count + self <= maxSkew (min is 0 for hostname; the count only changes
         // when the node takes a pod, i.e. with its version); dictionary key: the node's domain is its label
@@ -2301,6 +2308,10 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
           if (wave == win) {
             store_merged(reinterpret_cast<KReqs*>(a.ex_reqs + (size_t)ei * sizeof(KReqs)), rv, m_v, D.W, D.KB);
             if (lane < KP_NRES) a.ex_requests[(size_t)ei * KP_NRES + lane] += s_preq[lane];
+            if (lane < 4) {  // headroom rows of the first four requested resources
+              const int64_t d = lane == 0 ? ep0 : lane == 1 ? ep1 : lane == 2 ? ep2 : ep3;
+              a.ex_room[(size_t)lane * a.n_existing + ei] -= d;
+            }
             if (lane == 0) a.ex_ver[ei] += 1;
             if (lane == 0 && hpa) a.ex_hp[ei] |= hpa;
           }
@@ -2331,6 +2342,9 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
       else
         sort_newnodeclaims<NT>((GlbI32)a.g_order, (GlbI32)a.g_npods, s_ctl[2], s_ctl[10], s_ctl[11], s_ctl, &a.stats[31]);
       const int n_nc = s_ctl[2];
+      // a pod without requirements (at this level) merges into any NodeClaim without changing it: the append path
+      // is exact on every candidate, tagged or not (NodeClaim.Add = Fits over the remaining types)
+      const bool triv = s_B.present == 0;
       const int64_t p0 = rmask_all ? s_preq[rr0] : 0, p1 = rm1 ? s_preq[rr1] : 0;  // the pod, per record slot
       const int64_t p2 = rk2 >= 0 ? s_preq[rk2] : 0, p3 = rk3 >= 0 ? s_preq[rk3] : 0;
       const int start = res_strict ? 0 : min(min(s_ctl[19], s_ctl[16] >= 0 ? s_ctl[16] : INT32_MAX), n_nc);
@@ -2391,14 +2405,19 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
               cand = s_town[j].maxskew >= 0 ? c + s_town[j].self <= s_town[j].maxskew : (c > 0 || s_town[j].self);
             }
           if (cand) iflags |= 1u << k;  // passes everything that does not depend on the zone counts
-          if (cand && !own_n && fl >= NC_MERGED && !a.res_mode) tflags |= 1u << k;  // shape-level already merged: append path
+          bool pinned = true;  // every dictionary key the pod's groups spread over is one value on the NodeClaim
           for (int j = 0; j < own_n && cand; j++) {  // a NodeClaim pinned to one domain of a key can only take it
             const TopoOwn& o = s_town[j];
             if (o.key >= 0) {
               const uint8_t code = a.nc_tcode[(size_t)o.slot * a.hnc_stride + nc];
               cand = code == 0xFF || (code < 64 && ((s_tacc[j] >> (code & 63)) & 1));
+              pinned = pinned && code < 64;
             }
           }
+          // shape-level already merged: the append path (Fits alone). With topology groups only when the NodeClaim is
+          // pinned on their keys: topo_narrow then keeps its requirements (the acceptable domain is its own value,
+          // tested above; hostname rows exactly by the counts), so the Add changes nothing but requests and types
+          if (cand && (fl >= NC_MERGED || triv) && !a.res_mode && (!own_n || pinned)) tflags |= 1u << k;
           flags |= (cand ? 1u : 0u) << k;
         }
         if (own_n) first_pos_min<NT>(iflags, base + tid, &s_ctl[25]);
@@ -2444,7 +2463,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
             }
             if (tsub && lane == 0) tsub[0] += __builtin_amdgcn_s_memtime() - tm0;
             bool memo = !ok || !own_n;  // failures after the topology step depend on the counts
-            if (ok && own_n) ok = topo_narrow(D, own_n, s_town, s_tacc, s_tcnt, true, m_v, rv, vi);
+            if (ok && own_n && !fast) ok = topo_narrow(D, own_n, s_town, s_tacc, s_tcnt, true, m_v, rv, vi);
             if (ok && !fast) {
               const int pb = cat < 32 ? s_pvpb[cat] : a.pvp_base[sl * a.n_catalogs + cat];
               const uint64_t* pvp = a.shape_pvp + (size_t)pb * D.TW;
@@ -2472,7 +2491,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
                 store_merged(reinterpret_cast<KReqs*>(a.nc_reqs + (size_t)nc * sizeof(KReqs)), rv, m_v, D.W, D.KB);
                 if (a.n_tk) store_tcodes(a.n_tk, a.tk_keys, a.nc_tcode, a.hnc_stride, rv, m_v, nc);
               }
-              if (lane == 0 && !own_n && nc < a.ncc) a.nc_fail[(size_t)sl * a.ncc + nc] = NC_MERGED;
+              if (lane == 0 && nc < a.ncc) a.nc_fail[(size_t)sl * a.ncc + nc] = NC_MERGED;  // (count-independent)
               if (lane < D.TW) a.nc_X[(size_t)nc * D.TW + lane] = X;
               if (lane < KP_NRES) a.nc_requests[(size_t)nc * KP_NRES + lane] += s_preq[lane];
               if (lane == 0 && hpa) a.nc_hp[nc] |= hpa;
@@ -2602,7 +2621,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
                 if (a.hp_any) a.nc_hp[nc] = hpa;  // a template's HostPortUsage is empty
               }
               if (lane < KP_NRES) a.nc_fitj[(size_t)nc * KP_NRES + lane] = s_fitj[wave][lane];
-              if (lane == 0 && !own_n && nc < a.ncc) a.nc_fail[(size_t)sl * a.ncc + nc] = NC_MERGED;
+              if (lane == 0 && nc < a.ncc) a.nc_fail[(size_t)sl * a.ncc + nc] = NC_MERGED;
               if (a.res_mode) {
                 reserve_commit((int32_t LDS*)s_rcap, 0, nh);
                 if (lane == 0) a.nc_held[nc] = nh;
