@@ -1826,6 +1826,9 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
     }
   }
   for (uint32_t s = 0; s < in->n_shapes; s++) {
+    // each group once: the device Record gives every group of a pod its own lane
+    std::sort(recs[s].begin(), recs[s].end());
+    recs[s].erase(std::unique(recs[s].begin(), recs[s].end()), recs[s].end());
     cp.shape_rec_base[s] = (int32_t)cp.rec_list.size();
     cp.shape_rec_n[s] = (int32_t)recs[s].size();
     cp.rec_list.insert(cp.rec_list.end(), recs[s].begin(), recs[s].end());

@@ -2681,46 +2681,57 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
     // ---- Topology.Record: every group selecting the pod whose node filter admits the node counts it
     //      in the node's domain (dictionary keys: only once the key is a single value) -------------
     if (TOPO && placed != -1 && wave == 0) {
+      // lane i takes the i-th group: the groups' attributes are gathered together, and each lane updates its own
+      // group's counts (distinct groups: no two lanes touch one counter); node-filter terms go through the wave
       const int rn = a.shape_rec_n[shape];
+      const int rb = a.shape_rec_base[shape];
       const bool ex = placed <= -2;
       const int idx = ex ? -2 - placed : placed;
       const KReqs* fin = ex ? kreq_at(a.ex_reqs, idx) : kreq_at(a.nc_reqs, idx);
       const int ts = ex ? a.ex_taintset[idx] : a.nc_head[idx].taintset;
-      for (int i = 0; i < rn; i++) {
-        const int g = a.rec_list[a.shape_rec_base[shape] + i];
-        bool ok = a.tg_live[g] && ((a.tg_filt_tol[g] >> ts) & 1);
-        if (ok && a.tg_aff[g]) {  // TopologyNodeFilter.MatchesRequirements: Compatible(node reqs, some term)
-          const int tb = a.tg_term_base[g], nt = a.tg_nterm[g];
-          ok = false;
-          for (int ti = 0; ti < nt && !ok; ti++) {
+      for (int i0 = 0; i0 < rn; i0 += 64) {
+        const int i = i0 + lane;
+        const bool act = i < rn;
+        const int g = act ? a.rec_list[rb + i] : 0;
+        bool ok = act && a.tg_live[g] && ((a.tg_filt_tol[g] >> ts) & 1);
+        const int row = act ? a.tg_row[g] : -1;
+        const int k = act ? a.tg_key[g] : 0;
+        const int mskew = act ? a.tg_maxskew[g] : 0;
+        uint64_t need = __ballot(ok && a.tg_aff[g]);
+        while (need) {  // TopologyNodeFilter.MatchesRequirements: Compatible(node reqs, some term)
+          const int l = __builtin_ctzll(need);
+          need &= need - 1;
+          const int gg = __builtin_amdgcn_readlane(g, l);
+          const int tb = a.tg_term_base[gg], nt = a.tg_nterm[gg];
+          bool m = false;
+          for (int ti = 0; ti < nt && !m; ti++) {
             uint64_t mv;
             ReqView rv;
-            ok = merge_compatible(D, fin, kreq_at(a.tg_terms, tb + ti), a.tg_terms_negop[tb + ti], !ex, mv, rv, &slots[0], vi);
+            m = merge_compatible(D, fin, kreq_at(a.tg_terms, tb + ti), a.tg_terms_negop[tb + ti], !ex, mv, rv, &slots[0], vi);
           }
+          if (lane == l) ok = m;
         }
-        if (!ok) continue;
-        const int row = a.tg_row[g];
-        if (row >= 0) {
-          if (lane == 0) {
+        if (ok) {
+          if (row >= 0) {
             uint8_t* c = ex ? &a.hcnt_ex[(size_t)row * a.n_existing + idx] : &a.hcnt_nc[(size_t)row * a.hnc_stride + idx];
             *c = *c == 255 ? 1 : *c < 254 ? *c + 1 : 254;  // 255: an unregistered domain (Record registers it)
             a.tg_reg[g] = 1;  // hostname rows: some domain has a count (ends pod-affinity bootstrap)
-          }
-        } else {
-          const int k = a.tg_key[g];
-          const uint64_t v = fin->vals[k];
-          if (a.tg_maxskew[g] == 0) {  // pod anti-affinity: Record(domains.Values()...), every value of the key
-            if (((fin->present >> k) & 1) && lane == 0) {
-              for (uint64_t m = v; m; m &= m - 1) a.tg_cnt[(size_t)g * 64 + __builtin_ctzll(m)] += 1;
-              a.tg_reg[g] |= v;
+          } else {
+            const uint64_t v = fin->vals[k];
+            const bool has = (fin->present >> k) & 1;
+            if (mskew == 0) {  // pod anti-affinity: Record(domains.Values()...), every value of the key
+              if (has) {
+                for (uint64_t m = v; m; m &= m - 1) a.tg_cnt[(size_t)g * 64 + __builtin_ctzll(m)] += 1;
+                a.tg_reg[g] |= v;
+              }
+            } else if (has && !((fin->compl_ >> k) & 1) && __builtin_popcountll(v) == 1) {
+              const int d = __builtin_ctzll(v);
+              a.tg_cnt[(size_t)g * 64 + d] += 1;
+              a.tg_reg[g] |= 1ull << d;
             }
-          } else if (((fin->present >> k) & 1) && !((fin->compl_ >> k) & 1) && __builtin_popcountll(v) == 1 && lane == 0) {
-            const int d = __builtin_ctzll(v);
-            a.tg_cnt[(size_t)g * 64 + d] += 1;
-            a.tg_reg[g] |= 1ull << d;
           }
         }
-        bytes += 16;
+        bytes += 16 * (uint64_t)min(64, rn - i0);
       }
     }  // (the bookkeeping barrier below publishes the counts before the next pod stages them)
     TS(4);
