@@ -16,6 +16,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "kp/kp_abi.h"
 #include "kp_device.h"
 #include "kp_model.h"
@@ -1219,9 +1221,17 @@ __device__ void slow_sort_wave(P ord, P npods, int n) {
 }
 
 #define DBG_SERIAL 0
+#ifndef SH_PER_GLB
+#define SH_PER_GLB 8
+#endif
+#ifndef SORT_DIAG
+#define SORT_DIAG 0  // diagnostic: the full path's sort split (decision / shift cycles, shifted entries, modes) in stats[25..30]
+#endif
+__shared__ uint64_t g_sdiag[6];
 template <int NT, class P>
 __device__ void sort_newnodeclaims(P ord, P npods, int n, int mut, int p, int32_t* s_ctl, uint64_t* slow = nullptr) {
   const int tid = threadIdx.x;
+  const uint64_t sd0 = SORT_DIAG ? __builtin_amdgcn_s_memtime() : 0;
   // s_ctl[7]: 0 nothing, 1 shift-left block (p+1..q-1 -> p..q-2, elem -> q-1), 2 shift-right (q..n-2 -> q+1..n-1,
   // elem -> q), 3 slow path; s_ctl[8..9]: q / elem. Decided by wave 0 (lane-parallel searches).
   if (tid < 64) {
@@ -1281,9 +1291,10 @@ __device__ void sort_newnodeclaims(P ord, P npods, int n, int mut, int p, int32_
   }
   __syncthreads();
   const int mode = s_ctl[7], q = s_ctl[8], elem = s_ctl[9];
+  const uint64_t sd1 = SORT_DIAG ? __builtin_amdgcn_s_memtime() : 0;
   // shifts: SH_PER entries per thread between two barriers (a spilled order array shifts thousands of entries in
-  // global memory: the loads of a step are in flight together)
-  constexpr int SH_PER = 8;
+  // global memory: the loads of a step are in flight together, and each step costs a load and a store round trip)
+  constexpr int SH_PER = std::is_same<P, GlbI32>::value ? SH_PER_GLB : 8;
   if (mode == 1) {
     const int c = q - 1 - p;  // elements p+1..q-1 move left by one
     for (int off = 0; off < c; off += NT * SH_PER) {
@@ -1322,6 +1333,12 @@ __device__ void sort_newnodeclaims(P ord, P npods, int n, int mut, int p, int32_
     if (tid == 0) ord[q] = elem;
   }
   __syncthreads();
+  if (SORT_DIAG && tid == 0) {
+    g_sdiag[0] += sd1 - sd0;
+    g_sdiag[1] += __builtin_amdgcn_s_memtime() - sd1;
+    g_sdiag[2] += mode == 1 ? q - 1 - p : mode == 2 ? n - 1 - q : 0;
+    if (mode) g_sdiag[2 + mode] += 1;
+  }
   if (DBG_SERIAL && tid == 0) {
     for (int i = 1; i < n; i++)
       if (npods[ord[i]] < npods[ord[i - 1]]) {
@@ -1853,6 +1870,7 @@ if (!FL_NOTIME && tmg) {                                    \
 #endif
             if (FL_CNT32) FL_CNT32_APP;
             else bytes += (uint64_t)D.TW * 8 + KP_NRES * 8 + 8;
+            if (FT_FINE && tmg && __ballot(lane < KP_NRES && fl_fitj[lane] != j0_lane)) fcyc[13] += 1;  // rows loaded
           } else if (FL_SPLIT) {
             X = fl_full_add<TOPO>(((uint64_t)khi_i << 32) | klo_i, sl, cat, ncx, X0, q_lane, j0_lane, b_staged ? 1 : 0);
             b_staged = true;
@@ -2117,6 +2135,8 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
     g_fast.bytes = g_fast.attempts = g_fast.scanned = g_fast.starts = g_fast.fpods = 0;
     for (int i = 0; i < 16; i++) g_fast.fcyc[i] = 0;
     for (int i = 0; i < 8; i++) g_fast.fbail[i] = 0;
+    if (SORT_DIAG)
+      for (int i = 0; i < 6; i++) g_sdiag[i] = 0;
   }
   __syncthreads();
 
@@ -2797,6 +2817,8 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
     for (int i = 0; i < 6; i++) a.stats[25 + i] = g_fast.fcyc[i];
     if (FT_FINE && timing)
       for (int i = 0; i < 8; i++) a.stats[16 + i] = g_fast.fcyc[6 + i];
+    if (SORT_DIAG)
+      for (int i = 0; i < 6; i++) a.stats[25 + i] = g_sdiag[i];
   }
   if (s_ctl[5])
     for (int i = tid; i < s_ctl[2]; i += NT) {

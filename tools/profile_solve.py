@@ -37,6 +37,9 @@ if ac[5]:
 out["fast_pods"] = st["fast_pods"]
 out["slow_sorts"] = st["slow_sorts"]
 fc = st["fast_cycles"]
+if os.environ.get("SORT_DIAG"):  # variant build: the full path's sort split in place of the fast-lane phases
+    out["sort_diag_per_pop"] = {k: round(v / max(1, st["pops"]), 2) for k, v in
+                                zip(["decision_cycles", "shift_cycles", "shifted", "mode1", "mode2", "mode3"], fc)}
 if sum(fc):
     out["fast_cycles_per_fast_pod"] = {k: round(v / max(1, st["fast_pods"]), 1) for k, v in
                                        zip(["pop", "stage", "sort", "prepass", "attempts", "commit"], fc)}
