@@ -1245,6 +1245,7 @@ struct Compiled {
   vector<uint8_t> hcnt0;     // [GH][E]
   vector<int32_t> shape_rec_base, shape_rec_n, rec_list;
   vector<int32_t> sl_own_base, sl_own_n, own_group, own_self;
+  vector<int32_t> own_rec;  // [O][8] static part of an owned group: group, self, key, maxSkew, minDomains, row, key slot, 0
   vector<uint64_t> own_pd, sl_topo_keys;
   vector<int32_t> tkey_slot;  // [64]
   vector<int32_t> tk_keys;    // [TK]
@@ -1867,6 +1868,9 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
           cp.sl_topo_keys[sl] |= 1ull << k;
         }
         cp.own_pd.push_back(pd);
+        const int32_t rec[8] = {g, cp.own_self.back(), k, cp.tg_maxskew[g], cp.tg_mindom[g], cp.tg_row[g],
+                                k >= 0 ? cp.tkey_slot[k] : -1, 0};
+        cp.own_rec.insert(cp.own_rec.end(), rec, rec + 8);
       }
     }
   }
@@ -2775,7 +2779,7 @@ static int32_t SolvePrepareLocal(kp_ctx* ctx, const kp_solve_in* in, kp_comm* co
                o_tgnt = blob.put(C.tg_nterm),
                o_srb = blob.put(C.shape_rec_base), o_srn = blob.put(C.shape_rec_n), o_recl = blob.put(C.rec_list),
                o_slob = blob.put(C.sl_own_base), o_slon = blob.put(C.sl_own_n), o_owng = blob.put(C.own_group),
-               o_owns = blob.put(C.own_self), o_ownp = blob.put(C.own_pd), o_sltk = blob.put(C.sl_topo_keys),
+               o_owns = blob.put(C.own_self), o_ownp = blob.put(C.own_pd), o_ownr = blob.put(C.own_rec), o_sltk = blob.put(C.sl_topo_keys),
                o_tks = blob.put(C.tkey_slot), o_extc = blob.put(C.ex_tcode), o_tkk = blob.put(C.tk_keys);
   uint32_t rmask = 0;
   for (size_t i = 0; i < C.shape_requests.size(); i++)
@@ -2989,6 +2993,7 @@ static int32_t SolvePrepareLocal(kp_ctx* ctx, const kp_solve_in* in, kp_comm* co
   a.own_group = (const int32_t*)(base + o_owng);
   a.own_self = (const int32_t*)(base + o_owns);
   a.own_pd = (const uint64_t*)(base + o_ownp);
+  a.own_rec = (const int4*)(base + o_ownr);
   a.sl_topo_keys = (const uint64_t*)(base + o_sltk);
   a.tkey_slot = (const int32_t*)(base + o_tks);
   a.n_tk = C.TK;

@@ -1227,6 +1227,9 @@ __device__ void slow_sort_wave(P ord, P npods, int n) {
 #ifndef SORT_DIAG
 #define SORT_DIAG 0  // diagnostic: the full path's sort split (decision / shift cycles, shifted entries, modes) in stats[25..30]
 #endif
+#ifndef EX_DIAG
+#define EX_DIAG 0  // diagnostic: the existing-node scan (range, scanned, cursor clamp, scans, cycles, placed) in stats[25..30]
+#endif
 __shared__ uint64_t g_sdiag[6];
 template <int NT, class P>
 __device__ void sort_newnodeclaims(P ord, P npods, int n, int mut, int p, int32_t* s_ctl, uint64_t* slow = nullptr) {
@@ -1333,7 +1336,7 @@ __device__ void sort_newnodeclaims(P ord, P npods, int n, int mut, int p, int32_
     if (tid == 0) ord[q] = elem;
   }
   __syncthreads();
-  if (SORT_DIAG && tid == 0) {
+  if (SORT_DIAG && !EX_DIAG && tid == 0) {
     g_sdiag[0] += sd1 - sd0;
     g_sdiag[1] += __builtin_amdgcn_s_memtime() - sd1;
     g_sdiag[2] += mode == 1 ? q - 1 - p : mode == 2 ? n - 1 - q : 0;
@@ -2044,6 +2047,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
   __shared__ CatHdr s_hdrw[NW];                       // per-wave descriptor of a catalogue >= 8
   extern __shared__ int32_t s_dyn[];  // ord[a.sort_cap], npods[a.sort_cap] while n_nc <= a.sort_cap
   __shared__ int32_t s_rcap[KP_MAX_CLASSES];  // remaining capacity per reservation class (ReservationManager)
+  __shared__ uint64_t s_topo_keys;            // the popped pod's spread keys (staged per pod)
 
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
@@ -2135,7 +2139,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
     g_fast.bytes = g_fast.attempts = g_fast.scanned = g_fast.starts = g_fast.fpods = 0;
     for (int i = 0; i < 16; i++) g_fast.fcyc[i] = 0;
     for (int i = 0; i < 8; i++) g_fast.fbail[i] = 0;
-    if (SORT_DIAG)
+    if (SORT_DIAG || EX_DIAG)
       for (int i = 0; i < 6; i++) g_sdiag[i] = 0;
   }
   __syncthreads();
@@ -2203,26 +2207,32 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
         s_ctl[24] = INT32_MAX;  // first count-independent pass (existing / in-flight), topology shape-levels
         s_ctl[25] = INT32_MAX;
         s_ctl[27] = 0;  // addToNewNodeClaim met a ReservedOfferingError
+        if (TOPO) {  // the shape-level's owned groups (count, base) and spread keys, staged with the cursors
+          const int on = a.sl_own_n[sl];
+          s_ctl[28] = on;
+          s_ctl[29] = a.sl_own_base[sl];
+          s_topo_keys = on ? a.sl_topo_keys[sl] : 0;
+        }
       }
     }
     __syncthreads();
     TS(0);
+    const uint64_t exdS = EX_DIAG ? __builtin_amdgcn_s_memtime() : 0;
     const KReqs* B = &s_B;
     const uint64_t b_negop = a.shape_negop[sl];
     const uint64_t tolmask = a.shape_tolerates[shape];
     const uint64_t hpc = a.hp_any ? a.shape_hp_conf[shape] : 0, hpa = a.hp_any ? a.shape_hp_add[shape] : 0;
     int placed = -1;  // >= 0 NodeClaim id; <= -2 existing node; -1 not placed
     // ---- topology: stage the owned groups (one wave each) -----------------------------------------
-    const int own_n = TOPO ? a.sl_own_n[sl] : 0;
-    const uint64_t topo_keys = own_n ? a.sl_topo_keys[sl] : 0;
+    const int own_n = TOPO ? s_ctl[28] : 0;
+    const int own_base = TOPO ? s_ctl[29] : 0;
+    const uint64_t topo_keys = own_n ? s_topo_keys : 0;
     const uint64_t b_keys = s_B.present | topo_keys;  // keys whose type filter must be redone on Add
     if (own_n) {
       for (int j = wave; j < own_n; j += NW) {
-        const int oi = a.sl_own_base[sl] + j;
-        const int g = a.own_group[oi];
-        const int self = a.own_self[oi];
-        const int k = a.tg_key[g];
-        const int mskew = a.tg_maxskew[g];
+        const int oi = own_base + j;
+        const int4 r0 = a.own_rec[2 * oi], r1 = a.own_rec[2 * oi + 1];  // the static part: one load
+        const int g = r0.x, self = r0.y, k = r0.z, mskew = r0.w;
         uint64_t acc = 0;
         bool boot = false;  // pod affinity on a dictionary key: TopoOwn.self = bootstrap
         if (k >= 0) {
@@ -2232,7 +2242,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
           const int mn = wave_min_i32(sup ? c : INT32_MAX);
           const int num = __builtin_popcountll(reg & pd);
           int64_t m = num ? (int64_t)mn : (int64_t)INT32_MAX;
-          const int mind = a.tg_mindom[g];
+          const int mind = r1.x;
           if (mind > 0 && num < mind) m = 0;
           if (mskew > 0) {  // spread: count + self - min <= maxSkew
             acc = __ballot(((reg >> lane) & 1) && (int64_t)c + self - m <= mskew);
@@ -2250,7 +2260,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
         // has a count yet, tg_reg bit 0)
         const int self_eff = mskew >= 0 ? self : k < 0 ? (self && !(a.tg_reg[g] & 1)) : (boot ? 1 : 0);
         if (lane == 0) {
-          s_town[j] = TopoOwn{g, self_eff, k, a.tg_row[g], mskew, k >= 0 ? a.tkey_slot[k] : -1};
+          s_town[j] = TopoOwn{g, self_eff, k, r1.y, mskew, r1.z};
           s_tacc[j] = acc;
         }
       }
@@ -2260,8 +2270,12 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
     // ---- addToExistingNode: lowest index whose CanAdd succeeds -------------------------------
     const int64_t ep0 = rmask_all ? s_preq[rr0] : 0, ep1 = rm1 ? s_preq[rr1] : 0;  // the pod, per headroom row
     const int64_t ep2 = rk2 >= 0 ? s_preq[rk2] : 0, ep3 = rk3 >= 0 ? s_preq[rk3] : 0;
+    const uint64_t exd0 = EX_DIAG ? __builtin_amdgcn_s_memtime() : 0;
+    if (EX_DIAG && tid == 0) g_sdiag[0] += exd0 - exdS;  // topology staging
+    if (EX_DIAG && tid == 0 && s_ctl[17] < a.n_existing) g_sdiag[3] += 1;
     for (int base = s_ctl[17]; base < a.n_existing && placed == -1; base += 4 * NT) {
       uint32_t flags = 0, iflags = 0;
+      const uint64_t exd1 = EX_DIAG ? __builtin_amdgcn_s_memtime() : 0;
 #pragma unroll
       for (int k = 0; k < 4; k++) {  // 4 rounds per thread: independent, so their loads overlap
         const int ec = base + k * NT + tid;
@@ -2302,9 +2316,15 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
         }
         flags |= (cand ? 1u : 0u) << k;
       }
+      if (EX_DIAG) {  // the evaluation's cycles, as the slowest wave finishes them
+        __syncthreads();
+        if (tid == 0) g_sdiag[5] += __builtin_amdgcn_s_memtime() - exd1;
+      }
       if (own_n) first_pos_min<NT>(iflags, base + tid, &s_ctl[24]);
       const int n = compact_candidates_x4<NW>(flags, base + tid, s_list, s_wcnt);
       if (wave == 0) bytes += (uint64_t)min(4 * NT, a.n_existing - base) * (16 * a.n_req_res + 13);  // once
+      const uint64_t exd2 = EX_DIAG ? __builtin_amdgcn_s_memtime() : 0;
+      if (EX_DIAG && tid == 0) g_sdiag[1] += exd2 - exd1;
       for (int r0 = 0; r0 < n; r0 += NW) {
         const int li = r0 + wave;
         bool ok = false;
@@ -2340,8 +2360,12 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
         __syncthreads();
         if (win >= 0) break;
       }
+      if (EX_DIAG && tid == 0) g_sdiag[2] += __builtin_amdgcn_s_memtime() - exd2;
     }
 
+    if (EX_DIAG && tid == 0) {
+      g_sdiag[4] += __builtin_amdgcn_s_memtime() - exd0;
+    }
     if (tid == 0 && a.n_existing) {
       // cursor: every position before the winner failed; with topology, before the first position that passed
       // the count-independent checks (a zone-count failure may pass later)
@@ -2817,7 +2841,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
     for (int i = 0; i < 6; i++) a.stats[25 + i] = g_fast.fcyc[i];
     if (FT_FINE && timing)
       for (int i = 0; i < 8; i++) a.stats[16 + i] = g_fast.fcyc[6 + i];
-    if (SORT_DIAG)
+    if (SORT_DIAG || EX_DIAG)
       for (int i = 0; i < 6; i++) a.stats[25 + i] = g_sdiag[i];
   }
   if (s_ctl[5])

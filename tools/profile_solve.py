@@ -37,6 +37,9 @@ if ac[5]:
 out["fast_pods"] = st["fast_pods"]
 out["slow_sorts"] = st["slow_sorts"]
 fc = st["fast_cycles"]
+if os.environ.get("EX_DIAG"):  # variant build: the existing-node scan in place of the fast-lane phases
+    out["existing_diag_per_pop"] = {k: round(v / max(1, st["pops"]), 2) for k, v in
+                                    zip(["staging_cycles", "prepass_cycles", "attempt_cycles", "scans", "cycles", "eval_cycles"], fc)}
 if os.environ.get("SORT_DIAG"):  # variant build: the full path's sort split in place of the fast-lane phases
     out["sort_diag_per_pop"] = {k: round(v / max(1, st["pops"]), 2) for k, v in
                                 zip(["decision_cycles", "shift_cycles", "shifted", "mode1", "mode2", "mode3"], fc)}
