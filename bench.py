@@ -47,6 +47,9 @@ def main():
     ap.add_argument("--subsets", type=int, default=1_000_000)
     ap.add_argument("--cpu-sample-sims", type=int, default=16)
     ap.add_argument("--no-consolidation", action="store_true")
+    ap.add_argument("--general-nodes", type=int, default=2_000)
+    ap.add_argument("--general-subsets", type=int, default=200)
+    ap.add_argument("--only-general", action="store_true", help="the topology-cluster consolidation leg alone")
     ap.add_argument("--c3-pods", type=int, default=100_000)
     ap.add_argument("--c5-pods", type=int, default=1_000_000)
     ap.add_argument("--feas-rows", type=int, default=50_000)
@@ -93,6 +96,11 @@ def main():
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
+
+    if args.only_general:  # measurement of the general-path leg alone (not the bench contract's line)
+        print(json.dumps(_consolidation_general(args, cat, ctx, rank, world, barrier)), flush=True)
+        ctx.close()
+        return
 
     def max_over_ranks(x):
         if dist is None:
@@ -192,6 +200,8 @@ def main():
         progress("config5 done")
         line["consolidation"] = _consolidation(args, cat, ctx, dist, rank, world, barrier, kcomm)
         progress("consolidation done")
+        line["consolidation_general"] = _consolidation_general(args, cat, ctx, rank, world, barrier)
+        progress("general consolidation done")
     if rank == 0:
         print(json.dumps(line), flush=True)
     if kcomm is not None:
@@ -407,6 +417,71 @@ def _consolidation(args, cat, ctx, dist, rank, world, barrier, kcomm):
     plan.close()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = _cpu_baseline_sims(cl, cands, args.cpu_sample_sims)
+    return out
+
+
+def spread_cluster(cat, n_nodes, seed=4):
+    """Config 4 with topology spread: every shape labelled app-(i % 8), every other shape zone-spread (maxSkew 1,
+    DoNotSchedule) over its app. The batched sim kernels do not model spread, so kp_cluster_prepare takes the general
+    path: each subset's SimulateScheduling is a whole Solve on the device with the remaining nodes' pods counted."""
+    from kpamd import synth
+    from kpamd.model import LabelSelector, TopologySpread
+    cl = synth.config4(cat, n_nodes=n_nodes, seed=seed)
+    for i, sh in enumerate(cl.shapes):
+        sh.labels = dict(sh.labels or {}, app=f"app-{i % 8}")
+        if i % 2 == 0:
+            sh.topology_spread = [TopologySpread("topology.kubernetes.io/zone", 1, LabelSelector({"app": f"app-{i % 8}"}),
+                                                 "DoNotSchedule")]
+    return cl
+
+
+def _consolidation_general(args, cat, ctx, rank, world, barrier):
+    """Consolidation on a topology-spread cluster (the general simulation path): the 100
+    firstNConsolidationOption prefixes plus random subsets of 2..20 candidates through kp_consolidate_argmin, rank 0
+    only (the host compile per subset is the cost: no sharding claimed). Reported with and without kp_cluster_prepare."""
+    import numpy as np
+    import kpamd
+    from kpamd import disruption, synth
+    if rank != 0:
+        barrier()
+        return None
+    cl = spread_cluster(cat, args.general_nodes)
+    cands = np.asarray(cl.candidates, dtype=np.uint32)
+    mids = disruption.MultiNodeConsolidation.search_prefixes(len(cands))
+    subs = [list(cands[:m + 1]) for m in mids]
+    subs += synth.consolidation_subsets(cl, args.general_subsets, seed=5, max_size=20, prefixes=False)
+    offs = np.zeros(len(subs) + 1, dtype=np.uint32)
+    offs[1:] = np.cumsum([len(x) for x in subs])
+    flat = np.concatenate([np.asarray(x, dtype=np.uint32) for x in subs])
+    t0 = time.perf_counter()
+    plan = kpamd.ClusterPlan(ctx, cl)
+    prep_s = time.perf_counter() - t0
+    try:
+        plan.argmin(offs[:9], flat)  # warmup on the first 8 subsets
+        t0 = time.perf_counter()
+        choice, _, st = plan.argmin(offs, flat)
+        elapsed = time.perf_counter() - t0
+    finally:
+        plan.close()
+    barrier()
+    n = len(subs)
+    out = {"metric": "consolidation sims/s (general path: topology spread)", "value": round(n / elapsed, 1),
+           "unit": "sims/s", "subsets": n, "elapsed_s": round(elapsed, 3), "ms_per_sim": round(elapsed / n * 1e3, 3),
+           "sims_per_s_incl_prepare": round(n / (elapsed + prep_s), 1), "prepare_s": round(prep_s, 3),
+           "decisions": {"noop": choice["counts"][0], "delete": choice["counts"][1], "replace": choice["counts"][2]},
+           "workload": f"config4 variant: {args.general_nodes} nodes ({len(cl.pod_shape)} pods), every other shape "
+                       f"zone-spread (maxSkew 1, DoNotSchedule); {len(mids)} firstNConsolidationOption prefixes + "
+                       f"{args.general_subsets} random subsets of 2..20 candidates; each simulation a whole Solve on the "
+                       f"device (host compile + solve_kernel + finalize_kernel), decision on the host"}
+    if world == 1 and not args.no_cpu_baseline:
+        from oracle import pyoracle
+        sample = subs[len(mids):len(mids) + 8]
+        t0 = time.perf_counter()
+        pyoracle.simulate_batch(cl, sample)
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(len(sample) / dt, 2), "unit": "sims/s", "cores": 1, "kind": "port",
+                               "sample": f"8 random subsets of the same cluster, oracle computeConsolidation "
+                                         f"single-threaded, {dt:.1f} s"}
     return out
 
 
