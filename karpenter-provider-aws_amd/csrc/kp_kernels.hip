@@ -54,6 +54,9 @@
 #define FL_NOTIME 1  // the fast lane's per-phase s_memtime probes are compiled out (their registers cost 3.7 % even
                      // when KP_TIMING is off); the diagnostic build (tools/build_fine.sh) turns them back on
 #endif
+#ifndef FL_CACHE
+#define FL_CACHE 1  // the fast lane keeps its last append commit's NodeClaim state in registers (0: always reload)
+#endif
 #ifndef FT_FINE
 #define FT_FINE 0  // diagnostic: finer fast-lane probes (FTF) in place of the full path's attempt split
 #endif
@@ -1625,7 +1628,14 @@ __device__ __noinline__ int fast_lane(uint64_t kargs, int32_t LDS* s_dyn_arg, ui
   int qw_pod = S->qw_pod[lane], qw_shape = S->qw_shape[lane], qw_sl = S->qw_sl[lane], qw_lastlen = S->qw_lastlen[lane],
       qw_epoch = S->qw_epoch[lane];
   uint64_t bytes = 0, attempts = 0, scanned = 0, starts = 0, fcyc[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  int pops = 0, handoff = -1, fb = -1;
+  int pops = 0, handoff = -1, fb = -1, fl_last = -1;
+  // the NodeClaim this call's last append commit wrote, as it wrote it (the next pod usually starts there: reading
+  // its lines back right after the stores waits for them to drain): remaining types, requests, threshold indices
+  // (lane values), and its pre-check record. Only the fast lane writes NodeClaims during one call.
+  int c_nc = -1, c_cat = 0, c_ver = 0, c_ts = 0;
+  uint64_t c_X = 0, c_hm = 0;
+  int64_t c_q = 0, c_r0 = 0, c_r1 = 0, c_r2 = 0, c_r3 = 0;
+  int32_t c_fj = 0;
   int n_buf = 0, buf_pod = 0, buf_pl = 0;  // placements not yet written (lane i: the i-th)
 #if FL_CNT32
   NbUnits fnb{0, 0, 0};  // append-path byte model as event counts, converted on exit
@@ -1790,16 +1800,23 @@ if (!FL_NOTIME && tmg) {                                    \
         // speculative loads of the first position's NodeClaim (the usual winner), issued ahead of the pre-check
         // gathers (and outside their lane-divergent block) so that the two round trips overlap
         const int nc0 = __builtin_amdgcn_readlane(nc, 0);
-        const KReqs* cr0 = kreq_at(A->nc_reqs, nc0);
-        const uint64_t hm0 = cr0->hmin & cr0->present;
-        const int cat0 = A->nc_cat[nc0];
-        const uint64_t X00 = lane < D.TW ? A->nc_X[(size_t)nc0 * D.TW + lane] : 0;
-        const int64_t rq0 = lane < KP_NRES ? A->nc_requests[(size_t)nc0 * KP_NRES + lane] : 0;
-        const int32_t j00 = lane < KP_NRES ? A->nc_fitj[(size_t)nc0 * KP_NRES + lane] : 0;
+        uint64_t hm0 = c_hm, X00 = c_X;
+        int cat0 = c_cat;
+        int64_t rq0 = c_q;
+        int32_t j00 = c_fj;
+        if (nc0 != c_nc) {
+          const KReqs* cr0 = kreq_at(A->nc_reqs, nc0);
+          hm0 = cr0->hmin & cr0->present;
+          cat0 = A->nc_cat[nc0];
+          X00 = lane < D.TW ? A->nc_X[(size_t)nc0 * D.TW + lane] : 0;
+          rq0 = lane < KP_NRES ? A->nc_requests[(size_t)nc0 * KP_NRES + lane] : 0;
+          j00 = lane < KP_NRES ? A->nc_fitj[(size_t)nc0 * KP_NRES + lane] : 0;
+        }
         if (i < n_nc) {
           // every gather issued unconditionally: one round trip
           const int32_t fl = nc < A->ncc ? A->nc_fail[(size_t)sl * A->ncc + nc] : -2;
-          hv = load_head(A->nc_head + nc, four);
+          if (nc == c_nc) hv = HeadView{c_r0, c_r1, c_r2, c_r3, c_ver, c_ts};
+          else hv = load_head(A->nc_head + nc, four);
           ver = hv.ver;
           const int32_t ts = hv.ts;
           bool fit = hv.r0 >= pr0 && hv.r1 >= pr1 && hv.r2 >= pr2 && hv.r3 >= pr3;
@@ -1840,7 +1857,9 @@ if (!FL_NOTIME && tmg) {                                    \
           int cat = cat0;
           int64_t rq_lane = rq0;
           int32_t j0_lane = j00;
-          if (l != 0) {
+          if (l != 0 && ncx == c_nc) {
+            hm = c_hm, X0 = c_X, cat = c_cat, rq_lane = c_q, j0_lane = c_fj;
+          } else if (l != 0) {
             const KReqs* cr = kreq_at(A->nc_reqs, ncx);
             hm = cr->hmin & cr->present;
             cat = A->nc_cat[ncx];
@@ -1873,7 +1892,7 @@ if (!FL_NOTIME && tmg) {                                    \
 #endif
             if (FL_CNT32) FL_CNT32_APP;
             else bytes += (uint64_t)D.TW * 8 + KP_NRES * 8 + 8;
-            if (FT_FINE && tmg && __ballot(lane < KP_NRES && fl_fitj[lane] != j0_lane)) fcyc[13] += 1;  // rows loaded
+            if (FT_FINE && tmg && ncx == fl_last) fcyc[13] += 1;  // the previous pod's NodeClaim again
           } else if (FL_SPLIT) {
             X = fl_full_add<TOPO>(((uint64_t)khi_i << 32) | klo_i, sl, cat, ncx, X0, q_lane, j0_lane, b_staged ? 1 : 0);
             b_staged = true;
@@ -1934,6 +1953,17 @@ if (!FL_NOTIME && tmg) {                                    \
             }
             placed = ncx;
             wpos = base + l;
+            if (FT_FINE) fl_last = ncx;
+            if (FL_CACHE && !full_add) {  // the append path left the requirements (hmin, catalogue) as they were
+              c_nc = ncx, c_cat = cat, c_hm = hm, c_X = X, c_q = q_lane, c_fj = fj;
+              c_r0 = lane_bcast_i64(hv.r0, l) - pr0;
+              c_r1 = lane_bcast_i64(hv.r1, l) - pr1;
+              c_r2 = four ? lane_bcast_i64(hv.r2, l) - pr2 : INT64_MAX;  // (load_head's value for unused slots)
+              c_r3 = four ? lane_bcast_i64(hv.r3, l) - pr3 : INT64_MAX;
+              c_ver = verx + 1, c_ts = __builtin_amdgcn_readlane(hv.ts, l);
+            } else {
+              c_nc = -1;
+            }
             FTF(12);
             break;
           }
