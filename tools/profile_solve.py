@@ -14,7 +14,7 @@ cfg = sys.argv[1] if len(sys.argv) > 1 else "2"
 n = int(sys.argv[2]) if len(sys.argv) > 2 else {"2": 50000, "3": 100000, "5": 300000}[cfg]
 lib = kpamd.load_lib()
 cat = catalog.build_catalog(lib)
-prob = {"2": lambda: synth.config2(cat, n_pods=n, seed=2), "3": lambda: synth.config3(cat, n_pods=n),
+prob = {"2": lambda: synth.config2(cat, n_pods=n, seed=2), "3": lambda: synth.config3(cat, n_pods=n, n_deployments=int(os.environ.get("KP_C3_DEPLOYMENTS", "1000"))),
         "5": lambda: synth.config5(cat, n_pods=n)}[cfg]()
 ctx = kpamd.Context(0)
 sched = kpamd.Scheduler(ctx, prob)
