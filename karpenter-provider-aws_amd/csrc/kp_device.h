@@ -110,6 +110,8 @@ struct SolveArgs {
   const int32_t* own_group;
   const int32_t* own_self;           // the group's selector matches the owner pod
   const uint64_t* own_pd;            // podDomains (strict requirements) over the key's value ordinals
+  const int32_t* rec_aux;            // per rec_list entry: hostname row, else -1 - key slot (static)
+  const int32_t* sl_fast_topo;       // [SL] 1: the fast lane may place the level's pods
   const int4* own_rec;               // [O][2] group, self, key, maxSkew | minDomains, row, key slot, 0 (static)
   const uint64_t* sl_topo_keys;      // [SL] dictionary keys of the owned groups
   // first-fit cursors (exact): cur_*[sl] = {k, t}: the first k candidates of the scan order were known to

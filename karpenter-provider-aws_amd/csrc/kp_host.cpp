@@ -1245,6 +1245,8 @@ struct Compiled {
   vector<uint8_t> hcnt0;     // [GH][E]
   vector<int32_t> shape_rec_base, shape_rec_n, rec_list;
   vector<int32_t> sl_own_base, sl_own_n, own_group, own_self;
+  vector<int32_t> sl_fast_topo;  // [SL] 1: the fast lane may place the level's pods (append path; see CompileTopology)
+  vector<int32_t> rec_aux;       // per rec_list entry: the group's hostname row, else -1 - its key's slot
   vector<int32_t> own_rec;  // [O][8] static part of an owned group: group, self, key, maxSkew, minDomains, row, key slot, 0
   vector<uint64_t> own_pd, sl_topo_keys;
   vector<int32_t> tkey_slot;  // [64]
@@ -1432,6 +1434,7 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
   cp.sl_own_base.assign(SL, 0);
   cp.sl_own_n.assign(SL, 0);
   cp.sl_topo_keys.assign(SL, 0);
+  cp.sl_fast_topo.assign(SL, 1);
   bool any = false;
   for (uint32_t s = 0; s < in->n_shapes; s++)
     any |= in->shapes[s].n_topology_spread + PodTermCount(in->shapes[s]) > 0;
@@ -1873,6 +1876,27 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
         cp.own_rec.insert(cp.own_rec.end(), rec, rec + 8);
       }
     }
+  }
+  // shape-levels the fast lane may take: at most 4 owned groups, every owned and every recorded group a spread
+  // (maxSkew > 0) and no recorded group with node-filter terms (the fast lane's Record reads the NodeClaim's value
+  // codes); pods of other levels (affinity, anti-affinity, filtered groups) stay on the full path
+  for (uint32_t s = 0; s < in->n_shapes; s++) {
+    bool rec_ok = true;
+    for (int i = 0; i < cp.shape_rec_n[s]; i++) {
+      const int g = cp.rec_list[cp.shape_rec_base[s] + i];
+      rec_ok = rec_ok && cp.tg_maxskew[g] > 0 && !cp.tg_aff[g];
+    }
+    for (int l = 0; l < cp.shape_nlevels[s]; l++) {
+      const int sl = cp.shape_level_base[s] + l;
+      bool ok = rec_ok && cp.sl_own_n[sl] <= 4;
+      for (int j = 0; j < cp.sl_own_n[sl] && ok; j++) ok = cp.tg_maxskew[cp.own_group[cp.sl_own_base[sl] + j]] > 0;
+      cp.sl_fast_topo[sl] = ok ? 1 : 0;
+    }
+  }
+  cp.rec_aux.resize(cp.rec_list.size());
+  for (size_t i = 0; i < cp.rec_list.size(); i++) {
+    const int g = cp.rec_list[i];
+    cp.rec_aux[i] = cp.tg_row[g] >= 0 ? cp.tg_row[g] : -1 - cp.tkey_slot[cp.tg_key[g]];
   }
   // existing nodes: value ordinal of each topology key (0xFF: no label)
   cp.ex_tcode.assign((size_t)std::max(cp.TK, 1) * std::max(E, 1), 0xFF);
@@ -2777,7 +2801,7 @@ static int32_t SolvePrepareLocal(kp_ctx* ctx, const kp_solve_in* in, kp_comm* co
                o_tgm = blob.put(C.tg_mindom), o_tga = blob.put(C.tg_aff), o_tgtb = blob.put(C.tg_term_base),
                o_tgft = blob.put(C.tg_filt_tol), o_tgt = blob.put(C.tg_terms), o_tgtn = blob.put(C.tg_terms_negop),
                o_tgnt = blob.put(C.tg_nterm),
-               o_srb = blob.put(C.shape_rec_base), o_srn = blob.put(C.shape_rec_n), o_recl = blob.put(C.rec_list),
+               o_srb = blob.put(C.shape_rec_base), o_srn = blob.put(C.shape_rec_n), o_recl = blob.put(C.rec_list), o_recx = blob.put(C.rec_aux), o_slft = blob.put(C.sl_fast_topo),
                o_slob = blob.put(C.sl_own_base), o_slon = blob.put(C.sl_own_n), o_owng = blob.put(C.own_group),
                o_owns = blob.put(C.own_self), o_ownp = blob.put(C.own_pd), o_ownr = blob.put(C.own_rec), o_sltk = blob.put(C.sl_topo_keys),
                o_tks = blob.put(C.tkey_slot), o_extc = blob.put(C.ex_tcode), o_tkk = blob.put(C.tk_keys);
@@ -2988,6 +3012,8 @@ static int32_t SolvePrepareLocal(kp_ctx* ctx, const kp_solve_in* in, kp_comm* co
   a.shape_rec_base = (const int32_t*)(base + o_srb);
   a.shape_rec_n = (const int32_t*)(base + o_srn);
   a.rec_list = (const int32_t*)(base + o_recl);
+  a.rec_aux = (const int32_t*)(base + o_recx);
+  a.sl_fast_topo = (const int32_t*)(base + o_slft);
   a.sl_own_base = (const int32_t*)(base + o_slob);
   a.sl_own_n = (const int32_t*)(base + o_slon);
   a.own_group = (const int32_t*)(base + o_owng);

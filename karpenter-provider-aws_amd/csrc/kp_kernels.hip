@@ -1722,7 +1722,7 @@ if (!FL_NOTIME && tmg) {                                    \
           ce1 = a_cex_prev_stamp;
         }
       } else {
-        own = U((TOPO ? A->sl_own_n[sl] + A->shape_rec_n[shape] : 0) + (A->hp_any && A->shape_hp_conf[shape] ? 1 : 0));
+        own = U((TOPO ? 1 - A->sl_fast_topo[sl] : 0) + (A->hp_any && A->shape_hp_conf[shape] ? 1 : 0));
         ce0 = U(FL_HAS_EX ? A->cur_ex[2 * sl] : 0), ce1 = U(FL_HAS_EX ? A->cur_ex[2 * sl + 1] : 0);
         preq_lane = lane < KP_NRES ? A->shape_requests[(size_t)shape * KP_NRES + lane] : 0;
         tolmask = U64(A->shape_tolerates[shape]);
@@ -1733,7 +1733,7 @@ if (!FL_NOTIME && tmg) {                                    \
       if (off + 1 < qw_n) {  // the next entry's stage loads: in flight while this pod is sorted and placed
         const int nshape = __builtin_amdgcn_readlane(qw_shape, off + 1);
         const int nsl = __builtin_amdgcn_readlane(qw_sl, off + 1);
-        pf_own = (TOPO ? A->sl_own_n[nsl] + A->shape_rec_n[nshape] : 0) + (A->hp_any && A->shape_hp_conf[nshape] ? 1 : 0);
+        pf_own = (TOPO ? 1 - A->sl_fast_topo[nsl] : 0) + (A->hp_any && A->shape_hp_conf[nshape] ? 1 : 0);
         pf_ce0 = FL_HAS_EX ? A->cur_ex[2 * nsl] : 0, pf_ce1 = FL_HAS_EX ? A->cur_ex[2 * nsl + 1] : 0;
         pf_preq = lane < KP_NRES ? A->shape_requests[(size_t)nshape * KP_NRES + lane] : 0;
         pf_tol = A->shape_tolerates[nshape];
@@ -1754,6 +1754,37 @@ if (!FL_NOTIME && tmg) {                                    \
       }
       const int64_t pr0 = rmask_all ? lane_bcast_i64(preq_lane, rr0) : 0, pr1 = rm1 ? lane_bcast_i64(preq_lane, rr1) : 0;
       const int64_t pr2 = rk2 >= 0 ? lane_bcast_i64(preq_lane, rk2) : 0, pr3 = rk3 >= 0 ? lane_bcast_i64(preq_lane, rk3) : 0;
+      // topology (levels the host marked fast: spread groups only): the owned groups staged in registers, as the full
+      // path stages them into s_town / s_tacc (hostname rows: count + self <= maxSkew; dictionary keys: the domains
+      // whose count + self - min <= maxSkew)
+      int t_n = 0, rec_n = 0, rec_b = 0;
+      bool triv = false;  // no requirements at this level: Add on any NodeClaim is Fits alone (the full path's triv)
+      int t_key[4] = {0, 0, 0, 0}, t_row[4] = {0, 0, 0, 0}, t_slot[4] = {0, 0, 0, 0}, t_self[4] = {0, 0, 0, 0},
+          t_mskew[4] = {0, 0, 0, 0};
+      uint64_t t_acc[4] = {0, 0, 0, 0};
+      if (TOPO) {
+        t_n = A->sl_own_n[sl];
+        triv = kreq_at(A->shape_reqs, sl)->present == 0;
+        rec_n = A->shape_rec_n[shape];
+        rec_b = A->shape_rec_base[shape];
+        const int ob = A->sl_own_base[sl];
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+          if (j < t_n) {
+            const int4 r0 = A->own_rec[2 * (ob + j)], r1 = A->own_rec[2 * (ob + j) + 1];
+            t_key[j] = r0.z, t_row[j] = r1.y, t_slot[j] = r1.z, t_self[j] = r0.y, t_mskew[j] = r0.w;
+            if (r0.z >= 0) {
+              const int c = A->tg_cnt[(size_t)r0.x * 64 + lane];
+              const uint64_t reg = A->tg_reg[r0.x], pd = A->own_pd[ob + j];
+              const bool sup = ((reg & pd) >> lane) & 1;
+              const int mn = wave_min_i32(sup ? c : INT32_MAX);
+              const int num = __builtin_popcountll(reg & pd);
+              int64_t m = num ? (int64_t)mn : (int64_t)INT32_MAX;
+              if (r1.x > 0 && num < r1.x) m = 0;
+              t_acc[j] = __ballot(((reg >> lane) & 1) && (int64_t)c + r0.y - m <= r0.w);
+            }
+          }
+      }
       a_cex_prev_stamp = U(s_ctl[15]);
       if (FL_HAS_EX && lane == 0) {  // addToExistingNode: every position fails (cursor == n_existing)
         A->cur_ex[2 * sl] = A->n_existing;
@@ -1786,14 +1817,14 @@ if (!FL_NOTIME && tmg) {                                    \
       FT(2);
       // addToInflightNode: pre-checks 64 positions at a time, then the append-path attempts in order. A long scan
       // is the full path's (512-lane pre-pass).
-      int placed = -1, wpos = -1, why = FB_NONE;
+      int placed = -1, wpos = -1, why = FB_NONE, ipos = INT32_MAX;  // ipos: first count-independent pass (topology)
       bool b_staged = false;
       bool bail = n_nc - start > FAST_SCAN_MAX;
       if (bail) why = FB_SCAN;
       if (lane == 0 && !bail) starts += start;
       for (int base = start; base < n_nc && placed == -1 && !bail; base += 64) {
         const int i = base + lane;
-        bool cand = false, tag = false;
+        bool cand = false, tag = false, icand = false;
         const int nc = i < n_nc ? ord[i] : 0;
         int32_t ver = 0;
         HeadView hv{0, 0, 0, 0, 0, 0};
@@ -1829,13 +1860,32 @@ if (!FL_NOTIME && tmg) {                                    \
             }
           }
           cand = fit && fl != ver && fl != NC_NEVER && ((tolmask >> ts) & 1);
-          tag = cand && fl >= NC_MERGED;
+          bool pinned = true;  // every dictionary key the pod spreads over is one value on the NodeClaim
+          if (TOPO && t_n) {
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+              if (j < t_n && t_key[j] < 0)
+                cand = cand && (int)A->hcnt_nc[(size_t)t_row[j] * A->hnc_stride + nc] + t_self[j] <= t_mskew[j];
+            icand = cand;
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+              if (j < t_n && t_key[j] >= 0) {
+                const uint32_t code = A->nc_tcode[(size_t)t_slot[j] * A->hnc_stride + nc];
+                cand = cand && (code == 0xFF || (code < 64 && ((t_acc[j] >> code) & 1)));
+                pinned = pinned && code < 64;
+              }
+          }
+          tag = cand && (fl >= NC_MERGED || triv) && pinned;
         }
         if (lane == 0) scanned += min(64, n_nc - base);
         if (!FL_CNT32 && lane == 0) bytes += (uint64_t)min(64, n_nc - base) * (12 + 16 * A->n_req_res);
         FL_CNT32_SCAN(min(64, n_nc - base));
         uint64_t cm = __ballot(cand);
         const uint64_t tm = __ballot(tag);
+        if (TOPO && t_n && ipos == INT32_MAX) {
+          const uint64_t im = __ballot(icand);
+          if (im) ipos = base + __builtin_ctzll(im);
+        }
         // the next pod's prefetch was issued before these gathers, so it has landed: take it off the outstanding
         // list now rather than at the next pod's stage, where the wait would cover this pod's stores as well
         READY(pf_own);
@@ -1872,6 +1922,11 @@ if (!FL_NOTIME && tmg) {                                    \
           // append path (merged before, no minValues): Fits over the remaining types; otherwise NodeClaim.Add in
           // full, as the full path's attempt: Compatible + Add of the requirements, then the type filter
           const bool full_add = !tagged || hm;
+          if (TOPO && t_n && full_add) {  // the merge narrows by the counts (topo_narrow): the full path's
+            why = FB_MERGE;
+            bail = true;
+            break;
+          }
           uint64_t X = 0, m_v = 0;
           ReqView rv;
           bool perm = true;  // a failure here is permanent (NC_NEVER) unless it is Compatible's undefined-key rule
@@ -1954,6 +2009,32 @@ if (!FL_NOTIME && tmg) {                                    \
             placed = ncx;
             wpos = base + l;
             if (FT_FINE) fl_last = ncx;
+            if (TOPO && triv && lane == 0 && ncx < A->ncc) A->nc_fail[(size_t)sl * A->ncc + ncx] = NC_MERGED;
+            if (TOPO && rec_n) {
+              // Topology.Record, as the full path's: each recorded group (spreads only on fast levels) on its own lane;
+              // a dictionary key counts once the NodeClaim holds one value of it (its value code < 64)
+              const int tsx = __builtin_amdgcn_readlane(hv.ts, l);
+              for (int i0 = 0; i0 < rec_n; i0 += 64) {
+                const int ri = i0 + lane;
+                if (ri < rec_n) {
+                  const int g = A->rec_list[rec_b + ri], aux = A->rec_aux[rec_b + ri];
+                  if (A->tg_live[g] && ((A->tg_filt_tol[g] >> tsx) & 1)) {
+                    if (aux >= 0) {
+                      uint8_t* c = &A->hcnt_nc[(size_t)aux * A->hnc_stride + ncx];
+                      *c = *c == 255 ? 1 : *c < 254 ? *c + 1 : 254;  // 255: an unregistered domain
+                      A->tg_reg[g] = 1;
+                    } else {
+                      const uint32_t code = A->nc_tcode[(size_t)(-1 - aux) * A->hnc_stride + ncx];
+                      if (code < 64) {
+                        A->tg_cnt[(size_t)g * 64 + code] += 1;
+                        A->tg_reg[g] |= 1ull << code;
+                      }
+                    }
+                  }
+                }
+              }
+              bytes += 16 * (uint64_t)rec_n;
+            }
             if (FL_CACHE && !full_add) {  // the append path left the requirements (hmin, catalogue) as they were
               c_nc = ncx, c_cat = cat, c_hm = hm, c_X = X, c_q = q_lane, c_fj = fj;
               c_r0 = lane_bcast_i64(hv.r0, l) - pr0;
@@ -1978,12 +2059,15 @@ if (!FL_NOTIME && tmg) {                                    \
         break;
       }
       pops++;
-      a_cur_prev_pos = wpos;
+      // cursor: every position before the winner failed; with owned groups, before the first position that passed
+      // the count-independent checks (a zone-count failure may pass later), as the full path
+      const int cpos = TOPO && t_n ? min(ipos, wpos) : wpos;
+      a_cur_prev_pos = cpos;
       a_cur_prev_stamp = stk_t;
       mut = 1;
       mut_p = wpos;
       if (lane == 0) {
-        A->cur_nc[2 * sl] = wpos;
+        A->cur_nc[2 * sl] = cpos;
         A->cur_nc[2 * sl + 1] = a_cur_prev_stamp;
       }
       // placement / events: buffered one pod per lane, written 64 at a time (nothing reads them before the
