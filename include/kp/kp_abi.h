@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define KP_ABI_VERSION 9
+#define KP_ABI_VERSION 10
 
 enum kp_status {
   KP_OK = 0,
@@ -304,7 +304,8 @@ typedef struct kp_pod {
   uint32_t shape;
   uint32_t reserved_;
   int64_t creation_unix;  /* metadata.creationTimestamp (1 s resolution, as in the API) */
-  uint64_t uid_key;       /* order-preserving key of metadata.uid (string order of UIDs) */
+  uint64_t uid_key;       /* order-preserving key of metadata.uid (string order of UIDs); ignored when the batch
+                             passes the UIDs themselves (kp_solve_in.pod_uids / kp_cluster.pod_uids, ABI v10) */
 } kp_pod;
 
 /* In-flight or real node already in the cluster (upstream ExistingNode). */
@@ -352,6 +353,9 @@ typedef struct kp_solve_in {
    * Add whose NodeClaim is compatible with reserved offerings it cannot reserve, and does not relax the pod then. */
   uint32_t reserved_offering_mode;
   uint32_t reserved2_;
+  /* ABI v10: metadata.uid of every pod (n_pods strings), or NULL. Given, the Queue's last tie-break (upstream NewQueue:
+   * creationTimestamp, then UID) compares the UIDs as strings, exactly; kp_pod.uid_key is then ignored. */
+  const char* const* pod_uids;
 } kp_solve_in;
 
 #define KP_RESERVED_FALLBACK 0
@@ -399,6 +403,9 @@ typedef struct kp_solve_stats {
                                no in-flight NodeClaim took it, reserved */
   uint64_t reserved_offering_errors; /* ABI v9: pops whose addToNewNodeClaim failed on a ReservedOfferingError (strict
                                         mode; upstream Results.ReservedOfferingErrors: deferred, not relaxed) */
+  uint64_t order_chunks[5]; /* ABI v10, diagnostic: the chunked newNodeClaims order past the LDS sort capacity: peak
+                               chunks, chunk splits, emptied chunks, directory (re)builds, final order mode (1 LDS,
+                               2 chunked, 0 flat global) */
 } kp_solve_stats;
 
 /* ---- context ---------------------------------------------------------------------------- */
@@ -472,7 +479,7 @@ typedef struct kp_ec2_info {
   int32_t trunking;               /* Limits[name].IsTrunkingCompatible */
   int32_t branch_enis;            /* Limits[name].BranchInterface */
   int32_t in_limits_table;        /* name present in zz_generated.vpclimits.go */
-  int32_t reserved2_;
+  int32_t instance_storage_gb;    /* ABI v10: InstanceStorageInfo.TotalSizeInGB (any disk type); 0: local_nvme_gb */
 } kp_ec2_info;
 
 /* One kubelet eviction-signal value (memory.available / nodefs.available): a quantity or a percentage of the
@@ -495,7 +502,20 @@ typedef struct kp_kubelet {
   kp_eviction_value soft_memory_available, soft_nodefs_available;
 } kp_kubelet;
 
-/* EC2NodeClass subset that changes results (AMI family, kubelet overrides). */
+/* EC2NodeClass.spec.blockDeviceMappings entry (ABI v10): the fields ephemeralStorage reads
+ * (R:pkg/providers/instancetype/types.go:349-385). */
+typedef struct kp_block_device_mapping {
+  const char* device_name;  /* deviceName; NULL: unset */
+  int64_t volume_size;      /* ebs.volumeSize in bytes; < 0: nil */
+  int32_t root_volume;      /* rootVolume */
+  int32_t reserved_;
+} kp_block_device_mapping;
+
+/* EC2NodeClass.spec.instanceStorePolicy (ABI v10) */
+#define KP_INSTANCE_STORE_NONE 0
+#define KP_INSTANCE_STORE_RAID0 1
+
+/* EC2NodeClass subset that changes results (AMI family, kubelet overrides, block devices). */
 typedef struct kp_nodeclass {
   const char* region;
   const char* const* zones;      /* subnet zones (ZoneInfo) */
@@ -505,6 +525,12 @@ typedef struct kp_nodeclass {
   int32_t pods_per_core;         /* <= 0: nil */
   int32_t ami_family;            /* ABI v9: KP_AMI_* (EC2NodeClass.AMIFamily(); 0 = AL2023, the default alias) */
   const kp_kubelet* kubelet;     /* NULL: no kubelet block (defaults) */
+  /* ABI v10: ephemeral-storage capacity (R:types.go:349-385): RAID0 -> the instance store's total size; else the
+   * root-volume BDM's size, else (Custom) the last BDM's size or the 20Gi EBS default, else the BDM on the family's
+   * ephemeral device; else the family's default ephemeral volume */
+  const kp_block_device_mapping* block_device_mappings;
+  uint32_t n_block_device_mappings;
+  int32_t instance_store_policy; /* KP_INSTANCE_STORE_* */
 } kp_nodeclass;
 
 /* AMI families (R:pkg/providers/amifamily): their FeatureFlags (R:resolver.go:110-117, bottlerocket.go:126-132,
@@ -690,6 +716,7 @@ typedef struct kp_cluster {
   uint32_t n_pending;
   uint32_t n_namespaces;         /* ABI v8: the cluster's namespaces (pod affinity namespaceSelector) */
   const kp_namespace* namespaces;
+  const char* const* pod_uids;   /* ABI v10: metadata.uid of every pod, or NULL (see kp_solve_in.pod_uids) */
 } kp_cluster;
 
 enum kp_decision { KP_DECISION_NOOP = 0, KP_DECISION_DELETE = 1, KP_DECISION_REPLACE = 2 };

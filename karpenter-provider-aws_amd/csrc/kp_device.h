@@ -19,6 +19,15 @@ struct NcHead {
   int32_t pad_[6];
 };
 
+// One chunk of the spilled newNodeClaims order (solve_kernel's chunked mode): up to 64 NodeClaim ids in sorted order
+// and their len(Pods).
+struct ChkBlk {
+  int32_t id[64];
+  int32_t key[64];
+};
+#define CHK_MAXC 4096  // chunks (and blocks) of the chunked order; its directory lives in LDS
+#define CHK_LDS_BYTES (CHK_MAXC * 14)  // the directory: start, info, block epochs (4 B each), free list (2 B)
+
 struct SolveArgs {
   const DevDict* dict;
   const DevCatalog* cats;
@@ -68,6 +77,13 @@ struct SolveArgs {
   int32_t* g_order;                  // [P] newNodeClaims order
   int32_t sort_in_lds;               // unused (LDS until SORT_CAP NodeClaims, then global)
   int32_t sort_cap;
+  // past sort_cap NodeClaims the order is chunked (chk_blk, directory in LDS); when the directory is full (or
+  // chk_maxc == 0) it falls back to the flat global arrays g_order / g_npods
+  ChkBlk* chk_blk;                   // [CHK_MAXC]
+  int32_t* chk_dead;                 // [chk_dead_rows][CHK_MAXC] per (shape-level, block): the block's insertion epoch
+                                     // when every NodeClaim in it failed the shape-level permanently (-1 none)
+  int32_t chk_dead_rows;             // shape-levels < this keep dead marks
+  int32_t chk_maxc;                  // chunks the directory may use (<= CHK_MAXC; a test hook lowers it)
   // exact failure memo: outcome of Add/CanAdd depends only on (candidate state, pod shape-level), so a
   // recorded failure stays valid while the candidate's version is unchanged
   int32_t ncc;                       // NodeClaim ids < ncc are memoised

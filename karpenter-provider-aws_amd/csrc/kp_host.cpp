@@ -227,6 +227,9 @@ struct kp_catalog {
   uint64_t uid;  // process-unique identity (a new upload never reuses one, unlike its address)
   vector<HostType> types;
   bool reservations = false;  // some offering carries a capacity-reservation id or type
+  // false once kp_catalog_destroy ran: plans and cached bases that compiled this catalogue hold the token and refuse
+  // to run (or refresh) instead of reading a freed catalogue
+  std::shared_ptr<bool> alive = std::make_shared<bool>(true);
 };
 
 namespace {
@@ -948,7 +951,21 @@ int32_t kp_catalog_upload(kp_ctx* ctx, const kp_catalog_desc* desc, uint64_t seq
 }
 uint64_t kp_catalog_seqnum(const kp_catalog* c) { return c ? c->seqnum : 0; }
 uint32_t kp_catalog_size(const kp_catalog* c) { return c ? (uint32_t)c->types.size() : 0; }
-void kp_catalog_destroy(kp_catalog* c) { delete c; }
+namespace {
+void DropBasesOf(kp_ctx* ctx, const kp_catalog* c);
+}
+// A catalogue may be destroyed while plans prepared on it still exist: they (and the ctx's cached bases, which are
+// dropped here) see its alive token cleared and return KP_E_INVAL instead of reading it.
+void kp_catalog_destroy(kp_catalog* c) {
+  if (!c) return;
+  std::unique_lock<std::recursive_mutex> lock;
+  if (c->ctx) {
+    lock = std::unique_lock<std::recursive_mutex>(c->ctx->mu);
+    DropBasesOf(c->ctx, c);
+  }
+  *c->alive = false;
+  delete c;
+}
 
 // UnavailableOfferings.MarkUnavailable + SeqNum bump (R:pkg/cache/unavailableofferings.go:66-92) on the uploaded
 // offerings; the next prepare (or kp_filter_refresh) rebuilds Available exactly as createOfferings does
@@ -1013,6 +1030,39 @@ struct FamilyFlags {
   bool eni_memory, pods_per_core, eviction_soft, eni_density, windows;
   int64_t storage_bytes;
 };
+// ephemeralStorage (R:pkg/providers/instancetype/types.go:349-385), in bytes: instanceStorePolicy RAID0 -> the
+// instance store's total size ("%dG"); else the first root-volume BDM with a volumeSize; else for Custom the last
+// BDM's volumeSize or DefaultEBS (20Gi), for the other families the first BDM on the family's ephemeral device
+// (R:amifamily al2023.go:106-108, al2.go:114-116, bottlerocket.go:110-112, windows.go:97-99) with a volumeSize;
+// else the family's default BDM on that device (Bottlerocket :95-108 and the DefaultEBS families 20Gi, Windows
+// :88-95 50Gi, Custom none: DefaultEBS).
+int64_t EphemeralBytes(const kp_ec2_info* info, const kp_nodeclass* nc) {
+  const int64_t kDefaultEBS = 20ll << 30;
+  const int f = nc ? nc->ami_family : KP_AMI_AL2023;
+  const bool windows = f == KP_AMI_WINDOWS2019 || f == KP_AMI_WINDOWS2022;
+  if (nc && nc->instance_store_policy == KP_INSTANCE_STORE_RAID0) {
+    const int64_t gb = info->instance_storage_gb > 0 ? info->instance_storage_gb : info->local_nvme_gb;
+    if (gb > 0) return gb * 1000000000ll;
+  }
+  if (nc && nc->n_block_device_mappings && nc->block_device_mappings) {
+    const kp_block_device_mapping* b = nc->block_device_mappings;
+    const uint32_t n = nc->n_block_device_mappings;
+    for (uint32_t i = 0; i < n; i++)
+      if (b[i].root_volume) {  // lo.Find: the first root volume only
+        if (b[i].volume_size >= 0) return b[i].volume_size;
+        break;
+      }
+    if (f == KP_AMI_CUSTOM) return b[n - 1].volume_size >= 0 ? b[n - 1].volume_size : kDefaultEBS;
+    const char* dev = f == KP_AMI_BOTTLEROCKET ? "/dev/xvdb" : windows ? "/dev/sda1" : "/dev/xvda";
+    for (uint32_t i = 0; i < n; i++)
+      if (b[i].device_name && strcmp(b[i].device_name, dev) == 0) {
+        if (b[i].volume_size >= 0) return b[i].volume_size;
+        break;
+      }
+  }
+  return windows ? 50ll << 30 : kDefaultEBS;
+}
+
 FamilyFlags Family(const kp_nodeclass* nc) {
   const int f = nc ? nc->ami_family : KP_AMI_AL2023;
   if (f == KP_AMI_BOTTLEROCKET) return {false, false, false, true, false, 20ll << 30};
@@ -1045,7 +1095,7 @@ int32_t kp_instance_type_overhead(const kp_options* opts, const kp_ec2_info* inf
   memset(sys, 0, sizeof *sys);
   memset(ev, 0, sizeof *ev);
   const FamilyFlags fam = Family(nc);
-  const int64_t kStorageBytes = fam.storage_bytes;
+  const int64_t kStorageBytes = EphemeralBytes(info, nc);
   // kubeReservedResources: UsesENILimitedMemoryOverhead -> memory from ENILimitedPods(info, 0), else from pods(); the
   // CPU ranges accumulate with a truncation per range; then the user's keys replace the computed ones (lo.Assign)
   SetRes(kube, KP_RES_MEMORY, (11 * (fam.eni_memory ? EniLimitedPods(info, 0) : PodsOf(opts, info, nc)) + 255) * 1048576ll * 1000ll);
@@ -1100,7 +1150,7 @@ int32_t kp_instance_type_resolve(const kp_options* opts, const kp_ec2_info* info
   SetRes(capacity, KP_RES_CPU, (int64_t)info->vcpu * 1000);
   SetRes(capacity, KP_RES_MEMORY, MemoryBytes(opts, info) * 1000);
   const FamilyFlags fam = Family(nc);
-  SetRes(capacity, KP_RES_EPHEMERAL_STORAGE, fam.storage_bytes * 1000);
+  SetRes(capacity, KP_RES_EPHEMERAL_STORAGE, EphemeralBytes(info, nc) * 1000);
   SetRes(capacity, KP_RES_PODS, PodsOf(opts, info, nc) * 1000);
   SetRes(capacity, KP_RES_POD_ENI, (info->in_limits_table && info->trunking) ? (int64_t)info->branch_enis * 1000 : 0);
   const string gm = info->gpu_manufacturer ? info->gpu_manufacturer : "";
@@ -1165,7 +1215,8 @@ struct SolveBase {
   vector<int32_t> np_catalog;
   vector<int> np_order;
   vector<int64_t> np_daemon;          // [n_nodepools][NRES]
-  vector<const kp_catalog*> catalogs; // the catalogues compiled in (caller-owned, they outlive every plan on them)
+  vector<const kp_catalog*> catalogs; // the catalogues compiled in (caller-owned; see alive)
+  vector<std::shared_ptr<bool>> alive; // their kp_catalog::alive tokens: a destroyed one makes the base unusable
   vector<uint64_t> seqnums;           // their seqnums the offering arrays reflect
   string ident;                       // cache fingerprint without the seqnums
   string key;                         // cache fingerprint: ident + seqnums
@@ -1945,6 +1996,21 @@ vector<uint64_t> SeqnumsOf(const vector<const kp_catalog*>& cats) {
   for (auto* c : cats) v.push_back(c->seqnum);
   return v;
 }
+// the ctx's cached bases that compiled catalogue c (kp_catalog_destroy)
+void DropBasesOf(kp_ctx* ctx, const kp_catalog* c) {
+  auto& bases = ctx->bases;
+  bases.erase(std::remove_if(bases.begin(), bases.end(),
+                             [&](const std::shared_ptr<SolveBase>& b) {
+                               return std::find(b->catalogs.begin(), b->catalogs.end(), c) != b->catalogs.end();
+                             }),
+              bases.end());
+}
+// KP_OK while every catalogue a base (or plan) compiled is alive, else the error a run or refresh returns.
+int32_t CatalogsAlive(const vector<std::shared_ptr<bool>>& alive) {
+  for (auto& a : alive)
+    if (!*a) return fail(KP_E_INVAL, "a catalogue this plan was prepared on was destroyed (kp_catalog_destroy)");
+  return KP_OK;
+}
 string SeqKey(const vector<uint64_t>& seqs) {
   string k = "#";
   for (uint64_t q : seqs) k += std::to_string(q) + ";";
@@ -2245,6 +2311,7 @@ int32_t BuildBase(const kp_solve_in* in, const SolveRaw& raw, SolveBase& b) {
       b.np_daemon.push_back((np.daemon_requests.present >> r) & 1 ? np.daemon_requests.milli[r] : 0);
   }
   b.catalogs = cats;
+  for (auto* c : cats) b.alive.push_back(c->alive);
   b.seqnums = SeqnumsOf(cats);
   rc = ReservationTables(b);
   if (rc) return rc;
@@ -2262,6 +2329,23 @@ int32_t BuildBase(const kp_solve_in* in, const SolveRaw& raw, SolveBase& b) {
 }
 
 // Per-Solve half on a SolveBase: taint sets, limits, existing nodes, shapes (levels, PVP rows), topology, queue.
+// Exact Queue keys from the pods' UIDs (upstream NewQueue's last tie-break compares metadata.uid as strings): each
+// pod's rank in the batch sorted by UID, equal UIDs (invalid in a cluster) by batch index. false: a NULL UID.
+bool ExactUidKeys(const char* const* uids, uint32_t n, vector<uint64_t>& key) {
+  vector<uint32_t> idx(n);
+  for (uint32_t i = 0; i < n; i++) {
+    if (!uids[i]) return false;
+    idx[i] = i;
+  }
+  std::sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) {
+    const int c = strcmp(uids[a], uids[b]);
+    return c != 0 ? c < 0 : a < b;
+  });
+  key.assign(n, 0);
+  for (uint32_t r = 0; r < n; r++) key[idx[r]] = r;
+  return true;
+}
+
 int32_t CompilePerCall(const kp_solve_in* in, const SolveRaw& raw, Compiled& cp) {
   const SolveBase& b = *cp.B;
   const Dict& d = b.d;
@@ -2404,9 +2488,11 @@ int32_t CompilePerCall(const kp_solve_in* in, const SolveRaw& raw, Compiled& cp)
     int64_t creation;
     uint64_t uid;
   };
+  vector<uint64_t> uidk;  // the UIDs themselves (ABI v10): their rank in string order is the exact key
+  if (in->pod_uids && !ExactUidKeys(in->pod_uids, in->n_pods, uidk)) return fail(KP_E_INVAL, "null pod uid");
   vector<QKey> qk(in->n_pods);
   for (uint32_t p = 0; p < in->n_pods; p++)
-    qk[p] = {srank[cp.pod_shape[p]], (int32_t)p, in->pods[p].creation_unix, in->pods[p].uid_key};
+    qk[p] = {srank[cp.pod_shape[p]], (int32_t)p, in->pods[p].creation_unix, in->pod_uids ? uidk[p] : in->pods[p].uid_key};
   std::sort(qk.begin(), qk.end(), [](const QKey& p, const QKey& q) {
     if (p.rank != q.rank) return p.rank < q.rank;
     if (p.creation != q.creation) return p.creation < q.creation;
@@ -2424,7 +2510,15 @@ int32_t CompilePerCall(const kp_solve_in* in, const SolveRaw& raw, Compiled& cp)
 // templates changed: a NodePool whose types all became unavailable, or the reverse), < 0 on a device error.
 // Plans prepared on the base before the refresh see it through `version` (kp_solve_run refuses them until
 // kp_solve_refresh).
-int32_t RefreshOfferings(kp_ctx* ctx, SolveBase& b) {
+// The refreshed state becomes current (stale checks pass) only here, after every device copy succeeded: a failed
+// copy leaves the old seqnums, so the plans stay refused and a retried refresh copies again.
+void CommitRefresh(SolveBase& b) {
+  b.seqnums = SeqnumsOf(b.catalogs);
+  b.key = b.ident + SeqKey(b.seqnums);
+  b.version++;
+}
+
+int32_t RefreshOfferings(kp_ctx* ctx, SolveBase& b, bool commit = true) {
   map<ClassKey, int> classes;
   for (int c = 0; c < b.C; c++) classes[KeyOfClass(b.classes[c])] = c;
   for (auto* cat : b.catalogs)
@@ -2454,9 +2548,6 @@ int32_t RefreshOfferings(kp_ctx* ctx, SolveBase& b) {
   }
   b.tmpl_X.swap(tX);
   if (ReservationTables(b)) return 1;  // (reservation classes are fixed by the dictionary: cannot fail here)
-  b.seqnums = SeqnumsOf(b.catalogs);
-  b.key = b.ident + SeqKey(b.seqnums);
-  b.version++;
   if (b.on_device && ctx) {
     uint8_t* base = (uint8_t*)b.dev.p;
     hipStream_t st = ctx->stream;
@@ -2472,6 +2563,7 @@ int32_t RefreshOfferings(kp_ctx* ctx, SolveBase& b) {
     HIPCHK(hipMemcpyAsync(base + b.o_tX, b.tmpl_X.data(), b.tmpl_X.size() * 8, hipMemcpyHostToDevice, st));
     HIPCHK(hipStreamSynchronize(st));
   }
+  if (commit) CommitRefresh(b);
   return 0;
 }
 
@@ -2862,6 +2954,12 @@ static int32_t SolvePrepareLocal(kp_ctx* ctx, const kp_solve_in* in, kp_comm* co
   const size_t o_nct = blob.reserve_dev(sizeof(int32_t) * Pc);
   const size_t o_npods = blob.reserve_dev(sizeof(int32_t) * Pc);
   const size_t o_order = blob.reserve_dev(sizeof(int32_t) * Pc);
+  // chunked newNodeClaims order past the LDS sort capacity (blocks + per (shape-level, block) dead marks): only when
+  // the Solve can create more NodeClaims than the LDS holds
+  int sort_cap = 8192;  // newNodeClaims order lives in LDS (64 KiB) up to this many NodeClaims, then spills
+  if (const char* e = getenv("KP_SORT_CAP")) sort_cap = std::max(1, std::min(8192, atoi(e)));  // test hook
+  const bool chk_on = Pc > sort_cap;
+  const size_t o_chkblk = blob.reserve_dev(chk_on ? sizeof(ChkBlk) * CHK_MAXC : 8);
   const size_t o_maxalloc = blob.reserve_dev(sizeof(int64_t) * (size_t)Pc * KP_NRES);
   const size_t o_fitj = blob.reserve_dev(sizeof(int32_t) * (size_t)Pc * KP_NRES);
   const size_t o_nchead = blob.reserve_dev(sizeof(NcHead) * (size_t)Pc + 64);
@@ -2884,6 +2982,8 @@ static int32_t SolvePrepareLocal(kp_ctx* ctx, const kp_solve_in* in, kp_comm* co
   const size_t o_ncfail = blob.reserve_dev(sizeof(int32_t) * SLn * ncc);
   const size_t o_exfail = blob.reserve_dev(sizeof(int32_t) * SLn * std::max(E, 1));
   const size_t o_tfail = blob.reserve_dev(sizeof(int32_t) * SLn * std::max(NT, 1));
+  const int chk_dead_rows = chk_on ? (int)std::min<size_t>(SLn, ((size_t)64 << 20) / (4 * CHK_MAXC)) : 0;
+  const size_t o_chkdead = blob.reserve_dev(std::max<size_t>(sizeof(int32_t) * chk_dead_rows * CHK_MAXC, 8));
   const size_t n_fail = blob.total() - o_fail0;
   const int opt_stride = in->max_instance_types ? (int)in->max_instance_types : std::max(1, d.dd.T);
   const size_t o_opts = blob.reserve_dev(sizeof(uint32_t) * (size_t)Pc * opt_stride);
@@ -2966,9 +3066,13 @@ static int32_t SolvePrepareLocal(kp_ctx* ctx, const kp_solve_in* in, kp_comm* co
   a.g_npods = (int32_t*)(base + o_npods);
   a.g_order = (int32_t*)(base + o_order);
   a.sort_in_lds = 1;
-  a.sort_cap = 8192;  // newNodeClaims order lives in LDS (64 KiB) up to this many NodeClaims, then spills
-  if (const char* e = getenv("KP_SORT_CAP")) a.sort_cap = std::max(1, std::min(8192, atoi(e)));  // test hook
+  a.sort_cap = sort_cap;
   a.ncc = ncc;
+  a.chk_blk = (ChkBlk*)(base + o_chkblk);
+  a.chk_dead = (int32_t*)(base + o_chkdead);
+  a.chk_dead_rows = chk_dead_rows;
+  a.chk_maxc = chk_on ? CHK_MAXC : 0;
+  if (const char* e = getenv("KP_CHK_MAXC")) a.chk_maxc = chk_on ? std::max(0, std::min(CHK_MAXC, atoi(e))) : 0;  // test hook
   a.nc_head = (NcHead*)(((uintptr_t)(base + o_nchead) + 63) & ~(uintptr_t)63);
   a.nc_fail = (int32_t*)(base + o_ncfail);
   a.ex_ver = (int32_t*)(base + o_exver);
@@ -3101,6 +3205,7 @@ static int32_t SolvePrepareLocal(kp_ctx* ctx, const kp_solve_in* in, kp_comm* co
 // kp_solve_run on a plan whose catalogues changed since its data was derived would place pods on stale offerings
 static int32_t SolvePlanStale(const kp_solve_plan* plan) {
   const SolveBase& B = *plan->cp->B;
+  if (int32_t rc = CatalogsAlive(B.alive)) return rc;
   if (plan->base_version != B.version || SeqnumsOf(B.catalogs) != B.seqnums)
     return fail(KP_E_INVAL, "stale plan: a catalogue's seqnum changed since it was prepared (kp_solve_refresh)");
   return KP_OK;
@@ -3112,6 +3217,7 @@ int32_t kp_solve_refresh(kp_solve_plan* plan) {
   std::lock_guard<std::recursive_mutex> lock(ctx->mu);
   HIPCHK(hipSetDevice(ctx->device));
   SolveBase& B = *plan->cp->B;
+  if (int32_t rc = CatalogsAlive(B.alive)) return rc;
   if (SeqnumsOf(B.catalogs) != B.seqnums) {
     int32_t rc = RefreshOfferings(ctx, B);
     if (rc < 0) return rc;
@@ -3163,7 +3269,7 @@ int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out) {
   HIPCHK(hipMemsetAsync(base + plan->o_fail, 0xFF, plan->n_fail, st));
   if (plan->n_hcnc) HIPCHK(hipMemsetAsync(base + plan->o_hcnc, 0, plan->n_hcnc, st));
   const SolveArgs& a = plan->a;
-  const size_t dyn = (size_t)2 * a.sort_cap * sizeof(int32_t);
+  const size_t dyn = std::max<size_t>((size_t)2 * a.sort_cap * sizeof(int32_t), a.chk_maxc ? CHK_LDS_BYTES : 0);
   HIPCHK(hipEventRecord(ctx->ev0, st));
   HIPCHK(launch_solve(a, 8, dyn, st));
   HIPCHK(hipEventRecord(ctx->ev1, st));
@@ -3293,6 +3399,7 @@ int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out) {
   for (int i = 0; i < 6; i++) res->stats.fast_cycles[i] = stats[25 + i];
   for (int i = 0; i < 8; i++) res->stats.fast_bails[i] = stats[32 + i];
   res->stats.reserved_offering_errors = stats[40];
+  for (int i = 0; i < 5; i++) res->stats.order_chunks[i] = stats[41 + i];
   res->stats.host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   *out = res.release();
   return KP_OK;
@@ -3878,6 +3985,7 @@ struct OwnedCluster {
   vector<std::unique_ptr<uint8_t[]>> blocks;
   kp_cluster cl;
   vector<const kp_catalog*> cats;
+  vector<std::shared_ptr<bool>> alive;
   const char* S(const char* x) {
     if (!x) return nullptr;
     strs.emplace_back(x);
@@ -3948,6 +4056,7 @@ struct OwnedCluster {
   explicit OwnedCluster(const kp_cluster* in) {
     cl = *in;
     cats.assign(in->catalogs, in->catalogs + in->n_catalogs);
+    for (auto* c : cats) alive.push_back(c->alive);
     cl.catalogs = cats.data();
     cl.catalog_descs = nullptr;
     kp_nodepool* np = A(in->nodepools, in->n_nodepools);
@@ -3995,7 +4104,14 @@ struct OwnedCluster {
       x.preferred_affinity = Terms(x.preferred_affinity, x.n_preferred_affinity);
     }
     cl.shapes = sh;
-    cl.pods = A(in->pods, in->n_pods);
+    kp_pod* pods = A(in->pods, in->n_pods);
+    if (in->pod_uids && pods) {  // each subset's Solve sees the pods' exact UID ranks as their keys
+      vector<uint64_t> k;
+      if (ExactUidKeys(in->pod_uids, in->n_pods, k))
+        for (uint32_t i = 0; i < in->n_pods; i++) pods[i].uid_key = k[i];
+    }
+    cl.pods = pods;
+    cl.pod_uids = nullptr;
     cl.pending_pods = A(in->pending_pods, in->n_pending);
     kp_namespace* ns = A(in->namespaces, in->n_namespaces);
     for (uint32_t i = 0; ns && i < in->n_namespaces; i++) ns[i].name = S(ns[i].name), ns[i].labels = Labels(ns[i].labels, ns[i].n_labels);
@@ -4079,6 +4195,7 @@ static int32_t PrepareGeneral(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan
   in.max_instance_types = 100;
   in.namespaces = cl->namespaces;
   in.n_namespaces = cl->n_namespaces;
+  in.pod_uids = cl->pod_uids;
   Compiled C;
   int32_t rc = CompileSolve(&in, C);
   if (rc) return rc;
@@ -4127,6 +4244,7 @@ int32_t kp_cluster_prepare(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan** 
   in.max_instance_types = 100;
   in.namespaces = cl->namespaces;
   in.n_namespaces = cl->n_namespaces;
+  in.pod_uids = cl->pod_uids;
   int32_t rc = CompileSolve(&in, C);
   if (rc) return rc;
   const Dict& d = C.B->d;
@@ -4394,8 +4512,10 @@ int32_t kp_cluster_refresh(kp_cluster_plan* plan) {
   std::lock_guard<std::recursive_mutex> lock(ctx->mu);
   HIPCHK(hipSetDevice(ctx->device));
   SolveBase& B = *plan->cp->B;
+  if (int32_t rc = CatalogsAlive(B.alive)) return rc;
   if (SeqnumsOf(B.catalogs) == B.seqnums) return KP_OK;
-  int32_t rc = RefreshOfferings(nullptr, B);  // host side; the snapshot's own device copy is written below
+  // host side; the snapshot's own device copy is written below, and the new seqnums are committed only once it is
+  int32_t rc = RefreshOfferings(nullptr, B, false);
   if (rc < 0) return rc;
   if (rc > 0) return fail(KP_E_INVAL, "the offering update changed which NodePools keep instance types: prepare again");
   uint8_t* base = (uint8_t*)plan->buf.p;
@@ -4420,6 +4540,7 @@ int32_t kp_cluster_refresh(kp_cluster_plan* plan) {
   HIPCHK(hipMemcpyAsync(base + plan->o_nflags, plan->node_flags.data(), plan->node_flags.size(), hipMemcpyHostToDevice, st));
   HIPCHK(launch_sim_prep(plan->a, st));
   HIPCHK(hipStreamSynchronize(st));
+  CommitRefresh(B);
   return KP_OK;
 }
 
@@ -4472,6 +4593,7 @@ static int32_t GeneralSimLocked(kp_cluster_plan* plan, const uint32_t* offsets, 
   kp_ctx* ctx = plan->ctx;
   const kp_cluster& cl = plan->general->cl;
   const int N = (int)cl.n_nodes;
+  if (int32_t rc = CatalogsAlive(plan->general->alive)) return rc;
   if (offsets[0] != 0) return fail(KP_E_INVAL, "offsets[0] != 0");
   if (offsets[n_subsets] && !nodes) return fail(KP_E_INVAL, "null nodes");
   vector<std::map<string, string>> labels(N);
@@ -4659,6 +4781,7 @@ static int32_t SimLaunchLocked(kp_cluster_plan* plan, const uint32_t* offsets, c
                                int32_t multi_node, SimArgs& a_out) {
   kp_ctx* ctx = plan->ctx;
   if (plan->general) return GeneralSimLocked(plan, offsets, nodes, n_subsets, multi_node, a_out);
+  if (int32_t rc = CatalogsAlive(plan->cp->B->alive)) return rc;
   if (SeqnumsOf(plan->cp->B->catalogs) != plan->cp->B->seqnums)
     return fail(KP_E_INVAL, "stale plan: a catalogue's seqnum changed since it was prepared (kp_cluster_refresh)");
   if (offsets[0] != 0) return fail(KP_E_INVAL, "offsets[0] != 0");

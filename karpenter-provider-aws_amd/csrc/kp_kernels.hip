@@ -63,6 +63,9 @@
 #ifndef FAST_SCAN_MAX
 #define FAST_SCAN_MAX 512  // longest first-fit scan (positions) the fast lane takes on; longer: the 4-wave pre-pass
 #endif
+#ifndef FAST_CHK_LIVE
+#define FAST_CHK_LIVE 8  // chunked order: live (not dead) chunks the fast lane scans before the 4-wave pre-pass takes over
+#endif
 // Explicit address spaces: LDS data reached through a pointer would otherwise be read with FLAT loads (which wait
 // on the vector-memory counter too and take the long path); global rows get global_load.
 #define LDS __attribute__((address_space(3)))
@@ -1005,6 +1008,41 @@ __device__ __forceinline__ void first_pos_min(uint32_t flags, int pos0, int32_t*
   }
 }
 
+// The same two with an explicit entry / position per round (the chunked order's rounds are chunks, not strides).
+template <int NW>
+__device__ __forceinline__ int compact_candidates_x4e(uint32_t flags, const int* ent, int32_t* s_list, int32_t* s_wcnt,
+                                                      uint32_t tags) {
+  const int wave = threadIdx.x >> 6, lane = LANE;
+  uint64_t bal[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) bal[k] = __ballot((flags >> k) & 1);
+  if (lane < 4) s_wcnt[lane * NW + wave] = __builtin_popcountll(bal[lane & 3]);
+  __syncthreads();
+  int total = 0, before[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    int b = total;
+    for (int w = 0; w < NW; w++) {
+      const int c = s_wcnt[k * NW + w];
+      b += w < wave ? c : 0;
+      total += c;
+    }
+    before[k] = b;
+  }
+  const uint64_t lt = (1ull << lane) - 1;
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+    if ((flags >> k) & 1) s_list[before[k] + __builtin_popcountll(bal[k] & lt)] = ent[k] | (((tags >> k) & 1) ? LIST_TAG : 0);
+  __syncthreads();
+  return total;
+}
+__device__ __forceinline__ void first_pos_min_e(uint32_t flags, const int* pos, int32_t* dst) {
+  for (int k = 0; k < 4; k++) {
+    const uint64_t b = __ballot((flags >> k) & 1);
+    if (b && LANE == __builtin_ctzll(b)) atomicMin(dst, pos[k]);
+  }
+}
+
 template <int NW>
 __device__ __forceinline__ int first_ok(const int32_t* s_ok) {
   for (int w = 0; w < NW; w++)
@@ -1472,6 +1510,434 @@ __device__ __forceinline__ void mstack_push_reg(int32_t LDS* stk, int& n, int& l
   wave_sync();
 }
 
+// ---- the spilled newNodeClaims order as chunks ------------------------------------------------------------------
+// Past the LDS sort capacity the sorted order is a sequence of chunks of at most 64 NodeClaims: one global block per
+// chunk (ids and len(Pods) in order, ChkBlk), and a directory in LDS (the LDS sort arrays' space): per chunk its block,
+// count and last key, and the logical position of its first entry. sort.Slice's stable move (one NodeClaim from its
+// place to the end of its key run, or an appended one into place) then rewrites at most two blocks and a range of
+// directory start positions instead of shifting every entry between the two places (5.3k entries per pop on config 5
+// with the flat array). Each block carries the epoch of its last insertion: a shape-level's pre-pass marks a chunk
+// whose NodeClaims all fail it permanently (headroom, taints, host ports, NEVER in the failure memo: properties that
+// only get worse as a NodeClaim takes pods), and skips it while no NodeClaim entered the block since.
+// Every helper here is executed by one wave with uniform arguments.
+#define CHK_FILL 48        // entries per chunk when the directory is (re)built
+#define CHK_KEY_MAX 8191   // len(Pods) the directory's last-key field holds; more: the flat order
+struct ChkDir {
+  int32_t LDS* start;   // [CHK_MAXC] logical position of the chunk's first entry
+  uint32_t LDS* info;   // [CHK_MAXC] block | count << 12 | last key << 19
+  int32_t LDS* bep;     // [CHK_MAXC] per block id: epoch of its last insertion
+  uint16_t LDS* freel;  // [CHK_MAXC] free block ids (stack)
+};
+__device__ __forceinline__ ChkDir chk_dir(int32_t LDS* s) {
+  return ChkDir{s, (uint32_t LDS*)(s + CHK_MAXC), s + 2 * CHK_MAXC, (uint16_t LDS*)(s + 3 * CHK_MAXC)};
+}
+__device__ __forceinline__ int ci_blk(uint32_t v) { return (int)(v & 0xFFF); }
+__device__ __forceinline__ int ci_cnt(uint32_t v) { return (int)((v >> 12) & 0x7F); }
+__device__ __forceinline__ int ci_last(uint32_t v) { return (int)(v >> 19); }
+__device__ __forceinline__ uint32_t ci_make(int b, int cnt, int last) {
+  return (uint32_t)b | ((uint32_t)cnt << 12) | ((uint32_t)min(last, CHK_KEY_MAX) << 19);
+}
+struct ChkCtl {
+  int32_t nch, nfree, epoch, maxc;  // chunks, free blocks, insertion epoch counter, directory limit
+  int32_t nch_peak, splits, removals, rebuilds;  // diagnostics
+};
+__shared__ ChkCtl g_chk;
+
+// first index in [lo, hi) where the monotone predicate (false ... true) holds; hi if none. 64 samples per round.
+template <class Pred>
+__device__ __forceinline__ int wave_first_true(int lo, int hi, Pred pred) {
+  const int lane = LANE;
+  while (lo < hi) {
+    const int span = hi - lo;
+    const int step = span <= 64 ? 1 : (span + 63) >> 6;
+    const int idx = lo + lane * step;
+    const uint64_t bal = __ballot(idx < hi && pred(idx));
+    if (step == 1) return bal ? lo + __builtin_ctzll(bal) : hi;
+    if (!bal) {
+      lo = lo + (__popcll(__ballot(idx < hi)) - 1) * step + 1;
+    } else {
+      const int f = __builtin_ctzll(bal);
+      if (f == 0) return lo;
+      hi = lo + f * step;
+      lo = lo + (f - 1) * step + 1;
+    }
+  }
+  return lo;
+}
+// chunk holding logical position pos (< n)
+__device__ __forceinline__ int chk_find(const ChkDir& d, int nch, int pos) {
+  return wave_first_true(0, nch, [&](int c) { return d.start[c] > pos; }) - 1;
+}
+// the same by one lane (its own pos)
+__device__ __forceinline__ int chk_find_lane(const ChkDir& d, int nch, int pos) {
+  int lo = 0, hi = nch;
+  while (lo < hi) {
+    const int m = (lo + hi) >> 1;
+    if (d.start[m] > pos) hi = m;
+    else lo = m + 1;
+  }
+  return lo - 1;
+}
+__device__ __forceinline__ void chk_load(const ChkBlk* B, int b, int cnt, int& id, int& key) {
+  const int lane = LANE;
+  id = lane < cnt ? B[b].id[lane] : -1;
+  key = lane < cnt ? B[b].key[lane] : INT32_MAX;
+}
+__device__ __forceinline__ void chk_store(ChkBlk* B, int b, int cnt, int id, int key) {
+  const int lane = LANE;
+  if (lane < cnt) {
+    B[b].id[lane] = id;
+    B[b].key[lane] = key;
+  }
+}
+// directory entries [i, nch) move up by one (room at i) / [i + 1, nch) down by one (entry i removed)
+__device__ void chk_dir_open(const ChkDir& d, int nch, int i) {
+  const int lane = LANE;
+  for (int top = nch; top > i; top -= 64) {
+    const int j = top - 1 - lane;
+    const bool act = j >= i;
+    const int s = act ? d.start[j] : 0;
+    const uint32_t v = act ? d.info[j] : 0;
+    wave_sync();
+    if (act) {
+      d.start[j + 1] = s;
+      d.info[j + 1] = v;
+    }
+    wave_sync();
+  }
+}
+__device__ void chk_dir_close(const ChkDir& d, int nch, int i) {
+  const int lane = LANE;
+  for (int b = i + 1; b < nch; b += 64) {
+    const int j = b + lane;
+    const bool act = j < nch;
+    const int s = act ? d.start[j] : 0;
+    const uint32_t v = act ? d.info[j] : 0;
+    wave_sync();
+    if (act) {
+      d.start[j - 1] = s;
+      d.info[j - 1] = v;
+    }
+    wave_sync();
+  }
+}
+
+// (Re)builds the directory from a sorted flat order (order[i], npods[id]) of n entries, CHK_FILL per chunk; every block
+// gets a new epoch. false: it does not fit (the caller keeps the flat order).
+__device__ bool chk_build(const ChkDir& d, ChkCtl LDS* C, ChkBlk* B, const int32_t* order, const int32_t* npods, int n) {
+  const int lane = LANE;
+  const int nch = (n + CHK_FILL - 1) / CHK_FILL;
+  const int maxc = U(C->maxc);
+  if (nch > maxc) return false;
+  int kmax = 0;
+  for (int c = lane; c < nch; c += 64) {
+    const int cnt = min(CHK_FILL, n - c * CHK_FILL);
+    kmax = max(kmax, npods[order[c * CHK_FILL + cnt - 1]]);
+  }
+  kmax = -wave_min_i32(-kmax);
+  if (kmax > CHK_KEY_MAX) return false;
+  const int ep = U(C->epoch) + 1;
+  for (int i = lane; i < n; i += 64) {
+    const int id = order[i];
+    const int c = i / CHK_FILL, s = i - c * CHK_FILL;
+    B[c].id[s] = id;
+    B[c].key[s] = npods[id];
+  }
+  for (int c = lane; c < nch; c += 64) {
+    const int cnt = min(CHK_FILL, n - c * CHK_FILL);
+    d.start[c] = c * CHK_FILL;
+    d.info[c] = ci_make(c, cnt, npods[order[c * CHK_FILL + cnt - 1]]);
+  }
+  for (int b = lane; b < maxc; b += 64) {
+    d.bep[b] = ep;
+    if (b >= nch) d.freel[b - nch] = (uint16_t)b;
+  }
+  if (lane == 0) {
+    C->nch = nch;
+    C->nfree = maxc - nch;
+    C->epoch = ep;
+    C->nch_peak = max(C->nch_peak, nch);
+    C->rebuilds += 1;
+  }
+  wave_sync();
+  return true;
+}
+
+// The flat order (order / npods) from the chunks; `n` entries.
+__device__ void chk_materialize(const ChkDir& d, ChkCtl LDS* C, const ChkBlk* B, int32_t* order, int32_t* npods) {
+  const int lane = LANE;
+  const int nch = U(C->nch);
+  for (int c = 0; c < nch; c++) {
+    const uint32_t v = d.info[c];
+    const int cnt = ci_cnt(v), b = ci_blk(v), s0 = d.start[c];
+    if (lane < cnt) {
+      const int id = B[b].id[lane];
+      order[s0 + lane] = id;
+      npods[id] = B[b].key[lane];
+    }
+  }
+  wave_sync();
+}
+
+// Appends NodeClaim e (len(Pods) key) at the end of the order. false: the directory is full (no change made).
+__device__ bool chk_append(const ChkDir& d, ChkCtl LDS* C, ChkBlk* B, int e, int key) {
+  const int lane = LANE;
+  const int nch = U(C->nch);
+  if (nch > 0) {
+    const uint32_t v = d.info[nch - 1];
+    const int cnt = ci_cnt(v), b = ci_blk(v);
+    if (cnt < 64) {
+      const int ep = U(C->epoch) + 1;
+      if (lane == 0) {
+        B[b].id[cnt] = e;
+        B[b].key[cnt] = key;
+        d.info[nch - 1] = ci_make(b, cnt + 1, key);
+        d.bep[b] = ep;
+        C->epoch = ep;
+      }
+      wave_sync();
+      return true;
+    }
+  }
+  if (nch >= U(C->maxc) || U(C->nfree) == 0) return false;
+  const int nf = U(C->nfree) - 1;
+  const int b = d.freel[nf];
+  const int s0 = nch ? d.start[nch - 1] + ci_cnt(d.info[nch - 1]) : 0;
+  const int ep = U(C->epoch) + 1;
+  if (lane == 0) {
+    B[b].id[0] = e;
+    B[b].key[0] = key;
+    d.start[nch] = s0;
+    d.info[nch] = ci_make(b, 1, key);
+    d.bep[b] = ep;
+    C->epoch = ep;
+    C->nfree = nf;
+    C->nch = nch + 1;
+    C->nch_peak = max(C->nch_peak, nch + 1);
+  }
+  wave_sync();
+  return true;
+}
+
+// Moves the entry at (cf, sf) to just before the entry at (cx, sx) (cx < 0: to the end of the order), keeping every
+// other entry's relative order. false: the target chunk is full and the directory cannot take a split (no change).
+__device__ bool chk_move(const ChkDir& d, ChkCtl LDS* C, ChkBlk* B, int cf, int sf, int cx, int sx) {
+  const int lane = LANE;
+  int nch = U(C->nch);
+  const uint32_t vf = d.info[cf];
+  const int bf = ci_blk(vf), nf = ci_cnt(vf);
+  int idf, keyf;
+  chk_load(B, bf, nf, idf, keyf);
+  const int E = __builtin_amdgcn_readlane(idf, sf), KE = __builtin_amdgcn_readlane(keyf, sf);
+  int tc, ts;  // insert before slot ts of chunk tc (ts == count: at its end), in the pre-move contents
+  if (cx < 0) {
+    tc = nch - 1;
+    ts = ci_cnt(d.info[tc]);
+  } else {
+    tc = cx;
+    ts = sx;
+  }
+  if (ts == 0 && tc > 0) {  // before a chunk's first entry = after the previous chunk's last: no shift there
+    const int pc = ci_cnt(d.info[tc - 1]);
+    if (pc < 64 || tc - 1 == cf) {
+      tc -= 1;
+      ts = pc;
+    }
+  }
+  if (tc == cf) {  // within one chunk: remove slot sf, insert at ins (post-removal index)
+    const int ins = ts > sf ? ts - 1 : ts;
+    int src;
+    if (ins >= sf) src = lane < sf ? lane : lane < ins ? lane + 1 : lane == ins ? -1 : lane;
+    else src = lane < ins ? lane : lane == ins ? -1 : lane <= sf ? lane - 1 : lane;
+    const int sid = __shfl(idf, src < 0 ? 0 : src, 64), skey = __shfl(keyf, src < 0 ? 0 : src, 64);
+    const int nid = src < 0 ? E : sid, nkey = src < 0 ? KE : skey;
+    chk_store(B, bf, nf, nid, nkey);
+    const int last = __builtin_amdgcn_readlane(nkey, nf - 1);
+    if (lane == 0) d.info[cf] = ci_make(bf, nf, last);
+    wave_sync();
+    return true;
+  }
+  uint32_t vt = d.info[tc];
+  int bt = ci_blk(vt), nt = ci_cnt(vt);
+  int idt, keyt;
+  chk_load(B, bt, nt, idt, keyt);
+  if (nt == 64) {  // split the target chunk: its upper half into a new block and directory entry tc + 1
+    if (nch >= U(C->maxc) || U(C->nfree) == 0) return false;
+    const int nfr = U(C->nfree) - 1;
+    const int b2 = d.freel[nfr];
+    const int ep = U(C->epoch) + 1;
+    const int hid = __shfl(idt, (lane + 32) & 63, 64), hkey = __shfl(keyt, (lane + 32) & 63, 64);
+    chk_store(B, b2, 32, hid, hkey);
+    chk_dir_open(d, nch, tc + 1);
+    const int s_lo = d.start[tc];
+    if (lane == 0) {
+      d.start[tc + 1] = s_lo + 32;
+      d.info[tc] = ci_make(bt, 32, __builtin_amdgcn_readlane(keyt, 31));
+      d.info[tc + 1] = ci_make(b2, 32, __builtin_amdgcn_readlane(keyt, 63));
+      d.bep[b2] = ep;
+      C->epoch = ep;
+      C->nfree = nfr;
+      C->nch = nch + 1;
+      C->nch_peak = max(C->nch_peak, nch + 1);
+      C->splits += 1;
+    }
+    wave_sync();
+    nch += 1;
+    if (cf > tc) cf += 1;
+    if (ts > 32) {
+      tc += 1;
+      ts -= 32;
+      bt = b2;
+      idt = hid;
+      keyt = hkey;
+    }
+    nt = 32;
+  }
+  // remove from the source chunk
+  {
+    const int src = lane < sf ? lane : lane + 1;
+    const int nid = __shfl(idf, src & 63, 64), nkey = __shfl(keyf, src & 63, 64);
+    chk_store(B, bf, nf - 1, nid, nkey);
+    if (lane == 0 && nf > 1) d.info[cf] = ci_make(bf, nf - 1, __builtin_amdgcn_readlane(nkey, nf - 2));
+  }
+  // insert into the target chunk
+  {
+    const int src = lane < ts ? lane : lane - 1;
+    const int sid = __shfl(idt, src < 0 ? 0 : src, 64), skey = __shfl(keyt, src < 0 ? 0 : src, 64);
+    const int nid = lane == ts ? E : sid, nkey = lane == ts ? KE : skey;
+    chk_store(B, bt, nt + 1, nid, nkey);
+    const int last = __builtin_amdgcn_readlane(nkey, nt);
+    const int ep = U(C->epoch) + 1;
+    if (lane == 0) {
+      d.info[tc] = ci_make(bt, nt + 1, last);
+      d.bep[bt] = ep;
+      C->epoch = ep;
+    }
+  }
+  wave_sync();
+  // first positions between the two chunks shift by the moved entry
+  if (tc > cf) {
+    for (int c = cf + 1 + lane; c <= tc; c += 64) d.start[c] -= 1;
+  } else {
+    for (int c = tc + 1 + lane; c <= cf; c += 64) d.start[c] += 1;
+  }
+  wave_sync();
+  if (nf == 1) {  // the source chunk emptied: drop its directory entry, free its block
+    chk_dir_close(d, nch, cf);
+    if (lane == 0) {
+      const int nfr = C->nfree;
+      d.freel[nfr] = (uint16_t)bf;
+      C->nfree = nfr + 1;
+      C->nch = nch - 1;
+      C->removals += 1;
+    }
+    wave_sync();
+  }
+  return true;
+}
+
+// choosePivot's increasingHint (see wave_pivot_increasing) on the chunked order
+__device__ bool chk_pivot_increasing(const ChkDir& d, int nch, const ChkBlk* B, int n) {
+  const int lane = LANE;
+  const int t = lane / 3;
+  const int mid = (n / 4) * (t + 1);
+  int key = 0;
+  if (lane < 9) {
+    const int pos = mid + (lane % 3) - 1;
+    const int c = chk_find_lane(d, nch, pos);
+    key = B[ci_blk(d.info[c])].key[pos - d.start[c]];
+  }
+  const int prev = __shfl(key, lane > 0 ? lane - 1 : 0, 64);
+  const int midkey_prev = __shfl(key, lane >= 3 ? lane - 3 : 0, 64);
+  bool bad = false;
+  if (lane < 9 && (lane % 3) != 0 && key < prev) bad = true;
+  if (lane < 9 && (lane % 3) == 1 && lane >= 3 && key < midkey_prev) bad = true;
+  return __ballot(bad) == 0;
+}
+
+// sort.Slice(newNodeClaims) replay on the chunked order after one pending mutation (see sort_newnodeclaims): the same
+// decisions (stable move when pdqsort makes one, else the literal pdqsort over the materialised flat order, then a
+// rebuild). Returns the lowest sorted position whose NodeClaim changed or moved (-1: none); -3: the move does not fit
+// the directory (nothing changed; the caller continues on the flat order: chk_materialize, then the flat replay);
+// -4: the literal pdqsort ran and the rebuild did not fit (the flat order in order / npods is sorted, low = 0).
+__device__ int chk_sort(const ChkDir& d, ChkCtl LDS* C, ChkBlk* B, int n, int mut, int p, int32_t* order,
+                        int32_t* npods, uint64_t* slow) {
+  const int lane = LANE;
+  if (mut == 0) return -1;
+  const int nch = U(C->nch);
+  int mode = 0, cf = 0, sf = 0, K = 0;
+  int id = -1, key = INT32_MAX, cnt = 0;
+  if (mut == 1) {
+    cf = chk_find(d, nch, p);
+    sf = p - d.start[cf];
+    const uint32_t v = d.info[cf];
+    cnt = ci_cnt(v);
+    chk_load(B, ci_blk(v), cnt, id, key);
+    K = __builtin_amdgcn_readlane(key, sf);
+    if (K > CHK_KEY_MAX) return -3;
+    if (lane == 0) d.info[cf] = ci_make(ci_blk(v), cnt, __builtin_amdgcn_readlane(key, cnt - 1));  // the commit's +1
+    wave_sync();
+    int kn = INT32_MAX;
+    if (sf + 1 < cnt) kn = __builtin_amdgcn_readlane(key, sf + 1);
+    else if (cf + 1 < nch) kn = B[ci_blk(d.info[cf + 1])].key[0];
+    if (p + 1 < n && kn < K) mode = 1;
+  } else {
+    cf = nch - 1;
+    const uint32_t v = d.info[cf];
+    cnt = ci_cnt(v);
+    sf = cnt - 1;
+    chk_load(B, ci_blk(v), cnt, id, key);
+    K = __builtin_amdgcn_readlane(key, sf);
+    int kp = INT32_MIN;
+    if (sf >= 1) kp = __builtin_amdgcn_readlane(key, sf - 1);
+    else if (nch >= 2) {
+      const uint32_t w = d.info[nch - 2];
+      kp = B[ci_blk(w)].key[ci_cnt(w) - 1];
+    }
+    if (n >= 2 && K < kp) mode = 2;
+  }
+  if (!mode) return mut == 1 ? p : n - 1;
+  bool fast = n <= 12;
+  if (!fast && n >= 50) fast = chk_pivot_increasing(d, nch, B, n);
+  if (!fast) {  // the literal pdqsort over the flat order, then a rebuild
+    chk_materialize(d, C, B, order, npods);
+    slow_sort_wave((GlbI32)order, (GlbI32)npods, n);
+    if (lane == 0 && slow) slow[0] += 1;
+    return chk_build(d, C, B, order, npods, n) ? 0 : -4;
+  }
+  int cx = -1, sx = 0, low;
+  if (mode == 1) {  // q = first position > p with key >= K: within the chunk, else the first later chunk reaching K
+    const uint64_t bal = __ballot(lane > sf && lane < cnt && key >= K);
+    if (bal) {
+      cx = cf;
+      sx = __builtin_ctzll(bal);
+    } else {
+      const int c = wave_first_true(cf + 1, nch, [&](int c) { return ci_last(d.info[c]) >= K; });
+      if (c < nch) {
+        const uint32_t w = d.info[c];
+        const int kc = lane < ci_cnt(w) ? B[ci_blk(w)].key[lane] : INT32_MAX;
+        cx = c;
+        sx = __builtin_ctzll(__ballot(kc >= K));
+      }
+    }
+    low = p;
+  } else {  // q = first position in [0, n - 1) with key > K (the appended entry is the last)
+    const int c = wave_first_true(0, nch - 1, [&](int c) { return ci_last(d.info[c]) > K; });
+    if (c < nch - 1) {
+      const uint32_t w = d.info[c];
+      const int kc = lane < ci_cnt(w) ? B[ci_blk(w)].key[lane] : INT32_MIN;
+      cx = c;
+      sx = __builtin_ctzll(__ballot(kc > K));
+    } else {
+      cx = cf;
+      sx = __builtin_ctzll(__ballot(lane < sf && key > K));
+    }
+    low = d.start[cx] + sx;
+  }
+  if (!chk_move(d, C, B, cf, sf, cx, sx)) return -3;
+  return low;
+}
+
 // ---- solve_kernel's fast lane (wave 0), compiled as its own function ------------------------------------------
 // State shared with the kernel lives in LDS at file scope (one solve workgroup per CU); the kernel arguments are
 // read through the kernarg segment (scalar loads), so the lane's registers are allocated for this loop alone
@@ -1578,8 +2044,9 @@ __device__ __noinline__ uint64_t fl_full_add(uint64_t kargs, int sl_a, int cat_a
 }
 
 // Places popped pods while they need no requirement merge; returns the number placed. A pod it cannot place is
-// handed to the full path through g_ctl[6] / g_ctl[26]. Called by wave 0 only.
-template <bool TOPO>
+// handed to the full path through g_ctl[6] / g_ctl[26]. Called by wave 0 only. CHK: the order is chunked (the
+// directory in s_dyn, see chk_sort): the replay edits the blocks and the scan walks the live chunks, one per round.
+template <bool TOPO, bool CHK>
 __device__ __noinline__ int fast_lane(uint64_t kargs, int32_t LDS* s_dyn_arg, uint64_t pops_in_arg) {
   // a callee's arguments arrive in VGPRs and count as divergent: made provably uniform here, or every value and
   // branch that depends on them (the whole pod loop) would be compiled as divergent control flow
@@ -1623,7 +2090,7 @@ __device__ __noinline__ int fast_lane(uint64_t kargs, int32_t LDS* s_dyn_arg, ui
   int q_head = U(s_ctl[0]), q_len = U(s_ctl[1]), n_ev = U(s_ctl[4]), mut = U(s_ctl[10]), mut_p = U(s_ctl[11]);
   int stk_n = U(s_ctl[12]), stk_t = U(s_ctl[13]), stk_lost = U(s_ctl[20]);  // in-flight mutation stack
   const int n_nc_all = U(s_ctl[2]), epoch = U(s_ctl[3]);
-  const bool in_lds = U(s_ctl[5]) != 0;
+  const bool in_lds = U(s_ctl[5]) == 1;  // order mode: 1 LDS, 2 chunked, 0 flat global
   int qw_head = U(S->qw_head), qw_n = U(S->qw_n), qw_next = U(S->qw_next);
   int qw_pod = S->qw_pod[lane], qw_shape = S->qw_shape[lane], qw_sl = S->qw_sl[lane], qw_lastlen = S->qw_lastlen[lane],
       qw_epoch = S->qw_epoch[lane];
@@ -1791,23 +2258,41 @@ if (!FL_NOTIME && tmg) {                                    \
         A->cur_ex[2 * sl + 1] = a_cex_prev_stamp;
       }
       FT(1);
-      // sort.Slice(newNodeClaims) replay + first-fit start (sort arrays in LDS; spilled ones: the full path)
-      if (!in_lds) {
+      // sort.Slice(newNodeClaims) replay + first-fit start (sort arrays in LDS or chunked; the flat global order:
+      // the full path)
+      if (!CHK && !in_lds) {
         handoff = pod;
         fb = FB_SPILLED;
         break;
       }
       const LdsI32 ord = (LdsI32)s_dyn;
       const LdsI32 npods = (LdsI32)(s_dyn + A->sort_cap);
+      const ChkDir cd = chk_dir(s_dyn);
       const int c19 = min(cur, mstack_query_wave((LdsI32)s_stk[0], stk_n, stk_lost, stamp));
       const int n_nc = n_nc_all;
       FTF(8);
-      int low = mut == 0 ? -1 : (mut == 1 ? sort_mut1_window(ord, npods, n_nc, mut_p) : -2);
-      if (low == -2) low = sort_newnodeclaims_wave(ord, npods, n_nc, mut, mut_p, 256, &A->stats[31]);
-      if (low == -2) {  // a long shift: the full path sorts (the pending mutation is still in s_ctl[10..11])
-        handoff = pod;
-        fb = FB_SHIFT;
-        break;
+      int low;
+      if (CHK) {
+        low = mut == 0 ? -1 : chk_sort(cd, (ChkCtl LDS*)&g_chk, A->chk_blk, n_nc, mut, mut_p, A->g_order, A->g_npods,
+                                       &A->stats[31]);
+        if (low == -4) {  // the literal pdqsort ran and its rebuild did not fit: the flat order, the full path's
+          if (lane == 0) s_ctl[5] = 0;
+          mut = 0;
+          mstack_push_reg((int32_t LDS*)s_stk[0], stk_n, stk_lost, ++stk_t, 0);
+        }
+        if (low <= -3) {  // -3: nothing changed, the full path converts to the flat order and replays there
+          handoff = pod;
+          fb = FB_SHIFT;
+          break;
+        }
+      } else {
+        low = mut == 0 ? -1 : (mut == 1 ? sort_mut1_window(ord, npods, n_nc, mut_p) : -2);
+        if (low == -2) low = sort_newnodeclaims_wave(ord, npods, n_nc, mut, mut_p, 256, &A->stats[31]);
+        if (low == -2) {  // a long shift: the full path sorts (the pending mutation is still in s_ctl[10..11])
+          handoff = pod;
+          fb = FB_SHIFT;
+          break;
+        }
       }
       FTF(9);
       const int start = min(min(c19, low >= 0 ? low : INT32_MAX), n_nc);
@@ -1819,13 +2304,57 @@ if (!FL_NOTIME && tmg) {                                    \
       // is the full path's (512-lane pre-pass).
       int placed = -1, wpos = -1, why = FB_NONE, ipos = INT32_MAX;  // ipos: first count-independent pass (topology)
       bool b_staged = false;
-      bool bail = n_nc - start > FAST_SCAN_MAX;
+      bool bail = !CHK && n_nc - start > FAST_SCAN_MAX;
       if (bail) why = FB_SCAN;
       if (lane == 0 && !bail) starts += start;
-      for (int base = start; base < n_nc && placed == -1 && !bail; base += 64) {
-        const int i = base + lane;
-        bool cand = false, tag = false, icand = false;
-        const int nc = i < n_nc ? ord[i] : 0;
+      // chunked order: the start position's chunk and slot, the window of chunks whose live mask is in lm
+      int ch0 = 0, cs0 = 0, cc = 0, lm_base = 0, n_live = 0;
+      uint64_t lm = 0;
+      const bool can_dead = CHK && !t_n && sl < A->chk_dead_rows;
+      int32_t* const deadrow = A->chk_dead + (size_t)(can_dead ? sl : 0) * CHK_MAXC;
+      const int nch = CHK ? U(g_chk.nch) : 0;
+      if (CHK) {
+        ch0 = start < n_nc ? chk_find(cd, nch, start) : nch;
+        cs0 = ch0 < nch ? start - cd.start[ch0] : 0;
+        cc = ch0;
+      }
+      for (int base = start; placed == -1 && !bail;) {
+        int i, ck = -1, nscan;  // position of this lane's entry; its chunk; entries this round scans
+        bool valid;
+        int nc;
+        if (CHK) {
+          while (!lm && cc < nch) {  // the next window's live chunks (dead ones: every NodeClaim fails permanently)
+            bool live = false;
+            if (cc + lane < nch) {
+              const int b = ci_blk(cd.info[cc + lane]);
+              live = !(can_dead && deadrow[b] == cd.bep[b]);
+            }
+            lm = __ballot(live);
+            lm_base = cc;
+            cc = min(cc + 64, nch);
+          }
+          if (!lm) break;
+          if (++n_live > FAST_CHK_LIVE) {  // a long scan: the full path's (4 chunks per round)
+            bail = true;
+            why = FB_SCAN;
+            break;
+          }
+          ck = lm_base + __builtin_ctzll(lm);
+          lm &= lm - 1;
+          const uint32_t v = cd.info[ck];
+          valid = lane < ci_cnt(v) && !(ck == ch0 && lane < cs0);
+          nc = valid ? A->chk_blk[ci_blk(v)].id[lane] : 0;
+          i = cd.start[ck] + lane;
+          nscan = __popcll(__ballot(valid));
+        } else {
+          if (base >= n_nc) break;
+          i = base + lane;
+          valid = i < n_nc;
+          nc = valid ? ord[i] : 0;
+          nscan = min(64, n_nc - base);
+          base += 64;
+        }
+        bool cand = false, tag = false, icand = false, pfail = false;
         int32_t ver = 0;
         HeadView hv{0, 0, 0, 0, 0, 0};
         // speculative loads of the first position's NodeClaim (the usual winner), issued ahead of the pre-check
@@ -1843,7 +2372,7 @@ if (!FL_NOTIME && tmg) {                                    \
           rq0 = lane < KP_NRES ? A->nc_requests[(size_t)nc0 * KP_NRES + lane] : 0;
           j00 = lane < KP_NRES ? A->nc_fitj[(size_t)nc0 * KP_NRES + lane] : 0;
         }
-        if (i < n_nc) {
+        if (valid) {
           // every gather issued unconditionally: one round trip
           const int32_t fl = nc < A->ncc ? A->nc_fail[(size_t)sl * A->ncc + nc] : -2;
           if (nc == c_nc) hv = HeadView{c_r0, c_r1, c_r2, c_r3, c_ver, c_ts};
@@ -1860,6 +2389,7 @@ if (!FL_NOTIME && tmg) {                                    \
             }
           }
           cand = fit && fl != ver && fl != NC_NEVER && ((tolmask >> ts) & 1);
+          if (CHK) pfail = !fit || fl == NC_NEVER || !((tolmask >> ts) & 1);  // permanent (see the full path)
           bool pinned = true;  // every dictionary key the pod spreads over is one value on the NodeClaim
           if (TOPO && t_n) {
 #pragma unroll
@@ -1877,14 +2407,18 @@ if (!FL_NOTIME && tmg) {                                    \
           }
           tag = cand && (fl >= NC_MERGED || triv) && pinned;
         }
-        if (lane == 0) scanned += min(64, n_nc - base);
-        if (!FL_CNT32 && lane == 0) bytes += (uint64_t)min(64, n_nc - base) * (12 + 16 * A->n_req_res);
-        FL_CNT32_SCAN(min(64, n_nc - base));
+        if (lane == 0) scanned += nscan;
+        if (!FL_CNT32 && lane == 0) bytes += (uint64_t)nscan * (12 + 16 * A->n_req_res);
+        FL_CNT32_SCAN(nscan);
         uint64_t cm = __ballot(cand);
         const uint64_t tm = __ballot(tag);
         if (TOPO && t_n && ipos == INT32_MAX) {
           const uint64_t im = __ballot(icand);
-          if (im) ipos = base + __builtin_ctzll(im);
+          if (im) ipos = __builtin_amdgcn_readlane(i, __builtin_ctzll(im));
+        }
+        if (can_dead && !(ck == ch0 && cs0 > 0) && __ballot(valid && !pfail) == 0 && lane == 0) {
+          const int b = ci_blk(cd.info[ck]);  // every NodeClaim of the chunk fails the shape-level permanently
+          deadrow[b] = cd.bep[b];
         }
         // the next pod's prefetch was issued before these gathers, so it has landed: take it off the outstanding
         // list now rather than at the next pod's stage, where the wait would cover this pod's stores as well
@@ -1995,7 +2529,14 @@ if (!FL_NOTIME && tmg) {                                    \
             if (__ballot(lane < KP_NRES && fj != j0_lane)) {
               if (lane < KP_NRES) A->nc_fitj[(size_t)ncx * KP_NRES + lane] = fj;
             }
-            if (lane == 0) npods[ncx] += 1;
+            if (lane == 0) {
+              if (CHK) {  // len(Pods) in the chunk's block (the replay reads it there) and the flat copy
+                A->chk_blk[ci_blk(cd.info[ck])].key[l] += 1;
+                A->g_npods[ncx] += 1;
+              } else {
+                npods[ncx] += 1;
+              }
+            }
             if (lane == l) {  // the pre-check record, from this lane's copy: headroom minus the pod, version + 1
               int4* hp = reinterpret_cast<int4*>(A->nc_head + ncx);
               const int64_t n0 = hv.r0 - pr0, n1 = hv.r1 - pr1;
@@ -2007,7 +2548,7 @@ if (!FL_NOTIME && tmg) {                                    \
               A->nc_head[ncx].ver = verx + 1;
             }
             placed = ncx;
-            wpos = base + l;
+            wpos = __builtin_amdgcn_readlane(i, l);
             if (FT_FINE) fl_last = ncx;
             if (TOPO && triv && lane == 0 && ncx < A->ncc) A->nc_fail[(size_t)sl * A->ncc + ncx] = NC_MERGED;
             if (TOPO && rec_n) {
@@ -2227,7 +2768,8 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
     tlast = tnow;                                       \
   }
   if (timing) tlast = __builtin_amdgcn_s_memtime();
-  // control block (thread 0 owns): 0 head, 1 len, 2 n_nc, 3 lastLen epoch, 4 n_events, 5 sort arrays in LDS, 6 pod
+  // control block (thread 0 owns): 0 head, 1 len, 2 n_nc, 3 lastLen epoch, 4 n_events, 5 order mode (1 sort arrays in
+  // LDS, 2 chunked, 0 flat global), 6 pod
   if (tid == 0) {
     s_ctl[0] = 0;
     s_ctl[1] = a.n_pods;
@@ -2235,6 +2777,9 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
     s_ctl[3] = 1;
     s_ctl[4] = 0;
     s_ctl[5] = 1;
+    g_chk.nch = g_chk.nfree = g_chk.epoch = 0;
+    g_chk.maxc = min(a.chk_maxc, CHK_MAXC);
+    g_chk.nch_peak = g_chk.splits = g_chk.removals = g_chk.rebuilds = 0;
     s_ctl[10] = 0;  // pending mutation of newNodeClaims since the last sort: 0 none, 1 +1 at s_ctl[11], 2 appended
     s_ctl[11] = 0;
     s_ctl[12] = 0;  // in-flight mutation stack size / time / lost
@@ -2271,7 +2816,9 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
       if (fl_skip > 0) {
         fl_skip--;
       } else {
-        const int placed_fast = fast_lane<TOPO>((uint64_t)__builtin_amdgcn_kernarg_segment_ptr(), (int32_t LDS*)s_dyn, pops);
+        const uint64_t kargs = (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
+        const int placed_fast = s_ctl[5] == 2 ? fast_lane<TOPO, true>(kargs, (int32_t LDS*)s_dyn, pops)
+                                              : fast_lane<TOPO, false>(kargs, (int32_t LDS*)s_dyn, pops);
         pops += placed_fast;
         fl_fail = placed_fast ? 0 : fl_fail + 1;
         fl_skip = fl_fail >= 2 ? min(1 << min(fl_fail - 2, 6), 64) : 0;
@@ -2490,15 +3037,32 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
     }
     TS(1);
     if (placed == -1) {
-      const bool in_lds = s_ctl[5] != 0;
+      int cmode = s_ctl[5];  // 1 LDS, 2 chunked, 0 flat global
+      const ChkDir cd = chk_dir((int32_t LDS*)s_dyn);
       // ---- sort.Slice(newNodeClaims, len(Pods) asc) -----------------------------------------------
       // the cursor query (one lane of wave 1) overlaps the sort (thread 0); the pending mutation's own
       // clamp (s_ctl[16], known after the sort) is folded in below and pushed by thread 0 afterwards
       if (tid == 64) s_ctl[19] = min(s_ctl[22], mstack_query((LdsI32)s_stk[0], s_ctl[12], s_ctl[20], s_ctl[23]));
-      if (in_lds)
+      if (cmode == 1) {
         sort_newnodeclaims<NT>((LdsI32)s_dyn, (LdsI32)(s_dyn + a.sort_cap), s_ctl[2], s_ctl[10], s_ctl[11], s_ctl, &a.stats[31]);
-      else
+      } else if (cmode == 0) {
         sort_newnodeclaims<NT>((GlbI32)a.g_order, (GlbI32)a.g_npods, s_ctl[2], s_ctl[10], s_ctl[11], s_ctl, &a.stats[31]);
+      } else {  // chunked: one wave replays the move on the blocks and the directory
+        if (wave == 0) {
+          const int low = chk_sort(cd, (ChkCtl LDS*)&g_chk, a.chk_blk, s_ctl[2], s_ctl[10], s_ctl[11], a.g_order, a.g_npods, &a.stats[31]);
+          if (low == -3) chk_materialize(cd, (ChkCtl LDS*)&g_chk, a.chk_blk, a.g_order, a.g_npods);
+          if (lane == 0) {
+            s_ctl[18] = low;
+            s_ctl[16] = low == -4 ? 0 : low;
+            if (low <= -3) s_ctl[5] = 0;  // the directory is full: the flat order from here on
+          }
+        }
+        __syncthreads();
+        if (s_ctl[18] == -3)  // the pending mutation replays on the flat order
+          sort_newnodeclaims<NT>((GlbI32)a.g_order, (GlbI32)a.g_npods, s_ctl[2], s_ctl[10], s_ctl[11], s_ctl, &a.stats[31]);
+        cmode = s_ctl[5];
+      }
+      const bool in_lds = cmode == 1;
       const int n_nc = s_ctl[2];
       // a pod without requirements (at this level) merges into any NodeClaim without changing it: the append path
       // is exact on every candidate, tagged or not (NodeClaim.Add = Fits over the remaining types)
@@ -2512,20 +3076,94 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
       }
       TS(2);
       // ---- addToInflightNode: first NodeClaim in that order whose Add succeeds ------------------
-      for (int base = start; base < n_nc && placed == -1; base += 4 * NT) {
-        uint32_t flags = 0, iflags = 0, tflags = 0;
+      // chunked order: the scan walks the directory from the start position's chunk, skipping the chunks marked dead
+      // for this shape-level (see chk_build); 4 x NW live chunks per iteration, one per wave and round
+      __shared__ int32_t s_cw[2];
+      if (cmode == 2) {
+        if (wave == 0) {
+          const int nch = g_chk.nch;
+          const int c0 = start < n_nc ? chk_find(cd, nch, start) : nch;
+          if (lane == 0) {
+            s_cw[0] = c0;
+            s_cw[1] = c0 < nch ? start - cd.start[c0] : 0;
+          }
+        }
+        __syncthreads();
+      }
+      const int ch0 = cmode == 2 ? s_cw[0] : 0, cs0 = cmode == 2 ? s_cw[1] : 0;
+      const bool can_dead = cmode == 2 && !own_n && !a.res_mode && sl < a.chk_dead_rows;
+      int32_t* const deadrow = a.chk_dead + (size_t)(can_dead ? sl : 0) * CHK_MAXC;
+      // entry in s_list of a candidate: its position (LDS / flat order) or chunk << 6 | slot (chunked order)
+      auto ent_nc = [&](int e) -> int {
+        e = LIST_POS(e);
+        if (cmode == 1) return ((LdsI32)s_dyn)[e];
+        if (cmode == 0) return ((GlbI32)a.g_order)[e];
+        return a.chk_blk[ci_blk(cd.info[e >> 6])].id[e & 63];
+      };
+      auto ent_pos = [&](int e) -> int {
+        e = LIST_POS(e);
+        return cmode == 2 ? cd.start[e >> 6] + (e & 63) : e;
+      };
+      bool first_it = true;
+      for (int base = start, cc = ch0; placed == -1;) {
+        if (cmode == 2 ? cc >= g_chk.nch : base >= n_nc) break;
+        uint32_t flags = 0, iflags = 0, tflags = 0, pf = 0;
         // 4 rounds per thread: independent, so their loads overlap. A spilled order (thousands of NodeClaims, long
         // scans bound by the gathers' cache-line traffic) first filters on the headroom of the first two requested
         // resources (one 16-byte load per position) and gathers the memo and the rest of the record for survivors.
-        int ncs[4];
+        int ncs[4], pos[4], ent[4], tk[4];
         uint32_t room_ok = 0;
         int64_t r0s[4], r1s[4];
+        int n_scan;
+        if (cmode != 2) {
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-          const int i = base + k * NT + tid;
-          ncs[k] = i >= n_nc ? -1 : in_lds ? ((LdsI32)s_dyn)[i] : ((GlbI32)a.g_order)[i];
+          for (int k = 0; k < 4; k++) {
+            const int i = base + k * NT + tid;
+            ncs[k] = i >= n_nc ? -1 : in_lds ? ((LdsI32)s_dyn)[i] : ((GlbI32)a.g_order)[i];
+            pos[k] = ent[k] = i;
+            tk[k] = -1;
+          }
+          n_scan = min(4 * NT, n_nc - base);
+          base += 4 * NT;
+        } else {
+          // live chunks of the window [cc, cc + 64), in order (every wave computes the same mask); round k of wave w
+          // takes the (k * NW + w)-th
+          const int nch = g_chk.nch;
+          bool live = false;
+          if (cc + lane < nch) {
+            const int b = ci_blk(cd.info[cc + lane]);
+            live = !(can_dead && deadrow[b] == cd.bep[b]);
+          }
+          uint64_t lm = __ballot(live);
+          int nxt = min(cc + 64, nch);
+          n_scan = 0;
+#pragma unroll
+          for (int k = 0; k < 4; k++) tk[k] = -1;
+          for (int j = 0; j < 4 * NW && lm; j++) {
+            const int c = cc + __builtin_ctzll(lm);
+            lm &= lm - 1;
+            const int cnt = ci_cnt(cd.info[c]);
+            n_scan += c == ch0 ? cnt - cs0 : cnt;
+            if (j % NW == wave) tk[j / NW] = c;
+            if (j == 4 * NW - 1 && lm) nxt = c + 1;
+          }
+          cc = nxt;
+          if (n_scan == 0) continue;  // only dead chunks in this window
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            ncs[k] = -1;
+            pos[k] = ent[k] = 0;
+            const int c = tk[k];
+            if (c < 0) continue;
+            const uint32_t v = cd.info[c];
+            if (lane < ci_cnt(v) && !(c == ch0 && lane < cs0)) {
+              ncs[k] = a.chk_blk[ci_blk(v)].id[lane];
+              pos[k] = cd.start[c] + lane;
+              ent[k] = (c << 6) | lane;
+            }
+          }
         }
-        if (!in_lds) {
+        if (cmode == 0) {
 #pragma unroll
           for (int k = 0; k < 4; k++) {
             r0s[k] = r1s[k] = 0;
@@ -2540,15 +3178,17 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
         }
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-          const int i = base + k * NT + tid;
-          if (i >= n_nc || (!in_lds && !((room_ok >> k) & 1))) continue;
+          if (ncs[k] < 0 || (cmode == 0 && !((room_ok >> k) & 1))) continue;
           const int nc = ncs[k];
           // every gather is issued unconditionally so they overlap (one round trip instead of a chain)
           const int32_t fl = nc < a.ncc ? a.nc_fail[(size_t)sl * a.ncc + nc] : -2;
           const HeadView hv = load_head(a.nc_head + nc, four);
-          bool cand = hv.r0 >= p0 && hv.r1 >= p1 && hv.r2 >= p2 && hv.r3 >= p3;
-          cand = cand && fl != hv.ver && fl != NC_NEVER && ((tolmask >> hv.ts) & 1);
-          if (hpc) cand = cand && !(a.nc_hp[nc] & hpc);
+          const bool fit = hv.r0 >= p0 && hv.r1 >= p1 && hv.r2 >= p2 && hv.r3 >= p3;
+          const bool tol = (tolmask >> hv.ts) & 1;
+          const bool hpx = hpc && (a.nc_hp[nc] & hpc);
+          // a permanent failure: headroom, taints and used host ports only get worse, NEVER stays (chunk dead marks)
+          if (!fit || !tol || hpx || fl == NC_NEVER) pf |= 1u << k;
+          bool cand = fit && tol && !hpx && fl != hv.ver && fl != NC_NEVER;
           if (rr_b4 && cand) {
             const int64_t* rq = a.nc_requests + (size_t)nc * KP_NRES;
             const int64_t* mx = a.nc_maxalloc + (size_t)nc * KP_NRES;
@@ -2578,14 +3218,26 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
           if (cand && (fl >= NC_MERGED || triv) && !a.res_mode && (!own_n || pinned)) tflags |= 1u << k;
           flags |= (cand ? 1u : 0u) << k;
         }
-        if (own_n) first_pos_min<NT>(iflags, base + tid, &s_ctl[25]);
-        if (tid == 0) {
-          scanned += min(4 * NT, n_nc - base);
-          if (base == start) starts += start;
+        if (own_n) first_pos_min_e(iflags, pos, &s_ctl[25]);
+        if (can_dead) {  // a chunk scanned in full whose NodeClaims all failed permanently: dead for this shape-level
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            const int c = tk[k];
+            if (c < 0 || (c == ch0 && cs0 > 0)) continue;
+            if (__ballot(ncs[k] >= 0 && !((pf >> k) & 1)) == 0 && lane == 0) {
+              const int b = ci_blk(cd.info[c]);
+              deadrow[b] = cd.bep[b];
+            }
+          }
         }
-        const int n = compact_candidates_x4<NW>(flags, base + tid, s_list, s_wcnt, tflags);
+        if (tid == 0) {
+          scanned += n_scan;
+          if (first_it) starts += start;
+        }
+        first_it = false;
+        const int n = compact_candidates_x4e<NW>(flags, ent, s_list, s_wcnt, tflags);
         TS(6);
-        if (wave == 0) bytes += (uint64_t)min(4 * NT, n_nc - base) * (12 + 16 * a.n_req_res);  // counted once
+        if (wave == 0) bytes += (uint64_t)n_scan * (12 + 16 * a.n_req_res);  // counted once
         // a round whose first candidate takes the append path evaluates it alone (it is the likely winner and
         // costs a fraction of a full attempt, which the other waves would make the round wait for)
         for (int r0 = 0, width = NW; r0 < n; r0 += width) {
@@ -2596,7 +3248,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
           ReqView rv;
           int nc = -1;
           if (wave < width && li < n) {
-            nc = in_lds ? ((LdsI32)s_dyn)[LIST_POS(s_list[li])] : ((GlbI32)a.g_order)[LIST_POS(s_list[li])];
+            nc = ent_nc(s_list[li]);
             attempts++;
             uint64_t* tsub = (a.timing && wave == 0) ? s_tsub : nullptr;
             const uint64_t tm0 = tsub ? __builtin_amdgcn_s_memtime() : 0;
@@ -2654,8 +3306,15 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
               if (lane < KP_NRES) a.nc_requests[(size_t)nc * KP_NRES + lane] += s_preq[lane];
               if (lane == 0 && hpa) a.nc_hp[nc] |= hpa;
               if (lane == 0) {
-                if (in_lds) ((LdsI32)(s_dyn + a.sort_cap))[nc] += 1;
-                else ((GlbI32)a.g_npods)[nc] += 1;
+                if (in_lds) {
+                  ((LdsI32)(s_dyn + a.sort_cap))[nc] += 1;
+                } else {
+                  ((GlbI32)a.g_npods)[nc] += 1;
+                  if (cmode == 2) {  // len(Pods) in the NodeClaim's block as well (the sort replay reads it there)
+                    const int e = LIST_POS(s_list[li]);
+                    a.chk_blk[ci_blk(cd.info[e >> 6])].key[e & 63] += 1;
+                  }
+                }
                 NcHead* h = a.nc_head + nc;
                 h->ver += 1;
                 h->room[0] -= p0;
@@ -2669,8 +3328,8 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
                 if (lane == 0) a.nc_held[nc] = nh;
               }
             }
-            const int wpos = LIST_POS(s_list[r0 + win]);
-            placed = in_lds ? ((LdsI32)s_dyn)[wpos] : ((GlbI32)a.g_order)[wpos];
+            const int wpos = ent_pos(s_list[r0 + win]);
+            placed = ent_nc(s_list[r0 + win]);
             if (tid == 0) {
               s_ctl[10] = 1;
               s_ctl[11] = wpos;
@@ -2765,7 +3424,8 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
           __syncthreads();
           const int win = first_ok<NW>(s_ok);
           const int nc = s_ctl[2];
-          const bool in_lds = s_ctl[5] != 0;
+          const int cmode = s_ctl[5];
+          const bool in_lds = cmode == 1;
           if (win >= 0) {
             if (wave == win) {
               store_merged(reinterpret_cast<KReqs*>(a.nc_reqs + (size_t)nc * sizeof(KReqs)), rv, m_v, D.W, D.KB);
@@ -2812,21 +3472,43 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
           }
           __syncthreads();
           if (win >= 0) {
-            // append to newNodeClaims (spill the sort arrays to global memory past a.sort_cap)
-            if (in_lds && nc == a.sort_cap) {
+            // append to newNodeClaims: past a.sort_cap the sort arrays leave LDS for the chunked order (or, when its
+            // directory cannot hold them, the flat global arrays)
+            const bool spill = in_lds && nc == a.sort_cap;
+            if (spill) {
               for (int i = tid; i < nc; i += NT) {
                 a.g_order[i] = s_dyn[i];
                 a.g_npods[i] = s_dyn[a.sort_cap + i];
               }
             }
             __syncthreads();
-            if (tid == 0) {
-              const bool lds_now = in_lds && nc < a.sort_cap;
+            const ChkDir cd = chk_dir((int32_t LDS*)s_dyn);
+            if (spill && wave == 0) {
+              const bool ok = chk_build(cd, (ChkCtl LDS*)&g_chk, a.chk_blk, a.g_order, a.g_npods, nc);
+              if (lane == 0) s_ctl[5] = ok ? 2 : 0;
+            }
+            __syncthreads();
+            if (s_ctl[5] == 2) {
+              if (wave == 0) {
+                if (lane == 0) a.g_npods[nc] = 1;
+                if (!chk_append(cd, (ChkCtl LDS*)&g_chk, a.chk_blk, nc, 1)) {  // the directory is full: the flat order
+                  chk_materialize(cd, (ChkCtl LDS*)&g_chk, a.chk_blk, a.g_order, a.g_npods);
+                  if (lane == 0) {
+                    a.g_order[nc] = nc;
+                    s_ctl[5] = 0;
+                  }
+                }
+                if (lane == 0) {
+                  s_ctl[2] = nc + 1;
+                  s_ctl[10] = 2;
+                }
+              }
+            } else if (tid == 0) {
+              const bool lds_now = s_ctl[5] == 1;
               int32_t* ord = lds_now ? s_dyn : a.g_order;
               int32_t* npods = lds_now ? s_dyn + a.sort_cap : a.g_npods;
               ord[nc] = nc;
               npods[nc] = 1;
-              s_ctl[5] = lds_now ? 1 : 0;
               s_ctl[2] = nc + 1;
               s_ctl[10] = 2;
             }
@@ -2957,8 +3639,14 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
       for (int i = 0; i < 8; i++) a.stats[16 + i] = g_fast.fcyc[6 + i];
     if (SORT_DIAG || EX_DIAG)
       for (int i = 0; i < 6; i++) a.stats[25 + i] = g_sdiag[i];
+    // chunked order: peak chunks, splits, emptied chunks, (re)builds; final order mode
+    a.stats[41] = g_chk.nch_peak;
+    a.stats[42] = g_chk.splits;
+    a.stats[43] = g_chk.removals;
+    a.stats[44] = g_chk.rebuilds;
+    a.stats[45] = s_ctl[5];
   }
-  if (s_ctl[5])
+  if (s_ctl[5] == 1)
     for (int i = tid; i < s_ctl[2]; i += NT) {
       a.g_npods[i] = s_dyn[a.sort_cap + i];
       a.g_order[i] = s_dyn[i];

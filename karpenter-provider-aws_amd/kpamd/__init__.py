@@ -228,6 +228,7 @@ def stats_dict(st):
     d["attempt_cycles"] = list(st.attempt_cycles)
     d["fast_cycles"] = list(st.fast_cycles)
     d["fast_bails"] = list(st.fast_bails)
+    d["order_chunks"] = list(st.order_chunks)
     return d
 
 

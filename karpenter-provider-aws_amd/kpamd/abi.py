@@ -174,7 +174,8 @@ class SolveIn(C.Structure):
                 ("shapes", C.POINTER(PodShape)), ("pods", C.POINTER(Pod)), ("n_pods", C.c_uint32),
                 ("max_instance_types", C.c_uint32), ("bound_pods", C.POINTER(BoundPod)),
                 ("n_bound_pods", C.c_uint32), ("n_namespaces", C.c_uint32), ("namespaces", C.POINTER(Namespace)),
-                ("reserved_offering_mode", C.c_uint32), ("reserved2_", C.c_uint32)]
+                ("reserved_offering_mode", C.c_uint32), ("reserved2_", C.c_uint32),
+                ("pod_uids", C.POINTER(C.c_char_p))]
 
 
 class NodeClaimInfo(C.Structure):
@@ -190,7 +191,8 @@ class SolveStats(C.Structure):
                 ("scanned", C.c_uint64), ("cursor_starts", C.c_uint64), ("attempt_cycles", C.c_uint64 * 8),
                 ("catalog_ms", C.c_double), ("catalog_cached", C.c_uint32), ("catalog_refreshed", C.c_uint32),
                 ("fast_pods", C.c_uint64), ("fast_cycles", C.c_uint64 * 6), ("slow_sorts", C.c_uint64),
-                ("fast_bails", C.c_uint64 * 8), ("reserved_offering_errors", C.c_uint64)]
+                ("fast_bails", C.c_uint64 * 8), ("reserved_offering_errors", C.c_uint64),
+                ("order_chunks", C.c_uint64 * 5)]
 
 
 class Options(C.Structure):
@@ -206,7 +208,7 @@ class EC2Info(C.Structure):
                 ("gpu_memory_mib", C.c_int64), ("accel_name", C.c_char_p), ("accel_manufacturer", C.c_char_p),
                 ("accel_count", C.c_int32), ("neuron_devices", C.c_int32), ("neuron_cores_per_device", C.c_int32),
                 ("efa", C.c_int32), ("max_enis", C.c_int32), ("ipv4_per_eni", C.c_int32), ("trunking", C.c_int32),
-                ("branch_enis", C.c_int32), ("in_limits_table", C.c_int32), ("reserved2_", C.c_int32)]
+                ("branch_enis", C.c_int32), ("in_limits_table", C.c_int32), ("instance_storage_gb", C.c_int32)]
 
 
 class EvictionValue(C.Structure):
@@ -220,10 +222,20 @@ class Kubelet(C.Structure):
                 ("soft_memory_available", EvictionValue), ("soft_nodefs_available", EvictionValue)]
 
 
+class BlockDeviceMapping(C.Structure):
+    _fields_ = [("device_name", C.c_char_p), ("volume_size", C.c_int64), ("root_volume", C.c_int32),
+                ("reserved_", C.c_int32)]
+
+
 class NodeClass(C.Structure):
     _fields_ = [("region", C.c_char_p), ("zones", C.POINTER(C.c_char_p)), ("zone_ids", C.POINTER(C.c_char_p)),
                 ("n_zones", C.c_uint32), ("max_pods", C.c_int32), ("pods_per_core", C.c_int32),
-                ("ami_family", C.c_int32), ("kubelet", C.POINTER(Kubelet))]
+                ("ami_family", C.c_int32), ("kubelet", C.POINTER(Kubelet)),
+                ("block_device_mappings", C.POINTER(BlockDeviceMapping)), ("n_block_device_mappings", C.c_uint32),
+                ("instance_store_policy", C.c_int32)]
+
+
+INSTANCE_STORE_POLICIES = {None: 0, "RAID0": 1}
 
 
 AMI_FAMILIES = {"AL2023": 0, "AL2": 1, "Bottlerocket": 2, "Windows2019": 3, "Windows2022": 4, "Custom": 5}
@@ -241,7 +253,8 @@ class Cluster(C.Structure):
                 ("nodes", C.POINTER(ClusterNode)), ("n_nodes", C.c_uint32), ("n_shapes", C.c_uint32),
                 ("shapes", C.POINTER(PodShape)), ("pods", C.POINTER(Pod)), ("n_pods", C.c_uint32),
                 ("spot_to_spot", C.c_uint32), ("pending_pods", C.POINTER(C.c_uint32)), ("n_pending", C.c_uint32),
-                ("n_namespaces", C.c_uint32), ("namespaces", C.POINTER(Namespace))]
+                ("n_namespaces", C.c_uint32), ("namespaces", C.POINTER(Namespace)),
+                ("pod_uids", C.POINTER(C.c_char_p))]
 
 
 class SimResult(C.Structure):
@@ -319,6 +332,12 @@ class Arena:
             a[i] = it
         self.keep.append(a)
         return a
+
+    def uids(self, uids):
+        """[metadata.uid] -> const char*[] (None: the batch passes no UIDs)"""
+        if uids is None:
+            return None
+        return self.arr(C.c_char_p, [self.s(u) for u in uids])
 
     def resources(self, d):
         r = ResourceList()
@@ -470,7 +489,8 @@ def build_solve_in(arena, problem, catalog_handles=None):
     nsa, nns = arena.namespaces(getattr(problem, "namespaces", None))
     si = SolveIn(handles, descs, len(problem.catalogs), len(problem.nodepools), nps, ex, len(problem.existing),
                  len(problem.shapes), shapes, pods_ptr, len(problem.pod_shape), problem.max_instance_types,
-                 bps, nbp, nns, nsa if nns else None, getattr(problem, "reserved_offering_mode", 0), 0)
+                 bps, nbp, nns, nsa if nns else None, getattr(problem, "reserved_offering_mode", 0), 0,
+                 arena.uids(getattr(problem, "pod_uid_str", None)))
     arena.keep.append(si)
     return si
 
@@ -504,7 +524,8 @@ def build_cluster(arena, cl, catalog_handles=None):
     c = Cluster(handles, descs, len(cl.catalogs), len(cl.nodepools), nps, nodes_a, len(cl.nodes), len(cl.shapes),
                 shapes, _pods_array(arena, cl.pod_shape, cl.pod_creation, cl.pod_uid), len(cl.pod_shape),
                 1 if cl.spot_to_spot else 0,
-                arena.arr(C.c_uint32, pending) if pending else None, len(pending), nns, nsa if nns else None)
+                arena.arr(C.c_uint32, pending) if pending else None, len(pending), nns, nsa if nns else None,
+                arena.uids(getattr(cl, "pod_uid_str", None)))
     arena.keep.append(c)
     return c
 

@@ -231,11 +231,18 @@ def kubelet(arena, kube_reserved=None, system_reserved=None, eviction_hard=None,
 
 
 def nodeclass(arena, zones=ZONES, zone_ids=ZONE_IDS, max_pods=None, pods_per_core=None, kubelet_cfg=None,
-              ami_family="AL2023"):
+              ami_family="AL2023", block_device_mappings=None, instance_store_policy=None):
     """kp_nodeclass; kubelet_cfg: dict of kubelet(...) keyword arguments, or None for no kubelet block; ami_family:
-    a key of abi.AMI_FAMILIES (EC2NodeClass.AMIFamily())."""
+    a key of abi.AMI_FAMILIES (EC2NodeClass.AMIFamily()); block_device_mappings: [(deviceName or None, volumeSize bytes
+    or None, rootVolume)] (spec.blockDeviceMappings); instance_store_policy: None or "RAID0"."""
     nc = abi.NodeClass()
     nc.ami_family = abi.AMI_FAMILIES[ami_family]
+    bdms = list(block_device_mappings or [])
+    if bdms:
+        nc.block_device_mappings = arena.arr(abi.BlockDeviceMapping, [
+            abi.BlockDeviceMapping(arena.s(d), -1 if sz is None else int(sz), 1 if root else 0, 0) for d, sz, root in bdms])
+    nc.n_block_device_mappings = len(bdms)
+    nc.instance_store_policy = abi.INSTANCE_STORE_POLICIES[instance_store_policy]
     if kubelet_cfg is not None:
         nc.kubelet = C.pointer(kubelet(arena, **kubelet_cfg))
     nc.region = arena.s(REGION)
@@ -286,13 +293,15 @@ def spot_price_table(rows, zones=ZONES, seed=SPOT_SEED):
 
 
 def build_catalog(lib, rows=None, opts=None, max_pods=None, pods_per_core=None, zones=ZONES, zone_ids=ZONE_IDS,
-                  unavailable=frozenset(), kubelet_cfg=None, capacity_reservations=(), ami_family="AL2023"):
+                  unavailable=frozenset(), kubelet_cfg=None, capacity_reservations=(), ami_family="AL2023",
+                  block_device_mappings=None, instance_store_policy=None):
     """GetInstanceTypes for one EC2NodeClass: NewInstanceType for every row, then InjectOfferings
     (capacity_reservations: the NodeClass's reservations, ReservedCapacity feature gate on)."""
     rows = load_ec2_table() if rows is None else rows
     arena = abi.Arena()
     opts = opts or default_options()
-    nc = nodeclass(arena, zones, zone_ids, max_pods, pods_per_core, kubelet_cfg, ami_family)
+    nc = nodeclass(arena, zones, zone_ids, max_pods, pods_per_core, kubelet_cfg, ami_family, block_device_mappings,
+                   instance_store_policy)
     spot = spot_price_table(rows, zones)
     out = []
     for r in rows:

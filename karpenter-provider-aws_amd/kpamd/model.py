@@ -142,6 +142,7 @@ class Cluster:
     pending: List[int] = field(default_factory=list)  # provisionable pods bound to no node (indices into pod_*)
     spot_to_spot: bool = False                         # SpotToSpotConsolidation feature gate
     namespaces: Dict[str, Dict[str, str]] = field(default_factory=dict)  # cluster namespaces: name -> labels
+    pod_uid_str: Optional[List[str]] = None  # metadata.uid per pod (kp_cluster.pod_uids): the exact Queue tie-break
 
 
 @dataclass
@@ -158,6 +159,7 @@ class Problem:
     bound_pods: List[Tuple[str, Dict[str, str], int]] = field(default_factory=list)  # (namespace, labels, existing idx)
     namespaces: Dict[str, Dict[str, str]] = field(default_factory=dict)  # cluster namespaces: name -> labels
     reserved_offering_mode: int = 0  # 0 fallback (scheduler default), 1 strict (provisioner: DisableReservedCapacityFallback)
+    pod_uid_str: Optional[List[str]] = None  # metadata.uid per pod (kp_solve_in.pod_uids): NewQueue's exact UID tie-break
 
     @property
     def n_pods(self):

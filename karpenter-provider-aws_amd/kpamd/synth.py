@@ -93,13 +93,15 @@ def config2(catalog, n_pods=50_000, seed=2, n_shapes=256, burst=False):
     return Problem([catalog], pools, shapes, s, c, u, name=f"config2-{n_pods}")
 
 
-def config5(catalog, n_pods=1_000_000, seed=5, n_shapes=512):
-    """1M-pod burst over 20 weighted NodePools with cpu limits; 4 NVIDIA-GPU pools, 2 Neuron pools (tainted)."""
+def config5(catalog, n_pods=1_000_000, seed=5, n_shapes=512, limit_div=1):
+    """1M-pod burst over 20 weighted NodePools with cpu limits; 4 NVIDIA-GPU pools, 2 Neuron pools (tainted).
+    limit_div > 1 divides every pool's cpu limit: the regime where the limits bind (38.7 % of 1M pods unschedulable)
+    at a tenth of the pods (limit_div=10, 100k pods: 38.9 %)."""
     rng = np.random.default_rng(seed)
     pools = []
     for w in range(1, 21):
         name = f"pool-{w:02d}"
-        limits = {"cpu": int(rng.integers(20_000, 200_000)) * 1000}  # ~2.2M cores in all: the burst spills by weight
+        limits = {"cpu": int(rng.integers(20_000, 200_000)) * 1000 // limit_div}  # ~2.2M cores: the burst spills by weight
         if w <= 4:
             pools.append(NodePool(name, w, 0, [(K + "instance-gpu-manufacturer", "In", ["nvidia"])],
                                   taints=[("nvidia.com/gpu", "true", "NoSchedule")], limits=limits))

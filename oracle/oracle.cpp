@@ -806,6 +806,7 @@ struct PodState {
   int64_t cpu, mem;  // sort keys
   int64_t creation;
   uint64_t uid;
+  string uid_str;  // metadata.uid when the batch passes it (kp_solve_in.pod_uids): compared as a string
   // relaxable spec (Preferences.Relax mutates the pod)
   vector<Requirements> required_terms;
   vector<std::pair<int, Requirements>> preferred;  // (weight, preference)
@@ -1662,6 +1663,10 @@ static int32_t SolveCore(const Catalogs& cats, const kp_solve_in* in, kpo_result
     ps.shape = (int)p.shape;
     ps.creation = p.creation_unix;
     ps.uid = p.uid_key;
+    if (in->pod_uids) {
+      if (!in->pod_uids[i]) return KP_E_INVAL;
+      ps.uid_str = in->pod_uids[i];
+    }
     ps.requests = FromABI(sh.requests);
     ps.cpu = Get(ps.requests, KP_RES_CPU);
     ps.mem = Get(ps.requests, KP_RES_MEMORY);
@@ -1736,6 +1741,7 @@ static int32_t SolveCore(const Catalogs& cats, const kp_solve_in* in, kpo_result
     if (l.cpu != r.cpu) return l.cpu > r.cpu;
     if (l.mem != r.mem) return l.mem > r.mem;
     if (l.creation != r.creation) return l.creation < r.creation;
+    if (in->pod_uids) return l.uid_str < r.uid_str;  // (UIDs are unique in a cluster)
     return l.uid < r.uid;
   });
   std::vector<int> queue(q.begin(), q.end());
@@ -1896,21 +1902,18 @@ int32_t kpo_simulate_batch(const kp_cluster* cl, const uint32_t* offsets, const 
       }
     std::vector<kp_pod> pods;
     std::vector<int> kind;
-    for (uint32_t j = 0; j < cl->n_pending; j++) {
-      pods.push_back(cl->pods[cl->pending_pods[j]]);
-      kind.push_back(2);
-    }
+    std::vector<const char*> uids;
+    auto add = [&](uint32_t p, int k) {
+      pods.push_back(cl->pods[p]);
+      kind.push_back(k);
+      if (cl->pod_uids) uids.push_back(cl->pod_uids[p]);
+    };
+    for (uint32_t j = 0; j < cl->n_pending; j++) add(cl->pending_pods[j], 2);
     for (uint32_t i = 0; i < cl->n_nodes; i++)
       if (cl->nodes[i].deleting)
-        for (uint32_t j = 0; j < cl->nodes[i].n_pods; j++) {
-          pods.push_back(cl->pods[cl->nodes[i].pods[j]]);
-          kind.push_back(1);
-        }
+        for (uint32_t j = 0; j < cl->nodes[i].n_pods; j++) add(cl->nodes[i].pods[j], 1);
     for (uint32_t c : cand)
-      for (uint32_t j = 0; j < cl->nodes[c].n_pods; j++) {
-        pods.push_back(cl->pods[cl->nodes[c].pods[j]]);
-        kind.push_back(0);
-      }
+      for (uint32_t j = 0; j < cl->nodes[c].n_pods; j++) add(cl->nodes[c].pods[j], 0);
     for (uint32_t c : cand) inS[c] = 0;
     // Topology.countDomains lists every pod bound to a node except the pods being scheduled: the pods of the
     // remaining nodes are the bound pods (their shape's namespace and labels)
@@ -1941,6 +1944,7 @@ int32_t kpo_simulate_batch(const kp_cluster* cl, const uint32_t* offsets, const 
     in.n_bound_pods = (uint32_t)bound.size();
     in.namespaces = cl->namespaces;
     in.n_namespaces = cl->n_namespaces;
+    in.pod_uids = cl->pod_uids ? uids.data() : nullptr;
     kpo_result* res = nullptr;
     int32_t rc = SolveCore(cats, &in, &res);
     if (rc) return rc;
@@ -2515,6 +2519,65 @@ typedef struct kpo_overhead {
   kp_resource_list kube_reserved, system_reserved, eviction_threshold;
 } kpo_overhead;
 
+// ephemeralStorage(info, amiFamily, blockDeviceMappings, instanceStorePolicy) (R:types.go:349-385), in bytes, following
+// its control flow: RAID0 with InstanceStorageInfo.TotalSizeInGB -> "%dG"; BDMs: lo.Find(RootVolume) with a volumeSize;
+// Custom: the last BDM's volumeSize or DefaultEBS; other families: lo.Find(deviceName == EphemeralBlockDevice()) with a
+// volumeSize; then lo.Find(DefaultBlockDeviceMappings(), EphemeralBlockDevice()) -> its volumeSize; DefaultEBS.
+struct BDM {
+  std::string device;  // "" = nil
+  bool has_device;
+  bool root;
+  bool has_size;
+  int64_t size;
+};
+static int64_t EphemeralStorageBytes(const kp_ec2_info* info, const kp_nodeclass* nc) {
+  const int64_t DefaultEBSVolumeSize = 20ll * 1073741824ll;  // R:pkg/providers/amifamily/resolver.go DefaultEBS
+  const int fam = nc ? nc->ami_family : KP_AMI_AL2023;
+  if (nc && nc->instance_store_policy == KP_INSTANCE_STORE_RAID0) {
+    int64_t totalGB = info->instance_storage_gb ? info->instance_storage_gb : info->local_nvme_gb;
+    if (totalGB > 0) return totalGB * 1000 * 1000 * 1000;
+  }
+  std::vector<BDM> bdms;
+  for (uint32_t i = 0; nc && nc->block_device_mappings && i < nc->n_block_device_mappings; i++) {
+    const kp_block_device_mapping& b = nc->block_device_mappings[i];
+    bdms.push_back({b.device_name ? b.device_name : "", b.device_name != nullptr, b.root_volume != 0, b.volume_size >= 0,
+                    b.volume_size});
+  }
+  // EphemeralBlockDevice() and DefaultBlockDeviceMappings() per family (nil device: Custom)
+  std::string ephDevice;
+  bool hasEphDevice = true;
+  std::vector<BDM> defaults;
+  switch (fam) {
+    case KP_AMI_BOTTLEROCKET:
+      ephDevice = "/dev/xvdb";
+      defaults = {{"/dev/xvda", true, false, true, 4ll * 1073741824ll}, {"/dev/xvdb", true, false, true, DefaultEBSVolumeSize}};
+      break;
+    case KP_AMI_WINDOWS2019:
+    case KP_AMI_WINDOWS2022:
+      ephDevice = "/dev/sda1";
+      defaults = {{"/dev/sda1", true, false, true, 50ll * 1073741824ll}};
+      break;
+    case KP_AMI_CUSTOM:
+      hasEphDevice = false;
+      break;
+    default:
+      ephDevice = "/dev/xvda";
+      defaults = {{"/dev/xvda", true, false, true, DefaultEBSVolumeSize}};
+  }
+  if (!bdms.empty()) {
+    auto root = std::find_if(bdms.begin(), bdms.end(), [](const BDM& b) { return b.root; });
+    if (root != bdms.end() && root->has_size) return root->size;
+    if (!hasEphDevice) return bdms.back().has_size ? bdms.back().size : DefaultEBSVolumeSize;
+    auto dev = std::find_if(bdms.begin(), bdms.end(), [&](const BDM& b) { return b.has_device && b.device == ephDevice; });
+    if (dev != bdms.end() && dev->has_size) return dev->size;
+  }
+  if (hasEphDevice) {
+    auto def = std::find_if(defaults.begin(), defaults.end(), [&](const BDM& b) { return b.device == ephDevice; });
+    if (def != defaults.end()) return def->size;
+  }
+  return DefaultEBSVolumeSize;
+}
+
 static int64_t Mi(int64_t x) { return x * 1048576ll * 1000ll; }
 
 static int64_t ENILimitedPods(const kp_ec2_info* info, int reservedENIs) {
@@ -2534,8 +2597,7 @@ int32_t kpo_instance_type_resolve(const kp_options* opts, const kp_ec2_info* inf
   int64_t ovMiB = (int64_t)std::ceil(bytes * opts->vm_memory_overhead_percent / 1024 / 1024);
   cap[KP_RES_MEMORY] = Mi(mib - ovMiB);
   const AMIFamilyFlags fam = FamilyOf(nc);
-  // ephemeralStorage(): no BDMs -> the family's default ephemeral volume
-  int64_t storageBytes = fam.EphemeralGi * 1073741824ll;
+  int64_t storageBytes = EphemeralStorageBytes(info, nc);
   cap[KP_RES_EPHEMERAL_STORAGE] = storageBytes * 1000;
   // pods(): maxPods, else ENI-limited (SupportsENILimitedPodDensity), else 110; then podsPerCore (PodsPerCoreEnabled)
   int64_t pods;

@@ -6,6 +6,11 @@
   config3-100000  Solve of config 3 at 100k pods (zone + hostname spread onto 5k existing nodes): same digests
   config5-100000  Solve of config 5 (20 weighted pools, GPU/Neuron pools) at 100k pods: 17.5k NodeClaims, so the
                   device's newNodeClaims order spills past its 8,192-entry LDS capacity on its own
+  config5-limits-100000  config 5 at 100k pods with every pool's cpu limit divided by 10: the regime the 1M-pod burst
+                  ends in (NodePool limits bind: subtractMax across 20 weighted pools, filterByRemainingResources on a
+                  shrinking budget, failed pods cycling until a full pass makes no progress), 38.9 % unschedulable
+  config5-1000000 config 5 at BASELINE's 1M pods (38.7 % unschedulable, 48k NodeClaims), when generated (hours of
+                  oracle time: python tests/golden/make_fullsize_digests.py config5-1000000)
   config4-10000   computeConsolidation on the 10k-node config-4 cluster for every firstNConsolidationOption prefix
                   (candidates[0:mid+1], mid = 1..100) and 200 random subsets: every decision field
 
@@ -58,7 +63,9 @@ def _solves():
     from kpamd import synth
     return {"config2-50000": lambda cat: synth.config2(cat, n_pods=50_000, seed=2),
             "config3-100000": lambda cat: synth.config3(cat, n_pods=100_000),
-            "config5-100000": lambda cat: synth.config5(cat, n_pods=100_000)}
+            "config5-100000": lambda cat: synth.config5(cat, n_pods=100_000),
+            "config5-limits-100000": lambda cat: synth.config5(cat, n_pods=100_000, limit_div=10),
+            "config5-1000000": lambda cat: synth.config5(cat, n_pods=1_000_000)}
 
 
 def main():
@@ -70,7 +77,7 @@ def main():
     only = set(sys.argv[1:])
     out = json.load(open(OUT)) if os.path.exists(OUT) and only else {}
     for name, mk in SOLVES.items():
-        if only and name not in only:
+        if (only and name not in only) or (not only and name == "config5-1000000"):  # (hours: on request only)
             continue
         t = time.time()
         out[name] = solve_digest(pyoracle.solve(mk()))

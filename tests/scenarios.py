@@ -40,12 +40,12 @@ def _fake_offering_zones():
     return zones
 
 
-def _resolve(lib, row, zones, spot_price, offering_zones, ami_family="AL2023"):
+def _resolve(lib, row, zones, spot_price, offering_zones, ami_family="AL2023", **nodeclass_kw):
     from kpamd import abi, catalog
     from kpamd.model import InstanceType
     arena = abi.Arena()
     opts = catalog.default_options()
-    nc = catalog.nodeclass(arena, ami_family=ami_family)
+    nc = catalog.nodeclass(arena, ami_family=ami_family, **nodeclass_kw)
     info = catalog.ec2_info(arena, row)
     cap, ovh = abi.ResourceList(), abi.ResourceList()
     assert lib.kp_instance_type_resolve(C.byref(opts), C.byref(info), C.byref(nc), C.byref(cap), C.byref(ovh)) == 0
@@ -58,9 +58,10 @@ def _resolve(lib, row, zones, spot_price, offering_zones, ami_family="AL2023"):
     return InstanceType(row["name"], reqs, catalog.resource_dict(cap), catalog.resource_dict(ovh), offs)
 
 
-def fake_catalog(lib, ami_family="AL2023", extra_rows=()):
+def fake_catalog(lib, ami_family="AL2023", extra_rows=(), **nodeclass_kw):
     """The 16-type fake EC2 catalogue with its offering zones; on-demand prices from the static table, spot = the
-    default price (no spot update in the instancetype suite). extra_rows: more (row, offering zones) pairs."""
+    default price (no spot update in the instancetype suite). extra_rows: more (row, offering zones) pairs;
+    nodeclass_kw: more EC2NodeClass fields (catalog.nodeclass: block_device_mappings, instance_store_policy)."""
     from kpamd import catalog
     zones = _fake_offering_zones()
     rows = [(r, zones[r["name"]]) for r in catalog.load_ec2_table() if r["name"] in zones] + list(extra_rows)
@@ -68,7 +69,7 @@ def fake_catalog(lib, ami_family="AL2023", extra_rows=()):
     for r, rz in rows:
         z = [x for x in rz if x in catalog.ZONES]
         spot = {(r["name"], x): r["od_price"] for x in z}
-        out.append(_resolve(lib, r, catalog.ZONES, spot, z, ami_family))
+        out.append(_resolve(lib, r, catalog.ZONES, spot, z, ami_family, **nodeclass_kw))
     return out
 
 

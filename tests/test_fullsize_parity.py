@@ -2,7 +2,8 @@
 (tests/golden/fullsize_digests.json, generated in this container by tests/golden/make_fullsize_digests.py from the
 same generators and seeds): the headline config 2 at 50k pods, config 3 at 100k pods onto 5k existing nodes, and
 config 5 at 100k pods (17.5k NodeClaims: the newNodeClaims order spills past the device's LDS capacity by itself),
-config 4's 10k-node cluster on every firstNConsolidationOption prefix plus 200 random candidate subsets.
+config 5 at 100k pods with its pools' cpu limits divided by 10 (the regime where the 1M-pod burst ends: NodePool limits
+bind, 38.9 % of the pods unschedulable), config 5 at 1M pods when its digest has been generated, config 4's 10k-node cluster on every firstNConsolidationOption prefix plus 200 random candidate subsets.
 
 The -m "not gpu" test checks the fixture is consistent with the generators (counts and shapes)."""
 import json
@@ -25,6 +26,10 @@ def test_fixture_shape(digests):
     assert digests["config2-50000"]["placed"] == 50_000
     assert digests["config3-100000"]["on_existing"] > 0
     assert digests["config5-100000"]["nodeclaims"] > 2 * 8192, "past the device's LDS sort capacity without forcing it"
+    lim = digests["config5-limits-100000"]
+    assert 100_000 - lim["placed"] >= 25_000, "NodePool limits bind: at least 25 % of the pods end unschedulable"
+    if "config5-1000000" in digests:
+        assert 1_000_000 - digests["config5-1000000"]["placed"] >= 250_000
     c4 = digests["config4-10000"]
     assert len(c4["prefixes"]) == 100 and len(c4["random"]) == 200
     decisions = {r[0] for r in c4["random"]}
@@ -32,16 +37,20 @@ def test_fixture_shape(digests):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["config2-50000", "config3-100000", "config5-100000"])
+@pytest.mark.parametrize("name", ["config2-50000", "config3-100000", "config5-100000", "config5-limits-100000",
+                                  "config5-1000000"])
 def test_solve_fullsize(ctx, catalog, digests, name):
     import kpamd
     import make_fullsize_digests as mk
+    if name not in digests:
+        pytest.skip(f"{name}: digest not generated (make_fullsize_digests.py {name})")
     prob = mk._solves()[name](catalog)
     res = kpamd.Scheduler(ctx, prob).solve()
     got = mk.solve_digest(res)
     assert got == digests[name]
-    if name.startswith("config5"):
+    if name in ("config5-100000", "config5-1000000"):
         assert len(res["nodeclaims"]) > 8192
+        assert res["stats"]["order_chunks"][4] == 2, "the chunked order past the LDS capacity"
 
 
 @pytest.mark.gpu
