@@ -142,8 +142,8 @@ typedef struct kp_offering {
   int32_t reservation_capacity; /* Offering.ReservationCapacity (R:offering.go:178): read by ReservedOfferingFilter.
                                    Filter and launch plans take reserved offerings (ABI v7), Solve plans too (ABI
                                    v9: NodeClaim.reserveOfferings against each reservation's capacity, see
-                                   kp_solve_in.reserved_offering_mode); a cluster plan over a catalogue holding an
-                                   offering with a reservation id or type returns KP_E_UNSUPPORTED */
+                                   kp_solve_in.reserved_offering_mode), cluster plans too (ABI v10: every simulation
+                                   reserves strictly, as SimulateScheduling's DisableReservedCapacityFallback) */
 } kp_offering;
 
 /* cloudprovider.InstanceType after InjectOfferings. */
@@ -743,7 +743,9 @@ int32_t kp_simulate_batch(kp_ctx* ctx, const kp_cluster* cluster, const uint32_t
  * NodePool limits, pending pods, deleting nodes, spot-to-spot and host ports run in the batched kernels; topology
  * spread, pod (anti-)affinity and a pod NotIn/DoesNotExist requirement on a label key some node lacks take the general
  * path (each subset a whole device Solve). Returns KP_E_UNSUPPORTED (the Go path then runs) for > 65535 pods in one
- * subset and for catalogues holding capacity reservations. */
+ * subset. Catalogues holding capacity reservations take the general path too (ABI v10): every simulation's Solve reserves
+ * offerings strictly (SimulateScheduling's DisableReservedCapacityFallback); a candidate in a reservation is priced by
+ * its reserved offering (on-demand / 1e7, R:pkg/providers/instancetype/offering/offering.go:160-166). */
 typedef struct kp_cluster_plan kp_cluster_plan;
 int32_t kp_cluster_prepare(kp_ctx* ctx, const kp_cluster* cluster, kp_cluster_plan** out);
 int32_t kp_cluster_simulate(kp_cluster_plan* plan, const uint32_t* offsets, const uint32_t* nodes, uint32_t n_subsets,

@@ -4160,8 +4160,16 @@ bool NodeCandidatePrice(const HostType& t, const std::map<string, string>& label
     auto f = labels.find(key);
     return f != labels.end() && f->second != v;
   };
+  // the reservation keys: an offering without one requires DoesNotExist (R:offering.go:136-137), so a node labelled
+  // with a reservation id / type is compatible only with the offerings of that reservation
+  auto clash_res = [&](const char* key, bool has, const string& v) {
+    auto f = labels.find(key);
+    if (f == labels.end()) return false;
+    return !has || f->second != v;
+  };
   for (auto& o : t.offs) {
     if (clash(kCapType, true, o.ct) || clash(kZone, o.has_zone, o.zone) || clash(kZoneID, o.has_zid, o.zid)) continue;
+    if (clash_res(kResID, o.has_rid, o.rid) || clash_res(kResType, o.has_rt, o.rt)) continue;
     if (!any || o.price < p) p = o.price;
     any = true;
   }
@@ -4212,10 +4220,11 @@ int32_t kp_cluster_prepare(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan** 
   auto t0 = std::chrono::steady_clock::now();
   if (!ctx || !cl || !out) return fail(KP_E_INVAL, "null argument");
   if (cl->n_nodes && !cl->nodes) return fail(KP_E_INVAL, "null nodes");
-  for (uint32_t i = 0; i < cl->n_catalogs; i++)  // SimulateScheduling's reservation accounting is not modelled
-    if (cl->catalogs && cl->catalogs[i] && cl->catalogs[i]->reservations)
-      return fail(KP_E_UNSUPPORTED, "capacity-reservation offerings in a cluster catalogue");
+  // capacity reservations: SimulateScheduling's Solve reserves offerings strictly (DisableReservedCapacityFallback),
+  // which the batched kernels do not model: such clusters take the general path (whole device Solves)
   bool topo = false;
+  for (uint32_t i = 0; i < cl->n_catalogs; i++)
+    topo |= cl->catalogs && cl->catalogs[i] && cl->catalogs[i]->reservations;
   for (uint32_t i = 0; i < cl->n_shapes; i++)
     topo |= cl->shapes[i].n_topology_spread > 0 || PodTermCount(cl->shapes[i]) > 0;
   if (topo) return PrepareGeneral(ctx, cl, out, t0);
@@ -4567,7 +4576,16 @@ bool OfferAdmits(const Dict& d, const KReqs& R, const HostOffering& o) {
     if (b < 0) return ((R.compl_ >> k) & 1) != 0;
     return Has(d, R, k, b);
   };
-  return admits(kCapType, true, o.ct) && admits(kZone, o.has_zone, o.zone) && admits(kZoneID, o.has_zid, o.zid);
+  // reservation keys: an offering without one is DoesNotExist on it, compatible with NotIn / DoesNotExist only
+  auto admits_res = [&](const char* key, bool has, const string& v) {
+    if (has) return admits(key, true, v);
+    const int k = d.key(key);
+    if (k < 0 || !((R.present >> k) & 1)) return true;
+    const bool c = ((R.compl_ >> k) & 1) != 0, nz = KeyNonEmptyVals(d, R, k);
+    return (c && nz) || (!c && !nz);
+  };
+  return admits(kCapType, true, o.ct) && admits(kZone, o.has_zone, o.zone) && admits(kZoneID, o.has_zid, o.zid) &&
+         admits_res(kResID, o.has_rid, o.rid) && admits_res(kResType, o.has_rt, o.rt);
 }
 // Offerings.Available().Compatible(reqs).WorstLaunchPrice: capacity types in precedence reserved, spot, on-demand
 double WorstLaunch(const Dict& d, const KReqs& R, const HostType& t, bool spot_only) {
@@ -4682,6 +4700,7 @@ static int32_t GeneralSimLocked(kp_cluster_plan* plan, const uint32_t* offsets, 
     in.n_bound_pods = (uint32_t)bound.size();
     in.namespaces = cl.namespaces;
     in.n_namespaces = cl.n_namespaces;
+    in.reserved_offering_mode = KP_RESERVED_STRICT;  // SimulateScheduling: NewScheduler(..., DisableReservedCapacityFallback)
     kp_solve_plan* sp = nullptr;
     int32_t rc = SolvePrepare(ctx, &in, nullptr, &sp);
     if (rc) return rc;

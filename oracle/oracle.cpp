@@ -1945,6 +1945,8 @@ int32_t kpo_simulate_batch(const kp_cluster* cl, const uint32_t* offsets, const 
     in.namespaces = cl->namespaces;
     in.n_namespaces = cl->n_namespaces;
     in.pod_uids = cl->pod_uids ? uids.data() : nullptr;
+    // SimulateScheduling builds its scheduler with DisableReservedCapacityFallback: strict reservations
+    in.reserved_offering_mode = KP_RESERVED_STRICT;
     kpo_result* res = nullptr;
     int32_t rc = SolveCore(cats, &in, &res);
     if (rc) return rc;
