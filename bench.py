@@ -303,9 +303,9 @@ def _feasibility(args, cat, ctx, prob, barrier, max_over_ranks, world, steps=10)
         ach = alg / (k_ms / 1e3) / 1e9
         legs[name] = {"value": round(pairs * world * steps / elapsed, 1), "unit": "pairs/s", "rows": rows,
                       "instance_types": T, "kernel_ms": round(k_ms, 4),
-                      "roofline": {"bound": "hbm", "kernel": "feasibility_kernel", "achieved": round(ach, 1),
+                      "roofline": {"bound": "hbm", "kernel": "feasibility_bits_kernel", "achieved": round(ach, 1),
                                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                                   "traffic": _traffic("feasibility_kernel") if name == "distinct" else None,
+                                   "traffic": _traffic("feasibility_bits_kernel") if name == "distinct" else None,
                                    "algorithmic_bytes_per_launch": alg,
                                    "bytes_per_row": ROW_BYTES + 8 * T + 8 * ((T + 63) // 64),
                                    "l2_effective_GBs": round(pairs * L2_BYTES_PER_PAIR / (k_ms / 1e3) / 1e9, 1)}}
@@ -420,21 +420,6 @@ def _consolidation(args, cat, ctx, dist, rank, world, barrier, kcomm):
     return out
 
 
-def spread_cluster(cat, n_nodes, seed=4):
-    """Config 4 with topology spread: every shape labelled app-(i % 8), every other shape zone-spread (maxSkew 1,
-    DoNotSchedule) over its app. The batched sim kernels do not model spread, so kp_cluster_prepare takes the general
-    path: each subset's SimulateScheduling is a whole Solve on the device with the remaining nodes' pods counted."""
-    from kpamd import synth
-    from kpamd.model import LabelSelector, TopologySpread
-    cl = synth.config4(cat, n_nodes=n_nodes, seed=seed)
-    for i, sh in enumerate(cl.shapes):
-        sh.labels = dict(sh.labels or {}, app=f"app-{i % 8}")
-        if i % 2 == 0:
-            sh.topology_spread = [TopologySpread("topology.kubernetes.io/zone", 1, LabelSelector({"app": f"app-{i % 8}"}),
-                                                 "DoNotSchedule")]
-    return cl
-
-
 def _consolidation_general(args, cat, ctx, rank, world, barrier):
     """Consolidation on a topology-spread cluster (the general simulation path): the 100
     firstNConsolidationOption prefixes plus random subsets of 2..20 candidates through kp_consolidate_argmin, rank 0
@@ -445,7 +430,7 @@ def _consolidation_general(args, cat, ctx, rank, world, barrier):
     if rank != 0:
         barrier()
         return None
-    cl = spread_cluster(cat, args.general_nodes)
+    cl = synth.spread_cluster(cat, args.general_nodes)
     cands = np.asarray(cl.candidates, dtype=np.uint32)
     mids = disruption.MultiNodeConsolidation.search_prefixes(len(cands))
     subs = [list(cands[:m + 1]) for m in mids]

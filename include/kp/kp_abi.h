@@ -745,7 +745,12 @@ int32_t kp_simulate_batch(kp_ctx* ctx, const kp_cluster* cluster, const uint32_t
  * path (each subset a whole device Solve). Returns KP_E_UNSUPPORTED (the Go path then runs) for > 65535 pods in one
  * subset. Catalogues holding capacity reservations take the general path too (ABI v10): every simulation's Solve reserves
  * offerings strictly (SimulateScheduling's DisableReservedCapacityFallback); a candidate in a reservation is priced by
- * its reserved offering (on-demand / 1e7, R:pkg/providers/instancetype/offering/offering.go:160-166). */
+ * its reserved offering (on-demand / 1e7, R:pkg/providers/instancetype/offering/offering.go:160-166).
+ * The general path compiles the cluster once as a superset Solve (every node not being deleted existing, every pod
+ * a simulation can queue in its pod list) and runs the subsets' Solves batched, one workgroup each; a subset that
+ * would remove every owner of an inverse anti-affinity term (and every subset of a cluster whose superset compile is
+ * unsupported, or with KP_GENERAL_BATCH=0) is compiled on its own. stats (general path): phase_cycles[0] simulations
+ * batched, phase_cycles[1] simulations compiled per subset. */
 typedef struct kp_cluster_plan kp_cluster_plan;
 int32_t kp_cluster_prepare(kp_ctx* ctx, const kp_cluster* cluster, kp_cluster_plan** out);
 int32_t kp_cluster_simulate(kp_cluster_plan* plan, const uint32_t* offsets, const uint32_t* nodes, uint32_t n_subsets,

@@ -211,6 +211,19 @@ struct FinalizeArgs {
   uint32_t* out_n_remaining; // [n_nc]
   uint32_t* out_n_options;   // [n_nc]
   const uint64_t* nc_held;   // [n_nc] reservation classes held (FinalizeScheduling: reservation-id In {..}), or null
+  const uint64_t* solve_stats;  // batched finalize: the Solve's stats (n_nc = [3]); unused otherwise
+};
+
+// batch_init_kernel: per-arena initialisation of batched Solves (pristine copy + byte fills)
+constexpr int BATCH_INIT_FILLS = 12;
+struct BatchInitArgs {
+  uint8_t* base;
+  size_t stride;
+  const uint8_t* pristine;
+  size_t dst_off, n_copy;
+  int32_t n_fill;
+  uint32_t fill_byte[BATCH_INIT_FILLS];
+  size_t fill_off[BATCH_INIT_FILLS], fill_len[BATCH_INIT_FILLS];
 };
 
 struct FeasArgs {
@@ -396,5 +409,8 @@ const void* sim_kernel_ptr();
 
 hipError_t launch_solve(const SolveArgs& a, int nw, size_t dyn_lds, hipStream_t s);
 hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s);
+hipError_t launch_solve_batch(const SolveArgs& a0, const SolveArgs* dev_args, int n, size_t dyn_lds, hipStream_t s);
+hipError_t launch_finalize_batch(const FinalizeArgs& a0, const FinalizeArgs* dev_args, int n, hipStream_t s);
+hipError_t launch_batch_init(const BatchInitArgs& a, int n_arenas, hipStream_t s);
 hipError_t launch_feasibility(const FeasArgs& a, hipStream_t s);
 

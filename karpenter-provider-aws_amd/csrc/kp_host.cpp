@@ -1303,6 +1303,19 @@ struct Compiled {
   vector<int32_t> tkey_slot;  // [64]
   vector<int32_t> tk_keys;    // [TK]
   vector<uint8_t> ex_tcode;   // [TK][E]
+  // What each existing node (input index) contributes to the topology state, recorded by CompileTopology when
+  // track_nodes is set: the batched general-path simulations (GeneralBatch) remove a subset's nodes from it.
+  bool track_nodes = false;
+  vector<vector<int32_t>> node_cnt;  // [n_existing] tg_cnt entries (g * 64 + ordinal), one per bound pod counted
+  vector<vector<int32_t>> node_reg;  // [n_existing] (g * 64 + ordinal): a domain the node registers in dictionary-key group g
+  vector<vector<int32_t>> node_hrec; // [n_existing] hostname-row groups a bound pod on the node was recorded into
+  vector<vector<int32_t>> node_inv;  // [n_existing] inverse anti-affinity groups a bound pod on the node owns
+  vector<uint64_t> tg_reg_static;    // [G] domains registered without any existing node (NodePool / type offerings)
+  vector<int32_t> tg_hrec_total, tg_inv_total;  // [G]
+  vector<vector<int32_t>> shape_l0;  // [S] the spread groups each shape makes at level 0 (NewTopology, if it has pods)
+  vector<char> tg_spread;            // [G] 1: a topology-spread group
+  vector<vector<int32_t>> tg_unreg;  // [G] hostname spread groups: positions (sorted order) unregistered (255) when the
+                                     // group is created not live
 };
 
 // Requirements.Compatible(A, B, allowUndefinedWellKnown) on the host encoding.
@@ -1497,6 +1510,13 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
     any |= in->bound_pods[b].n_anti_affinity > 0;
   }
   if (!any) return KP_OK;
+  if (cp.track_nodes) {
+    cp.node_cnt.assign(in->n_existing, {});
+    cp.node_reg.assign(in->n_existing, {});
+    cp.node_hrec.assign(in->n_existing, {});
+    cp.node_inv.assign(in->n_existing, {});
+    cp.shape_l0.assign(in->n_shapes, {});
+  }
   vector<int> ex_pos(in->n_existing);
   for (int e = 0; e < E; e++) ex_pos[cp.ex_input[e]] = e;
   vector<std::map<string, string>> node_labels(in->n_existing);
@@ -1640,6 +1660,13 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
     cp.tg_reg.push_back(reg);
     for (int b = 0; b < 64; b++) cp.tg_cnt.push_back(0);
     if (row >= 0) cp.hcnt0.resize((size_t)cp.GH * std::max(E, 1), 0);
+    if (cp.track_nodes) {
+      cp.tg_reg_static.push_back(reg);
+      cp.tg_hrec_total.push_back(0);
+      cp.tg_inv_total.push_back(0);
+      cp.tg_spread.push_back(1);
+      cp.tg_unreg.emplace_back();
+    }
     // countDomains: bound pods the selector matches, on nodes the filter admits; then existing nodes' domains
     auto filter_ok = [&](uint32_t ni) {
       const int ts = cp.ex_taintset[ex_pos[ni]];
@@ -1663,6 +1690,7 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
         const int ord = d.bit(k, lv->second) - k * 64;  // value ordinal (key k's values live in word k)
         cp.tg_cnt[(size_t)g * 64 + ord]++;
         cp.tg_reg[g] |= 1ull << ord;
+        if (cp.track_nodes) cp.node_cnt[ni].push_back(g * 64 + ord);
       }
       }
     }
@@ -1679,6 +1707,19 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
         it = node_domains.emplace(fid, m).first;
       }
       cp.tg_reg[g] |= it->second;
+      if (cp.track_nodes)
+        for (uint32_t ni = 0; ni < in->n_existing; ni++) {
+          auto lv = node_labels[ni].find(key);
+          if (lv != node_labels[ni].end() && filter_ok(ni)) cp.node_reg[ni].push_back(g * 64 + d.bit(k, lv->second) - k * 64);
+        }
+    }
+    if (row >= 0 && cp.track_nodes && E) {  // the positions a not-live creation leaves unregistered (below)
+      vector<char> counted(in->n_existing, 0);
+      for (auto& bs : bsets)
+        if (ns == bs.ns && SelectorMatches(t.selector, bs.labels))
+          for (const uint32_t ni : bs.nodes) counted[ni] = 1;
+      for (uint32_t ni = 0; ni < in->n_existing; ni++)
+        if (!(filter_ok(ni) && (node_labels[ni].count(kHostname) || counted[ni]))) cp.tg_unreg[g].push_back(ex_pos[ni]);
     }
     if (row >= 0 && !live && E) {
       // a hostname group a relaxation creates (Topology.Update after NewTopology): its domains are only what
@@ -1729,6 +1770,10 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
       uint8_t& c = cp.hcnt0[(size_t)cp.tg_row[g] * std::max(E, 1) + ex_pos[ni]];
       if (c < 254) c++;
       cp.tg_reg[g] |= 1;
+      if (cp.track_nodes) {
+        cp.node_hrec[ni].push_back(g);
+        cp.tg_hrec_total[g]++;
+      }
     } else {
       const int k = cp.tg_key[g];
       auto lv = node_labels[ni].find(d.keys[k]);
@@ -1736,6 +1781,7 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
       const int ord = d.bit(k, lv->second) - k * 64;
       cp.tg_cnt[(size_t)g * 64 + ord]++;
       cp.tg_reg[g] |= 1ull << ord;
+      if (cp.track_nodes) cp.node_cnt[ni].push_back(g * 64 + ord);
     }
   };
   auto anti_group = [&](const kp_pod_affinity_term& t, const std::set<string>& nss, bool inverse, bool aff = false) -> int {
@@ -1774,13 +1820,24 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
     cp.tg_nterm.push_back(0);
     cp.tg_filt_tol.push_back(~0ull);
     uint64_t reg = 0;
+    if (cp.track_nodes) {
+      cp.tg_reg_static.push_back(0);
+      cp.tg_hrec_total.push_back(0);
+      cp.tg_inv_total.push_back(0);
+      cp.tg_spread.push_back(0);
+      cp.tg_unreg.emplace_back();
+    }
     if (k >= 0) {
       const vector<uint64_t>& dm = domains_of(k);
       for (int b = 0; b < 64; b++)
         if (dm[b]) reg |= 1ull << b;
+      if (cp.track_nodes) cp.tg_reg_static[g] = reg;
       for (uint32_t ni = 0; ni < in->n_existing; ni++) {
         auto lv = node_labels[ni].find(key);
-        if (lv != node_labels[ni].end()) reg |= 1ull << (d.bit(k, lv->second) - k * 64);
+        if (lv != node_labels[ni].end()) {
+          reg |= 1ull << (d.bit(k, lv->second) - k * 64);
+          if (cp.track_nodes) cp.node_reg[ni].push_back(g * 64 + d.bit(k, lv->second) - k * 64);
+        }
       }
     }
     cp.tg_reg.push_back(reg);
@@ -1820,6 +1877,10 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
       if (g < 0) return KP_E_UNSUPPORTED;
       if (std::find(inverse_groups.begin(), inverse_groups.end(), g) == inverse_groups.end()) inverse_groups.push_back(g);
       record_bound(g, bp.node);
+      if (cp.track_nodes) {
+        cp.node_inv[bp.node].push_back(g);
+        cp.tg_inv_total[g]++;
+      }
     }
   }
   // every other group a shape-level owns, before the recording lists are built: the groups of shapes without pods,
@@ -1844,6 +1905,8 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
     for (int l = 1; l < cp.shape_nlevels[s]; l++)
       for (int j : spread_levels[s][l])
         if (j < (int)sh.n_topology_spread && group_of(s, j, l, false) < 0) return KP_E_UNSUPPORTED;
+    if (cp.track_nodes)  // sgroup: the level-0 spread groups first, then the pod (anti-)affinity groups
+      cp.shape_l0[s].assign(sgroup[s].begin(), sgroup[s].begin() + std::min<size_t>(sgroup[s].size(), sh.n_topology_spread));
   }
   if (cp.G == 0) return KP_OK;
   if ((size_t)cp.GH * (size_t)(E + in->n_pods) > ((size_t)1 << 31))
@@ -2600,6 +2663,7 @@ int32_t CompileSolve(const kp_solve_in* in, Compiled& cp, kp_ctx* cache = nullpt
       }
   }
   Compiled fresh;
+  fresh.track_nodes = cp.track_nodes;
   rc = BuildBase(in, raw, *fresh.B);
   if (rc) return rc;
   fresh.B->ident = ident;
@@ -2678,6 +2742,325 @@ vector<DevCatalog> DevCats(uint8_t* base, const Compiled& cp, const vector<CatOf
   return out;
 }
 
+// Device layout of one Solve. Offsets are relative to the shared region (the batch's read-only data: shapes, PVP
+// rows, topology tables, the template-options table) or to the Solve's arena (its pods, the existing nodes it may
+// use, its mutable state, device-only scratch). A single Solve keeps both in one allocation (shared == arena base);
+// the batched general-path simulations (GeneralBatch) share one shared region between many arenas.
+struct SolveOffs {
+  // shared
+  size_t slb = 0, snl = 0, sreqs = 0, sneg = 0, sreq = 0, stol = 0, pvp = 0, pvpb = 0, pvps = 0, pvpn = 0, tlp = 0,
+         exts = 0, exav = 0, shpc = 0, shpa = 0, tgk = 0, tgr = 0, tgs = 0, tgm = 0, tga = 0, tgtb = 0, tgft = 0,
+         tgt = 0, tgtn = 0, tgnt = 0, srb = 0, srn = 0, recl = 0, recx = 0, slft = 0, slob = 0, slon = 0, owng = 0,
+         owns = 0, ownp = 0, ownr = 0, sltk = 0, tks = 0, extc = 0, tkk = 0, slsh = 0, tfeas = 0;
+  // arena: the Solve's inputs, then its mutable state [mut, mut_end) (restored before every run; [mut, common) is the
+  // part a batched simulation patches, [common, mut_end) the part every simulation starts from alike), then
+  // device-only regions
+  size_t pod_shape = 0, exso = 0, mut = 0, queue = 0, tgc = 0, tglv = 0, tgreg = 0, hcx = 0, common = 0,
+         pod_level = 0, lastlen = 0, lastlen_ep = 0, trem = 0, exr = 0, exrq = 0, exroom = 0, exhp = 0, mut_end = 0;
+  size_t pristine = 0, ncr = 0, ncX = 0, ncrq = 0, nct = 0, npods = 0, order = 0, chkblk = 0, maxalloc = 0, fitj = 0,
+         nchead = 0, nccat = 0, nchp = 0, place = 0, events = 0, stats = 0, ver0 = 0, exver = 0, tver = 0, curnc = 0,
+         curex = 0, held = 0, ver_end = 0, fail0 = 0, ncfail = 0, exfail = 0, tfail = 0, chkdead = 0, fail_end = 0,
+         opts = 0, nrem = 0, nopt = 0, hcnc = 0, nctc = 0, arena_end = 0;
+  size_t n_hcnc = 0;
+  int ncc = 0, chk_dead_rows = 0, sort_cap = 0, opt_stride = 0;
+  bool chk_on = false;
+};
+
+// the resources some shape requests or some template's daemon overhead holds: Fits iterates every resource of the
+// merged requests
+uint32_t RequestedResources(const Compiled& C) {
+  uint32_t m = 0;
+  for (size_t i = 0; i < C.shape_requests.size(); i++)
+    if (C.shape_requests[i] > 0) m |= 1u << (i % KP_NRES);
+  for (size_t i = 0; i < C.B->tmpl_daemon.size(); i++)
+    if (C.B->tmpl_daemon[i] > 0) m |= 1u << (i % KP_NRES);
+  return m;
+}
+
+// per existing node: 1 when its unrequested resources never fail a pod (they never change), else 0
+vector<uint8_t> ExStatic(const Compiled& C, uint32_t rmask) {
+  const int E = (int)C.ex_reqs.size();
+  vector<uint8_t> ok(std::max(E, 1), 0);
+  for (int e = 0; e < E; e++) {
+    bool good = true;
+    for (int r = 0; r < KP_NRES; r++) {
+      const int64_t av = C.ex_available[(size_t)e * KP_NRES + r], rq = C.ex_requests[(size_t)e * KP_NRES + r];
+      if (av < 0 || (!((rmask >> r) & 1) && rq > av)) good = false;
+    }
+    ok[e] = good ? 1 : 0;
+  }
+  return ok;
+}
+
+void PutShared(Blob& blob, const Compiled& C, SolveOffs& o) {
+  o.slb = blob.put(C.shape_level_base);
+  o.snl = blob.put(C.shape_nlevels);
+  o.sreqs = blob.put(C.shape_reqs);
+  o.sneg = blob.put(C.shape_negop);
+  o.sreq = blob.put(C.shape_requests);
+  o.stol = blob.put(C.shape_tolerates);
+  o.pvp = blob.put(C.pvp);
+  o.pvpb = blob.put(C.pvp_base);
+  o.pvps = blob.put(C.pvp_slot);
+  o.pvpn = blob.put(C.pvp_n);
+  o.tlp = blob.put(C.tmpl_limit_present);
+  o.exts = blob.put(C.ex_taintset);
+  o.exav = blob.put(C.ex_available);
+  o.shpc = blob.put(C.shape_hp_conf);
+  o.shpa = blob.put(C.shape_hp_add);
+  // topology (read-only part)
+  o.tgk = blob.put(C.tg_key), o.tgr = blob.put(C.tg_row), o.tgs = blob.put(C.tg_maxskew), o.tgm = blob.put(C.tg_mindom);
+  o.tga = blob.put(C.tg_aff), o.tgtb = blob.put(C.tg_term_base), o.tgft = blob.put(C.tg_filt_tol);
+  o.tgt = blob.put(C.tg_terms), o.tgtn = blob.put(C.tg_terms_negop), o.tgnt = blob.put(C.tg_nterm);
+  o.srb = blob.put(C.shape_rec_base), o.srn = blob.put(C.shape_rec_n), o.recl = blob.put(C.rec_list);
+  o.recx = blob.put(C.rec_aux), o.slft = blob.put(C.sl_fast_topo), o.slob = blob.put(C.sl_own_base);
+  o.slon = blob.put(C.sl_own_n), o.owng = blob.put(C.own_group), o.owns = blob.put(C.own_self);
+  o.ownp = blob.put(C.own_pd), o.ownr = blob.put(C.own_rec), o.sltk = blob.put(C.sl_topo_keys);
+  o.tks = blob.put(C.tkey_slot), o.extc = blob.put(C.ex_tcode), o.tkk = blob.put(C.tk_keys);
+  // shape of each shape-level (tmpl_feas_kernel)
+  vector<int32_t> sl_shape(std::max<size_t>(1, C.shape_reqs.size()), 0);
+  for (size_t sh = 0; sh < C.shape_level_base.size(); sh++)
+    for (int l = 0; l < C.shape_nlevels[sh]; l++) sl_shape[(size_t)C.shape_level_base[sh] + l] = (int32_t)sh;
+  o.slsh = blob.put(sl_shape);
+}
+
+// The arena's host-initialised part: the pods (pod_shape / queue of Pc entries), the existing nodes' static check,
+// then the mutable state.
+void PutArena(Blob& blob, const Compiled& C, const vector<int32_t>& pod_shape, const vector<int32_t>& queue, int Pc,
+              const vector<uint8_t>& ex_static, uint32_t rmask, SolveOffs& o) {
+  const int E = (int)C.ex_reqs.size();
+  o.pod_shape = blob.put(pod_shape);
+  o.exso = blob.put(ex_static);
+  o.mut = blob.reserve(0);
+  o.queue = blob.put(queue);
+  o.tgc = blob.put(C.tg_cnt);
+  o.tglv = blob.put(C.tg_live);
+  o.tgreg = blob.put(C.tg_reg);
+  o.hcx = blob.put(C.hcnt0);
+  o.common = blob.reserve(0);
+  const vector<int32_t> zeros_p(Pc, 0);
+  o.pod_level = blob.put(zeros_p);
+  o.lastlen = blob.put(zeros_p);
+  o.lastlen_ep = blob.put(zeros_p);
+  o.trem = blob.put(C.tmpl_remaining);
+  o.exr = blob.put(C.ex_reqs);
+  o.exrq = blob.put(C.ex_requests);
+  // headroom rows of the existing nodes for the first four requested resources (req_res_mask order)
+  vector<int64_t> ex_room((size_t)4 * std::max(E, 1), INT64_MAX);
+  for (int r = 0, k = 0; r < KP_NRES && k < 4; r++) {
+    if (!((rmask >> r) & 1)) continue;
+    for (int e = 0; e < E; e++)
+      ex_room[(size_t)k * E + e] = C.ex_available[(size_t)e * KP_NRES + r] - C.ex_requests[(size_t)e * KP_NRES + r];
+    k++;
+  }
+  o.exroom = blob.put(ex_room);
+  o.exhp = blob.put(C.ex_hp);
+  o.mut_end = blob.host.size();
+}
+
+// The arena's device-only regions (after every put of the blob). with_pristine: a device copy of the mutable state
+// (single Solves restore from it; batched simulations restore from the shared one).
+void ReserveArenaDev(Blob& blob, const Compiled& C, int Pc, int opt_stride, int sort_cap, bool with_pristine, SolveOffs& o) {
+  const int TW = C.B->TW, NT = (int)C.B->tmpl_reqs.size(), E = (int)C.ex_reqs.size();
+  o.pristine = with_pristine ? blob.reserve_dev(o.mut_end - o.mut) : 0;
+  o.ncr = blob.reserve_dev(sizeof(KReqs) * Pc);
+  o.ncX = blob.reserve_dev(sizeof(uint64_t) * (size_t)Pc * TW);
+  o.ncrq = blob.reserve_dev(sizeof(int64_t) * (size_t)Pc * KP_NRES);
+  o.nct = blob.reserve_dev(sizeof(int32_t) * Pc);
+  o.npods = blob.reserve_dev(sizeof(int32_t) * Pc);
+  o.order = blob.reserve_dev(sizeof(int32_t) * Pc);
+  // chunked newNodeClaims order past the LDS sort capacity (blocks + per (shape-level, block) dead marks): only when
+  // the Solve can create more NodeClaims than the LDS holds
+  o.sort_cap = sort_cap;
+  o.chk_on = Pc > sort_cap;
+  o.chkblk = blob.reserve_dev(o.chk_on ? sizeof(ChkBlk) * CHK_MAXC : 8);
+  o.maxalloc = blob.reserve_dev(sizeof(int64_t) * (size_t)Pc * KP_NRES);
+  o.fitj = blob.reserve_dev(sizeof(int32_t) * (size_t)Pc * KP_NRES);
+  o.nchead = blob.reserve_dev(sizeof(NcHead) * (size_t)Pc + 64);
+  o.nccat = blob.reserve_dev(sizeof(int32_t) * (size_t)Pc);
+  o.nchp = blob.reserve_dev(C.hp_any ? sizeof(uint64_t) * (size_t)Pc : 8);
+  o.place = blob.reserve_dev(sizeof(int32_t) * Pc);
+  o.events = blob.reserve_dev(sizeof(int32_t) * Pc);
+  o.stats = blob.reserve_dev(sizeof(uint64_t) * KP_SOLVE_STATS);
+  // failure memo (see SolveArgs): versions start at 0, memo entries at -1
+  const size_t SLn = std::max<size_t>(1, C.shape_reqs.size());
+  o.ncc = (int)std::min<size_t>((size_t)Pc, std::max<size_t>(1, ((size_t)256 << 20) / (4 * SLn)));
+  o.ver0 = blob.reserve_dev(0);
+  o.exver = blob.reserve_dev(sizeof(int32_t) * std::max(E, 1));
+  o.tver = blob.reserve_dev(sizeof(int32_t) * std::max(NT, 1));
+  o.curnc = blob.reserve_dev(sizeof(int32_t) * 2 * SLn);  // cursors start at {0, 0} (zeroed per run)
+  o.curex = blob.reserve_dev(sizeof(int32_t) * 2 * SLn);
+  o.held = blob.reserve_dev(C.B->res_cls ? sizeof(uint64_t) * (size_t)Pc : 8);
+  o.ver_end = blob.total();
+  o.fail0 = blob.reserve_dev(0);
+  o.ncfail = blob.reserve_dev(sizeof(int32_t) * SLn * o.ncc);
+  o.exfail = blob.reserve_dev(sizeof(int32_t) * SLn * std::max(E, 1));
+  o.tfail = blob.reserve_dev(sizeof(int32_t) * SLn * std::max(NT, 1));
+  o.chk_dead_rows = o.chk_on ? (int)std::min<size_t>(SLn, ((size_t)64 << 20) / (4 * CHK_MAXC)) : 0;
+  o.chkdead = blob.reserve_dev(std::max<size_t>(sizeof(int32_t) * o.chk_dead_rows * CHK_MAXC, 8));
+  o.fail_end = blob.total();
+  o.opt_stride = opt_stride;
+  o.opts = blob.reserve_dev(sizeof(uint32_t) * (size_t)Pc * opt_stride);
+  o.nrem = blob.reserve_dev(sizeof(uint32_t) * Pc);
+  o.nopt = blob.reserve_dev(sizeof(uint32_t) * Pc);
+  o.n_hcnc = (size_t)C.GH * Pc;
+  o.hcnc = blob.reserve_dev(std::max<size_t>(o.n_hcnc, 1));
+  o.nctc = blob.reserve_dev(std::max<size_t>((size_t)C.TK * Pc, 1));
+  o.arena_end = blob.total();
+}
+
+// SolveArgs of one Solve over the shared region `sh` and the arena `ar` (offsets from `o`).
+void BindSolve(SolveArgs& a, const Compiled& C, const SolveOffs& o, uint8_t* sh, uint8_t* ar, int n_pods, int Pc,
+               uint32_t rmask, int res_mode) {
+  uint8_t* cbase = (uint8_t*)C.B->dev.p;
+  memset(&a, 0, sizeof a);
+  a.dict = (const DevDict*)(cbase + C.B->o_dict);
+  a.cats = (const DevCatalog*)(cbase + C.B->o_cats);
+  a.n_catalogs = (int32_t)C.B->cats.size();
+  a.vint = (const int64_t*)(cbase + C.B->o_vint);
+  a.n_pods = n_pods;
+  a.pod_shape = (const int32_t*)(ar + o.pod_shape);
+  a.pod_level = (int32_t*)(ar + o.pod_level);
+  a.queue = (int32_t*)(ar + o.queue);
+  a.lastlen = (int32_t*)(ar + o.lastlen);
+  a.lastlen_epoch = (int32_t*)(ar + o.lastlen_ep);
+  a.shape_level_base = (const int32_t*)(sh + o.slb);
+  a.shape_nlevels = (const int32_t*)(sh + o.snl);
+  a.shape_reqs = sh + o.sreqs;
+  a.shape_negop = (const uint64_t*)(sh + o.sneg);
+  a.shape_requests = (const int64_t*)(sh + o.sreq);
+  a.shape_tolerates = (const uint64_t*)(sh + o.stol);
+  a.shape_pvp = (const uint64_t*)(sh + o.pvp);
+  a.pvp_base = (const int32_t*)(sh + o.pvpb);
+  a.pvp_slot = (const int32_t*)(sh + o.pvps);
+  a.sl_pvp_n = (const int32_t*)(sh + o.pvpn);
+  a.n_tmpl = (int32_t)C.B->tmpl_reqs.size();
+  a.tmpl_reqs = cbase + C.B->o_treqs;
+  a.tmpl_taintset = (const int32_t*)(cbase + C.B->o_tts);
+  a.tmpl_catalog = (const int32_t*)(cbase + C.B->o_tcat);
+  a.tmpl_X = (const uint64_t*)(cbase + C.B->o_tX);
+  a.tmpl_daemon = (const int64_t*)(cbase + C.B->o_tdm);
+  a.tmpl_limit_present = (const uint32_t*)(sh + o.tlp);
+  a.tmpl_remaining = (int64_t*)(ar + o.trem);
+  a.n_existing = (int32_t)C.ex_reqs.size();
+  a.ex_reqs = ar + o.exr;
+  a.ex_taintset = (const int32_t*)(sh + o.exts);
+  a.ex_available = (const int64_t*)(sh + o.exav);
+  a.ex_requests = (int64_t*)(ar + o.exrq);
+  a.ex_room = (int64_t*)(ar + o.exroom);
+  a.nc_reqs = ar + o.ncr;
+  a.nc_X = (uint64_t*)(ar + o.ncX);
+  a.nc_requests = (int64_t*)(ar + o.ncrq);
+  a.nc_tmpl = (int32_t*)(ar + o.nct);
+  a.g_npods = (int32_t*)(ar + o.npods);
+  a.g_order = (int32_t*)(ar + o.order);
+  a.sort_in_lds = 1;
+  a.sort_cap = o.sort_cap;
+  a.ncc = o.ncc;
+  a.chk_blk = (ChkBlk*)(ar + o.chkblk);
+  a.chk_dead = (int32_t*)(ar + o.chkdead);
+  a.chk_dead_rows = o.chk_dead_rows;
+  a.chk_maxc = o.chk_on ? CHK_MAXC : 0;
+  if (const char* e = getenv("KP_CHK_MAXC")) a.chk_maxc = o.chk_on ? std::max(0, std::min(CHK_MAXC, atoi(e))) : 0;  // test hook
+  a.nc_head = (NcHead*)(((uintptr_t)(ar + o.nchead) + 63) & ~(uintptr_t)63);
+  a.nc_fail = (int32_t*)(ar + o.ncfail);
+  a.ex_ver = (int32_t*)(ar + o.exver);
+  a.ex_fail = (int32_t*)(ar + o.exfail);
+  a.tmpl_ver = (int32_t*)(ar + o.tver);
+  a.tmpl_fail = (int32_t*)(ar + o.tfail);
+  a.cur_nc = (int32_t*)(ar + o.curnc);
+  a.cur_ex = (int32_t*)(ar + o.curex);
+  a.nc_maxalloc = (int64_t*)(ar + o.maxalloc);
+  a.nc_fitj = (int32_t*)(ar + o.fitj);
+  a.nc_cat = (int32_t*)(ar + o.nccat);
+  a.hp_any = C.hp_any ? 1 : 0;
+  a.shape_hp_conf = (const uint64_t*)(sh + o.shpc);
+  a.shape_hp_add = (const uint64_t*)(sh + o.shpa);
+  a.ex_hp = (uint64_t*)(ar + o.exhp);
+  a.nc_hp = (uint64_t*)(ar + o.nchp);
+  a.req_res_mask = rmask;
+  a.n_req_res = __builtin_popcount(rmask);
+  a.timing = getenv("KP_TIMING") ? 1 : 0;
+  a.n_groups = C.G;
+  a.tg_key = (const int32_t*)(sh + o.tgk);
+  a.tg_row = (const int32_t*)(sh + o.tgr);
+  a.tg_maxskew = (const int32_t*)(sh + o.tgs);
+  a.tg_mindom = (const int32_t*)(sh + o.tgm);
+  a.tg_aff = (const int32_t*)(sh + o.tga);
+  a.tg_term_base = (const int32_t*)(sh + o.tgtb);
+  a.tg_filt_tol = (const uint64_t*)(sh + o.tgft);
+  a.tg_terms = sh + o.tgt;
+  a.tg_terms_negop = (const uint64_t*)(sh + o.tgtn);
+  a.tg_cnt = (int32_t*)(ar + o.tgc);
+  a.tg_live = (int32_t*)(ar + o.tglv);
+  a.tg_nterm = (const int32_t*)(sh + o.tgnt);
+  a.tg_reg = (uint64_t*)(ar + o.tgreg);
+  a.hcnt_ex = ar + o.hcx;
+  a.hcnt_nc = ar + o.hcnc;
+  a.hnc_stride = Pc;
+  a.shape_rec_base = (const int32_t*)(sh + o.srb);
+  a.shape_rec_n = (const int32_t*)(sh + o.srn);
+  a.rec_list = (const int32_t*)(sh + o.recl);
+  a.rec_aux = (const int32_t*)(sh + o.recx);
+  a.sl_fast_topo = (const int32_t*)(sh + o.slft);
+  a.sl_own_base = (const int32_t*)(sh + o.slob);
+  a.sl_own_n = (const int32_t*)(sh + o.slon);
+  a.own_group = (const int32_t*)(sh + o.owng);
+  a.own_self = (const int32_t*)(sh + o.owns);
+  a.own_pd = (const uint64_t*)(sh + o.ownp);
+  a.own_rec = (const int4*)(sh + o.ownr);
+  a.sl_topo_keys = (const uint64_t*)(sh + o.sltk);
+  a.tkey_slot = (const int32_t*)(sh + o.tks);
+  a.n_tk = C.TK;
+  a.tk_keys = (const int32_t*)(sh + o.tkk);
+  a.nc_tcode = ar + o.nctc;
+  a.ex_static_ok = ar + o.exso;
+  a.ex_tcode = sh + o.extc;
+  a.placement = (int32_t*)(ar + o.place);
+  a.events = (int32_t*)(ar + o.events);
+  a.stats = (uint64_t*)(ar + o.stats);
+  a.res_mode = res_mode;
+  a.res_cls = C.B->res_cls;
+  a.nc_held = (uint64_t*)(ar + o.held);
+  for (int c = 0; c < KP_MAX_CLASSES; c++) a.res_cap0[c] = C.B->res_cap0.empty() ? 0 : C.B->res_cap0[c];
+}
+
+// The template-options table's launch over rows [row_lo, row_hi) (out: `words` u64 per (shape-level, template)).
+TfeasArgs TfeasOf(const SolveArgs& a, const uint8_t* sh, const SolveOffs& o, int rows, int words) {
+  TfeasArgs f;
+  memset(&f, 0, sizeof f);
+  f.dict = a.dict;
+  f.cats = a.cats;
+  f.n_catalogs = a.n_catalogs;
+  f.vint = a.vint;
+  f.n_tmpl = a.n_tmpl;
+  f.tmpl_reqs = a.tmpl_reqs;
+  f.tmpl_catalog = a.tmpl_catalog;
+  f.tmpl_X = a.tmpl_X;
+  f.tmpl_daemon = a.tmpl_daemon;
+  f.shape_reqs = a.shape_reqs;
+  f.shape_negop = a.shape_negop;
+  f.sl_shape = (const int32_t*)(sh + o.slsh);
+  f.shape_requests = a.shape_requests;
+  f.shape_pvp = a.shape_pvp;
+  f.pvp_base = a.pvp_base;
+  f.pvp_slot = a.pvp_slot;
+  f.sl_own_n = a.sl_own_n;
+  f.req_res_mask = a.req_res_mask;
+  f.row_lo = 0;
+  f.row_hi = rows;
+  f.words = words;
+  f.out = (uint64_t*)(sh + o.tfeas);
+  return f;
+}
+
+// the newNodeClaims order lives in LDS (64 KiB) up to this many NodeClaims, then spills
+int SortCapacity() {
+  int cap = 8192;
+  if (const char* e = getenv("KP_SORT_CAP")) cap = std::max(1, std::min(8192, atoi(e)));  // test hook
+  return cap;
+}
+
 }  // namespace
 
 extern "C" {
@@ -2754,6 +3137,7 @@ struct kp_solve_plan {
   DevBuf buf;  // per-Solve arena (the catalogue / template part lives in cp->B->dev, shared through the ctx cache)
   SolveArgs a;
   double catalog_ms = 0;  // SolveBase build time when this prepare missed the cache, else 0
+  double compile_ms = 0;  // host CompileSolve time of this prepare (KP_HOST_TIMING)
   size_t o_mut = 0, n_mut = 0, o_pristine = 0, o_ver = 0, n_ver = 0, o_fail = 0, n_fail = 0;
   size_t o_stats = 0, o_npods = 0, o_place = 0, o_events = 0, o_nct = 0, o_ncrq = 0, o_opts = 0, o_nrem = 0,
          o_nopt = 0, o_ncr = 0, o_hcnc = 0, n_hcnc = 0, o_held = 0;
@@ -2858,13 +3242,15 @@ static int32_t SolvePrepareLocal(kp_ctx* ctx, const kp_solve_in* in, kp_comm* co
   plan->ctx = ctx;
   plan->cp = std::make_unique<Compiled>();
   Compiled& C = *plan->cp;
+  const auto tc0 = std::chrono::steady_clock::now();
   int32_t rc = CompileSolve(in, C, ctx);
   if (rc) return rc;
+  plan->compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tc0).count();
   plan->catalog_ms = C.base_hit ? 0 : C.B->build_ms;
   rc = EnsureBaseOnDevice(ctx, *C.B);
   if (rc) return rc;
   const Dict& d = C.B->d;
-  const int TW = C.B->TW, P = (int)in->n_pods, NT = (int)C.B->tmpl_reqs.size(), E = (int)C.ex_reqs.size();
+  const int TW = C.B->TW, P = (int)in->n_pods, NT = (int)C.B->tmpl_reqs.size();
   const int Pc = std::max(P, 1);
   plan->P = P;
   plan->Pc = Pc;
@@ -2872,126 +3258,14 @@ static int32_t SolvePrepareLocal(kp_ctx* ctx, const kp_solve_in* in, kp_comm* co
   for (auto& q : C.B->tmpl_reqs) plan->any_min |= q.hmin != 0;
   for (auto& q : C.shape_reqs) plan->any_min |= q.hmin != 0;
 
+  const uint32_t rmask = RequestedResources(C);
   Blob blob;
-  const size_t o_pod_shape = blob.put(C.pod_shape);
-  const size_t o_slb = blob.put(C.shape_level_base);
-  const size_t o_snl = blob.put(C.shape_nlevels);
-  const size_t o_sreqs = blob.put(C.shape_reqs);
-  const size_t o_sneg = blob.put(C.shape_negop);
-  const size_t o_sreq = blob.put(C.shape_requests);
-  const size_t o_stol = blob.put(C.shape_tolerates);
-  const size_t o_pvp = blob.put(C.pvp);
-  const size_t o_pvpb = blob.put(C.pvp_base);
-  const size_t o_pvps = blob.put(C.pvp_slot);
-  const size_t o_pvpn = blob.put(C.pvp_n);
-  const size_t o_tlp = blob.put(C.tmpl_limit_present);
-  const size_t o_exts = blob.put(C.ex_taintset);
-  const size_t o_exav = blob.put(C.ex_available);
-  const size_t o_shpc = blob.put(C.shape_hp_conf), o_shpa = blob.put(C.shape_hp_add);
-  // topology (read-only part)
-  const size_t o_tgk = blob.put(C.tg_key), o_tgr = blob.put(C.tg_row), o_tgs = blob.put(C.tg_maxskew),
-               o_tgm = blob.put(C.tg_mindom), o_tga = blob.put(C.tg_aff), o_tgtb = blob.put(C.tg_term_base),
-               o_tgft = blob.put(C.tg_filt_tol), o_tgt = blob.put(C.tg_terms), o_tgtn = blob.put(C.tg_terms_negop),
-               o_tgnt = blob.put(C.tg_nterm),
-               o_srb = blob.put(C.shape_rec_base), o_srn = blob.put(C.shape_rec_n), o_recl = blob.put(C.rec_list), o_recx = blob.put(C.rec_aux), o_slft = blob.put(C.sl_fast_topo),
-               o_slob = blob.put(C.sl_own_base), o_slon = blob.put(C.sl_own_n), o_owng = blob.put(C.own_group),
-               o_owns = blob.put(C.own_self), o_ownp = blob.put(C.own_pd), o_ownr = blob.put(C.own_rec), o_sltk = blob.put(C.sl_topo_keys),
-               o_tks = blob.put(C.tkey_slot), o_extc = blob.put(C.ex_tcode), o_tkk = blob.put(C.tk_keys);
-  uint32_t rmask = 0;
-  for (size_t i = 0; i < C.shape_requests.size(); i++)
-    if (C.shape_requests[i] > 0) rmask |= 1u << (i % KP_NRES);
-  for (size_t i = 0; i < C.B->tmpl_daemon.size(); i++)
-    if (C.B->tmpl_daemon[i] > 0) rmask |= 1u << (i % KP_NRES);
-  vector<uint8_t> ex_static(std::max(E, 1), 0);  // unrequested resources of an existing node never change
-  for (int e = 0; e < E; e++) {
-    bool ok = true;
-    for (int r = 0; r < KP_NRES; r++) {
-      const int64_t av = C.ex_available[(size_t)e * KP_NRES + r], rq = C.ex_requests[(size_t)e * KP_NRES + r];
-      if (av < 0 || (!((rmask >> r) & 1) && rq > av)) ok = false;
-    }
-    ex_static[e] = ok ? 1 : 0;
-  }
-  const size_t o_exso = blob.put(ex_static);
-  // shape of each shape-level (tmpl_feas_kernel)
-  vector<int32_t> sl_shape(std::max<size_t>(1, C.shape_reqs.size()), 0);
-  for (size_t sh = 0; sh < C.shape_level_base.size(); sh++)
-    for (int l = 0; l < C.shape_nlevels[sh]; l++) sl_shape[(size_t)C.shape_level_base[sh] + l] = (int32_t)sh;
-  const size_t o_slsh = blob.put(sl_shape);
-  // ---- mutable state: restored from a pristine device copy before every run ----
-  vector<int32_t> zeros_p(Pc, 0);
-  const size_t o_mut = blob.reserve(0);
-  const size_t o_pod_level = blob.put(zeros_p);
-  const size_t o_queue = blob.put(C.queue);
-  const size_t o_lastlen = blob.put(zeros_p);
-  const size_t o_lastlen_ep = blob.put(zeros_p);
-  const size_t o_trem = blob.put(C.tmpl_remaining);
-  const size_t o_exr = blob.put(C.ex_reqs);
-  const size_t o_exrq = blob.put(C.ex_requests);
-  // headroom rows of the existing nodes for the first four requested resources (req_res_mask order)
-  vector<int64_t> ex_room((size_t)4 * std::max(E, 1), INT64_MAX);
-  {
-    int k = 0;
-    for (int r = 0; r < KP_NRES && k < 4; r++) {
-      if (!((rmask >> r) & 1)) continue;
-      for (int e = 0; e < E; e++)
-        ex_room[(size_t)k * E + e] = C.ex_available[(size_t)e * KP_NRES + r] - C.ex_requests[(size_t)e * KP_NRES + r];
-      k++;
-    }
-  }
-  const size_t o_exroom = blob.put(ex_room);
-  const size_t o_tgc = blob.put(C.tg_cnt);
-  const size_t o_tglv = blob.put(C.tg_live);
-  const size_t o_tgreg = blob.put(C.tg_reg);
-  const size_t o_hcx = blob.put(C.hcnt0);
-  const size_t o_exhp = blob.put(C.ex_hp);
-  const size_t n_mut = blob.host.size() - o_mut;
+  SolveOffs o;
+  PutShared(blob, C, o);
+  PutArena(blob, C, C.pod_shape, C.queue, Pc, ExStatic(C, rmask), rmask, o);
   const size_t host_bytes = blob.host.size();
-  const size_t o_pristine = blob.reserve_dev(n_mut);
-  // ---- device-only regions ----
-  const size_t o_ncr = blob.reserve_dev(sizeof(KReqs) * Pc);
-  const size_t o_ncX = blob.reserve_dev(sizeof(uint64_t) * (size_t)Pc * TW);
-  const size_t o_ncrq = blob.reserve_dev(sizeof(int64_t) * (size_t)Pc * KP_NRES);
-  const size_t o_nct = blob.reserve_dev(sizeof(int32_t) * Pc);
-  const size_t o_npods = blob.reserve_dev(sizeof(int32_t) * Pc);
-  const size_t o_order = blob.reserve_dev(sizeof(int32_t) * Pc);
-  // chunked newNodeClaims order past the LDS sort capacity (blocks + per (shape-level, block) dead marks): only when
-  // the Solve can create more NodeClaims than the LDS holds
-  int sort_cap = 8192;  // newNodeClaims order lives in LDS (64 KiB) up to this many NodeClaims, then spills
-  if (const char* e = getenv("KP_SORT_CAP")) sort_cap = std::max(1, std::min(8192, atoi(e)));  // test hook
-  const bool chk_on = Pc > sort_cap;
-  const size_t o_chkblk = blob.reserve_dev(chk_on ? sizeof(ChkBlk) * CHK_MAXC : 8);
-  const size_t o_maxalloc = blob.reserve_dev(sizeof(int64_t) * (size_t)Pc * KP_NRES);
-  const size_t o_fitj = blob.reserve_dev(sizeof(int32_t) * (size_t)Pc * KP_NRES);
-  const size_t o_nchead = blob.reserve_dev(sizeof(NcHead) * (size_t)Pc + 64);
-  const size_t o_nccat = blob.reserve_dev(sizeof(int32_t) * (size_t)Pc);
-  const size_t o_nchp = blob.reserve_dev(C.hp_any ? sizeof(uint64_t) * (size_t)Pc : 8);
-  const size_t o_place = blob.reserve_dev(sizeof(int32_t) * Pc);
-  const size_t o_events = blob.reserve_dev(sizeof(int32_t) * Pc);
-  const size_t o_stats = blob.reserve_dev(sizeof(uint64_t) * KP_SOLVE_STATS);
-  // failure memo (see SolveArgs): versions start at 0, memo entries at -1
-  const size_t SLn = std::max<size_t>(1, C.shape_reqs.size());
-  const int ncc = (int)std::min<size_t>((size_t)Pc, std::max<size_t>(1, ((size_t)256 << 20) / (4 * SLn)));
-  const size_t o_ver0 = blob.reserve_dev(0);
-  const size_t o_exver = blob.reserve_dev(sizeof(int32_t) * std::max(E, 1));
-  const size_t o_tver = blob.reserve_dev(sizeof(int32_t) * std::max(NT, 1));
-  const size_t o_curnc = blob.reserve_dev(sizeof(int32_t) * 2 * SLn);  // cursors start at {0, 0} (zeroed per run)
-  const size_t o_curex = blob.reserve_dev(sizeof(int32_t) * 2 * SLn);
-  const size_t o_held = blob.reserve_dev(C.B->res_cls ? sizeof(uint64_t) * (size_t)Pc : 8);
-  const size_t n_ver = blob.total() - o_ver0;
-  const size_t o_fail0 = blob.reserve_dev(0);
-  const size_t o_ncfail = blob.reserve_dev(sizeof(int32_t) * SLn * ncc);
-  const size_t o_exfail = blob.reserve_dev(sizeof(int32_t) * SLn * std::max(E, 1));
-  const size_t o_tfail = blob.reserve_dev(sizeof(int32_t) * SLn * std::max(NT, 1));
-  const int chk_dead_rows = chk_on ? (int)std::min<size_t>(SLn, ((size_t)64 << 20) / (4 * CHK_MAXC)) : 0;
-  const size_t o_chkdead = blob.reserve_dev(std::max<size_t>(sizeof(int32_t) * chk_dead_rows * CHK_MAXC, 8));
-  const size_t n_fail = blob.total() - o_fail0;
   const int opt_stride = in->max_instance_types ? (int)in->max_instance_types : std::max(1, d.dd.T);
-  const size_t o_opts = blob.reserve_dev(sizeof(uint32_t) * (size_t)Pc * opt_stride);
-  const size_t o_nrem = blob.reserve_dev(sizeof(uint32_t) * Pc);
-  const size_t o_nopt = blob.reserve_dev(sizeof(uint32_t) * Pc);
-  const size_t n_hcnc = (size_t)C.GH * Pc;
-  const size_t o_hcnc = blob.reserve_dev(std::max<size_t>(n_hcnc, 1));
-  const size_t o_nctc = blob.reserve_dev(std::max<size_t>((size_t)C.TK * Pc, 1));
+  ReserveArenaDev(blob, C, Pc, opt_stride, SortCapacity(), true, o);
   // template options per (shape-level, template): rows split evenly over the communicator's ranks (padded so that
   // every rank contributes the same byte count to the all-gather)
   const int SLi = (int)C.shape_reqs.size();
@@ -3002,7 +3276,7 @@ static int32_t SolvePrepareLocal(kp_ctx* ctx, const kp_solve_in* in, kp_comm* co
   const int tf_words = TW + KP_NRES / 2 + 1;
   const int rows_per_rank = (SLi + n_ranks - 1) / n_ranks;
   const size_t tf_bytes = tfeas_on ? (size_t)rows_per_rank * n_ranks * NT * tf_words * sizeof(uint64_t) : 0;
-  const size_t o_tfeas = blob.reserve_dev(std::max<size_t>(tf_bytes, 8));
+  o.tfeas = blob.reserve_dev(std::max<size_t>(tf_bytes, 8));
   const size_t total_bytes = blob.total();
 
   // the per-Solve arena: reuse the ctx's spare allocation when it is large enough
@@ -3018,185 +3292,50 @@ static int32_t SolvePrepareLocal(kp_ctx* ctx, const kp_solve_in* in, kp_comm* co
     HIPCHK(plan->buf.alloc(total_bytes));
   }
   uint8_t* base = (uint8_t*)plan->buf.p;
-  uint8_t* cbase = (uint8_t*)C.B->dev.p;
+  const size_t n_mut = o.mut_end - o.mut;
   HIPCHK(hipMemcpyAsync(base, blob.host.data(), host_bytes, hipMemcpyHostToDevice, ctx->stream));
-  HIPCHK(hipMemcpyAsync(base + o_pristine, base + o_mut, n_mut, hipMemcpyDeviceToDevice, ctx->stream));
+  HIPCHK(hipMemcpyAsync(base + o.pristine, base + o.mut, n_mut, hipMemcpyDeviceToDevice, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
 
   SolveArgs& a = plan->a;
-  memset(&a, 0, sizeof a);
-  a.dict = (const DevDict*)(cbase + C.B->o_dict);
-  a.cats = (const DevCatalog*)(cbase + C.B->o_cats);
-  a.n_catalogs = (int32_t)C.B->cats.size();
-  a.vint = (const int64_t*)(cbase + C.B->o_vint);
-  a.n_pods = P;
-  a.pod_shape = (const int32_t*)(base + o_pod_shape);
-  a.pod_level = (int32_t*)(base + o_pod_level);
-  a.queue = (int32_t*)(base + o_queue);
-  a.lastlen = (int32_t*)(base + o_lastlen);
-  a.lastlen_epoch = (int32_t*)(base + o_lastlen_ep);
-  a.shape_level_base = (const int32_t*)(base + o_slb);
-  a.shape_nlevels = (const int32_t*)(base + o_snl);
-  a.shape_reqs = base + o_sreqs;
-  a.shape_negop = (const uint64_t*)(base + o_sneg);
-  a.shape_requests = (const int64_t*)(base + o_sreq);
-  a.shape_tolerates = (const uint64_t*)(base + o_stol);
-  a.shape_pvp = (const uint64_t*)(base + o_pvp);
-  a.pvp_base = (const int32_t*)(base + o_pvpb);
-  a.pvp_slot = (const int32_t*)(base + o_pvps);
-  a.sl_pvp_n = (const int32_t*)(base + o_pvpn);
-  a.n_tmpl = NT;
-  a.tmpl_reqs = cbase + C.B->o_treqs;
-  a.tmpl_taintset = (const int32_t*)(cbase + C.B->o_tts);
-  a.tmpl_catalog = (const int32_t*)(cbase + C.B->o_tcat);
-  a.tmpl_X = (const uint64_t*)(cbase + C.B->o_tX);
-  a.tmpl_daemon = (const int64_t*)(cbase + C.B->o_tdm);
-  a.tmpl_limit_present = (const uint32_t*)(base + o_tlp);
-  a.tmpl_remaining = (int64_t*)(base + o_trem);
-  a.n_existing = E;
-  a.ex_reqs = base + o_exr;
-  a.ex_taintset = (const int32_t*)(base + o_exts);
-  a.ex_available = (const int64_t*)(base + o_exav);
-  a.ex_requests = (int64_t*)(base + o_exrq);
-  a.ex_room = (int64_t*)(base + o_exroom);
-  a.nc_reqs = base + o_ncr;
-  a.nc_X = (uint64_t*)(base + o_ncX);
-  a.nc_requests = (int64_t*)(base + o_ncrq);
-  a.nc_tmpl = (int32_t*)(base + o_nct);
-  a.g_npods = (int32_t*)(base + o_npods);
-  a.g_order = (int32_t*)(base + o_order);
-  a.sort_in_lds = 1;
-  a.sort_cap = sort_cap;
-  a.ncc = ncc;
-  a.chk_blk = (ChkBlk*)(base + o_chkblk);
-  a.chk_dead = (int32_t*)(base + o_chkdead);
-  a.chk_dead_rows = chk_dead_rows;
-  a.chk_maxc = chk_on ? CHK_MAXC : 0;
-  if (const char* e = getenv("KP_CHK_MAXC")) a.chk_maxc = chk_on ? std::max(0, std::min(CHK_MAXC, atoi(e))) : 0;  // test hook
-  a.nc_head = (NcHead*)(((uintptr_t)(base + o_nchead) + 63) & ~(uintptr_t)63);
-  a.nc_fail = (int32_t*)(base + o_ncfail);
-  a.ex_ver = (int32_t*)(base + o_exver);
-  a.ex_fail = (int32_t*)(base + o_exfail);
-  a.tmpl_ver = (int32_t*)(base + o_tver);
-  a.tmpl_fail = (int32_t*)(base + o_tfail);
-  a.cur_nc = (int32_t*)(base + o_curnc);
-  a.cur_ex = (int32_t*)(base + o_curex);
-  a.nc_maxalloc = (int64_t*)(base + o_maxalloc);
-  a.nc_fitj = (int32_t*)(base + o_fitj);
-  a.nc_cat = (int32_t*)(base + o_nccat);
-  a.hp_any = C.hp_any ? 1 : 0;
-  a.shape_hp_conf = (const uint64_t*)(base + o_shpc);
-  a.shape_hp_add = (const uint64_t*)(base + o_shpa);
-  a.ex_hp = (uint64_t*)(base + o_exhp);
-  a.nc_hp = (uint64_t*)(base + o_nchp);
-  a.req_res_mask = 0;
-  for (size_t i = 0; i < C.shape_requests.size(); i++)
-    if (C.shape_requests[i] > 0) a.req_res_mask |= 1u << (i % KP_NRES);
-  for (size_t i = 0; i < C.B->tmpl_daemon.size(); i++)  // Fits iterates every resource of the merged requests
-    if (C.B->tmpl_daemon[i] > 0) a.req_res_mask |= 1u << (i % KP_NRES);
-  a.n_req_res = __builtin_popcount(a.req_res_mask);
-  a.timing = getenv("KP_TIMING") ? 1 : 0;
-  a.n_groups = C.G;
-  a.tg_key = (const int32_t*)(base + o_tgk);
-  a.tg_row = (const int32_t*)(base + o_tgr);
-  a.tg_maxskew = (const int32_t*)(base + o_tgs);
-  a.tg_mindom = (const int32_t*)(base + o_tgm);
-  a.tg_aff = (const int32_t*)(base + o_tga);
-  a.tg_term_base = (const int32_t*)(base + o_tgtb);
-  a.tg_filt_tol = (const uint64_t*)(base + o_tgft);
-  a.tg_terms = base + o_tgt;
-  a.tg_terms_negop = (const uint64_t*)(base + o_tgtn);
-  a.tg_cnt = (int32_t*)(base + o_tgc);
-  a.tg_live = (int32_t*)(base + o_tglv);
-  a.tg_nterm = (const int32_t*)(base + o_tgnt);
-  a.tg_reg = (uint64_t*)(base + o_tgreg);
-  a.hcnt_ex = base + o_hcx;
-  a.hcnt_nc = base + o_hcnc;
-  a.hnc_stride = Pc;
-  a.shape_rec_base = (const int32_t*)(base + o_srb);
-  a.shape_rec_n = (const int32_t*)(base + o_srn);
-  a.rec_list = (const int32_t*)(base + o_recl);
-  a.rec_aux = (const int32_t*)(base + o_recx);
-  a.sl_fast_topo = (const int32_t*)(base + o_slft);
-  a.sl_own_base = (const int32_t*)(base + o_slob);
-  a.sl_own_n = (const int32_t*)(base + o_slon);
-  a.own_group = (const int32_t*)(base + o_owng);
-  a.own_self = (const int32_t*)(base + o_owns);
-  a.own_pd = (const uint64_t*)(base + o_ownp);
-  a.own_rec = (const int4*)(base + o_ownr);
-  a.sl_topo_keys = (const uint64_t*)(base + o_sltk);
-  a.tkey_slot = (const int32_t*)(base + o_tks);
-  a.n_tk = C.TK;
-  a.tk_keys = (const int32_t*)(base + o_tkk);
-  a.nc_tcode = base + o_nctc;
-  a.ex_static_ok = base + o_exso;
-  a.ex_tcode = base + o_extc;
-  plan->o_hcnc = o_hcnc;
-  plan->n_hcnc = n_hcnc;
-  a.placement = (int32_t*)(base + o_place);
-  a.events = (int32_t*)(base + o_events);
-  a.stats = (uint64_t*)(base + o_stats);
-  a.res_mode = !C.B->res_cls ? 0 : in->reserved_offering_mode == KP_RESERVED_STRICT ? 2 : 1;
-  a.res_cls = C.B->res_cls;
-  a.nc_held = (uint64_t*)(base + o_held);
-  for (int c = 0; c < KP_MAX_CLASSES; c++) a.res_cap0[c] = C.B->res_cap0.empty() ? 0 : C.B->res_cap0[c];
-  plan->o_held = o_held;
+  const int res_mode = !C.B->res_cls ? 0 : in->reserved_offering_mode == KP_RESERVED_STRICT ? 2 : 1;
+  BindSolve(a, C, o, base, base, P, Pc, rmask, res_mode);
+  plan->o_hcnc = o.hcnc;
+  plan->n_hcnc = o.n_hcnc;
+  plan->o_held = o.held;
   if (tfeas_on) {  // this rank's rows of the template-options table, then one all-gather (RCCL) of every rank's rows
-    TfeasArgs f;
-    memset(&f, 0, sizeof f);
-    f.dict = a.dict;
-    f.cats = a.cats;
-    f.n_catalogs = a.n_catalogs;
-    f.vint = a.vint;
-    f.n_tmpl = NT;
-    f.tmpl_reqs = a.tmpl_reqs;
-    f.tmpl_catalog = a.tmpl_catalog;
-    f.tmpl_X = a.tmpl_X;
-    f.tmpl_daemon = a.tmpl_daemon;
-    f.shape_reqs = a.shape_reqs;
-    f.shape_negop = a.shape_negop;
-    f.sl_shape = (const int32_t*)(base + o_slsh);
-    f.shape_requests = a.shape_requests;
-    f.shape_pvp = a.shape_pvp;
-    f.pvp_base = a.pvp_base;
-    f.pvp_slot = a.pvp_slot;
-    f.sl_own_n = a.sl_own_n;
-    f.req_res_mask = a.req_res_mask;
+    plan->tf = TfeasOf(a, base, o, SLi, tf_words);
+    plan->tfeas_on = true;
+    TfeasArgs f = plan->tf;
     f.row_lo = std::min(SLi, my_rank * rows_per_rank);
     f.row_hi = std::min(SLi, (my_rank + 1) * rows_per_rank);
-    f.words = tf_words;
-    f.out = (uint64_t*)(base + o_tfeas);
-    plan->tf = f;
-    plan->tf.row_lo = 0;
-    plan->tf.row_hi = SLi;
-    plan->tfeas_on = true;
     HIPCHK(launch_tmpl_feas(f, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     if (shard) {  // the all-gather of every rank's rows follows in SolvePrepare, after the ranks' status exchange
       gather_chunk = (size_t)rows_per_rank * NT * tf_words * sizeof(uint64_t);
-      gather_off = o_tfeas;
+      gather_off = o.tfeas;
     }
-    a.tfeas = (const uint64_t*)(base + o_tfeas);
+    a.tfeas = (const uint64_t*)(base + o.tfeas);
     a.tfeas_words = tf_words;
   }
 
-  plan->o_ver = o_ver0;
-  plan->n_ver = n_ver;
-  plan->o_fail = o_fail0;
-  plan->n_fail = n_fail;
-  plan->o_mut = o_mut;
+  plan->o_ver = o.ver0;
+  plan->n_ver = o.ver_end - o.ver0;
+  plan->o_fail = o.fail0;
+  plan->n_fail = o.fail_end - o.fail0;
+  plan->o_mut = o.mut;
   plan->n_mut = n_mut;
-  plan->o_pristine = o_pristine;
-  plan->o_stats = o_stats;
-  plan->o_npods = o_npods;
-  plan->o_place = o_place;
-  plan->o_events = o_events;
-  plan->o_nct = o_nct;
-  plan->o_ncrq = o_ncrq;
-  plan->o_opts = o_opts;
-  plan->o_nrem = o_nrem;
-  plan->o_nopt = o_nopt;
-  plan->o_ncr = o_ncr;
+  plan->o_pristine = o.pristine;
+  plan->o_stats = o.stats;
+  plan->o_npods = o.npods;
+  plan->o_place = o.place;
+  plan->o_events = o.events;
+  plan->o_nct = o.nct;
+  plan->o_ncrq = o.ncrq;
+  plan->o_opts = o.opts;
+  plan->o_nrem = o.nrem;
+  plan->o_nopt = o.nopt;
+  plan->o_ncr = o.ncr;
   plan->opt_stride = opt_stride;
   plan->base_version = C.B->version;
   return KP_OK;
@@ -3280,6 +3419,7 @@ int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out) {
                             (unsigned long long)stats[2]);
   const int n_nc = (int)stats[3];
   FinalizeArgs f;
+  f.solve_stats = nullptr;
   f.dict = a.dict;
   f.cats = a.cats;
   f.vint = a.vint;
@@ -4119,10 +4259,15 @@ struct OwnedCluster {
   }
 };
 
+struct GeneralBatch;
 struct kp_cluster_plan {
   kp_ctx* ctx = nullptr;
   std::unique_ptr<OwnedCluster> general;  // set: simulations run as whole Solves (kp_solve on this device)
   double general_ms = 0;                  // device time of the last general batch (solve + finalize kernels)
+  std::shared_ptr<GeneralBatch> gb;       // the general path's superset Solve (batched simulations), once built
+  vector<std::map<string, string>> general_labels;
+  bool gb_tried = false;
+  uint32_t general_batched = 0;           // simulations of the last general batch that ran batched
   std::unique_ptr<Compiled> cp;
   DevBuf buf;                       // resident snapshot
   DevBuf scratch;                   // per-wave state, grown on demand
@@ -4606,6 +4751,621 @@ double WorstLaunch(const Dict& d, const KReqs& R, const HostType& t, bool spot_o
 
 static int32_t SolvePrepare(kp_ctx* ctx, const kp_solve_in* in, kp_comm* comm, kp_solve_plan** out);
 
+// computeConsolidation's decision on one simulation's Solve (sim_kernel's decision; disruption.md:89-128). all: every
+// non-pending pod was scheduled (and no candidate pod onto an uninitialized node). The Solve made n_nc NodeClaims;
+// R / ci / nodepool / opts: the first one's final requirements (held reservation ids applied), catalogue, NodePool and
+// price-ordered options (after Truncate), minValues not yet checked on them.
+static void GeneralDecide(const kp_cluster& cl, const vector<std::map<string, string>>& labels,
+                          const vector<uint32_t>& cand, const SolveBase& B, bool all, int n_nc, const KReqs* R,
+                          int ci, uint32_t nodepool, const uint32_t* opts, uint32_t n_opts, int32_t multi_node,
+                          SimOut& r) {
+  double candPrice = 0;
+  bool priced = true, allSpot = true;
+  for (uint32_t c : cand) {
+    const kp_cluster_node& n = cl.nodes[c];
+    double p = 0;
+    if (!NodeCandidatePrice(cl.catalogs[n.catalog]->types[n.instance_type], labels[c], &p)) priced = false;
+    candPrice += p;
+    auto f = labels[c].find(kCapType);
+    if (f == labels[c].end() || f->second != "spot") allSpot = false;
+  }
+  r.candidate_price = priced ? candPrice : 0;
+  if (!all) return;  // no-op
+  if (n_nc == 0) {
+    r.decision = KP_DECISION_DELETE;
+    r.savings = r.candidate_price;
+    return;
+  }
+  if (n_nc != 1 || !priced) return;
+  const Dict& d = B.d;
+  const vector<HostType>& types = cl.catalogs[ci]->types;
+  const HostCat& hc = B.cats[ci];
+  const bool hasMin = (R->hmin & R->present) != 0;
+  if (hasMin) {  // Truncate(reqs, max): minValues must hold on the truncated options, else its pods fail (no-op)
+    vector<int> ts(opts, opts + n_opts);
+    if (!HostMinValuesOK(d, hc, *R, ts)) return;
+  }
+  const int kct = d.key(kCapType), bspot = kct >= 0 ? d.bit(kct, "spot") : -1;
+  const bool ncSpot = kct < 0 || !((R->present >> kct) & 1) || (bspot >= 0 ? Has(d, *R, kct, bspot) : ((R->compl_ >> kct) & 1));
+  const bool s2s = allSpot && ncSpot;  // spot-to-spot: only behind the feature gate
+  if (s2s && !cl.spot_to_spot) return;
+  vector<int> kept;
+  for (uint32_t i = 0; i < n_opts; i++)
+    if (WorstLaunch(d, *R, types[opts[i]], s2s) < candPrice) kept.push_back((int)opts[i]);
+  if (hasMin && !HostMinValuesOK(d, hc, *R, kept)) return;
+  if (kept.empty()) return;
+  if (multi_node) {  // filterOutSameType
+    std::map<string, double> prices;
+    for (uint32_t c : cand) {
+      const kp_cluster_node& n = cl.nodes[c];
+      const HostType& it = cl.catalogs[n.catalog]->types[n.instance_type];
+      double p = 0;
+      if (!NodeCandidatePrice(it, labels[c], &p)) continue;
+      auto f = prices.find(it.name);
+      if (f == prices.end() || p < f->second) prices[it.name] = p;
+    }
+    double maxPrice = std::numeric_limits<double>::max();
+    for (int t : kept) {
+      auto f = prices.find(types[t].name);
+      if (f != prices.end() && f->second < maxPrice) maxPrice = f->second;
+    }
+    vector<int> k2;
+    for (int t : kept)
+      if (WorstLaunch(d, *R, types[t], s2s) < maxPrice) k2.push_back(t);
+    if (hasMin && !HostMinValuesOK(d, hc, *R, k2)) return;
+    kept.swap(k2);
+    if (kept.empty()) return;
+  }
+  if (s2s && cand.size() == 1) {
+    if (kept.size() < 15) return;
+    kept.resize(std::min<size_t>(kept.size(), hasMin ? 100 : 15));
+  }
+  double best = std::numeric_limits<double>::max();
+  for (int t : kept) best = std::min(best, WorstLaunch(d, *R, types[t], s2s));
+  r.decision = KP_DECISION_REPLACE;
+  r.nodepool = nodepool;
+  r.replacement_price = best;
+  r.savings = candPrice - best;
+  r.n_options = (uint32_t)kept.size();
+}
+
+// FinalizeScheduling: a NodeClaim holding reservations launches only into them (reservation-id In {held ids})
+static void ApplyHeld(const SolveBase& B, uint64_t held, KReqs& q) {
+  if (!held) return;
+  const Dict& d = B.d;
+  const int k = d.key(kResID);
+  for (int wi = 0; wi < nwords(d, k); wi++) q.vals[kw(d, k, wi)] = 0;
+  for (uint64_t m = held; m; m &= m - 1) {
+    const int bit = B.classes[__builtin_ctzll(m)].rid_bit;
+    q.vals[bit / 64] |= 1ull << (bit % 64);
+  }
+  q.present |= 1ull << k;
+  q.compl_ &= ~(1ull << k);
+}
+
+// One subset's SimulateScheduling as its own Solve: compiled on the host from the subset's inputs (the path for
+// subsets the batch cannot take, and the whole path with KP_GENERAL_BATCH=0).
+static int32_t GeneralSimOne(kp_cluster_plan* plan, const vector<uint32_t>& cand, const vector<std::map<string, string>>& labels,
+                             int32_t multi_node, SimOut& r, uint64_t* counters, double* dev_ms) {
+  kp_ctx* ctx = plan->ctx;
+  const kp_cluster& cl = plan->general->cl;
+  const int N = (int)cl.n_nodes;
+  vector<char> inS(N, 0);
+  for (uint32_t c : cand) inS[c] = 1;
+  vector<kp_existing_node> ex;
+  vector<int> exNode;
+  for (int i = 0; i < N; i++)
+    if (!inS[i] && !cl.nodes[i].deleting) {
+      ex.push_back(cl.nodes[i].node);
+      exNode.push_back(i);
+    }
+  vector<kp_pod> pods;
+  vector<int> kind;  // 0 candidate pod, 1 deleting-node pod, 2 pending
+  for (uint32_t j = 0; j < cl.n_pending; j++) {
+    if (cl.pending_pods[j] >= cl.n_pods) return fail(KP_E_INVAL, "pending pod %u", cl.pending_pods[j]);
+    pods.push_back(cl.pods[cl.pending_pods[j]]);
+    kind.push_back(2);
+  }
+  for (int i = 0; i < N; i++)
+    if (cl.nodes[i].deleting)
+      for (uint32_t j = 0; j < cl.nodes[i].n_pods; j++) {
+        pods.push_back(cl.pods[cl.nodes[i].pods[j]]);
+        kind.push_back(1);
+      }
+  for (uint32_t c : cand)
+    for (uint32_t j = 0; j < cl.nodes[c].n_pods; j++) {
+      pods.push_back(cl.pods[cl.nodes[c].pods[j]]);
+      kind.push_back(0);
+    }
+  vector<kp_bound_pod> bound;
+  for (size_t e = 0; e < exNode.size(); e++) {
+    const kp_cluster_node& n = cl.nodes[exNode[e]];
+    for (uint32_t j = 0; j < n.n_pods; j++) {
+      const uint32_t p = n.pods[j];
+      if (p >= cl.n_pods || cl.pods[p].shape >= cl.n_shapes) return fail(KP_E_INVAL, "node %d: pod %u", exNode[e], p);
+      const kp_pod_shape& sh = cl.shapes[cl.pods[p].shape];
+      bound.push_back({sh.namespace_, sh.labels, sh.n_labels, (uint32_t)e, sh.required_anti_affinity,
+                       sh.n_required_anti_affinity, 0});
+    }
+  }
+  r.n_pods = (uint32_t)pods.size();
+  kp_solve_in in;
+  memset(&in, 0, sizeof in);
+  in.catalogs = cl.catalogs;
+  in.n_catalogs = cl.n_catalogs;
+  in.n_nodepools = cl.n_nodepools;
+  in.nodepools = cl.nodepools;
+  in.existing = ex.data();
+  in.n_existing = (uint32_t)ex.size();
+  in.n_shapes = cl.n_shapes;
+  in.shapes = cl.shapes;
+  in.pods = pods.data();
+  in.n_pods = (uint32_t)pods.size();
+  in.max_instance_types = 100;
+  in.bound_pods = bound.data();
+  in.n_bound_pods = (uint32_t)bound.size();
+  in.namespaces = cl.namespaces;
+  in.n_namespaces = cl.n_namespaces;
+  in.reserved_offering_mode = KP_RESERVED_STRICT;  // SimulateScheduling: NewScheduler(..., DisableReservedCapacityFallback)
+  kp_solve_plan* sp = nullptr;
+  int32_t rc = SolvePrepare(ctx, &in, nullptr, &sp);
+  if (rc) return rc;
+  std::unique_ptr<kp_solve_plan, void (*)(kp_solve_plan*)> spg(sp, kp_solve_plan_destroy);
+  kp_solve_result* res = nullptr;
+  rc = kp_solve_run(sp, &res);
+  if (rc) return rc;
+  std::unique_ptr<kp_solve_result, void (*)(kp_solve_result*)> rg(res, kp_result_destroy);
+  counters[0] += res->stats.attempts;
+  counters[1] += res->stats.bytes_algorithmic;
+  counters[2] += res->stats.pops;
+  *dev_ms += res->stats.device_ms;
+  // AllNonPendingPodsScheduled; a candidate pod on an uninitialized node is an error (deleting-node pods exempt)
+  bool all = true;
+  for (size_t p = 0; p < pods.size() && all; p++) {
+    const int32_t pl = res->placement[p];
+    if (kind[p] == 2) continue;
+    if (pl == -1) all = false;
+    else if (kind[p] == 0 && pl <= -2 && !ex[(size_t)(-2 - pl)].initialized) all = false;
+  }
+  const int n_nc = (int)res->ncs.size();
+  // (kp_solve_run already applied the held reservations and the minValues truncation check to NodeClaim 0)
+  GeneralDecide(cl, labels, cand, *sp->cp->B, all, n_nc, n_nc ? &res->fin[0] : nullptr, n_nc ? res->nc_cat[0] : 0,
+                n_nc ? res->ncs[0].nodepool : 0, n_nc ? res->ncs[0].options.data() : nullptr,
+                n_nc ? (uint32_t)res->ncs[0].options.size() : 0, multi_node, r);
+  return KP_OK;
+}
+
+// ---- batched general simulations ------------------------------------------------------------------------------
+// Compiling each subset's Solve on the host walks every node and every bound pod (~18 ms per subset at 2000 nodes).
+// Instead the cluster is compiled once as the superset Solve - every node not being deleted is an existing node,
+// every pod a simulation can queue (pending, deleting nodes', every node's) is in its pod list - with each node's
+// contribution to the topology state recorded (Compiled::track_nodes). A subset's Solve is that Solve with:
+//   * the subset's nodes excluded from placement (ex_static_ok 0) - the other nodes keep their relative order;
+//   * its queue: the pending and deleting-node pods plus the subset's pods, in the superset's queue order (the same
+//     keys: shape rank, creation, UID);
+//   * the bound pods on its nodes removed from the topology counts and registered domains (Topology.countDomains
+//     over the remaining nodes), hostname rows' "some domain has a count" recomputed;
+//   * the spread groups' liveness recomputed from the shapes it queues (NewTopology creates the groups of queued
+//     pods), and hostname groups that stop being live at creation get their unregistered nodes (255) back.
+// Subsets whose removal would make an inverse anti-affinity group vanish take the per-subset compile. Every
+// simulation of a batch is one workgroup of one solve_kernel launch (its own arena: mutable state + scratch).
+struct GeneralBatch {
+  std::unique_ptr<Compiled> C;
+  uint64_t base_version = 0;
+  vector<int32_t> node_input;   // cluster node -> existing input index of the superset (-1: being deleted)
+  vector<int32_t> node_sorted;  // cluster node -> position in the Solve's existing order (-1)
+  vector<int32_t> pos_node;     // existing position -> cluster node
+  vector<int32_t> pod_qpos;     // superset pod -> queue position
+  vector<int32_t> pod_shape;    // superset pod -> shape
+  vector<int32_t> base_pods;    // superset pods every simulation queues (pending, deleting nodes'), queue order
+  vector<uint8_t> pod_kind;     // superset pod -> 2 pending, 1 deleting node's, 0 a node's
+  vector<vector<int32_t>> node_pods;  // cluster node -> its superset pods
+  vector<uint8_t> ex_static;
+  vector<int32_t> regcnt;       // [G * 64] existing nodes registering each (group, ordinal)
+  vector<int32_t> live0;        // [G] liveness with only the base pods queued
+  uint32_t rmask = 0;
+  int res_mode = 0, opt_stride = 100, tf_words = 0;
+  bool tfeas_on = false;
+  SolveOffs so;                 // shared-region offsets
+  DevBuf shared;
+  // per arena size (Pc): the layout, the host template of [0, mut_end) and the device copy of [common, mut_end)
+  int Pc = 0;
+  SolveOffs o;
+  size_t stride = 0;
+  vector<uint8_t> tmpl;
+  DevBuf pristine;
+  DevBuf arenas, args;
+  size_t arenas_bytes = 0, args_bytes = 0;
+};
+
+// The superset Solve of a cluster (kp_cluster_plan: general). KP_E_UNSUPPORTED: the batch cannot take this cluster
+// (the caller keeps the per-subset compile).
+static int32_t GeneralBatchBuild(kp_cluster_plan* plan, std::shared_ptr<GeneralBatch>& out) {
+  kp_ctx* ctx = plan->ctx;
+  const kp_cluster& cl = plan->general->cl;
+  const int N = (int)cl.n_nodes;
+  auto gb = std::make_shared<GeneralBatch>();
+  vector<kp_existing_node> ex;
+  vector<kp_pod> pods;
+  vector<kp_bound_pod> bound;
+  gb->node_input.assign(N, -1);
+  gb->node_pods.assign(N, {});
+  for (uint32_t j = 0; j < cl.n_pending; j++) {
+    if (cl.pending_pods[j] >= cl.n_pods) return fail(KP_E_INVAL, "pending pod %u", cl.pending_pods[j]);
+    pods.push_back(cl.pods[cl.pending_pods[j]]);
+    gb->pod_kind.push_back(2);
+  }
+  for (int i = 0; i < N; i++)
+    if (cl.nodes[i].deleting)
+      for (uint32_t j = 0; j < cl.nodes[i].n_pods; j++) {
+        pods.push_back(cl.pods[cl.nodes[i].pods[j]]);
+        gb->pod_kind.push_back(1);
+      }
+  const int n_base = (int)pods.size();
+  for (int i = 0; i < N; i++) {
+    if (cl.nodes[i].deleting) continue;
+    const uint32_t e = (uint32_t)ex.size();
+    gb->node_input[i] = (int32_t)e;
+    ex.push_back(cl.nodes[i].node);
+    for (uint32_t j = 0; j < cl.nodes[i].n_pods; j++) {
+      const uint32_t p = cl.nodes[i].pods[j];
+      if (p >= cl.n_pods || cl.pods[p].shape >= cl.n_shapes) return fail(KP_E_INVAL, "node %d: pod %u", i, p);
+      const kp_pod_shape& sh = cl.shapes[cl.pods[p].shape];
+      bound.push_back({sh.namespace_, sh.labels, sh.n_labels, e, sh.required_anti_affinity, sh.n_required_anti_affinity, 0});
+      gb->node_pods[i].push_back((int32_t)pods.size());
+      pods.push_back(cl.pods[p]);
+      gb->pod_kind.push_back(0);
+    }
+  }
+  {  // queue ties broken by pod index would order differently per subset: only distinct (creation, UID) keys
+    vector<std::pair<int64_t, uint64_t>> keys;
+    for (auto& p : pods) keys.push_back({p.creation_unix, p.uid_key});
+    std::sort(keys.begin(), keys.end());
+    if (std::adjacent_find(keys.begin(), keys.end()) != keys.end())
+      return fail(KP_E_UNSUPPORTED, "pods with equal (creation, UID) keys");
+  }
+  kp_solve_in in;
+  memset(&in, 0, sizeof in);
+  in.catalogs = cl.catalogs;
+  in.n_catalogs = cl.n_catalogs;
+  in.n_nodepools = cl.n_nodepools;
+  in.nodepools = cl.nodepools;
+  in.existing = ex.data();
+  in.n_existing = (uint32_t)ex.size();
+  in.n_shapes = cl.n_shapes;
+  in.shapes = cl.shapes;
+  in.pods = pods.data();
+  in.n_pods = (uint32_t)pods.size();
+  in.max_instance_types = 100;
+  in.bound_pods = bound.data();
+  in.n_bound_pods = (uint32_t)bound.size();
+  in.namespaces = cl.namespaces;
+  in.n_namespaces = cl.n_namespaces;
+  in.reserved_offering_mode = KP_RESERVED_STRICT;
+  gb->C = std::make_unique<Compiled>();
+  Compiled& C = *gb->C;
+  C.track_nodes = true;
+  int32_t rc = CompileSolve(&in, C, ctx);
+  if (rc) return rc;
+  if (!C.track_nodes) return fail(KP_E_INVAL, "superset compile lost its node tracking");
+  rc = EnsureBaseOnDevice(ctx, *C.B);
+  if (rc) return rc;
+  gb->base_version = C.B->version;
+  const int E = (int)C.ex_input.size(), G = C.G, P = (int)pods.size();
+  gb->node_sorted.assign(N, -1);
+  gb->pos_node.assign(E, -1);
+  vector<int32_t> input_node(E, -1);
+  for (int i = 0; i < N; i++)
+    if (gb->node_input[i] >= 0) input_node[gb->node_input[i]] = i;
+  for (int e = 0; e < E; e++) {
+    gb->pos_node[e] = input_node[C.ex_input[e]];
+    gb->node_sorted[gb->pos_node[e]] = e;
+  }
+  gb->pod_qpos.assign(P, 0);
+  gb->pod_shape = C.pod_shape;
+  for (int q = 0; q < P; q++) gb->pod_qpos[C.queue[q]] = q;
+  for (int q = 0; q < P; q++)
+    if (C.queue[q] < n_base) gb->base_pods.push_back(C.queue[q]);
+  if (G) {
+    if (C.node_cnt.size() != (size_t)E || C.tg_spread.size() != (size_t)G || C.shape_l0.size() != cl.n_shapes)
+      return fail(KP_E_INVAL, "superset topology tracking incomplete");
+    gb->regcnt.assign((size_t)G * 64, 0);
+    for (auto& v : C.node_reg)
+      for (int32_t x : v) gb->regcnt[x]++;
+    gb->live0.assign(G, 0);
+    for (int g = 0; g < G; g++) gb->live0[g] = C.tg_live[g] && !C.tg_spread[g];
+    vector<char> seen(cl.n_shapes, 0);
+    for (int p : gb->base_pods) {
+      const int s = C.pod_shape[p];
+      if (seen[s]) continue;
+      seen[s] = 1;
+      for (int32_t g : C.shape_l0[s]) gb->live0[g] = 1;
+    }
+  }
+  gb->rmask = RequestedResources(C);
+  gb->ex_static = ExStatic(C, gb->rmask);
+  gb->res_mode = !C.B->res_cls ? 0 : 2;
+  gb->opt_stride = 100;
+  // the shared region: read-only data of every simulation + the template-options table
+  Blob blob;
+  PutShared(blob, C, gb->so);
+  const size_t host_bytes = blob.host.size();
+  const int NT = (int)C.B->tmpl_reqs.size(), SLi = (int)C.shape_reqs.size();
+  gb->tfeas_on = NT > 0 && SLi > 0 && getenv("KP_NO_TFEAS") == nullptr;
+  gb->tf_words = C.B->TW + KP_NRES / 2 + 1;
+  gb->so.tfeas = blob.reserve_dev(gb->tfeas_on ? (size_t)SLi * NT * gb->tf_words * sizeof(uint64_t) : 8);
+  HIPCHK(gb->shared.alloc(blob.total()));
+  uint8_t* sh = (uint8_t*)gb->shared.p;
+  HIPCHK(hipMemcpyAsync(sh, blob.host.data(), host_bytes, hipMemcpyHostToDevice, ctx->stream));
+  if (gb->tfeas_on) {
+    SolveArgs a;
+    BindSolve(a, C, gb->so, sh, sh, 0, 1, gb->rmask, gb->res_mode);
+    HIPCHK(launch_tmpl_feas(TfeasOf(a, sh, gb->so, SLi, gb->tf_words), ctx->stream));
+  }
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  out = gb;
+  return KP_OK;
+}
+
+// The arena layout for simulations of up to Pc pods: host template + the device copy of the common mutable part.
+static int32_t GeneralBatchLayout(kp_ctx* ctx, GeneralBatch& gb, int Pc) {
+  if (gb.Pc == Pc) return KP_OK;
+  const Compiled& C = *gb.C;
+  SolveOffs o = gb.so;
+  Blob blob;
+  const vector<int32_t> zeros(Pc, 0);
+  PutArena(blob, C, zeros, zeros, Pc, gb.ex_static, gb.rmask, o);
+  ReserveArenaDev(blob, C, Pc, gb.opt_stride, std::min(SortCapacity(), Pc), false, o);
+  gb.tmpl.assign(blob.host.begin(), blob.host.begin() + o.mut_end);
+  gb.stride = (o.arena_end + 255) & ~(size_t)255;
+  HIPCHK(gb.pristine.alloc(o.mut_end - o.common + 16));
+  HIPCHK(hipMemcpyAsync(gb.pristine.p, gb.tmpl.data() + o.common, o.mut_end - o.common, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  gb.o = o;
+  gb.Pc = Pc;
+  return KP_OK;
+}
+
+// One simulation's per-subset inputs: its queue (superset pods) and the patch of [0, common) of its arena. Returns 1
+// when the batch cannot take the subset (an inverse anti-affinity group would vanish).
+struct GenScratch {
+  vector<int32_t> inv, hdec, regdec, touched;
+  vector<char> shape_seen;
+};
+static int GeneralPatch(const GeneralBatch& gb, const kp_cluster& cl, const vector<uint32_t>& cand, GenScratch& s,
+                        vector<int32_t>& queue, uint8_t* patch) {
+  const Compiled& C = *gb.C;
+  const int G = C.G, E = (int)C.ex_input.size();
+  if (G) {  // an inverse group whose every owner sits on the subset's nodes does not exist in its Solve
+    s.inv.assign(G, 0);
+    bool vanish = false;
+    for (uint32_t c : cand)
+      for (int32_t g : C.node_inv[gb.node_input[c]])
+        if (++s.inv[g] == C.tg_inv_total[g]) vanish = true;
+    if (vanish) return 1;
+  }
+  queue = gb.base_pods;
+  const size_t nb = queue.size();
+  for (uint32_t c : cand) queue.insert(queue.end(), gb.node_pods[c].begin(), gb.node_pods[c].end());
+  auto byq = [&](int32_t x, int32_t y) { return gb.pod_qpos[x] < gb.pod_qpos[y]; };
+  std::sort(queue.begin() + nb, queue.end(), byq);
+  std::inplace_merge(queue.begin(), queue.begin() + nb, queue.end(), byq);
+  const SolveOffs& o = gb.o;
+  memcpy(patch, gb.tmpl.data(), o.common);
+  int32_t* ps = (int32_t*)(patch + o.pod_shape);
+  int32_t* qu = (int32_t*)(patch + o.queue);
+  for (size_t i = 0; i < queue.size(); i++) {
+    ps[i] = gb.pod_shape[queue[i]];
+    qu[i] = (int32_t)i;
+  }
+  uint8_t* exso = patch + o.exso;
+  for (uint32_t c : cand) exso[gb.node_sorted[c]] = 0;
+  if (!G) return 0;
+  int32_t* cnt = (int32_t*)(patch + o.tgc);
+  int32_t* live = (int32_t*)(patch + o.tglv);
+  uint64_t* reg = (uint64_t*)(patch + o.tgreg);
+  uint8_t* hcx = patch + o.hcx;
+  s.regdec.resize((size_t)G * 64);
+  s.hdec.assign(G, 0);
+  s.touched.clear();
+  for (uint32_t c : cand) {
+    const int e = gb.node_input[c];
+    for (int32_t x : C.node_cnt[e]) cnt[x]--;
+    for (int32_t x : C.node_reg[e]) {
+      if (s.regdec[x]++ == 0) s.touched.push_back(x);
+    }
+    for (int32_t g : C.node_hrec[e]) s.hdec[g]++;
+  }
+  for (int32_t x : s.touched) {
+    const int g = x / 64, ord = x % 64;
+    if (s.regdec[x] == gb.regcnt[x] && !((C.tg_reg_static[g] >> ord) & 1)) reg[g] &= ~(1ull << ord);
+    s.regdec[x] = 0;
+  }
+  for (int g = 0; g < G; g++)
+    if (s.hdec[g] && s.hdec[g] == C.tg_hrec_total[g]) reg[g] &= ~1ull;  // hostname row: no domain has a count
+  // liveness: the base pods' shapes, then the subset's
+  for (int g = 0; g < G; g++) live[g] = gb.live0[g];
+  s.shape_seen.assign(cl.n_shapes, 0);
+  for (size_t i = nb; i < queue.size(); i++) {
+    const int sh = gb.pod_shape[queue[i]];
+    if (s.shape_seen[sh]) continue;
+    s.shape_seen[sh] = 1;
+    for (int32_t g : C.shape_l0[sh]) live[g] = 1;
+  }
+  for (int g = 0; g < G; g++)  // a hostname spread group created not live: its unregistered nodes hold 255
+    if (C.tg_live[g] && !live[g] && C.tg_spread[g] && C.tg_row[g] >= 0)
+      for (int32_t pos : C.tg_unreg[g]) hcx[(size_t)C.tg_row[g] * E + pos] = 255;
+  return 0;
+}
+
+// Runs the batchable subsets `idx` (their candidate lists in cands) as batched Solves; outs[idx[i]] get the decisions.
+static int32_t GeneralBatchRun(kp_cluster_plan* plan, GeneralBatch& gb, const vector<vector<uint32_t>>& cands,
+                               const vector<int>& idx, const vector<std::map<string, string>>& labels, int32_t multi_node,
+                               vector<SimOut>& outs, uint64_t* counters, double* dev_ms, double* host_ms) {
+  kp_ctx* ctx = plan->ctx;
+  const kp_cluster& cl = plan->general->cl;
+  const Compiled& C = *gb.C;
+  hipStream_t st = ctx->stream;
+  // the arena size: every simulation of the batch fits (rounded up, so that nearby batches share a layout)
+  size_t max_pods = 1;
+  for (int i : idx) {
+    size_t n = gb.base_pods.size();
+    for (uint32_t c : cands[i]) n += gb.node_pods[c].size();
+    max_pods = std::max(max_pods, n);
+  }
+  int Pc = 64;
+  while ((size_t)Pc < max_pods) Pc *= 2;
+  if (int32_t rc = GeneralBatchLayout(ctx, gb, Pc)) return rc;
+  const SolveOffs& o = gb.o;
+  const size_t patch_bytes = o.common;
+  // simulations per launch: bounded by 2 GiB of arenas
+  const size_t per_launch = std::max<size_t>(1, std::min<size_t>(1024, ((size_t)2 << 30) / gb.stride));
+  const int sort_cap = std::min(SortCapacity(), Pc);
+  const size_t dyn = std::max<size_t>((size_t)2 * sort_cap * sizeof(int32_t), o.chk_on ? CHK_LDS_BYTES : 0);
+  GenScratch scratch;
+  vector<uint8_t> patches;
+  vector<vector<int32_t>> queues;
+  vector<SolveArgs> sargs;
+  vector<FinalizeArgs> fargs;
+  vector<uint64_t> stats;
+  vector<int32_t> place, nct;
+  vector<uint32_t> nopt, opts;
+  vector<KReqs> fin;
+  vector<uint64_t> held;
+  for (size_t b0 = 0; b0 < idx.size(); b0 += per_launch) {
+    const auto th0 = std::chrono::steady_clock::now();
+    const int n = (int)std::min(per_launch, idx.size() - b0);
+    if (gb.arenas_bytes < gb.stride * n) {
+      HIPCHK(gb.arenas.alloc(gb.stride * n));
+      gb.arenas_bytes = gb.stride * n;
+    }
+    const size_t args_need = sizeof(SolveArgs) * n + 256 + sizeof(FinalizeArgs) * n;
+    if (gb.args_bytes < args_need) {
+      HIPCHK(gb.args.alloc(args_need));
+      gb.args_bytes = args_need;
+    }
+    uint8_t* arenas = (uint8_t*)gb.arenas.p;
+    uint8_t* sh = (uint8_t*)gb.shared.p;
+    patches.resize(patch_bytes * n);
+    queues.resize(n);
+    sargs.resize(n);
+    fargs.resize(n);
+    for (int j = 0; j < n; j++) {
+      const int i = idx[b0 + j];
+      if (GeneralPatch(gb, cl, cands[i], scratch, queues[j], patches.data() + patch_bytes * j))
+        return fail(KP_E_INVAL, "subset %d: not batchable after the check", i);
+      uint8_t* ar = arenas + gb.stride * j;
+      SolveArgs& a = sargs[j];
+      BindSolve(a, C, o, sh, ar, (int)queues[j].size(), Pc, gb.rmask, gb.res_mode);
+      if (gb.tfeas_on) {
+        a.tfeas = (const uint64_t*)(sh + o.tfeas);
+        a.tfeas_words = gb.tf_words;
+      }
+      FinalizeArgs& f = fargs[j];
+      memset(&f, 0, sizeof f);
+      f.dict = a.dict;
+      f.cats = a.cats;
+      f.vint = a.vint;
+      f.nc_tmpl = a.nc_tmpl;
+      f.tmpl_catalog = a.tmpl_catalog;
+      f.nc_reqs = a.nc_reqs;
+      f.nc_X = a.nc_X;
+      f.max_types = 100;
+      f.opt_stride = gb.opt_stride;
+      f.out_options = (uint32_t*)(ar + o.opts);
+      f.out_n_remaining = (uint32_t*)(ar + o.nrem);
+      f.out_n_options = (uint32_t*)(ar + o.nopt);
+      f.nc_held = a.res_mode ? a.nc_held : nullptr;
+      f.solve_stats = a.stats;
+    }
+    SolveArgs* dargs = (SolveArgs*)gb.args.p;
+    FinalizeArgs* dfargs = (FinalizeArgs*)((uint8_t*)gb.args.p + ((sizeof(SolveArgs) * n + 255) & ~(size_t)255));
+    BatchInitArgs bi;
+    memset(&bi, 0, sizeof bi);
+    bi.base = arenas;
+    bi.stride = gb.stride;
+    bi.pristine = (const uint8_t*)gb.pristine.p;
+    bi.dst_off = o.common;
+    bi.n_copy = (o.mut_end - o.common + 15) & ~(size_t)15;
+    auto fill = [&](size_t off, size_t len, uint32_t byte) {
+      bi.fill_off[bi.n_fill] = off;
+      bi.fill_len[bi.n_fill] = (len + 15) & ~(size_t)15;
+      bi.fill_byte[bi.n_fill] = byte;
+      bi.n_fill++;
+    };
+    fill(o.stats, sizeof(uint64_t) * KP_SOLVE_STATS, 0);
+    fill(o.npods, sizeof(int32_t) * Pc, 0);
+    fill(o.place, sizeof(int32_t) * Pc, 0xFF);
+    fill(o.ver0, o.ver_end - o.ver0, 0);
+    fill(o.fail0, o.fail_end - o.fail0, 0xFF);
+    if (o.n_hcnc) fill(o.hcnc, o.n_hcnc, 0);
+    *host_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count();
+    HIPCHK(launch_batch_init(bi, n, st));
+    HIPCHK(hipMemcpy2DAsync(arenas, gb.stride, patches.data(), patch_bytes, patch_bytes, n, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(dargs, sargs.data(), sizeof(SolveArgs) * n, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(dfargs, fargs.data(), sizeof(FinalizeArgs) * n, hipMemcpyHostToDevice, st));
+    HIPCHK(hipEventRecord(ctx->ev0, st));
+    HIPCHK(launch_solve_batch(sargs[0], dargs, n, dyn, st));
+    HIPCHK(launch_finalize_batch(fargs[0], dfargs, n, st));
+    HIPCHK(hipEventRecord(ctx->ev1, st));
+    stats.resize((size_t)n * KP_SOLVE_STATS);
+    place.resize((size_t)n * Pc);
+    nct.resize(n);
+    nopt.resize(n);
+    opts.resize((size_t)n * gb.opt_stride);
+    fin.resize(n);
+    held.resize(n);
+    auto down = [&](void* dst, size_t off, size_t width) {
+      return hipMemcpy2DAsync(dst, width, arenas + off, gb.stride, width, n, hipMemcpyDeviceToHost, st);
+    };
+    HIPCHK(down(stats.data(), o.stats, sizeof(uint64_t) * KP_SOLVE_STATS));
+    HIPCHK(down(place.data(), o.place, sizeof(int32_t) * Pc));
+    HIPCHK(down(nct.data(), o.nct, sizeof(int32_t)));
+    HIPCHK(down(nopt.data(), o.nopt, sizeof(uint32_t)));
+    HIPCHK(down(opts.data(), o.opts, sizeof(uint32_t) * gb.opt_stride));
+    HIPCHK(down(fin.data(), o.ncr, sizeof(KReqs)));
+    if (gb.res_mode) HIPCHK(down(held.data(), o.held, sizeof(uint64_t)));
+    HIPCHK(hipStreamSynchronize(st));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    *dev_ms += ms;
+    const auto th1 = std::chrono::steady_clock::now();
+    for (int j = 0; j < n; j++) {
+      const int i = idx[b0 + j];
+      const uint64_t* sj = &stats[(size_t)j * KP_SOLVE_STATS];
+      if (sj[7]) return fail(KP_E_DEVICE, "solve_kernel exceeded its Queue.Pop bound in simulation %d: aborted", i);
+      counters[0] += sj[0];
+      counters[1] += sj[1];
+      counters[2] += sj[2];
+      const int n_nc = (int)sj[3];
+      const vector<int32_t>& q = queues[j];
+      SimOut& r = outs[i];
+      r.n_pods = (uint32_t)q.size();
+      // AllNonPendingPodsScheduled; a candidate pod on an uninitialized node is an error (deleting-node pods exempt)
+      bool all = true;
+      for (size_t p = 0; p < q.size() && all; p++) {
+        const uint8_t kind = gb.pod_kind[q[p]];
+        const int32_t pl = place[(size_t)j * Pc + p];
+        if (kind == 2) continue;
+        if (pl == -1) all = false;
+        else if (kind == 0 && pl <= -2 && !cl.nodes[gb.pos_node[-2 - pl]].node.initialized) all = false;
+      }
+      KReqs R = fin[j];
+      int ci = 0;
+      uint32_t np = 0;
+      if (n_nc == 1) {
+        if (gb.res_mode) ApplyHeld(*C.B, held[j], R);
+        ci = C.B->tmpl_catalog[nct[j]];
+        np = (uint32_t)C.B->tmpl_nodepool[nct[j]];
+      }
+      GeneralDecide(cl, labels, cands[i], *C.B, all, n_nc, &R, ci, np, &opts[(size_t)j * gb.opt_stride],
+                    n_nc == 1 ? nopt[j] : 0, multi_node, r);
+    }
+    *host_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th1).count();
+  }
+  return KP_OK;
+}
+
 static int32_t GeneralSimLocked(kp_cluster_plan* plan, const uint32_t* offsets, const uint32_t* nodes,
                                 uint32_t n_subsets, int32_t multi_node, SimArgs& a) {
   kp_ctx* ctx = plan->ctx;
@@ -4614,169 +5374,75 @@ static int32_t GeneralSimLocked(kp_cluster_plan* plan, const uint32_t* offsets, 
   if (int32_t rc = CatalogsAlive(plan->general->alive)) return rc;
   if (offsets[0] != 0) return fail(KP_E_INVAL, "offsets[0] != 0");
   if (offsets[n_subsets] && !nodes) return fail(KP_E_INVAL, "null nodes");
-  vector<std::map<string, string>> labels(N);
-  for (int i = 0; i < N; i++)
-    for (uint32_t j = 0; j < cl.nodes[i].node.n_labels; j++) {
-      const kp_label& l = cl.nodes[i].node.labels[j];
-      labels[i][Normalize(l.key ? l.key : "")] = l.value ? l.value : "";
-    }
-  vector<SimOut> outs(n_subsets);
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  vector<std::map<string, string>>& labels = plan->general_labels;  // the nodes' labels (NodeCandidatePrice), once
+  if ((int)labels.size() != N) {
+    labels.assign(N, {});
+    for (int i = 0; i < N; i++)
+      for (uint32_t j = 0; j < cl.nodes[i].node.n_labels; j++) {
+        const kp_label& l = cl.nodes[i].node.labels[j];
+        labels[i][Normalize(l.key ? l.key : "")] = l.value ? l.value : "";
+      }
+  }
+  vector<vector<uint32_t>> cands(n_subsets);
   vector<char> inS(N, 0);
-  uint64_t attempts = 0, pops = 0, bytes = 0;
-  double dev_ms = 0;
   for (uint32_t s = 0; s < n_subsets; s++) {
     if (offsets[s + 1] < offsets[s]) return fail(KP_E_INVAL, "offsets not monotone at %u", s);
-    vector<uint32_t> cand(nodes + offsets[s], nodes + offsets[s + 1]);
-    for (uint32_t c : cand) {
+    cands[s].assign(nodes + offsets[s], nodes + offsets[s + 1]);
+    for (uint32_t c : cands[s]) {
       if (c >= (uint32_t)N) return fail(KP_E_INVAL, "subset %u: node %u", s, c);
       if (cl.nodes[c].deleting) return fail(KP_E_INVAL, "subset %u: node %u is being deleted", s, c);
+      if (inS[c]) return fail(KP_E_INVAL, "subset %u: node %u twice", s, c);
       inS[c] = 1;
     }
-    vector<kp_existing_node> ex;
-    vector<int> exNode;
-    for (int i = 0; i < N; i++)
-      if (!inS[i] && !cl.nodes[i].deleting) {
-        ex.push_back(cl.nodes[i].node);
-        exNode.push_back(i);
-      }
-    vector<kp_pod> pods;
-    vector<int> kind;  // 0 candidate pod, 1 deleting-node pod, 2 pending
-    for (uint32_t j = 0; j < cl.n_pending; j++) {
-      if (cl.pending_pods[j] >= cl.n_pods) return fail(KP_E_INVAL, "pending pod %u", cl.pending_pods[j]);
-      pods.push_back(cl.pods[cl.pending_pods[j]]);
-      kind.push_back(2);
-    }
-    for (int i = 0; i < N; i++)
-      if (cl.nodes[i].deleting)
-        for (uint32_t j = 0; j < cl.nodes[i].n_pods; j++) {
-          pods.push_back(cl.pods[cl.nodes[i].pods[j]]);
-          kind.push_back(1);
-        }
-    for (uint32_t c : cand)
-      for (uint32_t j = 0; j < cl.nodes[c].n_pods; j++) {
-        pods.push_back(cl.pods[cl.nodes[c].pods[j]]);
-        kind.push_back(0);
-      }
-    vector<kp_bound_pod> bound;
-    for (size_t e = 0; e < exNode.size(); e++) {
-      const kp_cluster_node& n = cl.nodes[exNode[e]];
-      for (uint32_t j = 0; j < n.n_pods; j++) {
-        const uint32_t p = n.pods[j];
-        if (p >= cl.n_pods || cl.pods[p].shape >= cl.n_shapes) return fail(KP_E_INVAL, "node %d: pod %u", exNode[e], p);
-        const kp_pod_shape& sh = cl.shapes[cl.pods[p].shape];
-        bound.push_back({sh.namespace_, sh.labels, sh.n_labels, (uint32_t)e, sh.required_anti_affinity,
-                         sh.n_required_anti_affinity, 0});
-      }
-    }
-    for (uint32_t c : cand) inS[c] = 0;
-    SimOut& r = outs[s];
-    memset(&r, 0, sizeof r);
-    r.n_pods = (uint32_t)pods.size();
-    double candPrice = 0;
-    bool priced = true, allSpot = true;
-    for (uint32_t c : cand) {
-      const kp_cluster_node& n = cl.nodes[c];
-      double p = 0;
-      if (!NodeCandidatePrice(cl.catalogs[n.catalog]->types[n.instance_type], labels[c], &p)) priced = false;
-      candPrice += p;
-      auto f = labels[c].find(kCapType);
-      if (f == labels[c].end() || f->second != "spot") allSpot = false;
-    }
-    r.candidate_price = priced ? candPrice : 0;
-    kp_solve_in in;
-    memset(&in, 0, sizeof in);
-    in.catalogs = cl.catalogs;
-    in.n_catalogs = cl.n_catalogs;
-    in.n_nodepools = cl.n_nodepools;
-    in.nodepools = cl.nodepools;
-    in.existing = ex.data();
-    in.n_existing = (uint32_t)ex.size();
-    in.n_shapes = cl.n_shapes;
-    in.shapes = cl.shapes;
-    in.pods = pods.data();
-    in.n_pods = (uint32_t)pods.size();
-    in.max_instance_types = 100;
-    in.bound_pods = bound.data();
-    in.n_bound_pods = (uint32_t)bound.size();
-    in.namespaces = cl.namespaces;
-    in.n_namespaces = cl.n_namespaces;
-    in.reserved_offering_mode = KP_RESERVED_STRICT;  // SimulateScheduling: NewScheduler(..., DisableReservedCapacityFallback)
-    kp_solve_plan* sp = nullptr;
-    int32_t rc = SolvePrepare(ctx, &in, nullptr, &sp);
-    if (rc) return rc;
-    std::unique_ptr<kp_solve_plan, void (*)(kp_solve_plan*)> spg(sp, kp_solve_plan_destroy);
-    kp_solve_result* res = nullptr;
-    rc = kp_solve_run(sp, &res);
-    if (rc) return rc;
-    std::unique_ptr<kp_solve_result, void (*)(kp_solve_result*)> rg(res, kp_result_destroy);
-    attempts += res->stats.attempts;
-    pops += res->stats.pops;
-    bytes += res->stats.bytes_algorithmic;
-    dev_ms += res->stats.device_ms;
-    // AllNonPendingPodsScheduled; a candidate pod on an uninitialized node is an error (deleting-node pods exempt)
-    bool all = true;
-    for (size_t p = 0; p < pods.size() && all; p++) {
-      const int32_t pl = res->placement[p];
-      if (kind[p] == 2) continue;
-      if (pl == -1) all = false;
-      else if (kind[p] == 0 && pl <= -2 && !ex[(size_t)(-2 - pl)].initialized) all = false;
-    }
-    if (!all) continue;  // no-op
-    if (res->ncs.empty()) {
-      r.decision = KP_DECISION_DELETE;
-      r.savings = r.candidate_price;
-      continue;
-    }
-    if (res->ncs.size() != 1 || !priced) continue;
-    const Dict& d = sp->cp->B->d;
-    const KReqs& R = res->fin[0];
-    const int ci = res->nc_cat[0];
-    const vector<HostType>& types = cl.catalogs[ci]->types;
-    const HostCat& hc = sp->cp->B->cats[ci];
-    const int kct = d.key(kCapType), bspot = kct >= 0 ? d.bit(kct, "spot") : -1;
-    const bool ncSpot = kct < 0 || !((R.present >> kct) & 1) || (bspot >= 0 ? Has(d, R, kct, bspot) : ((R.compl_ >> kct) & 1));
-    const bool s2s = allSpot && ncSpot;  // spot-to-spot: only behind the feature gate
-    if (s2s && !cl.spot_to_spot) continue;
-    const bool hasMin = (R.hmin & R.present) != 0;
-    vector<int> kept;
-    for (uint32_t t : res->ncs[0].options)
-      if (WorstLaunch(d, R, types[t], s2s) < candPrice) kept.push_back((int)t);
-    if (hasMin && !HostMinValuesOK(d, hc, R, kept)) continue;
-    if (kept.empty()) continue;
-    if (multi_node) {  // filterOutSameType
-      std::map<string, double> prices;
-      for (uint32_t c : cand) {
-        const kp_cluster_node& n = cl.nodes[c];
-        const HostType& it = cl.catalogs[n.catalog]->types[n.instance_type];
-        double p = 0;
-        if (!NodeCandidatePrice(it, labels[c], &p)) continue;
-        auto f = prices.find(it.name);
-        if (f == prices.end() || p < f->second) prices[it.name] = p;
-      }
-      double maxPrice = std::numeric_limits<double>::max();
-      for (int t : kept) {
-        auto f = prices.find(types[t].name);
-        if (f != prices.end() && f->second < maxPrice) maxPrice = f->second;
-      }
-      vector<int> k2;
-      for (int t : kept)
-        if (WorstLaunch(d, R, types[t], s2s) < maxPrice) k2.push_back(t);
-      if (hasMin && !HostMinValuesOK(d, hc, R, k2)) continue;
-      kept.swap(k2);
-      if (kept.empty()) continue;
-    }
-    if (s2s && cand.size() == 1) {
-      if (kept.size() < 15) continue;
-      kept.resize(std::min<size_t>(kept.size(), hasMin ? 100 : 15));
-    }
-    double best = std::numeric_limits<double>::max();
-    for (int t : kept) best = std::min(best, WorstLaunch(d, R, types[t], s2s));
-    r.decision = KP_DECISION_REPLACE;
-    r.nodepool = res->ncs[0].nodepool;
-    r.replacement_price = best;
-    r.savings = candPrice - best;
-    r.n_options = (uint32_t)kept.size();
+    for (uint32_t c : cands[s]) inS[c] = 0;
   }
+  // the batched path: built once per plan (again after an offering refresh of its catalogues)
+  if (plan->gb) {
+    const SolveBase& B = *plan->gb->C->B;
+    if (CatalogsAlive(B.alive) || plan->gb->base_version != B.version || SeqnumsOf(B.catalogs) != B.seqnums) {
+      plan->gb.reset();
+      plan->gb_tried = false;
+    }
+  }
+  const char* gbe = getenv("KP_GENERAL_BATCH");
+  const bool batch_on = !(gbe && gbe[0] == '0');
+  if (batch_on && !plan->gb_tried) {
+    plan->gb_tried = true;
+    const int32_t rc = GeneralBatchBuild(plan, plan->gb);
+    if (rc && rc != KP_E_UNSUPPORTED) return rc;
+    if (rc) plan->gb.reset();
+  }
+  const double t_setup = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+  vector<SimOut> outs(n_subsets);
+  memset(outs.data(), 0, sizeof(SimOut) * outs.size());
+  uint64_t counters[3] = {0, 0, 0};
+  double dev_ms = 0, host_ms = 0;
+  vector<int> batched, single;
+  for (uint32_t s = 0; s < n_subsets; s++) {
+    bool ok = batch_on && plan->gb;
+    if (ok && plan->gb->C->G) {  // an inverse anti-affinity group would vanish: the per-subset compile
+      const Compiled& C = *plan->gb->C;
+      std::map<int, int> inv;
+      for (uint32_t c : cands[s])
+        for (int32_t g : C.node_inv[plan->gb->node_input[c]])
+          if (++inv[g] == C.tg_inv_total[g]) ok = false;
+    }
+    (ok ? batched : single).push_back((int)s);
+  }
+  const auto t1 = clk::now();
+  if (!batched.empty()) {
+    const int32_t rc = GeneralBatchRun(plan, *plan->gb, cands, batched, labels, multi_node, outs, counters, &dev_ms, &host_ms);
+    if (rc) return rc;
+  }
+  const double t_batch = std::chrono::duration<double, std::milli>(clk::now() - t1).count();
+  const auto t2 = clk::now();
+  for (int s : single) {
+    const int32_t rc = GeneralSimOne(plan, cands[s], labels, multi_node, outs[s], counters, &dev_ms);
+    if (rc) return rc;
+  }
+  const double t_single = std::chrono::duration<double, std::milli>(clk::now() - t2).count();
   // results and counters in device buffers, as the batched kernel leaves them
   const size_t need = sizeof(SimOut) * std::max<uint32_t>(n_subsets, 1) + 256 + sizeof(uint64_t) * 8;
   if (need > plan->batch_bytes) {
@@ -4788,11 +5454,15 @@ static int32_t GeneralSimLocked(kp_cluster_plan* plan, const uint32_t* offsets, 
   a = SimArgs{};
   a.out = (SimOut*)plan->batch.p;
   a.stats = (uint64_t*)((uint8_t*)plan->batch.p + ((sizeof(SimOut) * std::max<uint32_t>(n_subsets, 1) + 255) & ~(size_t)255));
-  uint64_t st[8] = {attempts, bytes, pops, 0, 0, 0, 0, 0};
+  uint64_t st[8] = {counters[0], counters[1], counters[2], (uint64_t)batched.size(), (uint64_t)single.size(), 0, 0, 0};
   if (n_subsets) HIPCHK(hipMemcpyAsync(a.out, outs.data(), sizeof(SimOut) * n_subsets, hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(hipMemcpyAsync(a.stats, st, sizeof st, hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
   plan->general_ms = dev_ms;
+  plan->general_batched = (uint32_t)batched.size();
+  if (getenv("KP_HOST_TIMING"))
+    fprintf(stderr, "[kp general] %u sims (%zu batched, %zu single): setup %.2f batch %.2f (host %.2f device %.2f) "
+            "single %.2f ms\n", n_subsets, batched.size(), single.size(), t_setup, t_batch, host_ms, dev_ms, t_single);
   return KP_OK;
 }
 
@@ -4919,6 +5589,7 @@ int32_t kp_cluster_simulate(kp_cluster_plan* plan, const uint32_t* offsets, cons
     stats->bytes_algorithmic = kst[1];
     stats->pops = kst[2];
     stats->phase_cycles[0] = kst[3];
+    if (plan->general) stats->phase_cycles[1] = kst[4];  // general path: simulations batched / compiled per subset
     stats->prepare_ms = plan->prepare_ms;
     stats->host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   }
@@ -5137,6 +5808,7 @@ int32_t kp_consolidate_argmin(kp_cluster_plan* plan, kp_comm* comm, const uint32
     stats->bytes_algorithmic = kst[1];
     stats->pops = kst[2];
     stats->phase_cycles[0] = kst[3];
+    if (plan->general) stats->phase_cycles[1] = kst[4];  // general path: simulations batched / compiled per subset
     stats->prepare_ms = plan->prepare_ms;
     stats->host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   }

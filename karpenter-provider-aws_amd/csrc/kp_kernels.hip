@@ -26,36 +26,9 @@
 #ifndef FASTLANE
 #define FASTLANE 1  // solve_kernel: wave-0 fast lane for merge-free placements (0 = full path only)
 #endif
-#ifndef FL_NI
-#define FL_NI 1  // the append attempt's rare Fits paths (>4 resource rows, catalogue >= 8) out of line: frees
-                 // registers in the append loop (config 2 kernel 211.6 -> 206.4 ms, same algorithmic bytes)
-#endif
-#ifndef FL_SPLIT
-#define FL_SPLIT 0  // variant under measurement: the fast lane's full NodeClaim.Add as a separate (noinline) function
-#endif
-#ifndef FL_CNT32
-#define FL_CNT32 1  // the fast lane's byte model as 32-bit event counts converted on exit (same totals; the 64-bit
-                    // accumulators cost 2.8 % of the loop)
-#endif
-#if FL_CNT32
-#define FL_CNT32_APP (n_app++)
-#define FL_CNT32_SCAN(x) (n_scan += (uint32_t)(x))
-#else
-#define FL_CNT32_APP ((void)0)
-#define FL_CNT32_SCAN(x) ((void)0)
-#endif
-#ifndef FL_NOBYTES
-#define FL_NOBYTES 0  // variant under measurement: no algorithmic-byte accounting in the fast lane
-#endif
-#ifndef FL_NOGUARD
-#define FL_NOGUARD 0  // variant under measurement: no runaway guard in the fast lane's loop
-#endif
 #ifndef FL_NOTIME
 #define FL_NOTIME 1  // the fast lane's per-phase s_memtime probes are compiled out (their registers cost 3.7 % even
                      // when KP_TIMING is off); the diagnostic build (tools/build_fine.sh) turns them back on
-#endif
-#ifndef FL_CACHE
-#define FL_CACHE 1  // the fast lane keeps its last append commit's NodeClaim state in registers (0: always reload)
 #endif
 #ifndef FT_FINE
 #define FT_FINE 0  // diagnostic: finer fast-lane probes (FTF) in place of the full path's attempt split
@@ -1063,22 +1036,38 @@ __device__ __forceinline__ int first_ok(const int32_t* s_ok) {
 // resource cannot take the pod (Fits fails for every remaining type) and the pre-pass skips it.
 // With `head`, the new NodeClaim's pre-check record is written as well: headroom = max allocatable - requests (q_lane:
 // lane r holds the requests of resource r) for the first four requested resources (INT64_MAX past them), version 0.
+// Max of row r of a [R][T] table over the type set X (lane w holds word w of X): lane l reads type 64 i + l for every
+// word i, so each word is one coalesced load and the loads of all words are independent (a per-lane walk over the
+// word's set bits made every load wait for the previous one: ~64 dependent round trips per resource).
+__device__ __forceinline__ int64_t max_over_types(const int64_t* row, uint64_t X, int TW, int T) {
+  const int lane = LANE;
+  int64_t mx = INT64_MIN;
+  for (int i0 = 0; i0 < TW; i0 += 4) {
+    int64_t v[4];
+    bool in[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int i = i0 + j;
+      const uint64_t w = i < TW ? lane_bcast(X, i) : 0;
+      const int t = i * 64 + lane;
+      in[j] = ((w >> lane) & 1) && t < T;
+      v[j] = in[j] ? row[t] : INT64_MIN;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) mx = v[j] > mx ? v[j] : mx;
+  }
+  return wave_max_i64(mx);
+}
+
 __device__ __forceinline__ void store_maxalloc(const int64_t* alloc, uint64_t X, int T, uint32_t rmask, int64_t* dst,
                                                NcHead* head = nullptr, int64_t q_lane = 0, int32_t taintset = 0) {
   const int lane = LANE;
   int64_t room0 = INT64_MAX, room1 = INT64_MAX, room2 = INT64_MAX, room3 = INT64_MAX;
   int k = 0;
+  const int TW = (T + 63) >> 6;
   for (int r = 0; r < KP_NRES; r++) {
     if (!((rmask >> r) & 1)) continue;
-    int64_t mx = INT64_MIN;
-    uint64_t m = X;
-    while (m) {
-      const int b = __builtin_ctzll(m);
-      m &= m - 1;
-      const int64_t v = alloc[(size_t)r * T + lane * 64 + b];
-      mx = v > mx ? v : mx;
-    }
-    mx = wave_max_i64(mx);
+    const int64_t mx = max_over_types(alloc + (size_t)r * T, X, TW, T);
     if (lane == 0) dst[r] = mx;
     if (head) {
       const int64_t room = mx - lane_bcast_i64(q_lane, r);
@@ -1262,9 +1251,7 @@ __device__ void slow_sort_wave(P ord, P npods, int n) {
 }
 
 #define DBG_SERIAL 0
-#ifndef SH_PER_GLB
-#define SH_PER_GLB 8
-#endif
+#define SH_PER_GLB 8  // stable-move shift: words per thread on the global order arrays
 #ifndef SORT_DIAG
 #define SORT_DIAG 0  // diagnostic: the full path's sort split (decision / shift cycles, shifted entries, modes) in stats[25..30]
 #endif
@@ -1720,14 +1707,16 @@ __device__ bool chk_append(const ChkDir& d, ChkCtl LDS* C, ChkBlk* B, int e, int
 }
 
 // Moves the entry at (cf, sf) to just before the entry at (cx, sx) (cx < 0: to the end of the order), keeping every
-// other entry's relative order. false: the target chunk is full and the directory cannot take a split (no change).
-__device__ bool chk_move(const ChkDir& d, ChkCtl LDS* C, ChkBlk* B, int cf, int sf, int cx, int sx) {
+// other entry's relative order. (idf, keyf): the source chunk's contents, as its lanes hold them; (lc, lid, lkey): chunk
+// lc's contents when lc >= 0 (the replay's search loaded it), so that no block is read twice. An entry landing at a
+// chunk's end is one store (the block is not read). false: the target chunk is full and the directory cannot take a
+// split (no change made).
+__device__ bool chk_move(const ChkDir& d, ChkCtl LDS* C, ChkBlk* B, int cf, int sf, int idf, int keyf, int cx, int sx,
+                         int lc, int lid, int lkey) {
   const int lane = LANE;
   int nch = U(C->nch);
   const uint32_t vf = d.info[cf];
   const int bf = ci_blk(vf), nf = ci_cnt(vf);
-  int idf, keyf;
-  chk_load(B, bf, nf, idf, keyf);
   const int E = __builtin_amdgcn_readlane(idf, sf), KE = __builtin_amdgcn_readlane(keyf, sf);
   int tc, ts;  // insert before slot ts of chunk tc (ts == count: at its end), in the pre-move contents
   if (cx < 0) {
@@ -1759,8 +1748,16 @@ __device__ bool chk_move(const ChkDir& d, ChkCtl LDS* C, ChkBlk* B, int cf, int 
   }
   uint32_t vt = d.info[tc];
   int bt = ci_blk(vt), nt = ci_cnt(vt);
-  int idt, keyt;
-  chk_load(B, bt, nt, idt, keyt);
+  const bool append = ts == nt && nt < 64;  // at the target chunk's end: its contents are not needed
+  int idt = 0, keyt = 0;
+  if (!append) {
+    if (tc == lc) {
+      idt = lid;
+      keyt = lkey;
+    } else {
+      chk_load(B, bt, nt, idt, keyt);
+    }
+  }
   if (nt == 64) {  // split the target chunk: its upper half into a new block and directory entry tc + 1
     if (nch >= U(C->maxc) || U(C->nfree) == 0) return false;
     const int nfr = U(C->nfree) - 1;
@@ -1801,18 +1798,24 @@ __device__ bool chk_move(const ChkDir& d, ChkCtl LDS* C, ChkBlk* B, int cf, int 
     if (lane == 0 && nf > 1) d.info[cf] = ci_make(bf, nf - 1, __builtin_amdgcn_readlane(nkey, nf - 2));
   }
   // insert into the target chunk
-  {
+  const int ep = U(C->epoch) + 1;
+  if (append) {
+    if (lane == 0) {
+      B[bt].id[nt] = E;
+      B[bt].key[nt] = KE;
+      d.info[tc] = ci_make(bt, nt + 1, KE);
+    }
+  } else {
     const int src = lane < ts ? lane : lane - 1;
     const int sid = __shfl(idt, src < 0 ? 0 : src, 64), skey = __shfl(keyt, src < 0 ? 0 : src, 64);
     const int nid = lane == ts ? E : sid, nkey = lane == ts ? KE : skey;
     chk_store(B, bt, nt + 1, nid, nkey);
     const int last = __builtin_amdgcn_readlane(nkey, nt);
-    const int ep = U(C->epoch) + 1;
-    if (lane == 0) {
-      d.info[tc] = ci_make(bt, nt + 1, last);
-      d.bep[bt] = ep;
-      C->epoch = ep;
-    }
+    if (lane == 0) d.info[tc] = ci_make(bt, nt + 1, last);
+  }
+  if (lane == 0) {
+    d.bep[bt] = ep;
+    C->epoch = ep;
   }
   wave_sync();
   // first positions between the two chunks shift by the moved entry
@@ -1836,30 +1839,15 @@ __device__ bool chk_move(const ChkDir& d, ChkCtl LDS* C, ChkBlk* B, int cf, int 
   return true;
 }
 
-// choosePivot's increasingHint (see wave_pivot_increasing) on the chunked order
-__device__ bool chk_pivot_increasing(const ChkDir& d, int nch, const ChkBlk* B, int n) {
-  const int lane = LANE;
-  const int t = lane / 3;
-  const int mid = (n / 4) * (t + 1);
-  int key = 0;
-  if (lane < 9) {
-    const int pos = mid + (lane % 3) - 1;
-    const int c = chk_find_lane(d, nch, pos);
-    key = B[ci_blk(d.info[c])].key[pos - d.start[c]];
-  }
-  const int prev = __shfl(key, lane > 0 ? lane - 1 : 0, 64);
-  const int midkey_prev = __shfl(key, lane >= 3 ? lane - 3 : 0, 64);
-  bool bad = false;
-  if (lane < 9 && (lane % 3) != 0 && key < prev) bad = true;
-  if (lane < 9 && (lane % 3) == 1 && lane >= 3 && key < midkey_prev) bad = true;
-  return __ballot(bad) == 0;
-}
-
 // sort.Slice(newNodeClaims) replay on the chunked order after one pending mutation (see sort_newnodeclaims): the same
 // decisions (stable move when pdqsort makes one, else the literal pdqsort over the materialised flat order, then a
 // rebuild). Returns the lowest sorted position whose NodeClaim changed or moved (-1: none); -3: the move does not fit
 // the directory (nothing changed; the caller continues on the flat order: chk_materialize, then the flat replay);
 // -4: the literal pdqsort ran and the rebuild did not fit (the flat order in order / npods is sorted, low = 0).
+// choosePivot's increasingHint (n >= 50) needs no loads here: the order was sorted before the mutation, so an appended
+// entry (at n - 1, past every sample) leaves every sampled triple non-decreasing, and a +1 at position p whose
+// successor is now smaller breaks exactly the triples holding the pair (p, p + 1): p = m - 1 or p = m for a sample
+// middle m = (n / 4) * (t + 1) (wave_pivot_increasing's predicate under that invariant).
 __device__ int chk_sort(const ChkDir& d, ChkCtl LDS* C, ChkBlk* B, int n, int mut, int p, int32_t* order,
                         int32_t* npods, uint64_t* slow) {
   const int lane = LANE;
@@ -1898,14 +1886,21 @@ __device__ int chk_sort(const ChkDir& d, ChkCtl LDS* C, ChkBlk* B, int n, int mu
   }
   if (!mode) return mut == 1 ? p : n - 1;
   bool fast = n <= 12;
-  if (!fast && n >= 50) fast = chk_pivot_increasing(d, nch, B, n);
+  if (!fast && n >= 50) {
+    fast = true;
+    if (mode == 1)
+      for (int t = 1; t <= 3; t++) {
+        const int m = (n / 4) * t;
+        if (p == m - 1 || p == m) fast = false;
+      }
+  }
   if (!fast) {  // the literal pdqsort over the flat order, then a rebuild
     chk_materialize(d, C, B, order, npods);
     slow_sort_wave((GlbI32)order, (GlbI32)npods, n);
     if (lane == 0 && slow) slow[0] += 1;
     return chk_build(d, C, B, order, npods, n) ? 0 : -4;
   }
-  int cx = -1, sx = 0, low;
+  int cx = -1, sx = 0, low, lc = -1, lid = 0, lkey = 0;
   if (mode == 1) {  // q = first position > p with key >= K: within the chunk, else the first later chunk reaching K
     const uint64_t bal = __ballot(lane > sf && lane < cnt && key >= K);
     if (bal) {
@@ -1915,9 +1910,9 @@ __device__ int chk_sort(const ChkDir& d, ChkCtl LDS* C, ChkBlk* B, int n, int mu
       const int c = wave_first_true(cf + 1, nch, [&](int c) { return ci_last(d.info[c]) >= K; });
       if (c < nch) {
         const uint32_t w = d.info[c];
-        const int kc = lane < ci_cnt(w) ? B[ci_blk(w)].key[lane] : INT32_MAX;
-        cx = c;
-        sx = __builtin_ctzll(__ballot(kc >= K));
+        chk_load(B, ci_blk(w), ci_cnt(w), lid, lkey);
+        lc = cx = c;
+        sx = __builtin_ctzll(__ballot(lkey >= K));
       }
     }
     low = p;
@@ -1925,16 +1920,16 @@ __device__ int chk_sort(const ChkDir& d, ChkCtl LDS* C, ChkBlk* B, int n, int mu
     const int c = wave_first_true(0, nch - 1, [&](int c) { return ci_last(d.info[c]) > K; });
     if (c < nch - 1) {
       const uint32_t w = d.info[c];
-      const int kc = lane < ci_cnt(w) ? B[ci_blk(w)].key[lane] : INT32_MIN;
-      cx = c;
-      sx = __builtin_ctzll(__ballot(kc > K));
+      chk_load(B, ci_blk(w), ci_cnt(w), lid, lkey);
+      lc = cx = c;
+      sx = __builtin_ctzll(__ballot(lane < ci_cnt(w) && lkey > K));
     } else {
       cx = cf;
       sx = __builtin_ctzll(__ballot(lane < sf && key > K));
     }
     low = d.start[cx] + sx;
   }
-  if (!chk_move(d, C, B, cf, sf, cx, sx)) return -3;
+  if (!chk_move(d, C, B, cf, sf, id, key, cx, sx, lc, lid, lkey)) return -3;
   return low;
 }
 
@@ -1964,8 +1959,9 @@ struct FastState {
 __shared__ FastState g_fast;
 
 __shared__ uint64_t fl_io[2];  // results of the fast lane's out-of-line helpers
-// Rare paths of the fast lane's append attempt as calls (FL_NI): a catalogue id >= 8 (descriptor copied to LDS)
-// and more than 4 requested resources (fits_filter); inlined, their registers weigh on every pod.
+// Rare paths of the fast lane's append attempt as calls: a catalogue id >= 8 (descriptor copied to LDS) and more
+// than 4 requested resources (fits_filter); inlined, their registers weigh on every pod (config 2 kernel 211.6 ->
+// 206.4 ms out of line, same algorithmic bytes).
 __device__ __noinline__ void fl_hdr_fill(uint64_t cats_a, int c_a, int C_a) {
   const DevCatalog* cats = (const DevCatalog*)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(cats_a >> 32)) << 32) |
                                                (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)cats_a));
@@ -1982,63 +1978,6 @@ __device__ __noinline__ uint64_t fl_fits_filter(int cat_a, uint64_t X0, int64_t 
   const uint64_t X = fits_filter(D, H, X0, q_lane, j0_lane, (const int64_t LDS*)g_fitv, (uint32_t)U((int)rmask_a),
                                  (RowPtr LDS*)fl_rl, &nb, fl_fitj);
   if (LANE == 0) fl_io[1] = nb;
-  wave_sync();
-  return X;
-}
-
-// NodeClaim.Add in full for the fast lane (Compatible + Add of the requirements, the type filter, minValues) as its
-// own function: the merge is the rare attempt, and inlined its registers burden every pod's append path. On
-// success the merged requirements (and topology codes) are stored and the memo marks the shape-level merged.
-// Returns this lane's word of the remaining types (0 everywhere: failed); fl_io[0] = permanent failure,
-// fl_io[1] = algorithmic bytes read.
-template <bool TOPO>
-__device__ __noinline__ uint64_t fl_full_add(uint64_t kargs, int sl_a, int cat_a, int ncx_a, uint64_t X0, int64_t q_lane,
-                                             int32_t j0_lane, int staged_a) {
-  const uint32_t klo = __builtin_amdgcn_readfirstlane((uint32_t)kargs);
-  const uint32_t khi = __builtin_amdgcn_readfirstlane((uint32_t)(kargs >> 32));
-  const KARG SolveArgs* A = (const KARG SolveArgs*)(((uint64_t)khi << 32) | klo);
-  const int sl = U(sl_a), cat = U(cat_a), ncx = U(ncx_a);
-  const DevDict& D = g_D;
-  const int lane = LANE;
-  uint64_t nb = 0;
-  if (!U(staged_a)) {  // the pod's requirement set, once per pod
-    constexpr int NQ = (int)(sizeof(KReqs) / 8);
-    const uint64_t* src = reinterpret_cast<const uint64_t*>(A->shape_reqs + (size_t)sl * sizeof(KReqs));
-    uint64_t* dstB = reinterpret_cast<uint64_t*>(&fl_B);
-    for (int i = lane; i < NQ; i += 64) dstB[i] = src[i];
-    wave_sync();
-  }
-  auto hdr = [&](int c) -> const CatHdr LDS* {
-    if (c < 8) return (const CatHdr LDS*)&g_hdr[c];
-    hdr_fill_wave((CatHdr LDS*)&fl_hdrw, &A->cats[c], D.C);
-    wave_sync();
-    return (const CatHdr LDS*)&fl_hdrw;
-  };
-  const CandReq crx = load_cand(D, kreq_at(A->nc_reqs, ncx));
-  const VInt vig = vint_global(A->vint);
-  const uint64_t b_negop = A->shape_negop[sl];
-  uint64_t m_v = 0, X = 0;
-  ReqView rv;
-  const bool mok = merge_compatible(D, crx, (const KReqs*)&fl_B, b_negop, true, m_v, rv, (WaveSlots*)&fl_slots, vig);
-  const bool perm = mok || (fl_B.present & ~crx.P & ~b_negop & ~D.wellknown) == 0;
-  nb += sizeof(KReqs);
-  if (mok) {
-    const int pb = A->pvp_base[sl * A->n_catalogs + cat];
-    const uint64_t* pvp = A->shape_pvp + (size_t)pb * D.TW;
-    X = filter_types(D, hdr(cat), rv, m_v, X0, fl_B.present, pvp, A->pvp_slot + (size_t)sl * KP_MAX_KEYS, q_lane,
-                     j0_lane, (const int64_t LDS*)g_fitv, A->req_res_mask, vig, (uint32_t*)fl_scratch,
-                     (RowPtr LDS*)fl_rl, &nb, fl_fitj);
-    nb += (uint64_t)D.TW * 8 + KP_NRES * 8;
-    if (__ballot(X != 0)) {
-      store_merged(reinterpret_cast<KReqs*>(A->nc_reqs + (size_t)ncx * sizeof(KReqs)), rv, m_v, D.W, D.KB);
-      if (TOPO && A->n_tk) store_tcodes(A->n_tk, A->tk_keys, A->nc_tcode, A->hnc_stride, rv, m_v, ncx);
-      if (lane == 0 && ncx < A->ncc) A->nc_fail[(size_t)sl * A->ncc + ncx] = NC_MERGED;
-    }
-  }
-  if (lane == 0) {
-    fl_io[0] = perm ? 1 : 0;
-    fl_io[1] = nb;
-  }
   wave_sync();
   return X;
 }
@@ -2104,13 +2043,10 @@ __device__ __noinline__ int fast_lane(uint64_t kargs, int32_t LDS* s_dyn_arg, ui
   int64_t c_q = 0, c_r0 = 0, c_r1 = 0, c_r2 = 0, c_r3 = 0;
   int32_t c_fj = 0;
   int n_buf = 0, buf_pod = 0, buf_pl = 0;  // placements not yet written (lane i: the i-th)
-#if FL_CNT32
-  NbUnits fnb{0, 0, 0};  // append-path byte model as event counts, converted on exit
+  // the append path's byte model as 32-bit event counts, converted on exit (the 64-bit accumulators cost 2.8 % of
+  // the loop)
+  NbUnits fnb{0, 0, 0};
   uint32_t n_app = 0, n_scan = 0;
-#define FL_NB fnb
-#else
-#define FL_NB bytes
-#endif
     const bool tmg = A->timing != 0;
 #define FL_HAS_EX (A->n_existing != 0)
     uint64_t ft = tmg ? __builtin_amdgcn_s_memtime() : 0;
@@ -2139,7 +2075,7 @@ if (!FL_NOTIME && tmg) {                                    \
       const KARG SolveArgs* A = (const KARG SolveArgs*)(((uint64_t)khi_i << 32) | klo_i);
       const int len = q_len;
       const int head = q_head;
-      if (len <= 0 || (!FL_NOGUARD && pops_in + pops > pop_cap)) break;
+      if (len <= 0 || pops_in + pops > pop_cap) break;
       // Queue.Pop from the prefetched window: entries [qw_head, qw_head + qw_n) of the ring were in the queue when
       // the window was read, and nothing rewrites a queued entry (pushes go to the tail) or its pod's level and
       // lastLen stamps while it waits, so lane i's copy of entry qw_head + i stays exact.
@@ -2408,8 +2344,7 @@ if (!FL_NOTIME && tmg) {                                    \
           tag = cand && (fl >= NC_MERGED || triv) && pinned;
         }
         if (lane == 0) scanned += nscan;
-        if (!FL_CNT32 && lane == 0) bytes += (uint64_t)nscan * (12 + 16 * A->n_req_res);
-        FL_CNT32_SCAN(nscan);
+        n_scan += (uint32_t)nscan;
         uint64_t cm = __ballot(cand);
         const uint64_t tm = __ballot(tag);
         if (TOPO && t_n && ipos == INT32_MAX) {
@@ -2465,28 +2400,15 @@ if (!FL_NOTIME && tmg) {                                    \
           ReqView rv;
           bool perm = true;  // a failure here is permanent (NC_NEVER) unless it is Compatible's undefined-key rule
           if (!full_add) {
-#if FL_NI
             if (n_rr <= 4 && cat < 8) {
               X = fits_lean(D, (const CatHdr LDS*)&g_hdr[cat], X0, q_lane, j0_lane, (const int64_t LDS*)g_fitv, rr_list,
-                            n_rr, FL_NB, (int32_t LDS*)fl_fitj);
+                            n_rr, fnb, (int32_t LDS*)fl_fitj);
             } else {
               X = fl_fits_filter(cat, X0, q_lane, j0_lane, A->req_res_mask, (uint64_t)(uintptr_t)A->cats);
               bytes += fl_io[1];
             }
-#else
-            X = n_rr <= 4 ? fits_lean(D, hdr(cat), X0, q_lane, j0_lane, (const int64_t LDS*)g_fitv, rr_list, n_rr, FL_NB,
-                                      (int32_t LDS*)fl_fitj)
-                          : fits_filter(D, hdr(cat), X0, q_lane, j0_lane, (const int64_t LDS*)g_fitv, A->req_res_mask,
-                                        (RowPtr LDS*)fl_rl, &bytes, fl_fitj);
-#endif
-            if (FL_CNT32) FL_CNT32_APP;
-            else bytes += (uint64_t)D.TW * 8 + KP_NRES * 8 + 8;
+            n_app++;
             if (FT_FINE && tmg && ncx == fl_last) fcyc[13] += 1;  // the previous pod's NodeClaim again
-          } else if (FL_SPLIT) {
-            X = fl_full_add<TOPO>(((uint64_t)khi_i << 32) | klo_i, sl, cat, ncx, X0, q_lane, j0_lane, b_staged ? 1 : 0);
-            b_staged = true;
-            perm = fl_io[0] != 0;
-            bytes += fl_io[1];
           } else {
             if (!b_staged) {  // the pod's requirement set, once per pod
               constexpr int NQ = (int)(sizeof(KReqs) / 8);
@@ -2514,7 +2436,7 @@ if (!FL_NOTIME && tmg) {                                    \
           }
           FTF(11);
           if (__ballot(X != 0)) {
-            if (full_add && !FL_SPLIT) {
+            if (full_add) {
               store_merged(reinterpret_cast<KReqs*>(A->nc_reqs + (size_t)ncx * sizeof(KReqs)), rv, m_v, D.W, D.KB);
               if (TOPO && A->n_tk) store_tcodes(A->n_tk, A->tk_keys, A->nc_tcode, A->hnc_stride, rv, m_v, ncx);
               if (lane == 0 && ncx < A->ncc) A->nc_fail[(size_t)sl * A->ncc + ncx] = NC_MERGED;
@@ -2576,7 +2498,7 @@ if (!FL_NOTIME && tmg) {                                    \
               }
               bytes += 16 * (uint64_t)rec_n;
             }
-            if (FL_CACHE && !full_add) {  // the append path left the requirements (hmin, catalogue) as they were
+            if (!full_add) {  // the append path left the requirements (hmin, catalogue) as they were
               c_nc = ncx, c_cat = cat, c_hm = hm, c_X = X, c_q = q_lane, c_fj = fj;
               c_r0 = lane_bcast_i64(hv.r0, l) - pr0;
               c_r1 = lane_bcast_i64(hv.r1, l) - pr1;
@@ -2633,7 +2555,6 @@ if (!FL_NOTIME && tmg) {                                    \
 #undef FT
 #undef FTF
 #undef FL_HAS_EX
-#undef FL_NB
   
   // write back: control block, window, counters, hand-off
   if (lane == 0) {
@@ -2652,13 +2573,9 @@ if (!FL_NOTIME && tmg) {                                    \
     S->qw_head = qw_head;
     S->qw_n = qw_n;
     S->qw_next = qw_next;
-#if FL_CNT32
     bytes += (uint64_t)fnb.probes * 512 + (uint64_t)fnb.rows * D.TW * 8 + (uint64_t)fnb.lb8 * 8 +
              (uint64_t)n_app * ((uint64_t)D.TW * 8 + KP_NRES * 8 + 8) + (uint64_t)n_scan * (12 + 16 * A->n_req_res);
-#endif
-#if !FL_NOBYTES
     S->bytes += bytes;
-#endif
     S->attempts += attempts;
     S->scanned += scanned;
     S->starts += starts;
@@ -2675,8 +2592,11 @@ if (!FL_NOTIME && tmg) {                                    \
   return pops;
 }
 
-template <int NW, bool TOPO>  // TOPO: the batch has topology spread groups (else that code compiles out)
-__global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
+// TOPO: the batch has topology spread groups (else that code compiles out). BATCH: one Solve per workgroup, each with
+// its own arguments batch[blockIdx.x] (the general consolidation path's simulations); else the kernel argument a0.
+template <int NW, bool TOPO, bool BATCH>
+__global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a0, const SolveArgs* __restrict__ batch) {
+  const SolveArgs& a = BATCH ? batch[blockIdx.x] : a0;
   constexpr int NT = NW * 64;
   DevDict& D = g_D;
   __shared__ WaveSlots slots[NW];
@@ -2816,7 +2736,8 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
       if (fl_skip > 0) {
         fl_skip--;
       } else {
-        const uint64_t kargs = (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
+        // the Solve's argument block: the kernarg segment (a0 is the first argument), or its entry of the batch
+        const uint64_t kargs = BATCH ? (uint64_t)&batch[blockIdx.x] : (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
         const int placed_fast = s_ctl[5] == 2 ? fast_lane<TOPO, true>(kargs, (int32_t LDS*)s_dyn, pops)
                                               : fast_lane<TOPO, false>(kargs, (int32_t LDS*)s_dyn, pops);
         pops += placed_fast;
@@ -3369,16 +3290,20 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
             X = lane < D.TW ? a.tmpl_X[(size_t)tm * D.TW + lane] : 0;
             const uint32_t lim = a.tmpl_limit_present[tm];
             if (lim) {  // filterByRemainingResources: capacity <= remaining for every limited resource
+              // lane l tests type 64 i + l of word i (coalesced capacity rows, independent loads across words)
               const int64_t* rem = a.tmpl_remaining + (size_t)tm * KP_NRES;
-              uint64_t m = lane < D.TW ? X : 0, keep = 0;
-              while (m) {
-                const int b = __builtin_ctzll(m);
-                m &= m - 1;
-                const int ty = lane * 64 + b;
-                bool viable = true;
-                for (int r = 0; r < KP_NRES; r++)
-                  if (((lim >> r) & 1) && H->d.cap[(size_t)r * D.T + ty] > rem[r]) viable = false;
-                if (viable) keep |= 1ull << b;
+              uint64_t keep = 0;
+              for (int i = 0; i < D.TW; i++) {
+                const uint64_t w = lane_bcast(X, i);
+                if (!w) continue;
+                const int ty = i * 64 + lane;
+                bool viable = ((w >> lane) & 1) && ty < D.T;
+                for (uint32_t rm = lim; rm && viable; rm &= rm - 1) {
+                  const int r = __builtin_ctz(rm);
+                  viable = H->d.cap[(size_t)r * D.T + ty] <= rem[r];
+                }
+                const uint64_t bal = __ballot(viable);
+                if (lane == i) keep = bal;
               }
               X = keep;
               bytes += (uint64_t)D.T * 8;
@@ -3454,15 +3379,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a) {
                 const CatHdr LDS* Hc = hdr(a.tmpl_catalog[tm]);
                 for (int r = 0; r < KP_NRES; r++) {
                   if (!((lim >> r) & 1)) continue;
-                  int64_t mx = INT64_MIN;
-                  uint64_t m = lane < D.TW ? X : 0;
-                  while (m) {
-                    const int b = __builtin_ctzll(m);
-                    m &= m - 1;
-                    const int64_t c = Hc->d.cap[(size_t)r * D.T + lane * 64 + b];
-                    mx = c > mx ? c : mx;
-                  }
-                  mx = wave_max_i64(mx);
+                  const int64_t mx = max_over_types(Hc->d.cap + (size_t)r * D.T, lane < D.TW ? X : 0, D.TW, D.T);
                   if (lane == 0) a.tmpl_remaining[(size_t)tm * KP_NRES + r] -= mx;
                 }
                 if (lane == 0) a.tmpl_ver[tm] += 1;
@@ -3729,13 +3646,18 @@ hipError_t launch_tmpl_feas(const TfeasArgs& a, hipStream_t s) {
 // ------------------------------------------------------------------------------------------------
 #define FIN_THREADS 256
 #define FIN_MAX_T 4096
-__global__ __launch_bounds__(FIN_THREADS) void finalize_kernel(FinalizeArgs a) {
+// BATCH: workgroup y finalizes NodeClaim 0 of simulation y (batch[y]) when that Solve made exactly one NodeClaim (the
+// only case a consolidation decision reads options from), its count read from the Solve's stats on the device.
+template <bool BATCH>
+__global__ __launch_bounds__(FIN_THREADS) void finalize_kernel(FinalizeArgs a0, const FinalizeArgs* __restrict__ batch) {
   __shared__ DevDict D;
   __shared__ uint64_t s_cls;
   __shared__ uint64_t s_key[FIN_MAX_T];
   __shared__ uint32_t s_idx[FIN_MAX_T];
   __shared__ uint32_t s_cnt;
-  const int nc = blockIdx.x;
+  const FinalizeArgs& a = BATCH ? batch[blockIdx.x] : a0;
+  if (BATCH && a.solve_stats[3] != 1) return;
+  const int nc = BATCH ? 0 : blockIdx.x;
   block_copy(D, a.dict);
   if (threadIdx.x == 0) s_cnt = 0;
   __syncthreads();
@@ -3988,20 +3910,9 @@ __global__ __launch_bounds__(FEAS_WAVES * 64) void feasibility_kernel(FeasArgs a
 // per-class-subset minima (a row copy, L2 -> HBM), or the min over the classes' price rows when C > KP_SUB_MAX_C.
 // The next row's header loads are issued before this row is evaluated.
 #define FEASB_WAVES 8
-#ifndef FEASB_CP
-#define FEASB_CP 8  // cheapest-row copy: loads in flight per lane before their stores (measured: 16 is slower)
-#endif
-#ifndef FEASB_EARLY
-#define FEASB_EARLY 0  // variant under measurement: the cheapest-row copy before the key / Fits / offering evaluation
-#endif
-#ifndef FEASB_MINW
+#define FEASB_CP 8    // cheapest-row copy: loads in flight per lane before their stores (measured: 16 is slower)
 #define FEASB_MINW 8  // waves per SIMD the register budget must allow (measured: 0.1574 -> 0.1245 ms on 50k rows)
-#endif
-#if FEASB_MINW
 __global__ __launch_bounds__(FEASB_WAVES * 64, FEASB_MINW) void feasibility_bits_kernel(FeasArgs a) {
-#else
-__global__ __launch_bounds__(FEASB_WAVES * 64) void feasibility_bits_kernel(FeasArgs a) {
-#endif
   __shared__ DevDict D;
   __shared__ int64_t s_vint[KP_MAX_BOUND_KEYS * 64];
   __shared__ OfferClass s_cls[KP_MAX_CLASSES];
@@ -4107,7 +4018,6 @@ __global__ __launch_bounds__(FEASB_WAVES * 64) void feasibility_bits_kernel(Feas
         }
       }
     };
-    if (FEASB_EARLY) cheapest_row();
     const uint32_t rmask = (uint32_t)__ballot(cur.rq > 0);
     uint64_t pass = nonneg;
     // Compatible(q, type, WK) part (a): types with a non-well-known key q does not define (rare: per-type loads)
@@ -4162,7 +4072,7 @@ __global__ __launch_bounds__(FEASB_WAVES * 64) void feasibility_bits_kernel(Feas
     for (uint64_t m = cls; m; m &= m - 1) av |= lw ? offer[(size_t)__builtin_ctzll(m) * TW + lane] : 0;
     pass &= av;
     if (lw) ((GLB uint64_t*)a.out_mask)[(size_t)q * TW + lane] = pass;
-    if (!FEASB_EARLY) cheapest_row();
+    cheapest_row();
   }
 }
 const void* feasibility_bits_kernel_ptr() { return (const void*)feasibility_bits_kernel; }
@@ -4657,17 +4567,49 @@ hipError_t launch_solve(const SolveArgs& a, int nw, size_t dyn_lds, hipStream_t 
   // candidates per attempt round cover the typical 2-3 attempts per pod. KP_SOLVE_WAVES=8: 8 waves.
   static const int nw4 = !(getenv("KP_SOLVE_WAVES") && atoi(getenv("KP_SOLVE_WAVES")) == 8);
   if (nw4) {
-    if (a.n_groups) hipLaunchKernelGGL((solve_kernel<4, true>), dim3(1), dim3(4 * 64), dyn_lds, s, a);
-    else hipLaunchKernelGGL((solve_kernel<4, false>), dim3(1), dim3(4 * 64), dyn_lds, s, a);
+    if (a.n_groups) hipLaunchKernelGGL((solve_kernel<4, true, false>), dim3(1), dim3(4 * 64), dyn_lds, s, a, nullptr);
+    else hipLaunchKernelGGL((solve_kernel<4, false, false>), dim3(1), dim3(4 * 64), dyn_lds, s, a, nullptr);
   } else {
-    if (a.n_groups) hipLaunchKernelGGL((solve_kernel<8, true>), dim3(1), dim3(8 * 64), dyn_lds, s, a);
-    else hipLaunchKernelGGL((solve_kernel<8, false>), dim3(1), dim3(8 * 64), dyn_lds, s, a);
+    if (a.n_groups) hipLaunchKernelGGL((solve_kernel<8, true, false>), dim3(1), dim3(8 * 64), dyn_lds, s, a, nullptr);
+    else hipLaunchKernelGGL((solve_kernel<8, false, false>), dim3(1), dim3(8 * 64), dyn_lds, s, a, nullptr);
   }
+  return hipGetLastError();
+}
+hipError_t launch_solve_batch(const SolveArgs& a0, const SolveArgs* dev_args, int n, size_t dyn_lds, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (a0.n_groups) hipLaunchKernelGGL((solve_kernel<4, true, true>), dim3(n), dim3(4 * 64), dyn_lds, s, a0, dev_args);
+  else hipLaunchKernelGGL((solve_kernel<4, false, true>), dim3(n), dim3(4 * 64), dyn_lds, s, a0, dev_args);
   return hipGetLastError();
 }
 hipError_t launch_finalize(const FinalizeArgs& a, hipStream_t s) {
   if (a.n_nc == 0) return hipSuccess;
-  hipLaunchKernelGGL(finalize_kernel, dim3(a.n_nc), dim3(FIN_THREADS), 0, s, a);
+  hipLaunchKernelGGL((finalize_kernel<false>), dim3(a.n_nc), dim3(FIN_THREADS), 0, s, a, nullptr);
+  return hipGetLastError();
+}
+hipError_t launch_finalize_batch(const FinalizeArgs& a0, const FinalizeArgs* dev_args, int n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL((finalize_kernel<true>), dim3(n), dim3(FIN_THREADS), 0, s, a0, dev_args);
+  return hipGetLastError();
+}
+// Batched Solves' arenas: every arena [y] = base + y * stride gets the shared pristine block copied to `dst_off` and
+// its `n_fill` ranges set to their byte (16-byte granules: offsets and lengths are multiples of 16).
+__global__ __launch_bounds__(256) void batch_init_kernel(BatchInitArgs a) {
+  uint8_t* arena = a.base + (size_t)blockIdx.y * a.stride;
+  const size_t n16 = a.n_copy / 16;
+  const uint4* src = reinterpret_cast<const uint4*>(a.pristine);
+  uint4* dst = reinterpret_cast<uint4*>(arena + a.dst_off);
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256) dst[i] = src[i];
+  for (int f = 0; f < a.n_fill; f++) {
+    const uint32_t b = a.fill_byte[f];
+    const uint4 v = make_uint4(b * 0x01010101u, b * 0x01010101u, b * 0x01010101u, b * 0x01010101u);
+    uint4* d = reinterpret_cast<uint4*>(arena + a.fill_off[f]);
+    const size_t m = a.fill_len[f] / 16;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < m; i += (size_t)gridDim.x * 256) d[i] = v;
+  }
+}
+hipError_t launch_batch_init(const BatchInitArgs& a, int n_arenas, hipStream_t s) {
+  if (n_arenas <= 0) return hipSuccess;
+  hipLaunchKernelGGL(batch_init_kernel, dim3(64, n_arenas), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_launch(const LaunchArgs& a, hipStream_t s) {

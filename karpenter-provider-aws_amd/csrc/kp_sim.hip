@@ -10,7 +10,8 @@
 //                     Node labels are single-valued In requirements, so Compatible is one dictionary-bit
 //                     test per pod key (lane = node, ballot -> 64-node word).
 //  sim_prep_kernel    per shape-level: the addToNewNodeClaim outcome (first NodeClaimTemplate whose Add
-//                     succeeds, and the NodeClaim it creates). Templates never change without limits.
+//                     succeeds, and the NodeClaim it creates), before the NodePool limits; sim_kernel applies
+//                     filterByRemainingResources on the replacement against the pools' remaining budget.
 //  sim_kernel         one WAVE per simulation, persistent over the batch. Per simulation: exclusion bitmap
 //                     of S and a "touched" bitmap in LDS, the pods of S sorted into Queue order (bitonic
 //                     sort of their global queue ranks in LDS), then the Solve loop:
@@ -25,9 +26,10 @@
 //                     then the decision: TruncateInstanceTypes (cheapest compatible offering, name; LDS
 //                     bitonic sort) + minValues, filterByPrice on WorstLaunchPrice, filterOutSameType.
 //
-// Exactness conditions checked by the host (else KP_E_UNSUPPORTED): no NodePool limits; no pod
-// NotIn/DoesNotExist requirement on a key some node lacks (then ExistingNode requirements can grow a key
-// and CanAdd is no longer a function of the snapshot).
+// The host routes the clusters these kernels do not model to the general path (each subset a whole device Solve,
+// batched one workgroup per subset on the cluster's superset Solve: kp_host.cpp GeneralBatch): topology spread and pod (anti-)affinity, a pod NotIn/DoesNotExist requirement on a
+// key some node lacks (ExistingNode requirements could then grow a key, and CanAdd would no longer be a function of
+// the snapshot), and catalogues holding capacity reservations (strict reservation accounting).
 
 __device__ __forceinline__ void sim_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
@@ -806,7 +808,7 @@ __global__ __launch_bounds__(ARGMAX_THREADS) void argmax_final_kernel(const Argm
 hipError_t launch_argmax(const SimOut* out, int n, ArgmaxPart* part, int n_parts, int64_t base, CommBest* dst,
                          hipStream_t s) {
   if (n > 0) hipLaunchKernelGGL(argmax_kernel, dim3(n_parts), dim3(ARGMAX_THREADS), 0, s, out, n, part);
-  else hipMemsetAsync(part, 0xFF, sizeof(ArgmaxPart) * n_parts, s);  // index -1 everywhere (counts fixed below)
+  else (void)hipMemsetAsync(part, 0xFF, sizeof(ArgmaxPart) * n_parts, s);  // index -1 everywhere (counts fixed below)
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(argmax_final_kernel, dim3(1), dim3(ARGMAX_THREADS), 0, s, part, n > 0 ? n_parts : 0, out, base, dst);

@@ -499,6 +499,19 @@ def consolidation_subsets(cluster, n_random, seed=44, max_size=100, prefixes=Tru
     return out
 
 
+def spread_cluster(catalog, n_nodes, seed=4):
+    """Config 4 with topology spread: every shape labelled app-(i % 8), every other shape zone-spread (maxSkew 1,
+    DoNotSchedule) over its app. The batched sim kernels do not model spread, so kp_cluster_prepare takes the general
+    path (each subset's SimulateScheduling a Solve on the device, the remaining nodes' pods counted)."""
+    cl = config4(catalog, n_nodes=n_nodes, seed=seed)
+    for i, sh in enumerate(cl.shapes):
+        sh.labels = dict(sh.labels or {}, app=f"app-{i % 8}")
+        if i % 2 == 0:
+            sh.topology_spread = [TopologySpread("topology.kubernetes.io/zone", 1, LabelSelector({"app": f"app-{i % 8}"}),
+                                                 "DoNotSchedule")]
+    return cl
+
+
 def random_cluster(catalog, seed, n_nodes=60, n_types=80, n_shapes=16, n_pools=2):
     """Randomized consolidation scenario: pools with taints / daemonsets / minValues, pods with selectors,
     NotIn / Gt affinities and relaxable preferences on keys every node carries, spot and uninitialized

@@ -30,3 +30,11 @@ def ctx():
     c = kpamd.Context(0)
     yield c
     c.close()
+
+
+@pytest.fixture(params=["batch", "single"])
+def general_mode(request, monkeypatch):
+    """The general consolidation path two ways: the superset Solve with batched simulations (default), and every
+    subset compiled on its own (KP_GENERAL_BATCH=0)."""
+    monkeypatch.setenv("KP_GENERAL_BATCH", "1" if request.param == "batch" else "0")
+    return request.param

@@ -13,6 +13,9 @@
                   oracle time: python tests/golden/make_fullsize_digests.py config5-1000000)
   config4-10000   computeConsolidation on the 10k-node config-4 cluster for every firstNConsolidationOption prefix
                   (candidates[0:mid+1], mid = 1..100) and 200 random subsets: every decision field
+  general-2000    the bench's general-path leg: computeConsolidation on the 2,000-node spread cluster
+                  (synth.spread_cluster: every other shape zone-spread) for the 100 firstNConsolidationOption prefixes
+                  and 200 random subsets of 2..20 candidates (synth.consolidation_subsets seed 5), every decision field
 
 Run from the repo root: python tests/golden/make_fullsize_digests.py [name ...]  (all: about 8 minutes); names given
 regenerate only those entries.
@@ -59,6 +62,15 @@ def sim_record(r):
             float(r["savings"]).hex(), int(r["n_options"]), int(r["n_pods"])]
 
 
+def general_subsets(cl):
+    import numpy as np
+    from kpamd import disruption, synth
+    cands = np.asarray(cl.candidates, dtype=np.uint32)
+    pre = [[int(x) for x in cands[:m + 1]] for m in disruption.MultiNodeConsolidation.search_prefixes(len(cands))]
+    rnd = [[int(x) for x in s] for s in synth.consolidation_subsets(cl, 200, seed=5, max_size=20, prefixes=False)]
+    return pre, rnd
+
+
 def _solves():
     from kpamd import synth
     return {"config2-50000": lambda cat: synth.config2(cat, n_pods=50_000, seed=2),
@@ -82,6 +94,14 @@ def main():
         t = time.time()
         out[name] = solve_digest(pyoracle.solve(mk()))
         print(name, out[name], f"{time.time() - t:.1f}s", flush=True)
+    if not only or "general-2000" in only:
+        t = time.time()
+        cl = synth.spread_cluster(cat, 2_000)
+        pre, rnd = general_subsets(cl)
+        res, _ = pyoracle.simulate_batch(cl, pre + rnd)
+        out["general-2000"] = {"prefixes": [sim_record(r) for r in res[:len(pre)]],
+                               "random": [sim_record(r) for r in res[len(pre):]]}
+        print("general-2000", len(res), f"{time.time() - t:.1f}s", flush=True)
     if only and "config4-10000" not in only:
         json.dump(out, open(OUT, "w"), indent=0)
         return

@@ -40,7 +40,7 @@ def _fake_offering_zones():
     return zones
 
 
-def _resolve(lib, row, zones, spot_price, offering_zones, ami_family="AL2023", **nodeclass_kw):
+def _resolve(lib, row, zones, spot_price, offering_zones, ami_family="AL2023", zone_ids=None, **nodeclass_kw):
     from kpamd import abi, catalog
     from kpamd.model import InstanceType
     arena = abi.Arena()
@@ -49,27 +49,36 @@ def _resolve(lib, row, zones, spot_price, offering_zones, ami_family="AL2023", *
     info = catalog.ec2_info(arena, row)
     cap, ovh = abi.ResourceList(), abi.ResourceList()
     assert lib.kp_instance_type_resolve(C.byref(opts), C.byref(info), C.byref(nc), C.byref(cap), C.byref(ovh)) == 0
-    reqs = catalog.compute_requirements(row, offering_zones=offering_zones, ami_family=ami_family)
-    priced = {(row["name"], z): spot_price.get((row["name"], z), 0.0) for z in catalog.ZONES}
-    offs = catalog.create_offerings(row, reqs, priced, catalog.ZONES, catalog.ZONE_IDS)
+    reqs = catalog.compute_requirements(row, zones=zones, zone_ids=zone_ids or catalog.ZONE_IDS,
+                                        offering_zones=offering_zones, ami_family=ami_family)
+    priced = {(row["name"], z): spot_price.get((row["name"], z), 0.0) for z in zones}
+    offs = catalog.create_offerings(row, reqs, priced, zones, zone_ids or catalog.ZONE_IDS)
     for o in offs:  # a spot offering without a spot price has no price (createOfferings: hasPrice false)
         if o.capacity_type == "spot" and (row["name"], o.zone) not in spot_price:
             o.available = False
     return InstanceType(row["name"], reqs, catalog.resource_dict(cap), catalog.resource_dict(ovh), offs)
 
 
-def fake_catalog(lib, ami_family="AL2023", extra_rows=(), **nodeclass_kw):
+def fake_catalog(lib, ami_family="AL2023", extra_rows=(), subnet_zones=None, spot_history=None, **nodeclass_kw):
     """The 16-type fake EC2 catalogue with its offering zones; on-demand prices from the static table, spot = the
     default price (no spot update in the instancetype suite). extra_rows: more (row, offering zones) pairs;
+    subnet_zones: the EC2NodeClass's subnet zones as [(zone, zone id)] (default the suite's three); spot_history: after
+    UpdateSpotPricing, {(type, zone): price} - only those spot offerings have a price (R:pricing.go:156-170);
     nodeclass_kw: more EC2NodeClass fields (catalog.nodeclass: block_device_mappings, instance_store_policy)."""
     from kpamd import catalog
     zones = _fake_offering_zones()
+    sz = [z for z, _ in subnet_zones] if subnet_zones else list(catalog.ZONES)
+    sid = [i for _, i in subnet_zones] if subnet_zones else list(catalog.ZONE_IDS)
     rows = [(r, zones[r["name"]]) for r in catalog.load_ec2_table() if r["name"] in zones] + list(extra_rows)
     out = []
     for r, rz in rows:
-        z = [x for x in rz if x in catalog.ZONES]
-        spot = {(r["name"], x): r["od_price"] for x in z}
-        out.append(_resolve(lib, r, catalog.ZONES, spot, z, ami_family, **nodeclass_kw))
+        z = [x for x in rz if x in sz]
+        if spot_history is None:
+            spot = {(r["name"], x): r["od_price"] for x in z}
+        else:
+            spot = {k: v for k, v in spot_history.items() if k[0] == r["name"]}
+        it = _resolve(lib, r, sz, spot, z, ami_family, zone_ids=sid, **nodeclass_kw)
+        out.append(it)
     return out
 
 
@@ -104,7 +113,9 @@ class Env:
     """One test environment: a catalogue (resident on the device for backend "device"), the fake EC2 API's
     InsufficientCapacityPools, and ExpectProvisioned."""
 
-    def __init__(self, backend, types, ctx=None, ice_pools=()):
+    def __init__(self, backend, types, ctx=None, ice_pools=(), zones=None):
+        from kpamd import catalog
+        self.zones = list(zones or catalog.ZONES)  # the EC2NodeClass's subnet zones (CreateFleet overrides)
         self.backend = backend
         self.types = types
         self.ice = set(ice_pools)  # (capacity type, instance type name, zone)
@@ -134,14 +145,14 @@ class Env:
             return []
         if self.backend == "device":
             import kpamd
-            plan = kpamd.LaunchPlan(self.ctx, self.cat, reqs, catalog.ZONES)
+            plan = kpamd.LaunchPlan(self.ctx, self.cat, reqs, self.zones)
             try:
                 out, _ = plan.run(read=True)
             finally:
                 plan.close()
             return out
         from oracle import pyoracle
-        return pyoracle.launch_select(self.types, reqs, catalog.ZONES)
+        return pyoracle.launch_select(self.types, reqs, self.zones)
 
     def mark_unavailable(self, pools):
         """UnavailableOfferings.MarkUnavailable for each (capacity type, type name, zone): SeqNum bump + re-inject."""

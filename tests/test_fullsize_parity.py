@@ -69,3 +69,27 @@ def test_consolidation_fullsize(ctx, catalog, digests):
     got = [mk.sim_record(r) for r in res]
     assert got[:len(pre)] == want["prefixes"]
     assert got[len(pre):] == want["random"]
+
+
+@pytest.mark.gpu
+def test_general_fullsize(ctx, catalog, digests, monkeypatch):
+    """The general path at the bench's size: 2,000-node spread cluster, 300 subsets batched on the superset Solve,
+    every decision field equal to the oracle's digest."""
+    import kpamd
+    import make_fullsize_digests as mk
+    from kpamd import synth
+    if "general-2000" not in digests:
+        pytest.skip("general-2000: digest not generated (make_fullsize_digests.py general-2000)")
+    monkeypatch.setenv("KP_GENERAL_BATCH", "1")
+    cl = synth.spread_cluster(catalog, 2_000)
+    pre, rnd = mk.general_subsets(cl)
+    plan = kpamd.ClusterPlan(ctx, cl)
+    try:
+        res, st = plan.simulate(pre + rnd)
+    finally:
+        plan.close()
+    assert st["phase_cycles"][:2] == [len(pre) + len(rnd), 0], "every subset batched"
+    want = digests["general-2000"]
+    got = [mk.sim_record(r) for r in res]
+    assert got[:len(pre)] == want["prefixes"]
+    assert got[len(pre):] == want["random"]

@@ -309,7 +309,7 @@ def test_gpu_random_anti_affinity(ctx, catalog, seed):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed", range(3))
-def test_gpu_consolidation_anti_affinity(ctx, catalog, seed):
+def test_gpu_consolidation_anti_affinity(ctx, catalog, seed, general_mode):
     from kpamd import synth
     from test_gpu_consolidation import check
     cl = synth.random_cluster(catalog, 70 + seed, n_nodes=[20, 30, 40][seed])

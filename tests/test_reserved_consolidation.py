@@ -124,7 +124,7 @@ def reservation_cluster(catalog, seed, n_nodes=8):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed", [70, 72, 74, 76, 78, 79])
-def test_gpu_random_reservation_clusters(ctx, lib, catalog, seed):
+def test_gpu_random_reservation_clusters(ctx, lib, catalog, seed, general_mode):
     from test_gpu_consolidation import check
     from kpamd import synth
     cl, crs = reservation_cluster(catalog, seed)

@@ -68,7 +68,7 @@ def test_product_host_compile_accepts_spread_clusters(catalog):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed", range(6))
-def test_gpu_spread_simulations(ctx, catalog, seed):
+def test_gpu_spread_simulations(ctx, catalog, seed, general_mode):
     from test_gpu_consolidation import check
     cl = cluster_with_spread(catalog, 40 + seed, n_nodes=[20, 30, 40][seed % 3])
     check(ctx, cl, subsets_of(cl, seed), multi_node=bool(seed % 2))
@@ -76,14 +76,14 @@ def test_gpu_spread_simulations(ctx, catalog, seed):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed", range(2))
-def test_gpu_missing_key_simulations(ctx, catalog, seed):
+def test_gpu_missing_key_simulations(ctx, catalog, seed, general_mode):
     from test_gpu_consolidation import check
     cl = cluster_with_missing_key(catalog, 60 + seed)
     check(ctx, cl, subsets_of(cl, seed), multi_node=bool(seed % 2))
 
 
 @pytest.mark.gpu
-def test_gpu_spread_argmin_and_disruption(ctx, catalog):
+def test_gpu_spread_argmin_and_disruption(ctx, catalog, general_mode):
     """kp_consolidate_argmin over the general path (device argmax of host-taken decisions), and the
     firstNConsolidationOption replay in kpamd.disruption on a topology cluster, against the oracle."""
     import kpamd
@@ -109,3 +109,28 @@ def test_gpu_spread_argmin_and_disruption(ctx, catalog):
             assert best["subset"] == -1
     finally:
         plan.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(4))
+def test_gpu_batched_simulations_counted(ctx, catalog, seed, monkeypatch):
+    """Every subset of a spread cluster runs batched (the superset Solve), and the decisions equal the per-subset
+    compile's subset by subset (the oracle too): batched == single == oracle, savings included."""
+    import kpamd
+    from oracle import pyoracle
+    cl = cluster_with_spread(catalog, 90 + seed, n_nodes=[16, 24, 36, 48][seed])
+    subs = subsets_of(cl, seed) + [list(cl.candidates[:k]) for k in (2, 5, 9) if k <= len(cl.candidates)]
+    runs = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("KP_GENERAL_BATCH", mode)
+        plan = kpamd.ClusterPlan(ctx, cl)
+        try:
+            runs[mode] = plan.simulate(subs, multi_node=bool(seed % 2))
+        finally:
+            plan.close()
+    (b, bst), (s, sst) = runs["1"], runs["0"]
+    assert bst["phase_cycles"][:2] == [len(subs), 0] and sst["phase_cycles"][:2] == [0, len(subs)]
+    want, _ = pyoracle.simulate_batch(cl, subs, multi_node=bool(seed % 2))
+    for i, (x, y, w) in enumerate(zip(b, s, want)):
+        assert x == y, (i, x, y)
+        assert (x["decision"], x["savings"]) == (w["decision"], w["savings"]), (i, x, w)

@@ -8,7 +8,8 @@ import csv
 import json
 import sys
 
-KERNELS = {"solve_kernel": "solve_kernel<", "feasibility_kernel": "feasibility_kernel(", "sim_kernel": "sim_kernel<",
+KERNELS = {"solve_kernel": "solve_kernel<", "feasibility_kernel": "feasibility_kernel(",
+           "feasibility_bits_kernel": "feasibility_bits_kernel(", "sim_kernel": "sim_kernel<",
            "finalize_kernel": "finalize_kernel("}
 
 
