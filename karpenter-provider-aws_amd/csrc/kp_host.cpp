@@ -820,7 +820,7 @@ std::shared_ptr<ReqOut> DecodeReqs(const Dict& d, const KReqs& q) {
   auto o = std::make_shared<ReqOut>();
   vector<int> ks;
   for (int k = 0; k < d.dd.K; k++)
-    if ((q.present >> k) & 1) ks.push_back(k);
+    if (((q.present >> k) & 1) && d.keys[k] != kHostname) ks.push_back(k);  // (the NodeClaim's placeholder)
   std::sort(ks.begin(), ks.end(), [&](int a, int b) { return d.keys[a] < d.keys[b]; });
   for (int k : ks) {
     const bool bnd = k < KP_MAX_BOUND_KEYS, c = (q.compl_ >> k) & 1;
@@ -2041,8 +2041,26 @@ struct SolveRaw {
   vector<vector<vector<RawReqs>>> filter_levels;  // per level: MakeTopologyNodeFilter's terms (nodeSelector + each
                                                   // remaining required term; the nodeSelector alone when none)
   std::set<string> topo_keys;                     // non-hostname spread keys (need a dictionary id)
-  vector<RawReqs> ex_labels;                      // per input existing node (hostname dropped)
+  vector<RawReqs> ex_labels;                      // per input existing node (hostname: see HostnameValue)
+  bool hostname = false;                          // some pod requirement names kubernetes.io/hostname
 };
+
+// kubernetes.io/hostname as a requirement key. Upstream gives every NodeClaim `hostname In {a unique placeholder}`
+// (NewNodeClaim) and every existing node `hostname In {its hostname}` (NewExistingNode: the label, else the node
+// name). A pod's hostname requirement only ever compares those values with the ones it names, so the dictionary
+// holds the named values plus two stand-ins: kHostOther for every hostname no pod names, kHostPlaceholder for the
+// NodeClaims' (templates carry it; the decoded NodeClaim requirements drop it, as FinalizeScheduling does).
+const char* kHostOther = "\x01other-hostname";
+const char* kHostPlaceholder = "\x01hostname-placeholder";
+
+void HostnameNames(const kp_requirements& r, bool* used, std::set<string>* named) {
+  for (uint32_t i = 0; i < r.n; i++) {
+    const kp_requirement& x = r.items[i];
+    if (!x.key || string(x.key) != kHostname) continue;
+    *used = true;
+    for (uint32_t j = 0; j < x.n_values; j++) named->insert(x.values[j] ? x.values[j] : "");
+  }
+}
 
 void KeyReqs(string& o, const RawReqs& rs) {
   for (auto& r : rs) {
@@ -2126,6 +2144,18 @@ int32_t ParseSolve(const kp_solve_in* in, SolveRaw& raw) {
   if (in->n_catalogs == 0 || !in->catalogs) return fail(KP_E_INVAL, "no catalogues");
   for (uint32_t c = 0; c < in->n_catalogs; c++)
     if (!in->catalogs[c]) return fail(KP_E_INVAL, "null catalogue");
+  std::set<string> host_named;  // hostname values the pods' requirements name
+  for (uint32_t s = 0; s < in->n_shapes; s++) {
+    const kp_pod_shape& sh = in->shapes[s];
+    for (uint32_t j = 0; j < sh.n_node_selector; j++)
+      if (sh.node_selector[j].key && string(sh.node_selector[j].key) == kHostname) {
+        raw.hostname = true;
+        host_named.insert(sh.node_selector[j].value ? sh.node_selector[j].value : "");
+      }
+    for (uint32_t j = 0; j < sh.n_required_terms; j++) HostnameNames(sh.required_terms[j], &raw.hostname, &host_named);
+    for (uint32_t j = 0; j < sh.n_preferred_terms; j++) HostnameNames(sh.preferred_terms[j].preference, &raw.hostname, &host_named);
+    HostnameNames(kp_requirements{sh.volume_requirements, sh.n_volume_requirements, 0}, &raw.hostname, &host_named);
+  }
   raw.np_reqs.resize(in->n_nodepools);
   raw.np_taints.resize(in->n_nodepools);
   for (uint32_t i = 0; i < in->n_nodepools; i++) {
@@ -2137,6 +2167,7 @@ int32_t ParseSolve(const kp_solve_in* in, SolveRaw& raw) {
     r.push_back({kNodePool, KP_OP_IN, {np.name ? np.name : ""}, -1});
     for (auto& x : r)
       if (x.key == kHostname) return fail(KP_E_UNSUPPORTED, "hostname requirement on nodepool");
+    if (raw.hostname) r.push_back({kHostname, KP_OP_IN, {kHostPlaceholder}, -1});  // NewNodeClaim's placeholder
     raw.np_reqs[i] = std::move(r);
     for (uint32_t j = 0; j < np.n_taints; j++)
       raw.np_taints[i].push_back({np.taints[j].key ? np.taints[j].key : "", np.taints[j].value ? np.taints[j].value : "",
@@ -2196,8 +2227,6 @@ int32_t ParseSolve(const kp_solve_in* in, SolveRaw& raw) {
       RawReqs r = ns;
       if (!pref.empty()) r.insert(r.end(), pref[0].second.begin(), pref[0].second.end());
       if (!req.empty()) r.insert(r.end(), req[0].begin(), req[0].end());
-      for (auto& x : r)
-        if (x.key == kHostname) return fail(KP_E_UNSUPPORTED, "hostname requirement on pod");
       raw.levels[s].push_back(std::move(r));
       RawReqs strict = ns;  // NewStrictPodRequirements: without the preferred term
       if (!req.empty()) strict.insert(strict.end(), req[0].begin(), req[0].end());
@@ -2238,8 +2267,17 @@ int32_t ParseSolve(const kp_solve_in* in, SolveRaw& raw) {
       if (k && k[0] && string(k) != kHostname) raw.topo_keys.insert(k);
     }
   raw.ex_labels.resize(in->n_existing);
-  for (uint32_t i = 0; i < in->n_existing; i++)
-    raw.ex_labels[i] = LabelReqs(in->existing[i].labels, in->existing[i].n_labels, true);
+  for (uint32_t i = 0; i < in->n_existing; i++) {
+    const kp_existing_node& e = in->existing[i];
+    raw.ex_labels[i] = LabelReqs(e.labels, e.n_labels, true);
+    if (raw.hostname) {  // NewExistingNode: hostname In {HostName()} (the label, else the node name)
+      string host;
+      for (uint32_t j = 0; j < e.n_labels; j++)
+        if (e.labels[j].key && string(e.labels[j].key) == kHostname && e.labels[j].value) host = e.labels[j].value;
+      if (host.empty()) host = e.name ? e.name : "";
+      raw.ex_labels[i].push_back({kHostname, KP_OP_IN, {host_named.count(host) ? host : string(kHostOther)}, -1});
+    }
+  }
   return KP_OK;
 }
 
@@ -4372,6 +4410,17 @@ int32_t kp_cluster_prepare(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan** 
     topo |= cl->catalogs && cl->catalogs[i] && cl->catalogs[i]->reservations;
   for (uint32_t i = 0; i < cl->n_shapes; i++)
     topo |= cl->shapes[i].n_topology_spread > 0 || PodTermCount(cl->shapes[i]) > 0;
+  {  // a pod requirement on kubernetes.io/hostname (the batched kernels' node compatibility drops the hostname)
+    std::set<string> named;
+    for (uint32_t i = 0; i < cl->n_shapes && !topo; i++) {
+      const kp_pod_shape& sh = cl->shapes[i];
+      for (uint32_t j = 0; j < sh.n_node_selector; j++)
+        topo |= sh.node_selector[j].key && string(sh.node_selector[j].key) == kHostname;
+      for (uint32_t j = 0; j < sh.n_required_terms; j++) HostnameNames(sh.required_terms[j], &topo, &named);
+      for (uint32_t j = 0; j < sh.n_preferred_terms; j++) HostnameNames(sh.preferred_terms[j].preference, &topo, &named);
+      HostnameNames(kp_requirements{sh.volume_requirements, sh.n_volume_requirements, 0}, &topo, &named);
+    }
+  }
   if (topo) return PrepareGeneral(ctx, cl, out, t0);
   std::lock_guard<std::recursive_mutex> lock(ctx->mu);
   HIPCHK(hipSetDevice(ctx->device));
