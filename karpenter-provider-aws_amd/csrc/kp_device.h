@@ -91,8 +91,10 @@ struct SolveArgs {
   int32_t* nc_fail;                  // [SL][ncc]
   int32_t* ex_ver;                   // [E]
   int32_t* ex_fail;                  // [SL][E]
-  int32_t* tmpl_ver;                 // [NT]
-  int32_t* tmpl_fail;                // [SL][NT]
+  int32_t* tmpl_ver;                 // [NT] bumped when the template's remaining limits change (subtractMax)
+  int32_t* tmpl_fail;                // [SL][NT] NC_NEVER: the template fails the shape-level for good
+  uint64_t* tmpl_xlim;               // [NT][TW] the template's options after filterByRemainingResources ...
+  int32_t* tmpl_xlim_ver;            // [NT] ... as of this tmpl_ver (-1: never computed)
   int64_t* nc_maxalloc;              // [P][NRES] max allocatable over the NodeClaim's types at creation
   int32_t* nc_fitj;                  // [P][NRES] threshold index of the last Fits per resource
   int32_t* nc_cat;                   // [P] catalogue of the NodeClaim's template

@@ -2798,7 +2798,7 @@ struct SolveOffs {
   size_t pristine = 0, ncr = 0, ncX = 0, ncrq = 0, nct = 0, npods = 0, order = 0, chkblk = 0, maxalloc = 0, fitj = 0,
          nchead = 0, nccat = 0, nchp = 0, place = 0, events = 0, stats = 0, ver0 = 0, exver = 0, tver = 0, curnc = 0,
          curex = 0, held = 0, ver_end = 0, fail0 = 0, ncfail = 0, exfail = 0, tfail = 0, chkdead = 0, fail_end = 0,
-         opts = 0, nrem = 0, nopt = 0, hcnc = 0, nctc = 0, arena_end = 0;
+         opts = 0, nrem = 0, nopt = 0, hcnc = 0, nctc = 0, txl = 0, txlv = 0, arena_end = 0;
   size_t n_hcnc = 0;
   int ncc = 0, chk_dead_rows = 0, sort_cap = 0, opt_stride = 0;
   bool chk_on = false;
@@ -2934,10 +2934,12 @@ void ReserveArenaDev(Blob& blob, const Compiled& C, int Pc, int opt_stride, int 
   o.ncfail = blob.reserve_dev(sizeof(int32_t) * SLn * o.ncc);
   o.exfail = blob.reserve_dev(sizeof(int32_t) * SLn * std::max(E, 1));
   o.tfail = blob.reserve_dev(sizeof(int32_t) * SLn * std::max(NT, 1));
+  o.txlv = blob.reserve_dev(sizeof(int32_t) * std::max(NT, 1));  // -1: not computed
   o.chk_dead_rows = o.chk_on ? (int)std::min<size_t>(SLn, ((size_t)64 << 20) / (4 * CHK_MAXC)) : 0;
   o.chkdead = blob.reserve_dev(std::max<size_t>(sizeof(int32_t) * o.chk_dead_rows * CHK_MAXC, 8));
   o.fail_end = blob.total();
   o.opt_stride = opt_stride;
+  o.txl = blob.reserve_dev(sizeof(uint64_t) * (size_t)std::max(NT, 1) * TW);
   o.opts = blob.reserve_dev(sizeof(uint32_t) * (size_t)Pc * opt_stride);
   o.nrem = blob.reserve_dev(sizeof(uint32_t) * Pc);
   o.nopt = blob.reserve_dev(sizeof(uint32_t) * Pc);
@@ -3006,6 +3008,8 @@ void BindSolve(SolveArgs& a, const Compiled& C, const SolveOffs& o, uint8_t* sh,
   a.ex_fail = (int32_t*)(ar + o.exfail);
   a.tmpl_ver = (int32_t*)(ar + o.tver);
   a.tmpl_fail = (int32_t*)(ar + o.tfail);
+  a.tmpl_xlim = (uint64_t*)(ar + o.txl);
+  a.tmpl_xlim_ver = (int32_t*)(ar + o.txlv);
   a.cur_nc = (int32_t*)(ar + o.curnc);
   a.cur_ex = (int32_t*)(ar + o.curex);
   a.nc_maxalloc = (int64_t*)(ar + o.maxalloc);
@@ -4363,8 +4367,10 @@ bool NodeCandidatePrice(const HostType& t, const std::map<string, string>& label
 
 extern "C" {
 
-// A cluster plan for the general path: the cluster is validated by a host compile (every node existing, every pod
-// pending) and kept as an owned copy; nothing is uploaded until a batch runs.
+struct GeneralBatch;
+static int32_t GeneralBatchBuild(kp_cluster_plan* plan, std::shared_ptr<GeneralBatch>& out);
+// A cluster plan for the general path: the cluster is kept as an owned copy and compiled as the batched simulations'
+// superset Solve (or, where that does not apply, validated by a host compile: every node existing, every pod pending).
 static int32_t PrepareGeneral(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan** out,
                               std::chrono::steady_clock::time_point t0) {
   for (uint32_t i = 0; i < cl->n_catalogs; i++)
@@ -4387,13 +4393,27 @@ static int32_t PrepareGeneral(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan
   in.namespaces = cl->namespaces;
   in.n_namespaces = cl->n_namespaces;
   in.pod_uids = cl->pod_uids;
-  Compiled C;
-  int32_t rc = CompileSolve(&in, C);
-  if (rc) return rc;
   auto plan = std::make_unique<kp_cluster_plan>();
   plan->ctx = ctx;
   plan->N = (int)cl->n_nodes;
   plan->general = std::make_unique<OwnedCluster>(cl);
+  // the superset Solve of the batched simulations, built now (it validates every node and pod as well); a cluster
+  // it does not take keeps the per-subset compile, validated here by the whole-cluster compile
+  const char* gbe = getenv("KP_GENERAL_BATCH");
+  int32_t rc = KP_E_UNSUPPORTED;
+  if (!(gbe && gbe[0] == '0')) {
+    std::lock_guard<std::recursive_mutex> lock(ctx->mu);
+    HIPCHK(hipSetDevice(ctx->device));
+    plan->gb_tried = true;
+    rc = GeneralBatchBuild(plan.get(), plan->gb);
+    if (rc && rc != KP_E_UNSUPPORTED) return rc;
+    if (rc) plan->gb.reset();
+  }
+  if (rc) {
+    Compiled C;
+    rc = CompileSolve(&in, C);
+    if (rc) return rc;
+  }
   plan->prepare_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   *out = plan.release();
   return KP_OK;
@@ -4800,6 +4820,69 @@ double WorstLaunch(const Dict& d, const KReqs& R, const HostType& t, bool spot_o
 
 static int32_t SolvePrepare(kp_ctx* ctx, const kp_solve_in* in, kp_comm* comm, kp_solve_plan** out);
 
+// The offerings as OfferAdmits reads them, resolved against one dictionary once (the batched decisions run
+// WorstLaunch over up to 100 options per simulation): per offering its capacity-type class and the dictionary bits
+// of its five offering keys (-1: a value the dictionary lacks, -2: the offering has no such requirement).
+struct OffBits {
+  int16_t ct_class;  // 0 reserved, 1 spot, 2 on-demand, 3 other
+  int16_t b[5];      // capacity type, zone, zone id, reservation id, reservation type
+};
+struct OfferTab {
+  int k[5];                                  // the five keys' dictionary ids (-1: absent)
+  vector<vector<vector<OffBits>>> off;       // [catalogue][type][offering]
+  void Build(const Dict& d, const kp_cluster& cl) {
+    const char* keys[5] = {kCapType, kZone, kZoneID, kResID, kResType};
+    for (int i = 0; i < 5; i++) k[i] = d.key(keys[i]);
+    off.assign(cl.n_catalogs, {});
+    for (uint32_t c = 0; c < cl.n_catalogs; c++) {
+      const vector<HostType>& types = cl.catalogs[c]->types;
+      off[c].resize(types.size());
+      for (size_t t = 0; t < types.size(); t++)
+        for (const HostOffering& o : types[t].offs) {
+          OffBits x;
+          x.ct_class = o.ct == "reserved" ? 0 : o.ct == "spot" ? 1 : o.ct == "on-demand" ? 2 : 3;
+          const string* v[5] = {&o.ct, &o.zone, &o.zid, &o.rid, &o.rt};
+          const bool has[5] = {true, o.has_zone, o.has_zid, o.has_rid, o.has_rt};
+          for (int i = 0; i < 5; i++) x.b[i] = !has[i] ? -2 : k[i] < 0 ? -1 : (int16_t)std::max(-1, d.bit(k[i], *v[i]));
+          off[c][t].push_back(x);
+        }
+    }
+  }
+  // OfferAdmits on the resolved bits
+  bool Admits(const Dict& d, const KReqs& R, const OffBits& x) const {
+    for (int i = 0; i < 5; i++) {
+      const int kk = k[i];
+      if (kk < 0 || !((R.present >> kk) & 1)) continue;  // undefined well-known key: allowed
+      if (x.b[i] == -2) {
+        if (i < 3) continue;  // no zone / zone-id requirement on the offering
+        const bool c = ((R.compl_ >> kk) & 1) != 0, nz = KeyNonEmptyVals(d, R, kk);  // DoesNotExist on it
+        if (!((c && nz) || (!c && !nz))) return false;
+      } else if (x.b[i] == -1) {
+        if (!((R.compl_ >> kk) & 1)) return false;
+      } else if (!Has(d, R, kk, x.b[i])) {
+        return false;
+      }
+    }
+    return true;
+  }
+  // WorstLaunch on the resolved bits
+  double Worst(const Dict& d, const KReqs& R, const HostType& t, const vector<OffBits>& ob, bool spot_only) const {
+    for (int cls = 0; cls < 3; cls++) {
+      if (spot_only && cls != 1) continue;
+      bool any = false;
+      double mx = 0;
+      for (size_t i = 0; i < t.offs.size(); i++) {
+        const HostOffering& o = t.offs[i];
+        if (!o.available || ob[i].ct_class != cls || !Admits(d, R, ob[i])) continue;
+        if (!any || o.price > mx) mx = o.price;
+        any = true;
+      }
+      if (any) return mx;
+    }
+    return std::numeric_limits<double>::max();
+  }
+};
+
 // computeConsolidation's decision on one simulation's Solve (sim_kernel's decision; disruption.md:89-128). all: every
 // non-pending pod was scheduled (and no candidate pod onto an uninitialized node). The Solve made n_nc NodeClaims;
 // R / ci / nodepool / opts: the first one's final requirements (held reservation ids applied), catalogue, NodePool and
@@ -4807,7 +4890,7 @@ static int32_t SolvePrepare(kp_ctx* ctx, const kp_solve_in* in, kp_comm* comm, k
 static void GeneralDecide(const kp_cluster& cl, const vector<std::map<string, string>>& labels,
                           const vector<uint32_t>& cand, const SolveBase& B, bool all, int n_nc, const KReqs* R,
                           int ci, uint32_t nodepool, const uint32_t* opts, uint32_t n_opts, int32_t multi_node,
-                          SimOut& r) {
+                          SimOut& r, const OfferTab* tab = nullptr) {
   double candPrice = 0;
   bool priced = true, allSpot = true;
   for (uint32_t c : cand) {
@@ -4838,9 +4921,12 @@ static void GeneralDecide(const kp_cluster& cl, const vector<std::map<string, st
   const bool ncSpot = kct < 0 || !((R->present >> kct) & 1) || (bspot >= 0 ? Has(d, *R, kct, bspot) : ((R->compl_ >> kct) & 1));
   const bool s2s = allSpot && ncSpot;  // spot-to-spot: only behind the feature gate
   if (s2s && !cl.spot_to_spot) return;
+  auto worst = [&](int t) {
+    return tab ? tab->Worst(d, *R, types[t], tab->off[ci][t], s2s) : WorstLaunch(d, *R, types[t], s2s);
+  };
   vector<int> kept;
   for (uint32_t i = 0; i < n_opts; i++)
-    if (WorstLaunch(d, *R, types[opts[i]], s2s) < candPrice) kept.push_back((int)opts[i]);
+    if (worst((int)opts[i]) < candPrice) kept.push_back((int)opts[i]);
   if (hasMin && !HostMinValuesOK(d, hc, *R, kept)) return;
   if (kept.empty()) return;
   if (multi_node) {  // filterOutSameType
@@ -4860,7 +4946,7 @@ static void GeneralDecide(const kp_cluster& cl, const vector<std::map<string, st
     }
     vector<int> k2;
     for (int t : kept)
-      if (WorstLaunch(d, *R, types[t], s2s) < maxPrice) k2.push_back(t);
+      if (worst(t) < maxPrice) k2.push_back(t);
     if (hasMin && !HostMinValuesOK(d, hc, *R, k2)) return;
     kept.swap(k2);
     if (kept.empty()) return;
@@ -4870,7 +4956,7 @@ static void GeneralDecide(const kp_cluster& cl, const vector<std::map<string, st
     kept.resize(std::min<size_t>(kept.size(), hasMin ? 100 : 15));
   }
   double best = std::numeric_limits<double>::max();
-  for (int t : kept) best = std::min(best, WorstLaunch(d, *R, types[t], s2s));
+  for (int t : kept) best = std::min(best, worst(t));
   r.decision = KP_DECISION_REPLACE;
   r.nodepool = nodepool;
   r.replacement_price = best;
@@ -5012,6 +5098,7 @@ struct GeneralBatch {
   vector<uint8_t> ex_static;
   vector<int32_t> regcnt;       // [G * 64] existing nodes registering each (group, ordinal)
   vector<int32_t> live0;        // [G] liveness with only the base pods queued
+  OfferTab offers;              // the decisions' offering bits (the superset's dictionary)
   uint32_t rmask = 0;
   int res_mode = 0, opt_stride = 100, tf_words = 0;
   bool tfeas_on = false;
@@ -5133,6 +5220,7 @@ static int32_t GeneralBatchBuild(kp_cluster_plan* plan, std::shared_ptr<GeneralB
   }
   gb->rmask = RequestedResources(C);
   gb->ex_static = ExStatic(C, gb->rmask);
+  gb->offers.Build(C.B->d, cl);
   gb->res_mode = !C.B->res_cls ? 0 : 2;
   gb->opt_stride = 100;
   // the shared region: read-only data of every simulation + the template-options table
@@ -5348,7 +5436,7 @@ static int32_t GeneralBatchRun(kp_cluster_plan* plan, GeneralBatch& gb, const ve
     fill(o.ver0, o.ver_end - o.ver0, 0);
     fill(o.fail0, o.fail_end - o.fail0, 0xFF);
     if (o.n_hcnc) fill(o.hcnc, o.n_hcnc, 0);
-    *host_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count();
+    host_ms[0] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count();
     HIPCHK(launch_batch_init(bi, n, st));
     HIPCHK(hipMemcpy2DAsync(arenas, gb.stride, patches.data(), patch_bytes, patch_bytes, n, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(dargs, sargs.data(), sizeof(SolveArgs) * n, hipMemcpyHostToDevice, st));
@@ -5408,9 +5496,9 @@ static int32_t GeneralBatchRun(kp_cluster_plan* plan, GeneralBatch& gb, const ve
         np = (uint32_t)C.B->tmpl_nodepool[nct[j]];
       }
       GeneralDecide(cl, labels, cands[i], *C.B, all, n_nc, &R, ci, np, &opts[(size_t)j * gb.opt_stride],
-                    n_nc == 1 ? nopt[j] : 0, multi_node, r);
+                    n_nc == 1 ? nopt[j] : 0, multi_node, r, &gb.offers);
     }
-    *host_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th1).count();
+    host_ms[1] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th1).count();
   }
   return KP_OK;
 }
@@ -5467,7 +5555,7 @@ static int32_t GeneralSimLocked(kp_cluster_plan* plan, const uint32_t* offsets, 
   vector<SimOut> outs(n_subsets);
   memset(outs.data(), 0, sizeof(SimOut) * outs.size());
   uint64_t counters[3] = {0, 0, 0};
-  double dev_ms = 0, host_ms = 0;
+  double dev_ms = 0, host_ms[2] = {0, 0};  // the batch's host work: overlays + arguments, decisions
   vector<int> batched, single;
   for (uint32_t s = 0; s < n_subsets; s++) {
     bool ok = batch_on && plan->gb;
@@ -5482,7 +5570,7 @@ static int32_t GeneralSimLocked(kp_cluster_plan* plan, const uint32_t* offsets, 
   }
   const auto t1 = clk::now();
   if (!batched.empty()) {
-    const int32_t rc = GeneralBatchRun(plan, *plan->gb, cands, batched, labels, multi_node, outs, counters, &dev_ms, &host_ms);
+    const int32_t rc = GeneralBatchRun(plan, *plan->gb, cands, batched, labels, multi_node, outs, counters, &dev_ms, host_ms);
     if (rc) return rc;
   }
   const double t_batch = std::chrono::duration<double, std::milli>(clk::now() - t1).count();
@@ -5510,8 +5598,9 @@ static int32_t GeneralSimLocked(kp_cluster_plan* plan, const uint32_t* offsets, 
   plan->general_ms = dev_ms;
   plan->general_batched = (uint32_t)batched.size();
   if (getenv("KP_HOST_TIMING"))
-    fprintf(stderr, "[kp general] %u sims (%zu batched, %zu single): setup %.2f batch %.2f (host %.2f device %.2f) "
-            "single %.2f ms\n", n_subsets, batched.size(), single.size(), t_setup, t_batch, host_ms, dev_ms, t_single);
+    fprintf(stderr, "[kp general] %u sims (%zu batched, %zu single): setup %.2f batch %.2f (overlays %.2f decisions %.2f "
+            "device %.2f) single %.2f ms\n", n_subsets, batched.size(), single.size(), t_setup, t_batch, host_ms[0],
+            host_ms[1], dev_ms, t_single);
   return KP_OK;
 }
 

@@ -3274,8 +3274,10 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a0, const Solv
       // ---- addToNewNodeClaim: templates in weight order --------------------------------------------
       for (int base = 0; base < a.n_tmpl && placed == -1; base += NT) {
         const int t = base + tid;
+        // a memoised failure is permanent: remaining limits only shrink, and the rest is a function of the
+        // (template, shape-level) pair (failures that depend on topology counts or reservations are not memoised)
         const bool cand = t < a.n_tmpl && ((tolmask >> a.tmpl_taintset[t]) & 1) &&
-                          a.tmpl_fail[(size_t)sl * a.n_tmpl + t] != a.tmpl_ver[t];
+                          a.tmpl_fail[(size_t)sl * a.n_tmpl + t] != NC_NEVER;
         const int n = compact_candidates<NW>(cand, t, s_list, s_wcnt);
         for (int r0 = 0; r0 < n; r0 += NW) {
           const int li = r0 + wave;
@@ -3290,22 +3292,29 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a0, const Solv
             X = lane < D.TW ? a.tmpl_X[(size_t)tm * D.TW + lane] : 0;
             const uint32_t lim = a.tmpl_limit_present[tm];
             if (lim) {  // filterByRemainingResources: capacity <= remaining for every limited resource
-              // lane l tests type 64 i + l of word i (coalesced capacity rows, independent loads across words)
-              const int64_t* rem = a.tmpl_remaining + (size_t)tm * KP_NRES;
-              uint64_t keep = 0;
-              for (int i = 0; i < D.TW; i++) {
-                const uint64_t w = lane_bcast(X, i);
-                if (!w) continue;
-                const int ty = i * 64 + lane;
-                bool viable = ((w >> lane) & 1) && ty < D.T;
-                for (uint32_t rm = lim; rm && viable; rm &= rm - 1) {
-                  const int r = __builtin_ctz(rm);
-                  viable = H->d.cap[(size_t)r * D.T + ty] <= rem[r];
+              const int32_t ver = a.tmpl_ver[tm];
+              if (a.tmpl_xlim_ver[tm] == ver) {  // computed since the last subtractMax on this template
+                X = lane < D.TW ? a.tmpl_xlim[(size_t)tm * D.TW + lane] : 0;
+              } else {
+                // lane l tests type 64 i + l of word i (coalesced capacity rows, independent loads across words)
+                const int64_t* rem = a.tmpl_remaining + (size_t)tm * KP_NRES;
+                uint64_t keep = 0;
+                for (int i = 0; i < D.TW; i++) {
+                  const uint64_t w = lane_bcast(X, i);
+                  if (!w) continue;
+                  const int ty = i * 64 + lane;
+                  bool viable = ((w >> lane) & 1) && ty < D.T;
+                  for (uint32_t rm = lim; rm && viable; rm &= rm - 1) {
+                    const int r = __builtin_ctz(rm);
+                    viable = H->d.cap[(size_t)r * D.T + ty] <= rem[r];
+                  }
+                  const uint64_t bal = __ballot(viable);
+                  if (lane == i) keep = bal;
                 }
-                const uint64_t bal = __ballot(viable);
-                if (lane == i) keep = bal;
+                X = keep;
+                if (lane < D.TW) a.tmpl_xlim[(size_t)tm * D.TW + lane] = X;
+                if (lane == 0) a.tmpl_xlim_ver[tm] = ver;
               }
-              X = keep;
               bytes += (uint64_t)D.T * 8;
             }
             bool memo = true;
@@ -3343,7 +3352,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a0, const Solv
                 }
               }
             }
-            if (!ok && memo && lane == 0) a.tmpl_fail[(size_t)sl * a.n_tmpl + tm] = a.tmpl_ver[tm];
+            if (!ok && memo && lane == 0) a.tmpl_fail[(size_t)sl * a.n_tmpl + tm] = NC_NEVER;
           }
           if (lane == 0) s_ok[wave] = ok ? 1 : 0;
           __syncthreads();

@@ -38,6 +38,12 @@ if os.environ.get("KP_TIMING"):
     tot = sum(st["phase_cycles"]) or 1
     out["phase_share"] = {k: round(v / tot, 4) for k, v in zip(names, st["phase_cycles"])}
     out["cycles_per_pop"] = round(tot / pops, 1)
+    fp = max(1, st["fast_pods"])
+    out["fast_cycles_per_fast_pod"] = dict(zip(["pop", "stage", "sort", "prepass", "attempts", "commit"],
+                                               [round(c / fp, 1) for c in st["fast_cycles"]]))
+    if "fine" in os.environ.get("KP_LIB", ""):  # FT_FINE build: attempt_cycles = the fast lane's finer split
+        out["fast_fine_per_fast_pod"] = dict(zip(["window", "stage", "cursor", "sort", "nc-loads", "fits", "commit",
+                                                   "same-nc"], [round(c / fp, 1) for c in st["attempt_cycles"]]))
 res = plan.run(read=True)
 out["nodeclaims"] = len(res["nodeclaims"])
 out["unschedulable"] = int((res["placement"] == -1).sum())
