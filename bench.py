@@ -184,6 +184,11 @@ def main():
     progress("feasibility done")
     if not args.quick:
         cfgs = {}
+        # config 2 with ReplicaSet bursts (each deployment's pods created within 2 s): 109-pod same-level runs
+        cfgs["config2_burst"] = _solve_leg("config2_burst", synth.config2(cat, n_pods=args.pods, seed=2, burst=True), ctx,
+                                           barrier, max_over_ranks, world, args.steps, 1, kcomm,
+                                           None if (rank or world > 1 or args.no_cpu_baseline) else ("2b", 10_000))
+        progress("config2 burst done")
         cfgs["config1"] = _solve_leg("config1", synth.config1(cat, n_pods=1000, seed=1), ctx, barrier,
                                      max_over_ranks, world, args.steps, 1, kcomm,
                                      None if (rank or world > 1 or args.no_cpu_baseline) else ("1", 1000))
@@ -261,6 +266,7 @@ def _cpu_baseline_cfg(cfg, n):
     from oracle import pyoracle
     cat = catalog.build_catalog(kpamd.load_lib())
     prob = {"1": lambda: synth.config1(cat, n_pods=n, seed=1),
+            "2b": lambda: synth.config2(cat, n_pods=n, seed=2, burst=True),
             "3": lambda: synth.config3(cat, n_pods=n, n_deployments=max(1, n // 50), n_existing=max(1, n // 20)),
             "5": lambda: synth.config5(cat, n_pods=n)}[cfg]()
     t0 = time.perf_counter()

@@ -3,6 +3,8 @@
 
   config2-50000   Solve of config 2 at 50k pods: digest of the placement array and of the NodeClaims
                   (nodepool, pods in add order, options after OrderByPrice + Truncate, requirements)
+  config2-burst-50000  config 2 with ReplicaSet bursts (synth.config2(burst=True): each deployment's pods created
+                  within 2 s of its start): same digests
   config3-100000  Solve of config 3 at 100k pods (zone + hostname spread onto 5k existing nodes): same digests
   config5-100000  Solve of config 5 (20 weighted pools, GPU/Neuron pools) at 100k pods: 17.5k NodeClaims, so the
                   device's newNodeClaims order spills past its 8,192-entry LDS capacity on its own
@@ -74,6 +76,7 @@ def general_subsets(cl):
 def _solves():
     from kpamd import synth
     return {"config2-50000": lambda cat: synth.config2(cat, n_pods=50_000, seed=2),
+            "config2-burst-50000": lambda cat: synth.config2(cat, n_pods=50_000, seed=2, burst=True),
             "config3-100000": lambda cat: synth.config3(cat, n_pods=100_000),
             "config5-100000": lambda cat: synth.config5(cat, n_pods=100_000),
             "config5-limits-100000": lambda cat: synth.config5(cat, n_pods=100_000, limit_div=10),

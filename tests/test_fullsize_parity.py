@@ -37,8 +37,8 @@ def test_fixture_shape(digests):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["config2-50000", "config3-100000", "config5-100000", "config5-limits-100000",
-                                  "config5-1000000"])
+@pytest.mark.parametrize("name", ["config2-50000", "config2-burst-50000", "config3-100000", "config5-100000",
+                                  "config5-limits-100000", "config5-1000000"])
 def test_solve_fullsize(ctx, catalog, digests, name):
     import kpamd
     import make_fullsize_digests as mk

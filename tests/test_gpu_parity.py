@@ -183,3 +183,11 @@ def test_feasibility_lds_staged_equals_global(ctx, catalog, monkeypatch):
         want_k, want_c = pyoracle.compatible_available_filter(catalog, *queries[qi])
         assert (k1[qi] == want_k).all(), f"row {qi}"
         np.testing.assert_array_equal(c1[qi][want_k], want_c[want_k])
+
+
+@pytest.mark.parametrize("n_pods", [3_000, 12_000])
+def test_config2_burst(ctx, catalog, n_pods):
+    """config 2 with ReplicaSet bursts (long same-shape-level runs onto one NodeClaim)."""
+    from kpamd import synth
+    got, want = run_both(ctx, synth.config2(catalog, n_pods=n_pods, seed=5, burst=True))
+    check_same(got, want)

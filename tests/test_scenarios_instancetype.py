@@ -15,9 +15,9 @@ suite applies it, its Windows 2022 NodePool / EC2NodeClass (:172-216).
   :1033-1049 local zones: the only subnet in test-zone-1a-local, a pod requiring that zone is scheduled
   :2245-2310 spot priced in test-zone-1a only: a spot m5.large NodePool pinned to test-zone-1b cannot launch; unpinned
             it launches
-Not transcribed: :639-711 (vpc.amazonaws.com/PrivateIPv4Address, a Windows extended resource outside the device's
-11-resource model) and the deprecated accelerator labels the fake puts on g4dn.8xlarge (:254-258, the suite's own
-TODO: a GPU type carries Neuron labels only in the fake data).
+The Windows vpc.amazonaws.com/PrivateIPv4Address cases (:639-711) are in tests/test_reference_scenarios.py. Not
+transcribed: the accelerator labels the fake puts on g4dn.8xlarge (:254-258, the suite's own TODO: a GPU type carries
+Neuron labels only in the fake data; here the individual-label test finds them on inf2).
 """
 import pytest
 
