@@ -4883,6 +4883,27 @@ struct OfferTab {
   }
 };
 
+// getCandidatePrices' per-node terms, once per cluster plan (the nodes' labels and offerings do not change between
+// batches; a catalogue refresh rebuilds the batch and with it this cache)
+struct CandCache {
+  vector<double> price;        // cheapest label-compatible offering price
+  vector<char> priced, spot;   // some offering is compatible; the node is labelled spot
+  void Build(const kp_cluster& cl, const vector<std::map<string, string>>& labels) {
+    const int N = (int)cl.n_nodes;
+    price.assign(N, 0);
+    priced.assign(N, 0);
+    spot.assign(N, 0);
+    for (int c = 0; c < N; c++) {
+      const kp_cluster_node& n = cl.nodes[c];
+      double p = 0;
+      priced[c] = NodeCandidatePrice(cl.catalogs[n.catalog]->types[n.instance_type], labels[c], &p) ? 1 : 0;
+      price[c] = p;
+      auto f = labels[c].find(kCapType);
+      spot[c] = f != labels[c].end() && f->second == "spot";
+    }
+  }
+};
+
 // computeConsolidation's decision on one simulation's Solve (sim_kernel's decision; disruption.md:89-128). all: every
 // non-pending pod was scheduled (and no candidate pod onto an uninitialized node). The Solve made n_nc NodeClaims;
 // R / ci / nodepool / opts: the first one's final requirements (held reservation ids applied), catalogue, NodePool and
@@ -4890,10 +4911,16 @@ struct OfferTab {
 static void GeneralDecide(const kp_cluster& cl, const vector<std::map<string, string>>& labels,
                           const vector<uint32_t>& cand, const SolveBase& B, bool all, int n_nc, const KReqs* R,
                           int ci, uint32_t nodepool, const uint32_t* opts, uint32_t n_opts, int32_t multi_node,
-                          SimOut& r, const OfferTab* tab = nullptr) {
+                          SimOut& r, const OfferTab* tab = nullptr, const CandCache* cc = nullptr) {
   double candPrice = 0;
   bool priced = true, allSpot = true;
   for (uint32_t c : cand) {
+    if (cc) {
+      priced = priced && cc->priced[c];
+      candPrice += cc->price[c];
+      allSpot = allSpot && cc->spot[c];
+      continue;
+    }
     const kp_cluster_node& n = cl.nodes[c];
     double p = 0;
     if (!NodeCandidatePrice(cl.catalogs[n.catalog]->types[n.instance_type], labels[c], &p)) priced = false;
@@ -4929,21 +4956,26 @@ static void GeneralDecide(const kp_cluster& cl, const vector<std::map<string, st
     if (worst((int)opts[i]) < candPrice) kept.push_back((int)opts[i]);
   if (hasMin && !HostMinValuesOK(d, hc, *R, kept)) return;
   if (kept.empty()) return;
-  if (multi_node) {  // filterOutSameType
-    std::map<string, double> prices;
+  if (multi_node) {  // filterOutSameType: the candidates' cheapest price per type name
+    vector<std::pair<const string*, double>> prices;
     for (uint32_t c : cand) {
       const kp_cluster_node& n = cl.nodes[c];
       const HostType& it = cl.catalogs[n.catalog]->types[n.instance_type];
       double p = 0;
-      if (!NodeCandidatePrice(it, labels[c], &p)) continue;
-      auto f = prices.find(it.name);
-      if (f == prices.end() || p < f->second) prices[it.name] = p;
+      if (cc ? !cc->priced[c] : !NodeCandidatePrice(it, labels[c], &p)) continue;
+      if (cc) p = cc->price[c];
+      bool found = false;
+      for (auto& e : prices)
+        if (*e.first == it.name) {
+          e.second = std::min(e.second, p);
+          found = true;
+        }
+      if (!found) prices.push_back({&it.name, p});
     }
     double maxPrice = std::numeric_limits<double>::max();
-    for (int t : kept) {
-      auto f = prices.find(types[t].name);
-      if (f != prices.end() && f->second < maxPrice) maxPrice = f->second;
-    }
+    for (int t : kept)
+      for (auto& e : prices)
+        if (*e.first == types[t].name && e.second < maxPrice) maxPrice = e.second;
     vector<int> k2;
     for (int t : kept)
       if (worst(t) < maxPrice) k2.push_back(t);
@@ -5099,6 +5131,7 @@ struct GeneralBatch {
   vector<int32_t> regcnt;       // [G * 64] existing nodes registering each (group, ordinal)
   vector<int32_t> live0;        // [G] liveness with only the base pods queued
   OfferTab offers;              // the decisions' offering bits (the superset's dictionary)
+  CandCache cands;              // the candidates' prices
   uint32_t rmask = 0;
   int res_mode = 0, opt_stride = 100, tf_words = 0;
   bool tfeas_on = false;
@@ -5221,6 +5254,15 @@ static int32_t GeneralBatchBuild(kp_cluster_plan* plan, std::shared_ptr<GeneralB
   gb->rmask = RequestedResources(C);
   gb->ex_static = ExStatic(C, gb->rmask);
   gb->offers.Build(C.B->d, cl);
+  {
+    vector<std::map<string, string>> labels(N);
+    for (int i = 0; i < N; i++)
+      for (uint32_t j = 0; j < cl.nodes[i].node.n_labels; j++) {
+        const kp_label& l = cl.nodes[i].node.labels[j];
+        labels[i][Normalize(l.key ? l.key : "")] = l.value ? l.value : "";
+      }
+    gb->cands.Build(cl, labels);
+  }
   gb->res_mode = !C.B->res_cls ? 0 : 2;
   gb->opt_stride = 100;
   // the shared region: read-only data of every simulation + the template-options table
@@ -5496,7 +5538,7 @@ static int32_t GeneralBatchRun(kp_cluster_plan* plan, GeneralBatch& gb, const ve
         np = (uint32_t)C.B->tmpl_nodepool[nct[j]];
       }
       GeneralDecide(cl, labels, cands[i], *C.B, all, n_nc, &R, ci, np, &opts[(size_t)j * gb.opt_stride],
-                    n_nc == 1 ? nopt[j] : 0, multi_node, r, &gb.offers);
+                    n_nc == 1 ? nopt[j] : 0, multi_node, r, &gb.offers, &gb.cands);
     }
     host_ms[1] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th1).count();
   }

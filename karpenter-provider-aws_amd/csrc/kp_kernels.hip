@@ -710,13 +710,13 @@ __device__ __forceinline__ uint64_t fits_lean(const DevDict& D, const CatHdr LDS
     if (__ballot(!same) == 0) {
       nb_probe(nb, (uint32_t)__popcll(act), TW);  // the algorithm's probe + row bytes, as below
       nb_row(nb, (uint32_t)__popcll(act), TW);
-      if (lane < KP_NRES) jout[lane] = in_rr && q_lane > 0 ? j0_lane : 0;
+      if (lane < KP_NRES) jout[lane] = j0_lane;
       return X;
     }
   }
   const uint64_t GLB* rowp[4] = {nullptr, nullptr, nullptr, nullptr};
   bool zero = false;
-  int32_t j_lane = 0;
+  int32_t j_lane = j0_lane;  // (resources outside rr keep their index)
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     if (k >= nr) break;
@@ -2013,12 +2013,6 @@ __device__ __noinline__ int fast_lane(uint64_t kargs, int32_t LDS* s_dyn_arg, ui
   const uint32_t rm1 = rmask_all & (rmask_all - 1);
   const int rr1 = rm1 ? __builtin_ctz(rm1) : rr0;
   const uint32_t rr_rest = rm1 & (rm1 - 1);
-  int8_t rr_list[4] = {0, 0, 0, 0};
-  int n_rr = 0;
-  for (uint32_t m = rmask_all; m; m &= m - 1) {
-    if (n_rr < 4) rr_list[n_rr] = (int8_t)__builtin_ctz(m);
-    n_rr++;
-  }
   // the pre-check record holds the first four requested resources' headroom; more come from requests / maxalloc
   const int rk2 = kth_res(rmask_all, 2), rk3 = kth_res(rmask_all, 3);
   uint32_t rr_b4 = rr_rest;
@@ -2157,6 +2151,17 @@ if (!FL_NOTIME && tmg) {                                    \
       }
       const int64_t pr0 = rmask_all ? lane_bcast_i64(preq_lane, rr0) : 0, pr1 = rm1 ? lane_bcast_i64(preq_lane, rr1) : 0;
       const int64_t pr2 = rk2 >= 0 ? lane_bcast_i64(preq_lane, rk2) : 0, pr3 = rk3 >= 0 ? lane_bcast_i64(preq_lane, rk3) : 0;
+      // the resources this pod requests: Fits on an in-flight NodeClaim only re-tests those (its remaining types
+      // already fit its own requests on every other resource, and a zero request leaves them so), and the fifth and
+      // later ones' pre-check (requests + pod <= max allocatable) holds trivially for a zero request
+      const uint32_t pod_rm = rmask_all & (uint32_t)__ballot(lane < KP_NRES && preq_lane > 0);
+      const uint32_t rr_b4p = rr_b4 & pod_rm;
+      int8_t rrp[4] = {0, 0, 0, 0};
+      int n_rrp = 0;
+      for (uint32_t m = pod_rm; m; m &= m - 1) {
+        if (n_rrp < 4) rrp[n_rrp] = (int8_t)__builtin_ctz(m);
+        n_rrp++;
+      }
       // topology (levels the host marked fast: spread groups only): the owned groups staged in registers, as the full
       // path stages them into s_town / s_tacc (hostname rows: count + self <= maxSkew; dictionary keys: the domains
       // whose count + self - min <= maxSkew)
@@ -2316,10 +2321,10 @@ if (!FL_NOTIME && tmg) {                                    \
           ver = hv.ver;
           const int32_t ts = hv.ts;
           bool fit = hv.r0 >= pr0 && hv.r1 >= pr1 && hv.r2 >= pr2 && hv.r3 >= pr3;
-          if (rr_b4) {  // a fifth requested resource and beyond
+          if (rr_b4p) {  // a fifth requested resource and beyond (that the pod requests)
             const int64_t* rq = A->nc_requests + (size_t)nc * KP_NRES;
             const int64_t* mx = A->nc_maxalloc + (size_t)nc * KP_NRES;
-            for (uint32_t rm = rr_b4; rm; rm &= rm - 1) {
+            for (uint32_t rm = rr_b4p; rm; rm &= rm - 1) {
               const int r = __builtin_ctz(rm);
               fit = fit & (rq[r] + lane_bcast_i64(preq_lane, r) <= mx[r]);
             }
@@ -2400,9 +2405,9 @@ if (!FL_NOTIME && tmg) {                                    \
           ReqView rv;
           bool perm = true;  // a failure here is permanent (NC_NEVER) unless it is Compatible's undefined-key rule
           if (!full_add) {
-            if (n_rr <= 4 && cat < 8) {
-              X = fits_lean(D, (const CatHdr LDS*)&g_hdr[cat], X0, q_lane, j0_lane, (const int64_t LDS*)g_fitv, rr_list,
-                            n_rr, fnb, (int32_t LDS*)fl_fitj);
+            if (n_rrp <= 4 && cat < 8) {
+              X = fits_lean(D, (const CatHdr LDS*)&g_hdr[cat], X0, q_lane, j0_lane, (const int64_t LDS*)g_fitv, rrp,
+                            n_rrp, fnb, (int32_t LDS*)fl_fitj);
             } else {
               X = fl_fits_filter(cat, X0, q_lane, j0_lane, A->req_res_mask, (uint64_t)(uintptr_t)A->cats);
               bytes += fl_io[1];
@@ -2651,12 +2656,6 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a0, const Solv
   const uint32_t rm1 = rmask_all & (rmask_all - 1);
   const int rr1 = rm1 ? __builtin_ctz(rm1) : rr0;
   const uint32_t rr_rest = rm1 & (rm1 - 1);
-  int8_t rr_list[4] = {0, 0, 0, 0};  // the requested resources in order (fits_lean), when there are <= 4
-  int n_rr = 0;
-  for (uint32_t m = rmask_all; m; m &= m - 1) {
-    if (n_rr < 4) rr_list[n_rr] = (int8_t)__builtin_ctz(m);
-    n_rr++;
-  }
   const int rk2 = kth_res(rmask_all, 2), rk3 = kth_res(rmask_all, 3);  // pre-check record: resources 0..3
   uint32_t rr_b4 = rr_rest;
   for (int i = 0; i < 2 && rr_b4; i++) rr_b4 &= rr_b4 - 1;
@@ -3110,12 +3109,12 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a0, const Solv
           // a permanent failure: headroom, taints and used host ports only get worse, NEVER stays (chunk dead marks)
           if (!fit || !tol || hpx || fl == NC_NEVER) pf |= 1u << k;
           bool cand = fit && tol && !hpx && fl != hv.ver && fl != NC_NEVER;
-          if (rr_b4 && cand) {
+          if (rr_b4 && cand) {  // (a zero request holds trivially: requests <= max allocatable)
             const int64_t* rq = a.nc_requests + (size_t)nc * KP_NRES;
             const int64_t* mx = a.nc_maxalloc + (size_t)nc * KP_NRES;
             for (uint32_t rm = rr_b4; rm && cand; rm &= rm - 1) {
               const int r = __builtin_ctz(rm);
-              cand = rq[r] + s_preq[r] <= mx[r];
+              if (s_preq[r] > 0) cand = rq[r] + s_preq[r] <= mx[r];
             }
           }
           for (int j = 0; j < own_n && cand; j++)  // hostname topologies, exact (count changes with the version)
