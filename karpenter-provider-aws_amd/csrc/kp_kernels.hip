@@ -1848,8 +1848,10 @@ __device__ bool chk_move(const ChkDir& d, ChkCtl LDS* C, ChkBlk* B, int cf, int 
 // entry (at n - 1, past every sample) leaves every sampled triple non-decreasing, and a +1 at position p whose
 // successor is now smaller breaks exactly the triples holding the pair (p, p + 1): p = m - 1 or p = m for a sample
 // middle m = (n / 4) * (t + 1) (wave_pivot_increasing's predicate under that invariant).
+// hc / hid / hkey: a chunk whose block the caller holds in registers as it now is (ids and keys, lane values; the
+// fast lane's last commit chunk, its key already +1), or hc = -1.
 __device__ int chk_sort(const ChkDir& d, ChkCtl LDS* C, ChkBlk* B, int n, int mut, int p, int32_t* order,
-                        int32_t* npods, uint64_t* slow) {
+                        int32_t* npods, uint64_t* slow, int hc = -1, int hblk = -1, int hid = 0, int hkey = 0) {
   const int lane = LANE;
   if (mut == 0) return -1;
   const int nch = U(C->nch);
@@ -1860,7 +1862,12 @@ __device__ int chk_sort(const ChkDir& d, ChkCtl LDS* C, ChkBlk* B, int n, int mu
     sf = p - d.start[cf];
     const uint32_t v = d.info[cf];
     cnt = ci_cnt(v);
-    chk_load(B, ci_blk(v), cnt, id, key);
+    if (cf == hc && ci_blk(v) == hblk) {  // the block the commit just updated: no reload
+      id = lane < cnt ? hid : -1;
+      key = lane < cnt ? hkey : INT32_MAX;
+    } else {
+      chk_load(B, ci_blk(v), cnt, id, key);
+    }
     K = __builtin_amdgcn_readlane(key, sf);
     if (K > CHK_KEY_MAX) return -3;
     if (lane == 0) d.info[cf] = ci_make(ci_blk(v), cnt, __builtin_amdgcn_readlane(key, cnt - 1));  // the commit's +1
@@ -2037,6 +2044,8 @@ __device__ __noinline__ int fast_lane(uint64_t kargs, int32_t LDS* s_dyn_arg, ui
   int64_t c_q = 0, c_r0 = 0, c_r1 = 0, c_r2 = 0, c_r3 = 0;
   int32_t c_fj = 0;
   int n_buf = 0, buf_pod = 0, buf_pl = 0;  // placements not yet written (lane i: the i-th)
+  // chunked order: the block of the last commit's chunk as the commit left it (ids, keys), for the next replay
+  int h_ck = -1, h_blk = -1, h_id = 0, h_key = 0;
   // the append path's byte model as 32-bit event counts, converted on exit (the 64-bit accumulators cost 2.8 % of
   // the loop)
   NbUnits fnb{0, 0, 0};
@@ -2215,7 +2224,8 @@ if (!FL_NOTIME && tmg) {                                    \
       int low;
       if (CHK) {
         low = mut == 0 ? -1 : chk_sort(cd, (ChkCtl LDS*)&g_chk, A->chk_blk, n_nc, mut, mut_p, A->g_order, A->g_npods,
-                                       &A->stats[31]);
+                                       &A->stats[31], h_ck, h_blk, h_id, h_key);
+        h_ck = -1;  // (the replay may have moved entries)
         if (low == -4) {  // the literal pdqsort ran and its rebuild did not fit: the flat order, the full path's
           if (lane == 0) s_ctl[5] = 0;
           mut = 0;
@@ -2262,7 +2272,7 @@ if (!FL_NOTIME && tmg) {                                    \
       for (int base = start; placed == -1 && !bail;) {
         int i, ck = -1, nscan;  // position of this lane's entry; its chunk; entries this round scans
         bool valid;
-        int nc;
+        int nc, c_bid = 0, c_bkey = 0;
         if (CHK) {
           while (!lm && cc < nch) {  // the next window's live chunks (dead ones: every NodeClaim fails permanently)
             bool live = false;
@@ -2284,7 +2294,10 @@ if (!FL_NOTIME && tmg) {                                    \
           lm &= lm - 1;
           const uint32_t v = cd.info[ck];
           valid = lane < ci_cnt(v) && !(ck == ch0 && lane < cs0);
-          nc = valid ? A->chk_blk[ci_blk(v)].id[lane] : 0;
+          // the chunk's block (ids and keys) in one batch: the winner's chunk is the next replay's
+          c_bid = lane < ci_cnt(v) ? A->chk_blk[ci_blk(v)].id[lane] : -1;
+          c_bkey = lane < ci_cnt(v) ? A->chk_blk[ci_blk(v)].key[lane] : INT32_MAX;
+          nc = valid ? c_bid : 0;
           i = cd.start[ck] + lane;
           nscan = __popcll(__ballot(valid));
         } else {
@@ -2476,6 +2489,12 @@ if (!FL_NOTIME && tmg) {                                    \
             }
             placed = ncx;
             wpos = __builtin_amdgcn_readlane(i, l);
+            if (CHK) {  // the block as the commit left it, for the next pod's replay
+              h_ck = ck;
+              h_blk = ci_blk(cd.info[ck]);
+              h_id = c_bid;
+              h_key = c_bkey + (lane == l ? 1 : 0);
+            }
             if (FT_FINE) fl_last = ncx;
             if (TOPO && triv && lane == 0 && ncx < A->ncc) A->nc_fail[(size_t)sl * A->ncc + ncx] = NC_MERGED;
             if (TOPO && rec_n) {
