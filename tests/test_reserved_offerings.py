@@ -296,16 +296,24 @@ def test_device_launch_reserved_kat(ctx):
 
 
 @pytest.mark.gpu
-def test_cluster_refuses_reservations(ctx, catalog):
-    """SimulateScheduling's reservation accounting is not modelled: a consolidation cluster over a catalogue with
-    reservation offerings is KP_E_UNSUPPORTED (the shim keeps the Go path for it). A Solve takes them (ABI v9,
-    tests/test_reserved_solve.py)."""
+def test_cluster_over_reservations(ctx, catalog):
+    """A consolidation cluster over a catalogue with reservation offerings (ABI v10) takes the general path, every
+    simulation batched on the superset Solve with strict reservations; decisions equal the oracle's
+    (tests/test_reserved_consolidation.py holds the design KATs)."""
     import kpamd
     from kpamd import synth
+    from oracle import pyoracle
     cat = reserved_catalogue(catalog, 200, 0)
     cl = synth.random_cluster(cat, 0, n_nodes=10)
-    with pytest.raises(kpamd.KPError, match="reservation"):
-        kpamd.ClusterPlan(ctx, cl)
+    subs = synth.consolidation_subsets(cl, 8, seed=3, max_size=5) + [[c] for c in cl.candidates[:5]]
+    plan = kpamd.ClusterPlan(ctx, cl)
+    try:
+        got, st = plan.simulate(subs)
+    finally:
+        plan.close()
+    assert st["phase_cycles"][0] == len(subs)
+    want, _ = pyoracle.simulate_batch(cl, subs)
+    assert [(g["decision"], g["savings"]) for g in got] == [(w["decision"], w["savings"]) for w in want]
 
 
 @pytest.mark.gpu
