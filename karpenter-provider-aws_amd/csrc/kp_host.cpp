@@ -5414,11 +5414,12 @@ static int32_t GeneralBatchRun(kp_cluster_plan* plan, GeneralBatch& gb, const ve
   for (size_t b0 = 0; b0 < idx.size(); b0 += per_launch) {
     const auto th0 = std::chrono::steady_clock::now();
     const int n = (int)std::min(per_launch, idx.size() - b0);
-    if (gb.arenas_bytes < gb.stride * n) {
-      HIPCHK(gb.arenas.alloc(gb.stride * n));
-      gb.arenas_bytes = gb.stride * n;
+    if (gb.arenas_bytes < gb.stride * n) {  // sized for a whole launch at once: later batches reuse it
+      const size_t cap = gb.stride * std::max<size_t>((size_t)n, per_launch);
+      HIPCHK(gb.arenas.alloc(cap));
+      gb.arenas_bytes = cap;
     }
-    const size_t args_need = sizeof(SolveArgs) * n + 256 + sizeof(FinalizeArgs) * n;
+    const size_t args_need = (sizeof(SolveArgs) + sizeof(FinalizeArgs)) * per_launch + 256;
     if (gb.args_bytes < args_need) {
       HIPCHK(gb.args.alloc(args_need));
       gb.args_bytes = args_need;

@@ -3936,31 +3936,13 @@ __global__ __launch_bounds__(FEAS_WAVES * 64) void feasibility_kernel(FeasArgs a
 // per-type work. The cheapest compatible available price per type is the row price_sub[cls] of the precomputed
 // per-class-subset minima (a row copy, L2 -> HBM), or the min over the classes' price rows when C > KP_SUB_MAX_C.
 // The next row's header loads are issued before this row is evaluated.
-// The row's type-set rows are not loaded key by key: their pointers go to a per-wave LDS list first (scalar work), then
-// out in batches of FEASB_LB independent loads, combined in list order (one or two L2 round trips per row instead of
-// one per key / resource / class). Rows carry a mode: OR into the group's accumulator (acc), into the valued-types
-// mask (nk) or the excluded-values union (ex); the group's last row ANDs acc, or for a complement walk
-// acc | (~nk & ~ex), into the verdict. The first FEASB_FV_RES resources' Fits thresholds are staged in LDS.
 #define FEASB_WAVES 8
 #define FEASB_CP 8    // cheapest-row copy: loads in flight per lane before their stores (measured: 16 is slower)
 #define FEASB_MINW 8  // waves per SIMD the register budget must allow (measured: 0.1574 -> 0.1245 ms on 50k rows)
-#define FEASB_RL 32   // row-list capacity per wave
-#define FEASB_LB 8    // loads per batch
-#define FEASB_FV_RES 3
-#define FEASB_FV_CAP 1024
-#define FM_ACC 1u
-#define FM_NK 2u
-#define FM_EX 4u
-#define FM_END 8u
-#define FM_COMPL 16u
 __global__ __launch_bounds__(FEASB_WAVES * 64, FEASB_MINW) void feasibility_bits_kernel(FeasArgs a) {
   __shared__ DevDict D;
   __shared__ int64_t s_vint[KP_MAX_BOUND_KEYS * 64];
   __shared__ OfferClass s_cls[KP_MAX_CLASSES];
-  __shared__ RowPtr s_fr[FEASB_WAVES][FEASB_RL];
-  __shared__ uint32_t s_fm[FEASB_WAVES][FEASB_RL];
-  __shared__ int64_t s_fv[FEASB_FV_RES][FEASB_FV_CAP];
-  __shared__ int32_t s_fvslot[KP_NRES];
   block_copy(D, a.dict);
   const int tid = threadIdx.x;
   constexpr int NT = FEASB_WAVES * 64;
@@ -3979,19 +3961,6 @@ __global__ __launch_bounds__(FEASB_WAVES * 64, FEASB_MINW) void feasibility_bits
   const int T = D.T, TW = D.TW, C = D.C;
   for (int i = tid; i < D.KB * 64; i += NT) s_vint[i] = a.vint[i];
   for (int i = tid; i < C; i += NT) s_cls[i] = Cd.cls[i];
-  if (tid == 0) {  // Fits thresholds staged in LDS: the first FEASB_FV_RES resources that fit
-    int slot = 0;
-    for (int r = 0; r < KP_NRES; r++) {
-      const bool st = slot < FEASB_FV_RES && fit_n[r] <= FEASB_FV_CAP;
-      s_fvslot[r] = st ? slot++ : -1;
-    }
-  }
-  __syncthreads();
-  for (int r = 0; r < KP_NRES; r++) {
-    const int sl = s_fvslot[r];
-    if (sl < 0) continue;
-    for (int i = tid; i < fit_n[r]; i += NT) s_fv[sl][i] = fit_vals[(size_t)r * T + i];
-  }
   __syncthreads();
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = LANE;
   const bool lw = lane < TW;  // this lane holds a type word
@@ -4088,50 +4057,10 @@ __global__ __launch_bounds__(FEASB_WAVES * 64, FEASB_MINW) void feasibility_bits
         }
       pass = keep;
     }
-    int nr = 0;            // rows in the list
-    bool zero = false;     // some step keeps no type
-    uint64_t acc = 0, nk = 0, ex = 0;
-    auto flush = [&]() {
-      wave_sync();
-      for (int g = 0; g < nr; g += FEASB_LB) {
-        uint64_t w[FEASB_LB];
-#pragma unroll
-        for (int i = 0; i < FEASB_LB; i++) {
-          const uint64_t pp = g + i < nr ? U64((uint64_t)(uintptr_t)s_fr[wave][g + i]) : 0;
-          const GLB uint64_t* p = (const GLB uint64_t*)(uintptr_t)pp;
-          w[i] = (pp && lw) ? p[lane] : 0;
-        }
-#pragma unroll
-        for (int i = 0; i < FEASB_LB; i++) {
-          if (g + i >= nr) break;
-          const uint32_t m = (uint32_t)U((int)s_fm[wave][g + i]);
-          if (m & FM_ACC) acc |= w[i];
-          if (m & FM_NK) nk |= w[i];
-          if (m & FM_EX) ex |= w[i];
-          if (m & FM_END) {
-            pass &= (m & FM_COMPL) ? (acc | (~nk & ~ex)) : acc;
-            acc = nk = ex = 0;
-          }
-        }
-      }
-      nr = 0;
-      wave_sync();
-    };
-    auto push = [&](const GLB uint64_t* p, uint32_t m) {
-      if (nr == FEASB_RL) flush();
-      if (lane == 0) {
-        s_fr[wave][nr] = (RowPtr)p;
-        s_fm[wave][nr] = m;
-      }
-      nr++;
-    };
-    auto end_group = [&](uint32_t m) {  // (the group's last row is still in the list: flush only runs inside push)
-      if (lane == 0) s_fm[wave][nr - 1] |= m;
-    };
-    // Intersects over the shared keys, one OR-group per key
+    // Intersects over the shared keys, one key's type set at a time
     for (uint64_t km = rv.present & D.catalog_keys; km; km &= km - 1) {
       const int k = __builtin_ctzll(km);
-      const bool ng = (negQ >> k) & 1;
+      uint64_t acc = lw ? NOKEY[(size_t)k * TW + lane] | (((negQ >> k) & 1) ? DNE[(size_t)k * TW + lane] : 0) : 0;
       // the key's value words: allowed (A) and excluded (E) value bits
       int nA = 0, nE = 0;
       uint64_t wm = 1ull << k;
@@ -4142,18 +4071,19 @@ __global__ __launch_bounds__(FEASB_WAVES * 64, FEASB_MINW) void feasibility_bits
         nA += __builtin_popcountll(aw & D.validbits[w]);
         nE += __builtin_popcountll(~aw & D.validbits[w]);
       }
-      // complement walk (single-valued key, fewer excluded values): valued types (not NOKEY, not DNE) outside the
-      // excluded values' union
-      const bool cw = ((D.single_valued >> k) & 1) && nE < nA;
-      push((const GLB uint64_t*)NOKEY + (size_t)k * TW, cw ? FM_ACC | FM_NK : FM_ACC);
-      if (ng || cw) push((const GLB uint64_t*)DNE + (size_t)k * TW, (ng ? FM_ACC : 0u) | (cw ? FM_NK : 0u));
+      const bool compl_walk = ((D.single_valued >> k) & 1) && nE < nA;
+      uint64_t u = 0;
       for (uint64_t m = wm; m; m &= m - 1) {
         const int w = __builtin_ctzll(m);
         const uint64_t aw = lane_bcast(allowed, w);
-        for (uint64_t bits = (cw ? ~aw : aw) & D.validbits[w]; bits; bits &= bits - 1)
-          push((const GLB uint64_t*)TM + (size_t)(w * 64 + __builtin_ctzll(bits)) * TW, cw ? FM_EX : FM_ACC);
+        for (uint64_t bits = (compl_walk ? ~aw : aw) & D.validbits[w]; bits; bits &= bits - 1)
+          u |= lw ? TM[(size_t)(w * 64 + __builtin_ctzll(bits)) * TW + lane] : 0;
       }
-      end_group(cw ? FM_END | FM_COMPL : FM_END);
+      if (compl_walk) {  // valued types (single-valued key: not NOKEY, not DNE) outside the excluded values' union
+        const uint64_t nk = lw ? NOKEY[(size_t)k * TW + lane] | DNE[(size_t)k * TW + lane] : ~0ull;
+        u = ~nk & ~u;
+      }
+      pass &= acc | u;
     }
     // Fits on the requested resources: the threshold row of the first allocatable >= the request
     for (uint32_t rm = rmask; rm; rm &= rm - 1) {
@@ -4161,18 +4091,13 @@ __global__ __launch_bounds__(FEASB_WAVES * 64, FEASB_MINW) void feasibility_bits
       const int64_t need = lane_bcast_i64(cur.rq, r);
       uint64_t nb = 0;
       const int n = fit_n[r];
-      const int sl = s_fvslot[r];
-      const int j = sl >= 0 ? wave_lower_bound((const int64_t LDS*)s_fv[sl], n, need, &nb)
-                            : wave_lower_bound(fit_vals + (size_t)r * T, n, need, &nb);
-      if (j >= n) zero = true;
-      else push((const GLB uint64_t*)fit_mask + ((size_t)r * T + j) * TW, FM_ACC | FM_END);
+      const int j = wave_lower_bound(fit_vals + (size_t)r * T, n, need, &nb);
+      pass &= (j < n && lw) ? fit_mask[((size_t)r * T + j) * TW + lane] : 0;
     }
     // an available offering of a compatible class
-    if (!cls) zero = true;
-    for (uint64_t m = cls; m; m &= m - 1) push((const GLB uint64_t*)offer + (size_t)__builtin_ctzll(m) * TW, FM_ACC);
-    if (cls) end_group(FM_END);
-    flush();
-    if (zero) pass = 0;
+    uint64_t av = 0;
+    for (uint64_t m = cls; m; m &= m - 1) av |= lw ? offer[(size_t)__builtin_ctzll(m) * TW + lane] : 0;
+    pass &= av;
     if (lw) ((GLB uint64_t*)a.out_mask)[(size_t)q * TW + lane] = pass;
     cheapest_row();
   }
