@@ -416,6 +416,9 @@ typedef struct kp_options {
 } kp_options;
 
 int32_t kp_ctx_create(const kp_options* opts, kp_ctx** out);
+/* Drops the caller's reference. Catalogues, plans and communicators created on the context hold their own, so they
+ * may be destroyed before or after it (a garbage collector finalizes in any order); the context's stream, events and
+ * spare arena are freed with the last reference. */
 void kp_ctx_destroy(kp_ctx* ctx);
 const char* kp_last_error(void);
 int32_t kp_abi_version(void);

@@ -7,7 +7,7 @@
 
 #define KP_SOLVE_STATS 48
 // why the fast lane handed a popped pod to the full path (stats[32 + FB_*])
-enum { FB_INELIGIBLE = 0, FB_SPILLED = 1, FB_SHIFT = 2, FB_SCAN = 3, FB_MERGE = 4, FB_MINVALUES = 5, FB_NONE = 6 };
+enum { FB_INELIGIBLE = 0, FB_SPILLED = 1, FB_SHIFT = 2, FB_SCAN = 3, FB_MERGE = 4, FB_MINVALUES = 5, FB_NONE = 6, FB_MEMO = 7 };
 
 // The in-flight pre-check's view of one NodeClaim in one 64-byte line (one gather per candidate position instead of
 // one per field): headroom = max allocatable over its types at creation minus its requests, for the first four
@@ -138,6 +138,11 @@ struct SolveArgs {
   // topology groups do not use them (their outcome depends on the counts).
   int32_t* cur_nc;                   // [SL][2] in-flight NodeClaims (positions in the sorted order)
   int32_t* cur_ex;                   // [SL][2] existing nodes (upstream order)
+  // [SL] unschedulable memo: the NodeClaim count when a pod of the shape-level last failed every placement (-1:
+  // never). Without topology or reservations and with no positive custom key at the level, every failure is
+  // permanent (existing nodes and NodeClaims only fill up and narrow, limits only shrink as NodeClaims are created),
+  // so a later pod of the level fails again exactly while no NodeClaim was created since
+  int32_t* sl_fail;
   int32_t n_tk;                      // topology keys (dictionary keys some group spreads over)
   const int32_t* tk_keys;            // [TK]
   uint8_t* nc_tcode;                 // [TK][hnc_stride] pinned value ordinal per NodeClaim (store_tcodes)

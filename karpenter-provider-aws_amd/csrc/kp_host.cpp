@@ -219,10 +219,43 @@ struct kp_ctx {
   // per-Solve device arena handed back by kp_solve_plan_destroy and reused by the next kp_solve_prepare
   void* spare = nullptr;
   size_t spare_bytes = 0;
+  // kp_ctx_destroy's reference plus one per live dependent (catalogue, plan, communicator): the context is freed
+  // when the last goes, so a dependent may be destroyed after the context (any order, e.g. a garbage collector's)
+  std::atomic<int> refs{1};
+};
+static void CtxFree(kp_ctx* c) {
+  (void)hipSetDevice(c->device);
+  c->bases.clear();
+  if (c->spare) (void)hipFree(c->spare);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->ev2) (void)hipEventDestroy(c->ev2);
+  if (c->ev3) (void)hipEventDestroy(c->ev3);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+inline void CtxUnref(kp_ctx* c) {
+  if (c && c->refs.fetch_sub(1) == 1) CtxFree(c);
+}
+// A dependent's context pointer holding a reference (assignment takes one, destruction drops it).
+struct CtxRef {
+  kp_ctx* p = nullptr;
+  CtxRef() = default;
+  CtxRef(const CtxRef&) = delete;
+  CtxRef& operator=(const CtxRef&) = delete;
+  CtxRef& operator=(kp_ctx* c) {
+    if (c) c->refs.fetch_add(1);
+    CtxUnref(p);
+    p = c;
+    return *this;
+  }
+  ~CtxRef() { CtxUnref(p); }
+  kp_ctx* operator->() const { return p; }
+  operator kp_ctx*() const { return p; }
 };
 
 struct kp_catalog {
-  kp_ctx* ctx;
+  CtxRef ctx;
   uint64_t seqnum;
   uint64_t uid;  // process-unique identity (a new upload never reuses one, unlike its address)
   vector<HostType> types;
@@ -901,18 +934,8 @@ int32_t kp_ctx_create(const kp_options* opts, kp_ctx** out) {
   *out = c;
   return KP_OK;
 }
-void kp_ctx_destroy(kp_ctx* c) {
-  if (!c) return;
-  (void)hipSetDevice(c->device);
-  c->bases.clear();
-  if (c->spare) (void)hipFree(c->spare);
-  if (c->ev0) (void)hipEventDestroy(c->ev0);
-  if (c->ev1) (void)hipEventDestroy(c->ev1);
-  if (c->ev2) (void)hipEventDestroy(c->ev2);
-  if (c->ev3) (void)hipEventDestroy(c->ev3);
-  if (c->stream) (void)hipStreamDestroy(c->stream);
-  delete c;
-}
+void kp_ctx_destroy(kp_ctx* c) { CtxUnref(c); }
+
 
 int32_t kp_catalog_upload(kp_ctx* ctx, const kp_catalog_desc* desc, uint64_t seqnum, kp_catalog** out) {
   if (!desc || !out) return fail(KP_E_INVAL, "null argument");  // ctx NULL: host-only (kp_solve_validate)
@@ -964,6 +987,7 @@ void kp_catalog_destroy(kp_catalog* c) {
     DropBasesOf(c->ctx, c);
   }
   *c->alive = false;
+  if (lock.owns_lock()) lock.unlock();  // (the delete may drop the context's last reference)
   delete c;
 }
 
@@ -2798,7 +2822,7 @@ struct SolveOffs {
   size_t pristine = 0, ncr = 0, ncX = 0, ncrq = 0, nct = 0, npods = 0, order = 0, chkblk = 0, maxalloc = 0, fitj = 0,
          nchead = 0, nccat = 0, nchp = 0, place = 0, events = 0, stats = 0, ver0 = 0, exver = 0, tver = 0, curnc = 0,
          curex = 0, held = 0, ver_end = 0, fail0 = 0, ncfail = 0, exfail = 0, tfail = 0, chkdead = 0, fail_end = 0,
-         opts = 0, nrem = 0, nopt = 0, hcnc = 0, nctc = 0, txl = 0, txlv = 0, arena_end = 0;
+         opts = 0, nrem = 0, nopt = 0, hcnc = 0, nctc = 0, txl = 0, txlv = 0, slfail = 0, arena_end = 0;
   size_t n_hcnc = 0;
   int ncc = 0, chk_dead_rows = 0, sort_cap = 0, opt_stride = 0;
   bool chk_on = false;
@@ -2935,6 +2959,7 @@ void ReserveArenaDev(Blob& blob, const Compiled& C, int Pc, int opt_stride, int 
   o.exfail = blob.reserve_dev(sizeof(int32_t) * SLn * std::max(E, 1));
   o.tfail = blob.reserve_dev(sizeof(int32_t) * SLn * std::max(NT, 1));
   o.txlv = blob.reserve_dev(sizeof(int32_t) * std::max(NT, 1));  // -1: not computed
+  o.slfail = blob.reserve_dev(sizeof(int32_t) * SLn);  // -1: no failure yet
   o.chk_dead_rows = o.chk_on ? (int)std::min<size_t>(SLn, ((size_t)64 << 20) / (4 * CHK_MAXC)) : 0;
   o.chkdead = blob.reserve_dev(std::max<size_t>(sizeof(int32_t) * o.chk_dead_rows * CHK_MAXC, 8));
   o.fail_end = blob.total();
@@ -3010,6 +3035,7 @@ void BindSolve(SolveArgs& a, const Compiled& C, const SolveOffs& o, uint8_t* sh,
   a.tmpl_fail = (int32_t*)(ar + o.tfail);
   a.tmpl_xlim = (uint64_t*)(ar + o.txl);
   a.tmpl_xlim_ver = (int32_t*)(ar + o.txlv);
+  a.sl_fail = (int32_t*)(ar + o.slfail);
   a.cur_nc = (int32_t*)(ar + o.curnc);
   a.cur_ex = (int32_t*)(ar + o.curex);
   a.nc_maxalloc = (int64_t*)(ar + o.maxalloc);
@@ -3112,7 +3138,7 @@ extern "C" {
 // A communicator of n_ranks kp_ctx (one per GPU): RCCL (kp_comm_init / kp_comm_init_all), or a caller-supplied host
 // all-gather (kp_comm_init_host). Its settings are read once here, so that every rank takes the same decisions.
 struct kp_comm {
-  kp_ctx* ctx = nullptr;
+  CtxRef ctx;
   ncclComm_t comm = nullptr;        // RCCL transport (null: host transport)
   kp_allgather_fn host_fn = nullptr;
   void* host_user = nullptr;
@@ -3174,7 +3200,7 @@ void CommReadSettings(kp_comm* c) {
 }  // namespace
 
 struct kp_solve_plan {
-  kp_ctx* ctx = nullptr;
+  CtxRef ctx;
   std::unique_ptr<Compiled> cp;
   DevBuf buf;  // per-Solve arena (the catalogue / template part lives in cp->B->dev, shared through the ctx cache)
   SolveArgs a;
@@ -3417,16 +3443,18 @@ int32_t kp_solve_refresh(kp_solve_plan* plan) {
 void kp_solve_plan_destroy(kp_solve_plan* p) {
   if (!p) return;
   kp_ctx* ctx = p->ctx;
-  std::lock_guard<std::recursive_mutex> lock(ctx->mu);
-  (void)hipSetDevice(ctx->device);
-  if (p->buf.p && p->buf.n >= ctx->spare_bytes) {  // keep the larger arena for the next prepare
-    if (ctx->spare) (void)hipFree(ctx->spare);
-    ctx->spare = p->buf.p;
-    ctx->spare_bytes = p->buf.n;
-    p->buf.p = nullptr;
-    p->buf.n = 0;
+  {
+    std::lock_guard<std::recursive_mutex> lock(ctx->mu);
+    (void)hipSetDevice(ctx->device);
+    if (p->buf.p && p->buf.n >= ctx->spare_bytes) {  // keep the larger arena for the next prepare
+      if (ctx->spare) (void)hipFree(ctx->spare);
+      ctx->spare = p->buf.p;
+      ctx->spare_bytes = p->buf.n;
+      p->buf.p = nullptr;
+      p->buf.n = 0;
+    }
   }
-  delete p;
+  delete p;  // (after the lock: it may drop the context's last reference)
 }
 
 // One Solve over resident inputs: restore mutable state, solve_kernel, finalize_kernel, copy results.
@@ -3722,7 +3750,7 @@ static int32_t RefreshOfferings(kp_ctx* ctx, const kp_catalog* cat, Compiled& cp
 }
 
 struct kp_filter_plan {
-  kp_ctx* ctx = nullptr;
+  CtxRef ctx;
   DevBuf buf;
   FeasArgs fa;
   uint32_t n_queries = 0;
@@ -3889,7 +3917,7 @@ static void FillReservationTables(const Dict& d, const vector<HostType>& types, 
 }
 
 struct kp_launch_plan {
-  kp_ctx* ctx = nullptr;
+  CtxRef ctx;
   DevBuf buf;
   LaunchArgs la;
   uint32_t n = 0, max_types = 0, ovr_stride = 0;
@@ -4303,7 +4331,7 @@ struct OwnedCluster {
 
 struct GeneralBatch;
 struct kp_cluster_plan {
-  kp_ctx* ctx = nullptr;
+  CtxRef ctx;
   std::unique_ptr<OwnedCluster> general;  // set: simulations run as whole Solves (kp_solve on this device)
   double general_ms = 0;                  // device time of the last general batch (solve + finalize kernels)
   std::shared_ptr<GeneralBatch> gb;       // the general path's superset Solve (batched simulations), once built

@@ -43,6 +43,11 @@
 // on the vector-memory counter too and take the long path); global rows get global_load.
 #define LDS __attribute__((address_space(3)))
 #define GLB __attribute__((address_space(1)))
+// raw buffer descriptor word 3 for gfx9-family parts (gfx950): 32-bit data format, no swizzle; with stride 0 the
+// record count is in bytes and an access whose VGPR + immediate offset is at or past it returns 0 / is dropped
+// (callers keep the SGPR offset 0: the range check is only relied on for the VGPR + immediate part)
+#define KP_BUF_DWORD3 0x00020000
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 #define FITV_RES 4      // requested resources whose Fits thresholds are staged in LDS
 #define FITV_CAP 1024   // distinct allocatable values per staged resource
 
@@ -136,7 +141,8 @@ __device__ __forceinline__ uint64_t bounds_mask(const DevDict& D, uint64_t bk, u
 
 // bounds_mask with the bound slots held by the lanes (lane k: key k's gt / lt) and the parsed integers of the staged
 // words in LDS: no generic (FLAT) loads, whose waits would also cover every outstanding global load and store.
-__device__ __forceinline__ uint64_t bounds_mask_lanes(const DevDict& D, uint64_t bk, uint64_t hgt, uint64_t hlt,
+template <class DD>  // DevDict in LDS, or in the constant address space (scalar loads)
+__device__ __forceinline__ uint64_t bounds_mask_lanes(const DD& D, uint64_t bk, uint64_t hgt, uint64_t hlt,
                                                       int64_t gt_lane, int64_t lt_lane, const int64_t LDS* vl, int nl,
                                                       const GLB int64_t* vg) {
   const int lane = LANE;
@@ -202,7 +208,8 @@ __device__ __forceinline__ uint64_t negop_mask(uint64_t present, uint64_t compl_
 }
 
 // keys with at least one value bit: word k is key k's first word, so one ballot + the few overflow keys
-__device__ __forceinline__ uint64_t nz_keys(const DevDict& D, uint64_t v) {
+template <class DD>
+__device__ __forceinline__ uint64_t nz_keys(const DD& D, uint64_t v) {
   const uint64_t bal = __ballot(v != 0 && LANE < D.W);
   uint64_t nz = bal & D.firstmask;
   const uint64_t ov = bal & ~D.firstmask;
@@ -338,8 +345,8 @@ __device__ __forceinline__ bool bit_of(uint64_t allowed_lane_word, int bit) {
 // Offering classes compatible with requirement set rv (Offerings.Compatible): a reservation key the class does not
 // carry is DoesNotExist, compatible when rv leaves the key out or admits its absence.
 // RES = false (Solve, consolidation: their catalogues hold no reservation classes) skips the reservation bits.
-template <bool RES = false, class ClsP>
-__device__ uint64_t allowed_classes(const DevDict& D, ClsP cls_tab, const ReqView& rv, uint64_t allowed, uint64_t negR) {
+template <bool RES = false, class ClsP, class DD>
+__device__ uint64_t allowed_classes(const DD& D, ClsP cls_tab, const ReqView& rv, uint64_t allowed, uint64_t negR) {
   if (!RES && D.res_any) return allowed_classes<true>(D, cls_tab, rv, allowed, negR);  // Solve over reservations
   const bool res_ok = !(rv.present & D.resid_key_bit) || (negR & D.resid_key_bit);
   const bool rt_ok = !(rv.present & D.restype_key_bit) || (negR & D.restype_key_bit);
@@ -689,7 +696,7 @@ __device__ __forceinline__ void nb_lb(NbUnits& nb, uint64_t b) { nb.lb8 += (uint
 // rows as one batch of independent loads, ANDed into X. Same result and threshold indices as fits_filter.
 template <class NB>
 __device__ __forceinline__ uint64_t fits_lean(const DevDict& D, const CatHdr LDS* H, uint64_t X, int64_t q_lane,
-                                              int32_t j0_lane, const int64_t LDS* fitv_lds, const int8_t* rr, int nr,
+                                              int32_t j0_lane, const int64_t LDS* fitv_lds, uint32_t rr, int nr,
                                               NB& nb, int32_t LDS* jout) {
   const int lane = LANE;
   const int TW = D.TW;
@@ -700,7 +707,7 @@ __device__ __forceinline__ uint64_t fits_lean(const DevDict& D, const CatHdr LDS
     bool in_rr = false;
 #pragma unroll
     for (int k = 0; k < 4; k++)
-      if (k < nr && rr[k] == lane) in_rr = true;
+      if (k < nr && (int)((rr >> (8 * k)) & 0xff) == lane) in_rr = true;
     if (in_rr && q_lane > 0) {
       const int n = H->fit_n[lane];
       const int slot = H->fit_slot[lane];
@@ -720,7 +727,7 @@ __device__ __forceinline__ uint64_t fits_lean(const DevDict& D, const CatHdr LDS
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     if (k >= nr) break;
-    const int r = rr[k];
+    const int r = (rr >> (8 * k)) & 0xff;
     const int64_t q = lane_bcast_i64(q_lane, r);
     if (q <= 0) continue;
     const int j0 = __builtin_amdgcn_readlane(j0_lane, r);
@@ -2025,17 +2032,24 @@ __device__ __noinline__ int fast_lane(uint64_t kargs, int32_t LDS* s_dyn_arg, ui
   uint32_t rr_b4 = rr_rest;
   for (int i = 0; i < 2 && rr_b4; i++) rr_b4 &= rr_b4 - 1;
   const bool four = rk2 >= 0;
+  uint32_t rrp_all = 0;  // the requested resources (first four as bytes), for pods requesting all of them
+  int n_rrp_all = 0;
+  for (uint32_t m = rmask_all; m; m &= m - 1) {
+    if (n_rrp_all < 4) rrp_all |= (uint32_t)__builtin_ctz(m) << (8 * n_rrp_all);
+    n_rrp_all++;
+  }
   const uint64_t pop_cap = (uint64_t)A->n_pods * 64 + 65536;
   // control state in registers for the loop; written back on exit
   int q_head = U(s_ctl[0]), q_len = U(s_ctl[1]), n_ev = U(s_ctl[4]), mut = U(s_ctl[10]), mut_p = U(s_ctl[11]);
   int stk_n = U(s_ctl[12]), stk_t = U(s_ctl[13]), stk_lost = U(s_ctl[20]);  // in-flight mutation stack
-  const int n_nc_all = U(s_ctl[2]), epoch = U(s_ctl[3]);
+  const int n_nc_all = U(s_ctl[2]);
+  int epoch = U(s_ctl[3]);  // Queue's lastLen generation (a relaxed memo failure starts a new one)
   const bool in_lds = U(s_ctl[5]) == 1;  // order mode: 1 LDS, 2 chunked, 0 flat global
   int qw_head = U(S->qw_head), qw_n = U(S->qw_n), qw_next = U(S->qw_next);
   int qw_pod = S->qw_pod[lane], qw_shape = S->qw_shape[lane], qw_sl = S->qw_sl[lane], qw_lastlen = S->qw_lastlen[lane],
       qw_epoch = S->qw_epoch[lane];
   uint64_t bytes = 0, attempts = 0, scanned = 0, starts = 0, fcyc[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  int pops = 0, handoff = -1, fb = -1, fl_last = -1;
+  int pops = 0, memo_pops = 0, handoff = -1, fb = -1, fl_last = -1;
   // the NodeClaim this call's last append commit wrote, as it wrote it (the next pod usually starts there: reading
   // its lines back right after the stores waits for them to drain): remaining types, requests, threshold indices
   // (lane values), and its pre-check record. Only the fast lane writes NodeClaims during one call.
@@ -2078,7 +2092,7 @@ if (!FL_NOTIME && tmg) {                                    \
       const KARG SolveArgs* A = (const KARG SolveArgs*)(((uint64_t)khi_i << 32) | klo_i);
       const int len = q_len;
       const int head = q_head;
-      if (len <= 0 || pops_in + pops > pop_cap) break;
+      if (len <= 0 || pops_in + pops + memo_pops > pop_cap) break;
       // Queue.Pop from the prefetched window: entries [qw_head, qw_head + qw_n) of the ring were in the queue when
       // the window was read, and nothing rewrites a queued entry (pushes go to the tail) or its pod's level and
       // lastLen stamps while it waits, so lane i's copy of entry qw_head + i stays exact.
@@ -2150,6 +2164,9 @@ if (!FL_NOTIME && tmg) {                                    \
       FTF(7);
       q_head = head + 1 == A->n_pods ? 0 : head + 1;
       q_len = len - 1;
+      // the unschedulable memo (SolveArgs::sl_fail; chunked orders, where failing pods are many): the pod fails
+      // every placement, so after the sort replay below the lane does the full path's failure bookkeeping itself
+      const bool memo = CHK && !TOPO && A->sl_fail[sl] == n_nc_all;
       bool eligible = own == 0;
       if (FL_HAS_EX) eligible = eligible && min(ce0, mstack_query_wave((LdsI32)s_stk[1], U(s_ctl[14]), U(s_ctl[21]), ce1)) >= A->n_existing;
       FT(0);
@@ -2160,16 +2177,22 @@ if (!FL_NOTIME && tmg) {                                    \
       }
       const int64_t pr0 = rmask_all ? lane_bcast_i64(preq_lane, rr0) : 0, pr1 = rm1 ? lane_bcast_i64(preq_lane, rr1) : 0;
       const int64_t pr2 = rk2 >= 0 ? lane_bcast_i64(preq_lane, rk2) : 0, pr3 = rk3 >= 0 ? lane_bcast_i64(preq_lane, rk3) : 0;
-      // the resources this pod requests: Fits on an in-flight NodeClaim only re-tests those (its remaining types
-      // already fit its own requests on every other resource, and a zero request leaves them so), and the fifth and
-      // later ones' pre-check (requests + pod <= max allocatable) holds trivially for a zero request
-      const uint32_t pod_rm = rmask_all & (uint32_t)__ballot(lane < KP_NRES && preq_lane > 0);
-      const uint32_t rr_b4p = rr_b4 & pod_rm;
-      int8_t rrp[4] = {0, 0, 0, 0};
-      int n_rrp = 0;
-      for (uint32_t m = pod_rm; m; m &= m - 1) {
-        if (n_rrp < 4) rrp[n_rrp] = (int8_t)__builtin_ctz(m);
-        n_rrp++;
+      // the resources this pod requests (chunked orders: many NodeClaims, pools whose pods request few of the
+      // resources): Fits on an in-flight NodeClaim only re-tests those (its remaining types already fit its own
+      // requests on every other resource, and a zero request leaves them so), and the fifth and later ones'
+      // pre-check (requests + pod <= max allocatable) holds trivially for a zero request. Elsewhere the
+      // loop-invariant list (the per-pod mask cost 6 % of config 2, measured)
+      uint32_t rr_b4p = rr_b4, rrp = rrp_all;  // rrp: the first four as bytes (registers: no indexed array)
+      int n_rrp = n_rrp_all;
+      if (CHK) {
+        const uint32_t pod_rm = rmask_all & (uint32_t)__ballot(lane < KP_NRES && preq_lane > 0);
+        if (pod_rm != rmask_all) {
+          rr_b4p = rr_b4 & pod_rm, rrp = 0, n_rrp = 0;
+          for (uint32_t m = pod_rm; m; m &= m - 1) {
+            if (n_rrp < 4) rrp |= (uint32_t)__builtin_ctz(m) << (8 * n_rrp);
+            n_rrp++;
+          }
+        }
       }
       // topology (levels the host marked fast: spread groups only): the owned groups staged in registers, as the full
       // path stages them into s_town / s_tacc (hostname rows: count + self <= maxSkew; dictionary keys: the domains
@@ -2251,6 +2274,29 @@ if (!FL_NOTIME && tmg) {                                    \
       if (low >= 0) mstack_push_reg((int32_t LDS*)s_stk[0], stk_n, stk_lost, ++stk_t, low);
       wave_sync();
       FT(2);
+      if (memo) {  // the full path's failure: cursors at the end, Preferences.Relax, Queue.Push
+        a_cur_prev_pos = n_nc;
+        a_cur_prev_stamp = stk_t;
+        const int lvl = sl - A->shape_level_base[shape];
+        const bool relaxed = lvl + 1 < A->shape_nlevels[shape];
+        int tail = q_head + q_len;
+        if (tail >= A->n_pods) tail -= A->n_pods;
+        q_len += 1;
+        if (lane == 0) {
+          A->cur_nc[2 * sl] = n_nc;
+          A->cur_nc[2 * sl + 1] = stk_t;
+          A->placement[pod] = -1;
+          if (relaxed) A->pod_level[pod] = lvl + 1;
+          A->queue[tail] = pod;
+          if (!relaxed) {
+            A->lastlen[pod] = q_len;
+            A->lastlen_epoch[pod] = epoch;
+          }
+        }
+        if (relaxed) epoch += 1;  // lastLen = map{}
+        memo_pops++;
+        continue;
+      }
       // addToInflightNode: pre-checks 64 positions at a time, then the append-path attempts in order. A long scan
       // is the full path's (512-lane pre-pass).
       int placed = -1, wpos = -1, why = FB_NONE, ipos = INT32_MAX;  // ipos: first count-independent pass (topology)
@@ -2584,6 +2630,7 @@ if (!FL_NOTIME && tmg) {                                    \
   if (lane == 0) {
     s_ctl[0] = q_head;
     s_ctl[1] = q_len;
+    s_ctl[3] = epoch;
     s_ctl[4] = n_ev;
     s_ctl[10] = mut;
     s_ctl[11] = mut_p;
@@ -2606,6 +2653,7 @@ if (!FL_NOTIME && tmg) {                                    \
     S->fpods += pops;
     for (int i = 0; i < 14; i++) S->fcyc[i] += fcyc[i];
     if (fb >= 0) S->fbail[fb] += 1;
+    S->fbail[FB_MEMO] += memo_pops;  // (not a hand-off: the pods the lane failed by the memo)
   }
   S->qw_pod[lane] = qw_pod;
   S->qw_shape[lane] = qw_shape;
@@ -2613,7 +2661,7 @@ if (!FL_NOTIME && tmg) {                                    \
   S->qw_lastlen[lane] = qw_lastlen;
   S->qw_epoch[lane] = qw_epoch;
   wave_sync();
-  return pops;
+  return pops + memo_pops;
 }
 
 // TOPO: the batch has topology spread groups (else that code compiles out). BATCH: one Solve per workgroup, each with
@@ -2807,6 +2855,8 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a0, const Solv
         s_ctl[24] = INT32_MAX;  // first count-independent pass (existing / in-flight), topology shape-levels
         s_ctl[25] = INT32_MAX;
         s_ctl[27] = 0;  // addToNewNodeClaim met a ReservedOfferingError
+        // the unschedulable memo (SolveArgs::sl_fail): no NodeClaim created since a pod of this level failed everything
+        s_ctl[31] = !TOPO && !a.res_mode && a.sl_fail[sl] == s_ctl[2];
         if (TOPO) {  // the shape-level's owned groups (count, base) and spread keys, staged with the cursors
           const int on = a.sl_own_n[sl];
           s_ctl[28] = on;
@@ -2823,6 +2873,9 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a0, const Solv
     const uint64_t tolmask = a.shape_tolerates[shape];
     const uint64_t hpc = a.hp_any ? a.shape_hp_conf[shape] : 0, hpa = a.hp_any ? a.shape_hp_add[shape] : 0;
     int placed = -1;  // >= 0 NodeClaim id; <= -2 existing node; -1 not placed
+    // a memo hit fails the pod without the scans: the existing and in-flight cursors move to the end as a failed scan
+    // leaves them, and the sort replay still runs (the order every later pod sees is the reference's)
+    const bool memo_fail = s_ctl[31] != 0;
     // ---- topology: stage the owned groups (one wave each) -----------------------------------------
     const int own_n = TOPO ? s_ctl[28] : 0;
     const int own_base = TOPO ? s_ctl[29] : 0;
@@ -2873,7 +2926,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a0, const Solv
     const uint64_t exd0 = EX_DIAG ? __builtin_amdgcn_s_memtime() : 0;
     if (EX_DIAG && tid == 0) g_sdiag[0] += exd0 - exdS;  // topology staging
     if (EX_DIAG && tid == 0 && s_ctl[17] < a.n_existing) g_sdiag[3] += 1;
-    for (int base = s_ctl[17]; base < a.n_existing && placed == -1; base += 4 * NT) {
+    for (int base = s_ctl[17]; base < a.n_existing && placed == -1 && !memo_fail; base += 4 * NT) {
       uint32_t flags = 0, iflags = 0;
       const uint64_t exd1 = EX_DIAG ? __builtin_amdgcn_s_memtime() : 0;
 #pragma unroll
@@ -3044,7 +3097,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a0, const Solv
         return cmode == 2 ? cd.start[e >> 6] + (e & 63) : e;
       };
       bool first_it = true;
-      for (int base = start, cc = ch0; placed == -1;) {
+      for (int base = start, cc = ch0; placed == -1 && !memo_fail;) {
         if (cmode == 2 ? cc >= g_chk.nch : base >= n_nc) break;
         uint32_t flags = 0, iflags = 0, tflags = 0, pf = 0;
         // 4 rounds per thread: independent, so their loads overlap. A spilled order (thousands of NodeClaims, long
@@ -3290,7 +3343,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a0, const Solv
         a.cur_nc[2 * sl + 1] = s_ctl[13];
       }
       // ---- addToNewNodeClaim: templates in weight order --------------------------------------------
-      for (int base = 0; base < a.n_tmpl && placed == -1; base += NT) {
+      for (int base = 0; base < a.n_tmpl && placed == -1 && !memo_fail; base += NT) {
         const int t = base + tid;
         // a memoised failure is permanent: remaining limits only shrink, and the rest is a function of the
         // (template, shape-level) pair (failures that depend on topology counts or reservations are not memoised)
@@ -3526,6 +3579,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a0, const Solv
         a.events[s_ctl[4]++] = pod;
       } else {
         a.placement[pod] = -1;
+        if (!TOPO && !a.res_mode && (s_B.present & ~b_negop & ~D.wellknown) == 0) a.sl_fail[sl] = s_ctl[2];
         const bool res_err = s_ctl[27] != 0;  // a ReservedOfferingError is not relaxed (upstream trySchedule)
         if (res_err) a.stats[40] += 1;
         const bool relaxed = !res_err && lvl + 1 < a.shape_nlevels[shape];
@@ -3577,7 +3631,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a0, const Solv
     atomicAdd((unsigned long long*)&a.stats[0], (unsigned long long)g_fast.attempts);
     atomicAdd((unsigned long long*)&a.stats[1], (unsigned long long)g_fast.bytes);
     a.stats[24] = g_fast.fpods;
-    for (int i = 0; i < 7; i++) a.stats[32 + i] = g_fast.fbail[i];
+    for (int i = 0; i < 8; i++) a.stats[32 + i] = g_fast.fbail[i];
     for (int i = 0; i < 6; i++) a.stats[25 + i] = g_fast.fcyc[i];
     if (FT_FINE && timing)
       for (int i = 0; i < 8; i++) a.stats[16 + i] = g_fast.fcyc[6 + i];
@@ -3941,9 +3995,9 @@ __global__ __launch_bounds__(FEAS_WAVES * 64) void feasibility_kernel(FeasArgs a
 #define FEASB_MINW 8  // waves per SIMD the register budget must allow (measured: 0.1574 -> 0.1245 ms on 50k rows)
 __global__ __launch_bounds__(FEASB_WAVES * 64, FEASB_MINW) void feasibility_bits_kernel(FeasArgs a) {
   __shared__ DevDict D;
+  block_copy(D, a.dict);
   __shared__ int64_t s_vint[KP_MAX_BOUND_KEYS * 64];
   __shared__ OfferClass s_cls[KP_MAX_CLASSES];
-  block_copy(D, a.dict);
   const int tid = threadIdx.x;
   constexpr int NT = FEASB_WAVES * 64;
   const DevCatalog Cd = *a.cat;
@@ -4014,27 +4068,25 @@ __global__ __launch_bounds__(FEASB_WAVES * 64, FEASB_MINW) void feasibility_bits
     auto cheapest_row = [&]() {
       if (!a.out_cheapest) return;
       GLB double* oc = (GLB double*)a.out_cheapest + (size_t)q * T;
-      if (price_sub) {  // a row copy: FEASB_CP loads in flight per lane before their stores (the pointers may alias)
-        const GLB double* ps = price_sub + (size_t)cls * T;
+      if (price_sub) {
+        // a row copy through range-checked buffer descriptors (num_records = the row's bytes: the hardware drops
+        // the tail lanes' accesses), so the loop has no per-element branch: FEASB_CP loads in flight per lane, each
+        // store waiting only for its own load (predicated stores compiled to one branch and a full drain each)
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(uintptr_t)(price_sub + (size_t)cls * T), 0, T * 8, KP_BUF_DWORD3);
+        const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)oc, 0, T * 8, KP_BUF_DWORD3);
+        const bool nt = a.pad_ & 1;
         for (int t0 = 0; t0 < T; t0 += 64 * FEASB_CP) {
-          double vv[FEASB_CP];
+          const int vo = (t0 + lane) * 8;  // the whole offset in the VGPR + immediate (the range-checked part)
+          u32x2 vv[FEASB_CP];
 #pragma unroll
-          for (int i = 0; i < FEASB_CP; i++) {
-            const int t = t0 + i * 64 + lane;
-            vv[i] = t < T ? ps[t] : 0.0;
-          }
-          if (a.pad_ & 1) {
+          for (int i = 0; i < FEASB_CP; i++) vv[i] = __builtin_amdgcn_raw_buffer_load_b64(rs, vo + i * 512, 0, 0);
+          if (nt) {
 #pragma unroll
-            for (int i = 0; i < FEASB_CP; i++) {
-              const int t = t0 + i * 64 + lane;
-              if (t < T) __builtin_nontemporal_store(vv[i], (double*)&oc[t]);
-            }
+            for (int i = 0; i < FEASB_CP; i++) __builtin_amdgcn_raw_buffer_store_b64(vv[i], ro, vo + i * 512, 0, 2);
           } else {
 #pragma unroll
-            for (int i = 0; i < FEASB_CP; i++) {
-              const int t = t0 + i * 64 + lane;
-              if (t < T) oc[t] = vv[i];
-            }
+            for (int i = 0; i < FEASB_CP; i++) __builtin_amdgcn_raw_buffer_store_b64(vv[i], ro, vo + i * 512, 0, 0);
           }
         }
       } else {

@@ -29,7 +29,7 @@ pops = max(1, st["pops"])
 out.update({"pops": st["pops"], "attempts_per_pop": round(st["attempts"] / pops, 3), "fast_pods": st["fast_pods"],
             "fast_share": round(st["fast_pods"] / pops, 4), "scanned_per_pop": round(st["scanned"] / pops, 1),
             "cursor_start_per_pop": round(st["cursor_starts"] / pops, 1), "slow_sorts": st["slow_sorts"],
-            "fast_bails": dict(zip(["ineligible", "spilled", "shift", "scan", "merge", "minvalues", "none", "-"],
+            "fast_bails": dict(zip(["ineligible", "spilled", "shift", "scan", "merge", "minvalues", "none", "memo"],
                                    st["fast_bails"])),
             "order_chunks": dict(zip(["peak_chunks", "splits", "emptied", "builds", "final_mode"], st["order_chunks"]))})
 if os.environ.get("KP_TIMING"):

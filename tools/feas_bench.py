@@ -24,7 +24,7 @@ for spec in sys.argv[1:] or ["lds"]:
     for kv in filter(None, envs.split(",")):
         k, _, v = kv.partition("=")
         os.environ[k] = v
-    for cheapest in (True, False):
+    for cheapest in ((True,) if os.environ.get("FEAS_CHEAPEST_ONLY") else (True, False)):
         fp = kpamd.FilterPlan(ctx, ch, qs, cheapest=cheapest)
         fp.run()
         sts = [fp.run() for _ in range(int(os.environ.get("FEAS_REPS", "10")))]
