@@ -280,6 +280,11 @@ L2_BYTES_PER_PAIR = 208  # SURVEY §8d type row (64 B value ids + 96 B allocatab
 ROW_BYTES = 880 + 96     # one compiled requirement row (KReqs) + its requests, read once per row
 
 
+def _feas_kernel_name(T):
+    """The bitset filter kernel kp_filter_run launches for a catalogue of T types (csrc launch_feasibility)."""
+    return "feasibility_quad_kernel" if T <= 1024 else "feasibility_bits_kernel"
+
+
 def _feasibility(args, cat, ctx, prob, barrier, max_over_ranks, world, steps=10):
     """CompatibleAvailableFilter (R:pkg/providers/instance/filter/filter.go:39-64) batched on the device: mask +
     cheapest compatible available offering price per (row, type), rows resident in HBM. Two row sets, both without
@@ -309,9 +314,9 @@ def _feasibility(args, cat, ctx, prob, barrier, max_over_ranks, world, steps=10)
         ach = alg / (k_ms / 1e3) / 1e9
         legs[name] = {"value": round(pairs * world * steps / elapsed, 1), "unit": "pairs/s", "rows": rows,
                       "instance_types": T, "kernel_ms": round(k_ms, 4),
-                      "roofline": {"bound": "hbm", "kernel": "feasibility_bits_kernel", "achieved": round(ach, 1),
+                      "roofline": {"bound": "hbm", "kernel": _feas_kernel_name(T), "achieved": round(ach, 1),
                                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                                   "traffic": _traffic("feasibility_bits_kernel") if name == "distinct" else None,
+                                   "traffic": _traffic(_feas_kernel_name(T)) if name == "distinct" else None,
                                    "algorithmic_bytes_per_launch": alg,
                                    "bytes_per_row": ROW_BYTES + 8 * T + 8 * ((T + 63) // 64),
                                    "l2_effective_GBs": round(pairs * L2_BYTES_PER_PAIR / (k_ms / 1e3) / 1e9, 1)}}

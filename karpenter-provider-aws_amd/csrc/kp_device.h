@@ -244,9 +244,12 @@ struct FeasArgs {
   const uint8_t* q_reqs;     // [Q] KReqs
   const int64_t* q_requests; // [Q][NRES]
   uint64_t* out_mask;        // [Q][tiles]
-  double* out_cheapest;      // [Q][T] or null
-  int32_t bits;              // 1: feasibility_bits_kernel (bitsets over the catalogue), 0: feasibility_kernel
+  double* out_cheapest;      // [Q][ch_stride] (the first T of each row) or null
+  int32_t bits;              // 1: bitsets over the catalogue (feasibility_quad_kernel when T <= 1024, else
+                             // feasibility_bits_kernel), 0: feasibility_kernel
   int32_t blocks;            // its grid (rows are strided over the waves)
+  int32_t one_row;           // 1: feasibility_bits_kernel at any T (its cross-check, KP_FEAS_ONE_ROW)
+  int32_t ch_stride;         // doubles per out_cheapest row: T rounded up to whole 128-byte lines (rows start aligned)
 };
 
 // ---- launch-side selection (kp_launch_select) ------------------------------------------------------

@@ -3756,6 +3756,7 @@ struct kp_filter_plan {
   uint32_t n_queries = 0;
   int T = 0;
   size_t tiles = 0, o_mask = 0, o_ch = 0;
+  int ch_stride = 0;  // doubles per device cheapest-price row (whole 128-byte lines; the caller's rows are T long)
   bool cheapest = false;
   double prepare_ms = 0;
   const kp_catalog* cat = nullptr;  // kp_filter_refresh: catalogue, compiled form and its offering offsets
@@ -3797,7 +3798,8 @@ int32_t kp_filter_prepare(kp_ctx* ctx, const kp_catalog* cat, const kp_feasibili
   const size_t host_bytes = blob.host.size();
   const size_t tiles = (size_t)(T + 63) / 64;
   plan->o_mask = blob.reserve(sizeof(uint64_t) * std::max<size_t>(1, n_queries * tiles));
-  plan->o_ch = with_cheapest ? blob.reserve(sizeof(double) * std::max<size_t>(1, (size_t)n_queries * T)) : 0;
+  plan->ch_stride = (T + 15) & ~15;
+  plan->o_ch = with_cheapest ? blob.reserve(sizeof(double) * std::max<size_t>(1, (size_t)n_queries * plan->ch_stride)) : 0;
   HIPCHK(hipMalloc(&plan->buf.p, blob.host.size()));
   uint8_t* base = (uint8_t*)plan->buf.p;
   vector<DevCatalog> dc = DevCats(base, cp, coffs);
@@ -3816,11 +3818,13 @@ int32_t kp_filter_prepare(kp_ctx* ctx, const kp_catalog* cat, const kp_feasibili
   fa.q_requests = (const int64_t*)(base + o_qr);
   fa.out_mask = (uint64_t*)(base + plan->o_mask);
   fa.out_cheapest = with_cheapest ? (double*)(base + plan->o_ch) : nullptr;
+  fa.ch_stride = plan->ch_stride;
   // the bitset kernel (KP_FEAS_GLOBAL: the per-type global-gather kernel, kept as its cross-check)
   fa.bits = getenv("KP_FEAS_GLOBAL") ? 0 : 1;
   fa.blocks = (int32_t)std::min<uint32_t>(std::max<uint32_t>((n_queries + 7) / 8, 1), 8192);
   if (const char* e = getenv("KP_FEAS_BLOCKS")) fa.blocks = std::max(1, std::min(65535, atoi(e)));  // measurement knob
   fa.pad_ = getenv("KP_FEAS_TEMPORAL") ? 0 : 1;  // bit 0: the cheapest-price stream as non-temporal stores
+  fa.one_row = getenv("KP_FEAS_ONE_ROW") ? 1 : 0;  // cross-check: the one-row-per-wave kernel at any catalogue size
   plan->n_queries = n_queries;
   plan->T = T;
   plan->tiles = tiles;
@@ -3853,7 +3857,8 @@ int32_t kp_filter_run(kp_filter_plan* plan, uint64_t* out_mask, double* out_chea
   if (n && out_mask)
     HIPCHK(hipMemcpyAsync(out_mask, base + plan->o_mask, sizeof(uint64_t) * n * plan->tiles, hipMemcpyDeviceToHost, ctx->stream));
   if (n && out_cheapest)
-    HIPCHK(hipMemcpyAsync(out_cheapest, base + plan->o_ch, sizeof(double) * (size_t)n * plan->T, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpy2DAsync(out_cheapest, sizeof(double) * plan->T, base + plan->o_ch, sizeof(double) * plan->ch_stride,
+                            sizeof(double) * plan->T, n, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
   float ms = 0;
   HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));

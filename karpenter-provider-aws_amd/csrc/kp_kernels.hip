@@ -3971,7 +3971,7 @@ __global__ __launch_bounds__(FEAS_WAVES * 64) void feasibility_kernel(FeasArgs a
       const int nt = min(FEAS_NT, tiles - c0);
       if (lane < nt) a.out_mask[(size_t)q * tiles + c0 + lane] = myword;
       if (a.out_cheapest) {
-        double* oc = a.out_cheapest + (size_t)q * T;
+        double* oc = a.out_cheapest + (size_t)q * a.ch_stride;
 #pragma unroll
         for (int i = 0; i < FEAS_NT; i++)
           if ((valid >> i) & 1) oc[tt[i]] = cheapest[i];
@@ -4067,7 +4067,7 @@ __global__ __launch_bounds__(FEASB_WAVES * 64, FEASB_MINW) void feasibility_bits
     // cheapest compatible available offering price per type
     auto cheapest_row = [&]() {
       if (!a.out_cheapest) return;
-      GLB double* oc = (GLB double*)a.out_cheapest + (size_t)q * T;
+      GLB double* oc = (GLB double*)a.out_cheapest + (size_t)q * a.ch_stride;
       if (price_sub) {
         // a row copy through range-checked buffer descriptors (num_records = the row's bytes: the hardware drops
         // the tail lanes' accesses), so the loop has no per-element branch: FEASB_CP loads in flight per lane, each
@@ -4155,6 +4155,310 @@ __global__ __launch_bounds__(FEASB_WAVES * 64, FEASB_MINW) void feasibility_bits
   }
 }
 const void* feasibility_bits_kernel_ptr() { return (const void*)feasibility_bits_kernel; }
+
+// feasibility_quad_kernel: feasibility_bits_kernel's filter for catalogues of <= 1024 types (TW <= 16), four rows per
+// wave. Each row is decoded by the whole wave as there (requirement words, bounds, Offerings classes: the lane layout
+// needs all 64 lanes) and staged in LDS; then the type-set work runs once for the four rows at a time: lane group g
+// (lanes 16 g .. 16 g + 15) evaluates row g, lane l of the group holding type word l. One load instruction gathers
+// the four rows' words, so the per-row cost of the key walks, the Fits lower bounds (16-ary, in the group) and the
+// offering rows drops by up to four; the groups' loops diverge only where the rows do. The rows' cheapest-price
+// copies follow, one row at a time over the whole wave. Every type-set load is a buffer load whose inactive lanes
+// carry an out-of-range offset (they read 0): no load sits in a branch.
+#define FEASQ_OOB 0x7ffffff0  // a buffer offset past every record count (reads 0)
+#ifndef FEASQ_EW
+#define FEASQ_EW 7      // eval waves per block (the other FEASB_WAVES - FEASQ_EW copy the cheapest-price rows)
+#endif
+#ifndef FEASQ_ROWS
+#define FEASQ_ROWS 28   // rows per block (one quad per eval wave)
+#endif
+#ifndef FEASQ_B128
+#define FEASQ_B128 1    // copy waves move 16 bytes per lane and instruction (0: 8)
+#endif
+#ifndef FEASQ_SKIP_EVAL
+#define FEASQ_SKIP_EVAL 0  // measurement only: decode + copies, no type-set work (wrong masks)
+#endif
+__global__ __launch_bounds__(FEASB_WAVES * 64, FEASB_MINW) void feasibility_quad_kernel(FeasArgs a) {
+  __shared__ DevDict D;
+  __shared__ int64_t s_vint[KP_MAX_BOUND_KEYS * 64];
+  __shared__ OfferClass s_cls[KP_MAX_CLASSES];
+  __shared__ int32_t s_fitn[KP_NRES];
+  __shared__ uint64_t s_allow[FEASB_WAVES][4][KP_MAX_WORDS];  // each row's allowed value words
+  __shared__ uint64_t s_rowh[FEASB_WAVES][4][4];              // keys, negQ, classes, requested-resource mask
+  __shared__ int64_t s_rq[FEASB_WAVES][4][KP_NRES];           // requests
+  __shared__ uint64_t s_pass0[FEASB_WAVES][4][16];            // the type words before the AND chain
+  __shared__ uint64_t s_rcls[FEASQ_ROWS];                      // each row's offering classes, for the copy waves
+  __shared__ int32_t s_ready[FEASQ_ROWS];                      // ... once published
+  for (int i = threadIdx.x; i < FEASQ_ROWS; i += FEASB_WAVES * 64) s_ready[i] = 0;
+  block_copy(D, a.dict);
+  const int tid = threadIdx.x;
+  constexpr int NT = FEASB_WAVES * 64;
+  const DevCatalog Cd = *a.cat;
+  const GLB double* price_sub = (const GLB double*)Cd.price_sub;
+  const GLB double* price_cm = (const GLB double*)Cd.price_cm;
+  const GLB uint64_t* custom = (const GLB uint64_t*)Cd.custom_nonneg;
+  __syncthreads();
+  const int T = D.T, TW = D.TW, C = D.C;
+  for (int i = tid; i < D.KB * 64; i += NT) s_vint[i] = a.vint[i];
+  for (int i = tid; i < C; i += NT) s_cls[i] = Cd.cls[i];
+  for (int i = tid; i < KP_NRES; i += NT) s_fitn[i] = Cd.fit_n[i];
+  __syncthreads();
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = LANE;
+  const bool lw = lane < TW;
+  const uint64_t nonneg = lw ? ((const GLB uint64_t*)Cd.nonneg)[lane] : 0;
+  const int row8 = TW * 8;
+  const __amdgpu_buffer_rsrc_t r_tm = __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)Cd.TM, 0, D.W * 64 * row8, KP_BUF_DWORD3);
+  const __amdgpu_buffer_rsrc_t r_nk = __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)Cd.NOKEY, 0, D.K * row8, KP_BUF_DWORD3);
+  const __amdgpu_buffer_rsrc_t r_dne = __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)Cd.DNE, 0, D.K * row8, KP_BUF_DWORD3);
+  const __amdgpu_buffer_rsrc_t r_fv = __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)Cd.fit_vals, 0, KP_NRES * T * 8, KP_BUF_DWORD3);
+  const __amdgpu_buffer_rsrc_t r_fm = __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)Cd.fit_mask, 0, KP_NRES * T * row8, KP_BUF_DWORD3);
+  const __amdgpu_buffer_rsrc_t r_of = __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)Cd.offer_avail, 0, C * row8, KP_BUF_DWORD3);
+  auto ld64 = [](const __amdgpu_buffer_rsrc_t& r, int off) -> uint64_t {
+    const u32x2 x = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+    return ((uint64_t)x.y << 32) | x.x;
+  };
+  struct RowHdr {
+    uint64_t hw, v;
+    int64_t rq, gt, lt;
+  };
+  auto load_row = [&](long q) {
+    RowHdr h;
+    const GLB KReqs* Q = reinterpret_cast<const GLB KReqs*>((const GLB uint8_t*)a.q_reqs + (size_t)q * sizeof(KReqs));
+    h.hw = lane < 6 ? reinterpret_cast<const GLB uint64_t*>(Q)[lane] : 0;
+    h.v = lane < D.W ? Q->vals[lane] : 0;
+    h.rq = lane < KP_NRES ? ((const GLB int64_t*)a.q_requests)[(size_t)q * KP_NRES + lane] : 0;
+    h.gt = lane < KP_MAX_BOUND_KEYS ? Q->gt[lane] : 0;
+    h.lt = lane < KP_MAX_BOUND_KEYS ? Q->lt[lane] : 0;
+    return h;
+  };
+  // the block's rows: [row0, row1), FEASQ_ROWS per block; eval waves take its quads in turn, copy waves its rows
+  const long n = a.n_queries;
+  const long row0 = (long)blockIdx.x * FEASQ_ROWS, row1 = min(row0 + FEASQ_ROWS, n);
+  if (wave >= FEASQ_EW) {  // ---- a copy wave: each row's cheapest-price row once its eval wave published the classes
+    if (a.out_cheapest) {
+      // items = (row, half): T <= 1024, so a row is two 512-type halves (a short one reads 0 / drops its stores). The
+      // next item's loads are issued before this item's stores: the in-order vector-memory counter then waits for a
+      // load without waiting for the stores issued just before it
+      const int ncw = FEASB_WAVES - FEASQ_EW, cw = wave - FEASQ_EW;
+      const long nrows = row1 - row0;
+      const int nitems = nrows > cw ? 2 * (int)((nrows - cw + ncw - 1) / ncw) : 0;
+      auto row_of = [&](int it) { return row0 + cw + (long)(it >> 1) * ncw; };
+#if FEASQ_B128
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      auto issue = [&](int it, u32x4 (&v)[8]) {
+        const long q = row_of(it);
+        const int j = (int)(q - row0);
+        while (__hip_atomic_load(&s_ready[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) __builtin_amdgcn_s_sleep(2);
+        asm volatile("" ::: "memory");
+        const uint64_t cls = s_rcls[j];
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(uintptr_t)(price_sub + (size_t)cls * T), 0, T * 8, KP_BUF_DWORD3);
+        const int vo = ((it & 1) * 512 + lane * 2) * 8;
+#pragma unroll
+        for (int i = 0; i < 4; i++) v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, vo + i * 1024, 0, 0);
+      };
+      auto store = [&](int it, const u32x4 (&v)[8]) {
+        GLB double* oc = (GLB double*)a.out_cheapest + (size_t)row_of(it) * a.ch_stride;
+        const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)oc, 0, T * 8, KP_BUF_DWORD3);
+        const int vo = ((it & 1) * 512 + lane * 2) * 8;
+#pragma unroll
+        for (int i = 0; i < 4; i++) __builtin_amdgcn_raw_buffer_store_b128(v[i], ro, vo + i * 1024, 0, 2);
+      };
+      typedef u32x4 CpT;
+#else
+      typedef u32x2 CpT;
+      auto issue = [&](int it, u32x2 (&v)[8]) {
+        const long q = row_of(it);
+        const int j = (int)(q - row0);
+        while (__hip_atomic_load(&s_ready[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) __builtin_amdgcn_s_sleep(2);
+        asm volatile("" ::: "memory");  // (the classes are read after the flag: LDS requests complete in order)
+        const uint64_t cls = s_rcls[j];
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(uintptr_t)(price_sub + (size_t)cls * T), 0, T * 8, KP_BUF_DWORD3);
+        const int vo = ((it & 1) * 512 + lane) * 8;
+#pragma unroll
+        for (int i = 0; i < 8; i++) v[i] = __builtin_amdgcn_raw_buffer_load_b64(rs, vo + i * 512, 0, 0);
+      };
+      auto store = [&](int it, const u32x2 (&v)[8]) {
+        GLB double* oc = (GLB double*)a.out_cheapest + (size_t)row_of(it) * a.ch_stride;
+        const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)oc, 0, T * 8, KP_BUF_DWORD3);
+        const int vo = ((it & 1) * 512 + lane) * 8;
+        if (a.pad_ & 1) {
+#pragma unroll
+          for (int i = 0; i < 8; i++) __builtin_amdgcn_raw_buffer_store_b64(v[i], ro, vo + i * 512, 0, 2);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 8; i++) __builtin_amdgcn_raw_buffer_store_b64(v[i], ro, vo + i * 512, 0, 0);
+        }
+      };
+#endif
+      if (price_sub) {
+        CpT P[8], Q[8];
+        if (nitems) issue(0, P);
+        for (int it = 0; it < nitems; it += 2) {  // (nitems is even)
+          issue(it + 1, Q);
+          store(it, P);
+          if (it + 2 < nitems) issue(it + 2, P);
+          store(it + 1, Q);
+        }
+      } else {
+        for (long q = row0 + cw; q < row1; q += ncw) {
+          const int j = (int)(q - row0);
+          while (__hip_atomic_load(&s_ready[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) __builtin_amdgcn_s_sleep(2);
+        asm volatile("" ::: "memory");  // (the classes are read after the flag: LDS requests complete in order)
+          const uint64_t cls = s_rcls[j];
+          GLB double* oc = (GLB double*)a.out_cheapest + (size_t)q * a.ch_stride;
+          for (int t = lane; t < T; t += 64) {
+            double ch = __builtin_huge_val();
+            for (uint64_t m = cls; m; m &= m - 1) ch = fmin(ch, price_cm[(size_t)__builtin_ctzll(m) * T + t]);
+            oc[t] = ch;
+          }
+        }
+      }
+    }
+    return;
+  }
+  const long quads = (row1 - row0 + 3) / 4;
+  long qi = wave;
+  RowHdr nxt = qi < quads ? load_row(row0 + 4 * qi) : RowHdr{0, 0, 0, 0, 0};
+  for (; qi < quads; qi += FEASQ_EW) {
+    const long qd_base = row0 + 4 * qi;
+    // ---- phase 1: decode the four rows (the next row's header loads in flight meanwhile)
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const long q = qd_base + r;
+      const long qn = r < 3 ? q + 1 : qd_base + 4 * FEASQ_EW;
+      const RowHdr cur = nxt;
+      if (qn < row1) nxt = load_row(qn);
+      if (q >= row1) {  // past the block's last row: an empty group
+        if (lane < 4) s_rowh[wave][r][lane] = 0;
+        if (lane < 16) s_pass0[wave][r][lane] = 0;
+        continue;
+      }
+      const uint64_t v = cur.v;
+      ReqView rv;
+      rv.present = lane_bcast(cur.hw, 0);
+      rv.compl_ = lane_bcast(cur.hw, 1) & rv.present;
+      rv.hgt = lane_bcast(cur.hw, 2);
+      rv.hlt = lane_bcast(cur.hw, 3);
+      rv.hmin = lane_bcast(cur.hw, 4);
+      rv.nz = nz_keys(D, v);
+      rv.dne = 0;
+      rv.gt = rv.lt = nullptr;
+      rv.minv = nullptr;
+      const uint64_t negQ = negop_mask(rv.present, rv.compl_, rv.nz);
+      uint64_t allowed;
+      {
+        const uint64_t bk = (rv.hgt | rv.hlt) & rv.present & rv.compl_ & ((1ull << D.KB) - 1);
+        const uint64_t bm = bk ? bounds_mask_lanes(D, bk, rv.hgt, rv.hlt, cur.gt, cur.lt, (const int64_t LDS*)s_vint, D.KB,
+                                                   (const GLB int64_t*)a.vint)
+                               : ~0ull;
+        const int k = lane < D.W ? (int)D.wkey[lane] : 0;
+        allowed = lane >= D.W ? 0
+                  : !((rv.present >> k) & 1) ? D.validbits[lane]
+                  : ((rv.compl_ >> k) & 1)   ? (~v & D.validbits[lane] & bm)
+                                              : v;
+      }
+      const uint64_t cls = allowed_classes<true>(D, (const OfferClass LDS*)s_cls, rv, allowed, negQ);
+      if (lane == 0) {  // published to the copy waves (LDS writes complete in order: the classes before the flag;
+                        // a relaxed workgroup-scope flag keeps this wave's vector-memory queue undrained)
+        s_rcls[q - row0] = cls;
+        asm volatile("" ::: "memory");
+        __hip_atomic_store(&s_ready[q - row0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      uint64_t pass = nonneg;
+      // Compatible(q, type, WK) part (a): types with a non-well-known key q does not define (rare: per-type loads)
+      if (a.mode_compatible && (Cd.custom_any & ~rv.present) && __ballot(lw && pass)) {
+        uint64_t keep = 0;
+        if (lw)
+          for (uint64_t m = pass; m; m &= m - 1) {
+            const int b = __builtin_ctzll(m);
+            if (!(custom[lane * 64 + b] & ~rv.present)) keep |= 1ull << b;
+          }
+        pass = keep;
+      }
+      s_allow[wave][r][lane] = allowed;
+      if (lane < 16) s_pass0[wave][r][lane] = pass;
+      if (lane < KP_NRES) s_rq[wave][r][lane] = cur.rq;
+      const uint64_t rmask = (uint64_t)(uint32_t)__ballot(cur.rq > 0);
+      if (lane == 0) {
+        s_rowh[wave][r][0] = rv.present & D.catalog_keys;
+        s_rowh[wave][r][1] = negQ;
+        s_rowh[wave][r][2] = cls;
+        s_rowh[wave][r][3] = rmask;
+      }
+    }
+    wave_sync();
+    // ---- phase 2: the four rows' type-set work, lane group g on row g
+    if (!FEASQ_SKIP_EVAL) {
+      const int g = lane >> 4, l = lane & 15;
+      const bool gl = l < TW;
+      const int lo8 = l * 8;
+      const long q = qd_base + g;
+      const uint64_t keys = s_rowh[wave][g][0], negQ = s_rowh[wave][g][1], cls = s_rowh[wave][g][2];
+      const uint32_t rmask = (uint32_t)s_rowh[wave][g][3];
+      uint64_t pass = gl ? s_pass0[wave][g][l] : 0;
+      auto off = [&](int row) { return gl ? row * row8 + lo8 : FEASQ_OOB; };
+      // Intersects over the shared keys (as feasibility_bits_kernel; a single-valued key with fewer excluded than
+      // allowed values: the complement of (negQ ? 0 : DNE) | the excluded values' TM rows, NOKEY, DNE and the TM
+      // rows being disjoint by construction)
+      for (uint64_t km = keys; km; km &= km - 1) {
+        const int k = __builtin_ctzll(km);
+        const bool nq = (negQ >> k) & 1;
+        uint64_t wm = 1ull << k;
+        if ((D.multiword >> k) & 1) wm |= D.ovfmask[k];
+        int nA = 0, nE = 0;
+        for (uint64_t m = wm; m; m &= m - 1) {
+          const int w = __builtin_ctzll(m);
+          const uint64_t aw = s_allow[wave][g][w], vb = D.validbits[w];
+          nA += __builtin_popcountll(aw & vb);
+          nE += __builtin_popcountll(~aw & vb);
+        }
+        const bool compl_walk = ((D.single_valued >> k) & 1) && nE < nA;
+        uint64_t u = compl_walk ? (nq ? 0 : ld64(r_dne, off(k))) : (ld64(r_nk, off(k)) | (nq ? ld64(r_dne, off(k)) : 0));
+        for (uint64_t m = wm; m; m &= m - 1) {
+          const int w = __builtin_ctzll(m);
+          const uint64_t aw = s_allow[wave][g][w];
+          for (uint64_t bits = (compl_walk ? ~aw : aw) & D.validbits[w]; bits; bits &= bits - 1)
+            u |= ld64(r_tm, off(w * 64 + __builtin_ctzll(bits)));
+        }
+        pass &= compl_walk ? ~u : u;
+      }
+      // Fits: the threshold row of the first allocatable >= the request (a 16-ary lower bound in the group)
+      for (uint32_t rm = rmask; rm; rm &= rm - 1) {
+        const int r = __builtin_ctz(rm);
+        const int64_t need = s_rq[wave][g][r];
+        const int nr = s_fitn[r];
+        int lo = 0, hi = nr;
+        while (lo < hi) {
+          const int span = hi - lo, step = span <= 16 ? 1 : (span + 15) / 16, idx = lo + l * step;
+          const int64_t x = (int64_t)ld64(r_fv, idx < hi ? (r * T + idx) * 8 : FEASQ_OOB);
+          const uint32_t gb = (uint32_t)(__ballot(idx < hi && x >= need) >> (16 * g)) & 0xffffu;
+          if (span <= 16) {
+            lo = hi = gb ? lo + __builtin_ctz(gb) : hi;
+          } else if (!gb) {
+            lo = lo + min(15, (hi - 1 - lo) / step) * step + 1;
+          } else {
+            const int f = __builtin_ctz(gb);
+            if (f == 0) {
+              hi = lo;
+            } else {
+              const int nlo = lo + (f - 1) * step + 1;
+              hi = lo + f * step;
+              lo = nlo;
+            }
+          }
+        }
+        pass &= ld64(r_fm, lo < nr ? off(r * T + lo) : FEASQ_OOB);  // no threshold: 0
+      }
+      // an available offering of a compatible class
+      uint64_t av = 0;
+      for (uint64_t m = cls; m; m &= m - 1) av |= ld64(r_of, off(__builtin_ctzll(m)));
+      pass &= av;
+      if (gl && q < row1) ((GLB uint64_t*)a.out_mask)[(size_t)q * TW + l] = pass;
+    }
+    wave_sync();  // (phase 1 of the next quad rewrites this wave's LDS rows)
+  }
+}
 
 // ------------------------------------------------------------------------------------------------
 // launch_kernel: instance.DefaultProvider.Create's launch-side selection (R:pkg/providers/instance/instance.go:
@@ -4700,7 +5004,12 @@ hipError_t launch_launch(const LaunchArgs& a, hipStream_t s) {
 }
 hipError_t launch_feasibility(const FeasArgs& a, hipStream_t s) {
   if (a.bits) {
-    hipLaunchKernelGGL(feasibility_bits_kernel, dim3((unsigned)max(1, a.blocks)), dim3(FEASB_WAVES * 64), 0, s, a);
+    if (a.T <= 1024 && !a.one_row) {  // TW <= 16: four rows per wave
+      const long blocks = max(((long)a.n_queries + FEASQ_ROWS - 1) / FEASQ_ROWS, 1L);  // one chunk of rows each
+      hipLaunchKernelGGL(feasibility_quad_kernel, dim3((unsigned)blocks), dim3(FEASB_WAVES * 64), 0, s, a);
+    } else {
+      hipLaunchKernelGGL(feasibility_bits_kernel, dim3((unsigned)max(1, a.blocks)), dim3(FEASB_WAVES * 64), 0, s, a);
+    }
     return hipGetLastError();
   }
   long blocks = ((long)a.n_queries + FEAS_WAVES - 1) / FEAS_WAVES;

@@ -158,26 +158,41 @@ def test_filter_plan_pod_rows(ctx, catalog):
 
 
 def test_feasibility_lds_staged_equals_global(ctx, catalog, monkeypatch):
-    """feasibility_lds_kernel (catalogue columns staged in LDS) == feasibility_kernel (global gathers, KP_FEAS_GLOBAL)
-    bit for bit on pairwise-distinct rows (the bench's roofline leg: Gt/Lt bounds, NotIn, zones, capacity types), and
-    both == the oracle on a sample of rows."""
+    """The bitset kernels (feasibility_quad_kernel, four rows per wave, at this catalogue size; feasibility_bits_kernel,
+    KP_FEAS_ONE_ROW) == feasibility_kernel (per-type global gathers, KP_FEAS_GLOBAL) bit for bit on pairwise-distinct
+    rows (the bench's roofline leg: Gt/Lt bounds, NotIn, zones, capacity types; a row count that leaves the last quad
+    partial), and == the oracle on a sample of rows."""
     import kpamd
     from kpamd import synth
     from oracle import pyoracle
-    queries = synth.distinct_queries(catalog, 3000)
+    queries = synth.distinct_queries(catalog, 3001)
     cat = kpamd.Catalog(ctx, catalog)
+
+    def run(qs, **env):
+        for k in ("KP_FEAS_GLOBAL", "KP_FEAS_ONE_ROW"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        fp = kpamd.FilterPlan(ctx, cat, qs, cheapest=True)
+        try:
+            k, c, _ = fp.run(read=True)
+        finally:
+            fp.close()
+        return k, c
     try:
-        fp = kpamd.FilterPlan(ctx, cat, queries, cheapest=True)
-        k1, c1, _ = fp.run(read=True)
-        fp.close()
-        monkeypatch.setenv("KP_FEAS_GLOBAL", "1")
-        fp = kpamd.FilterPlan(ctx, cat, queries, cheapest=True)
-        k2, c2, _ = fp.run(read=True)
-        fp.close()
+        k1, c1 = run(queries)
+        k2, c2 = run(queries, KP_FEAS_GLOBAL="1")
+        k3, c3 = run(queries, KP_FEAS_ONE_ROW="1")
+        for nq in (1, 2, 3, 5):  # partial quads only
+            ka, ca = run(queries[:nq])
+            kb, cb = run(queries[:nq], KP_FEAS_ONE_ROW="1")
+            assert (ka == kb).all() and (ka == k1[:nq]).all(), nq
+            np.testing.assert_array_equal(ca, cb)
     finally:
         cat.close()
-    assert (k1 == k2).all()
+    assert (k1 == k2).all() and (k1 == k3).all()
     np.testing.assert_array_equal(c1, c2)
+    np.testing.assert_array_equal(c1, c3)
     assert k1.any() and not k1.all()
     for qi in range(0, len(queries), 97):
         want_k, want_c = pyoracle.compatible_available_filter(catalog, *queries[qi])

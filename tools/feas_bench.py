@@ -16,7 +16,7 @@ ctx = kpamd.Context(0)
 ch = kpamd.Catalog(ctx, cat)
 qs = synth.distinct_queries(cat, rows)
 out = {}
-KNOBS = ("KP_FEAS_GLOBAL", "KP_FEAS_NO_KEYS", "KP_FEAS_NO_RES", "KP_FEAS_NO_PRICE", "KP_FEAS_BLOCKS", "KP_FEAS_DBG")
+KNOBS = ("KP_FEAS_GLOBAL", "KP_FEAS_ONE_ROW", "KP_FEAS_BLOCKS", "KP_FEAS_TEMPORAL")
 for spec in sys.argv[1:] or ["lds"]:
     name, _, envs = spec.partition("=")
     for k in KNOBS:

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Instruction-mix / stall PMC passes over the feasibility leg (feasibility_bits_kernel, 50k distinct rows, one
+# Instruction-mix / stall PMC passes over the feasibility leg (feasibility_quad_kernel / feasibility_bits_kernel, 50k distinct rows, one
 # warm-up + FEAS_REPS launches), one pass per counter group.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp FEAS_CHEAPEST_ONLY=1 FEAS_REPS=2
@@ -11,7 +11,7 @@ import csv, glob, collections
 acc = collections.defaultdict(float); n = collections.defaultdict(set)
 for f in glob.glob('gpurun_out/pmcf_*/**/*counter_collection.csv', recursive=True):
     for r in csv.DictReader(open(f)):
-        if 'feasibility_bits_kernel' in r['Kernel_Name']:
+        if 'feasibility_' in r['Kernel_Name'] and 'kernel(' in r['Kernel_Name']:
             acc[r['Counter_Name']] += float(r['Counter_Value'])
             n[r['Counter_Name']].add(r.get('Dispatch_Id', r.get('Correlation_Id', '')))
 for k, v in sorted(acc.items()):

@@ -9,7 +9,8 @@ import json
 import sys
 
 KERNELS = {"solve_kernel": "solve_kernel<", "feasibility_kernel": "feasibility_kernel(",
-           "feasibility_bits_kernel": "feasibility_bits_kernel(", "sim_kernel": "sim_kernel<",
+           "feasibility_bits_kernel": "feasibility_bits_kernel(", "feasibility_quad_kernel": "feasibility_quad_kernel(",
+           "sim_kernel": "sim_kernel<",
            "finalize_kernel": "finalize_kernel("}
 
 
