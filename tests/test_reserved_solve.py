@@ -244,3 +244,41 @@ def test_device_random_reserved_matches_oracle(ctx, catalog, seed, mode):
     check_same(got, want)
     assert got["stats"]["reserved_offering_errors"] == want["stats"]["reserved_offering_errors"]
     assert sum(req_of(n, RID) is not None for n in got["nodeclaims"]) > 0
+
+
+@pytest.mark.gpu
+def test_device_reserved_solve_refresh_matches_oracle(ctx, catalog):
+    """A strict-mode Solve plan on a reservation catalogue, refreshed in place after reservation capacity / ICE
+    updates by id (kp_catalog_update_offerings + kp_solve_refresh: the capacities the ReservationManager starts from
+    are recomputed), equals the oracle on the updated catalogue; and the refreshed plan differs from its first run."""
+    import kpamd
+    from oracle import pyoracle
+    from test_gpu_parity import check_same
+    from test_reserved_offerings import reserved_catalogue
+    cat = reserved_catalogue(catalog, 300, 0)
+    prob = random_reserved_problem(cat, 1500, 0, STRICT)
+    sched = kpamd.Scheduler(ctx, prob)
+    plan = sched.prepare()
+    try:
+        first = plan.run()
+        ch = sched.catalogs[0]
+        ups, k = [], 0
+        for ti, t in enumerate(ch.instance_types):
+            for o in t.offerings:
+                if o.reservation_id:
+                    cap = [0, 1, 2][k % 3]
+                    k += 1
+                    ups.append((ti, "reserved", o.zone, cap != 0, None, o.reservation_id, cap))
+        assert ups
+        ch.update_offerings(ups, ch.seqnum() + 1)
+        plan.refresh()
+        got = plan.run()
+    finally:
+        plan.close()
+        for c in sched.catalogs:
+            c.close()
+    want = pyoracle.solve(prob)  # prob's catalogue objects carry the updates
+    check_same(got, want)
+    assert got["stats"]["reserved_offering_errors"] == want["stats"]["reserved_offering_errors"]
+    assert ([n["requirements"] for n in got["nodeclaims"]] != [n["requirements"] for n in first["nodeclaims"]]
+            or got["stats"]["reserved_offering_errors"] != first["stats"]["reserved_offering_errors"])
