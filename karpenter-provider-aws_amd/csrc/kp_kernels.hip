@@ -23,6 +23,12 @@
 #include "kp_model.h"
 
 #define LANE ((int)(threadIdx.x & 63))
+// The file builds as two translation units (Makefile): KP_TU 1 = the Solve, template, finalize, launch and
+// consolidation kernels with their launchers (scheduled for ILP: the single-wave Solve loop is issue-bound), KP_TU 2 =
+// the filter kernels and launch_feasibility (the default scheduler: measured 2.6 % faster there). 3 = both.
+#ifndef KP_TU
+#define KP_TU 3
+#endif
 #ifndef FASTLANE
 #define FASTLANE 1  // solve_kernel: wave-0 fast lane for merge-free placements (0 = full path only)
 #endif
@@ -2666,6 +2672,7 @@ if (!FL_NOTIME && tmg) {                                    \
 
 // TOPO: the batch has topology spread groups (else that code compiles out). BATCH: one Solve per workgroup, each with
 // its own arguments batch[blockIdx.x] (the general consolidation path's simulations); else the kernel argument a0.
+#if KP_TU & 1
 template <int NW, bool TOPO, bool BATCH>
 __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a0, const SolveArgs* __restrict__ batch) {
   const SolveArgs& a = BATCH ? batch[blockIdx.x] : a0;
@@ -3824,6 +3831,8 @@ __global__ __launch_bounds__(FIN_THREADS) void finalize_kernel(FinalizeArgs a0, 
   }
 }
 
+#endif  // KP_TU & 1
+#if KP_TU & 2
 // ------------------------------------------------------------------------------------------------
 // feasibility_kernel: CompatibleAvailableFilter, one query row per wave, lane = type.
 // ------------------------------------------------------------------------------------------------
@@ -4154,7 +4163,6 @@ __global__ __launch_bounds__(FEASB_WAVES * 64, FEASB_MINW) void feasibility_bits
     cheapest_row();
   }
 }
-const void* feasibility_bits_kernel_ptr() { return (const void*)feasibility_bits_kernel; }
 
 // feasibility_quad_kernel: feasibility_bits_kernel's filter for catalogues of <= 1024 types (TW <= 16), four rows per
 // wave. Each row is decoded by the whole wave as there (requirement words, bounds, Offerings classes: the lane layout
@@ -4460,6 +4468,8 @@ __global__ __launch_bounds__(FEASB_WAVES * 64, FEASB_MINW) void feasibility_quad
   }
 }
 
+#endif  // KP_TU & 2
+#if KP_TU & 1
 // ------------------------------------------------------------------------------------------------
 // launch_kernel: instance.DefaultProvider.Create's launch-side selection (R:pkg/providers/instance/instance.go:
 // 117-125, 242-270, 336-355, 392-439, 504-518), one wave per NodeClaim request. Lane = list entry: the
@@ -5002,6 +5012,8 @@ hipError_t launch_launch(const LaunchArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(launch_kernel, dim3((unsigned)blocks), dim3(LAUNCH_WAVES * 64), 0, s, a);
   return hipGetLastError();
 }
+#endif  // KP_TU & 1
+#if KP_TU & 2
 hipError_t launch_feasibility(const FeasArgs& a, hipStream_t s) {
   if (a.bits) {
     if (a.T <= 1024 && !a.one_row) {  // TW <= 16: four rows per wave
@@ -5018,3 +5030,4 @@ hipError_t launch_feasibility(const FeasArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(feasibility_kernel, dim3((unsigned)blocks), dim3(FEAS_WAVES * 64), 0, s, a);
   return hipGetLastError();
 }
+#endif  // KP_TU & 2

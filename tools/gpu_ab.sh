@@ -2,6 +2,7 @@
 # GPU call: A/B of the in-tree library against tools/variants/*: config-2 quick bench and config-5 1M, interleaved
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp; rm -f gpurun_out/ab.txt
+[ -n "$AB_PRE_TESTS" ] && { bash tools/gpu_tests.sh $AB_PRE_TESTS || exit $?; }
 for round in 1 2; do
   for lib in karpenter-provider-aws_amd/libkp.so tools/variants/*/libkp.so; do
     KP_LIB=$PWD/$lib timeout -k 10 200 python -u bench.py --quick --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/v.json 2> gpurun_out/v.err || { echo "$lib failed"; tail -5 gpurun_out/v.err; exit 1; }
