@@ -434,7 +434,8 @@ def _consolidation(args, cat, ctx, dist, rank, world, barrier, kcomm):
 def _consolidation_general(args, cat, ctx, rank, world, barrier):
     """Consolidation on a topology-spread cluster (the general simulation path): the 100
     firstNConsolidationOption prefixes plus random subsets of 2..20 candidates through kp_consolidate_argmin, rank 0
-    only (the host compile per subset is the cost: no sharding claimed). Reported with and without kp_cluster_prepare."""
+    only (each batch of subsets is one solve_kernel launch over overlays on the resident superset Solve: no sharding
+    claimed). Reported with and without kp_cluster_prepare."""
     import numpy as np
     import kpamd
     from kpamd import disruption, synth

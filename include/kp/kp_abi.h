@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define KP_ABI_VERSION 10
+#define KP_ABI_VERSION 11
 
 enum kp_status {
   KP_OK = 0,
@@ -51,6 +51,7 @@ enum kp_status {
   KP_E_DEVICE = -3,
   KP_E_UNSUPPORTED = -4,
   KP_E_NOTFOUND = -5,
+  KP_E_CANCELED = -6, /* ABI v11: the caller's kp_cancel token was set while the call ran (ctx.Done) */
 };
 
 /* Resource axis, fixed (R:pkg/providers/instancetype/types.go:317-329,151-153; R:pkg/apis/v1/labels.go:69-81). */
@@ -667,6 +668,19 @@ int32_t kp_solve_prepare(kp_ctx* ctx, const kp_solve_in* in, kp_solve_plan** out
 struct kp_comm;
 int32_t kp_solve_prepare_comm(kp_ctx* ctx, const kp_solve_in* in, struct kp_comm* comm, kp_solve_plan** out);
 int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out);
+/* ABI v11: cancellation (upstream Solve observes ctx.Done() between pods; SURVEY §5 failure handling). A kp_cancel
+ * is a flag in host-mapped memory that solve_kernel polls about every 1,024 Queue pops; kp_cancel_set is lock-free
+ * and may be called from any thread while a call runs (the cgo shim calls it when ctx.Done() fires). A run that sees
+ * it set stops placing pods and returns KP_E_CANCELED with no result; the plan stays usable (every run restores its
+ * state). The token stays set until kp_cancel_reset. One token may serve many calls, one at a time. */
+typedef struct kp_cancel kp_cancel;
+int32_t kp_cancel_create(kp_ctx* ctx, kp_cancel** out);
+int32_t kp_cancel_set(kp_cancel* c);
+int32_t kp_cancel_reset(kp_cancel* c);
+void kp_cancel_destroy(kp_cancel* c);
+/* kp_solve_run / kp_solve with a cancellation token (NULL: not cancellable, as kp_solve_run). */
+int32_t kp_solve_run_cancellable(kp_solve_plan* plan, kp_cancel* cancel, kp_solve_result** out);
+int32_t kp_solve_cancellable(kp_ctx* ctx, const kp_solve_in* in, kp_cancel* cancel, kp_solve_result** out);
 /* A prepared plan after kp_catalog_update_offerings (UnavailableOfferings.MarkUnavailable + SeqNum,
  * R:pkg/cache/unavailableofferings.go:66-92): re-applies the catalogues' current availability and prices to the
  * resident catalogue half (offering masks, class prices and subset minima, the NodeClaimTemplates' options) and the

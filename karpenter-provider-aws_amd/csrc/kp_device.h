@@ -46,7 +46,7 @@ struct SolveArgs {
   const uint8_t* shape_reqs;         // [SL] KReqs
   const uint64_t* shape_negop;       // [SL]
   const int64_t* shape_requests;     // [S][NRES]
-  const uint64_t* shape_tolerates;   // [S] bit ts: tolerates taint set ts
+  const uint64_t* shape_tolerates;   // [SL] bit ts: tolerates taint set ts (per level: toleratePreferNoScheduleTaints)
   const uint64_t* shape_pvp;         // rows of TW words
   const int32_t* pvp_base;           // [SL][n_catalogs] first row
   const int32_t* pvp_slot;           // [SL][64] row offset of key k (relative to base)
@@ -100,6 +100,7 @@ struct SolveArgs {
   int32_t* nc_cat;                   // [P] catalogue of the NodeClaim's template
   uint32_t req_res_mask;             // resources some pod shape requests (> 0)
   int32_t timing;                    // 1: thread 0 accumulates per-phase s_memtime deltas into stats[8..15]
+  const int32_t* cancel;             // kp_cancel flag (host-mapped, polled every ~1024 pops), NULL: none
   // topology spread (upstream Topology, TopologyTypeSpread groups). A group on a dictionary key keeps a
   // count per value ordinal and the mask of registered domains; a hostname group a saturating u8 count per
   // node (existing positions: hcnt_ex, NodeClaim ids: hcnt_nc).

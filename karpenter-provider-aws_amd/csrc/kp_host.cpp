@@ -1296,7 +1296,8 @@ struct Compiled {
   // shapes
   vector<int32_t> shape_level_base, shape_nlevels;
   vector<KReqs> shape_reqs;
-  vector<uint64_t> shape_negop, shape_tolerates;
+  vector<uint64_t> shape_negop, shape_tolerates;  // per shape-level (tolerations change at the PreferNoSchedule level)
+  vector<char> sl_pns;                             // per shape-level: toleratePreferNoScheduleTaints' level
   vector<int64_t> shape_requests;
   vector<uint64_t> pvp;
   vector<int32_t> pvp_base, pvp_slot, pvp_n;  // pvp_n: rows of catalogue 0 per shape-level
@@ -1510,6 +1511,19 @@ int32_t EncodeHostPorts(const vector<vector<HostPortKey>>& shapes, const vector<
   return KP_OK;
 }
 
+// the toleration Preferences.toleratePreferNoScheduleTaints appends, and whether the pod already carries it
+// (corev1 Toleration.MatchToleration: equal key, operator, value and effect)
+const kp_toleration kPnsToleration = {"", "", KP_TOL_EXISTS, KP_EFFECT_PREFER_NO_SCHEDULE};
+bool HasPnsToleration(const kp_pod_shape& sh) {
+  for (uint32_t j = 0; j < sh.n_tolerations; j++) {
+    const kp_toleration& t = sh.tolerations[j];
+    if ((!t.key || !t.key[0]) && (!t.value || !t.value[0]) && t.op == KP_TOL_EXISTS &&
+        t.effect == KP_EFFECT_PREFER_NO_SCHEDULE)
+      return true;
+  }
+  return false;
+}
+
 int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector<RawReqs>>& strict_levels,
                         const vector<vector<vector<int>>>& spread_levels, const vector<int>& np_taintset,
                         const vector<vector<vector<RawReqs>>>& filter_levels) {
@@ -1629,9 +1643,11 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
     for (auto& f : filts) fcanon += "[" + KCanon(d, f) + "]";
     string id = key + "|" + std::to_string(t.max_skew) + "|" + (sh.namespace_ ? sh.namespace_ : "") + "|" +
                 SelectorCanon(t.selector) + "|" + std::to_string(aff) + std::to_string(taint) + "|" + fcanon;
+    const int sl = cp.shape_level_base[s] + l;
+    const uint64_t ltol = cp.shape_tolerates[sl];  // the level's tolerations (Relax may have appended one)
     if (taint)
-      for (uint32_t i = 0; i < sh.n_tolerations; i++) {
-        const kp_toleration& x = sh.tolerations[i];
+      for (uint32_t i = 0; i < sh.n_tolerations + (cp.sl_pns[sl] ? 1 : 0); i++) {
+        const kp_toleration& x = i < sh.n_tolerations ? sh.tolerations[i] : kPnsToleration;
         id += string("(") + (x.key ? x.key : "") + "," + (x.value ? x.value : "") + "," + std::to_string(x.op) + "," +
               std::to_string(x.effect) + ")";
       }
@@ -1673,13 +1689,13 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
         cp.tg_terms.push_back(f);
         cp.tg_terms_negop.push_back(NegOp(d, f));
       }
-    cp.tg_filt_tol.push_back(taint ? cp.shape_tolerates[s] : ~0ull);
+    cp.tg_filt_tol.push_back(taint ? ltol : ~0ull);
     // NewTopologyGroup: every known domain of the key, with a zero count (ForEachDomain + taint policy)
     uint64_t reg = 0;
     if (k >= 0) {
       const vector<uint64_t>& dm = domains_of(k);
       for (int b = 0; b < 64; b++)
-        if (dm[b] && (!taint || (dm[b] & cp.shape_tolerates[s]))) reg |= 1ull << b;
+        if (dm[b] && (!taint || (dm[b] & ltol))) reg |= 1ull << b;
     }
     cp.tg_reg.push_back(reg);
     for (int b = 0; b < 64; b++) cp.tg_cnt.push_back(0);
@@ -1694,7 +1710,7 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
     // countDomains: bound pods the selector matches, on nodes the filter admits; then existing nodes' domains
     auto filter_ok = [&](uint32_t ni) {
       const int ts = cp.ex_taintset[ex_pos[ni]];
-      if (taint && !((cp.shape_tolerates[s] >> ts) & 1)) return false;
+      if (taint && !((ltol >> ts) & 1)) return false;
       if (!(aff && nonempty)) return true;
       for (auto& f : filts)
         if (HostCompatible(d, node_reqs[ni], f, false)) return true;
@@ -1719,7 +1735,7 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
       }
     }
     if (k >= 0) {  // the existing nodes' domains depend only on (key, node filter): cached across groups
-      string fid = key + "|" + std::to_string(aff && nonempty) + fcanon + (taint ? std::to_string(cp.shape_tolerates[s]) : string("-"));
+      string fid = key + "|" + std::to_string(aff && nonempty) + fcanon + (taint ? std::to_string(ltol) : string("-"));
       auto it = node_domains.find(fid);
       if (it == node_domains.end()) {
         uint64_t m = 0;
@@ -2065,6 +2081,8 @@ struct SolveRaw {
   vector<vector<vector<RawReqs>>> filter_levels;  // per level: MakeTopologyNodeFilter's terms (nodeSelector + each
                                                   // remaining required term; the nodeSelector alone when none)
   std::set<string> topo_keys;                     // non-hostname spread keys (need a dictionary id)
+  bool tolerate_pns = false;                      // some NodePool taint has effect PreferNoSchedule (NewScheduler)
+  vector<int> pns_level;                          // per shape: the level toleratePreferNoScheduleTaints adds, or -1
   vector<RawReqs> ex_labels;                      // per input existing node (hostname: see HostnameValue)
   bool hostname = false;                          // some pod requirement names kubernetes.io/hostname
 };
@@ -2193,10 +2211,14 @@ int32_t ParseSolve(const kp_solve_in* in, SolveRaw& raw) {
       if (x.key == kHostname) return fail(KP_E_UNSUPPORTED, "hostname requirement on nodepool");
     if (raw.hostname) r.push_back({kHostname, KP_OP_IN, {kHostPlaceholder}, -1});  // NewNodeClaim's placeholder
     raw.np_reqs[i] = std::move(r);
-    for (uint32_t j = 0; j < np.n_taints; j++)
+    for (uint32_t j = 0; j < np.n_taints; j++) {
       raw.np_taints[i].push_back({np.taints[j].key ? np.taints[j].key : "", np.taints[j].value ? np.taints[j].value : "",
                                   np.taints[j].effect});
+      // upstream NewScheduler: Preferences{ToleratePreferNoSchedule} when any NodePool template taint has that effect
+      if (np.taints[j].effect == KP_EFFECT_PREFER_NO_SCHEDULE) raw.tolerate_pns = true;
+    }
   }
+  raw.pns_level.assign(in->n_shapes, -1);
   raw.levels.assign(in->n_shapes, {});
   raw.strict_levels.assign(in->n_shapes, {});
   raw.spread_levels.assign(in->n_shapes, {});
@@ -2283,6 +2305,16 @@ int32_t ParseSolve(const kp_solve_in* in, SolveRaw& raw) {
         spreads[i] = spreads.back();
         spreads.pop_back();
       }
+    }
+    // toleratePreferNoScheduleTaints (the last relaxation, only with Preferences.ToleratePreferNoSchedule): appends
+    // {Operator: Exists, Effect: PreferNoSchedule} unless a toleration already equals it (corev1 MatchToleration:
+    // key, operator, value and effect equal), so the pod's requirements and terms stay those of the last level
+    if (raw.tolerate_pns && !HasPnsToleration(sh)) {
+      raw.pns_level[s] = (int)raw.levels[s].size();
+      raw.levels[s].push_back(raw.levels[s].back());
+      raw.strict_levels[s].push_back(raw.strict_levels[s].back());
+      raw.filter_levels[s].push_back(raw.filter_levels[s].back());
+      raw.spread_levels[s].push_back(raw.spread_levels[s].back());
     }
   }
   for (uint32_t b = 0; b < in->n_bound_pods; b++)  // inverse anti-affinity keys need a dictionary id too
@@ -2519,24 +2551,33 @@ int32_t CompilePerCall(const kp_solve_in* in, const SolveRaw& raw, Compiled& cp)
     cp.shape_level_base.push_back(sl);
     cp.shape_nlevels.push_back((int32_t)raw.levels[s].size());
     for (int r = 0; r < KP_NRES; r++) cp.shape_requests.push_back((sh.requests.present >> r) & 1 ? sh.requests.milli[r] : 0);
-    uint64_t tol = 0;
-    for (auto& kv : tsets) {
-      bool all = true;
-      for (auto& taint : kv.first) {  // Taints.ToleratesPod
-        bool ok = false;
-        for (uint32_t j = 0; j < sh.n_tolerations && !ok; j++) {
-          const kp_toleration& t = sh.tolerations[j];
-          const string tk = t.key ? t.key : "", tv = t.value ? t.value : "";
-          if (t.effect != KP_EFFECT_ANY && t.effect != taint.effect) continue;
-          if (!tk.empty() && tk != taint.key) continue;
-          if (t.op == KP_TOL_EQUAL) ok = tv == taint.value;
-          else if (t.op == KP_TOL_EXISTS) ok = true;
+    // Taints.ToleratesPod per taint set, with the pod's tolerations (+ toleratePreferNoScheduleTaints' at its level)
+    auto tolerates = [&](bool pns) {
+      uint64_t tol = 0;
+      for (auto& kv : tsets) {
+        bool all = true;
+        for (auto& taint : kv.first) {
+          bool ok = false;
+          for (uint32_t j = 0; j < sh.n_tolerations + (pns ? 1 : 0) && !ok; j++) {
+            const kp_toleration& t = j < sh.n_tolerations ? sh.tolerations[j] : kPnsToleration;
+            const string tk = t.key ? t.key : "", tv = t.value ? t.value : "";
+            if (t.effect != KP_EFFECT_ANY && t.effect != taint.effect) continue;
+            if (!tk.empty() && tk != taint.key) continue;
+            if (t.op == KP_TOL_EQUAL) ok = tv == taint.value;
+            else if (t.op == KP_TOL_EXISTS) ok = true;
+          }
+          if (!ok) all = false;
         }
-        if (!ok) all = false;
+        if (all) tol |= 1ull << kv.second;
       }
-      if (all) tol |= 1ull << kv.second;
+      return tol;
+    };
+    const uint64_t tol0 = tolerates(false);
+    for (size_t l = 0; l < raw.levels[s].size(); l++) {  // per shape-level: the PreferNoSchedule level differs
+      const bool pns = (int)l == raw.pns_level[s];
+      cp.shape_tolerates.push_back(pns ? tolerates(true) : tol0);
+      cp.sl_pns.push_back(pns ? 1 : 0);
     }
-    cp.shape_tolerates.push_back(tol);
     for (auto& lv : raw.levels[s]) {
       KReqs q = Compile(d, lv);
       cp.shape_reqs.push_back(q);
@@ -3457,10 +3498,53 @@ void kp_solve_plan_destroy(kp_solve_plan* p) {
   delete p;  // (after the lock: it may drop the context's last reference)
 }
 
+// kp_cancel: one int32 flag in pinned, host-mapped memory (written by the host, polled by solve_kernel)
+struct kp_cancel {
+  CtxRef ctx;
+  int32_t* flag = nullptr;  // hipHostMalloc: coherent, mapped; the same address on the device (unified addressing)
+};
+
+int32_t kp_cancel_create(kp_ctx* ctx, kp_cancel** out) {
+  if (!ctx || !out) return fail(KP_E_INVAL, "null argument");
+  std::lock_guard<std::recursive_mutex> lock(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device));
+  auto c = std::make_unique<kp_cancel>();
+  c->ctx = ctx;
+  void* p = nullptr;
+  HIPCHK(hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocCoherent));
+  c->flag = (int32_t*)p;
+  __atomic_store_n(c->flag, 0, __ATOMIC_SEQ_CST);
+  *out = c.release();
+  return KP_OK;
+}
+// lock-free: called from another thread while a run holds the context's lock
+int32_t kp_cancel_set(kp_cancel* c) {
+  if (!c) return fail(KP_E_INVAL, "null argument");
+  __atomic_store_n(c->flag, 1, __ATOMIC_SEQ_CST);
+  return KP_OK;
+}
+int32_t kp_cancel_reset(kp_cancel* c) {
+  if (!c) return fail(KP_E_INVAL, "null argument");
+  __atomic_store_n(c->flag, 0, __ATOMIC_SEQ_CST);
+  return KP_OK;
+}
+void kp_cancel_destroy(kp_cancel* c) {
+  if (!c) return;
+  {
+    std::lock_guard<std::recursive_mutex> lock(c->ctx->mu);  // (no run is reading it once the lock is ours)
+    (void)hipSetDevice(c->ctx->device);
+    if (c->flag) (void)hipHostFree(c->flag);
+  }
+  delete c;
+}
+
 // One Solve over resident inputs: restore mutable state, solve_kernel, finalize_kernel, copy results.
-int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out) {
+int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out) { return kp_solve_run_cancellable(plan, nullptr, out); }
+
+int32_t kp_solve_run_cancellable(kp_solve_plan* plan, kp_cancel* cancel, kp_solve_result** out) {
   auto t0 = std::chrono::steady_clock::now();
   if (!plan || !out) return fail(KP_E_INVAL, "null argument");
+  if (cancel && cancel->ctx.p != plan->ctx.p) return fail(KP_E_INVAL, "the cancel token belongs to another context");
   kp_ctx* ctx = plan->ctx;
   std::lock_guard<std::recursive_mutex> lock(ctx->mu);
   if (int32_t rc = SolvePlanStale(plan)) return rc;
@@ -3477,7 +3561,13 @@ int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out) {
   HIPCHK(hipMemsetAsync(base + plan->o_ver, 0, plan->n_ver, st));
   HIPCHK(hipMemsetAsync(base + plan->o_fail, 0xFF, plan->n_fail, st));
   if (plan->n_hcnc) HIPCHK(hipMemsetAsync(base + plan->o_hcnc, 0, plan->n_hcnc, st));
-  const SolveArgs& a = plan->a;
+  SolveArgs a = plan->a;
+  if (cancel) {
+    if (__atomic_load_n(cancel->flag, __ATOMIC_SEQ_CST)) return fail(KP_E_CANCELED, "cancelled before the run");
+    void* dp = nullptr;
+    HIPCHK(hipHostGetDevicePointer(&dp, cancel->flag, 0));
+    a.cancel = (const int32_t*)dp;
+  }
   const size_t dyn = std::max<size_t>((size_t)2 * a.sort_cap * sizeof(int32_t), a.chk_maxc ? CHK_LDS_BYTES : 0);
   HIPCHK(hipEventRecord(ctx->ev0, st));
   HIPCHK(launch_solve(a, 8, dyn, st));
@@ -3487,6 +3577,7 @@ int32_t kp_solve_run(kp_solve_plan* plan, kp_solve_result** out) {
   HIPCHK(hipStreamSynchronize(st));
   if (stats[7]) return fail(KP_E_DEVICE, "solve_kernel exceeded its Queue.Pop bound (%llu pops): aborted",
                             (unsigned long long)stats[2]);
+  if (stats[46]) return fail(KP_E_CANCELED, "Solve cancelled after %llu pops (kp_cancel_set)", (unsigned long long)stats[2]);
   const int n_nc = (int)stats[3];
   FinalizeArgs f;
   f.solve_stats = nullptr;
@@ -3622,11 +3713,13 @@ int32_t kp_solve_validate(const kp_solve_in* in) {
   return CompileSolve(in, C);
 }
 
-int32_t kp_solve(kp_ctx* ctx, const kp_solve_in* in, kp_solve_result** out) {
+int32_t kp_solve(kp_ctx* ctx, const kp_solve_in* in, kp_solve_result** out) { return kp_solve_cancellable(ctx, in, nullptr, out); }
+
+int32_t kp_solve_cancellable(kp_ctx* ctx, const kp_solve_in* in, kp_cancel* cancel, kp_solve_result** out) {
   kp_solve_plan* plan = nullptr;
   int32_t rc = kp_solve_prepare(ctx, in, &plan);
   if (rc) return rc;
-  rc = kp_solve_run(plan, out);
+  rc = kp_solve_run_cancellable(plan, cancel, out);
   kp_solve_plan_destroy(plan);
   return rc;
 }
@@ -3760,6 +3853,7 @@ struct kp_filter_plan {
   bool cheapest = false;
   double prepare_ms = 0;
   const kp_catalog* cat = nullptr;  // kp_filter_refresh: catalogue, compiled form and its offering offsets
+  std::shared_ptr<bool> alive;      // cat's alive token: run / refresh after kp_catalog_destroy return KP_E_INVAL
   uint64_t seqnum = 0;              // catalogue seqnum the resident offerings reflect
   Compiled cp;
   CatOffsets coff{};
@@ -3830,6 +3924,7 @@ int32_t kp_filter_prepare(kp_ctx* ctx, const kp_catalog* cat, const kp_feasibili
   plan->tiles = tiles;
   plan->cheapest = with_cheapest != 0;
   plan->cat = cat;
+  plan->alive = cat->alive;
   plan->seqnum = cat->seqnum;
   plan->coff = coffs[0];
   plan->cp = std::move(cp);
@@ -3845,6 +3940,7 @@ int32_t kp_filter_run(kp_filter_plan* plan, uint64_t* out_mask, double* out_chea
   if (out_cheapest && !plan->cheapest) return fail(KP_E_INVAL, "plan was prepared without cheapest prices");
   kp_ctx* ctx = plan->ctx;
   std::lock_guard<std::recursive_mutex> lock(ctx->mu);
+  if (int32_t rc = CatalogsAlive({plan->alive})) return rc;
   if (plan->cat->seqnum != plan->seqnum)  // R:instancetype.go:225-237: a changed seqnum invalidates the offerings
     return fail(KP_E_INVAL, "stale plan: catalogue seqnum %llu, plan built at %llu (kp_filter_refresh)",
                 (unsigned long long)plan->cat->seqnum, (unsigned long long)plan->seqnum);
@@ -3876,6 +3972,7 @@ int32_t kp_filter_run(kp_filter_plan* plan, uint64_t* out_mask, double* out_chea
 // ids, then only the offering arrays are copied over their resident copies.
 int32_t kp_filter_refresh(kp_filter_plan* plan, const kp_catalog* cat) {
   if (!plan || !cat) return fail(KP_E_INVAL, "null argument");
+  if (int32_t rc = CatalogsAlive({plan->alive})) return rc;
   if (cat != plan->cat || (int)cat->types.size() != plan->T)
     return fail(KP_E_INVAL, "kp_filter_refresh: the plan was prepared on another catalogue");
   const int32_t rc = RefreshOfferings(plan->ctx, cat, plan->cp, plan->coff, (uint8_t*)plan->buf.p);
@@ -3929,6 +4026,7 @@ struct kp_launch_plan {
   size_t o_out = 0, o_types = 0, o_ovr = 0, o_stats = 0, o_pall = 0, o_rcap = 0;
   double prepare_ms = 0;
   const kp_catalog* cat = nullptr;  // kp_launch_refresh
+  std::shared_ptr<bool> alive;      // cat's alive token (as kp_filter_plan)
   uint64_t seqnum = 0;              // catalogue seqnum the resident offerings reflect
   int T = 0;
   Compiled cp;
@@ -4096,6 +4194,7 @@ int32_t kp_launch_prepare(kp_ctx* ctx, const kp_catalog* cat, const kp_launch_re
   plan->max_types = max_types;
   plan->ovr_stride = ovr_stride;
   plan->cat = cat;
+  plan->alive = cat->alive;
   plan->seqnum = cat->seqnum;
   plan->T = T;
   plan->coff = coffs[0];
@@ -4113,6 +4212,7 @@ int32_t kp_launch_run(kp_launch_plan* plan, kp_launch_result* out, uint32_t* out
   if (!plan) return fail(KP_E_INVAL, "null argument");
   kp_ctx* ctx = plan->ctx;
   std::lock_guard<std::recursive_mutex> lock(ctx->mu);
+  if (int32_t rc = CatalogsAlive({plan->alive})) return rc;
   if (plan->cat->seqnum != plan->seqnum)
     return fail(KP_E_INVAL, "stale plan: catalogue seqnum %llu, plan built at %llu (kp_launch_refresh)",
                 (unsigned long long)plan->cat->seqnum, (unsigned long long)plan->seqnum);
@@ -4150,6 +4250,7 @@ int32_t kp_launch_run(kp_launch_plan* plan, kp_launch_result* out, uint32_t* out
 // the subnet-zone classes do not change with availability or price).
 int32_t kp_launch_refresh(kp_launch_plan* plan, const kp_catalog* cat) {
   if (!plan || !cat) return fail(KP_E_INVAL, "null argument");
+  if (int32_t rc = CatalogsAlive({plan->alive})) return rc;
   if (cat != plan->cat || (int)cat->types.size() != plan->T)
     return fail(KP_E_INVAL, "kp_launch_refresh: the plan was prepared on another catalogue");
   int32_t rc = RefreshOfferings(plan->ctx, cat, plan->cp, plan->coff, (uint8_t*)plan->buf.p);
@@ -4439,6 +4540,8 @@ static int32_t PrepareGeneral(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan
     HIPCHK(hipSetDevice(ctx->device));
     plan->gb_tried = true;
     rc = GeneralBatchBuild(plan.get(), plan->gb);
+    // the batched layout is an optimisation: a device that cannot hold it leaves the per-subset compile
+    if (rc == KP_E_NOMEM || rc == KP_E_DEVICE) (void)hipGetLastError(), rc = KP_E_UNSUPPORTED;
     if (rc && rc != KP_E_UNSUPPORTED) return rc;
     if (rc) plan->gb.reset();
   }
@@ -4456,6 +4559,9 @@ int32_t kp_cluster_prepare(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan** 
   auto t0 = std::chrono::steady_clock::now();
   if (!ctx || !cl || !out) return fail(KP_E_INVAL, "null argument");
   if (cl->n_nodes && !cl->nodes) return fail(KP_E_INVAL, "null nodes");
+  if (cl->pod_uids)  // one rule on every path (batched kernels, general batch, per-subset compile): as kp_solve
+    for (uint32_t i = 0; i < cl->n_pods; i++)
+      if (!cl->pod_uids[i]) return fail(KP_E_INVAL, "null pod uid");
   // capacity reservations: SimulateScheduling's Solve reserves offerings strictly (DisableReservedCapacityFallback),
   // which the batched kernels do not model: such clusters take the general path (whole device Solves)
   bool topo = false;
@@ -5447,15 +5553,24 @@ static int32_t GeneralBatchRun(kp_cluster_plan* plan, GeneralBatch& gb, const ve
   for (size_t b0 = 0; b0 < idx.size(); b0 += per_launch) {
     const auto th0 = std::chrono::steady_clock::now();
     const int n = (int)std::min(per_launch, idx.size() - b0);
-    if (gb.arenas_bytes < gb.stride * n) {  // sized for a whole launch at once: later batches reuse it
-      const size_t cap = gb.stride * std::max<size_t>((size_t)n, per_launch);
-      HIPCHK(gb.arenas.alloc(cap));
-      gb.arenas_bytes = cap;
+    // arenas for this launch's n simulations, grown geometrically (a few subsets do not pin 2 GiB on the plan);
+    // when the device cannot hold them, this batch and the rest run one simulation at a time (GeneralSimOne)
+    hipError_t ae = hipSuccess;
+    if (gb.arenas_bytes < gb.stride * n) {
+      const size_t sims = std::min(per_launch, std::max<size_t>((size_t)n, 2 * gb.arenas_bytes / gb.stride));
+      ae = gb.arenas.alloc(gb.stride * sims);
+      gb.arenas_bytes = ae == hipSuccess ? gb.stride * sims : 0;
     }
-    const size_t args_need = (sizeof(SolveArgs) + sizeof(FinalizeArgs)) * per_launch + 256;
-    if (gb.args_bytes < args_need) {
-      HIPCHK(gb.args.alloc(args_need));
-      gb.args_bytes = args_need;
+    const size_t args_need = (sizeof(SolveArgs) + sizeof(FinalizeArgs)) * (size_t)n + 512;
+    if (ae == hipSuccess && gb.args_bytes < args_need) {
+      ae = gb.args.alloc(args_need);
+      gb.args_bytes = ae == hipSuccess ? args_need : 0;
+    }
+    if (ae != hipSuccess) {
+      (void)hipGetLastError();
+      for (size_t j = b0; j < idx.size(); j++)
+        if (int32_t rc = GeneralSimOne(plan, cands[idx[j]], labels, multi_node, outs[idx[j]], counters, dev_ms)) return rc;
+      break;
     }
     uint8_t* arenas = (uint8_t*)gb.arenas.p;
     uint8_t* sh = (uint8_t*)gb.shared.p;
@@ -5623,7 +5738,8 @@ static int32_t GeneralSimLocked(kp_cluster_plan* plan, const uint32_t* offsets, 
   const bool batch_on = !(gbe && gbe[0] == '0');
   if (batch_on && !plan->gb_tried) {
     plan->gb_tried = true;
-    const int32_t rc = GeneralBatchBuild(plan, plan->gb);
+    int32_t rc = GeneralBatchBuild(plan, plan->gb);
+    if (rc == KP_E_NOMEM || rc == KP_E_DEVICE) (void)hipGetLastError(), rc = KP_E_UNSUPPORTED;  // (as at prepare)
     if (rc && rc != KP_E_UNSUPPORTED) return rc;
     if (rc) plan->gb.reset();
   }

@@ -29,6 +29,19 @@
 #ifndef KP_TU
 #define KP_TU 3
 #endif
+// Measurement knobs (FASTLANE, FL_NOTIME, FT_FINE, SORT_DIAG, EX_DIAG, FEASQ_SKIP_EVAL, the scan / grid shapes) are
+// set only by the tools/ variant builds, which force-include tools/kp_diag.h (KP_DIAG_BUILD). Here they take their
+// production values; a -D of any of them in any other build is an error, so no stray flag can turn a production
+// kernel into a measurement stub.
+#if !defined(KP_DIAG_BUILD) &&                                                                                       \
+    (defined(FASTLANE) || defined(FL_NOTIME) || defined(FT_FINE) || defined(FAST_SCAN_MAX) ||                        \
+     defined(FAST_CHK_LIVE) || defined(SORT_DIAG) || defined(EX_DIAG) || defined(FEAS_MAX_BLOCKS) ||                 \
+     defined(FEASQ_EW) || defined(FEASQ_ROWS) || defined(FEASQ_B128) || defined(FEASQ_SKIP_EVAL))
+#error "a measurement knob is set outside a tools/ variant build (tools/kp_diag.h)"
+#endif
+#ifndef KP_DIAG_BUILD
+#define KP_DIAG_BUILD 0
+#endif
 #ifndef FASTLANE
 #define FASTLANE 1  // solve_kernel: wave-0 fast lane for merge-free placements (0 = full path only)
 #endif
@@ -2002,6 +2015,11 @@ __device__ __noinline__ uint64_t fl_fits_filter(int cat_a, uint64_t X0, int64_t 
   return X;
 }
 
+// kp_cancel: the caller's flag in host-mapped memory, read past every cache (system scope)
+__device__ __forceinline__ bool cancel_set(const int32_t* flag) {
+  return flag && __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+}
+
 // Places popped pods while they need no requirement merge; returns the number placed. A pod it cannot place is
 // handed to the full path through g_ctl[6] / g_ctl[26]. Called by wave 0 only. CHK: the order is chunked (the
 // directory in s_dyn, see chk_sort): the replay edits the blocks and the scan walks the live chunks, one per round.
@@ -2056,6 +2074,7 @@ __device__ __noinline__ int fast_lane(uint64_t kargs, int32_t LDS* s_dyn_arg, ui
       qw_epoch = S->qw_epoch[lane];
   uint64_t bytes = 0, attempts = 0, scanned = 0, starts = 0, fcyc[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   int pops = 0, memo_pops = 0, handoff = -1, fb = -1, fl_last = -1;
+  int chk_next = U(s_ctl[18]);  // kp_cancel: Queue pops (the Solve's total) at which the flag is read next
   // the NodeClaim this call's last append commit wrote, as it wrote it (the next pod usually starts there: reading
   // its lines back right after the stores waits for them to drain): remaining types, requests, threshold indices
   // (lane values), and its pre-check record. Only the fast lane writes NodeClaims during one call.
@@ -2105,6 +2124,13 @@ if (!FL_NOTIME && tmg) {                                    \
       int off = head - qw_head;
       if (off < 0) off += A->n_pods;
       if (off != qw_next || off >= qw_n) {  // exhausted, or the ring wrapped onto re-pushed entries
+        if (A->cancel && (int)(pops_in + pops + memo_pops) >= chk_next) {  // ctx.Done(): at most every 1024 pops
+          chk_next = (int)(pops_in + pops + memo_pops) + 1024;
+          if (cancel_set(A->cancel)) {
+            s_ctl[19] = 1;
+            break;
+          }
+        }
         qw_head = head;
         qw_n = min(64, len);
         off = 0;
@@ -2151,7 +2177,7 @@ if (!FL_NOTIME && tmg) {                                    \
         own = U((TOPO ? 1 - A->sl_fast_topo[sl] : 0) + (A->hp_any && A->shape_hp_conf[shape] ? 1 : 0));
         ce0 = U(FL_HAS_EX ? A->cur_ex[2 * sl] : 0), ce1 = U(FL_HAS_EX ? A->cur_ex[2 * sl + 1] : 0);
         preq_lane = lane < KP_NRES ? A->shape_requests[(size_t)shape * KP_NRES + lane] : 0;
-        tolmask = U64(A->shape_tolerates[shape]);
+        tolmask = U64(A->shape_tolerates[sl]);
         cur = U(A->cur_nc[2 * sl]), stamp = U(A->cur_nc[2 * sl + 1]);
         READY(preq_lane);
       }
@@ -2162,7 +2188,7 @@ if (!FL_NOTIME && tmg) {                                    \
         pf_own = (TOPO ? 1 - A->sl_fast_topo[nsl] : 0) + (A->hp_any && A->shape_hp_conf[nshape] ? 1 : 0);
         pf_ce0 = FL_HAS_EX ? A->cur_ex[2 * nsl] : 0, pf_ce1 = FL_HAS_EX ? A->cur_ex[2 * nsl + 1] : 0;
         pf_preq = lane < KP_NRES ? A->shape_requests[(size_t)nshape * KP_NRES + lane] : 0;
-        pf_tol = A->shape_tolerates[nshape];
+        pf_tol = A->shape_tolerates[nsl];
         pf_cur = A->cur_nc[2 * nsl], pf_stamp = A->cur_nc[2 * nsl + 1];
         pf_off = off + 1;
       }
@@ -2643,6 +2669,7 @@ if (!FL_NOTIME && tmg) {                                    \
     s_ctl[12] = stk_n;
     s_ctl[13] = stk_t;
     s_ctl[20] = stk_lost;
+    s_ctl[18] = chk_next;
     if (handoff >= 0) {
       s_ctl[6] = handoff;
       s_ctl[26] = 1;
@@ -2785,6 +2812,8 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a0, const Solv
     s_ctl[22] = 0;  // in-flight cursor of the popped pod's shape-level (staged)
     s_ctl[23] = 0;
     s_ctl[26] = 0;  // 1: the fast lane popped s_ctl[6] and hands it to the full path
+    s_ctl[18] = 0;  // kp_cancel: pops at which the flag is read next; [19] 1: the Solve was cancelled
+    s_ctl[19] = 0;
     g_fast.qw_head = 0;  // the fast lane's Queue window (empty) and counters
     g_fast.qw_n = 0;
     g_fast.qw_next = -1;
@@ -2823,8 +2852,14 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a0, const Solv
     if (tid == 0) {
       const int len = s_ctl[1];
       int pod = -1;
+      if (a.cancel && !s_ctl[19] && (int)pops >= s_ctl[18]) {  // ctx.Done(): the flag, at most every 1024 pops
+        s_ctl[18] = (int)pops + 1024;
+        if (cancel_set(a.cancel)) s_ctl[19] = 1;
+      }
       if (pops > pop_cap) {  // runaway guard (a correct Solve stays far below): end the launch, report it
         a.stats[7] = 1;
+      } else if (s_ctl[19]) {  // cancelled: end the launch without placing the rest (the host reports KP_E_CANCELED)
+        a.stats[46] = 1;
       } else if (s_ctl[26]) {  // popped by the fast lane
         pod = s_ctl[6];
         s_ctl[26] = 0;
@@ -2877,7 +2912,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a0, const Solv
     const uint64_t exdS = EX_DIAG ? __builtin_amdgcn_s_memtime() : 0;
     const KReqs* B = &s_B;
     const uint64_t b_negop = a.shape_negop[sl];
-    const uint64_t tolmask = a.shape_tolerates[shape];
+    const uint64_t tolmask = a.shape_tolerates[sl];
     const uint64_t hpc = a.hp_any ? a.shape_hp_conf[shape] : 0, hpa = a.hp_any ? a.shape_hp_add[shape] : 0;
     int placed = -1;  // >= 0 NodeClaim id; <= -2 existing node; -1 not placed
     // a memo hit fails the pod without the scans: the existing and in-flight cursors move to the end as a failed scan
@@ -4185,6 +4220,10 @@ __global__ __launch_bounds__(FEASB_WAVES * 64, FEASB_MINW) void feasibility_bits
 #ifndef FEASQ_SKIP_EVAL
 #define FEASQ_SKIP_EVAL 0  // measurement only: decode + copies, no type-set work (wrong masks)
 #endif
+static_assert(KP_DIAG_BUILD || (FASTLANE == 1 && FL_NOTIME == 1 && FT_FINE == 0 && FAST_SCAN_MAX == 512 &&
+                                 FAST_CHK_LIVE == 8 && SORT_DIAG == 0 && EX_DIAG == 0 && FEAS_MAX_BLOCKS == 65536 &&
+                                 FEASQ_EW == 7 && FEASQ_ROWS == 28 && FEASQ_B128 == 1 && FEASQ_SKIP_EVAL == 0),
+              "the production build carries the production values of every measurement knob");
 __global__ __launch_bounds__(FEASB_WAVES * 64, FEASB_MINW) void feasibility_quad_kernel(FeasArgs a) {
   __shared__ DevDict D;
   __shared__ int64_t s_vint[KP_MAX_BOUND_KEYS * 64];

@@ -135,7 +135,7 @@ __global__ __launch_bounds__(SIM_WAVES * 64) void sim_usable_kernel(SimArgs a) {
     s_allow[wave][lane] = allowed_word(D, rv, v, vint_global(a.vint));
     wave_sync();
     const uint64_t negB = a.shape_negop[sl];
-    const uint64_t tol = a.shape_tolerates[shape];
+    const uint64_t tol = a.shape_tolerates[sl];
     const int e = w * 64 + lane;
     bool ok = e < a.E;
     if (ok) ok = (tol >> a.ex_taintset[e]) & 1;
@@ -194,7 +194,7 @@ __global__ __launch_bounds__(SIM_WAVES * 64) void sim_prep_kernel(SimArgs a) {
     wave_sync();
     SimNC* out = &a.tres[sl];
     const uint64_t negB = a.shape_negop[sl];
-    const uint64_t tol = a.shape_tolerates[shape];
+    const uint64_t tol = a.shape_tolerates[sl];
     int won = -1;
     for (int t = 0; t < a.n_tmpl && won < 0; t++) {
       if (!((tol >> a.tmpl_taintset[t]) & 1)) continue;
@@ -455,7 +455,7 @@ __global__ __launch_bounds__(NW * 64) void sim_kernel(SimArgs a) {
       }
       // addToInflightNode (at most one NodeClaim exists)
       if (placed == -1 && n_nc == 1) {
-        const uint64_t tol = a.shape_tolerates[shape];
+        const uint64_t tol = a.shape_tolerates[sl];
         bool cand = ((tol >> nc->taintset) & 1) && ncfail[sl] != nc->ver && !(nc->hp & hpc);
         if (cand)
           for (int r = 0; r < KP_NRES; r++)

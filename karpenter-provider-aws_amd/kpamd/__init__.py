@@ -70,6 +70,12 @@ def load_lib(path=None):
         "kp_solve_prepare": (C.c_int32, [C.c_void_p, P(abi.SolveIn), P(C.c_void_p)]),
         "kp_solve_prepare_comm": (C.c_int32, [C.c_void_p, P(abi.SolveIn), C.c_void_p, P(C.c_void_p)]),
         "kp_solve_run": (C.c_int32, [C.c_void_p, P(C.c_void_p)]),
+        "kp_solve_run_cancellable": (C.c_int32, [C.c_void_p, C.c_void_p, P(C.c_void_p)]),
+        "kp_solve_cancellable": (C.c_int32, [C.c_void_p, P(abi.SolveIn), C.c_void_p, P(C.c_void_p)]),
+        "kp_cancel_create": (C.c_int32, [C.c_void_p, P(C.c_void_p)]),
+        "kp_cancel_set": (C.c_int32, [C.c_void_p]),
+        "kp_cancel_reset": (C.c_int32, [C.c_void_p]),
+        "kp_cancel_destroy": (None, [C.c_void_p]),
         "kp_solve_refresh": (C.c_int32, [C.c_void_p]),
         "kp_cluster_refresh": (C.c_int32, [C.c_void_p]),
         "kp_solve_plan_destroy": (None, [C.c_void_p]),
@@ -276,6 +282,33 @@ class Scheduler:
         return SolvePlan(self, comm)
 
 
+class Cancel:
+    """kp_cancel: the token a Go shim sets when ctx.Done() fires during a Solve (set() is lock-free, any thread)."""
+
+    def __init__(self, ctx):
+        self.ctx = ctx
+        h = C.c_void_p()
+        _check(ctx.lib, ctx.lib.kp_cancel_create(ctx.h, C.byref(h)))
+        self.h = h
+
+    def set(self):
+        _check(self.ctx.lib, self.ctx.lib.kp_cancel_set(self.h))
+
+    def reset(self):
+        _check(self.ctx.lib, self.ctx.lib.kp_cancel_reset(self.h))
+
+    def close(self):
+        if self.h:
+            self.ctx.lib.kp_cancel_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class SolvePlan:
     def __init__(self, sched, comm=None):
         self.sched = sched
@@ -289,10 +322,14 @@ class SolvePlan:
             _check(lib, lib.kp_solve_prepare_comm(sched.ctx.h, C.byref(si), comm.h, C.byref(h)))
         self.h = h
 
-    def run(self, read=True):
+    def run(self, read=True, cancel=None):
+        """kp_solve_run; with a Cancel token, kp_solve_run_cancellable (KPError KP_E_CANCELED once it is set)."""
         lib = self.sched.ctx.lib
         res = C.c_void_p()
-        _check(lib, lib.kp_solve_run(self.h, C.byref(res)))
+        if cancel is None:
+            _check(lib, lib.kp_solve_run(self.h, C.byref(res)))
+        else:
+            _check(lib, lib.kp_solve_run_cancellable(self.h, cancel.h, C.byref(res)))
         try:
             if read:
                 return read_result(lib, res, self.sched.problem.n_pods)

@@ -9,7 +9,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(HERE)
 
-KP_OK, KP_E_INVAL, KP_E_NOMEM, KP_E_DEVICE, KP_E_UNSUPPORTED, KP_E_NOTFOUND = 0, -1, -2, -3, -4, -5
+KP_OK, KP_E_INVAL, KP_E_NOMEM, KP_E_DEVICE, KP_E_UNSUPPORTED, KP_E_NOTFOUND, KP_E_CANCELED = 0, -1, -2, -3, -4, -5, -6
 NUM_RES = 12
 RES_NAMES = ["cpu", "memory", "ephemeral-storage", "pods", "vpc.amazonaws.com/pod-eni", "vpc.amazonaws.com/efa",
              "nvidia.com/gpu", "amd.com/gpu", "aws.amazon.com/neuron", "aws.amazon.com/neuroncore",

@@ -165,6 +165,10 @@ def ec2_info(arena, row):
     i.ebs_bandwidth_mbps = int(row["ebs_bandwidth"] or 0)
     i.network_bandwidth_mbps = int(row["network_bandwidth"] or 0)
     i.local_nvme_gb = int(row["local_nvme_gb"] or 0)
+    # InstanceStorageInfo.TotalSizeInGB (RAID0 ephemeral storage, any disk type). The reference's offline tables only
+    # carry it for NVMe instance stores (the instance-local-nvme label, R:types.go computeRequirements), so a row
+    # without "instance_storage_gb" falls back to local_nvme_gb; a caller with the full EC2 answer passes both.
+    i.instance_storage_gb = int(row.get("instance_storage_gb") or row["local_nvme_gb"] or 0)
     i.gpu_name = s(row["gpu_name"])
     i.gpu_manufacturer = s(row["gpu_manufacturer"])
     i.gpu_count = row["gpu_count"]

@@ -202,7 +202,7 @@ def config3(catalog, n_pods=100_000, seed=3, n_deployments=1000, n_existing=5000
 
 
 def random_topology_problem(catalog, seed, n_types=80, n_pods=240, n_existing=12, n_shapes=10, n_pools=2,
-                            multi_terms=0.0):
+                            multi_terms=0.0, pns=0.0):
     """Randomized topology-spread scenario: zone / hostname / capacity-type keys, maxSkew 1-3, minDomains,
     ScheduleAnyway (relaxed away), selectors on own / other deployments / nil / expressions, node affinity
     and taint inclusion policies, zone-restricted pools and pods, bound pods seeding the counts.
@@ -279,15 +279,39 @@ def random_topology_problem(catalog, seed, n_types=80, n_pods=240, n_existing=12
             j = int(rng.integers(0, n_shapes))
             bound.append((shapes[j].namespace, dict(shapes[j].labels), e))
     s, c, u = _pods(rng, n_pods, len(shapes))
+    if pns:
+        add_prefer_no_schedule(seed, pools, shapes, existing, pns)
     return Problem([cat], pools, shapes, s, c, u, existing=existing, bound_pods=bound, name=f"random-topology-{seed}")
+
+
+def add_prefer_no_schedule(seed, pools, shapes, nodes, share):
+    """Sprinkle PreferNoSchedule taints over a generated problem (its own rng, so the base scenario is unchanged):
+    a share of the NodePools and existing nodes get a `soft=<name>:PreferNoSchedule` taint (upstream NewScheduler
+    then turns on Preferences.ToleratePreferNoSchedule: pods relax to tolerate them last), and some shapes carry the
+    exact toleration the relaxation would add (no extra level) or a key-specific one."""
+    rng = np.random.default_rng(seed + 7919)
+    for i, p in enumerate(pools):
+        if rng.random() < share:
+            p.taints = list(p.taints or []) + [("soft", f"p{i}", "PreferNoSchedule")]
+    for n in nodes:
+        if rng.random() < share:
+            n.taints = list(n.taints or []) + [("soft", "node", "PreferNoSchedule")]
+    for sh in shapes:
+        u = rng.random()
+        if u < 0.1:
+            sh.tolerations = list(sh.tolerations or []) + [("", "Exists", "", "PreferNoSchedule")]
+        elif u < 0.2:
+            sh.tolerations = list(sh.tolerations or []) + [("soft", "Exists", "", "PreferNoSchedule")]
 
 
 # ------------------------------------------------------------------------------------------------
 # randomized parity scenarios (oracle vs device), small enough for the set-based oracle
 # ------------------------------------------------------------------------------------------------
-def random_problem(catalog, seed, n_types=120, n_pods=300, n_pools=3, n_existing=0, n_shapes=24, n_catalogs=1):
+def random_problem(catalog, seed, n_types=120, n_pods=300, n_pools=3, n_existing=0, n_shapes=24, n_catalogs=1,
+                   pns=0.0):
     """Random scenario. n_catalogs > 1: pool i resolves GetInstanceTypes to catalogue i % n_catalogs, each a
-    different random subset of the docs catalogue (multi-NodeClass clusters)."""
+    different random subset of the docs catalogue (multi-NodeClass clusters). pns: the share of pools and existing
+    nodes with a PreferNoSchedule taint (add_prefer_no_schedule)."""
     rng = np.random.default_rng(seed)
     idx = np.sort(rng.choice(len(catalog), size=min(n_types, len(catalog)), replace=False))
     cat = [catalog[i] for i in idx]
@@ -372,6 +396,8 @@ def random_problem(catalog, seed, n_types=120, n_pods=300, n_pools=3, n_existing
                                      [("dedicated", "team0", "NoSchedule")] if rng.random() < 0.1 else [],
                                      bool(rng.random() < 0.9)))
     s, c, u = _pods(rng, n_pods, len(shapes))
+    if pns:
+        add_prefer_no_schedule(seed, pools, shapes, existing, pns)
     return Problem(cats, pools, shapes, s, c, u, existing=existing, name=f"random-{seed}")
 
 
@@ -512,7 +538,7 @@ def spread_cluster(catalog, n_nodes, seed=4):
     return cl
 
 
-def random_cluster(catalog, seed, n_nodes=60, n_types=80, n_shapes=16, n_pools=2):
+def random_cluster(catalog, seed, n_nodes=60, n_types=80, n_shapes=16, n_pools=2, pns=0.0):
     """Randomized consolidation scenario: pools with taints / daemonsets / minValues, pods with selectors,
     NotIn / Gt affinities and relaxable preferences on keys every node carries, spot and uninitialized
     nodes."""
@@ -588,6 +614,11 @@ def random_cluster(catalog, seed, n_nodes=60, n_types=80, n_shapes=16, n_pools=2
         nodes.append(ClusterNode(ExistingNode(name, labels, avail, {}, list(pool.taints), bool(rng.random() < 0.95)),
                                  0, ti, pods))
     cands = sorted(range(n_nodes), key=lambda i: (len(nodes[i].pods), nodes[i].node.name))
+    if pns:  # (nodes keep their pool's taints; a PreferNoSchedule pool's nodes carry its taint too)
+        add_prefer_no_schedule(seed, pools, shapes, [], pns)
+        for n in nodes:
+            pool = next(p for p in pools if p.name == n.node.labels["karpenter.sh/nodepool"])
+            n.node.taints = list(pool.taints)
     return Cluster([cat], pools, nodes, shapes, np.asarray(pod_shape, dtype=np.uint32),
                    np.asarray(pod_creation, dtype=np.int64), np.asarray(pod_uid, dtype=np.uint64),
                    candidates=cands, name=f"random-cluster-{seed}")

@@ -847,9 +847,16 @@ static Requirements StrictPodRequirements(const PodState& p) {
 }
 
 // Preferences.Relax (UP preferences.go): first applicable of removeRequiredNodeAffinityTerm (only when
-// >1 terms), [pod affinity/anti-affinity: not in the ABI], removePreferredNodeAffinityTerm (heaviest),
-// removeTopologySpreadScheduleAnyway (first ScheduleAnyway constraint, swap-with-last removal).
-static bool Relax(PodState& p) {
+// >1 terms), removePreferredPodAffinityTerm, removePreferredPodAntiAffinityTerm (heaviest first),
+// removePreferredNodeAffinityTerm (heaviest), removeTopologySpreadScheduleAnyway (first ScheduleAnyway
+// constraint, swap-with-last removal), and, only when Preferences.ToleratePreferNoSchedule is set (NewScheduler:
+// some NodePool template taint has effect PreferNoSchedule), toleratePreferNoScheduleTaints.
+// Order of the preferred terms: the docs say "by ascending weight (lowest weight is relaxed first)"
+// (R:website/content/en/preview/concepts/scheduling.md:216); the upstream code sorts them by weight descending
+// and removes element 0, the heaviest. The code is followed: NewPodRequirements applies only the heaviest
+// preferred term as a requirement, so dropping the lightest one first would leave the failing requirement in
+// place and change nothing (DESIGN.md §2 records the conflict).
+static bool Relax(PodState& p, bool toleratePNS) {
   if (p.required_terms.size() > 1) {
     p.required_terms.erase(p.required_terms.begin());
     return true;
@@ -880,6 +887,13 @@ static bool Relax(PodState& p) {
       p.spreads.pop_back();
       return true;
     }
+  if (toleratePNS) {  // toleratePreferNoScheduleTaints: {Operator: Exists, Effect: PreferNoSchedule}
+    for (auto& t : p.tolerations)  // corev1 Toleration.MatchToleration: key, operator, value, effect all equal
+      if (t.key.empty() && t.value.empty() && t.op == KP_TOL_EXISTS && t.effect == KP_EFFECT_PREFER_NO_SCHEDULE)
+        return false;
+    p.tolerations.push_back({"", "", KP_TOL_EXISTS, KP_EFFECT_PREFER_NO_SCHEDULE});
+    return true;
+  }
   return false;
 }
 
@@ -1541,6 +1555,11 @@ static int32_t SolveCore(const Catalogs& cats, const kp_solve_in* in, kpo_result
   const NamespaceList nsl = NamespacesFromABI(in->namespaces, in->n_namespaces);
   auto t0 = std::chrono::steady_clock::now();
   Scheduler s;
+  // NewScheduler: Preferences.ToleratePreferNoSchedule when any NodePool template taint has that effect
+  bool toleratePNS = false;
+  for (uint32_t i = 0; i < in->n_nodepools; i++)
+    for (uint32_t j = 0; j < in->nodepools[i].n_taints; j++)
+      toleratePNS = toleratePNS || in->nodepools[i].taints[j].effect == KP_EFFECT_PREFER_NO_SCHEDULE;
   // NewScheduler: templates per NodePool ordered by weight desc, name asc; options pre-filtered by the
   // template requirements with empty requests.
   std::vector<int> order(in->n_nodepools);
@@ -1764,7 +1783,7 @@ static int32_t SolveCore(const Catalogs& cats, const kp_solve_in* in, kpo_result
     errored[pi] = 1;
     // a ReservedOfferingError is not relaxed: the pod waits for capacity another NodeClaim may release
     if (s.anyReservedErr) s.counters.reserved_errors++;
-    bool relaxed = !s.anyReservedErr && Relax(p);
+    bool relaxed = !s.anyReservedErr && Relax(p, toleratePNS);
     queue.push_back(pi);
     if (relaxed) {
       lastLen.clear();

@@ -23,7 +23,7 @@ def test_all_declared_symbols_exported():
 
 def test_abi_version_and_struct_sizes():
     lib = kpamd.load_lib()
-    assert lib.kp_abi_version() == 10
+    assert lib.kp_abi_version() == 11
     from kpamd import abi
     assert C.sizeof(abi.ResourceList) == 12 * 8 + 8
     assert C.sizeof(abi.Offering) == 5 * 8 + 8 + 8

@@ -21,11 +21,11 @@ GI = 1 << 30
 EPH = "ephemeral-storage"
 
 
-def _resolve(lib, name, family="AL2023", bdms=None, policy=None):
+def _resolve(lib, name, family="AL2023", bdms=None, policy=None, row_update=None):
     rows = {r["name"]: r for r in catalog.load_ec2_table()}
     arena = abi.Arena()
     opts = catalog.default_options()
-    info = catalog.ec2_info(arena, rows[name])
+    info = catalog.ec2_info(arena, dict(rows[name], **(row_update or {})))
     nc = catalog.nodeclass(arena, ami_family=family, block_device_mappings=bdms, instance_store_policy=policy)
     cap, total = abi.ResourceList(), abi.ResourceList()
     assert lib.kp_instance_type_resolve(C.byref(opts), C.byref(info), C.byref(nc), C.byref(cap), C.byref(total)) == 0
@@ -101,3 +101,14 @@ def test_raid0_scenario(request, lib, backend, policy):
         return
     assert pod_node == [0] and nodes[0]["type"] == "m6idn.32xlarge"
     assert next(t for t in types if t.name == "m6idn.32xlarge").capacity[EPH] == 7600 * 10**9 * 1000
+
+
+def test_raid0_non_nvme_instance_store(lib):
+    """RAID0 reads InstanceStorageInfo.TotalSizeInGB whatever the disk type. The reference's offline tables hold the
+    total only for NVMe stores (instance-local-nvme), so the catalogue builder falls back to that; an EC2 answer for a
+    non-NVMe store (no local-NVMe label, a total given) is used as is. NVMe: m6idn.32xlarge 7600G; a synthetic
+    non-NVMe row: m5.large given a 6000 GB store and no NVMe label."""
+    assert _resolve(lib, "m6idn.32xlarge", policy="RAID0", row_update={"instance_storage_gb": 7600})[0] == 7600 * 10**9
+    non_nvme = {"instance_storage_gb": 6000, "local_nvme_gb": 0}
+    assert _resolve(lib, "m5.large", policy="RAID0", row_update=non_nvme)[0] == 6000 * 10**9
+    assert _resolve(lib, "m5.large", row_update=non_nvme)[0] == 20 * GI  # no policy: the EBS default
