@@ -583,6 +583,16 @@ typedef struct kp_filter_plan kp_filter_plan;
 int32_t kp_filter_prepare(kp_ctx* ctx, const kp_catalog* cat, const kp_feasibility_query* queries, uint32_t n_queries,
                           int32_t with_cheapest, kp_filter_plan** out);
 int32_t kp_filter_run(kp_filter_plan* plan, uint64_t* out_mask, double* out_cheapest, kp_solve_stats* stats);
+/* ABI v11, the compact result (prepare with with_cheapest = KP_FILTER_COMPACT): per query the mask and the set of
+ * offering classes its requirements admit (out_classes[q], bit c = class c of kp_filter_class_prices), instead of n_types
+ * prices. The cheapest compatible available offering price of type t for query q is then
+ *   min over c in out_classes[q] of prices[c * n_types + t]   (+inf: none)
+ * which equals kp_filter_run's out_cheapest bit for bit: a class's price row is the cheapest available offering of
+ * the type in that class. kp_filter_class_prices copies the plan's resident [C][n_types] table (C <= 64 classes) and
+ * its class count; the consumer reads it once per catalogue seqnum, not per query. */
+enum { KP_FILTER_MASK_ONLY = 0, KP_FILTER_CHEAPEST = 1, KP_FILTER_COMPACT = 2 };
+int32_t kp_filter_run_compact(kp_filter_plan* plan, uint64_t* out_mask, uint64_t* out_classes, kp_solve_stats* stats);
+int32_t kp_filter_class_prices(kp_filter_plan* plan, double* out, uint32_t capacity, uint32_t* n_classes);
 void kp_filter_plan_destroy(kp_filter_plan* plan);
 /* Re-apply the catalogue's current offerings to a prepared plan: only the offering section of the resident
  * catalogue (available-class masks, per-(type, class) prices; ~C*T*16 bytes) is rebuilt and copied to the

@@ -251,6 +251,7 @@ struct FeasArgs {
   int32_t blocks;            // its grid (rows are strided over the waves)
   int32_t one_row;           // 1: feasibility_bits_kernel at any T (its cross-check, KP_FEAS_ONE_ROW)
   int32_t ch_stride;         // doubles per out_cheapest row: T rounded up to whole 128-byte lines (rows start aligned)
+  uint64_t* out_classes;     // [Q] compact result: the row's compatible offering classes (kp_filter_run_compact), or null
 };
 
 // ---- launch-side selection (kp_launch_select) ------------------------------------------------------

@@ -3848,7 +3848,8 @@ struct kp_filter_plan {
   FeasArgs fa;
   uint32_t n_queries = 0;
   int T = 0;
-  size_t tiles = 0, o_mask = 0, o_ch = 0;
+  size_t tiles = 0, o_mask = 0, o_ch = 0, o_cls = 0;
+  bool compact = false;  // KP_FILTER_COMPACT: classes per row instead of the cheapest-price rows
   int ch_stride = 0;  // doubles per device cheapest-price row (whole 128-byte lines; the caller's rows are T long)
   bool cheapest = false;
   double prepare_ms = 0;
@@ -3866,10 +3867,15 @@ int32_t kp_filter_prepare(kp_ctx* ctx, const kp_catalog* cat, const kp_feasibili
                           int32_t with_cheapest, kp_filter_plan** out) {
   auto t0 = std::chrono::steady_clock::now();
   if (!ctx || !cat || (!queries && n_queries) || !out) return fail(KP_E_INVAL, "null argument");
+  if (with_cheapest < KP_FILTER_MASK_ONLY || with_cheapest > KP_FILTER_COMPACT)
+    return fail(KP_E_INVAL, "with_cheapest %d", with_cheapest);
+  const bool compact = with_cheapest == KP_FILTER_COMPACT;
+  if (compact) with_cheapest = 0;  // (no price rows: the classes and the resident class prices instead)
   std::lock_guard<std::recursive_mutex> lock(ctx->mu);
   HIPCHK(hipSetDevice(ctx->device));
   auto plan = std::make_unique<kp_filter_plan>();
   plan->ctx = ctx;
+  plan->compact = compact;
   Compiled cp;
   vector<RawReqs> qs(n_queries);
   for (uint32_t i = 0; i < n_queries; i++) qs[i] = ParseReqs(queries[i].requirements);
@@ -3894,6 +3900,7 @@ int32_t kp_filter_prepare(kp_ctx* ctx, const kp_catalog* cat, const kp_feasibili
   plan->o_mask = blob.reserve(sizeof(uint64_t) * std::max<size_t>(1, n_queries * tiles));
   plan->ch_stride = (T + 15) & ~15;
   plan->o_ch = with_cheapest ? blob.reserve(sizeof(double) * std::max<size_t>(1, (size_t)n_queries * plan->ch_stride)) : 0;
+  plan->o_cls = compact ? blob.reserve(sizeof(uint64_t) * std::max<size_t>(1, n_queries)) : 0;
   HIPCHK(hipMalloc(&plan->buf.p, blob.host.size()));
   uint8_t* base = (uint8_t*)plan->buf.p;
   vector<DevCatalog> dc = DevCats(base, cp, coffs);
@@ -3912,6 +3919,7 @@ int32_t kp_filter_prepare(kp_ctx* ctx, const kp_catalog* cat, const kp_feasibili
   fa.q_requests = (const int64_t*)(base + o_qr);
   fa.out_mask = (uint64_t*)(base + plan->o_mask);
   fa.out_cheapest = with_cheapest ? (double*)(base + plan->o_ch) : nullptr;
+  fa.out_classes = compact ? (uint64_t*)(base + plan->o_cls) : nullptr;
   fa.ch_stride = plan->ch_stride;
   // the bitset kernel (KP_FEAS_GLOBAL: the per-type global-gather kernel, kept as its cross-check)
   fa.bits = getenv("KP_FEAS_GLOBAL") ? 0 : 1;
@@ -3965,6 +3973,37 @@ int32_t kp_filter_run(kp_filter_plan* plan, uint64_t* out_mask, double* out_chea
     stats->prepare_ms = plan->prepare_ms;
     stats->host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   }
+  return KP_OK;
+}
+
+// The compact result: the same launch, the rows' class sets copied out instead of the price rows.
+int32_t kp_filter_run_compact(kp_filter_plan* plan, uint64_t* out_mask, uint64_t* out_classes, kp_solve_stats* stats) {
+  if (!plan) return fail(KP_E_INVAL, "null argument");
+  if (out_classes && !plan->compact) return fail(KP_E_INVAL, "plan was not prepared with KP_FILTER_COMPACT");
+  int32_t rc = kp_filter_run(plan, out_mask, nullptr, stats);
+  if (rc || !out_classes || !plan->n_queries) return rc;
+  kp_ctx* ctx = plan->ctx;
+  std::lock_guard<std::recursive_mutex> lock(ctx->mu);
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipMemcpyAsync(out_classes, (uint8_t*)plan->buf.p + plan->o_cls, sizeof(uint64_t) * plan->n_queries,
+                        hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return KP_OK;
+}
+
+// The per-(class, type) cheapest available offering prices the compact result indexes (class-major, +inf: none),
+// as the plan's resident catalogue holds them (kp_filter_refresh keeps them current).
+int32_t kp_filter_class_prices(kp_filter_plan* plan, double* out, uint32_t capacity, uint32_t* n_classes) {
+  if (!plan || !n_classes) return fail(KP_E_INVAL, "null argument");
+  std::lock_guard<std::recursive_mutex> lock(plan->ctx->mu);
+  if (int32_t rc = CatalogsAlive({plan->alive})) return rc;
+  const HostCat& hc = plan->cp.B->cats[0];
+  const int C = plan->cp.B->C, T = plan->T;
+  *n_classes = (uint32_t)C;
+  if (!out) return KP_OK;
+  if ((size_t)capacity < (size_t)C * T) return fail(KP_E_INVAL, "capacity %u < %d classes x %d types", capacity, C, T);
+  for (int c = 0; c < C; c++)
+    for (int t = 0; t < T; t++) out[(size_t)c * T + t] = hc.price_cm[(size_t)c * hc.S + t];
   return KP_OK;
 }
 

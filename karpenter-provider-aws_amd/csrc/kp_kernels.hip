@@ -1972,7 +1972,7 @@ __device__ int chk_sort(const ChkDir& d, ChkCtl LDS* C, ChkBlk* B, int n, int mu
 // instead of inheriting the full path's pressure (whose spills and copies dominated the per-pod instruction count).
 #define KARG __attribute__((address_space(4)))
 __shared__ DevDict g_D;
-__shared__ int32_t g_ctl[32];
+__shared__ int32_t g_ctl[34];  // [32] kp_cancel: pops at the next flag read, [33] 1: cancelled
 __shared__ int32_t g_stk[2][2 * MSTK_CAP];  // mutation stacks: [0] in-flight positions, [1] existing positions
 __shared__ int64_t g_fitv[FITV_RES * FITV_CAP];  // Fits threshold values of catalogue 0 (CatHdr.fit_slot rows)
 __shared__ CatHdr g_hdr[8];                      // catalogue descriptors 0..7
@@ -2074,7 +2074,7 @@ __device__ __noinline__ int fast_lane(uint64_t kargs, int32_t LDS* s_dyn_arg, ui
       qw_epoch = S->qw_epoch[lane];
   uint64_t bytes = 0, attempts = 0, scanned = 0, starts = 0, fcyc[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   int pops = 0, memo_pops = 0, handoff = -1, fb = -1, fl_last = -1;
-  int chk_next = U(s_ctl[18]);  // kp_cancel: Queue pops (the Solve's total) at which the flag is read next
+  int chk_next = U(s_ctl[32]);  // kp_cancel: Queue pops (the Solve's total) at which the flag is read next
   // the NodeClaim this call's last append commit wrote, as it wrote it (the next pod usually starts there: reading
   // its lines back right after the stores waits for them to drain): remaining types, requests, threshold indices
   // (lane values), and its pre-check record. Only the fast lane writes NodeClaims during one call.
@@ -2127,7 +2127,7 @@ if (!FL_NOTIME && tmg) {                                    \
         if (A->cancel && (int)(pops_in + pops + memo_pops) >= chk_next) {  // ctx.Done(): at most every 1024 pops
           chk_next = (int)(pops_in + pops + memo_pops) + 1024;
           if (cancel_set(A->cancel)) {
-            s_ctl[19] = 1;
+            s_ctl[33] = 1;
             break;
           }
         }
@@ -2669,7 +2669,7 @@ if (!FL_NOTIME && tmg) {                                    \
     s_ctl[12] = stk_n;
     s_ctl[13] = stk_t;
     s_ctl[20] = stk_lost;
-    s_ctl[18] = chk_next;
+    s_ctl[32] = chk_next;
     if (handoff >= 0) {
       s_ctl[6] = handoff;
       s_ctl[26] = 1;
@@ -2708,7 +2708,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a0, const Solv
   __shared__ WaveSlots slots[NW];
   __shared__ int32_t s_ok[NW];
   __shared__ int32_t s_wcnt[4 * NW];
-  int32_t (&s_ctl)[32] = g_ctl;
+  int32_t (&s_ctl)[34] = g_ctl;
   auto& s_stk = g_stk;  // mutation stacks: [0] in-flight positions, [1] existing positions
   __shared__ int32_t s_list[4 * NT];
   __shared__ uint32_t s_scratch[NW][2 * KP_MAX_WORDS];
@@ -2812,8 +2812,8 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a0, const Solv
     s_ctl[22] = 0;  // in-flight cursor of the popped pod's shape-level (staged)
     s_ctl[23] = 0;
     s_ctl[26] = 0;  // 1: the fast lane popped s_ctl[6] and hands it to the full path
-    s_ctl[18] = 0;  // kp_cancel: pops at which the flag is read next; [19] 1: the Solve was cancelled
-    s_ctl[19] = 0;
+    s_ctl[32] = 0;  // kp_cancel: pops at which the flag is read next; [33] 1: the Solve was cancelled
+    s_ctl[33] = 0;
     g_fast.qw_head = 0;  // the fast lane's Queue window (empty) and counters
     g_fast.qw_n = 0;
     g_fast.qw_next = -1;
@@ -2852,13 +2852,13 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a0, const Solv
     if (tid == 0) {
       const int len = s_ctl[1];
       int pod = -1;
-      if (a.cancel && !s_ctl[19] && (int)pops >= s_ctl[18]) {  // ctx.Done(): the flag, at most every 1024 pops
-        s_ctl[18] = (int)pops + 1024;
-        if (cancel_set(a.cancel)) s_ctl[19] = 1;
+      if (a.cancel && !s_ctl[33] && (int)pops >= s_ctl[32]) {  // ctx.Done(): the flag, at most every 1024 pops
+        s_ctl[32] = (int)pops + 1024;
+        if (cancel_set(a.cancel)) s_ctl[33] = 1;
       }
       if (pops > pop_cap) {  // runaway guard (a correct Solve stays far below): end the launch, report it
         a.stats[7] = 1;
-      } else if (s_ctl[19]) {  // cancelled: end the launch without placing the rest (the host reports KP_E_CANCELED)
+      } else if (s_ctl[33]) {  // cancelled: end the launch without placing the rest (the host reports KP_E_CANCELED)
         a.stats[46] = 1;
       } else if (s_ctl[26]) {  // popped by the fast lane
         pod = s_ctl[6];
@@ -3910,6 +3910,7 @@ __global__ __launch_bounds__(FEAS_WAVES * 64) void feasibility_kernel(FeasArgs a
     const uint64_t negQ = negop_mask(rv.present, rv.compl_, rv.nz);
     const uint64_t allowed = allowed_word(D, rv, v, vint_global(a.vint));
     const uint64_t cls = allowed_classes<true>(D, Cg.cls, rv, allowed, negQ);
+    if (a.out_classes && lane == 0) a.out_classes[q] = cls;
     s_allowed[wave][lane] = allowed;
     const uint32_t rmask = (uint32_t)__ballot(rq_lane > 0);
     wave_sync();
@@ -4108,6 +4109,7 @@ __global__ __launch_bounds__(FEASB_WAVES * 64, FEASB_MINW) void feasibility_bits
                                             : v;
     }
     const uint64_t cls = allowed_classes<true>(D, (const OfferClass LDS*)s_cls, rv, allowed, negQ);
+    if (a.out_classes && lane == 0) a.out_classes[q] = cls;
     // cheapest compatible available offering price per type
     auto cheapest_row = [&]() {
       if (!a.out_cheapest) return;
@@ -4406,6 +4408,7 @@ __global__ __launch_bounds__(FEASB_WAVES * 64, FEASB_MINW) void feasibility_quad
                                               : v;
       }
       const uint64_t cls = allowed_classes<true>(D, (const OfferClass LDS*)s_cls, rv, allowed, negQ);
+      if (lane == 0 && a.out_classes) a.out_classes[q] = cls;  // the compact result
       if (lane == 0) {  // published to the copy waves (LDS writes complete in order: the classes before the flag;
                         // a relaxed workgroup-scope flag keeps this wave's vector-memory queue undrained)
         s_rcls[q - row0] = cls;

@@ -54,6 +54,8 @@ def load_lib(path=None):
         "kp_filter_prepare": (C.c_int32, [C.c_void_p, C.c_void_p, P(abi.FeasibilityQuery), C.c_uint32, C.c_int32,
                                           P(C.c_void_p)]),
         "kp_filter_run": (C.c_int32, [C.c_void_p, P(C.c_uint64), P(C.c_double), P(abi.SolveStats)]),
+        "kp_filter_run_compact": (C.c_int32, [C.c_void_p, P(C.c_uint64), P(C.c_uint64), P(abi.SolveStats)]),
+        "kp_filter_class_prices": (C.c_int32, [C.c_void_p, P(C.c_double), C.c_uint32, P(C.c_uint32)]),
         "kp_filter_plan_destroy": (None, [C.c_void_p]),
         "kp_filter_refresh": (C.c_int32, [C.c_void_p, C.c_void_p]),
         "kp_launch_refresh": (C.c_int32, [C.c_void_p, C.c_void_p]),
@@ -377,15 +379,17 @@ class FilterPlan:
     """kp_filter_prepare / kp_filter_run: CompatibleAvailableFilter rows resident on the device."""
 
     def __init__(self, ctx, catalog, queries, cheapest=True):
+        """cheapest: True (KP_FILTER_CHEAPEST: a price row per query), False (mask only) or "compact"
+        (KP_FILTER_COMPACT: the query's compatible offering classes; prices via class_prices())."""
         self.ctx = ctx
         self.T = len(catalog.instance_types)
         self.n = len(queries)
+        mode = 2 if cheapest == "compact" else (1 if cheapest else 0)
         arena = Arena()
         qs = arena.arr(abi.FeasibilityQuery, [abi.FeasibilityQuery(arena.requirements(r), arena.resources(q))
                                               for r, q in queries])
         h = C.c_void_p()
-        _check(ctx.lib, ctx.lib.kp_filter_prepare(ctx.h, catalog.h, qs, len(queries), 1 if cheapest else 0,
-                                                  C.byref(h)))
+        _check(ctx.lib, ctx.lib.kp_filter_prepare(ctx.h, catalog.h, qs, len(queries), mode, C.byref(h)))
         self.h = h
 
     def run(self, read=False):
@@ -402,6 +406,40 @@ class FilterPlan:
                                       cheapest.ctypes.data_as(C.POINTER(C.c_double)), C.byref(st)))
         bits = np.unpackbits(mask[:self.n * tiles].view(np.uint8), bitorder="little").reshape(self.n, tiles * 64)
         return bits[:, :self.T].astype(bool), cheapest[:self.n * self.T].reshape(self.n, self.T), stats_dict(st)
+
+    def run_compact(self, read=True):
+        """kp_filter_run_compact: (kept bool[Q,T], classes uint64[Q], stats); read=False: stats only."""
+        st = abi.SolveStats()
+        lib = self.ctx.lib
+        if not read:
+            _check(lib, lib.kp_filter_run_compact(self.h, None, None, C.byref(st)))
+            return stats_dict(st)
+        tiles = (self.T + 63) // 64
+        mask = np.zeros(max(1, self.n * tiles), dtype=np.uint64)
+        cls = np.zeros(max(1, self.n), dtype=np.uint64)
+        _check(lib, lib.kp_filter_run_compact(self.h, mask.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                              cls.ctypes.data_as(C.POINTER(C.c_uint64)), C.byref(st)))
+        bits = np.unpackbits(mask[:self.n * tiles].view(np.uint8), bitorder="little").reshape(self.n, tiles * 64)
+        return bits[:, :self.T].astype(bool), cls[:self.n], stats_dict(st)
+
+    def class_prices(self):
+        """kp_filter_class_prices: float64[C, T], the cheapest available offering of each type per offering class."""
+        lib = self.ctx.lib
+        n = C.c_uint32()
+        _check(lib, lib.kp_filter_class_prices(self.h, None, 0, C.byref(n)))
+        out = np.zeros(max(1, n.value * self.T), dtype=np.float64)
+        _check(lib, lib.kp_filter_class_prices(self.h, out.ctypes.data_as(C.POINTER(C.c_double)), out.size,
+                                               C.byref(n)))
+        return out[:n.value * self.T].reshape(n.value, self.T)
+
+    @staticmethod
+    def cheapest_from_compact(classes, class_prices):
+        """min over the row's classes of the class price rows (+inf: none) = kp_filter_run's out_cheapest."""
+        out = np.full((len(classes), class_prices.shape[1]), np.inf)
+        for c in range(class_prices.shape[0]):
+            sel = ((classes >> np.uint64(c)) & np.uint64(1)).astype(bool)
+            out[sel] = np.minimum(out[sel], class_prices[c])
+        return out
 
     def refresh(self, catalog):
         """kp_filter_refresh: re-apply the catalogue's current offerings (ICE / price) to the resident plan."""

@@ -18,6 +18,8 @@
   general-2000    the bench's general-path leg: computeConsolidation on the 2,000-node spread cluster
                   (synth.spread_cluster: every other shape zone-spread) for the 100 firstNConsolidationOption prefixes
                   and 200 random subsets of 2..20 candidates (synth.consolidation_subsets seed 5), every decision field
+  general-10000   the general path at config 4's size: the 10,000-node spread cluster, the 100 prefixes and 200
+                  random subsets of 2..100 candidates (seed 6), every decision field (4 oracle processes, ~4 minutes)
 
 Run from the repo root: python tests/golden/make_fullsize_digests.py [name ...]  (all: about 8 minutes); names given
 regenerate only those entries.
@@ -73,6 +75,24 @@ def general_subsets(cl):
     return pre, rnd
 
 
+def general10k_subsets(cl):
+    import numpy as np
+    from kpamd import disruption, synth
+    cands = np.asarray(cl.candidates, dtype=np.uint32)
+    pre = [[int(x) for x in cands[:m + 1]] for m in disruption.MultiNodeConsolidation.search_prefixes(len(cands))]
+    rnd = [[int(x) for x in s] for s in synth.consolidation_subsets(cl, 200, seed=6, max_size=100, prefixes=False)]
+    return pre, rnd
+
+
+def _general10k_worker(subs):
+    import kpamd
+    from kpamd import catalog, synth
+    from oracle import pyoracle
+    cl = synth.spread_cluster(catalog.build_catalog(kpamd.load_lib()), 10_000)
+    res, _ = pyoracle.simulate_batch(cl, subs)
+    return [sim_record(r) for r in res]
+
+
 def _solves():
     from kpamd import synth
     return {"config2-50000": lambda cat: synth.config2(cat, n_pods=50_000, seed=2),
@@ -105,6 +125,20 @@ def main():
         out["general-2000"] = {"prefixes": [sim_record(r) for r in res[:len(pre)]],
                                "random": [sim_record(r) for r in res[len(pre):]]}
         print("general-2000", len(res), f"{time.time() - t:.1f}s", flush=True)
+    if "general-10000" in only:  # (on request: minutes of oracle time)
+        import multiprocessing as mp
+        t = time.time()
+        cl = synth.spread_cluster(cat, 10_000)
+        pre, rnd = general10k_subsets(cl)
+        allsubs = pre + rnd
+        parts = [allsubs[i::4] for i in range(4)]
+        with mp.get_context("spawn").Pool(4) as pool:
+            outs = pool.map(_general10k_worker, parts)
+        recs = [None] * len(allsubs)
+        for i, o in enumerate(outs):
+            recs[i::4] = o
+        out["general-10000"] = {"prefixes": recs[:len(pre)], "random": recs[len(pre):]}
+        print("general-10000", len(recs), f"{time.time() - t:.1f}s", flush=True)
     if only and "config4-10000" not in only:
         json.dump(out, open(OUT, "w"), indent=0)
         return

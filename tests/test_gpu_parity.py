@@ -206,3 +206,36 @@ def test_config2_burst(ctx, catalog, n_pods):
     from kpamd import synth
     got, want = run_both(ctx, synth.config2(catalog, n_pods=n_pods, seed=5, burst=True))
     check_same(got, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kernel_env", [{}, {"KP_FEAS_ONE_ROW": "1"}, {"KP_FEAS_GLOBAL": "1"}])
+def test_filter_compact_equals_expanded(ctx, catalog, monkeypatch, kernel_env):
+    """KP_FILTER_COMPACT (ABI v11): the mask and each row's compatible offering classes; min over those classes of
+    kp_filter_class_prices equals kp_filter_run's cheapest-price rows bit for bit, on every kernel (quad, one-row,
+    per-type), including after an ICE refresh (R:pkg/providers/instance/filter/filter.go:39-64)."""
+    import copy
+    import kpamd
+    from kpamd import synth
+    for k, v in kernel_env.items():
+        monkeypatch.setenv(k, v)
+    queries = synth.distinct_queries(catalog, 1001)
+    its = copy.deepcopy(catalog)
+    cat = kpamd.Catalog(ctx, its, seqnum=1)
+    fe = kpamd.FilterPlan(ctx, cat, queries, cheapest=True)
+    fc = kpamd.FilterPlan(ctx, cat, queries, cheapest="compact")
+    for step in range(2):
+        k1, c1, _ = fe.run(read=True)
+        k2, cls, _ = fc.run_compact(read=True)
+        assert (k1 == k2).all()
+        c2 = kpamd.FilterPlan.cheapest_from_compact(cls, fc.class_prices())
+        np.testing.assert_array_equal(c1[k1], c2[k1])
+        if step == 0:  # ICE marks: both plans refreshed in place
+            cat.update_offerings([(t, "spot", "test-zone-1a", False) for t in range(0, len(catalog), 3)], seqnum=2)
+            fe.refresh(cat)
+            fc.refresh(cat)
+    with pytest.raises(kpamd.KPError):
+        fe.run_compact(read=True)  # prepared without KP_FILTER_COMPACT
+    fe.close()
+    fc.close()
+    cat.close()
