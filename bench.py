@@ -47,8 +47,9 @@ def main():
     ap.add_argument("--subsets", type=int, default=1_000_000)
     ap.add_argument("--cpu-sample-sims", type=int, default=16)
     ap.add_argument("--no-consolidation", action="store_true")
-    ap.add_argument("--general-nodes", type=int, default=2_000)
-    ap.add_argument("--general-subsets", type=int, default=200)
+    ap.add_argument("--general-nodes", type=int, default=10_000)
+    ap.add_argument("--general-subsets", type=int, default=100_000)
+    ap.add_argument("--general-max-size", type=int, default=100)
     ap.add_argument("--only-general", action="store_true", help="the topology-cluster consolidation leg alone")
     ap.add_argument("--c3-pods", type=int, default=100_000)
     ap.add_argument("--c5-pods", type=int, default=1_000_000)
@@ -175,6 +176,7 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = _cpu_baseline(cat, args.cpu_sample_pods)
+        _attach_full_size(line["cpu_baseline"], "config2")
     def progress(msg):  # stderr progress per leg (rank 0): long runs keep writing
         if rank == 0:
             print(f"[bench] {msg} ({time.perf_counter() - t_start:.1f} s)", file=sys.stderr, flush=True)
@@ -256,7 +258,25 @@ def _solve_leg(name, prob, ctx, barrier, max_over_ranks, world, steps, warmup, k
            "workload": prob.name}
     if cpu is not None:
         out["cpu_baseline"] = _cpu_baseline_cfg(cpu[0], cpu[1])
+        _attach_full_size(out["cpu_baseline"], {"3": "config3", "5": "config5"}.get(cpu[0]), prob.n_pods)
     return out
+
+
+def _attach_full_size(cb, name, n_pods=None):
+    """The oracle timed on the whole config (tools/cpu_fullsize.py -> profiles/r05/cpu_fullsize.json, committed: the
+    full-size runs take minutes to an hour, too long for the bench), beside the bounded sample timed live. The
+    sample's rate overstates the CPU where per-pod work grows with the Solve (more NodeClaims to scan)."""
+    if not name:
+        return
+    try:
+        rec = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r05",
+                                          "cpu_fullsize.json"))).get(name)
+    except (OSError, ValueError):
+        rec = None
+    if rec and (n_pods is None or rec["pods"] == n_pods):
+        cb["full_size"] = {"value": rec["pods_per_s"], "unit": "pods/s", "pods": rec["pods"], "seconds": rec["seconds"],
+                           "cores": rec["threads"], "kind": "port",
+                           "machine": f"{rec['cpu']} ({rec['host']}): this build's container, not the GPU box"}
 
 
 def _cpu_baseline_cfg(cfg, n):
@@ -452,10 +472,11 @@ def _consolidation(args, cat, ctx, dist, rank, world, barrier, kcomm):
 
 
 def _consolidation_general(args, cat, ctx, rank, world, barrier):
-    """Consolidation on a topology-spread cluster (the general simulation path): the 100
-    firstNConsolidationOption prefixes plus random subsets of 2..20 candidates through kp_consolidate_argmin, rank 0
-    only (each batch of subsets is one solve_kernel launch over overlays on the resident superset Solve: no sharding
-    claimed). Reported with and without kp_cluster_prepare."""
+    """Consolidation on a topology-spread cluster (the general simulation path) at config 4's size: a
+    10k-node cluster whose every other shape is zone-spread, the 100 firstNConsolidationOption prefixes plus 100k random
+    subsets of 2..100 candidates through kp_consolidate_argmin, rank 0 only (each launch of up to 4096 subsets is one
+    solve_kernel grid over overlays on the resident superset Solve, two launch slots so the host overlays of one
+    overlap the device time of the other; no sharding claimed). Reported with and without kp_cluster_prepare."""
     import numpy as np
     import kpamd
     from kpamd import disruption, synth
@@ -466,7 +487,7 @@ def _consolidation_general(args, cat, ctx, rank, world, barrier):
     cands = np.asarray(cl.candidates, dtype=np.uint32)
     mids = disruption.MultiNodeConsolidation.search_prefixes(len(cands))
     subs = [list(cands[:m + 1]) for m in mids]
-    subs += synth.consolidation_subsets(cl, args.general_subsets, seed=5, max_size=20, prefixes=False)
+    subs += synth.consolidation_subsets(cl, args.general_subsets, seed=6, max_size=args.general_max_size, prefixes=False)
     offs = np.zeros(len(subs) + 1, dtype=np.uint32)
     offs[1:] = np.cumsum([len(x) for x in subs])
     flat = np.concatenate([np.asarray(x, dtype=np.uint32) for x in subs])
@@ -488,7 +509,7 @@ def _consolidation_general(args, cat, ctx, rank, world, barrier):
            "decisions": {"noop": choice["counts"][0], "delete": choice["counts"][1], "replace": choice["counts"][2]},
            "workload": f"config4 variant: {args.general_nodes} nodes ({len(cl.pod_shape)} pods), every other shape "
                        f"zone-spread (maxSkew 1, DoNotSchedule); {len(mids)} firstNConsolidationOption prefixes + "
-                       f"{args.general_subsets} random subsets of 2..20 candidates; each simulation a whole Solve on the "
+                       f"{args.general_subsets} random subsets of 2..{args.general_max_size} candidates; each simulation a whole Solve on the "
                        f"device (host compile + solve_kernel + finalize_kernel), decision on the host"}
     if world == 1 and not args.no_cpu_baseline:
         from oracle import pyoracle

@@ -5294,6 +5294,47 @@ static int32_t GeneralSimOne(kp_cluster_plan* plan, const vector<uint32_t>& cand
 //     pods), and hostname groups that stop being live at creation get their unregistered nodes (255) back.
 // Subsets whose removal would make an inverse anti-affinity group vanish take the per-subset compile. Every
 // simulation of a batch is one workgroup of one solve_kernel launch (its own arena: mutable state + scratch).
+// Host memory the device copies read from / write into while the host prepares the next launch (pinned: an async
+// copy from pageable memory would stage synchronously), grown geometrically.
+struct PinnedBuf {
+  void* p = nullptr;
+  size_t n = 0;
+  PinnedBuf() = default;
+  PinnedBuf(const PinnedBuf&) = delete;
+  PinnedBuf& operator=(const PinnedBuf&) = delete;
+  ~PinnedBuf() {
+    if (p) (void)hipHostFree(p);
+  }
+  hipError_t reserve(size_t bytes) {
+    if (bytes <= n) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    n = 0;
+    const size_t want = std::max(bytes, (size_t)(1.5 * (double)bytes));
+    const hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    if (e == hipSuccess) n = want;
+    else p = nullptr;
+    return e;
+  }
+  uint8_t* at(size_t off) const { return (uint8_t*)p + off; }
+};
+
+// One launch slot of the general batch: device arenas + argument blocks, the pinned host copies its launch reads
+// (overlays, arguments) and writes (results), and the event that marks its results landed.
+struct GenSlot {
+  DevBuf arenas, args;
+  size_t arenas_bytes = 0, args_bytes = 0;
+  PinnedBuf up, down;
+  hipEvent_t done = nullptr, t0 = nullptr, t1 = nullptr;  // results landed; the launch's kernels (timing)
+  int n = 0;
+  size_t b0 = 0;
+  vector<vector<int32_t>> queues;
+  ~GenSlot() {
+    for (hipEvent_t e : {done, t0, t1})
+      if (e) (void)hipEventDestroy(e);
+  }
+};
+
 struct GeneralBatch {
   std::unique_ptr<Compiled> C;
   uint64_t base_version = 0;
@@ -5321,8 +5362,7 @@ struct GeneralBatch {
   size_t stride = 0;
   vector<uint8_t> tmpl;
   DevBuf pristine;
-  DevBuf arenas, args;
-  size_t arenas_bytes = 0, args_bytes = 0;
+  GenSlot slot[2];  // two launch slots (GeneralBatchRun)
 };
 
 // The superset Solve of a cluster (kp_cluster_plan: general). KP_E_UNSUPPORTED: the batch cannot take this cluster
@@ -5565,9 +5605,11 @@ static int32_t GeneralBatchRun(kp_cluster_plan* plan, GeneralBatch& gb, const ve
   hipStream_t st = ctx->stream;
   // the arena size: every simulation of the batch fits (rounded up, so that nearby batches share a layout)
   size_t max_pods = 1;
+  vector<size_t> len(cands.size(), 0);
   for (int i : idx) {
     size_t n = gb.base_pods.size();
     for (uint32_t c : cands[i]) n += gb.node_pods[c].size();
+    len[i] = n;
     max_pods = std::max(max_pods, n);
   }
   int Pc = 64;
@@ -5575,130 +5617,57 @@ static int32_t GeneralBatchRun(kp_cluster_plan* plan, GeneralBatch& gb, const ve
   if (int32_t rc = GeneralBatchLayout(ctx, gb, Pc)) return rc;
   const SolveOffs& o = gb.o;
   const size_t patch_bytes = o.common;
-  // simulations per launch: bounded by 2 GiB of arenas
-  const size_t per_launch = std::max<size_t>(1, std::min<size_t>(1024, ((size_t)2 << 30) / gb.stride));
+  // simulations per launch: two launch slots (the host prepares one while the device runs the other), each at most
+  // an eighth of the free device memory in arenas and 4096 simulations (one Solve workgroup per CU runs at a time;
+  // the rest queue behind it)
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = (size_t)8 << 30;
+  const size_t held_b = gb.slot[0].arenas_bytes + gb.slot[1].arenas_bytes;
+  const size_t budget = std::max<size_t>((free_b + held_b) / 8, (size_t)1 << 30);
+  size_t per_launch = std::max<size_t>(1, std::min<size_t>(4096, budget / gb.stride));
+  if (idx.size() > per_launch && idx.size() < 2 * per_launch) per_launch = (idx.size() + 1) / 2;  // two even launches
+  // longest simulations first (queue length: pending + the candidates' pods): they start on the first CUs instead
+  // of trailing the launch
+  vector<int> order(idx);
+  std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return len[x] > len[y]; });
+  if (getenv("KP_HOST_TIMING"))
+    fprintf(stderr, "[kp general] arena stride %.2f MB, %zu simulations per launch, Pc %d\n", gb.stride / 1e6, per_launch, Pc);
   const int sort_cap = std::min(SortCapacity(), Pc);
   const size_t dyn = std::max<size_t>((size_t)2 * sort_cap * sizeof(int32_t), o.chk_on ? CHK_LDS_BYTES : 0);
   GenScratch scratch;
-  vector<uint8_t> patches;
-  vector<vector<int32_t>> queues;
   vector<SolveArgs> sargs;
   vector<FinalizeArgs> fargs;
-  vector<uint64_t> stats;
-  vector<int32_t> place, nct;
-  vector<uint32_t> nopt, opts;
-  vector<KReqs> fin;
-  vector<uint64_t> held;
-  for (size_t b0 = 0; b0 < idx.size(); b0 += per_launch) {
-    const auto th0 = std::chrono::steady_clock::now();
-    const int n = (int)std::min(per_launch, idx.size() - b0);
-    // arenas for this launch's n simulations, grown geometrically (a few subsets do not pin 2 GiB on the plan);
-    // when the device cannot hold them, this batch and the rest run one simulation at a time (GeneralSimOne)
-    hipError_t ae = hipSuccess;
-    if (gb.arenas_bytes < gb.stride * n) {
-      const size_t sims = std::min(per_launch, std::max<size_t>((size_t)n, 2 * gb.arenas_bytes / gb.stride));
-      ae = gb.arenas.alloc(gb.stride * sims);
-      gb.arenas_bytes = ae == hipSuccess ? gb.stride * sims : 0;
-    }
-    const size_t args_need = (sizeof(SolveArgs) + sizeof(FinalizeArgs)) * (size_t)n + 512;
-    if (ae == hipSuccess && gb.args_bytes < args_need) {
-      ae = gb.args.alloc(args_need);
-      gb.args_bytes = ae == hipSuccess ? args_need : 0;
-    }
-    if (ae != hipSuccess) {
-      (void)hipGetLastError();
-      for (size_t j = b0; j < idx.size(); j++)
-        if (int32_t rc = GeneralSimOne(plan, cands[idx[j]], labels, multi_node, outs[idx[j]], counters, dev_ms)) return rc;
-      break;
-    }
-    uint8_t* arenas = (uint8_t*)gb.arenas.p;
-    uint8_t* sh = (uint8_t*)gb.shared.p;
-    patches.resize(patch_bytes * n);
-    queues.resize(n);
-    sargs.resize(n);
-    fargs.resize(n);
-    for (int j = 0; j < n; j++) {
-      const int i = idx[b0 + j];
-      if (GeneralPatch(gb, cl, cands[i], scratch, queues[j], patches.data() + patch_bytes * j))
-        return fail(KP_E_INVAL, "subset %d: not batchable after the check", i);
-      uint8_t* ar = arenas + gb.stride * j;
-      SolveArgs& a = sargs[j];
-      BindSolve(a, C, o, sh, ar, (int)queues[j].size(), Pc, gb.rmask, gb.res_mode);
-      if (gb.tfeas_on) {
-        a.tfeas = (const uint64_t*)(sh + o.tfeas);
-        a.tfeas_words = gb.tf_words;
-      }
-      FinalizeArgs& f = fargs[j];
-      memset(&f, 0, sizeof f);
-      f.dict = a.dict;
-      f.cats = a.cats;
-      f.vint = a.vint;
-      f.nc_tmpl = a.nc_tmpl;
-      f.tmpl_catalog = a.tmpl_catalog;
-      f.nc_reqs = a.nc_reqs;
-      f.nc_X = a.nc_X;
-      f.max_types = 100;
-      f.opt_stride = gb.opt_stride;
-      f.out_options = (uint32_t*)(ar + o.opts);
-      f.out_n_remaining = (uint32_t*)(ar + o.nrem);
-      f.out_n_options = (uint32_t*)(ar + o.nopt);
-      f.nc_held = a.res_mode ? a.nc_held : nullptr;
-      f.solve_stats = a.stats;
-    }
-    SolveArgs* dargs = (SolveArgs*)gb.args.p;
-    FinalizeArgs* dfargs = (FinalizeArgs*)((uint8_t*)gb.args.p + ((sizeof(SolveArgs) * n + 255) & ~(size_t)255));
-    BatchInitArgs bi;
-    memset(&bi, 0, sizeof bi);
-    bi.base = arenas;
-    bi.stride = gb.stride;
-    bi.pristine = (const uint8_t*)gb.pristine.p;
-    bi.dst_off = o.common;
-    bi.n_copy = (o.mut_end - o.common + 15) & ~(size_t)15;
-    auto fill = [&](size_t off, size_t len, uint32_t byte) {
-      bi.fill_off[bi.n_fill] = off;
-      bi.fill_len[bi.n_fill] = (len + 15) & ~(size_t)15;
-      bi.fill_byte[bi.n_fill] = byte;
-      bi.n_fill++;
-    };
-    fill(o.stats, sizeof(uint64_t) * KP_SOLVE_STATS, 0);
-    fill(o.npods, sizeof(int32_t) * Pc, 0);
-    fill(o.place, sizeof(int32_t) * Pc, 0xFF);
-    fill(o.ver0, o.ver_end - o.ver0, 0);
-    fill(o.fail0, o.fail_end - o.fail0, 0xFF);
-    if (o.n_hcnc) fill(o.hcnc, o.n_hcnc, 0);
-    host_ms[0] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count();
-    HIPCHK(launch_batch_init(bi, n, st));
-    HIPCHK(hipMemcpy2DAsync(arenas, gb.stride, patches.data(), patch_bytes, patch_bytes, n, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(dargs, sargs.data(), sizeof(SolveArgs) * n, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(dfargs, fargs.data(), sizeof(FinalizeArgs) * n, hipMemcpyHostToDevice, st));
-    HIPCHK(hipEventRecord(ctx->ev0, st));
-    HIPCHK(launch_solve_batch(sargs[0], dargs, n, dyn, st));
-    HIPCHK(launch_finalize_batch(fargs[0], dfargs, n, st));
-    HIPCHK(hipEventRecord(ctx->ev1, st));
-    stats.resize((size_t)n * KP_SOLVE_STATS);
-    place.resize((size_t)n * Pc);
-    nct.resize(n);
-    nopt.resize(n);
-    opts.resize((size_t)n * gb.opt_stride);
-    fin.resize(n);
-    held.resize(n);
-    auto down = [&](void* dst, size_t off, size_t width) {
-      return hipMemcpy2DAsync(dst, width, arenas + off, gb.stride, width, n, hipMemcpyDeviceToHost, st);
-    };
-    HIPCHK(down(stats.data(), o.stats, sizeof(uint64_t) * KP_SOLVE_STATS));
-    HIPCHK(down(place.data(), o.place, sizeof(int32_t) * Pc));
-    HIPCHK(down(nct.data(), o.nct, sizeof(int32_t)));
-    HIPCHK(down(nopt.data(), o.nopt, sizeof(uint32_t)));
-    HIPCHK(down(opts.data(), o.opts, sizeof(uint32_t) * gb.opt_stride));
-    HIPCHK(down(fin.data(), o.ncr, sizeof(KReqs)));
-    if (gb.res_mode) HIPCHK(down(held.data(), o.held, sizeof(uint64_t)));
-    HIPCHK(hipStreamSynchronize(st));
+  // per-launch result layout in the slot's pinned download buffer
+  const size_t r_stats = 0, r_place = r_stats + sizeof(uint64_t) * KP_SOLVE_STATS * per_launch;
+  const size_t r_nct = r_place + sizeof(int32_t) * (size_t)Pc * per_launch;
+  const size_t r_nopt = r_nct + sizeof(int32_t) * per_launch;
+  const size_t r_opts = r_nopt + sizeof(uint32_t) * per_launch;
+  const size_t r_fin = (r_opts + sizeof(uint32_t) * (size_t)gb.opt_stride * per_launch + 63) & ~(size_t)63;
+  const size_t r_held = r_fin + sizeof(KReqs) * per_launch;
+  const size_t r_end = r_held + sizeof(uint64_t) * per_launch;
+  const size_t u_args = (patch_bytes * per_launch + 255) & ~(size_t)255;
+  const size_t u_fargs = u_args + ((sizeof(SolveArgs) * per_launch + 255) & ~(size_t)255);
+  const size_t u_end = u_fargs + sizeof(FinalizeArgs) * per_launch;
+
+  // the host decisions of a finished launch (its results in the slot's download buffer)
+  auto decide = [&](GenSlot& sl) -> int32_t {
+    HIPCHK(hipEventSynchronize(sl.done));
     float ms = 0;
-    HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    HIPCHK(hipEventElapsedTime(&ms, sl.t0, sl.t1));
     *dev_ms += ms;
     const auto th1 = std::chrono::steady_clock::now();
+    const int n = sl.n;
+    const size_t b0 = sl.b0;
+    const uint64_t* stats = reinterpret_cast<uint64_t*>(sl.down.at(r_stats));
+    const int32_t* place = reinterpret_cast<int32_t*>(sl.down.at(r_place));
+    const int32_t* nct = reinterpret_cast<int32_t*>(sl.down.at(r_nct));
+    const uint32_t* nopt = reinterpret_cast<uint32_t*>(sl.down.at(r_nopt));
+    uint32_t* opts = reinterpret_cast<uint32_t*>(sl.down.at(r_opts));
+    const KReqs* fin = reinterpret_cast<KReqs*>(sl.down.at(r_fin));
+    const uint64_t* held = reinterpret_cast<uint64_t*>(sl.down.at(r_held));
+    const vector<vector<int32_t>>& queues = sl.queues;
     for (int j = 0; j < n; j++) {
-      const int i = idx[b0 + j];
+      const int i = order[b0 + j];
       const uint64_t* sj = &stats[(size_t)j * KP_SOLVE_STATS];
       if (sj[7]) return fail(KP_E_DEVICE, "solve_kernel exceeded its Queue.Pop bound in simulation %d: aborted", i);
       counters[0] += sj[0];
@@ -5729,6 +5698,135 @@ static int32_t GeneralBatchRun(kp_cluster_plan* plan, GeneralBatch& gb, const ve
                     n_nc == 1 ? nopt[j] : 0, multi_node, r, &gb.offers, &gb.cands);
     }
     host_ms[1] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th1).count();
+    return KP_OK;
+  };
+
+  GenSlot* slots = gb.slot;
+  for (int k = 0; k < 2; k++)
+    if (!slots[k].done) {
+      HIPCHK(hipEventCreateWithFlags(&slots[k].done, hipEventDisableTiming));
+      HIPCHK(hipEventCreate(&slots[k].t0));
+      HIPCHK(hipEventCreate(&slots[k].t1));
+    }
+  int pending = -1;  // the slot whose launch is in flight and not yet decided
+  int launch_no = 0;
+  for (size_t b0 = 0; b0 < idx.size(); b0 += per_launch, launch_no++) {
+    GenSlot& sl = slots[launch_no & 1];
+    const auto th0 = std::chrono::steady_clock::now();
+    const int n = (int)std::min(per_launch, idx.size() - b0);
+    // arenas for this launch's n simulations, grown geometrically (a few subsets do not pin gigabytes on the plan);
+    // when the device cannot hold them, this batch and the rest run one simulation at a time (GeneralSimOne)
+    hipError_t ae = hipSuccess;
+    if (sl.arenas_bytes < gb.stride * n) {
+      const size_t sims = std::min(per_launch, std::max<size_t>((size_t)n, 2 * sl.arenas_bytes / gb.stride));
+      ae = sl.arenas.alloc(gb.stride * sims);
+      sl.arenas_bytes = ae == hipSuccess ? gb.stride * sims : 0;
+    }
+    const size_t args_need = (sizeof(SolveArgs) + sizeof(FinalizeArgs)) * (size_t)n + 512;
+    if (ae == hipSuccess && sl.args_bytes < args_need) {
+      ae = sl.args.alloc(args_need);
+      sl.args_bytes = ae == hipSuccess ? args_need : 0;
+    }
+    if (ae == hipSuccess) ae = sl.up.reserve(u_end);
+    if (ae == hipSuccess) ae = sl.down.reserve(r_end);
+    if (ae != hipSuccess) {
+      (void)hipGetLastError();
+      if (pending >= 0) {
+        if (int32_t rc = decide(slots[pending])) return rc;
+        pending = -1;
+      }
+      for (size_t j = b0; j < idx.size(); j++)
+        if (int32_t rc = GeneralSimOne(plan, cands[order[j]], labels, multi_node, outs[order[j]], counters, dev_ms)) return rc;
+      break;
+    }
+    uint8_t* arenas = (uint8_t*)sl.arenas.p;
+    uint8_t* sh = (uint8_t*)gb.shared.p;
+    uint8_t* patches = reinterpret_cast<uint8_t*>(sl.up.at(0));
+    sl.queues.resize(n);
+    vector<vector<int32_t>>& queues = sl.queues;
+    sargs.resize(n);
+    fargs.resize(n);
+    for (int j = 0; j < n; j++) {
+      const int i = order[b0 + j];
+      if (GeneralPatch(gb, cl, cands[i], scratch, queues[j], patches + patch_bytes * j))
+        return fail(KP_E_INVAL, "subset %d: not batchable after the check", i);
+      uint8_t* ar = arenas + gb.stride * j;
+      SolveArgs& a = sargs[j];
+      BindSolve(a, C, o, sh, ar, (int)queues[j].size(), Pc, gb.rmask, gb.res_mode);
+      if (gb.tfeas_on) {
+        a.tfeas = (const uint64_t*)(sh + o.tfeas);
+        a.tfeas_words = gb.tf_words;
+      }
+      FinalizeArgs& f = fargs[j];
+      memset(&f, 0, sizeof f);
+      f.dict = a.dict;
+      f.cats = a.cats;
+      f.vint = a.vint;
+      f.nc_tmpl = a.nc_tmpl;
+      f.tmpl_catalog = a.tmpl_catalog;
+      f.nc_reqs = a.nc_reqs;
+      f.nc_X = a.nc_X;
+      f.max_types = 100;
+      f.opt_stride = gb.opt_stride;
+      f.out_options = (uint32_t*)(ar + o.opts);
+      f.out_n_remaining = (uint32_t*)(ar + o.nrem);
+      f.out_n_options = (uint32_t*)(ar + o.nopt);
+      f.nc_held = a.res_mode ? a.nc_held : nullptr;
+      f.solve_stats = a.stats;
+    }
+    memcpy(reinterpret_cast<uint8_t*>(sl.up.at(u_args)), sargs.data(), sizeof(SolveArgs) * n);
+    memcpy(reinterpret_cast<uint8_t*>(sl.up.at(u_fargs)), fargs.data(), sizeof(FinalizeArgs) * n);
+    SolveArgs* dargs = (SolveArgs*)sl.args.p;
+    FinalizeArgs* dfargs = (FinalizeArgs*)((uint8_t*)sl.args.p + ((sizeof(SolveArgs) * n + 255) & ~(size_t)255));
+    BatchInitArgs bi;
+    memset(&bi, 0, sizeof bi);
+    bi.base = arenas;
+    bi.stride = gb.stride;
+    bi.pristine = (const uint8_t*)gb.pristine.p;
+    bi.dst_off = o.common;
+    bi.n_copy = (o.mut_end - o.common + 15) & ~(size_t)15;
+    auto fill = [&](size_t off, size_t len, uint32_t byte) {
+      bi.fill_off[bi.n_fill] = off;
+      bi.fill_len[bi.n_fill] = (len + 15) & ~(size_t)15;
+      bi.fill_byte[bi.n_fill] = byte;
+      bi.n_fill++;
+    };
+    fill(o.stats, sizeof(uint64_t) * KP_SOLVE_STATS, 0);
+    fill(o.npods, sizeof(int32_t) * Pc, 0);
+    fill(o.place, sizeof(int32_t) * Pc, 0xFF);
+    fill(o.ver0, o.ver_end - o.ver0, 0);
+    fill(o.fail0, o.fail_end - o.fail0, 0xFF);
+    if (o.n_hcnc) fill(o.hcnc, o.n_hcnc, 0);
+    host_ms[0] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count();
+    HIPCHK(launch_batch_init(bi, n, st));
+    HIPCHK(hipMemcpy2DAsync(arenas, gb.stride, patches, patch_bytes, patch_bytes, n, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(dargs, reinterpret_cast<uint8_t*>(sl.up.at(u_args)), sizeof(SolveArgs) * n, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(dfargs, reinterpret_cast<uint8_t*>(sl.up.at(u_fargs)), sizeof(FinalizeArgs) * n, hipMemcpyHostToDevice, st));
+    HIPCHK(hipEventRecord(sl.t0, st));
+    HIPCHK(launch_solve_batch(sargs[0], dargs, n, dyn, st));
+    HIPCHK(launch_finalize_batch(fargs[0], dfargs, n, st));
+    HIPCHK(hipEventRecord(sl.t1, st));
+    auto down = [&](size_t roff, size_t off, size_t width) {
+      return hipMemcpy2DAsync(reinterpret_cast<uint8_t*>(sl.down.at(roff)), width, arenas + off, gb.stride, width, n, hipMemcpyDeviceToHost, st);
+    };
+    HIPCHK(down(r_stats, o.stats, sizeof(uint64_t) * KP_SOLVE_STATS));
+    HIPCHK(down(r_place, o.place, sizeof(int32_t) * Pc));
+    HIPCHK(down(r_nct, o.nct, sizeof(int32_t)));
+    HIPCHK(down(r_nopt, o.nopt, sizeof(uint32_t)));
+    HIPCHK(down(r_opts, o.opts, sizeof(uint32_t) * gb.opt_stride));
+    HIPCHK(down(r_fin, o.ncr, sizeof(KReqs)));
+    if (gb.res_mode) HIPCHK(down(r_held, o.held, sizeof(uint64_t)));
+    HIPCHK(hipEventRecord(sl.done, st));
+    sl.n = n;
+    sl.b0 = b0;
+    // the previous launch's decisions while this one runs
+    if (pending >= 0) {
+      if (int32_t rc = decide(slots[pending])) return rc;
+    }
+    pending = launch_no & 1;
+  }
+  if (pending >= 0) {
+    if (int32_t rc = decide(slots[pending])) return rc;
   }
   return KP_OK;
 }

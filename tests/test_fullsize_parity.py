@@ -93,3 +93,27 @@ def test_general_fullsize(ctx, catalog, digests, monkeypatch):
     got = [mk.sim_record(r) for r in res]
     assert got[:len(pre)] == want["prefixes"]
     assert got[len(pre):] == want["random"]
+
+
+@pytest.mark.gpu
+def test_general_10000(ctx, catalog, digests, monkeypatch):
+    """The general path at config 4's size: the 10,000-node spread cluster (83k pods), the 100 prefixes and 200 random
+    subsets of 2..100 candidates, batched on the superset Solve, every decision field equal to the oracle's digest."""
+    import kpamd
+    import make_fullsize_digests as mk
+    from kpamd import synth
+    if "general-10000" not in digests:
+        pytest.skip("general-10000: digest not generated (make_fullsize_digests.py general-10000)")
+    monkeypatch.setenv("KP_GENERAL_BATCH", "1")
+    cl = synth.spread_cluster(catalog, 10_000)
+    pre, rnd = mk.general10k_subsets(cl)
+    plan = kpamd.ClusterPlan(ctx, cl)
+    try:
+        res, st = plan.simulate(pre + rnd)
+    finally:
+        plan.close()
+    assert st["phase_cycles"][:2] == [len(pre) + len(rnd), 0], "every subset batched"
+    want = digests["general-10000"]
+    got = [mk.sim_record(r) for r in res]
+    assert got[:len(pre)] == want["prefixes"]
+    assert got[len(pre):] == want["random"]

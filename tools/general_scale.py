@@ -49,7 +49,7 @@ def main():
     if "--digest" in sys.argv:  # the committed oracle digest of the 100 prefixes + 200 random subsets (seed 6)
         import make_fullsize_digests as mk
         pre, rnd = mk.general10k_subsets(cl)
-        res = plan.simulate(pre + rnd)
+        res, _ = plan.simulate(pre + rnd)
         got = [mk.sim_record(r) for r in res]
         want = json.load(open(os.path.join(ROOT, "tests", "golden", "fullsize_digests.json"))).get("general-10000")
         if want:
