@@ -35,7 +35,7 @@
 // kernel into a measurement stub.
 #if !defined(KP_DIAG_BUILD) &&                                                                                       \
     (defined(FASTLANE) || defined(FL_NOTIME) || defined(FT_FINE) || defined(FAST_SCAN_MAX) ||                        \
-     defined(FAST_CHK_LIVE) || defined(SORT_DIAG) || defined(EX_DIAG) || defined(FEAS_MAX_BLOCKS) ||                 \
+     defined(FAST_CHK_LIVE) || defined(FAST_EX_ROUNDS) || defined(SORT_DIAG) || defined(EX_DIAG) || defined(FEAS_MAX_BLOCKS) ||                 \
      defined(FEASQ_EW) || defined(FEASQ_ROWS) || defined(FEASQ_B128) || defined(FEASQ_SKIP_EVAL))
 #error "a measurement knob is set outside a tools/ variant build (tools/kp_diag.h)"
 #endif
@@ -57,6 +57,9 @@
 #endif
 #ifndef FAST_CHK_LIVE
 #define FAST_CHK_LIVE 8  // chunked order: live (not dead) chunks the fast lane scans before the 4-wave pre-pass takes over
+#endif
+#ifndef FAST_EX_ROUNDS
+#define FAST_EX_ROUNDS 8  // existing nodes: 64-position rounds the fast lane scans before the 4-wave pre-pass takes over
 #endif
 // Explicit address spaces: LDS data reached through a pointer would otherwise be read with FLAT loads (which wait
 // on the vector-memory counter too and take the long path); global rows get global_load.
@@ -2106,7 +2109,7 @@ if (!FL_NOTIME && tmg) {                                    \
 }
     // next pod's stage data, loaded while the current pod is placed (window offset pf_off; -1: none)
     int pf_off = -1, pf_own = 0, pf_ce0 = 0, pf_ce1 = 0, pf_cur = 0, pf_stamp = 0, prev_sl = -1;
-    int a_cur_prev_pos = 0, a_cur_prev_stamp = 0, a_cex_prev_stamp = 0;  // cursors the previous pod stored
+    int a_cur_prev_pos = 0, a_cur_prev_stamp = 0, a_cex_prev_stamp = 0, a_cex_prev_pos = 0;  // cursors the previous pod stored
     int64_t pf_preq = 0;
     uint64_t pf_tol = 0;
     for (;;) {
@@ -2170,7 +2173,7 @@ if (!FL_NOTIME && tmg) {                                    \
         if (sl == prev_sl) {  // the previous pod (same shape-level) advanced both cursors after the loads
           cur = a_cur_prev_pos;
           stamp = a_cur_prev_stamp;
-          ce0 = A->n_existing;
+          ce0 = a_cex_prev_pos;
           ce1 = a_cex_prev_stamp;
         }
       } else {
@@ -2200,7 +2203,9 @@ if (!FL_NOTIME && tmg) {                                    \
       // every placement, so after the sort replay below the lane does the full path's failure bookkeeping itself
       const bool memo = CHK && !TOPO && A->sl_fail[sl] == n_nc_all;
       bool eligible = own == 0;
-      if (FL_HAS_EX) eligible = eligible && min(ce0, mstack_query_wave((LdsI32)s_stk[1], U(s_ctl[14]), U(s_ctl[21]), ce1)) >= A->n_existing;
+      // addToExistingNode's start: the first-fit cursor, clamped by the existing positions mutated since it was stored
+      const int ex_start = FL_HAS_EX ? min(ce0, mstack_query_wave((LdsI32)s_stk[1], U(s_ctl[14]), U(s_ctl[21]), ce1))
+                                     : 0;
       FT(0);
       if (!eligible) {
         handoff = pod;
@@ -2258,9 +2263,166 @@ if (!FL_NOTIME && tmg) {                                    \
           }
       }
       a_cex_prev_stamp = U(s_ctl[15]);
-      if (FL_HAS_EX && lane == 0) {  // addToExistingNode: every position fails (cursor == n_existing)
-        A->cur_ex[2 * sl] = A->n_existing;
-        A->cur_ex[2 * sl + 1] = a_cex_prev_stamp;
+      bool b_staged = false;  // fl_B holds the pod's requirement set (staged on the first merge)
+      // ---- addToExistingNode on the wave: ExistingNode.CanAdd at the lowest position that takes the pod, the
+      // full path's checks 64 positions per round (headroom rows, failure memo, static fit, taints, hostname counts,
+      // then the zone-like keys' value codes), then the requirement merge on the first candidates. An existing node's
+      // labels are single values and its codes were checked against the accepted domains, so the topology narrowing
+      // has nothing to narrow. A scan longer than FAST_EX_ROUNDS rounds goes to the full path's 1,024-lane pre-pass.
+      if (FL_HAS_EX && ex_start < A->n_existing && !memo) {
+        const int E = A->n_existing;
+        int ex_pl = -1, ex_ipos = INT32_MAX, rounds = 0;
+        bool ex_bail = false;
+        for (int base = ex_start; base < E && ex_pl < 0; base += 64) {
+          if (++rounds > FAST_EX_ROUNDS) {
+            ex_bail = true;
+            break;
+          }
+          const int ec = base + lane;
+          const bool valid = ec < E;
+          bool cand = false, icand = false;
+          int32_t ver = 0, ts = 0;
+          if (valid) {
+            const int32_t fl = A->ex_fail[(size_t)sl * E + ec];
+            ver = A->ex_ver[ec];
+            ts = A->ex_taintset[ec];
+            const uint8_t sok = A->ex_static_ok[ec];
+            cand = A->ex_room[ec] >= pr0 && A->ex_room[(size_t)E + ec] >= pr1;
+            if (four) cand = cand && A->ex_room[2 * (size_t)E + ec] >= pr2 && A->ex_room[3 * (size_t)E + ec] >= pr3;
+            cand = cand && fl != ver && fl != NC_NEVER && sok && ((tolmask >> ts) & 1);
+            if (rr_b4p && cand) {  // a fifth requested resource and beyond
+              const int64_t* av = A->ex_available + (size_t)ec * KP_NRES;
+              const int64_t* rq = A->ex_requests + (size_t)ec * KP_NRES;
+              for (uint32_t rm = rr_b4p; rm; rm &= rm - 1) {
+                const int r = __builtin_ctz(rm);
+                cand = cand && rq[r] + lane_bcast_i64(preq_lane, r) <= av[r];
+              }
+            }
+            if (TOPO && t_n) {
+#pragma unroll
+              for (int j = 0; j < 4; j++)
+                if (j < t_n && t_key[j] < 0)
+                  cand = cand && (int)A->hcnt_ex[(size_t)t_row[j] * E + ec] + t_self[j] <= t_mskew[j];
+              icand = cand;
+#pragma unroll
+              for (int j = 0; j < 4; j++)
+                if (j < t_n && t_key[j] >= 0) {
+                  const uint32_t code = A->ex_tcode[(size_t)t_slot[j] * E + ec];
+                  cand = cand && code != 0xFF && ((t_acc[j] >> (code & 63)) & 1);
+                }
+            }
+          }
+          if (TOPO && t_n && ex_ipos == INT32_MAX) {
+            const uint64_t im = __ballot(icand);
+            if (im) ex_ipos = base + __builtin_ctzll(im);
+          }
+          if (lane == 0) bytes += (uint64_t)min(64, E - base) * (16 * A->n_req_res + 13);  // (the full path's model)
+          uint64_t cm = __ballot(cand);
+          while (cm) {
+            const int l = __builtin_ctzll(cm);
+            cm &= cm - 1;
+            const int ei = base + l;
+            const int32_t verx = __builtin_amdgcn_readlane(ver, l);
+            attempts++;
+            if (!b_staged) {  // the pod's requirement set, once per pod
+              constexpr int NQ = (int)(sizeof(KReqs) / 8);
+              const uint64_t* src = reinterpret_cast<const uint64_t*>(A->shape_reqs + (size_t)sl * sizeof(KReqs));
+              uint64_t* dstB = reinterpret_cast<uint64_t*>(&fl_B);
+              for (int i = lane; i < NQ; i += 64) dstB[i] = src[i];
+              wave_sync();
+              b_staged = true;
+            }
+            KReqs* er = reinterpret_cast<KReqs*>(A->ex_reqs + (size_t)ei * sizeof(KReqs));
+            const CandReq crx = load_cand(D, er);
+            uint64_t m_v = 0;
+            ReqView rv;
+            const uint64_t b_negop = A->shape_negop[sl];
+            const bool mok = merge_compatible(D, crx, (const KReqs*)&fl_B, b_negop, false, m_v, rv, (WaveSlots*)&fl_slots,
+                                              vint_global(A->vint));
+            bytes += sizeof(KReqs);
+            if (!mok) {  // permanent unless the undefined-key rule failed (no well-known exemption here)
+              if (lane == 0) A->ex_fail[(size_t)sl * E + ei] = (fl_B.present & ~crx.P & ~b_negop) == 0 ? NC_NEVER : verx;
+              continue;
+            }
+            // commit: ExistingNode.Add (requirements, requests, headroom rows, version), Topology.Record
+            store_merged(er, rv, m_v, D.W, D.KB);
+            if (lane < KP_NRES) A->ex_requests[(size_t)ei * KP_NRES + lane] += preq_lane;
+            if (lane < 4) {  // headroom rows of the first four requested resources
+              const int64_t d = lane == 0 ? pr0 : lane == 1 ? pr1 : lane == 2 ? pr2 : pr3;
+              A->ex_room[(size_t)lane * E + ei] -= d;
+            }
+            if (lane == 0) A->ex_ver[ei] = verx + 1;
+            if (TOPO && rec_n) {
+              const int tsx = __builtin_amdgcn_readlane(ts, l);
+              for (int i0 = 0; i0 < rec_n; i0 += 64) {
+                const int ri = i0 + lane;
+                if (ri < rec_n) {
+                  const int g = A->rec_list[rec_b + ri], aux = A->rec_aux[rec_b + ri];
+                  if (A->tg_live[g] && ((A->tg_filt_tol[g] >> tsx) & 1)) {
+                    if (aux >= 0) {
+                      uint8_t* c = &A->hcnt_ex[(size_t)aux * E + ei];
+                      *c = *c == 255 ? 1 : *c < 254 ? *c + 1 : 254;  // 255: an unregistered domain
+                      A->tg_reg[g] = 1;
+                    } else {
+                      const uint32_t code = A->ex_tcode[(size_t)(-1 - aux) * E + ei];
+                      if (code < 64) {
+                        A->tg_cnt[(size_t)g * 64 + code] += 1;
+                        A->tg_reg[g] |= 1ull << code;
+                      }
+                    }
+                  }
+                }
+              }
+              bytes += 16 * (uint64_t)rec_n;
+            }
+            ex_pl = ei;
+            break;
+          }
+        }
+        if (ex_bail) {  // a long scan: the full path's (nothing was placed; the failure memos stay valid)
+          handoff = pod;
+          fb = FB_SCAN;
+          break;
+        }
+        // cursor: every position before the winner failed; with owned groups, before the first position that passed
+        // the count-independent checks (a zone-count failure may pass later), as the full path
+        const int cpos = TOPO && t_n ? min(ex_ipos, E) : (ex_pl >= 0 ? ex_pl : E);
+        if (lane == 0) {
+          A->cur_ex[2 * sl] = cpos;
+          A->cur_ex[2 * sl + 1] = a_cex_prev_stamp;
+        }
+        a_cex_prev_pos = cpos;
+        if (ex_pl >= 0) {
+          int ex_n = U(s_ctl[14]), ex_lost = U(s_ctl[21]);
+          mstack_push_reg((int32_t LDS*)s_stk[1], ex_n, ex_lost, a_cex_prev_stamp + 1, ex_pl);
+          if (lane == 0) {
+            s_ctl[14] = ex_n;
+            s_ctl[21] = ex_lost;
+            s_ctl[15] = a_cex_prev_stamp + 1;
+          }
+          wave_sync();
+          // the in-flight cursor is untouched (no in-flight scan): the next pod of this level reads the same one
+          a_cur_prev_pos = cur;
+          a_cur_prev_stamp = stamp;
+          pops++;
+          if (lane == n_buf) {
+            buf_pod = pod;
+            buf_pl = -2 - ex_pl;
+          }
+          if (++n_buf == 64) {
+            A->placement[buf_pod] = buf_pl;
+            A->events[n_ev + lane] = buf_pod;
+            n_ev += 64;
+            n_buf = 0;
+          }
+          continue;
+        }
+      } else if (FL_HAS_EX) {  // addToExistingNode: every position fails (cursor == n_existing)
+        if (lane == 0) {
+          A->cur_ex[2 * sl] = A->n_existing;
+          A->cur_ex[2 * sl + 1] = a_cex_prev_stamp;
+        }
+        a_cex_prev_pos = A->n_existing;
       }
       FT(1);
       // sort.Slice(newNodeClaims) replay + first-fit start (sort arrays in LDS or chunked; the flat global order:
@@ -2332,7 +2494,6 @@ if (!FL_NOTIME && tmg) {                                    \
       // addToInflightNode: pre-checks 64 positions at a time, then the append-path attempts in order. A long scan
       // is the full path's (512-lane pre-pass).
       int placed = -1, wpos = -1, why = FB_NONE, ipos = INT32_MAX;  // ipos: first count-independent pass (topology)
-      bool b_staged = false;
       bool bail = !CHK && n_nc - start > FAST_SCAN_MAX;
       if (bail) why = FB_SCAN;
       if (lane == 0 && !bail) starts += start;
@@ -4223,7 +4384,7 @@ __global__ __launch_bounds__(FEASB_WAVES * 64, FEASB_MINW) void feasibility_bits
 #define FEASQ_SKIP_EVAL 0  // measurement only: decode + copies, no type-set work (wrong masks)
 #endif
 static_assert(KP_DIAG_BUILD || (FASTLANE == 1 && FL_NOTIME == 1 && FT_FINE == 0 && FAST_SCAN_MAX == 512 &&
-                                 FAST_CHK_LIVE == 8 && SORT_DIAG == 0 && EX_DIAG == 0 && FEAS_MAX_BLOCKS == 65536 &&
+                                 FAST_CHK_LIVE == 8 && FAST_EX_ROUNDS == 8 && SORT_DIAG == 0 && EX_DIAG == 0 && FEAS_MAX_BLOCKS == 65536 &&
                                  FEASQ_EW == 7 && FEASQ_ROWS == 28 && FEASQ_B128 == 1 && FEASQ_SKIP_EVAL == 0),
               "the production build carries the production values of every measurement knob");
 __global__ __launch_bounds__(FEASB_WAVES * 64, FEASB_MINW) void feasibility_quad_kernel(FeasArgs a) {
