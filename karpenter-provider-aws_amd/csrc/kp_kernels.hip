@@ -2235,6 +2235,9 @@ if (!FL_NOTIME && tmg) {                                    \
       // path stages them into s_town / s_tacc (hostname rows: count + self <= maxSkew; dictionary keys: the domains
       // whose count + self - min <= maxSkew)
       int t_n = 0, rec_n = 0, rec_b = 0;
+      // the recorded groups of the shape (lane i: the i-th, up to 64), loaded with the stage so that Topology.Record
+      // at the commit starts from registers: group, hostname row / key slot, and whether it counts the node's taints
+      int r_g = 0, r_aux = 0;
       bool triv = false;  // no requirements at this level: Add on any NodeClaim is Fits alone (the full path's triv)
       int t_key[4] = {0, 0, 0, 0}, t_row[4] = {0, 0, 0, 0}, t_slot[4] = {0, 0, 0, 0}, t_self[4] = {0, 0, 0, 0},
           t_mskew[4] = {0, 0, 0, 0};
@@ -2244,6 +2247,10 @@ if (!FL_NOTIME && tmg) {                                    \
         triv = kreq_at(A->shape_reqs, sl)->present == 0;
         rec_n = A->shape_rec_n[shape];
         rec_b = A->shape_rec_base[shape];
+        if (lane < rec_n) {  // (the group's liveness and taint filter are read at the commit: no wait here)
+          r_g = A->rec_list[rec_b + lane];
+          r_aux = A->rec_aux[rec_b + lane];
+        }
         const int ob = A->sl_own_base[sl];
 #pragma unroll
         for (int j = 0; j < 4; j++)
@@ -2271,6 +2278,7 @@ if (!FL_NOTIME && tmg) {                                    \
       // has nothing to narrow. A scan longer than FAST_EX_ROUNDS rounds goes to the full path's 1,024-lane pre-pass.
       if (FL_HAS_EX && ex_start < A->n_existing && !memo) {
         const int E = A->n_existing;
+        const bool ex_triv = TOPO ? triv : kreq_at(A->shape_reqs, sl)->present == 0;
         int ex_pl = -1, ex_ipos = INT32_MAX, rounds = 0;
         bool ex_bail = false;
         for (int base = ex_start; base < E && ex_pl < 0; base += 64) {
@@ -2278,6 +2286,7 @@ if (!FL_NOTIME && tmg) {                                    \
             ex_bail = true;
             break;
           }
+          if (FT_FINE && tmg) fcyc[13] += 1;  // diagnostic: existing-scan rounds
           const int ec = base + lane;
           const bool valid = ec < E;
           bool cand = false, icand = false;
@@ -2324,7 +2333,7 @@ if (!FL_NOTIME && tmg) {                                    \
             const int ei = base + l;
             const int32_t verx = __builtin_amdgcn_readlane(ver, l);
             attempts++;
-            if (!b_staged) {  // the pod's requirement set, once per pod
+            if (!b_staged && !ex_triv) {  // the pod's requirement set, once per pod
               constexpr int NQ = (int)(sizeof(KReqs) / 8);
               const uint64_t* src = reinterpret_cast<const uint64_t*>(A->shape_reqs + (size_t)sl * sizeof(KReqs));
               uint64_t* dstB = reinterpret_cast<uint64_t*>(&fl_B);
@@ -2333,19 +2342,23 @@ if (!FL_NOTIME && tmg) {                                    \
               b_staged = true;
             }
             KReqs* er = reinterpret_cast<KReqs*>(A->ex_reqs + (size_t)ei * sizeof(KReqs));
-            const CandReq crx = load_cand(D, er);
-            uint64_t m_v = 0;
-            ReqView rv;
-            const uint64_t b_negop = A->shape_negop[sl];
-            const bool mok = merge_compatible(D, crx, (const KReqs*)&fl_B, b_negop, false, m_v, rv, (WaveSlots*)&fl_slots,
-                                              vint_global(A->vint));
             bytes += sizeof(KReqs);
-            if (!mok) {  // permanent unless the undefined-key rule failed (no well-known exemption here)
-              if (lane == 0) A->ex_fail[(size_t)sl * E + ei] = (fl_B.present & ~crx.P & ~b_negop) == 0 ? NC_NEVER : verx;
-              continue;
+            // a pod without requirements at this level: Compatible holds and Add leaves the node's requirements as
+            // they are (nothing to intersect), so neither the merge nor its store is needed
+            if (!ex_triv) {
+              const CandReq crx = load_cand(D, er);
+              uint64_t m_v = 0;
+              ReqView rv;
+              const uint64_t b_negop = A->shape_negop[sl];
+              const bool mok = merge_compatible(D, crx, (const KReqs*)&fl_B, b_negop, false, m_v, rv,
+                                                (WaveSlots*)&fl_slots, vint_global(A->vint));
+              if (!mok) {  // permanent unless the undefined-key rule failed (no well-known exemption here)
+                if (lane == 0) A->ex_fail[(size_t)sl * E + ei] = (fl_B.present & ~crx.P & ~b_negop) == 0 ? NC_NEVER : verx;
+                continue;
+              }
+              // commit: ExistingNode.Add (requirements, requests, headroom rows, version), Topology.Record
+              store_merged(er, rv, m_v, D.W, D.KB);
             }
-            // commit: ExistingNode.Add (requirements, requests, headroom rows, version), Topology.Record
-            store_merged(er, rv, m_v, D.W, D.KB);
             if (lane < KP_NRES) A->ex_requests[(size_t)ei * KP_NRES + lane] += preq_lane;
             if (lane < 4) {  // headroom rows of the first four requested resources
               const int64_t d = lane == 0 ? pr0 : lane == 1 ? pr1 : lane == 2 ? pr2 : pr3;
@@ -2357,14 +2370,20 @@ if (!FL_NOTIME && tmg) {                                    \
               for (int i0 = 0; i0 < rec_n; i0 += 64) {
                 const int ri = i0 + lane;
                 if (ri < rec_n) {
-                  const int g = A->rec_list[rec_b + ri], aux = A->rec_aux[rec_b + ri];
-                  if (A->tg_live[g] && ((A->tg_filt_tol[g] >> tsx) & 1)) {
+                  int g = r_g, aux = r_aux;
+                  if (i0) g = A->rec_list[rec_b + ri], aux = A->rec_aux[rec_b + ri];  // (past the 64 prefetched)
+                  // liveness, taint filter and the node's value code in one round trip
+                  const int live = A->tg_live[g];
+                  const uint64_t ftol = A->tg_filt_tol[g];
+                  const uint32_t code0 = aux < 0 ? A->ex_tcode[(size_t)(-1 - aux) * E + ei] : 0xFF;
+                  uint8_t* c = &A->hcnt_ex[(size_t)(aux >= 0 ? aux : 0) * E + ei];
+                  const uint32_t hc0 = aux >= 0 ? *c : 0;
+                  if (live && ((ftol >> tsx) & 1)) {
                     if (aux >= 0) {
-                      uint8_t* c = &A->hcnt_ex[(size_t)aux * E + ei];
-                      *c = *c == 255 ? 1 : *c < 254 ? *c + 1 : 254;  // 255: an unregistered domain
+                      *c = hc0 == 255 ? 1 : hc0 < 254 ? hc0 + 1 : 254;  // 255: an unregistered domain
                       A->tg_reg[g] = 1;
                     } else {
-                      const uint32_t code = A->ex_tcode[(size_t)(-1 - aux) * E + ei];
+                      const uint32_t code = code0;
                       if (code < 64) {
                         A->tg_cnt[(size_t)g * 64 + code] += 1;
                         A->tg_reg[g] |= 1ull << code;
@@ -2743,14 +2762,20 @@ if (!FL_NOTIME && tmg) {                                    \
               for (int i0 = 0; i0 < rec_n; i0 += 64) {
                 const int ri = i0 + lane;
                 if (ri < rec_n) {
-                  const int g = A->rec_list[rec_b + ri], aux = A->rec_aux[rec_b + ri];
-                  if (A->tg_live[g] && ((A->tg_filt_tol[g] >> tsx) & 1)) {
+                  int g = r_g, aux = r_aux;
+                  if (i0) g = A->rec_list[rec_b + ri], aux = A->rec_aux[rec_b + ri];  // (past the 64 prefetched)
+                  // liveness, taint filter and the NodeClaim's value code in one round trip
+                  const int live = A->tg_live[g];
+                  const uint64_t ftol = A->tg_filt_tol[g];
+                  const uint32_t code0 = aux < 0 ? A->nc_tcode[(size_t)(-1 - aux) * A->hnc_stride + ncx] : 0xFF;
+                  uint8_t* c = &A->hcnt_nc[(size_t)(aux >= 0 ? aux : 0) * A->hnc_stride + ncx];
+                  const uint32_t hc0 = aux >= 0 ? *c : 0;
+                  if (live && ((ftol >> tsx) & 1)) {
                     if (aux >= 0) {
-                      uint8_t* c = &A->hcnt_nc[(size_t)aux * A->hnc_stride + ncx];
-                      *c = *c == 255 ? 1 : *c < 254 ? *c + 1 : 254;  // 255: an unregistered domain
+                      *c = hc0 == 255 ? 1 : hc0 < 254 ? hc0 + 1 : 254;  // 255: an unregistered domain
                       A->tg_reg[g] = 1;
                     } else {
-                      const uint32_t code = A->nc_tcode[(size_t)(-1 - aux) * A->hnc_stride + ncx];
+                      const uint32_t code = code0;
                       if (code < 64) {
                         A->tg_cnt[(size_t)g * 64 + code] += 1;
                         A->tg_reg[g] |= 1ull << code;
