@@ -404,6 +404,8 @@ typedef struct kp_solve_stats {
                                no in-flight NodeClaim took it, reserved */
   uint64_t reserved_offering_errors; /* ABI v9: pops whose addToNewNodeClaim failed on a ReservedOfferingError (strict
                                         mode; upstream Results.ReservedOfferingErrors: deferred, not relaxed) */
+  uint64_t run_length_pods; /* ABI v11: pods the fast lane committed as part of a run (queue runs of one shape-level
+                               onto one NodeClaim, committed k at a time: solve_kernel's run-length commit) */
   uint64_t order_chunks[5]; /* ABI v10, diagnostic: the chunked newNodeClaims order past the LDS sort capacity: peak
                                chunks, chunk splits, emptied chunks, directory (re)builds, final order mode (1 LDS,
                                2 chunked, 0 flat global) */

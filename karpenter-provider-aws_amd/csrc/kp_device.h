@@ -101,6 +101,7 @@ struct SolveArgs {
   uint32_t req_res_mask;             // resources some pod shape requests (> 0)
   int32_t timing;                    // 1: thread 0 accumulates per-phase s_memtime deltas into stats[8..15]
   const int32_t* cancel;             // kp_cancel flag (host-mapped, polled every ~1024 pops), NULL: none
+  int32_t cont;                      // 1: the fast lane variant with the continuation round (queue runs of one shape)
   // topology spread (upstream Topology, TopologyTypeSpread groups). A group on a dictionary key keeps a
   // count per value ordinal and the mask of registered domains; a hostname group a saturating u8 count per
   // node (existing positions: hcnt_ex, NodeClaim ids: hcnt_nc).

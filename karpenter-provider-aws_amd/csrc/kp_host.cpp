@@ -1295,6 +1295,7 @@ struct Compiled {
   vector<int64_t> tmpl_remaining;
   // shapes
   vector<int32_t> shape_level_base, shape_nlevels;
+  int32_t cont_hint = 0;  // most queue neighbours share their shape: the fast lane with its continuation round
   vector<KReqs> shape_reqs;
   vector<uint64_t> shape_negop, shape_tolerates;  // per shape-level (tolerations change at the PreferNoSchedule level)
   vector<char> sl_pns;                             // per shape-level: toleratePreferNoScheduleTaints' level
@@ -2666,6 +2667,13 @@ int32_t CompilePerCall(const kp_solve_in* in, const SolveRaw& raw, Compiled& cp)
     return p.pod < q.pod;
   });
   for (uint32_t p = 0; p < in->n_pods; p++) cp.queue[p] = qk[p].pod;
+  {  // the fast lane's continuation round pays where most queue neighbours share their shape (deployments created in
+     // bursts: runs of one shape-level); elsewhere its registers cost more than it saves (measured)
+    uint32_t same = 0;
+    for (uint32_t p = 1; p < in->n_pods; p++) same += cp.pod_shape[cp.queue[p]] == cp.pod_shape[cp.queue[p - 1]];
+    cp.cont_hint = in->n_pods > 1 && 2 * same >= in->n_pods ? 1 : 0;
+    if (const char* e = getenv("KP_CONT")) cp.cont_hint = atoi(e) != 0;  // tests: force either fast-lane variant
+  }
   return KP_OK;
 }
 
@@ -3090,6 +3098,7 @@ void BindSolve(SolveArgs& a, const Compiled& C, const SolveOffs& o, uint8_t* sh,
   a.req_res_mask = rmask;
   a.n_req_res = __builtin_popcount(rmask);
   a.timing = getenv("KP_TIMING") ? 1 : 0;
+  a.cont = C.cont_hint;
   a.n_groups = C.G;
   a.tg_key = (const int32_t*)(sh + o.tgk);
   a.tg_row = (const int32_t*)(sh + o.tgr);
@@ -3701,6 +3710,7 @@ int32_t kp_solve_run_cancellable(kp_solve_plan* plan, kp_cancel* cancel, kp_solv
   for (int i = 0; i < 8; i++) res->stats.fast_bails[i] = stats[32 + i];
   res->stats.reserved_offering_errors = stats[40];
   for (int i = 0; i < 5; i++) res->stats.order_chunks[i] = stats[41 + i];
+  res->stats.run_length_pods = stats[47];
   res->stats.host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   *out = res.release();
   return KP_OK;

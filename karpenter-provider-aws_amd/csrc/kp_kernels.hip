@@ -35,7 +35,7 @@
 // kernel into a measurement stub.
 #if !defined(KP_DIAG_BUILD) &&                                                                                       \
     (defined(FASTLANE) || defined(FL_NOTIME) || defined(FT_FINE) || defined(FAST_SCAN_MAX) ||                        \
-     defined(FAST_CHK_LIVE) || defined(FAST_EX_ROUNDS) || defined(SORT_DIAG) || defined(EX_DIAG) || defined(FEAS_MAX_BLOCKS) ||                 \
+     defined(FAST_CHK_LIVE) || defined(FAST_EX_ROUNDS) || defined(FAST_CONT) || defined(SORT_DIAG) || defined(EX_DIAG) || defined(FEAS_MAX_BLOCKS) ||                 \
      defined(FEASQ_EW) || defined(FEASQ_ROWS) || defined(FEASQ_B128) || defined(FEASQ_SKIP_EVAL))
 #error "a measurement knob is set outside a tools/ variant build (tools/kp_diag.h)"
 #endif
@@ -60,6 +60,9 @@
 #endif
 #ifndef FAST_EX_ROUNDS
 #define FAST_EX_ROUNDS 8  // existing nodes: 64-position rounds the fast lane scans before the 4-wave pre-pass takes over
+#endif
+#ifndef FAST_CONT
+#define FAST_CONT 1  // the continuation round (the previous pod's NodeClaim tested from registers first)
 #endif
 // Explicit address spaces: LDS data reached through a pointer would otherwise be read with FLAT loads (which wait
 // on the vector-memory counter too and take the long path); global rows get global_load.
@@ -1472,7 +1475,7 @@ __device__ __forceinline__ int sort_newnodeclaims_wave(P ord, P npods, int n, in
 // LDS reads in all). When pdqsort would do a stable move (n <= 12: insertion sort; n >= 50 with increasingHint:
 // partialInsertionSort) and the moved NodeClaim's new place is within the window, the ids already in registers
 // are written back shifted. Returns the cursor clamp (p), or -2: the general replay (sort_newnodeclaims_wave).
-__device__ __forceinline__ int sort_mut1_window(LdsI32 ord, LdsI32 npods, int n, int p) {
+__device__ __forceinline__ int sort_mut1_window(LdsI32 ord, LdsI32 npods, int n, int p, bool* moved = nullptr) {
   const int lane = LANE;
   const int i = p + lane;
   const int t = lane / 3;
@@ -1485,6 +1488,7 @@ __device__ __forceinline__ int sort_mut1_window(LdsI32 ord, LdsI32 npods, int n,
   const int K = __builtin_amdgcn_readfirstlane(key);  // npods of the mutated NodeClaim (position p)
   const uint64_t less = __ballot(lane > 0 && i < n && key < K);
   if (!((less >> 1) & 1)) return p;  // Less(p + 1, p) false: sort.Slice leaves the order as it is
+  if (moved) *moved = true;
   if (n > 12) {
     if (n < 50) return -2;
     const int prev = __shfl(pkey, lane > 0 ? lane - 1 : 0, 64);
@@ -1988,7 +1992,7 @@ __shared__ uint32_t fl_scratch[2 * KP_MAX_WORDS];
 struct FastState {
   int32_t qw_head, qw_n, qw_next, reserved_;
   int32_t qw_pod[64], qw_shape[64], qw_sl[64], qw_lastlen[64], qw_epoch[64];  // lane i: queue entry qw_head + i
-  uint64_t bytes, attempts, scanned, starts, fpods;
+  uint64_t bytes, attempts, scanned, starts, fpods, runpods;
   uint64_t fcyc[16];  // [0..5] phases; [6..13] finer probes (FT_FINE builds, exported in place of stats[16..23])
   uint32_t fbail[8];
 };
@@ -2026,7 +2030,9 @@ __device__ __forceinline__ bool cancel_set(const int32_t* flag) {
 // Places popped pods while they need no requirement merge; returns the number placed. A pod it cannot place is
 // handed to the full path through g_ctl[6] / g_ctl[26]. Called by wave 0 only. CHK: the order is chunked (the
 // directory in s_dyn, see chk_sort): the replay edits the blocks and the scan walks the live chunks, one per round.
-template <bool TOPO, bool CHK>
+// EX: the Solve has existing nodes (addToExistingNode on the wave); without, that code is compiled out, so it costs
+// the Solves without existing nodes no registers (measured: 9 % of config 2's kernel when only skipped at run time).
+template <bool TOPO, bool CHK, bool EX, bool CONT>
 __device__ __noinline__ int fast_lane(uint64_t kargs, int32_t LDS* s_dyn_arg, uint64_t pops_in_arg) {
   // a callee's arguments arrive in VGPRs and count as divergent: made provably uniform here, or every value and
   // branch that depends on them (the whole pod loop) would be compiled as divergent control flow
@@ -2082,6 +2088,7 @@ __device__ __noinline__ int fast_lane(uint64_t kargs, int32_t LDS* s_dyn_arg, ui
   // its lines back right after the stores waits for them to drain): remaining types, requests, threshold indices
   // (lane values), and its pre-check record. Only the fast lane writes NodeClaims during one call.
   int c_nc = -1, c_cat = 0, c_ver = 0, c_ts = 0;
+  int cont_w = -1, cont_sl = -1;  // the last commit's position and shape-level when it was an append on c_nc
   uint64_t c_X = 0, c_hm = 0;
   int64_t c_q = 0, c_r0 = 0, c_r1 = 0, c_r2 = 0, c_r3 = 0;
   int32_t c_fj = 0;
@@ -2093,7 +2100,7 @@ __device__ __noinline__ int fast_lane(uint64_t kargs, int32_t LDS* s_dyn_arg, ui
   NbUnits fnb{0, 0, 0};
   uint32_t n_app = 0, n_scan = 0;
     const bool tmg = A->timing != 0;
-#define FL_HAS_EX (A->n_existing != 0)
+#define FL_HAS_EX (EX)
     uint64_t ft = tmg ? __builtin_amdgcn_s_memtime() : 0;
 #define FTF(i)                                               \
   if (FT_FINE && tmg) {                                      \
@@ -2423,6 +2430,7 @@ if (!FL_NOTIME && tmg) {                                    \
           // the in-flight cursor is untouched (no in-flight scan): the next pod of this level reads the same one
           a_cur_prev_pos = cur;
           a_cur_prev_stamp = stamp;
+          cont_w = -1;
           pops++;
           if (lane == n_buf) {
             buf_pod = pod;
@@ -2458,6 +2466,8 @@ if (!FL_NOTIME && tmg) {                                    \
       const int n_nc = n_nc_all;
       FTF(8);
       int low;
+      bool n_moved = false;  // the pending mutation moved its NodeClaim (sort_mut1_window)
+      const bool mut_was1 = mut == 1 && mut_p == cont_w;  // ... and it is the previous pod's commit at cont_w
       if (CHK) {
         low = mut == 0 ? -1 : chk_sort(cd, (ChkCtl LDS*)&g_chk, A->chk_blk, n_nc, mut, mut_p, A->g_order, A->g_npods,
                                        &A->stats[31], h_ck, h_blk, h_id, h_key);
@@ -2473,7 +2483,7 @@ if (!FL_NOTIME && tmg) {                                    \
           break;
         }
       } else {
-        low = mut == 0 ? -1 : (mut == 1 ? sort_mut1_window(ord, npods, n_nc, mut_p) : -2);
+        low = mut == 0 ? -1 : (mut == 1 ? sort_mut1_window(ord, npods, n_nc, mut_p, &n_moved) : -2);
         if (low == -2) low = sort_newnodeclaims_wave(ord, npods, n_nc, mut, mut_p, 256, &A->stats[31]);
         if (low == -2) {  // a long shift: the full path sorts (the pending mutation is still in s_ctl[10..11])
           handoff = pod;
@@ -2508,12 +2518,20 @@ if (!FL_NOTIME && tmg) {                                    \
         }
         if (relaxed) epoch += 1;  // lastLen = map{}
         memo_pops++;
+        cont_w = -1;
         continue;
       }
       // addToInflightNode: pre-checks 64 positions at a time, then the append-path attempts in order. A long scan
       // is the full path's (512-lane pre-pass).
       int placed = -1, wpos = -1, why = FB_NONE, ipos = INT32_MAX;  // ipos: first count-independent pass (topology)
-      bool bail = !CHK && n_nc - start > FAST_SCAN_MAX;
+      // continuation: the previous pod (same shape-level) appended to NodeClaim c_nc at position cont_w, the replay
+      // left it there, and the first-fit scan starts there (every earlier position failed this level and is
+      // unchanged): the first candidate is c_nc itself, whose pre-check record, remaining types, requests and
+      // threshold indices the wave holds from that commit — no gathers for this round (c_nc is tagged with the
+      // level: memo NC_MERGED). A failed attempt falls back to the scan from the next position.
+      bool cont = CONT && FAST_CONT && !CHK && !TOPO && c_nc >= 0 && cont_w >= 0 && cont_w == start &&
+                  mut_was1 && !n_moved && sl == cont_sl && rr_b4p == 0 && c_hm == 0;
+      bool bail = !CHK && n_nc - start > FAST_SCAN_MAX && !cont;
       if (bail) why = FB_SCAN;
       if (lane == 0 && !bail) starts += start;
       // chunked order: the start position's chunk and slot, the window of chunks whose live mask is in lm
@@ -2558,14 +2576,28 @@ if (!FL_NOTIME && tmg) {                                    \
           nc = valid ? c_bid : 0;
           i = cd.start[ck] + lane;
           nscan = __popcll(__ballot(valid));
+        } else if (cont) {  // the continuation round: position start alone, from registers
+          if (base >= n_nc) break;
+          i = base + lane;
+          valid = lane == 0;
+          nc = valid ? c_nc : 0;
+          nscan = 1;
+          base += 1;
         } else {
           if (base >= n_nc) break;
+          if (n_nc - base > FAST_SCAN_MAX && base != start) {  // (after a failed continuation round: a long scan)
+            bail = true;
+            why = FB_SCAN;
+            break;
+          }
           i = base + lane;
           valid = i < n_nc;
           nc = valid ? ord[i] : 0;
           nscan = min(64, n_nc - base);
           base += 64;
         }
+        const bool cont_round = !CHK && cont;
+        cont = false;
         bool cand = false, tag = false, icand = false, pfail = false;
         int32_t ver = 0;
         HeadView hv{0, 0, 0, 0, 0, 0};
@@ -2586,7 +2618,7 @@ if (!FL_NOTIME && tmg) {                                    \
         }
         if (valid) {
           // every gather issued unconditionally: one round trip
-          const int32_t fl = nc < A->ncc ? A->nc_fail[(size_t)sl * A->ncc + nc] : -2;
+          const int32_t fl = cont_round ? NC_MERGED : nc < A->ncc ? A->nc_fail[(size_t)sl * A->ncc + nc] : -2;
           if (nc == c_nc) hv = HeadView{c_r0, c_r1, c_r2, c_r3, c_ver, c_ts};
           else hv = load_head(A->nc_head + nc, four);
           ver = hv.ver;
@@ -2810,6 +2842,8 @@ if (!FL_NOTIME && tmg) {                                    \
         break;
       }
       pops++;
+      cont_w = c_nc >= 0 ? wpos : -1;  // (c_nc: this commit was an append, its NodeClaim held in registers)
+      cont_sl = sl;
       // cursor: every position before the winner failed; with owned groups, before the first position that passed
       // the count-independent checks (a zone-count failure may pass later), as the full path
       const int cpos = TOPO && t_n ? min(ipos, wpos) : wpos;
@@ -2832,6 +2866,94 @@ if (!FL_NOTIME && tmg) {                                    \
         A->events[n_ev + lane] = buf_pod;
         n_ev += 64;
         n_buf = 0;
+      }
+      // ---- run-length commit (the continuation variant: queue runs of one shape-level). The next k window entries
+      // share this pod's level, and for each of them, one at a time, the reference would do exactly what it just did:
+      // sort.Slice leaves this NodeClaim where it is (the entry after it keeps len(Pods) >= its own), the first-fit
+      // scan starts at its position (every earlier one failed the level and is unchanged), and NodeClaim.Add is Fits
+      // over its remaining types with every requested resource still under the threshold value it just passed (the
+      // remaining types, and so the result, unchanged). k is the largest count for which all of that holds in
+      // closed form; the k pods are committed at once: requests + k * pod, len(Pods) + k, headroom - k * pod, version
+      // + k, the same cursor and one mutation-stack entry for the k identical ones. Anything else: the pod loop.
+      if (CONT && cont_w == wpos && c_cat == 0 && c_hm == 0 && rr_b4p == 0 && n_rrp <= 4) {
+        const int e = off + 1 + lane;  // lane j: the j-th window entry after this pod
+        const int e_sl = __shfl(qw_sl, e & 63, 64), e_ep = __shfl(qw_epoch, e & 63, 64),
+                  e_ll = __shfl(qw_lastlen, e & 63, 64), e_pod = __shfl(qw_pod, e & 63, 64);
+        // Queue.Pop would stop at an entry last pushed at the length it would pop it at (lastLen)
+        const bool ok = e < qw_n && e_sl == sl && !(e_ep == epoch && e_ll == q_len - lane);
+        const uint64_t okm = __ballot(ok);
+        int k = (int)__builtin_ctzll(~okm);
+        // sort.Slice: batched pod m (1-based) replays len(Pods) = c + m - 1 at wpos against the next entry's
+        const int c1 = npods[placed];
+        const int nxt = wpos + 1 < n_nc_all ? npods[ord[wpos + 1]] : INT32_MAX;
+        if (nxt != INT32_MAX) k = min(k, max(0, nxt - c1 + 1));
+        // Fits: every requested resource stays at or under the threshold value of its current index
+        int kf = INT32_MAX;
+        if (lane < KP_NRES && preq_lane > 0) {
+          const int slot = g_hdr[0].fit_slot[lane], n = g_hdr[0].fit_n[lane];
+          kf = 0;
+          if (slot >= 0 && c_fj < n) {
+            const int64_t room = g_fitv[slot * FITV_CAP + c_fj] - c_q;
+            kf = room >= 0 ? (int)min<int64_t>(room / preq_lane, 64) : 0;
+          }
+        }
+        k = min(k, wave_min_i32(kf));
+        k = min(k, 63);
+        if (k > 0) {
+          const int64_t kk = k;
+          // the NodeClaim: requests, len(Pods), pre-check record (headroom, version)
+          c_q += kk * preq_lane;
+          if (lane < KP_NRES) A->nc_requests[(size_t)placed * KP_NRES + lane] = c_q;
+          c_r0 -= kk * pr0, c_r1 -= kk * pr1;
+          if (four) c_r2 -= kk * pr2, c_r3 -= kk * pr3;
+          c_ver += k;
+          if (lane == 0) {
+            npods[placed] = c1 + k;
+            int4* hp = reinterpret_cast<int4*>(A->nc_head + placed);
+            hp[0] = make_int4((int)c_r0, (int)(c_r0 >> 32), (int)c_r1, (int)(c_r1 >> 32));
+            if (four) hp[1] = make_int4((int)c_r2, (int)(c_r2 >> 32), (int)c_r3, (int)(c_r3 >> 32));
+            A->nc_head[placed].ver = c_ver;
+          }
+          // the k replays: one mutation-stack entry at wpos (k identical pushes leave just the last), the cursor
+          stk_t += k;
+          mstack_push_reg((int32_t LDS*)s_stk[0], stk_n, stk_lost, stk_t, wpos);
+          a_cur_prev_stamp = stk_t;
+          if (lane == 0) {
+            A->cur_nc[2 * sl] = wpos;
+            A->cur_nc[2 * sl + 1] = stk_t;
+          }
+          // the k pods: popped, placed (events in queue order after the buffered ones)
+          if (n_buf + k > 64) {
+            if (lane < n_buf) {
+              A->placement[buf_pod] = buf_pl;
+              A->events[n_ev + lane] = buf_pod;
+            }
+            n_ev += n_buf;
+            n_buf = 0;
+          }
+          const int bp = __shfl(e_pod, (lane - n_buf) & 63, 64);
+          if (lane >= n_buf && lane < n_buf + k) {
+            buf_pod = bp;
+            buf_pl = placed;
+          }
+          n_buf += k;
+          if (n_buf == 64) {
+            A->placement[buf_pod] = buf_pl;
+            A->events[n_ev + lane] = buf_pod;
+            n_ev += 64;
+            n_buf = 0;
+          }
+          q_head += k;
+          if (q_head >= A->n_pods) q_head -= A->n_pods;
+          q_len -= k;
+          qw_next = off + 1 + k;
+          pf_off = -1;
+          pops += k;
+          attempts += k;
+          n_app += (uint32_t)k;
+          n_scan += (uint32_t)k;
+          if (lane == 0) S->runpods += k;
+        }
       }
       FT(5);
     }
@@ -3003,7 +3125,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a0, const Solv
     g_fast.qw_head = 0;  // the fast lane's Queue window (empty) and counters
     g_fast.qw_n = 0;
     g_fast.qw_next = -1;
-    g_fast.bytes = g_fast.attempts = g_fast.scanned = g_fast.starts = g_fast.fpods = 0;
+    g_fast.bytes = g_fast.attempts = g_fast.scanned = g_fast.starts = g_fast.fpods = g_fast.runpods = 0;
     for (int i = 0; i < 16; i++) g_fast.fcyc[i] = 0;
     for (int i = 0; i < 8; i++) g_fast.fbail[i] = 0;
     if (SORT_DIAG || EX_DIAG)
@@ -3026,8 +3148,18 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a0, const Solv
       } else {
         // the Solve's argument block: the kernarg segment (a0 is the first argument), or its entry of the batch
         const uint64_t kargs = BATCH ? (uint64_t)&batch[blockIdx.x] : (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
-        const int placed_fast = s_ctl[5] == 2 ? fast_lane<TOPO, true>(kargs, (int32_t LDS*)s_dyn, pops)
-                                              : fast_lane<TOPO, false>(kargs, (int32_t LDS*)s_dyn, pops);
+        // instantiations: chunked order or not, existing nodes or none (compiled out), the continuation round (LDS
+        // order, no topology, queue runs of one shape)
+        int placed_fast;
+        if (s_ctl[5] == 2)
+          placed_fast = a.n_existing ? fast_lane<TOPO, true, true, false>(kargs, (int32_t LDS*)s_dyn, pops)
+                                     : fast_lane<TOPO, true, false, false>(kargs, (int32_t LDS*)s_dyn, pops);
+        else if (a.n_existing)
+          placed_fast = fast_lane<TOPO, false, true, false>(kargs, (int32_t LDS*)s_dyn, pops);
+        else if (!TOPO && a.cont)
+          placed_fast = fast_lane<TOPO, false, false, !TOPO>(kargs, (int32_t LDS*)s_dyn, pops);
+        else
+          placed_fast = fast_lane<TOPO, false, false, false>(kargs, (int32_t LDS*)s_dyn, pops);
         pops += placed_fast;
         fl_fail = placed_fast ? 0 : fl_fail + 1;
         fl_skip = fl_fail >= 2 ? min(1 << min(fl_fail - 2, 6), 64) : 0;
@@ -3871,6 +4003,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a0, const Solv
     a.stats[43] = g_chk.removals;
     a.stats[44] = g_chk.rebuilds;
     a.stats[45] = s_ctl[5];
+    a.stats[47] = g_fast.runpods;
   }
   if (s_ctl[5] == 1)
     for (int i = tid; i < s_ctl[2]; i += NT) {
@@ -4409,7 +4542,7 @@ __global__ __launch_bounds__(FEASB_WAVES * 64, FEASB_MINW) void feasibility_bits
 #define FEASQ_SKIP_EVAL 0  // measurement only: decode + copies, no type-set work (wrong masks)
 #endif
 static_assert(KP_DIAG_BUILD || (FASTLANE == 1 && FL_NOTIME == 1 && FT_FINE == 0 && FAST_SCAN_MAX == 512 &&
-                                 FAST_CHK_LIVE == 8 && FAST_EX_ROUNDS == 8 && SORT_DIAG == 0 && EX_DIAG == 0 && FEAS_MAX_BLOCKS == 65536 &&
+                                 FAST_CHK_LIVE == 8 && FAST_EX_ROUNDS == 8 && FAST_CONT == 1 && SORT_DIAG == 0 && EX_DIAG == 0 && FEAS_MAX_BLOCKS == 65536 &&
                                  FEASQ_EW == 7 && FEASQ_ROWS == 28 && FEASQ_B128 == 1 && FEASQ_SKIP_EVAL == 0),
               "the production build carries the production values of every measurement knob");
 __global__ __launch_bounds__(FEASB_WAVES * 64, FEASB_MINW) void feasibility_quad_kernel(FeasArgs a) {

@@ -105,7 +105,11 @@ def load_lib(path=None):
         "kp_choice_reduce": (C.c_int32, [P(abi.Choice), C.c_uint32, P(abi.Choice)]),
     }
     for name, (res, args) in sig.items():
-        f = getattr(lib, name)
+        f = getattr(lib, name, None)
+        if f is None and path != LIB_PATH:  # a tools/ build of an older commit (A/B): its ABI may lack newer entries
+            continue
+        if f is None:
+            raise KPError(abi.KP_E_DEVICE, f"{path} lacks {name}: rebuild (__graft_entry__.build())")
         f.restype = res
         f.argtypes = args
     _LIB = lib

@@ -191,7 +191,7 @@ class SolveStats(C.Structure):
                 ("scanned", C.c_uint64), ("cursor_starts", C.c_uint64), ("attempt_cycles", C.c_uint64 * 8),
                 ("catalog_ms", C.c_double), ("catalog_cached", C.c_uint32), ("catalog_refreshed", C.c_uint32),
                 ("fast_pods", C.c_uint64), ("fast_cycles", C.c_uint64 * 6), ("slow_sorts", C.c_uint64),
-                ("fast_bails", C.c_uint64 * 8), ("reserved_offering_errors", C.c_uint64),
+                ("fast_bails", C.c_uint64 * 8), ("reserved_offering_errors", C.c_uint64), ("run_length_pods", C.c_uint64),
                 ("order_chunks", C.c_uint64 * 5)]
 
 

@@ -100,3 +100,20 @@ def test_device_uid_strings_larger_batch(ctx, catalog):
     prob.pod_uid[:] = 0
     prob.pod_uid_str = _uids(rng, prob.n_pods)
     check_same(kpamd.Scheduler(ctx, prob).solve(), pyoracle.solve(prob))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("spread", [False, True])
+def test_cluster_null_uid_is_invalid(ctx, catalog, general_mode, spread):
+    """A NULL entry in kp_cluster.pod_uids is KP_E_INVAL on every consolidation path (batched kernels, the general
+    path batched or per subset), as kp_solve rejects it — not a silent fallback to uid_key."""
+    import kpamd
+    from kpamd import synth
+    cl = synth.spread_cluster(catalog, 40) if spread else synth.config4(catalog, n_nodes=40)
+    rng = np.random.default_rng(3)
+    uids = _uids(rng, len(cl.pod_shape))
+    uids[len(uids) // 2] = None
+    cl.pod_uid_str = uids
+    with pytest.raises(kpamd.KPError) as e:
+        kpamd.ClusterPlan(ctx, cl)
+    assert e.value.code == kpamd.abi.KP_E_INVAL

@@ -1,0 +1,25 @@
+"""solve_kernel time of one config (default 2): 1 warmup + 5 timed kp_solve calls; prints the kernel ms (min, mean).
+Works with any libkp build selected by KP_LIB (older ABIs included). usage: kernel_time.py [2|3|5] [pods]"""
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "karpenter-provider-aws_amd"))
+import kpamd  # noqa: E402
+from kpamd import catalog, synth  # noqa: E402
+
+cfg = sys.argv[1] if len(sys.argv) > 1 else "2"
+if cfg.endswith("-off"):  # the fast lane without its continuation variant (kp_solve's choice overridden)
+    os.environ["KP_CONT"] = "0"
+    cfg = cfg[:-4]
+n = int(sys.argv[2]) if len(sys.argv) > 2 else {"2": 50000, "2b": 50000, "3": 100000, "5": 100000}[cfg]
+lib = kpamd.load_lib()
+cat = catalog.build_catalog(lib)
+prob = {"2": lambda: synth.config2(cat, n_pods=n, seed=2), "2b": lambda: synth.config2(cat, n_pods=n, seed=2, burst=True),
+        "3": lambda: synth.config3(cat, n_pods=n), "5": lambda: synth.config5(cat, n_pods=n)}[cfg]()
+ctx = kpamd.Context(0)
+sched = kpamd.Scheduler(ctx, prob)
+sched.solve(read=False)
+ks = [sched.solve(read=False)["stats"]["solve_kernel_ms"] for _ in range(5)]
+print(json.dumps({"min_ms": round(min(ks), 2), "mean_ms": round(sum(ks) / len(ks), 2)}))

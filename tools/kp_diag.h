@@ -12,6 +12,8 @@
  *   FT_FINE [0]          finer fast-lane probes in place of the full path's attempt split
  *   FAST_SCAN_MAX [512]  longest first-fit scan the fast lane takes on
  *   FAST_CHK_LIVE [8]    chunked order: live chunks the fast lane scans before the 4-wave pre-pass
+ *   FAST_EX_ROUNDS [8]   existing nodes: 64-position rounds the fast lane scans before the full path
+ *   FAST_CONT [1]        the continuation round (the previous commit's NodeClaim first, from registers)
  *   SORT_DIAG [0]        the full path's sort split in stats[25..30]
  *   EX_DIAG [0]          the existing-node scan split in stats[25..30]
  *   FEAS_MAX_BLOCKS [65536], FEASQ_EW [7], FEASQ_ROWS [28], FEASQ_B128 [1]  feasibility grid / block shape

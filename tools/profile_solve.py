@@ -11,10 +11,10 @@ import kpamd  # noqa: E402
 from kpamd import catalog, synth  # noqa: E402
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "2"
-n = int(sys.argv[2]) if len(sys.argv) > 2 else {"2": 50000, "3": 100000, "5": 300000}[cfg]
+n = int(sys.argv[2]) if len(sys.argv) > 2 else {"2": 50000, "2b": 50000, "3": 100000, "5": 300000}[cfg]
 lib = kpamd.load_lib()
 cat = catalog.build_catalog(lib)
-prob = {"2": lambda: synth.config2(cat, n_pods=n, seed=2), "3": lambda: synth.config3(cat, n_pods=n, n_deployments=int(os.environ.get("KP_C3_DEPLOYMENTS", "1000"))),
+prob = {"2": lambda: synth.config2(cat, n_pods=n, seed=2), "2b": lambda: synth.config2(cat, n_pods=n, seed=2, burst=True), "3": lambda: synth.config3(cat, n_pods=n, n_deployments=int(os.environ.get("KP_C3_DEPLOYMENTS", "1000"))),
         "5": lambda: synth.config5(cat, n_pods=n)}[cfg]()
 ctx = kpamd.Context(0)
 sched = kpamd.Scheduler(ctx, prob)
