@@ -139,6 +139,7 @@ RawReqs ParseReqs(const kp_requirements& in) {
 }
 RawReqs LabelReqs(const kp_label* l, uint32_t n, bool drop_hostname) {
   RawReqs out;
+  out.reserve(n + 1);
   for (uint32_t i = 0; i < n; i++) {
     string k = Normalize(l[i].key ? l[i].key : "");
     if (drop_hostname && k == kHostname) continue;
@@ -431,9 +432,10 @@ KReqs Single(const Dict& d, const RawReq& r) {
 
 // A = A.Add(B) per key (Requirement.Intersection for shared keys).
 void HostAdd(const Dict& d, KReqs& A, const KReqs& B) {
-  for (int k = 0; k < d.dd.K; k++) {
+  // B's keys in increasing order (each key is independent of the others)
+  for (uint64_t km = B.present & (d.dd.K >= 64 ? ~0ull : (1ull << d.dd.K) - 1); km; km &= km - 1) {
+    const int k = __builtin_ctzll(km);
     const uint64_t kb = 1ull << k;
-    if (!(B.present & kb)) continue;
     const int nw = nwords(d, k);
     const bool bnd = k < KP_MAX_BOUND_KEYS;
     if (!(A.present & kb)) {
@@ -1525,6 +1527,18 @@ bool HasPnsToleration(const kp_pod_shape& sh) {
   return false;
 }
 
+// KP_HOST_TIMING=1: host compile phases on stderr (diagnostics only)
+struct PhaseTimer {
+  bool on = getenv("KP_HOST_TIMING") != nullptr;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  void lap(const char* what) {
+    if (!on) return;
+    const auto n = std::chrono::steady_clock::now();
+    fprintf(stderr, "[kp compile] %-22s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(n - t).count());
+    t = n;
+  }
+};
+
 int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector<RawReqs>>& strict_levels,
                         const vector<vector<vector<int>>>& spread_levels, const vector<int>& np_taintset,
                         const vector<vector<vector<RawReqs>>>& filter_levels) {
@@ -1549,6 +1563,7 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
     any |= in->bound_pods[b].n_anti_affinity > 0;
   }
   if (!any) return KP_OK;
+  PhaseTimer pt;
   if (cp.track_nodes) {
     cp.node_cnt.assign(in->n_existing, {});
     cp.node_reg.assign(in->n_existing, {});
@@ -1558,12 +1573,33 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
   }
   vector<int> ex_pos(in->n_existing);
   for (int e = 0; e < E; e++) ex_pos[cp.ex_input[e]] = e;
-  vector<std::map<string, string>> node_labels(in->n_existing);
   vector<KReqs> node_reqs(in->n_existing);
-  for (uint32_t i = 0; i < in->n_existing; i++) {
-    node_labels[i] = LabelMap(in->existing[i].labels, in->existing[i].n_labels);
-    node_reqs[i] = cp.ex_reqs[ex_pos[i]];
-  }
+  for (uint32_t i = 0; i < in->n_existing; i++) node_reqs[i] = cp.ex_reqs[ex_pos[i]];
+  // the existing nodes' value of one label key (LabelMap's: the last entry wins; nullptr: no such label), computed
+  // once per key that some group reads (a few keys against thousands of nodes)
+  std::unordered_map<string, vector<const char*>> node_kv;
+  auto node_vals = [&](const string& key) -> const vector<const char*>& {
+    auto it = node_kv.find(key);
+    if (it != node_kv.end()) return it->second;
+    vector<const char*> v(in->n_existing, nullptr);
+    for (uint32_t i = 0; i < in->n_existing; i++) {
+      const kp_existing_node& e = in->existing[i];
+      for (uint32_t j = 0; j < e.n_labels; j++)
+        if (key == (e.labels[j].key ? e.labels[j].key : "")) v[i] = e.labels[j].value ? e.labels[j].value : "";
+    }
+    return node_kv.emplace(key, std::move(v)).first->second;
+  };
+  // ... and its value ordinal for a dictionary key k (-1: no such label)
+  std::unordered_map<int, vector<int>> node_ko;
+  auto node_ords = [&](int k) -> const vector<int>& {
+    auto it = node_ko.find(k);
+    if (it != node_ko.end()) return it->second;
+    const vector<const char*>& v = node_vals(d.keys[k]);
+    vector<int> o(in->n_existing, -1);
+    for (uint32_t i = 0; i < in->n_existing; i++)
+      if (v[i]) o[i] = d.bit(k, v[i]) - k * 64;
+    return node_ko.emplace(k, std::move(o)).first->second;
+  };
   // buildDomainGroups for one key: value ordinal -> taint sets of the NodePools offering it
   std::map<int, vector<uint64_t>> domain_tsets;  // key -> [64] taint-set masks
   auto domains_of = [&](int k) -> const vector<uint64_t>& {
@@ -1603,20 +1639,54 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
     vector<uint32_t> nodes;  // input indices, one entry per bound pod
   };
   vector<BoundSet> bsets;
+  // the sets indexed by (namespace, label) and by namespace: a matchLabels selector only tests the sets carrying its
+  // first label (index lists are in set order, so a group visits its sets in the order a full scan would)
+  std::unordered_map<string, vector<int>> bs_by_label, bs_by_ns;
   {
-    std::map<std::pair<string, std::map<string, string>>, int> idx;
+    std::unordered_map<string, int> idx;  // canonical (namespace, LabelMap) -> set
+    vector<std::pair<const char*, const char*>> kv;
+    string canon;
     for (uint32_t b = 0; b < in->n_bound_pods; b++) {
       const kp_bound_pod& bp = in->bound_pods[b];
       if (bp.node >= in->n_existing) return fail(KP_E_INVAL, "bound pod %u: node %u", b, bp.node);
-      auto key = std::make_pair(string(bp.namespace_ ? bp.namespace_ : ""), LabelMap(bp.labels, bp.n_labels));
-      auto it = idx.find(key);
+      // LabelMap without the map: the entries by key, stable, the last of equal keys kept
+      kv.clear();
+      for (uint32_t j = 0; j < bp.n_labels; j++)
+        kv.push_back({bp.labels[j].key ? bp.labels[j].key : "", bp.labels[j].value ? bp.labels[j].value : ""});
+      std::stable_sort(kv.begin(), kv.end(), [](const auto& x, const auto& y) { return strcmp(x.first, y.first) < 0; });
+      canon.assign(bp.namespace_ ? bp.namespace_ : "");
+      for (size_t j = 0; j < kv.size(); j++) {
+        if (j + 1 < kv.size() && strcmp(kv[j].first, kv[j + 1].first) == 0) continue;
+        canon += '\x01';
+        canon += kv[j].first;
+        canon += '\x02';
+        canon += kv[j].second;
+      }
+      auto it = idx.find(canon);
       if (it == idx.end()) {
-        it = idx.emplace(key, (int)bsets.size()).first;
-        bsets.push_back({key.first, key.second, {}});
+        const int id = (int)bsets.size();
+        it = idx.emplace(canon, id).first;
+        const string ns = bp.namespace_ ? bp.namespace_ : "";
+        bsets.push_back({ns, LabelMap(bp.labels, bp.n_labels), {}});
+        bs_by_ns[ns].push_back(id);
+        for (auto& l : bsets.back().labels) bs_by_label[ns + '\x01' + l.first + '\x01' + l.second].push_back(id);
       }
       bsets[it->second].nodes.push_back(bp.node);
     }
   }
+  static const vector<int> kNoSets;
+  // the bound-pod sets a selector can match in namespace ns (a superset; callers still test SelectorMatches)
+  auto sets_for = [&](const kp_label_selector& sel, const string& ns) -> const vector<int>& {
+    if (sel.is_nil) return kNoSets;
+    if (sel.n_match_labels) {
+      auto it = bs_by_label.find(ns + '\x01' + (sel.match_labels[0].key ? sel.match_labels[0].key : "") + '\x01' +
+                                 (sel.match_labels[0].value ? sel.match_labels[0].value : ""));
+      return it == bs_by_label.end() ? kNoSets : it->second;
+    }
+    auto it = bs_by_ns.find(ns);
+    return it == bs_by_ns.end() ? kNoSets : it->second;
+  };
+  pt.lap("  topo: labels+bsets");
   std::map<string, int> ids;
   std::map<string, uint64_t> node_domains;
   vector<int> g_shape;  // shape that created the group (its tolerations / filter)
@@ -1718,21 +1788,22 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
       return false;
     };
     const string ns = sh.namespace_ ? sh.namespace_ : "";
-    for (auto& bs : bsets) {
-      if (ns != bs.ns || !SelectorMatches(t.selector, bs.labels)) continue;
+    const vector<int>* ords = k >= 0 ? &node_ords(k) : nullptr;  // value ordinal per node (key k's values: word k)
+    for (int bi : sets_for(t.selector, ns)) {
+      const BoundSet& bs = bsets[bi];
+      if (!SelectorMatches(t.selector, bs.labels)) continue;
       for (const uint32_t ni : bs.nodes) {
-      if (row >= 0) {  // hostname: the node's label or, failing that, its name — one domain per node
-        if (!filter_ok(ni)) continue;
-        uint8_t& c = cp.hcnt0[(size_t)row * std::max(E, 1) + ex_pos[ni]];
-        if (c < 254) c++;  // (255: an unregistered domain, below)
-      } else {
-        auto lv = node_labels[ni].find(key);
-        if (lv == node_labels[ni].end() || !filter_ok(ni)) continue;
-        const int ord = d.bit(k, lv->second) - k * 64;  // value ordinal (key k's values live in word k)
-        cp.tg_cnt[(size_t)g * 64 + ord]++;
-        cp.tg_reg[g] |= 1ull << ord;
-        if (cp.track_nodes) cp.node_cnt[ni].push_back(g * 64 + ord);
-      }
+        if (row >= 0) {  // hostname: the node's label or, failing that, its name — one domain per node
+          if (!filter_ok(ni)) continue;
+          uint8_t& c = cp.hcnt0[(size_t)row * std::max(E, 1) + ex_pos[ni]];
+          if (c < 254) c++;  // (255: an unregistered domain, below)
+        } else {
+          const int ord = (*ords)[ni];
+          if (ord < 0 || !filter_ok(ni)) continue;
+          cp.tg_cnt[(size_t)g * 64 + ord]++;
+          cp.tg_reg[g] |= 1ull << ord;
+          if (cp.track_nodes) cp.node_cnt[ni].push_back(g * 64 + ord);
+        }
       }
     }
     if (k >= 0) {  // the existing nodes' domains depend only on (key, node filter): cached across groups
@@ -1740,42 +1811,34 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
       auto it = node_domains.find(fid);
       if (it == node_domains.end()) {
         uint64_t m = 0;
-        for (uint32_t ni = 0; ni < in->n_existing; ni++) {
-          auto lv = node_labels[ni].find(key);
-          if (lv == node_labels[ni].end() || !filter_ok(ni)) continue;
-          m |= 1ull << (d.bit(k, lv->second) - k * 64);
-        }
+        for (uint32_t ni = 0; ni < in->n_existing; ni++)
+          if ((*ords)[ni] >= 0 && filter_ok(ni)) m |= 1ull << (*ords)[ni];
         it = node_domains.emplace(fid, m).first;
       }
       cp.tg_reg[g] |= it->second;
       if (cp.track_nodes)
-        for (uint32_t ni = 0; ni < in->n_existing; ni++) {
-          auto lv = node_labels[ni].find(key);
-          if (lv != node_labels[ni].end() && filter_ok(ni)) cp.node_reg[ni].push_back(g * 64 + d.bit(k, lv->second) - k * 64);
-        }
+        for (uint32_t ni = 0; ni < in->n_existing; ni++)
+          if ((*ords)[ni] >= 0 && filter_ok(ni)) cp.node_reg[ni].push_back(g * 64 + (*ords)[ni]);
     }
-    if (row >= 0 && cp.track_nodes && E) {  // the positions a not-live creation leaves unregistered (below)
+    if (row >= 0 && E && (cp.track_nodes || !live)) {
+      // the nodes this group registers: the filter-matching ones with a hostname label, and the nodes of the pods it
+      // counted (both uses below)
+      const vector<const char*>& hn = node_vals(kHostname);
       vector<char> counted(in->n_existing, 0);
-      for (auto& bs : bsets)
-        if (ns == bs.ns && SelectorMatches(t.selector, bs.labels))
-          for (const uint32_t ni : bs.nodes) counted[ni] = 1;
-      for (uint32_t ni = 0; ni < in->n_existing; ni++)
-        if (!(filter_ok(ni) && (node_labels[ni].count(kHostname) || counted[ni]))) cp.tg_unreg[g].push_back(ex_pos[ni]);
-    }
-    if (row >= 0 && !live && E) {
+      for (int bi : sets_for(t.selector, ns))
+        if (SelectorMatches(t.selector, bsets[bi].labels))
+          for (const uint32_t ni : bsets[bi].nodes) counted[ni] = 1;
+      // the positions a not-live creation leaves unregistered (below)
+      if (cp.track_nodes)
+        for (uint32_t ni = 0; ni < in->n_existing; ni++)
+          if (!(filter_ok(ni) && (hn[ni] || counted[ni]))) cp.tg_unreg[g].push_back(ex_pos[ni]);
       // a hostname group a relaxation creates (Topology.Update after NewTopology): its domains are only what
-      // countDomains registers, the filter-matching nodes with a hostname label and the nodes of the pods it counted
-      // (NewTopology's Register of every existing node came before it). An unregistered node holds 255: the spread
-      // test fails on it until a Record registers it; the NodeClaims created before the group get 255 on the device
-      // when the group comes to exist.
-      vector<char> counted(in->n_existing, 0);
-      for (auto& bs : bsets)
-        if (ns == bs.ns && SelectorMatches(t.selector, bs.labels))
-          for (const uint32_t ni : bs.nodes) counted[ni] = 1;
-      for (uint32_t ni = 0; ni < in->n_existing; ni++) {
-        const bool reg = filter_ok(ni) && (node_labels[ni].count(kHostname) || counted[ni]);
-        if (!reg) cp.hcnt0[(size_t)row * E + ex_pos[ni]] = 255;
-      }
+      // countDomains registers (NewTopology's Register of every existing node came before it). An unregistered node
+      // holds 255: the spread test fails on it until a Record registers it; the NodeClaims created before the group
+      // get 255 on the device when the group comes to exist.
+      if (!live)
+        for (uint32_t ni = 0; ni < in->n_existing; ni++)
+          if (!(filter_ok(ni) && (hn[ni] || counted[ni]))) cp.hcnt0[(size_t)row * E + ex_pos[ni]] = 255;
     }
     return g;
   };
@@ -1817,9 +1880,8 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
       }
     } else {
       const int k = cp.tg_key[g];
-      auto lv = node_labels[ni].find(d.keys[k]);
-      if (lv == node_labels[ni].end()) return;
-      const int ord = d.bit(k, lv->second) - k * 64;
+      const int ord = node_ords(k)[ni];
+      if (ord < 0) return;
       cp.tg_cnt[(size_t)g * 64 + ord]++;
       cp.tg_reg[g] |= 1ull << ord;
       if (cp.track_nodes) cp.node_cnt[ni].push_back(g * 64 + ord);
@@ -1873,22 +1935,28 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
       for (int b = 0; b < 64; b++)
         if (dm[b]) reg |= 1ull << b;
       if (cp.track_nodes) cp.tg_reg_static[g] = reg;
+      const vector<int>& ords = node_ords(k);
       for (uint32_t ni = 0; ni < in->n_existing; ni++) {
-        auto lv = node_labels[ni].find(key);
-        if (lv != node_labels[ni].end()) {
-          reg |= 1ull << (d.bit(k, lv->second) - k * 64);
-          if (cp.track_nodes) cp.node_reg[ni].push_back(g * 64 + d.bit(k, lv->second) - k * 64);
+        if (ords[ni] >= 0) {
+          reg |= 1ull << ords[ni];
+          if (cp.track_nodes) cp.node_reg[ni].push_back(g * 64 + ords[ni]);
         }
       }
     }
     cp.tg_reg.push_back(reg);
     for (int b = 0; b < 64; b++) cp.tg_cnt.push_back(0);
     if (row >= 0) cp.hcnt0.resize((size_t)cp.GH * std::max(E, 1), 0);
-    if (!inverse)
-      for (auto& bs : bsets) {
-        if (!nss.count(bs.ns) || !SelectorMatches(t.selector, bs.labels)) continue;
-        for (const uint32_t ni : bs.nodes) record_bound(g, ni);
+    if (!inverse) {  // (the sets of every namespace the term selects, in set order)
+      vector<int> sets;
+      for (const string& n : nss) {
+        const vector<int>& v = sets_for(t.selector, n);
+        sets.insert(sets.end(), v.begin(), v.end());
       }
+      std::sort(sets.begin(), sets.end());
+      for (int bi : sets)
+        if (SelectorMatches(t.selector, bsets[bi].labels))
+          for (const uint32_t ni : bsets[bi].nodes) record_bound(g, ni);
+    }
     return g;
   };
   for (uint32_t p = 0; p < in->n_pods; p++) {  // NewTopology: Update(pod) in pod order
@@ -1909,6 +1977,7 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
       sgroup[s].push_back(g);
     }
   }
+  pt.lap("  topo: NewTopology");
   vector<int> inverse_groups;  // updateInverseAffinities: after the batch's groups
   for (uint32_t b = 0; b < in->n_bound_pods; b++) {
     const kp_bound_pod& bp = in->bound_pods[b];
@@ -1949,6 +2018,7 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
     if (cp.track_nodes)  // sgroup: the level-0 spread groups first, then the pod (anti-)affinity groups
       cp.shape_l0[s].assign(sgroup[s].begin(), sgroup[s].begin() + std::min<size_t>(sgroup[s].size(), sh.n_topology_spread));
   }
+  pt.lap("  topo: other groups");
   if (cp.G == 0) return KP_OK;
   if ((size_t)cp.GH * (size_t)(E + in->n_pods) > ((size_t)1 << 31))
     return fail(KP_E_UNSUPPORTED, "%d hostname topologies x %u nodes", cp.GH, E + in->n_pods);
@@ -1992,6 +2062,7 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
     cp.shape_rec_n[s] = (int32_t)recs[s].size();
     cp.rec_list.insert(cp.rec_list.end(), recs[s].begin(), recs[s].end());
   }
+  pt.lap("  topo: record lists");
   // owned groups per shape-level: (group, self-selecting, podDomains mask over the key's value ordinals)
   for (uint32_t s = 0; s < in->n_shapes; s++) {
     const kp_pod_shape& sh = in->shapes[s];
@@ -2032,6 +2103,7 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
       }
     }
   }
+  pt.lap("  topo: owned");
   // shape-levels the fast lane may take: at most 4 owned groups, every owned and every recorded group a spread
   // (maxSkew > 0) and no recorded group with node-filter terms (the fast lane's Record reads the NodeClaim's value
   // codes); pods of other levels (affinity, anti-affinity, filtered groups) stay on the full path
@@ -2057,11 +2129,9 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
   cp.ex_tcode.assign((size_t)std::max(cp.TK, 1) * std::max(E, 1), 0xFF);
   for (int k = 0; k < KP_MAX_KEYS; k++) {
     if (cp.tkey_slot[k] < 0) continue;
-    for (int e = 0; e < E; e++) {
-      auto lv = node_labels[cp.ex_input[e]].find(d.keys[k]);
-      if (lv != node_labels[cp.ex_input[e]].end())
-        cp.ex_tcode[(size_t)cp.tkey_slot[k] * E + e] = (uint8_t)(d.bit(k, lv->second) - k * 64);
-    }
+    const vector<int>& ords = node_ords(k);
+    for (int e = 0; e < E; e++)
+      if (ords[cp.ex_input[e]] >= 0) cp.ex_tcode[(size_t)cp.tkey_slot[k] * E + e] = (uint8_t)ords[cp.ex_input[e]];
   }
   if (cp.tg_terms.empty()) {
     KReqs z;
@@ -2318,6 +2388,7 @@ int32_t ParseSolve(const kp_solve_in* in, SolveRaw& raw) {
       raw.spread_levels[s].push_back(raw.spread_levels[s].back());
     }
   }
+  PhaseTimer pt;
   for (uint32_t b = 0; b < in->n_bound_pods; b++)  // inverse anti-affinity keys need a dictionary id too
     for (uint32_t j = 0; j < in->bound_pods[b].n_anti_affinity; j++) {
       const char* k = in->bound_pods[b].anti_affinity[j].topology_key;
@@ -2335,6 +2406,7 @@ int32_t ParseSolve(const kp_solve_in* in, SolveRaw& raw) {
       raw.ex_labels[i].push_back({kHostname, KP_OP_IN, {host_named.count(host) ? host : string(kHostOther)}, -1});
     }
   }
+  pt.lap(" parse: node labels");
   return KP_OK;
 }
 
@@ -2508,6 +2580,7 @@ int32_t CompilePerCall(const kp_solve_in* in, const SolveRaw& raw, Compiled& cp)
   const SolveBase& b = *cp.B;
   const Dict& d = b.d;
   const int TW = b.TW;
+  PhaseTimer pt;
   map<vector<TaintT>, int> tsets;
   for (size_t i = 0; i < b.tsets.size(); i++) tsets[b.tsets[i]] = (int)i;
   auto tset = [&](vector<TaintT> v) {
@@ -2545,6 +2618,7 @@ int32_t CompilePerCall(const kp_solve_in* in, const SolveRaw& raw, Compiled& cp)
     }
   }
   if (tsets.size() > 64) return fail(KP_E_UNSUPPORTED, "%zu distinct taint sets (max 64)", tsets.size());
+  pt.lap(" existing nodes");
   // shapes: levels, negop, tolerations, requests, per-catalogue PVP rows
   int sl = 0;
   for (uint32_t s = 0; s < in->n_shapes; s++) {
@@ -2611,6 +2685,7 @@ int32_t CompilePerCall(const kp_solve_in* in, const SolveRaw& raw, Compiled& cp)
     }
   }
   if (cp.pvp.empty()) cp.pvp.assign(TW, 0);
+  pt.lap(" shapes");
   {  // host ports: shapes, then the existing nodes in upstream order
     vector<vector<HostPortKey>> hs(in->n_shapes), hn;
     string err;
@@ -2625,8 +2700,10 @@ int32_t CompilePerCall(const kp_solve_in* in, const SolveRaw& raw, Compiled& cp)
     const int32_t hrc = EncodeHostPorts(hs, hn, cp);
     if (hrc) return hrc;
   }
+  pt.lap(" host ports");
   int32_t rc = CompileTopology(in, cp, raw.strict_levels, raw.spread_levels, b.np_taintset, raw.filter_levels);
   if (rc) return rc;
+  pt.lap(" topology");
   // pods: Queue order byCPUAndMemoryDescending (cpu desc, memory desc, creation asc, uid asc)
   cp.pod_shape.resize(in->n_pods);
   cp.queue.resize(in->n_pods);
@@ -2674,6 +2751,7 @@ int32_t CompilePerCall(const kp_solve_in* in, const SolveRaw& raw, Compiled& cp)
     cp.cont_hint = in->n_pods > 1 && 2 * same >= in->n_pods ? 1 : 0;
     if (const char* e = getenv("KP_CONT")) cp.cont_hint = atoi(e) != 0;  // tests: force either fast-lane variant
   }
+  pt.lap(" queue");
   return KP_OK;
 }
 
@@ -2745,8 +2823,10 @@ int32_t RefreshOfferings(kp_ctx* ctx, SolveBase& b, bool commit = true) {
 // and its dictionary covers the batch; without one (kp_solve_validate) it is always built.
 int32_t CompileSolve(const kp_solve_in* in, Compiled& cp, kp_ctx* cache = nullptr) {
   SolveRaw raw;
+  PhaseTimer pt;
   int32_t rc = ParseSolve(in, raw);
   if (rc) return rc;
+  pt.lap("parse");
   const string ident = BaseIdent(in, raw);
   const string key = ident + SeqKey(SeqnumsOf(vector<const kp_catalog*>(in->catalogs, in->catalogs + in->n_catalogs)));
   if (cache) {
@@ -2762,7 +2842,9 @@ int32_t CompileSolve(const kp_solve_in* in, Compiled& cp, kp_ctx* cache = nullpt
         }
         cp.B = b;
         cp.base_hit = true;
+        pt.lap("base lookup");
         rc = CompilePerCall(in, raw, cp);
+        pt.lap("per-call compile");
         if (rc == KP_OK) {
           std::rotate(cache->bases.begin() + i, cache->bases.begin() + i + 1, cache->bases.end());  // most recent last
           cache->base_hits++;

@@ -1,4 +1,5 @@
-"""solve_kernel time of one config (default 2): 1 warmup + 5 timed kp_solve calls; prints the kernel ms (min, mean).
+"""solve_kernel time of one config (default 2): 1 warmup + 5 timed kp_solve calls; prints the kernel ms (min, mean),
+the per-Solve prepare and the whole call (means).
 Works with any libkp build selected by KP_LIB (older ABIs included). usage: kernel_time.py [2|3|5] [pods]"""
 import json
 import os
@@ -20,6 +21,14 @@ prob = {"2": lambda: synth.config2(cat, n_pods=n, seed=2), "2b": lambda: synth.c
         "3": lambda: synth.config3(cat, n_pods=n), "5": lambda: synth.config5(cat, n_pods=n)}[cfg]()
 ctx = kpamd.Context(0)
 sched = kpamd.Scheduler(ctx, prob)
+import time  # noqa: E402
 sched.solve(read=False)
-ks = [sched.solve(read=False)["stats"]["solve_kernel_ms"] for _ in range(5)]
-print(json.dumps({"min_ms": round(min(ks), 2), "mean_ms": round(sum(ks) / len(ks), 2)}))
+ks, ps, ws = [], [], []
+for _ in range(5):
+    t0 = time.perf_counter()
+    st = sched.solve(read=False)["stats"]
+    ws.append((time.perf_counter() - t0) * 1e3)
+    ks.append(st["solve_kernel_ms"])
+    ps.append(st["prepare_ms"])
+print(json.dumps({"min_ms": round(min(ks), 2), "mean_ms": round(sum(ks) / len(ks), 2),
+                  "prep_ms": round(sum(ps) / len(ps), 2), "step_ms": round(sum(ws) / len(ws), 2)}))
