@@ -2024,7 +2024,43 @@ __device__ __noinline__ uint64_t fl_fits_filter(int cat_a, uint64_t X0, int64_t 
 
 // kp_cancel: the caller's flag in host-mapped memory, read past every cache (system scope)
 __device__ __forceinline__ bool cancel_set(const int32_t* flag) {
-  return flag && __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+  // (readfirstlane: every lane reads the same word; without it the atomic load counts as divergent, and a loop that
+  // breaks on it is compiled as divergent control flow)
+  return flag && __builtin_amdgcn_readfirstlane(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) != 0;
+}
+
+// A SolveArgs field from the fast lane's lane table (kt0..kt4: dword 64 k + l in lane l of kt<k>); off is a constant,
+// so this is one v_readlane per dword.
+// A pointer field is rebuilt as a global-address-space pointer and cast to a generic one: kernel-argument pointers
+// point to global memory, which the backend infers for pointers it loads from the kernarg segment but not for lane
+// values; through the cast, accesses stay global_* instructions instead of FLAT ones (which also wait on the LDS
+// counter).
+template <class T>
+struct ka_type {
+  using type = T;
+};
+template <class U>
+struct ka_type<U*> {
+  using type = U GLB*;
+};
+template <class T>
+__device__ __forceinline__ T ka_read(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3, uint32_t k4, unsigned off) {
+  static_assert(sizeof(T) == 4 || sizeof(T) == 8, "4- or 8-byte fields");
+  auto rd = [&](unsigned j) -> uint32_t {
+    const uint32_t v = j < 64 ? k0 : j < 128 ? k1 : j < 192 ? k2 : j < 256 ? k3 : k4;
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)(j & 63));
+  };
+  if constexpr (sizeof(T) == 8) {
+    const uint64_t x = ((uint64_t)rd(off / 4 + 1) << 32) | rd(off / 4);
+    typename ka_type<T>::type g;
+    __builtin_memcpy(&g, &x, 8);
+    return (T)g;
+  } else {
+    const uint32_t x = rd(off / 4);
+    T t;
+    __builtin_memcpy(&t, &x, 4);
+    return t;
+  }
 }
 
 // Places popped pods while they need no requirement merge; returns the number placed. A pod it cannot place is
@@ -2065,6 +2101,9 @@ __device__ __noinline__ int fast_lane(uint64_t kargs, int32_t LDS* s_dyn_arg, ui
   uint32_t rr_b4 = rr_rest;
   for (int i = 0; i < 2 && rr_b4; i++) rr_b4 &= rr_b4 - 1;
   const bool four = rk2 >= 0;
+  static_assert(KP_NRES < 63, "lane 63 of the request vector is the zero slot");
+  const uint32_t pr_idx = (uint32_t)(rmask_all ? rr0 : 63) | (uint32_t)(rm1 ? rr1 : 63) << 8 |
+                          (uint32_t)(rk2 >= 0 ? rk2 : 63) << 16 | (uint32_t)(rk3 >= 0 ? rk3 : 63) << 24;
   uint32_t rrp_all = 0;  // the requested resources (first four as bytes), for pods requesting all of them
   int n_rrp_all = 0;
   for (uint32_t m = rmask_all; m; m &= m - 1) {
@@ -2100,6 +2139,19 @@ __device__ __noinline__ int fast_lane(uint64_t kargs, int32_t LDS* s_dyn_arg, ui
   NbUnits fnb{0, 0, 0};
   uint32_t n_app = 0, n_scan = 0;
     const bool tmg = A->timing != 0;
+    // the argument block as a lane table: dword 64 k + l of SolveArgs in lane l of kt<k>
+    static_assert(sizeof(SolveArgs) <= 1280, "SolveArgs outgrew the fast lane's argument table");
+    uint32_t kt0, kt1, kt2, kt3, kt4;
+    {
+      const KARG uint32_t* aw = (const KARG uint32_t*)A;
+      const int nw = (int)(sizeof(SolveArgs) / 4);
+      kt0 = aw[lane];
+      kt1 = 64 + lane < nw ? aw[64 + lane] : 0;
+      kt2 = 128 + lane < nw ? aw[128 + lane] : 0;
+      kt3 = 192 + lane < nw ? aw[192 + lane] : 0;
+      kt4 = 256 + lane < nw ? aw[256 + lane] : 0;
+    }
+#define KA(f) ka_read<decltype(SolveArgs::f)>(kt0, kt1, kt2, kt3, kt4, offsetof(SolveArgs, f))
 #define FL_HAS_EX (EX)
     uint64_t ft = tmg ? __builtin_amdgcn_s_memtime() : 0;
 #define FTF(i)                                               \
@@ -2120,11 +2172,10 @@ if (!FL_NOTIME && tmg) {                                    \
     int64_t pf_preq = 0;
     uint64_t pf_tol = 0;
     for (;;) {
-      // the argument block re-derived per pod (opaque to the optimiser): its fields are scalar-loaded where they are
-      // used instead of being held in registers across the whole loop (which spilled SGPRs into VGPR lanes)
-      uint32_t klo_i = klo, khi_i = khi;
-      asm volatile("" : "+s"(klo_i), "+s"(khi_i));
-      const KARG SolveArgs* A = (const KARG SolveArgs*)(((uint64_t)khi_i << 32) | klo_i);
+      // the argument block's fields are read from the lane table (KA): one or two v_readlane where used, made opaque per
+      // pod so that they are not hoisted into SGPRs held across the loop (which spilled into VGPR lanes), and with no
+      // scalar load whose lgkmcnt wait would also drain the wave's outstanding LDS operations
+      asm volatile("" : "+v"(kt0), "+v"(kt1), "+v"(kt2), "+v"(kt3), "+v"(kt4));
       const int len = q_len;
       const int head = q_head;
       if (len <= 0 || pops_in + pops + memo_pops > pop_cap) break;
@@ -2132,11 +2183,11 @@ if (!FL_NOTIME && tmg) {                                    \
       // the window was read, and nothing rewrites a queued entry (pushes go to the tail) or its pod's level and
       // lastLen stamps while it waits, so lane i's copy of entry qw_head + i stays exact.
       int off = head - qw_head;
-      if (off < 0) off += A->n_pods;
+      if (off < 0) off += KA(n_pods);
       if (off != qw_next || off >= qw_n) {  // exhausted, or the ring wrapped onto re-pushed entries
-        if (A->cancel && (int)(pops_in + pops + memo_pops) >= chk_next) {  // ctx.Done(): at most every 1024 pops
+        if (KA(cancel) && (int)(pops_in + pops + memo_pops) >= chk_next) {  // ctx.Done(): at most every 1024 pops
           chk_next = (int)(pops_in + pops + memo_pops) + 1024;
-          if (cancel_set(A->cancel)) {
+          if (cancel_set(KA(cancel))) {
             s_ctl[33] = 1;
             break;
           }
@@ -2146,13 +2197,13 @@ if (!FL_NOTIME && tmg) {                                    \
         off = 0;
         pf_off = -1;
         int qi = head + lane;
-        if (qi >= A->n_pods) qi -= A->n_pods;
+        if (qi >= KA(n_pods)) qi -= KA(n_pods);
         if (lane < qw_n) {
-          qw_pod = A->queue[qi];
-          qw_shape = A->pod_shape[qw_pod];
-          qw_sl = A->shape_level_base[qw_shape] + A->pod_level[qw_pod];
-          qw_lastlen = A->lastlen[qw_pod];
-          qw_epoch = A->lastlen_epoch[qw_pod];
+          qw_pod = KA(queue)[qi];
+          qw_shape = KA(pod_shape)[qw_pod];
+          qw_sl = KA(shape_level_base)[qw_shape] + KA(pod_level)[qw_pod];
+          qw_lastlen = KA(lastlen)[qw_pod];
+          qw_epoch = KA(lastlen_epoch)[qw_pod];
         }
         // wait for the window here, in the rare branch: at the join the compiler would otherwise wait for every
         // outstanding vector-memory operation (the previous pod's stores included) on the common path too
@@ -2184,31 +2235,31 @@ if (!FL_NOTIME && tmg) {                                    \
           ce1 = a_cex_prev_stamp;
         }
       } else {
-        own = U((TOPO ? 1 - A->sl_fast_topo[sl] : 0) + (A->hp_any && A->shape_hp_conf[shape] ? 1 : 0));
-        ce0 = U(FL_HAS_EX ? A->cur_ex[2 * sl] : 0), ce1 = U(FL_HAS_EX ? A->cur_ex[2 * sl + 1] : 0);
-        preq_lane = lane < KP_NRES ? A->shape_requests[(size_t)shape * KP_NRES + lane] : 0;
-        tolmask = U64(A->shape_tolerates[sl]);
-        cur = U(A->cur_nc[2 * sl]), stamp = U(A->cur_nc[2 * sl + 1]);
+        own = U((TOPO ? 1 - KA(sl_fast_topo)[sl] : 0) + (KA(hp_any) && KA(shape_hp_conf)[shape] ? 1 : 0));
+        ce0 = U(FL_HAS_EX ? KA(cur_ex)[2 * sl] : 0), ce1 = U(FL_HAS_EX ? KA(cur_ex)[2 * sl + 1] : 0);
+        preq_lane = lane < KP_NRES ? KA(shape_requests)[(size_t)shape * KP_NRES + lane] : 0;
+        tolmask = U64(KA(shape_tolerates)[sl]);
+        cur = U(KA(cur_nc)[2 * sl]), stamp = U(KA(cur_nc)[2 * sl + 1]);
         READY(preq_lane);
       }
       pf_off = -1;
       if (off + 1 < qw_n) {  // the next entry's stage loads: in flight while this pod is sorted and placed
         const int nshape = __builtin_amdgcn_readlane(qw_shape, off + 1);
         const int nsl = __builtin_amdgcn_readlane(qw_sl, off + 1);
-        pf_own = (TOPO ? 1 - A->sl_fast_topo[nsl] : 0) + (A->hp_any && A->shape_hp_conf[nshape] ? 1 : 0);
-        pf_ce0 = FL_HAS_EX ? A->cur_ex[2 * nsl] : 0, pf_ce1 = FL_HAS_EX ? A->cur_ex[2 * nsl + 1] : 0;
-        pf_preq = lane < KP_NRES ? A->shape_requests[(size_t)nshape * KP_NRES + lane] : 0;
-        pf_tol = A->shape_tolerates[nsl];
-        pf_cur = A->cur_nc[2 * nsl], pf_stamp = A->cur_nc[2 * nsl + 1];
+        pf_own = (TOPO ? 1 - KA(sl_fast_topo)[nsl] : 0) + (KA(hp_any) && KA(shape_hp_conf)[nshape] ? 1 : 0);
+        pf_ce0 = FL_HAS_EX ? KA(cur_ex)[2 * nsl] : 0, pf_ce1 = FL_HAS_EX ? KA(cur_ex)[2 * nsl + 1] : 0;
+        pf_preq = lane < KP_NRES ? KA(shape_requests)[(size_t)nshape * KP_NRES + lane] : 0;
+        pf_tol = KA(shape_tolerates)[nsl];
+        pf_cur = KA(cur_nc)[2 * nsl], pf_stamp = KA(cur_nc)[2 * nsl + 1];
         pf_off = off + 1;
       }
       prev_sl = sl;
       FTF(7);
-      q_head = head + 1 == A->n_pods ? 0 : head + 1;
+      q_head = head + 1 == KA(n_pods) ? 0 : head + 1;
       q_len = len - 1;
       // the unschedulable memo (SolveArgs::sl_fail; chunked orders, where failing pods are many): the pod fails
       // every placement, so after the sort replay below the lane does the full path's failure bookkeeping itself
-      const bool memo = CHK && !TOPO && A->sl_fail[sl] == n_nc_all;
+      const bool memo = CHK && !TOPO && KA(sl_fail)[sl] == n_nc_all;
       bool eligible = own == 0;
       // addToExistingNode's start: the first-fit cursor, clamped by the existing positions mutated since it was stored
       const int ex_start = FL_HAS_EX ? min(ce0, mstack_query_wave((LdsI32)s_stk[1], U(s_ctl[14]), U(s_ctl[21]), ce1))
@@ -2219,8 +2270,9 @@ if (!FL_NOTIME && tmg) {                                    \
         fb = FB_INELIGIBLE;
         break;
       }
-      const int64_t pr0 = rmask_all ? lane_bcast_i64(preq_lane, rr0) : 0, pr1 = rm1 ? lane_bcast_i64(preq_lane, rr1) : 0;
-      const int64_t pr2 = rk2 >= 0 ? lane_bcast_i64(preq_lane, rk2) : 0, pr3 = rk3 >= 0 ? lane_bcast_i64(preq_lane, rk3) : 0;
+      // the first four requested resources' requests (lane 63 holds 0 for an unused slot): no branches
+      const int64_t pr0 = lane_bcast_i64(preq_lane, pr_idx & 0xff), pr1 = lane_bcast_i64(preq_lane, (pr_idx >> 8) & 0xff);
+      const int64_t pr2 = lane_bcast_i64(preq_lane, (pr_idx >> 16) & 0xff), pr3 = lane_bcast_i64(preq_lane, pr_idx >> 24);
       // the resources this pod requests (chunked orders: many NodeClaims, pools whose pods request few of the
       // resources): Fits on an in-flight NodeClaim only re-tests those (its remaining types already fit its own
       // requests on every other resource, and a zero request leaves them so), and the fifth and later ones'
@@ -2250,23 +2302,23 @@ if (!FL_NOTIME && tmg) {                                    \
           t_mskew[4] = {0, 0, 0, 0};
       uint64_t t_acc[4] = {0, 0, 0, 0};
       if (TOPO) {
-        t_n = A->sl_own_n[sl];
-        triv = kreq_at(A->shape_reqs, sl)->present == 0;
-        rec_n = A->shape_rec_n[shape];
-        rec_b = A->shape_rec_base[shape];
+        t_n = KA(sl_own_n)[sl];
+        triv = kreq_at(KA(shape_reqs), sl)->present == 0;
+        rec_n = KA(shape_rec_n)[shape];
+        rec_b = KA(shape_rec_base)[shape];
         if (lane < rec_n) {  // (the group's liveness and taint filter are read at the commit: no wait here)
-          r_g = A->rec_list[rec_b + lane];
-          r_aux = A->rec_aux[rec_b + lane];
+          r_g = KA(rec_list)[rec_b + lane];
+          r_aux = KA(rec_aux)[rec_b + lane];
         }
-        const int ob = A->sl_own_base[sl];
+        const int ob = KA(sl_own_base)[sl];
 #pragma unroll
         for (int j = 0; j < 4; j++)
           if (j < t_n) {
-            const int4 r0 = A->own_rec[2 * (ob + j)], r1 = A->own_rec[2 * (ob + j) + 1];
+            const int4 r0 = KA(own_rec)[2 * (ob + j)], r1 = KA(own_rec)[2 * (ob + j) + 1];
             t_key[j] = r0.z, t_row[j] = r1.y, t_slot[j] = r1.z, t_self[j] = r0.y, t_mskew[j] = r0.w;
             if (r0.z >= 0) {
-              const int c = A->tg_cnt[(size_t)r0.x * 64 + lane];
-              const uint64_t reg = A->tg_reg[r0.x], pd = A->own_pd[ob + j];
+              const int c = KA(tg_cnt)[(size_t)r0.x * 64 + lane];
+              const uint64_t reg = KA(tg_reg)[r0.x], pd = KA(own_pd)[ob + j];
               const bool sup = ((reg & pd) >> lane) & 1;
               const int mn = wave_min_i32(sup ? c : INT32_MAX);
               const int num = __builtin_popcountll(reg & pd);
@@ -2276,16 +2328,16 @@ if (!FL_NOTIME && tmg) {                                    \
             }
           }
       }
-      a_cex_prev_stamp = U(s_ctl[15]);
+      if (FL_HAS_EX) a_cex_prev_stamp = U(s_ctl[15]);
       bool b_staged = false;  // fl_B holds the pod's requirement set (staged on the first merge)
       // ---- addToExistingNode on the wave: ExistingNode.CanAdd at the lowest position that takes the pod, the
       // full path's checks 64 positions per round (headroom rows, failure memo, static fit, taints, hostname counts,
       // then the zone-like keys' value codes), then the requirement merge on the first candidates. An existing node's
       // labels are single values and its codes were checked against the accepted domains, so the topology narrowing
       // has nothing to narrow. A scan longer than FAST_EX_ROUNDS rounds goes to the full path's 1,024-lane pre-pass.
-      if (FL_HAS_EX && ex_start < A->n_existing && !memo) {
-        const int E = A->n_existing;
-        const bool ex_triv = TOPO ? triv : kreq_at(A->shape_reqs, sl)->present == 0;
+      if (FL_HAS_EX && ex_start < KA(n_existing) && !memo) {
+        const int E = KA(n_existing);
+        const bool ex_triv = TOPO ? triv : kreq_at(KA(shape_reqs), sl)->present == 0;
         int ex_pl = -1, ex_ipos = INT32_MAX, rounds = 0;
         bool ex_bail = false;
         for (int base = ex_start; base < E && ex_pl < 0; base += 64) {
@@ -2299,16 +2351,16 @@ if (!FL_NOTIME && tmg) {                                    \
           bool cand = false, icand = false;
           int32_t ver = 0, ts = 0;
           if (valid) {
-            const int32_t fl = A->ex_fail[(size_t)sl * E + ec];
-            ver = A->ex_ver[ec];
-            ts = A->ex_taintset[ec];
-            const uint8_t sok = A->ex_static_ok[ec];
-            cand = A->ex_room[ec] >= pr0 && A->ex_room[(size_t)E + ec] >= pr1;
-            if (four) cand = cand && A->ex_room[2 * (size_t)E + ec] >= pr2 && A->ex_room[3 * (size_t)E + ec] >= pr3;
+            const int32_t fl = KA(ex_fail)[(size_t)sl * E + ec];
+            ver = KA(ex_ver)[ec];
+            ts = KA(ex_taintset)[ec];
+            const uint8_t sok = KA(ex_static_ok)[ec];
+            cand = KA(ex_room)[ec] >= pr0 && KA(ex_room)[(size_t)E + ec] >= pr1;
+            if (four) cand = cand && KA(ex_room)[2 * (size_t)E + ec] >= pr2 && KA(ex_room)[3 * (size_t)E + ec] >= pr3;
             cand = cand && fl != ver && fl != NC_NEVER && sok && ((tolmask >> ts) & 1);
             if (rr_b4p && cand) {  // a fifth requested resource and beyond
-              const int64_t* av = A->ex_available + (size_t)ec * KP_NRES;
-              const int64_t* rq = A->ex_requests + (size_t)ec * KP_NRES;
+              const int64_t* av = KA(ex_available) + (size_t)ec * KP_NRES;
+              const int64_t* rq = KA(ex_requests) + (size_t)ec * KP_NRES;
               for (uint32_t rm = rr_b4p; rm; rm &= rm - 1) {
                 const int r = __builtin_ctz(rm);
                 cand = cand && rq[r] + lane_bcast_i64(preq_lane, r) <= av[r];
@@ -2318,12 +2370,12 @@ if (!FL_NOTIME && tmg) {                                    \
 #pragma unroll
               for (int j = 0; j < 4; j++)
                 if (j < t_n && t_key[j] < 0)
-                  cand = cand && (int)A->hcnt_ex[(size_t)t_row[j] * E + ec] + t_self[j] <= t_mskew[j];
+                  cand = cand && (int)KA(hcnt_ex)[(size_t)t_row[j] * E + ec] + t_self[j] <= t_mskew[j];
               icand = cand;
 #pragma unroll
               for (int j = 0; j < 4; j++)
                 if (j < t_n && t_key[j] >= 0) {
-                  const uint32_t code = A->ex_tcode[(size_t)t_slot[j] * E + ec];
+                  const uint32_t code = KA(ex_tcode)[(size_t)t_slot[j] * E + ec];
                   cand = cand && code != 0xFF && ((t_acc[j] >> (code & 63)) & 1);
                 }
             }
@@ -2332,7 +2384,7 @@ if (!FL_NOTIME && tmg) {                                    \
             const uint64_t im = __ballot(icand);
             if (im) ex_ipos = base + __builtin_ctzll(im);
           }
-          if (lane == 0) bytes += (uint64_t)min(64, E - base) * (16 * A->n_req_res + 13);  // (the full path's model)
+          if (lane == 0) bytes += (uint64_t)min(64, E - base) * (16 * KA(n_req_res) + 13);  // (the full path's model)
           uint64_t cm = __ballot(cand);
           while (cm) {
             const int l = __builtin_ctzll(cm);
@@ -2342,13 +2394,13 @@ if (!FL_NOTIME && tmg) {                                    \
             attempts++;
             if (!b_staged && !ex_triv) {  // the pod's requirement set, once per pod
               constexpr int NQ = (int)(sizeof(KReqs) / 8);
-              const uint64_t* src = reinterpret_cast<const uint64_t*>(A->shape_reqs + (size_t)sl * sizeof(KReqs));
+              const uint64_t* src = reinterpret_cast<const uint64_t*>(KA(shape_reqs) + (size_t)sl * sizeof(KReqs));
               uint64_t* dstB = reinterpret_cast<uint64_t*>(&fl_B);
               for (int i = lane; i < NQ; i += 64) dstB[i] = src[i];
               wave_sync();
               b_staged = true;
             }
-            KReqs* er = reinterpret_cast<KReqs*>(A->ex_reqs + (size_t)ei * sizeof(KReqs));
+            KReqs* er = reinterpret_cast<KReqs*>(KA(ex_reqs) + (size_t)ei * sizeof(KReqs));
             bytes += sizeof(KReqs);
             // a pod without requirements at this level: Compatible holds and Add leaves the node's requirements as
             // they are (nothing to intersect), so neither the merge nor its store is needed
@@ -2356,44 +2408,44 @@ if (!FL_NOTIME && tmg) {                                    \
               const CandReq crx = load_cand(D, er);
               uint64_t m_v = 0;
               ReqView rv;
-              const uint64_t b_negop = A->shape_negop[sl];
+              const uint64_t b_negop = KA(shape_negop)[sl];
               const bool mok = merge_compatible(D, crx, (const KReqs*)&fl_B, b_negop, false, m_v, rv,
-                                                (WaveSlots*)&fl_slots, vint_global(A->vint));
+                                                (WaveSlots*)&fl_slots, vint_global(KA(vint)));
               if (!mok) {  // permanent unless the undefined-key rule failed (no well-known exemption here)
-                if (lane == 0) A->ex_fail[(size_t)sl * E + ei] = (fl_B.present & ~crx.P & ~b_negop) == 0 ? NC_NEVER : verx;
+                if (lane == 0) KA(ex_fail)[(size_t)sl * E + ei] = (fl_B.present & ~crx.P & ~b_negop) == 0 ? NC_NEVER : verx;
                 continue;
               }
               // commit: ExistingNode.Add (requirements, requests, headroom rows, version), Topology.Record
               store_merged(er, rv, m_v, D.W, D.KB);
             }
-            if (lane < KP_NRES) A->ex_requests[(size_t)ei * KP_NRES + lane] += preq_lane;
+            if (lane < KP_NRES) KA(ex_requests)[(size_t)ei * KP_NRES + lane] += preq_lane;
             if (lane < 4) {  // headroom rows of the first four requested resources
               const int64_t d = lane == 0 ? pr0 : lane == 1 ? pr1 : lane == 2 ? pr2 : pr3;
-              A->ex_room[(size_t)lane * E + ei] -= d;
+              KA(ex_room)[(size_t)lane * E + ei] -= d;
             }
-            if (lane == 0) A->ex_ver[ei] = verx + 1;
+            if (lane == 0) KA(ex_ver)[ei] = verx + 1;
             if (TOPO && rec_n) {
               const int tsx = __builtin_amdgcn_readlane(ts, l);
               for (int i0 = 0; i0 < rec_n; i0 += 64) {
                 const int ri = i0 + lane;
                 if (ri < rec_n) {
                   int g = r_g, aux = r_aux;
-                  if (i0) g = A->rec_list[rec_b + ri], aux = A->rec_aux[rec_b + ri];  // (past the 64 prefetched)
+                  if (i0) g = KA(rec_list)[rec_b + ri], aux = KA(rec_aux)[rec_b + ri];  // (past the 64 prefetched)
                   // liveness, taint filter and the node's value code in one round trip
-                  const int live = A->tg_live[g];
-                  const uint64_t ftol = A->tg_filt_tol[g];
-                  const uint32_t code0 = aux < 0 ? A->ex_tcode[(size_t)(-1 - aux) * E + ei] : 0xFF;
-                  uint8_t* c = &A->hcnt_ex[(size_t)(aux >= 0 ? aux : 0) * E + ei];
+                  const int live = KA(tg_live)[g];
+                  const uint64_t ftol = KA(tg_filt_tol)[g];
+                  const uint32_t code0 = aux < 0 ? KA(ex_tcode)[(size_t)(-1 - aux) * E + ei] : 0xFF;
+                  uint8_t* c = &KA(hcnt_ex)[(size_t)(aux >= 0 ? aux : 0) * E + ei];
                   const uint32_t hc0 = aux >= 0 ? *c : 0;
                   if (live && ((ftol >> tsx) & 1)) {
                     if (aux >= 0) {
                       *c = hc0 == 255 ? 1 : hc0 < 254 ? hc0 + 1 : 254;  // 255: an unregistered domain
-                      A->tg_reg[g] = 1;
+                      KA(tg_reg)[g] = 1;
                     } else {
                       const uint32_t code = code0;
                       if (code < 64) {
-                        A->tg_cnt[(size_t)g * 64 + code] += 1;
-                        A->tg_reg[g] |= 1ull << code;
+                        KA(tg_cnt)[(size_t)g * 64 + code] += 1;
+                        KA(tg_reg)[g] |= 1ull << code;
                       }
                     }
                   }
@@ -2414,8 +2466,8 @@ if (!FL_NOTIME && tmg) {                                    \
         // the count-independent checks (a zone-count failure may pass later), as the full path
         const int cpos = TOPO && t_n ? min(ex_ipos, E) : (ex_pl >= 0 ? ex_pl : E);
         if (lane == 0) {
-          A->cur_ex[2 * sl] = cpos;
-          A->cur_ex[2 * sl + 1] = a_cex_prev_stamp;
+          KA(cur_ex)[2 * sl] = cpos;
+          KA(cur_ex)[2 * sl + 1] = a_cex_prev_stamp;
         }
         a_cex_prev_pos = cpos;
         if (ex_pl >= 0) {
@@ -2437,8 +2489,8 @@ if (!FL_NOTIME && tmg) {                                    \
             buf_pl = -2 - ex_pl;
           }
           if (++n_buf == 64) {
-            A->placement[buf_pod] = buf_pl;
-            A->events[n_ev + lane] = buf_pod;
+            KA(placement)[buf_pod] = buf_pl;
+            KA(events)[n_ev + lane] = buf_pod;
             n_ev += 64;
             n_buf = 0;
           }
@@ -2446,10 +2498,10 @@ if (!FL_NOTIME && tmg) {                                    \
         }
       } else if (FL_HAS_EX) {  // addToExistingNode: every position fails (cursor == n_existing)
         if (lane == 0) {
-          A->cur_ex[2 * sl] = A->n_existing;
-          A->cur_ex[2 * sl + 1] = a_cex_prev_stamp;
+          KA(cur_ex)[2 * sl] = KA(n_existing);
+          KA(cur_ex)[2 * sl + 1] = a_cex_prev_stamp;
         }
-        a_cex_prev_pos = A->n_existing;
+        a_cex_prev_pos = KA(n_existing);
       }
       FT(1);
       // sort.Slice(newNodeClaims) replay + first-fit start (sort arrays in LDS or chunked; the flat global order:
@@ -2460,7 +2512,7 @@ if (!FL_NOTIME && tmg) {                                    \
         break;
       }
       const LdsI32 ord = (LdsI32)s_dyn;
-      const LdsI32 npods = (LdsI32)(s_dyn + A->sort_cap);
+      const LdsI32 npods = (LdsI32)(s_dyn + KA(sort_cap));
       const ChkDir cd = chk_dir(s_dyn);
       const int c19 = min(cur, mstack_query_wave((LdsI32)s_stk[0], stk_n, stk_lost, stamp));
       const int n_nc = n_nc_all;
@@ -2469,8 +2521,8 @@ if (!FL_NOTIME && tmg) {                                    \
       bool n_moved = false;  // the pending mutation moved its NodeClaim (sort_mut1_window)
       const bool mut_was1 = mut == 1 && mut_p == cont_w;  // ... and it is the previous pod's commit at cont_w
       if (CHK) {
-        low = mut == 0 ? -1 : chk_sort(cd, (ChkCtl LDS*)&g_chk, A->chk_blk, n_nc, mut, mut_p, A->g_order, A->g_npods,
-                                       &A->stats[31], h_ck, h_blk, h_id, h_key);
+        low = mut == 0 ? -1 : chk_sort(cd, (ChkCtl LDS*)&g_chk, KA(chk_blk), n_nc, mut, mut_p, KA(g_order), KA(g_npods),
+                                       &KA(stats)[31], h_ck, h_blk, h_id, h_key);
         h_ck = -1;  // (the replay may have moved entries)
         if (low == -4) {  // the literal pdqsort ran and its rebuild did not fit: the flat order, the full path's
           if (lane == 0) s_ctl[5] = 0;
@@ -2484,7 +2536,7 @@ if (!FL_NOTIME && tmg) {                                    \
         }
       } else {
         low = mut == 0 ? -1 : (mut == 1 ? sort_mut1_window(ord, npods, n_nc, mut_p, &n_moved) : -2);
-        if (low == -2) low = sort_newnodeclaims_wave(ord, npods, n_nc, mut, mut_p, 256, &A->stats[31]);
+        if (low == -2) low = sort_newnodeclaims_wave(ord, npods, n_nc, mut, mut_p, 256, &KA(stats)[31]);
         if (low == -2) {  // a long shift: the full path sorts (the pending mutation is still in s_ctl[10..11])
           handoff = pod;
           fb = FB_SHIFT;
@@ -2500,20 +2552,20 @@ if (!FL_NOTIME && tmg) {                                    \
       if (memo) {  // the full path's failure: cursors at the end, Preferences.Relax, Queue.Push
         a_cur_prev_pos = n_nc;
         a_cur_prev_stamp = stk_t;
-        const int lvl = sl - A->shape_level_base[shape];
-        const bool relaxed = lvl + 1 < A->shape_nlevels[shape];
+        const int lvl = sl - KA(shape_level_base)[shape];
+        const bool relaxed = lvl + 1 < KA(shape_nlevels)[shape];
         int tail = q_head + q_len;
-        if (tail >= A->n_pods) tail -= A->n_pods;
+        if (tail >= KA(n_pods)) tail -= KA(n_pods);
         q_len += 1;
         if (lane == 0) {
-          A->cur_nc[2 * sl] = n_nc;
-          A->cur_nc[2 * sl + 1] = stk_t;
-          A->placement[pod] = -1;
-          if (relaxed) A->pod_level[pod] = lvl + 1;
-          A->queue[tail] = pod;
+          KA(cur_nc)[2 * sl] = n_nc;
+          KA(cur_nc)[2 * sl + 1] = stk_t;
+          KA(placement)[pod] = -1;
+          if (relaxed) KA(pod_level)[pod] = lvl + 1;
+          KA(queue)[tail] = pod;
           if (!relaxed) {
-            A->lastlen[pod] = q_len;
-            A->lastlen_epoch[pod] = epoch;
+            KA(lastlen)[pod] = q_len;
+            KA(lastlen_epoch)[pod] = epoch;
           }
         }
         if (relaxed) epoch += 1;  // lastLen = map{}
@@ -2537,8 +2589,8 @@ if (!FL_NOTIME && tmg) {                                    \
       // chunked order: the start position's chunk and slot, the window of chunks whose live mask is in lm
       int ch0 = 0, cs0 = 0, cc = 0, lm_base = 0, n_live = 0;
       uint64_t lm = 0;
-      const bool can_dead = CHK && !t_n && sl < A->chk_dead_rows;
-      int32_t* const deadrow = A->chk_dead + (size_t)(can_dead ? sl : 0) * CHK_MAXC;
+      const bool can_dead = CHK && !t_n && sl < KA(chk_dead_rows);
+      int32_t* const deadrow = KA(chk_dead) + (size_t)(can_dead ? sl : 0) * CHK_MAXC;
       const int nch = CHK ? U(g_chk.nch) : 0;
       if (CHK) {
         ch0 = start < n_nc ? chk_find(cd, nch, start) : nch;
@@ -2571,8 +2623,8 @@ if (!FL_NOTIME && tmg) {                                    \
           const uint32_t v = cd.info[ck];
           valid = lane < ci_cnt(v) && !(ck == ch0 && lane < cs0);
           // the chunk's block (ids and keys) in one batch: the winner's chunk is the next replay's
-          c_bid = lane < ci_cnt(v) ? A->chk_blk[ci_blk(v)].id[lane] : -1;
-          c_bkey = lane < ci_cnt(v) ? A->chk_blk[ci_blk(v)].key[lane] : INT32_MAX;
+          c_bid = lane < ci_cnt(v) ? KA(chk_blk)[ci_blk(v)].id[lane] : -1;
+          c_bkey = lane < ci_cnt(v) ? KA(chk_blk)[ci_blk(v)].key[lane] : INT32_MAX;
           nc = valid ? c_bid : 0;
           i = cd.start[ck] + lane;
           nscan = __popcll(__ballot(valid));
@@ -2609,24 +2661,24 @@ if (!FL_NOTIME && tmg) {                                    \
         int64_t rq0 = c_q;
         int32_t j00 = c_fj;
         if (nc0 != c_nc) {
-          const KReqs* cr0 = kreq_at(A->nc_reqs, nc0);
+          const KReqs* cr0 = kreq_at(KA(nc_reqs), nc0);
           hm0 = cr0->hmin & cr0->present;
-          cat0 = A->nc_cat[nc0];
-          X00 = lane < D.TW ? A->nc_X[(size_t)nc0 * D.TW + lane] : 0;
-          rq0 = lane < KP_NRES ? A->nc_requests[(size_t)nc0 * KP_NRES + lane] : 0;
-          j00 = lane < KP_NRES ? A->nc_fitj[(size_t)nc0 * KP_NRES + lane] : 0;
+          cat0 = KA(nc_cat)[nc0];
+          X00 = lane < D.TW ? KA(nc_X)[(size_t)nc0 * D.TW + lane] : 0;
+          rq0 = lane < KP_NRES ? KA(nc_requests)[(size_t)nc0 * KP_NRES + lane] : 0;
+          j00 = lane < KP_NRES ? KA(nc_fitj)[(size_t)nc0 * KP_NRES + lane] : 0;
         }
         if (valid) {
           // every gather issued unconditionally: one round trip
-          const int32_t fl = cont_round ? NC_MERGED : nc < A->ncc ? A->nc_fail[(size_t)sl * A->ncc + nc] : -2;
+          const int32_t fl = cont_round ? NC_MERGED : nc < KA(ncc) ? KA(nc_fail)[(size_t)sl * KA(ncc) + nc] : -2;
           if (nc == c_nc) hv = HeadView{c_r0, c_r1, c_r2, c_r3, c_ver, c_ts};
-          else hv = load_head(A->nc_head + nc, four);
+          else hv = load_head(KA(nc_head) + nc, four);
           ver = hv.ver;
           const int32_t ts = hv.ts;
           bool fit = hv.r0 >= pr0 && hv.r1 >= pr1 && hv.r2 >= pr2 && hv.r3 >= pr3;
           if (rr_b4p) {  // a fifth requested resource and beyond (that the pod requests)
-            const int64_t* rq = A->nc_requests + (size_t)nc * KP_NRES;
-            const int64_t* mx = A->nc_maxalloc + (size_t)nc * KP_NRES;
+            const int64_t* rq = KA(nc_requests) + (size_t)nc * KP_NRES;
+            const int64_t* mx = KA(nc_maxalloc) + (size_t)nc * KP_NRES;
             for (uint32_t rm = rr_b4p; rm; rm &= rm - 1) {
               const int r = __builtin_ctz(rm);
               fit = fit & (rq[r] + lane_bcast_i64(preq_lane, r) <= mx[r]);
@@ -2639,12 +2691,12 @@ if (!FL_NOTIME && tmg) {                                    \
 #pragma unroll
             for (int j = 0; j < 4; j++)
               if (j < t_n && t_key[j] < 0)
-                cand = cand && (int)A->hcnt_nc[(size_t)t_row[j] * A->hnc_stride + nc] + t_self[j] <= t_mskew[j];
+                cand = cand && (int)KA(hcnt_nc)[(size_t)t_row[j] * KA(hnc_stride) + nc] + t_self[j] <= t_mskew[j];
             icand = cand;
 #pragma unroll
             for (int j = 0; j < 4; j++)
               if (j < t_n && t_key[j] >= 0) {
-                const uint32_t code = A->nc_tcode[(size_t)t_slot[j] * A->hnc_stride + nc];
+                const uint32_t code = KA(nc_tcode)[(size_t)t_slot[j] * KA(hnc_stride) + nc];
                 cand = cand && (code == 0xFF || (code < 64 && ((t_acc[j] >> code) & 1)));
                 pinned = pinned && code < 64;
               }
@@ -2687,12 +2739,12 @@ if (!FL_NOTIME && tmg) {                                    \
           if (l != 0 && ncx == c_nc) {
             hm = c_hm, X0 = c_X, cat = c_cat, rq_lane = c_q, j0_lane = c_fj;
           } else if (l != 0) {
-            const KReqs* cr = kreq_at(A->nc_reqs, ncx);
+            const KReqs* cr = kreq_at(KA(nc_reqs), ncx);
             hm = cr->hmin & cr->present;
-            cat = A->nc_cat[ncx];
-            X0 = lane < D.TW ? A->nc_X[(size_t)ncx * D.TW + lane] : 0;
-            rq_lane = lane < KP_NRES ? A->nc_requests[(size_t)ncx * KP_NRES + lane] : 0;
-            j0_lane = lane < KP_NRES ? A->nc_fitj[(size_t)ncx * KP_NRES + lane] : 0;
+            cat = KA(nc_cat)[ncx];
+            X0 = lane < D.TW ? KA(nc_X)[(size_t)ncx * D.TW + lane] : 0;
+            rq_lane = lane < KP_NRES ? KA(nc_requests)[(size_t)ncx * KP_NRES + lane] : 0;
+            j0_lane = lane < KP_NRES ? KA(nc_fitj)[(size_t)ncx * KP_NRES + lane] : 0;
           }
           FTF(10);
           const int64_t q_lane = rq_lane + preq_lane;
@@ -2712,7 +2764,7 @@ if (!FL_NOTIME && tmg) {                                    \
               X = fits_lean(D, (const CatHdr LDS*)&g_hdr[cat], X0, q_lane, j0_lane, (const int64_t LDS*)g_fitv, rrp,
                             n_rrp, fnb, (int32_t LDS*)fl_fitj);
             } else {
-              X = fl_fits_filter(cat, X0, q_lane, j0_lane, A->req_res_mask, (uint64_t)(uintptr_t)A->cats);
+              X = fl_fits_filter(cat, X0, q_lane, j0_lane, KA(req_res_mask), (uint64_t)(uintptr_t)KA(cats));
               bytes += fl_io[1];
             }
             n_app++;
@@ -2720,24 +2772,24 @@ if (!FL_NOTIME && tmg) {                                    \
           } else {
             if (!b_staged) {  // the pod's requirement set, once per pod
               constexpr int NQ = (int)(sizeof(KReqs) / 8);
-              const uint64_t* src = reinterpret_cast<const uint64_t*>(A->shape_reqs + (size_t)sl * sizeof(KReqs));
+              const uint64_t* src = reinterpret_cast<const uint64_t*>(KA(shape_reqs) + (size_t)sl * sizeof(KReqs));
               uint64_t* dstB = reinterpret_cast<uint64_t*>(&fl_B);
               for (int i = lane; i < NQ; i += 64) dstB[i] = src[i];
               wave_sync();
               b_staged = true;
             }
-            const CandReq crx = load_cand(D, kreq_at(A->nc_reqs, ncx));
-            const VInt vig = vint_global(A->vint);
-            const uint64_t b_negop = A->shape_negop[sl];
+            const CandReq crx = load_cand(D, kreq_at(KA(nc_reqs), ncx));
+            const VInt vig = vint_global(KA(vint));
+            const uint64_t b_negop = KA(shape_negop)[sl];
             bool mok = merge_compatible(D, crx, (const KReqs*)&fl_B, b_negop, true, m_v, rv,
                                         (WaveSlots*)&fl_slots, vig);
             if (!mok) perm = (fl_B.present & ~crx.P & ~b_negop & ~D.wellknown) == 0;
             bytes += sizeof(KReqs);
             if (mok) {
-              const int pb = A->pvp_base[sl * A->n_catalogs + cat];
-              const uint64_t* pvp = A->shape_pvp + (size_t)pb * D.TW;
-              X = filter_types(D, hdr(cat), rv, m_v, X0, fl_B.present, pvp, A->pvp_slot + (size_t)sl * KP_MAX_KEYS,
-                               q_lane, j0_lane, (const int64_t LDS*)g_fitv, A->req_res_mask, vig, (uint32_t*)fl_scratch,
+              const int pb = KA(pvp_base)[sl * KA(n_catalogs) + cat];
+              const uint64_t* pvp = KA(shape_pvp) + (size_t)pb * D.TW;
+              X = filter_types(D, hdr(cat), rv, m_v, X0, fl_B.present, pvp, KA(pvp_slot) + (size_t)sl * KP_MAX_KEYS,
+                               q_lane, j0_lane, (const int64_t LDS*)g_fitv, KA(req_res_mask), vig, (uint32_t*)fl_scratch,
                                (RowPtr LDS*)fl_rl, &bytes, fl_fitj);
               bytes += (uint64_t)D.TW * 8 + KP_NRES * 8;
             }
@@ -2745,37 +2797,37 @@ if (!FL_NOTIME && tmg) {                                    \
           FTF(11);
           if (__ballot(X != 0)) {
             if (full_add) {
-              store_merged(reinterpret_cast<KReqs*>(A->nc_reqs + (size_t)ncx * sizeof(KReqs)), rv, m_v, D.W, D.KB);
-              if (TOPO && A->n_tk) store_tcodes(A->n_tk, A->tk_keys, A->nc_tcode, A->hnc_stride, rv, m_v, ncx);
-              if (lane == 0 && ncx < A->ncc) A->nc_fail[(size_t)sl * A->ncc + ncx] = NC_MERGED;
+              store_merged(reinterpret_cast<KReqs*>(KA(nc_reqs) + (size_t)ncx * sizeof(KReqs)), rv, m_v, D.W, D.KB);
+              if (TOPO && KA(n_tk)) store_tcodes(KA(n_tk), KA(tk_keys), KA(nc_tcode), KA(hnc_stride), rv, m_v, ncx);
+              if (lane == 0 && ncx < KA(ncc)) KA(nc_fail)[(size_t)sl * KA(ncc) + ncx] = NC_MERGED;
             }
             // the remaining types and threshold indices are stored only when they changed (the append path
             // usually leaves both as they were): fewer vector-memory operations ahead of the next pod's loads
             const int32_t fj = lane < KP_NRES ? fl_fitj[lane] : 0;
             if (__ballot(lane < D.TW && X != X0)) {
-              if (lane < D.TW) A->nc_X[(size_t)ncx * D.TW + lane] = X;
+              if (lane < D.TW) KA(nc_X)[(size_t)ncx * D.TW + lane] = X;
             }
-            if (lane < KP_NRES) A->nc_requests[(size_t)ncx * KP_NRES + lane] = q_lane;
+            if (lane < KP_NRES) KA(nc_requests)[(size_t)ncx * KP_NRES + lane] = q_lane;
             if (__ballot(lane < KP_NRES && fj != j0_lane)) {
-              if (lane < KP_NRES) A->nc_fitj[(size_t)ncx * KP_NRES + lane] = fj;
+              if (lane < KP_NRES) KA(nc_fitj)[(size_t)ncx * KP_NRES + lane] = fj;
             }
             if (lane == 0) {
               if (CHK) {  // len(Pods) in the chunk's block (the replay reads it there) and the flat copy
-                A->chk_blk[ci_blk(cd.info[ck])].key[l] += 1;
-                A->g_npods[ncx] += 1;
+                KA(chk_blk)[ci_blk(cd.info[ck])].key[l] += 1;
+                KA(g_npods)[ncx] += 1;
               } else {
                 npods[ncx] += 1;
               }
             }
             if (lane == l) {  // the pre-check record, from this lane's copy: headroom minus the pod, version + 1
-              int4* hp = reinterpret_cast<int4*>(A->nc_head + ncx);
+              int4* hp = reinterpret_cast<int4*>(KA(nc_head) + ncx);
               const int64_t n0 = hv.r0 - pr0, n1 = hv.r1 - pr1;
               hp[0] = make_int4((int)n0, (int)(n0 >> 32), (int)n1, (int)(n1 >> 32));
               if (four) {
                 const int64_t n2 = hv.r2 - pr2, n3 = hv.r3 - pr3;
                 hp[1] = make_int4((int)n2, (int)(n2 >> 32), (int)n3, (int)(n3 >> 32));
               }
-              A->nc_head[ncx].ver = verx + 1;
+              KA(nc_head)[ncx].ver = verx + 1;
             }
             placed = ncx;
             wpos = __builtin_amdgcn_readlane(i, l);
@@ -2786,7 +2838,7 @@ if (!FL_NOTIME && tmg) {                                    \
               h_key = c_bkey + (lane == l ? 1 : 0);
             }
             if (FT_FINE) fl_last = ncx;
-            if (TOPO && triv && lane == 0 && ncx < A->ncc) A->nc_fail[(size_t)sl * A->ncc + ncx] = NC_MERGED;
+            if (TOPO && triv && lane == 0 && ncx < KA(ncc)) KA(nc_fail)[(size_t)sl * KA(ncc) + ncx] = NC_MERGED;
             if (TOPO && rec_n) {
               // Topology.Record, as the full path's: each recorded group (spreads only on fast levels) on its own lane;
               // a dictionary key counts once the NodeClaim holds one value of it (its value code < 64)
@@ -2795,22 +2847,22 @@ if (!FL_NOTIME && tmg) {                                    \
                 const int ri = i0 + lane;
                 if (ri < rec_n) {
                   int g = r_g, aux = r_aux;
-                  if (i0) g = A->rec_list[rec_b + ri], aux = A->rec_aux[rec_b + ri];  // (past the 64 prefetched)
+                  if (i0) g = KA(rec_list)[rec_b + ri], aux = KA(rec_aux)[rec_b + ri];  // (past the 64 prefetched)
                   // liveness, taint filter and the NodeClaim's value code in one round trip
-                  const int live = A->tg_live[g];
-                  const uint64_t ftol = A->tg_filt_tol[g];
-                  const uint32_t code0 = aux < 0 ? A->nc_tcode[(size_t)(-1 - aux) * A->hnc_stride + ncx] : 0xFF;
-                  uint8_t* c = &A->hcnt_nc[(size_t)(aux >= 0 ? aux : 0) * A->hnc_stride + ncx];
+                  const int live = KA(tg_live)[g];
+                  const uint64_t ftol = KA(tg_filt_tol)[g];
+                  const uint32_t code0 = aux < 0 ? KA(nc_tcode)[(size_t)(-1 - aux) * KA(hnc_stride) + ncx] : 0xFF;
+                  uint8_t* c = &KA(hcnt_nc)[(size_t)(aux >= 0 ? aux : 0) * KA(hnc_stride) + ncx];
                   const uint32_t hc0 = aux >= 0 ? *c : 0;
                   if (live && ((ftol >> tsx) & 1)) {
                     if (aux >= 0) {
                       *c = hc0 == 255 ? 1 : hc0 < 254 ? hc0 + 1 : 254;  // 255: an unregistered domain
-                      A->tg_reg[g] = 1;
+                      KA(tg_reg)[g] = 1;
                     } else {
                       const uint32_t code = code0;
                       if (code < 64) {
-                        A->tg_cnt[(size_t)g * 64 + code] += 1;
-                        A->tg_reg[g] |= 1ull << code;
+                        KA(tg_cnt)[(size_t)g * 64 + code] += 1;
+                        KA(tg_reg)[g] |= 1ull << code;
                       }
                     }
                   }
@@ -2831,7 +2883,7 @@ if (!FL_NOTIME && tmg) {                                    \
             FTF(12);
             break;
           }
-          if (lane == 0 && ncx < A->ncc) A->nc_fail[(size_t)sl * A->ncc + ncx] = perm ? NC_NEVER : verx;
+          if (lane == 0 && ncx < KA(ncc)) KA(nc_fail)[(size_t)sl * KA(ncc) + ncx] = perm ? NC_NEVER : verx;
         }
       }
       wave_sync();
@@ -2852,8 +2904,8 @@ if (!FL_NOTIME && tmg) {                                    \
       mut = 1;
       mut_p = wpos;
       if (lane == 0) {
-        A->cur_nc[2 * sl] = cpos;
-        A->cur_nc[2 * sl + 1] = a_cur_prev_stamp;
+        KA(cur_nc)[2 * sl] = cpos;
+        KA(cur_nc)[2 * sl + 1] = a_cur_prev_stamp;
       }
       // placement / events: buffered one pod per lane, written 64 at a time (nothing reads them before the
       // fast lane returns)
@@ -2862,8 +2914,8 @@ if (!FL_NOTIME && tmg) {                                    \
         buf_pl = placed;
       }
       if (++n_buf == 64) {
-        A->placement[buf_pod] = buf_pl;
-        A->events[n_ev + lane] = buf_pod;
+        KA(placement)[buf_pod] = buf_pl;
+        KA(events)[n_ev + lane] = buf_pod;
         n_ev += 64;
         n_buf = 0;
       }
@@ -2903,30 +2955,30 @@ if (!FL_NOTIME && tmg) {                                    \
           const int64_t kk = k;
           // the NodeClaim: requests, len(Pods), pre-check record (headroom, version)
           c_q += kk * preq_lane;
-          if (lane < KP_NRES) A->nc_requests[(size_t)placed * KP_NRES + lane] = c_q;
+          if (lane < KP_NRES) KA(nc_requests)[(size_t)placed * KP_NRES + lane] = c_q;
           c_r0 -= kk * pr0, c_r1 -= kk * pr1;
           if (four) c_r2 -= kk * pr2, c_r3 -= kk * pr3;
           c_ver += k;
           if (lane == 0) {
             npods[placed] = c1 + k;
-            int4* hp = reinterpret_cast<int4*>(A->nc_head + placed);
+            int4* hp = reinterpret_cast<int4*>(KA(nc_head) + placed);
             hp[0] = make_int4((int)c_r0, (int)(c_r0 >> 32), (int)c_r1, (int)(c_r1 >> 32));
             if (four) hp[1] = make_int4((int)c_r2, (int)(c_r2 >> 32), (int)c_r3, (int)(c_r3 >> 32));
-            A->nc_head[placed].ver = c_ver;
+            KA(nc_head)[placed].ver = c_ver;
           }
           // the k replays: one mutation-stack entry at wpos (k identical pushes leave just the last), the cursor
           stk_t += k;
           mstack_push_reg((int32_t LDS*)s_stk[0], stk_n, stk_lost, stk_t, wpos);
           a_cur_prev_stamp = stk_t;
           if (lane == 0) {
-            A->cur_nc[2 * sl] = wpos;
-            A->cur_nc[2 * sl + 1] = stk_t;
+            KA(cur_nc)[2 * sl] = wpos;
+            KA(cur_nc)[2 * sl + 1] = stk_t;
           }
           // the k pods: popped, placed (events in queue order after the buffered ones)
           if (n_buf + k > 64) {
             if (lane < n_buf) {
-              A->placement[buf_pod] = buf_pl;
-              A->events[n_ev + lane] = buf_pod;
+              KA(placement)[buf_pod] = buf_pl;
+              KA(events)[n_ev + lane] = buf_pod;
             }
             n_ev += n_buf;
             n_buf = 0;
@@ -2938,13 +2990,13 @@ if (!FL_NOTIME && tmg) {                                    \
           }
           n_buf += k;
           if (n_buf == 64) {
-            A->placement[buf_pod] = buf_pl;
-            A->events[n_ev + lane] = buf_pod;
+            KA(placement)[buf_pod] = buf_pl;
+            KA(events)[n_ev + lane] = buf_pod;
             n_ev += 64;
             n_buf = 0;
           }
           q_head += k;
-          if (q_head >= A->n_pods) q_head -= A->n_pods;
+          if (q_head >= KA(n_pods)) q_head -= KA(n_pods);
           q_len -= k;
           qw_next = off + 1 + k;
           pf_off = -1;
@@ -2958,13 +3010,14 @@ if (!FL_NOTIME && tmg) {                                    \
       FT(5);
     }
     if (lane < n_buf) {
-      A->placement[buf_pod] = buf_pl;
-      A->events[n_ev + lane] = buf_pod;
+      KA(placement)[buf_pod] = buf_pl;
+      KA(events)[n_ev + lane] = buf_pod;
     }
     n_ev += n_buf;
 #undef FT
 #undef FTF
 #undef FL_HAS_EX
+#undef KA
   
   // write back: control block, window, counters, hand-off
   if (lane == 0) {
