@@ -14,6 +14,9 @@ cfg = sys.argv[1] if len(sys.argv) > 1 else "2"
 if cfg.endswith("-off"):  # the fast lane without its continuation variant (kp_solve's choice overridden)
     os.environ["KP_CONT"] = "0"
     cfg = cfg[:-4]
+elif cfg.endswith("-on"):  # the fast lane with its continuation variant
+    os.environ["KP_CONT"] = "1"
+    cfg = cfg[:-3]
 n = int(sys.argv[2]) if len(sys.argv) > 2 else {"2": 50000, "2b": 50000, "3": 100000, "5": 100000}[cfg]
 lib = kpamd.load_lib()
 cat = catalog.build_catalog(lib)
