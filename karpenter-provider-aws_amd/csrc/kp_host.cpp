@@ -2562,17 +2562,33 @@ int32_t BuildBase(const kp_solve_in* in, const SolveRaw& raw, SolveBase& b) {
 // Exact Queue keys from the pods' UIDs (upstream NewQueue's last tie-break compares metadata.uid as strings): each
 // pod's rank in the batch sorted by UID, equal UIDs (invalid in a cluster) by batch index. false: a NULL UID.
 bool ExactUidKeys(const char* const* uids, uint32_t n, vector<uint64_t>& key) {
-  vector<uint32_t> idx(n);
+  // sorted by the first 8 bytes as a big-endian integer (zero-padded: the string order), strcmp only between equal
+  // prefixes; equal strings keep their input order
+  struct Ent {
+    uint64_t pre;
+    uint32_t i;
+  };
+  vector<Ent> e(n);
   for (uint32_t i = 0; i < n; i++) {
     if (!uids[i]) return false;
-    idx[i] = i;
+    uint64_t p = 0;
+    const unsigned char* u = (const unsigned char*)uids[i];
+    for (int j = 0; j < 8; j++) {
+      p = (p << 8) | u[j];
+      if (!u[j]) {  // shorter: the rest stays zero
+        p <<= 8 * (7 - j);
+        break;
+      }
+    }
+    e[i] = {p, i};
   }
-  std::sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) {
-    const int c = strcmp(uids[a], uids[b]);
-    return c != 0 ? c < 0 : a < b;
+  std::sort(e.begin(), e.end(), [&](const Ent& a, const Ent& b) {
+    if (a.pre != b.pre) return a.pre < b.pre;
+    const int c = strcmp(uids[a.i], uids[b.i]);
+    return c != 0 ? c < 0 : a.i < b.i;
   });
   key.assign(n, 0);
-  for (uint32_t r = 0; r < n; r++) key[idx[r]] = r;
+  for (uint32_t r = 0; r < n; r++) key[e[r].i] = r;
   return true;
 }
 
@@ -2734,6 +2750,7 @@ int32_t CompilePerCall(const kp_solve_in* in, const SolveRaw& raw, Compiled& cp)
   };
   vector<uint64_t> uidk;  // the UIDs themselves (ABI v10): their rank in string order is the exact key
   if (in->pod_uids && !ExactUidKeys(in->pod_uids, in->n_pods, uidk)) return fail(KP_E_INVAL, "null pod uid");
+  pt.lap(" queue: uid ranks");
   vector<QKey> qk(in->n_pods);
   for (uint32_t p = 0; p < in->n_pods; p++)
     qk[p] = {srank[cp.pod_shape[p]], (int32_t)p, in->pods[p].creation_unix, in->pod_uids ? uidk[p] : in->pods[p].uid_key};

@@ -82,6 +82,10 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 // wave-uniform value made provably uniform (SGPR): values read from LDS or global memory at a uniform address are
 // uniform in fact, but where the compiler cannot prove it the loop and branches around them become divergent code
 __device__ __forceinline__ int U(int x) { return __builtin_amdgcn_readfirstlane(x); }
+// Branch-weight hints for the single-wave Solve loop: the block placement makes the hinted-likely successor the
+// fall-through, and a taken branch costs a single wave ~20 cycles of instruction refetch (tools/micro/issue.hip)
+#define LIKELY(x) __builtin_expect(!!(x), 1)
+#define UNLIKELY(x) __builtin_expect(!!(x), 0)
 // the value's load has completed here (the compiler places the wait at this point, not at a later join)
 #define READY(x) asm volatile("" ::"v"(x))
 __device__ __forceinline__ uint64_t U64(uint64_t x) {
@@ -739,7 +743,7 @@ __device__ __forceinline__ uint64_t fits_lean(const DevDict& D, const CatHdr LDS
       same = j0_lane < n && slot >= 0 && fitv_lds[slot * FITV_CAP + j0_lane] >= q_lane;
     }
     const uint64_t act = __ballot(in_rr && q_lane > 0);
-    if (__ballot(!same) == 0) {
+    if (LIKELY(__ballot(!same) == 0)) {
       nb_probe(nb, (uint32_t)__popcll(act), TW);  // the algorithm's probe + row bytes, as below
       nb_row(nb, (uint32_t)__popcll(act), TW);
       if (lane < KP_NRES) jout[lane] = j0_lane;
@@ -1170,7 +1174,7 @@ __device__ __forceinline__ void mstack_push(int32_t LDS* stk, int32_t LDS* n_, i
 
 // mstack_query by one wave: 64 stack entries per step (two dependent LDS reads for a full stack instead of nine).
 __device__ __forceinline__ int mstack_query_wave(const int32_t LDS* stk, int n, int lost, int stamp) {
-  if (stamp < lost) return 0;
+  if (UNLIKELY(stamp < lost)) return 0;
   const int lane = LANE;
   int lo = 0, hi = n;  // answer: first entry with t > stamp, in [lo, hi]
   while (hi - lo > 64) {
@@ -1487,7 +1491,7 @@ __device__ __forceinline__ int sort_mut1_window(LdsI32 ord, LdsI32 npods, int n,
   const int pkey = piv ? npods[pid] : 0;
   const int K = __builtin_amdgcn_readfirstlane(key);  // npods of the mutated NodeClaim (position p)
   const uint64_t less = __ballot(lane > 0 && i < n && key < K);
-  if (!((less >> 1) & 1)) return p;  // Less(p + 1, p) false: sort.Slice leaves the order as it is
+  if (LIKELY(!((less >> 1) & 1))) return p;  // Less(p + 1, p) false: sort.Slice leaves the order as it is
   if (moved) *moved = true;
   if (n > 12) {
     if (n < 50) return -2;
@@ -2178,13 +2182,13 @@ if (!FL_NOTIME && tmg) {                                    \
       asm volatile("" : "+v"(kt0), "+v"(kt1), "+v"(kt2), "+v"(kt3), "+v"(kt4));
       const int len = q_len;
       const int head = q_head;
-      if (len <= 0 || pops_in + pops + memo_pops > pop_cap) break;
+      if (UNLIKELY(len <= 0 || pops_in + pops + memo_pops > pop_cap)) break;
       // Queue.Pop from the prefetched window: entries [qw_head, qw_head + qw_n) of the ring were in the queue when
       // the window was read, and nothing rewrites a queued entry (pushes go to the tail) or its pod's level and
       // lastLen stamps while it waits, so lane i's copy of entry qw_head + i stays exact.
       int off = head - qw_head;
       if (off < 0) off += KA(n_pods);
-      if (off != qw_next || off >= qw_n) {  // exhausted, or the ring wrapped onto re-pushed entries
+      if (UNLIKELY(off != qw_next || off >= qw_n)) {  // exhausted, or the ring wrapped onto re-pushed entries
         if (KA(cancel) && (int)(pops_in + pops + memo_pops) >= chk_next) {  // ctx.Done(): at most every 1024 pops
           chk_next = (int)(pops_in + pops + memo_pops) + 1024;
           if (cancel_set(KA(cancel))) {
@@ -2215,7 +2219,7 @@ if (!FL_NOTIME && tmg) {                                    \
       }
       qw_next = off + 1;  // only the fast lane pops: the next pop reads the following entry
       const int pod = __builtin_amdgcn_readlane(qw_pod, off);
-      if (__builtin_amdgcn_readlane(qw_epoch, off) == epoch && __builtin_amdgcn_readlane(qw_lastlen, off) == len)
+      if (UNLIKELY(__builtin_amdgcn_readlane(qw_epoch, off) == epoch && __builtin_amdgcn_readlane(qw_lastlen, off) == len))
         break;  // the full path's pop sees the same queue and ends the Solve
       FTF(6);
       const int shape = __builtin_amdgcn_readlane(qw_shape, off);
@@ -2225,7 +2229,7 @@ if (!FL_NOTIME && tmg) {                                    \
       int own, ce0, ce1, cur, stamp;
       int64_t preq_lane;
       uint64_t tolmask;
-      if (pf_off == off) {
+      if (LIKELY(pf_off == off)) {
         own = U(pf_own), ce0 = U(pf_ce0), ce1 = U(pf_ce1), cur = U(pf_cur), stamp = U(pf_stamp), preq_lane = pf_preq,
         tolmask = U64(pf_tol);
         if (sl == prev_sl) {  // the previous pod (same shape-level) advanced both cursors after the loads
@@ -2243,7 +2247,7 @@ if (!FL_NOTIME && tmg) {                                    \
         READY(preq_lane);
       }
       pf_off = -1;
-      if (off + 1 < qw_n) {  // the next entry's stage loads: in flight while this pod is sorted and placed
+      if (LIKELY(off + 1 < qw_n)) {  // the next entry's stage loads: in flight while this pod is sorted and placed
         const int nshape = __builtin_amdgcn_readlane(qw_shape, off + 1);
         const int nsl = __builtin_amdgcn_readlane(qw_sl, off + 1);
         pf_own = (TOPO ? 1 - KA(sl_fast_topo)[nsl] : 0) + (KA(hp_any) && KA(shape_hp_conf)[nshape] ? 1 : 0);
@@ -2265,7 +2269,7 @@ if (!FL_NOTIME && tmg) {                                    \
       const int ex_start = FL_HAS_EX ? min(ce0, mstack_query_wave((LdsI32)s_stk[1], U(s_ctl[14]), U(s_ctl[21]), ce1))
                                      : 0;
       FT(0);
-      if (!eligible) {
+      if (UNLIKELY(!eligible)) {
         handoff = pod;
         fb = FB_INELIGIBLE;
         break;
@@ -2506,7 +2510,7 @@ if (!FL_NOTIME && tmg) {                                    \
       FT(1);
       // sort.Slice(newNodeClaims) replay + first-fit start (sort arrays in LDS or chunked; the flat global order:
       // the full path)
-      if (!CHK && !in_lds) {
+      if (UNLIKELY(!CHK && !in_lds)) {
         handoff = pod;
         fb = FB_SPILLED;
         break;
@@ -2536,8 +2540,8 @@ if (!FL_NOTIME && tmg) {                                    \
         }
       } else {
         low = mut == 0 ? -1 : (mut == 1 ? sort_mut1_window(ord, npods, n_nc, mut_p, &n_moved) : -2);
-        if (low == -2) low = sort_newnodeclaims_wave(ord, npods, n_nc, mut, mut_p, 256, &KA(stats)[31]);
-        if (low == -2) {  // a long shift: the full path sorts (the pending mutation is still in s_ctl[10..11])
+        if (UNLIKELY(low == -2)) low = sort_newnodeclaims_wave(ord, npods, n_nc, mut, mut_p, 256, &KA(stats)[31]);
+        if (UNLIKELY(low == -2)) {  // a long shift: the full path sorts (the pending mutation is still in s_ctl[10..11])
           handoff = pod;
           fb = FB_SHIFT;
           break;
@@ -2759,8 +2763,8 @@ if (!FL_NOTIME && tmg) {                                    \
           uint64_t X = 0, m_v = 0;
           ReqView rv;
           bool perm = true;  // a failure here is permanent (NC_NEVER) unless it is Compatible's undefined-key rule
-          if (!full_add) {
-            if (n_rrp <= 4 && cat < 8) {
+          if (LIKELY(!full_add)) {
+            if (LIKELY(n_rrp <= 4 && cat < 8)) {
               X = fits_lean(D, (const CatHdr LDS*)&g_hdr[cat], X0, q_lane, j0_lane, (const int64_t LDS*)g_fitv, rrp,
                             n_rrp, fnb, (int32_t LDS*)fl_fitj);
             } else {
@@ -2795,8 +2799,8 @@ if (!FL_NOTIME && tmg) {                                    \
             }
           }
           FTF(11);
-          if (__ballot(X != 0)) {
-            if (full_add) {
+          if (LIKELY(__ballot(X != 0))) {
+            if (UNLIKELY(full_add)) {
               store_merged(reinterpret_cast<KReqs*>(KA(nc_reqs) + (size_t)ncx * sizeof(KReqs)), rv, m_v, D.W, D.KB);
               if (TOPO && KA(n_tk)) store_tcodes(KA(n_tk), KA(tk_keys), KA(nc_tcode), KA(hnc_stride), rv, m_v, ncx);
               if (lane == 0 && ncx < KA(ncc)) KA(nc_fail)[(size_t)sl * KA(ncc) + ncx] = NC_MERGED;
@@ -2804,11 +2808,11 @@ if (!FL_NOTIME && tmg) {                                    \
             // the remaining types and threshold indices are stored only when they changed (the append path
             // usually leaves both as they were): fewer vector-memory operations ahead of the next pod's loads
             const int32_t fj = lane < KP_NRES ? fl_fitj[lane] : 0;
-            if (__ballot(lane < D.TW && X != X0)) {
+            if (UNLIKELY(__ballot(lane < D.TW && X != X0))) {
               if (lane < D.TW) KA(nc_X)[(size_t)ncx * D.TW + lane] = X;
             }
             if (lane < KP_NRES) KA(nc_requests)[(size_t)ncx * KP_NRES + lane] = q_lane;
-            if (__ballot(lane < KP_NRES && fj != j0_lane)) {
+            if (UNLIKELY(__ballot(lane < KP_NRES && fj != j0_lane))) {
               if (lane < KP_NRES) KA(nc_fitj)[(size_t)ncx * KP_NRES + lane] = fj;
             }
             if (lane == 0) {
@@ -2870,7 +2874,7 @@ if (!FL_NOTIME && tmg) {                                    \
               }
               bytes += 16 * (uint64_t)rec_n;
             }
-            if (!full_add) {  // the append path left the requirements (hmin, catalogue) as they were
+            if (LIKELY(!full_add)) {  // the append path left the requirements (hmin, catalogue) as they were
               c_nc = ncx, c_cat = cat, c_hm = hm, c_X = X, c_q = q_lane, c_fj = fj;
               c_r0 = lane_bcast_i64(hv.r0, l) - pr0;
               c_r1 = lane_bcast_i64(hv.r1, l) - pr1;
@@ -2888,7 +2892,7 @@ if (!FL_NOTIME && tmg) {                                    \
       }
       wave_sync();
       FT(4);
-      if (placed == -1) {  // templates, a merge, minValues or a long scan: the full path takes over this pod
+      if (UNLIKELY(placed == -1)) {  // templates, a merge, minValues or a long scan: the full path takes over this pod
         handoff = pod;
         fb = why;
         break;
@@ -2913,7 +2917,7 @@ if (!FL_NOTIME && tmg) {                                    \
         buf_pod = pod;
         buf_pl = placed;
       }
-      if (++n_buf == 64) {
+      if (UNLIKELY(++n_buf == 64)) {
         KA(placement)[buf_pod] = buf_pl;
         KA(events)[n_ev + lane] = buf_pod;
         n_ev += 64;
