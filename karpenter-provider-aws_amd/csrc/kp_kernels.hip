@@ -2115,6 +2115,8 @@ __device__ __noinline__ int fast_lane(uint64_t kargs, int32_t LDS* s_dyn_arg, ui
     n_rrp_all++;
   }
   const uint64_t pop_cap = (uint64_t)A->n_pods * 64 + 65536;
+  // the pops this call may still make before the runaway guard (a 32-bit scalar compare per pod)
+  const int pop_left = U(pops_in >= pop_cap ? -1 : (int)min<uint64_t>(pop_cap - pops_in, (uint64_t)INT32_MAX));
   // control state in registers for the loop; written back on exit
   int q_head = U(s_ctl[0]), q_len = U(s_ctl[1]), n_ev = U(s_ctl[4]), mut = U(s_ctl[10]), mut_p = U(s_ctl[11]);
   int stk_n = U(s_ctl[12]), stk_t = U(s_ctl[13]), stk_lost = U(s_ctl[20]);  // in-flight mutation stack
@@ -2154,6 +2156,9 @@ __device__ __noinline__ int fast_lane(uint64_t kargs, int32_t LDS* s_dyn_arg, ui
       kt2 = 128 + lane < nw ? aw[128 + lane] : 0;
       kt3 = 192 + lane < nw ? aw[192 + lane] : 0;
       kt4 = 256 + lane < nw ? aw[256 + lane] : 0;
+      // landed before the loop: the per-pod asm barrier on these registers then needs no wait (otherwise the
+      // waitcnt pass puts a vmcnt(0) at every pod's start, which also waits for the previous pod's stores)
+      __builtin_amdgcn_s_waitcnt(0);
     }
 #define KA(f) ka_read<decltype(SolveArgs::f)>(kt0, kt1, kt2, kt3, kt4, offsetof(SolveArgs, f))
 #define FL_HAS_EX (EX)
@@ -2182,7 +2187,7 @@ if (!FL_NOTIME && tmg) {                                    \
       asm volatile("" : "+v"(kt0), "+v"(kt1), "+v"(kt2), "+v"(kt3), "+v"(kt4));
       const int len = q_len;
       const int head = q_head;
-      if (UNLIKELY(len <= 0 || pops_in + pops + memo_pops > pop_cap)) break;
+      if (UNLIKELY(len <= 0 || pops + memo_pops > pop_left)) break;
       // Queue.Pop from the prefetched window: entries [qw_head, qw_head + qw_n) of the ring were in the queue when
       // the window was read, and nothing rewrites a queued entry (pushes go to the tail) or its pod's level and
       // lastLen stamps while it waits, so lane i's copy of entry qw_head + i stays exact.
