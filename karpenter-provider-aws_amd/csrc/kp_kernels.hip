@@ -2076,7 +2076,11 @@ template <bool TOPO, bool CHK, bool EX, bool CONT>
 __device__ __noinline__ int fast_lane(uint64_t kargs, int32_t LDS* s_dyn_arg, uint64_t pops_in_arg) {
   // a callee's arguments arrive in VGPRs and count as divergent: made provably uniform here, or every value and
   // branch that depends on them (the whole pod loop) would be compiled as divergent control flow
-  int32_t LDS* s_dyn = (int32_t LDS*)(uintptr_t)__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)s_dyn_arg);
+  // (opaque: every caller passes the kernel's dynamic LDS array, and once the optimiser propagates that into this
+  // function each use becomes a scalar load of its offset from the dynamic-LDS table, with an lgkmcnt wait)
+  uint32_t s_dyn_off = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)s_dyn_arg);
+  asm volatile("" : "+s"(s_dyn_off));
+  int32_t LDS* s_dyn = (int32_t LDS*)(uintptr_t)s_dyn_off;
   const uint64_t pops_in = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(pops_in_arg >> 32)) << 32) |
                            (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)pops_in_arg);
   // the kernel's argument block (the kernarg segment pointer is only defined in the kernel itself: it passes it);
