@@ -25,6 +25,7 @@
 #include <set>
 #include <stdexcept>
 #include <string>
+#include <string_view>
 #include <unordered_map>
 #include <vector>
 
@@ -2142,6 +2143,71 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
   return KP_OK;
 }
 
+// An existing node's labels as requirements (NewExistingNode: each label `In {value}`, in input order), without the
+// per-label strings of a RawReqs: views into the caller's kp_labels (keys normalized), plus the hostname requirement's
+// value when some pod names kubernetes.io/hostname. Thousands of nodes × ~20 labels made the RawReqs form the largest
+// part of a Solve's host compile.
+struct NodeLabels {
+  vector<std::pair<std::string_view, std::string_view>> kv;  // normalized key, value (the hostname label dropped)
+  string host;                                               // the hostname requirement's value (has_host)
+  bool has_host = false;
+};
+// karpv1.NormalizedLabels (Normalize) without a string copy: the alias's target or the key itself
+std::string_view NormalizeSV(const char* k) {
+  static const std::pair<const char*, string> aliases[] = {
+      {"failure-domain.beta.kubernetes.io/zone", "topology.kubernetes.io/zone"},
+      {"beta.kubernetes.io/arch", "kubernetes.io/arch"},
+      {"beta.kubernetes.io/os", "kubernetes.io/os"},
+      {"beta.kubernetes.io/instance-type", "node.kubernetes.io/instance-type"},
+      {"failure-domain.beta.kubernetes.io/region", "topology.kubernetes.io/region"},
+      {"topology.ebs.csi.aws.com/zone", "topology.kubernetes.io/zone"},
+  };
+  for (auto& a : aliases)
+    if (strcmp(k, a.first) == 0) return a.second;
+  return k;
+}
+// Dictionary ids of label keys and values by view, memoised per compile (the Dict's maps take strings)
+struct LabelIds {
+  const Dict& d;
+  std::unordered_map<std::string_view, int> key;
+  std::unordered_map<int, std::unordered_map<std::string_view, int>> val;
+  explicit LabelIds(const Dict& dd) : d(dd) {}
+  int k(std::string_view s) {
+    auto it = key.find(s);
+    if (it != key.end()) return it->second;
+    return key.emplace(s, d.key(string(s))).first->second;
+  }
+  int b(int kk, std::string_view v) {
+    auto& m = val[kk];
+    auto it = m.find(v);
+    if (it != m.end()) return it->second;
+    return m.emplace(v, d.bit(kk, string(v))).first->second;
+  }
+};
+
+// Compile(d, labels as RawReqs) for a NodeLabels: each label Single(In {value}) Added in order, then the hostname one
+KReqs CompileNode(const Dict& d, const NodeLabels& nl, LabelIds& ids) {
+  KReqs q, s;
+  memset(&q, 0, sizeof q);
+  memset(&s, 0, sizeof s);
+  auto add = [&](int k, int bit) {  // Single(d, {key k, In, {value bit}}) then HostAdd, s back to zero after
+    s.present = 1ull << k;
+    s.vals[bit / 64] |= 1ull << (bit % 64);
+    HostAdd(d, q, s);
+    s.vals[bit / 64] = 0;
+    s.present = 0;
+  };
+  for (auto& kv : nl.kv) {
+    const int k = ids.k(kv.first);
+    add(k, ids.b(k, kv.second));
+  }
+  if (nl.has_host) {
+    const int k = d.key(kHostname);
+    add(k, d.bit(k, nl.host));
+  }
+  return q;
+}
+
 // Inputs of one Solve that are not part of its SolveBase: the pods' relaxation levels, node labels, spread keys.
 struct SolveRaw {
   vector<RawReqs> np_reqs;                        // per input NodePool (requirements + labels + nodepool key)
@@ -2154,7 +2220,7 @@ struct SolveRaw {
   std::set<string> topo_keys;                     // non-hostname spread keys (need a dictionary id)
   bool tolerate_pns = false;                      // some NodePool taint has effect PreferNoSchedule (NewScheduler)
   vector<int> pns_level;                          // per shape: the level toleratePreferNoScheduleTaints adds, or -1
-  vector<RawReqs> ex_labels;                      // per input existing node (hostname: see HostnameValue)
+  vector<NodeLabels> ex_labels;                   // per input existing node (hostname: see HostnameValue)
   bool hostname = false;                          // some pod requirement names kubernetes.io/hostname
 };
 
@@ -2245,8 +2311,17 @@ bool BaseCovers(const SolveBase& b, const SolveRaw& raw) {
   for (auto& lv : raw.levels)
     for (auto& r : lv)
       if (!Covers(b.d, r)) return false;
-  for (auto& l : raw.ex_labels)
-    if (!Covers(b.d, l)) return false;
+  {  // the node labels: every key and value in the dictionary (In requirements: no bound slots needed)
+    LabelIds ids(b.d);
+    const int kh = raw.hostname ? b.d.key(kHostname) : -1;
+    for (auto& nl : raw.ex_labels) {
+      for (auto& kv : nl.kv) {
+        const int k = ids.k(kv.first);
+        if (k < 0 || ids.b(k, kv.second) < 0) return false;
+      }
+      if (nl.has_host && (kh < 0 || b.d.bit(kh, nl.host) < 0)) return false;
+    }
+  }
   for (auto& k : raw.topo_keys)
     if (b.d.key(k) < 0) return false;
   return true;
@@ -2397,13 +2472,20 @@ int32_t ParseSolve(const kp_solve_in* in, SolveRaw& raw) {
   raw.ex_labels.resize(in->n_existing);
   for (uint32_t i = 0; i < in->n_existing; i++) {
     const kp_existing_node& e = in->existing[i];
-    raw.ex_labels[i] = LabelReqs(e.labels, e.n_labels, true);
+    NodeLabels& nl = raw.ex_labels[i];
+    nl.kv.reserve(e.n_labels);
+    for (uint32_t j = 0; j < e.n_labels; j++) {
+      const std::string_view k = NormalizeSV(e.labels[j].key ? e.labels[j].key : "");
+      if (k == kHostname) continue;  // (NewExistingNode's hostname requirement, below)
+      nl.kv.emplace_back(k, e.labels[j].value ? e.labels[j].value : "");
+    }
     if (raw.hostname) {  // NewExistingNode: hostname In {HostName()} (the label, else the node name)
       string host;
       for (uint32_t j = 0; j < e.n_labels; j++)
         if (e.labels[j].key && string(e.labels[j].key) == kHostname && e.labels[j].value) host = e.labels[j].value;
       if (host.empty()) host = e.name ? e.name : "";
-      raw.ex_labels[i].push_back({kHostname, KP_OP_IN, {host_named.count(host) ? host : string(kHostOther)}, -1});
+      nl.host = host_named.count(host) ? host : string(kHostOther);
+      nl.has_host = true;
     }
   }
   pt.lap(" parse: node labels");
@@ -2469,8 +2551,10 @@ int32_t BuildBase(const kp_solve_in* in, const SolveRaw& raw, SolveBase& b) {
   for (auto& lv : raw.levels)
     for (auto& r : lv) db.addReqs(r);
   for (auto& k : raw.topo_keys) db.bounded[k];
-  for (auto& l : raw.ex_labels)
-    for (auto& r : l) db.addLabel(r.key, r.values[0]);
+  for (auto& nl : raw.ex_labels) {
+    for (auto& kv : nl.kv) db.addLabel(string(kv.first), string(kv.second));
+    if (nl.has_host) db.addLabel(kHostname, nl.host);
+  }
   int32_t rc = db.build(b.d);
   if (rc) return rc;
   const Dict& d = b.d;
@@ -2620,10 +2704,11 @@ int32_t CompilePerCall(const kp_solve_in* in, const SolveRaw& raw, Compiled& cp)
     if ((p.initialized != 0) != (q.initialized != 0)) return p.initialized != 0;
     return strcmp(p.name ? p.name : "", q.name ? q.name : "") < 0;
   });
+  LabelIds lids(d);
   for (int i : ex) {
     const kp_existing_node& e = in->existing[i];
     cp.ex_input.push_back(i);
-    cp.ex_reqs.push_back(Compile(d, raw.ex_labels[i]));
+    cp.ex_reqs.push_back(CompileNode(d, raw.ex_labels[i], lids));
     vector<TaintT> ts;
     for (uint32_t j = 0; j < e.n_taints; j++)
       ts.push_back({e.taints[j].key ? e.taints[j].key : "", e.taints[j].value ? e.taints[j].value : "", e.taints[j].effect});
