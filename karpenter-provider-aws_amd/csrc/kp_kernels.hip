@@ -36,7 +36,7 @@
 #if !defined(KP_DIAG_BUILD) &&                                                                                       \
     (defined(FASTLANE) || defined(FL_NOTIME) || defined(FT_FINE) || defined(FAST_SCAN_MAX) ||                        \
      defined(FAST_CHK_LIVE) || defined(FAST_EX_ROUNDS) || defined(FAST_CONT) || defined(SORT_DIAG) || defined(EX_DIAG) || defined(FEAS_MAX_BLOCKS) ||                 \
-     defined(FEASQ_EW) || defined(FEASQ_ROWS) || defined(FEASQ_B128) || defined(FEASQ_SKIP_EVAL))
+     defined(FEASQ_EW) || defined(FEASQ_ROWS) || defined(FEASQ_B128) || defined(FEASQ_SKIP_EVAL) || defined(FL_SKIP))
 #error "a measurement knob is set outside a tools/ variant build (tools/kp_diag.h)"
 #endif
 #ifndef KP_DIAG_BUILD
@@ -64,6 +64,10 @@
 #ifndef FAST_CONT
 #define FAST_CONT 1  // the continuation round (the previous pod's NodeClaim tested from registers first)
 #endif
+#ifndef FL_SKIP
+#define FL_SKIP 0  // diagnostic cost attribution, WRONG PLACEMENTS: bit 0 no sort replay, bit 1 no mutation stack
+#endif             // (cursor as stored), bit 2 no statistics counters
+
 // Explicit address spaces: LDS data reached through a pointer would otherwise be read with FLAT loads (which wait
 // on the vector-memory counter too and take the long path); global rows get global_load.
 #define LDS __attribute__((address_space(3)))
@@ -1177,11 +1181,14 @@ __device__ __forceinline__ int mstack_query_wave(const int32_t LDS* stk, int n, 
   if (UNLIKELY(stamp < lost)) return 0;
   const int lane = LANE;
   int lo = 0, hi = n;  // answer: first entry with t > stamp, in [lo, hi]
+  // (every LDS read below is unconditional, at a clamped index, and its value masked after: a load under a lane
+  // condition is an exec-masked block with a branch and its own wait)
   while (hi - lo > 64) {
     const int step = (hi - lo + 63) >> 6;
     const int idx = lo + lane * step;
     const bool in = idx < hi;
-    const uint64_t bal = __ballot(in && stk[2 * idx] > stamp);
+    const int tv = stk[2 * min(idx, MSTK_CAP - 1)];
+    const uint64_t bal = __ballot(in && tv > stamp);
     if (!bal) {
       lo = lo + (__popcll(__ballot(in)) - 1) * step + 1;  // past the last sample taken (< hi)
     } else {
@@ -1195,7 +1202,8 @@ __device__ __forceinline__ int mstack_query_wave(const int32_t LDS* stk, int n, 
     }
   }
   if (hi > lo) {
-    const uint64_t bal = __ballot(lo + lane < hi && stk[2 * (lo + lane)] > stamp);
+    const int tv = stk[2 * min(lo + lane, MSTK_CAP - 1)];
+    const uint64_t bal = __ballot(lo + lane < hi && tv > stamp);
     lo = bal ? lo + __builtin_ctzll(bal) : hi;
   }
   return lo < n ? stk[2 * lo + 1] : INT32_MAX;
@@ -1479,16 +1487,21 @@ __device__ __forceinline__ int sort_newnodeclaims_wave(P ord, P npods, int n, in
 // LDS reads in all). When pdqsort would do a stable move (n <= 12: insertion sort; n >= 50 with increasingHint:
 // partialInsertionSort) and the moved NodeClaim's new place is within the window, the ids already in registers
 // are written back shifted. Returns the cursor clamp (p), or -2: the general replay (sort_newnodeclaims_wave).
-__device__ __forceinline__ int sort_mut1_window(LdsI32 ord, LdsI32 npods, int n, int p, bool* moved = nullptr) {
+__device__ __forceinline__ int sort_mut1_window(LdsI32 ord, LdsI32 npods, int n, int p, int cap,
+                                                 bool* moved = nullptr) {
   const int lane = LANE;
   const int i = p + lane;
   const int t = lane / 3;
   const int pidx = (n / 4) * (t + 1) + (lane % 3) - 1;  // choosePivot's samples (lanes 0..8, n >= 50)
   const bool piv = lane < 9 && n >= 50;
-  const int id = i < n ? ord[i] : 0;
-  const int pid = piv ? ord[pidx] : 0;
-  const int key = i < n ? npods[id] : INT32_MAX;
-  const int pkey = piv ? npods[pid] : 0;
+  // unconditional reads at clamped indices (cap: the arrays' length), values masked after: no exec-masked blocks
+  const int id_r = ord[min(i, cap - 1)];
+  const int pid_r = ord[piv ? pidx : 0];
+  const int id = i < n ? id_r : 0;
+  const int pid = piv ? pid_r : 0;
+  const int key_r = npods[id], pkey_r = npods[pid];
+  const int key = i < n ? key_r : INT32_MAX;
+  const int pkey = piv ? pkey_r : 0;
   const int K = __builtin_amdgcn_readfirstlane(key);  // npods of the mutated NodeClaim (position p)
   const uint64_t less = __ballot(lane > 0 && i < n && key < K);
   if (LIKELY(!((less >> 1) & 1))) return p;  // Less(p + 1, p) false: sort.Slice leaves the order as it is
@@ -1514,7 +1527,17 @@ __device__ __forceinline__ int sort_mut1_window(LdsI32 ord, LdsI32 npods, int n,
 // mutation stack push (mstack_push) with the stack's size / lost time / clock in registers (uniform)
 __device__ __forceinline__ void mstack_push_reg(int32_t LDS* stk, int& n, int& lost, int t, int pos) {
   const int lane = LANE;
-  while (n > 0 && stk[2 * (n - 1) + 1] >= pos) n--;
+  // pop the entries whose position is >= pos: positions increase bottom to top, so they are a suffix, found 64 entries
+  // per LDS read (one read in the common case instead of one dependent read per popped entry)
+  for (;;) {
+    const int base = max(0, n - 64);
+    const int j = base + lane;
+    const int pv = stk[2 * min(j, MSTK_CAP - 1) + 1];
+    const uint64_t ge = __ballot(j < n && pv >= pos);
+    if (!ge) break;                         // nothing to pop
+    n = base + __builtin_ctzll(ge);         // the suffix starts here ...
+    if (n > base || base == 0) break;       // ... unless it may reach below this window
+  }
   if (n == MSTK_CAP) {
     const int h = MSTK_CAP / 2;
     lost = stk[2 * (h - 1)];
@@ -2130,7 +2153,9 @@ __device__ __noinline__ int fast_lane(uint64_t kargs, int32_t LDS* s_dyn_arg, ui
   int qw_head = U(S->qw_head), qw_n = U(S->qw_n), qw_next = U(S->qw_next);
   int qw_pod = S->qw_pod[lane], qw_shape = S->qw_shape[lane], qw_sl = S->qw_sl[lane], qw_lastlen = S->qw_lastlen[lane],
       qw_epoch = S->qw_epoch[lane];
-  uint64_t bytes = 0, attempts = 0, scanned = 0, starts = 0, fcyc[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  // statistics: uniform counters (a lane-0 update of a per-lane 64-bit value costs an exec-masked block per pod: 6 % of
+  // config 2's kernel, measured); the positions scanned are n_scan below
+  uint64_t bytes = 0, attempts = 0, starts = 0, fcyc[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   int pops = 0, memo_pops = 0, handoff = -1, fb = -1, fl_last = -1;
   int chk_next = U(s_ctl[32]);  // kp_cancel: Queue pops (the Solve's total) at which the flag is read next
   // the NodeClaim this call's last append commit wrote, as it wrote it (the next pod usually starts there: reading
@@ -2527,7 +2552,7 @@ if (!FL_NOTIME && tmg) {                                    \
       const LdsI32 ord = (LdsI32)s_dyn;
       const LdsI32 npods = (LdsI32)(s_dyn + KA(sort_cap));
       const ChkDir cd = chk_dir(s_dyn);
-      const int c19 = min(cur, mstack_query_wave((LdsI32)s_stk[0], stk_n, stk_lost, stamp));
+      const int c19 = (FL_SKIP & 2) ? cur : min(cur, mstack_query_wave((LdsI32)s_stk[0], stk_n, stk_lost, stamp));
       const int n_nc = n_nc_all;
       FTF(8);
       int low;
@@ -2548,7 +2573,7 @@ if (!FL_NOTIME && tmg) {                                    \
           break;
         }
       } else {
-        low = mut == 0 ? -1 : (mut == 1 ? sort_mut1_window(ord, npods, n_nc, mut_p, &n_moved) : -2);
+        low = mut == 0 ? -1 : (mut == 1 ? ((FL_SKIP & 1) ? mut_p : sort_mut1_window(ord, npods, n_nc, mut_p, KA(sort_cap), &n_moved)) : -2);
         if (UNLIKELY(low == -2)) low = sort_newnodeclaims_wave(ord, npods, n_nc, mut, mut_p, 256, &KA(stats)[31]);
         if (UNLIKELY(low == -2)) {  // a long shift: the full path sorts (the pending mutation is still in s_ctl[10..11])
           handoff = pod;
@@ -2559,7 +2584,7 @@ if (!FL_NOTIME && tmg) {                                    \
       FTF(9);
       const int start = min(min(c19, low >= 0 ? low : INT32_MAX), n_nc);
       mut = 0;
-      if (low >= 0) mstack_push_reg((int32_t LDS*)s_stk[0], stk_n, stk_lost, ++stk_t, low);
+      if (low >= 0 && !(FL_SKIP & 2)) mstack_push_reg((int32_t LDS*)s_stk[0], stk_n, stk_lost, ++stk_t, low);
       wave_sync();
       FT(2);
       if (memo) {  // the full path's failure: cursors at the end, Preferences.Relax, Queue.Push
@@ -2598,7 +2623,7 @@ if (!FL_NOTIME && tmg) {                                    \
                   mut_was1 && !n_moved && sl == cont_sl && rr_b4p == 0 && c_hm == 0;
       bool bail = !CHK && n_nc - start > FAST_SCAN_MAX && !cont;
       if (bail) why = FB_SCAN;
-      if (lane == 0 && !bail) starts += start;
+      if (!(FL_SKIP & 4) && !bail) starts += (uint32_t)start;
       // chunked order: the start position's chunk and slot, the window of chunks whose live mask is in lm
       int ch0 = 0, cs0 = 0, cc = 0, lm_base = 0, n_live = 0;
       uint64_t lm = 0;
@@ -2657,7 +2682,8 @@ if (!FL_NOTIME && tmg) {                                    \
           }
           i = base + lane;
           valid = i < n_nc;
-          nc = valid ? ord[i] : 0;
+          const int nc_r = ord[min(i, KA(sort_cap) - 1)];  // (unconditional read, masked after)
+          nc = valid ? nc_r : 0;
           nscan = min(64, n_nc - base);
           base += 64;
         }
@@ -2716,8 +2742,7 @@ if (!FL_NOTIME && tmg) {                                    \
           }
           tag = cand && (fl >= NC_MERGED || triv) && pinned;
         }
-        if (lane == 0) scanned += nscan;
-        n_scan += (uint32_t)nscan;
+        if (!(FL_SKIP & 4)) n_scan += (uint32_t)nscan;
         uint64_t cm = __ballot(cand);
         const uint64_t tm = __ballot(tag);
         if (TOPO && t_n && ipos == INT32_MAX) {
@@ -3055,7 +3080,7 @@ if (!FL_NOTIME && tmg) {                                    \
              (uint64_t)n_app * ((uint64_t)D.TW * 8 + KP_NRES * 8 + 8) + (uint64_t)n_scan * (12 + 16 * A->n_req_res);
     S->bytes += bytes;
     S->attempts += attempts;
-    S->scanned += scanned;
+    S->scanned += n_scan;
     S->starts += starts;
     S->fpods += pops;
     for (int i = 0; i < 14; i++) S->fcyc[i] += fcyc[i];
@@ -4609,7 +4634,7 @@ __global__ __launch_bounds__(FEASB_WAVES * 64, FEASB_MINW) void feasibility_bits
 #endif
 static_assert(KP_DIAG_BUILD || (FASTLANE == 1 && FL_NOTIME == 1 && FT_FINE == 0 && FAST_SCAN_MAX == 512 &&
                                  FAST_CHK_LIVE == 8 && FAST_EX_ROUNDS == 8 && FAST_CONT == 1 && SORT_DIAG == 0 && EX_DIAG == 0 && FEAS_MAX_BLOCKS == 65536 &&
-                                 FEASQ_EW == 7 && FEASQ_ROWS == 28 && FEASQ_B128 == 1 && FEASQ_SKIP_EVAL == 0),
+                                 FEASQ_EW == 7 && FEASQ_ROWS == 28 && FEASQ_B128 == 1 && FEASQ_SKIP_EVAL == 0 && FL_SKIP == 0),
               "the production build carries the production values of every measurement knob");
 __global__ __launch_bounds__(FEASB_WAVES * 64, FEASB_MINW) void feasibility_quad_kernel(FeasArgs a) {
   __shared__ DevDict D;
