@@ -741,10 +741,12 @@ __device__ __forceinline__ uint64_t fits_lean(const DevDict& D, const CatHdr LDS
 #pragma unroll
     for (int k = 0; k < 4; k++)
       if (k < nr && (int)((rr >> (8 * k)) & 0xff) == lane) in_rr = true;
-    if (in_rr && q_lane > 0) {
-      const int n = H->fit_n[lane];
-      const int slot = H->fit_slot[lane];
-      same = j0_lane < n && slot >= 0 && fitv_lds[slot * FITV_CAP + j0_lane] >= q_lane;
+    {  // unconditional LDS reads at clamped indices, the lanes outside the requested resources masked after
+      const int ln = min(lane, KP_NRES - 1);
+      const int n = H->fit_n[ln];
+      const int slot = H->fit_slot[ln];
+      const int64_t fv = fitv_lds[max(slot, 0) * FITV_CAP + min(max(j0_lane, 0), FITV_CAP - 1)];
+      same = !(in_rr && q_lane > 0) || (j0_lane < n && slot >= 0 && fv >= q_lane);
     }
     const uint64_t act = __ballot(in_rr && q_lane > 0);
     if (LIKELY(__ballot(!same) == 0)) {
@@ -2275,7 +2277,8 @@ if (!FL_NOTIME && tmg) {                                    \
       } else {
         own = U((TOPO ? 1 - KA(sl_fast_topo)[sl] : 0) + (KA(hp_any) && KA(shape_hp_conf)[shape] ? 1 : 0));
         ce0 = U(FL_HAS_EX ? KA(cur_ex)[2 * sl] : 0), ce1 = U(FL_HAS_EX ? KA(cur_ex)[2 * sl + 1] : 0);
-        preq_lane = lane < KP_NRES ? KA(shape_requests)[(size_t)shape * KP_NRES + lane] : 0;
+        const int64_t pq_r = KA(shape_requests)[(size_t)shape * KP_NRES + min(lane, KP_NRES - 1)];
+        preq_lane = lane < KP_NRES ? pq_r : 0;
         tolmask = U64(KA(shape_tolerates)[sl]);
         cur = U(KA(cur_nc)[2 * sl]), stamp = U(KA(cur_nc)[2 * sl + 1]);
         READY(preq_lane);
@@ -2286,7 +2289,8 @@ if (!FL_NOTIME && tmg) {                                    \
         const int nsl = __builtin_amdgcn_readlane(qw_sl, off + 1);
         pf_own = (TOPO ? 1 - KA(sl_fast_topo)[nsl] : 0) + (KA(hp_any) && KA(shape_hp_conf)[nshape] ? 1 : 0);
         pf_ce0 = FL_HAS_EX ? KA(cur_ex)[2 * nsl] : 0, pf_ce1 = FL_HAS_EX ? KA(cur_ex)[2 * nsl + 1] : 0;
-        pf_preq = lane < KP_NRES ? KA(shape_requests)[(size_t)nshape * KP_NRES + lane] : 0;
+        const int64_t pq_r = KA(shape_requests)[(size_t)nshape * KP_NRES + min(lane, KP_NRES - 1)];
+        pf_preq = lane < KP_NRES ? pq_r : 0;
         pf_tol = KA(shape_tolerates)[nsl];
         pf_cur = KA(cur_nc)[2 * nsl], pf_stamp = KA(cur_nc)[2 * nsl + 1];
         pf_off = off + 1;
@@ -2388,33 +2392,36 @@ if (!FL_NOTIME && tmg) {                                    \
           const bool valid = ec < E;
           bool cand = false, icand = false;
           int32_t ver = 0, ts = 0;
-          if (valid) {
-            const int32_t fl = KA(ex_fail)[(size_t)sl * E + ec];
-            ver = KA(ex_ver)[ec];
-            ts = KA(ex_taintset)[ec];
-            const uint8_t sok = KA(ex_static_ok)[ec];
-            cand = KA(ex_room)[ec] >= pr0 && KA(ex_room)[(size_t)E + ec] >= pr1;
-            if (four) cand = cand && KA(ex_room)[2 * (size_t)E + ec] >= pr2 && KA(ex_room)[3 * (size_t)E + ec] >= pr3;
-            cand = cand && fl != ver && fl != NC_NEVER && sok && ((tolmask >> ts) & 1);
-            if (rr_b4p && cand) {  // a fifth requested resource and beyond
-              const int64_t* av = KA(ex_available) + (size_t)ec * KP_NRES;
-              const int64_t* rq = KA(ex_requests) + (size_t)ec * KP_NRES;
+          {  // every read unconditional at a clamped position, the lanes past E masked after (no exec-masked block)
+            const int ecc = min(ec, E - 1);
+            const int32_t fl = KA(ex_fail)[(size_t)sl * E + ecc];
+            ver = KA(ex_ver)[ecc];
+            ts = KA(ex_taintset)[ecc];
+            const uint8_t sok = KA(ex_static_ok)[ecc];
+            const int64_t er0 = KA(ex_room)[ecc], er1 = KA(ex_room)[(size_t)E + ecc];
+            const int64_t er2 = four ? KA(ex_room)[2 * (size_t)E + ecc] : INT64_MAX;
+            const int64_t er3 = four ? KA(ex_room)[3 * (size_t)E + ecc] : INT64_MAX;
+            cand = valid & (er0 >= pr0) & (er1 >= pr1) & (er2 >= pr2) & (er3 >= pr3) & (fl != ver) & (fl != NC_NEVER) &
+                   (sok != 0) & (((tolmask >> ts) & 1) != 0);
+            if (UNLIKELY(rr_b4p)) {  // a fifth requested resource and beyond
+              const int64_t* av = KA(ex_available) + (size_t)ecc * KP_NRES;
+              const int64_t* rq = KA(ex_requests) + (size_t)ecc * KP_NRES;
               for (uint32_t rm = rr_b4p; rm; rm &= rm - 1) {
                 const int r = __builtin_ctz(rm);
-                cand = cand && rq[r] + lane_bcast_i64(preq_lane, r) <= av[r];
+                cand = cand & (rq[r] + lane_bcast_i64(preq_lane, r) <= av[r]);
               }
             }
             if (TOPO && t_n) {
 #pragma unroll
               for (int j = 0; j < 4; j++)
                 if (j < t_n && t_key[j] < 0)
-                  cand = cand && (int)KA(hcnt_ex)[(size_t)t_row[j] * E + ec] + t_self[j] <= t_mskew[j];
+                  cand = cand & ((int)KA(hcnt_ex)[(size_t)t_row[j] * E + ecc] + t_self[j] <= t_mskew[j]);
               icand = cand;
 #pragma unroll
               for (int j = 0; j < 4; j++)
                 if (j < t_n && t_key[j] >= 0) {
-                  const uint32_t code = KA(ex_tcode)[(size_t)t_slot[j] * E + ec];
-                  cand = cand && code != 0xFF && ((t_acc[j] >> (code & 63)) & 1);
+                  const uint32_t code = KA(ex_tcode)[(size_t)t_slot[j] * E + ecc];
+                  cand = cand & (code != 0xFF) & (((t_acc[j] >> (code & 63)) & 1) != 0);
                 }
             }
           }
@@ -2703,19 +2710,33 @@ if (!FL_NOTIME && tmg) {                                    \
           const KReqs* cr0 = kreq_at(KA(nc_reqs), nc0);
           hm0 = cr0->hmin & cr0->present;
           cat0 = KA(nc_cat)[nc0];
-          X00 = lane < D.TW ? KA(nc_X)[(size_t)nc0 * D.TW + lane] : 0;
-          rq0 = lane < KP_NRES ? KA(nc_requests)[(size_t)nc0 * KP_NRES + lane] : 0;
-          j00 = lane < KP_NRES ? KA(nc_fitj)[(size_t)nc0 * KP_NRES + lane] : 0;
+          // (unconditional reads at clamped lanes, masked after)
+          const uint64_t x_r = KA(nc_X)[(size_t)nc0 * D.TW + min(lane, D.TW - 1)];
+          const int64_t q_r = KA(nc_requests)[(size_t)nc0 * KP_NRES + min(lane, KP_NRES - 1)];
+          const int32_t j_r = KA(nc_fitj)[(size_t)nc0 * KP_NRES + min(lane, KP_NRES - 1)];
+          X00 = lane < D.TW ? x_r : 0;
+          rq0 = lane < KP_NRES ? q_r : 0;
+          j00 = lane < KP_NRES ? j_r : 0;
         }
-        if (valid) {
-          // every gather issued unconditionally: one round trip
-          const int32_t fl = cont_round ? NC_MERGED : nc < KA(ncc) ? KA(nc_fail)[(size_t)sl * KA(ncc) + nc] : -2;
-          if (nc == c_nc) hv = HeadView{c_r0, c_r1, c_r2, c_r3, c_ver, c_ts};
-          else hv = load_head(KA(nc_head) + nc, four);
+        {
+          // every gather issued unconditionally (the lanes past the order read NodeClaim 0 and are masked after): one
+          // round trip and no exec-masked block
+          int32_t fl = NC_MERGED;
+          if (LIKELY(!cont_round)) {
+            const int ncc_ = KA(ncc);
+            const int32_t fl_r = KA(nc_fail)[(size_t)sl * ncc_ + min(nc, ncc_ - 1)];
+            fl = nc < ncc_ ? fl_r : -2;
+            const HeadView ld = load_head(KA(nc_head) + nc, four);
+            const bool mine = nc == c_nc;
+            hv = HeadView{mine ? c_r0 : ld.r0, mine ? c_r1 : ld.r1, mine ? c_r2 : ld.r2,
+                          mine ? c_r3 : ld.r3, mine ? c_ver : ld.ver, mine ? c_ts : ld.ts};
+          } else {
+            hv = HeadView{c_r0, c_r1, c_r2, c_r3, c_ver, c_ts};
+          }
           ver = hv.ver;
           const int32_t ts = hv.ts;
-          bool fit = hv.r0 >= pr0 && hv.r1 >= pr1 && hv.r2 >= pr2 && hv.r3 >= pr3;
-          if (rr_b4p) {  // a fifth requested resource and beyond (that the pod requests)
+          bool fit = (hv.r0 >= pr0) & (hv.r1 >= pr1) & (hv.r2 >= pr2) & (hv.r3 >= pr3);
+          if (UNLIKELY(rr_b4p)) {  // a fifth requested resource and beyond (that the pod requests)
             const int64_t* rq = KA(nc_requests) + (size_t)nc * KP_NRES;
             const int64_t* mx = KA(nc_maxalloc) + (size_t)nc * KP_NRES;
             for (uint32_t rm = rr_b4p; rm; rm &= rm - 1) {
@@ -2723,20 +2744,20 @@ if (!FL_NOTIME && tmg) {                                    \
               fit = fit & (rq[r] + lane_bcast_i64(preq_lane, r) <= mx[r]);
             }
           }
-          cand = fit && fl != ver && fl != NC_NEVER && ((tolmask >> ts) & 1);
+          cand = valid & fit & (fl != ver) & (fl != NC_NEVER) & (((tolmask >> ts) & 1) != 0);
           if (CHK) pfail = !fit || fl == NC_NEVER || !((tolmask >> ts) & 1);  // permanent (see the full path)
           bool pinned = true;  // every dictionary key the pod spreads over is one value on the NodeClaim
           if (TOPO && t_n) {
 #pragma unroll
             for (int j = 0; j < 4; j++)
               if (j < t_n && t_key[j] < 0)
-                cand = cand && (int)KA(hcnt_nc)[(size_t)t_row[j] * KA(hnc_stride) + nc] + t_self[j] <= t_mskew[j];
+                cand = cand & ((int)KA(hcnt_nc)[(size_t)t_row[j] * KA(hnc_stride) + nc] + t_self[j] <= t_mskew[j]);
             icand = cand;
 #pragma unroll
             for (int j = 0; j < 4; j++)
               if (j < t_n && t_key[j] >= 0) {
                 const uint32_t code = KA(nc_tcode)[(size_t)t_slot[j] * KA(hnc_stride) + nc];
-                cand = cand && (code == 0xFF || (code < 64 && ((t_acc[j] >> code) & 1)));
+                cand = cand & ((code == 0xFF) | ((code < 64) & (((t_acc[j] >> (code & 63)) & 1) != 0)));
                 pinned = pinned && code < 64;
               }
           }
@@ -2780,9 +2801,12 @@ if (!FL_NOTIME && tmg) {                                    \
             const KReqs* cr = kreq_at(KA(nc_reqs), ncx);
             hm = cr->hmin & cr->present;
             cat = KA(nc_cat)[ncx];
-            X0 = lane < D.TW ? KA(nc_X)[(size_t)ncx * D.TW + lane] : 0;
-            rq_lane = lane < KP_NRES ? KA(nc_requests)[(size_t)ncx * KP_NRES + lane] : 0;
-            j0_lane = lane < KP_NRES ? KA(nc_fitj)[(size_t)ncx * KP_NRES + lane] : 0;
+            const uint64_t x_r = KA(nc_X)[(size_t)ncx * D.TW + min(lane, D.TW - 1)];
+            const int64_t q_r = KA(nc_requests)[(size_t)ncx * KP_NRES + min(lane, KP_NRES - 1)];
+            const int32_t j_r = KA(nc_fitj)[(size_t)ncx * KP_NRES + min(lane, KP_NRES - 1)];
+            X0 = lane < D.TW ? x_r : 0;
+            rq_lane = lane < KP_NRES ? q_r : 0;
+            j0_lane = lane < KP_NRES ? j_r : 0;
           }
           FTF(10);
           const int64_t q_lane = rq_lane + preq_lane;
