@@ -579,8 +579,13 @@ __device__ __forceinline__ int32_t fits_rows(const DevDict& D, const CatHdr LDS*
     const int slot = H->fit_slot[r];
     const int idx = j0 + lane;
     uint64_t bal;
-    if (slot >= 0) bal = __ballot(idx < n && fitv_lds[slot * FITV_CAP + idx] >= q);
-    else bal = __ballot(idx < n && H->d.fit_vals[(size_t)r * D.T + idx] >= q);
+    if (slot >= 0) {  // (unconditional reads at a clamped index, masked after)
+      const int64_t fv = fitv_lds[slot * FITV_CAP + min(idx, FITV_CAP - 1)];
+      bal = __ballot(idx < n && fv >= q);
+    } else {
+      const int64_t fv = H->d.fit_vals[(size_t)r * D.T + min(idx, D.T - 1)];
+      bal = __ballot(idx < n && fv >= q);
+    }
     nb += 512;
     int j;
     if (bal) j = j0 + __builtin_ctzll(bal);
@@ -770,8 +775,13 @@ __device__ __forceinline__ uint64_t fits_lean(const DevDict& D, const CatHdr LDS
     const int slot = H->fit_slot[r];
     const int idx = j0 + lane;
     uint64_t bal;
-    if (slot >= 0) bal = __ballot(idx < n && fitv_lds[slot * FITV_CAP + idx] >= q);
-    else bal = __ballot(idx < n && H->d.fit_vals[(size_t)r * D.T + idx] >= q);
+    if (slot >= 0) {  // (unconditional reads at a clamped index, masked after)
+      const int64_t fv = fitv_lds[slot * FITV_CAP + min(idx, FITV_CAP - 1)];
+      bal = __ballot(idx < n && fv >= q);
+    } else {
+      const int64_t fv = H->d.fit_vals[(size_t)r * D.T + min(idx, D.T - 1)];
+      bal = __ballot(idx < n && fv >= q);
+    }
     nb_probe(nb, 1, TW);
     int j;
     if (bal) j = j0 + __builtin_ctzll(bal);
@@ -790,10 +800,10 @@ __device__ __forceinline__ uint64_t fits_lean(const DevDict& D, const CatHdr LDS
   if (lane < KP_NRES) jout[lane] = j_lane;
   if (zero) return 0;
   const bool lv = lane < TW;
-  const uint64_t w0 = (rowp[0] && lv) ? rowp[0][lane] : ~0ull;
-  const uint64_t w1 = (rowp[1] && lv) ? rowp[1][lane] : ~0ull;
-  const uint64_t w2 = (rowp[2] && lv) ? rowp[2][lane] : ~0ull;
-  const uint64_t w3 = (rowp[3] && lv) ? rowp[3][lane] : ~0ull;
+  const int lw = min(lane, TW - 1);  // (unconditional row reads at a clamped word, masked after)
+  const uint64_t r0 = rowp[0] ? rowp[0][lw] : ~0ull, r1 = rowp[1] ? rowp[1][lw] : ~0ull;
+  const uint64_t r2 = rowp[2] ? rowp[2][lw] : ~0ull, r3 = rowp[3] ? rowp[3][lw] : ~0ull;
+  const uint64_t w0 = lv ? r0 : ~0ull, w1 = lv ? r1 : ~0ull, w2 = lv ? r2 : ~0ull, w3 = lv ? r3 : ~0ull;
   return X & w0 & w1 & w2 & w3;
 }
 
@@ -2865,7 +2875,8 @@ if (!FL_NOTIME && tmg) {                                    \
             }
             // the remaining types and threshold indices are stored only when they changed (the append path
             // usually leaves both as they were): fewer vector-memory operations ahead of the next pod's loads
-            const int32_t fj = lane < KP_NRES ? fl_fitj[lane] : 0;
+            const int32_t fj_r = fl_fitj[min(lane, KP_NRES - 1)];  // (unconditional, masked after)
+            const int32_t fj = lane < KP_NRES ? fj_r : 0;
             if (UNLIKELY(__ballot(lane < D.TW && X != X0))) {
               if (lane < D.TW) KA(nc_X)[(size_t)ncx * D.TW + lane] = X;
             }
