@@ -1639,8 +1639,9 @@ __device__ __forceinline__ int chk_find_lane(const ChkDir& d, int nch, int pos) 
 }
 __device__ __forceinline__ void chk_load(const ChkBlk* B, int b, int cnt, int& id, int& key) {
   const int lane = LANE;
-  id = lane < cnt ? B[b].id[lane] : -1;
-  key = lane < cnt ? B[b].key[lane] : INT32_MAX;
+  const int id_r = B[b].id[lane], key_r = B[b].key[lane];  // (unconditional: a block holds 64 entries)
+  id = lane < cnt ? id_r : -1;
+  key = lane < cnt ? key_r : INT32_MAX;
 }
 __device__ __forceinline__ void chk_store(ChkBlk* B, int b, int cnt, int id, int key) {
   const int lane = LANE;
@@ -2658,11 +2659,10 @@ if (!FL_NOTIME && tmg) {                                    \
         int nc, c_bid = 0, c_bkey = 0;
         if (CHK) {
           while (!lm && cc < nch) {  // the next window's live chunks (dead ones: every NodeClaim fails permanently)
-            bool live = false;
-            if (cc + lane < nch) {
-              const int b = ci_blk(cd.info[cc + lane]);
-              live = !(can_dead && deadrow[b] == cd.bep[b]);
-            }
+            // (unconditional reads at a clamped directory index, masked after)
+            const int b = ci_blk(cd.info[min(cc + lane, CHK_MAXC - 1)]);
+            const bool dead = can_dead && deadrow[b] == cd.bep[b];
+            const bool live = cc + lane < nch && !dead;
             lm = __ballot(live);
             lm_base = cc;
             cc = min(cc + 64, nch);
@@ -2678,8 +2678,9 @@ if (!FL_NOTIME && tmg) {                                    \
           const uint32_t v = cd.info[ck];
           valid = lane < ci_cnt(v) && !(ck == ch0 && lane < cs0);
           // the chunk's block (ids and keys) in one batch: the winner's chunk is the next replay's
-          c_bid = lane < ci_cnt(v) ? KA(chk_blk)[ci_blk(v)].id[lane] : -1;
-          c_bkey = lane < ci_cnt(v) ? KA(chk_blk)[ci_blk(v)].key[lane] : INT32_MAX;
+          const int bid_r = KA(chk_blk)[ci_blk(v)].id[lane], bkey_r = KA(chk_blk)[ci_blk(v)].key[lane];
+          c_bid = lane < ci_cnt(v) ? bid_r : -1;
+          c_bkey = lane < ci_cnt(v) ? bkey_r : INT32_MAX;
           nc = valid ? c_bid : 0;
           i = cd.start[ck] + lane;
           nscan = __popcll(__ballot(valid));
@@ -3607,11 +3608,9 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a0, const Solv
           // live chunks of the window [cc, cc + 64), in order (every wave computes the same mask); round k of wave w
           // takes the (k * NW + w)-th
           const int nch = g_chk.nch;
-          bool live = false;
-          if (cc + lane < nch) {
-            const int b = ci_blk(cd.info[cc + lane]);
-            live = !(can_dead && deadrow[b] == cd.bep[b]);
-          }
+          const int b = ci_blk(cd.info[min(cc + lane, CHK_MAXC - 1)]);  // (unconditional, masked after)
+          const bool dead = can_dead && deadrow[b] == cd.bep[b];
+          const bool live = cc + lane < nch && !dead;
           uint64_t lm = __ballot(live);
           int nxt = min(cc + 64, nch);
           n_scan = 0;
