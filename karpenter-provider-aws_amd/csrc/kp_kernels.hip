@@ -2885,12 +2885,14 @@ if (!FL_NOTIME && tmg) {                                    \
             if (UNLIKELY(__ballot(lane < KP_NRES && fj != j0_lane))) {
               if (lane < KP_NRES) KA(nc_fitj)[(size_t)ncx * KP_NRES + lane] = fj;
             }
+            if (!CHK) {  // len(Pods) + 1: one uniform read, every lane writes the same value (no exec-masked block)
+              const int cnt1 = npods[ncx] + 1;
+              npods[ncx] = cnt1;
+            }
             if (lane == 0) {
               if (CHK) {  // len(Pods) in the chunk's block (the replay reads it there) and the flat copy
                 KA(chk_blk)[ci_blk(cd.info[ck])].key[l] += 1;
                 KA(g_npods)[ncx] += 1;
-              } else {
-                npods[ncx] += 1;
               }
             }
             if (lane == l) {  // the pre-check record, from this lane's copy: headroom minus the pod, version + 1
@@ -2977,10 +2979,8 @@ if (!FL_NOTIME && tmg) {                                    \
       a_cur_prev_stamp = stk_t;
       mut = 1;
       mut_p = wpos;
-      if (lane == 0) {
-        KA(cur_nc)[2 * sl] = cpos;
-        KA(cur_nc)[2 * sl + 1] = a_cur_prev_stamp;
-      }
+      // (every lane stores the same 8 bytes: one coalesced store, no exec-masked block)
+      *reinterpret_cast<int2*>(&KA(cur_nc)[2 * sl]) = make_int2(cpos, a_cur_prev_stamp);
       // placement / events: buffered one pod per lane, written 64 at a time (nothing reads them before the
       // fast lane returns)
       if (lane == n_buf) {
