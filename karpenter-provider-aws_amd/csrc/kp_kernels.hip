@@ -2185,7 +2185,7 @@ __device__ __noinline__ int fast_lane(uint64_t kargs, int32_t LDS* s_dyn_arg, ui
   // the append path's byte model as 32-bit event counts, converted on exit (the 64-bit accumulators cost 2.8 % of
   // the loop)
   NbUnits fnb{0, 0, 0};
-  uint32_t n_app = 0, n_scan = 0;
+  uint32_t n_app = 0, n_scan = 0, n_run = 0;
     const bool tmg = A->timing != 0;
     // the argument block as a lane table: dword 64 k + l of SolveArgs in lane l of kt<k>
     static_assert(sizeof(SolveArgs) <= 1280, "SolveArgs outgrew the fast lane's argument table");
@@ -2872,7 +2872,7 @@ if (!FL_NOTIME && tmg) {                                    \
             if (UNLIKELY(full_add)) {
               store_merged(reinterpret_cast<KReqs*>(KA(nc_reqs) + (size_t)ncx * sizeof(KReqs)), rv, m_v, D.W, D.KB);
               if (TOPO && KA(n_tk)) store_tcodes(KA(n_tk), KA(tk_keys), KA(nc_tcode), KA(hnc_stride), rv, m_v, ncx);
-              if (lane == 0 && ncx < KA(ncc)) KA(nc_fail)[(size_t)sl * KA(ncc) + ncx] = NC_MERGED;
+              if (ncx < KA(ncc)) KA(nc_fail)[(size_t)sl * KA(ncc) + ncx] = NC_MERGED;  // (uniform: every lane)
             }
             // the remaining types and threshold indices are stored only when they changed (the append path
             // usually leaves both as they were): fewer vector-memory operations ahead of the next pod's loads
@@ -2895,7 +2895,9 @@ if (!FL_NOTIME && tmg) {                                    \
                 KA(g_npods)[ncx] += 1;
               }
             }
-            if (lane == l) {  // the pre-check record, from this lane's copy: headroom minus the pod, version + 1
+            // the pre-check record, from lane l's copy: headroom minus the pod, version + 1 (kept lane-masked: the
+            // broadcast for an all-lane store measured +0.5 % on config 2)
+            if (lane == l) {
               int4* hp = reinterpret_cast<int4*>(KA(nc_head) + ncx);
               const int64_t n0 = hv.r0 - pr0, n1 = hv.r1 - pr1;
               hp[0] = make_int4((int)n0, (int)(n0 >> 32), (int)n1, (int)(n1 >> 32));
@@ -2914,7 +2916,7 @@ if (!FL_NOTIME && tmg) {                                    \
               h_key = c_bkey + (lane == l ? 1 : 0);
             }
             if (FT_FINE) fl_last = ncx;
-            if (TOPO && triv && lane == 0 && ncx < KA(ncc)) KA(nc_fail)[(size_t)sl * KA(ncc) + ncx] = NC_MERGED;
+            if (TOPO && triv && ncx < KA(ncc)) KA(nc_fail)[(size_t)sl * KA(ncc) + ncx] = NC_MERGED;
             if (TOPO && rec_n) {
               // Topology.Record, as the full path's: each recorded group (spreads only on fast levels) on its own lane;
               // a dictionary key counts once the NodeClaim holds one value of it (its value code < 64)
@@ -2959,7 +2961,7 @@ if (!FL_NOTIME && tmg) {                                    \
             FTF(12);
             break;
           }
-          if (lane == 0 && ncx < KA(ncc)) KA(nc_fail)[(size_t)sl * KA(ncc) + ncx] = perm ? NC_NEVER : verx;
+          if (ncx < KA(ncc)) KA(nc_fail)[(size_t)sl * KA(ncc) + ncx] = perm ? NC_NEVER : verx;  // (every lane)
         }
       }
       wave_sync();
@@ -3029,11 +3031,14 @@ if (!FL_NOTIME && tmg) {                                    \
           const int64_t kk = k;
           // the NodeClaim: requests, len(Pods), pre-check record (headroom, version)
           c_q += kk * preq_lane;
-          if (lane < KP_NRES) KA(nc_requests)[(size_t)placed * KP_NRES + lane] = c_q;
+          {
+            const int64_t q_top = lane_bcast_i64(c_q, KP_NRES - 1);
+            KA(nc_requests)[(size_t)placed * KP_NRES + min(lane, KP_NRES - 1)] = lane < KP_NRES ? c_q : q_top;
+          }
           c_r0 -= kk * pr0, c_r1 -= kk * pr1;
           if (four) c_r2 -= kk * pr2, c_r3 -= kk * pr3;
           c_ver += k;
-          if (lane == 0) {
+          {  // (uniform values, every lane stores)
             npods[placed] = c1 + k;
             int4* hp = reinterpret_cast<int4*>(KA(nc_head) + placed);
             hp[0] = make_int4((int)c_r0, (int)(c_r0 >> 32), (int)c_r1, (int)(c_r1 >> 32));
@@ -3044,10 +3049,7 @@ if (!FL_NOTIME && tmg) {                                    \
           stk_t += k;
           mstack_push_reg((int32_t LDS*)s_stk[0], stk_n, stk_lost, stk_t, wpos);
           a_cur_prev_stamp = stk_t;
-          if (lane == 0) {
-            KA(cur_nc)[2 * sl] = wpos;
-            KA(cur_nc)[2 * sl + 1] = stk_t;
-          }
+          *reinterpret_cast<int2*>(&KA(cur_nc)[2 * sl]) = make_int2(wpos, stk_t);
           // the k pods: popped, placed (events in queue order after the buffered ones)
           if (n_buf + k > 64) {
             if (lane < n_buf) {
@@ -3078,7 +3080,7 @@ if (!FL_NOTIME && tmg) {                                    \
           attempts += k;
           n_app += (uint32_t)k;
           n_scan += (uint32_t)k;
-          if (lane == 0) S->runpods += k;
+          n_run += (uint32_t)k;
         }
       }
       FT(5);
@@ -3119,6 +3121,7 @@ if (!FL_NOTIME && tmg) {                                    \
     S->scanned += n_scan;
     S->starts += starts;
     S->fpods += pops;
+    S->runpods += n_run;
     for (int i = 0; i < 14; i++) S->fcyc[i] += fcyc[i];
     if (fb >= 0) S->fbail[fb] += 1;
     S->fbail[FB_MEMO] += memo_pops;  // (not a hand-off: the pods the lane failed by the memo)
