@@ -2359,9 +2359,12 @@ if (!FL_NOTIME && tmg) {                                    \
         triv = kreq_at(KA(shape_reqs), sl)->present == 0;
         rec_n = KA(shape_rec_n)[shape];
         rec_b = KA(shape_rec_base)[shape];
-        if (lane < rec_n) {  // (the group's liveness and taint filter are read at the commit: no wait here)
-          r_g = KA(rec_list)[rec_b + lane];
-          r_aux = KA(rec_aux)[rec_b + lane];
+        if (rec_n) {  // (the group's liveness and taint filter are read at the commit: no wait here)
+          // (uniform branch; reads at clamped lanes, masked after: no exec-masked block)
+          const int rl = rec_b + min(lane, rec_n - 1);
+          const int g_r = KA(rec_list)[rl], a_r = KA(rec_aux)[rl];
+          r_g = lane < rec_n ? g_r : 0;
+          r_aux = lane < rec_n ? a_r : 0;
         }
         const int ob = KA(sl_own_base)[sl];
 #pragma unroll
@@ -2440,7 +2443,7 @@ if (!FL_NOTIME && tmg) {                                    \
             const uint64_t im = __ballot(icand);
             if (im) ex_ipos = base + __builtin_ctzll(im);
           }
-          if (lane == 0) bytes += (uint64_t)min(64, E - base) * (16 * KA(n_req_res) + 13);  // (the full path's model)
+          bytes += (uint64_t)min(64, E - base) * (16 * KA(n_req_res) + 13);  // (the full path's model)
           uint64_t cm = __ballot(cand);
           while (cm) {
             const int l = __builtin_ctzll(cm);
@@ -2468,18 +2471,25 @@ if (!FL_NOTIME && tmg) {                                    \
               const bool mok = merge_compatible(D, crx, (const KReqs*)&fl_B, b_negop, false, m_v, rv,
                                                 (WaveSlots*)&fl_slots, vint_global(KA(vint)));
               if (!mok) {  // permanent unless the undefined-key rule failed (no well-known exemption here)
-                if (lane == 0) KA(ex_fail)[(size_t)sl * E + ei] = (fl_B.present & ~crx.P & ~b_negop) == 0 ? NC_NEVER : verx;
+                KA(ex_fail)[(size_t)sl * E + ei] = (fl_B.present & ~crx.P & ~b_negop) == 0 ? NC_NEVER : verx;
                 continue;
               }
               // commit: ExistingNode.Add (requirements, requests, headroom rows, version), Topology.Record
               store_merged(er, rv, m_v, D.W, D.KB);
             }
-            if (lane < KP_NRES) KA(ex_requests)[(size_t)ei * KP_NRES + lane] += preq_lane;
-            if (lane < 4) {  // headroom rows of the first four requested resources
-              const int64_t d = lane == 0 ? pr0 : lane == 1 ? pr1 : lane == 2 ? pr2 : pr3;
-              KA(ex_room)[(size_t)lane * E + ei] -= d;
+            {  // requests + pod, the headroom rows of the first four requested resources - pod, version + 1: every
+               // lane reads and stores (the lanes past the rows repeat the last row's value), no exec-masked block
+              int64_t* rqp = KA(ex_requests) + (size_t)ei * KP_NRES + min(lane, KP_NRES - 1);
+              const int64_t rq_n = *rqp + preq_lane;
+              const int64_t rq_top = lane_bcast_i64(rq_n, KP_NRES - 1);
+              const int hl = min(lane, 3);
+              int64_t* hrp = KA(ex_room) + (size_t)hl * E + ei;
+              const int64_t d = hl == 0 ? pr0 : hl == 1 ? pr1 : hl == 2 ? pr2 : pr3;
+              const int64_t hr_n = *hrp - d;
+              *rqp = lane < KP_NRES ? rq_n : rq_top;
+              *hrp = hr_n;
+              KA(ex_ver)[ei] = verx + 1;
             }
-            if (lane == 0) KA(ex_ver)[ei] = verx + 1;
             if (TOPO && rec_n) {
               const int tsx = __builtin_amdgcn_readlane(ts, l);
               for (int i0 = 0; i0 < rec_n; i0 += 64) {
@@ -2521,10 +2531,7 @@ if (!FL_NOTIME && tmg) {                                    \
         // cursor: every position before the winner failed; with owned groups, before the first position that passed
         // the count-independent checks (a zone-count failure may pass later), as the full path
         const int cpos = TOPO && t_n ? min(ex_ipos, E) : (ex_pl >= 0 ? ex_pl : E);
-        if (lane == 0) {
-          KA(cur_ex)[2 * sl] = cpos;
-          KA(cur_ex)[2 * sl + 1] = a_cex_prev_stamp;
-        }
+        *reinterpret_cast<int2*>(&KA(cur_ex)[2 * sl]) = make_int2(cpos, a_cex_prev_stamp);  // (every lane)
         a_cex_prev_pos = cpos;
         if (ex_pl >= 0) {
           int ex_n = U(s_ctl[14]), ex_lost = U(s_ctl[21]);
@@ -2553,10 +2560,7 @@ if (!FL_NOTIME && tmg) {                                    \
           continue;
         }
       } else if (FL_HAS_EX) {  // addToExistingNode: every position fails (cursor == n_existing)
-        if (lane == 0) {
-          KA(cur_ex)[2 * sl] = KA(n_existing);
-          KA(cur_ex)[2 * sl + 1] = a_cex_prev_stamp;
-        }
+        *reinterpret_cast<int2*>(&KA(cur_ex)[2 * sl]) = make_int2(KA(n_existing), a_cex_prev_stamp);  // (every lane)
         a_cex_prev_pos = KA(n_existing);
       }
       FT(1);
