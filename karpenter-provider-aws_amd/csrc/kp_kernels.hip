@@ -1494,6 +1494,43 @@ __device__ __forceinline__ int sort_newnodeclaims_wave(P ord, P npods, int n, in
 }
 
 
+// Topology.Record of a commit on one node (existing position or NodeClaim id `node`, hcnt / tcode rows of `stride`),
+// as the full path's: recorded group i on lane i (rec_list[rec_b + i]; the first 64 prefetched in g0 / aux0, the lanes
+// past rec_n repeating the last entry); counted when the group is live and its filter admits the node's taint set
+// tsx. A hostname group bumps the node's saturating u8 count; a dictionary key counts once the node holds one value
+// of it (value code < 64). Every read is unconditional (the hostname count or the value code through one selected
+// row pointer, then the group's count and registered mask): two round trips, the stores masked after.
+__device__ __forceinline__ void record_node(int rec_n, int rec_b, int g0, int aux0, int tsx, const int32_t* rec_list,
+                                            const int32_t* rec_auxv, const int32_t* tg_live,
+                                            const uint64_t* tg_filt_tol, const uint8_t* tcode, uint8_t* hcnt,
+                                            size_t stride, int node, int32_t* tg_cnt, uint64_t* tg_reg) {
+  const int lane = LANE;
+  for (int i0 = 0; i0 < rec_n; i0 += 64) {
+    const int ri = i0 + lane;
+    int g = g0, aux = aux0;
+    if (i0) {  // (past the 64 prefetched; uniform branch)
+      const int rc = rec_b + min(ri, rec_n - 1);
+      g = rec_list[rc], aux = rec_auxv[rc];
+    }
+    const int live = tg_live[g];
+    const uint64_t ftol = tg_filt_tol[g];
+    const uint8_t GLB* src = aux >= 0 ? (const uint8_t GLB*)hcnt + (size_t)aux * stride + node
+                                      : (const uint8_t GLB*)tcode + (size_t)(-1 - aux) * stride + node;
+    const uint32_t b0 = *src;  // the hostname count (255: an unregistered domain), or the node's value code
+    const int cnt0 = ((const int32_t GLB*)tg_cnt)[(size_t)g * 64 + (b0 & 63)];
+    const uint64_t reg0 = ((const uint64_t GLB*)tg_reg)[g];
+    if (ri < rec_n && live && ((ftol >> tsx) & 1)) {
+      if (aux >= 0) {
+        hcnt[(size_t)aux * stride + node] = b0 == 255 ? 1 : b0 < 254 ? b0 + 1 : 254;
+        tg_reg[g] = 1;
+      } else if (b0 < 64) {
+        tg_cnt[(size_t)g * 64 + b0] = cnt0 + 1;
+        tg_reg[g] = reg0 | (1ull << b0);
+      }
+    }
+  }
+}
+
 // sort.Slice replay after NodeClaim.Add at sorted position p (pending mutation 1), the common case in one batch:
 // lanes read ord[p..p+63] and, for pdqsort's choosePivot, the nine sampled positions, then their keys (two dependent
 // LDS reads in all). When pdqsort would do a stable move (n <= 12: insertion sort; n >= 50 with increasingHint:
@@ -2363,8 +2400,7 @@ if (!FL_NOTIME && tmg) {                                    \
           // (uniform branch; reads at clamped lanes, masked after: no exec-masked block)
           const int rl = rec_b + min(lane, rec_n - 1);
           const int g_r = KA(rec_list)[rl], a_r = KA(rec_aux)[rl];
-          r_g = lane < rec_n ? g_r : 0;
-          r_aux = lane < rec_n ? a_r : 0;
+          r_g = g_r, r_aux = a_r;  // (the lanes past rec_n repeat the last entry: record_node masks them)
         }
         const int ob = KA(sl_own_base)[sl];
 #pragma unroll
@@ -2491,32 +2527,9 @@ if (!FL_NOTIME && tmg) {                                    \
               KA(ex_ver)[ei] = verx + 1;
             }
             if (TOPO && rec_n) {
-              const int tsx = __builtin_amdgcn_readlane(ts, l);
-              for (int i0 = 0; i0 < rec_n; i0 += 64) {
-                const int ri = i0 + lane;
-                if (ri < rec_n) {
-                  int g = r_g, aux = r_aux;
-                  if (i0) g = KA(rec_list)[rec_b + ri], aux = KA(rec_aux)[rec_b + ri];  // (past the 64 prefetched)
-                  // liveness, taint filter and the node's value code in one round trip
-                  const int live = KA(tg_live)[g];
-                  const uint64_t ftol = KA(tg_filt_tol)[g];
-                  const uint32_t code0 = aux < 0 ? KA(ex_tcode)[(size_t)(-1 - aux) * E + ei] : 0xFF;
-                  uint8_t* c = &KA(hcnt_ex)[(size_t)(aux >= 0 ? aux : 0) * E + ei];
-                  const uint32_t hc0 = aux >= 0 ? *c : 0;
-                  if (live && ((ftol >> tsx) & 1)) {
-                    if (aux >= 0) {
-                      *c = hc0 == 255 ? 1 : hc0 < 254 ? hc0 + 1 : 254;  // 255: an unregistered domain
-                      KA(tg_reg)[g] = 1;
-                    } else {
-                      const uint32_t code = code0;
-                      if (code < 64) {
-                        KA(tg_cnt)[(size_t)g * 64 + code] += 1;
-                        KA(tg_reg)[g] |= 1ull << code;
-                      }
-                    }
-                  }
-                }
-              }
+              record_node(rec_n, rec_b, r_g, r_aux, __builtin_amdgcn_readlane(ts, l), KA(rec_list), KA(rec_aux),
+                          KA(tg_live), KA(tg_filt_tol), KA(ex_tcode), KA(hcnt_ex), (size_t)E, ei, KA(tg_cnt),
+                          KA(tg_reg));
               bytes += 16 * (uint64_t)rec_n;
             }
             ex_pl = ei;
@@ -2924,32 +2937,9 @@ if (!FL_NOTIME && tmg) {                                    \
             if (TOPO && rec_n) {
               // Topology.Record, as the full path's: each recorded group (spreads only on fast levels) on its own lane;
               // a dictionary key counts once the NodeClaim holds one value of it (its value code < 64)
-              const int tsx = __builtin_amdgcn_readlane(hv.ts, l);
-              for (int i0 = 0; i0 < rec_n; i0 += 64) {
-                const int ri = i0 + lane;
-                if (ri < rec_n) {
-                  int g = r_g, aux = r_aux;
-                  if (i0) g = KA(rec_list)[rec_b + ri], aux = KA(rec_aux)[rec_b + ri];  // (past the 64 prefetched)
-                  // liveness, taint filter and the NodeClaim's value code in one round trip
-                  const int live = KA(tg_live)[g];
-                  const uint64_t ftol = KA(tg_filt_tol)[g];
-                  const uint32_t code0 = aux < 0 ? KA(nc_tcode)[(size_t)(-1 - aux) * KA(hnc_stride) + ncx] : 0xFF;
-                  uint8_t* c = &KA(hcnt_nc)[(size_t)(aux >= 0 ? aux : 0) * KA(hnc_stride) + ncx];
-                  const uint32_t hc0 = aux >= 0 ? *c : 0;
-                  if (live && ((ftol >> tsx) & 1)) {
-                    if (aux >= 0) {
-                      *c = hc0 == 255 ? 1 : hc0 < 254 ? hc0 + 1 : 254;  // 255: an unregistered domain
-                      KA(tg_reg)[g] = 1;
-                    } else {
-                      const uint32_t code = code0;
-                      if (code < 64) {
-                        KA(tg_cnt)[(size_t)g * 64 + code] += 1;
-                        KA(tg_reg)[g] |= 1ull << code;
-                      }
-                    }
-                  }
-                }
-              }
+              record_node(rec_n, rec_b, r_g, r_aux, __builtin_amdgcn_readlane(hv.ts, l), KA(rec_list), KA(rec_aux),
+                          KA(tg_live), KA(tg_filt_tol), KA(nc_tcode), KA(hcnt_nc), (size_t)KA(hnc_stride), ncx,
+                          KA(tg_cnt), KA(tg_reg));
               bytes += 16 * (uint64_t)rec_n;
             }
             if (LIKELY(!full_add)) {  // the append path left the requirements (hmin, catalogue) as they were
