@@ -2630,9 +2630,8 @@ if (!FL_NOTIME && tmg) {                                    \
         int tail = q_head + q_len;
         if (tail >= KA(n_pods)) tail -= KA(n_pods);
         q_len += 1;
-        if (lane == 0) {
-          KA(cur_nc)[2 * sl] = n_nc;
-          KA(cur_nc)[2 * sl + 1] = stk_t;
+        {  // (uniform values: every lane stores, no exec-masked block)
+          *reinterpret_cast<int2*>(&KA(cur_nc)[2 * sl]) = make_int2(n_nc, stk_t);
           KA(placement)[pod] = -1;
           if (relaxed) KA(pod_level)[pod] = lvl + 1;
           KA(queue)[tail] = pod;
@@ -2798,7 +2797,7 @@ if (!FL_NOTIME && tmg) {                                    \
           const uint64_t im = __ballot(icand);
           if (im) ipos = __builtin_amdgcn_readlane(i, __builtin_ctzll(im));
         }
-        if (can_dead && !(ck == ch0 && cs0 > 0) && __ballot(valid && !pfail) == 0 && lane == 0) {
+        if (can_dead && !(ck == ch0 && cs0 > 0) && __ballot(valid && !pfail) == 0) {  // (uniform: every lane)
           const int b = ci_blk(cd.info[ck]);  // every NodeClaim of the chunk fails the shape-level permanently
           deadrow[b] = cd.bep[b];
         }
