@@ -2549,7 +2549,7 @@ if (!FL_NOTIME && tmg) {                                    \
         if (ex_pl >= 0) {
           int ex_n = U(s_ctl[14]), ex_lost = U(s_ctl[21]);
           mstack_push_reg((int32_t LDS*)s_stk[1], ex_n, ex_lost, a_cex_prev_stamp + 1, ex_pl);
-          if (lane == 0) {
+          {  // (uniform values: every lane stores, no exec-masked block)
             s_ctl[14] = ex_n;
             s_ctl[21] = ex_lost;
             s_ctl[15] = a_cex_prev_stamp + 1;
