@@ -167,7 +167,7 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(alg_bytes / (k_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 6),
-            "traffic": _traffic("solve_kernel"),
+            "traffic": _traffic("solve2"),
             "algorithmic_bytes_per_launch": int(alg_bytes),
             "algorithmic_bytes_per_pod": round(alg_bytes / prob.n_pods, 1),
             "note": "single-workgroup sequential FFD: latency-bound (dependent L2 round trips + barriers per pod)",
@@ -336,7 +336,7 @@ def _feasibility(args, cat, ctx, prob, barrier, max_over_ranks, world, steps=10)
                       "instance_types": T, "kernel_ms": round(k_ms, 4),
                       "roofline": {"bound": "hbm", "kernel": _feas_kernel_name(T), "achieved": round(ach, 1),
                                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                                   "traffic": _traffic(_feas_kernel_name(T)) if name == "distinct" else None,
+                                   "traffic": _traffic("feas_rows") if name == "distinct" else None,
                                    "algorithmic_bytes_per_launch": alg,
                                    "bytes_per_row": ROW_BYTES + 8 * T + 8 * ((T + 63) // 64),
                                    "l2_effective_GBs": round(pairs * L2_BYTES_PER_PAIR / (k_ms / 1e3) / 1e9, 1)}}
@@ -356,6 +356,7 @@ def _feasibility(args, cat, ctx, prob, barrier, max_over_ranks, world, steps=10)
                 "value": round(pairs * world * steps / el_c, 1), "unit": "pairs/s", "kernel_ms": round(kc_ms, 4),
                 "roofline": {"bound": "hbm", "kernel": _feas_kernel_name(T), "achieved": round(ach_c, 1),
                              "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach_c / HBM_PEAK_GBS, 4),
+                             "traffic": _traffic("feas_compact"),
                              "algorithmic_bytes_per_launch": alg_c,
                              "bytes_per_row": ROW_BYTES + 8 * ((T + 63) // 64) + 8},
                 "note": "no cheapest-price rows: each row's compatible offering classes (8 B) index the resident "
@@ -441,6 +442,8 @@ def _consolidation(args, cat, ctx, dist, rank, world, barrier, kcomm):
         "elapsed_s": round(elapsed, 4),
         "sim_kernel_ms_rank0": round(st["solve_kernel_ms"], 3),
         "pods_rescheduled_rank0": int(st["pops"]),
+        "roofline": _sim_roofline("sim_kernel", "sweep", st, len(sw_offs) - 1,
+                                  "one launch of this rank's sweep subsets; persistent waves, one subset per wave"),
         "decisions": {"noop": choice["counts"][0], "delete": choice["counts"][1], "replace": choice["counts"][2]},
         "best": {"subset": choice["subset"], "decision": choice["result"]["decision"],
                  "savings": choice["result"]["savings"]},
@@ -501,11 +504,15 @@ def _consolidation_general(args, cat, ctx, rank, world, barrier):
         elapsed = time.perf_counter() - t0
     finally:
         plan.close()
+    roof = _sim_roofline("solve_kernel<4,*,true>", "general", st, len(subs),
+                         "batched Solves, one workgroup per simulation, launches of up to 4,096 (solve_kernel + "
+                         "finalize_kernel time per launch, HIP events)")
     barrier()
     n = len(subs)
     out = {"metric": "consolidation sims/s (general path: topology spread)", "value": round(n / elapsed, 1),
            "unit": "sims/s", "subsets": n, "elapsed_s": round(elapsed, 3), "ms_per_sim": round(elapsed / n * 1e3, 3),
            "sims_per_s_incl_prepare": round(n / (elapsed + prep_s), 1), "prepare_s": round(prep_s, 3),
+           "device_ms": round(st["solve_kernel_ms"], 3), "roofline": roof,
            "decisions": {"noop": choice["counts"][0], "delete": choice["counts"][1], "replace": choice["counts"][2]},
            "workload": f"config4 variant: {args.general_nodes} nodes ({len(cl.pod_shape)} pods), every other shape "
                        f"zone-spread (maxSkew 1, DoNotSchedule); {len(mids)} firstNConsolidationOption prefixes + "
@@ -580,15 +587,33 @@ def _latency_roofline(kernel_ms, pods):
         return None
 
 
-def _traffic(kernel):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc passes (profiles/traffic.json), if any."""
+def _traffic(leg):
+    """HBM bytes per launch of the leg's kernel from the committed rocprofv3 --pmc passes of tools/prof_leg.py <leg>
+    (profiles/traffic.json, written by tools/pmc_traffic.py: one figure per leg, never shared between two variants of
+    one kernel), if any."""
     p = os.path.join(REPO, "profiles", "traffic.json")
     if os.path.exists(p):
         try:
-            return json.load(open(p)).get(kernel, {}).get("hbm_bytes_per_launch")
+            return json.load(open(p)).get(leg, {}).get("hbm_bytes_per_launch")
         except Exception:
             return None
     return None
+
+
+def _sim_roofline(kernel, leg, st, n_sims, note):
+    """Consolidation legs (SURVEY §8d "Consolidation sim": unit = one subset simulation, B = the bytes its Solve reads
+    and writes, counted inside the kernel by the same model as the Solve's): in-kernel algorithmic bytes over the
+    kernel's HIP-event time. traffic is per launch of the profiled leg (tools/prof_leg.py), alg_bytes here per launch
+    of this run, so compare traffic with algorithmic_bytes_per_sim x the profiled leg's sims per launch."""
+    ms = st["solve_kernel_ms"]
+    b = float(st["bytes_algorithmic"])
+    if ms <= 0 or n_sims <= 0:
+        return None
+    ach = b / (ms / 1e3) / 1e9
+    return {"bound": "hbm", "kernel": kernel, "achieved": round(ach, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 6), "traffic": _traffic(leg), "traffic_leg": f"tools/prof_leg.py {leg}",
+            "algorithmic_bytes": int(b), "algorithmic_bytes_per_sim": round(b / n_sims, 1),
+            "kernel_ms": round(ms, 3), "sims": n_sims, "note": note}
 
 
 def _cpu_baseline(cat, n_pods):

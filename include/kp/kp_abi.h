@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define KP_ABI_VERSION 11
+#define KP_ABI_VERSION 12
 
 enum kp_status {
   KP_OK = 0,
@@ -419,6 +419,28 @@ typedef struct kp_options {
 } kp_options;
 
 int32_t kp_ctx_create(const kp_options* opts, kp_ctx** out);
+/* ABI v12: test and measurement overrides of the library's kernel and path choices. Every field 0 (the state a context
+ * is created in) is the production choice; no environment variable changes a path (a stray variable in the
+ * controller's environment cannot pick another kernel). Cross-check tests and benchmarks set them per context,
+ * between calls (not while a call on the context runs). */
+typedef struct kp_overrides {
+  int32_t fast_lane;           /* 0 auto (the run-length-commit variant where most queue neighbours share their shape),
+                                  1 the plain variant, 2 the run-length-commit variant */
+  int32_t sort_capacity;       /* 0: 8192 NodeClaims in the LDS order; n > 0: the chunked order past n NodeClaims */
+  int32_t chunk_capacity;      /* 0: the chunked order's full directory; n > 0: at most n chunks (then the flat order);
+                                  n < 0: no chunks (the flat order past sort_capacity) */
+  int32_t template_table;      /* 0: Solve reads the template-options table; 1: it re-filters per template attempt */
+  uint64_t table_shard_min;    /* 0: 1 << 20 (shape-level, template) pairs before a communicator shards the table */
+  int32_t general_batch;       /* 0: batched general simulations (superset Solve); 1: every subset compiled alone */
+  int32_t feasibility_kernel;  /* 0 by catalogue size (quad <= 1024 types, else bits); 1 the per-type global-gather
+                                  kernel; 2 the one-row bits kernel at any size */
+  int32_t feasibility_blocks;  /* 0: by row count; n > 0: n blocks */
+  int32_t feasibility_temporal;/* 0: cheapest-price rows as non-temporal stores; 1: temporal stores */
+  int32_t timing;              /* 1: solve_kernel phase probes (kp_solve_stats phase_cycles / fast_cycles) */
+  int32_t host_timing;         /* 1: host compile / general-path phases on stderr */
+} kp_overrides;
+int32_t kp_ctx_set_overrides(kp_ctx* ctx, const kp_overrides* ov); /* NULL: back to all 0 */
+int32_t kp_ctx_get_overrides(const kp_ctx* ctx, kp_overrides* out);
 /* Drops the caller's reference. Catalogues, plans and communicators created on the context hold their own, so they
  * may be destroyed before or after it (a garbage collector finalizes in any order); the context's stream, events and
  * spare arena are freed with the last reference. */
@@ -589,9 +611,11 @@ int32_t kp_filter_run(kp_filter_plan* plan, uint64_t* out_mask, double* out_chea
  * offering classes its requirements admit (out_classes[q], bit c = class c of kp_filter_class_prices), instead of n_types
  * prices. The cheapest compatible available offering price of type t for query q is then
  *   min over c in out_classes[q] of prices[c * n_types + t]   (+inf: none)
- * which equals kp_filter_run's out_cheapest bit for bit: a class's price row is the cheapest available offering of
- * the type in that class. kp_filter_class_prices copies the plan's resident [C][n_types] table (C <= 64 classes) and
- * its class count; the consumer reads it once per catalogue seqnum, not per query. */
+ * which equals kp_filter_run's out_cheapest bit for bit for every type, whether its mask bit is set or not (both are
+ * the cheapest available offering among the query's compatible classes; the mask adds the type's requirements and Fits):
+ * a class's price row is the cheapest available offering of the type in that class. kp_filter_class_prices copies the
+ * plan's resident [C][n_types] table (C <= 64 classes) and its class count; the consumer reads it once per catalogue
+ * seqnum, not per query, and a plan whose catalogue seqnum moved refuses it (KP_E_INVAL) until kp_filter_refresh. */
 enum { KP_FILTER_MASK_ONLY = 0, KP_FILTER_CHEAPEST = 1, KP_FILTER_COMPACT = 2 };
 int32_t kp_filter_run_compact(kp_filter_plan* plan, uint64_t* out_mask, uint64_t* out_classes, kp_solve_stats* stats);
 int32_t kp_filter_class_prices(kp_filter_plan* plan, double* out, uint32_t capacity, uint32_t* n_classes);
@@ -739,7 +763,8 @@ typedef struct kp_cluster {
   const kp_pod_shape* shapes;
   const kp_pod* pods;
   uint32_t n_pods;
-  uint32_t spot_to_spot;      /* SpotToSpotConsolidation feature gate (only 0 supported) */
+  uint32_t spot_to_spot;      /* SpotToSpotConsolidation feature gate (default off; 1: spot candidates may be replaced
+                                 by cheaper spot capacity, R:website/content/en/preview/concepts/disruption.md:110-128) */
   const uint32_t* pending_pods;  /* provisionable pods not bound to any node (indices into pods): they join every
                                     simulation, but their own scheduling errors do not block a decision */
   uint32_t n_pending;
@@ -778,12 +803,21 @@ int32_t kp_simulate_batch(kp_ctx* ctx, const kp_cluster* cluster, const uint32_t
  * The general path compiles the cluster once as a superset Solve (every node not being deleted existing, every pod
  * a simulation can queue in its pod list) and runs the subsets' Solves batched, one workgroup each; a subset that
  * would remove every owner of an inverse anti-affinity term (and every subset of a cluster whose superset compile is
- * unsupported, or with KP_GENERAL_BATCH=0) is compiled on its own. stats (general path): phase_cycles[0] simulations
- * batched, phase_cycles[1] simulations compiled per subset. */
+ * unsupported, or with kp_overrides.general_batch = 1) is compiled on its own. stats (general path): phase_cycles[0] simulations
+ * batched, phase_cycles[1] simulations compiled per subset, phase_cycles[2] batched solve_kernel launches. */
 typedef struct kp_cluster_plan kp_cluster_plan;
 int32_t kp_cluster_prepare(kp_ctx* ctx, const kp_cluster* cluster, kp_cluster_plan** out);
 int32_t kp_cluster_simulate(kp_cluster_plan* plan, const uint32_t* offsets, const uint32_t* nodes, uint32_t n_subsets,
                             int32_t multi_node, kp_sim_result* out, kp_solve_stats* stats);
+/* ABI v12: kp_cluster_simulate with a cancellation token (NULL: as kp_cluster_simulate). Upstream runs consolidation
+ * under a timeout and counts the ones that expire (karpenter_voluntary_disruption_consolidation_timeouts_total,
+ * R:website/content/en/preview/reference/metrics.md:186-187); the disruption shim sets the token when its context
+ * expires. The batched kernel reads the flag between a wave's subsets, the general path before each launch and inside
+ * each simulation's Solve (every ~1,024 pops): the call returns KP_E_CANCELED with no result within about one
+ * simulation's time, and the plan stays usable. */
+int32_t kp_cluster_simulate_cancellable(kp_cluster_plan* plan, kp_cancel* cancel, const uint32_t* offsets,
+                                        const uint32_t* nodes, uint32_t n_subsets, int32_t multi_node, kp_sim_result* out,
+                                        kp_solve_stats* stats);
 /* kp_solve_refresh for a cluster snapshot: after kp_catalog_update_offerings the catalogues' availability and
  * prices, the templates' options and the candidates' prices are re-applied in place and the per shape-level template
  * outcomes recomputed; kp_cluster_simulate / kp_consolidate_argmin refuse the plan until then. */
@@ -834,6 +868,13 @@ typedef struct kp_choice {
 int32_t kp_consolidate_argmin(kp_cluster_plan* plan, kp_comm* comm, const uint32_t* offsets, const uint32_t* nodes,
                               uint32_t n_subsets, uint64_t base_index, int32_t multi_node, kp_sim_result* out,
                               kp_choice* best, kp_solve_stats* stats);
+/* ABI v12: the sweep step with a cancellation token (see kp_cluster_simulate_cancellable). A rank whose token fires
+ * still takes part in the all-gather (a KP_CHOICE_FAILED record holding KP_E_CANCELED), so no peer waits; every rank
+ * then returns an error. */
+int32_t kp_consolidate_argmin_cancellable(kp_cluster_plan* plan, kp_comm* comm, kp_cancel* cancel,
+                                          const uint32_t* offsets, const uint32_t* nodes, uint32_t n_subsets,
+                                          uint64_t base_index, int32_t multi_node, kp_sim_result* out, kp_choice* best,
+                                          kp_solve_stats* stats);
 /* The reduction kp_consolidate_argmin applies to the gathered per-rank records (host-only; exposed for callers that
  * reduce over another transport, and for tests): counts are summed, the best record wins. */
 int32_t kp_choice_reduce(const kp_choice* per_rank, uint32_t n, kp_choice* out);

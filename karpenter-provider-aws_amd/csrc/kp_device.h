@@ -398,7 +398,8 @@ struct SimArgs {
   SimNC* s_nc;                       // [slot]
   int32_t* s_ncfail;                 // [slot][SL]
   SimOut* out;                       // [n_subsets]
-  uint64_t* stats;                   // [8] attempts, bytes, pops, existing words scanned
+  uint64_t* stats;                   // [8] attempts, bytes, pops, existing words scanned, -, cancelled
+  const int32_t* cancel;             // kp_cancel flag (host-mapped) or null: polled between a wave's subsets
 };
 
 // kp_consolidate_argmin: per-block partial bests, and the record each rank contributes to the all-gather

@@ -40,6 +40,7 @@ using std::vector;
 namespace {
 
 thread_local string g_err;
+std::atomic<bool> g_host_timing{false};  // kp_overrides.host_timing of the last context that set it (stderr only)
 int32_t fail(int32_t code, const char* fmt, ...) {
   char buf[1024];
   va_list ap;
@@ -214,6 +215,7 @@ struct kp_ctx {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
   kp_options opts;
+  kp_overrides ov{};  // kp_ctx_set_overrides (tests, measurement); all 0 = production
   std::recursive_mutex mu;  // recursive: the general simulation path runs whole Solves under the cluster plan's lock
   // resident compiled catalogues + templates of recent Solves (most recent last), see SolveBase
   vector<std::shared_ptr<SolveBase>> bases;
@@ -939,6 +941,19 @@ int32_t kp_ctx_create(const kp_options* opts, kp_ctx** out) {
 }
 void kp_ctx_destroy(kp_ctx* c) { CtxUnref(c); }
 
+int32_t kp_ctx_set_overrides(kp_ctx* ctx, const kp_overrides* ov) {
+  if (!ctx) return fail(KP_E_INVAL, "null argument");
+  std::lock_guard<std::recursive_mutex> lock(ctx->mu);
+  ctx->ov = ov ? *ov : kp_overrides{};
+  g_host_timing.store(ctx->ov.host_timing != 0);
+  return KP_OK;
+}
+int32_t kp_ctx_get_overrides(const kp_ctx* ctx, kp_overrides* out) {
+  if (!ctx || !out) return fail(KP_E_INVAL, "null argument");
+  *out = ctx->ov;
+  return KP_OK;
+}
+
 
 int32_t kp_catalog_upload(kp_ctx* ctx, const kp_catalog_desc* desc, uint64_t seqnum, kp_catalog** out) {
   if (!desc || !out) return fail(KP_E_INVAL, "null argument");  // ctx NULL: host-only (kp_solve_validate)
@@ -1291,6 +1306,7 @@ int32_t ReservationTables(SolveBase& b) {
 }
 
 struct Compiled {
+  kp_overrides ov{};  // the context's overrides at compile time (CompileSolve with a ctx)
   std::shared_ptr<SolveBase> B = std::make_shared<SolveBase>();
   bool base_hit = false;              // the base came from the ctx cache
   bool base_refreshed = false;        // ... after an in-place offering refresh (a new catalogue seqnum)
@@ -1528,9 +1544,9 @@ bool HasPnsToleration(const kp_pod_shape& sh) {
   return false;
 }
 
-// KP_HOST_TIMING=1: host compile phases on stderr (diagnostics only)
+// kp_overrides.host_timing: host compile phases on stderr (diagnostics only)
 struct PhaseTimer {
-  bool on = getenv("KP_HOST_TIMING") != nullptr;
+  bool on = g_host_timing.load(std::memory_order_relaxed);
   std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
   void lap(const char* what) {
     if (!on) return;
@@ -1717,12 +1733,14 @@ int32_t CompileTopology(const kp_solve_in* in, Compiled& cp, const vector<vector
                 SelectorCanon(t.selector) + "|" + std::to_string(aff) + std::to_string(taint) + "|" + fcanon;
     const int sl = cp.shape_level_base[s] + l;
     const uint64_t ltol = cp.shape_tolerates[sl];  // the level's tolerations (Relax may have appended one)
-    if (taint)
-      for (uint32_t i = 0; i < sh.n_tolerations + (cp.sl_pns[sl] ? 1 : 0); i++) {
-        const kp_toleration& x = i < sh.n_tolerations ? sh.tolerations[i] : kPnsToleration;
-        id += string("(") + (x.key ? x.key : "") + "," + (x.value ? x.value : "") + "," + std::to_string(x.op) + "," +
-              std::to_string(x.effect) + ")";
-      }
+    // upstream MakeTopologyNodeFilter keeps the pod's tolerations under every taint policy and TopologyGroup.Hash
+    // hashes the whole filter: the tolerations are part of the identity even when the policy ignores them (a pod
+    // relaxed to tolerate PreferNoSchedule makes a new group, counted from the cluster alone)
+    for (uint32_t i = 0; i < sh.n_tolerations + (cp.sl_pns[sl] ? 1 : 0); i++) {
+      const kp_toleration& x = i < sh.n_tolerations ? sh.tolerations[i] : kPnsToleration;
+      id += string("(") + (x.key ? x.key : "") + "," + (x.value ? x.value : "") + "," + std::to_string(x.op) + "," +
+            std::to_string(x.effect) + ")";
+    }
     auto it = ids.find(id);
     if (it != ids.end()) {
       if (live) cp.tg_live[it->second] = 1;
@@ -2862,7 +2880,6 @@ int32_t CompilePerCall(const kp_solve_in* in, const SolveRaw& raw, Compiled& cp)
     uint32_t same = 0;
     for (uint32_t p = 1; p < in->n_pods; p++) same += cp.pod_shape[cp.queue[p]] == cp.pod_shape[cp.queue[p - 1]];
     cp.cont_hint = in->n_pods > 1 && 2 * same >= in->n_pods ? 1 : 0;
-    if (const char* e = getenv("KP_CONT")) cp.cont_hint = atoi(e) != 0;  // tests: force either fast-lane variant
   }
   pt.lap(" queue");
   return KP_OK;
@@ -2935,6 +2952,7 @@ int32_t RefreshOfferings(kp_ctx* ctx, SolveBase& b, bool commit = true) {
 // Compile a Solve. With a ctx, the SolveBase comes from (and goes to) the ctx cache when its fingerprint matches
 // and its dictionary covers the batch; without one (kp_solve_validate) it is always built.
 int32_t CompileSolve(const kp_solve_in* in, Compiled& cp, kp_ctx* cache = nullptr) {
+  if (cache) cp.ov = cache->ov;
   SolveRaw raw;
   PhaseTimer pt;
   int32_t rc = ParseSolve(in, raw);
@@ -3270,7 +3288,7 @@ void BindSolve(SolveArgs& a, const Compiled& C, const SolveOffs& o, uint8_t* sh,
   a.chk_dead = (int32_t*)(ar + o.chkdead);
   a.chk_dead_rows = o.chk_dead_rows;
   a.chk_maxc = o.chk_on ? CHK_MAXC : 0;
-  if (const char* e = getenv("KP_CHK_MAXC")) a.chk_maxc = o.chk_on ? std::max(0, std::min(CHK_MAXC, atoi(e))) : 0;  // test hook
+  if (C.ov.chunk_capacity) a.chk_maxc = o.chk_on ? std::max(0, std::min(CHK_MAXC, C.ov.chunk_capacity)) : 0;
   a.nc_head = (NcHead*)(((uintptr_t)(ar + o.nchead) + 63) & ~(uintptr_t)63);
   a.nc_fail = (int32_t*)(ar + o.ncfail);
   a.ex_ver = (int32_t*)(ar + o.exver);
@@ -3292,8 +3310,8 @@ void BindSolve(SolveArgs& a, const Compiled& C, const SolveOffs& o, uint8_t* sh,
   a.nc_hp = (uint64_t*)(ar + o.nchp);
   a.req_res_mask = rmask;
   a.n_req_res = __builtin_popcount(rmask);
-  a.timing = getenv("KP_TIMING") ? 1 : 0;
-  a.cont = C.cont_hint;
+  a.timing = C.ov.timing ? 1 : 0;
+  a.cont = C.ov.fast_lane ? (C.ov.fast_lane == 2 ? 1 : 0) : C.cont_hint;
   a.n_groups = C.G;
   a.tg_key = (const int32_t*)(sh + o.tgk);
   a.tg_row = (const int32_t*)(sh + o.tgr);
@@ -3368,11 +3386,7 @@ TfeasArgs TfeasOf(const SolveArgs& a, const uint8_t* sh, const SolveOffs& o, int
 }
 
 // the newNodeClaims order lives in LDS (64 KiB) up to this many NodeClaims, then spills
-int SortCapacity() {
-  int cap = 8192;
-  if (const char* e = getenv("KP_SORT_CAP")) cap = std::max(1, std::min(8192, atoi(e)));  // test hook
-  return cap;
-}
+int SortCapacity(const kp_overrides& ov) { return ov.sort_capacity > 0 ? std::min(8192, ov.sort_capacity) : 8192; }
 
 }  // namespace
 
@@ -3388,7 +3402,7 @@ struct kp_comm {
   kp_allgather_fn host_fn = nullptr;
   void* host_user = nullptr;
   int n_ranks = 1, rank = 0;
-  bool no_tfeas = false;            // KP_NO_TFEAS at init: no template-options table
+  bool no_tfeas = false;            // kp_overrides.template_table at init: no template-options table
   uint64_t tfeas_shard_min = 0;     // shard the table over the ranks from this many (shape-level, template) pairs
   DevBuf buf;  // [0]: this rank's record, [1..n_ranks]: the gathered records
 };
@@ -3437,10 +3451,10 @@ int32_t CommAllGatherDev(kp_comm* c, const void* send, void* recv, size_t bytes)
   return KP_OK;
 }
 void CommReadSettings(kp_comm* c) {
-  c->no_tfeas = getenv("KP_NO_TFEAS") != nullptr;
+  c->no_tfeas = c->ctx->ov.template_table != 0;
   // the table costs ~10 us per 1k pairs on one GPU and an all-gather tens of us: shard only tables worth it
   c->tfeas_shard_min = 1u << 20;
-  if (const char* e = getenv("KP_TFEAS_SHARD_MIN")) c->tfeas_shard_min = strtoull(e, nullptr, 10);
+  if (c->ctx->ov.table_shard_min) c->tfeas_shard_min = c->ctx->ov.table_shard_min;
 }
 }  // namespace
 
@@ -3578,11 +3592,11 @@ static int32_t SolvePrepareLocal(kp_ctx* ctx, const kp_solve_in* in, kp_comm* co
   PutArena(blob, C, C.pod_shape, C.queue, Pc, ExStatic(C, rmask), rmask, o);
   const size_t host_bytes = blob.host.size();
   const int opt_stride = in->max_instance_types ? (int)in->max_instance_types : std::max(1, d.dd.T);
-  ReserveArenaDev(blob, C, Pc, opt_stride, SortCapacity(), true, o);
+  ReserveArenaDev(blob, C, Pc, opt_stride, SortCapacity(C.ov), true, o);
   // template options per (shape-level, template): rows split evenly over the communicator's ranks (padded so that
   // every rank contributes the same byte count to the all-gather)
   const int SLi = (int)C.shape_reqs.size();
-  const bool tfeas_on = NT > 0 && SLi > 0 && !(comm ? comm->no_tfeas : getenv("KP_NO_TFEAS") != nullptr);
+  const bool tfeas_on = NT > 0 && SLi > 0 && !(comm ? comm->no_tfeas : ctx->ov.template_table != 0);
   // shard the rows over the ranks only when the table is large enough to repay the all-gather (kp_comm settings)
   const bool shard = tfeas_on && comm && comm->n_ranks > 1 && (uint64_t)SLi * NT >= comm->tfeas_shard_min;
   const int n_ranks = shard ? comm->n_ranks : 1, my_rank = shard ? comm->rank : 0;
@@ -3753,6 +3767,8 @@ int32_t kp_solve_run_cancellable(kp_solve_plan* plan, kp_cancel* cancel, kp_solv
   std::lock_guard<std::recursive_mutex> lock(ctx->mu);
   if (int32_t rc = SolvePlanStale(plan)) return rc;
   HIPCHK(hipSetDevice(ctx->device));
+  // (a token already set: nothing is queued on the stream)
+  if (cancel && __atomic_load_n(cancel->flag, __ATOMIC_SEQ_CST)) return fail(KP_E_CANCELED, "cancelled before the run");
   const Compiled& C = *plan->cp;
   const Dict& d = C.B->d;
   uint8_t* base = (uint8_t*)plan->buf.p;
@@ -3767,7 +3783,6 @@ int32_t kp_solve_run_cancellable(kp_solve_plan* plan, kp_cancel* cancel, kp_solv
   if (plan->n_hcnc) HIPCHK(hipMemsetAsync(base + plan->o_hcnc, 0, plan->n_hcnc, st));
   SolveArgs a = plan->a;
   if (cancel) {
-    if (__atomic_load_n(cancel->flag, __ATOMIC_SEQ_CST)) return fail(KP_E_CANCELED, "cancelled before the run");
     void* dp = nullptr;
     HIPCHK(hipHostGetDevicePointer(&dp, cancel->flag, 0));
     a.cancel = (const int32_t*)dp;
@@ -4127,11 +4142,12 @@ int32_t kp_filter_prepare(kp_ctx* ctx, const kp_catalog* cat, const kp_feasibili
   fa.out_classes = compact ? (uint64_t*)(base + plan->o_cls) : nullptr;
   fa.ch_stride = plan->ch_stride;
   // the bitset kernel (KP_FEAS_GLOBAL: the per-type global-gather kernel, kept as its cross-check)
-  fa.bits = getenv("KP_FEAS_GLOBAL") ? 0 : 1;
+  const kp_overrides& ov = plan->ctx->ov;
+  fa.bits = ov.feasibility_kernel == 1 ? 0 : 1;
   fa.blocks = (int32_t)std::min<uint32_t>(std::max<uint32_t>((n_queries + 7) / 8, 1), 8192);
-  if (const char* e = getenv("KP_FEAS_BLOCKS")) fa.blocks = std::max(1, std::min(65535, atoi(e)));  // measurement knob
-  fa.pad_ = getenv("KP_FEAS_TEMPORAL") ? 0 : 1;  // bit 0: the cheapest-price stream as non-temporal stores
-  fa.one_row = getenv("KP_FEAS_ONE_ROW") ? 1 : 0;  // cross-check: the one-row-per-wave kernel at any catalogue size
+  if (ov.feasibility_blocks > 0) fa.blocks = std::min(65535, ov.feasibility_blocks);  // measurement knob
+  fa.pad_ = ov.feasibility_temporal ? 0 : 1;  // bit 0: the cheapest-price stream as non-temporal stores
+  fa.one_row = ov.feasibility_kernel == 2 ? 1 : 0;  // cross-check: the one-row-per-wave kernel at any catalogue size
   plan->n_queries = n_queries;
   plan->T = T;
   plan->tiles = tiles;
@@ -4202,6 +4218,9 @@ int32_t kp_filter_class_prices(kp_filter_plan* plan, double* out, uint32_t capac
   if (!plan || !n_classes) return fail(KP_E_INVAL, "null argument");
   std::lock_guard<std::recursive_mutex> lock(plan->ctx->mu);
   if (int32_t rc = CatalogsAlive({plan->alive})) return rc;
+  if (plan->cat->seqnum != plan->seqnum)  // (a consumer caches the table per seqnum: never hand out the old prices)
+    return fail(KP_E_INVAL, "stale plan: catalogue seqnum %llu, plan built at %llu (kp_filter_refresh)",
+                (unsigned long long)plan->cat->seqnum, (unsigned long long)plan->seqnum);
   const HostCat& hc = plan->cp.B->cats[0];
   const int C = plan->cp.B->C, T = plan->T;
   *n_classes = (uint32_t)C;
@@ -4777,9 +4796,8 @@ static int32_t PrepareGeneral(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan
   plan->general = std::make_unique<OwnedCluster>(cl);
   // the superset Solve of the batched simulations, built now (it validates every node and pod as well); a cluster
   // it does not take keeps the per-subset compile, validated here by the whole-cluster compile
-  const char* gbe = getenv("KP_GENERAL_BATCH");
   int32_t rc = KP_E_UNSUPPORTED;
-  if (!(gbe && gbe[0] == '0')) {
+  if (ctx->ov.general_batch == 0) {
     std::lock_guard<std::recursive_mutex> lock(ctx->mu);
     HIPCHK(hipSetDevice(ctx->device));
     plan->gb_tried = true;
@@ -5396,7 +5414,7 @@ static void ApplyHeld(const SolveBase& B, uint64_t held, KReqs& q) {
 // One subset's SimulateScheduling as its own Solve: compiled on the host from the subset's inputs (the path for
 // subsets the batch cannot take, and the whole path with KP_GENERAL_BATCH=0).
 static int32_t GeneralSimOne(kp_cluster_plan* plan, const vector<uint32_t>& cand, const vector<std::map<string, string>>& labels,
-                             int32_t multi_node, SimOut& r, uint64_t* counters, double* dev_ms) {
+                             int32_t multi_node, SimOut& r, uint64_t* counters, double* dev_ms, kp_cancel* cancel) {
   kp_ctx* ctx = plan->ctx;
   const kp_cluster& cl = plan->general->cl;
   const int N = (int)cl.n_nodes;
@@ -5462,7 +5480,7 @@ static int32_t GeneralSimOne(kp_cluster_plan* plan, const vector<uint32_t>& cand
   if (rc) return rc;
   std::unique_ptr<kp_solve_plan, void (*)(kp_solve_plan*)> spg(sp, kp_solve_plan_destroy);
   kp_solve_result* res = nullptr;
-  rc = kp_solve_run(sp, &res);
+  rc = kp_solve_run_cancellable(sp, cancel, &res);
   if (rc) return rc;
   std::unique_ptr<kp_solve_result, void (*)(kp_solve_result*)> rg(res, kp_result_destroy);
   counters[0] += res->stats.attempts;
@@ -5693,7 +5711,7 @@ static int32_t GeneralBatchBuild(kp_cluster_plan* plan, std::shared_ptr<GeneralB
   PutShared(blob, C, gb->so);
   const size_t host_bytes = blob.host.size();
   const int NT = (int)C.B->tmpl_reqs.size(), SLi = (int)C.shape_reqs.size();
-  gb->tfeas_on = NT > 0 && SLi > 0 && getenv("KP_NO_TFEAS") == nullptr;
+  gb->tfeas_on = NT > 0 && SLi > 0 && ctx->ov.template_table == 0;
   gb->tf_words = C.B->TW + KP_NRES / 2 + 1;
   gb->so.tfeas = blob.reserve_dev(gb->tfeas_on ? (size_t)SLi * NT * gb->tf_words * sizeof(uint64_t) : 8);
   HIPCHK(gb->shared.alloc(blob.total()));
@@ -5717,7 +5735,7 @@ static int32_t GeneralBatchLayout(kp_ctx* ctx, GeneralBatch& gb, int Pc) {
   Blob blob;
   const vector<int32_t> zeros(Pc, 0);
   PutArena(blob, C, zeros, zeros, Pc, gb.ex_static, gb.rmask, o);
-  ReserveArenaDev(blob, C, Pc, gb.opt_stride, std::min(SortCapacity(), Pc), false, o);
+  ReserveArenaDev(blob, C, Pc, gb.opt_stride, std::min(SortCapacity(C.ov), Pc), false, o);
   gb.tmpl.assign(blob.host.begin(), blob.host.begin() + o.mut_end);
   gb.stride = (o.arena_end + 255) & ~(size_t)255;
   HIPCHK(gb.pristine.alloc(o.mut_end - o.common + 16));
@@ -5803,11 +5821,24 @@ static int GeneralPatch(const GeneralBatch& gb, const kp_cluster& cl, const vect
 // Runs the batchable subsets `idx` (their candidate lists in cands) as batched Solves; outs[idx[i]] get the decisions.
 static int32_t GeneralBatchRun(kp_cluster_plan* plan, GeneralBatch& gb, const vector<vector<uint32_t>>& cands,
                                const vector<int>& idx, const vector<std::map<string, string>>& labels, int32_t multi_node,
-                               vector<SimOut>& outs, uint64_t* counters, double* dev_ms, double* host_ms) {
+                               vector<SimOut>& outs, uint64_t* counters, double* dev_ms, double* host_ms,
+                               kp_cancel* cancel, uint64_t* n_launches) {
   kp_ctx* ctx = plan->ctx;
   const kp_cluster& cl = plan->general->cl;
   const Compiled& C = *gb.C;
   hipStream_t st = ctx->stream;
+  // kp_cancel: solve_kernel polls the flag (every ~1,024 pops of each simulation) and the host reads it before each
+  // launch; any early return (cancellation, an error) first drains the launches this call queued
+  const int32_t* dcancel = nullptr;
+  if (cancel) {
+    void* dp = nullptr;
+    HIPCHK(hipHostGetDevicePointer(&dp, cancel->flag, 0));
+    dcancel = (const int32_t*)dp;
+  }
+  struct Drain {
+    hipStream_t s;
+    ~Drain() { (void)hipStreamSynchronize(s); }
+  } drain{st};
   // the arena size: every simulation of the batch fits (rounded up, so that nearby batches share a layout)
   size_t max_pods = 1;
   vector<size_t> len(cands.size(), 0);
@@ -5835,9 +5866,9 @@ static int32_t GeneralBatchRun(kp_cluster_plan* plan, GeneralBatch& gb, const ve
   // of trailing the launch
   vector<int> order(idx);
   std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return len[x] > len[y]; });
-  if (getenv("KP_HOST_TIMING"))
+  if (ctx->ov.host_timing)
     fprintf(stderr, "[kp general] arena stride %.2f MB, %zu simulations per launch, Pc %d\n", gb.stride / 1e6, per_launch, Pc);
-  const int sort_cap = std::min(SortCapacity(), Pc);
+  const int sort_cap = std::min(SortCapacity(C.ov), Pc);
   const size_t dyn = std::max<size_t>((size_t)2 * sort_cap * sizeof(int32_t), o.chk_on ? CHK_LDS_BYTES : 0);
   GenScratch scratch;
   vector<SolveArgs> sargs;
@@ -5875,6 +5906,7 @@ static int32_t GeneralBatchRun(kp_cluster_plan* plan, GeneralBatch& gb, const ve
       const int i = order[b0 + j];
       const uint64_t* sj = &stats[(size_t)j * KP_SOLVE_STATS];
       if (sj[7]) return fail(KP_E_DEVICE, "solve_kernel exceeded its Queue.Pop bound in simulation %d: aborted", i);
+      if (sj[46]) return fail(KP_E_CANCELED, "consolidation simulations cancelled (kp_cancel_set)");
       counters[0] += sj[0];
       counters[1] += sj[1];
       counters[2] += sj[2];
@@ -5916,6 +5948,8 @@ static int32_t GeneralBatchRun(kp_cluster_plan* plan, GeneralBatch& gb, const ve
   int pending = -1;  // the slot whose launch is in flight and not yet decided
   int launch_no = 0;
   for (size_t b0 = 0; b0 < idx.size(); b0 += per_launch, launch_no++) {
+    if (cancel && __atomic_load_n(cancel->flag, __ATOMIC_SEQ_CST))
+      return fail(KP_E_CANCELED, "consolidation simulations cancelled (kp_cancel_set) after %zu of %zu", b0, idx.size());
     GenSlot& sl = slots[launch_no & 1];
     const auto th0 = std::chrono::steady_clock::now();
     const int n = (int)std::min(per_launch, idx.size() - b0);
@@ -5941,7 +5975,7 @@ static int32_t GeneralBatchRun(kp_cluster_plan* plan, GeneralBatch& gb, const ve
         pending = -1;
       }
       for (size_t j = b0; j < idx.size(); j++)
-        if (int32_t rc = GeneralSimOne(plan, cands[order[j]], labels, multi_node, outs[order[j]], counters, dev_ms)) return rc;
+        if (int32_t rc = GeneralSimOne(plan, cands[order[j]], labels, multi_node, outs[order[j]], counters, dev_ms, cancel)) return rc;
       break;
     }
     uint8_t* arenas = (uint8_t*)sl.arenas.p;
@@ -5958,6 +5992,7 @@ static int32_t GeneralBatchRun(kp_cluster_plan* plan, GeneralBatch& gb, const ve
       uint8_t* ar = arenas + gb.stride * j;
       SolveArgs& a = sargs[j];
       BindSolve(a, C, o, sh, ar, (int)queues[j].size(), Pc, gb.rmask, gb.res_mode);
+      a.cancel = dcancel;
       if (gb.tfeas_on) {
         a.tfeas = (const uint64_t*)(sh + o.tfeas);
         a.tfeas_words = gb.tf_words;
@@ -6029,6 +6064,7 @@ static int32_t GeneralBatchRun(kp_cluster_plan* plan, GeneralBatch& gb, const ve
       if (int32_t rc = decide(slots[pending])) return rc;
     }
     pending = launch_no & 1;
+    ++*n_launches;
   }
   if (pending >= 0) {
     if (int32_t rc = decide(slots[pending])) return rc;
@@ -6037,7 +6073,7 @@ static int32_t GeneralBatchRun(kp_cluster_plan* plan, GeneralBatch& gb, const ve
 }
 
 static int32_t GeneralSimLocked(kp_cluster_plan* plan, const uint32_t* offsets, const uint32_t* nodes,
-                                uint32_t n_subsets, int32_t multi_node, SimArgs& a) {
+                                uint32_t n_subsets, int32_t multi_node, SimArgs& a, kp_cancel* cancel) {
   kp_ctx* ctx = plan->ctx;
   const kp_cluster& cl = plan->general->cl;
   const int N = (int)cl.n_nodes;
@@ -6076,8 +6112,7 @@ static int32_t GeneralSimLocked(kp_cluster_plan* plan, const uint32_t* offsets, 
       plan->gb_tried = false;
     }
   }
-  const char* gbe = getenv("KP_GENERAL_BATCH");
-  const bool batch_on = !(gbe && gbe[0] == '0');
+  const bool batch_on = ctx->ov.general_batch == 0;
   if (batch_on && !plan->gb_tried) {
     plan->gb_tried = true;
     int32_t rc = GeneralBatchBuild(plan, plan->gb);
@@ -6088,7 +6123,7 @@ static int32_t GeneralSimLocked(kp_cluster_plan* plan, const uint32_t* offsets, 
   const double t_setup = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
   vector<SimOut> outs(n_subsets);
   memset(outs.data(), 0, sizeof(SimOut) * outs.size());
-  uint64_t counters[3] = {0, 0, 0};
+  uint64_t counters[3] = {0, 0, 0}, n_launches = 0;
   double dev_ms = 0, host_ms[2] = {0, 0};  // the batch's host work: overlays + arguments, decisions
   vector<int> batched, single;
   for (uint32_t s = 0; s < n_subsets; s++) {
@@ -6104,13 +6139,14 @@ static int32_t GeneralSimLocked(kp_cluster_plan* plan, const uint32_t* offsets, 
   }
   const auto t1 = clk::now();
   if (!batched.empty()) {
-    const int32_t rc = GeneralBatchRun(plan, *plan->gb, cands, batched, labels, multi_node, outs, counters, &dev_ms, host_ms);
+    const int32_t rc = GeneralBatchRun(plan, *plan->gb, cands, batched, labels, multi_node, outs, counters, &dev_ms, host_ms,
+                                       cancel, &n_launches);
     if (rc) return rc;
   }
   const double t_batch = std::chrono::duration<double, std::milli>(clk::now() - t1).count();
   const auto t2 = clk::now();
   for (int s : single) {
-    const int32_t rc = GeneralSimOne(plan, cands[s], labels, multi_node, outs[s], counters, &dev_ms);
+    const int32_t rc = GeneralSimOne(plan, cands[s], labels, multi_node, outs[s], counters, &dev_ms, cancel);
     if (rc) return rc;
   }
   const double t_single = std::chrono::duration<double, std::milli>(clk::now() - t2).count();
@@ -6125,13 +6161,14 @@ static int32_t GeneralSimLocked(kp_cluster_plan* plan, const uint32_t* offsets, 
   a = SimArgs{};
   a.out = (SimOut*)plan->batch.p;
   a.stats = (uint64_t*)((uint8_t*)plan->batch.p + ((sizeof(SimOut) * std::max<uint32_t>(n_subsets, 1) + 255) & ~(size_t)255));
-  uint64_t st[8] = {counters[0], counters[1], counters[2], (uint64_t)batched.size(), (uint64_t)single.size(), 0, 0, 0};
+  uint64_t st[8] = {counters[0], counters[1], counters[2], (uint64_t)batched.size(), (uint64_t)single.size(), 0, n_launches,
+                    0};
   if (n_subsets) HIPCHK(hipMemcpyAsync(a.out, outs.data(), sizeof(SimOut) * n_subsets, hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(hipMemcpyAsync(a.stats, st, sizeof st, hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
   plan->general_ms = dev_ms;
   plan->general_batched = (uint32_t)batched.size();
-  if (getenv("KP_HOST_TIMING"))
+  if (ctx->ov.host_timing)
     fprintf(stderr, "[kp general] %u sims (%zu batched, %zu single): setup %.2f batch %.2f (overlays %.2f decisions %.2f "
             "device %.2f) single %.2f ms\n", n_subsets, batched.size(), single.size(), t_setup, t_batch, host_ms[0],
             host_ms[1], dev_ms, t_single);
@@ -6139,9 +6176,11 @@ static int32_t GeneralSimLocked(kp_cluster_plan* plan, const uint32_t* offsets, 
 }
 
 static int32_t SimLaunchLocked(kp_cluster_plan* plan, const uint32_t* offsets, const uint32_t* nodes, uint32_t n_subsets,
-                               int32_t multi_node, SimArgs& a_out) {
+                               int32_t multi_node, SimArgs& a_out, kp_cancel* cancel) {
   kp_ctx* ctx = plan->ctx;
-  if (plan->general) return GeneralSimLocked(plan, offsets, nodes, n_subsets, multi_node, a_out);
+  if (cancel && __atomic_load_n(cancel->flag, __ATOMIC_SEQ_CST))
+    return fail(KP_E_CANCELED, "cancelled before the simulations");
+  if (plan->general) return GeneralSimLocked(plan, offsets, nodes, n_subsets, multi_node, a_out, cancel);
   if (int32_t rc = CatalogsAlive(plan->cp->B->alive)) return rc;
   if (SeqnumsOf(plan->cp->B->catalogs) != plan->cp->B->seqnums)
     return fail(KP_E_INVAL, "stale plan: a catalogue's seqnum changed since it was prepared (kp_cluster_refresh)");
@@ -6169,6 +6208,12 @@ static int32_t SimLaunchLocked(kp_cluster_plan* plan, const uint32_t* offsets, c
   a.cap2 = cap2;
   a.wave_lds = (int)(((size_t)16 * a.EW + (size_t)6 * cap2 + 15) & ~(size_t)15);
   a.multi_node = multi_node ? 1 : 0;
+  a.cancel = nullptr;
+  if (cancel) {
+    void* dp = nullptr;
+    HIPCHK(hipHostGetDevicePointer(&dp, cancel->flag, 0));
+    a.cancel = (const int32_t*)dp;
+  }
   hipFuncAttributes fa;
   HIPCHK(hipFuncGetAttributes(&fa, sim_kernel_ptr()));
   const size_t lds_wg = fa.sharedSizeBytes + (size_t)SIM_WAVES * a.wave_lds;
@@ -6235,21 +6280,29 @@ static int32_t SimLaunchLocked(kp_cluster_plan* plan, const uint32_t* offsets, c
 
 int32_t kp_cluster_simulate(kp_cluster_plan* plan, const uint32_t* offsets, const uint32_t* nodes, uint32_t n_subsets,
                             int32_t multi_node, kp_sim_result* out, kp_solve_stats* stats) {
+  return kp_cluster_simulate_cancellable(plan, nullptr, offsets, nodes, n_subsets, multi_node, out, stats);
+}
+
+int32_t kp_cluster_simulate_cancellable(kp_cluster_plan* plan, kp_cancel* cancel, const uint32_t* offsets,
+                                        const uint32_t* nodes, uint32_t n_subsets, int32_t multi_node, kp_sim_result* out,
+                                        kp_solve_stats* stats) {
   auto t0 = std::chrono::steady_clock::now();
   if (!plan || (n_subsets && (!offsets || !out))) return fail(KP_E_INVAL, "null argument");
+  if (cancel && cancel->ctx.p != plan->ctx.p) return fail(KP_E_INVAL, "the cancel token belongs to another context");
   kp_ctx* ctx = plan->ctx;
   std::lock_guard<std::recursive_mutex> lock(ctx->mu);
   HIPCHK(hipSetDevice(ctx->device));
   if (stats) memset(stats, 0, sizeof *stats);
   if (n_subsets == 0) return KP_OK;
   SimArgs a;
-  int32_t rc = SimLaunchLocked(plan, offsets, nodes, n_subsets, multi_node, a);
+  int32_t rc = SimLaunchLocked(plan, offsets, nodes, n_subsets, multi_node, a, cancel);
   if (rc) return rc;
   hipStream_t st = ctx->stream;
   uint64_t kst[8];
   HIPCHK(hipMemcpyAsync(out, a.out, sizeof(SimOut) * n_subsets, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(kst, a.stats, sizeof kst, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  if (!plan->general && kst[5]) return fail(KP_E_CANCELED, "consolidation simulations cancelled (kp_cancel_set)");
   float ms = (float)plan->general_ms;
   if (!plan->general) HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
   for (uint32_t s = 0; s < n_subsets; s++)
@@ -6261,7 +6314,10 @@ int32_t kp_cluster_simulate(kp_cluster_plan* plan, const uint32_t* offsets, cons
     stats->bytes_algorithmic = kst[1];
     stats->pops = kst[2];
     stats->phase_cycles[0] = kst[3];
-    if (plan->general) stats->phase_cycles[1] = kst[4];  // general path: simulations batched / compiled per subset
+    if (plan->general) {  // general path: simulations batched / compiled per subset, batched launches
+      stats->phase_cycles[1] = kst[4];
+      stats->phase_cycles[2] = kst[6];
+    }
     stats->prepare_ms = plan->prepare_ms;
     stats->host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   }
@@ -6414,8 +6470,17 @@ void kp_comm_destroy(kp_comm* c) {
 int32_t kp_consolidate_argmin(kp_cluster_plan* plan, kp_comm* comm, const uint32_t* offsets, const uint32_t* nodes,
                               uint32_t n_subsets, uint64_t base_index, int32_t multi_node, kp_sim_result* out,
                               kp_choice* best, kp_solve_stats* stats) {
+  return kp_consolidate_argmin_cancellable(plan, comm, nullptr, offsets, nodes, n_subsets, base_index, multi_node, out,
+                                           best, stats);
+}
+
+int32_t kp_consolidate_argmin_cancellable(kp_cluster_plan* plan, kp_comm* comm, kp_cancel* cancel,
+                                          const uint32_t* offsets, const uint32_t* nodes, uint32_t n_subsets,
+                                          uint64_t base_index, int32_t multi_node, kp_sim_result* out, kp_choice* best,
+                                          kp_solve_stats* stats) {
   auto t0 = std::chrono::steady_clock::now();
   if (!plan || !best || (n_subsets && !offsets)) return fail(KP_E_INVAL, "null argument");
+  if (cancel && cancel->ctx.p != plan->ctx.p) return fail(KP_E_INVAL, "the cancel token belongs to another context");
   if (comm && comm->ctx->device != plan->ctx->device) return fail(KP_E_INVAL, "comm and plan are on different GPUs");
   kp_ctx* ctx = plan->ctx;
   std::lock_guard<std::recursive_mutex> lock(ctx->mu);
@@ -6436,7 +6501,7 @@ int32_t kp_consolidate_argmin(kp_cluster_plan* plan, kp_comm* comm, const uint32
     HIPCHK(parts.alloc(sizeof(ArgmaxPart) * n_parts));
     HIPCHK(rec.alloc(sizeof(CommBest)));
     if (n_subsets) {
-      int32_t rc = SimLaunchLocked(plan, offsets, nodes, n_subsets, multi_node, a);
+      int32_t rc = SimLaunchLocked(plan, offsets, nodes, n_subsets, multi_node, a, cancel);
       if (rc) return rc;
       if (out) HIPCHK(hipMemcpyAsync(out, a.out, sizeof(SimOut) * n_subsets, hipMemcpyDeviceToHost, st));
       HIPCHK(hipMemcpyAsync(kst, a.stats, sizeof kst, hipMemcpyDeviceToHost, st));
@@ -6445,6 +6510,8 @@ int32_t kp_consolidate_argmin(kp_cluster_plan* plan, kp_comm* comm, const uint32
                          (int64_t)base_index, (CommBest*)rec.p, st));
     HIPCHK(hipMemcpyAsync(&mine, rec.p, sizeof mine, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    if (n_subsets && !plan->general && kst[5])
+      return fail(KP_E_CANCELED, "consolidation sweep cancelled (kp_cancel_set)");
     if (n_subsets && plan->general) ms = (float)plan->general_ms;
     else if (n_subsets) HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
     return KP_OK;
@@ -6480,7 +6547,10 @@ int32_t kp_consolidate_argmin(kp_cluster_plan* plan, kp_comm* comm, const uint32
     stats->bytes_algorithmic = kst[1];
     stats->pops = kst[2];
     stats->phase_cycles[0] = kst[3];
-    if (plan->general) stats->phase_cycles[1] = kst[4];  // general path: simulations batched / compiled per subset
+    if (plan->general) {  // general path: simulations batched / compiled per subset, batched launches
+      stats->phase_cycles[1] = kst[4];
+      stats->phase_cycles[2] = kst[6];
+    }
     stats->prepare_ms = plan->prepare_ms;
     stats->host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   }

@@ -5437,17 +5437,11 @@ __global__ __launch_bounds__(LAUNCH_WAVES * 64) void launch_kernel(LaunchArgs a)
 // launchers
 // ------------------------------------------------------------------------------------------------
 hipError_t launch_solve(const SolveArgs& a, int nw, size_t dyn_lds, hipStream_t s) {
-  (void)nw;  // 8 waves: one candidate per wave, 512 pre-pass lanes
-  // 4 waves (one per SIMD): the per-pod barriers and pre-pass compaction are cheaper than with 8, and 4
-  // candidates per attempt round cover the typical 2-3 attempts per pod. KP_SOLVE_WAVES=8: 8 waves.
-  static const int nw4 = !(getenv("KP_SOLVE_WAVES") && atoi(getenv("KP_SOLVE_WAVES")) == 8);
-  if (nw4) {
-    if (a.n_groups) hipLaunchKernelGGL((solve_kernel<4, true, false>), dim3(1), dim3(4 * 64), dyn_lds, s, a, nullptr);
-    else hipLaunchKernelGGL((solve_kernel<4, false, false>), dim3(1), dim3(4 * 64), dyn_lds, s, a, nullptr);
-  } else {
-    if (a.n_groups) hipLaunchKernelGGL((solve_kernel<8, true, false>), dim3(1), dim3(8 * 64), dyn_lds, s, a, nullptr);
-    else hipLaunchKernelGGL((solve_kernel<8, false, false>), dim3(1), dim3(8 * 64), dyn_lds, s, a, nullptr);
-  }
+  (void)nw;
+  // 4 waves (one per SIMD): the per-pod barriers and pre-pass compaction are cheaper than with 8, and 4 candidates per
+  // attempt round cover the typical 2-3 attempts per pod (8 waves measured slower)
+  if (a.n_groups) hipLaunchKernelGGL((solve_kernel<4, true, false>), dim3(1), dim3(4 * 64), dyn_lds, s, a, nullptr);
+  else hipLaunchKernelGGL((solve_kernel<4, false, false>), dim3(1), dim3(4 * 64), dyn_lds, s, a, nullptr);
   return hipGetLastError();
 }
 hipError_t launch_solve_batch(const SolveArgs& a0, const SolveArgs* dev_args, int n, size_t dyn_lds, hipStream_t s) {

@@ -302,7 +302,13 @@ __global__ __launch_bounds__(NW * 64) void sim_kernel(SimArgs a) {
   int32_t vcount = 0;
   const uint32_t rmask = a.req_res_mask;
 
-  for (int sim = slot; sim < a.n_subsets; sim += a.n_slots) {
+  bool cancelled = false;
+  for (int sim = slot, it = 0; sim < a.n_subsets; sim += a.n_slots, it++) {
+    // kp_cancel (consolidation timeouts): the flag every 8 subsets of this wave; a set flag ends the wave's share
+    if ((it & 7) == 0 && cancel_set(a.cancel)) {
+      cancelled = true;
+      break;
+    }
     const uint32_t s0 = a.sub_off[sim];
     const int ns = (int)(a.sub_off[sim + 1] - s0);
     for (int w = lane; w < EW; w += 64) {
@@ -707,6 +713,7 @@ __global__ __launch_bounds__(NW * 64) void sim_kernel(SimArgs a) {
     atomicAdd((unsigned long long*)&a.stats[1], (unsigned long long)bytes);
     atomicAdd((unsigned long long*)&a.stats[2], (unsigned long long)pops);
     atomicAdd((unsigned long long*)&a.stats[3], (unsigned long long)words);
+    if (cancelled) atomicAdd((unsigned long long*)&a.stats[5], 1ull);
   }
 }
 

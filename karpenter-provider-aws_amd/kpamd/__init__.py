@@ -40,6 +40,8 @@ def load_lib(path=None):
         "kp_abi_version": (C.c_int32, []),
         "kp_ctx_create": (C.c_int32, [P(abi.Options), P(C.c_void_p)]),
         "kp_ctx_destroy": (None, [C.c_void_p]),
+        "kp_ctx_set_overrides": (C.c_int32, [C.c_void_p, P(abi.Overrides)]),
+        "kp_ctx_get_overrides": (C.c_int32, [C.c_void_p, P(abi.Overrides)]),
         "kp_catalog_upload": (C.c_int32, [C.c_void_p, P(abi.CatalogDesc), C.c_uint64, P(C.c_void_p)]),
         "kp_catalog_seqnum": (C.c_uint64, [C.c_void_p]),
         "kp_catalog_size": (C.c_uint32, [C.c_void_p]),
@@ -91,6 +93,8 @@ def load_lib(path=None):
         "kp_cluster_prepare": (C.c_int32, [C.c_void_p, P(abi.Cluster), P(C.c_void_p)]),
         "kp_cluster_simulate": (C.c_int32, [C.c_void_p, P(C.c_uint32), P(C.c_uint32), C.c_uint32, C.c_int32,
                                             P(abi.SimResult), P(abi.SolveStats)]),
+        "kp_cluster_simulate_cancellable": (C.c_int32, [C.c_void_p, C.c_void_p, P(C.c_uint32), P(C.c_uint32), C.c_uint32,
+                                                        C.c_int32, P(abi.SimResult), P(abi.SolveStats)]),
         "kp_cluster_plan_destroy": (None, [C.c_void_p]),
         "kp_comm_unique_id": (C.c_int32, [C.c_char_p]),
         "kp_comm_init": (C.c_int32, [C.c_void_p, C.c_char_p, C.c_int32, C.c_int32, P(C.c_void_p)]),
@@ -102,6 +106,9 @@ def load_lib(path=None):
         "kp_consolidate_argmin": (C.c_int32, [C.c_void_p, C.c_void_p, P(C.c_uint32), P(C.c_uint32), C.c_uint32,
                                               C.c_uint64, C.c_int32, P(abi.SimResult), P(abi.Choice),
                                               P(abi.SolveStats)]),
+        "kp_consolidate_argmin_cancellable": (C.c_int32, [C.c_void_p, C.c_void_p, C.c_void_p, P(C.c_uint32),
+                                                          P(C.c_uint32), C.c_uint32, C.c_uint64, C.c_int32,
+                                                          P(abi.SimResult), P(abi.Choice), P(abi.SolveStats)]),
         "kp_choice_reduce": (C.c_int32, [P(abi.Choice), C.c_uint32, P(abi.Choice)]),
     }
     for name, (res, args) in sig.items():
@@ -130,6 +137,17 @@ class Context:
         h = C.c_void_p()
         _check(self.lib, self.lib.kp_ctx_create(C.byref(self.opts), C.byref(h)))
         self.h = h
+
+    def overrides(self):
+        """kp_ctx_get_overrides -> dict of the kp_overrides fields."""
+        ov = abi.Overrides()
+        _check(self.lib, self.lib.kp_ctx_get_overrides(self.h, C.byref(ov)))
+        return {k: getattr(ov, k) for k, _ in abi.Overrides._fields_}
+
+    def set_overrides(self, **kw):
+        """kp_ctx_set_overrides: the given kp_overrides fields, every other field 0 (the production choice)."""
+        ov = abi.Overrides(**kw)
+        _check(self.lib, self.lib.kp_ctx_set_overrides(self.h, C.byref(ov)))
 
     def close(self):
         if self.h:
@@ -566,20 +584,21 @@ class ClusterPlan:
         """kp_cluster_refresh: re-apply the catalogues' current offerings (after update_offerings) in place."""
         _check(self.ctx.lib, self.ctx.lib.kp_cluster_refresh(self.h))
 
-    def simulate(self, subsets, multi_node=True, raw=False):
+    def simulate(self, subsets, multi_node=True, raw=False, cancel=None):
         """subsets: list of node-index lists (candidate order). Returns (results, stats); raw=True returns
-        the kp_sim_result array instead of dicts."""
+        the kp_sim_result array instead of dicts. cancel: a Cancel token (kp_cluster_simulate_cancellable)."""
         arena = Arena()
         offs, flat = abi.subsets_csr(arena, subsets)
         out = (abi.SimResult * max(1, len(subsets)))()
         st = abi.SolveStats()
-        _check(self.ctx.lib, self.ctx.lib.kp_cluster_simulate(self.h, offs, flat, len(subsets), 1 if multi_node else 0,
-                                                              out, C.byref(st)))
+        _check(self.ctx.lib, self.ctx.lib.kp_cluster_simulate_cancellable(
+            self.h, cancel.h if cancel is not None else None, offs, flat, len(subsets), 1 if multi_node else 0,
+            out, C.byref(st)))
         if raw:
             return out, stats_dict(st)
         return [sim_dict(out[i]) for i in range(len(subsets))], stats_dict(st)
 
-    def simulate_csr(self, offsets, nodes, multi_node=True):
+    def simulate_csr(self, offsets, nodes, multi_node=True, cancel=None):
         """CSR batch (uint32 offsets[n+1], node indices) -> numpy structured array (abi.sim_dtype()), stats."""
         offsets = np.ascontiguousarray(offsets, dtype=np.uint32)
         nodes = np.ascontiguousarray(nodes, dtype=np.uint32)
@@ -587,15 +606,15 @@ class ClusterPlan:
         out = np.zeros(max(n, 1), dtype=abi.sim_dtype())
         st = abi.SolveStats()
         P = C.POINTER
-        _check(self.ctx.lib, self.ctx.lib.kp_cluster_simulate(
-            self.h, offsets.ctypes.data_as(P(C.c_uint32)), nodes.ctypes.data_as(P(C.c_uint32)) if len(nodes) else None,
+        _check(self.ctx.lib, self.ctx.lib.kp_cluster_simulate_cancellable(
+            self.h, cancel.h if cancel is not None else None, offsets.ctypes.data_as(P(C.c_uint32)), nodes.ctypes.data_as(P(C.c_uint32)) if len(nodes) else None,
             n, 1 if multi_node else 0, out.ctypes.data_as(P(abi.SimResult)), C.byref(st)))
         return out[:n], stats_dict(st)
 
-    def argmin(self, offsets, nodes, base_index=0, comm=None, multi_node=True, read_all=False):
+    def argmin(self, offsets, nodes, base_index=0, comm=None, multi_node=True, read_all=False, cancel=None):
         """kp_consolidate_argmin: this rank's subsets (CSR, global indices base_index + i) simulated, reduced on the
         device and across ranks (RCCL all-gather when comm is a Comm). Returns (choice dict, per-subset results
-        or None, stats)."""
+        or None, stats). cancel: a Cancel token (kp_consolidate_argmin_cancellable)."""
         offsets = np.ascontiguousarray(offsets, dtype=np.uint32)
         nodes = np.ascontiguousarray(nodes, dtype=np.uint32)
         n = len(offsets) - 1
@@ -603,8 +622,9 @@ class ClusterPlan:
         ch = abi.Choice()
         st = abi.SolveStats()
         P = C.POINTER
-        _check(self.ctx.lib, self.ctx.lib.kp_consolidate_argmin(
-            self.h, comm.h if comm is not None else None, offsets.ctypes.data_as(P(C.c_uint32)),
+        _check(self.ctx.lib, self.ctx.lib.kp_consolidate_argmin_cancellable(
+            self.h, comm.h if comm is not None else None, cancel.h if cancel is not None else None,
+            offsets.ctypes.data_as(P(C.c_uint32)),
             nodes.ctypes.data_as(P(C.c_uint32)) if len(nodes) else None, n, int(base_index), 1 if multi_node else 0,
             out.ctypes.data_as(P(abi.SimResult)) if out is not None else None, C.byref(ch), C.byref(st)))
         return choice_dict(ch), (out[:n] if out is not None else None), stats_dict(st)

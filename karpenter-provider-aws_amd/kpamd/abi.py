@@ -199,6 +199,14 @@ class Options(C.Structure):
     _fields_ = [("vm_memory_overhead_percent", C.c_double), ("reserved_enis", C.c_int32), ("device", C.c_int32)]
 
 
+class Overrides(C.Structure):
+    """kp_overrides (ABI v12): test / measurement overrides of kernel and path choices; all 0 = production."""
+    _fields_ = [("fast_lane", C.c_int32), ("sort_capacity", C.c_int32), ("chunk_capacity", C.c_int32),
+                ("template_table", C.c_int32), ("table_shard_min", C.c_uint64), ("general_batch", C.c_int32),
+                ("feasibility_kernel", C.c_int32), ("feasibility_blocks", C.c_int32),
+                ("feasibility_temporal", C.c_int32), ("timing", C.c_int32), ("host_timing", C.c_int32)]
+
+
 class EC2Info(C.Structure):
     _fields_ = [("name", C.c_char_p), ("vcpu", C.c_int32), ("reserved0_", C.c_int32), ("memory_mib", C.c_int64),
                 ("arch", C.c_char_p), ("hypervisor", C.c_char_p), ("encryption_in_transit", C.c_int32),

@@ -1046,7 +1046,7 @@ struct Topology {
   }
 
   // MakeTopologyNodeFilter + NewTopologyGroup; identity = upstream TopologyGroup.Hash fields (key, type,
-  // namespaces, selector, maxSkew, node filter).
+  // namespaces, selector, maxSkew, node filter = requirements, both policies and the pod's tolerations).
   std::unique_ptr<TopologyGroup> NewGroup(const PodState& p, const Spread& s) const {
     auto g = std::make_unique<TopologyGroup>();
     g->key = s.key;
@@ -1069,8 +1069,8 @@ struct Topology {
     string id = s.key + "|" + std::to_string(s.maxSkew) + "|" + p.ns + "|" + s.sel.Canon() + "|" +
                 std::to_string(g->affinityHonor) + std::to_string(g->taintHonor) + "|";
     for (auto& f : g->filter) id += "[" + ReqsCanon(f) + "]";
-    if (g->taintHonor)
-      for (auto& t : g->tols) id += "(" + t.key + "," + t.value + "," + std::to_string(t.op) + "," + std::to_string(t.effect) + ")";
+    // the filter's tolerations under every taint policy (upstream TopologyNodeFilter.Tolerations, hashed with it)
+    for (auto& t : g->tols) id += "(" + t.key + "," + t.value + "," + std::to_string(t.op) + "," + std::to_string(t.effect) + ")";
     g->id = id;
     // domainGroup.ForEachDomain(pod, taintPolicy): register every known domain with a zero count
     auto dg = domainGroups.find(s.key);

@@ -32,9 +32,17 @@ def ctx():
     c.close()
 
 
+@pytest.fixture
+def ov(ctx):
+    """kp_ctx_set_overrides on the session context for one test (keyword fields of kp_overrides); every override is
+    reset to the production choice after the test."""
+    yield ctx.set_overrides
+    ctx.set_overrides()
+
+
 @pytest.fixture(params=["batch", "single"])
-def general_mode(request, monkeypatch):
+def general_mode(request, ov):
     """The general consolidation path two ways: the superset Solve with batched simulations (default), and every
-    subset compiled on its own (KP_GENERAL_BATCH=0)."""
-    monkeypatch.setenv("KP_GENERAL_BATCH", "1" if request.param == "batch" else "0")
+    subset compiled on its own (kp_overrides.general_batch = 1)."""
+    ov(general_batch=0 if request.param == "batch" else 1)
     return request.param

@@ -23,7 +23,7 @@ def test_all_declared_symbols_exported():
 
 def test_abi_version_and_struct_sizes():
     lib = kpamd.load_lib()
-    assert lib.kp_abi_version() == 11
+    assert lib.kp_abi_version() == 12
     from kpamd import abi
     assert C.sizeof(abi.ResourceList) == 12 * 8 + 8
     assert C.sizeof(abi.Offering) == 5 * 8 + 8 + 8
@@ -66,7 +66,7 @@ def test_struct_sizes_match_the_c_header(tmp_path):
              "kp_options": abi.Options, "kp_ec2_info": abi.EC2Info, "kp_nodeclaim_info": abi.NodeClaimInfo,
              "kp_launch_request": abi.LaunchRequest, "kp_feasibility_query": abi.FeasibilityQuery,
              "kp_instance_type": abi.InstanceType, "kp_preferred_term": abi.PreferredTerm,
-             "kp_label_selector": abi.LabelSelector, "kp_pod": abi.Pod}
+             "kp_label_selector": abi.LabelSelector, "kp_pod": abi.Pod, "kp_overrides": abi.Overrides}
     src = tmp_path / "sz.c"
     src.write_text('#include <stdio.h>\n#include "kp/kp_abi.h"\nint main(void){\n' +
                    "".join(f'printf("%zu\\n", sizeof({k}));\n' for k in pairs) + "return 0;}\n")
@@ -74,3 +74,15 @@ def test_struct_sizes_match_the_c_header(tmp_path):
     subprocess.check_call(["gcc", "-I", os.path.dirname(os.path.dirname(HDR)), str(src), "-o", str(exe)])
     got = [int(x) for x in subprocess.check_output([str(exe)]).split()]
     assert got == [C.sizeof(t) for t in pairs.values()], dict(zip(pairs, got))
+
+
+def test_library_reads_no_environment():
+    """ABI v12: no environment variable picks a kernel or a path in production (kp_overrides, set per context, replaces
+    the test hooks): libkp.so does not import getenv / secure_getenv."""
+    import shutil
+    import subprocess
+    import pytest
+    if not shutil.which("nm"):
+        pytest.skip("nm not available")
+    syms = subprocess.check_output(["nm", "-D", "--undefined-only", kpamd.LIB_PATH], text=True)
+    assert not [l for l in syms.splitlines() if l.split()[-1].split("@")[0] in ("getenv", "secure_getenv")]

@@ -72,7 +72,7 @@ def test_consolidation_fullsize(ctx, catalog, digests):
 
 
 @pytest.mark.gpu
-def test_general_fullsize(ctx, catalog, digests, monkeypatch):
+def test_general_fullsize(ctx, catalog, digests):
     """The general path at the bench's size: 2,000-node spread cluster, 300 subsets batched on the superset Solve,
     every decision field equal to the oracle's digest."""
     import kpamd
@@ -80,7 +80,6 @@ def test_general_fullsize(ctx, catalog, digests, monkeypatch):
     from kpamd import synth
     if "general-2000" not in digests:
         pytest.skip("general-2000: digest not generated (make_fullsize_digests.py general-2000)")
-    monkeypatch.setenv("KP_GENERAL_BATCH", "1")
     cl = synth.spread_cluster(catalog, 2_000)
     pre, rnd = mk.general_subsets(cl)
     plan = kpamd.ClusterPlan(ctx, cl)
@@ -96,7 +95,7 @@ def test_general_fullsize(ctx, catalog, digests, monkeypatch):
 
 
 @pytest.mark.gpu
-def test_general_10000(ctx, catalog, digests, monkeypatch):
+def test_general_10000(ctx, catalog, digests):
     """The general path at config 4's size: the 10,000-node spread cluster (83k pods), the 100 prefixes and 200 random
     subsets of 2..100 candidates, batched on the superset Solve, every decision field equal to the oracle's digest."""
     import kpamd
@@ -104,7 +103,6 @@ def test_general_10000(ctx, catalog, digests, monkeypatch):
     from kpamd import synth
     if "general-10000" not in digests:
         pytest.skip("general-10000: digest not generated (make_fullsize_digests.py general-10000)")
-    monkeypatch.setenv("KP_GENERAL_BATCH", "1")
     cl = synth.spread_cluster(catalog, 10_000)
     pre, rnd = mk.general10k_subsets(cl)
     plan = kpamd.ClusterPlan(ctx, cl)

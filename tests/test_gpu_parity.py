@@ -100,10 +100,10 @@ def test_feasibility_kernel_vs_oracle(ctx, catalog, n_types):
         np.testing.assert_array_equal(cheapest[qi][want_k], want_c[want_k])
 
 
-def test_sort_spill_to_global(ctx, catalog, monkeypatch):
+def test_sort_spill_to_global(ctx, catalog, ov):
     """newNodeClaims order spills from LDS to global memory past the LDS capacity (forced small here)."""
     from kpamd import synth
-    monkeypatch.setenv("KP_SORT_CAP", "5")
+    ov(sort_capacity=5)
     got, want = run_both(ctx, synth.config2(catalog, n_pods=2500, seed=11))
     check_same(got, want)
     assert len(got["nodeclaims"]) > 5
@@ -157,9 +157,9 @@ def test_filter_plan_pod_rows(ctx, catalog):
         np.testing.assert_array_equal(cheapest[qi][want_k], want_c[want_k])
 
 
-def test_feasibility_lds_staged_equals_global(ctx, catalog, monkeypatch):
+def test_feasibility_lds_staged_equals_global(ctx, catalog, ov):
     """The bitset kernels (feasibility_quad_kernel, four rows per wave, at this catalogue size; feasibility_bits_kernel,
-    KP_FEAS_ONE_ROW) == feasibility_kernel (per-type global gathers, KP_FEAS_GLOBAL) bit for bit on pairwise-distinct
+    kp_overrides.feasibility_kernel 2) == feasibility_kernel (per-type global gathers, feasibility_kernel 1) bit for bit on pairwise-distinct
     rows (the bench's roofline leg: Gt/Lt bounds, NotIn, zones, capacity types; a row count that leaves the last quad
     partial), and == the oracle on a sample of rows."""
     import kpamd
@@ -168,11 +168,8 @@ def test_feasibility_lds_staged_equals_global(ctx, catalog, monkeypatch):
     queries = synth.distinct_queries(catalog, 3001)
     cat = kpamd.Catalog(ctx, catalog)
 
-    def run(qs, **env):
-        for k in ("KP_FEAS_GLOBAL", "KP_FEAS_ONE_ROW"):
-            monkeypatch.delenv(k, raising=False)
-        for k, v in env.items():
-            monkeypatch.setenv(k, v)
+    def run(qs, kernel=0):
+        ov(feasibility_kernel=kernel)
         fp = kpamd.FilterPlan(ctx, cat, qs, cheapest=True)
         try:
             k, c, _ = fp.run(read=True)
@@ -181,11 +178,11 @@ def test_feasibility_lds_staged_equals_global(ctx, catalog, monkeypatch):
         return k, c
     try:
         k1, c1 = run(queries)
-        k2, c2 = run(queries, KP_FEAS_GLOBAL="1")
-        k3, c3 = run(queries, KP_FEAS_ONE_ROW="1")
+        k2, c2 = run(queries, 1)
+        k3, c3 = run(queries, 2)
         for nq in (1, 2, 3, 5):  # partial quads only
             ka, ca = run(queries[:nq])
-            kb, cb = run(queries[:nq], KP_FEAS_ONE_ROW="1")
+            kb, cb = run(queries[:nq], 2)
             assert (ka == kb).all() and (ka == k1[:nq]).all(), nq
             np.testing.assert_array_equal(ca, cb)
     finally:
@@ -209,16 +206,15 @@ def test_config2_burst(ctx, catalog, n_pods):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kernel_env", [{}, {"KP_FEAS_ONE_ROW": "1"}, {"KP_FEAS_GLOBAL": "1"}])
-def test_filter_compact_equals_expanded(ctx, catalog, monkeypatch, kernel_env):
+@pytest.mark.parametrize("kernel", [0, 2, 1])
+def test_filter_compact_equals_expanded(ctx, catalog, ov, kernel):
     """KP_FILTER_COMPACT (ABI v11): the mask and each row's compatible offering classes; min over those classes of
     kp_filter_class_prices equals kp_filter_run's cheapest-price rows bit for bit, on every kernel (quad, one-row,
     per-type), including after an ICE refresh (R:pkg/providers/instance/filter/filter.go:39-64)."""
     import copy
     import kpamd
     from kpamd import synth
-    for k, v in kernel_env.items():
-        monkeypatch.setenv(k, v)
+    ov(feasibility_kernel=kernel)
     queries = synth.distinct_queries(catalog, 1001)
     its = copy.deepcopy(catalog)
     cat = kpamd.Catalog(ctx, its, seqnum=1)
@@ -229,9 +225,11 @@ def test_filter_compact_equals_expanded(ctx, catalog, monkeypatch, kernel_env):
         k2, cls, _ = fc.run_compact(read=True)
         assert (k1 == k2).all()
         c2 = kpamd.FilterPlan.cheapest_from_compact(cls, fc.class_prices())
-        np.testing.assert_array_equal(c1[k1], c2[k1])
+        np.testing.assert_array_equal(c1, c2)  # every type, its mask bit set or not (kp_abi.h)
         if step == 0:  # ICE marks: both plans refreshed in place
             cat.update_offerings([(t, "spot", "test-zone-1a", False) for t in range(0, len(catalog), 3)], seqnum=2)
+            with pytest.raises(kpamd.KPError):  # the class prices of a stale plan are refused until the refresh
+                fc.class_prices()
             fe.refresh(cat)
             fc.refresh(cat)
     with pytest.raises(kpamd.KPError):

@@ -131,10 +131,11 @@ def _canon(res):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cfg", ["2", "5"])
-def test_prepare_sharded_table_two_ranks(ctx2, catalog, cfg, monkeypatch):
+def test_prepare_sharded_table_two_ranks(ctx2, catalog, cfg):
     import kpamd
     from kpamd import synth
-    monkeypatch.setenv("KP_TFEAS_SHARD_MIN", "0")  # shard every table (read when the communicator is created)
+    for c in ctx2:  # shard every table (read when the communicator is created)
+        c.set_overrides(table_shard_min=1)
     prob = synth.config2(catalog, n_pods=3000, seed=2) if cfg == "2" else synth.config5(catalog, n_pods=4000)
     ag = kpamd.ThreadAllGather(2)
     comms = [kpamd.Comm.host(ctx2[r], 2, r, ag) for r in range(2)]
@@ -155,10 +156,11 @@ def test_prepare_sharded_table_two_ranks(ctx2, catalog, cfg, monkeypatch):
 
 
 @pytest.mark.gpu
-def test_prepare_mismatched_batches_fail_together(ctx2, catalog, monkeypatch):
+def test_prepare_mismatched_batches_fail_together(ctx2, catalog):
     import kpamd
     from kpamd import synth
-    monkeypatch.setenv("KP_TFEAS_SHARD_MIN", "0")
+    for c in ctx2:
+        c.set_overrides(table_shard_min=1)
     probs = [synth.config5(catalog, n_pods=500), synth.config2(catalog, n_pods=500, seed=2)]
     ag = kpamd.ThreadAllGather(2)
     comms = [kpamd.Comm.host(ctx2[r], 2, r, ag) for r in range(2)]

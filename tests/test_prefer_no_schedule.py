@@ -169,16 +169,50 @@ def test_prefer_no_schedule_with_spread(request, catalog, backend):
     assert sum(1 for p in res["placement"] if p != -1) >= 3
 
 
-def test_host_compile_adds_the_level(catalog):
-    """The host compile gives a shape one more relaxation level exactly when a NodePool carries a PreferNoSchedule
-    taint and the shape lacks the exact toleration."""
+@pytest.mark.parametrize("backend", BACKENDS)
+def test_relaxed_level_spread_group_with_ignore_policy(request, catalog, backend):
+    """A DoNotSchedule zone spread with the DEFAULT taint policy (Ignore). Upstream MakeTopologyNodeFilter keeps the
+    pod's tolerations under every policy and TopologyGroup.Hash hashes them, so the PreferNoSchedule level's group is a
+    new group counted from the cluster alone (Topology.Update): the in-flight placement of the unrelaxed level is not in
+    its counts. The untainted pool admits test-zone-1a only and one c5.xlarge (cpu limit): pod 2 fails its level (1a
+    holds pod 1), relaxes, and the new group lets it join pod 1's NodeClaim in 1a; with the old group (in-flight counts
+    kept) it would have gone to the tainted pool in another zone. Pods 3 and 4 then spread over 1b and 1c."""
+    from kpamd import synth
+    from kpamd.model import LabelSelector, PodShape, TopologySpread
+    pools = _pools(plain_limit_cpu=4000, plain_zone="test-zone-1a")
+    pools[0].requirements = [r for r in pools[0].requirements if r[0] != "topology.kubernetes.io/zone"]  # soft: all AZs
+    sh = PodShape(synth.req_res(1000, 512), labels={"app": "w"},
+                  topology_spread=[TopologySpread("topology.kubernetes.io/zone", 1, LabelSelector({"app": "w"}))])
+    res = _solve(request, backend, _problem(catalog, pools, [sh], [4]))
+    got = _pools_of(res, pools)
+    assert got == ["plain", "plain", "soft", "soft"], got
+    assert res["placement"][0] == res["placement"][1]
+    zones = [dict((k, v) for k, op, v, *_ in n["requirements"] if op == "In").get("topology.kubernetes.io/zone")
+             for n in res["nodeclaims"]]
+    assert sorted(tuple(z) for z in zones) == [("test-zone-1a",), ("test-zone-1b",), ("test-zone-1c",)], zones
+
+
+@pytest.mark.parametrize("backend", BACKENDS)
+def test_compile_adds_the_level(request, catalog, backend):
+    """The compile gives a shape one more relaxation level exactly when a NodePool carries a PreferNoSchedule taint and
+    the shape lacks the exact toleration: a pod that fits nowhere is popped once per level (Relax re-queues it after
+    each step), so its pops grow by one with the tainted pool, and not at all when it carries the toleration. The
+    host compile (kp_solve_validate) accepts every variant."""
     import kpamd
     from kpamd import synth
     from kpamd.model import PodShape
-    shapes = [PodShape(synth.req_res(500, 512)), PodShape(synth.req_res(500, 512), tolerations=[("", "Exists", "", PNS)])]
-    for taint in (True, False):
-        prob = _problem(catalog, _pools(soft_taint=taint), shapes, [1, 1])
-        assert kpamd.validate(prob) == 0
+    huge = synth.req_res(10_000_000, 512)  # fits no instance type
+    shapes = {"plain": PodShape(dict(huge)), "tolerating": PodShape(dict(huge), tolerations=[("", "Exists", "", PNS)])}
+    pops = {}
+    for name, sh in shapes.items():
+        for taint in (True, False):
+            prob = _problem(catalog, _pools(soft_taint=taint), [sh], [1])
+            assert kpamd.validate(prob) == 0
+            res = _solve(request, backend, prob)
+            assert list(res["placement"]) == [-1]
+            pops[name, taint] = int(res["stats"]["pops"])
+    assert pops["plain", True] == pops["plain", False] + 1, pops
+    assert pops["tolerating", True] == pops["tolerating", False], pops
 
 
 def _random(catalog, seed):

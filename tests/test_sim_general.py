@@ -113,7 +113,7 @@ def test_gpu_spread_argmin_and_disruption(ctx, catalog, general_mode):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed", range(4))
-def test_gpu_batched_simulations_counted(ctx, catalog, seed, monkeypatch):
+def test_gpu_batched_simulations_counted(ctx, catalog, seed, ov):
     """Every subset of a spread cluster runs batched (the superset Solve), and the decisions equal the per-subset
     compile's subset by subset (the oracle too): batched == single == oracle, savings included."""
     import kpamd
@@ -122,7 +122,7 @@ def test_gpu_batched_simulations_counted(ctx, catalog, seed, monkeypatch):
     subs = subsets_of(cl, seed) + [list(cl.candidates[:k]) for k in (2, 5, 9) if k <= len(cl.candidates)]
     runs = {}
     for mode in ("1", "0"):
-        monkeypatch.setenv("KP_GENERAL_BATCH", mode)
+        ov(general_batch=0 if mode == "1" else 1)
         plan = kpamd.ClusterPlan(ctx, cl)
         try:
             runs[mode] = plan.simulate(subs, multi_node=bool(seed % 2))

@@ -5,7 +5,7 @@ reads one entry per template attempt instead of re-filtering the template's type
 CPU: the row partition, and the exchange step over a world-size-2 gloo group (each rank fills its rows of a table
 with the oracle's CompatibleAvailableFilter for (NodePool requirements, pod shape) rows, pads its chunk, all-gathers;
 the reassembled table equals the one a single process computes). GPU: Solve with the table equals Solve without it
-(KP_NO_TFEAS) and the oracle, and the single-rank collective prepare equals kp_solve."""
+(kp_overrides.template_table) and the oracle, and the single-rank collective prepare equals kp_solve."""
 import os
 
 import numpy as np
@@ -96,13 +96,13 @@ def _canon(res):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cfg", ["2", "5"])
-def test_solve_with_and_without_table(ctx, catalog, cfg, monkeypatch):
+def test_solve_with_and_without_table(ctx, catalog, cfg, ov):
     import kpamd
     from kpamd import synth
     from oracle import pyoracle
     prob = synth.config2(catalog, n_pods=3000, seed=2) if cfg == "2" else synth.config5(catalog, n_pods=4000)
     with_table = kpamd.Scheduler(ctx, prob).solve()
-    monkeypatch.setenv("KP_NO_TFEAS", "1")
+    ov(template_table=1)
     without = kpamd.Scheduler(ctx, prob).solve()
     assert _canon(with_table) == _canon(without)
     if cfg == "5":

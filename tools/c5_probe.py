@@ -16,6 +16,8 @@ lib = kpamd.load_lib()
 cat = catalog.build_catalog(lib)
 prob = synth.config5(cat, n_pods=n, limit_div=div)
 ctx = kpamd.Context(0)
+import _ov  # noqa: E402  (tools only: diagnostic variables -> kp_overrides)
+_ov.apply(ctx)
 plan = kpamd.Scheduler(ctx, prob).prepare()
 out = {"pods": n, "limit_div": div, "runs": []}
 for _ in range(int(os.environ.get("REPS", "2"))):

@@ -13,6 +13,8 @@ rows = int(os.environ.get("FEAS_ROWS", "50000"))
 lib = kpamd.load_lib()
 cat = catalog.build_catalog(lib)
 ctx = kpamd.Context(0)
+import _ov  # noqa: E402  (tools only: diagnostic variables -> kp_overrides)
+_ov.apply(ctx)
 ch = kpamd.Catalog(ctx, cat)
 qs = synth.distinct_queries(cat, rows)
 out = {}
@@ -24,6 +26,7 @@ for spec in sys.argv[1:] or ["lds"]:
     for kv in filter(None, envs.split(",")):
         k, _, v = kv.partition("=")
         os.environ[k] = v
+    _ov.apply(ctx)
     for cheapest in ((True,) if os.environ.get("FEAS_CHEAPEST_ONLY") else (True, False)):
         fp = kpamd.FilterPlan(ctx, ch, qs, cheapest=cheapest)
         fp.run()

@@ -23,6 +23,8 @@ def main():
     lib = kpamd.load_lib()
     cat = kc.build_catalog(lib)
     ctx = kpamd.Context(0)
+    import _ov  # noqa: E402  (tools only: diagnostic variables -> kp_overrides)
+    _ov.apply(ctx)
     t0 = time.perf_counter()
     cl = synth.spread_cluster(cat, n_nodes)
     gen_s = time.perf_counter() - t0

@@ -17,6 +17,8 @@ cat = catalog.build_catalog(lib)
 prob = {"2": lambda: synth.config2(cat, n_pods=n, seed=2), "2b": lambda: synth.config2(cat, n_pods=n, seed=2, burst=True), "3": lambda: synth.config3(cat, n_pods=n, n_deployments=int(os.environ.get("KP_C3_DEPLOYMENTS", "1000"))),
         "5": lambda: synth.config5(cat, n_pods=n)}[cfg]()
 ctx = kpamd.Context(0)
+import _ov  # noqa: E402  (tools only: diagnostic variables -> kp_overrides)
+_ov.apply(ctx)
 sched = kpamd.Scheduler(ctx, prob)
 sched.solve(read=False)
 r = sched.solve(read=True)
