@@ -600,6 +600,14 @@ def _traffic(leg):
     return None
 
 
+def _traffic_per_sim(leg):
+    p = os.path.join(REPO, "profiles", "traffic.json")
+    try:
+        return json.load(open(p)).get(leg, {}).get("hbm_bytes_per_sim")
+    except Exception:
+        return None
+
+
 def _sim_roofline(kernel, leg, st, n_sims, note):
     """Consolidation legs (SURVEY §8d "Consolidation sim": unit = one subset simulation, B = the bytes its Solve reads
     and writes, counted inside the kernel by the same model as the Solve's): in-kernel algorithmic bytes over the
@@ -609,11 +617,17 @@ def _sim_roofline(kernel, leg, st, n_sims, note):
     b = float(st["bytes_algorithmic"])
     if ms <= 0 or n_sims <= 0:
         return None
+    launches = int(st["phase_cycles"][2]) if leg == "general" else 1  # general path: batched launches of this run
+    launches = max(1, launches)
     ach = b / (ms / 1e3) / 1e9
+    tps = _traffic_per_sim(leg)
     return {"bound": "hbm", "kernel": kernel, "achieved": round(ach, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(ach / HBM_PEAK_GBS, 6), "traffic": _traffic(leg), "traffic_leg": f"tools/prof_leg.py {leg}",
-            "algorithmic_bytes": int(b), "algorithmic_bytes_per_sim": round(b / n_sims, 1),
-            "kernel_ms": round(ms, 3), "sims": n_sims, "note": note}
+            "frac": round(ach / HBM_PEAK_GBS, 6),
+            # per launch of this run: the profiled leg's HBM bytes per simulation x this run's simulations per launch
+            "traffic": None if tps is None else int(tps * n_sims / launches),
+            "traffic_per_sim": tps, "traffic_leg": f"tools/prof_leg.py {leg}",
+            "algorithmic_bytes_per_launch": int(b / launches), "algorithmic_bytes_per_sim": round(b / n_sims, 1),
+            "launches": launches, "kernel_ms_per_launch": round(ms / launches, 3), "sims": n_sims, "note": note}
 
 
 def _cpu_baseline(cat, n_pods):

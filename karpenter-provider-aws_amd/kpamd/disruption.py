@@ -15,12 +15,73 @@ CS3 and R:website/content/en/preview/concepts/disruption.md:89-128):
                                             RCCL all-gather of the ranks' records inside libkp)
   local_choice(...)                         a rank's kp_choice record from per-subset results on the host
                                             (what the device argmax produces; CPU tests and other transports)
+  Emptiness.compute_command                 the candidates without reschedulable pods, deleted in one command
+  candidate_order(cluster)                  the consolidatable nodes in disruption-cost order (ReschedulingCost of
+                                            default-priority pods = their count; ties by node name)
+  Controller.compute_command(cluster, plan) one disruption pass over the methods the e2e consolidation suite
+                                            exercises, in upstream order (Emptiness, MultiNodeConsolidation,
+                                            SingleNodeConsolidation): the first method that returns a command wins
 
 Decisions are kp_decision values: 0 no-op, 1 delete, 2 replace.
 """
 import numpy as np
 
 NOOP, DELETE, REPLACE = 0, 1, 2
+
+
+class Command:
+    """A disruption command: the method that produced it, its candidates (cluster node indices, candidate order), the
+    decision (DELETE / REPLACE) and the computeConsolidation result (savings, replacement NodePool and price, ...)."""
+
+    def __init__(self, method, candidates, decision, result=None):
+        self.method = method
+        self.candidates = list(candidates)
+        self.decision = decision
+        self.result = result or {}
+
+    def __repr__(self):
+        return f"Command({self.method}, {self.candidates}, {('noop', 'delete', 'replace')[self.decision]})"
+
+
+def candidate_order(cluster, nodes=None):
+    """Consolidation candidates in disruption-cost order (R:website/content/en/preview/concepts/disruption.md:101-103:
+    the candidates that are cheapest to disrupt first). Every pod here has the default priority and deletion cost, so
+    ReschedulingCost is the pod count; nodes marked for deletion are never candidates; ties go by node name (upstream
+    sorts a slice built from a map: parity unpinned)."""
+    idx = [i for i in (range(len(cluster.nodes)) if nodes is None else nodes) if not cluster.nodes[i].deleting]
+    return sorted(idx, key=lambda i: (len(cluster.nodes[i].pods), cluster.nodes[i].node.name))
+
+
+class Emptiness:
+    """Emptiness (WhenEmptyOrUnderutilized with consolidateAfter elapsed): every candidate node without reschedulable
+    pods is deleted, all in one command (disruption budgets are not modelled: 100 %)."""
+
+    def compute_command(self, cluster, candidates):
+        empty = [c for c in candidates if not cluster.nodes[c].pods]
+        return Command("emptiness", empty, DELETE, {"decision": DELETE}) if empty else None
+
+
+class Controller:
+    """One pass of the disruption controller over the consolidation methods, in upstream order: Emptiness, then
+    MultiNodeConsolidation (firstNConsolidationOption over the disruption-cost order), then SingleNodeConsolidation
+    (the first candidate whose computeConsolidation is not a no-op). plan: the resident snapshot of `cluster`
+    (ClusterPlan, or any object with the same simulate(subsets, multi_node))."""
+
+    def compute_command(self, cluster, plan):
+        cands = candidate_order(cluster)
+        cmd = Emptiness().compute_command(cluster, cands)
+        if cmd is not None:
+            return cmd
+        cands = [c for c in cands if cluster.nodes[c].pods]
+        hit = MultiNodeConsolidation(plan).first_n_option(cands)
+        if hit is not None:
+            n, r = hit
+            return Command("multi", cands[:n], r["decision"], r)
+        hit = SingleNodeConsolidation(plan).compute_command(cands)
+        if hit is not None:
+            c, r = hit
+            return Command("single", [c], r["decision"], r)
+        return None
 
 
 class SingleNodeConsolidation:

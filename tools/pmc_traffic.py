@@ -44,11 +44,20 @@ def main():
             continue
         nf, f_kb = per_launch(ff, "FETCH_SIZE", pat)
         nw, w_kb = per_launch(wf, "WRITE_SIZE", pat)
+        sims = None  # the simulations the profiled run made (consolidation legs: tools/prof_leg.py's JSON line)
+        try:
+            line = [l for l in open(os.path.join(root, f"{leg}_fetch.log")) if l.startswith("{")][-1]
+            sims = json.loads(line).get("subsets")
+        except (OSError, IndexError, ValueError):
+            pass
         out[leg] = {"kernel": kernel, "kernel_name_match": pat, "launches": [nf, nw],
                     "fetch_size_kb": round(f_kb, 2), "write_size_kb": round(w_kb, 2),
                     "hbm_bytes_per_launch": int(round((2 * f_kb + w_kb) * 1024)),
                     "correction": "2 x FETCH_SIZE + WRITE_SIZE (kB = 1024 B), MI355X_MICROARCH.md HBM section",
                     "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate runs of tools/prof_leg.py {leg}"}
+        if sims:
+            out[leg]["sims"] = sims
+            out[leg]["hbm_bytes_per_sim"] = round((2 * f_kb + w_kb) * 1024 * nf / sims, 1)
     s = json.dumps(out, indent=1)
     if len(sys.argv) > 2:
         open(sys.argv[2], "w").write(s + "\n")
