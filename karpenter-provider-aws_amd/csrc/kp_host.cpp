@@ -2988,6 +2988,7 @@ int32_t CompileSolve(const kp_solve_in* in, Compiled& cp, kp_ctx* cache = nullpt
   }
   Compiled fresh;
   fresh.track_nodes = cp.track_nodes;
+  fresh.ov = cp.ov;
   rc = BuildBase(in, raw, *fresh.B);
   if (rc) return rc;
   fresh.B->ident = ident;

@@ -36,7 +36,8 @@
 #if !defined(KP_DIAG_BUILD) &&                                                                                       \
     (defined(FASTLANE) || defined(FL_NOTIME) || defined(FT_FINE) || defined(FAST_SCAN_MAX) ||                        \
      defined(FAST_CHK_LIVE) || defined(FAST_EX_ROUNDS) || defined(FAST_CONT) || defined(SORT_DIAG) || defined(EX_DIAG) || defined(FEAS_MAX_BLOCKS) ||                 \
-     defined(FEASQ_EW) || defined(FEASQ_ROWS) || defined(FEASQ_B128) || defined(FEASQ_SKIP_EVAL) || defined(FL_SKIP))
+     defined(FEASQ_EW) || defined(FEASQ_ROWS) || defined(FEASQ_B128) || defined(FEASQ_SKIP_EVAL) || defined(FL_SKIP) ||  \
+     defined(SIM_WPE))
 #error "a measurement knob is set outside a tools/ variant build (tools/kp_diag.h)"
 #endif
 #ifndef KP_DIAG_BUILD

@@ -256,8 +256,16 @@ __global__ __launch_bounds__(SIM_WAVES * 64) void sim_prep_kernel(SimArgs a) {
 // ------------------------------------------------------------------------------------------------
 // sim_kernel: one wave per simulation
 // ------------------------------------------------------------------------------------------------
+#ifndef SIM_WPE
+#define SIM_WPE 0  // waves per SIMD the register allocation targets (0: the compiler's choice; tools/kp_diag.h)
+#endif
+#if SIM_WPE
+#define SIM_OCCUPANCY __attribute__((amdgpu_waves_per_eu(SIM_WPE, SIM_WPE)))
+#else
+#define SIM_OCCUPANCY
+#endif
 template <int NW>
-__global__ __launch_bounds__(NW * 64) void sim_kernel(SimArgs a) {
+__global__ __launch_bounds__(NW * 64) SIM_OCCUPANCY void sim_kernel(SimArgs a) {
   __shared__ DevDict D;
   __shared__ WaveSlots slots[NW];
   __shared__ KReqs s_B[NW];
