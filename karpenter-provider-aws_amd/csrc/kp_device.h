@@ -100,6 +100,7 @@ struct SolveArgs {
   int32_t* nc_cat;                   // [P] catalogue of the NodeClaim's template
   uint32_t req_res_mask;             // resources some pod shape requests (> 0)
   int32_t timing;                    // 1: thread 0 accumulates per-phase s_memtime deltas into stats[8..15]
+  int32_t stop_nc;                   // > 0 (consolidation simulations): end the Solve once this many NodeClaims exist
   const int32_t* cancel;             // kp_cancel flag (host-mapped, polled every ~1024 pops), NULL: none
   int32_t cont;                      // 1: the fast lane variant with the continuation round (queue runs of one shape)
   // topology spread (upstream Topology, TopologyTypeSpread groups). A group on a dictionary key keeps a

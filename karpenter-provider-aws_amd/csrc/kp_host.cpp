@@ -5994,6 +5994,7 @@ static int32_t GeneralBatchRun(kp_cluster_plan* plan, GeneralBatch& gb, const ve
       SolveArgs& a = sargs[j];
       BindSolve(a, C, o, sh, ar, (int)queues[j].size(), Pc, gb.rmask, gb.res_mode);
       a.cancel = dcancel;
+      a.stop_nc = 2;  // a second NodeClaim decides the simulation (no-op): the kernel ends its Solve there
       if (gb.tfeas_on) {
         a.tfeas = (const uint64_t*)(sh + o.tfeas);
         a.tfeas_words = gb.tf_words;

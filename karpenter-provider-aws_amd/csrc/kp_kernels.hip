@@ -3258,6 +3258,10 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a0, const Solv
   __syncthreads();
 
   for (;;) {
+    // a consolidation simulation (general path) whose Solve has made stop_nc (2) NodeClaims: computeConsolidation's
+    // decision is already a no-op ("len(NewNodeClaims) != 1"; NodeClaims are never removed), so the rest of the Solve
+    // cannot change it (uniform: s_ctl[2] was written before the previous iteration's barrier)
+    if (BATCH && a.stop_nc > 0 && s_ctl[2] >= a.stop_nc) break;
     // ---- fast lane: wave 0 alone places every pod whose placement needs no requirement merge ----------------
     // The pod owns/feeds no topology group, every existing node is known to fail it (first-fit cursor), and the
     // first in-flight NodeClaim (sort order) that passes the pre-checks already carries the pod's shape-level

@@ -32,6 +32,9 @@ def main():
     lib = kpamd.load_lib()
     cat = catalog.build_catalog(lib)
     ctx = kpamd.Context(0)
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import _ov  # (tools only: KP_HOST_TIMING=1 etc. -> kp_overrides)
+    _ov.apply(ctx)
     out = {"leg": leg}
     if leg == "solve2":
         sched = kpamd.Scheduler(ctx, synth.config2(cat, n_pods=50_000, seed=2))
@@ -69,7 +72,8 @@ def main():
         cands = np.asarray(cl.candidates, dtype=np.uint32)
         mids = disruption.MultiNodeConsolidation.search_prefixes(len(cands))
         subs = [list(cands[:m + 1]) for m in mids]
-        subs += synth.consolidation_subsets(cl, 8192 - len(mids), seed=6, max_size=100, prefixes=False)
+        n_sub = int(os.environ.get("GEN_SUBSETS", "8192"))
+        subs += synth.consolidation_subsets(cl, n_sub - len(mids), seed=6, max_size=100, prefixes=False)
         offs = np.zeros(len(subs) + 1, dtype=np.uint32)
         offs[1:] = np.cumsum([len(x) for x in subs])
         flat = np.concatenate([np.asarray(x, dtype=np.uint32) for x in subs])
