@@ -63,6 +63,11 @@ struct SolveArgs {
   // existing nodes (upstream order)
   int32_t n_existing;
   uint8_t* ex_reqs;                  // [E] KReqs (mutable)
+  // batched simulations: the existing nodes' requirements copy-on-write. ex_reqs_ro = the pristine [E] KReqs (shared by
+  // every simulation), ex_own = [ceil(E/64)] bits, set once the simulation wrote its own copy into ex_reqs (store_merged
+  // writes a complete set: no copy first). ex_reqs_ro null: ex_reqs is complete (single Solves restore it per run).
+  const uint8_t* ex_reqs_ro;
+  uint64_t* ex_own;
   const int32_t* ex_taintset;        // [E]
   const int64_t* ex_available;       // [E][NRES]
   int64_t* ex_requests;              // [E][NRES] (mutable)
@@ -230,7 +235,7 @@ struct BatchInitArgs {
   uint8_t* base;
   size_t stride;
   const uint8_t* pristine;
-  size_t dst_off, n_copy;
+  size_t dst_off, n_copy;  // [dst_off, dst_off + n_copy) of every arena from pristine
   int32_t n_fill;
   uint32_t fill_byte[BATCH_INIT_FILLS];
   size_t fill_off[BATCH_INIT_FILLS], fill_len[BATCH_INIT_FILLS];

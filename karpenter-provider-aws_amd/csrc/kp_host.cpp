@@ -26,6 +26,7 @@
 #include <stdexcept>
 #include <string>
 #include <string_view>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -3084,7 +3085,7 @@ struct SolveOffs {
          pod_level = 0, lastlen = 0, lastlen_ep = 0, trem = 0, exr = 0, exrq = 0, exroom = 0, exhp = 0, mut_end = 0;
   size_t pristine = 0, ncr = 0, ncX = 0, ncrq = 0, nct = 0, npods = 0, order = 0, chkblk = 0, maxalloc = 0, fitj = 0,
          nchead = 0, nccat = 0, nchp = 0, place = 0, events = 0, stats = 0, ver0 = 0, exver = 0, tver = 0, curnc = 0,
-         curex = 0, held = 0, ver_end = 0, fail0 = 0, ncfail = 0, exfail = 0, tfail = 0, chkdead = 0, fail_end = 0,
+         curex = 0, held = 0, exown = 0, ver_end = 0, fail0 = 0, ncfail = 0, exfail = 0, tfail = 0, chkdead = 0, fail_end = 0,
          opts = 0, nrem = 0, nopt = 0, hcnc = 0, nctc = 0, txl = 0, txlv = 0, slfail = 0, arena_end = 0;
   size_t n_hcnc = 0;
   int ncc = 0, chk_dead_rows = 0, sort_cap = 0, opt_stride = 0;
@@ -3168,7 +3169,6 @@ void PutArena(Blob& blob, const Compiled& C, const vector<int32_t>& pod_shape, c
   o.lastlen = blob.put(zeros_p);
   o.lastlen_ep = blob.put(zeros_p);
   o.trem = blob.put(C.tmpl_remaining);
-  o.exr = blob.put(C.ex_reqs);
   o.exrq = blob.put(C.ex_requests);
   // headroom rows of the existing nodes for the first four requested resources (req_res_mask order)
   vector<int64_t> ex_room((size_t)4 * std::max(E, 1), INT64_MAX);
@@ -3180,6 +3180,8 @@ void PutArena(Blob& blob, const Compiled& C, const vector<int32_t>& pod_shape, c
   }
   o.exroom = blob.put(ex_room);
   o.exhp = blob.put(C.ex_hp);
+  // last of the mutable block: a batched simulation does not copy it (copy-on-write from the pristine block, ex_own)
+  o.exr = blob.put(C.ex_reqs);
   o.mut_end = blob.host.size();
 }
 
@@ -3216,6 +3218,7 @@ void ReserveArenaDev(Blob& blob, const Compiled& C, int Pc, int opt_stride, int 
   o.curnc = blob.reserve_dev(sizeof(int32_t) * 2 * SLn);  // cursors start at {0, 0} (zeroed per run)
   o.curex = blob.reserve_dev(sizeof(int32_t) * 2 * SLn);
   o.held = blob.reserve_dev(C.B->res_cls ? sizeof(uint64_t) * (size_t)Pc : 8);
+  o.exown = blob.reserve_dev(sizeof(uint64_t) * (size_t)std::max(1, (E + 63) / 64));  // copy-on-write bits (zeroed)
   o.ver_end = blob.total();
   o.fail0 = blob.reserve_dev(0);
   o.ncfail = blob.reserve_dev(sizeof(int32_t) * SLn * o.ncc);
@@ -3272,6 +3275,8 @@ void BindSolve(SolveArgs& a, const Compiled& C, const SolveOffs& o, uint8_t* sh,
   a.tmpl_remaining = (int64_t*)(ar + o.trem);
   a.n_existing = (int32_t)C.ex_reqs.size();
   a.ex_reqs = ar + o.exr;
+  a.ex_reqs_ro = nullptr;  // (batched simulations: GeneralBatchRun points it at the pristine block)
+  a.ex_own = (uint64_t*)(ar + o.exown);
   a.ex_taintset = (const int32_t*)(sh + o.exts);
   a.ex_available = (const int64_t*)(sh + o.exav);
   a.ex_requests = (int64_t*)(ar + o.exrq);
@@ -5550,12 +5555,22 @@ struct GenSlot {
   size_t arenas_bytes = 0, args_bytes = 0;
   PinnedBuf up, down;
   hipEvent_t done = nullptr, t0 = nullptr, t1 = nullptr;  // results landed; the launch's kernels (timing)
+  hipEvent_t uploaded = nullptr;                            // the launch's overlays and arguments on the device
   int n = 0;
   size_t b0 = 0;
   vector<vector<int32_t>> queues;
   ~GenSlot() {
-    for (hipEvent_t e : {done, t0, t1})
+    for (hipEvent_t e : {done, t0, t1, uploaded})
       if (e) (void)hipEventDestroy(e);
+  }
+};
+// the batch's copy streams: uploads (the next launch's overlays) and downloads (the last launch's results) overlap the
+// kernels on the context stream instead of queueing between them
+struct CopyStreams {
+  hipStream_t up = nullptr, down = nullptr;
+  ~CopyStreams() {
+    if (up) (void)hipStreamDestroy(up);
+    if (down) (void)hipStreamDestroy(down);
   }
 };
 
@@ -5587,6 +5602,7 @@ struct GeneralBatch {
   vector<uint8_t> tmpl;
   DevBuf pristine;
   GenSlot slot[2];  // two launch slots (GeneralBatchRun)
+  CopyStreams cs;
 };
 
 // The superset Solve of a cluster (kp_cluster_plan: general). KP_E_UNSUPPORTED: the batch cannot take this cluster
@@ -5753,6 +5769,23 @@ struct GenScratch {
   vector<int32_t> inv, hdec, regdec, touched;
   vector<char> shape_seen;
 };
+// The host work of a batched launch is per simulation (the overlays before it, the decisions after it): split over up
+// to kMaxHostThreads threads, f(begin, end, thread index). Workers never call fail() (its message is thread-local).
+constexpr int kMaxHostThreads = 16;
+extern "C++" template <class F>
+static void ParallelFor(int n, F f) {
+  static const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
+  const int T = std::max(1, std::min(std::min(hw, kMaxHostThreads), n / 128));
+  if (T <= 1) {
+    f(0, n, 0);
+    return;
+  }
+  vector<std::thread> th;
+  th.reserve(T - 1);
+  for (int t = 1; t < T; t++) th.emplace_back(f, (int)((int64_t)n * t / T), (int)((int64_t)n * (t + 1) / T), t);
+  f(0, (int)((int64_t)n / T), 0);
+  for (auto& x : th) x.join();
+}
 static int GeneralPatch(const GeneralBatch& gb, const kp_cluster& cl, const vector<uint32_t>& cand, GenScratch& s,
                         vector<int32_t>& queue, uint8_t* patch) {
   const Compiled& C = *gb.C;
@@ -5871,7 +5904,7 @@ static int32_t GeneralBatchRun(kp_cluster_plan* plan, GeneralBatch& gb, const ve
     fprintf(stderr, "[kp general] arena stride %.2f MB, %zu simulations per launch, Pc %d\n", gb.stride / 1e6, per_launch, Pc);
   const int sort_cap = std::min(SortCapacity(C.ov), Pc);
   const size_t dyn = std::max<size_t>((size_t)2 * sort_cap * sizeof(int32_t), o.chk_on ? CHK_LDS_BYTES : 0);
-  GenScratch scratch;
+  vector<GenScratch> scratches(kMaxHostThreads);
   vector<SolveArgs> sargs;
   vector<FinalizeArgs> fargs;
   // per-launch result layout in the slot's pinned download buffer
@@ -5903,14 +5936,23 @@ static int32_t GeneralBatchRun(kp_cluster_plan* plan, GeneralBatch& gb, const ve
     const KReqs* fin = reinterpret_cast<KReqs*>(sl.down.at(r_fin));
     const uint64_t* held = reinterpret_cast<uint64_t*>(sl.down.at(r_held));
     const vector<vector<int32_t>>& queues = sl.queues;
-    for (int j = 0; j < n; j++) {
+    std::atomic<int> bad_runaway{-1}, cancelled{0};
+    uint64_t tcount[kMaxHostThreads][3] = {};
+    ParallelFor(n, [&](int j_lo, int j_hi, int t) {
+    for (int j = j_lo; j < j_hi; j++) {
       const int i = order[b0 + j];
       const uint64_t* sj = &stats[(size_t)j * KP_SOLVE_STATS];
-      if (sj[7]) return fail(KP_E_DEVICE, "solve_kernel exceeded its Queue.Pop bound in simulation %d: aborted", i);
-      if (sj[46]) return fail(KP_E_CANCELED, "consolidation simulations cancelled (kp_cancel_set)");
-      counters[0] += sj[0];
-      counters[1] += sj[1];
-      counters[2] += sj[2];
+      if (sj[7]) {
+        bad_runaway = i;
+        return;
+      }
+      if (sj[46]) {
+        cancelled = 1;
+        return;
+      }
+      tcount[t][0] += sj[0];
+      tcount[t][1] += sj[1];
+      tcount[t][2] += sj[2];
       const int n_nc = (int)sj[3];
       const vector<int32_t>& q = queues[j];
       SimOut& r = outs[i];
@@ -5935,6 +5977,12 @@ static int32_t GeneralBatchRun(kp_cluster_plan* plan, GeneralBatch& gb, const ve
       GeneralDecide(cl, labels, cands[i], *C.B, all, n_nc, &R, ci, np, &opts[(size_t)j * gb.opt_stride],
                     n_nc == 1 ? nopt[j] : 0, multi_node, r, &gb.offers, &gb.cands);
     }
+    });
+    for (int t = 0; t < kMaxHostThreads; t++)
+      for (int k = 0; k < 3; k++) counters[k] += tcount[t][k];
+    if (bad_runaway >= 0)
+      return fail(KP_E_DEVICE, "solve_kernel exceeded its Queue.Pop bound in simulation %d: aborted", bad_runaway.load());
+    if (cancelled) return fail(KP_E_CANCELED, "consolidation simulations cancelled (kp_cancel_set)");
     host_ms[1] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th1).count();
     return KP_OK;
   };
@@ -5943,9 +5991,22 @@ static int32_t GeneralBatchRun(kp_cluster_plan* plan, GeneralBatch& gb, const ve
   for (int k = 0; k < 2; k++)
     if (!slots[k].done) {
       HIPCHK(hipEventCreateWithFlags(&slots[k].done, hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&slots[k].uploaded, hipEventDisableTiming));
       HIPCHK(hipEventCreate(&slots[k].t0));
       HIPCHK(hipEventCreate(&slots[k].t1));
     }
+  if (!gb.cs.up) {
+    HIPCHK(hipStreamCreateWithFlags(&gb.cs.up, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&gb.cs.down, hipStreamNonBlocking));
+  }
+  hipStream_t up = gb.cs.up, dn = gb.cs.down;
+  struct DrainCopies {  // (early returns: nothing left in flight on the copy streams either)
+    hipStream_t u, d;
+    ~DrainCopies() {
+      (void)hipStreamSynchronize(u);
+      (void)hipStreamSynchronize(d);
+    }
+  } drain_copies{up, dn};
   int pending = -1;  // the slot whose launch is in flight and not yet decided
   int launch_no = 0;
   for (size_t b0 = 0; b0 < idx.size(); b0 += per_launch, launch_no++) {
@@ -5986,15 +6047,20 @@ static int32_t GeneralBatchRun(kp_cluster_plan* plan, GeneralBatch& gb, const ve
     vector<vector<int32_t>>& queues = sl.queues;
     sargs.resize(n);
     fargs.resize(n);
-    for (int j = 0; j < n; j++) {
+    std::atomic<int> unbatchable{-1};
+    ParallelFor(n, [&](int j_lo, int j_hi, int t) {
+    for (int j = j_lo; j < j_hi; j++) {
       const int i = order[b0 + j];
-      if (GeneralPatch(gb, cl, cands[i], scratch, queues[j], patches + patch_bytes * j))
-        return fail(KP_E_INVAL, "subset %d: not batchable after the check", i);
+      if (GeneralPatch(gb, cl, cands[i], scratches[t], queues[j], patches + patch_bytes * j)) {
+        unbatchable = i;
+        return;
+      }
       uint8_t* ar = arenas + gb.stride * j;
       SolveArgs& a = sargs[j];
       BindSolve(a, C, o, sh, ar, (int)queues[j].size(), Pc, gb.rmask, gb.res_mode);
       a.cancel = dcancel;
       a.stop_nc = 2;  // a second NodeClaim decides the simulation (no-op): the kernel ends its Solve there
+      a.ex_reqs_ro = (const uint8_t*)gb.pristine.p + (o.exr - o.common);  // (the arena's copy is written on demand)
       if (gb.tfeas_on) {
         a.tfeas = (const uint64_t*)(sh + o.tfeas);
         a.tfeas_words = gb.tf_words;
@@ -6016,6 +6082,8 @@ static int32_t GeneralBatchRun(kp_cluster_plan* plan, GeneralBatch& gb, const ve
       f.nc_held = a.res_mode ? a.nc_held : nullptr;
       f.solve_stats = a.stats;
     }
+    });
+    if (unbatchable >= 0) return fail(KP_E_INVAL, "subset %d: not batchable after the check", unbatchable.load());
     memcpy(reinterpret_cast<uint8_t*>(sl.up.at(u_args)), sargs.data(), sizeof(SolveArgs) * n);
     memcpy(reinterpret_cast<uint8_t*>(sl.up.at(u_fargs)), fargs.data(), sizeof(FinalizeArgs) * n);
     SolveArgs* dargs = (SolveArgs*)sl.args.p;
@@ -6026,7 +6094,7 @@ static int32_t GeneralBatchRun(kp_cluster_plan* plan, GeneralBatch& gb, const ve
     bi.stride = gb.stride;
     bi.pristine = (const uint8_t*)gb.pristine.p;
     bi.dst_off = o.common;
-    bi.n_copy = (o.mut_end - o.common + 15) & ~(size_t)15;
+    bi.n_copy = (o.exr - o.common + 15) & ~(size_t)15;  // not the existing nodes' requirements: copy-on-write
     auto fill = [&](size_t off, size_t len, uint32_t byte) {
       bi.fill_off[bi.n_fill] = off;
       bi.fill_len[bi.n_fill] = (len + 15) & ~(size_t)15;
@@ -6040,16 +6108,23 @@ static int32_t GeneralBatchRun(kp_cluster_plan* plan, GeneralBatch& gb, const ve
     fill(o.fail0, o.fail_end - o.fail0, 0xFF);
     if (o.n_hcnc) fill(o.hcnc, o.n_hcnc, 0);
     host_ms[0] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count();
+    // uploads on their own stream (they overlap the previous launch's kernels; this slot's arenas and buffers were
+    // last used by the launch before that one, whose results decide() has already waited for); batch_init writes
+    // [common, mut_end) of the arenas, the overlays [0, common)
+    HIPCHK(hipMemcpy2DAsync(arenas, gb.stride, patches, patch_bytes, patch_bytes, n, hipMemcpyHostToDevice, up));
+    HIPCHK(hipMemcpyAsync(dargs, reinterpret_cast<uint8_t*>(sl.up.at(u_args)), sizeof(SolveArgs) * n, hipMemcpyHostToDevice, up));
+    HIPCHK(hipMemcpyAsync(dfargs, reinterpret_cast<uint8_t*>(sl.up.at(u_fargs)), sizeof(FinalizeArgs) * n, hipMemcpyHostToDevice, up));
+    HIPCHK(hipEventRecord(sl.uploaded, up));
     HIPCHK(launch_batch_init(bi, n, st));
-    HIPCHK(hipMemcpy2DAsync(arenas, gb.stride, patches, patch_bytes, patch_bytes, n, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(dargs, reinterpret_cast<uint8_t*>(sl.up.at(u_args)), sizeof(SolveArgs) * n, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(dfargs, reinterpret_cast<uint8_t*>(sl.up.at(u_fargs)), sizeof(FinalizeArgs) * n, hipMemcpyHostToDevice, st));
+    HIPCHK(hipStreamWaitEvent(st, sl.uploaded, 0));
     HIPCHK(hipEventRecord(sl.t0, st));
     HIPCHK(launch_solve_batch(sargs[0], dargs, n, dyn, st));
     HIPCHK(launch_finalize_batch(fargs[0], dfargs, n, st));
     HIPCHK(hipEventRecord(sl.t1, st));
+    // downloads on their own stream once the kernels are done (the next launch's kernels need not wait for them)
+    HIPCHK(hipStreamWaitEvent(dn, sl.t1, 0));
     auto down = [&](size_t roff, size_t off, size_t width) {
-      return hipMemcpy2DAsync(reinterpret_cast<uint8_t*>(sl.down.at(roff)), width, arenas + off, gb.stride, width, n, hipMemcpyDeviceToHost, st);
+      return hipMemcpy2DAsync(reinterpret_cast<uint8_t*>(sl.down.at(roff)), width, arenas + off, gb.stride, width, n, hipMemcpyDeviceToHost, dn);
     };
     HIPCHK(down(r_stats, o.stats, sizeof(uint64_t) * KP_SOLVE_STATS));
     HIPCHK(down(r_place, o.place, sizeof(int32_t) * Pc));
@@ -6058,7 +6133,7 @@ static int32_t GeneralBatchRun(kp_cluster_plan* plan, GeneralBatch& gb, const ve
     HIPCHK(down(r_opts, o.opts, sizeof(uint32_t) * gb.opt_stride));
     HIPCHK(down(r_fin, o.ncr, sizeof(KReqs)));
     if (gb.res_mode) HIPCHK(down(r_held, o.held, sizeof(uint64_t)));
-    HIPCHK(hipEventRecord(sl.done, st));
+    HIPCHK(hipEventRecord(sl.done, dn));
     sl.n = n;
     sl.b0 = b0;
     // the previous launch's decisions while this one runs

@@ -931,6 +931,13 @@ __device__ __forceinline__ const KReqs* kreq_at(const uint8_t* base, size_t i) {
   return reinterpret_cast<const KReqs*>(base + i * sizeof(KReqs));
 }
 
+// An existing node's requirements to read: a batched simulation's own copy once it wrote one, else the pristine set
+// shared by every simulation (ro null: rw is complete)
+__device__ __forceinline__ const KReqs* ex_req_src(const uint8_t* rw, const uint8_t* ro, const uint64_t* own, int ei) {
+  if (ro && !((own[ei >> 6] >> (ei & 63)) & 1)) return reinterpret_cast<const KReqs*>(ro + (size_t)ei * sizeof(KReqs));
+  return reinterpret_cast<const KReqs*>(rw + (size_t)ei * sizeof(KReqs));
+}
+
 __device__ __forceinline__ void store_merged(KReqs* dst, const ReqView& rv, uint64_t m_v, int W, int KB) {
   const int lane = LANE;
   if (lane < W) dst->vals[lane] = m_v;
@@ -2497,11 +2504,12 @@ if (!FL_NOTIME && tmg) {                                    \
               b_staged = true;
             }
             KReqs* er = reinterpret_cast<KReqs*>(KA(ex_reqs) + (size_t)ei * sizeof(KReqs));
+            const KReqs* er_src = ex_req_src(KA(ex_reqs), KA(ex_reqs_ro), KA(ex_own), ei);
             bytes += sizeof(KReqs);
             // a pod without requirements at this level: Compatible holds and Add leaves the node's requirements as
             // they are (nothing to intersect), so neither the merge nor its store is needed
             if (!ex_triv) {
-              const CandReq crx = load_cand(D, er);
+              const CandReq crx = load_cand(D, er_src);
               uint64_t m_v = 0;
               ReqView rv;
               const uint64_t b_negop = KA(shape_negop)[sl];
@@ -2513,6 +2521,7 @@ if (!FL_NOTIME && tmg) {                                    \
               }
               // commit: ExistingNode.Add (requirements, requests, headroom rows, version), Topology.Record
               store_merged(er, rv, m_v, D.W, D.KB);
+              if (KA(ex_reqs_ro)) KA(ex_own)[ei >> 6] |= 1ull << (ei & 63);  // (uniform: every lane stores the same)
             }
             {  // requests + pod, the headroom rows of the first four requested resources - pod, version + 1: every
                // lane reads and stores (the lanes past the rows repeat the last row's value), no exec-masked block
@@ -3475,7 +3484,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a0, const Solv
         if (li < n) {
           ei = s_list[li];
           attempts++;
-          const KReqs* er = kreq_at(a.ex_reqs, ei);
+          const KReqs* er = ex_req_src(a.ex_reqs, a.ex_reqs_ro, a.ex_own, ei);
           ok = merge_compatible(D, er, B, b_negop, false, m_v, rv, &slots[wave], vi);
           bytes += sizeof(KReqs);
           if (!ok && lane == 0)  // permanent unless the undefined-key rule failed (no well-known exemption here)
@@ -3488,6 +3497,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a0, const Solv
         if (win >= 0) {
           if (wave == win) {
             store_merged(reinterpret_cast<KReqs*>(a.ex_reqs + (size_t)ei * sizeof(KReqs)), rv, m_v, D.W, D.KB);
+            if (a.ex_reqs_ro && lane == 0) a.ex_own[ei >> 6] |= 1ull << (ei & 63);
             if (lane < KP_NRES) a.ex_requests[(size_t)ei * KP_NRES + lane] += s_preq[lane];
             if (lane < 4) {  // headroom rows of the first four requested resources
               const int64_t d = lane == 0 ? ep0 : lane == 1 ? ep1 : lane == 2 ? ep2 : ep3;
@@ -4010,7 +4020,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a0, const Solv
       const int rb = a.shape_rec_base[shape];
       const bool ex = placed <= -2;
       const int idx = ex ? -2 - placed : placed;
-      const KReqs* fin = ex ? kreq_at(a.ex_reqs, idx) : kreq_at(a.nc_reqs, idx);
+      const KReqs* fin = ex ? ex_req_src(a.ex_reqs, a.ex_reqs_ro, a.ex_own, idx) : kreq_at(a.nc_reqs, idx);
       const int ts = ex ? a.ex_taintset[idx] : a.nc_head[idx].taintset;
       for (int i0 = 0; i0 < rn; i0 += 64) {
         const int i = i0 + lane;
