@@ -68,6 +68,14 @@ struct SolveArgs {
   // writes a complete set: no copy first). ex_reqs_ro null: ex_reqs is complete (single Solves restore it per run).
   const uint8_t* ex_reqs_ro;
   uint64_t* ex_own;
+  // batched simulations: per shape-level the existing positions that can ever pass its count-independent checks
+  // (headroom, taints, static check, host ports on the superset's pristine state; nodes only fill up and a simulation
+  // only excludes nodes), ascending: ex_ulist[ex_ulist_off[sl] .. ex_ulist_off[sl + 1]), and ex_uidx[sl][e] = the first
+  // list index whose position is >= e. The full path's addToExistingNode scans the list instead of every position.
+  // Null: scan every position.
+  const int32_t* ex_ulist;
+  const int32_t* ex_ulist_off;
+  const int32_t* ex_uidx;
   const int32_t* ex_taintset;        // [E]
   const int64_t* ex_available;       // [E][NRES]
   int64_t* ex_requests;              // [E][NRES] (mutable)

@@ -3077,7 +3077,8 @@ struct SolveOffs {
   size_t slb = 0, snl = 0, sreqs = 0, sneg = 0, sreq = 0, stol = 0, pvp = 0, pvpb = 0, pvps = 0, pvpn = 0, tlp = 0,
          exts = 0, exav = 0, shpc = 0, shpa = 0, tgk = 0, tgr = 0, tgs = 0, tgm = 0, tga = 0, tgtb = 0, tgft = 0,
          tgt = 0, tgtn = 0, tgnt = 0, srb = 0, srn = 0, recl = 0, recx = 0, slft = 0, slob = 0, slon = 0, owng = 0,
-         owns = 0, ownp = 0, ownr = 0, sltk = 0, tks = 0, extc = 0, tkk = 0, slsh = 0, tfeas = 0;
+         owns = 0, ownp = 0, ownr = 0, sltk = 0, tks = 0, extc = 0, tkk = 0, slsh = 0, tfeas = 0, exul = 0, exuo = 0,
+         exui = 0;
   // arena: the Solve's inputs, then its mutable state [mut, mut_end) (restored before every run; [mut, common) is the
   // part a batched simulation patches, [common, mut_end) the part every simulation starts from alike), then
   // device-only regions
@@ -4709,6 +4710,7 @@ struct kp_cluster_plan {
   CtxRef ctx;
   std::unique_ptr<OwnedCluster> general;  // set: simulations run as whole Solves (kp_solve on this device)
   double general_ms = 0;                  // device time of the last general batch (solve + finalize kernels)
+  uint64_t general_phase[8] = {};         // kp_overrides.timing: the batch's solve_kernel phase cycles, summed
   std::shared_ptr<GeneralBatch> gb;       // the general path's superset Solve (batched simulations), once built
   vector<std::map<string, string>> general_labels;
   bool gb_tried = false;
@@ -5726,6 +5728,33 @@ static int32_t GeneralBatchBuild(kp_cluster_plan* plan, std::shared_ptr<GeneralB
   // the shared region: read-only data of every simulation + the template-options table
   Blob blob;
   PutShared(blob, C, gb->so);
+  {  // per shape-level, the positions that can ever take one of its pods (DeviceArgs::ex_ulist): the kernel's
+     // count-independent checks on the pristine state
+    const int E = (int)C.ex_input.size(), SLn = (int)C.shape_reqs.size();
+    vector<int32_t> sl_shape(SLn, 0), off(SLn + 1, 0), list, uidx((size_t)SLn * std::max(E, 1), 0);
+    for (size_t s = 0; s < C.shape_level_base.size(); s++)
+      for (int l = 0; l < C.shape_nlevels[s]; l++) sl_shape[C.shape_level_base[s] + l] = (int32_t)s;
+    for (int sl = 0; sl < SLn; sl++) {
+      off[sl] = (int32_t)list.size();
+      const int s = sl_shape[sl];
+      const int64_t* pq = &C.shape_requests[(size_t)s * KP_NRES];
+      const uint64_t tol = C.shape_tolerates[sl], hpc = C.hp_any ? C.shape_hp_conf[s] : 0;
+      for (int e = 0; e < E; e++) {
+        uidx[(size_t)sl * E + e] = (int32_t)(list.size() - off[sl]);
+        bool ok = gb->ex_static[e] && ((tol >> C.ex_taintset[e]) & 1) && !(hpc && (C.ex_hp[e] & hpc));
+        for (uint32_t m = gb->rmask; m && ok; m &= m - 1) {
+          const int r = __builtin_ctz(m);
+          ok = C.ex_available[(size_t)e * KP_NRES + r] - C.ex_requests[(size_t)e * KP_NRES + r] >= pq[r];
+        }
+        if (ok) list.push_back(e);
+      }
+    }
+    off[SLn] = (int32_t)list.size();
+    if (list.empty()) list.push_back(0);
+    gb->so.exul = blob.put(list);
+    gb->so.exuo = blob.put(off);
+    gb->so.exui = blob.put(uidx);
+  }
   const size_t host_bytes = blob.host.size();
   const int NT = (int)C.B->tmpl_reqs.size(), SLi = (int)C.shape_reqs.size();
   gb->tfeas_on = NT > 0 && SLi > 0 && ctx->ov.template_table == 0;
@@ -5937,7 +5966,7 @@ static int32_t GeneralBatchRun(kp_cluster_plan* plan, GeneralBatch& gb, const ve
     const uint64_t* held = reinterpret_cast<uint64_t*>(sl.down.at(r_held));
     const vector<vector<int32_t>>& queues = sl.queues;
     std::atomic<int> bad_runaway{-1}, cancelled{0};
-    uint64_t tcount[kMaxHostThreads][3] = {};
+    uint64_t tcount[kMaxHostThreads][3] = {}, tphase[kMaxHostThreads][8] = {};
     ParallelFor(n, [&](int j_lo, int j_hi, int t) {
     for (int j = j_lo; j < j_hi; j++) {
       const int i = order[b0 + j];
@@ -5953,6 +5982,7 @@ static int32_t GeneralBatchRun(kp_cluster_plan* plan, GeneralBatch& gb, const ve
       tcount[t][0] += sj[0];
       tcount[t][1] += sj[1];
       tcount[t][2] += sj[2];
+      for (int k = 0; k < 8; k++) tphase[t][k] += sj[8 + k];  // (zero unless kp_overrides.timing)
       const int n_nc = (int)sj[3];
       const vector<int32_t>& q = queues[j];
       SimOut& r = outs[i];
@@ -5978,8 +6008,10 @@ static int32_t GeneralBatchRun(kp_cluster_plan* plan, GeneralBatch& gb, const ve
                     n_nc == 1 ? nopt[j] : 0, multi_node, r, &gb.offers, &gb.cands);
     }
     });
-    for (int t = 0; t < kMaxHostThreads; t++)
+    for (int t = 0; t < kMaxHostThreads; t++) {
       for (int k = 0; k < 3; k++) counters[k] += tcount[t][k];
+      for (int k = 0; k < 8; k++) plan->general_phase[k] += tphase[t][k];
+    }
     if (bad_runaway >= 0)
       return fail(KP_E_DEVICE, "solve_kernel exceeded its Queue.Pop bound in simulation %d: aborted", bad_runaway.load());
     if (cancelled) return fail(KP_E_CANCELED, "consolidation simulations cancelled (kp_cancel_set)");
@@ -6061,6 +6093,9 @@ static int32_t GeneralBatchRun(kp_cluster_plan* plan, GeneralBatch& gb, const ve
       a.cancel = dcancel;
       a.stop_nc = 2;  // a second NodeClaim decides the simulation (no-op): the kernel ends its Solve there
       a.ex_reqs_ro = (const uint8_t*)gb.pristine.p + (o.exr - o.common);  // (the arena's copy is written on demand)
+      a.ex_ulist = (const int32_t*)(sh + gb.so.exul);
+      a.ex_ulist_off = (const int32_t*)(sh + gb.so.exuo);
+      a.ex_uidx = (const int32_t*)(sh + gb.so.exui);
       if (gb.tfeas_on) {
         a.tfeas = (const uint64_t*)(sh + o.tfeas);
         a.tfeas_words = gb.tf_words;
@@ -6201,6 +6236,7 @@ static int32_t GeneralSimLocked(kp_cluster_plan* plan, const uint32_t* offsets, 
   vector<SimOut> outs(n_subsets);
   memset(outs.data(), 0, sizeof(SimOut) * outs.size());
   uint64_t counters[3] = {0, 0, 0}, n_launches = 0;
+  memset(plan->general_phase, 0, sizeof plan->general_phase);
   double dev_ms = 0, host_ms[2] = {0, 0};  // the batch's host work: overlays + arguments, decisions
   vector<int> batched, single;
   for (uint32_t s = 0; s < n_subsets; s++) {
@@ -6394,6 +6430,7 @@ int32_t kp_cluster_simulate_cancellable(kp_cluster_plan* plan, kp_cancel* cancel
     if (plan->general) {  // general path: simulations batched / compiled per subset, batched launches
       stats->phase_cycles[1] = kst[4];
       stats->phase_cycles[2] = kst[6];
+      for (int k = 0; k < 8; k++) stats->attempt_cycles[k] = plan->general_phase[k];  // (timing diagnostics)
     }
     stats->prepare_ms = plan->prepare_ms;
     stats->host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -6627,6 +6664,7 @@ int32_t kp_consolidate_argmin_cancellable(kp_cluster_plan* plan, kp_comm* comm, 
     if (plan->general) {  // general path: simulations batched / compiled per subset, batched launches
       stats->phase_cycles[1] = kst[4];
       stats->phase_cycles[2] = kst[6];
+      for (int k = 0; k < 8; k++) stats->attempt_cycles[k] = plan->general_phase[k];  // (timing diagnostics)
     }
     stats->prepare_ms = plan->prepare_ms;
     stats->host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

@@ -2440,14 +2440,22 @@ if (!FL_NOTIME && tmg) {                                    \
         const bool ex_triv = TOPO ? triv : kreq_at(KA(shape_reqs), sl)->present == 0;
         int ex_pl = -1, ex_ipos = INT32_MAX, rounds = 0;
         bool ex_bail = false;
-        for (int base = ex_start; base < E && ex_pl < 0; base += 64) {
+        // the scan runs over list indices: every position, or (batched simulations) the shape-level's usable list
+        const int32_t* ul = KA(ex_ulist);
+        int u_base = 0, u_n = E, u_start = ex_start;
+        if (ul) {
+          u_base = KA(ex_ulist_off)[sl];
+          u_n = KA(ex_ulist_off)[sl + 1] - u_base;
+          u_start = KA(ex_uidx)[(size_t)sl * E + ex_start];
+        }
+        for (int base = u_start; base < u_n && ex_pl < 0; base += 64) {
           if (++rounds > FAST_EX_ROUNDS) {
             ex_bail = true;
             break;
           }
           if (FT_FINE && tmg) fcyc[13] += 1;  // diagnostic: existing-scan rounds
-          const int ec = base + lane;
-          const bool valid = ec < E;
+          const bool valid = base + lane < u_n;
+          const int ec = ul ? ul[u_base + min(base + lane, u_n - 1)] : base + lane;  // (clamped: masked by valid)
           bool cand = false, icand = false;
           int32_t ver = 0, ts = 0;
           {  // every read unconditional at a clamped position, the lanes past E masked after (no exec-masked block)
@@ -2485,14 +2493,14 @@ if (!FL_NOTIME && tmg) {                                    \
           }
           if (TOPO && t_n && ex_ipos == INT32_MAX) {
             const uint64_t im = __ballot(icand);
-            if (im) ex_ipos = base + __builtin_ctzll(im);
+            if (im) ex_ipos = __builtin_amdgcn_readlane(ec, __builtin_ctzll(im));
           }
-          bytes += (uint64_t)min(64, E - base) * (16 * KA(n_req_res) + 13);  // (the full path's model)
+          bytes += (uint64_t)min(64, u_n - base) * (16 * KA(n_req_res) + 13);  // (the full path's model)
           uint64_t cm = __ballot(cand);
           while (cm) {
             const int l = __builtin_ctzll(cm);
             cm &= cm - 1;
-            const int ei = base + l;
+            const int ei = __builtin_amdgcn_readlane(ec, l);
             const int32_t verx = __builtin_amdgcn_readlane(ver, l);
             attempts++;
             if (!b_staged && !ex_triv) {  // the pod's requirement set, once per pod
@@ -3423,13 +3431,24 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a0, const Solv
     const uint64_t exd0 = EX_DIAG ? __builtin_amdgcn_s_memtime() : 0;
     if (EX_DIAG && tid == 0) g_sdiag[0] += exd0 - exdS;  // topology staging
     if (EX_DIAG && tid == 0 && s_ctl[17] < a.n_existing) g_sdiag[3] += 1;
-    for (int base = s_ctl[17]; base < a.n_existing && placed == -1 && !memo_fail; base += 4 * NT) {
+    // the scan runs over list indices: every position, or (batched simulations) the shape-level's usable list
+    const int32_t* ul = BATCH ? a.ex_ulist : nullptr;
+    int u_base = 0, u_n = a.n_existing, u_start = s_ctl[17];
+    if (ul) {
+      u_base = a.ex_ulist_off[sl];
+      u_n = a.ex_ulist_off[sl + 1] - u_base;
+      u_start = u_start >= a.n_existing ? u_n : a.ex_uidx[(size_t)sl * a.n_existing + u_start];
+    }
+    for (int base = u_start; base < u_n && placed == -1 && !memo_fail; base += 4 * NT) {
       uint32_t flags = 0, iflags = 0;
+      int pk[4];  // this thread's positions of the round (-1: past the list)
       const uint64_t exd1 = EX_DIAG ? __builtin_amdgcn_s_memtime() : 0;
 #pragma unroll
       for (int k = 0; k < 4; k++) {  // 4 rounds per thread: independent, so their loads overlap
-        const int ec = base + k * NT + tid;
-        if (ec >= a.n_existing) continue;
+        const int ix = base + k * NT + tid;
+        pk[k] = ix < u_n ? (ul ? ul[u_base + ix] : ix) : -1;
+        const int ec = pk[k];
+        if (ec < 0) continue;
         const int32_t fl = a.ex_fail[(size_t)sl * a.n_existing + ec], ver = a.ex_ver[ec];
         const uint8_t sok = a.ex_static_ok[ec];
         const int32_t ts = a.ex_taintset[ec];
@@ -3470,9 +3489,9 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a0, const Solv
         __syncthreads();
         if (tid == 0) g_sdiag[5] += __builtin_amdgcn_s_memtime() - exd1;
       }
-      if (own_n) first_pos_min<NT>(iflags, base + tid, &s_ctl[24]);
-      const int n = compact_candidates_x4<NW>(flags, base + tid, s_list, s_wcnt);
-      if (wave == 0) bytes += (uint64_t)min(4 * NT, a.n_existing - base) * (16 * a.n_req_res + 13);  // once
+      if (own_n) first_pos_min_e(iflags, pk, &s_ctl[24]);
+      const int n = compact_candidates_x4e<NW>(flags, pk, s_list, s_wcnt, 0);
+      if (wave == 0) bytes += (uint64_t)min(4 * NT, u_n - base) * (16 * a.n_req_res + 13);  // once
       const uint64_t exd2 = EX_DIAG ? __builtin_amdgcn_s_memtime() : 0;
       if (EX_DIAG && tid == 0) g_sdiag[1] += exd2 - exd1;
       for (int r0 = 0; r0 < n; r0 += NW) {

@@ -82,7 +82,13 @@ def main():
         plan.close()
         # totals over the launches (launch count and per-launch averages: the kernel trace / pmc_traffic.py)
         out.update(launches=None, subsets=len(subs), kernel_ms=st["solve_kernel_ms"],
-                   bytes_algorithmic=st["bytes_algorithmic"], counts=ch["counts"])
+                   bytes_algorithmic=st["bytes_algorithmic"], counts=ch["counts"], pops=st["pops"])
+        if os.environ.get("KP_TIMING"):  # the batched Solves' phase split (solve_kernel probes, summed over sims)
+            names = ["pop+stage", "existing", "sort", "inflight-commit", "templates", "record+bookkeeping",
+                     "inflight-prepass", "inflight-attempts"]
+            tot = sum(st["attempt_cycles"]) or 1
+            out["phase_share"] = {k: round(v / tot, 4) for k, v in zip(names, st["attempt_cycles"])}
+            out["cycles_per_sim"] = round(tot / len(subs), 1)
     else:
         raise SystemExit(f"unknown leg {leg}")
     ctx.close()
