@@ -300,9 +300,11 @@ L2_BYTES_PER_PAIR = 208  # SURVEY §8d type row (64 B value ids + 96 B allocatab
 ROW_BYTES = 880 + 96     # one compiled requirement row (KReqs) + its requests, read once per row
 
 
-def _feas_kernel_name(T):
-    """The bitset filter kernel kp_filter_run launches for a catalogue of T types (csrc launch_feasibility)."""
-    return "feasibility_quad_kernel" if T <= 1024 else "feasibility_bits_kernel"
+def _feas_kernel_name(T, prices=True):
+    """The bitset filter kernel kp_filter_run launches for a catalogue of T types (csrc launch_feasibility): the quad
+    kernel with seven eval waves and a price-row copy wave, or all eight evaluating without price rows."""
+    return ("feasibility_quad_kernel<7>" if prices else "feasibility_quad_kernel<8>") if T <= 1024 else \
+        "feasibility_bits_kernel"
 
 
 def _feasibility(args, cat, ctx, prob, barrier, max_over_ranks, world, steps=10):
@@ -354,7 +356,7 @@ def _feasibility(args, cat, ctx, prob, barrier, max_over_ranks, world, steps=10)
             ach_c = alg_c / (kc_ms / 1e3) / 1e9
             legs[name]["compact"] = {
                 "value": round(pairs * world * steps / el_c, 1), "unit": "pairs/s", "kernel_ms": round(kc_ms, 4),
-                "roofline": {"bound": "hbm", "kernel": _feas_kernel_name(T), "achieved": round(ach_c, 1),
+                "roofline": {"bound": "hbm", "kernel": _feas_kernel_name(T, prices=False), "achieved": round(ach_c, 1),
                              "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach_c / HBM_PEAK_GBS, 4),
                              "traffic": _traffic("feas_compact"),
                              "algorithmic_bytes_per_launch": alg_c,

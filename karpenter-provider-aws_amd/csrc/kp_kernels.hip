@@ -37,7 +37,7 @@
     (defined(FASTLANE) || defined(FL_NOTIME) || defined(FT_FINE) || defined(FAST_SCAN_MAX) ||                        \
      defined(FAST_CHK_LIVE) || defined(FAST_EX_ROUNDS) || defined(FAST_CONT) || defined(SORT_DIAG) || defined(EX_DIAG) || defined(FEAS_MAX_BLOCKS) ||                 \
      defined(FEASQ_EW) || defined(FEASQ_ROWS) || defined(FEASQ_B128) || defined(FEASQ_SKIP_EVAL) || defined(FL_SKIP) ||  \
-     defined(SIM_WPE))
+     defined(SIM_WPE) || defined(FEASQ_MINW))
 #error "a measurement knob is set outside a tools/ variant build (tools/kp_diag.h)"
 #endif
 #ifndef KP_DIAG_BUILD
@@ -4696,11 +4696,19 @@ __global__ __launch_bounds__(FEASB_WAVES * 64, FEASB_MINW) void feasibility_bits
 #ifndef FEASQ_SKIP_EVAL
 #define FEASQ_SKIP_EVAL 0  // measurement only: decode + copies, no type-set work (wrong masks)
 #endif
+#ifndef FEASQ_MINW
+#define FEASQ_MINW 6  // waves per SIMD the quad kernel's register budget targets (8: 9 VGPRs spilled; 6: none, -4..6 %)
+#endif
 static_assert(KP_DIAG_BUILD || (FASTLANE == 1 && FL_NOTIME == 1 && FT_FINE == 0 && FAST_SCAN_MAX == 512 &&
                                  FAST_CHK_LIVE == 8 && FAST_EX_ROUNDS == 8 && FAST_CONT == 1 && SORT_DIAG == 0 && EX_DIAG == 0 && FEAS_MAX_BLOCKS == 65536 &&
-                                 FEASQ_EW == 7 && FEASQ_ROWS == 28 && FEASQ_B128 == 1 && FEASQ_SKIP_EVAL == 0 && FL_SKIP == 0),
+                                 FEASQ_EW == 7 && FEASQ_ROWS == 28 && FEASQ_B128 == 1 && FEASQ_SKIP_EVAL == 0 && FL_SKIP == 0 &&
+                                 FEASQ_MINW == 6),
               "the production build carries the production values of every measurement knob");
-__global__ __launch_bounds__(FEASB_WAVES * 64, FEASB_MINW) void feasibility_quad_kernel(FeasArgs a) {
+// EW eval waves (4 * EW rows per block); FEASB_WAVES - EW copy waves write the cheapest-price rows. Without price rows
+// (mask only, or the compact result) every wave evaluates: EW = FEASB_WAVES.
+template <int EW>
+__global__ __launch_bounds__(FEASB_WAVES * 64, FEASQ_MINW) void feasibility_quad_kernel(FeasArgs a) {
+  constexpr int ROWS = 4 * EW;
   __shared__ DevDict D;
   __shared__ int64_t s_vint[KP_MAX_BOUND_KEYS * 64];
   __shared__ OfferClass s_cls[KP_MAX_CLASSES];
@@ -4709,9 +4717,9 @@ __global__ __launch_bounds__(FEASB_WAVES * 64, FEASB_MINW) void feasibility_quad
   __shared__ uint64_t s_rowh[FEASB_WAVES][4][4];              // keys, negQ, classes, requested-resource mask
   __shared__ int64_t s_rq[FEASB_WAVES][4][KP_NRES];           // requests
   __shared__ uint64_t s_pass0[FEASB_WAVES][4][16];            // the type words before the AND chain
-  __shared__ uint64_t s_rcls[FEASQ_ROWS];                      // each row's offering classes, for the copy waves
-  __shared__ int32_t s_ready[FEASQ_ROWS];                      // ... once published
-  for (int i = threadIdx.x; i < FEASQ_ROWS; i += FEASB_WAVES * 64) s_ready[i] = 0;
+  __shared__ uint64_t s_rcls[ROWS];                      // each row's offering classes, for the copy waves
+  __shared__ int32_t s_ready[ROWS];                      // ... once published
+  for (int i = threadIdx.x; i < ROWS; i += FEASB_WAVES * 64) s_ready[i] = 0;
   block_copy(D, a.dict);
   const int tid = threadIdx.x;
   constexpr int NT = FEASB_WAVES * 64;
@@ -4753,15 +4761,15 @@ __global__ __launch_bounds__(FEASB_WAVES * 64, FEASB_MINW) void feasibility_quad
     h.lt = lane < KP_MAX_BOUND_KEYS ? Q->lt[lane] : 0;
     return h;
   };
-  // the block's rows: [row0, row1), FEASQ_ROWS per block; eval waves take its quads in turn, copy waves its rows
+  // the block's rows: [row0, row1), ROWS per block; eval waves take its quads in turn, copy waves its rows
   const long n = a.n_queries;
-  const long row0 = (long)blockIdx.x * FEASQ_ROWS, row1 = min(row0 + FEASQ_ROWS, n);
-  if (wave >= FEASQ_EW) {  // ---- a copy wave: each row's cheapest-price row once its eval wave published the classes
+  const long row0 = (long)blockIdx.x * ROWS, row1 = min(row0 + ROWS, n);
+  if (wave >= EW) {  // ---- a copy wave: each row's cheapest-price row once its eval wave published the classes
     if (a.out_cheapest) {
       // items = (row, half): T <= 1024, so a row is two 512-type halves (a short one reads 0 / drops its stores). The
       // next item's loads are issued before this item's stores: the in-order vector-memory counter then waits for a
       // load without waiting for the stores issued just before it
-      const int ncw = FEASB_WAVES - FEASQ_EW, cw = wave - FEASQ_EW;
+      const int ncw = FEASB_WAVES - EW, cw = wave - EW;
       const long nrows = row1 - row0;
       const int nitems = nrows > cw ? 2 * (int)((nrows - cw + ncw - 1) / ncw) : 0;
       auto row_of = [&](int it) { return row0 + cw + (long)(it >> 1) * ncw; };
@@ -4843,13 +4851,13 @@ __global__ __launch_bounds__(FEASB_WAVES * 64, FEASB_MINW) void feasibility_quad
   const long quads = (row1 - row0 + 3) / 4;
   long qi = wave;
   RowHdr nxt = qi < quads ? load_row(row0 + 4 * qi) : RowHdr{0, 0, 0, 0, 0};
-  for (; qi < quads; qi += FEASQ_EW) {
+  for (; qi < quads; qi += EW) {
     const long qd_base = row0 + 4 * qi;
     // ---- phase 1: decode the four rows (the next row's header loads in flight meanwhile)
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       const long q = qd_base + r;
-      const long qn = r < 3 ? q + 1 : qd_base + 4 * FEASQ_EW;
+      const long qn = r < 3 ? q + 1 : qd_base + 4 * EW;
       const RowHdr cur = nxt;
       if (qn < row1) nxt = load_row(qn);
       if (q >= row1) {  // past the block's last row: an empty group
@@ -5527,8 +5535,13 @@ hipError_t launch_launch(const LaunchArgs& a, hipStream_t s) {
 hipError_t launch_feasibility(const FeasArgs& a, hipStream_t s) {
   if (a.bits) {
     if (a.T <= 1024 && !a.one_row) {  // TW <= 16: four rows per wave
-      const long blocks = max(((long)a.n_queries + FEASQ_ROWS - 1) / FEASQ_ROWS, 1L);  // one chunk of rows each
-      hipLaunchKernelGGL(feasibility_quad_kernel, dim3((unsigned)blocks), dim3(FEASB_WAVES * 64), 0, s, a);
+      if (a.out_cheapest) {  // seven eval waves and a copy wave for the price rows
+        const long blocks = max(((long)a.n_queries + 4 * FEASQ_EW - 1) / (4 * FEASQ_EW), 1L);  // one chunk of rows each
+        hipLaunchKernelGGL(feasibility_quad_kernel<FEASQ_EW>, dim3((unsigned)blocks), dim3(FEASB_WAVES * 64), 0, s, a);
+      } else {  // no price rows: every wave evaluates
+        const long blocks = max(((long)a.n_queries + 4 * FEASB_WAVES - 1) / (4 * FEASB_WAVES), 1L);
+        hipLaunchKernelGGL(feasibility_quad_kernel<FEASB_WAVES>, dim3((unsigned)blocks), dim3(FEASB_WAVES * 64), 0, s, a);
+      }
     } else {
       hipLaunchKernelGGL(feasibility_bits_kernel, dim3((unsigned)max(1, a.blocks)), dim3(FEASB_WAVES * 64), 0, s, a);
     }

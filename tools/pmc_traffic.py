@@ -17,8 +17,8 @@ import sys
 
 # leg -> (the kernel the bench line's roofline names, its Kernel_Name pattern)
 LEGS = {"solve2": ("solve_kernel", "solve_kernel<4, false, false>"),
-        "feas_rows": ("feasibility_quad_kernel", "feasibility_quad_kernel("),
-        "feas_compact": ("feasibility_quad_kernel", "feasibility_quad_kernel("),
+        "feas_rows": ("feasibility_quad_kernel<7>", "feasibility_quad_kernel<7>"),
+        "feas_compact": ("feasibility_quad_kernel<8>", "feasibility_quad_kernel<8>"),
         "sweep": ("sim_kernel", "sim_kernel<"),
         "general": ("solve_kernel<4,*,true>", ", true>(SolveArgs")}
 
