@@ -18,6 +18,7 @@
  *   EX_DIAG [0]          the existing-node scan split in stats[25..30]
  *   FEAS_MAX_BLOCKS [65536], FEASQ_EW [7], FEASQ_ROWS [28], FEASQ_B128 [1]  feasibility grid / block shape
  *   FEASQ_SKIP_EVAL [0]  decode + copies only, no type-set work: WRONG MASKS, timing experiments only
+ *   FEASQ_MINW [6]       feasibility_quad_kernel register budget (waves per SIMD)
  *   SIM_WPE [0]          sim_kernel's register budget as waves per SIMD (amdgpu_waves_per_eu; 0: the compiler's)
  *   FL_SKIP [0]          fast-lane cost attribution, WRONG PLACEMENTS: bit 0 no sort replay, bit 1 no mutation stack,
  *                        bit 2 no statistics counters
