@@ -2214,7 +2214,7 @@ __device__ __noinline__ int fast_lane(uint64_t kargs, int32_t LDS* s_dyn_arg, ui
   // statistics: uniform counters (a lane-0 update of a per-lane 64-bit value costs an exec-masked block per pod: 6 % of
   // config 2's kernel, measured); the positions scanned are n_scan below
   uint64_t bytes = 0, attempts = 0, starts = 0, fcyc[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  int pops = 0, memo_pops = 0, handoff = -1, fb = -1, fl_last = -1;
+  int pops = 0, memo_pops = 0, handoff = -1, fb = -1;
   int chk_next = U(s_ctl[32]);  // kp_cancel: Queue pops (the Solve's total) at which the flag is read next
   // the NodeClaim this call's last append commit wrote, as it wrote it (the next pod usually starts there: reading
   // its lines back right after the stores waits for them to drain): remaining types, requests, threshold indices
@@ -2453,7 +2453,6 @@ if (!FL_NOTIME && tmg) {                                    \
             ex_bail = true;
             break;
           }
-          if (FT_FINE && tmg) fcyc[13] += 1;  // diagnostic: existing-scan rounds
           const bool valid = base + lane < u_n;
           const int ec = ul ? ul[u_base + min(base + lane, u_n - 1)] : base + lane;  // (clamped: masked by valid)
           bool cand = false, icand = false;
@@ -2588,6 +2587,7 @@ if (!FL_NOTIME && tmg) {                                    \
             n_ev += 64;
             n_buf = 0;
           }
+          FTF(13);  // diagnostic: FT(0) to an existing-node placement
           continue;
         }
       } else if (FL_HAS_EX) {  // addToExistingNode: every position fails (cursor == n_existing)
@@ -2875,7 +2875,6 @@ if (!FL_NOTIME && tmg) {                                    \
               bytes += fl_io[1];
             }
             n_app++;
-            if (FT_FINE && tmg && ncx == fl_last) fcyc[13] += 1;  // the previous pod's NodeClaim again
           } else {
             if (!b_staged) {  // the pod's requirement set, once per pod
               constexpr int NQ = (int)(sizeof(KReqs) / 8);
@@ -2949,7 +2948,6 @@ if (!FL_NOTIME && tmg) {                                    \
               h_id = c_bid;
               h_key = c_bkey + (lane == l ? 1 : 0);
             }
-            if (FT_FINE) fl_last = ncx;
             if (TOPO && triv && ncx < KA(ncc)) KA(nc_fail)[(size_t)sl * KA(ncc) + ncx] = NC_MERGED;
             if (TOPO && rec_n) {
               // Topology.Record, as the full path's: each recorded group (spreads only on fast levels) on its own lane;

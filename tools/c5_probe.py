@@ -45,7 +45,7 @@ if os.environ.get("KP_TIMING"):
                                                [round(c / fp, 1) for c in st["fast_cycles"]]))
     if "fine" in os.environ.get("KP_LIB", ""):  # FT_FINE build: attempt_cycles = the fast lane's finer split
         out["fast_fine_per_fast_pod"] = dict(zip(["window", "stage", "cursor", "sort", "nc-loads", "fits", "commit",
-                                                   "same-nc"], [round(c / fp, 1) for c in st["attempt_cycles"]]))
+                                                   "existing-placed"], [round(c / fp, 1) for c in st["attempt_cycles"]]))
 res = plan.run(read=True)
 out["nodeclaims"] = len(res["nodeclaims"])
 out["unschedulable"] = int((res["placement"] == -1).sum())

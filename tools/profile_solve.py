@@ -48,7 +48,9 @@ if os.environ.get("SORT_DIAG"):  # variant build: the full path's sort split in 
 if sum(fc):
     out["fast_cycles_per_fast_pod"] = {k: round(v / max(1, st["fast_pods"]), 1) for k, v in
                                        zip(["pop", "stage", "sort", "prepass", "attempts", "commit"], fc)}
-out["fast_fine_per_fast_pod"] = [round(v / max(1, st["fast_pods"]), 1) for v in ac]  # FT_FINE builds: probes 6..13
+out["fast_fine_per_fast_pod"] = dict(zip(["window", "stage", "cursor", "sort", "nc-loads", "fits", "commit",
+                                          "existing-placed"], [round(v / max(1, st["fast_pods"]), 1) for v in ac]))
+# (FT_FINE builds: probes 6..13; "existing-placed" is FT(0) to a placement on an existing node, those pods only)
 out["fast_bails"] = dict(zip(["ineligible", "spilled", "shift", "scan", "merge", "minvalues", "none", "-"],
                              st["fast_bails"]))
 print(json.dumps(out))
