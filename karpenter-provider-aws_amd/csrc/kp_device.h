@@ -148,6 +148,7 @@ struct SolveArgs {
   const int32_t* sl_fast_topo;       // [SL] 1: the fast lane may place the level's pods
   const int4* own_rec;               // [O][2] group, self, key, maxSkew | minDomains, row, key slot, 0 (static)
   const uint64_t* sl_topo_keys;      // [SL] dictionary keys of the owned groups
+  const int32_t* sl_stage;           // [SL][64] the fast lane's stage record (topology Solves; kp_host StageRecords)
   // first-fit cursors (exact): cur_*[sl] = {k, t}: the first k candidates of the scan order were known to
   // fail for shape-level sl at mutation time t; a mutation stack (t, position, in LDS) clamps k to the lowest
   // position changed since (monotone stack: suffix minimum by binary search). Shape-levels that own

@@ -3078,7 +3078,7 @@ struct SolveOffs {
          exts = 0, exav = 0, shpc = 0, shpa = 0, tgk = 0, tgr = 0, tgs = 0, tgm = 0, tga = 0, tgtb = 0, tgft = 0,
          tgt = 0, tgtn = 0, tgnt = 0, srb = 0, srn = 0, recl = 0, recx = 0, slft = 0, slob = 0, slon = 0, owng = 0,
          owns = 0, ownp = 0, ownr = 0, sltk = 0, tks = 0, extc = 0, tkk = 0, slsh = 0, tfeas = 0, exul = 0, exuo = 0,
-         exui = 0;
+         exui = 0, slst = 0;
   // arena: the Solve's inputs, then its mutable state [mut, mut_end) (restored before every run; [mut, common) is the
   // part a batched simulation patches, [common, mut_end) the part every simulation starts from alike), then
   // device-only regions
@@ -3119,6 +3119,42 @@ vector<uint8_t> ExStatic(const Compiled& C, uint32_t rmask) {
   return ok;
 }
 
+// The fast lane's stage record of each shape-level (topology Solves; SolveArgs::sl_stage): everything static the pod
+// loop reads at a pod's start in one 256-byte row, so that the next pod's row is one prefetched load (lane d holds
+// dword d) instead of three dependent rounds (level -> owned-group base -> owned-group records -> counts).
+//   [0] 0: the fast lane may take the level (sl_fast_topo, no host-port conflicts)  [1..2] tolerated taint sets
+//   [3] owned groups  [4] 1: no requirements at the level  [5..6] recorded groups: count, rec_list base
+//   [8 + 8j ..] owned group j < 4: own_rec's eight dwords  [40 + 2j ..] its podDomains  [48 + 2i ..] recorded
+//   group i < 8: (group, rec_aux)
+vector<int32_t> StageRecords(const Compiled& C) {
+  const size_t SL = C.shape_reqs.size();
+  if (!C.G) return vector<int32_t>(64, 0);
+  vector<int32_t> st(std::max<size_t>(SL, 1) * 64, 0);
+  for (size_t sh = 0; sh < C.shape_level_base.size(); sh++)
+    for (int l = 0; l < C.shape_nlevels[sh]; l++) {
+      const size_t sl = (size_t)C.shape_level_base[sh] + l;
+      int32_t* r = &st[sl * 64];
+      r[0] = (1 - C.sl_fast_topo[sl]) + (C.hp_any && C.shape_hp_conf[sh] ? 1 : 0);
+      r[1] = (int32_t)(uint32_t)C.shape_tolerates[sl];
+      r[2] = (int32_t)(uint32_t)(C.shape_tolerates[sl] >> 32);
+      const int on = C.sl_own_n[sl], ob = C.sl_own_base[sl];
+      r[3] = on;
+      r[4] = C.shape_reqs[sl].present == 0 ? 1 : 0;
+      r[5] = C.shape_rec_n[sh];
+      r[6] = C.shape_rec_base[sh];
+      for (int j = 0; j < std::min(on, 4); j++) {
+        for (int k = 0; k < 8; k++) r[8 + 8 * j + k] = C.own_rec[(size_t)(ob + j) * 8 + k];
+        r[40 + 2 * j] = (int32_t)(uint32_t)C.own_pd[ob + j];
+        r[41 + 2 * j] = (int32_t)(uint32_t)(C.own_pd[ob + j] >> 32);
+      }
+      for (int i = 0; i < std::min(C.shape_rec_n[sh], 8); i++) {
+        r[48 + 2 * i] = C.rec_list[(size_t)C.shape_rec_base[sh] + i];
+        r[49 + 2 * i] = C.rec_aux[(size_t)C.shape_rec_base[sh] + i];
+      }
+    }
+  return st;
+}
+
 void PutShared(Blob& blob, const Compiled& C, SolveOffs& o) {
   o.slb = blob.put(C.shape_level_base);
   o.snl = blob.put(C.shape_nlevels);
@@ -3149,6 +3185,7 @@ void PutShared(Blob& blob, const Compiled& C, SolveOffs& o) {
   for (size_t sh = 0; sh < C.shape_level_base.size(); sh++)
     for (int l = 0; l < C.shape_nlevels[sh]; l++) sl_shape[(size_t)C.shape_level_base[sh] + l] = (int32_t)sh;
   o.slsh = blob.put(sl_shape);
+  o.slst = blob.put(StageRecords(C));
 }
 
 // The arena's host-initialised part: the pods (pod_shape / queue of Pc entries), the existing nodes' static check,
@@ -3347,6 +3384,7 @@ void BindSolve(SolveArgs& a, const Compiled& C, const SolveOffs& o, uint8_t* sh,
   a.own_self = (const int32_t*)(sh + o.owns);
   a.own_pd = (const uint64_t*)(sh + o.ownp);
   a.own_rec = (const int4*)(sh + o.ownr);
+  a.sl_stage = (const int32_t*)(sh + o.slst);
   a.sl_topo_keys = (const uint64_t*)(sh + o.sltk);
   a.tkey_slot = (const int32_t*)(sh + o.tks);
   a.n_tk = C.TK;

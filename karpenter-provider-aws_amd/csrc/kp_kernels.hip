@@ -35,7 +35,7 @@
 // kernel into a measurement stub.
 #if !defined(KP_DIAG_BUILD) &&                                                                                       \
     (defined(FASTLANE) || defined(FL_NOTIME) || defined(FT_FINE) || defined(FAST_SCAN_MAX) ||                        \
-     defined(FAST_CHK_LIVE) || defined(FAST_EX_ROUNDS) || defined(FAST_CONT) || defined(SORT_DIAG) || defined(EX_DIAG) || defined(FEAS_MAX_BLOCKS) ||                 \
+     defined(FAST_CHK_LIVE) || defined(FAST_EX_ROUNDS) || defined(FAST_CONT) || defined(SORT_DIAG) || defined(EX_DIAG) || defined(FX_DIAG) || defined(FEAS_MAX_BLOCKS) ||                 \
      defined(FEASQ_EW) || defined(FEASQ_ROWS) || defined(FEASQ_B128) || defined(FEASQ_SKIP_EVAL) || defined(FL_SKIP) ||  \
      defined(SIM_WPE) || defined(FEASQ_MINW))
 #error "a measurement knob is set outside a tools/ variant build (tools/kp_diag.h)"
@@ -1322,6 +1322,9 @@ __device__ void slow_sort_wave(P ord, P npods, int n) {
 #ifndef EX_DIAG
 #define EX_DIAG 0  // diagnostic: the existing-node scan (range, scanned, cursor clamp, scans, cycles, placed) in stats[25..30]
 #endif
+#ifndef FX_DIAG
+#define FX_DIAG 0  // diagnostic: the fast lane's existing-node scans (scans, rounds, placed, skipped, failed, bailed) in stats[25..30]
+#endif
 __shared__ uint64_t g_sdiag[6];
 template <int NT, class P>
 __device__ void sort_newnodeclaims(P ord, P npods, int n, int mut, int p, int32_t* s_ctl, uint64_t* slow = nullptr) {
@@ -1535,6 +1538,43 @@ __device__ __forceinline__ void record_node(int rec_n, int rec_b, int g0, int au
         tg_cnt[(size_t)g * 64 + b0] = cnt0 + 1;
         tg_reg[g] = reg0 | (1ull << b0);
       }
+    }
+  }
+}
+
+// record_node in two halves for a commit of at most 64 recorded groups: the reads that do not depend on the commit
+// (liveness, taint filter, registered mask, the node's hostname count or value code) issued ahead of the commit's
+// stores, so that their wait does not also drain those stores; the group's count (indexed by the code) after.
+struct RecRead {
+  uint64_t reg0;
+  uint32_t b0;
+  bool ok;
+};
+__device__ __forceinline__ RecRead record_read(int rec_n, int g, int aux, int tsx, const int32_t* tg_live,
+                                               const uint64_t* tg_filt_tol, const uint8_t* tcode, const uint8_t* hcnt,
+                                               size_t stride, int node, const uint64_t* tg_reg) {
+  const int lane = LANE;
+  const int live = ((const int32_t GLB*)tg_live)[g];
+  const uint64_t ftol = ((const uint64_t GLB*)tg_filt_tol)[g];
+  const uint8_t GLB* src = aux >= 0 ? (const uint8_t GLB*)hcnt + (size_t)aux * stride + node
+                                    : (const uint8_t GLB*)tcode + (size_t)(-1 - aux) * stride + node;
+  RecRead r;
+  r.b0 = *src;
+  r.reg0 = ((const uint64_t GLB*)tg_reg)[g];
+  r.ok = lane < rec_n && live && ((ftol >> tsx) & 1);
+  return r;
+}
+__device__ __forceinline__ void record_write(const RecRead& r, int g, int aux, uint8_t* hcnt, size_t stride, int node,
+                                             int32_t* tg_cnt, uint64_t* tg_reg) {
+  const uint32_t b0 = r.b0;
+  const int cnt0 = ((const int32_t GLB*)tg_cnt)[(size_t)g * 64 + (b0 & 63)];
+  if (r.ok) {
+    if (aux >= 0) {
+      hcnt[(size_t)aux * stride + node] = b0 == 255 ? 1 : b0 < 254 ? b0 + 1 : 254;
+      tg_reg[g] = 1;
+    } else if (b0 < 64) {
+      tg_cnt[(size_t)g * 64 + b0] = cnt0 + 1;
+      tg_reg[g] = r.reg0 | (1ull << b0);
     }
   }
 }
@@ -2264,6 +2304,7 @@ if (!FL_NOTIME && tmg) {                                    \
 }
     // next pod's stage data, loaded while the current pod is placed (window offset pf_off; -1: none)
     int pf_off = -1, pf_own = 0, pf_ce0 = 0, pf_ce1 = 0, pf_cur = 0, pf_stamp = 0, prev_sl = -1;
+    int pf_stg = 0;  // topology Solves: the next entry's stage record (lane d: dword d of SolveArgs::sl_stage's row)
     int a_cur_prev_pos = 0, a_cur_prev_stamp = 0, a_cex_prev_stamp = 0, a_cex_prev_pos = 0;  // cursors the previous pod stored
     int64_t pf_preq = 0;
     uint64_t pf_tol = 0;
@@ -2321,9 +2362,15 @@ if (!FL_NOTIME && tmg) {                                    \
       int own, ce0, ce1, cur, stamp;
       int64_t preq_lane;
       uint64_t tolmask;
+      int stg = 0;  // topology Solves: the shape-level's stage record (eligibility, tolerations, owned / recorded groups)
       if (LIKELY(pf_off == off)) {
         own = U(pf_own), ce0 = U(pf_ce0), ce1 = U(pf_ce1), cur = U(pf_cur), stamp = U(pf_stamp), preq_lane = pf_preq,
         tolmask = U64(pf_tol);
+        if (TOPO) {
+          stg = pf_stg;
+          own = __builtin_amdgcn_readlane(stg, 0);
+          tolmask = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(stg, 2) << 32) | (uint32_t)__builtin_amdgcn_readlane(stg, 1);
+        }
         if (sl == prev_sl) {  // the previous pod (same shape-level) advanced both cursors after the loads
           cur = a_cur_prev_pos;
           stamp = a_cur_prev_stamp;
@@ -2331,11 +2378,17 @@ if (!FL_NOTIME && tmg) {                                    \
           ce1 = a_cex_prev_stamp;
         }
       } else {
-        own = U((TOPO ? 1 - KA(sl_fast_topo)[sl] : 0) + (KA(hp_any) && KA(shape_hp_conf)[shape] ? 1 : 0));
+        if (!TOPO) own = U(KA(hp_any) && KA(shape_hp_conf)[shape] ? 1 : 0);
         ce0 = U(FL_HAS_EX ? KA(cur_ex)[2 * sl] : 0), ce1 = U(FL_HAS_EX ? KA(cur_ex)[2 * sl + 1] : 0);
         const int64_t pq_r = KA(shape_requests)[(size_t)shape * KP_NRES + min(lane, KP_NRES - 1)];
         preq_lane = lane < KP_NRES ? pq_r : 0;
-        tolmask = U64(KA(shape_tolerates)[sl]);
+        if (!TOPO) {
+          tolmask = U64(KA(shape_tolerates)[sl]);
+        } else {
+          stg = KA(sl_stage)[(size_t)sl * 64 + lane];
+          own = __builtin_amdgcn_readlane(stg, 0);
+          tolmask = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(stg, 2) << 32) | (uint32_t)__builtin_amdgcn_readlane(stg, 1);
+        }
         cur = U(KA(cur_nc)[2 * sl]), stamp = U(KA(cur_nc)[2 * sl + 1]);
         READY(preq_lane);
       }
@@ -2343,11 +2396,12 @@ if (!FL_NOTIME && tmg) {                                    \
       if (LIKELY(off + 1 < qw_n)) {  // the next entry's stage loads: in flight while this pod is sorted and placed
         const int nshape = __builtin_amdgcn_readlane(qw_shape, off + 1);
         const int nsl = __builtin_amdgcn_readlane(qw_sl, off + 1);
-        pf_own = (TOPO ? 1 - KA(sl_fast_topo)[nsl] : 0) + (KA(hp_any) && KA(shape_hp_conf)[nshape] ? 1 : 0);
+        if (!TOPO) pf_own = KA(hp_any) && KA(shape_hp_conf)[nshape] ? 1 : 0;
+        else pf_stg = KA(sl_stage)[(size_t)nsl * 64 + lane];  // (eligibility and tolerations come from it)
         pf_ce0 = FL_HAS_EX ? KA(cur_ex)[2 * nsl] : 0, pf_ce1 = FL_HAS_EX ? KA(cur_ex)[2 * nsl + 1] : 0;
         const int64_t pq_r = KA(shape_requests)[(size_t)nshape * KP_NRES + min(lane, KP_NRES - 1)];
         pf_preq = lane < KP_NRES ? pq_r : 0;
-        pf_tol = KA(shape_tolerates)[nsl];
+        if (!TOPO) pf_tol = KA(shape_tolerates)[nsl];
         pf_cur = KA(cur_nc)[2 * nsl], pf_stamp = KA(cur_nc)[2 * nsl + 1];
         pf_off = off + 1;
       }
@@ -2399,32 +2453,42 @@ if (!FL_NOTIME && tmg) {                                    \
       int t_key[4] = {0, 0, 0, 0}, t_row[4] = {0, 0, 0, 0}, t_slot[4] = {0, 0, 0, 0}, t_self[4] = {0, 0, 0, 0},
           t_mskew[4] = {0, 0, 0, 0};
       uint64_t t_acc[4] = {0, 0, 0, 0};
-      if (TOPO) {
-        t_n = KA(sl_own_n)[sl];
-        triv = kreq_at(KA(shape_reqs), sl)->present == 0;
-        rec_n = KA(shape_rec_n)[shape];
-        rec_b = KA(shape_rec_base)[shape];
+      if (TOPO) {  // (every static field from the stage record's registers: the counts are the only loads)
+        t_n = __builtin_amdgcn_readlane(stg, 3);
+        triv = __builtin_amdgcn_readlane(stg, 4) != 0;
+        rec_n = __builtin_amdgcn_readlane(stg, 5);
+        rec_b = __builtin_amdgcn_readlane(stg, 6);
         if (rec_n) {  // (the group's liveness and taint filter are read at the commit: no wait here)
-          // (uniform branch; reads at clamped lanes, masked after: no exec-masked block)
-          const int rl = rec_b + min(lane, rec_n - 1);
-          const int g_r = KA(rec_list)[rl], a_r = KA(rec_aux)[rl];
-          r_g = g_r, r_aux = a_r;  // (the lanes past rec_n repeat the last entry: record_node masks them)
+          // (the lanes past rec_n repeat the last entry: record_node masks them)
+          if (LIKELY(rec_n <= 8)) {  // from the record: lane i takes dwords 48 + 2i and 49 + 2i
+            const int src = 48 + 2 * min(lane, rec_n - 1);
+            r_g = __builtin_amdgcn_ds_bpermute(src << 2, stg);
+            r_aux = __builtin_amdgcn_ds_bpermute((src + 1) << 2, stg);
+          } else {  // (uniform branch; reads at clamped lanes, masked after: no exec-masked block)
+            const int rl = rec_b + min(lane, rec_n - 1);
+            const int g_r = KA(rec_list)[rl], a_r = KA(rec_aux)[rl];
+            r_g = g_r, r_aux = a_r;
+          }
         }
-        const int ob = KA(sl_own_base)[sl];
 #pragma unroll
         for (int j = 0; j < 4; j++)
           if (j < t_n) {
-            const int4 r0 = KA(own_rec)[2 * (ob + j)], r1 = KA(own_rec)[2 * (ob + j) + 1];
-            t_key[j] = r0.z, t_row[j] = r1.y, t_slot[j] = r1.z, t_self[j] = r0.y, t_mskew[j] = r0.w;
-            if (r0.z >= 0) {
-              const int c = KA(tg_cnt)[(size_t)r0.x * 64 + lane];
-              const uint64_t reg = KA(tg_reg)[r0.x], pd = KA(own_pd)[ob + j];
+            const int g = __builtin_amdgcn_readlane(stg, 8 + 8 * j), self = __builtin_amdgcn_readlane(stg, 9 + 8 * j);
+            const int key = __builtin_amdgcn_readlane(stg, 10 + 8 * j), mskew = __builtin_amdgcn_readlane(stg, 11 + 8 * j);
+            t_key[j] = key, t_row[j] = __builtin_amdgcn_readlane(stg, 13 + 8 * j);
+            t_slot[j] = __builtin_amdgcn_readlane(stg, 14 + 8 * j), t_self[j] = self, t_mskew[j] = mskew;
+            if (key >= 0) {
+              const int c = KA(tg_cnt)[(size_t)g * 64 + lane];
+              const uint64_t reg = KA(tg_reg)[g];
+              const uint64_t pd = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(stg, 41 + 2 * j) << 32) |
+                                  (uint32_t)__builtin_amdgcn_readlane(stg, 40 + 2 * j);
+              const int mind = __builtin_amdgcn_readlane(stg, 12 + 8 * j);
               const bool sup = ((reg & pd) >> lane) & 1;
               const int mn = wave_min_i32(sup ? c : INT32_MAX);
               const int num = __builtin_popcountll(reg & pd);
               int64_t m = num ? (int64_t)mn : (int64_t)INT32_MAX;
-              if (r1.x > 0 && num < r1.x) m = 0;
-              t_acc[j] = __ballot(((reg >> lane) & 1) && (int64_t)c + r0.y - m <= r0.w);
+              if (mind > 0 && num < mind) m = 0;
+              t_acc[j] = __ballot(((reg >> lane) & 1) && (int64_t)c + self - m <= mskew);
             }
           }
       }
@@ -2448,11 +2512,13 @@ if (!FL_NOTIME && tmg) {                                    \
           u_n = KA(ex_ulist_off)[sl + 1] - u_base;
           u_start = KA(ex_uidx)[(size_t)sl * E + ex_start];
         }
+        if (FX_DIAG && lane == 0) g_sdiag[0] += 1;
         for (int base = u_start; base < u_n && ex_pl < 0; base += 64) {
           if (++rounds > FAST_EX_ROUNDS) {
             ex_bail = true;
             break;
           }
+          if (FX_DIAG && lane == 0) g_sdiag[1] += 1;
           const bool valid = base + lane < u_n;
           const int ec = ul ? ul[u_base + min(base + lane, u_n - 1)] : base + lane;  // (clamped: masked by valid)
           bool cand = false, icand = false;
@@ -2530,6 +2596,10 @@ if (!FL_NOTIME && tmg) {                                    \
               store_merged(er, rv, m_v, D.W, D.KB);
               if (KA(ex_reqs_ro)) KA(ex_own)[ei >> 6] |= 1ull << (ei & 63);  // (uniform: every lane stores the same)
             }
+            RecRead rrd{0, 0, false};  // Topology.Record's reads, ahead of the commit's stores (<= 64 groups)
+            if (TOPO && rec_n && rec_n <= 64)
+              rrd = record_read(rec_n, r_g, r_aux, __builtin_amdgcn_readlane(ts, l), KA(tg_live), KA(tg_filt_tol),
+                                KA(ex_tcode), KA(hcnt_ex), (size_t)E, ei, KA(tg_reg));
             {  // requests + pod, the headroom rows of the first four requested resources - pod, version + 1: every
                // lane reads and stores (the lanes past the rows repeat the last row's value), no exec-masked block
               int64_t* rqp = KA(ex_requests) + (size_t)ei * KP_NRES + min(lane, KP_NRES - 1);
@@ -2544,15 +2614,19 @@ if (!FL_NOTIME && tmg) {                                    \
               KA(ex_ver)[ei] = verx + 1;
             }
             if (TOPO && rec_n) {
-              record_node(rec_n, rec_b, r_g, r_aux, __builtin_amdgcn_readlane(ts, l), KA(rec_list), KA(rec_aux),
-                          KA(tg_live), KA(tg_filt_tol), KA(ex_tcode), KA(hcnt_ex), (size_t)E, ei, KA(tg_cnt),
-                          KA(tg_reg));
+              if (LIKELY(rec_n <= 64))
+                record_write(rrd, r_g, r_aux, KA(hcnt_ex), (size_t)E, ei, KA(tg_cnt), KA(tg_reg));
+              else
+                record_node(rec_n, rec_b, r_g, r_aux, __builtin_amdgcn_readlane(ts, l), KA(rec_list), KA(rec_aux),
+                            KA(tg_live), KA(tg_filt_tol), KA(ex_tcode), KA(hcnt_ex), (size_t)E, ei, KA(tg_cnt),
+                            KA(tg_reg));
               bytes += 16 * (uint64_t)rec_n;
             }
             ex_pl = ei;
             break;
           }
         }
+        if (FX_DIAG && lane == 0) g_sdiag[ex_bail ? 5 : ex_pl >= 0 ? 2 : 4] += 1;
         if (ex_bail) {  // a long scan: the full path's (nothing was placed; the failure memos stay valid)
           handoff = pod;
           fb = FB_SCAN;
@@ -2591,6 +2665,7 @@ if (!FL_NOTIME && tmg) {                                    \
           continue;
         }
       } else if (FL_HAS_EX) {  // addToExistingNode: every position fails (cursor == n_existing)
+        if (FX_DIAG && lane == 0) g_sdiag[3] += 1;
         *reinterpret_cast<int2*>(&KA(cur_ex)[2 * sl]) = make_int2(KA(n_existing), a_cex_prev_stamp);  // (every lane)
         a_cex_prev_pos = KA(n_existing);
       }
@@ -2822,6 +2897,7 @@ if (!FL_NOTIME && tmg) {                                    \
         // the next pod's prefetch was issued before these gathers, so it has landed: take it off the outstanding
         // list now rather than at the next pod's stage, where the wait would cover this pod's stores as well
         READY(pf_own);
+        if (TOPO) READY(pf_stg);
         READY(pf_ce0);
         READY(pf_ce1);
         READY(pf_preq);
@@ -2902,6 +2978,12 @@ if (!FL_NOTIME && tmg) {                                    \
           }
           FTF(11);
           if (LIKELY(__ballot(X != 0))) {
+            // Topology.Record's reads ahead of the stores (a merge may set the NodeClaim's value codes: then the
+            // code is read again after store_tcodes)
+            RecRead rrd{0, 0, false};
+            if (TOPO && rec_n && rec_n <= 64)
+              rrd = record_read(rec_n, r_g, r_aux, __builtin_amdgcn_readlane(hv.ts, l), KA(tg_live), KA(tg_filt_tol),
+                                KA(nc_tcode), KA(hcnt_nc), (size_t)KA(hnc_stride), ncx, KA(tg_reg));
             if (UNLIKELY(full_add)) {
               store_merged(reinterpret_cast<KReqs*>(KA(nc_reqs) + (size_t)ncx * sizeof(KReqs)), rv, m_v, D.W, D.KB);
               if (TOPO && KA(n_tk)) store_tcodes(KA(n_tk), KA(tk_keys), KA(nc_tcode), KA(hnc_stride), rv, m_v, ncx);
@@ -2952,9 +3034,12 @@ if (!FL_NOTIME && tmg) {                                    \
             if (TOPO && rec_n) {
               // Topology.Record, as the full path's: each recorded group (spreads only on fast levels) on its own lane;
               // a dictionary key counts once the NodeClaim holds one value of it (its value code < 64)
-              record_node(rec_n, rec_b, r_g, r_aux, __builtin_amdgcn_readlane(hv.ts, l), KA(rec_list), KA(rec_aux),
-                          KA(tg_live), KA(tg_filt_tol), KA(nc_tcode), KA(hcnt_nc), (size_t)KA(hnc_stride), ncx,
-                          KA(tg_cnt), KA(tg_reg));
+              if (LIKELY(rec_n <= 64 && !full_add))
+                record_write(rrd, r_g, r_aux, KA(hcnt_nc), (size_t)KA(hnc_stride), ncx, KA(tg_cnt), KA(tg_reg));
+              else
+                record_node(rec_n, rec_b, r_g, r_aux, __builtin_amdgcn_readlane(hv.ts, l), KA(rec_list), KA(rec_aux),
+                            KA(tg_live), KA(tg_filt_tol), KA(nc_tcode), KA(hcnt_nc), (size_t)KA(hnc_stride), ncx,
+                            KA(tg_cnt), KA(tg_reg));
               bytes += 16 * (uint64_t)rec_n;
             }
             if (LIKELY(!full_add)) {  // the append path left the requirements (hmin, catalogue) as they were
@@ -3267,7 +3352,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a0, const Solv
     g_fast.bytes = g_fast.attempts = g_fast.scanned = g_fast.starts = g_fast.fpods = g_fast.runpods = 0;
     for (int i = 0; i < 16; i++) g_fast.fcyc[i] = 0;
     for (int i = 0; i < 8; i++) g_fast.fbail[i] = 0;
-    if (SORT_DIAG || EX_DIAG)
+    if (SORT_DIAG || EX_DIAG || FX_DIAG)
       for (int i = 0; i < 6; i++) g_sdiag[i] = 0;
   }
   __syncthreads();
@@ -4148,7 +4233,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a0, const Solv
     for (int i = 0; i < 6; i++) a.stats[25 + i] = g_fast.fcyc[i];
     if (FT_FINE && timing)
       for (int i = 0; i < 8; i++) a.stats[16 + i] = g_fast.fcyc[6 + i];
-    if (SORT_DIAG || EX_DIAG)
+    if (SORT_DIAG || EX_DIAG || FX_DIAG)
       for (int i = 0; i < 6; i++) a.stats[25 + i] = g_sdiag[i];
     // chunked order: peak chunks, splits, emptied chunks, (re)builds; final order mode
     a.stats[41] = g_chk.nch_peak;
@@ -4698,7 +4783,7 @@ __global__ __launch_bounds__(FEASB_WAVES * 64, FEASB_MINW) void feasibility_bits
 #define FEASQ_MINW 6  // waves per SIMD the quad kernel's register budget targets (8: 9 VGPRs spilled; 6: none, -4..6 %)
 #endif
 static_assert(KP_DIAG_BUILD || (FASTLANE == 1 && FL_NOTIME == 1 && FT_FINE == 0 && FAST_SCAN_MAX == 512 &&
-                                 FAST_CHK_LIVE == 8 && FAST_EX_ROUNDS == 8 && FAST_CONT == 1 && SORT_DIAG == 0 && EX_DIAG == 0 && FEAS_MAX_BLOCKS == 65536 &&
+                                 FAST_CHK_LIVE == 8 && FAST_EX_ROUNDS == 8 && FAST_CONT == 1 && SORT_DIAG == 0 && EX_DIAG == 0 && FX_DIAG == 0 && FEAS_MAX_BLOCKS == 65536 &&
                                  FEASQ_EW == 7 && FEASQ_ROWS == 28 && FEASQ_B128 == 1 && FEASQ_SKIP_EVAL == 0 && FL_SKIP == 0 &&
                                  FEASQ_MINW == 6),
               "the production build carries the production values of every measurement knob");
@@ -4767,7 +4852,7 @@ __global__ __launch_bounds__(FEASB_WAVES * 64, FEASQ_MINW) void feasibility_quad
       // items = (row, half): T <= 1024, so a row is two 512-type halves (a short one reads 0 / drops its stores). The
       // next item's loads are issued before this item's stores: the in-order vector-memory counter then waits for a
       // load without waiting for the stores issued just before it
-      const int ncw = FEASB_WAVES - EW, cw = wave - EW;
+      const int ncw = FEASB_WAVES - EW > 0 ? FEASB_WAVES - EW : 1, cw = wave - EW;  // (EW == FEASB_WAVES: no copy wave)
       const long nrows = row1 - row0;
       const int nitems = nrows > cw ? 2 * (int)((nrows - cw + ncw - 1) / ncw) : 0;
       auto row_of = [&](int it) { return row0 + cw + (long)(it >> 1) * ncw; };

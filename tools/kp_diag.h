@@ -16,6 +16,7 @@
  *   FAST_CONT [1]        the continuation round (the previous commit's NodeClaim first, from registers)
  *   SORT_DIAG [0]        the full path's sort split in stats[25..30]
  *   EX_DIAG [0]          the existing-node scan split in stats[25..30]
+ *   FX_DIAG [0]          the fast lane's existing-node scans (scans, rounds, placed, skipped, failed, bailed) in stats[25..30]
  *   FEAS_MAX_BLOCKS [65536], FEASQ_EW [7], FEASQ_ROWS [28], FEASQ_B128 [1]  feasibility grid / block shape
  *   FEASQ_SKIP_EVAL [0]  decode + copies only, no type-set work: WRONG MASKS, timing experiments only
  *   FEASQ_MINW [6]       feasibility_quad_kernel register budget (waves per SIMD)

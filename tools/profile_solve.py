@@ -42,6 +42,8 @@ fc = st["fast_cycles"]
 if os.environ.get("EX_DIAG"):  # variant build: the existing-node scan in place of the fast-lane phases
     out["existing_diag_per_pop"] = {k: round(v / max(1, st["pops"]), 2) for k, v in
                                     zip(["staging_cycles", "prepass_cycles", "attempt_cycles", "scans", "cycles", "eval_cycles"], fc)}
+if os.environ.get("FX_DIAG"):  # variant build: the fast lane's existing-node scans (counts over the Solve)
+    out["fast_existing_scans"] = dict(zip(["scans", "rounds", "placed", "skipped", "failed", "bailed"], fc))
 if os.environ.get("SORT_DIAG"):  # variant build: the full path's sort split in place of the fast-lane phases
     out["sort_diag_per_pop"] = {k: round(v / max(1, st["pops"]), 2) for k, v in
                                 zip(["decision_cycles", "shift_cycles", "shifted", "mode1", "mode2", "mode3"], fc)}
