@@ -2736,6 +2736,41 @@ if (!FL_NOTIME && tmg) {                                    \
         if (relaxed) epoch += 1;  // lastLen = map{}
         memo_pops++;
         cont_w = -1;
+        if (!relaxed && off + 1 < qw_n) {
+          // the window entries right behind this pod that fail by the memo as well, at their last relaxation level:
+          // their pops change nothing the next of them reads (no NodeClaim, mutation or relaxation, the queue length
+          // stays len, the order stays as replayed), so each does exactly this pod's bookkeeping — cursors at the
+          // end, placement -1, Queue.Push with lastLen = len — and they are done at once, window entry i on lane i,
+          // up to the first that would end the Solve (popped again at the same length), needs the full path, or
+          // breaks the run
+          const int j0 = off + 1;
+          const bool inw = lane >= j0 && lane < qw_n;
+          const int gsl = inw ? qw_sl : 0, gsh = inw ? qw_shape : 0;  // (reads at valid indices, masked after)
+          const int32_t sf = KA(sl_fail)[gsl];
+          const int lb = KA(shape_level_base)[gsh], nl = KA(shape_nlevels)[gsh];
+          const uint64_t hpc = KA(hp_any) ? KA(shape_hp_conf)[gsh] : 0;
+          const bool ok = inw && sf == n_nc && gsl - lb + 1 >= nl && hpc == 0 &&
+                          !(qw_epoch == epoch && qw_lastlen == q_len);
+          const uint64_t okm = __ballot(ok) >> j0;
+          const int k = min(__builtin_ctzll(~okm), pop_left - (pops + memo_pops));
+          if (k > 0) {
+            if (lane >= j0 && lane < j0 + k) {
+              const int np = KA(n_pods);
+              const int tail_i = (int)(((int64_t)q_head + q_len + (lane - j0)) % np);
+              KA(placement)[qw_pod] = -1;
+              KA(queue)[tail_i] = qw_pod;
+              KA(lastlen)[qw_pod] = q_len;
+              KA(lastlen_epoch)[qw_pod] = epoch;
+              *reinterpret_cast<int2*>(&KA(cur_nc)[2 * gsl]) = make_int2(n_nc, stk_t);
+              if (FL_HAS_EX) *reinterpret_cast<int2*>(&KA(cur_ex)[2 * gsl]) = make_int2(KA(n_existing), a_cex_prev_stamp);
+            }
+            q_head = (int)(((int64_t)q_head + k) % KA(n_pods));
+            memo_pops += k;
+            qw_next = j0 + k;
+            pf_off = -1;  // (the prefetched stage was the next entry's)
+            prev_sl = -1;
+          }
+        }
         continue;
       }
       // addToInflightNode: pre-checks 64 positions at a time, then the append-path attempts in order. A long scan
