@@ -2716,6 +2716,10 @@ if (!FL_NOTIME && tmg) {                                    \
       wave_sync();
       FT(2);
       if (memo) {  // the full path's failure: cursors at the end, Preferences.Relax, Queue.Push
+        if (FX_DIAG && lane == 0) {  // diagnostic (config 5 has no existing nodes: the slots are free there)
+          g_sdiag[0] += 1;
+          if (cont_w >= 0) g_sdiag[2] += 1;
+        }
         a_cur_prev_pos = n_nc;
         a_cur_prev_stamp = stk_t;
         const int lvl = sl - KA(shape_level_base)[shape];
@@ -2766,6 +2770,10 @@ if (!FL_NOTIME && tmg) {                                    \
             }
             q_head = (int)(((int64_t)q_head + k) % KA(n_pods));
             memo_pops += k;
+            if (FX_DIAG && lane == 0) {
+              g_sdiag[1] += k;
+              g_sdiag[3] += 1;
+            }
             qw_next = j0 + k;
             pf_off = -1;  // (the prefetched stage was the next entry's)
             prev_sl = -1;

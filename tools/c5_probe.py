@@ -34,6 +34,8 @@ out.update({"pops": st["pops"], "attempts_per_pop": round(st["attempts"] / pops,
             "fast_bails": dict(zip(["ineligible", "spilled", "shift", "scan", "merge", "minvalues", "none", "memo"],
                                    st["fast_bails"])),
             "order_chunks": dict(zip(["peak_chunks", "splits", "emptied", "builds", "final_mode"], st["order_chunks"]))})
+if os.environ.get("FX_DIAG"):  # variant build (tools/kp_diag.h FX_DIAG): the fast lane's memo pops
+    out["memo_pops"] = dict(zip(["single", "batched", "single_after_placement", "batches"], st["fast_cycles"][:4]))
 if os.environ.get("KP_TIMING"):
     names = ["pop+stage", "existing", "sort", "inflight-commit", "templates", "record+bookkeeping", "inflight-prepass",
              "inflight-attempts"]
