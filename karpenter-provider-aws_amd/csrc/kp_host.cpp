@@ -4836,10 +4836,12 @@ static int32_t PrepareGeneral(kp_ctx* ctx, const kp_cluster* cl, kp_cluster_plan
   in.namespaces = cl->namespaces;
   in.n_namespaces = cl->n_namespaces;
   in.pod_uids = cl->pod_uids;
+  PhaseTimer pt;
   auto plan = std::make_unique<kp_cluster_plan>();
   plan->ctx = ctx;
   plan->N = (int)cl->n_nodes;
   plan->general = std::make_unique<OwnedCluster>(cl);
+  pt.lap("general: owned copy");
   // the superset Solve of the batched simulations, built now (it validates every node and pod as well); a cluster
   // it does not take keeps the per-subset compile, validated here by the whole-cluster compile
   int32_t rc = KP_E_UNSUPPORTED;
@@ -5651,6 +5653,7 @@ static int32_t GeneralBatchBuild(kp_cluster_plan* plan, std::shared_ptr<GeneralB
   kp_ctx* ctx = plan->ctx;
   const kp_cluster& cl = plan->general->cl;
   const int N = (int)cl.n_nodes;
+  PhaseTimer pt;
   auto gb = std::make_shared<GeneralBatch>();
   vector<kp_existing_node> ex;
   vector<kp_pod> pods;
@@ -5709,11 +5712,13 @@ static int32_t GeneralBatchBuild(kp_cluster_plan* plan, std::shared_ptr<GeneralB
   in.namespaces = cl.namespaces;
   in.n_namespaces = cl.n_namespaces;
   in.reserved_offering_mode = KP_RESERVED_STRICT;
+  pt.lap("general: inputs");
   gb->C = std::make_unique<Compiled>();
   Compiled& C = *gb->C;
   C.track_nodes = true;
   int32_t rc = CompileSolve(&in, C, ctx);
   if (rc) return rc;
+  pt.lap("general: superset compile");
   if (!C.track_nodes) return fail(KP_E_INVAL, "superset compile lost its node tracking");
   rc = EnsureBaseOnDevice(ctx, *C.B);
   if (rc) return rc;
@@ -5749,9 +5754,11 @@ static int32_t GeneralBatchBuild(kp_cluster_plan* plan, std::shared_ptr<GeneralB
       for (int32_t g : C.shape_l0[s]) gb->live0[g] = 1;
     }
   }
+  pt.lap("general: tracking");
   gb->rmask = RequestedResources(C);
   gb->ex_static = ExStatic(C, gb->rmask);
   gb->offers.Build(C.B->d, cl);
+  pt.lap("general: offers");
   {
     vector<std::map<string, string>> labels(N);
     for (int i = 0; i < N; i++)
@@ -5761,11 +5768,13 @@ static int32_t GeneralBatchBuild(kp_cluster_plan* plan, std::shared_ptr<GeneralB
       }
     gb->cands.Build(cl, labels);
   }
+  pt.lap("general: candidates");
   gb->res_mode = !C.B->res_cls ? 0 : 2;
   gb->opt_stride = 100;
   // the shared region: read-only data of every simulation + the template-options table
   Blob blob;
   PutShared(blob, C, gb->so);
+  pt.lap("general: shared blob");
   {  // per shape-level, the positions that can ever take one of its pods (DeviceArgs::ex_ulist): the kernel's
      // count-independent checks on the pristine state
     const int E = (int)C.ex_input.size(), SLn = (int)C.shape_reqs.size();
@@ -5793,6 +5802,7 @@ static int32_t GeneralBatchBuild(kp_cluster_plan* plan, std::shared_ptr<GeneralB
     gb->so.exuo = blob.put(off);
     gb->so.exui = blob.put(uidx);
   }
+  pt.lap("general: usable lists");
   const size_t host_bytes = blob.host.size();
   const int NT = (int)C.B->tmpl_reqs.size(), SLi = (int)C.shape_reqs.size();
   gb->tfeas_on = NT > 0 && SLi > 0 && ctx->ov.template_table == 0;
@@ -5807,6 +5817,7 @@ static int32_t GeneralBatchBuild(kp_cluster_plan* plan, std::shared_ptr<GeneralB
     HIPCHK(launch_tmpl_feas(TfeasOf(a, sh, gb->so, SLi, gb->tf_words), ctx->stream));
   }
   HIPCHK(hipStreamSynchronize(ctx->stream));
+  pt.lap("general: upload + table");
   out = gb;
   return KP_OK;
 }

@@ -65,3 +65,24 @@ def test_multi_term_kats(ctx, catalog):
     for prob in [kat.problem(catalog, [a], [9]), kat.problem(catalog, [b, a], [2, 3]), kat.problem(catalog, [c, h], [2, 2])]:
         got, want = run_both(ctx, prob)
         check_same(got, want)
+
+
+@pytest.mark.parametrize("n_groups,n_existing", [(12, 0), (12, 9), (70, 0), (70, 9)])
+def test_many_recorded_groups(ctx, catalog, n_groups, n_existing):
+    """Every pod is counted by n_groups spread groups (one per shape: the same tier selector, its own maxSkew, zone
+    or hostname key): more than the stage record's 8 recorded groups (their list read from memory) and, at 70, more
+    than one 64-lane Topology.Record pass (record_node instead of the reads issued ahead of the commit stores), on
+    NodeClaims and on existing nodes."""
+    from kpamd import synth
+    from kpamd.model import ExistingNode, LabelSelector, PodShape, TopologySpread
+    sel = LabelSelector(match_labels={"tier": "web"})
+    shapes = [PodShape(synth.req_res(100 + 50 * (i % 5), 256), labels={"app": f"d{i}", "tier": "web"},
+                       topology_spread=[TopologySpread(kat.ZONE if i % 2 == 0 else kat.HOST, 2 + i, sel)])
+              for i in range(n_groups)]
+    it = catalog[synth._type_named(catalog, "m5.xlarge")]
+    alloc = it.allocatable()
+    nodes = [ExistingNode(f"n{e}", synth.node_labels(it, e % 3, "on-demand", "default", f"n{e}"),
+                          {k: alloc[k] for k in ("cpu", "memory", "pods")}) for e in range(n_existing)]
+    prob = kat.problem(catalog, shapes, [3] * n_groups, existing=nodes)
+    got, want = run_both(ctx, prob)
+    check_same(got, want)
