@@ -5759,12 +5759,14 @@ static int32_t GeneralBatchBuild(kp_cluster_plan* plan, std::shared_ptr<GeneralB
   gb->ex_static = ExStatic(C, gb->rmask);
   gb->offers.Build(C.B->d, cl);
   pt.lap("general: offers");
-  {
+  {  // (the candidate prices read the capacity-type, zone, zone-id and reservation labels only)
     vector<std::map<string, string>> labels(N);
     for (int i = 0; i < N; i++)
       for (uint32_t j = 0; j < cl.nodes[i].node.n_labels; j++) {
         const kp_label& l = cl.nodes[i].node.labels[j];
-        labels[i][Normalize(l.key ? l.key : "")] = l.value ? l.value : "";
+        string k = Normalize(l.key ? l.key : "");
+        if (k == kCapType || k == kZone || k == kZoneID || k == kResID || k == kResType)
+          labels[i][std::move(k)] = l.value ? l.value : "";
       }
     gb->cands.Build(cl, labels);
   }

@@ -571,14 +571,21 @@ class ClusterPlan:
     candidate subsets as computeConsolidation would (kp_cluster_simulate)."""
 
     def __init__(self, ctx, cluster, catalogs=None):
+        import time
         self.ctx = ctx
         self.cluster = cluster
+        t0 = time.perf_counter()
         self.catalogs = catalogs or [Catalog(ctx, c) for c in cluster.catalogs]
+        t1 = time.perf_counter()
         arena = Arena()
         cl = abi.build_cluster(arena, cluster, catalog_handles=[c.h.value for c in self.catalogs])
+        t2 = time.perf_counter()
         h = C.c_void_p()
         _check(ctx.lib, ctx.lib.kp_cluster_prepare(ctx.h, C.byref(cl), C.byref(h)))
         self.h = h
+        # where the construction's time went: catalogue upload (when not passed in), this binding's marshalling of the
+        # cluster into kp_cluster structs (a caller's shim builds those itself), and kp_cluster_prepare
+        self.prepare_times = {"catalog_s": t1 - t0, "marshal_s": t2 - t1, "kp_cluster_prepare_s": time.perf_counter() - t2}
 
     def refresh(self):
         """kp_cluster_refresh: re-apply the catalogues' current offerings (after update_offerings) in place."""
