@@ -3992,6 +3992,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a0, const Solv
                           a.tmpl_fail[(size_t)sl * a.n_tmpl + t] != NC_NEVER;
         const int n = compact_candidates<NW>(cand, t, s_list, s_wcnt);
         for (int r0 = 0; r0 < n; r0 += NW) {
+          if (FX_DIAG && tid == 0) g_sdiag[4] += 1;  // diagnostic: template rounds
           const int li = r0 + wave;
           bool ok = false;
           uint64_t m_v = 0, X = 0, nh = 0;
@@ -4090,6 +4091,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a0, const Solv
                 reserve_commit((int32_t LDS*)s_rcap, 0, nh);
                 if (lane == 0) a.nc_held[nc] = nh;
               }
+              const uint64_t fxd0 = FX_DIAG ? __builtin_amdgcn_s_memtime() : 0;
               store_maxalloc(hdr(a.tmpl_catalog[tm])->d.alloc, lane < D.TW ? X : 0, D.T, a.req_res_mask,
                              a.nc_maxalloc + (size_t)nc * KP_NRES, a.nc_head + nc,
                              lane < KP_NRES ? a.tmpl_daemon[(size_t)tm * KP_NRES + lane] + s_preq[lane] : 0,
@@ -4105,6 +4107,7 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a0, const Solv
                 }
                 if (lane == 0) a.tmpl_ver[tm] += 1;
               }
+              if (FX_DIAG && lane == 0) g_sdiag[5] += __builtin_amdgcn_s_memtime() - fxd0;  // diagnostic
             }
             placed = nc;
           }

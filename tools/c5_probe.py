@@ -36,6 +36,7 @@ out.update({"pops": st["pops"], "attempts_per_pop": round(st["attempts"] / pops,
             "order_chunks": dict(zip(["peak_chunks", "splits", "emptied", "builds", "final_mode"], st["order_chunks"]))})
 if os.environ.get("FX_DIAG"):  # variant build (tools/kp_diag.h FX_DIAG): the fast lane's memo pops
     out["memo_pops"] = dict(zip(["single", "batched", "single_after_placement", "batches"], st["fast_cycles"][:4]))
+    out["new_nodeclaims"] = {"template_rounds": st["fast_cycles"][4], "maxalloc_cycles": st["fast_cycles"][5]}
 if os.environ.get("KP_TIMING"):
     names = ["pop+stage", "existing", "sort", "inflight-commit", "templates", "record+bookkeeping", "inflight-prepass",
              "inflight-attempts"]
