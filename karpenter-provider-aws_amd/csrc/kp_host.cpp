@@ -5607,12 +5607,13 @@ struct GenSlot {
   }
 };
 // the batch's copy streams: uploads (the next launch's overlays) and downloads (the last launch's results) overlap the
-// kernels on the context stream instead of queueing between them
+// kernels instead of queueing between them; and one kernel stream per launch slot, so that a launch's batch_init and
+// first workgroups fill the CUs the previous launch's last simulations leave idle (the slots share only read-only data)
 struct CopyStreams {
-  hipStream_t up = nullptr, down = nullptr;
+  hipStream_t up = nullptr, down = nullptr, k[2] = {nullptr, nullptr};
   ~CopyStreams() {
-    if (up) (void)hipStreamDestroy(up);
-    if (down) (void)hipStreamDestroy(down);
+    for (hipStream_t x : {up, down, k[0], k[1]})
+      if (x) (void)hipStreamDestroy(x);
   }
 };
 
@@ -6081,15 +6082,16 @@ static int32_t GeneralBatchRun(kp_cluster_plan* plan, GeneralBatch& gb, const ve
   if (!gb.cs.up) {
     HIPCHK(hipStreamCreateWithFlags(&gb.cs.up, hipStreamNonBlocking));
     HIPCHK(hipStreamCreateWithFlags(&gb.cs.down, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&gb.cs.k[0], hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&gb.cs.k[1], hipStreamNonBlocking));
   }
   hipStream_t up = gb.cs.up, dn = gb.cs.down;
-  struct DrainCopies {  // (early returns: nothing left in flight on the copy streams either)
-    hipStream_t u, d;
+  struct DrainCopies {  // (early returns: nothing left in flight on the copy or kernel streams either)
+    hipStream_t u, d, k0, k1;
     ~DrainCopies() {
-      (void)hipStreamSynchronize(u);
-      (void)hipStreamSynchronize(d);
+      for (hipStream_t x : {k0, k1, u, d}) (void)hipStreamSynchronize(x);
     }
-  } drain_copies{up, dn};
+  } drain_copies{up, dn, gb.cs.k[0], gb.cs.k[1]};
   int pending = -1;  // the slot whose launch is in flight and not yet decided
   int launch_no = 0;
   for (size_t b0 = 0; b0 < idx.size(); b0 += per_launch, launch_no++) {
@@ -6131,13 +6133,17 @@ static int32_t GeneralBatchRun(kp_cluster_plan* plan, GeneralBatch& gb, const ve
     sargs.resize(n);
     fargs.resize(n);
     std::atomic<int> unbatchable{-1};
+    const bool ht = ctx->ov.host_timing != 0;
+    double tpatch[kMaxHostThreads] = {};  // (kp_overrides.host_timing: the overlays' own share)
     ParallelFor(n, [&](int j_lo, int j_hi, int t) {
     for (int j = j_lo; j < j_hi; j++) {
       const int i = order[b0 + j];
+      const auto tp0 = ht ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point{};
       if (GeneralPatch(gb, cl, cands[i], scratches[t], queues[j], patches + patch_bytes * j)) {
         unbatchable = i;
         return;
       }
+      if (ht) tpatch[t] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp0).count();
       uint8_t* ar = arenas + gb.stride * j;
       SolveArgs& a = sargs[j];
       BindSolve(a, C, o, sh, ar, (int)queues[j].size(), Pc, gb.rmask, gb.res_mode);
@@ -6170,6 +6176,13 @@ static int32_t GeneralBatchRun(kp_cluster_plan* plan, GeneralBatch& gb, const ve
     }
     });
     if (unbatchable >= 0) return fail(KP_E_INVAL, "subset %d: not batchable after the check", unbatchable.load());
+    if (ht) {
+      double tp = 0;
+      for (double x : tpatch) tp += x;
+      fprintf(stderr, "[kp general] launch %d: %d sims, patch %zu B each, GeneralPatch %.2f thread-ms, overlays %.2f ms\n",
+              launch_no, n, patch_bytes, tp,
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th0).count());
+    }
     memcpy(reinterpret_cast<uint8_t*>(sl.up.at(u_args)), sargs.data(), sizeof(SolveArgs) * n);
     memcpy(reinterpret_cast<uint8_t*>(sl.up.at(u_fargs)), fargs.data(), sizeof(FinalizeArgs) * n);
     SolveArgs* dargs = (SolveArgs*)sl.args.p;
@@ -6201,12 +6214,13 @@ static int32_t GeneralBatchRun(kp_cluster_plan* plan, GeneralBatch& gb, const ve
     HIPCHK(hipMemcpyAsync(dargs, reinterpret_cast<uint8_t*>(sl.up.at(u_args)), sizeof(SolveArgs) * n, hipMemcpyHostToDevice, up));
     HIPCHK(hipMemcpyAsync(dfargs, reinterpret_cast<uint8_t*>(sl.up.at(u_fargs)), sizeof(FinalizeArgs) * n, hipMemcpyHostToDevice, up));
     HIPCHK(hipEventRecord(sl.uploaded, up));
-    HIPCHK(launch_batch_init(bi, n, st));
-    HIPCHK(hipStreamWaitEvent(st, sl.uploaded, 0));
-    HIPCHK(hipEventRecord(sl.t0, st));
-    HIPCHK(launch_solve_batch(sargs[0], dargs, n, dyn, st));
-    HIPCHK(launch_finalize_batch(fargs[0], dfargs, n, st));
-    HIPCHK(hipEventRecord(sl.t1, st));
+    hipStream_t ks = gb.cs.k[launch_no & 1];  // (the slot's kernel stream)
+    HIPCHK(launch_batch_init(bi, n, ks));
+    HIPCHK(hipStreamWaitEvent(ks, sl.uploaded, 0));
+    HIPCHK(hipEventRecord(sl.t0, ks));
+    HIPCHK(launch_solve_batch(sargs[0], dargs, n, dyn, ks));
+    HIPCHK(launch_finalize_batch(fargs[0], dfargs, n, ks));
+    HIPCHK(hipEventRecord(sl.t1, ks));
     // downloads on their own stream once the kernels are done (the next launch's kernels need not wait for them)
     HIPCHK(hipStreamWaitEvent(dn, sl.t1, 0));
     auto down = [&](size_t roff, size_t off, size_t width) {
