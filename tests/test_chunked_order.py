@@ -66,3 +66,14 @@ def test_chunked_topology(ctx, catalog, ov):
     prob = synth.config3(catalog, n_pods=3000, n_deployments=40, n_existing=60)
     oc, n = _solve(ctx, prob, ov, 16)
     assert oc[4] == MODE_CHUNKED and n > 16
+
+
+@pytest.mark.parametrize("limit_div,sort_cap", [(300, 8), (500, 8), (500, 64)])
+def test_chunked_memo_runs(ctx, catalog, ov, limit_div, sort_cap):
+    """Binding limits on the chunked order: many pods fail every placement, so the fast lane's unschedulable memo takes
+    runs of them at once (window entries on lanes), up to the pop that ends the Solve once a pass makes no progress, with
+    the queue shorter than the 64-entry window at the end (its ring wraps onto re-pushed entries)."""
+    from kpamd import synth
+    prob = synth.config5(catalog, n_pods=4000, seed=5, limit_div=limit_div)
+    oc, n = _solve(ctx, prob, ov, sort_cap)
+    assert oc[4] == MODE_CHUNKED and n > sort_cap
