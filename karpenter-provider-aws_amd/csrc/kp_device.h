@@ -245,6 +245,7 @@ struct BatchInitArgs {
   size_t stride;
   const uint8_t* pristine;
   size_t dst_off, n_copy;  // [dst_off, dst_off + n_copy) of every arena from pristine
+  size_t skip_off, skip_len;  // except [dst_off + skip_off, + skip_len) (16-byte multiples; 0: none)
   int32_t n_fill;
   uint32_t fill_byte[BATCH_INIT_FILLS];
   size_t fill_off[BATCH_INIT_FILLS], fill_len[BATCH_INIT_FILLS];

@@ -6197,6 +6197,12 @@ static int32_t GeneralBatchRun(kp_cluster_plan* plan, GeneralBatch& gb, const ve
     bi.pristine = (const uint8_t*)gb.pristine.p;
     bi.dst_off = o.common;
     bi.n_copy = (o.exr - o.common + 15) & ~(size_t)15;  // not the existing nodes' requirements: copy-on-write
+    if (__builtin_popcount(gb.rmask) <= 4) {
+      // the existing nodes' request rows are read only for a fifth requested resource and beyond (the first four are
+      // their headroom rows); with four or fewer a commit's read-modify-write leaves the unread values unread
+      bi.skip_off = o.exrq - o.common;
+      bi.skip_len = (o.exroom - o.exrq) & ~(size_t)15;
+    }
     auto fill = [&](size_t off, size_t len, uint32_t byte) {
       bi.fill_off[bi.n_fill] = off;
       bi.fill_len[bi.n_fill] = (len + 15) & ~(size_t)15;

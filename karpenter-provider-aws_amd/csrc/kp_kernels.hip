@@ -5631,14 +5631,17 @@ hipError_t launch_finalize_batch(const FinalizeArgs& a0, const FinalizeArgs* dev
   hipLaunchKernelGGL((finalize_kernel<true>), dim3(n), dim3(FIN_THREADS), 0, s, a0, dev_args);
   return hipGetLastError();
 }
-// Batched Solves' arenas: every arena [y] = base + y * stride gets the shared pristine block copied to `dst_off` and
-// its `n_fill` ranges set to their byte (16-byte granules: offsets and lengths are multiples of 16).
+// Batched Solves' arenas: every arena [y] = base + y * stride gets the shared pristine block copied to `dst_off` (but
+// for one hole the Solve never reads before writing) and its `n_fill` ranges set to their byte (16-byte granules:
+// offsets and lengths are multiples of 16).
 __global__ __launch_bounds__(256) void batch_init_kernel(BatchInitArgs a) {
   uint8_t* arena = a.base + (size_t)blockIdx.y * a.stride;
   const size_t n16 = a.n_copy / 16;
   const uint4* src = reinterpret_cast<const uint4*>(a.pristine);
   uint4* dst = reinterpret_cast<uint4*>(arena + a.dst_off);
-  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256) dst[i] = src[i];
+  const size_t s0 = a.skip_off / 16, s1 = (a.skip_off + a.skip_len) / 16;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256)
+    if (i < s0 || i >= s1) dst[i] = src[i];
   for (int f = 0; f < a.n_fill; f++) {
     const uint32_t b = a.fill_byte[f];
     const uint4 v = make_uint4(b * 0x01010101u, b * 0x01010101u, b * 0x01010101u, b * 0x01010101u);

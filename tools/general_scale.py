@@ -40,7 +40,7 @@ def main():
     plan = kpamd.ClusterPlan(ctx, cl)
     out["prepare_s"] = round(time.perf_counter() - t0, 3)
     print("prepare", out["prepare_s"], flush=True)
-    plan.argmin(offs[:9], flat)  # warmup (the batch layout)
+    plan.argmin(offs[:min(len(subs), 8192) + 1], flat)  # warmup: the batch layout and both slots' arenas (steady state)
     t0 = time.perf_counter()
     choice, _, st = plan.argmin(offs, flat)
     el = time.perf_counter() - t0
