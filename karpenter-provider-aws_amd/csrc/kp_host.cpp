@@ -3225,7 +3225,8 @@ void PutArena(Blob& blob, const Compiled& C, const vector<int32_t>& pod_shape, c
 
 // The arena's device-only regions (after every put of the blob). with_pristine: a device copy of the mutable state
 // (single Solves restore from it; batched simulations restore from the shared one).
-void ReserveArenaDev(Blob& blob, const Compiled& C, int Pc, int opt_stride, int sort_cap, bool with_pristine, SolveOffs& o) {
+void ReserveArenaDev(Blob& blob, const Compiled& C, int Pc, int opt_stride, int sort_cap, bool with_pristine, SolveOffs& o,
+                     size_t ex_fail_entries = SIZE_MAX) {
   const int TW = C.B->TW, NT = (int)C.B->tmpl_reqs.size(), E = (int)C.ex_reqs.size();
   o.pristine = with_pristine ? blob.reserve_dev(o.mut_end - o.mut) : 0;
   o.ncr = blob.reserve_dev(sizeof(KReqs) * Pc);
@@ -3260,7 +3261,9 @@ void ReserveArenaDev(Blob& blob, const Compiled& C, int Pc, int opt_stride, int 
   o.ver_end = blob.total();
   o.fail0 = blob.reserve_dev(0);
   o.ncfail = blob.reserve_dev(sizeof(int32_t) * SLn * o.ncc);
-  o.exfail = blob.reserve_dev(sizeof(int32_t) * SLn * std::max(E, 1));
+  // (batched simulations: one entry per usable-list entry of each shape-level, SolveArgs::ex_ulist)
+  o.exfail = blob.reserve_dev(sizeof(int32_t) * (ex_fail_entries != SIZE_MAX ? std::max<size_t>(ex_fail_entries, 1)
+                                                                               : SLn * std::max(E, 1)));
   o.tfail = blob.reserve_dev(sizeof(int32_t) * SLn * std::max(NT, 1));
   o.txlv = blob.reserve_dev(sizeof(int32_t) * std::max(NT, 1));  // -1: not computed
   o.slfail = blob.reserve_dev(sizeof(int32_t) * SLn);  // -1: no failure yet
@@ -5619,6 +5622,7 @@ struct CopyStreams {
 
 struct GeneralBatch {
   std::unique_ptr<Compiled> C;
+  size_t ulist_total = 0;  // entries of the per-shape-level usable lists (the batched existing-node memo's size)
   uint64_t base_version = 0;
   vector<int32_t> node_input;   // cluster node -> existing input index of the superset (-1: being deleted)
   vector<int32_t> node_sorted;  // cluster node -> position in the Solve's existing order (-1)
@@ -5800,6 +5804,7 @@ static int32_t GeneralBatchBuild(kp_cluster_plan* plan, std::shared_ptr<GeneralB
       }
     }
     off[SLn] = (int32_t)list.size();
+    gb->ulist_total = list.size();  // (the batched arenas' existing-node memo: one entry per list entry)
     if (list.empty()) list.push_back(0);
     gb->so.exul = blob.put(list);
     gb->so.exuo = blob.put(off);
@@ -5833,7 +5838,7 @@ static int32_t GeneralBatchLayout(kp_ctx* ctx, GeneralBatch& gb, int Pc) {
   Blob blob;
   const vector<int32_t> zeros(Pc, 0);
   PutArena(blob, C, zeros, zeros, Pc, gb.ex_static, gb.rmask, o);
-  ReserveArenaDev(blob, C, Pc, gb.opt_stride, std::min(SortCapacity(C.ov), Pc), false, o);
+  ReserveArenaDev(blob, C, Pc, gb.opt_stride, std::min(SortCapacity(C.ov), Pc), false, o, gb.ulist_total);
   gb.tmpl.assign(blob.host.begin(), blob.host.begin() + o.mut_end);
   gb.stride = (o.arena_end + 255) & ~(size_t)255;
   HIPCHK(gb.pristine.alloc(o.mut_end - o.common + 16));

@@ -2520,12 +2520,14 @@ if (!FL_NOTIME && tmg) {                                    \
           }
           if (FX_DIAG && lane == 0) g_sdiag[1] += 1;
           const bool valid = base + lane < u_n;
-          const int ec = ul ? ul[u_base + min(base + lane, u_n - 1)] : base + lane;  // (clamped: masked by valid)
+          const int li = min(base + lane, u_n - 1);
+          const int ec = ul ? ul[u_base + li] : base + lane;  // (clamped: masked by valid)
           bool cand = false, icand = false;
           int32_t ver = 0, ts = 0;
           {  // every read unconditional at a clamped position, the lanes past E masked after (no exec-masked block)
             const int ecc = min(ec, E - 1);
-            const int32_t fl = KA(ex_fail)[(size_t)sl * E + ecc];
+            // the failure memo: [shape-level][position], or (batched simulations) one entry per list entry
+            const int32_t fl = KA(ex_fail)[ul ? (size_t)u_base + li : (size_t)sl * E + ecc];
             ver = KA(ex_ver)[ecc];
             ts = KA(ex_taintset)[ecc];
             const uint8_t sok = KA(ex_static_ok)[ecc];
@@ -2589,7 +2591,8 @@ if (!FL_NOTIME && tmg) {                                    \
               const bool mok = merge_compatible(D, crx, (const KReqs*)&fl_B, b_negop, false, m_v, rv,
                                                 (WaveSlots*)&fl_slots, vint_global(KA(vint)));
               if (!mok) {  // permanent unless the undefined-key rule failed (no well-known exemption here)
-                KA(ex_fail)[(size_t)sl * E + ei] = (fl_B.present & ~crx.P & ~b_negop) == 0 ? NC_NEVER : verx;
+                KA(ex_fail)[ul ? (size_t)u_base + __builtin_amdgcn_readlane(li, l) : (size_t)sl * E + ei] =
+                    (fl_B.present & ~crx.P & ~b_negop) == 0 ? NC_NEVER : verx;
                 continue;
               }
               // commit: ExistingNode.Add (requirements, requests, headroom rows, version), Topology.Record
@@ -3575,7 +3578,8 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a0, const Solv
         pk[k] = ix < u_n ? (ul ? ul[u_base + ix] : ix) : -1;
         const int ec = pk[k];
         if (ec < 0) continue;
-        const int32_t fl = a.ex_fail[(size_t)sl * a.n_existing + ec], ver = a.ex_ver[ec];
+        // the failure memo: [shape-level][position], or (batched simulations) one entry per list entry
+        const int32_t fl = a.ex_fail[ul ? (size_t)u_base + ix : (size_t)sl * a.n_existing + ec], ver = a.ex_ver[ec];
         const uint8_t sok = a.ex_static_ok[ec];
         const int32_t ts = a.ex_taintset[ec];
         // Fits(Merge(requests, pod), available), exact: unrequested resources never change. The headroom rows
@@ -3633,7 +3637,8 @@ __global__ __launch_bounds__(NW * 64) void solve_kernel(SolveArgs a0, const Solv
           ok = merge_compatible(D, er, B, b_negop, false, m_v, rv, &slots[wave], vi);
           bytes += sizeof(KReqs);
           if (!ok && lane == 0)  // permanent unless the undefined-key rule failed (no well-known exemption here)
-            a.ex_fail[(size_t)sl * a.n_existing + ei] = (B->present & ~er->present & ~b_negop) == 0 ? NC_NEVER : a.ex_ver[ei];
+            a.ex_fail[ul ? (size_t)u_base + a.ex_uidx[(size_t)sl * a.n_existing + ei] : (size_t)sl * a.n_existing + ei] =
+                (B->present & ~er->present & ~b_negop) == 0 ? NC_NEVER : a.ex_ver[ei];
           if (ok && own_n) ok = topo_narrow(D, own_n, s_town, s_tacc, s_tcnt, false, m_v, rv, vi);  // not memoised
         }
         if (lane == 0) s_ok[wave] = ok ? 1 : 0;
