@@ -5989,7 +5989,8 @@ static int32_t GeneralBatchRun(kp_cluster_plan* plan, GeneralBatch& gb, const ve
   if (ctx->ov.host_timing)
     fprintf(stderr, "[kp general] arena stride %.2f MB, %zu simulations per launch, Pc %d; batch_init per simulation: copy %zu B, "
             "fills stats %zu npods %zu place %zu ver %zu fail %zu hcnc %zu B\n", gb.stride / 1e6, per_launch, Pc,
-            gb.o.exr - gb.o.common, sizeof(uint64_t) * KP_SOLVE_STATS, sizeof(int32_t) * (size_t)Pc, sizeof(int32_t) * (size_t)Pc,
+            gb.o.exr - gb.o.common - (__builtin_popcount(gb.rmask) <= 4 ? gb.o.exroom - gb.o.exrq : 0),
+            sizeof(uint64_t) * KP_SOLVE_STATS, sizeof(int32_t) * (size_t)Pc, sizeof(int32_t) * (size_t)Pc,
             gb.o.ver_end - gb.o.ver0, gb.o.fail_end - gb.o.fail0, gb.o.n_hcnc);
   const int sort_cap = std::min(SortCapacity(C.ov), Pc);
   const size_t dyn = std::max<size_t>((size_t)2 * sort_cap * sizeof(int32_t), o.chk_on ? CHK_LDS_BYTES : 0);
