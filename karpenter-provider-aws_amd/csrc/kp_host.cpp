@@ -6283,18 +6283,47 @@ static int32_t GeneralSimLocked(kp_cluster_plan* plan, const uint32_t* offsets, 
         labels[i][Normalize(l.key ? l.key : "")] = l.value ? l.value : "";
       }
   }
-  vector<vector<uint32_t>> cands(n_subsets);
-  vector<char> inS(N, 0);
-  for (uint32_t s = 0; s < n_subsets; s++) {
+  for (uint32_t s = 0; s < n_subsets; s++)
     if (offsets[s + 1] < offsets[s]) return fail(KP_E_INVAL, "offsets not monotone at %u", s);
-    cands[s].assign(nodes + offsets[s], nodes + offsets[s + 1]);
-    for (uint32_t c : cands[s]) {
+  // the subsets' candidate lists, checked on up to 16 threads (each with its own membership marks); the error reported
+  // is the first subset's, as the serial check would report it
+  vector<vector<uint32_t>> cands(n_subsets);
+  std::atomic<int64_t> bad_s{INT64_MAX};
+  vector<vector<char>> inS(kMaxHostThreads);
+  ParallelFor((int)n_subsets, [&](int s_lo, int s_hi, int t) {
+    vector<char>& mark = inS[t];
+    mark.assign(N, 0);
+    for (int s = s_lo; s < s_hi; s++) {
+      cands[s].assign(nodes + offsets[s], nodes + offsets[s + 1]);
+      bool ok = true;
+      size_t k = 0;
+      for (; k < cands[s].size(); k++) {
+        const uint32_t c = cands[s][k];
+        if (c >= (uint32_t)N || cl.nodes[c].deleting || mark[c]) {
+          ok = false;
+          break;
+        }
+        mark[c] = 1;
+      }
+      for (size_t j = 0; j < k; j++) mark[cands[s][j]] = 0;
+      if (!ok) {
+        int64_t cur = bad_s.load();
+        while (s < cur && !bad_s.compare_exchange_weak(cur, s)) {
+        }
+        return;
+      }
+    }
+  });
+  if (bad_s.load() != INT64_MAX) {  // the serial check's message for the first bad subset
+    const uint32_t s = (uint32_t)bad_s.load();
+    vector<char> mark(N, 0);
+    for (uint32_t k = offsets[s]; k < offsets[s + 1]; k++) {
+      const uint32_t c = nodes[k];
       if (c >= (uint32_t)N) return fail(KP_E_INVAL, "subset %u: node %u", s, c);
       if (cl.nodes[c].deleting) return fail(KP_E_INVAL, "subset %u: node %u is being deleted", s, c);
-      if (inS[c]) return fail(KP_E_INVAL, "subset %u: node %u twice", s, c);
-      inS[c] = 1;
+      if (mark[c]) return fail(KP_E_INVAL, "subset %u: node %u twice", s, c);
+      mark[c] = 1;
     }
-    for (uint32_t c : cands[s]) inS[c] = 0;
   }
   // the batched path: built once per plan (again after an offering refresh of its catalogues)
   if (plan->gb) {
@@ -6319,17 +6348,21 @@ static int32_t GeneralSimLocked(kp_cluster_plan* plan, const uint32_t* offsets, 
   memset(plan->general_phase, 0, sizeof plan->general_phase);
   double dev_ms = 0, host_ms[2] = {0, 0};  // the batch's host work: overlays + arguments, decisions
   vector<int> batched, single;
-  for (uint32_t s = 0; s < n_subsets; s++) {
-    bool ok = batch_on && plan->gb;
-    if (ok && plan->gb->C->G) {  // an inverse anti-affinity group would vanish: the per-subset compile
-      const Compiled& C = *plan->gb->C;
-      std::map<int, int> inv;
-      for (uint32_t c : cands[s])
-        for (int32_t g : C.node_inv[plan->gb->node_input[c]])
-          if (++inv[g] == C.tg_inv_total[g]) ok = false;
+  vector<char> batchable(n_subsets, 0);
+  ParallelFor((int)n_subsets, [&](int s_lo, int s_hi, int) {
+    for (int s = s_lo; s < s_hi; s++) {
+      bool ok = batch_on && plan->gb;
+      if (ok && plan->gb->C->G) {  // an inverse anti-affinity group would vanish: the per-subset compile
+        const Compiled& C = *plan->gb->C;
+        std::map<int, int> inv;
+        for (uint32_t c : cands[s])
+          for (int32_t g : C.node_inv[plan->gb->node_input[c]])
+            if (++inv[g] == C.tg_inv_total[g]) ok = false;
+      }
+      batchable[s] = ok ? 1 : 0;
     }
-    (ok ? batched : single).push_back((int)s);
-  }
+  });
+  for (uint32_t s = 0; s < n_subsets; s++) (batchable[s] ? batched : single).push_back((int)s);
   const auto t1 = clk::now();
   if (!batched.empty()) {
     const int32_t rc = GeneralBatchRun(plan, *plan->gb, cands, batched, labels, multi_node, outs, counters, &dev_ms, host_ms,

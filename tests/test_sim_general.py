@@ -134,3 +134,39 @@ def test_gpu_batched_simulations_counted(ctx, catalog, seed, ov):
     for i, (x, y, w) in enumerate(zip(b, s, want)):
         assert x == y, (i, x, y)
         assert (x["decision"], x["savings"]) == (w["decision"], w["savings"]), (i, x, w)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bad,msg", [("twice", "twice"), ("range", "node 9999"), ("order", "not monotone")])
+def test_general_invalid_subsets(ctx, catalog, bad, msg):
+    """A bad subset in a general-path batch (checked on the host threads): KP_E_INVAL naming the first bad subset, as
+    the serial check reports it; the plan stays usable afterwards."""
+    import numpy as np
+    import kpamd
+    from kpamd import synth
+    cl = synth.spread_cluster(catalog, 40)
+    cands = [int(c) for c in cl.candidates]
+    subs = [cands[i:i + 3] for i in range(0, 30, 3)]
+    if bad == "twice":
+        subs[6] = [cands[0], cands[1], cands[0]]
+        subs[8] = [cands[2], cands[2]]
+    elif bad == "range":
+        subs[4] = [cands[0], 9999]
+        subs[7] = [9998]
+    offs = np.zeros(len(subs) + 1, dtype=np.uint32)
+    offs[1:] = np.cumsum([len(x) for x in subs])
+    flat = np.concatenate([np.asarray(x, dtype=np.uint32) for x in subs])
+    if bad == "order":
+        offs[5] = offs[6] + 1
+    plan = kpamd.ClusterPlan(ctx, cl)
+    try:
+        with pytest.raises(kpamd.KPError) as e:
+            plan.simulate_csr(offs, flat)
+        assert e.value.code == kpamd.abi.KP_E_INVAL
+        want = {"twice": "subset 6", "range": "subset 4", "order": "at 5"}[bad]
+        assert msg in str(e.value) and want in str(e.value), str(e.value)
+        good = [cands[i:i + 3] for i in range(0, 9, 3)]
+        res, _ = plan.simulate(good)
+        assert len(res) == 3
+    finally:
+        plan.close()
